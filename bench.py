@@ -1,0 +1,145 @@
+#!/usr/bin/env python3
+"""Headline benchmark for the MI355X reduction-collective hot path.
+
+BASELINE.json metric: "Allreduce busBW GB/s @256MiB fp32 SUM at 2/4/8 GPUs;
+MPI_Op HBM GB/s".
+
+* N = 1 (configs[1]): the MPI_Op 3-buffer kernel, fp32 SUM, 1 GiB per buffer
+  (the top of the 4 KiB-1 GiB sweep; 3 GiB of HBM traffic per step, well past
+  the 256 MiB Infinity Cache).  value = algorithmic HBM GB/s = 3*n*4 B / t.
+* N > 1 (configs[3] headline point): MPI_Allreduce fp32 SUM of 256 MiB per
+  rank through the xGMI IPC collective.  value = busBW = S/t * 2(N-1)/N.
+
+A step is one pass of the hot path over one batch of synthetic input that is
+already resident in HBM.  Timing: W untimed warmup steps, barrier +
+synchronize, K timed steps, barrier + synchronize, max over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+XGMI_LINK_GBS = 153.0          # per-link, R(N) = (N-1) x 153
+METRIC = "Allreduce busBW GB/s @256MiB fp32 SUM at 2/4/8 GPUs; MPI_Op HBM GB/s"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--op-bytes", type=int, default=1 << 30, help="bytes per op buffer (N=1)")
+    p.add_argument("--ar-bytes", type=int, default=256 << 20, help="allreduce bytes (N>1)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    return p.parse_args()
+
+
+def cpu_baseline_op(seconds: float) -> dict:
+    """The oracle's op/base restatement (scalar C loop, 1 thread) on a
+    bounded sample of the same workload: 3-buffer fp32 SUM, 64 MiB/buffer."""
+    import numpy as np
+
+    from oracle import oracle as orc
+
+    n = (64 << 20) // 4
+    rng = np.random.default_rng(20261015)
+    a = rng.standard_normal(n, dtype=np.float32)
+    b = rng.standard_normal(n, dtype=np.float32)
+    out = np.empty_like(a)
+    orc.time_op_3buff(3, 15, a, b, out, n, 1)  # warm
+    iters, total = 0, 0.0
+    while total < seconds:
+        total += orc.time_op_3buff(3, 15, a, b, out, n, 4)
+        iters += 4
+    gbs = 3.0 * n * 4 * iters / total / 1e9
+    return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"oracle op/base restatement, 3-buffer fp32 SUM, 64 MiB/buffer, "
+                      f"{iters} iterations in {total:.1f} s, 1 thread"}
+
+
+def bench_op(args):
+    import torch
+
+    from ompi_amd import op as mop
+
+    n = args.op_bytes // 4
+    g = torch.Generator(device="cuda").manual_seed(20261015)
+    a = torch.randn(n, device="cuda", generator=g)
+    b = torch.randn(n, device="cuda", generator=g)
+    out = torch.empty_like(a)
+    stream = torch.cuda.current_stream()
+    for _ in range(args.warmup):
+        mop.reduce_local_3buff_async(a, b, out, n, mop.MPI_FLOAT, mop.MPI_SUM, stream=stream)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        mop.reduce_local_3buff_async(a, b, out, n, mop.MPI_FLOAT, mop.MPI_SUM, stream=stream)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # events on the launch stream
+    algo_bytes = 3.0 * n * 4
+    achieved = algo_bytes / (kernel_ms * 1e-3) / 1e9
+    res = {
+        "metric": METRIC,
+        "value": round(algo_bytes * args.steps / wall / 1e9, 2),
+        "unit": "GB/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (torch.randn, seed 20261015), resident in HBM",
+        "config": {"workload": "MPI_Op 3-buffer SUM fp32, 1 GiB per buffer (BASELINE configs[1])",
+                   "count": n, "bytes_per_buffer": args.op_bytes, "op": "MPI_SUM",
+                   "datatype": "MPI_FLOAT", "kernel": "op_vec_kernel<float,SUM,3buff>"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": load_traffic("op_sum_f32_3buff_1GiB"),
+                     "kernel_ms": round(kernel_ms, 4),
+                     "algorithmic_bytes_per_launch": int(algo_bytes)},
+    }
+    return res
+
+
+def load_traffic(key: str):
+    """HBM bytes per launch from the committed PMC pass (profiles/pmc.json,
+    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM + WRITE_SIZE)."""
+    path = os.path.join(ROOT, "profiles", "pmc.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(key)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 or args.gpus > 1:
+        from ompi_amd import coll_bench
+        res = coll_bench.bench_allreduce(args, METRIC, XGMI_LINK_GBS)
+        if res is None:
+            return
+    else:
+        res = bench_op(args)
+        if not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline_op(args.cpu_seconds)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

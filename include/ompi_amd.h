@@ -1,0 +1,128 @@
+/*
+ * ompi_amd — MI355X-native reduction-collective hot path for Open MPI.
+ *
+ * C ABI of libompi_amd.so.  Plain pointers and sizes only; every entry point
+ * returns an int status (no C++ exceptions cross this boundary).  Streams are
+ * passed as `void *` (a hipStream_t; NULL = the calling thread's per-thread
+ * stream).  Device pointers are HIP device (or managed) allocations.
+ *
+ * Each group of entry points names the reference interface it replaces.
+ */
+#ifndef OMPI_AMD_H
+#define OMPI_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ */
+/* Status codes (mapped to OMPI_ERR_* by the MCA glue)                 */
+/* ------------------------------------------------------------------ */
+#define OMPI_AMD_SUCCESS            0
+#define OMPI_AMD_ERR_UNSUPPORTED   (-1)  /* (op,type) slot not provided   */
+#define OMPI_AMD_ERR_BAD_PARAM     (-2)
+#define OMPI_AMD_ERR_HIP           (-3)  /* a HIP runtime call failed      */
+#define OMPI_AMD_ERR_TIMEOUT       (-4)  /* a peer never reached a flag    */
+#define OMPI_AMD_ERR_NOT_DEVICE    (-5)  /* buffer is not device memory    */
+#define OMPI_AMD_ERR_BOOTSTRAP     (-6)  /* shared-memory rendezvous failed */
+
+/* ------------------------------------------------------------------ */
+/* Op and type codes — numerically identical to the reference enums so */
+/* the MCA glue passes them straight through:                          */
+/*   op   = OMPI_OP_BASE_FORTRAN_*  (ompi/mca/op/op.h:203-237)         */
+/*   type = OMPI_OP_BASE_TYPE_*     (ompi/mca/op/op.h:104-190)         */
+/* ------------------------------------------------------------------ */
+enum {
+    OMPI_AMD_OP_NULL = 0, OMPI_AMD_OP_MAX = 1, OMPI_AMD_OP_MIN = 2,
+    OMPI_AMD_OP_SUM = 3, OMPI_AMD_OP_PROD = 4, OMPI_AMD_OP_LAND = 5,
+    OMPI_AMD_OP_BAND = 6, OMPI_AMD_OP_LOR = 7, OMPI_AMD_OP_BOR = 8,
+    OMPI_AMD_OP_LXOR = 9, OMPI_AMD_OP_BXOR = 10, OMPI_AMD_OP_MAXLOC = 11,
+    OMPI_AMD_OP_MINLOC = 12, OMPI_AMD_OP_REPLACE = 13, OMPI_AMD_OP_NO_OP = 14,
+    OMPI_AMD_OP_COUNT = 15             /* OMPI_OP_BASE_FORTRAN_OP_MAX */
+};
+
+enum {
+    OMPI_AMD_TYPE_INT8_T = 0, OMPI_AMD_TYPE_UINT8_T = 1,
+    OMPI_AMD_TYPE_INT16_T = 2, OMPI_AMD_TYPE_UINT16_T = 3,
+    OMPI_AMD_TYPE_INT32_T = 4, OMPI_AMD_TYPE_UINT32_T = 5,
+    OMPI_AMD_TYPE_INT64_T = 6, OMPI_AMD_TYPE_UINT64_T = 7,
+    OMPI_AMD_TYPE_FLOAT = 15, OMPI_AMD_TYPE_DOUBLE = 16,
+    OMPI_AMD_TYPE_BOOL = 25, OMPI_AMD_TYPE_BYTE = 30,
+    OMPI_AMD_TYPE_FLOAT_INT = 34, OMPI_AMD_TYPE_DOUBLE_INT = 35,
+    OMPI_AMD_TYPE_LONG_INT = 36, OMPI_AMD_TYPE_2INT = 37,
+    OMPI_AMD_TYPE_SHORT_INT = 38,
+    OMPI_AMD_TYPE_COUNT = 41           /* OMPI_OP_BASE_TYPE_MAX */
+};
+
+/* Library identity / build check. */
+const char *ompi_amd_version(void);
+/* Number of visible HIP devices (0 on a host without a GPU). */
+int ompi_amd_device_count(void);
+/* Last HIP error string seen by this thread (diagnostics only). */
+const char *ompi_amd_last_error(void);
+/* hipPointerGetAttributes: 1 device/managed, 0 host — replaces
+ * mca_common_cuda_is_gpu_buffer (opal/mca/common/cuda/common_cuda.c:
+ * 1739-1792) used by the convertor and the handlers to pick the path. */
+int ompi_amd_is_device_pointer(const void *ptr);
+
+/* ================================================================== */
+/* 1. MPI_Op kernels — replaces op/base's handler loops                */
+/*    ompi/mca/op/base/op_base_functions.c:40-104 (2-buffer),          */
+/*    :654-731 (3-buffer); tables :1485-1655.                          */
+/* ================================================================== */
+
+/* 1 if this library provides a device kernel for (op,type). */
+int ompi_amd_op_supported(int op, int type);
+/* Element stride (datatype extent) in bytes; 0 for unknown types. */
+size_t ompi_amd_type_extent(int type);
+
+/* inout[i] = inout[i] (op) in[i]  — 2-buffer handler semantics.
+ * Stream-ordered; returns before the kernel completes. */
+int ompi_amd_op_reduce(int op, int type, const void *in, void *inout,
+                       size_t count, void *stream);
+/* out[i] = in1[i] (op) in2[i]     — 3-buffer handler semantics. */
+int ompi_amd_op_reduce_3buff(int op, int type, const void *in1,
+                             const void *in2, void *out, size_t count,
+                             void *stream);
+
+/* --- the op framework seam (ompi/mca/op/op.h:258-273, 362-378) ---- */
+/* Handler signatures are exactly ompi_op_base_handler_fn_1_0_0_t and
+ * ompi_op_base_3buff_handler_fn_1_0_0_t.  The handlers run the device
+ * kernel on the calling thread's stream and synchronise before returning
+ * (the caller sends the result immediately; handlers return void).  When
+ * the buffers are host memory they call the fallback registered for the
+ * slot (the previous, lower-priority handler — op_example_module_max.c
+ * pattern); with no fallback registered they abort loudly. */
+struct ompi_datatype_t;
+struct ompi_op_base_module_1_0_0_t;
+typedef void (*ompi_amd_op_handler_fn_t)(const void *, void *, int *,
+                                         struct ompi_datatype_t **,
+                                         struct ompi_op_base_module_1_0_0_t *);
+typedef void (*ompi_amd_op_3buff_handler_fn_t)(const void *, const void *,
+                                               void *, int *,
+                                               struct ompi_datatype_t **,
+                                               struct ompi_op_base_module_1_0_0_t *);
+
+/* Row `op` of the 2-/3-buffer handler tables: OMPI_AMD_TYPE_COUNT entries,
+ * NULL where this library provides no kernel (keep the lower priority
+ * slot, op_base_op_select.c:137-178). NULL for an unknown op. */
+const ompi_amd_op_handler_fn_t *ompi_amd_op_handler_row(int op);
+const ompi_amd_op_3buff_handler_fn_t *ompi_amd_op_3buff_handler_row(int op);
+
+/* Register the host-memory fallback for a slot (what the glue finds in
+ * op->o_func.intrinsic.fns[type] / .modules[type] at query time). */
+int ompi_amd_op_set_fallback(int op, int type, ompi_amd_op_handler_fn_t fn,
+                             struct ompi_op_base_module_1_0_0_t *module,
+                             ompi_amd_op_3buff_handler_fn_t fn3,
+                             struct ompi_op_base_module_1_0_0_t *module3);
+
+/* Stream the handlers of the calling thread use (NULL = per-thread). */
+int ompi_amd_set_thread_stream(void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OMPI_AMD_H */

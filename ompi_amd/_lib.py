@@ -1,0 +1,125 @@
+"""ctypes binding of libompi_amd.so (the C ABI declared in include/ompi_amd.h).
+
+The shared library is built in-tree by ``__graft_entry__.build()`` (or
+``make -C ompi_amd/csrc``).  There is no fallback: if the library is missing
+every entry point raises, so a test or bench can never silently run on a
+CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libompi_amd.so")
+
+# status codes (include/ompi_amd.h)
+SUCCESS = 0
+ERR_UNSUPPORTED = -1
+ERR_BAD_PARAM = -2
+ERR_HIP = -3
+ERR_TIMEOUT = -4
+ERR_NOT_DEVICE = -5
+ERR_BOOTSTRAP = -6
+
+_ERRNAMES = {
+    ERR_UNSUPPORTED: "unsupported (op,type)",
+    ERR_BAD_PARAM: "bad parameter",
+    ERR_HIP: "HIP error",
+    ERR_TIMEOUT: "timeout waiting for a peer",
+    ERR_NOT_DEVICE: "buffer is not device memory",
+    ERR_BOOTSTRAP: "bootstrap failure",
+}
+
+
+class OmpiAmdError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        detail = ""
+        if _lib is not None:
+            detail = _lib.ompi_amd_last_error().decode(errors="replace")
+        super().__init__(f"{what}: {_ERRNAMES.get(code, code)} {detail}".strip())
+        self.code = code
+
+
+_lib = None
+
+HANDLER_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p,
+                              ctypes.POINTER(ctypes.c_int), ctypes.c_void_p,
+                              ctypes.c_void_p)
+HANDLER3_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_void_p, ctypes.POINTER(ctypes.c_int),
+                               ctypes.c_void_p, ctypes.c_void_p)
+
+
+class DdtBlock(ctypes.Structure):
+    _fields_ = [("disp", ctypes.c_int64), ("len", ctypes.c_int64)]
+
+
+# (name, restype, argtypes) for every symbol include/ompi_amd.h declares
+_C = ctypes
+PROTOTYPES = [
+    ("ompi_amd_version", _C.c_char_p, []),
+    ("ompi_amd_device_count", _C.c_int, []),
+    ("ompi_amd_last_error", _C.c_char_p, []),
+    ("ompi_amd_op_supported", _C.c_int, [_C.c_int, _C.c_int]),
+    ("ompi_amd_type_extent", _C.c_size_t, [_C.c_int]),
+    ("ompi_amd_op_reduce", _C.c_int,
+     [_C.c_int, _C.c_int, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p]),
+    ("ompi_amd_op_reduce_3buff", _C.c_int,
+     [_C.c_int, _C.c_int, _C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p]),
+    ("ompi_amd_op_handler_row", _C.POINTER(_C.c_void_p), [_C.c_int]),
+    ("ompi_amd_op_3buff_handler_row", _C.POINTER(_C.c_void_p), [_C.c_int]),
+    ("ompi_amd_op_set_fallback", _C.c_int,
+     [_C.c_int, _C.c_int, _C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_void_p]),
+    ("ompi_amd_set_thread_stream", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_ddt_create", _C.c_int,
+     [_C.POINTER(DdtBlock), _C.c_int, _C.c_int64, _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_ddt_destroy", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_ddt_size", _C.c_size_t, [_C.c_void_p]),
+    ("ompi_amd_ddt_pack", _C.c_int,
+     [_C.c_void_p, _C.c_size_t, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_size_t,
+      _C.POINTER(_C.c_size_t), _C.c_void_p]),
+    ("ompi_amd_ddt_unpack", _C.c_int,
+     [_C.c_void_p, _C.c_size_t, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_size_t,
+      _C.POINTER(_C.c_size_t), _C.c_void_p]),
+    ("ompi_amd_is_device_pointer", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_comm_create", _C.c_int,
+     [_C.c_char_p, _C.c_int, _C.c_int, _C.c_int, _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_comm_destroy", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_comm_rank", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_comm_size", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_comm_set_param", _C.c_int, [_C.c_void_p, _C.c_char_p, _C.c_int64]),
+    ("ompi_amd_allreduce", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p]),
+    ("ompi_amd_reduce_scatter_block", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p]),
+    ("ompi_amd_allgather", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p]),
+    ("ompi_amd_bcast", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_void_p]),
+]
+
+
+def load(path: str = LIB_PATH):
+    """Load libompi_amd.so once; raise loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(
+            f"libompi_amd.so not built at {path}: run __graft_entry__.build() "
+            "(or make -C ompi_amd/csrc). There is no CPU fallback.")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    for name, res, args in PROTOTYPES:
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue  # checked explicitly by tests/test_abi.py
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != SUCCESS:
+        raise OmpiAmdError(rc, what)

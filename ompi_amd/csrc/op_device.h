@@ -1,0 +1,144 @@
+// Device-side MPI_Op semantics shared by the op kernels and the fused
+// collective reductions.  gfx950 only.
+//
+// f(x, y) is the reference's element rule with x = the OUT operand of the
+// 2-buffer handler (inout) or in1 of the 3-buffer handler, y = in / in2:
+//   ompi/mca/op/base/op_base_functions.c
+//     OP_FUNC   :40-51   b = b op a            -> f(x,y) = x op y
+//     FUNC_FUNC :60-73   b = current_func(b,a) -> MAX (x > y ? x : y) :153
+//                                                 MIN (x < y ? x : y) :216
+//     LOC_FUNC  :88-104, LOC_FUNC_3BUF :709-731 (differ; see loc2/loc3)
+// MAX/MIN are compare+select, never v_max/v_min: NaN and ±0 must resolve to
+// the second operand exactly as the C ternary does.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ompi_amd.h"
+
+namespace ompi_amd {
+
+// MAXLOC/MINLOC pair types (op_base_functions.c:602-607); layouts match the
+// C ABI (DOUBLE_INT: extent 16, v at 0, k at 8, 4 pad bytes).
+struct float_int_t { float v; int k; };
+struct double_int_t { double v; int k; };
+struct long_int_t { long v; int k; };
+struct two_int_t { int v; int k; };
+struct short_int_t { short v; int k; };
+static_assert(sizeof(double_int_t) == 16 && sizeof(short_int_t) == 8, "pair ABI");
+
+template <typename T> struct is_pair { static constexpr bool value = false; };
+template <> struct is_pair<float_int_t> { static constexpr bool value = true; };
+template <> struct is_pair<double_int_t> { static constexpr bool value = true; };
+template <> struct is_pair<long_int_t> { static constexpr bool value = true; };
+template <> struct is_pair<two_int_t> { static constexpr bool value = true; };
+template <> struct is_pair<short_int_t> { static constexpr bool value = true; };
+
+// Pair types whose extent exceeds v+k: the reference never writes the gap.
+template <typename T> struct has_gap { static constexpr bool value = false; };
+template <> struct has_gap<double_int_t> { static constexpr bool value = true; };
+template <> struct has_gap<long_int_t> { static constexpr bool value = true; };
+template <> struct has_gap<short_int_t> { static constexpr bool value = true; };
+
+// type code -> C type
+template <int TYPE> struct type_of;
+template <> struct type_of<OMPI_AMD_TYPE_INT8_T> { using type = int8_t; };
+template <> struct type_of<OMPI_AMD_TYPE_UINT8_T> { using type = uint8_t; };
+template <> struct type_of<OMPI_AMD_TYPE_INT16_T> { using type = int16_t; };
+template <> struct type_of<OMPI_AMD_TYPE_UINT16_T> { using type = uint16_t; };
+template <> struct type_of<OMPI_AMD_TYPE_INT32_T> { using type = int32_t; };
+template <> struct type_of<OMPI_AMD_TYPE_UINT32_T> { using type = uint32_t; };
+template <> struct type_of<OMPI_AMD_TYPE_INT64_T> { using type = int64_t; };
+template <> struct type_of<OMPI_AMD_TYPE_UINT64_T> { using type = uint64_t; };
+template <> struct type_of<OMPI_AMD_TYPE_FLOAT> { using type = float; };
+template <> struct type_of<OMPI_AMD_TYPE_DOUBLE> { using type = double; };
+template <> struct type_of<OMPI_AMD_TYPE_BOOL> { using type = bool; };
+template <> struct type_of<OMPI_AMD_TYPE_BYTE> { using type = char; };
+template <> struct type_of<OMPI_AMD_TYPE_FLOAT_INT> { using type = float_int_t; };
+template <> struct type_of<OMPI_AMD_TYPE_DOUBLE_INT> { using type = double_int_t; };
+template <> struct type_of<OMPI_AMD_TYPE_LONG_INT> { using type = long_int_t; };
+template <> struct type_of<OMPI_AMD_TYPE_2INT> { using type = two_int_t; };
+template <> struct type_of<OMPI_AMD_TYPE_SHORT_INT> { using type = short_int_t; };
+
+// Which (op,type) slots exist — the op/base table pattern
+// (op_base_functions.c:1485-1569) restricted to the predefined C types.
+__host__ __device__ constexpr bool is_c_int(int t) { return t >= 0 && t <= 7; }
+__host__ __device__ constexpr bool is_fp(int t) { return t == OMPI_AMD_TYPE_FLOAT || t == OMPI_AMD_TYPE_DOUBLE; }
+__host__ __device__ constexpr bool is_pair_type(int t) {
+    return t == OMPI_AMD_TYPE_FLOAT_INT || t == OMPI_AMD_TYPE_DOUBLE_INT ||
+           t == OMPI_AMD_TYPE_LONG_INT || t == OMPI_AMD_TYPE_2INT || t == OMPI_AMD_TYPE_SHORT_INT;
+}
+__host__ __device__ constexpr bool slot_supported(int op, int t) {
+    return (op == OMPI_AMD_OP_MAX || op == OMPI_AMD_OP_MIN || op == OMPI_AMD_OP_SUM ||
+            op == OMPI_AMD_OP_PROD) ? (is_c_int(t) || is_fp(t))
+         : (op == OMPI_AMD_OP_LAND || op == OMPI_AMD_OP_LOR || op == OMPI_AMD_OP_LXOR)
+               ? (is_c_int(t) || t == OMPI_AMD_TYPE_BOOL)
+         : (op == OMPI_AMD_OP_BAND || op == OMPI_AMD_OP_BOR || op == OMPI_AMD_OP_BXOR)
+               ? (is_c_int(t) || t == OMPI_AMD_TYPE_BYTE)
+         : (op == OMPI_AMD_OP_MAXLOC || op == OMPI_AMD_OP_MINLOC) ? is_pair_type(t)
+                                                                 : false;
+}
+
+// Element rule.  THREE selects the 3-buffer LOC variant (it returns in2 on
+// an unordered compare; the 2-buffer one keeps out).
+template <int OP, bool THREE> struct opfn;
+
+#define OMPI_AMD_ARITH(OPC, EXPR)                                              \
+    template <bool THREE> struct opfn<OPC, THREE> {                           \
+        template <typename T> __device__ __forceinline__ static T f(T x, T y) { return (T)(EXPR); } \
+    };
+OMPI_AMD_ARITH(OMPI_AMD_OP_SUM, x + y)
+OMPI_AMD_ARITH(OMPI_AMD_OP_PROD, x * y)
+OMPI_AMD_ARITH(OMPI_AMD_OP_MAX, (x > y) ? x : y)
+OMPI_AMD_ARITH(OMPI_AMD_OP_MIN, (x < y) ? x : y)
+OMPI_AMD_ARITH(OMPI_AMD_OP_LAND, x && y)
+OMPI_AMD_ARITH(OMPI_AMD_OP_LOR, x || y)
+OMPI_AMD_ARITH(OMPI_AMD_OP_LXOR, (x ? 1 : 0) ^ (y ? 1 : 0))
+OMPI_AMD_ARITH(OMPI_AMD_OP_BAND, x & y)
+OMPI_AMD_ARITH(OMPI_AMD_OP_BOR, x | y)
+OMPI_AMD_ARITH(OMPI_AMD_OP_BXOR, x ^ y)
+#undef OMPI_AMD_ARITH
+
+template <int OP, bool THREE> struct locfn {
+    template <typename S> __device__ __forceinline__ static S f(S x, S y) {
+        S r = x;  // keeps x's gap bytes (2-buffer: x = out)
+        if (!THREE) {
+            // LOC_FUNC: a = in = y, b = out = x
+            const bool take = (OP == OMPI_AMD_OP_MAXLOC) ? (y.v > x.v) : (y.v < x.v);
+            if (take) { r.v = y.v; r.k = y.k; }
+            else if (y.v == x.v) { r.k = (x.k < y.k) ? x.k : y.k; }
+        } else {
+            // LOC_FUNC_3BUF: a1 = x, a2 = y
+            const bool take = (OP == OMPI_AMD_OP_MAXLOC) ? (x.v > y.v) : (x.v < y.v);
+            if (take) { /* r = x */ }
+            else if (x.v == y.v) { r.k = (y.k < x.k) ? y.k : x.k; }
+            else { r.v = y.v; r.k = y.k; }
+        }
+        return r;
+    }
+};
+template <bool THREE> struct opfn<OMPI_AMD_OP_MAXLOC, THREE> : locfn<OMPI_AMD_OP_MAXLOC, THREE> {};
+template <bool THREE> struct opfn<OMPI_AMD_OP_MINLOC, THREE> : locfn<OMPI_AMD_OP_MINLOC, THREE> {};
+
+// 16-byte vector used for every global access on the streaming paths.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T> union vec16 {
+    u32x4 v;
+    T e[16 / sizeof(T)];
+};
+
+// Store one element.  Gapped pair types in 3-buffer mode write only v and k
+// (LOC_FUNC_3BUF never touches out's gap).
+template <typename T, bool THREE>
+__device__ __forceinline__ void store_elem(T *p, const T &r) {
+    if constexpr (THREE && has_gap<T>::value) {
+        p->v = r.v;
+        p->k = r.k;
+    } else {
+        *p = r;
+    }
+}
+
+}  // namespace ompi_amd

@@ -1,0 +1,304 @@
+// MPI_Op streaming reduction kernels for gfx950 and the op-framework handler
+// tables built on them.
+//
+// Replaces op/base's scalar loops (ompi/mca/op/base/op_base_functions.c:
+// 40-104 2-buffer, 654-731 3-buffer, tables 1485-1655).  The work is
+// HBM-bound streaming (1 op per 3*sizeof(T) bytes): every lane moves 16 B
+// per global access (global_load_dwordx4 / global_store_dwordx4), UNROLL
+// independent 16-B vectors per operand are in flight per lane, and the grid
+// is capped so every CU stays busy while blocks grid-stride.  No LDS, no
+// MFMA: nothing here is reused or contracted.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <array>
+#include <utility>
+
+#include "op_device.h"
+#include "runtime.h"
+
+namespace ompi_amd {
+
+constexpr int kOpThreads = 256;
+constexpr int kOpUnroll = 4;
+
+// dst[i] = f(x[i], y[i]).  2-buffer: x = dst = inout, y = in.
+// 3-buffer: x = in1, y = in2, dst = out.  x/dst may alias, so no restrict;
+// every lane loads all its vectors before storing any.
+template <typename T, int OP, bool THREE>
+__global__ __launch_bounds__(kOpThreads) void op_vec_kernel(const T *x, const T *y, T *dst,
+                                                            size_t nvec, size_t n) {
+    using F = opfn<OP, THREE>;
+    constexpr int E = 16 / sizeof(T);
+    constexpr size_t chunk = (size_t)kOpThreads * kOpUnroll;
+    const u32x4 *xv = reinterpret_cast<const u32x4 *>(x);
+    const u32x4 *yv = reinterpret_cast<const u32x4 *>(y);
+    u32x4 *dv = reinterpret_cast<u32x4 *>(dst);
+    const size_t stride = (size_t)gridDim.x * chunk;
+
+    for (size_t base = (size_t)blockIdx.x * chunk + threadIdx.x; base < nvec; base += stride) {
+        vec16<T> a[kOpUnroll], b[kOpUnroll];
+#pragma unroll
+        for (int u = 0; u < kOpUnroll; ++u) {
+            const size_t i = base + (size_t)u * kOpThreads;
+            if (i < nvec) {
+                a[u].v = __builtin_nontemporal_load(xv + i);
+                b[u].v = __builtin_nontemporal_load(yv + i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kOpUnroll; ++u) {
+            const size_t i = base + (size_t)u * kOpThreads;
+            if (i < nvec) {
+                vec16<T> r;
+                r.v = a[u].v;
+#pragma unroll
+                for (int e = 0; e < E; ++e) r.e[e] = F::template f<T>(a[u].e[e], b[u].e[e]);
+                if constexpr (THREE && has_gap<T>::value) {
+#pragma unroll
+                    for (int e = 0; e < E; ++e) store_elem<T, THREE>(dst + i * E + e, r.e[e]);
+                } else {
+                    __builtin_nontemporal_store(r.v, dv + i);
+                }
+            }
+        }
+    }
+    // scalar tail: elements past the last whole 16-B vector
+    if (blockIdx.x == 0) {
+        for (size_t i = nvec * E + threadIdx.x; i < n; i += kOpThreads)
+            store_elem<T, THREE>(dst + i, F::template f<T>(x[i], y[i]));
+    }
+}
+
+// Unaligned operands: one element per lane, grid-stride.
+template <typename T, int OP, bool THREE>
+__global__ __launch_bounds__(kOpThreads) void op_scalar_kernel(const T *x, const T *y, T *dst,
+                                                               size_t n) {
+    using F = opfn<OP, THREE>;
+    const size_t stride = (size_t)gridDim.x * kOpThreads;
+    for (size_t i = (size_t)blockIdx.x * kOpThreads + threadIdx.x; i < n; i += stride)
+        store_elem<T, THREE>(dst + i, F::template f<T>(x[i], y[i]));
+}
+
+static int g_max_blocks = -1;
+
+static int op_max_blocks() {
+    if (g_max_blocks < 0) {
+        const char *s = getenv("OMPI_AMD_OP_MAX_BLOCKS");
+        // 256 CUs x 8 resident 256-thread blocks
+        g_max_blocks = (s && atoi(s) > 0) ? atoi(s) : 2048;
+    }
+    return g_max_blocks;
+}
+
+template <typename T, int OP, bool THREE>
+static hipError_t launch_typed(const void *x, const void *y, void *dst, size_t n,
+                               hipStream_t s) {
+    constexpr int E = 16 / sizeof(T);
+    const bool aligned = ((((uintptr_t)x) | ((uintptr_t)y) | ((uintptr_t)dst)) & 15) == 0;
+    const size_t max_blocks = (size_t)op_max_blocks();
+    if (aligned) {
+        const size_t nvec = n / E;
+        const size_t chunk = (size_t)kOpThreads * kOpUnroll;
+        size_t blocks = (nvec + chunk - 1) / chunk;
+        if (blocks == 0) blocks = 1;
+        if (blocks > max_blocks) blocks = max_blocks;
+        hipLaunchKernelGGL((op_vec_kernel<T, OP, THREE>), dim3((unsigned)blocks), dim3(kOpThreads),
+                           0, s, (const T *)x, (const T *)y, (T *)dst, nvec, n);
+    } else {
+        size_t blocks = (n + kOpThreads - 1) / kOpThreads;
+        if (blocks > max_blocks) blocks = max_blocks;
+        hipLaunchKernelGGL((op_scalar_kernel<T, OP, THREE>), dim3((unsigned)blocks),
+                           dim3(kOpThreads), 0, s, (const T *)x, (const T *)y, (T *)dst, n);
+    }
+    return hipGetLastError();
+}
+
+// ---- (op,type) dispatch -------------------------------------------------
+template <int OP, int TYPE, bool THREE>
+static hipError_t launch_slot(const void *x, const void *y, void *dst, size_t n, hipStream_t s) {
+    if constexpr (slot_supported(OP, TYPE)) {
+        return launch_typed<typename type_of<TYPE>::type, OP, THREE>(x, y, dst, n, s);
+    } else {
+        return hipErrorInvalidValue;
+    }
+}
+
+using launch_fn = hipError_t (*)(const void *, const void *, void *, size_t, hipStream_t);
+
+template <int OP, bool THREE, int... T>
+static constexpr std::array<launch_fn, OMPI_AMD_TYPE_COUNT> make_launch_row(
+    std::integer_sequence<int, T...>) {
+    return {{(slot_supported(OP, T) ? &launch_slot<OP, T, THREE> : (launch_fn) nullptr)...}};
+}
+
+template <bool THREE, int... O>
+static constexpr std::array<std::array<launch_fn, OMPI_AMD_TYPE_COUNT>, OMPI_AMD_OP_COUNT>
+make_launch_table(std::integer_sequence<int, O...>) {
+    return {{make_launch_row<O, THREE>(std::make_integer_sequence<int, OMPI_AMD_TYPE_COUNT>{})...}};
+}
+
+static const auto g_launch2 =
+    make_launch_table<false>(std::make_integer_sequence<int, OMPI_AMD_OP_COUNT>{});
+static const auto g_launch3 =
+    make_launch_table<true>(std::make_integer_sequence<int, OMPI_AMD_OP_COUNT>{});
+
+int op_launch(int op, int type, bool three, const void *x, const void *y, void *dst,
+              size_t n, hipStream_t s) {
+    if (op < 0 || op >= OMPI_AMD_OP_COUNT || type < 0 || type >= OMPI_AMD_TYPE_COUNT)
+        return OMPI_AMD_ERR_BAD_PARAM;
+    launch_fn f = three ? g_launch3[op][type] : g_launch2[op][type];
+    if (f == nullptr) return OMPI_AMD_ERR_UNSUPPORTED;
+    if (n == 0) return OMPI_AMD_SUCCESS;
+    hipError_t e = f(x, y, dst, n, s);
+    return record_hip(e, "op kernel launch");
+}
+
+// ---- op-framework handlers ----------------------------------------------
+struct fallback_slot {
+    ompi_amd_op_handler_fn_t fn;
+    ompi_op_base_module_1_0_0_t *module;
+    ompi_amd_op_3buff_handler_fn_t fn3;
+    ompi_op_base_module_1_0_0_t *module3;
+};
+static fallback_slot g_fallback[OMPI_AMD_OP_COUNT][OMPI_AMD_TYPE_COUNT];
+
+[[noreturn]] static void handler_abort(const char *what, int op, int type) {
+    fprintf(stderr, "ompi_amd: op handler (op %d, type %d): %s: %s\n", op, type, what,
+            ompi_amd_last_error());
+    abort();
+}
+
+// kind: 1 = all device, 0 = all host, -1 = mixed
+static int buffers_kind(const void *a, const void *b, const void *c) {
+    const int da = ompi_amd_is_device_pointer(a), db = ompi_amd_is_device_pointer(b);
+    const int dc = c ? ompi_amd_is_device_pointer(c) : db;
+    if (da && db && dc) return 1;
+    if (!da && !db && !dc) return 0;
+    return -1;
+}
+
+template <int OP, int TYPE>
+static void handler2(const void *in, void *inout, int *count, ompi_datatype_t **dtype,
+                     ompi_op_base_module_1_0_0_t *module) {
+    if (*count <= 0) return;
+    const int kind = buffers_kind(in, inout, nullptr);
+    if (kind == 1) {
+        hipStream_t s = thread_stream();
+        int rc = op_launch(OP, TYPE, false, inout, in, inout, (size_t)*count, s);
+        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipStreamSynchronize(s), "op sync");
+        if (rc != OMPI_AMD_SUCCESS) handler_abort("device reduction failed", OP, TYPE);
+        return;
+    }
+    const fallback_slot &fb = g_fallback[OP][TYPE];
+    if (kind == 0 && fb.fn) { fb.fn(in, inout, count, dtype, fb.module); return; }
+    handler_abort(kind == 0 ? "host buffers and no fallback registered"
+                            : "mixed host/device buffers", OP, TYPE);
+}
+
+template <int OP, int TYPE>
+static void handler3(const void *in1, const void *in2, void *out, int *count,
+                     ompi_datatype_t **dtype, ompi_op_base_module_1_0_0_t *module) {
+    if (*count <= 0) return;
+    const int kind = buffers_kind(in1, in2, out);
+    if (kind == 1) {
+        hipStream_t s = thread_stream();
+        int rc = op_launch(OP, TYPE, true, in1, in2, out, (size_t)*count, s);
+        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipStreamSynchronize(s), "op sync");
+        if (rc != OMPI_AMD_SUCCESS) handler_abort("device reduction failed", OP, TYPE);
+        return;
+    }
+    const fallback_slot &fb = g_fallback[OP][TYPE];
+    if (kind == 0 && fb.fn3) { fb.fn3(in1, in2, out, count, dtype, fb.module3); return; }
+    handler_abort(kind == 0 ? "host buffers and no fallback registered"
+                            : "mixed host/device buffers", OP, TYPE);
+}
+
+template <int OP, int... T>
+static constexpr std::array<ompi_amd_op_handler_fn_t, OMPI_AMD_TYPE_COUNT> make_h2_row(
+    std::integer_sequence<int, T...>) {
+    return {{(slot_supported(OP, T) ? &handler2<OP, T> : (ompi_amd_op_handler_fn_t) nullptr)...}};
+}
+template <int OP, int... T>
+static constexpr std::array<ompi_amd_op_3buff_handler_fn_t, OMPI_AMD_TYPE_COUNT> make_h3_row(
+    std::integer_sequence<int, T...>) {
+    return {{(slot_supported(OP, T) ? &handler3<OP, T>
+                                    : (ompi_amd_op_3buff_handler_fn_t) nullptr)...}};
+}
+template <int... O>
+static constexpr std::array<std::array<ompi_amd_op_handler_fn_t, OMPI_AMD_TYPE_COUNT>,
+                            OMPI_AMD_OP_COUNT>
+make_h2_table(std::integer_sequence<int, O...>) {
+    return {{make_h2_row<O>(std::make_integer_sequence<int, OMPI_AMD_TYPE_COUNT>{})...}};
+}
+template <int... O>
+static constexpr std::array<std::array<ompi_amd_op_3buff_handler_fn_t, OMPI_AMD_TYPE_COUNT>,
+                            OMPI_AMD_OP_COUNT>
+make_h3_table(std::integer_sequence<int, O...>) {
+    return {{make_h3_row<O>(std::make_integer_sequence<int, OMPI_AMD_TYPE_COUNT>{})...}};
+}
+static const auto g_h2 = make_h2_table(std::make_integer_sequence<int, OMPI_AMD_OP_COUNT>{});
+static const auto g_h3 = make_h3_table(std::make_integer_sequence<int, OMPI_AMD_OP_COUNT>{});
+
+}  // namespace ompi_amd
+
+using namespace ompi_amd;
+
+extern "C" {
+
+int ompi_amd_op_supported(int op, int type) {
+    if (op < 0 || op >= OMPI_AMD_OP_COUNT || type < 0 || type >= OMPI_AMD_TYPE_COUNT) return 0;
+    return g_launch2[op][type] != nullptr;
+}
+
+size_t ompi_amd_type_extent(int type) {
+    switch (type) {
+    case OMPI_AMD_TYPE_INT8_T: case OMPI_AMD_TYPE_UINT8_T: case OMPI_AMD_TYPE_BOOL:
+    case OMPI_AMD_TYPE_BYTE: return 1;
+    case OMPI_AMD_TYPE_INT16_T: case OMPI_AMD_TYPE_UINT16_T: return 2;
+    case OMPI_AMD_TYPE_INT32_T: case OMPI_AMD_TYPE_UINT32_T: case OMPI_AMD_TYPE_FLOAT: return 4;
+    case OMPI_AMD_TYPE_INT64_T: case OMPI_AMD_TYPE_UINT64_T: case OMPI_AMD_TYPE_DOUBLE: return 8;
+    case OMPI_AMD_TYPE_FLOAT_INT: return sizeof(float_int_t);
+    case OMPI_AMD_TYPE_DOUBLE_INT: return sizeof(double_int_t);
+    case OMPI_AMD_TYPE_LONG_INT: return sizeof(long_int_t);
+    case OMPI_AMD_TYPE_2INT: return sizeof(two_int_t);
+    case OMPI_AMD_TYPE_SHORT_INT: return sizeof(short_int_t);
+    default: return 0;
+    }
+}
+
+int ompi_amd_op_reduce(int op, int type, const void *in, void *inout, size_t count,
+                       void *stream) {
+    if (count && (!in || !inout)) return OMPI_AMD_ERR_BAD_PARAM;
+    return op_launch(op, type, false, inout, in, inout, count, as_stream(stream));
+}
+
+int ompi_amd_op_reduce_3buff(int op, int type, const void *in1, const void *in2, void *out,
+                             size_t count, void *stream) {
+    if (count && (!in1 || !in2 || !out)) return OMPI_AMD_ERR_BAD_PARAM;
+    return op_launch(op, type, true, in1, in2, out, count, as_stream(stream));
+}
+
+const ompi_amd_op_handler_fn_t *ompi_amd_op_handler_row(int op) {
+    if (op < 0 || op >= OMPI_AMD_OP_COUNT) return nullptr;
+    return g_h2[op].data();
+}
+
+const ompi_amd_op_3buff_handler_fn_t *ompi_amd_op_3buff_handler_row(int op) {
+    if (op < 0 || op >= OMPI_AMD_OP_COUNT) return nullptr;
+    return g_h3[op].data();
+}
+
+int ompi_amd_op_set_fallback(int op, int type, ompi_amd_op_handler_fn_t fn,
+                             ompi_op_base_module_1_0_0_t *module,
+                             ompi_amd_op_3buff_handler_fn_t fn3,
+                             ompi_op_base_module_1_0_0_t *module3) {
+    if (op < 0 || op >= OMPI_AMD_OP_COUNT || type < 0 || type >= OMPI_AMD_TYPE_COUNT)
+        return OMPI_AMD_ERR_BAD_PARAM;
+    g_fallback[op][type] = {fn, module, fn3, module3};
+    return OMPI_AMD_SUCCESS;
+}
+
+}  // extern "C"

@@ -1,0 +1,67 @@
+// Host runtime helpers: error capture, per-thread streams, pointer queries.
+#include "runtime.h"
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+namespace ompi_amd {
+
+static thread_local char tls_err[512] = "";
+static thread_local hipStream_t tls_stream = nullptr;
+
+int record_hip(hipError_t e, const char *what) {
+    if (e == hipSuccess) return OMPI_AMD_SUCCESS;
+    snprintf(tls_err, sizeof(tls_err), "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+    return OMPI_AMD_ERR_HIP;
+}
+
+void record_msg(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(tls_err, sizeof(tls_err), fmt, ap);
+    va_end(ap);
+}
+
+hipStream_t thread_stream() { return tls_stream ? tls_stream : hipStreamPerThread; }
+
+}  // namespace ompi_amd
+
+using namespace ompi_amd;
+
+extern "C" {
+
+const char *ompi_amd_version(void) { return "ompi_amd 0.1 gfx950"; }
+
+const char *ompi_amd_last_error(void) { return tls_err; }
+
+int ompi_amd_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+int ompi_amd_set_thread_stream(void *stream) {
+    tls_stream = static_cast<hipStream_t>(stream);
+    return OMPI_AMD_SUCCESS;
+}
+
+// hipPointerGetAttributes: device and managed memory run on the GPU;
+// anything else (pageable or pinned host) is host memory for the handlers
+// (common_cuda.c:1739-1792 counterpart).
+int ompi_amd_is_device_pointer(const void *ptr) {
+    if (ptr == nullptr) return 0;
+    hipPointerAttribute_t attr;
+    memset(&attr, 0, sizeof(attr));
+    hipError_t e = hipPointerGetAttributes(&attr, ptr);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // unregistered host memory
+        return 0;
+    }
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+}  // extern "C"

@@ -1,0 +1,25 @@
+// Shared host-side runtime helpers of libompi_amd.so (error capture, streams).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/ompi_amd.h"
+
+namespace ompi_amd {
+
+// Record a HIP error (thread-local message) and map it to a status code.
+int record_hip(hipError_t e, const char *what);
+// Record a non-HIP failure message.
+void record_msg(const char *fmt, ...);
+
+// The stream handlers of this thread run on (ompi_amd_set_thread_stream).
+hipStream_t thread_stream();
+// `void *` stream argument of the C ABI -> hipStream_t (NULL = per-thread).
+inline hipStream_t as_stream(void *s) {
+    return s ? static_cast<hipStream_t>(s) : hipStreamPerThread;
+}
+
+int op_launch(int op, int type, bool three, const void *x, const void *y, void *dst,
+              size_t n, hipStream_t s);
+
+}  // namespace ompi_amd

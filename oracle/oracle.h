@@ -1,0 +1,115 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's reduction-collective hot path, used by
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as the
+ * CHECKER.  Nothing in ompi_amd/ (the product) links, loads or calls this.
+ *
+ * Pinned against: the reference's own known-answer tests
+ * (test/datatype/reduce_local.c, test/datatype/check_op.sh,
+ * test/datatype/ddt_test.c, test/datatype/opal_datatype_test.c) restated as
+ * fixtures in tests/golden/, and the reference executions recorded in
+ * SURVEY.md §8(c) (op/base NaN / ±0 / MAXLOC tie behaviour, ring and
+ * recursive-doubling summation orders).  See DESIGN.md "Oracle".
+ *
+ * Codes follow the reference enums so fixtures can be read against it:
+ *   op   = OMPI_OP_BASE_FORTRAN_*  (ompi/mca/op/op.h:203-237)
+ *   type = OMPI_OP_BASE_TYPE_*     (ompi/mca/op/op.h:104-190)
+ */
+#ifndef OMPI_AMD_ORACLE_H
+#define OMPI_AMD_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* op codes (Fortran index, ompi/mca/op/op.h:203-237) */
+enum {
+    ORC_OP_NULL = 0, ORC_OP_MAX, ORC_OP_MIN, ORC_OP_SUM, ORC_OP_PROD,
+    ORC_OP_LAND, ORC_OP_BAND, ORC_OP_LOR, ORC_OP_BOR, ORC_OP_LXOR,
+    ORC_OP_BXOR, ORC_OP_MAXLOC, ORC_OP_MINLOC, ORC_OP_REPLACE, ORC_OP_NO_OP,
+    ORC_OP_COUNT
+};
+
+/* type codes (ompi/mca/op/op.h:104-190); only the predefined C types this
+ * oracle restates are named. */
+enum {
+    ORC_T_INT8 = 0, ORC_T_UINT8 = 1, ORC_T_INT16 = 2, ORC_T_UINT16 = 3,
+    ORC_T_INT32 = 4, ORC_T_UINT32 = 5, ORC_T_INT64 = 6, ORC_T_UINT64 = 7,
+    ORC_T_FLOAT = 15, ORC_T_DOUBLE = 16, ORC_T_BOOL = 25, ORC_T_BYTE = 30,
+    ORC_T_FLOAT_INT = 34, ORC_T_DOUBLE_INT = 35, ORC_T_LONG_INT = 36,
+    ORC_T_2INT = 37, ORC_T_SHORT_INT = 38,
+    ORC_T_COUNT = 41
+};
+
+/* ---- op/base restatement (ompi/mca/op/base/op_base_functions.c) ---- */
+/* 1 if the reference's op/base table has a handler for (op,type) AND this
+ * oracle restates it. */
+int    orc_op_defined(int op, int type);
+/* bytes between consecutive elements (the datatype extent) */
+size_t orc_type_extent(int type);
+/* 2-buffer: inout[i] = inout[i] (op) in[i]   (OP_FUNC/FUNC_FUNC/LOC_FUNC) */
+int    orc_op_2buff(int op, int type, const void *in, void *inout, size_t count);
+/* 3-buffer: out[i] = in1[i] (op) in2[i]      (*_3BUF macros) */
+int    orc_op_3buff(int op, int type, const void *in1, const void *in2,
+                    void *out, size_t count);
+
+/* ---- coll/base allreduce restatement (coll_base_allreduce.c) ---- */
+enum {
+    ORC_AR_TUNED = 0,              /* coll_tuned_decision_fixed.c:45-89 */
+    ORC_AR_RECURSIVE_DOUBLING = 3, /* coll_base_allreduce.c:130-274 */
+    ORC_AR_RING = 4,               /* coll_base_allreduce.c:341-536 */
+    ORC_AR_RING_SEGMENTED = 5,     /* coll_base_allreduce.c:618-856 */
+    ORC_AR_REDSCAT_ALLGATHER = 6   /* coll_base_allreduce.c:970-1243 */
+};
+/* Simulates the algorithm's message flow over `nranks` in-memory ranks.
+ * sbufs[r] is rank r's send buffer, rbufs[r] its receive buffer (both
+ * count*extent bytes).  Returns the algorithm actually run (tuned resolves
+ * to 3/4/5), or <0 on error. */
+int orc_allreduce(int algorithm, int nranks, const void *const *sbufs,
+                  void *const *rbufs, size_t count, int op, int type,
+                  size_t segsize);
+
+/* Block partition COLL_BASE_COMPUTE_BLOCKCOUNT (coll_base_functions.h:425-431) */
+void orc_blockcount(size_t count, int nblocks, size_t *split,
+                    size_t *early, size_t *late);
+
+/* reduce_scatter_block / allgather / bcast reference results (data
+ * movement; reduce order = rank order 0..N-1 folded with 2-buffer op). */
+int orc_reduce_scatter_block(int nranks, const void *const *sbufs,
+                             void *const *rbufs, size_t rcount, int op, int type);
+int orc_allgather(int nranks, const void *const *sbufs, void *const *rbufs,
+                  size_t bytes_per_rank);
+int orc_bcast(int nranks, int root, void *const *bufs, size_t bytes);
+
+/* ---- opal_datatype convertor restatement (opal/datatype/) ---- */
+/* A committed datatype flattened to its typemap: nblocks contiguous byte
+ * runs {disp, len} in typemap order, repeated every `extent` bytes. */
+typedef struct {
+    int64_t disp;
+    int64_t len;
+} orc_block_t;
+
+/* pack bytes [offset, offset+bytes) of the packed stream of `count`
+ * elements at `src` into `dst` (opal_generic_simple_pack semantics for a
+ * homogeneous convertor; stream position == bConverted). Returns bytes
+ * packed (truncated at the stream end). */
+size_t orc_pack(const orc_block_t *blocks, int nblocks, int64_t extent,
+                size_t count, const void *src, void *dst, size_t offset,
+                size_t bytes);
+/* inverse of orc_pack (opal_generic_simple_unpack) */
+size_t orc_unpack(const orc_block_t *blocks, int nblocks, int64_t extent,
+                  size_t count, const void *src, void *dst, size_t offset,
+                  size_t bytes);
+
+/* ---- CPU baseline helper: op loop timing (bench.py cpu_baseline) ---- */
+double orc_time_op_3buff(int op, int type, const void *in1, const void *in2,
+                         void *out, size_t count, int iters);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

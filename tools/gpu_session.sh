@@ -1,0 +1,27 @@
+#!/bin/bash
+# Run a sequence of GPU steps on the gpurun box.  Each step has its own time
+# limit; a step that faults, aborts or times out ends the session (no later
+# GPU step runs).  A step that merely fails (e.g. pytest assertion, exit 1)
+# is logged and the session continues.
+# usage: tools/gpu_session.sh "<name>:<seconds>:<command>" ...
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+status=0
+for spec in "$@"; do
+    name="${spec%%:*}"; rest="${spec#*:}"
+    secs="${rest%%:*}"; cmd="${rest#*:}"
+    echo "=== [$name] (limit ${secs}s): $cmd" | tee -a gpurun_out/session.log
+    start=$(date +%s)
+    timeout -k 10 "$secs" bash -c "$cmd" > "gpurun_out/$name.log" 2>&1
+    rc=$?
+    echo "=== [$name] rc=$rc in $(( $(date +%s) - start ))s" | tee -a gpurun_out/session.log
+    tail -n 5 "gpurun_out/$name.log"
+    case $rc in
+        0) ;;
+        1|2|5) status=1 ;;                     # failures, not faults
+        *) echo "=== stopping: step $name ended with $rc" | tee -a gpurun_out/session.log
+           exit $rc ;;
+    esac
+done
+exit $status
