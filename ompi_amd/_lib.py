@@ -72,10 +72,12 @@ PROTOTYPES = [
     ("ompi_amd_op_set_fallback", _C.c_int,
      [_C.c_int, _C.c_int, _C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_void_p]),
     ("ompi_amd_set_thread_stream", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_set_tuning", _C.c_int, [_C.c_char_p, _C.c_int64]),
     ("ompi_amd_ddt_create", _C.c_int,
      [_C.POINTER(DdtBlock), _C.c_int, _C.c_int64, _C.POINTER(_C.c_void_p)]),
     ("ompi_amd_ddt_destroy", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_ddt_size", _C.c_size_t, [_C.c_void_p]),
+    ("ompi_amd_ddt_nelems", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_ddt_pack", _C.c_int,
      [_C.c_void_p, _C.c_size_t, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_size_t,
       _C.POINTER(_C.c_size_t), _C.c_void_p]),

@@ -1,0 +1,264 @@
+// Datatype pack/unpack for device buffers (gfx950).
+//
+// The reference walks opt_desc on the host and issues one memcpy — for
+// device memory one cuMemcpy — per contiguous run (opal_datatype_pack.h:
+// 37-206, opal_datatype_cuda.c:121-145).  Here a datatype becomes a small
+// device program of {count, blocklen, stride, disp} elements (the shape of
+// opal's ddt_elem_desc, opal_datatype_internal.h:157-164) staged in LDS, and
+// one launch moves a whole convertor window: every lane owns G-byte
+// granules of the packed stream (G = the widest power of two <= 16 that
+// divides every run, displacement and stride, so a granule never crosses a
+// run), maps its stream position to the typed address with two integer
+// divisions, and copies G bytes.  Packed-side accesses are contiguous across
+// lanes (coalesced dwordx4 at G = 16); typed-side accesses are as contiguous
+// as the datatype allows.  HBM-bound: 2 x packed bytes of algorithmic
+// traffic.  A window that starts or ends off the granule grid is handled
+// with byte granules for its unaligned head and tail.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/ompi_amd_ddt.h"
+#include "runtime.h"
+
+namespace ompi_amd {
+
+struct ddt_elem {
+    int64_t count;   // repetitions
+    int64_t blen;    // bytes per repetition
+    int64_t stride;  // bytes between repetitions
+    int64_t disp;    // byte displacement of the first repetition
+    int64_t prefix;  // packed bytes of the type before this element
+};
+
+constexpr int kDdtThreads = 256;
+constexpr int kDdtLdsElems = 256;
+
+struct ddt_desc {
+    const ddt_elem *elems;  // device copy
+    int nelem;
+    int64_t size;    // packed bytes per datatype element
+    int64_t extent;
+};
+
+// Largest i with elems[i].prefix <= q.
+__device__ __forceinline__ int find_elem(const ddt_elem *e, int n, int64_t q) {
+    if (n <= 8) {
+        int i = 0;
+        for (int j = 1; j < n; ++j)
+            if (e[j].prefix <= q) i = j;
+        return i;
+    }
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (e[mid].prefix <= q) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+template <int G> struct granule;
+template <> struct granule<1> { using t = uint8_t; };
+template <> struct granule<2> { using t = uint16_t; };
+template <> struct granule<4> { using t = uint32_t; };
+template <> struct granule<8> { using t = uint64_t; };
+template <> struct granule<16> { typedef unsigned int t __attribute__((ext_vector_type(4))); };
+
+// Typed-layout byte address of packed stream position p.
+template <typename I>
+__device__ __forceinline__ int64_t typed_offset(const ddt_elem *e, int n, I size, int64_t extent,
+                                                I p) {
+    const I el = p / size;
+    const I q = p - el * size;
+    const int i = find_elem(e, n, (int64_t)q);
+    const I r = q - (I)e[i].prefix;
+    const I k = r / (I)e[i].blen;
+    const I w = r - k * (I)e[i].blen;
+    return (int64_t)el * extent + e[i].disp + (int64_t)k * e[i].stride + (int64_t)w;
+}
+
+// UNPACK = false: dst[p - start] = typed[p];  true: typed[p] = src[p - start].
+// Granules cover stream positions [start + j*G, ...), j < ngran.
+template <int G, bool UNPACK, typename I>
+__global__ __launch_bounds__(kDdtThreads) void ddt_kernel(ddt_desc d, const char *src, char *dst,
+                                                          int64_t start, int64_t ngran,
+                                                          int64_t packed_base) {
+    __shared__ ddt_elem lds[kDdtLdsElems];
+    const ddt_elem *el = d.elems;
+    if (d.nelem <= kDdtLdsElems) {
+        for (int i = threadIdx.x; i < d.nelem; i += kDdtThreads) lds[i] = d.elems[i];
+        __syncthreads();
+        el = lds;
+    }
+    using T = typename granule<G>::t;
+    const int64_t stride = (int64_t)gridDim.x * kDdtThreads;
+    for (int64_t j = (int64_t)blockIdx.x * kDdtThreads + threadIdx.x; j < ngran; j += stride) {
+        const int64_t p = start + j * G;
+        const int64_t t = typed_offset<I>(el, d.nelem, (I)d.size, d.extent, (I)p);
+        const int64_t c = p - packed_base;  // offset in the contiguous buffer
+        if (!UNPACK) {
+            *reinterpret_cast<T *>(dst + c) = *reinterpret_cast<const T *>(src + t);
+        } else {
+            *reinterpret_cast<T *>(dst + t) = *reinterpret_cast<const T *>(src + c);
+        }
+    }
+}
+
+}  // namespace ompi_amd
+
+struct ompi_amd_ddt {
+    std::vector<ompi_amd::ddt_elem> host;
+    ompi_amd::ddt_elem *dev = nullptr;
+    int64_t size = 0;
+    int64_t extent = 0;
+    int gran = 1;  // power of two dividing every blen, disp, stride, extent
+};
+
+namespace ompi_amd {
+
+static int pow2_gran(uint64_t v) {
+    int g = 16;
+    while (g > 1 && (v % (uint64_t)g) != 0) g >>= 1;
+    return g;
+}
+
+template <bool UNPACK, typename I>
+static hipError_t launch_g(int G, const ddt_desc &d, const char *src, char *dst, int64_t start,
+                           int64_t ngran, int64_t base, hipStream_t s) {
+    if (ngran <= 0) return hipSuccess;
+    int64_t blocks = (ngran + kDdtThreads - 1) / kDdtThreads;
+    blocks = std::min<int64_t>(blocks, 4096);
+    const dim3 grid((unsigned)blocks), block(kDdtThreads);
+    switch (G) {
+    case 16: hipLaunchKernelGGL((ddt_kernel<16, UNPACK, I>), grid, block, 0, s, d, src, dst, start, ngran, base); break;
+    case 8: hipLaunchKernelGGL((ddt_kernel<8, UNPACK, I>), grid, block, 0, s, d, src, dst, start, ngran, base); break;
+    case 4: hipLaunchKernelGGL((ddt_kernel<4, UNPACK, I>), grid, block, 0, s, d, src, dst, start, ngran, base); break;
+    case 2: hipLaunchKernelGGL((ddt_kernel<2, UNPACK, I>), grid, block, 0, s, d, src, dst, start, ngran, base); break;
+    default: hipLaunchKernelGGL((ddt_kernel<1, UNPACK, I>), grid, block, 0, s, d, src, dst, start, ngran, base); break;
+    }
+    return hipGetLastError();
+}
+
+template <bool UNPACK>
+static int ddt_run(const ompi_amd_ddt_t *ddt, size_t count, const void *typed, void *contig,
+                   size_t offset, size_t bytes, size_t *done, hipStream_t s) {
+    if (!ddt || (!typed && count) || !done) return OMPI_AMD_ERR_BAD_PARAM;
+    const uint64_t total = (uint64_t)ddt->size * count;
+    *done = 0;
+    if (offset >= total || bytes == 0) return OMPI_AMD_SUCCESS;
+    if (bytes > total - offset) bytes = (size_t)(total - offset);
+    if (!contig) return OMPI_AMD_ERR_BAD_PARAM;
+
+    ddt_desc d{ddt->dev, (int)ddt->host.size(), ddt->size, ddt->extent};
+    // Granule: divides the type program, the typed base and the contiguous
+    // buffer's alignment relative to the stream position.
+    const uint64_t contig_skew = (uint64_t)((uintptr_t)contig - (uintptr_t)offset);
+    int G = std::min({ddt->gran, pow2_gran((uintptr_t)typed), pow2_gran(contig_skew)});
+    const int64_t start = (int64_t)offset, end = (int64_t)(offset + bytes);
+    const int64_t body0 = (start + G - 1) / G * G;
+    const int64_t body1 = std::max(body0, end / G * G);
+    // contiguous buffer is indexed from `offset`: pass base = offset
+    const char *tsrc = UNPACK ? (const char *)contig : (const char *)typed;
+    char *tdst = UNPACK ? (char *)typed : (char *)contig;
+    hipError_t e = hipSuccess;
+    const bool small = total < (1ull << 31);
+    auto go = [&](int g, int64_t from, int64_t to) {
+        if (e != hipSuccess || to <= from) return;
+        const int64_t ng = (to - from) / g;
+        e = small ? launch_g<UNPACK, uint32_t>(g, d, tsrc, tdst, from, ng, start, s)
+                  : launch_g<UNPACK, uint64_t>(g, d, tsrc, tdst, from, ng, start, s);
+    };
+    if (body0 >= end) {
+        go(1, start, end);
+    } else {
+        go(1, start, body0);
+        go(G, body0, body1);
+        go(1, body1, end);
+    }
+    if (e != hipSuccess) return record_hip(e, "ddt kernel launch");
+    *done = bytes;
+    return OMPI_AMD_SUCCESS;
+}
+
+}  // namespace ompi_amd
+
+using namespace ompi_amd;
+
+extern "C" {
+
+int ompi_amd_ddt_create(const ompi_amd_ddt_block_t *blocks, int nblocks, int64_t extent,
+                        ompi_amd_ddt_t **out) {
+    if (!out || nblocks <= 0 || !blocks) return OMPI_AMD_ERR_BAD_PARAM;
+    // 1) merge runs that touch (disp_i + len_i == disp_{i+1})
+    std::vector<ompi_amd_ddt_block_t> runs;
+    for (int i = 0; i < nblocks; ++i) {
+        if (blocks[i].len <= 0) return OMPI_AMD_ERR_BAD_PARAM;
+        if (!runs.empty() && runs.back().disp + runs.back().len == blocks[i].disp)
+            runs.back().len += blocks[i].len;
+        else
+            runs.push_back(blocks[i]);
+    }
+    // 2) fold equal-length runs at a constant stride into one element
+    auto *d = new (std::nothrow) ompi_amd_ddt;
+    if (!d) return OMPI_AMD_ERR_BAD_PARAM;
+    int64_t prefix = 0;
+    uint64_t gcd_acc = (uint64_t)(extent < 0 ? -extent : extent);
+    for (size_t i = 0; i < runs.size();) {
+        ddt_elem e{1, runs[i].len, runs[i].len, runs[i].disp, prefix};
+        size_t j = i + 1;
+        if (j < runs.size() && runs[j].len == e.blen) {
+            const int64_t st = runs[j].disp - runs[i].disp;
+            while (j < runs.size() && runs[j].len == e.blen &&
+                   runs[j].disp - runs[j - 1].disp == st) ++j;
+            e.count = (int64_t)(j - i);
+            e.stride = st;
+        }
+        prefix += e.count * e.blen;
+        gcd_acc |= (uint64_t)e.blen | (uint64_t)(e.disp < 0 ? -e.disp : e.disp) |
+                   (uint64_t)(e.stride < 0 ? -e.stride : e.stride);
+        d->host.push_back(e);
+        i = j;
+    }
+    d->size = prefix;
+    d->extent = extent;
+    d->gran = pow2_gran(gcd_acc);
+    const size_t nb = d->host.size() * sizeof(ddt_elem);
+    hipError_t err = hipMalloc(&d->dev, nb);
+    if (err == hipSuccess) err = hipMemcpy(d->dev, d->host.data(), nb, hipMemcpyHostToDevice);
+    if (err != hipSuccess) {
+        int rc = record_hip(err, "ddt descriptor upload");
+        if (d->dev) (void)hipFree(d->dev);
+        delete d;
+        return rc;
+    }
+    *out = d;
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_ddt_destroy(ompi_amd_ddt_t *ddt) {
+    if (!ddt) return OMPI_AMD_SUCCESS;
+    if (ddt->dev) (void)hipFree(ddt->dev);
+    delete ddt;
+    return OMPI_AMD_SUCCESS;
+}
+
+size_t ompi_amd_ddt_size(const ompi_amd_ddt_t *ddt) { return ddt ? (size_t)ddt->size : 0; }
+
+int ompi_amd_ddt_nelems(const ompi_amd_ddt_t *ddt) { return ddt ? (int)ddt->host.size() : 0; }
+
+int ompi_amd_ddt_pack(const ompi_amd_ddt_t *ddt, size_t count, const void *src, void *dst,
+                      size_t offset, size_t bytes, size_t *done, void *stream) {
+    return ddt_run<false>(ddt, count, src, dst, offset, bytes, done, as_stream(stream));
+}
+
+int ompi_amd_ddt_unpack(const ompi_amd_ddt_t *ddt, size_t count, const void *src, void *dst,
+                        size_t offset, size_t bytes, size_t *done, void *stream) {
+    return ddt_run<true>(ddt, count, dst, (void *)src, offset, bytes, done, as_stream(stream));
+}
+
+}  // extern "C"

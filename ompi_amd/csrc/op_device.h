@@ -13,6 +13,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "../../include/ompi_amd.h"
@@ -134,8 +135,11 @@ template <typename T> union vec16 {
 template <typename T, bool THREE>
 __device__ __forceinline__ void store_elem(T *p, const T &r) {
     if constexpr (THREE && has_gap<T>::value) {
-        p->v = r.v;
-        p->k = r.k;
+        // byte-addressed member stores: the compiler may not widen them over
+        // the gap the way it may for member stores of the struct type
+        char *c = reinterpret_cast<char *>(p);
+        __builtin_memcpy(c + offsetof(T, v), &r.v, sizeof(r.v));
+        __builtin_memcpy(c + offsetof(T, k), &r.k, sizeof(r.k));
     } else {
         *p = r;
     }

@@ -21,8 +21,35 @@
 
 namespace ompi_amd {
 
+// Build-time tuning knobs (tools/op_tune.py builds variants; the defaults
+// are the measured best on MI355X, see DESIGN.md "op kernel").
+#ifndef OMPI_AMD_OP_UNROLL
+#define OMPI_AMD_OP_UNROLL 4
+#endif
+#ifndef OMPI_AMD_OP_NT_LOADS
+#define OMPI_AMD_OP_NT_LOADS 1
+#endif
+#ifndef OMPI_AMD_OP_NT_STORES
+#define OMPI_AMD_OP_NT_STORES 1
+#endif
 constexpr int kOpThreads = 256;
-constexpr int kOpUnroll = 4;
+constexpr int kOpUnroll = OMPI_AMD_OP_UNROLL;
+
+__device__ __forceinline__ u32x4 ld16(const u32x4 *p) {
+#if OMPI_AMD_OP_NT_LOADS
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
+__device__ __forceinline__ void st16(u32x4 *p, u32x4 v) {
+#if OMPI_AMD_OP_NT_STORES
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
 
 // dst[i] = f(x[i], y[i]).  2-buffer: x = dst = inout, y = in.
 // 3-buffer: x = in1, y = in2, dst = out.  x/dst may alias, so no restrict;
@@ -44,8 +71,8 @@ __global__ __launch_bounds__(kOpThreads) void op_vec_kernel(const T *x, const T 
         for (int u = 0; u < kOpUnroll; ++u) {
             const size_t i = base + (size_t)u * kOpThreads;
             if (i < nvec) {
-                a[u].v = __builtin_nontemporal_load(xv + i);
-                b[u].v = __builtin_nontemporal_load(yv + i);
+                a[u].v = ld16(xv + i);
+                b[u].v = ld16(yv + i);
             }
         }
 #pragma unroll
@@ -60,7 +87,7 @@ __global__ __launch_bounds__(kOpThreads) void op_vec_kernel(const T *x, const T 
 #pragma unroll
                     for (int e = 0; e < E; ++e) store_elem<T, THREE>(dst + i * E + e, r.e[e]);
                 } else {
-                    __builtin_nontemporal_store(r.v, dv + i);
+                    st16(dv + i, r.v);
                 }
             }
         }
@@ -91,6 +118,12 @@ static int op_max_blocks() {
         g_max_blocks = (s && atoi(s) > 0) ? atoi(s) : 2048;
     }
     return g_max_blocks;
+}
+
+int op_set_max_blocks(int64_t v) {
+    if (v <= 0 || v > (1 << 24)) return OMPI_AMD_ERR_BAD_PARAM;
+    g_max_blocks = (int)v;
+    return OMPI_AMD_SUCCESS;
 }
 
 template <typename T, int OP, bool THREE>

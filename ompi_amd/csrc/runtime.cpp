@@ -44,6 +44,13 @@ int ompi_amd_device_count(void) {
     return n;
 }
 
+int ompi_amd_set_tuning(const char *key, int64_t value) {
+    if (!key) return OMPI_AMD_ERR_BAD_PARAM;
+    if (strcmp(key, "op_max_blocks") == 0) return op_set_max_blocks(value);
+    record_msg("unknown tuning key '%s'", key);
+    return OMPI_AMD_ERR_BAD_PARAM;
+}
+
 int ompi_amd_set_thread_stream(void *stream) {
     tls_stream = static_cast<hipStream_t>(stream);
     return OMPI_AMD_SUCCESS;

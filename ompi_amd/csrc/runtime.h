@@ -19,6 +19,7 @@ inline hipStream_t as_stream(void *s) {
     return s ? static_cast<hipStream_t>(s) : hipStreamPerThread;
 }
 
+int op_set_max_blocks(int64_t v);
 int op_launch(int op, int type, bool three, const void *x, const void *y, void *dst,
               size_t n, hipStream_t s);
 
