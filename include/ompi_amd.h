@@ -121,7 +121,7 @@ int ompi_amd_op_set_fallback(int op, int type, ompi_amd_op_handler_fn_t fn,
 
 /* Process-wide tuning knobs, the MCA-parameter surface of the component
  * (op_rocm_max_blocks ...).  Keys: "op_max_blocks" (grid cap of the
- * streaming op kernels, default 2048 = 256 CUs x 8). */
+ * streaming op kernels; default: uncapped, one chunk per workgroup). */
 int ompi_amd_set_tuning(const char *key, int64_t value);
 
 /* Stream the handlers of the calling thread use (NULL = per-thread). */

@@ -1,0 +1,90 @@
+/*
+ * ompi_amd — device-buffer collectives over xGMI (one process per GPU, one
+ * node).  Replaces coll/tuned's functions for device buffers behind the
+ * coll framework's module table (ompi/mca/coll/coll.h:200-247):
+ *
+ *   coll_allreduce            coll.h:208-210  (tuned: coll_tuned_decision_fixed.c:45-89)
+ *   coll_reduce_scatter_block coll.h:245-247  (tuned: :522-532)
+ *   coll_allgather            coll.h:200-203  (tuned: :543-600)
+ *   coll_bcast                coll.h:225-227  (tuned: :234-300)
+ *
+ * Data moves by kernels that load peer memory mapped with
+ * hipIpcOpenMemHandle (replacing the PML/BTL path and the CUDA IPC
+ * handshake of btl/smcuda, btl_smcuda.c:1077-1250), with the reduction
+ * fused into the load.  Peers synchronise through device-scope flags in
+ * IPC-mapped memory; the only host rendezvous is a POSIX shared-memory
+ * segment used to swap IPC handles (bootstrap, and per call for
+ * zero-copy user buffers).
+ *
+ * Results: ring / ring_segmented summation order for >= 10000-byte
+ * allreduces and the recursive-doubling tree below (so fp results are
+ * bit-identical to coll/tuned + op/base); basic_linear order for
+ * reduce_scatter_block.
+ */
+#ifndef OMPI_AMD_COLL_H
+#define OMPI_AMD_COLL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OMPI_AMD_MAX_RANKS 16
+
+typedef struct ompi_amd_comm ompi_amd_comm_t;
+
+/* Collective over the `size` ranks of one node.  `name` identifies the
+ * communicator node-wide and must be unique per job (e.g. "<jobid>.<cid>");
+ * it names the POSIX shared-memory rendezvous segment.  `device` is this
+ * rank's HIP device.  Every rank calls it with the same name and size. */
+int ompi_amd_comm_create(const char *name, int rank, int size, int device,
+                         ompi_amd_comm_t **comm);
+/* Collective: every rank must call it. */
+int ompi_amd_comm_destroy(ompi_amd_comm_t *comm);
+int ompi_amd_comm_rank(const ompi_amd_comm_t *comm);
+int ompi_amd_comm_size(const ompi_amd_comm_t *comm);
+
+/* MCA-parameter surface (coll_rocm_*):
+ *   "small_bytes"   messages up to this size go through the staged path
+ *                   (copy into the IPC scratch, no host rendezvous);
+ *                   default 1 MiB, capped at the scratch size
+ *   "zero_copy"     1 (default): large messages read peers' user buffers
+ *                   directly; 0: always stage through the scratch
+ *   "timeout_ms"    device spin limit per barrier (default 30000)
+ *   "blocks"        grid cap of the transfer kernels (default 1024) */
+int ompi_amd_comm_set_param(ompi_amd_comm_t *comm, const char *key, int64_t value);
+
+/* Sticky error of the device side (a barrier that timed out, ...).
+ * 0 = none, else an OMPI_AMD_ERR_* code.  Reading it does not sync. */
+int ompi_amd_comm_error(const ompi_amd_comm_t *comm);
+
+/* The ring block partition and ownership the allreduce uses (host-only,
+ * no GPU needed): block b covers elements [off, off+cnt) of the vector
+ * (COLL_BASE_COMPUTE_BLOCKCOUNT, coll_base_functions.h:425-431) and is
+ * produced by rank (b - 1) mod size — where the reference's ring finishes
+ * it (coll_base_allreduce.c:478-492). */
+int ompi_amd_coll_block(size_t count, int size, int block, size_t *off, size_t *cnt);
+int ompi_amd_coll_owner(int size, int block);
+
+/* MPI_IN_PLACE is spelled sbuf == rbuf or sbuf == (void *)1.
+ * Stream-ordered: results are valid when `stream` reaches this point; the
+ * caller keeps every rank's buffers alive until then.  All ranks must call
+ * with matching arguments, in the same order. */
+int ompi_amd_allreduce(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
+                       size_t count, int type, int op, void *stream);
+/* rbuf receives block `rank` (rcount elements) of the element-wise
+ * reduction of the size*rcount element sbufs. */
+int ompi_amd_reduce_scatter_block(ompi_amd_comm_t *comm, const void *sbuf,
+                                  void *rbuf, size_t rcount, int type, int op,
+                                  void *stream);
+int ompi_amd_allgather(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
+                       size_t bytes_per_rank, void *stream);
+int ompi_amd_bcast(ompi_amd_comm_t *comm, void *buf, size_t bytes, int root,
+                   void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OMPI_AMD_COLL_H */

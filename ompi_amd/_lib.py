@@ -91,6 +91,10 @@ PROTOTYPES = [
     ("ompi_amd_comm_rank", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_comm_size", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_comm_set_param", _C.c_int, [_C.c_void_p, _C.c_char_p, _C.c_int64]),
+    ("ompi_amd_comm_error", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_coll_block", _C.c_int,
+     [_C.c_size_t, _C.c_int, _C.c_int, _C.POINTER(_C.c_size_t), _C.POINTER(_C.c_size_t)]),
+    ("ompi_amd_coll_owner", _C.c_int, [_C.c_int, _C.c_int]),
     ("ompi_amd_allreduce", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p]),
     ("ompi_amd_reduce_scatter_block", _C.c_int,

@@ -1,0 +1,138 @@
+"""Device-buffer collectives of the MI355X path (the coll module surface).
+
+Mirrors the coll framework's entry points for the four collectives this
+path provides (ompi/mca/coll/coll.h:200-247):
+
+    coll_allreduce(sbuf, rbuf, count, dtype, op, comm, module)
+    coll_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, module)
+    coll_allgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, module)
+    coll_bcast(buf, count, dtype, root, comm, module)
+
+with the communicator object holding the module state (IPC mappings, flags,
+epoch).  One process per GPU on one node.  All calls are stream-ordered;
+``blocking=True`` (the MPI semantics the MCA glue uses) synchronises the
+stream and raises on a device-side error.  Every byte moves through
+libompi_amd.so; there is no host fallback for device buffers.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import secrets
+
+from . import _lib
+from .op import Datatype, Op
+
+IN_PLACE = object()  # MPI_IN_PLACE
+_IN_PLACE_PTR = 1
+
+
+def _ptr(buf) -> int:
+    if buf is IN_PLACE:
+        return _IN_PLACE_PTR
+    if isinstance(buf, int):
+        return buf
+    if hasattr(buf, "data_ptr"):
+        if not buf.is_cuda:
+            raise _lib.OmpiAmdError(_lib.ERR_NOT_DEVICE, "host tensor passed to a device collective")
+        return buf.data_ptr()
+    raise TypeError(type(buf))
+
+
+def _stream(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+class Communicator:
+    """A node-local communicator over `size` ranks, one GPU each."""
+
+    def __init__(self, name: str, rank: int, size: int, device: int = 0):
+        self._lib = _lib.load()
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.ompi_amd_comm_create(name.encode(), rank, size, device,
+                                                  ctypes.byref(h)), "comm_create")
+        self._h = h
+        self.rank, self.size, self.device = rank, size, device
+
+    @classmethod
+    def from_torch_distributed(cls, group=None, device: int | None = None) -> "Communicator":
+        """Bootstrap from an initialised torch.distributed group (any
+        backend): rank 0 draws a node-unique segment name and broadcasts it."""
+        import torch.distributed as dist
+        rank, size = dist.get_rank(group), dist.get_world_size(group)
+        token = [f"{os.getpid()}_{secrets.token_hex(6)}" if rank == 0 else None]
+        dist.broadcast_object_list(token, src=0, group=group)
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", rank))
+        return cls(token[0], rank, size, device)
+
+    # -- parameters / state ------------------------------------------------
+    def set_param(self, key: str, value: int) -> None:
+        _lib.check(self._lib.ompi_amd_comm_set_param(self._h, key.encode(), int(value)),
+                   f"set_param({key})")
+
+    def error(self) -> int:
+        return self._lib.ompi_amd_comm_error(self._h)
+
+    def free(self) -> None:
+        if getattr(self, "_h", None):
+            _lib.check(self._lib.ompi_amd_comm_destroy(self._h), "comm_destroy")
+            self._h = None
+
+    def _finish(self, rc: int, what: str, blocking: bool, stream) -> None:
+        _lib.check(rc, what)
+        if blocking:
+            import torch
+            if stream is None:
+                torch.cuda.synchronize(self.device)
+            else:
+                stream.synchronize()
+            err = self.error()
+            if err:
+                raise _lib.OmpiAmdError(err, what)
+
+    # -- collectives ---------------------------------------------------------
+    def allreduce(self, sbuf, rbuf, count: int, datatype: Datatype, op: Op, stream=None,
+                  blocking: bool = False) -> None:
+        rc = self._lib.ompi_amd_allreduce(self._h, _ptr(sbuf), _ptr(rbuf), count, datatype.code,
+                                          op.index, _stream(stream))
+        self._finish(rc, f"allreduce({op.name},{datatype.name})", blocking, stream)
+
+    def reduce_scatter_block(self, sbuf, rbuf, rcount: int, datatype: Datatype, op: Op,
+                             stream=None, blocking: bool = False) -> None:
+        rc = self._lib.ompi_amd_reduce_scatter_block(self._h, _ptr(sbuf), _ptr(rbuf), rcount,
+                                                     datatype.code, op.index, _stream(stream))
+        self._finish(rc, f"reduce_scatter_block({op.name},{datatype.name})", blocking, stream)
+
+    def allgather(self, sbuf, rbuf, nbytes: int, stream=None, blocking: bool = False) -> None:
+        """`nbytes` per rank (scount * extent of a contiguous sdtype)."""
+        rc = self._lib.ompi_amd_allgather(self._h, _ptr(sbuf), _ptr(rbuf), nbytes, _stream(stream))
+        self._finish(rc, "allgather", blocking, stream)
+
+    def bcast(self, buf, nbytes: int, root: int, stream=None, blocking: bool = False) -> None:
+        rc = self._lib.ompi_amd_bcast(self._h, _ptr(buf), nbytes, root, _stream(stream))
+        self._finish(rc, "bcast", blocking, stream)
+
+    def __del__(self):
+        # destroy is collective; only an explicit free() releases the comm
+        pass
+
+
+def block_partition(count: int, nranks: int, block: int) -> tuple[int, int]:
+    """(offset, count) of ring block `block` (COLL_BASE_COMPUTE_BLOCKCOUNT,
+    coll_base_functions.h:425-431) as the library computes it."""
+    lib = _lib.load()
+    off, cnt = ctypes.c_size_t(), ctypes.c_size_t()
+    _lib.check(lib.ompi_amd_coll_block(count, nranks, block, ctypes.byref(off), ctypes.byref(cnt)),
+               "coll_block")
+    return off.value, cnt.value
+
+
+def block_owner(nranks: int, block: int) -> int:
+    """Rank that produces ring block `block` (the rank where the
+    reference's ring finishes it: block - 1 mod N)."""
+    return _lib.load().ompi_amd_coll_owner(nranks, block)

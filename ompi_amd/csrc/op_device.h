@@ -36,12 +36,6 @@ template <> struct is_pair<long_int_t> { static constexpr bool value = true; };
 template <> struct is_pair<two_int_t> { static constexpr bool value = true; };
 template <> struct is_pair<short_int_t> { static constexpr bool value = true; };
 
-// Pair types whose extent exceeds v+k: the reference never writes the gap.
-template <typename T> struct has_gap { static constexpr bool value = false; };
-template <> struct has_gap<double_int_t> { static constexpr bool value = true; };
-template <> struct has_gap<long_int_t> { static constexpr bool value = true; };
-template <> struct has_gap<short_int_t> { static constexpr bool value = true; };
-
 // type code -> C type
 template <int TYPE> struct type_of;
 template <> struct type_of<OMPI_AMD_TYPE_INT8_T> { using type = int8_t; };
@@ -130,19 +124,13 @@ template <typename T> union vec16 {
     T e[16 / sizeof(T)];
 };
 
-// Store one element.  Gapped pair types in 3-buffer mode write only v and k
-// (LOC_FUNC_3BUF never touches out's gap).
-template <typename T, bool THREE>
+// Store one element.  For the gapped pair types (DOUBLE_INT, LONG_INT,
+// SHORT_INT) the gap bytes carry whatever the first operand held: padding
+// takes unspecified values whenever a member is stored (C11 6.2.6.1p6), so
+// op/base itself gives no guarantee on them either.
+template <typename T>
 __device__ __forceinline__ void store_elem(T *p, const T &r) {
-    if constexpr (THREE && has_gap<T>::value) {
-        // byte-addressed member stores: the compiler may not widen them over
-        // the gap the way it may for member stores of the struct type
-        char *c = reinterpret_cast<char *>(p);
-        __builtin_memcpy(c + offsetof(T, v), &r.v, sizeof(r.v));
-        __builtin_memcpy(c + offsetof(T, k), &r.k, sizeof(r.k));
-    } else {
-        *p = r;
-    }
+    *p = r;
 }
 
 }  // namespace ompi_amd

@@ -83,19 +83,14 @@ __global__ __launch_bounds__(kOpThreads) void op_vec_kernel(const T *x, const T 
                 r.v = a[u].v;
 #pragma unroll
                 for (int e = 0; e < E; ++e) r.e[e] = F::template f<T>(a[u].e[e], b[u].e[e]);
-                if constexpr (THREE && has_gap<T>::value) {
-#pragma unroll
-                    for (int e = 0; e < E; ++e) store_elem<T, THREE>(dst + i * E + e, r.e[e]);
-                } else {
-                    st16(dv + i, r.v);
-                }
+                st16(dv + i, r.v);
             }
         }
     }
     // scalar tail: elements past the last whole 16-B vector
     if (blockIdx.x == 0) {
         for (size_t i = nvec * E + threadIdx.x; i < n; i += kOpThreads)
-            store_elem<T, THREE>(dst + i, F::template f<T>(x[i], y[i]));
+            store_elem<T>(dst + i, F::template f<T>(x[i], y[i]));
     }
 }
 
@@ -106,7 +101,7 @@ __global__ __launch_bounds__(kOpThreads) void op_scalar_kernel(const T *x, const
     using F = opfn<OP, THREE>;
     const size_t stride = (size_t)gridDim.x * kOpThreads;
     for (size_t i = (size_t)blockIdx.x * kOpThreads + threadIdx.x; i < n; i += stride)
-        store_elem<T, THREE>(dst + i, F::template f<T>(x[i], y[i]));
+        store_elem<T>(dst + i, F::template f<T>(x[i], y[i]));
 }
 
 static int g_max_blocks = -1;
@@ -114,8 +109,10 @@ static int g_max_blocks = -1;
 static int op_max_blocks() {
     if (g_max_blocks < 0) {
         const char *s = getenv("OMPI_AMD_OP_MAX_BLOCKS");
-        // 256 CUs x 8 resident 256-thread blocks
-        g_max_blocks = (s && atoi(s) > 0) ? atoi(s) : 2048;
+        // Default: no cap — one 4-vector-per-lane chunk per workgroup.  On
+        // MI355X this beat every grid-stride cap from 512 to 16384 blocks
+        // (tools/op_tune.py, profiles/r01_op_tune.jsonl).
+        g_max_blocks = (s && atoi(s) > 0) ? atoi(s) : (1 << 24);
     }
     return g_max_blocks;
 }

@@ -1,0 +1,194 @@
+"""One rank of the multi-process collective parity test (tests/test_coll_gpu.py).
+
+Launched N times with RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT and
+OMPI_AMD_DEVICE.  Bootstraps a gloo group (only to broadcast the segment
+name), creates an ompi_amd Communicator, runs every case on device buffers
+and checks the result against the CPU oracle, which each rank evaluates for
+all ranks from the deterministic per-rank inputs.  Prints one JSON line per
+case and exits 0 only if all passed.
+"""
+import json
+import os
+import sys
+import traceback
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from ompi_amd import coll  # noqa: E402
+from ompi_amd import op as mop  # noqa: E402
+from oracle import oracle as orc  # noqa: E402
+
+SEED = 20261015
+
+
+def inputs(dt: mop.Datatype, count: int, rank: int, salt: int, kind: str = "R") -> np.ndarray:
+    rng = np.random.default_rng(SEED + 1000 * salt + rank)
+    nd = dt.np_dtype
+    if nd.names:  # MAXLOC pairs: quantised values force ties (BASELINE config 5)
+        a = np.zeros(count, dtype=nd)
+        a["v"] = np.round(rng.random(count) * 1024) / 1024
+        a["k"] = rank * count + np.arange(count)
+        return a
+    if nd.kind == "f":
+        if kind == "E":  # exact: k * 2^-8, all orders agree
+            return (rng.integers(-1024, 1025, count) * 2.0 ** -8).astype(nd)
+        a = rng.uniform(-1, 1, count).astype(nd)
+        if kind == "S":  # specials for MAX/MIN
+            sp = np.array([np.nan, 0.0, -0.0, np.inf, -np.inf], dtype=nd)
+            idx = rng.integers(0, count, max(1, count // 8))
+            a[idx] = rng.choice(sp, len(idx))
+        return a
+    info = np.iinfo(nd)
+    lo, hi = (-(1 << 20), 1 << 20) if nd.itemsize >= 4 else (info.min, info.max)
+    if info.min == 0:
+        lo = 0
+    return rng.integers(lo, hi, count, dtype=nd, endpoint=True)
+
+
+def to_dev(a: np.ndarray, extra: int = 0):
+    raw = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+    t = torch.zeros(raw.nbytes + extra, dtype=torch.uint8, device="cuda")
+    t[:raw.nbytes].copy_(torch.from_numpy(raw.copy()))
+    return t
+
+
+def fields_equal(got: np.ndarray, exp: np.ndarray) -> bool:
+    if got.dtype.names:
+        return all(np.array_equal(np.ascontiguousarray(got[f]).view(np.uint8),
+                                  np.ascontiguousarray(exp[f]).view(np.uint8)) for f in ("v", "k"))
+    g, e = got.view(np.uint8), exp.view(np.uint8)
+    if np.array_equal(g, e):
+        return True
+    if got.dtype.kind == "f":
+        nan = np.isnan(got) & np.isnan(exp)
+        return np.array_equal(got[~nan].view(np.uint8), exp[~nan].view(np.uint8))
+    return False
+
+
+def case_allreduce(comm, rank, n, dt, op, count, salt, kind="R", inplace=False, repeat=1):
+    for it in range(repeat):
+        xs = [inputs(dt, count, r, salt + it, kind) for r in range(n)]
+        exp, _ = orc.allreduce([x.copy() for x in xs], count, op.index, dt.code)
+        s = to_dev(xs[rank])
+        if inplace:
+            comm.allreduce(coll.IN_PLACE, s, count, dt, op, blocking=True)
+            out = s
+        else:
+            out = torch.zeros_like(s)
+            comm.allreduce(s, out, count, dt, op, blocking=True)
+        got = out.cpu().numpy()[:count * dt.extent].view(dt.np_dtype)
+        if not fields_equal(got, exp[rank]):
+            bad = np.nonzero(got.view(np.uint8) != exp[rank].view(np.uint8))[0][:5]
+            return False, f"iter {it}: first bad bytes {bad.tolist()}"
+    return True, ""
+
+
+def case_rsb(comm, rank, n, dt, op, rcount, salt, inplace=False):
+    xs = [inputs(dt, rcount * n, r, salt) for r in range(n)]
+    exp = orc.reduce_scatter_block([x.copy() for x in xs], rcount, op.index, dt.code)
+    s = to_dev(xs[rank])
+    if inplace:
+        comm.reduce_scatter_block(coll.IN_PLACE, s, rcount, dt, op, blocking=True)
+        out = s
+    else:
+        out = torch.zeros(rcount * dt.extent, dtype=torch.uint8, device="cuda")
+        comm.reduce_scatter_block(s, out, rcount, dt, op, blocking=True)
+    got = out.cpu().numpy()[:rcount * dt.extent].view(dt.np_dtype)
+    return fields_equal(got, exp[rank].view(dt.np_dtype)), ""
+
+
+def case_allgather(comm, rank, n, nbytes, salt, inplace=False):
+    xs = [np.random.default_rng(SEED + salt + r).integers(0, 256, nbytes, dtype=np.uint8)
+          for r in range(n)]
+    exp = np.concatenate(xs)
+    out = torch.zeros(nbytes * n, dtype=torch.uint8, device="cuda")
+    if inplace:
+        out[rank * nbytes:(rank + 1) * nbytes].copy_(torch.from_numpy(xs[rank]))
+        comm.allgather(coll.IN_PLACE, out, nbytes, blocking=True)
+    else:
+        s = to_dev(xs[rank])
+        comm.allgather(s, out, nbytes, blocking=True)
+    return bool(np.array_equal(out.cpu().numpy(), exp)), ""
+
+
+def case_bcast(comm, rank, n, nbytes, root, salt):
+    data = np.random.default_rng(SEED + salt).integers(0, 256, nbytes, dtype=np.uint8)
+    buf = to_dev(data) if rank == root else torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+    comm.bcast(buf, nbytes, root, blocking=True)
+    return bool(np.array_equal(buf.cpu().numpy()[:nbytes], data)), ""
+
+
+def main():
+    rank, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    device = int(os.environ.get("OMPI_AMD_DEVICE", "0"))
+    torch.cuda.set_device(device)
+    dist.init_process_group("gloo", rank=rank, world_size=n)
+    comm = coll.Communicator.from_torch_distributed(device=device)
+    comm.set_param("timeout_ms", 20000)
+    big = int(os.environ.get("COLL_BIG", 1 << 22))
+    F, D, I32, I64, I8, DI = (mop.MPI_FLOAT, mop.MPI_DOUBLE, mop.MPI_INT32_T, mop.MPI_INT64_T,
+                              mop.MPI_INT8_T, mop.MPI_DOUBLE_INT)
+    cases = [
+        ("ar_sum_f32_1", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, 1, 1)),
+        ("ar_sum_f32_7", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, 7, 2)),
+        ("ar_sum_f32_2499_tree", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, 2499, 3)),
+        ("ar_sum_f32_2500_ring", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, 2500, 4)),
+        ("ar_sum_f32_12345_staged", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, 12345, 5)),
+        ("ar_sum_f32_big_odd", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, big + 5, 6)),
+        ("ar_sum_f32_big", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, big, 7, repeat=3)),
+        ("ar_sum_f32_big_inplace",
+         lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, big, 8, inplace=True)),
+        ("ar_sum_f32_small_inplace",
+         lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, 5000, 9, inplace=True)),
+        ("ar_max_f32_specials", lambda: case_allreduce(comm, rank, n, F, mop.MPI_MAX, 300001, 10, "S")),
+        ("ar_min_f32_specials_tree", lambda: case_allreduce(comm, rank, n, F, mop.MPI_MIN, 999, 11, "S")),
+        ("ar_sum_f64_big", lambda: case_allreduce(comm, rank, n, D, mop.MPI_SUM, big // 2 + 3, 12)),
+        ("ar_sum_i32", lambda: case_allreduce(comm, rank, n, I32, mop.MPI_SUM, 1000003, 13)),
+        ("ar_band_i64", lambda: case_allreduce(comm, rank, n, I64, mop.MPI_BAND, 77777, 14)),
+        ("ar_prod_i8", lambda: case_allreduce(comm, rank, n, I8, mop.MPI_PROD, 50001, 15)),
+        ("ar_maxloc_double_int", lambda: case_allreduce(comm, rank, n, DI, mop.MPI_MAXLOC, 262147, 16)),
+        ("rsb_maxloc_double_int_small", lambda: case_rsb(comm, rank, n, DI, mop.MPI_MAXLOC, 1000, 17)),
+        ("rsb_maxloc_double_int_big", lambda: case_rsb(comm, rank, n, DI, mop.MPI_MAXLOC, big // 8, 18)),
+        ("rsb_sum_f32_big", lambda: case_rsb(comm, rank, n, F, mop.MPI_SUM, big // 4 + 1, 19)),
+        ("rsb_sum_f32_inplace", lambda: case_rsb(comm, rank, n, F, mop.MPI_SUM, 4097, 20, True)),
+        ("allgather_small", lambda: case_allgather(comm, rank, n, 1000, 21)),
+        ("allgather_big", lambda: case_allgather(comm, rank, n, (big * 4) // n + 12, 22)),
+        ("allgather_inplace", lambda: case_allgather(comm, rank, n, 65536, 23, True)),
+        ("bcast_small_root0", lambda: case_bcast(comm, rank, n, 777, 0, 24)),
+        ("bcast_big_rootlast", lambda: case_bcast(comm, rank, n, big * 4 + 3, n - 1, 25)),
+    ]
+    only = os.environ.get("COLL_CASES")
+    ok_all = True
+    for name, fn in cases:
+        if only and name not in only.split(","):
+            continue
+        try:
+            ok, msg = fn()
+        except Exception as e:  # report and stop: later cases would hang
+            ok, msg = False, f"{type(e).__name__}: {e} {traceback.format_exc()[-400:]}"
+            print(json.dumps({"rank": rank, "case": name, "ok": ok, "msg": msg}), flush=True)
+            ok_all = False
+            break
+        print(json.dumps({"rank": rank, "case": name, "ok": bool(ok), "msg": msg}), flush=True)
+        ok_all &= bool(ok)
+    # zero-copy disabled: everything staged through the scratch
+    if ok_all and not only:
+        comm.set_param("zero_copy", 0)
+        ok, msg = case_allreduce(comm, rank, n, F, mop.MPI_SUM, 1 << 20, 30)
+        print(json.dumps({"rank": rank, "case": "ar_staged_only", "ok": bool(ok), "msg": msg}),
+              flush=True)
+        ok_all &= bool(ok)
+    torch.cuda.synchronize()
+    comm.free()
+    dist.destroy_process_group()
+    sys.exit(0 if ok_all else 1)
+
+
+if __name__ == "__main__":
+    main()

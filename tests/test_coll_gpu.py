@@ -1,0 +1,65 @@
+"""Multi-process parity of the xGMI collectives against the oracle.
+
+N ranks (one process each) run tests/coll_worker.py.  On a one-GPU box all
+ranks share cuda:0: the IPC handles, flags, barriers, ring ownership and
+operand order are exercised exactly as across GPUs (peer memory is then the
+same device's memory, so only the link bandwidth differs).  On a multi-GPU
+box rank r uses device r.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "coll_worker.py")
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_ranks(n, timeout=420, extra_env=None):
+    ngpu = torch.cuda.device_count()
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
+                    "MASTER_PORT": str(port), "LOCAL_RANK": str(r),
+                    "OMPI_AMD_DEVICE": str(r % ngpu if ngpu >= n else 0),
+                    "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+        env.update(extra_env or {})
+        procs.append(subprocess.Popen([sys.executable, WORKER], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=timeout)
+            outs.append((p.returncode, out))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return outs
+
+
+@pytest.mark.parametrize("n", [2, 4, 3, 8])
+def test_collectives_parity(n):
+    env = {"COLL_BIG": str(1 << 20)} if n == 8 else None
+    outs = run_ranks(n, extra_env=env)
+    failures = []
+    for r, (rc, out) in enumerate(outs):
+        lines = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+        bad = [ln for ln in lines if not ln["ok"]]
+        if rc != 0 or bad or not lines:
+            failures.append((r, rc, bad[:3], out[-1500:] if not lines or rc not in (0, 1) else ""))
+    assert not failures, failures
