@@ -53,12 +53,19 @@ int ompi_amd_comm_size(const ompi_amd_comm_t *comm);
  *   "zero_copy"     1 (default): large messages read peers' user buffers
  *                   directly; 0: always stage through the scratch
  *   "timeout_ms"    device spin limit per barrier (default 30000)
- *   "blocks"        grid cap of the transfer kernels (default 1024) */
+ *   "blocks"        grid cap of the transfer kernels (default 1024)
+ *   "profile"       1: bracket the allreduce's reduce and gather kernels with
+ *                   HIP events (read with ompi_amd_comm_phase_ms) */
 int ompi_amd_comm_set_param(ompi_amd_comm_t *comm, const char *key, int64_t value);
 
 /* Sticky error of the device side (a barrier that timed out, ...).
  * 0 = none, else an OMPI_AMD_ERR_* code.  Reading it does not sync. */
 int ompi_amd_comm_error(const ompi_amd_comm_t *comm);
+
+/* Kernel time of the profiled allreduce phases since the last read:
+ * phase 0 = the fused peer-load reduction, 1 = the peer gather.  Waits for
+ * the recorded events. */
+int ompi_amd_comm_phase_ms(ompi_amd_comm_t *comm, int phase, double *total_ms, int *calls);
 
 /* The ring block partition and ownership the allreduce uses (host-only,
  * no GPU needed): block b covers elements [off, off+cnt) of the vector

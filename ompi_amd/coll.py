@@ -78,6 +78,14 @@ class Communicator:
     def error(self) -> int:
         return self._lib.ompi_amd_comm_error(self._h)
 
+    def phase_ms(self, phase: int) -> tuple[float, int]:
+        """(total kernel ms, calls) of a profiled allreduce phase (0 =
+        reduce, 1 = gather) since the last read."""
+        tot, n = ctypes.c_double(), ctypes.c_int()
+        _lib.check(self._lib.ompi_amd_comm_phase_ms(self._h, phase, ctypes.byref(tot),
+                                                    ctypes.byref(n)), "phase_ms")
+        return tot.value, n.value
+
     def free(self) -> None:
         if getattr(self, "_h", None):
             _lib.check(self._lib.ompi_amd_comm_destroy(self._h), "comm_destroy")

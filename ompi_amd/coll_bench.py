@@ -1,0 +1,125 @@
+"""Multi-GPU leg of bench.py: MPI_Allreduce fp32 SUM over the xGMI IPC
+collective, one process per GPU (torch.distributed.run), with RCCL's
+allreduce of the same buffer timed beside it as the comparator.
+
+busBW = S / t * 2(N-1)/N; roofline R(N) = (N-1) x 153 GB/s.
+The dominant kernel is the fused peer-load reduction (phase 0): per launch
+it pulls (N-1)/N * S bytes over xGMI into this GPU; its achieved rate is
+those bytes over its event-timed duration.
+"""
+from __future__ import annotations
+
+import os
+import time
+
+
+def _timed(fn, steps, warmup, dist, torch, dev="cuda"):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def bench_allreduce(args, metric: str, link_gbs: float):
+    import torch
+    import torch.distributed as dist
+
+    from . import coll
+    from . import op as mop
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # OMPI_AMD_BENCH_SHARE_GPU=1: rehearsal with every rank on cuda:0 (a
+    # one-GPU box); RCCL refuses two ranks per GPU, so gloo carries the
+    # timing barrier and the comparator is skipped.
+    shared = os.environ.get("OMPI_AMD_BENCH_SHARE_GPU") == "1"
+    if shared:
+        local = 0
+    torch.cuda.set_device(local)
+    if shared:
+        dist.init_process_group("gloo")
+    else:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    tdev = "cpu" if shared else "cuda"
+    rank, world = dist.get_rank(), dist.get_world_size()
+    comm = coll.Communicator.from_torch_distributed(device=local)
+
+    n = args.ar_bytes // 4
+    g = torch.Generator(device="cuda").manual_seed(20261015 + rank)
+    x = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    y = torch.empty_like(x)
+    stream = torch.cuda.current_stream()
+
+    def ours():
+        comm.allreduce(x, y, n, mop.MPI_FLOAT, mop.MPI_SUM, stream=stream)
+
+    t = _timed(ours, args.steps, args.warmup, dist, torch, tdev)
+    err = comm.error()
+    # per-phase kernel time over one more profiled pass of K steps
+    comm.set_param("profile", 1)
+    for _ in range(args.steps):
+        ours()
+    torch.cuda.synchronize()
+    comm.set_param("profile", 0)
+    red_ms, red_calls = comm.phase_ms(0)
+    gat_ms, gat_calls = comm.phase_ms(1)
+
+    t_rccl = None
+    if not shared:
+        rccl_buf = x.clone()
+
+        def rccl():
+            dist.all_reduce(rccl_buf)
+
+        t_rccl = _timed(rccl, args.steps, args.warmup, dist, torch)
+
+    S = n * 4
+    factor = 2.0 * (world - 1) / world
+    busbw = S / (t / args.steps) * factor / 1e9
+    busbw_rccl = S / (t_rccl / args.steps) * factor / 1e9 if t_rccl else None
+    roof = (world - 1) * link_gbs
+    red_avg = red_ms / max(1, red_calls)
+    red_bytes = (world - 1) / world * S  # xGMI bytes pulled by one reduce launch
+    red_gbs = red_bytes / (red_avg * 1e-3) / 1e9 if red_avg > 0 else None
+    res = {
+        "metric": metric,
+        "value": round(busbw, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(t * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic U(-1,1) per rank (seed 20261015+rank), resident in HBM",
+        "config": {"workload": "MPI_Allreduce fp32 SUM 256 MiB per rank, xGMI IPC ring-order "
+                               "reduce + peer gather (BASELINE configs[3] headline point)",
+                   "count": n, "bytes": S, "op": "MPI_SUM", "datatype": "MPI_FLOAT",
+                   "parallelism": f"{world} ranks, 1 GPU each", "busbw_factor": factor},
+        "roofline": {"bound": "xgmi", "achieved": round(red_gbs, 1) if red_gbs else None,
+                     "peak": roof, "unit": "GB/s",
+                     "frac": round(red_gbs / roof, 4) if red_gbs else None,
+                     "traffic": None, "kernel": "reduce_kernel<float,SUM> (phase 0)",
+                     "kernel_ms": round(red_avg, 4),
+                     "gather_kernel_ms": round(gat_ms / max(1, gat_calls), 4),
+                     "busbw_frac_of_R": round(busbw / roof, 4)},
+        "rccl_comparator": ({"busbw": round(busbw_rccl, 2), "unit": "GB/s",
+                             "ms_per_step": round(t_rccl * 1e3 / args.steps, 4)}
+                            if t_rccl else None),
+        "shared_gpu_rehearsal": shared,
+        "device_error": err,
+    }
+    comm.free()
+    dist.barrier()
+    dist.destroy_process_group()
+    return res if rank == 0 else None

@@ -309,6 +309,10 @@ struct ompi_amd_comm {
     std::vector<imp_entry> imports;
     uint64_t use_clock = 0;
     void *opened[kMaxRanks][2] = {};      // flags / scratch mappings of peers
+    // per-phase kernel timing (param "profile"): event pairs per call
+    int profile = 0;
+    std::vector<hipEvent_t> ev_free;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_phase[2];
 };
 
 namespace ompi_amd {
@@ -460,6 +464,29 @@ static int launch_reduce(ompi_amd_comm_t *c, int op, int type, const ptr_set &sr
                       "reduce launch");
 }
 
+// Bracket one phase launch with timing events when profiling.
+static hipEvent_t prof_event(ompi_amd_comm_t *c) {
+    if (!c->ev_free.empty()) {
+        hipEvent_t e = c->ev_free.back();
+        c->ev_free.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+template <typename F>
+static int timed_phase(ompi_amd_comm_t *c, int phase, hipStream_t s, F &&launch) {
+    if (!c->profile) return launch();
+    hipEvent_t a = prof_event(c), b = prof_event(c);
+    if (a) (void)hipEventRecord(a, s);
+    const int rc = launch();
+    if (b) (void)hipEventRecord(b, s);
+    if (a && b) c->ev_phase[phase].emplace_back(a, b);
+    return rc;
+}
+
 static int check_sticky(ompi_amd_comm_t *c) {
     const int e = __atomic_load_n(c->err_host, __ATOMIC_ACQUIRE);
     if (e != 0) {
@@ -573,6 +600,12 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     if (c->flags) (void)hipFree(c->flags);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->err_host) (void)hipHostFree(c->err_host);
+    for (int ph = 0; ph < 2; ++ph)
+        for (auto &pr : c->ev_phase[ph]) {
+            (void)hipEventDestroy(pr.first);
+            (void)hipEventDestroy(pr.second);
+        }
+    for (auto e : c->ev_free) (void)hipEventDestroy(e);
     c->boot.detach();
     delete c;
     return OMPI_AMD_SUCCESS;
@@ -592,6 +625,26 @@ int ompi_amd_coll_owner(int size, int block) {
     return (block + size - 1) % size;
 }
 
+int ompi_amd_comm_phase_ms(ompi_amd_comm_t *c, int phase, double *total_ms, int *calls) {
+    if (!c || phase < 0 || phase > 1 || !total_ms || !calls) return OMPI_AMD_ERR_BAD_PARAM;
+    double tot = 0.0;
+    int n = 0;
+    for (auto &pr : c->ev_phase[phase]) {
+        float ms = 0.f;
+        if (hipEventSynchronize(pr.second) == hipSuccess &&
+            hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) {
+            tot += ms;
+            ++n;
+        }
+        c->ev_free.push_back(pr.first);
+        c->ev_free.push_back(pr.second);
+    }
+    c->ev_phase[phase].clear();
+    *total_ms = tot;
+    *calls = n;
+    return OMPI_AMD_SUCCESS;
+}
+
 int ompi_amd_comm_rank(const ompi_amd_comm_t *c) { return c ? c->rank : -1; }
 int ompi_amd_comm_size(const ompi_amd_comm_t *c) { return c ? c->size : -1; }
 
@@ -609,6 +662,8 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
     } else if (!strcmp(key, "timeout_ms")) {
         if (v <= 0) return OMPI_AMD_ERR_BAD_PARAM;
         c->timeout_ms = v;
+    } else if (!strcmp(key, "profile")) {
+        c->profile = v ? 1 : 0;
     } else if (!strcmp(key, "blocks")) {
         if (v <= 0 || v > 65535) return OMPI_AMD_ERR_BAD_PARAM;
         c->max_blocks = (int)v;
@@ -668,7 +723,7 @@ int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
     const int mine = (c->rank + 1) % n;  // the block the reference ring finishes here
     TRY(launch_barrier(c, s));
     ring_jobs((int64_t)count, n, &jobs, mine);
-    TRY(launch_reduce(c, op, type, sp, rbuf, order, jobs, s));
+    TRY(timed_phase(c, 0, s, [&] { return launch_reduce(c, op, type, sp, rbuf, order, jobs, s); }));
     TRY(launch_barrier(c, s));
     int64_t split, early, late;
     blockcount((int64_t)count, n, &split, &early, &late);
@@ -680,7 +735,7 @@ int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
         cj.j[cj.n++] = {rp.p[owner] + off, (char *)rbuf + off,
                         block_cnt(b, split, early, late) * (int64_t)ext};
     }
-    TRY(launch_copy(c, cj, s));
+    TRY(timed_phase(c, 1, s, [&] { return launch_copy(c, cj, s); }));
     return launch_barrier(c, s);
 }
 
