@@ -38,7 +38,8 @@ typedef struct ompi_amd_comm ompi_amd_comm_t;
 /* Collective over the `size` ranks of one node.  `name` identifies the
  * communicator node-wide and must be unique per job (e.g. "<jobid>.<cid>");
  * it names the POSIX shared-memory rendezvous segment.  `device` is this
- * rank's HIP device.  Every rank calls it with the same name and size. */
+ * rank's HIP device (-1: the calling thread's current device).  Every rank
+ * calls it with the same name and size. */
 int ompi_amd_comm_create(const char *name, int rank, int size, int device,
                          ompi_amd_comm_t **comm);
 /* Collective: every rank must call it. */
@@ -61,6 +62,16 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *comm, const char *key, int64_t valu
 /* Sticky error of the device side (a barrier that timed out, ...).
  * 0 = none, else an OMPI_AMD_ERR_* code.  Reading it does not sync. */
 int ompi_amd_comm_error(const ompi_amd_comm_t *comm);
+
+/* Host-side agreement across the communicator (shared-memory rendezvous,
+ * no GPU work): *all_ok = 1 iff every rank passed local_ok != 0.  The MCA
+ * glue uses it so that all ranks take the device path or all fall back to
+ * the saved tuned functions (buffer residency may differ across ranks). */
+int ompi_amd_comm_agree(ompi_amd_comm_t *comm, int local_ok, int *all_ok);
+
+/* Wait for `stream` (NULL = per-thread) and report a sticky device error:
+ * the blocking completion the MPI entry points need. */
+int ompi_amd_comm_sync(ompi_amd_comm_t *comm, void *stream);
 
 /* Kernel time of the profiled allreduce phases since the last read:
  * phase 0 = the fused peer-load reduction, 1 = the peer gather.  Waits for

@@ -92,6 +92,8 @@ PROTOTYPES = [
     ("ompi_amd_comm_size", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_comm_set_param", _C.c_int, [_C.c_void_p, _C.c_char_p, _C.c_int64]),
     ("ompi_amd_comm_error", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_comm_agree", _C.c_int, [_C.c_void_p, _C.c_int, _C.POINTER(_C.c_int)]),
+    ("ompi_amd_comm_sync", _C.c_int, [_C.c_void_p, _C.c_void_p]),
     ("ompi_amd_comm_phase_ms", _C.c_int,
      [_C.c_void_p, _C.c_int, _C.POINTER(_C.c_double), _C.POINTER(_C.c_int)]),
     ("ompi_amd_coll_block", _C.c_int,

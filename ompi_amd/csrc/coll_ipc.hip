@@ -535,6 +535,11 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
     if (!c) return OMPI_AMD_ERR_BAD_PARAM;
     c->rank = rank;
     c->size = size;
+    if (device < 0 && hipGetDevice(&device) != hipSuccess) {
+        (void)hipGetLastError();
+        delete c;
+        return OMPI_AMD_ERR_HIP;
+    }
     c->device = device;
     if (const char *t = getenv("OMPI_AMD_COLL_TIMEOUT_MS")) c->timeout_ms = atoll(t);
     int rc = set_dev(c);
@@ -643,6 +648,23 @@ int ompi_amd_comm_phase_ms(ompi_amd_comm_t *c, int phase, double *total_ms, int 
     *total_ms = tot;
     *calls = n;
     return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_comm_agree(ompi_amd_comm_t *c, int local_ok, int *all_ok) {
+    if (!c || !all_ok) return OMPI_AMD_ERR_BAD_PARAM;
+    int mine = local_ok ? 1 : 0, all[kMaxRanks];
+    TRY(c->boot.allgather(&mine, all, sizeof(int)));
+    int ok = 1;
+    for (int p = 0; p < c->size; ++p) ok &= all[p];
+    *all_ok = ok;
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_comm_sync(ompi_amd_comm_t *c, void *stream) {
+    if (!c) return OMPI_AMD_ERR_BAD_PARAM;
+    TRY(set_dev(c));
+    TRY(record_hip(hipStreamSynchronize(as_stream(stream)), "hipStreamSynchronize"));
+    return check_sticky(c);
 }
 
 int ompi_amd_comm_rank(const ompi_amd_comm_t *c) { return c ? c->rank : -1; }

@@ -1,0 +1,67 @@
+/*
+ * coll/rocm — MI355X coll component for Open MPI's coll framework.
+ *
+ * Drop-in: copy this directory to ompi/mca/coll/rocm/ (INTEGRATION.md §2).
+ * The module provides coll_allreduce, coll_reduce_scatter_block,
+ * coll_allgather and coll_bcast (ompi/mca/coll/coll.h:200-247) for device
+ * buffers through libompi_amd.so, and interposes on the previously selected
+ * functions (coll/tuned) for everything else, exactly like coll/cuda does
+ * (ompi/mca/coll/cuda/coll_cuda_module.c:120-155).
+ */
+#ifndef MCA_COLL_ROCM_EXPORT_H
+#define MCA_COLL_ROCM_EXPORT_H
+
+#include "ompi_config.h"
+
+#include "mpi.h"
+#include "ompi/communicator/communicator.h"
+#include "ompi/mca/coll/base/coll_base_functions.h"
+#include "ompi/mca/coll/coll.h"
+#include "opal/class/opal_object.h"
+
+#include "ompi_amd_coll.h"
+
+BEGIN_C_DECLS
+
+typedef struct mca_coll_rocm_module_t {
+    mca_coll_base_module_t super;
+    /* the functions this module replaces, saved at enable time */
+    mca_coll_base_comm_coll_t c_coll;
+    /* libompi_amd communicator (IPC mappings, flags, epoch) */
+    ompi_amd_comm_t *dev_comm;
+} mca_coll_rocm_module_t;
+
+OBJ_CLASS_DECLARATION(mca_coll_rocm_module_t);
+
+typedef struct mca_coll_rocm_component_t {
+    mca_coll_base_component_2_0_0_t super;
+    int priority;        /* coll_rocm_priority (default 80: above coll/cuda's 78) */
+    int small_bytes;     /* coll_rocm_small_bytes */
+    int zero_copy;       /* coll_rocm_zero_copy */
+    int timeout_ms;      /* coll_rocm_timeout_ms */
+} mca_coll_rocm_component_t;
+
+OMPI_MODULE_DECLSPEC extern mca_coll_rocm_component_t mca_coll_rocm_component;
+
+int mca_coll_rocm_init_query(bool enable_progress_threads, bool enable_mpi_threads);
+mca_coll_base_module_t *mca_coll_rocm_comm_query(struct ompi_communicator_t *comm,
+                                                 int *priority);
+int mca_coll_rocm_module_enable(mca_coll_base_module_t *module,
+                                struct ompi_communicator_t *comm);
+
+int mca_coll_rocm_allreduce(const void *sbuf, void *rbuf, int count,
+                            struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                            struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+int mca_coll_rocm_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount,
+                                       struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                       struct ompi_communicator_t *comm,
+                                       mca_coll_base_module_t *module);
+int mca_coll_rocm_allgather(const void *sbuf, int scount, struct ompi_datatype_t *sdtype,
+                            void *rbuf, int rcount, struct ompi_datatype_t *rdtype,
+                            struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+int mca_coll_rocm_bcast(void *buf, int count, struct ompi_datatype_t *dtype, int root,
+                        struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+
+END_C_DECLS
+
+#endif /* MCA_COLL_ROCM_EXPORT_H */

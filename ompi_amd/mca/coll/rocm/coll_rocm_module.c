@@ -1,0 +1,267 @@
+/*
+ * coll/rocm component + module.
+ *
+ * Selection: comm_query accepts node-local intra-communicators of at most
+ * OMPI_AMD_MAX_RANKS ranks when a HIP device is visible; enable saves the
+ * previously selected allreduce / reduce_scatter_block / allgather / bcast
+ * (coll/tuned, coll_base_comm_select.c:158-232 enables in ascending
+ * priority) and creates the libompi_amd communicator.
+ *
+ * Per call every rank decides locally whether the device path applies
+ * (predefined datatype, intrinsic op with a device kernel, device buffers),
+ * then the ranks agree (ompi_amd_comm_agree) so that all of them take the
+ * same path — MPI lets buffer residency differ between ranks.  The device
+ * path is blocking like every MPI collective: ompi_amd_comm_sync waits for
+ * the stream and surfaces a device-side timeout as an MPI error.
+ */
+#include "ompi_config.h"
+
+#include <stdio.h>
+#include <string.h>
+
+#include "mpi.h"
+#include "ompi/constants.h"
+#include "ompi/communicator/communicator.h"
+#include "ompi/datatype/ompi_datatype.h"
+#include "ompi/mca/coll/base/base.h"
+#include "ompi/mca/coll/coll.h"
+#include "ompi/op/op.h"
+#include "ompi/runtime/ompi_rte.h"
+#include "opal/mca/base/mca_base_var.h"
+
+#include "coll_rocm.h"
+#include "ompi_amd.h"
+
+/* ------------------------------------------------------------- component */
+
+static int rocm_register(void);
+
+mca_coll_rocm_component_t mca_coll_rocm_component = {
+    .super = {
+        .collm_version = {
+            MCA_COLL_BASE_VERSION_2_0_0,
+            .mca_component_name = "rocm",
+            MCA_BASE_MAKE_VERSION(component, OMPI_MAJOR_VERSION, OMPI_MINOR_VERSION,
+                                  OMPI_RELEASE_VERSION),
+            .mca_register_component_params = rocm_register,
+        },
+        .collm_data = { MCA_BASE_METADATA_PARAM_CHECKPOINT },
+        .collm_init_query = mca_coll_rocm_init_query,
+        .collm_comm_query = mca_coll_rocm_comm_query,
+    },
+    .priority = 80,
+    .small_bytes = 1 << 20,
+    .zero_copy = 1,
+    .timeout_ms = 30000,
+};
+
+static int rocm_register(void)
+{
+    mca_base_component_t *c = &mca_coll_rocm_component.super.collm_version;
+    (void) mca_base_component_var_register(c, "priority", "Priority of coll/rocm",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_coll_rocm_component.priority);
+    (void) mca_base_component_var_register(c, "small_bytes",
+                                           "Messages up to this size are staged through the IPC scratch",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_coll_rocm_component.small_bytes);
+    (void) mca_base_component_var_register(c, "zero_copy",
+                                           "Read peers' user buffers directly for large messages",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_coll_rocm_component.zero_copy);
+    (void) mca_base_component_var_register(c, "timeout_ms",
+                                           "Device barrier spin limit before the collective fails",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_coll_rocm_component.timeout_ms);
+    return OMPI_SUCCESS;
+}
+
+/* ------------------------------------------------------------- module */
+
+static void rocm_module_construct(mca_coll_rocm_module_t *m)
+{
+    memset(&m->c_coll, 0, sizeof(m->c_coll));
+    m->dev_comm = NULL;
+}
+
+static void rocm_module_destruct(mca_coll_rocm_module_t *m)
+{
+    if (NULL != m->c_coll.coll_allreduce_module) OBJ_RELEASE(m->c_coll.coll_allreduce_module);
+    if (NULL != m->c_coll.coll_reduce_scatter_block_module)
+        OBJ_RELEASE(m->c_coll.coll_reduce_scatter_block_module);
+    if (NULL != m->c_coll.coll_allgather_module) OBJ_RELEASE(m->c_coll.coll_allgather_module);
+    if (NULL != m->c_coll.coll_bcast_module) OBJ_RELEASE(m->c_coll.coll_bcast_module);
+    if (NULL != m->dev_comm) (void) ompi_amd_comm_destroy(m->dev_comm);
+}
+
+OBJ_CLASS_INSTANCE(mca_coll_rocm_module_t, mca_coll_base_module_t, rocm_module_construct,
+                   rocm_module_destruct);
+
+int mca_coll_rocm_init_query(bool enable_progress_threads, bool enable_mpi_threads)
+{
+    return ompi_amd_device_count() > 0 ? OMPI_SUCCESS : OMPI_ERR_NOT_AVAILABLE;
+}
+
+mca_coll_base_module_t *mca_coll_rocm_comm_query(struct ompi_communicator_t *comm,
+                                                 int *priority)
+{
+    mca_coll_rocm_module_t *m;
+    if (OMPI_COMM_IS_INTER(comm) || ompi_comm_size(comm) < 2 ||
+        ompi_comm_size(comm) > OMPI_AMD_MAX_RANKS ||
+        ompi_group_have_remote_peers(comm->c_local_group)) {
+        return NULL;  /* one node, one process per GPU */
+    }
+    m = OBJ_NEW(mca_coll_rocm_module_t);
+    if (NULL == m) return NULL;
+    *priority = mca_coll_rocm_component.priority;
+    m->super.coll_module_enable = mca_coll_rocm_module_enable;
+    m->super.coll_allreduce = mca_coll_rocm_allreduce;
+    m->super.coll_reduce_scatter_block = mca_coll_rocm_reduce_scatter_block;
+    m->super.coll_allgather = mca_coll_rocm_allgather;
+    m->super.coll_bcast = mca_coll_rocm_bcast;
+    return &m->super;
+}
+
+int mca_coll_rocm_module_enable(mca_coll_base_module_t *module, struct ompi_communicator_t *comm)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    char name[128];
+    int rc;
+
+#define SAVE(fn)                                                            \
+    do {                                                                    \
+        if (NULL == comm->c_coll->coll_##fn##_module) return OMPI_ERR_NOT_FOUND; \
+        m->c_coll.coll_##fn = comm->c_coll->coll_##fn;                     \
+        m->c_coll.coll_##fn##_module = comm->c_coll->coll_##fn##_module;   \
+        OBJ_RETAIN(m->c_coll.coll_##fn##_module);                          \
+    } while (0)
+    SAVE(allreduce);
+    SAVE(reduce_scatter_block);
+    SAVE(allgather);
+    SAVE(bcast);
+#undef SAVE
+
+    /* node-unique segment name: job id + communicator id */
+    snprintf(name, sizeof(name), "%u.%u", (unsigned) OMPI_PROC_MY_NAME->jobid,
+             (unsigned) ompi_comm_get_cid(comm));
+    rc = ompi_amd_comm_create(name, ompi_comm_rank(comm), ompi_comm_size(comm), -1, &m->dev_comm);
+    if (OMPI_AMD_SUCCESS != rc) return OMPI_ERR_NOT_AVAILABLE;
+    (void) ompi_amd_comm_set_param(m->dev_comm, "small_bytes", mca_coll_rocm_component.small_bytes);
+    (void) ompi_amd_comm_set_param(m->dev_comm, "zero_copy", mca_coll_rocm_component.zero_copy);
+    (void) ompi_amd_comm_set_param(m->dev_comm, "timeout_ms", mca_coll_rocm_component.timeout_ms);
+    return OMPI_SUCCESS;
+}
+
+/* ------------------------------------------------------------- helpers */
+
+static int to_ompi_err(int rc)
+{
+    switch (rc) {
+    case OMPI_AMD_SUCCESS: return OMPI_SUCCESS;
+    case OMPI_AMD_ERR_BAD_PARAM: return OMPI_ERR_BAD_PARAM;
+    case OMPI_AMD_ERR_UNSUPPORTED: return OMPI_ERR_NOT_SUPPORTED;
+    case OMPI_AMD_ERR_TIMEOUT: return OMPI_ERR_TIMEOUT;
+    default: return OMPI_ERROR;
+    }
+}
+
+/* op/type code of a predefined datatype, or -1 */
+static int type_code(struct ompi_datatype_t *dtype)
+{
+    if (!ompi_datatype_is_predefined(dtype)) return -1;
+    return ompi_op_ddt_map[dtype->id];
+}
+
+static int dev(const void *p)
+{
+    return MPI_IN_PLACE == p || ompi_amd_is_device_pointer(p);
+}
+
+/* every rank must answer the same way (buffer residency may differ) */
+static bool take_device_path(mca_coll_rocm_module_t *m, int local_ok)
+{
+    int all_ok = 0;
+    if (OMPI_AMD_SUCCESS != ompi_amd_comm_agree(m->dev_comm, local_ok, &all_ok)) return false;
+    return all_ok != 0;
+}
+
+/* ------------------------------------------------------------- collectives */
+
+int mca_coll_rocm_allreduce(const void *sbuf, void *rbuf, int count,
+                            struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                            struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const int t = type_code(dtype);
+    const int ok = t >= 0 && ompi_op_is_intrinsic(op) &&
+                   ompi_amd_op_supported(op->o_f_to_c_index, t) && dev(sbuf) && dev(rbuf);
+    int rc;
+    if (!take_device_path(m, ok)) {
+        return m->c_coll.coll_allreduce(sbuf, rbuf, count, dtype, op, comm,
+                                        m->c_coll.coll_allreduce_module);
+    }
+    rc = ompi_amd_allreduce(m->dev_comm, MPI_IN_PLACE == sbuf ? rbuf : sbuf, rbuf,
+                            (size_t) count, t, op->o_f_to_c_index, NULL);
+    if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_comm_sync(m->dev_comm, NULL);
+    return to_ompi_err(rc);
+}
+
+int mca_coll_rocm_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount,
+                                       struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                       struct ompi_communicator_t *comm,
+                                       mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const int t = type_code(dtype);
+    const int ok = t >= 0 && ompi_op_is_intrinsic(op) &&
+                   ompi_amd_op_supported(op->o_f_to_c_index, t) && dev(sbuf) && dev(rbuf);
+    int rc;
+    if (!take_device_path(m, ok)) {
+        return m->c_coll.coll_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm,
+                                                   m->c_coll.coll_reduce_scatter_block_module);
+    }
+    rc = ompi_amd_reduce_scatter_block(m->dev_comm, MPI_IN_PLACE == sbuf ? rbuf : sbuf, rbuf,
+                                       (size_t) rcount, t, op->o_f_to_c_index, NULL);
+    if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_comm_sync(m->dev_comm, NULL);
+    return to_ompi_err(rc);
+}
+
+int mca_coll_rocm_allgather(const void *sbuf, int scount, struct ompi_datatype_t *sdtype,
+                            void *rbuf, int rcount, struct ompi_datatype_t *rdtype,
+                            struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    size_t rsize = 0;
+    int rc, ok;
+    (void) ompi_datatype_type_size(rdtype, &rsize);
+    /* contiguous, gap-free receive type: the gather is a byte copy */
+    ok = ompi_datatype_is_contiguous_memory_layout(rdtype, rcount) && dev(rbuf) && dev(sbuf) &&
+         (MPI_IN_PLACE == sbuf || ompi_datatype_is_contiguous_memory_layout(sdtype, scount));
+    if (!take_device_path(m, ok)) {
+        return m->c_coll.coll_allgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm,
+                                        m->c_coll.coll_allgather_module);
+    }
+    rc = ompi_amd_allgather(m->dev_comm, MPI_IN_PLACE == sbuf ? (const void *) 1 : sbuf, rbuf,
+                            rsize * (size_t) rcount, NULL);
+    if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_comm_sync(m->dev_comm, NULL);
+    return to_ompi_err(rc);
+}
+
+int mca_coll_rocm_bcast(void *buf, int count, struct ompi_datatype_t *dtype, int root,
+                        struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    size_t size = 0;
+    int rc;
+    (void) ompi_datatype_type_size(dtype, &size);
+    if (!take_device_path(m, ompi_datatype_is_contiguous_memory_layout(dtype, count) && dev(buf))) {
+        return m->c_coll.coll_bcast(buf, count, dtype, root, comm, m->c_coll.coll_bcast_module);
+    }
+    rc = ompi_amd_bcast(m->dev_comm, buf, size * (size_t) count, root, NULL);
+    if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_comm_sync(m->dev_comm, NULL);
+    return to_ompi_err(rc);
+}

@@ -1,0 +1,150 @@
+/*
+ * op/rocm component: query / enable glue between Open MPI's op framework
+ * (ompi/mca/op/op.h:294-378, selection ompi/mca/op/base/op_base_op_select.c:
+ * 90-211) and libompi_amd.so (include/ompi_amd.h).
+ *
+ * For each intrinsic MPI_Op the query builds one module whose slot i is
+ * libompi_amd's handler when BOTH op/base and the library have slot i
+ * (op_base_op_select.c:182-204 requires the NULL pattern to stay op/base's;
+ * NULL = keep the lower-priority handler).  The slot's current handler —
+ * op/base's, installed before any component is queried
+ * (op_base_op_select.c:113-122) — is registered with the library as the
+ * host-buffer fallback.
+ */
+#include "ompi_config.h"
+
+#include "ompi/constants.h"
+#include "ompi/op/op.h"
+#include "ompi/mca/op/op.h"
+#include "ompi/mca/op/base/base.h"
+#include "opal/class/opal_object.h"
+#include "opal/mca/base/mca_base_var.h"
+
+#include "op_rocm.h"
+#include "ompi_amd.h"
+
+static int rocm_component_open(void);
+static int rocm_component_close(void);
+static int rocm_component_register(void);
+static int rocm_component_init_query(bool enable_progress_threads,
+                                     bool enable_mpi_thread_multiple);
+static struct ompi_op_base_module_1_0_0_t *
+rocm_component_op_query(struct ompi_op_t *op, int *priority);
+
+ompi_op_rocm_component_t mca_op_rocm_component = {
+    .super = {
+        .opc_version = {
+            OMPI_OP_BASE_VERSION_1_0_0,
+            .mca_component_name = "rocm",
+            MCA_BASE_MAKE_VERSION(component, OMPI_MAJOR_VERSION, OMPI_MINOR_VERSION,
+                                  OMPI_RELEASE_VERSION),
+            .mca_open_component = rocm_component_open,
+            .mca_close_component = rocm_component_close,
+            .mca_register_component_params = rocm_component_register,
+        },
+        .opc_data = {
+            /* the component is checkpoint-ready */
+            MCA_BASE_METADATA_PARAM_CHECKPOINT
+        },
+        .opc_init_query = rocm_component_init_query,
+        .opc_op_query = rocm_component_op_query,
+    },
+    .priority = 60,     /* above op/avx (50): device buffers are ours */
+    .max_blocks = 0,    /* 0 = library default (uncapped grid) */
+    .have_gpu = false,
+};
+
+static int rocm_component_register(void)
+{
+    (void) mca_base_component_var_register(&mca_op_rocm_component.super.opc_version,
+                                           "priority",
+                                           "Priority of the op/rocm component",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0,
+                                           OPAL_INFO_LVL_9, MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_op_rocm_component.priority);
+    (void) mca_base_component_var_register(&mca_op_rocm_component.super.opc_version,
+                                           "max_blocks",
+                                           "Grid cap of the streaming op kernels (0 = uncapped)",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0,
+                                           OPAL_INFO_LVL_9, MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_op_rocm_component.max_blocks);
+    return OMPI_SUCCESS;
+}
+
+static int rocm_component_open(void)
+{
+    return OMPI_SUCCESS;
+}
+
+static int rocm_component_close(void)
+{
+    return OMPI_SUCCESS;
+}
+
+static int rocm_component_init_query(bool enable_progress_threads,
+                                     bool enable_mpi_thread_multiple)
+{
+    /* Handlers keep no global mutable state beyond the fallback table
+       written here at init, and run on the calling thread's HIP stream, so
+       MPI_THREAD_MULTIPLE is fine. */
+    mca_op_rocm_component.have_gpu = ompi_amd_device_count() > 0;
+    if (!mca_op_rocm_component.have_gpu) {
+        return OMPI_ERR_NOT_SUPPORTED;
+    }
+    if (mca_op_rocm_component.max_blocks > 0) {
+        (void) ompi_amd_set_tuning("op_max_blocks", mca_op_rocm_component.max_blocks);
+    }
+    return OMPI_SUCCESS;
+}
+
+static struct ompi_op_base_module_1_0_0_t *
+rocm_component_op_query(struct ompi_op_t *op, int *priority)
+{
+    const ompi_amd_op_handler_fn_t *row2;
+    const ompi_amd_op_3buff_handler_fn_t *row3;
+    ompi_op_base_module_t *module;
+    int i, used = 0;
+
+    if (0 == (OMPI_OP_FLAGS_INTRINSIC & op->o_flags)) {
+        return NULL;
+    }
+    row2 = ompi_amd_op_handler_row(op->o_f_to_c_index);
+    row3 = ompi_amd_op_3buff_handler_row(op->o_f_to_c_index);
+    if (NULL == row2 || NULL == row3) {
+        return NULL;
+    }
+    module = OBJ_NEW(ompi_op_base_module_t);
+    if (NULL == module) {
+        return NULL;
+    }
+    for (i = 0; i < OMPI_OP_BASE_TYPE_MAX; ++i) {
+        ompi_op_base_handler_fn_t base2 = op->o_func.intrinsic.fns[i];
+        ompi_op_base_3buff_handler_fn_t base3 = op->o_3buff_intrinsic.fns[i];
+        if (NULL != base2 && NULL != row2[i]) {
+            module->opm_fns[i] = (ompi_op_base_handler_fn_t) row2[i];
+            ++used;
+        }
+        if (NULL != base3 && NULL != row3[i]) {
+            module->opm_3buff_fns[i] = (ompi_op_base_3buff_handler_fn_t) row3[i];
+            ++used;
+        }
+        if (NULL != module->opm_fns[i] || NULL != module->opm_3buff_fns[i]) {
+            /* host buffers in this slot go back to op/base */
+            ompi_op_base_module_t *m2 = op->o_func.intrinsic.modules[i];
+            ompi_op_base_module_t *m3 = op->o_3buff_intrinsic.modules[i];
+            if (NULL != m2) OBJ_RETAIN(m2);
+            if (NULL != m3) OBJ_RETAIN(m3);
+            (void) ompi_amd_op_set_fallback(op->o_f_to_c_index, i,
+                                            (ompi_amd_op_handler_fn_t) base2,
+                                            (struct ompi_op_base_module_1_0_0_t *) m2,
+                                            (ompi_amd_op_3buff_handler_fn_t) base3,
+                                            (struct ompi_op_base_module_1_0_0_t *) m3);
+        }
+    }
+    if (0 == used) {
+        OBJ_RELEASE(module);
+        return NULL;
+    }
+    *priority = mca_op_rocm_component.priority;
+    return module;
+}
