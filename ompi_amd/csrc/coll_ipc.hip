@@ -56,7 +56,7 @@ enum order_t { ORDER_RING = 0, ORDER_TREE = 1, ORDER_LINEAR = 2 };
 struct red_job {
     int64_t off, cnt, off_dst;
     int first;  // ring order: the block id b (sources start at rank b)
-    int vec;    // 1: every source and dst are 16-B aligned at off
+    int head;   // elements before the 16-B aligned body; -1: no common alignment
 };
 struct red_jobs { red_job j[kMaxRanks]; int n; };
 
@@ -157,35 +157,37 @@ __global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, T *ds
     const red_job jb = jobs.j[blockIdx.y];
     constexpr int E = 16 / sizeof(T);
     const int64_t gstride = (int64_t)gridDim.x * kXferThreads;
-    int64_t done = 0;
-    if (jb.vec) {
-        const int64_t nvec = jb.cnt / E;
-        for (int64_t i = (int64_t)blockIdx.x * kXferThreads + threadIdx.x; i < nvec; i += gstride) {
-            vec16<T> v[kMaxRanks];
+    const int64_t tid = (int64_t)blockIdx.x * kXferThreads + threadIdx.x;
+    // vector body [head, head + nvec*E): every source and dst 16-B aligned
+    // there (head < 0: no common alignment, all scalar)
+    const int64_t head = jb.head < 0 ? jb.cnt : jb.head;
+    const int64_t nvec = jb.head < 0 ? 0 : (jb.cnt - head) / E;
+    for (int64_t i = tid; i < nvec; i += gstride) {
+        vec16<T> v[kMaxRanks];
 #pragma unroll
-            for (int j = 0; j < kMaxRanks; ++j) {
-                if (j < n) {
-                    const int r = (order == ORDER_RING) ? (jb.first + j) % n : j;
-                    const u32x4 *p = reinterpret_cast<const u32x4 *>(
-                        reinterpret_cast<const T *>(src.p[r]) + jb.off);
-                    v[j].v = __builtin_nontemporal_load(p + i);
-                }
+        for (int j = 0; j < kMaxRanks; ++j) {
+            if (j < n) {
+                const int r = (order == ORDER_RING) ? (jb.first + j) % n : j;
+                const u32x4 *p = reinterpret_cast<const u32x4 *>(
+                    reinterpret_cast<const T *>(src.p[r]) + jb.off + head);
+                v[j].v = __builtin_nontemporal_load(p + i);
             }
-            vec16<T> out;
-#pragma unroll
-            for (int e = 0; e < E; ++e) {
-                T s[kMaxRanks];
-#pragma unroll
-                for (int j = 0; j < kMaxRanks; ++j) s[j] = v[j].e[e];
-                out.e[e] = fold<T, OP>(s, n, order);
-            }
-            u32x4 *d = reinterpret_cast<u32x4 *>(dst + jb.off_dst);
-            d[i] = out.v;
         }
-        done = nvec * E;
+        vec16<T> out;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            T s[kMaxRanks];
+#pragma unroll
+            for (int j = 0; j < kMaxRanks; ++j) s[j] = v[j].e[e];
+            out.e[e] = fold<T, OP>(s, n, order);
+        }
+        reinterpret_cast<u32x4 *>(dst + jb.off_dst + head)[i] = out.v;
     }
-    for (int64_t e = done + (int64_t)blockIdx.x * kXferThreads + threadIdx.x; e < jb.cnt;
-         e += gstride) {
+    // scalar head [0, head) and tail [head + nvec*E, cnt)
+    const int64_t tail0 = head + nvec * E;
+    const int64_t nscalar = head + (jb.cnt - tail0);
+    for (int64_t k = tid; k < nscalar; k += gstride) {
+        const int64_t e = k < head ? k : tail0 + (k - head);
         T s[kMaxRanks];
         gather_scalar<T>(s, src, n, order, jb.first, jb.off + e);
         store_elem<T>(dst + jb.off_dst + e, fold<T, OP>(s, n, order));
@@ -195,19 +197,25 @@ __global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, T *ds
 }
 
 // ---------------------------------------------------------------- copy
+// Byte copy with a peeled head so that the body runs 16 B (or 4 B) per
+// lane whenever src and dst share their alignment phase.
 __global__ __launch_bounds__(kXferThreads) void copy_kernel(cp_jobs jobs) {
     sys_acquire();
     const cp_job jb = jobs.j[blockIdx.y];
     const int64_t gstride = (int64_t)gridDim.x * kXferThreads;
     const int64_t tid = (int64_t)blockIdx.x * kXferThreads + threadIdx.x;
-    const uintptr_t al = (uintptr_t)jb.src | (uintptr_t)jb.dst;
-    int64_t done = 0;
-    if ((al & 15) == 0) {
-        const int64_t nv = jb.bytes / 16;
-        const u32x4 *s = reinterpret_cast<const u32x4 *>(jb.src);
-        u32x4 *d = reinterpret_cast<u32x4 *>(jb.dst);
+    const uintptr_t phase = (uintptr_t)jb.src ^ (uintptr_t)jb.dst;
+    const int g = (phase & 15) == 0 ? 16 : ((phase & 3) == 0 ? 4 : 1);
+    int64_t head = (int64_t)((g - ((uintptr_t)jb.src & (uintptr_t)(g - 1))) & (uintptr_t)(g - 1));
+    if (head > jb.bytes) head = jb.bytes;
+    const int64_t nbody = (jb.bytes - head) / g;
+    const char *sb = jb.src + head;
+    char *db = jb.dst + head;
+    if (g == 16) {
+        const u32x4 *s = reinterpret_cast<const u32x4 *>(sb);
+        u32x4 *d = reinterpret_cast<u32x4 *>(db);
         int64_t i = tid;
-        for (; i + 3 * gstride < nv; i += 4 * gstride) {
+        for (; i + 3 * gstride < nbody; i += 4 * gstride) {
             const u32x4 a = __builtin_nontemporal_load(s + i);
             const u32x4 b = __builtin_nontemporal_load(s + i + gstride);
             const u32x4 c = __builtin_nontemporal_load(s + i + 2 * gstride);
@@ -217,16 +225,20 @@ __global__ __launch_bounds__(kXferThreads) void copy_kernel(cp_jobs jobs) {
             d[i + 2 * gstride] = c;
             d[i + 3 * gstride] = e;
         }
-        for (; i < nv; i += gstride) d[i] = __builtin_nontemporal_load(s + i);
-        done = nv * 16;
-    } else if ((al & 3) == 0) {
-        const int64_t nw = jb.bytes / 4;
-        const uint32_t *s = reinterpret_cast<const uint32_t *>(jb.src);
-        uint32_t *d = reinterpret_cast<uint32_t *>(jb.dst);
-        for (int64_t i = tid; i < nw; i += gstride) d[i] = s[i];
-        done = nw * 4;
+        for (; i < nbody; i += gstride) d[i] = __builtin_nontemporal_load(s + i);
+    } else if (g == 4) {
+        const uint32_t *s = reinterpret_cast<const uint32_t *>(sb);
+        uint32_t *d = reinterpret_cast<uint32_t *>(db);
+        for (int64_t i = tid; i < nbody; i += gstride) d[i] = s[i];
+    } else {
+        for (int64_t i = tid; i < nbody; i += gstride) db[i] = sb[i];
     }
-    for (int64_t i = done + tid; i < jb.bytes; i += gstride) jb.dst[i] = jb.src[i];
+    const int64_t tail0 = head + nbody * g;
+    const int64_t nrest = head + (jb.bytes - tail0);
+    for (int64_t k = tid; k < nrest; k += gstride) {
+        const int64_t i = k < head ? k : tail0 + (k - head);
+        jb.dst[i] = jb.src[i];
+    }
     __syncthreads();
     if (threadIdx.x == 0) sys_release();
 }
@@ -451,10 +463,14 @@ static int launch_reduce(ompi_amd_comm_t *c, int op, int type, const ptr_set &sr
     int64_t most = 0;
     for (int i = 0; i < jobs.n; ++i) {
         red_job &j = jobs.j[i];
-        bool al = ((uintptr_t)((const char *)dst + j.off_dst * ext) & 15) == 0;
+        // every source and dst must sit at the same phase mod 16 B, and that
+        // phase must be a whole number of elements from 16-B alignment
+        const uintptr_t ph = (uintptr_t)((const char *)dst + j.off_dst * ext) & 15;
+        bool same = ext <= 16 && 16 % ext == 0;
         for (int r = 0; r < c->size; ++r)
-            al = al && (((uintptr_t)(src.p[r] + j.off * ext)) & 15) == 0;
-        j.vec = (al && ext <= 16 && 16 % ext == 0) ? 1 : 0;
+            same = same && ((((uintptr_t)(src.p[r] + j.off * ext)) & 15) == ph);
+        const int64_t lead = (int64_t)((16 - ph) & 15);
+        j.head = (same && lead % (int64_t)ext == 0) ? (int)std::min<int64_t>(lead / (int64_t)ext, j.cnt) : -1;
         most = std::max(most, j.cnt);
     }
     const int64_t per = (int64_t)(16 / ext) * kXferThreads;
@@ -519,7 +535,7 @@ static void ring_jobs(int64_t count, int n, red_jobs *jobs, int only_block) {
         j.cnt = block_cnt(b, split, early, late);
         j.off_dst = j.off;
         j.first = b;
-        j.vec = 0;
+        j.head = -1;
     }
 }
 
@@ -731,7 +747,7 @@ int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
         TRY(launch_barrier(c, s));
         if (tree) {
             jobs.n = 1;
-            jobs.j[0] = {0, (int64_t)count, 0, 0, 0};
+            jobs.j[0] = {0, (int64_t)count, 0, 0, -1};
         } else {
             ring_jobs((int64_t)count, n, &jobs, -1);
         }
@@ -776,7 +792,7 @@ int ompi_amd_reduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *rb
     const void *src = inplace ? rbuf : sbuf;  // in place: the input is rbuf (n*rcount)
     red_jobs jobs;
     jobs.n = 1;
-    jobs.j[0] = {(int64_t)(rcount * (size_t)c->rank), (int64_t)rcount, 0, 0, 0};
+    jobs.j[0] = {(int64_t)(rcount * (size_t)c->rank), (int64_t)rcount, 0, 0, -1};
     if (n == 1) {
         if (inplace) return OMPI_AMD_SUCCESS;
         return record_hip(hipMemcpyAsync(rbuf, src, rcount * ext, hipMemcpyDeviceToDevice, s), "copy");
