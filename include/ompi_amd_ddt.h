@@ -22,6 +22,17 @@ typedef struct {
     int64_t len;    /* bytes (> 0) */
 } ompi_amd_ddt_block_t;
 
+/* One element of the device program: `count` runs of `blocklen` bytes,
+ * `stride` bytes apart, the first at `disp` — the shape of opal's optimized
+ * ddt_elem_desc {count, blocklen, extent, disp} (opal_datatype_internal.h:
+ * 157-164).  MPI_Type_vector(n, bl, st, MPI_DOUBLE) is ONE such element. */
+typedef struct {
+    int64_t count;
+    int64_t blocklen;
+    int64_t stride;
+    int64_t disp;
+} ompi_amd_ddt_elem_t;
+
 typedef struct ompi_amd_ddt ompi_amd_ddt_t;
 
 /* Build the device program of a datatype from its typemap (nblocks runs in
@@ -31,6 +42,9 @@ typedef struct ompi_amd_ddt ompi_amd_ddt_t;
  * opal_datatype_internal.h:157-164; opal_datatype_optimize.c:261). */
 int ompi_amd_ddt_create(const ompi_amd_ddt_block_t *blocks, int nblocks,
                         int64_t extent, ompi_amd_ddt_t **ddt);
+/* Same, from an already-optimized element list (typemap order). */
+int ompi_amd_ddt_create_elems(const ompi_amd_ddt_elem_t *elems, int nelems,
+                              int64_t extent, ompi_amd_ddt_t **ddt);
 int ompi_amd_ddt_destroy(ompi_amd_ddt_t *ddt);
 /* packed bytes per datatype element (the MPI type size) */
 size_t ompi_amd_ddt_size(const ompi_amd_ddt_t *ddt);

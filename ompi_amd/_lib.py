@@ -55,6 +55,11 @@ class DdtBlock(ctypes.Structure):
     _fields_ = [("disp", ctypes.c_int64), ("len", ctypes.c_int64)]
 
 
+class DdtElem(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_int64), ("blocklen", ctypes.c_int64),
+                ("stride", ctypes.c_int64), ("disp", ctypes.c_int64)]
+
+
 # (name, restype, argtypes) for every symbol include/ompi_amd.h declares
 _C = ctypes
 PROTOTYPES = [
@@ -75,6 +80,8 @@ PROTOTYPES = [
     ("ompi_amd_set_tuning", _C.c_int, [_C.c_char_p, _C.c_int64]),
     ("ompi_amd_ddt_create", _C.c_int,
      [_C.POINTER(DdtBlock), _C.c_int, _C.c_int64, _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_ddt_create_elems", _C.c_int,
+     [_C.POINTER(DdtElem), _C.c_int, _C.c_int64, _C.POINTER(_C.c_void_p)]),
     ("ompi_amd_ddt_destroy", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_ddt_size", _C.c_size_t, [_C.c_void_p]),
     ("ompi_amd_ddt_nelems", _C.c_int, [_C.c_void_p]),

@@ -191,38 +191,24 @@ using namespace ompi_amd;
 
 extern "C" {
 
-int ompi_amd_ddt_create(const ompi_amd_ddt_block_t *blocks, int nblocks, int64_t extent,
-                        ompi_amd_ddt_t **out) {
-    if (!out || nblocks <= 0 || !blocks) return OMPI_AMD_ERR_BAD_PARAM;
-    // 1) merge runs that touch (disp_i + len_i == disp_{i+1})
-    std::vector<ompi_amd_ddt_block_t> runs;
-    for (int i = 0; i < nblocks; ++i) {
-        if (blocks[i].len <= 0) return OMPI_AMD_ERR_BAD_PARAM;
-        if (!runs.empty() && runs.back().disp + runs.back().len == blocks[i].disp)
-            runs.back().len += blocks[i].len;
-        else
-            runs.push_back(blocks[i]);
-    }
-    // 2) fold equal-length runs at a constant stride into one element
+int ompi_amd_ddt_create_elems(const ompi_amd_ddt_elem_t *elems, int nelems, int64_t extent,
+                              ompi_amd_ddt_t **out) {
+    if (!out || nelems <= 0 || !elems) return OMPI_AMD_ERR_BAD_PARAM;
     auto *d = new (std::nothrow) ompi_amd_ddt;
     if (!d) return OMPI_AMD_ERR_BAD_PARAM;
     int64_t prefix = 0;
     uint64_t gcd_acc = (uint64_t)(extent < 0 ? -extent : extent);
-    for (size_t i = 0; i < runs.size();) {
-        ddt_elem e{1, runs[i].len, runs[i].len, runs[i].disp, prefix};
-        size_t j = i + 1;
-        if (j < runs.size() && runs[j].len == e.blen) {
-            const int64_t st = runs[j].disp - runs[i].disp;
-            while (j < runs.size() && runs[j].len == e.blen &&
-                   runs[j].disp - runs[j - 1].disp == st) ++j;
-            e.count = (int64_t)(j - i);
-            e.stride = st;
+    for (int i = 0; i < nelems; ++i) {
+        const ompi_amd_ddt_elem_t &x = elems[i];
+        if (x.count <= 0 || x.blocklen <= 0) {
+            delete d;
+            return OMPI_AMD_ERR_BAD_PARAM;
         }
+        ddt_elem e{x.count, x.blocklen, x.count > 1 ? x.stride : x.blocklen, x.disp, prefix};
         prefix += e.count * e.blen;
         gcd_acc |= (uint64_t)e.blen | (uint64_t)(e.disp < 0 ? -e.disp : e.disp) |
                    (uint64_t)(e.stride < 0 ? -e.stride : e.stride);
         d->host.push_back(e);
-        i = j;
     }
     d->size = prefix;
     d->extent = extent;
@@ -238,6 +224,36 @@ int ompi_amd_ddt_create(const ompi_amd_ddt_block_t *blocks, int nblocks, int64_t
     }
     *out = d;
     return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_ddt_create(const ompi_amd_ddt_block_t *blocks, int nblocks, int64_t extent,
+                        ompi_amd_ddt_t **out) {
+    if (!out || nblocks <= 0 || !blocks) return OMPI_AMD_ERR_BAD_PARAM;
+    // 1) merge runs that touch (disp_i + len_i == disp_{i+1})
+    std::vector<ompi_amd_ddt_block_t> runs;
+    for (int i = 0; i < nblocks; ++i) {
+        if (blocks[i].len <= 0) return OMPI_AMD_ERR_BAD_PARAM;
+        if (!runs.empty() && runs.back().disp + runs.back().len == blocks[i].disp)
+            runs.back().len += blocks[i].len;
+        else
+            runs.push_back(blocks[i]);
+    }
+    // 2) fold equal-length runs at a constant stride into one element
+    std::vector<ompi_amd_ddt_elem_t> elems;
+    for (size_t i = 0; i < runs.size();) {
+        ompi_amd_ddt_elem_t e{1, runs[i].len, runs[i].len, runs[i].disp};
+        size_t j = i + 1;
+        if (j < runs.size() && runs[j].len == e.blocklen) {
+            const int64_t st = runs[j].disp - runs[i].disp;
+            while (j < runs.size() && runs[j].len == e.blocklen &&
+                   runs[j].disp - runs[j - 1].disp == st) ++j;
+            e.count = (int64_t)(j - i);
+            e.stride = st;
+        }
+        elems.push_back(e);
+        i = j;
+    }
+    return ompi_amd_ddt_create_elems(elems.data(), (int)elems.size(), extent, out);
 }
 
 int ompi_amd_ddt_destroy(ompi_amd_ddt_t *ddt) {

@@ -21,14 +21,14 @@ def dev_bytes(n, seed=None, offset=0):
 
 
 def span_of(dt, count):
-    return (count - 1) * dt.extent + max(d + n for d, n in dt.runs)
+    return (count - 1) * dt.extent + dt.true_span
 
 
 def kat_types(golden):
     out = []
     for t in golden("ddt_kat.json")["types"]:
         blocks = [tuple(b) for b in t["blocks"]]
-        dt = dd.Datatype(t["name"], blocks, 0, t["extent"])
+        dt = dd.from_runs(t["name"], blocks, t["extent"])
         out.append((dt, t["count"], t["chunks"], blocks))
     return out
 

@@ -226,3 +226,29 @@ def test_ddt_pack_unpack_kat(orc, golden):
                 n = orc.unpack(blocks, t["extent"], count, full[pos:pos + chunk].copy(), dst, pos)
                 pos += n
             assert np.array_equal(_np_pack(blocks, t["extent"], count, dst), full)
+
+
+def test_datatype_builders_match_reference_types(golden):
+    """The host-side constructors (ompi_amd/datatype.py) reproduce the
+    typemaps, sizes and extents of the reference tests' datatypes, and fold
+    them the way opal's optimizer does (vector -> 1 element, blacs -> 13)."""
+    from ompi_amd import datatype as dd
+    d, i32 = dd.predefined("MPI_DOUBLE"), dd.predefined("MPI_INT")
+    kat = {t["name"]: t for t in golden("ddt_kat.json")["types"]}
+    lens = [13, 13, 13, 13, 13, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1]
+    disps = [286, 308, 330, 352, 374, 396, 419, 442, 465, 488, 511, 534, 557, 580, 603,
+             626, 649, 672]
+    built = {
+        "vector_450_10_11_double": (dd.type_vector(450, 10, 11, d), 1),
+        "blacs_indexed_int": (dd.type_indexed(lens, disps, i32), 13),
+        "upper_matrix_100": (dd.type_indexed([100 - k for k in range(100)],
+                                             [k * 100 + k for k in range(100)], d), 100),
+        "struct_char_double": (dd.type_struct([1, 1], [0, 8], [dd.predefined("MPI_CHAR"), d]), 2),
+        "twice_two_doubles": (dd.type_vector(2, 2, 5, d), 1),
+        "struct_int_double": (dd.type_struct([1, 1], [0, 8], [i32, d]), 2),
+    }
+    for name, (dt, nel) in built.items():
+        t = kat[name]
+        assert dt.runs == [tuple(b) for b in t["blocks"]], name
+        assert dt.size == t["size"] and dt.extent == t["extent"], name
+        assert len(dt.elems) == nel, (name, dt.elems[:4])

@@ -21,7 +21,7 @@ PEAK = 8000.0
 
 
 def span(dt, count):
-    return (count - 1) * dt.extent + max(d + n for d, n in dt.runs)
+    return (count - 1) * dt.extent + dt.true_span
 
 
 def bench_type(name, dt, count, chunks, top_iters=20):
