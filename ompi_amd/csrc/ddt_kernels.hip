@@ -28,12 +28,35 @@
 
 namespace ompi_amd {
 
+// Division by a launch-invariant 32-bit divisor d as multiply-high + shifts
+// (Granlund-Montgomery round-up method): q = (t + ((n - t) >> s1)) >> s2,
+// t = umulhi(n, m); d = 1 gives m = 0, s1 = s2 = 0.  Exact for every
+// 32-bit n.  Replaces two v_div-style ~40-instruction sequences per granule.
+struct fastdiv {
+    uint32_t m, s1, s2;
+};
+
+static fastdiv make_fdiv(uint32_t d) {
+    if (d <= 1) return {0u, 0u, 0u};
+    uint32_t l = 0;
+    while ((1ull << l) < d) ++l;  // ceil(log2 d)
+    const uint64_t m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+    return {(uint32_t)m, 1u, l - 1};
+}
+
+__device__ __forceinline__ uint32_t fdiv_q(uint32_t n, const fastdiv &f) {
+    const uint32_t t = __umulhi(n, f.m);
+    return (t + ((n - t) >> f.s1)) >> f.s2;
+}
+
 struct ddt_elem {
     int64_t count;   // repetitions
     int64_t blen;    // bytes per repetition
     int64_t stride;  // bytes between repetitions
     int64_t disp;    // byte displacement of the first repetition
     int64_t prefix;  // packed bytes of the type before this element
+    fastdiv bdiv[5];    // blen / G for G = 1, 2, 4, 8, 16 (when it fits 32 bits)
+    uint32_t pad;
 };
 
 constexpr int kDdtThreads = 256;
@@ -44,6 +67,7 @@ struct ddt_desc {
     int nelem;
     int64_t size;    // packed bytes per datatype element
     int64_t extent;
+    fastdiv sdiv;       // size / G of this launch (fast path only)
 };
 
 // Largest i with elems[i].prefix <= q.
@@ -82,12 +106,46 @@ __device__ __forceinline__ int64_t typed_offset(const ddt_elem *e, int n, I size
     return (int64_t)el * extent + e[i].disp + (int64_t)k * e[i].stride + (int64_t)w;
 }
 
-// UNPACK = false: dst[p - start] = typed[p];  true: typed[p] = src[p - start].
-// Granules cover stream positions [start + j*G, ...), j < ngran.
+// Fast path: all quantities in G-granule units fit 32 bits.
+template <int G>
+__device__ __forceinline__ int64_t typed_offset_fast(const ddt_elem *e, int n, uint32_t size_g,
+                                                     const fastdiv &sdiv, int64_t extent,
+                                                     uint32_t pg) {
+    constexpr int LG = G == 16 ? 4 : G == 8 ? 3 : G == 4 ? 2 : G == 2 ? 1 : 0;
+    const uint32_t el = fdiv_q(pg, sdiv);
+    const uint32_t q = pg - el * size_g;
+    const int i = find_elem(e, n, (int64_t)q << LG);
+    const uint32_t r = q - (uint32_t)(e[i].prefix >> LG);
+    const uint32_t k = fdiv_q(r, e[i].bdiv[LG]);
+    const uint32_t w = r - k * (uint32_t)(e[i].blen >> LG);
+    return (int64_t)el * extent + e[i].disp + (int64_t)k * e[i].stride + ((int64_t)w << LG);
+}
+
+// One convertor window [start, start + head + ngran*G + tail) of the packed
+// stream: a G-granule body plus byte-granule head/tail (when the window
+// starts or ends off the granule grid), all in ONE launch.
+struct ddt_window {
+    int64_t start;   // stream position of contiguous byte 0
+    int64_t body0;   // first body position (multiple of G)
+    int64_t ngran;   // body granules
+    int64_t head;    // bytes [start, start + head)
+    int64_t tail0;   // tail bytes [tail0, tail0 + tail)
+    int64_t tail;
+};
+
+template <bool UNPACK>
+__device__ __forceinline__ void move_byte(const ddt_elem *el, const ddt_desc &d, const char *src,
+                                          char *dst, int64_t p, int64_t start) {
+    const int64_t t = typed_offset<uint64_t>(el, d.nelem, (uint64_t)d.size, d.extent, (uint64_t)p);
+    if (!UNPACK) dst[p - start] = src[t];
+    else dst[t] = src[p - start];
+}
+
+// UNPACK = false: contig[p - start] = typed[p];  true: typed[p] = contig[p - start].
+// I = uint32_t: fast-division path (stream position / G < 2^32).
 template <int G, bool UNPACK, typename I>
 __global__ __launch_bounds__(kDdtThreads) void ddt_kernel(ddt_desc d, const char *src, char *dst,
-                                                          int64_t start, int64_t ngran,
-                                                          int64_t packed_base) {
+                                                          ddt_window w) {
     __shared__ ddt_elem lds[kDdtLdsElems];
     const ddt_elem *el = d.elems;
     if (d.nelem <= kDdtLdsElems) {
@@ -97,14 +155,25 @@ __global__ __launch_bounds__(kDdtThreads) void ddt_kernel(ddt_desc d, const char
     }
     using T = typename granule<G>::t;
     const int64_t stride = (int64_t)gridDim.x * kDdtThreads;
-    for (int64_t j = (int64_t)blockIdx.x * kDdtThreads + threadIdx.x; j < ngran; j += stride) {
-        const int64_t p = start + j * G;
-        const int64_t t = typed_offset<I>(el, d.nelem, (I)d.size, d.extent, (I)p);
-        const int64_t c = p - packed_base;  // offset in the contiguous buffer
+    for (int64_t j = (int64_t)blockIdx.x * kDdtThreads + threadIdx.x; j < w.ngran; j += stride) {
+        const int64_t p = w.body0 + j * G;
+        int64_t t;
+        if constexpr (sizeof(I) == 4)
+            t = typed_offset_fast<G>(el, d.nelem, (uint32_t)(d.size / G), d.sdiv, d.extent,
+                                     (uint32_t)(p / G));
+        else
+            t = typed_offset<I>(el, d.nelem, (I)d.size, d.extent, (I)p);
+        const int64_t c = p - w.start;  // offset in the contiguous buffer
         if (!UNPACK) {
             *reinterpret_cast<T *>(dst + c) = *reinterpret_cast<const T *>(src + t);
         } else {
             *reinterpret_cast<T *>(dst + t) = *reinterpret_cast<const T *>(src + c);
+        }
+    }
+    if (blockIdx.x == gridDim.x - 1) {
+        for (int64_t k = threadIdx.x; k < w.head + w.tail; k += kDdtThreads) {
+            const int64_t p = k < w.head ? w.start + k : w.tail0 + (k - w.head);
+            move_byte<UNPACK>(el, d, src, dst, p, w.start);
         }
     }
 }
@@ -116,6 +185,7 @@ struct ompi_amd_ddt {
     ompi_amd::ddt_elem *dev = nullptr;
     int64_t size = 0;
     int64_t extent = 0;
+    int64_t max_blen = 0;
     int gran = 1;  // power of two dividing every blen, disp, stride, extent
 };
 
@@ -128,18 +198,17 @@ static int pow2_gran(uint64_t v) {
 }
 
 template <bool UNPACK, typename I>
-static hipError_t launch_g(int G, const ddt_desc &d, const char *src, char *dst, int64_t start,
-                           int64_t ngran, int64_t base, hipStream_t s) {
-    if (ngran <= 0) return hipSuccess;
-    int64_t blocks = (ngran + kDdtThreads - 1) / kDdtThreads;
-    blocks = std::min<int64_t>(blocks, 4096);
+static hipError_t launch_g(int G, const ddt_desc &d, const char *src, char *dst,
+                           const ddt_window &w, hipStream_t s) {
+    int64_t blocks = (w.ngran + kDdtThreads - 1) / kDdtThreads;
+    blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, 4096));
     const dim3 grid((unsigned)blocks), block(kDdtThreads);
     switch (G) {
-    case 16: hipLaunchKernelGGL((ddt_kernel<16, UNPACK, I>), grid, block, 0, s, d, src, dst, start, ngran, base); break;
-    case 8: hipLaunchKernelGGL((ddt_kernel<8, UNPACK, I>), grid, block, 0, s, d, src, dst, start, ngran, base); break;
-    case 4: hipLaunchKernelGGL((ddt_kernel<4, UNPACK, I>), grid, block, 0, s, d, src, dst, start, ngran, base); break;
-    case 2: hipLaunchKernelGGL((ddt_kernel<2, UNPACK, I>), grid, block, 0, s, d, src, dst, start, ngran, base); break;
-    default: hipLaunchKernelGGL((ddt_kernel<1, UNPACK, I>), grid, block, 0, s, d, src, dst, start, ngran, base); break;
+    case 16: hipLaunchKernelGGL((ddt_kernel<16, UNPACK, I>), grid, block, 0, s, d, src, dst, w); break;
+    case 8: hipLaunchKernelGGL((ddt_kernel<8, UNPACK, I>), grid, block, 0, s, d, src, dst, w); break;
+    case 4: hipLaunchKernelGGL((ddt_kernel<4, UNPACK, I>), grid, block, 0, s, d, src, dst, w); break;
+    case 2: hipLaunchKernelGGL((ddt_kernel<2, UNPACK, I>), grid, block, 0, s, d, src, dst, w); break;
+    default: hipLaunchKernelGGL((ddt_kernel<1, UNPACK, I>), grid, block, 0, s, d, src, dst, w); break;
     }
     return hipGetLastError();
 }
@@ -154,7 +223,7 @@ static int ddt_run(const ompi_amd_ddt_t *ddt, size_t count, const void *typed, v
     if (bytes > total - offset) bytes = (size_t)(total - offset);
     if (!contig) return OMPI_AMD_ERR_BAD_PARAM;
 
-    ddt_desc d{ddt->dev, (int)ddt->host.size(), ddt->size, ddt->extent};
+    ddt_desc d{ddt->dev, (int)ddt->host.size(), ddt->size, ddt->extent, {0u, 0u, 0u}};
     // Granule: divides the type program, the typed base and the contiguous
     // buffer's alignment relative to the stream position.
     const uint64_t contig_skew = (uint64_t)((uintptr_t)contig - (uintptr_t)offset);
@@ -165,20 +234,19 @@ static int ddt_run(const ompi_amd_ddt_t *ddt, size_t count, const void *typed, v
     // contiguous buffer is indexed from `offset`: pass base = offset
     const char *tsrc = UNPACK ? (const char *)contig : (const char *)typed;
     char *tdst = UNPACK ? (char *)typed : (char *)contig;
-    hipError_t e = hipSuccess;
-    const bool small = total < (1ull << 31);
-    auto go = [&](int g, int64_t from, int64_t to) {
-        if (e != hipSuccess || to <= from) return;
-        const int64_t ng = (to - from) / g;
-        e = small ? launch_g<UNPACK, uint32_t>(g, d, tsrc, tdst, from, ng, start, s)
-                  : launch_g<UNPACK, uint64_t>(g, d, tsrc, tdst, from, ng, start, s);
-    };
-    if (body0 >= end) {
-        go(1, start, end);
+    ddt_window w{start, body0, (body1 - body0) / G, body0 - start, body1, end - body1};
+    if (body0 >= end) w = {start, start, 0, end - start, end, 0};
+    // 32-bit granule arithmetic when positions, the type size and every
+    // blocklen fit in G units
+    const bool fast = total / (uint64_t)G < (1ull << 32) &&
+                      (uint64_t)ddt->max_blen / (uint64_t)G < (1ull << 32) &&
+                      (uint64_t)ddt->size / (uint64_t)G < (1ull << 32);
+    hipError_t e;
+    if (fast) {
+        d.sdiv = make_fdiv((uint32_t)(ddt->size / G));
+        e = launch_g<UNPACK, uint32_t>(G, d, tsrc, tdst, w, s);
     } else {
-        go(1, start, body0);
-        go(G, body0, body1);
-        go(1, body1, end);
+        e = launch_g<UNPACK, uint64_t>(G, d, tsrc, tdst, w, s);
     }
     if (e != hipSuccess) return record_hip(e, "ddt kernel launch");
     *done = bytes;
@@ -204,7 +272,13 @@ int ompi_amd_ddt_create_elems(const ompi_amd_ddt_elem_t *elems, int nelems, int6
             delete d;
             return OMPI_AMD_ERR_BAD_PARAM;
         }
-        ddt_elem e{x.count, x.blocklen, x.count > 1 ? x.stride : x.blocklen, x.disp, prefix};
+        ddt_elem e{x.count, x.blocklen, x.count > 1 ? x.stride : x.blocklen, x.disp, prefix, {}, 0};
+        for (int lg = 0; lg < 5; ++lg) {
+            const int64_t bg = e.blen >> lg;
+            e.bdiv[lg] = ((e.blen & ((1 << lg) - 1)) == 0 && bg < (1ll << 32))
+                             ? make_fdiv((uint32_t)bg) : fastdiv{0u, 0u, 0u};
+        }
+        d->max_blen = std::max(d->max_blen, e.blen);
         prefix += e.count * e.blen;
         gcd_acc |= (uint64_t)e.blen | (uint64_t)(e.disp < 0 ? -e.disp : e.disp) |
                    (uint64_t)(e.stride < 0 ? -e.stride : e.stride);
