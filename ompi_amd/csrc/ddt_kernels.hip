@@ -60,6 +60,7 @@ struct ddt_elem {
 };
 
 constexpr int kDdtThreads = 256;
+constexpr int kDdtUnroll = 4;
 constexpr int kDdtLdsElems = 256;
 
 struct ddt_desc {
@@ -154,20 +155,42 @@ __global__ __launch_bounds__(kDdtThreads) void ddt_kernel(ddt_desc d, const char
         el = lds;
     }
     using T = typename granule<G>::t;
+    constexpr int U = kDdtUnroll;
     const int64_t stride = (int64_t)gridDim.x * kDdtThreads;
-    for (int64_t j = (int64_t)blockIdx.x * kDdtThreads + threadIdx.x; j < w.ngran; j += stride) {
-        const int64_t p = w.body0 + j * G;
-        int64_t t;
-        if constexpr (sizeof(I) == 4)
-            t = typed_offset_fast<G>(el, d.nelem, (uint32_t)(d.size / G), d.sdiv, d.extent,
-                                     (uint32_t)(p / G));
-        else
-            t = typed_offset<I>(el, d.nelem, (I)d.size, d.extent, (I)p);
-        const int64_t c = p - w.start;  // offset in the contiguous buffer
-        if (!UNPACK) {
-            *reinterpret_cast<T *>(dst + c) = *reinterpret_cast<const T *>(src + t);
-        } else {
-            *reinterpret_cast<T *>(dst + t) = *reinterpret_cast<const T *>(src + c);
+    // U granules per lane per pass, lane-contiguous for each u: all U
+    // typed addresses first, then U loads in flight, then U stores
+    for (int64_t j0 = (int64_t)blockIdx.x * kDdtThreads + threadIdx.x; j0 < w.ngran;
+         j0 += stride * U) {
+        int64_t toff[U];
+        T v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = j0 + u * stride;
+            const int64_t p = w.body0 + j * G;
+            if (j < w.ngran) {
+                if constexpr (sizeof(I) == 4)
+                    toff[u] = typed_offset_fast<G>(el, d.nelem, (uint32_t)(d.size / G), d.sdiv,
+                                                   d.extent, (uint32_t)(p / G));
+                else
+                    toff[u] = typed_offset<I>(el, d.nelem, (I)d.size, d.extent, (I)p);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = j0 + u * stride;
+            const int64_t c = w.body0 + j * G - w.start;  // offset in the contiguous buffer
+            if (j < w.ngran)
+                v[u] = UNPACK ? *reinterpret_cast<const T *>(src + c)
+                              : *reinterpret_cast<const T *>(src + toff[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = j0 + u * stride;
+            const int64_t c = w.body0 + j * G - w.start;
+            if (j < w.ngran) {
+                if (UNPACK) *reinterpret_cast<T *>(dst + toff[u]) = v[u];
+                else *reinterpret_cast<T *>(dst + c) = v[u];
+            }
         }
     }
     if (blockIdx.x == gridDim.x - 1) {
@@ -200,8 +223,8 @@ static int pow2_gran(uint64_t v) {
 template <bool UNPACK, typename I>
 static hipError_t launch_g(int G, const ddt_desc &d, const char *src, char *dst,
                            const ddt_window &w, hipStream_t s) {
-    int64_t blocks = (w.ngran + kDdtThreads - 1) / kDdtThreads;
-    blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, 4096));
+    int64_t blocks = (w.ngran + kDdtThreads * kDdtUnroll - 1) / (kDdtThreads * kDdtUnroll);
+    blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, 8192));
     const dim3 grid((unsigned)blocks), block(kDdtThreads);
     switch (G) {
     case 16: hipLaunchKernelGGL((ddt_kernel<16, UNPACK, I>), grid, block, 0, s, d, src, dst, w); break;
@@ -238,7 +261,8 @@ static int ddt_run(const ompi_amd_ddt_t *ddt, size_t count, const void *typed, v
     if (body0 >= end) w = {start, start, 0, end - start, end, 0};
     // 32-bit granule arithmetic when positions, the type size and every
     // blocklen fit in G units
-    const bool fast = total / (uint64_t)G < (1ull << 32) &&
+    static const bool fast_ok = !getenv("OMPI_AMD_DDT_FASTDIV") || atoi(getenv("OMPI_AMD_DDT_FASTDIV"));
+    const bool fast = fast_ok && total / (uint64_t)G < (1ull << 32) &&
                       (uint64_t)ddt->max_blen / (uint64_t)G < (1ull << 32) &&
                       (uint64_t)ddt->size / (uint64_t)G < (1ull << 32);
     hipError_t e;
