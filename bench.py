@@ -39,6 +39,8 @@ def parse():
     p.add_argument("--ar-bytes", type=int, default=256 << 20, help="allreduce bytes (N>1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--no-extras", action="store_true",
+                   help="N>1: skip the exactness check, size sweep and configs[4] collectives")
     return p.parse_args()
 
 

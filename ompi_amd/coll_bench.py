@@ -119,7 +119,82 @@ def bench_allreduce(args, metric: str, link_gbs: float):
         "shared_gpu_rehearsal": shared,
         "device_error": err,
     }
+    if not args.no_extras:
+        try:
+            res["check"] = _check_exact(comm, dist, torch, mop, n, rank, shared)
+            res["sweep"] = _sweep(comm, dist, torch, mop, world, shared, tdev)
+            res["config5"] = _config5(comm, dist, torch, mop, world, rank, tdev)
+        except Exception as e:  # extras never break the headline line
+            res["extras_error"] = f"{type(e).__name__}: {e}"
     comm.free()
     dist.barrier()
     dist.destroy_process_group()
     return res if rank == 0 else None
+
+
+def _check_exact(comm, dist, torch, mop, n, rank, shared):
+    """Dataset E (k * 2^-8, |k| <= 1024): every summation order is exact,
+    so our result must equal RCCL's (and the integer sum) bit for bit."""
+    g = torch.Generator(device="cuda").manual_seed(777 + rank)
+    k = torch.randint(-1024, 1025, (n,), device="cuda", generator=g, dtype=torch.int32)
+    x = k.to(torch.float32) * (2.0 ** -8)
+    y = torch.empty_like(x)
+    comm.allreduce(x, y, n, mop.MPI_FLOAT, mop.MPI_SUM, blocking=True)
+    if shared:
+        return {"dataset": "E", "note": "shared-GPU rehearsal: exactness checked by tests"}
+    ksum = k.clone()
+    dist.all_reduce(ksum)
+    exact = ksum.to(torch.float32) * (2.0 ** -8)
+    ok = bool(torch.equal(y, exact))
+    flag = torch.tensor([1 if ok else 0], device="cuda")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return {"dataset": "E", "bytes": n * 4, "bit_exact_all_ranks": bool(flag.item())}
+
+
+def _sweep(comm, dist, torch, mop, world, shared, tdev):
+    """BASELINE configs[3]: fp32 SUM allreduce busBW, 8 B .. 1 GiB, ours
+    and RCCL side by side."""
+    out = []
+    factor = 2.0 * (world - 1) / world
+    for nbytes in (8, 1024, 65536, 1 << 20, 16 << 20, 64 << 20, 256 << 20, 1 << 30):
+        n = max(1, nbytes // 4)
+        x = torch.ones(n, device="cuda")
+        y = torch.empty_like(x)
+        steps = 20 if nbytes <= (64 << 20) else 5
+        t = _timed(lambda: comm.allreduce(x, y, n, mop.MPI_FLOAT, mop.MPI_SUM), steps, 3,
+                   dist, torch, tdev) / steps
+        row = {"bytes": n * 4, "us": round(t * 1e6, 2),
+               "busbw": round(n * 4 / t * factor / 1e9, 3)}
+        if not shared:
+            tr = _timed(lambda: dist.all_reduce(x), steps, 3, dist, torch) / steps
+            row["rccl_us"] = round(tr * 1e6, 2)
+            row["rccl_busbw"] = round(n * 4 / tr * factor / 1e9, 3)
+        out.append(row)
+        del x, y
+    return out
+
+
+def _config5(comm, dist, torch, mop, world, rank, tdev):
+    """BASELINE configs[4]: reduce_scatter_block (MPI_DOUBLE_INT MAXLOC),
+    allgather and bcast, 64 MiB per rank; busBW per nccl-tests convention."""
+    res = {}
+    rcount = (64 << 20) // 16 // world
+    buf = torch.zeros(rcount * world * 16, dtype=torch.uint8, device="cuda")
+    out = torch.zeros(rcount * 16, dtype=torch.uint8, device="cuda")
+    S = rcount * world * 16
+    t = _timed(lambda: comm.reduce_scatter_block(buf, out, rcount, mop.MPI_DOUBLE_INT,
+                                                 mop.MPI_MAXLOC), 10, 3, dist, torch, tdev) / 10
+    res["reduce_scatter_block_maxloc_double_int"] = {
+        "bytes_total": S, "us": round(t * 1e6, 2),
+        "busbw": round(S / t * (world - 1) / world / 1e9, 3)}
+    per = (64 << 20) // world
+    src = torch.zeros(per, dtype=torch.uint8, device="cuda")
+    dst = torch.zeros(per * world, dtype=torch.uint8, device="cuda")
+    t = _timed(lambda: comm.allgather(src, dst, per), 10, 3, dist, torch, tdev) / 10
+    res["allgather"] = {"bytes_total": per * world, "us": round(t * 1e6, 2),
+                        "busbw": round(per * world / t * (world - 1) / world / 1e9, 3)}
+    b = torch.zeros(64 << 20, dtype=torch.uint8, device="cuda")
+    t = _timed(lambda: comm.bcast(b, b.numel(), 0), 10, 3, dist, torch, tdev) / 10
+    res["bcast"] = {"bytes": b.numel(), "us": round(t * 1e6, 2),
+                    "busbw": round(b.numel() / t / 1e9, 3)}
+    return res
