@@ -60,7 +60,7 @@ struct ddt_elem {
 };
 
 constexpr int kDdtThreads = 256;
-constexpr int kDdtUnroll = 4;
+constexpr int kDdtUnroll = 8;
 constexpr int kDdtLdsElems = 256;
 
 struct ddt_desc {
@@ -224,7 +224,7 @@ template <bool UNPACK, typename I>
 static hipError_t launch_g(int G, const ddt_desc &d, const char *src, char *dst,
                            const ddt_window &w, hipStream_t s) {
     int64_t blocks = (w.ngran + kDdtThreads * kDdtUnroll - 1) / (kDdtThreads * kDdtUnroll);
-    blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, 8192));
+    blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, 1 << 20));
     const dim3 grid((unsigned)blocks), block(kDdtThreads);
     switch (G) {
     case 16: hipLaunchKernelGGL((ddt_kernel<16, UNPACK, I>), grid, block, 0, s, d, src, dst, w); break;
@@ -261,7 +261,9 @@ static int ddt_run(const ompi_amd_ddt_t *ddt, size_t count, const void *typed, v
     if (body0 >= end) w = {start, start, 0, end - start, end, 0};
     // 32-bit granule arithmetic when positions, the type size and every
     // blocklen fit in G units
-    static const bool fast_ok = !getenv("OMPI_AMD_DDT_FASTDIV") || atoi(getenv("OMPI_AMD_DDT_FASTDIV"));
+    // multiply-high division measured no faster than the 64-bit divide on
+    // MI355X (profiles/r01_ddt_sweep_*fastdiv.jsonl): opt-in only
+    static const bool fast_ok = getenv("OMPI_AMD_DDT_FASTDIV") && atoi(getenv("OMPI_AMD_DDT_FASTDIV"));
     const bool fast = fast_ok && total / (uint64_t)G < (1ull << 32) &&
                       (uint64_t)ddt->max_blen / (uint64_t)G < (1ull << 32) &&
                       (uint64_t)ddt->size / (uint64_t)G < (1ull << 32);
