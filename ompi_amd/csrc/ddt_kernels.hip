@@ -201,6 +201,74 @@ __global__ __launch_bounds__(kDdtThreads) void ddt_kernel(ddt_desc d, const char
     }
 }
 
+// Single-element datatypes (every vector / contiguous-of-runs type, the
+// common case): positions advance by a constant stride S granules per pass,
+// so each lane decomposes its first position once (el, k, w) with divisions
+// and then walks by constant increments with one carry per level — no
+// division in the loop.  position = el*size + disp + k*stride + w (granules
+// of G bytes within a run of blen bytes).
+struct ddt_walk {
+    int64_t count, bg, stride, disp, extent;  // bg = blen / G
+    int64_t size_g;                            // count * bg
+};
+
+template <int G, bool UNPACK>
+__global__ __launch_bounds__(kDdtThreads) void ddt_vec_kernel(ddt_walk v, const char *src,
+                                                              char *dst, ddt_window w) {
+    using T = typename granule<G>::t;
+    constexpr int U = kDdtUnroll;
+    const int64_t S = (int64_t)gridDim.x * kDdtThreads;  // granules per step
+    const int64_t S_el = S / v.size_g, S_q = S % v.size_g;
+    const int64_t S_k = S_q / v.bg, S_w = S_q % v.bg;
+    const int64_t j0 = (int64_t)blockIdx.x * kDdtThreads + threadIdx.x;
+    if (j0 < w.ngran) {
+        const int64_t pg0 = w.body0 / G + j0;
+        int64_t el = pg0 / v.size_g;
+        const int64_t q = pg0 - el * v.size_g;
+        int64_t k = q / v.bg;
+        int64_t ww = q - k * v.bg;
+        for (int64_t j = j0; j < w.ngran; j += S * U) {
+            int64_t toff[U];
+            T val[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                toff[u] = el * v.extent + v.disp + k * v.stride + ww * G;
+                ww += S_w;
+                k += S_k;
+                if (ww >= v.bg) { ww -= v.bg; ++k; }
+                if (k >= v.count) { k -= v.count; ++el; }
+                el += S_el;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t jj = j + u * S;
+                const int64_t c = w.body0 + jj * G - w.start;
+                if (jj < w.ngran)
+                    val[u] = UNPACK ? *reinterpret_cast<const T *>(src + c)
+                                    : *reinterpret_cast<const T *>(src + toff[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t jj = j + u * S;
+                const int64_t c = w.body0 + jj * G - w.start;
+                if (jj < w.ngran) {
+                    if (UNPACK) *reinterpret_cast<T *>(dst + toff[u]) = val[u];
+                    else *reinterpret_cast<T *>(dst + c) = val[u];
+                }
+            }
+        }
+    }
+}
+
+// byte head/tail of a single-element window (tiny; generic mapping)
+template <bool UNPACK>
+__global__ void ddt_vec_edges(ddt_desc d, const char *src, char *dst, ddt_window w) {
+    for (int64_t k = threadIdx.x; k < w.head + w.tail; k += blockDim.x) {
+        const int64_t p = k < w.head ? w.start + k : w.tail0 + (k - w.head);
+        move_byte<UNPACK>(d.elems, d, src, dst, p, w.start);
+    }
+}
+
 }  // namespace ompi_amd
 
 struct ompi_amd_ddt {
@@ -237,6 +305,26 @@ static hipError_t launch_g(int G, const ddt_desc &d, const char *src, char *dst,
 }
 
 template <bool UNPACK>
+static hipError_t launch_vec(int G, const ddt_walk &v, const ddt_desc &d, const char *src,
+                             char *dst, const ddt_window &w, hipStream_t s) {
+    if (w.ngran > 0) {
+        int64_t blocks = (w.ngran + kDdtThreads * kDdtUnroll - 1) / (kDdtThreads * kDdtUnroll);
+        blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, 1 << 20));
+        const dim3 grid((unsigned)blocks), block(kDdtThreads);
+        switch (G) {
+        case 16: hipLaunchKernelGGL((ddt_vec_kernel<16, UNPACK>), grid, block, 0, s, v, src, dst, w); break;
+        case 8: hipLaunchKernelGGL((ddt_vec_kernel<8, UNPACK>), grid, block, 0, s, v, src, dst, w); break;
+        case 4: hipLaunchKernelGGL((ddt_vec_kernel<4, UNPACK>), grid, block, 0, s, v, src, dst, w); break;
+        case 2: hipLaunchKernelGGL((ddt_vec_kernel<2, UNPACK>), grid, block, 0, s, v, src, dst, w); break;
+        default: hipLaunchKernelGGL((ddt_vec_kernel<1, UNPACK>), grid, block, 0, s, v, src, dst, w); break;
+        }
+    }
+    if (w.head + w.tail > 0)
+        hipLaunchKernelGGL((ddt_vec_edges<UNPACK>), dim3(1), dim3(64), 0, s, d, src, dst, w);
+    return hipGetLastError();
+}
+
+template <bool UNPACK>
 static int ddt_run(const ompi_amd_ddt_t *ddt, size_t count, const void *typed, void *contig,
                    size_t offset, size_t bytes, size_t *done, hipStream_t s) {
     if (!ddt || (!typed && count) || !done) return OMPI_AMD_ERR_BAD_PARAM;
@@ -268,7 +356,11 @@ static int ddt_run(const ompi_amd_ddt_t *ddt, size_t count, const void *typed, v
                       (uint64_t)ddt->max_blen / (uint64_t)G < (1ull << 32) &&
                       (uint64_t)ddt->size / (uint64_t)G < (1ull << 32);
     hipError_t e;
-    if (fast) {
+    if (ddt->host.size() == 1) {
+        const ddt_elem &x = ddt->host[0];
+        const ddt_walk v{x.count, x.blen / G, x.stride, x.disp, ddt->extent, x.count * (x.blen / G)};
+        e = launch_vec<UNPACK>(G, v, d, tsrc, tdst, w, s);
+    } else if (fast) {
         d.sdiv = make_fdiv((uint32_t)(ddt->size / G));
         e = launch_g<UNPACK, uint32_t>(G, d, tsrc, tdst, w, s);
     } else {
