@@ -32,7 +32,10 @@ namespace ompi_amd {
 #ifndef OMPI_AMD_OP_NT_STORES
 #define OMPI_AMD_OP_NT_STORES 1
 #endif
-constexpr int kOpThreads = 256;
+#ifndef OMPI_AMD_OP_THREADS
+#define OMPI_AMD_OP_THREADS 256
+#endif
+constexpr int kOpThreads = OMPI_AMD_OP_THREADS;
 constexpr int kOpUnroll = OMPI_AMD_OP_UNROLL;
 
 __device__ __forceinline__ u32x4 ld16(const u32x4 *p) {

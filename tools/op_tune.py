@@ -46,7 +46,7 @@ if __name__ == "__main__":
         run_variant(sys.argv[2], [int(x) for x in sys.argv[3].split(",")], int(sys.argv[4]),
                     int(sys.argv[5]))
         sys.exit(0)
-    blocks = "512,1024,2048,4096,8192,16384,65536"
+    blocks = os.environ.get("TUNE_BLOCKS", "16777216,8192,2048")
     nbytes = int(os.environ.get("TUNE_BYTES", 1 << 30))
     for lib in sorted(os.listdir(TUNE)):
         if lib.endswith(".so"):
