@@ -133,7 +133,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 or args.gpus > 1:
         from ompi_amd import coll_bench
-        res = coll_bench.bench_allreduce(args, METRIC, XGMI_LINK_GBS)
+        try:
+            res = coll_bench.bench_allreduce(args, METRIC, XGMI_LINK_GBS)
+        except Exception as e:
+            # say what failed on the one line the driver reads, then fail
+            if int(os.environ.get("RANK", "0")) == 0:
+                print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "GB/s",
+                                  "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                                  "higher_is_better": True, "scaling": "weak",
+                                  "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+                                  "config": {"workload": "MPI_Allreduce fp32 SUM 256 MiB"},
+                                  "error": f"{type(e).__name__}: {e}"}), flush=True)
+            raise
         if res is None:
             return
     else:

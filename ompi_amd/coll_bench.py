@@ -124,6 +124,7 @@ def bench_allreduce(args, metric: str, link_gbs: float):
             res["check"] = _check_exact(comm, dist, torch, mop, n, rank, shared)
             res["sweep"] = _sweep(comm, dist, torch, mop, world, shared, tdev)
             res["config5"] = _config5(comm, dist, torch, mop, world, rank, tdev)
+            res["variants"] = _variants(comm, dist, torch, mop, world, tdev)
         except Exception as e:  # extras never break the headline line
             res["extras_error"] = f"{type(e).__name__}: {e}"
     comm.free()
@@ -198,3 +199,37 @@ def _config5(comm, dist, torch, mop, world, rank, tdev):
     res["bcast"] = {"bytes": b.numel(), "us": round(t * 1e6, 2),
                     "busbw": round(b.numel() / t / 1e9, 3)}
     return res
+
+
+def _variants(comm, dist, torch, mop, world, tdev):
+    """Design A/B points measured in the same run (the multi-GPU node is only
+    reachable through this bench): workgroup count of the 256 MiB transfer
+    kernels, and staged one-shot (every rank folds all N blocks from the
+    peers' scratch) vs zero-copy two-shot (own block, then gather) around
+    the small_bytes switch."""
+    factor = 2.0 * (world - 1) / world
+    out = {"blocks_256MiB": [], "small_path": []}
+    n = (256 << 20) // 4
+    x = torch.ones(n, device="cuda")
+    y = torch.empty_like(x)
+    for blocks in (256, 512, 2048, 4096, 1024):
+        comm.set_param("blocks", blocks)
+        t = _timed(lambda: comm.allreduce(x, y, n, mop.MPI_FLOAT, mop.MPI_SUM), 5, 2,
+                   dist, torch, tdev) / 5
+        out["blocks_256MiB"].append({"blocks": blocks, "us": round(t * 1e6, 2),
+                                     "busbw": round(n * 4 / t * factor / 1e9, 3)})
+    del x, y
+    for nbytes in (64 << 10, 256 << 10, 1 << 20, 4 << 20):
+        n = nbytes // 4
+        x = torch.ones(n, device="cuda")
+        y = torch.empty_like(x)
+        row = {"bytes": nbytes}
+        for name, small in (("staged_one_shot", 4 << 20), ("zero_copy_two_shot", 0)):
+            comm.set_param("small_bytes", small)
+            t = _timed(lambda: comm.allreduce(x, y, n, mop.MPI_FLOAT, mop.MPI_SUM), 20, 3,
+                       dist, torch, tdev) / 20
+            row[name + "_us"] = round(t * 1e6, 2)
+        out["small_path"].append(row)
+        del x, y
+    comm.set_param("small_bytes", 1 << 20)
+    return out

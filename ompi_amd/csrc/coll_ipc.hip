@@ -304,8 +304,9 @@ struct ompi_amd_comm {
     ShmBoot boot;
     uint64_t *flags = nullptr;            // [kMaxRanks] epochs written by peers
     flag_set peer_flags{};
-    char *scratch = nullptr;              // staged-path landing zone
-    size_t scratch_bytes = 0;
+    char *scratch = nullptr;              // staged-path landing zone: two halves
+    size_t scratch_bytes = 0;             // bytes per half
+    uint64_t stage_seq = 0;               // staged calls so far (selects the half)
     ptr_set peer_scratch{};
     int *err_host = nullptr, *err_dev = nullptr;
     uint64_t epoch = 0;
@@ -523,6 +524,23 @@ static bool in_place(const void *sbuf, const void *rbuf) {
     return sbuf == rbuf || sbuf == (const void *)1;
 }
 
+// Staged calls alternate between the two scratch halves, so a call never
+// needs a trailing barrier: the next call that writes the same half comes
+// after the following call's barrier, which every peer passes only once
+// its reads of this half are done (stream order).  Every rank makes the
+// same sequence of staged calls, so the halves agree.
+struct stage_half {
+    char *mine;
+    ptr_set peers;
+};
+static stage_half next_half(ompi_amd_comm_t *c) {
+    const size_t h = (size_t)(c->stage_seq++ & 1) * c->scratch_bytes;
+    stage_half r;
+    r.mine = c->scratch + h;
+    for (int p = 0; p < kMaxRanks; ++p) r.peers.p[p] = c->peer_scratch.p[p] ? c->peer_scratch.p[p] + h : nullptr;
+    return r;
+}
+
 // Fill one ring-order job per block in `blocks` (or every block).
 static void ring_jobs(int64_t count, int n, red_jobs *jobs, int only_block) {
     int64_t split, early, late;
@@ -562,10 +580,10 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
     if (rc == OMPI_AMD_SUCCESS) rc = c->boot.attach(name, rank, size, 120.0);
     if (rc != OMPI_AMD_SUCCESS) { delete c; return rc; }
     // device resources: fine-grained flags, scratch, pinned error word
-    c->scratch_bytes = std::max<size_t>(c->small_bytes, 4 << 20);
+    c->scratch_bytes = std::max<size_t>(c->small_bytes, 4 << 20);  // per half
     hipError_t e = hipExtMallocWithFlags((void **)&c->flags, 4096, hipDeviceMallocUncached);
     if (e == hipSuccess) e = hipMemset(c->flags, 0, 4096);
-    if (e == hipSuccess) e = hipMalloc((void **)&c->scratch, c->scratch_bytes);
+    if (e == hipSuccess) e = hipMalloc((void **)&c->scratch, 2 * c->scratch_bytes);
     if (e == hipSuccess) e = hipHostMalloc((void **)&c->err_host, 64, hipHostMallocMapped);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&c->err_dev, c->err_host, 0);
     if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -738,11 +756,13 @@ int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
             record_msg("staged allreduce of %zu B exceeds the %zu B scratch", bytes, c->scratch_bytes);
             return OMPI_AMD_ERR_BAD_PARAM;
         }
-        // staged: my contribution -> my scratch, barrier, every rank folds
-        // all blocks from all scratches, barrier (scratch free again)
+        // staged one-shot: my contribution -> my scratch half, barrier,
+        // every rank folds all blocks from all scratches (no trailing
+        // barrier: see next_half)
+        const stage_half sh = next_half(c);
         cp_jobs cj{};
         cj.n = 1;
-        cj.j[0] = {(const char *)src, c->scratch, (int64_t)bytes};
+        cj.j[0] = {(const char *)src, sh.mine, (int64_t)bytes};
         TRY(launch_copy(c, cj, s));
         TRY(launch_barrier(c, s));
         if (tree) {
@@ -751,8 +771,7 @@ int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
         } else {
             ring_jobs((int64_t)count, n, &jobs, -1);
         }
-        TRY(launch_reduce(c, op, type, c->peer_scratch, rbuf, order, jobs, s));
-        return launch_barrier(c, s);
+        return launch_reduce(c, op, type, sh.peers, rbuf, order, jobs, s);
     }
     // zero-copy: reduce my ring block from every peer's sbuf, then gather
     ptr_set sp{}, rp{};
@@ -799,13 +818,13 @@ int ompi_amd_reduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *rb
     }
     if (total <= c->small_bytes || !c->zero_copy) {
         if (total > c->scratch_bytes) return OMPI_AMD_ERR_BAD_PARAM;
+        const stage_half sh = next_half(c);
         cp_jobs cj{};
         cj.n = 1;
-        cj.j[0] = {(const char *)src, c->scratch, (int64_t)total};
+        cj.j[0] = {(const char *)src, sh.mine, (int64_t)total};
         TRY(launch_copy(c, cj, s));
         TRY(launch_barrier(c, s));
-        TRY(launch_reduce(c, op, type, c->peer_scratch, rbuf, ORDER_LINEAR, jobs, s));
-        return launch_barrier(c, s);
+        return launch_reduce(c, op, type, sh.peers, rbuf, ORDER_LINEAR, jobs, s);
     }
     ptr_set sp{}, rp{};
     TRY(exchange_bufs(c, src, nullptr, &sp, &rp));
@@ -828,17 +847,17 @@ int ompi_amd_allgather(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
     cp_jobs cj{};
     if (bytes <= c->small_bytes || !c->zero_copy) {
         if (bytes > c->scratch_bytes) return OMPI_AMD_ERR_BAD_PARAM;
+        const stage_half sh = next_half(c);
         cj.n = 1;
-        cj.j[0] = {inplace ? my_slot : (const char *)sbuf, c->scratch, (int64_t)bytes};
+        cj.j[0] = {inplace ? my_slot : (const char *)sbuf, sh.mine, (int64_t)bytes};
         TRY(launch_copy(c, cj, s));
         TRY(launch_barrier(c, s));
         cj.n = 0;
         for (int p = 0; p < n; ++p) {
             if (p == c->rank && inplace) continue;
-            cj.j[cj.n++] = {c->peer_scratch.p[p], (char *)rbuf + (size_t)p * bytes, (int64_t)bytes};
+            cj.j[cj.n++] = {sh.peers.p[p], (char *)rbuf + (size_t)p * bytes, (int64_t)bytes};
         }
-        TRY(launch_copy(c, cj, s));
-        return launch_barrier(c, s);
+        return launch_copy(c, cj, s);
     }
     ptr_set sp{}, rp{};
     TRY(exchange_bufs(c, inplace ? my_slot : sbuf, nullptr, &sp, &rp));
@@ -860,18 +879,19 @@ int ompi_amd_bcast(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, void *
     cp_jobs cj{};
     if (bytes <= c->small_bytes || !c->zero_copy) {
         if (bytes > c->scratch_bytes) return OMPI_AMD_ERR_BAD_PARAM;
+        const stage_half sh = next_half(c);
         if (c->rank == root) {
             cj.n = 1;
-            cj.j[0] = {(const char *)buf, c->scratch, (int64_t)bytes};
+            cj.j[0] = {(const char *)buf, sh.mine, (int64_t)bytes};
             TRY(launch_copy(c, cj, s));
         }
         TRY(launch_barrier(c, s));
         if (c->rank != root) {
             cj.n = 1;
-            cj.j[0] = {c->peer_scratch.p[root], (char *)buf, (int64_t)bytes};
+            cj.j[0] = {sh.peers.p[root], (char *)buf, (int64_t)bytes};
             TRY(launch_copy(c, cj, s));
         }
-        return launch_barrier(c, s);
+        return OMPI_AMD_SUCCESS;
     }
     ptr_set sp{}, rp{};
     TRY(exchange_bufs(c, c->rank == root ? buf : nullptr, nullptr, &sp, &rp));

@@ -124,6 +124,55 @@ def case_bcast(comm, rank, n, nbytes, root, salt):
     return bool(np.array_equal(buf.cpu().numpy()[:nbytes], data)), ""
 
 
+def case_pipelined(comm, rank, n, salt):
+    """Back-to-back NON-blocking collectives on one stream (staged scratch
+    halves reused every other call, zero-copy mixed in), one sync at the
+    end, host-side skew between ranks; every result checked afterwards."""
+    import time
+    F, I32 = mop.MPI_FLOAT, mop.MPI_INT32_T
+    plan = [("ar", F, mop.MPI_SUM, 3001), ("ar", I32, mop.MPI_MAX, 20000),
+            ("ag", None, None, 4099), ("ar", F, mop.MPI_SUM, 100003),
+            ("bc", None, None, 70001), ("ar", I32, mop.MPI_SUM, 5),
+            ("ar", F, mop.MPI_SUM, 600000), ("ar", I32, mop.MPI_BOR, 77),
+            ("ag", None, None, 100), ("ar", F, mop.MPI_SUM, 20001)]
+    pending = []
+    for i, (kind, dt, op, cnt) in enumerate(plan):
+        if (i + rank) % 3 == 0:
+            time.sleep(0.002 * (rank + 1))
+        if kind == "ar":
+            xs = [inputs(dt, cnt, r, salt + i) for r in range(n)]
+            exp, _ = orc.allreduce([x.copy() for x in xs], cnt, op.index, dt.code)
+            s = to_dev(xs[rank])
+            out = torch.zeros_like(s)
+            comm.allreduce(s, out, cnt, dt, op)
+            pending.append((i, out, exp[rank], dt, cnt * dt.extent, s))
+        elif kind == "ag":
+            xs = [np.random.default_rng(SEED + salt + i + r).integers(0, 256, cnt, dtype=np.uint8)
+                  for r in range(n)]
+            s = to_dev(xs[rank])
+            out = torch.zeros(cnt * n, dtype=torch.uint8, device="cuda")
+            comm.allgather(s, out, cnt)
+            pending.append((i, out, np.concatenate(xs), None, cnt * n, s))
+        else:
+            data = np.random.default_rng(SEED + salt + i).integers(0, 256, cnt, dtype=np.uint8)
+            root = i % n
+            buf = to_dev(data) if rank == root else torch.zeros(cnt, dtype=torch.uint8, device="cuda")
+            comm.bcast(buf, cnt, root)
+            pending.append((i, buf, data, None, cnt, None))
+    torch.cuda.synchronize()
+    if comm.error() != 0:
+        return False, f"device error {comm.error()}"
+    for i, out, exp, dt, nb, _ in pending:
+        got = out.cpu().numpy()[:nb]
+        if dt is not None:
+            ok = fields_equal(got.view(dt.np_dtype), exp)
+        else:
+            ok = np.array_equal(got, exp)
+        if not ok:
+            return False, f"step {i} ({plan[i][0]}) mismatch"
+    return True, ""
+
+
 def main():
     rank, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     device = int(os.environ.get("OMPI_AMD_DEVICE", "0"))
@@ -162,6 +211,7 @@ def main():
         ("allgather_inplace", lambda: case_allgather(comm, rank, n, 65536, 23, True)),
         ("bcast_small_root0", lambda: case_bcast(comm, rank, n, 777, 0, 24)),
         ("bcast_big_rootlast", lambda: case_bcast(comm, rank, n, big * 4 + 3, n - 1, 25)),
+        ("pipelined_nonblocking", lambda: case_pipelined(comm, rank, n, 26)),
     ]
     only = os.environ.get("COLL_CASES")
     ok_all = True

@@ -1,0 +1,179 @@
+// HBM ceiling probe for the MPI_Op streaming kernels (standalone, no torch).
+//
+// Measures, over 1 GiB operands on one MI355X, what plain 16-B-per-lane
+// streaming reaches for the access mixes the op kernels use, so that the
+// op kernel's roofline fraction can be read against the achievable rate:
+//   rd2    two read streams (a, b), no write (XOR folded, stored only if magic)
+//   wr1    one write stream
+//   cp     one read + one write stream (copy)
+//   op     two reads + one write (out = a + b), the op kernel's shape
+//          (threads x unroll, one chunk per workgroup, nt loads + stores)
+//   opseq  same, but each workgroup walks SEQ consecutive chunks (longer
+//          runs per DRAM page)
+// Output: one JSON line per variant.
+// Build: hipcc --offload-arch=gfx950 -O3 -o hbm_probe hbm_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define CK(x)                                                                   \
+    do {                                                                        \
+        hipError_t e_ = (x);                                                    \
+        if (e_ != hipSuccess) {                                                 \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                            \
+        }                                                                       \
+    } while (0)
+
+template <int T, int U>
+__global__ __launch_bounds__(T) void k_rd2(const u32x4 *a, const u32x4 *b, u32x4 *out, size_t nvec) {
+    const size_t base = (size_t)blockIdx.x * T * U + threadIdx.x;
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + (size_t)u * T;
+        if (i < nvec) acc ^= __builtin_nontemporal_load(a + i) ^ __builtin_nontemporal_load(b + i);
+    }
+    if (acc.x == 0x9e3779b9u && acc.y == 0x7f4a7c15u) out[base] = acc;
+}
+
+template <int T, int U>
+__global__ __launch_bounds__(T) void k_wr1(u32x4 *out, size_t nvec) {
+    const size_t base = (size_t)blockIdx.x * T * U + threadIdx.x;
+    const u32x4 v = {(unsigned)base, 1u, 2u, 3u};
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + (size_t)u * T;
+        if (i < nvec) __builtin_nontemporal_store(v, out + i);
+    }
+}
+
+template <int T, int U>
+__global__ __launch_bounds__(T) void k_cp(const u32x4 *a, u32x4 *out, size_t nvec) {
+    const size_t base = (size_t)blockIdx.x * T * U + threadIdx.x;
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + (size_t)u * T;
+        if (i < nvec) v[u] = __builtin_nontemporal_load(a + i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + (size_t)u * T;
+        if (i < nvec) __builtin_nontemporal_store(v[u], out + i);
+    }
+}
+
+template <int T, int U, int SEQ>
+__global__ __launch_bounds__(T) void k_op(const f32x4 *a, const f32x4 *b, f32x4 *out, size_t nvec) {
+    for (int s = 0; s < SEQ; ++s) {
+        const size_t base = ((size_t)blockIdx.x * SEQ + s) * T * U + threadIdx.x;
+        f32x4 x[U], y[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * T;
+            if (i < nvec) {
+                x[u] = __builtin_nontemporal_load(a + i);
+                y[u] = __builtin_nontemporal_load(b + i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = base + (size_t)u * T;
+            if (i < nvec) __builtin_nontemporal_store(x[u] + y[u], out + i);
+        }
+    }
+}
+
+struct Bufs {
+    void *a, *b, *c;
+    size_t bytes, nvec;
+};
+
+template <typename L>
+static double time_ms(L &&launch, int reps) {
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int i = 0; i < 3; ++i) launch();
+    CK(hipDeviceSynchronize());
+    std::vector<float> v;
+    for (int r = 0; r < 3; ++r) {
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < reps; ++i) launch();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        v.push_back(ms / reps);
+    }
+    std::sort(v.begin(), v.end());
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    return v[1];
+}
+
+static void report(const char *name, int T, int U, int seq, double ms, double bytes) {
+    const double gbs = bytes / (ms * 1e-3) / 1e9;
+    printf("{\"variant\": \"%s\", \"threads\": %d, \"unroll\": %d, \"seq\": %d, \"ms\": %.4f, "
+           "\"GBps\": %.1f, \"frac\": %.4f}\n",
+           name, T, U, seq, ms, gbs, gbs / 8000.0);
+    fflush(stdout);
+}
+
+template <int T, int U>
+static void run_basic(const Bufs &B, int reps) {
+    const size_t chunk = (size_t)T * U;
+    const unsigned grid = (unsigned)((B.nvec + chunk - 1) / chunk);
+    const u32x4 *a = (const u32x4 *)B.a, *b = (const u32x4 *)B.b;
+    u32x4 *c = (u32x4 *)B.c;
+    report("rd2", T, U, 1, time_ms([&] { hipLaunchKernelGGL((k_rd2<T, U>), dim3(grid), dim3(T), 0, 0, a, b, c, B.nvec); }, reps), 2.0 * B.bytes);
+    report("wr1", T, U, 1, time_ms([&] { hipLaunchKernelGGL((k_wr1<T, U>), dim3(grid), dim3(T), 0, 0, c, B.nvec); }, reps), 1.0 * B.bytes);
+    report("cp", T, U, 1, time_ms([&] { hipLaunchKernelGGL((k_cp<T, U>), dim3(grid), dim3(T), 0, 0, a, c, B.nvec); }, reps), 2.0 * B.bytes);
+}
+
+template <int T, int U, int SEQ>
+static void run_op(const Bufs &B, int reps) {
+    const size_t chunk = (size_t)T * U * SEQ;
+    const unsigned grid = (unsigned)((B.nvec + chunk - 1) / chunk);
+    const f32x4 *a = (const f32x4 *)B.a, *b = (const f32x4 *)B.b;
+    f32x4 *c = (f32x4 *)B.c;
+    report(SEQ == 1 ? "op" : "opseq", T, U, SEQ,
+           time_ms([&] { hipLaunchKernelGGL((k_op<T, U, SEQ>), dim3(grid), dim3(T), 0, 0, a, b, c, B.nvec); }, reps),
+           3.0 * B.bytes);
+}
+
+int main(int argc, char **argv) {
+    const size_t bytes = (argc > 1) ? strtoull(argv[1], nullptr, 0) : (1ull << 30);
+    const int reps = 20;
+    Bufs B{};
+    B.bytes = bytes;
+    B.nvec = bytes / 16;
+    CK(hipMalloc(&B.a, bytes));
+    CK(hipMalloc(&B.b, bytes));
+    CK(hipMalloc(&B.c, bytes));
+    CK(hipMemset(B.a, 0x11, bytes));
+    CK(hipMemset(B.b, 0x22, bytes));
+    CK(hipMemset(B.c, 0, bytes));
+    CK(hipDeviceSynchronize());
+    run_basic<256, 4>(B, reps);
+    run_basic<256, 8>(B, reps);
+    run_basic<512, 4>(B, reps);
+    run_op<256, 4, 1>(B, reps);
+    run_op<256, 8, 1>(B, reps);
+    run_op<512, 4, 1>(B, reps);
+    run_op<1024, 2, 1>(B, reps);
+    run_op<256, 4, 4>(B, reps);
+    run_op<256, 4, 16>(B, reps);
+    run_op<256, 2, 8>(B, reps);
+    CK(hipFree(B.a));
+    CK(hipFree(B.b));
+    CK(hipFree(B.c));
+    return 0;
+}
