@@ -1,10 +1,14 @@
 /*
  * ompi_amd — device-buffer collectives over xGMI (one process per GPU, one
- * node).  Replaces coll/tuned's functions for device buffers behind the
- * coll framework's module table (ompi/mca/coll/coll.h:200-247):
+ * node).  Replaces coll/tuned's (and coll/basic's) functions for device
+ * buffers behind the coll framework's module table
+ * (ompi/mca/coll/coll.h:200-247):
  *
  *   coll_allreduce            coll.h:208-210  (tuned: coll_tuned_decision_fixed.c:45-89)
+ *   coll_reduce               coll.h:239-241  (tuned: :354-428)
  *   coll_reduce_scatter_block coll.h:245-247  (tuned: :522-532)
+ *   coll_scan / coll_exscan   coll.h:248-250, 228-230 (basic: coll_base_scan.c:35-122,
+ *                                                      coll_base_exscan.c:35-107)
  *   coll_allgather            coll.h:200-203  (tuned: :543-600)
  *   coll_bcast                coll.h:225-227  (tuned: :234-300)
  *
@@ -17,9 +21,11 @@
  * zero-copy user buffers).
  *
  * Results: ring / ring_segmented summation order for >= 10000-byte
- * allreduces and the recursive-doubling tree below (so fp results are
- * bit-identical to coll/tuned + op/base); basic_linear order for
- * reduce_scatter_block.
+ * allreduces and the recursive-doubling tree below; for reduce and
+ * reduce_scatter_block the operand order of the algorithm coll/tuned's
+ * fixed decision picks (basic_linear, in-order binomial, pipeline chain or
+ * binary tree); the linear order for scan/exscan — so fp results are
+ * bit-identical to coll/tuned (+ coll/basic) + op/base.
  */
 #ifndef OMPI_AMD_COLL_H
 #define OMPI_AMD_COLL_H
@@ -55,6 +61,13 @@ int ompi_amd_comm_size(const ompi_amd_comm_t *comm);
  *                   directly; 0: always stage through the scratch
  *   "timeout_ms"    device spin limit per barrier (default 30000)
  *   "blocks"        grid cap of the transfer kernels (default 1024)
+ *   "algorithm"     data movement of zero-copy allreduces (all ranks alike):
+ *                   0 pull (default: reduce own block from peers' sbufs,
+ *                   then pull the other blocks), 1 pull+push (reduce own
+ *                   block and store it into every rbuf in the same pass),
+ *                   2 push (scatter blocks into the owners' landing
+ *                   buffers, owners reduce locally and store into every
+ *                   rbuf).  Env OMPI_AMD_COLL_ALGORITHM sets the default.
  *   "profile"       1: bracket the allreduce's reduce and gather kernels with
  *                   HIP events (read with ompi_amd_comm_phase_ms) */
 int ompi_amd_comm_set_param(ompi_amd_comm_t *comm, const char *key, int64_t value);
@@ -85,6 +98,13 @@ int ompi_amd_comm_phase_ms(ompi_amd_comm_t *comm, int phase, double *total_ms, i
  * it (coll_base_allreduce.c:478-492). */
 int ompi_amd_coll_block(size_t count, int size, int block, size_t *off, size_t *cnt);
 int ompi_amd_coll_owner(int size, int block);
+/* The operand order coll/tuned's fixed reduce decision gives a commutative
+ * op (coll_tuned_decision_fixed.c:354-428; msg_bytes = type size * count):
+ * *order 2 = chain (basic_linear when *first == 0 and no root in-place
+ * swap, else pipeline rooted at *first), 3 = in-order binomial, 4 = binary
+ * tree, rooted at *first.  Host-only. */
+int ompi_amd_coll_reduce_order(int size, size_t msg_bytes, size_t count, int root,
+                               int root_inplace, int *order, int *first);
 
 /* MPI_IN_PLACE is spelled sbuf == rbuf or sbuf == (void *)1.
  * Stream-ordered: results are valid when `stream` reaches this point; the
@@ -92,11 +112,22 @@ int ompi_amd_coll_owner(int size, int block);
  * with matching arguments, in the same order. */
 int ompi_amd_allreduce(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
                        size_t count, int type, int op, void *stream);
+/* MPI_Reduce to `root` (coll.h:239-241).  rbuf matters at the root only;
+ * the root may pass sbuf = MPI_IN_PLACE.  Every rank folds one block of the
+ * vector from every rank's sbuf and stores it into the root's rbuf. */
+int ompi_amd_reduce(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
+                    size_t count, int type, int op, int root, void *stream);
 /* rbuf receives block `rank` (rcount elements) of the element-wise
  * reduction of the size*rcount element sbufs. */
 int ompi_amd_reduce_scatter_block(ompi_amd_comm_t *comm, const void *sbuf,
                                   void *rbuf, size_t rcount, int type, int op,
                                   void *stream);
+/* MPI_Scan / MPI_Exscan (coll.h:248-250, 228-230): rank r receives the
+ * reduction of ranks 0..r (exscan: 0..r-1; rank 0's rbuf is untouched). */
+int ompi_amd_scan(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
+                  size_t count, int type, int op, void *stream);
+int ompi_amd_exscan(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
+                    size_t count, int type, int op, void *stream);
 int ompi_amd_allgather(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
                        size_t bytes_per_rank, void *stream);
 int ompi_amd_bcast(ompi_amd_comm_t *comm, void *buf, size_t bytes, int root,

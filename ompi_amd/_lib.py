@@ -106,9 +106,19 @@ PROTOTYPES = [
     ("ompi_amd_coll_block", _C.c_int,
      [_C.c_size_t, _C.c_int, _C.c_int, _C.POINTER(_C.c_size_t), _C.POINTER(_C.c_size_t)]),
     ("ompi_amd_coll_owner", _C.c_int, [_C.c_int, _C.c_int]),
+    ("ompi_amd_coll_reduce_order", _C.c_int,
+     [_C.c_int, _C.c_size_t, _C.c_size_t, _C.c_int, _C.c_int, _C.POINTER(_C.c_int),
+      _C.POINTER(_C.c_int)]),
     ("ompi_amd_allreduce", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p]),
+    ("ompi_amd_reduce", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_int,
+      _C.c_void_p]),
     ("ompi_amd_reduce_scatter_block", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p]),
+    ("ompi_amd_scan", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p]),
+    ("ompi_amd_exscan", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p]),
     ("ompi_amd_allgather", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p]),

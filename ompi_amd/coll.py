@@ -110,6 +110,25 @@ class Communicator:
                                           op.index, _stream(stream))
         self._finish(rc, f"allreduce({op.name},{datatype.name})", blocking, stream)
 
+    def reduce(self, sbuf, rbuf, count: int, datatype: Datatype, op: Op, root: int,
+               stream=None, blocking: bool = False) -> None:
+        """MPI_Reduce; rbuf may be None off the root, sbuf IN_PLACE at the root."""
+        rc = self._lib.ompi_amd_reduce(self._h, _ptr(sbuf), _ptr(rbuf) if rbuf is not None else None,
+                                       count, datatype.code, op.index, root, _stream(stream))
+        self._finish(rc, f"reduce({op.name},{datatype.name},root={root})", blocking, stream)
+
+    def scan(self, sbuf, rbuf, count: int, datatype: Datatype, op: Op, stream=None,
+             blocking: bool = False) -> None:
+        rc = self._lib.ompi_amd_scan(self._h, _ptr(sbuf), _ptr(rbuf), count, datatype.code,
+                                     op.index, _stream(stream))
+        self._finish(rc, f"scan({op.name},{datatype.name})", blocking, stream)
+
+    def exscan(self, sbuf, rbuf, count: int, datatype: Datatype, op: Op, stream=None,
+               blocking: bool = False) -> None:
+        rc = self._lib.ompi_amd_exscan(self._h, _ptr(sbuf), _ptr(rbuf), count, datatype.code,
+                                       op.index, _stream(stream))
+        self._finish(rc, f"exscan({op.name},{datatype.name})", blocking, stream)
+
     def reduce_scatter_block(self, sbuf, rbuf, rcount: int, datatype: Datatype, op: Op,
                              stream=None, blocking: bool = False) -> None:
         rc = self._lib.ompi_amd_reduce_scatter_block(self._h, _ptr(sbuf), _ptr(rbuf), rcount,
@@ -138,6 +157,20 @@ def block_partition(count: int, nranks: int, block: int) -> tuple[int, int]:
     _lib.check(lib.ompi_amd_coll_block(count, nranks, block, ctypes.byref(off), ctypes.byref(cnt)),
                "coll_block")
     return off.value, cnt.value
+
+
+ORDER_NAMES = {0: "ring", 1: "recursive_doubling", 2: "chain", 3: "binomial", 4: "binary"}
+
+
+def reduce_order(nranks: int, msg_bytes: int, count: int, root: int,
+                 root_inplace: bool = False) -> tuple[str, int]:
+    """(operand order, virtual-rank-0) the library folds a reduce / rsb in:
+    coll/tuned's fixed reduce decision (coll_tuned_decision_fixed.c:354-428)."""
+    o, f = ctypes.c_int(), ctypes.c_int()
+    _lib.check(_lib.load().ompi_amd_coll_reduce_order(nranks, msg_bytes, count, root,
+                                                      1 if root_inplace else 0, ctypes.byref(o),
+                                                      ctypes.byref(f)), "coll_reduce_order")
+    return ORDER_NAMES[o.value], f.value
 
 
 def block_owner(nranks: int, block: int) -> int:

@@ -61,6 +61,25 @@ def bench_allreduce(args, metric: str, link_gbs: float):
     def ours():
         comm.allreduce(x, y, n, mop.MPI_FLOAT, mop.MPI_SUM, stream=stream)
 
+    # Pick the data-movement scheme (param "algorithm") by measurement, the
+    # way a coll/tuned dynamic-rules file would: every scheme is first
+    # checked bit-exact on dataset E at this size, then timed; the fastest
+    # exact one runs the headline.  All ranks see the same max-over-ranks
+    # times, so they agree.
+    S = n * 4
+    factor = 2.0 * (world - 1) / world
+    schemes = {}
+    for a, name in ALGORITHMS:
+        comm.set_param("algorithm", a)
+        exact = _exact_ok(comm, dist, torch, mop, n, rank, shared)
+        ta = _timed(ours, 5, 2, dist, torch, tdev) / 5
+        schemes[name] = {"algorithm": a, "bit_exact": exact, "us": round(ta * 1e6, 2),
+                         "busbw": round(S / ta * factor / 1e9, 2)}
+    usable = [v for v in schemes.values() if v["bit_exact"] is not False]
+    best = min(usable or schemes.values(), key=lambda v: v["us"])
+    comm.set_param("algorithm", best["algorithm"])
+    best_name = next(k for k, v in schemes.items() if v is best)
+
     t = _timed(ours, args.steps, args.warmup, dist, torch, tdev)
     err = comm.error()
     # per-phase kernel time over one more profiled pass of K steps
@@ -81,13 +100,14 @@ def bench_allreduce(args, metric: str, link_gbs: float):
 
         t_rccl = _timed(rccl, args.steps, args.warmup, dist, torch)
 
-    S = n * 4
-    factor = 2.0 * (world - 1) / world
     busbw = S / (t / args.steps) * factor / 1e9
     busbw_rccl = S / (t_rccl / args.steps) * factor / 1e9 if t_rccl else None
     roof = (world - 1) * link_gbs
     red_avg = red_ms / max(1, red_calls)
-    red_bytes = (world - 1) / world * S  # xGMI bytes pulled by one reduce launch
+    # xGMI bytes arriving at this GPU during one reduce launch: pull and
+    # push move one block per peer ((N-1)/N * S); pull+push also receives
+    # every peer's finished block in the same launch
+    red_bytes = (world - 1) / world * S * (2 if best["algorithm"] == 1 else 1)
     red_gbs = red_bytes / (red_avg * 1e-3) / 1e9 if red_avg > 0 else None
     res = {
         "metric": metric,
@@ -103,9 +123,10 @@ def bench_allreduce(args, metric: str, link_gbs: float):
         "dtype": "f32",
         "data": "synthetic U(-1,1) per rank (seed 20261015+rank), resident in HBM",
         "config": {"workload": "MPI_Allreduce fp32 SUM 256 MiB per rank, xGMI IPC ring-order "
-                               "reduce + peer gather (BASELINE configs[3] headline point)",
+                               "fused reduce (BASELINE configs[3] headline point)",
                    "count": n, "bytes": S, "op": "MPI_SUM", "datatype": "MPI_FLOAT",
-                   "parallelism": f"{world} ranks, 1 GPU each", "busbw_factor": factor},
+                   "parallelism": f"{world} ranks, 1 GPU each", "busbw_factor": factor,
+                   "algorithm": best_name, "schemes": schemes},
         "roofline": {"bound": "xgmi", "achieved": round(red_gbs, 1) if red_gbs else None,
                      "peak": roof, "unit": "GB/s",
                      "frac": round(red_gbs / roof, 4) if red_gbs else None,
@@ -131,6 +152,18 @@ def bench_allreduce(args, metric: str, link_gbs: float):
     dist.barrier()
     dist.destroy_process_group()
     return res if rank == 0 else None
+
+
+ALGORITHMS = ((0, "pull"), (1, "pull_push"), (2, "push"))
+
+
+def _exact_ok(comm, dist, torch, mop, n, rank, shared):
+    """Dataset E bit-exactness of the current scheme on all ranks (None in
+    the shared-GPU rehearsal, where RCCL is unavailable: tests cover it)."""
+    if shared:
+        return None
+    res = _check_exact(comm, dist, torch, mop, n, rank, shared)
+    return bool(res["bit_exact_all_ranks"])
 
 
 def _check_exact(comm, dist, torch, mop, n, rank, shared):
@@ -198,6 +231,15 @@ def _config5(comm, dist, torch, mop, world, rank, tdev):
     t = _timed(lambda: comm.bcast(b, b.numel(), 0), 10, 3, dist, torch, tdev) / 10
     res["bcast"] = {"bytes": b.numel(), "us": round(t * 1e6, 2),
                     "busbw": round(b.numel() / t / 1e9, 3)}
+    # MPI_Reduce fp32 SUM 64 MiB to root 0 (tuned pipeline order); every
+    # rank reduces 1/N of the vector and stores it into the root's rbuf
+    nf = (64 << 20) // 4
+    xr = torch.ones(nf, device="cuda")
+    yr = torch.zeros(nf, device="cuda") if rank == 0 else None
+    t = _timed(lambda: comm.reduce(xr, yr, nf, mop.MPI_FLOAT, mop.MPI_SUM, 0), 10, 3,
+               dist, torch, tdev) / 10
+    res["reduce_sum_f32_root0"] = {"bytes": nf * 4, "us": round(t * 1e6, 2),
+                                   "algbw": round(nf * 4 / t / 1e9, 3)}
     return res
 
 

@@ -1,20 +1,39 @@
-// Device-buffer collectives over xGMI for gfx950: allreduce,
-// reduce_scatter_block, allgather, bcast (include/ompi_amd_coll.h).
+// Device-buffer collectives over xGMI for gfx950: allreduce, reduce,
+// reduce_scatter_block, scan, exscan, allgather, bcast
+// (include/ompi_amd_coll.h).
 //
-// Reference path being replaced (coll/tuned over PML ob1 + btl/sm):
+// Reference path being replaced (coll/tuned + coll/basic over PML ob1 +
+// btl/sm):
 //   allreduce  coll_tuned_decision_fixed.c:45-89 ->
 //              ring_segmented coll_base_allreduce.c:618-856 (1 MiB segments,
 //              N-1 hops per segment, host bounce buffers, one op call per hop)
-// Here each rank owns one ring block (COLL_BASE_COMPUTE_BLOCKCOUNT,
+//   reduce     coll_tuned_decision_fixed.c:354-428 -> basic_linear / binomial
+//              / pipeline / binary (coll_base_reduce.c:62-735)
+//   rsb        coll_base_reduce_scatter_block.c:54-110 (tuned reduce to 0 +
+//              scatter)
+//   scan/exscan coll_base_scan.c:35-122, coll_base_exscan.c:35-107 (linear)
+// Here each rank owns one block of the vector (allreduce: the ring block the
+// reference finishes on it, COLL_BASE_COMPUTE_BLOCKCOUNT,
 // coll_base_functions.h:425-431) and produces it in ONE pass that loads the
-// block from every peer's buffer over xGMI at once (all N-1 links busy) and
-// folds the values in exactly the ring's operand order
-//     block b = x[b-1] (+) (x[b-2] (+) (... (x[b+1] (+) x[b])))
-// with (+) the 2-buffer op rule f(out, in) — so fp results are bit-identical
-// to the reference — then every rank pulls the other N-1 finished blocks
-// from their owners (again all links at once).  Below 10000 bytes the
-// reference runs recursive doubling (coll_base_allreduce.c:130-274); the
-// same pass then folds in that algorithm's pairwise-tree order.
+// block from every rank at once (all N-1 links busy) and folds the N values
+// in registers in exactly the reference algorithm's operand order, so fp
+// results are bit-identical to the reference:
+//   ring        block b = x[b-1] (+) (x[b-2] (+) (... (x[b+1] (+) x[b])))
+//   recursive doubling, basic_linear, pipeline chain, in-order binomial and
+//   binary trees: see fold() (orders restated in oracle/coll_*oracle.c)
+// with (+) the 2-buffer op rule f(out, in).
+//
+// Allreduce data movement (param "algorithm", all ranks alike):
+//   0 pull       barrier, reduce my block pulling every rank's sbuf, barrier,
+//                pull the N-1 other blocks from their owners, barrier
+//   1 pull+push  barrier, reduce my block pulling every rank's sbuf and store
+//                it into every rank's rbuf in the same pass, barrier
+//   2 push       every rank stores block b of its sbuf into the owner's
+//                landing slot (writes only over xGMI), barrier, the owner
+//                reduces from local memory and stores the result into every
+//                rank's rbuf, barrier
+// Below `small_bytes` every rank stages its input in IPC scratch and folds
+// all blocks itself (one barrier, no host rendezvous).
 //
 // Synchronisation: a monotonically increasing epoch per communicator.  A
 // barrier is one 64-lane workgroup: lane p stores the epoch into peer p's
@@ -24,7 +43,8 @@
 // Kernel boundaries on the stream order the barrier after the producer of
 // the data; every transfer workgroup opens with a system-scope acquire
 // (buffer_inv sc0 sc1: drops stale lines of peer memory from this XCD's
-// caches) and closes with a system-scope release (buffer_wbl2 sc0 sc1).
+// caches) and closes, after every wave has drained its stores, with a
+// system-scope release (buffer_wbl2 sc0 sc1).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -49,13 +69,24 @@ constexpr int kXferThreads = 256;
 struct ptr_set { const char *p[kMaxRanks]; };
 struct flag_set { uint64_t *p[kMaxRanks]; };
 
-enum order_t { ORDER_RING = 0, ORDER_TREE = 1, ORDER_LINEAR = 2 };
+// Operand orders of the reference's reduction algorithms.  Sources are
+// loaded in virtual-rank order v[j] = x[(first + j) % n].
+enum order_t {
+    ORDER_RING = 0,      // ring / ring_segmented block `first`; linear scan (first 0)
+    ORDER_TREE = 1,      // recursive doubling (first 0)
+    ORDER_CHAIN = 2,     // pipeline chain rooted at `first`; basic_linear = chain at 0, no swap
+    ORDER_BINOMIAL = 3,  // in-order binomial tree rooted at `first`
+    ORDER_BINARY = 4,    // binary tree rooted at `first`
+};
+// The root passed MPI_IN_PLACE: its first combine is f(own, child)
+// (coll_base_reduce.c:170-171, 196-199).
+constexpr int FOLD_ROOT_INPLACE = 1;
 
 // One reduction job: elements [off, off+cnt) of every source, combined in
-// `order` and written to dst + off_dst (element units).
+// the call's order and written to dst + off_dst (element units).
 struct red_job {
     int64_t off, cnt, off_dst;
-    int first;  // ring order: the block id b (sources start at rank b)
+    int first;  // virtual rank 0 (ring block b, tree root)
     int head;   // elements before the 16-B aligned body; -1: no common alignment
 };
 struct red_jobs { red_job j[kMaxRanks]; int n; };
@@ -67,6 +98,14 @@ __device__ __forceinline__ void sys_acquire() { __builtin_amdgcn_fence(__ATOMIC_
 __device__ __forceinline__ void sys_release() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Every storing wave drains its stores before the workgroup's single
+// system-scope release (MI355X_MICROARCH.md, inter-workgroup visibility).
+__device__ __forceinline__ void xfer_epilogue() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) sys_release();
 }
 
 // ---------------------------------------------------------------- barrier
@@ -93,9 +132,13 @@ __global__ __launch_bounds__(64) void barrier_kernel(uint64_t *local, flag_set p
 }
 
 // ---------------------------------------------------------------- reduce
+// Fold v[0..n) (virtual-rank order) with the 2-buffer rule f(out, in).  All
+// array indices are compile-time constants after unrolling; n, order and
+// flags are wave-uniform.
 template <typename T, int OP>
-__device__ __forceinline__ T fold(const T (&v)[kMaxRanks], int n, int order) {
-    using F = opfn<OP, false>;  // 2-buffer rule: f(out, in)
+__device__ __forceinline__ T fold(const T (&v)[kMaxRanks], int n, int order, int flags) {
+    using F = opfn<OP, false>;
+    const bool swap = (flags & FOLD_ROOT_INPLACE) != 0;
     if (order == ORDER_RING) {
         // v[j] = x[(b + j) % n]; acc = x[b]; acc = f(x[b+j], acc)
         T acc = v[0];
@@ -104,15 +147,57 @@ __device__ __forceinline__ T fold(const T (&v)[kMaxRanks], int n, int order) {
             if (j < n) acc = F::template f<T>(v[j], acc);
         return acc;
     }
-    if (order == ORDER_LINEAR) {
-        // basic_linear reduce (coll_base_reduce.c:627-700): acc = x[n-1];
-        // for i = n-2..0: acc = f(acc, x[i])
+    if (order == ORDER_CHAIN) {
+        // chain fanout 1 (coll_base_topo.c:588-600) under the generic reduce
+        // (coll_base_reduce.c:206-215): node k's only child is k+1,
+        // acc_k = f(acc_(k+1), x_k); basic_linear (:680-721) is the same
+        // expression at first = 0.
         T acc = v[kMaxRanks - 1];
 #pragma unroll
-        for (int j = kMaxRanks - 1; j >= 0; --j)
+        for (int j = kMaxRanks - 1; j >= 0; --j) {
             if (j == n - 1) acc = v[j];
-            else if (j < n - 1) acc = F::template f<T>(acc, v[j]);
+            else if (j < n - 1) acc = (j == 0 && swap) ? F::template f<T>(v[0], acc)
+                                                       : F::template f<T>(acc, v[j]);
+        }
         return acc;
+    }
+    if (order == ORDER_BINOMIAL) {
+        // in-order binomial (coll_base_topo.c:402-458): vrank u's children
+        // are u+1, u+2, u+4, ... while the bit is clear; first child:
+        // acc = f(child, own), later ones acc = f(acc, child).
+        T w[kMaxRanks];
+#pragma unroll
+        for (int i = 0; i < kMaxRanks; ++i) w[i] = v[i];
+#pragma unroll
+        for (int u = 0; u + 1 < kMaxRanks; u += 2)
+            if (u + 1 < n) w[u] = (u == 0 && swap) ? F::template f<T>(w[0], w[1])
+                                                   : F::template f<T>(w[u + 1], w[u]);
+#pragma unroll
+        for (int m = 2; m < kMaxRanks; m <<= 1) {
+#pragma unroll
+            for (int u = 0; u + m < kMaxRanks; u += 2 * m)
+                if (u + m < n) w[u] = F::template f<T>(w[u], w[u + m]);
+        }
+        return w[0];
+    }
+    if (order == ORDER_BINARY) {
+        // build_tree(2) (coll_base_topo.c:77-175): shifted rank s has
+        // children s + d and s + 2d, d = largest power of two <= s + 1;
+        // children have larger s, so descending s sees them finished.
+        T w[kMaxRanks];
+#pragma unroll
+        for (int i = 0; i < kMaxRanks; ++i) w[i] = v[i];
+#pragma unroll
+        for (int s = kMaxRanks - 1; s >= 0; --s) {
+            int d = 1;
+            while (2 * d <= s + 1) d *= 2;
+            const int c0 = s + d, c1 = s + 2 * d;
+            if (c0 < kMaxRanks && c0 < n)
+                w[s] = (s == 0 && swap) ? F::template f<T>(w[0], w[c0])
+                                        : F::template f<T>(w[c0], w[s]);
+            if (c1 < kMaxRanks && c1 < n) w[s] = F::template f<T>(w[s], w[c1]);
+        }
+        return w[0];
     }
     // recursive doubling (coll_base_allreduce.c:184-236): fold the
     // 2*extra lowest ranks pairwise, then a pairwise tree; every combine is
@@ -137,22 +222,28 @@ __device__ __forceinline__ T fold(const T (&v)[kMaxRanks], int n, int order) {
     return w[0];
 }
 
-// Gather v[j] for element index e of the sources in the job's order.
+// Gather v[j] for element index e of the sources in virtual-rank order.
 template <typename T>
 __device__ __forceinline__ void gather_scalar(T (&v)[kMaxRanks], const ptr_set &src, int n,
-                                              int order, int first, int64_t e) {
+                                              int first, int64_t e) {
 #pragma unroll
     for (int j = 0; j < kMaxRanks; ++j) {
         if (j < n) {
-            const int r = (order == ORDER_RING) ? (first + j) % n : j;
+            const int r = (first + j) % n;
             v[j] = reinterpret_cast<const T *>(src.p[r])[e];
         }
     }
 }
 
+// n sources (virtual ranks 0..n), result stored to dst.p[0 .. ndst): ndst =
+// 1 is a plain reduce into one buffer; ndst = size is the fused push of the
+// owner's block into every rank's rbuf (the host orders dst local first,
+// then peers rank+1, rank+2, ... so concurrent owners spread their stores
+// over the links).
 template <typename T, int OP>
-__global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, T *dst, int n,
-                                                              int order, red_jobs jobs) {
+__global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, ptr_set dst, int ndst,
+                                                              int n, int order, int flags,
+                                                              red_jobs jobs) {
     sys_acquire();
     const red_job jb = jobs.j[blockIdx.y];
     constexpr int E = 16 / sizeof(T);
@@ -167,7 +258,7 @@ __global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, T *ds
 #pragma unroll
         for (int j = 0; j < kMaxRanks; ++j) {
             if (j < n) {
-                const int r = (order == ORDER_RING) ? (jb.first + j) % n : j;
+                const int r = (jb.first + j) % n;
                 const u32x4 *p = reinterpret_cast<const u32x4 *>(
                     reinterpret_cast<const T *>(src.p[r]) + jb.off + head);
                 v[j].v = __builtin_nontemporal_load(p + i);
@@ -179,9 +270,13 @@ __global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, T *ds
             T s[kMaxRanks];
 #pragma unroll
             for (int j = 0; j < kMaxRanks; ++j) s[j] = v[j].e[e];
-            out.e[e] = fold<T, OP>(s, n, order);
+            out.e[e] = fold<T, OP>(s, n, order, flags);
         }
-        reinterpret_cast<u32x4 *>(dst + jb.off_dst + head)[i] = out.v;
+#pragma unroll
+        for (int k = 0; k < kMaxRanks; ++k)
+            if (k < ndst)
+                reinterpret_cast<u32x4 *>(reinterpret_cast<T *>(const_cast<char *>(dst.p[k])) +
+                                          jb.off_dst + head)[i] = out.v;
     }
     // scalar head [0, head) and tail [head + nvec*E, cnt)
     const int64_t tail0 = head + nvec * E;
@@ -189,11 +284,15 @@ __global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, T *ds
     for (int64_t k = tid; k < nscalar; k += gstride) {
         const int64_t e = k < head ? k : tail0 + (k - head);
         T s[kMaxRanks];
-        gather_scalar<T>(s, src, n, order, jb.first, jb.off + e);
-        store_elem<T>(dst + jb.off_dst + e, fold<T, OP>(s, n, order));
+        gather_scalar<T>(s, src, n, jb.first, jb.off + e);
+        const T r = fold<T, OP>(s, n, order, flags);
+#pragma unroll
+        for (int d = 0; d < kMaxRanks; ++d)
+            if (d < ndst)
+                store_elem<T>(reinterpret_cast<T *>(const_cast<char *>(dst.p[d])) + jb.off_dst + e,
+                              r);
     }
-    __syncthreads();
-    if (threadIdx.x == 0) sys_release();
+    xfer_epilogue();
 }
 
 // ---------------------------------------------------------------- copy
@@ -239,21 +338,21 @@ __global__ __launch_bounds__(kXferThreads) void copy_kernel(cp_jobs jobs) {
         const int64_t i = k < head ? k : tail0 + (k - head);
         jb.dst[i] = jb.src[i];
     }
-    __syncthreads();
-    if (threadIdx.x == 0) sys_release();
+    xfer_epilogue();
 }
 
 // ---------------------------------------------------------------- dispatch
-using red_launch_fn = hipError_t (*)(dim3, const ptr_set &, void *, int, int, const red_jobs &,
-                                     hipStream_t);
+using red_launch_fn = hipError_t (*)(dim3, const ptr_set &, const ptr_set &, int, int, int, int,
+                                     const red_jobs &, hipStream_t);
 
 template <int OP, int TYPE>
-static hipError_t red_launch_slot(dim3 grid, const ptr_set &src, void *dst, int n, int order,
-                                  const red_jobs &jobs, hipStream_t s) {
+static hipError_t red_launch_slot(dim3 grid, const ptr_set &src, const ptr_set &dst, int ndst,
+                                  int n, int order, int flags, const red_jobs &jobs,
+                                  hipStream_t s) {
     if constexpr (slot_supported(OP, TYPE)) {
         using T = typename type_of<TYPE>::type;
-        hipLaunchKernelGGL((reduce_kernel<T, OP>), grid, dim3(kXferThreads), 0, s, src, (T *)dst,
-                           n, order, jobs);
+        hipLaunchKernelGGL((reduce_kernel<T, OP>), grid, dim3(kXferThreads), 0, s, src, dst, ndst,
+                           n, order, flags, jobs);
         return hipGetLastError();
     } else {
         return hipErrorInvalidValue;
@@ -272,8 +371,8 @@ make_red_table(std::integer_sequence<int, O...>) {
 }
 static const auto g_red = make_red_table(std::make_integer_sequence<int, OMPI_AMD_OP_COUNT>{});
 
-// MPI type size (bytes of data) — the tuned decision uses it, not the extent
-// (ompi_datatype_module.c:404-430: DOUBLE_INT size 12 / extent 16).
+// MPI type size (bytes of data) — the tuned decisions use it, not the
+// extent (ompi_datatype_module.c:404-430: DOUBLE_INT size 12 / extent 16).
 static size_t type_size(int type) {
     switch (type) {
     case OMPI_AMD_TYPE_DOUBLE_INT: case OMPI_AMD_TYPE_LONG_INT: return 12;
@@ -294,6 +393,23 @@ static int64_t block_cnt(int64_t b, int64_t split, int64_t early, int64_t late) 
     return b < split ? early : late;
 }
 
+// The operand order of coll/tuned's reduce for a commutative op
+// (coll_tuned_decision_fixed.c:354-428; msg = type size * count).
+struct red_order { int order, first, flags; };
+static red_order tuned_reduce_order(int n, size_t msg, size_t count, int root, bool root_inplace) {
+    const double a1 = 0.6016 / 1024.0, b1 = 1.3496;
+    const double a2 = 0.0410 / 1024.0, b2 = 9.7128;
+    const double a3 = 0.0422 / 1024.0, b3 = 1.1614;
+    const int fl = root_inplace ? FOLD_ROOT_INPLACE : 0;
+    const double m = (double)msg;
+    if (n < 8 && msg < 512) return {ORDER_CHAIN, 0, 0};  // basic_linear
+    if ((n < 8 && msg < 20480) || msg < 2048 || count <= 1) return {ORDER_BINOMIAL, root, fl};
+    if (n > a1 * m + b1) return {ORDER_BINOMIAL, root, fl};
+    if (n > a2 * m + b2) return {ORDER_CHAIN, root, fl};  // pipeline, 1 KiB segments
+    if (n > a3 * m + b3) return {ORDER_BINARY, root, fl};
+    return {ORDER_CHAIN, root, fl};                      // pipeline, 32/64 KiB segments
+}
+
 }  // namespace ompi_amd
 
 using namespace ompi_amd;
@@ -308,6 +424,10 @@ struct ompi_amd_comm {
     size_t scratch_bytes = 0;             // bytes per half
     uint64_t stage_seq = 0;               // staged calls so far (selects the half)
     ptr_set peer_scratch{};
+    char *land = nullptr;                 // grow-on-demand landing buffer (push
+    size_t land_bytes = 0;                //   allreduce, large scan/exscan)
+    ptr_set peer_land{};
+    void *land_opened[kMaxRanks] = {};
     int *err_host = nullptr, *err_dev = nullptr;
     uint64_t epoch = 0;
     // params
@@ -315,6 +435,7 @@ struct ompi_amd_comm {
     int zero_copy = 1;
     int64_t timeout_ms = 30000;
     int max_blocks = 1024;
+    int algorithm = 0;
     // IPC caches
     struct exp_entry { void *base; size_t size; unsigned long long id; hipIpcMemHandle_t h; };
     struct imp_entry { int peer; hipIpcMemHandle_t h; void *base; uint64_t last_use; };
@@ -329,6 +450,8 @@ struct ompi_amd_comm {
 };
 
 namespace ompi_amd {
+
+enum { ALG_PULL = 0, ALG_PULL_PUSH = 1, ALG_PUSH = 2, ALG_COUNT = 3 };
 
 struct ipc_blob {
     hipIpcMemHandle_t flags, scratch;
@@ -414,7 +537,8 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
     return OMPI_AMD_SUCCESS;
 }
 
-// Swap (sbuf, rbuf) descriptors with every peer and map theirs.
+// Swap (sbuf, rbuf) descriptors with every peer and map theirs (either may
+// be NULL: nothing is exported for it).
 static int exchange_bufs(ompi_amd_comm_t *c, const void *sbuf, const void *rbuf, ptr_set *s,
                          ptr_set *r) {
     call_blob mine{};
@@ -433,6 +557,74 @@ static int exchange_bufs(ompi_amd_comm_t *c, const void *sbuf, const void *rbuf,
         if ((rc = import_buf(c, p, all[p].s, &s->p[p])) != OMPI_AMD_SUCCESS) return rc;
         if ((rc = import_buf(c, p, all[p].r, &r->p[p])) != OMPI_AMD_SUCCESS) return rc;
     }
+    return OMPI_AMD_SUCCESS;
+}
+
+static void release_landing(ompi_amd_comm_t *c) {
+    for (int p = 0; p < kMaxRanks; ++p) {
+        if (c->land_opened[p]) (void)hipIpcCloseMemHandle(c->land_opened[p]);
+        c->land_opened[p] = nullptr;
+        c->peer_land.p[p] = nullptr;
+    }
+    if (c->land) (void)hipFree(c->land);
+    c->land = nullptr;
+    c->land_bytes = 0;
+}
+
+// Collective: every rank reaches it in the same call with the same `need`.
+// Growing waits for all earlier work of every rank (no kernel may still
+// touch the old buffers), then swaps handles of the new one.
+static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
+    if (need <= c->land_bytes) return OMPI_AMD_SUCCESS;
+    const size_t want = (need + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+    int rc = record_hip(hipDeviceSynchronize(), "landing: drain");
+    if (rc == OMPI_AMD_SUCCESS) rc = c->boot.barrier();
+    if (rc != OMPI_AMD_SUCCESS) return rc;
+    for (int p = 0; p < kMaxRanks; ++p) {
+        if (c->land_opened[p]) (void)hipIpcCloseMemHandle(c->land_opened[p]);
+        c->land_opened[p] = nullptr;
+        c->peer_land.p[p] = nullptr;
+    }
+    rc = c->boot.barrier();  // nobody maps the old buffer any more
+    if (rc != OMPI_AMD_SUCCESS) return rc;
+    if (c->land) (void)hipFree(c->land);
+    c->land = nullptr;
+    c->land_bytes = 0;
+    struct { hipIpcMemHandle_t h; int ok; } mine{}, all[kMaxRanks];
+    hipError_t e = hipMalloc((void **)&c->land, want);
+    if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.h, c->land);
+    mine.ok = e == hipSuccess;
+    if (e != hipSuccess) record_hip(e, "landing buffer");
+    rc = c->boot.allgather(&mine, all, sizeof(mine));
+    if (rc != OMPI_AMD_SUCCESS) return rc;
+    bool ok = true;
+    for (int p = 0; p < c->size; ++p) ok = ok && all[p].ok;
+    for (int p = 0; ok && p < c->size; ++p) {
+        if (p == c->rank) {
+            c->peer_land.p[p] = c->land;
+            continue;
+        }
+        void *m = nullptr;
+        e = hipIpcOpenMemHandle(&m, all[p].h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+            record_hip(e, "hipIpcOpenMemHandle (landing)");
+            ok = false;
+            break;
+        }
+        c->land_opened[p] = m;
+        c->peer_land.p[p] = (const char *)m;
+    }
+    int all_ok = 0, mine_ok = ok ? 1 : 0, oks[kMaxRanks];
+    rc = c->boot.allgather(&mine_ok, oks, sizeof(int));
+    if (rc != OMPI_AMD_SUCCESS) return rc;
+    all_ok = 1;
+    for (int p = 0; p < c->size; ++p) all_ok &= oks[p];
+    if (!all_ok) {
+        (void)c->boot.barrier();
+        release_landing(c);
+        return OMPI_AMD_ERR_HIP;
+    }
+    c->land_bytes = want;
     return OMPI_AMD_SUCCESS;
 }
 
@@ -455,29 +647,49 @@ static int launch_copy(ompi_amd_comm_t *c, const cp_jobs &jobs, hipStream_t s) {
     return record_hip(hipGetLastError(), "copy launch");
 }
 
-static int launch_reduce(ompi_amd_comm_t *c, int op, int type, const ptr_set &src, void *dst,
-                         int order, red_jobs jobs, hipStream_t s) {
+static ptr_set one_ptr(const void *p) {
+    ptr_set r{};
+    r.p[0] = (const char *)p;
+    return r;
+}
+
+// Every rank's buffer in push order: mine first, then rank+1, rank+2, ...
+static ptr_set push_order(const ompi_amd_comm_t *c, const ptr_set &bufs) {
+    ptr_set r{};
+    for (int k = 0; k < c->size; ++k) r.p[k] = bufs.p[(c->rank + k) % c->size];
+    return r;
+}
+
+// Reduce `nsrc` sources (ranks 0..nsrc of src) in `order`, store to the
+// ndst buffers of dst.
+static int launch_reduce(ompi_amd_comm_t *c, int op, int type, const ptr_set &src, int nsrc,
+                         const ptr_set &dst, int ndst, int order, int flags, red_jobs jobs,
+                         hipStream_t s) {
     red_launch_fn f = g_red[op][type];
     if (!f) return OMPI_AMD_ERR_UNSUPPORTED;
-    if (jobs.n == 0) return OMPI_AMD_SUCCESS;
+    if (jobs.n == 0 || nsrc < 1) return OMPI_AMD_SUCCESS;
     const size_t ext = ompi_amd_type_extent(type);
     int64_t most = 0;
     for (int i = 0; i < jobs.n; ++i) {
         red_job &j = jobs.j[i];
         // every source and dst must sit at the same phase mod 16 B, and that
         // phase must be a whole number of elements from 16-B alignment
-        const uintptr_t ph = (uintptr_t)((const char *)dst + j.off_dst * ext) & 15;
+        const uintptr_t ph = (uintptr_t)(dst.p[0] + j.off_dst * ext) & 15;
         bool same = ext <= 16 && 16 % ext == 0;
-        for (int r = 0; r < c->size; ++r)
+        for (int r = 0; r < nsrc; ++r)
             same = same && ((((uintptr_t)(src.p[r] + j.off * ext)) & 15) == ph);
+        for (int d = 1; d < ndst; ++d)
+            same = same && ((((uintptr_t)(dst.p[d] + j.off_dst * ext)) & 15) == ph);
         const int64_t lead = (int64_t)((16 - ph) & 15);
         j.head = (same && lead % (int64_t)ext == 0) ? (int)std::min<int64_t>(lead / (int64_t)ext, j.cnt) : -1;
         most = std::max(most, j.cnt);
     }
+    if (most == 0) return OMPI_AMD_SUCCESS;
     const int64_t per = (int64_t)(16 / ext) * kXferThreads;
     int64_t blocks = (most + per - 1) / per;
     blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, std::max(1, c->max_blocks / jobs.n)));
-    return record_hip(f(dim3((unsigned)blocks, (unsigned)jobs.n), src, dst, c->size, order, jobs, s),
+    return record_hip(f(dim3((unsigned)blocks, (unsigned)jobs.n), src, dst, ndst, nsrc, order,
+                        flags, jobs, s),
                       "reduce launch");
 }
 
@@ -541,7 +753,7 @@ static stage_half next_half(ompi_amd_comm_t *c) {
     return r;
 }
 
-// Fill one ring-order job per block in `blocks` (or every block).
+// Fill one ring-order job per block (or only `only_block`).
 static void ring_jobs(int64_t count, int n, red_jobs *jobs, int only_block) {
     int64_t split, early, late;
     blockcount(count, n, &split, &early, &late);
@@ -555,6 +767,140 @@ static void ring_jobs(int64_t count, int n, red_jobs *jobs, int only_block) {
         j.first = b;
         j.head = -1;
     }
+}
+
+static int stage_in(ompi_amd_comm_t *c, const void *src, size_t bytes, stage_half *sh,
+                    hipStream_t s) {
+    if (bytes > c->scratch_bytes) {
+        record_msg("staged collective of %zu B exceeds the %zu B scratch", bytes, c->scratch_bytes);
+        return OMPI_AMD_ERR_BAD_PARAM;
+    }
+    *sh = next_half(c);
+    cp_jobs cj{};
+    cj.n = 1;
+    cj.j[0] = {(const char *)src, sh->mine, (int64_t)bytes};
+    TRY(launch_copy(c, cj, s));
+    return launch_barrier(c, s);
+}
+
+// ---- large allreduce, three data-movement schemes (header comment) ----
+static int allreduce_pull(ompi_amd_comm_t *c, const void *src, void *rbuf, int64_t count,
+                          int op, int type, bool inplace, hipStream_t s) {
+    const int n = c->size, mine = (c->rank + 1) % n;
+    const int64_t ext = (int64_t)ompi_amd_type_extent(type);
+    ptr_set sp{}, rp{};
+    TRY(exchange_bufs(c, src, rbuf, &sp, &rp));
+    if (inplace) sp = rp;
+    TRY(launch_barrier(c, s));
+    red_jobs jobs;
+    ring_jobs(count, n, &jobs, mine);
+    TRY(timed_phase(c, 0, s, [&] {
+        return launch_reduce(c, op, type, sp, n, one_ptr(rbuf), 1, ORDER_RING, 0, jobs, s);
+    }));
+    TRY(launch_barrier(c, s));
+    int64_t split, early, late;
+    blockcount(count, n, &split, &early, &late);
+    cp_jobs cj{};
+    for (int b = 0; b < n; ++b) {
+        if (b == mine) continue;
+        const int owner = (b + n - 1) % n;
+        const int64_t off = block_off(b, split, early, late) * ext;
+        cj.j[cj.n++] = {rp.p[owner] + off, (char *)rbuf + off, block_cnt(b, split, early, late) * ext};
+    }
+    TRY(timed_phase(c, 1, s, [&] { return launch_copy(c, cj, s); }));
+    return launch_barrier(c, s);
+}
+
+static int allreduce_pull_push(ompi_amd_comm_t *c, const void *src, void *rbuf, int64_t count,
+                               int op, int type, bool inplace, hipStream_t s) {
+    const int n = c->size, mine = (c->rank + 1) % n;
+    ptr_set sp{}, rp{};
+    TRY(exchange_bufs(c, src, rbuf, &sp, &rp));
+    if (inplace) sp = rp;  // only the owner of a block touches it, in place or not
+    TRY(launch_barrier(c, s));
+    red_jobs jobs;
+    ring_jobs(count, n, &jobs, mine);
+    const ptr_set dsts = push_order(c, rp);
+    TRY(timed_phase(c, 0, s, [&] {
+        return launch_reduce(c, op, type, sp, n, dsts, n, ORDER_RING, 0, jobs, s);
+    }));
+    return launch_barrier(c, s);
+}
+
+static int allreduce_push(ompi_amd_comm_t *c, const void *src, void *rbuf, int64_t count,
+                          int op, int type, hipStream_t s) {
+    const int n = c->size, mine = (c->rank + 1) % n;
+    const int64_t ext = (int64_t)ompi_amd_type_extent(type);
+    int64_t split, early, late;
+    blockcount(count, n, &split, &early, &late);
+    // slot r of the owner's landing buffer receives rank r's copy of the
+    // owner's block, at the block's own phase mod 16 B
+    const size_t slot = ((size_t)(early * ext) + 16 + 255) & ~(size_t)255;
+    TRY(ensure_landing(c, slot * (size_t)n));
+    ptr_set sp{}, rp{};
+    TRY(exchange_bufs(c, nullptr, rbuf, &sp, &rp));
+    cp_jobs cj{};
+    for (int b = 0; b < n; ++b) {
+        if (b == mine) continue;
+        const int owner = (b + n - 1) % n;
+        const int64_t off = block_off(b, split, early, late) * ext;
+        char *dst = const_cast<char *>(c->peer_land.p[owner]) + (size_t)c->rank * slot + (off & 15);
+        cj.j[cj.n++] = {(const char *)src + off, dst, block_cnt(b, split, early, late) * ext};
+    }
+    // the owner's previous reads of its landing ended before the previous
+    // push call's trailing barrier, so the scatter needs no leading one
+    TRY(timed_phase(c, 1, s, [&] { return launch_copy(c, cj, s); }));
+    TRY(launch_barrier(c, s));
+    const int64_t offm = block_off(mine, split, early, late) * ext;
+    ptr_set srcs{};
+    for (int r = 0; r < n; ++r)
+        srcs.p[r] = (r == c->rank) ? (const char *)src
+                                   : c->land + (size_t)r * slot + (offm & 15) - offm;
+    red_jobs jobs;
+    ring_jobs(count, n, &jobs, mine);
+    const ptr_set dsts = push_order(c, rp);
+    TRY(timed_phase(c, 0, s, [&] {
+        return launch_reduce(c, op, type, srcs, n, dsts, n, ORDER_RING, 0, jobs, s);
+    }));
+    return launch_barrier(c, s);
+}
+
+// scan (exclusive = false) / exscan: rank r folds ranks 0..r (0..r-1) in
+// the linear scan's order, which is the ring fold at first = 0.
+static int scan_common(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
+                       int op, void *stream, bool exclusive) {
+    if (!c || !rbuf) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
+    TRY(check_sticky(c));
+    if (count == 0) return OMPI_AMD_SUCCESS;
+    TRY(set_dev(c));
+    hipStream_t s = as_stream(stream);
+    const size_t bytes = count * ompi_amd_type_extent(type);
+    const bool inplace = in_place(sbuf, rbuf);
+    const void *src = inplace ? rbuf : sbuf;
+    const int nsrc = exclusive ? c->rank : c->rank + 1;
+    red_jobs jobs;
+    jobs.n = 1;
+    jobs.j[0] = {0, (int64_t)count, 0, 0, -1};
+    if (c->size == 1) {
+        if (exclusive || inplace) return OMPI_AMD_SUCCESS;
+        return record_hip(hipMemcpyAsync(rbuf, src, bytes, hipMemcpyDeviceToDevice, s), "copy");
+    }
+    if (bytes <= c->small_bytes || !c->zero_copy) {
+        stage_half sh;
+        TRY(stage_in(c, src, bytes, &sh, s));
+        return launch_reduce(c, op, type, sh.peers, nsrc, one_ptr(rbuf), 1, ORDER_RING, 0, jobs, s);
+    }
+    // large: inputs go through the landing buffers (a peer may still read
+    // my input while I write my result in place), then one fold per rank
+    TRY(ensure_landing(c, bytes + 256));
+    cp_jobs cj{};
+    cj.n = 1;
+    cj.j[0] = {(const char *)src, c->land, (int64_t)bytes};
+    TRY(launch_copy(c, cj, s));
+    TRY(launch_barrier(c, s));
+    TRY(launch_reduce(c, op, type, c->peer_land, nsrc, one_ptr(rbuf), 1, ORDER_RING, 0, jobs, s));
+    return launch_barrier(c, s);
 }
 
 }  // namespace ompi_amd
@@ -576,6 +922,10 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
     }
     c->device = device;
     if (const char *t = getenv("OMPI_AMD_COLL_TIMEOUT_MS")) c->timeout_ms = atoll(t);
+    if (const char *a = getenv("OMPI_AMD_COLL_ALGORITHM")) {
+        const int v = atoi(a);
+        if (v >= 0 && v < ALG_COUNT) c->algorithm = v;
+    }
     int rc = set_dev(c);
     if (rc == OMPI_AMD_SUCCESS) rc = c->boot.attach(name, rank, size, 120.0);
     if (rc != OMPI_AMD_SUCCESS) { delete c; return rc; }
@@ -632,12 +982,16 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     (void)hipDeviceSynchronize();
     (void)c->boot.barrier();  // nobody still reads our memory
     for (auto &x : c->imports) (void)hipIpcCloseMemHandle(x.base);
-    for (int p = 0; p < kMaxRanks; ++p)
+    for (int p = 0; p < kMaxRanks; ++p) {
         for (int k = 0; k < 2; ++k)
             if (c->opened[p][k]) (void)hipIpcCloseMemHandle(c->opened[p][k]);
+        if (c->land_opened[p]) (void)hipIpcCloseMemHandle(c->land_opened[p]);
+        c->land_opened[p] = nullptr;
+    }
     (void)c->boot.barrier();
     if (c->flags) (void)hipFree(c->flags);
     if (c->scratch) (void)hipFree(c->scratch);
+    if (c->land) (void)hipFree(c->land);
     if (c->err_host) (void)hipHostFree(c->err_host);
     for (int ph = 0; ph < 2; ++ph)
         for (auto &pr : c->ev_phase[ph]) {
@@ -662,6 +1016,15 @@ int ompi_amd_coll_block(size_t count, int size, int block, size_t *off, size_t *
 int ompi_amd_coll_owner(int size, int block) {
     if (size < 1 || block < 0 || block >= size) return -1;
     return (block + size - 1) % size;
+}
+
+int ompi_amd_coll_reduce_order(int size, size_t msg_bytes, size_t count, int root,
+                               int root_inplace, int *order, int *first) {
+    if (size < 1 || root < 0 || root >= size || !order || !first) return OMPI_AMD_ERR_BAD_PARAM;
+    const red_order ro = tuned_reduce_order(size, msg_bytes, count, root, root_inplace != 0);
+    *order = ro.order;
+    *first = ro.first;
+    return OMPI_AMD_SUCCESS;
 }
 
 int ompi_amd_comm_phase_ms(ompi_amd_comm_t *c, int phase, double *total_ms, int *calls) {
@@ -723,6 +1086,9 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
     } else if (!strcmp(key, "blocks")) {
         if (v <= 0 || v > 65535) return OMPI_AMD_ERR_BAD_PARAM;
         c->max_blocks = (int)v;
+    } else if (!strcmp(key, "algorithm")) {
+        if (v < 0 || v >= ALG_COUNT) return OMPI_AMD_ERR_BAD_PARAM;
+        c->algorithm = (int)v;
     } else {
         record_msg("unknown coll param '%s'", key);
         return OMPI_AMD_ERR_BAD_PARAM;
@@ -749,50 +1115,82 @@ int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
     }
     // order of coll/tuned's fixed decision: < 10000 B recursive doubling
     const bool tree = type_size(type) * count < 10000 || count < (size_t)n;
-    const int order = tree ? ORDER_TREE : ORDER_RING;
-    red_jobs jobs;
     if (bytes <= c->small_bytes || !c->zero_copy || tree) {
-        if (bytes > c->scratch_bytes) {
-            record_msg("staged allreduce of %zu B exceeds the %zu B scratch", bytes, c->scratch_bytes);
-            return OMPI_AMD_ERR_BAD_PARAM;
-        }
         // staged one-shot: my contribution -> my scratch half, barrier,
         // every rank folds all blocks from all scratches (no trailing
         // barrier: see next_half)
-        const stage_half sh = next_half(c);
-        cp_jobs cj{};
-        cj.n = 1;
-        cj.j[0] = {(const char *)src, sh.mine, (int64_t)bytes};
-        TRY(launch_copy(c, cj, s));
-        TRY(launch_barrier(c, s));
+        stage_half sh;
+        TRY(stage_in(c, src, bytes, &sh, s));
+        red_jobs jobs;
         if (tree) {
             jobs.n = 1;
             jobs.j[0] = {0, (int64_t)count, 0, 0, -1};
         } else {
             ring_jobs((int64_t)count, n, &jobs, -1);
         }
-        return launch_reduce(c, op, type, sh.peers, rbuf, order, jobs, s);
+        return launch_reduce(c, op, type, sh.peers, n, one_ptr(rbuf), 1,
+                             tree ? ORDER_TREE : ORDER_RING, 0, jobs, s);
     }
-    // zero-copy: reduce my ring block from every peer's sbuf, then gather
+    switch (c->algorithm) {
+    case ALG_PULL_PUSH:
+        return allreduce_pull_push(c, src, rbuf, (int64_t)count, op, type, inplace, s);
+    case ALG_PUSH:
+        return allreduce_push(c, src, rbuf, (int64_t)count, op, type, s);
+    default:
+        return allreduce_pull(c, src, rbuf, (int64_t)count, op, type, inplace, s);
+    }
+}
+
+int ompi_amd_reduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
+                    int op, int root, void *stream) {
+    if (!c || root < 0 || root >= c->size || (c->rank == root && !rbuf))
+        return OMPI_AMD_ERR_BAD_PARAM;
+    if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
+    TRY(check_sticky(c));
+    if (count == 0) return OMPI_AMD_SUCCESS;
+    TRY(set_dev(c));
+    hipStream_t s = as_stream(stream);
+    const int n = c->size;
+    const size_t bytes = count * ompi_amd_type_extent(type);
+    const bool root_inplace = c->rank == root && in_place(sbuf, rbuf);
+    const void *src = root_inplace ? rbuf : sbuf;
+    if (!src) return OMPI_AMD_ERR_BAD_PARAM;
+    if (n == 1) {
+        if (root_inplace) return OMPI_AMD_SUCCESS;
+        return record_hip(hipMemcpyAsync(rbuf, src, bytes, hipMemcpyDeviceToDevice, s), "copy");
+    }
+    // the in-place flag only changes the root's first combine; every rank
+    // must fold the same expression, so the root's choice is made known
+    int flag = root_inplace ? 1 : 0, flags_all[kMaxRanks];
+    TRY(c->boot.allgather(&flag, flags_all, sizeof(int)));
+    const red_order ro = tuned_reduce_order(n, type_size(type) * count, count, root,
+                                            flags_all[root] != 0);
+    red_jobs jobs;
+    if (bytes <= c->small_bytes || !c->zero_copy) {
+        // staged: everyone stages, the root folds everything
+        stage_half sh;
+        TRY(stage_in(c, src, bytes, &sh, s));
+        if (c->rank != root) return OMPI_AMD_SUCCESS;
+        jobs.n = 1;
+        jobs.j[0] = {0, (int64_t)count, 0, ro.first, -1};
+        return launch_reduce(c, op, type, sh.peers, n, one_ptr(rbuf), 1, ro.order, ro.flags, jobs, s);
+    }
+    // zero-copy: every rank folds one block of the vector from every
+    // rank's sbuf and stores it straight into the root's rbuf
     ptr_set sp{}, rp{};
-    TRY(exchange_bufs(c, src, rbuf, &sp, &rp));
-    if (inplace) sp = rp;
-    const int mine = (c->rank + 1) % n;  // the block the reference ring finishes here
-    TRY(launch_barrier(c, s));
-    ring_jobs((int64_t)count, n, &jobs, mine);
-    TRY(timed_phase(c, 0, s, [&] { return launch_reduce(c, op, type, sp, rbuf, order, jobs, s); }));
+    TRY(exchange_bufs(c, src, c->rank == root ? rbuf : nullptr, &sp, &rp));
     TRY(launch_barrier(c, s));
     int64_t split, early, late;
     blockcount((int64_t)count, n, &split, &early, &late);
-    cp_jobs cj{};
-    for (int b = 0; b < n; ++b) {
-        if (b == mine) continue;
-        const int owner = (b + n - 1) % n;
-        const int64_t off = block_off(b, split, early, late) * (int64_t)ext;
-        cj.j[cj.n++] = {rp.p[owner] + off, (char *)rbuf + off,
-                        block_cnt(b, split, early, late) * (int64_t)ext};
-    }
-    TRY(timed_phase(c, 1, s, [&] { return launch_copy(c, cj, s); }));
+    jobs.n = 1;
+    jobs.j[0].off = block_off(c->rank, split, early, late);
+    jobs.j[0].cnt = block_cnt(c->rank, split, early, late);
+    jobs.j[0].off_dst = jobs.j[0].off;
+    jobs.j[0].first = ro.first;
+    jobs.j[0].head = -1;
+    TRY(timed_phase(c, 0, s, [&] {
+        return launch_reduce(c, op, type, sp, n, one_ptr(rp.p[root]), 1, ro.order, ro.flags, jobs, s);
+    }));
     return launch_barrier(c, s);
 }
 
@@ -809,28 +1207,37 @@ int ompi_amd_reduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *rb
     const size_t total = rcount * (size_t)n * ext;
     const bool inplace = in_place(sbuf, rbuf);
     const void *src = inplace ? rbuf : sbuf;  // in place: the input is rbuf (n*rcount)
-    red_jobs jobs;
-    jobs.n = 1;
-    jobs.j[0] = {(int64_t)(rcount * (size_t)c->rank), (int64_t)rcount, 0, 0, -1};
     if (n == 1) {
         if (inplace) return OMPI_AMD_SUCCESS;
         return record_hip(hipMemcpyAsync(rbuf, src, rcount * ext, hipMemcpyDeviceToDevice, s), "copy");
     }
+    // basic_linear rsb = tuned reduce of the whole vector to rank 0 (never
+    // in place at that level) + scatter: my block folds in that order
+    const size_t tcount = rcount * (size_t)n;
+    const red_order ro = tuned_reduce_order(n, type_size(type) * tcount, tcount, 0, false);
+    red_jobs jobs;
+    jobs.n = 1;
+    jobs.j[0] = {(int64_t)(rcount * (size_t)c->rank), (int64_t)rcount, 0, ro.first, -1};
     if (total <= c->small_bytes || !c->zero_copy) {
-        if (total > c->scratch_bytes) return OMPI_AMD_ERR_BAD_PARAM;
-        const stage_half sh = next_half(c);
-        cp_jobs cj{};
-        cj.n = 1;
-        cj.j[0] = {(const char *)src, sh.mine, (int64_t)total};
-        TRY(launch_copy(c, cj, s));
-        TRY(launch_barrier(c, s));
-        return launch_reduce(c, op, type, sh.peers, rbuf, ORDER_LINEAR, jobs, s);
+        stage_half sh;
+        TRY(stage_in(c, src, total, &sh, s));
+        return launch_reduce(c, op, type, sh.peers, n, one_ptr(rbuf), 1, ro.order, ro.flags, jobs, s);
     }
     ptr_set sp{}, rp{};
     TRY(exchange_bufs(c, src, nullptr, &sp, &rp));
     TRY(launch_barrier(c, s));
-    TRY(launch_reduce(c, op, type, sp, rbuf, ORDER_LINEAR, jobs, s));
+    TRY(launch_reduce(c, op, type, sp, n, one_ptr(rbuf), 1, ro.order, ro.flags, jobs, s));
     return launch_barrier(c, s);
+}
+
+int ompi_amd_scan(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
+                  int op, void *stream) {
+    return scan_common(c, sbuf, rbuf, count, type, op, stream, false);
+}
+
+int ompi_amd_exscan(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
+                    int op, void *stream) {
+    return scan_common(c, sbuf, rbuf, count, type, op, stream, true);
 }
 
 int ompi_amd_allgather(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t bytes,
@@ -846,13 +1253,8 @@ int ompi_amd_allgather(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
     char *my_slot = (char *)rbuf + (size_t)c->rank * bytes;
     cp_jobs cj{};
     if (bytes <= c->small_bytes || !c->zero_copy) {
-        if (bytes > c->scratch_bytes) return OMPI_AMD_ERR_BAD_PARAM;
-        const stage_half sh = next_half(c);
-        cj.n = 1;
-        cj.j[0] = {inplace ? my_slot : (const char *)sbuf, sh.mine, (int64_t)bytes};
-        TRY(launch_copy(c, cj, s));
-        TRY(launch_barrier(c, s));
-        cj.n = 0;
+        stage_half sh;
+        TRY(stage_in(c, inplace ? my_slot : sbuf, bytes, &sh, s));
         for (int p = 0; p < n; ++p) {
             if (p == c->rank && inplace) continue;
             cj.j[cj.n++] = {sh.peers.p[p], (char *)rbuf + (size_t)p * bytes, (int64_t)bytes};

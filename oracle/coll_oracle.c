@@ -278,22 +278,7 @@ int orc_allreduce(int algorithm, int n, const void *const *sb, void *const *rb,
     }
 }
 
-/* rsb: basic_linear = reduce to root (coll_base_reduce.c:627-700: rbuf =
- * x[N-1]; for i = N-2..0: rbuf = x[i] op rbuf) then scatter of block r. */
-int orc_reduce_scatter_block(int n, const void *const *sb, void *const *rb,
-                             size_t rcount, int op, int type)
-{
-    const size_t ext = orc_type_extent(type), total = rcount * (size_t)n;
-    char *acc;
-    int i, r;
-    if (ext == 0 || !orc_op_defined(op, type)) return -1;
-    acc = malloc(total * ext + 1);
-    memcpy(acc, sb[n - 1], total * ext);
-    for (i = n - 2; i >= 0; --i) orc_op_2buff(op, type, sb[i], acc, total);
-    for (r = 0; r < n; r++) memcpy(rb[r], acc + (size_t)r * rcount * ext, rcount * ext);
-    free(acc);
-    return 0;
-}
+/* reduce_scatter_block, reduce, scan, exscan: coll_reduce_oracle.c */
 
 int orc_allgather(int n, const void *const *sb, void *const *rb, size_t bytes)
 {

@@ -77,10 +77,33 @@ int orc_allreduce(int algorithm, int nranks, const void *const *sbufs,
 void orc_blockcount(size_t count, int nblocks, size_t *split,
                     size_t *early, size_t *late);
 
-/* reduce_scatter_block / allgather / bcast reference results (data
- * movement; reduce order = rank order 0..N-1 folded with 2-buffer op). */
+/* ---- coll/tuned reduce restatement (coll_reduce_oracle.c) ---- */
+enum {
+    ORC_RED_TUNED = 0,     /* coll_tuned_decision_fixed.c:354-428 */
+    ORC_RED_LINEAR = 1,    /* basic_linear, coll_base_reduce.c:627-735 */
+    ORC_RED_PIPELINE = 3,  /* chain fanout 1, coll_base_reduce.c:409-438 */
+    ORC_RED_BINARY = 4,    /* coll_base_reduce.c:440-469 */
+    ORC_RED_BINOMIAL = 5   /* in-order binomial, coll_base_reduce.c:471-500 */
+};
+/* The algorithm the fixed decision picks for a commutative op; msg = type
+ * size * count. */
+int orc_reduce_decision(int nranks, size_t msg, size_t count);
+/* Reduce of sbufs[0..n) to `root` into rbuf_root; root_inplace = the root
+ * passed MPI_IN_PLACE (its sbufs[root] is its recvbuf).  Returns the
+ * algorithm run (tuned resolves to 1/3/4/5), <0 on error. */
+int orc_reduce(int algorithm, int nranks, const void *const *sbufs, void *rbuf_root,
+               size_t count, int op, int type, int root, int root_inplace);
+/* reduce_scatter_block = tuned reduce of n*rcount elements to rank 0 +
+ * scatter (coll_base_reduce_scatter_block.c:54-110).  Returns the reduce
+ * algorithm run. */
 int orc_reduce_scatter_block(int nranks, const void *const *sbufs,
                              void *const *rbufs, size_t rcount, int op, int type);
+/* linear scan (exclusive = 0) / exscan (exclusive = 1); exscan leaves
+ * rbufs[0] untouched. */
+int orc_scan(int exclusive, int nranks, const void *const *sbufs, void *const *rbufs,
+             size_t count, int op, int type);
+
+/* allgather / bcast reference results (data movement only). */
 int orc_allgather(int nranks, const void *const *sbufs, void *const *rbufs,
                   size_t bytes_per_rank);
 int orc_bcast(int nranks, int root, void *const *bufs, size_t bytes);

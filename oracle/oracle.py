@@ -46,7 +46,12 @@ def lib():
                                     c.c_size_t]
         L.orc_reduce_scatter_block.argtypes = [c.c_int, c.POINTER(c.c_void_p),
                                                c.POINTER(c.c_void_p), c.c_size_t, c.c_int, c.c_int]
-        L.orc_allgather.argtypes = [c.c_int, c.POINTER(c.c_void_p), c.POINTER(c.c_void_p),
+        L.orc_reduce_decision.argtypes = [c.c_int, c.c_size_t, c.c_size_t]
+        L.orc_reduce.argtypes = [c.c_int, c.c_int, c.POINTER(c.c_void_p), c.c_void_p,
+                                 c.c_size_t, c.c_int, c.c_int, c.c_int, c.c_int]
+        L.orc_scan.argtypes = [c.c_int, c.c_int, c.POINTER(c.c_void_p), c.POINTER(c.c_void_p),
+                               c.c_size_t, c.c_int, c.c_int]
+        L.orc_allgather.argtypes =[c.c_int, c.POINTER(c.c_void_p), c.POINTER(c.c_void_p),
                                     c.c_size_t]
         L.orc_bcast.argtypes = [c.c_int, c.c_int, c.POINTER(c.c_void_p), c.c_size_t]
         L.orc_blockcount.argtypes = [c.c_size_t, c.c_int, c.POINTER(c.c_size_t),
@@ -103,8 +108,40 @@ def reduce_scatter_block(sbufs: list[np.ndarray], rcount: int, op: int,
     rbufs = [np.zeros(rcount * ext, dtype=np.uint8) for _ in range(n)]
     sp = (ctypes.c_void_p * n)(*[_p(s) for s in sbufs])
     rp = (ctypes.c_void_p * n)(*[_p(r) for r in rbufs])
-    if lib().orc_reduce_scatter_block(n, sp, rp, rcount, op, type_code) != 0:
+    if lib().orc_reduce_scatter_block(n, sp, rp, rcount, op, type_code) < 0:
         raise ValueError("oracle rsb failed")
+    return rbufs
+
+
+RED_TUNED, RED_LINEAR, RED_PIPELINE, RED_BINARY, RED_BINOMIAL = 0, 1, 3, 4, 5
+
+
+def reduce_decision(n: int, msg: int, count: int) -> int:
+    return lib().orc_reduce_decision(n, msg, count)
+
+
+def reduce(sbufs: list[np.ndarray], count: int, op: int, type_code: int, root: int,
+           root_inplace: bool = False, algorithm: int = RED_TUNED) -> tuple[np.ndarray, int]:
+    """coll/tuned reduce of sbufs to `root`: (root's result, algorithm run)."""
+    n = len(sbufs)
+    out = np.zeros_like(sbufs[root])
+    sp = (ctypes.c_void_p * n)(*[_p(s) for s in sbufs])
+    alg = lib().orc_reduce(algorithm, n, sp, _p(out), count, op, type_code, root,
+                           1 if root_inplace else 0)
+    if alg < 0:
+        raise ValueError(f"oracle reduce failed ({alg})")
+    return out, alg
+
+
+def scan(sbufs: list[np.ndarray], count: int, op: int, type_code: int,
+         exclusive: bool = False) -> list[np.ndarray]:
+    """Linear scan / exscan; exscan's rank-0 result stays all-zero bytes."""
+    n = len(sbufs)
+    rbufs = [np.zeros_like(s) for s in sbufs]
+    sp = (ctypes.c_void_p * n)(*[_p(s) for s in sbufs])
+    rp = (ctypes.c_void_p * n)(*[_p(r) for r in rbufs])
+    if lib().orc_scan(1 if exclusive else 0, n, sp, rp, count, op, type_code) != 0:
+        raise ValueError("oracle scan failed")
     return rbufs
 
 

@@ -89,8 +89,12 @@ def case_allreduce(comm, rank, n, dt, op, count, salt, kind="R", inplace=False, 
     return True, ""
 
 
-def case_rsb(comm, rank, n, dt, op, rcount, salt, inplace=False):
-    xs = [inputs(dt, rcount * n, r, salt) for r in range(n)]
+def case_rsb_kind(comm, rank, n, dt, op, rcount, salt, kind):
+    return case_rsb(comm, rank, n, dt, op, rcount, salt, kind=kind)
+
+
+def case_rsb(comm, rank, n, dt, op, rcount, salt, inplace=False, kind="R"):
+    xs = [inputs(dt, rcount * n, r, salt, kind) for r in range(n)]
     exp = orc.reduce_scatter_block([x.copy() for x in xs], rcount, op.index, dt.code)
     s = to_dev(xs[rank])
     if inplace:
@@ -100,6 +104,44 @@ def case_rsb(comm, rank, n, dt, op, rcount, salt, inplace=False):
         out = torch.zeros(rcount * dt.extent, dtype=torch.uint8, device="cuda")
         comm.reduce_scatter_block(s, out, rcount, dt, op, blocking=True)
     got = out.cpu().numpy()[:rcount * dt.extent].view(dt.np_dtype)
+    return fields_equal(got, exp[rank].view(dt.np_dtype)), ""
+
+
+def case_reduce(comm, rank, n, dt, op, count, root, salt, inplace=False, kind="R"):
+    root = root % n
+    xs = [inputs(dt, count, r, salt, kind) for r in range(n)]
+    exp, _ = orc.reduce([x.copy() for x in xs], count, op.index, dt.code, root, inplace)
+    s = to_dev(xs[rank])
+    out = None
+    if rank == root:
+        if inplace:
+            comm.reduce(coll.IN_PLACE, s, count, dt, op, root, blocking=True)
+            out = s
+        else:
+            out = torch.zeros_like(s)
+            comm.reduce(s, out, count, dt, op, root, blocking=True)
+    else:
+        comm.reduce(s, None, count, dt, op, root, blocking=True)
+    if rank != root:
+        return True, ""
+    got = out.cpu().numpy()[:count * dt.extent].view(dt.np_dtype)
+    return fields_equal(got, exp.view(dt.np_dtype)), ""
+
+
+def case_scan(comm, rank, n, dt, op, count, salt, exclusive=False, inplace=False):
+    xs = [inputs(dt, count, r, salt) for r in range(n)]
+    exp = orc.scan([x.copy() for x in xs], count, op.index, dt.code, exclusive)
+    s = to_dev(xs[rank])
+    fn = comm.exscan if exclusive else comm.scan
+    if inplace:
+        fn(coll.IN_PLACE, s, count, dt, op, blocking=True)
+        out = s
+    else:
+        out = torch.zeros_like(s)
+        fn(s, out, count, dt, op, blocking=True)
+    if exclusive and rank == 0:
+        return True, ""
+    got = out.cpu().numpy()[:count * dt.extent].view(dt.np_dtype)
     return fields_equal(got, exp[rank].view(dt.np_dtype)), ""
 
 
@@ -173,6 +215,19 @@ def case_pipelined(comm, rank, n, salt):
     return True, ""
 
 
+def report(rank, n, obj):
+    """One JSON line per case on stdout (read by the test) and, when
+    COLL_LOG_DIR is set, appended to a per-rank file there (progress that a
+    watchdog on the GPU box can see while the test still runs)."""
+    line = json.dumps(obj)
+    print(line, flush=True)
+    d = os.environ.get("COLL_LOG_DIR")
+    if d:
+        os.makedirs(d, exist_ok=True)
+        with open(os.path.join(d, f"coll_n{n}_rank{rank}.jsonl"), "a") as f:
+            f.write(line + "\n")
+
+
 def main():
     rank, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     device = int(os.environ.get("OMPI_AMD_DEVICE", "0"))
@@ -212,7 +267,61 @@ def main():
         ("bcast_small_root0", lambda: case_bcast(comm, rank, n, 777, 0, 24)),
         ("bcast_big_rootlast", lambda: case_bcast(comm, rank, n, big * 4 + 3, n - 1, 25)),
         ("pipelined_nonblocking", lambda: case_pipelined(comm, rank, n, 26)),
+        # reduce: staged (linear / binomial / binary by size) and zero-copy
+        ("reduce_sum_f32_100_rootlast",
+         lambda: case_reduce(comm, rank, n, F, mop.MPI_SUM, 100, n - 1, 40)),
+        ("reduce_sum_f32_3000_root1",
+         lambda: case_reduce(comm, rank, n, F, mop.MPI_SUM, 3000, 1, 41)),
+        ("reduce_sum_f32_6000_root1_inplace",
+         lambda: case_reduce(comm, rank, n, F, mop.MPI_SUM, 6000, 1, 42, inplace=True)),
+        ("reduce_max_f32_specials_3000_inplace",
+         lambda: case_reduce(comm, rank, n, F, mop.MPI_MAX, 3000, 0, 43, True, "S")),
+        ("reduce_sum_f32_big_root2",
+         lambda: case_reduce(comm, rank, n, F, mop.MPI_SUM, big + 3, 2, 44)),
+        ("reduce_sum_f64_big_root0_inplace",
+         lambda: case_reduce(comm, rank, n, D, mop.MPI_SUM, big // 2 + 1, 0, 45, inplace=True)),
+        ("reduce_maxloc_double_int_big",
+         lambda: case_reduce(comm, rank, n, DI, mop.MPI_MAXLOC, big // 8 + 7, n - 1, 46)),
+        # rsb in the binomial / binary range of the tuned reduce decision
+        ("rsb_sum_f32_mid", lambda: case_rsb(comm, rank, n, F, mop.MPI_SUM, 1500, 47)),
+        ("rsb_sum_f32_small", lambda: case_rsb(comm, rank, n, F, mop.MPI_SUM, 300, 48)),
+        ("rsb_max_f32_mid_specials",
+         lambda: case_rsb_kind(comm, rank, n, F, mop.MPI_MAX, 1000, 49, "S")),
+        # scan / exscan: staged and landing paths, in place
+        ("scan_sum_f32_small", lambda: case_scan(comm, rank, n, F, mop.MPI_SUM, 5000, 50)),
+        ("scan_sum_f32_big", lambda: case_scan(comm, rank, n, F, mop.MPI_SUM, big + 1, 51)),
+        ("scan_sum_f32_big_inplace",
+         lambda: case_scan(comm, rank, n, F, mop.MPI_SUM, big, 52, inplace=True)),
+        ("exscan_sum_f64_small", lambda: case_scan(comm, rank, n, D, mop.MPI_SUM, 999, 53, True)),
+        ("exscan_max_i32_big", lambda: case_scan(comm, rank, n, I32, mop.MPI_MAX, big, 54, True)),
+        ("exscan_prod_i8_inplace",
+         lambda: case_scan(comm, rank, n, I8, mop.MPI_PROD, 70001, 55, True, True)),
     ]
+    # zero-copy allreduce under the two push schemes (param "algorithm")
+    for alg in (1, 2):
+        def with_alg(fn, a=alg):
+            def run():
+                comm.set_param("algorithm", a)
+                try:
+                    return fn()
+                finally:
+                    comm.set_param("algorithm", 0)
+            return run
+        cases += [
+            (f"alg{alg}_ar_sum_f32_big",
+             with_alg(lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, big, 60, repeat=2))),
+            (f"alg{alg}_ar_sum_f32_big_odd",
+             with_alg(lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, big + 5, 61))),
+            (f"alg{alg}_ar_sum_f32_big_inplace",
+             with_alg(lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, big, 62, inplace=True))),
+            (f"alg{alg}_ar_sum_f64_big",
+             with_alg(lambda: case_allreduce(comm, rank, n, D, mop.MPI_SUM, big // 2 + 3, 63))),
+            (f"alg{alg}_ar_maxloc_double_int",
+             with_alg(lambda: case_allreduce(comm, rank, n, DI, mop.MPI_MAXLOC, 262147, 64))),
+            (f"alg{alg}_ar_max_f32_specials",
+             with_alg(lambda: case_allreduce(comm, rank, n, F, mop.MPI_MAX, 300001, 65, "S"))),
+            (f"alg{alg}_pipelined_nonblocking", with_alg(lambda: case_pipelined(comm, rank, n, 66))),
+        ]
     only = os.environ.get("COLL_CASES")
     ok_all = True
     for name, fn in cases:
@@ -222,17 +331,16 @@ def main():
             ok, msg = fn()
         except Exception as e:  # report and stop: later cases would hang
             ok, msg = False, f"{type(e).__name__}: {e} {traceback.format_exc()[-400:]}"
-            print(json.dumps({"rank": rank, "case": name, "ok": ok, "msg": msg}), flush=True)
+            report(rank, n, {"rank": rank, "case": name, "ok": ok, "msg": msg})
             ok_all = False
             break
-        print(json.dumps({"rank": rank, "case": name, "ok": bool(ok), "msg": msg}), flush=True)
+        report(rank, n, {"rank": rank, "case": name, "ok": bool(ok), "msg": msg})
         ok_all &= bool(ok)
     # zero-copy disabled: everything staged through the scratch
     if ok_all and not only:
         comm.set_param("zero_copy", 0)
         ok, msg = case_allreduce(comm, rank, n, F, mop.MPI_SUM, 1 << 20, 30)
-        print(json.dumps({"rank": rank, "case": "ar_staged_only", "ok": bool(ok), "msg": msg}),
-              flush=True)
+        report(rank, n, {"rank": rank, "case": "ar_staged_only", "ok": bool(ok), "msg": msg})
         ok_all &= bool(ok)
     torch.cuda.synchronize()
     comm.free()

@@ -27,7 +27,7 @@ def free_port():
         return s.getsockname()[1]
 
 
-def run_ranks(n, timeout=420, extra_env=None):
+def run_ranks(n, timeout=600, extra_env=None):
     ngpu = torch.cuda.device_count()
     port = free_port()
     procs = []

@@ -1,0 +1,165 @@
+"""Reduce / reduce_scatter_block / scan operand orders (CPU only).
+
+The device folds each element in closed form (coll_ipc.hip fold(): chain,
+in-order binomial and binary trees in virtual-rank order).  Here that closed
+form is restated in Python and checked bit-exactly against the oracle's
+independent message-flow simulation of coll_base_reduce.c's generic tree
+reduce + coll_base_topo.c's trees, for every comm size 2..16, every root,
+with and without MPI_IN_PLACE at the root, on inputs where operand order
+changes fp bits (signed random sums, MAX over NaN/±0).  The library's host
+decision (ompi_amd_coll_reduce_order) is checked against the oracle's
+restatement of coll_tuned_decision_fixed.c:354-428.
+
+No reference execution of coll_base_reduce.c is available in this container
+(it needs the configure-generated headers), so these orders are pinned by
+the restated source only: see DESIGN.md §5.
+"""
+import numpy as np
+import pytest
+
+MAX, SUM = 1, 3
+F32 = 15
+CHAIN, BINOMIAL, BINARY = "chain", "binomial", "binary"
+
+
+def f(orc, op, out, inb):
+    """2-buffer rule f(out, in) through the oracle's op/base loop."""
+    r = out.copy()
+    orc.op_2buff(op, F32, inb, r, r.size)
+    return r
+
+
+def fold(orc, op, v, order, swap):
+    """Python twin of coll_ipc.hip fold() for the reduce orders."""
+    n = len(v)
+    if order == CHAIN:
+        acc = v[n - 1]
+        for j in range(n - 2, -1, -1):
+            acc = f(orc, op, v[0], acc) if (j == 0 and swap) else f(orc, op, acc, v[j])
+        return acc
+    w = list(v)
+    if order == BINOMIAL:
+        for u in range(0, n - 1, 2):
+            w[u] = f(orc, op, w[0], w[1]) if (u == 0 and swap) else f(orc, op, w[u + 1], w[u])
+        m = 2
+        while m < n:
+            for u in range(0, n - m, 2 * m):
+                w[u] = f(orc, op, w[u], w[u + m])
+            m *= 2
+        return w[0]
+    assert order == BINARY
+    for s in range(n - 1, -1, -1):
+        d = 1
+        while 2 * d <= s + 1:
+            d *= 2
+        c0, c1 = s + d, s + 2 * d
+        if c0 < n:
+            w[s] = f(orc, op, w[0], w[c0]) if (s == 0 and swap) else f(orc, op, w[c0], w[s])
+        if c1 < n:
+            w[s] = f(orc, op, w[s], w[c1])
+    return w[0]
+
+
+def _inputs(n, count, seed, specials):
+    rng = np.random.default_rng(seed)
+    xs = [rng.uniform(-1, 1, count).astype(np.float32) for _ in range(n)]
+    if specials:
+        sp = np.array([np.nan, 0.0, -0.0, 1.0], dtype=np.float32)
+        for x in xs:
+            idx = rng.integers(0, count, count // 2)
+            x[idx] = rng.choice(sp, idx.size)
+    return xs
+
+
+def _bits_equal(a, b):
+    nan = np.isnan(a) & np.isnan(b)
+    return np.array_equal(a[~nan].view(np.uint32), b[~nan].view(np.uint32)) and \
+        np.array_equal(np.isnan(a), np.isnan(b))
+
+
+ALGS = [(CHAIN, 3), (BINOMIAL, 5), (BINARY, 4)]
+
+
+@pytest.mark.parametrize("n", list(range(2, 17)))
+def test_closed_form_fold_equals_message_flow(orc, n):
+    count = 257
+    for op, specials in ((SUM, False), (MAX, True)):
+        xs = _inputs(n, count, 1000 + n, specials)
+        for root in range(n):
+            for inplace in (False, True):
+                v = [xs[(root + j) % n] for j in range(n)]
+                for name, alg in ALGS:
+                    exp, ran = orc.reduce(xs, count, op, F32, root, inplace, algorithm=alg)
+                    assert ran == alg
+                    got = fold(orc, op, v, name, inplace)
+                    assert _bits_equal(got, exp), (n, root, inplace, name, op)
+                # basic_linear = chain rooted at 0 without the swap, any root
+                exp, ran = orc.reduce(xs, count, op, F32, root, inplace, algorithm=1)
+                assert ran == 1
+                assert _bits_equal(fold(orc, op, list(xs), CHAIN, False), exp)
+
+
+def test_orders_differ_on_fp(orc):
+    """The orders are distinguishable on these inputs (the test above is not
+    vacuous)."""
+    xs = _inputs(8, 4096, 5, False)
+    outs = {alg: orc.reduce(xs, 4096, SUM, F32, 0, False, algorithm=alg)[0].view(np.uint32)
+            for alg in (1, 3, 4, 5)}
+    assert not np.array_equal(outs[1], outs[5])
+    assert not np.array_equal(outs[5], outs[4])
+    assert np.array_equal(outs[1], outs[3])  # pipeline rooted at 0 == basic_linear
+
+
+def test_reduce_decision_matches_reference_table(orc):
+    """Spot values of coll_tuned_decision_fixed.c:395-428 for commutative ops."""
+    d = orc.reduce_decision
+    assert d(4, 511, 100) == 1            # n < 8 and msg < 512: linear
+    assert d(4, 512, 128) == 5            # n < 8 and msg < 20480: binomial
+    assert d(8, 511, 100) == 5            # msg < 2048: binomial
+    assert d(8, 4096, 1024) == 5          # 8 > 0.6016/1024*4096 + 1.3496
+    assert d(8, 16384, 4096) == 4         # binary: 8 > 0.0422/1024*m + 1.1614
+    assert d(8, 64 << 20, 16 << 20) == 3  # pipeline 64K
+    assert d(2, 1 << 20, 262144) == 3
+    assert d(4, 40000, 10000) == 4
+    assert d(4, 80000, 20000) == 3
+    assert d(16, 1 << 30, 1) == 5         # count <= 1
+
+
+def test_library_decision_matches_oracle(orc):
+    from ompi_amd import coll
+    names = {1: "chain", 3: "chain", 4: "binary", 5: "binomial"}
+    for n in (2, 3, 4, 5, 7, 8, 9, 12, 16):
+        for msg in (4, 500, 512, 2000, 2048, 4096, 9000, 11000, 12000, 20000, 20480, 40000,
+                    100000, 165000, 170000, 1 << 20, 256 << 20):
+            for tsize in (4, 8, 12):
+                count = max(1, msg // tsize)
+                alg = orc.reduce_decision(n, count * tsize, count)
+                for root in (0, n - 1):
+                    name, first = coll.reduce_order(n, count * tsize, count, root)
+                    assert name == names[alg], (n, msg, tsize)
+                    assert first == (0 if alg == 1 else root)
+
+
+def test_rsb_is_tuned_reduce_then_scatter(orc):
+    for n, rcount in ((8, 300), (8, 4000), (8, 100000), (3, 2000), (4, 5000)):
+        xs = _inputs(n, rcount * n, 77 + n, False)
+        rb = orc.reduce_scatter_block(xs, rcount, SUM, F32)
+        full, _ = orc.reduce(xs, rcount * n, SUM, F32, 0)
+        for r in range(n):
+            assert np.array_equal(rb[r].view(np.float32), full[r * rcount:(r + 1) * rcount])
+
+
+@pytest.mark.parametrize("exclusive", [False, True])
+def test_scan_linear_order(orc, exclusive):
+    n, count = 7, 1001
+    xs = _inputs(n, count, 9, False)
+    res = orc.scan(xs, count, SUM, F32, exclusive)
+    acc = xs[0].copy()
+    if not exclusive:
+        assert np.array_equal(res[0], acc)
+    else:
+        assert not res[0].any()
+    for r in range(1, n):
+        nxt = f(orc, SUM, xs[r], acc)          # P_r = f(out = x_r, in = P_(r-1))
+        assert np.array_equal(res[r], acc if exclusive else nxt), r
+        acc = nxt
