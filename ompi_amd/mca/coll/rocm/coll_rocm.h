@@ -2,10 +2,11 @@
  * coll/rocm — MI355X coll component for Open MPI's coll framework.
  *
  * Drop-in: copy this directory to ompi/mca/coll/rocm/ (INTEGRATION.md §2).
- * The module provides coll_allreduce, coll_reduce_scatter_block,
- * coll_allgather and coll_bcast (ompi/mca/coll/coll.h:200-247) for device
- * buffers through libompi_amd.so, and interposes on the previously selected
- * functions (coll/tuned) for everything else, exactly like coll/cuda does
+ * The module provides coll_allreduce, coll_reduce, coll_reduce_scatter_block,
+ * coll_scan, coll_exscan, coll_allgather and coll_bcast
+ * (ompi/mca/coll/coll.h:200-250) for device buffers through libompi_amd.so,
+ * and interposes on the previously selected functions (coll/tuned, coll/basic
+ * for scan/exscan) for everything else, exactly like coll/cuda does
  * (ompi/mca/coll/cuda/coll_cuda_module.c:120-155).
  */
 #ifndef MCA_COLL_ROCM_EXPORT_H
@@ -39,6 +40,7 @@ typedef struct mca_coll_rocm_component_t {
     int small_bytes;     /* coll_rocm_small_bytes */
     int zero_copy;       /* coll_rocm_zero_copy */
     int timeout_ms;      /* coll_rocm_timeout_ms */
+    int algorithm;       /* coll_rocm_allreduce_algorithm (0 pull, 1 pull+push, 2 push) */
 } mca_coll_rocm_component_t;
 
 OMPI_MODULE_DECLSPEC extern mca_coll_rocm_component_t mca_coll_rocm_component;
@@ -52,6 +54,15 @@ int mca_coll_rocm_module_enable(mca_coll_base_module_t *module,
 int mca_coll_rocm_allreduce(const void *sbuf, void *rbuf, int count,
                             struct ompi_datatype_t *dtype, struct ompi_op_t *op,
                             struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+int mca_coll_rocm_reduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                         struct ompi_op_t *op, int root, struct ompi_communicator_t *comm,
+                         mca_coll_base_module_t *module);
+int mca_coll_rocm_scan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                       struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                       mca_coll_base_module_t *module);
+int mca_coll_rocm_exscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                         struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                         mca_coll_base_module_t *module);
 int mca_coll_rocm_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount,
                                        struct ompi_datatype_t *dtype, struct ompi_op_t *op,
                                        struct ompi_communicator_t *comm,

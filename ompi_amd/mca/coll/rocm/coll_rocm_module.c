@@ -3,9 +3,10 @@
  *
  * Selection: comm_query accepts node-local intra-communicators of at most
  * OMPI_AMD_MAX_RANKS ranks when a HIP device is visible; enable saves the
- * previously selected allreduce / reduce_scatter_block / allgather / bcast
- * (coll/tuned, coll_base_comm_select.c:158-232 enables in ascending
- * priority) and creates the libompi_amd communicator.
+ * previously selected allreduce / reduce / reduce_scatter_block / scan /
+ * exscan / allgather / bcast (coll/tuned, coll/basic for scan and exscan;
+ * coll_base_comm_select.c:158-232 enables in ascending priority) and creates
+ * the libompi_amd communicator.
  *
  * Per call every rank decides locally whether the device path applies
  * (predefined datatype, intrinsic op with a device kernel, device buffers),
@@ -53,6 +54,7 @@ mca_coll_rocm_component_t mca_coll_rocm_component = {
     .small_bytes = 1 << 20,
     .zero_copy = 1,
     .timeout_ms = 30000,
+    .algorithm = 0,
 };
 
 static int rocm_register(void)
@@ -77,6 +79,11 @@ static int rocm_register(void)
                                            MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_coll_rocm_component.timeout_ms);
+    (void) mca_base_component_var_register(c, "allreduce_algorithm",
+                                           "Large-message allreduce data movement: 0 pull, 1 pull+push, 2 push",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_coll_rocm_component.algorithm);
     return OMPI_SUCCESS;
 }
 
@@ -91,6 +98,9 @@ static void rocm_module_construct(mca_coll_rocm_module_t *m)
 static void rocm_module_destruct(mca_coll_rocm_module_t *m)
 {
     if (NULL != m->c_coll.coll_allreduce_module) OBJ_RELEASE(m->c_coll.coll_allreduce_module);
+    if (NULL != m->c_coll.coll_reduce_module) OBJ_RELEASE(m->c_coll.coll_reduce_module);
+    if (NULL != m->c_coll.coll_scan_module) OBJ_RELEASE(m->c_coll.coll_scan_module);
+    if (NULL != m->c_coll.coll_exscan_module) OBJ_RELEASE(m->c_coll.coll_exscan_module);
     if (NULL != m->c_coll.coll_reduce_scatter_block_module)
         OBJ_RELEASE(m->c_coll.coll_reduce_scatter_block_module);
     if (NULL != m->c_coll.coll_allgather_module) OBJ_RELEASE(m->c_coll.coll_allgather_module);
@@ -120,6 +130,9 @@ mca_coll_base_module_t *mca_coll_rocm_comm_query(struct ompi_communicator_t *com
     *priority = mca_coll_rocm_component.priority;
     m->super.coll_module_enable = mca_coll_rocm_module_enable;
     m->super.coll_allreduce = mca_coll_rocm_allreduce;
+    m->super.coll_reduce = mca_coll_rocm_reduce;
+    m->super.coll_scan = mca_coll_rocm_scan;
+    m->super.coll_exscan = mca_coll_rocm_exscan;
     m->super.coll_reduce_scatter_block = mca_coll_rocm_reduce_scatter_block;
     m->super.coll_allgather = mca_coll_rocm_allgather;
     m->super.coll_bcast = mca_coll_rocm_bcast;
@@ -140,6 +153,9 @@ int mca_coll_rocm_module_enable(mca_coll_base_module_t *module, struct ompi_comm
         OBJ_RETAIN(m->c_coll.coll_##fn##_module);                          \
     } while (0)
     SAVE(allreduce);
+    SAVE(reduce);
+    SAVE(scan);
+    SAVE(exscan);
     SAVE(reduce_scatter_block);
     SAVE(allgather);
     SAVE(bcast);
@@ -153,6 +169,7 @@ int mca_coll_rocm_module_enable(mca_coll_base_module_t *module, struct ompi_comm
     (void) ompi_amd_comm_set_param(m->dev_comm, "small_bytes", mca_coll_rocm_component.small_bytes);
     (void) ompi_amd_comm_set_param(m->dev_comm, "zero_copy", mca_coll_rocm_component.zero_copy);
     (void) ompi_amd_comm_set_param(m->dev_comm, "timeout_ms", mca_coll_rocm_component.timeout_ms);
+    (void) ompi_amd_comm_set_param(m->dev_comm, "algorithm", mca_coll_rocm_component.algorithm);
     return OMPI_SUCCESS;
 }
 
@@ -208,6 +225,64 @@ int mca_coll_rocm_allreduce(const void *sbuf, void *rbuf, int count,
                             (size_t) count, t, op->o_f_to_c_index, NULL);
     if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_comm_sync(m->dev_comm, NULL);
     return to_ompi_err(rc);
+}
+
+/* MPI_Reduce: rbuf is significant at the root only (MPI-3.1 §5.9.1), so
+ * only the root's rbuf residency enters the local decision. */
+int mca_coll_rocm_reduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                         struct ompi_op_t *op, int root, struct ompi_communicator_t *comm,
+                         mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const int t = type_code(dtype);
+    const int is_root = ompi_comm_rank(comm) == root;
+    const int ok = t >= 0 && ompi_op_is_intrinsic(op) &&
+                   ompi_amd_op_supported(op->o_f_to_c_index, t) &&
+                   (is_root ? dev(rbuf) && dev(sbuf) : ompi_amd_is_device_pointer(sbuf));
+    int rc;
+    if (!take_device_path(m, ok)) {
+        return m->c_coll.coll_reduce(sbuf, rbuf, count, dtype, op, root, comm,
+                                     m->c_coll.coll_reduce_module);
+    }
+    rc = ompi_amd_reduce(m->dev_comm, sbuf, is_root ? rbuf : NULL, (size_t) count, t,
+                         op->o_f_to_c_index, root, NULL);
+    if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_comm_sync(m->dev_comm, NULL);
+    return to_ompi_err(rc);
+}
+
+static int rocm_scan_common(const void *sbuf, void *rbuf, int count,
+                            struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                            struct ompi_communicator_t *comm, mca_coll_rocm_module_t *m,
+                            int exclusive)
+{
+    const int t = type_code(dtype);
+    const int ok = t >= 0 && ompi_op_is_intrinsic(op) &&
+                   ompi_amd_op_supported(op->o_f_to_c_index, t) && dev(sbuf) && dev(rbuf);
+    int rc;
+    if (!take_device_path(m, ok)) {
+        return exclusive ? m->c_coll.coll_exscan(sbuf, rbuf, count, dtype, op, comm,
+                                                 m->c_coll.coll_exscan_module)
+                         : m->c_coll.coll_scan(sbuf, rbuf, count, dtype, op, comm,
+                                               m->c_coll.coll_scan_module);
+    }
+    rc = (exclusive ? ompi_amd_exscan : ompi_amd_scan)(m->dev_comm, sbuf, rbuf, (size_t) count, t,
+                                                       op->o_f_to_c_index, NULL);
+    if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_comm_sync(m->dev_comm, NULL);
+    return to_ompi_err(rc);
+}
+
+int mca_coll_rocm_scan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                       struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                       mca_coll_base_module_t *module)
+{
+    return rocm_scan_common(sbuf, rbuf, count, dtype, op, comm, (mca_coll_rocm_module_t *) module, 0);
+}
+
+int mca_coll_rocm_exscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                         struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                         mca_coll_base_module_t *module)
+{
+    return rocm_scan_common(sbuf, rbuf, count, dtype, op, comm, (mca_coll_rocm_module_t *) module, 1);
 }
 
 int mca_coll_rocm_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount,

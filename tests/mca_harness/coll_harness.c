@@ -1,0 +1,373 @@
+/*
+ * TEST HARNESS ONLY.  One rank of a multi-process run that drives
+ * ompi_amd/mca/coll/rocm/coll_rocm_module.c the way the coll framework does
+ * (coll_base_comm_select.c:158-232): the previously selected functions are
+ * played by counting stand-ins ("tuned"), the component is queried, the
+ * module enabled (it saves and retains the stand-ins) and its functions
+ * installed in the communicator's table; then every collective is called
+ * through that table.
+ *
+ *   CPU (HARNESS_GPU=0): init_query refuses without a device; comm_query
+ *   accepts only node-local intra-communicators of 2..16 ranks.
+ *   GPU (HARNESS_GPU=1): device buffers run the library and match the CPU
+ *   oracle bit for bit; host buffers, mixed residency across ranks and
+ *   non-intrinsic ops go to the saved functions on every rank.
+ *
+ * usage: coll_harness <segment-name> <rank> <size>; prints "ok" / "ok gpu".
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mpi.h"
+#include "ompi/communicator/communicator.h"
+#include "ompi/constants.h"
+#include "ompi/datatype/ompi_datatype.h"
+#include "ompi/op/op.h"
+#include "ompi/runtime/ompi_rte.h"
+#include "../../oracle/oracle.h"
+#include "coll_rocm.h"
+#include "ompi_amd.h"
+
+extern mca_coll_rocm_component_t mca_coll_rocm_component;
+extern int harness_dev_alloc_copy(void **d, const void *h, size_t bytes);
+extern int harness_dev_copy_back(void *h, const void *d, size_t bytes);
+extern int harness_dev_free(void *d);
+
+OBJ_CLASS_INSTANCE(mca_coll_base_module_t, opal_object_t, NULL, NULL);
+harness_proc_name_t harness_proc_name = {4242, 0};
+int ompi_op_ddt_map[64];
+
+#define CHECK(c, ...)                                                   \
+    do {                                                                \
+        if (!(c)) {                                                     \
+            fprintf(stderr, "FAIL rank %d %s:%d: ", g_rank, __FILE__, __LINE__); \
+            fprintf(stderr, __VA_ARGS__);                               \
+            fprintf(stderr, "\n");                                      \
+            exit(1);                                                    \
+        }                                                               \
+    } while (0)
+
+static int g_rank, g_size;
+static int tuned_calls;
+
+/* ---- the previously selected functions ("tuned"): count and succeed ---- */
+static int t_allreduce(const void *s, void *r, int c, struct ompi_datatype_t *d,
+                       struct ompi_op_t *o, struct ompi_communicator_t *cm,
+                       mca_coll_base_module_t *m) { tuned_calls++; return OMPI_SUCCESS; }
+static int t_reduce(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                    int root, struct ompi_communicator_t *cm, mca_coll_base_module_t *m)
+{ tuned_calls++; return OMPI_SUCCESS; }
+static int t_rsb(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                 struct ompi_communicator_t *cm, mca_coll_base_module_t *m)
+{ tuned_calls++; return OMPI_SUCCESS; }
+static int t_scan(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                  struct ompi_communicator_t *cm, mca_coll_base_module_t *m)
+{ tuned_calls++; return OMPI_SUCCESS; }
+static int t_allgather(const void *s, int sc, struct ompi_datatype_t *sd, void *r, int rc,
+                       struct ompi_datatype_t *rd, struct ompi_communicator_t *cm,
+                       mca_coll_base_module_t *m) { tuned_calls++; return OMPI_SUCCESS; }
+static int t_bcast(void *b, int c, struct ompi_datatype_t *d, int root,
+                   struct ompi_communicator_t *cm, mca_coll_base_module_t *m)
+{ tuned_calls++; return OMPI_SUCCESS; }
+
+static void fill_tuned(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *tm)
+{
+    memset(t, 0, sizeof(*t));
+#define SET(fn, f) do { t->coll_##fn = f; t->coll_##fn##_module = tm; OBJ_RETAIN(tm); } while (0)
+    SET(allreduce, t_allreduce);
+    SET(reduce, t_reduce);
+    SET(reduce_scatter_block, t_rsb);
+    SET(scan, t_scan);
+    SET(exscan, t_scan);
+    SET(allgather, t_allgather);
+    SET(bcast, t_bcast);
+#undef SET
+}
+
+/* coll_base_comm_select.c:210-232: install what the module provides */
+static void install(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *m)
+{
+#define INST(fn) if (m->coll_##fn) { OBJ_RELEASE(t->coll_##fn##_module); t->coll_##fn = m->coll_##fn; \
+                                      t->coll_##fn##_module = m; OBJ_RETAIN(m); }
+    INST(allreduce) INST(reduce) INST(reduce_scatter_block) INST(scan) INST(exscan)
+    INST(allgather) INST(bcast)
+#undef INST
+}
+
+static void release_table(mca_coll_base_comm_coll_t *t)
+{
+    OBJ_RELEASE(t->coll_allreduce_module);
+    OBJ_RELEASE(t->coll_reduce_module);
+    OBJ_RELEASE(t->coll_reduce_scatter_block_module);
+    OBJ_RELEASE(t->coll_scan_module);
+    OBJ_RELEASE(t->coll_exscan_module);
+    OBJ_RELEASE(t->coll_allgather_module);
+    OBJ_RELEASE(t->coll_bcast_module);
+}
+
+/* deterministic per-rank floats in [-1, 1): fp sums depend on order */
+static void gen(float *x, size_t n, int rank, int salt)
+{
+    unsigned long long s = 0x9E3779B97F4A7C15ull * (unsigned long long)(rank * 131 + salt + 1);
+    for (size_t i = 0; i < n; ++i) {
+        s ^= s >> 12; s ^= s << 25; s ^= s >> 27;
+        x[i] = (float)((double)((s * 2685821657736338717ull) >> 40) / (double)(1ull << 24)) * 2.f - 1.f;
+    }
+}
+
+static float **all_inputs(size_t n, int salt)
+{
+    float **xs = malloc(sizeof(float *) * (size_t)g_size);
+    for (int r = 0; r < g_size; ++r) {
+        xs[r] = malloc(n * sizeof(float) + 4);
+        gen(xs[r], n, r, salt);
+    }
+    return xs;
+}
+
+static void free_inputs(float **xs)
+{
+    for (int r = 0; r < g_size; ++r) free(xs[r]);
+    free(xs);
+}
+
+static void *dev_of(const void *h, size_t bytes)
+{
+    void *d = NULL;
+    CHECK(harness_dev_alloc_copy(&d, h, bytes) == 0, "device alloc");
+    return d;
+}
+
+static void expect_dev(const void *d, const void *exp, size_t bytes, const char *what)
+{
+    char *got = malloc(bytes + 1);
+    CHECK(harness_dev_copy_back(got, d, bytes) == 0, "copy back");
+    CHECK(memcmp(got, exp, bytes) == 0, "%s differs from the oracle", what);
+    free(got);
+}
+
+int main(int argc, char **argv)
+{
+    const int use_gpu = getenv("HARNESS_GPU") && atoi(getenv("HARNESS_GPU"));
+    ompi_group_t local = {0}, remote = {1};
+    mca_coll_base_comm_coll_t table;
+    ompi_communicator_t comm;
+    mca_coll_base_module_t *tm, *m;
+    ompi_datatype_t dfloat = {ORC_T_FLOAT, 4, 1, 1}, ddouble = {ORC_T_DOUBLE, 8, 1, 1};
+    ompi_datatype_t dbyte = {ORC_T_BYTE, 1, 1, 1};
+    ompi_op_t sum = {OMPI_OP_FLAGS_INTRINSIC, ORC_OP_SUM}, user = {0, ORC_OP_SUM};
+    int prio = -1, i;
+
+    if (argc < 4) return 2;
+    g_rank = atoi(argv[2]);
+    g_size = atoi(argv[3]);
+    harness_proc_name.jobid = (unsigned) strtoul(argv[1], NULL, 16);
+    for (i = 0; i < 64; ++i) ompi_op_ddt_map[i] = i;
+
+    tm = OBJ_NEW(mca_coll_base_module_t);
+    fill_tuned(&table, tm);
+    comm = (ompi_communicator_t){g_rank, g_size, 3, 0, &local, &table};
+
+    /* selection (coll_base_comm_select.c): init_query, comm_query */
+    CHECK((mca_coll_rocm_component.super.collm_init_query(false, false) == OMPI_SUCCESS) ==
+              (ompi_amd_device_count() > 0), "init_query vs device presence");
+    m = mca_coll_rocm_component.super.collm_comm_query(&comm, &prio);
+    CHECK(m != NULL && prio == 80, "comm_query on a local intra-communicator");
+    CHECK(m->coll_allreduce && m->coll_reduce && m->coll_reduce_scatter_block && m->coll_scan &&
+              m->coll_exscan && m->coll_allgather && m->coll_bcast && m->coll_module_enable,
+          "module function table");
+    {
+        ompi_communicator_t c1 = comm, ci = comm, cr = comm;
+        mca_coll_base_module_t *x;
+        c1.size = 1;
+        ci.inter = 1;
+        cr.c_local_group = &remote;
+        CHECK(mca_coll_rocm_component.super.collm_comm_query(&c1, &prio) == NULL, "size 1");
+        CHECK(mca_coll_rocm_component.super.collm_comm_query(&ci, &prio) == NULL, "inter");
+        CHECK(mca_coll_rocm_component.super.collm_comm_query(&cr, &prio) == NULL, "remote peers");
+        c1.size = OMPI_AMD_MAX_RANKS + 1;
+        x = mca_coll_rocm_component.super.collm_comm_query(&c1, &prio);
+        CHECK(x == NULL, "too many ranks");
+    }
+    if (!use_gpu) {
+        OBJ_RELEASE(m);
+        release_table(&table);
+        OBJ_RELEASE(tm);
+        printf("ok\n");
+        return 0;
+    }
+
+    CHECK(m->coll_module_enable(m, &comm) == OMPI_SUCCESS, "enable");
+    CHECK(tm->super.obj_reference_count == 1 + 7 + 7, "enable retains the saved modules (%d)",
+          tm->super.obj_reference_count);
+    install(&table, m);
+
+    /* 1. allreduce: staged (1000) and zero-copy (300001) sizes */
+    {
+        const int counts[2] = {1000, 300001};
+        for (int k = 0; k < 2; ++k) {
+            const size_t n = (size_t) counts[k];
+            float **xs = all_inputs(n, 10 + k);
+            float **rb = malloc(sizeof(float *) * (size_t) g_size);
+            void *ds, *dr;
+            for (int r = 0; r < g_size; ++r) rb[r] = calloc(n, sizeof(float));
+            CHECK(orc_allreduce(ORC_AR_TUNED, g_size, (const void *const *) xs, (void *const *) rb,
+                                n, ORC_OP_SUM, ORC_T_FLOAT, 0) >= 0, "oracle allreduce");
+            ds = dev_of(xs[g_rank], n * 4);
+            dr = dev_of(rb[g_rank], n * 4);  /* contents irrelevant */
+            tuned_calls = 0;
+            CHECK(table.coll_allreduce(ds, dr, (int) n, &dfloat, &sum, &comm,
+                                       table.coll_allreduce_module) == OMPI_SUCCESS, "allreduce");
+            CHECK(tuned_calls == 0, "device allreduce fell back");
+            expect_dev(dr, rb[g_rank], n * 4, "allreduce");
+            /* in place */
+            CHECK(table.coll_allreduce(MPI_IN_PLACE, ds, (int) n, &dfloat, &sum, &comm,
+                                       table.coll_allreduce_module) == OMPI_SUCCESS, "allreduce ip");
+            expect_dev(ds, rb[g_rank], n * 4, "allreduce in place");
+            harness_dev_free(ds);
+            harness_dev_free(dr);
+            for (int r = 0; r < g_size; ++r) free(rb[r]);
+            free(rb);
+            free_inputs(xs);
+        }
+    }
+    /* 2. reduce to the last rank (tuned decision order), root in place */
+    {
+        const size_t n = 5000;
+        const int root = g_size - 1;
+        float **xs = all_inputs(n, 20);
+        float *exp = calloc(n, sizeof(float)), *expip = calloc(n, sizeof(float));
+        void *ds = dev_of(xs[g_rank], n * 4), *dr = dev_of(exp, n * 4);
+        CHECK(orc_reduce(ORC_RED_TUNED, g_size, (const void *const *) xs, exp, n, ORC_OP_SUM,
+                         ORC_T_FLOAT, root, 0) >= 0, "oracle reduce");
+        CHECK(orc_reduce(ORC_RED_TUNED, g_size, (const void *const *) xs, expip, n, ORC_OP_SUM,
+                         ORC_T_FLOAT, root, 1) >= 0, "oracle reduce in place");
+        CHECK(table.coll_reduce(ds, g_rank == root ? dr : NULL, (int) n, &dfloat, &sum, root, &comm,
+                                table.coll_reduce_module) == OMPI_SUCCESS, "reduce");
+        if (g_rank == root) expect_dev(dr, exp, n * 4, "reduce");
+        CHECK(table.coll_reduce(g_rank == root ? MPI_IN_PLACE : ds, g_rank == root ? ds : NULL,
+                                (int) n, &dfloat, &sum, root, &comm,
+                                table.coll_reduce_module) == OMPI_SUCCESS, "reduce in place");
+        if (g_rank == root) expect_dev(ds, expip, n * 4, "reduce in place");
+        harness_dev_free(ds);
+        harness_dev_free(dr);
+        free(exp);
+        free(expip);
+        free_inputs(xs);
+    }
+    /* 3. scan / exscan, fp64 */
+    for (int ex = 0; ex < 2; ++ex) {
+        const size_t n = 2000;
+        double **xs = malloc(sizeof(double *) * (size_t) g_size);
+        double **rb = malloc(sizeof(double *) * (size_t) g_size);
+        float *tmp = malloc(n * sizeof(float));
+        void *ds, *dr;
+        for (int r = 0; r < g_size; ++r) {
+            xs[r] = malloc(n * 8);
+            rb[r] = calloc(n, 8);
+            gen(tmp, n, r, 30 + ex);
+            for (size_t k = 0; k < n; ++k) xs[r][k] = (double) tmp[k] / 3.0;
+        }
+        CHECK(orc_scan(ex, g_size, (const void *const *) xs, (void *const *) rb, n, ORC_OP_SUM,
+                       ORC_T_DOUBLE) == 0, "oracle scan");
+        ds = dev_of(xs[g_rank], n * 8);
+        dr = dev_of(rb[g_rank], n * 8);
+        CHECK((ex ? table.coll_exscan(ds, dr, (int) n, &ddouble, &sum, &comm,
+                                      table.coll_exscan_module)
+                  : table.coll_scan(ds, dr, (int) n, &ddouble, &sum, &comm,
+                                    table.coll_scan_module)) == OMPI_SUCCESS, "scan");
+        if (!(ex && g_rank == 0)) expect_dev(dr, rb[g_rank], n * 8, ex ? "exscan" : "scan");
+        harness_dev_free(ds);
+        harness_dev_free(dr);
+        for (int r = 0; r < g_size; ++r) { free(xs[r]); free(rb[r]); }
+        free(xs); free(rb); free(tmp);
+    }
+    /* 4. reduce_scatter_block (tuned reduce-to-0 order) */
+    {
+        const size_t rc = 1500, n = rc * (size_t) g_size;
+        float **xs = all_inputs(n, 40);
+        float **rb = malloc(sizeof(float *) * (size_t) g_size);
+        void *ds, *dr;
+        for (int r = 0; r < g_size; ++r) rb[r] = calloc(rc, sizeof(float));
+        CHECK(orc_reduce_scatter_block(g_size, (const void *const *) xs, (void *const *) rb, rc,
+                                       ORC_OP_SUM, ORC_T_FLOAT) >= 0, "oracle rsb");
+        ds = dev_of(xs[g_rank], n * 4);
+        dr = dev_of(rb[g_rank], rc * 4);
+        CHECK(table.coll_reduce_scatter_block(ds, dr, (int) rc, &dfloat, &sum, &comm,
+                                              table.coll_reduce_scatter_block_module) ==
+                  OMPI_SUCCESS, "rsb");
+        expect_dev(dr, rb[g_rank], rc * 4, "reduce_scatter_block");
+        harness_dev_free(ds);
+        harness_dev_free(dr);
+        for (int r = 0; r < g_size; ++r) free(rb[r]);
+        free(rb);
+        free_inputs(xs);
+    }
+    /* 5. allgather and bcast of bytes */
+    {
+        const size_t b = 1000;
+        unsigned char *mine = malloc(b), *all = malloc(b * (size_t) g_size);
+        void *ds, *dr;
+        for (int r = 0; r < g_size; ++r)
+            for (size_t k = 0; k < b; ++k) all[(size_t) r * b + k] = (unsigned char)(r * 17 + k * 3);
+        memcpy(mine, all + (size_t) g_rank * b, b);
+        ds = dev_of(mine, b);
+        {
+            unsigned char *zero = calloc(b * (size_t) g_size, 1);
+            dr = dev_of(zero, b * (size_t) g_size);
+            free(zero);
+        }
+        CHECK(table.coll_allgather(ds, (int) b, &dbyte, dr, (int) b, &dbyte, &comm,
+                                   table.coll_allgather_module) == OMPI_SUCCESS, "allgather");
+        expect_dev(dr, all, b * (size_t) g_size, "allgather");
+        /* bcast from rank 1 % size of its slot */
+        {
+            const int root = 1 % g_size;
+            void *bb = dev_of(g_rank == root ? all + (size_t) root * b : mine, b);
+            CHECK(table.coll_bcast(bb, (int) b, &dbyte, root, &comm, table.coll_bcast_module) ==
+                      OMPI_SUCCESS, "bcast");
+            expect_dev(bb, all + (size_t) root * b, b, "bcast");
+            harness_dev_free(bb);
+        }
+        harness_dev_free(ds);
+        harness_dev_free(dr);
+        free(mine);
+        free(all);
+    }
+    /* 6. delegation: host buffers, mixed residency, non-intrinsic op */
+    {
+        const size_t n = 4096;
+        float *h = calloc(n, sizeof(float)), *h2 = calloc(n, sizeof(float));
+        void *d = dev_of(h, n * 4), *d2 = dev_of(h2, n * 4);
+        tuned_calls = 0;
+        CHECK(table.coll_allreduce(h, h2, (int) n, &dfloat, &sum, &comm,
+                                   table.coll_allreduce_module) == OMPI_SUCCESS, "host");
+        CHECK(tuned_calls == 1, "host buffers must go to the saved allreduce");
+        CHECK(table.coll_allreduce(g_rank == 0 ? (void *) h : d, g_rank == 0 ? (void *) h2 : d2,
+                                   (int) n, &dfloat, &sum, &comm,
+                                   table.coll_allreduce_module) == OMPI_SUCCESS, "mixed");
+        CHECK(tuned_calls == 2, "mixed residency must fall back on every rank");
+        CHECK(table.coll_allreduce(d, d2, (int) n, &dfloat, &user, &comm,
+                                   table.coll_allreduce_module) == OMPI_SUCCESS, "user op");
+        CHECK(tuned_calls == 3, "non-intrinsic op must fall back");
+        CHECK(table.coll_scan(h, h2, (int) n, &dfloat, &sum, &comm, table.coll_scan_module) ==
+                  OMPI_SUCCESS && tuned_calls == 4, "host scan falls back");
+        CHECK(table.coll_reduce(h, g_rank == 0 ? h2 : NULL, (int) n, &dfloat, &sum, 0, &comm,
+                                table.coll_reduce_module) == OMPI_SUCCESS && tuned_calls == 5,
+              "host reduce falls back");
+        harness_dev_free(d);
+        harness_dev_free(d2);
+        free(h);
+        free(h2);
+    }
+    /* teardown: the table's references, then the module (its destructor
+     * releases the saved modules and destroys the device communicator) */
+    release_table(&table);
+    OBJ_RELEASE(m);
+    CHECK(tm->super.obj_reference_count == 1, "saved modules released (%d)",
+          tm->super.obj_reference_count);
+    OBJ_RELEASE(tm);
+    printf("ok gpu\n");
+    return 0;
+}

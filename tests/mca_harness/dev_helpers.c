@@ -12,3 +12,8 @@ int harness_dev_copy_back(void *h, const void *d, size_t bytes)
 {
     return hipMemcpy(h, d, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
+
+int harness_dev_free(void *d)
+{
+    return hipFree(d) == hipSuccess ? 0 : -1;
+}

@@ -32,3 +32,54 @@ def test_op_component_device_path(harness):
     r = subprocess.run([harness], capture_output=True, text=True, timeout=120,
                        env={**os.environ, "HARNESS_GPU": "1"})
     assert r.returncode == 0 and r.stdout.strip() == "ok gpu", (r.stdout, r.stderr)
+
+
+# ---- coll/rocm (ompi_amd/mca/coll/rocm) through tests/mca_harness/coll_harness.c ----
+
+@pytest.fixture(scope="module")
+def coll_harness(tmp_path_factory):
+    from ompi_amd import _lib
+    from oracle import oracle as orc
+    _lib.load()
+    orc.lib()
+    out = str(tmp_path_factory.mktemp("mca") / "coll_harness")
+    subprocess.run(["bash", os.path.join(ROOT, "tests", "mca_harness", "build_coll.sh"), out],
+                   check=True)
+    return out
+
+
+def _run_coll_harness(exe, n, gpu, timeout):
+    import secrets
+    name = secrets.token_hex(3)
+    env = {**os.environ, "HARNESS_GPU": "1" if gpu else "0", "HSA_ENABLE_IPC_MODE_LEGACY": "0",
+           "OMPI_AMD_COLL_TIMEOUT_MS": "20000"}
+    procs = [subprocess.Popen([exe, name, str(r), str(n)], stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True, env=env) for r in range(n)]
+    outs = []
+    try:
+        for p in procs:
+            out, err = p.communicate(timeout=timeout)
+            outs.append((p.returncode, out.strip(), err[-2000:]))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return outs
+
+
+def test_coll_component_selection(coll_harness):
+    """comm_query accepts node-local intra-communicators of 2..16 ranks;
+    init_query refuses without a device (coll_base_comm_select.c protocol)."""
+    for rc, out, err in _run_coll_harness(coll_harness, 2, False, 60):
+        assert rc == 0 and out == "ok", (rc, out, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 3])
+def test_coll_component_device_path(coll_harness, n):
+    """enable saves/retains the previous functions; every collective called
+    through the communicator's table runs on device buffers and matches the
+    oracle bit for bit; host / mixed / user-op calls go to the saved
+    functions on every rank; release destroys the device communicator."""
+    for rc, out, err in _run_coll_harness(coll_harness, n, True, 240):
+        assert rc == 0 and out == "ok gpu", (rc, out, err)
