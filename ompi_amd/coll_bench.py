@@ -3,9 +3,12 @@ collective, one process per GPU (torch.distributed.run), with RCCL's
 allreduce of the same buffer timed beside it as the comparator.
 
 busBW = S / t * 2(N-1)/N; roofline R(N) = (N-1) x 153 GB/s.
-The dominant kernel is the fused peer-load reduction (phase 0): per launch
-it pulls (N-1)/N * S bytes over xGMI into this GPU; its achieved rate is
-those bytes over its event-timed duration.
+Before the timed region the data-movement scheme (pull, pull+push, push)
+and the transfer grid are chosen by measurement among the variants that
+are bit-exact on dataset E (a dynamic-rules file in coll/tuned terms); all
+candidates are reported in config.schemes.  The dominant kernel is the
+fused ring-order reduction (phase 0); its achieved rate is the xGMI bytes
+arriving at this GPU during the launch over its event-timed duration.
 """
 from __future__ import annotations
 
@@ -71,13 +74,18 @@ def bench_allreduce(args, metric: str, link_gbs: float):
     schemes = {}
     for a, name in ALGORITHMS:
         comm.set_param("algorithm", a)
+        comm.set_param("blocks", 1024)
         exact = _exact_ok(comm, dist, torch, mop, n, rank, shared)
-        ta = _timed(ours, 5, 2, dist, torch, tdev) / 5
-        schemes[name] = {"algorithm": a, "bit_exact": exact, "us": round(ta * 1e6, 2),
-                         "busbw": round(S / ta * factor / 1e9, 2)}
+        for blocks in BLOCKS:
+            comm.set_param("blocks", blocks)
+            ta = _timed(ours, 5, 2, dist, torch, tdev) / 5
+            schemes[f"{name}/{blocks}"] = {"algorithm": a, "blocks": blocks, "bit_exact": exact,
+                                           "us": round(ta * 1e6, 2),
+                                           "busbw": round(S / ta * factor / 1e9, 2)}
     usable = [v for v in schemes.values() if v["bit_exact"] is not False]
     best = min(usable or schemes.values(), key=lambda v: v["us"])
     comm.set_param("algorithm", best["algorithm"])
+    comm.set_param("blocks", best["blocks"])
     best_name = next(k for k, v in schemes.items() if v is best)
 
     t = _timed(ours, args.steps, args.warmup, dist, torch, tdev)
@@ -155,6 +163,7 @@ def bench_allreduce(args, metric: str, link_gbs: float):
 
 
 ALGORITHMS = ((0, "pull"), (1, "pull_push"), (2, "push"))
+BLOCKS = (256, 512, 1024, 2048)  # grid cap of the transfer kernels
 
 
 def _exact_ok(comm, dist, torch, mop, n, rank, shared):
@@ -245,33 +254,25 @@ def _config5(comm, dist, torch, mop, world, rank, tdev):
 
 def _variants(comm, dist, torch, mop, world, tdev):
     """Design A/B points measured in the same run (the multi-GPU node is only
-    reachable through this bench): workgroup count of the 256 MiB transfer
-    kernels, and staged one-shot (every rank folds all N blocks from the
-    peers' scratch) vs zero-copy two-shot (own block, then gather) around
-    the small_bytes switch."""
-    factor = 2.0 * (world - 1) / world
-    out = {"blocks_256MiB": [], "small_path": []}
-    n = (256 << 20) // 4
-    x = torch.ones(n, device="cuda")
-    y = torch.empty_like(x)
-    for blocks in (256, 512, 2048, 4096, 1024):
-        comm.set_param("blocks", blocks)
-        t = _timed(lambda: comm.allreduce(x, y, n, mop.MPI_FLOAT, mop.MPI_SUM), 5, 2,
-                   dist, torch, tdev) / 5
-        out["blocks_256MiB"].append({"blocks": blocks, "us": round(t * 1e6, 2),
-                                     "busbw": round(n * 4 / t * factor / 1e9, 3)})
-    del x, y
-    for nbytes in (64 << 10, 256 << 10, 1 << 20, 4 << 20):
+    reachable through this bench): the small/medium-message paths around
+    the fused_bytes / small_bytes switches — one fused launch (every rank
+    folds all blocks), staged two-shot (scratch, no host rendezvous) and
+    zero-copy (per-call IPC handle swap) — at the headline's scheme."""
+    out = {"small_path": []}
+    paths = (("fused", 4 << 20, 4 << 20), ("staged_two_shot", 0, 4 << 20), ("zero_copy", 0, 0))
+    for nbytes in (16 << 10, 64 << 10, 256 << 10, 1 << 20, 2 << 20):
         n = nbytes // 4
         x = torch.ones(n, device="cuda")
         y = torch.empty_like(x)
         row = {"bytes": nbytes}
-        for name, small in (("staged_one_shot", 4 << 20), ("zero_copy_two_shot", 0)):
+        for name, fused, small in paths:
+            comm.set_param("fused_bytes", fused)
             comm.set_param("small_bytes", small)
             t = _timed(lambda: comm.allreduce(x, y, n, mop.MPI_FLOAT, mop.MPI_SUM), 20, 3,
                        dist, torch, tdev) / 20
             row[name + "_us"] = round(t * 1e6, 2)
         out["small_path"].append(row)
         del x, y
+    comm.set_param("fused_bytes", 64 << 10)
     comm.set_param("small_bytes", 1 << 20)
     return out

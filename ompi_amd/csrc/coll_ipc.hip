@@ -295,6 +295,74 @@ __global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, ptr_s
     xfer_epilogue();
 }
 
+// ---------------------------------------------------------------- fused small allreduce
+// One launch for small messages (param "fused_bytes"): every workgroup
+// stages its slice of my input in my scratch half, signals the peers on its
+// own flag row, waits for the same slice of every peer and folds it.
+// Workgroup g depends only on the peers' workgroup g (same slice), so there
+// is no grid-wide sync.  Flag slot [g * kMaxRanks + p] of rank r holds the
+// last epoch peer p's workgroup g signalled to r (row 0 doubles as the
+// barrier kernel's row; epochs only grow, so the users never collide).
+constexpr int kFusedMaxGroups = 4096 / (int)sizeof(uint64_t) / kMaxRanks;  // 32 rows
+
+struct fused_args {
+    const char *src;
+    char *dst, *mine;
+    ptr_set peers;
+    uint64_t *flags;
+    flag_set peer_flags;
+    int rank, n, order;
+    int64_t count, split, early, late;
+    uint64_t epoch, timeout_ticks;
+    int *err;
+};
+
+template <typename T, int OP>
+__global__ __launch_bounds__(kXferThreads) void fused_allreduce_kernel(fused_args a) {
+    const int t = threadIdx.x;
+    const int g = blockIdx.y * gridDim.x + blockIdx.x;
+    int64_t off = 0, cnt = a.count;
+    int first = 0;
+    if (a.order == ORDER_RING) {  // grid row y = ring block y
+        const int64_t b = blockIdx.y;
+        off = b < a.split ? b * a.early : b * a.late + a.split;
+        cnt = b < a.split ? a.early : a.late;
+        first = (int)b;
+    }
+    const int64_t per = (cnt + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = off + min(cnt, per * (int64_t)blockIdx.x);
+    const int64_t hi = off + min(cnt, per * (int64_t)(blockIdx.x + 1));
+    const T *src = reinterpret_cast<const T *>(a.src);
+    T *mine = reinterpret_cast<T *>(a.mine);
+    for (int64_t e = lo + t; e < hi; e += kXferThreads) mine[e] = src[e];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) sys_release();
+    __syncthreads();
+    if (t < a.n && t != a.rank) {
+        __hip_atomic_store(a.peer_flags.p[t] + g * kMaxRanks + a.rank, a.epoch, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(a.flags + g * kMaxRanks + t, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM) < a.epoch) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+                __hip_atomic_store(a.err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    sys_acquire();
+    T *dst = reinterpret_cast<T *>(a.dst);
+    for (int64_t e = lo + t; e < hi; e += kXferThreads) {
+        T v[kMaxRanks];
+        gather_scalar<T>(v, a.peers, a.n, first, e);
+        store_elem<T>(dst + e, fold<T, OP>(v, a.n, a.order, 0));
+    }
+}
+
 // ---------------------------------------------------------------- copy
 // Byte copy with a peeled head so that the body runs 16 B (or 4 B) per
 // lane whenever src and dst share their alignment phase.
@@ -371,6 +439,30 @@ make_red_table(std::integer_sequence<int, O...>) {
 }
 static const auto g_red = make_red_table(std::make_integer_sequence<int, OMPI_AMD_OP_COUNT>{});
 
+using fused_launch_fn = hipError_t (*)(dim3, const fused_args &, hipStream_t);
+
+template <int OP, int TYPE>
+static hipError_t fused_launch_slot(dim3 grid, const fused_args &a, hipStream_t s) {
+    if constexpr (slot_supported(OP, TYPE)) {
+        using T = typename type_of<TYPE>::type;
+        hipLaunchKernelGGL((fused_allreduce_kernel<T, OP>), grid, dim3(kXferThreads), 0, s, a);
+        return hipGetLastError();
+    } else {
+        return hipErrorInvalidValue;
+    }
+}
+template <int OP, int... T>
+static constexpr std::array<fused_launch_fn, OMPI_AMD_TYPE_COUNT> make_fused_row(
+    std::integer_sequence<int, T...>) {
+    return {{(slot_supported(OP, T) ? &fused_launch_slot<OP, T> : (fused_launch_fn) nullptr)...}};
+}
+template <int... O>
+static constexpr std::array<std::array<fused_launch_fn, OMPI_AMD_TYPE_COUNT>, OMPI_AMD_OP_COUNT>
+make_fused_table(std::integer_sequence<int, O...>) {
+    return {{make_fused_row<O>(std::make_integer_sequence<int, OMPI_AMD_TYPE_COUNT>{})...}};
+}
+static const auto g_fused = make_fused_table(std::make_integer_sequence<int, OMPI_AMD_OP_COUNT>{});
+
 // MPI type size (bytes of data) — the tuned decisions use it, not the
 // extent (ompi_datatype_module.c:404-430: DOUBLE_INT size 12 / extent 16).
 static size_t type_size(int type) {
@@ -432,6 +524,7 @@ struct ompi_amd_comm {
     uint64_t epoch = 0;
     // params
     size_t small_bytes = 1 << 20;
+    size_t fused_bytes = 64 << 10;
     int zero_copy = 1;
     int64_t timeout_ms = 30000;
     int max_blocks = 1024;
@@ -784,6 +877,76 @@ static int stage_in(ompi_amd_comm_t *c, const void *src, size_t bytes, stage_hal
 }
 
 // ---- large allreduce, three data-movement schemes (header comment) ----
+// ---- small allreduce: one fused launch (flags per workgroup) ----
+static int allreduce_fused(ompi_amd_comm_t *c, const void *src, void *rbuf, int64_t count,
+                           int op, int type, bool tree, hipStream_t s) {
+    fused_launch_fn f = g_fused[op][type];
+    if (!f) return OMPI_AMD_ERR_UNSUPPORTED;
+    const int n = c->size;
+    const stage_half sh = next_half(c);
+    fused_args a{};
+    a.src = (const char *)src;
+    a.dst = (char *)rbuf;
+    a.mine = sh.mine;
+    a.peers = sh.peers;
+    a.flags = c->flags;
+    a.peer_flags = c->peer_flags;
+    a.rank = c->rank;
+    a.n = n;
+    a.order = tree ? ORDER_TREE : ORDER_RING;
+    a.count = count;
+    blockcount(count, n, &a.split, &a.early, &a.late);
+    a.epoch = ++c->epoch;
+    a.timeout_ticks = (uint64_t)c->timeout_ms * 100000ull;  // s_memrealtime: 100 MHz
+    a.err = c->err_dev;
+    const int rows = tree ? 1 : n;
+    const int64_t most = tree ? count : a.early;
+    const int64_t cols = std::max<int64_t>(
+        1, std::min<int64_t>((most + 4 * kXferThreads - 1) / (4 * kXferThreads),
+                             kFusedMaxGroups / rows));
+    return record_hip(f(dim3((unsigned)cols, (unsigned)rows), a, s), "fused allreduce launch");
+}
+
+// ---- medium allreduce, staged two-shot: my input -> my scratch, barrier,
+// my ring block folded from every scratch into my rbuf and into a result
+// area of my scratch, barrier, the other blocks pulled from their owners'
+// result areas.  No host rendezvous; no trailing barrier (next_half).
+static size_t two_shot_result_off(size_t bytes) { return (bytes + 255) & ~(size_t)255; }
+
+static bool two_shot_fits(const ompi_amd_comm_t *c, int64_t count, size_t ext) {
+    int64_t split, early, late;
+    blockcount(count, c->size, &split, &early, &late);
+    return two_shot_result_off((size_t)count * ext) + (size_t)early * ext + 16 <= c->scratch_bytes;
+}
+
+static int allreduce_staged_two_shot(ompi_amd_comm_t *c, const void *src, void *rbuf,
+                                     int64_t count, int op, int type, hipStream_t s) {
+    const int n = c->size, mine = (c->rank + 1) % n;
+    const int64_t ext = (int64_t)ompi_amd_type_extent(type);
+    const size_t res = two_shot_result_off((size_t)count * ext);
+    int64_t split, early, late;
+    blockcount(count, n, &split, &early, &late);
+    stage_half sh;
+    TRY(stage_in(c, src, (size_t)(count * ext), &sh, s));
+    const int64_t offm = block_off(mine, split, early, late) * ext;
+    ptr_set dst{};
+    dst.p[0] = (const char *)rbuf;
+    dst.p[1] = sh.mine + res + (offm & 15) - offm;
+    red_jobs jobs;
+    ring_jobs(count, n, &jobs, mine);
+    TRY(launch_reduce(c, op, type, sh.peers, n, dst, 2, ORDER_RING, 0, jobs, s));
+    TRY(launch_barrier(c, s));
+    cp_jobs cj{};
+    for (int b = 0; b < n; ++b) {
+        if (b == mine) continue;
+        const int owner = (b + n - 1) % n;
+        const int64_t off = block_off(b, split, early, late) * ext;
+        cj.j[cj.n++] = {sh.peers.p[owner] + res + (off & 15), (char *)rbuf + off,
+                        block_cnt(b, split, early, late) * ext};
+    }
+    return launch_copy(c, cj, s);
+}
+
 static int allreduce_pull(ompi_amd_comm_t *c, const void *src, void *rbuf, int64_t count,
                           int op, int type, bool inplace, hipStream_t s) {
     const int n = c->size, mine = (c->rank + 1) % n;
@@ -1086,6 +1249,9 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
     } else if (!strcmp(key, "blocks")) {
         if (v <= 0 || v > 65535) return OMPI_AMD_ERR_BAD_PARAM;
         c->max_blocks = (int)v;
+    } else if (!strcmp(key, "fused_bytes")) {
+        if (v < 0) return OMPI_AMD_ERR_BAD_PARAM;
+        c->fused_bytes = std::min<size_t>((size_t)v, c->scratch_bytes);
     } else if (!strcmp(key, "algorithm")) {
         if (v < 0 || v >= ALG_COUNT) return OMPI_AMD_ERR_BAD_PARAM;
         c->algorithm = (int)v;
@@ -1115,6 +1281,11 @@ int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
     }
     // order of coll/tuned's fixed decision: < 10000 B recursive doubling
     const bool tree = type_size(type) * count < 10000 || count < (size_t)n;
+    if (bytes <= c->fused_bytes && bytes <= c->scratch_bytes)
+        return allreduce_fused(c, src, rbuf, (int64_t)count, op, type, tree, s);
+    if (!tree && (bytes <= c->small_bytes || !c->zero_copy) &&
+        two_shot_fits(c, (int64_t)count, ext))
+        return allreduce_staged_two_shot(c, src, rbuf, (int64_t)count, op, type, s);
     if (bytes <= c->small_bytes || !c->zero_copy || tree) {
         // staged one-shot: my contribution -> my scratch half, barrier,
         // every rank folds all blocks from all scratches (no trailing

@@ -250,6 +250,12 @@ def main():
          lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, big, 8, inplace=True)),
         ("ar_sum_f32_small_inplace",
          lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, 5000, 9, inplace=True)),
+        ("ar_sum_f32_200003_two_shot",
+         lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, 200003, 67, repeat=2)),
+        ("ar_sum_f64_two_shot_inplace",
+         lambda: case_allreduce(comm, rank, n, D, mop.MPI_SUM, 60001, 68, inplace=True)),
+        ("ar_maxloc_double_int_fused",
+         lambda: case_allreduce(comm, rank, n, DI, mop.MPI_MAXLOC, 3001, 69)),
         ("ar_max_f32_specials", lambda: case_allreduce(comm, rank, n, F, mop.MPI_MAX, 300001, 10, "S")),
         ("ar_min_f32_specials_tree", lambda: case_allreduce(comm, rank, n, F, mop.MPI_MIN, 999, 11, "S")),
         ("ar_sum_f64_big", lambda: case_allreduce(comm, rank, n, D, mop.MPI_SUM, big // 2 + 3, 12)),
