@@ -91,6 +91,33 @@ __global__ __launch_bounds__(T) void k_op(const f32x4 *a, const f32x4 *b, f32x4 
     }
 }
 
+// Cache-policy variants of the op shape through buffer intrinsics: LP / SP
+// are the load / store aux bits (gfx950: 1 = sc0, 2 = nt, 16 = sc1).
+template <int T, int U, int LP, int SP>
+__global__ __launch_bounds__(T) void k_oppol(const float *a, const float *b, float *out,
+                                             size_t nvec) {
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a), 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(b), 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(out, 0, 0x7fffffff, 0x00020000);
+    const size_t base = (size_t)blockIdx.x * T * U + threadIdx.x;
+    f32x4 x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + (size_t)u * T;
+        if (i < nvec) {
+            x[u] = __builtin_amdgcn_raw_buffer_load_b128(ra, (int)(i * 16), 0, LP);
+            y[u] = __builtin_amdgcn_raw_buffer_load_b128(rb, (int)(i * 16), 0, LP);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + (size_t)u * T;
+        if (i < nvec) __builtin_amdgcn_raw_buffer_store_b128(x[u] + y[u], ro, (int)(i * 16), 0, SP);
+    }
+}
+
+struct Bufs;
+
 struct Bufs {
     void *a, *b, *c;
     size_t bytes, nvec;
@@ -149,6 +176,19 @@ static void run_op(const Bufs &B, int reps) {
            3.0 * B.bytes);
 }
 
+template <int T, int U, int LP, int SP>
+static void run_pol(const Bufs &B, int reps) {
+    const size_t chunk = (size_t)T * U;
+    const unsigned grid = (unsigned)((B.nvec + chunk - 1) / chunk);
+    const float *a = (const float *)B.a, *b = (const float *)B.b;
+    float *c = (float *)B.c;
+    const double ms = time_ms([&] { hipLaunchKernelGGL((k_oppol<T, U, LP, SP>), dim3(grid), dim3(T), 0, 0, a, b, c, B.nvec); }, reps);
+    const double gbs = 3.0 * B.bytes / (ms * 1e-3) / 1e9;
+    printf("{\"variant\": \"oppol\", \"threads\": %d, \"unroll\": %d, \"load_aux\": %d, \"store_aux\": %d, "
+           "\"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f}\n", T, U, LP, SP, ms, gbs, gbs / 8000.0);
+    fflush(stdout);
+}
+
 int main(int argc, char **argv) {
     const size_t bytes = (argc > 1) ? strtoull(argv[1], nullptr, 0) : (1ull << 30);
     const int reps = 20;
@@ -162,6 +202,23 @@ int main(int argc, char **argv) {
     CK(hipMemset(B.b, 0x22, bytes));
     CK(hipMemset(B.c, 0, bytes));
     CK(hipDeviceSynchronize());
+    if (argc > 2 && atoi(argv[2]) == 1) {  // cache-policy sweep only
+        run_op<256, 4, 1>(B, reps);
+        run_pol<256, 4, 2, 2>(B, reps);
+        run_pol<256, 4, 0, 0>(B, reps);
+        run_pol<256, 4, 2, 17>(B, reps);
+        run_pol<256, 4, 2, 19>(B, reps);
+        run_pol<256, 4, 2, 16>(B, reps);
+        run_pol<256, 4, 2, 18>(B, reps);
+        run_pol<256, 4, 16, 2>(B, reps);
+        run_pol<256, 4, 19, 2>(B, reps);
+        run_pol<256, 4, 18, 18>(B, reps);
+        run_pol<256, 4, 1, 1>(B, reps);
+        run_pol<256, 8, 2, 2>(B, reps);
+        run_pol<256, 8, 2, 17>(B, reps);
+        run_pol<512, 4, 2, 17>(B, reps);
+        return 0;
+    }
     run_basic<256, 4>(B, reps);
     run_basic<256, 8>(B, reps);
     run_basic<512, 4>(B, reps);
