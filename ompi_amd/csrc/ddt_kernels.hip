@@ -269,6 +269,100 @@ __global__ void ddt_vec_edges(ddt_desc d, const char *src, char *dst, ddt_window
     }
 }
 
+
+// Staged pack for periodic layouts (the LDS staging of strided gathers).
+// The packed stream is a sequence of periods — one datatype instance, or one
+// run of a single-run-per-instance vector — of `psize` packed bytes each;
+// period j's bytes live at typed + base + j * pext + map[q] (q = byte in the
+// period; map = identity for a run).  A workgroup loads the typed span of
+// `nper` consecutive periods into LDS with 16-B nt loads (gaps included: the
+// dispatcher only takes layouts whose gaps are small enough that HBM fetches
+// those sectors anyway), then assembles 16-B packed chunks from LDS at the
+// type's granule and stores them with one dwordx4 each.  Sub-16-B runs
+// (struct{int,double}, blacs indexed, vector of single doubles) thus move
+// with 16-B global accesses on both sides instead of 4- or 8-B granules.
+struct ddt_period {
+    int64_t psize;      // packed bytes per period
+    int64_t pext;       // typed bytes between consecutive periods
+    int64_t base;       // typed offset of period 0's lowest byte
+    int64_t span;       // typed bytes from a period's lowest byte past its highest
+    int64_t nper;       // periods per tile
+    int64_t map_bytes;  // LDS bytes holding the map (0: identity)
+    const uint16_t *map;  // psize entries: typed offset - lowest, per packed byte
+};
+
+template <int G, bool IDENT>
+__global__ __launch_bounds__(kDdtThreads) void ddt_pack_tile_kernel(ddt_period P,
+                                                                   const char *typed,
+                                                                   char *contig, int64_t start,
+                                                                   int64_t j0, int64_t j1) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    using T = typename granule<G>::t;
+    typedef unsigned int v4 __attribute__((ext_vector_type(4)));
+    const int t = threadIdx.x;
+    uint16_t *map = reinterpret_cast<uint16_t *>(lds);
+    char *data = lds + P.map_bytes;
+    if (!IDENT)
+        for (int64_t i = t; i < P.psize; i += kDdtThreads) map[i] = P.map[i];
+    constexpr int64_t step = 16 * kDdtThreads;  // packed bytes per lane pass
+    const int64_t st_j = step / P.psize, st_q = step % P.psize;
+    for (int64_t tile = blockIdx.x;; tile += gridDim.x) {
+        const int64_t jt = j0 + tile * P.nper;
+        if (jt >= j1) break;
+        const int64_t nj = min(P.nper, j1 - jt);
+        const char *t0 = typed + P.base + jt * P.pext;
+        const uintptr_t a0 = (uintptr_t)t0 & ~(uintptr_t)15;
+        const uintptr_t a1 = ((uintptr_t)(t0 + (nj - 1) * P.pext + P.span) + 15) & ~(uintptr_t)15;
+        const int64_t nv = (int64_t)(a1 - a0) / 16;
+        __syncthreads();  // map staged / previous tile's LDS reads done
+        for (int64_t v = t; v < nv; v += kDdtThreads)
+            reinterpret_cast<v4 *>(data)[v] =
+                __builtin_nontemporal_load(reinterpret_cast<const v4 *>(a0) + v);
+        __syncthreads();
+        const int64_t toff = (int64_t)((uintptr_t)t0 - a0);
+        const int64_t len = nj * P.psize;               // packed bytes of this tile
+        char *c0 = contig + (jt * P.psize - start);     // its first packed byte
+        const uintptr_t A0 = (uintptr_t)c0 & ~(uintptr_t)15;
+        const int64_t nch = (int64_t)((((uintptr_t)(c0 + len) + 15) & ~(uintptr_t)15) - A0) / 16;
+        int64_t r = (int64_t)(A0 - (uintptr_t)c0) + 16 * (int64_t)t;  // tile-relative offset
+        int64_t jj = 0, q = 0;
+        bool walk = false;
+        for (int64_t ch = t; ch < nch; ch += kDdtThreads, r += step) {
+            char *cp = reinterpret_cast<char *>(A0 + 16 * ch);
+            if (r >= 0 && r + 16 <= len) {
+                if (!walk) {  // one division per lane per tile, then walk
+                    jj = r / P.psize;
+                    q = r - jj * P.psize;
+                    walk = true;
+                }
+                union { v4 v; T e[16 / G]; } buf;
+                int64_t j2 = jj, q2 = q;
+#pragma unroll
+                for (int g = 0; g < 16 / G; ++g) {
+                    const int64_t off = toff + j2 * P.pext + (IDENT ? q2 : (int64_t)map[q2]);
+                    buf.e[g] = *reinterpret_cast<const T *>(data + off);
+                    q2 += G;
+                    if (q2 == P.psize) { q2 = 0; ++j2; }
+                }
+                __builtin_nontemporal_store(buf.v, reinterpret_cast<v4 *>(cp));
+            } else {
+                for (int g = 0; g < 16 / G; ++g) {  // tile-edge chunk: in-range granules
+                    const int64_t rg = r + g * G;
+                    if (rg < 0 || rg >= len) continue;
+                    const int64_t jg = rg / P.psize, qg = rg - jg * P.psize;
+                    const int64_t off = toff + jg * P.pext + (IDENT ? qg : (int64_t)map[qg]);
+                    *reinterpret_cast<T *>(cp + g * G) = *reinterpret_cast<const T *>(data + off);
+                }
+            }
+            if (walk) {
+                q += st_q;
+                jj += st_j;
+                if (q >= P.psize) { q -= P.psize; ++jj; }
+            }
+        }
+    }
+}
+
 }  // namespace ompi_amd
 
 struct ompi_amd_ddt {
@@ -278,6 +372,10 @@ struct ompi_amd_ddt {
     int64_t extent = 0;
     int64_t max_blen = 0;
     int gran = 1;  // power of two dividing every blen, disp, stride, extent
+    // staged-pack plan for one instance as the period (ddt_pack_tile_kernel)
+    bool inst_tile = false;
+    int64_t lo = 0, hi = 0;     // lowest / one past highest typed byte of an instance
+    uint16_t *dmap = nullptr;   // size entries: typed offset - lo per packed byte
 };
 
 namespace ompi_amd {
@@ -324,6 +422,97 @@ static hipError_t launch_vec(int G, const ddt_walk &v, const ddt_desc &d, const 
     return hipGetLastError();
 }
 
+// Staged tile pack when the layout is periodic, sub-16-B granular (or
+// multi-element) and dense enough.  Returns false when the
+// generic / walker kernels should run instead.
+constexpr int64_t kTileMaxGap = 128;          // bytes of gap the tile reads through
+constexpr int64_t kTileDataDefault = 16 << 10;  // LDS data bytes per workgroup (tuned)
+constexpr int64_t kTileMinWindow = 256 << 10;   // smaller windows: one generic launch
+
+// Layouts whose granule is already 16 B are staged too (vector bl2 / bl8:
+// +28 / +30 %, profiles/r01_ddt_tile_wide.jsonl); OMPI_AMD_DDT_TILE_WIDE=0
+// restricts the tile to sub-16-B granules and multi-element types.
+static bool tile_wide() {
+    static const bool v = !(getenv("OMPI_AMD_DDT_TILE_WIDE") && atoi(getenv("OMPI_AMD_DDT_TILE_WIDE")) == 0);
+    return v;
+}
+
+static int64_t tile_data_bytes() {
+    static const int64_t v = [] {
+        const char *e = getenv("OMPI_AMD_DDT_TILE_BYTES");
+        const int64_t x = e ? atoll(e) : 0;
+        return (x >= 4096 && x <= (60 << 10)) ? x : kTileDataDefault;
+    }();
+    return v;
+}
+
+static bool tile_pack(const ompi_amd_ddt_t *ddt, size_t count, int G, const char *typed,
+                      char *contig, int64_t start, int64_t end, const ddt_desc &d,
+                      hipStream_t s, hipError_t *err) {
+    static const bool off = getenv("OMPI_AMD_DDT_TILE") && atoi(getenv("OMPI_AMD_DDT_TILE")) == 0;
+    if (off || end - start < kTileMinWindow) return false;
+    ddt_period P{};
+    bool ident = false;
+    const ddt_elem &x = ddt->host[0];
+    if (ddt->host.size() == 1 && x.count > 1 && (G < 16 || tile_wide()) &&
+        (count == 1 || ddt->extent == x.count * x.stride) && x.stride > 0 &&
+        x.stride - x.blen <= kTileMaxGap && x.stride <= tile_data_bytes() / 4) {
+        ident = true;  // period = one run
+        P.psize = x.blen;
+        P.pext = x.stride;
+        P.base = x.disp;
+        P.span = x.blen;
+    } else if (ddt->inst_tile && (ddt->host.size() > 1 || G < 16 || tile_wide()) &&
+               ddt->hi - ddt->lo <= tile_data_bytes() / 4) {
+        P.psize = ddt->size;  // period = one instance
+        P.pext = ddt->extent;
+        P.base = ddt->lo;
+        P.span = ddt->hi - ddt->lo;
+        P.map = ddt->dmap;
+        P.map_bytes = (P.psize * 2 + 15) & ~(int64_t)15;
+    } else {
+        return false;
+    }
+    if (P.pext < 0 || P.psize % G != 0) return false;
+    const int64_t j0 = (start + P.psize - 1) / P.psize, j1 = end / P.psize;
+    if (j1 <= j0) return false;
+    P.nper = std::max<int64_t>(1, (tile_data_bytes() - P.span) / std::max<int64_t>(P.pext, 1) + 1);
+    const int64_t tiles = (j1 - j0 + P.nper - 1) / P.nper;
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(tiles, 2048));
+    const size_t lds = (size_t)P.map_bytes +
+                       (size_t)(((P.nper - 1) * P.pext + P.span + 15) & ~(int64_t)15) + 32;
+    hipError_t e = hipSuccess;
+#define TILE(GG)                                                                               \
+    case GG:                                                                                   \
+        if (ident)                                                                             \
+            hipLaunchKernelGGL((ddt_pack_tile_kernel<GG, true>), dim3(grid), dim3(kDdtThreads), \
+                               lds, s, P, typed, contig, start, j0, j1);                        \
+        else                                                                                   \
+            hipLaunchKernelGGL((ddt_pack_tile_kernel<GG, false>), dim3(grid), dim3(kDdtThreads), \
+                               lds, s, P, typed, contig, start, j0, j1);                        \
+        break;
+    switch (G) {
+        TILE(16)
+        TILE(8)
+        TILE(4)
+        TILE(2)
+        TILE(1)
+    default:
+        return false;
+    }
+#undef TILE
+    e = hipGetLastError();
+    // partial periods at the window ends: generic byte mapping
+    const ddt_window w{start, start, 0, j0 * P.psize - start, j1 * P.psize, end - j1 * P.psize};
+    if (e == hipSuccess && w.head + w.tail > 0) {
+        hipLaunchKernelGGL((ddt_vec_edges<false>), dim3(1), dim3(kDdtThreads), 0, s, d, typed,
+                           contig, w);
+        e = hipGetLastError();
+    }
+    *err = e;
+    return true;
+}
+
 template <bool UNPACK>
 static int ddt_run(const ompi_amd_ddt_t *ddt, size_t count, const void *typed, void *contig,
                    size_t offset, size_t bytes, size_t *done, hipStream_t s) {
@@ -356,7 +545,9 @@ static int ddt_run(const ompi_amd_ddt_t *ddt, size_t count, const void *typed, v
                       (uint64_t)ddt->max_blen / (uint64_t)G < (1ull << 32) &&
                       (uint64_t)ddt->size / (uint64_t)G < (1ull << 32);
     hipError_t e;
-    if (ddt->host.size() == 1) {
+    if (!UNPACK && tile_pack(ddt, count, G, tsrc, tdst, start, end, d, s, &e)) {
+        // staged LDS tile pack (+ generic bytes for partial periods)
+    } else if (ddt->host.size() == 1) {
         const ddt_elem &x = ddt->host[0];
         const ddt_walk v{x.count, x.blen / G, x.stride, x.disp, ddt->extent, x.count * (x.blen / G)};
         e = launch_vec<UNPACK>(G, v, d, tsrc, tdst, w, s);
@@ -405,12 +596,46 @@ int ompi_amd_ddt_create_elems(const ompi_amd_ddt_elem_t *elems, int nelems, int6
     d->size = prefix;
     d->extent = extent;
     d->gran = pow2_gran(gcd_acc);
+    // Staged-pack plan with one instance as the period: small instances
+    // whose runs leave gaps of at most kTileMaxGap bytes (within an
+    // instance and between consecutive instances).
+    std::vector<uint16_t> imap;
+    if (d->size <= 8192) {
+        std::vector<std::pair<int64_t, int64_t>> runs;  // [begin, end) typed
+        for (const auto &e : d->host)
+            for (int64_t k = 0; k < e.count; ++k)
+                runs.emplace_back(e.disp + k * e.stride, e.disp + k * e.stride + e.blen);
+        int64_t lo = runs[0].first, hi = runs[0].second;
+        for (const auto &r : runs) { lo = std::min(lo, r.first); hi = std::max(hi, r.second); }
+        std::vector<std::pair<int64_t, int64_t>> sorted = runs;
+        std::sort(sorted.begin(), sorted.end());
+        int64_t gap = 0, reach = sorted[0].second;
+        for (const auto &r : sorted) {
+            gap = std::max(gap, r.first - reach);
+            reach = std::max(reach, r.second);
+        }
+        gap = std::max(gap, extent - (hi - lo));
+        if (hi - lo < 65536 && gap <= kTileMaxGap && extent > 0) {
+            for (const auto &r : runs)
+                for (int64_t b = r.first; b < r.second; ++b) imap.push_back((uint16_t)(b - lo));
+            d->inst_tile = true;
+            d->lo = lo;
+            d->hi = hi;
+        }
+    }
     const size_t nb = d->host.size() * sizeof(ddt_elem);
     hipError_t err = hipMalloc(&d->dev, nb);
     if (err == hipSuccess) err = hipMemcpy(d->dev, d->host.data(), nb, hipMemcpyHostToDevice);
+    if (err == hipSuccess && d->inst_tile) {
+        err = hipMalloc(&d->dmap, imap.size() * sizeof(uint16_t));
+        if (err == hipSuccess)
+            err = hipMemcpy(d->dmap, imap.data(), imap.size() * sizeof(uint16_t),
+                            hipMemcpyHostToDevice);
+    }
     if (err != hipSuccess) {
         int rc = record_hip(err, "ddt descriptor upload");
         if (d->dev) (void)hipFree(d->dev);
+        if (d->dmap) (void)hipFree(d->dmap);
         delete d;
         return rc;
     }
@@ -451,6 +676,7 @@ int ompi_amd_ddt_create(const ompi_amd_ddt_block_t *blocks, int nblocks, int64_t
 int ompi_amd_ddt_destroy(ompi_amd_ddt_t *ddt) {
     if (!ddt) return OMPI_AMD_SUCCESS;
     if (ddt->dev) (void)hipFree(ddt->dev);
+    if (ddt->dmap) (void)hipFree(ddt->dmap);
     delete ddt;
     return OMPI_AMD_SUCCESS;
 }

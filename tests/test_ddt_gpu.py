@@ -140,3 +140,45 @@ def test_indexed_upper_triangular_large(orc):
     s, t = src[:span].cpu().numpy(), dst[:span].cpu().numpy()
     assert np.array_equal(s[mask], t[mask])
     assert not t[~mask].any()
+
+
+@pytest.mark.parametrize("layout", ["struct_int_double", "blacs", "vector_bl1_single",
+                                    "vector5_bl1_tiled", "struct_neg_lb", "contig_resized"])
+def test_tile_pack_layouts(orc, layout):
+    """Layouts the staged LDS tile pack takes (periodic, sub-16-B granules,
+    small gaps), many tiles, whole-stream and odd-chunk windows, misaligned
+    packed destination: byte-exact vs the oracle."""
+    i32, f64 = dd.predefined("MPI_INT"), dd.predefined("MPI_DOUBLE")
+    if layout == "struct_int_double":
+        dt, count = dd.type_struct([1, 1], [0, 8], [i32, f64]), 200003
+    elif layout == "blacs":
+        lens = [13, 13, 13, 13, 13, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1]
+        disps = [286, 308, 330, 352, 374, 396, 419, 442, 465, 488, 511, 534, 557, 580, 603,
+                 626, 649, 672]
+        dt, count = dd.type_indexed(lens, disps, i32), 4001
+    elif layout == "vector_bl1_single":
+        dt, count = dd.type_vector(300007, 1, 2, f64), 1
+    elif layout == "vector5_bl1_tiled":
+        dt, count = dd.type_vector(5, 1, 2, f64), 50001
+    elif layout == "struct_neg_lb":
+        dt, count = dd.type_struct([1, 2], [-8, 4], [f64, i32]), 70001
+    else:
+        dt, count = dd.type_struct([3], [4], [i32]), 100001   # 12 B at +4, extent 16
+    total = dt.size * count
+    lb = min(d for d, _ in dt.runs)
+    src = dev_bytes(span_of(dt, count) + max(0, -lb), seed=11)
+    base = src.data_ptr() + max(0, -lb)
+    src_np = src.cpu().numpy()[max(0, -lb):]
+    if lb < 0:  # oracle indexes from the typed base: shift the runs
+        runs = [(d - lb, n) for d, n in dt.runs]
+        exp = orc.pack(runs, dt.extent, count, src.cpu().numpy().copy(), 0, total)
+    else:
+        exp = orc.pack(dt.runs, dt.extent, count, src_np.copy(), 0, total)
+    for chunk, dst_off in ((total, 0), (300007, 5), (262147, 0), (65536, 0), (7777, 8)):
+        packed = dev_bytes(total, offset=dst_off)
+        conv = dd.Convertor()
+        conv.prepare_for_send(dt, count, base)
+        chunked(conv, conv.pack, packed.data_ptr() + dst_off, total, chunk)
+        torch.cuda.synchronize()
+        got = packed[dst_off:dst_off + total].cpu().numpy()
+        assert np.array_equal(got, exp), (layout, chunk, dst_off)
