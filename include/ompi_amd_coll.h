@@ -7,6 +7,7 @@
  *   coll_allreduce            coll.h:208-210  (tuned: coll_tuned_decision_fixed.c:45-89)
  *   coll_reduce               coll.h:239-241  (tuned: :354-428)
  *   coll_reduce_scatter_block coll.h:245-247  (tuned: :522-532)
+ *   coll_reduce_scatter       coll.h:242-244  (tuned: :466-512)
  *   coll_scan / coll_exscan   coll.h:248-250, 228-230 (basic: coll_base_scan.c:35-122,
  *                                                      coll_base_exscan.c:35-107)
  *   coll_allgather            coll.h:200-203  (tuned: :543-600)
@@ -122,6 +123,13 @@ int ompi_amd_reduce(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
 int ompi_amd_reduce_scatter_block(ompi_amd_comm_t *comm, const void *sbuf,
                                   void *rbuf, size_t rcount, int type, int op,
                                   void *stream);
+/* MPI_Reduce_scatter (coll.h:242-244): rbuf receives rcounts[rank]
+ * elements — this rank's block, at offset sum(rcounts[0..rank)) of the
+ * element-wise reduction of the sum(rcounts)-element sbufs — in the operand
+ * order of coll/tuned's decision (recursive halving or ring,
+ * coll_base_reduce_scatter.c:132-623).  rcounts has `size` entries. */
+int ompi_amd_reduce_scatter(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
+                            const size_t *rcounts, int type, int op, void *stream);
 /* MPI_Scan / MPI_Exscan (coll.h:248-250, 228-230): rank r receives the
  * reduction of ranks 0..r (exscan: 0..r-1; rank 0's rbuf is untouched). */
 int ompi_amd_scan(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,

@@ -116,6 +116,9 @@ PROTOTYPES = [
       _C.c_void_p]),
     ("ompi_amd_reduce_scatter_block", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p]),
+    ("ompi_amd_reduce_scatter", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.POINTER(_C.c_size_t), _C.c_int, _C.c_int,
+      _C.c_void_p]),
     ("ompi_amd_scan", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p]),
     ("ompi_amd_exscan", _C.c_int,

@@ -1,10 +1,13 @@
 """Device-buffer collectives of the MI355X path (the coll module surface).
 
-Mirrors the coll framework's entry points for the four collectives this
-path provides (ompi/mca/coll/coll.h:200-247):
+Mirrors the coll framework's entry points this path provides
+(ompi/mca/coll/coll.h:200-250):
 
     coll_allreduce(sbuf, rbuf, count, dtype, op, comm, module)
+    coll_reduce(sbuf, rbuf, count, dtype, op, root, comm, module)
+    coll_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, module)
     coll_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, module)
+    coll_scan / coll_exscan(sbuf, rbuf, count, dtype, op, comm, module)
     coll_allgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, module)
     coll_bcast(buf, count, dtype, root, comm, module)
 
@@ -128,6 +131,14 @@ class Communicator:
         rc = self._lib.ompi_amd_exscan(self._h, _ptr(sbuf), _ptr(rbuf), count, datatype.code,
                                        op.index, _stream(stream))
         self._finish(rc, f"exscan({op.name},{datatype.name})", blocking, stream)
+
+    def reduce_scatter(self, sbuf, rbuf, rcounts, datatype: Datatype, op: Op, stream=None,
+                       blocking: bool = False) -> None:
+        """MPI_Reduce_scatter: rbuf gets rcounts[rank] elements of the reduction."""
+        arr = (ctypes.c_size_t * self.size)(*[int(c) for c in rcounts])
+        rc = self._lib.ompi_amd_reduce_scatter(self._h, _ptr(sbuf), _ptr(rbuf), arr, datatype.code,
+                                               op.index, _stream(stream))
+        self._finish(rc, f"reduce_scatter({op.name},{datatype.name})", blocking, stream)
 
     def reduce_scatter_block(self, sbuf, rbuf, rcount: int, datatype: Datatype, op: Op,
                              stream=None, blocking: bool = False) -> None:

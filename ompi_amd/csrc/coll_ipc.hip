@@ -77,6 +77,7 @@ enum order_t {
     ORDER_CHAIN = 2,     // pipeline chain rooted at `first`; basic_linear = chain at 0, no swap
     ORDER_BINOMIAL = 3,  // in-order binomial tree rooted at `first`
     ORDER_BINARY = 4,    // binary tree rooted at `first`
+    ORDER_HALVING = 5,   // recursive-halving reduce_scatter, owner tmp rank in flags >> 8
 };
 // The root passed MPI_IN_PLACE: its first combine is f(own, child)
 // (coll_base_reduce.c:170-171, 196-199).
@@ -198,6 +199,37 @@ __device__ __forceinline__ T fold(const T (&v)[kMaxRanks], int n, int order, int
             if (c1 < kMaxRanks && c1 < n) w[s] = F::template f<T>(w[s], w[c1]);
         }
         return w[0];
+    }
+    if (order == ORDER_HALVING) {
+        // recursive-halving reduce_scatter (coll_base_reduce_scatter.c:
+        // 203-345): the 2*remain lowest ranks fold pairwise (odd keeps:
+        // f(odd, even)), then at every mask from the top the rank holding
+        // the owner's half does f(mine, partner's).  tb = the owner's tmp
+        // rank; holders at mask m agree with tb on bit m, and their
+        // partners never do, so the update can run in place.
+        int adj = 1;
+        while (adj * 2 <= n) adj *= 2;
+        const int remain = n - adj;
+        const int tb = (flags >> 8) & 0xff;
+        T w[kMaxRanks];
+#pragma unroll
+        for (int u = 0; u < kMaxRanks; ++u) {
+            if (2 * u + 1 < kMaxRanks && u < remain) w[u] = F::template f<T>(v[2 * u + 1], v[2 * u]);
+            else if (u < adj) w[u] = v[u + remain];
+        }
+#pragma unroll
+        for (int m = kMaxRanks / 2; m >= 1; m >>= 1) {
+            if (m < adj) {
+#pragma unroll
+                for (int u = 0; u < kMaxRanks; ++u)
+                    if (u < adj && (u & m) == (tb & m)) w[u] = F::template f<T>(w[u], w[u ^ m]);
+            }
+        }
+        T r = w[0];
+#pragma unroll
+        for (int u = 1; u < kMaxRanks; ++u)
+            if (u == tb) r = w[u];
+        return r;
     }
     // recursive doubling (coll_base_allreduce.c:184-236): fold the
     // 2*extra lowest ranks pairwise, then a pairwise tree; every combine is
@@ -559,6 +591,7 @@ struct buf_desc {
 };
 struct call_blob {
     buf_desc s, r;
+    uint64_t flags;  // per-call rank flags (bit 0: MPI_IN_PLACE)
 };
 
 static int set_dev(ompi_amd_comm_t *c) {
@@ -633,8 +666,9 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
 // Swap (sbuf, rbuf) descriptors with every peer and map theirs (either may
 // be NULL: nothing is exported for it).
 static int exchange_bufs(ompi_amd_comm_t *c, const void *sbuf, const void *rbuf, ptr_set *s,
-                         ptr_set *r) {
+                         ptr_set *r, uint64_t myflags = 0, uint64_t *allflags = nullptr) {
     call_blob mine{};
+    mine.flags = myflags;
     int rc = export_buf(c, sbuf, &mine.s);
     if (rc == OMPI_AMD_SUCCESS) rc = export_buf(c, rbuf, &mine.r);
     if (rc != OMPI_AMD_SUCCESS) return rc;
@@ -642,6 +676,7 @@ static int exchange_bufs(ompi_amd_comm_t *c, const void *sbuf, const void *rbuf,
     rc = c->boot.allgather(&mine, all, sizeof(call_blob));
     if (rc != OMPI_AMD_SUCCESS) return rc;
     for (int p = 0; p < c->size; ++p) {
+        if (allflags) allflags[p] = all[p].flags;
         if (p == c->rank) {
             s->p[p] = (const char *)sbuf;
             r->p[p] = (const char *)rbuf;
@@ -666,10 +701,34 @@ static void release_landing(ompi_amd_comm_t *c) {
 
 // Collective: every rank reaches it in the same call with the same `need`.
 // Growing waits for all earlier work of every rank (no kernel may still
-// touch the old buffers), then swaps handles of the new one.
+// touch the old buffers), then swaps handles of the new one.  The new buffer
+// is allocated (and exported) while the old one is still alive, so it never
+// reuses the old one's address range: on ROCm 7.2 an IPC export of a fresh
+// allocation at a just-freed range failed with hipErrorInvalidValue (seen
+// at 4 ranks, third growth).  Sizes grow geometrically, in 32 MiB steps.
+static hipError_t alloc_exportable(size_t bytes, char **out, hipIpcMemHandle_t *h) {
+    std::vector<void *> failed;
+    hipError_t e = hipErrorInvalidValue;
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        void *p = nullptr;
+        e = hipMalloc(&p, bytes + (size_t)attempt * (2u << 20));
+        if (e != hipSuccess) break;
+        e = hipIpcGetMemHandle(h, p);
+        if (e == hipSuccess) {
+            *out = (char *)p;
+            break;
+        }
+        (void)hipGetLastError();
+        failed.push_back(p);  // keep it alive so the next try gets another range
+    }
+    for (void *p : failed) (void)hipFree(p);
+    return e;
+}
+
 static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     if (need <= c->land_bytes) return OMPI_AMD_SUCCESS;
-    const size_t want = (need + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+    constexpr size_t kStep = 32u << 20;
+    const size_t want = std::max((need + kStep - 1) / kStep * kStep, 2 * c->land_bytes);
     int rc = record_hip(hipDeviceSynchronize(), "landing: drain");
     if (rc == OMPI_AMD_SUCCESS) rc = c->boot.barrier();
     if (rc != OMPI_AMD_SUCCESS) return rc;
@@ -678,18 +737,19 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
         c->land_opened[p] = nullptr;
         c->peer_land.p[p] = nullptr;
     }
-    rc = c->boot.barrier();  // nobody maps the old buffer any more
-    if (rc != OMPI_AMD_SUCCESS) return rc;
-    if (c->land) (void)hipFree(c->land);
-    c->land = nullptr;
-    c->land_bytes = 0;
     struct { hipIpcMemHandle_t h; int ok; } mine{}, all[kMaxRanks];
-    hipError_t e = hipMalloc((void **)&c->land, want);
-    if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.h, c->land);
+    char *fresh = nullptr;
+    hipError_t e = alloc_exportable(want, &fresh, &mine.h);
     mine.ok = e == hipSuccess;
     if (e != hipSuccess) record_hip(e, "landing buffer");
-    rc = c->boot.allgather(&mine, all, sizeof(mine));
-    if (rc != OMPI_AMD_SUCCESS) return rc;
+    rc = c->boot.allgather(&mine, all, sizeof(mine));  // also: nobody maps the old one now
+    if (rc != OMPI_AMD_SUCCESS) {
+        if (fresh) (void)hipFree(fresh);
+        return rc;
+    }
+    if (c->land) (void)hipFree(c->land);
+    c->land = fresh;
+    c->land_bytes = 0;
     bool ok = true;
     for (int p = 0; p < c->size; ++p) ok = ok && all[p].ok;
     for (int p = 0; ok && p < c->size; ++p) {
@@ -1026,6 +1086,43 @@ static int allreduce_push(ompi_amd_comm_t *c, const void *src, void *rbuf, int64
         return launch_reduce(c, op, type, srcs, n, dsts, n, ORDER_RING, 0, jobs, s);
     }));
     return launch_barrier(c, s);
+}
+
+// reduce_scatter_block / reduce_scatter: my block [off, off + cnt) of the
+// full vector folded from every rank's input into rbuf[0, cnt).
+// Staged: inputs in the scratch halves.  Zero-copy: peers' inputs read in
+// place; a rank that passed MPI_IN_PLACE must not overwrite its rbuf (a
+// peer may still read its own block there), so every rank learns the
+// in-place flags with the handle swap and in-place ranks fold into their
+// landing buffer and copy after the trailing barrier.
+static int reduce_my_block(ompi_amd_comm_t *c, const void *src, void *rbuf, size_t total_bytes,
+                           int64_t off, int64_t cnt, int64_t max_cnt, int op, int type,
+                           red_order ro, bool inplace, hipStream_t s) {
+    red_jobs jobs;
+    jobs.n = 1;
+    jobs.j[0] = {off, cnt, 0, ro.first, -1};
+    const int n = c->size;
+    const size_t ext = ompi_amd_type_extent(type);
+    if (total_bytes <= c->small_bytes || !c->zero_copy) {
+        stage_half sh;
+        TRY(stage_in(c, src, total_bytes, &sh, s));
+        return launch_reduce(c, op, type, sh.peers, n, one_ptr(rbuf), 1, ro.order, ro.flags, jobs, s);
+    }
+    ptr_set sp{}, rp{};
+    uint64_t fl[kMaxRanks] = {};
+    TRY(exchange_bufs(c, src, nullptr, &sp, &rp, inplace ? 1 : 0, fl));
+    bool any_inplace = false;
+    for (int p = 0; p < n; ++p) any_inplace = any_inplace || (fl[p] & 1);
+    if (any_inplace)  // collective: every rank sees the same flags and max_cnt
+        TRY(ensure_landing(c, (size_t)max_cnt * ext + 256));
+    TRY(launch_barrier(c, s));
+    void *dst = inplace ? (void *)c->land : rbuf;
+    TRY(launch_reduce(c, op, type, sp, n, one_ptr(dst), 1, ro.order, ro.flags, jobs, s));
+    TRY(launch_barrier(c, s));
+    if (inplace && cnt > 0)
+        return record_hip(hipMemcpyAsync(rbuf, c->land, (size_t)cnt * ext, hipMemcpyDeviceToDevice, s),
+                          "in-place result copy");
+    return OMPI_AMD_SUCCESS;
 }
 
 // scan (exclusive = false) / exscan: rank r folds ranks 0..r (0..r-1) in
@@ -1386,19 +1483,54 @@ int ompi_amd_reduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *rb
     // in place at that level) + scatter: my block folds in that order
     const size_t tcount = rcount * (size_t)n;
     const red_order ro = tuned_reduce_order(n, type_size(type) * tcount, tcount, 0, false);
-    red_jobs jobs;
-    jobs.n = 1;
-    jobs.j[0] = {(int64_t)(rcount * (size_t)c->rank), (int64_t)rcount, 0, ro.first, -1};
-    if (total <= c->small_bytes || !c->zero_copy) {
-        stage_half sh;
-        TRY(stage_in(c, src, total, &sh, s));
-        return launch_reduce(c, op, type, sh.peers, n, one_ptr(rbuf), 1, ro.order, ro.flags, jobs, s);
+    return reduce_my_block(c, src, rbuf, total, (int64_t)(rcount * (size_t)c->rank),
+                           (int64_t)rcount, (int64_t)rcount, op, type, ro, inplace, s);
+}
+
+// coll/tuned's reduce_scatter decision (coll_tuned_decision_fixed.c:
+// 466-512, commutative): recursive halving for small totals or
+// power-of-two sizes up to 256 KiB, else the ring.
+static red_order tuned_reduce_scatter_order(int n, size_t total_bytes, int block) {
+    int pow2 = 1;
+    while (pow2 < n) pow2 <<= 1;
+    if (total_bytes <= 12 * 1024 || (total_bytes <= 256 * 1024 && pow2 == n) ||
+        (double)n >= 0.0012 * (double)total_bytes + 8.0) {
+        int adj = 1;
+        while (adj * 2 <= n) adj *= 2;
+        const int remain = n - adj;
+        const int tb = block < 2 * remain ? block / 2 : block - remain;
+        return {ORDER_HALVING, 0, tb << 8};
     }
-    ptr_set sp{}, rp{};
-    TRY(exchange_bufs(c, src, nullptr, &sp, &rp));
-    TRY(launch_barrier(c, s));
-    TRY(launch_reduce(c, op, type, sp, n, one_ptr(rbuf), 1, ro.order, ro.flags, jobs, s));
-    return launch_barrier(c, s);
+    // ring: block b starts at rank b+1 and ends at b (coll_base_reduce_scatter.c:551-605)
+    return {ORDER_RING, (block + 1) % n, 0};
+}
+
+int ompi_amd_reduce_scatter(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
+                            const size_t *rcounts, int type, int op, void *stream) {
+    if (!c || !rbuf || !rcounts) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
+    TRY(check_sticky(c));
+    const int n = c->size;
+    size_t total = 0, off = 0, maxc = 0;
+    for (int p = 0; p < n; ++p) {
+        if (p < c->rank) off += rcounts[p];
+        total += rcounts[p];
+        maxc = std::max(maxc, rcounts[p]);
+    }
+    if (total == 0) return OMPI_AMD_SUCCESS;
+    TRY(set_dev(c));
+    hipStream_t s = as_stream(stream);
+    const size_t ext = ompi_amd_type_extent(type);
+    const bool inplace = in_place(sbuf, rbuf);
+    const void *src = inplace ? rbuf : sbuf;
+    if (n == 1) {
+        if (inplace) return OMPI_AMD_SUCCESS;
+        return record_hip(hipMemcpyAsync(rbuf, src, rcounts[0] * ext, hipMemcpyDeviceToDevice, s),
+                          "copy");
+    }
+    const red_order ro = tuned_reduce_scatter_order(n, total * type_size(type), c->rank);
+    return reduce_my_block(c, src, rbuf, total * ext, (int64_t)off, (int64_t)rcounts[c->rank],
+                           (int64_t)maxc, op, type, ro, inplace, s);
 }
 
 int ompi_amd_scan(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,

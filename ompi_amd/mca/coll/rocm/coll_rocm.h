@@ -2,7 +2,8 @@
  * coll/rocm — MI355X coll component for Open MPI's coll framework.
  *
  * Drop-in: copy this directory to ompi/mca/coll/rocm/ (INTEGRATION.md §2).
- * The module provides coll_allreduce, coll_reduce, coll_reduce_scatter_block,
+ * The module provides coll_allreduce, coll_reduce, coll_reduce_scatter,
+ * coll_reduce_scatter_block,
  * coll_scan, coll_exscan, coll_allgather and coll_bcast
  * (ompi/mca/coll/coll.h:200-250) for device buffers through libompi_amd.so,
  * and interposes on the previously selected functions (coll/tuned, coll/basic
@@ -63,6 +64,9 @@ int mca_coll_rocm_scan(const void *sbuf, void *rbuf, int count, struct ompi_data
 int mca_coll_rocm_exscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
                          struct ompi_op_t *op, struct ompi_communicator_t *comm,
                          mca_coll_base_module_t *module);
+int mca_coll_rocm_reduce_scatter(const void *sbuf, void *rbuf, const int *rcounts,
+                                 struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                 struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
 int mca_coll_rocm_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount,
                                        struct ompi_datatype_t *dtype, struct ompi_op_t *op,
                                        struct ompi_communicator_t *comm,

@@ -3,8 +3,8 @@
  *
  * Selection: comm_query accepts node-local intra-communicators of at most
  * OMPI_AMD_MAX_RANKS ranks when a HIP device is visible; enable saves the
- * previously selected allreduce / reduce / reduce_scatter_block / scan /
- * exscan / allgather / bcast (coll/tuned, coll/basic for scan and exscan;
+ * previously selected allreduce / reduce / reduce_scatter /
+ * reduce_scatter_block / scan / exscan / allgather / bcast (coll/tuned, coll/basic for scan and exscan;
  * coll_base_comm_select.c:158-232 enables in ascending priority) and creates
  * the libompi_amd communicator.
  *
@@ -99,6 +99,8 @@ static void rocm_module_destruct(mca_coll_rocm_module_t *m)
 {
     if (NULL != m->c_coll.coll_allreduce_module) OBJ_RELEASE(m->c_coll.coll_allreduce_module);
     if (NULL != m->c_coll.coll_reduce_module) OBJ_RELEASE(m->c_coll.coll_reduce_module);
+    if (NULL != m->c_coll.coll_reduce_scatter_module)
+        OBJ_RELEASE(m->c_coll.coll_reduce_scatter_module);
     if (NULL != m->c_coll.coll_scan_module) OBJ_RELEASE(m->c_coll.coll_scan_module);
     if (NULL != m->c_coll.coll_exscan_module) OBJ_RELEASE(m->c_coll.coll_exscan_module);
     if (NULL != m->c_coll.coll_reduce_scatter_block_module)
@@ -131,6 +133,7 @@ mca_coll_base_module_t *mca_coll_rocm_comm_query(struct ompi_communicator_t *com
     m->super.coll_module_enable = mca_coll_rocm_module_enable;
     m->super.coll_allreduce = mca_coll_rocm_allreduce;
     m->super.coll_reduce = mca_coll_rocm_reduce;
+    m->super.coll_reduce_scatter = mca_coll_rocm_reduce_scatter;
     m->super.coll_scan = mca_coll_rocm_scan;
     m->super.coll_exscan = mca_coll_rocm_exscan;
     m->super.coll_reduce_scatter_block = mca_coll_rocm_reduce_scatter_block;
@@ -154,6 +157,7 @@ int mca_coll_rocm_module_enable(mca_coll_base_module_t *module, struct ompi_comm
     } while (0)
     SAVE(allreduce);
     SAVE(reduce);
+    SAVE(reduce_scatter);
     SAVE(scan);
     SAVE(exscan);
     SAVE(reduce_scatter_block);
@@ -283,6 +287,28 @@ int mca_coll_rocm_exscan(const void *sbuf, void *rbuf, int count, struct ompi_da
                          mca_coll_base_module_t *module)
 {
     return rocm_scan_common(sbuf, rbuf, count, dtype, op, comm, (mca_coll_rocm_module_t *) module, 1);
+}
+
+int mca_coll_rocm_reduce_scatter(const void *sbuf, void *rbuf, const int *rcounts,
+                                 struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                 struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const int t = type_code(dtype);
+    const int n = ompi_comm_size(comm);
+    const int ok = t >= 0 && ompi_op_is_intrinsic(op) &&
+                   ompi_amd_op_supported(op->o_f_to_c_index, t) && dev(sbuf) && dev(rbuf);
+    size_t counts[OMPI_AMD_MAX_RANKS];
+    int rc, i;
+    if (!take_device_path(m, ok)) {
+        return m->c_coll.coll_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm,
+                                             m->c_coll.coll_reduce_scatter_module);
+    }
+    for (i = 0; i < n; ++i) counts[i] = (size_t) rcounts[i];
+    rc = ompi_amd_reduce_scatter(m->dev_comm, MPI_IN_PLACE == sbuf ? rbuf : sbuf, rbuf, counts, t,
+                                 op->o_f_to_c_index, NULL);
+    if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_comm_sync(m->dev_comm, NULL);
+    return to_ompi_err(rc);
 }
 
 int mca_coll_rocm_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount,

@@ -238,3 +238,157 @@ int orc_scan(int exclusive, int n, const void *const *sb, void *const *rb, size_
     free(cur);
     return 0;
 }
+
+/* ---------------- reduce_scatter (vector counts) ----------------
+ *   decision            coll_tuned_decision_fixed.c:466-512
+ *   recursive halving   coll_base_reduce_scatter.c:132-391
+ *   ring                coll_base_reduce_scatter.c:456-623 */
+int orc_reduce_scatter_decision(int n, size_t total_bytes)
+{
+    int pow2 = 1;
+    while (pow2 < n) pow2 <<= 1;                      /* next_poweroftwo_inclusive */
+    if (total_bytes <= 12 * 1024 || (total_bytes <= 256 * 1024 && pow2 == n) ||
+        (double)n >= 0.0012 * (double)total_bytes + 8.0)
+        return ORC_RS_HALVING;
+    return ORC_RS_RING;
+}
+
+static void rs_halving(int n, const void *const *sb, void *const *rb, const size_t *rcounts,
+                       int op, int type)
+{
+    const size_t ext = orc_type_extent(type);
+    size_t *disps = calloc((size_t)n, sizeof(size_t)), count;
+    char **res = calloc((size_t)n, sizeof(char *)), **msg = calloc((size_t)n, sizeof(char *));
+    int *trank = calloc((size_t)n, sizeof(int));
+    int r, i, tmp_size = 1, remain, mask;
+    for (r = 1; r < n; r++) disps[r] = disps[r - 1] + rcounts[r - 1];
+    count = disps[n - 1] + rcounts[n - 1];
+    for (r = 0; r < n; r++) {
+        res[r] = malloc(count * ext + 1);
+        msg[r] = malloc(count * ext + 1);
+        memcpy(res[r], sb[r], count * ext);            /* result_buf <- sbuf (:190) */
+    }
+    while (tmp_size <= n) tmp_size <<= 1;              /* opal_next_poweroftwo(size) >> 1 */
+    tmp_size >>= 1;
+    remain = n - tmp_size;
+    /* non-pof2 fold (:203-228): odd r < 2*remain: res = res (op) even's res */
+    for (r = 0; r < n; r++) {
+        if (r < 2 * remain) {
+            if ((r & 1) == 0) trank[r] = -1;
+            else {
+                orc_op_2buff(op, type, res[r - 1], res[r], count);
+                trank[r] = r / 2;
+            }
+        } else {
+            trank[r] = r - remain;
+        }
+    }
+    {
+        size_t *trc = calloc((size_t)tmp_size, sizeof(size_t));
+        size_t *tds = calloc((size_t)tmp_size, sizeof(size_t));
+        int *sidx = calloc((size_t)n, sizeof(int)), *ridx = calloc((size_t)n, sizeof(int));
+        int *lidx = calloc((size_t)n, sizeof(int));
+        for (i = 0; i < tmp_size; i++)
+            trc[i] = (i < remain) ? rcounts[i * 2 + 1] + rcounts[i * 2] : rcounts[i + remain];
+        for (i = 0; i + 1 < tmp_size; i++) tds[i + 1] = tds[i] + trc[i];
+        for (r = 0; r < n; r++) { sidx[r] = ridx[r] = 0; lidx[r] = tmp_size; }
+        for (mask = tmp_size >> 1; mask > 0; mask >>= 1) {
+            /* every participant sends the half it gives away (:276-323) */
+            int *snd = calloc((size_t)n, sizeof(int)), *rcv = calloc((size_t)n, sizeof(int));
+            for (r = 0; r < n; r++) {
+                int tp;
+                if (trank[r] < 0) continue;
+                tp = trank[r] ^ mask;
+                if (trank[r] < tp) { snd[r] = ridx[r] + mask; rcv[r] = ridx[r]; }
+                else { rcv[r] = sidx[r] + mask; snd[r] = sidx[r]; }
+                memcpy(msg[r], res[r], count * ext);   /* snapshot = what r sends */
+            }
+            for (r = 0; r < n; r++) {
+                int tp, peer, hi_end;
+                size_t rc = 0;
+                if (trank[r] < 0) continue;
+                tp = trank[r] ^ mask;
+                peer = (tp < remain) ? tp * 2 + 1 : tp + remain;
+                hi_end = (trank[r] < tp) ? snd[r] : lidx[r];
+                for (i = rcv[r]; i < hi_end; i++) rc += trc[i];
+                if (rc > 0)   /* :335-338: res[recv] = res[recv] (op) peer's */
+                    orc_op_2buff(op, type, msg[peer] + tds[rcv[r]] * ext, res[r] + tds[rcv[r]] * ext, rc);
+            }
+            for (r = 0; r < n; r++) {                  /* :342-344 */
+                if (trank[r] < 0) continue;
+                sidx[r] = rcv[r];
+                ridx[r] = rcv[r];
+                lidx[r] = rcv[r] + mask;
+            }
+            free(snd);
+            free(rcv);
+        }
+        free(trc); free(tds); free(sidx); free(ridx); free(lidx);
+    }
+    /* results: participants copy their block (:348-357); odd ranks below
+     * 2*remain also hand the even neighbour its block (:365-383) */
+    for (r = 0; r < n; r++) {
+        if (trank[r] < 0) continue;
+        memcpy(rb[r], res[r] + disps[r] * ext, rcounts[r] * ext);
+        if (r < 2 * remain) memcpy(rb[r - 1], res[r] + disps[r - 1] * ext, rcounts[r - 1] * ext);
+    }
+    for (r = 0; r < n; r++) { free(res[r]); free(msg[r]); }
+    free(res); free(msg); free(disps); free(trank);
+}
+
+static void rs_ring(int n, const void *const *sb, void *const *rb, const size_t *rcounts, int op,
+                    int type)
+{
+    const size_t ext = orc_type_extent(type);
+    size_t *disps = calloc((size_t)n, sizeof(size_t)), total, maxb = 0;
+    char **acc = calloc((size_t)n, sizeof(char *)), **msg = calloc((size_t)n, sizeof(char *));
+    char **nmsg = calloc((size_t)n, sizeof(char *));
+    int r, k;
+    for (r = 1; r < n; r++) disps[r] = disps[r - 1] + rcounts[r - 1];
+    total = disps[n - 1] + rcounts[n - 1];
+    for (r = 0; r < n; r++) if (rcounts[r] > maxb) maxb = rcounts[r];
+    for (r = 0; r < n; r++) {
+        acc[r] = malloc(total * ext + 1);
+        msg[r] = malloc(maxb * ext + 1);
+        nmsg[r] = malloc(maxb * ext + 1);
+        memcpy(acc[r], sb[r], total * ext);           /* accumbuf <- sbuf (:530) */
+    }
+    for (r = 0; r < n; r++) {                          /* first send: block r-1 (:560) */
+        int b = (r + n - 1) % n;
+        memcpy(msg[r], acc[r] + disps[b] * ext, rcounts[b] * ext);
+    }
+    for (k = 2; k < n; k++) {                          /* :566-592 */
+        for (r = 0; r < n; r++) {
+            int from = (r + n - 1) % n, pb = (r + n - k) % n;
+            orc_op_2buff(op, type, msg[from], acc[r] + disps[pb] * ext, rcounts[pb]);
+            memcpy(nmsg[r], acc[r] + disps[pb] * ext, rcounts[pb] * ext);
+        }
+        for (r = 0; r < n; r++) { char *t = msg[r]; msg[r] = nmsg[r]; nmsg[r] = t; }
+    }
+    for (r = 0; r < n; r++) {                          /* my block (:598-605) */
+        int from = (r + n - 1) % n;
+        orc_op_2buff(op, type, msg[from], acc[r] + disps[r] * ext, rcounts[r]);
+        memcpy(rb[r], acc[r] + disps[r] * ext, rcounts[r] * ext);
+    }
+    for (r = 0; r < n; r++) { free(acc[r]); free(msg[r]); free(nmsg[r]); }
+    free(acc); free(msg); free(nmsg); free(disps);
+}
+
+int orc_reduce_scatter(int algorithm, int n, const void *const *sb, void *const *rb,
+                       const size_t *rcounts, int op, int type)
+{
+    size_t total = 0;
+    int r;
+    if (n < 1 || orc_type_extent(type) == 0 || !orc_op_defined(op, type)) return -1;
+    for (r = 0; r < n; r++) total += rcounts[r];
+    if (total == 0) return algorithm;
+    if (n == 1) {
+        memmove(rb[0], sb[0], rcounts[0] * orc_type_extent(type));
+        return algorithm;
+    }
+    if (algorithm == ORC_RS_TUNED) algorithm = orc_reduce_scatter_decision(n, total * type_size(type));
+    if (algorithm == ORC_RS_HALVING) rs_halving(n, sb, rb, rcounts, op, type);
+    else if (algorithm == ORC_RS_RING) rs_ring(n, sb, rb, rcounts, op, type);
+    else return -2;
+    return algorithm;
+}

@@ -98,6 +98,13 @@ int orc_reduce(int algorithm, int nranks, const void *const *sbufs, void *rbuf_r
  * algorithm run. */
 int orc_reduce_scatter_block(int nranks, const void *const *sbufs,
                              void *const *rbufs, size_t rcount, int op, int type);
+/* reduce_scatter with per-rank counts (coll_tuned_decision_fixed.c:466-512,
+ * coll_base_reduce_scatter.c:132-623).  rbufs[r] receives rcounts[r]
+ * elements.  Returns the algorithm run. */
+enum { ORC_RS_TUNED = 0, ORC_RS_HALVING = 1, ORC_RS_RING = 2 };
+int orc_reduce_scatter_decision(int nranks, size_t total_bytes);
+int orc_reduce_scatter(int algorithm, int nranks, const void *const *sbufs,
+                       void *const *rbufs, const size_t *rcounts, int op, int type);
 /* linear scan (exclusive = 0) / exscan (exclusive = 1); exscan leaves
  * rbufs[0] untouched. */
 int orc_scan(int exclusive, int nranks, const void *const *sbufs, void *const *rbufs,

@@ -49,6 +49,10 @@ def lib():
         L.orc_reduce_decision.argtypes = [c.c_int, c.c_size_t, c.c_size_t]
         L.orc_reduce.argtypes = [c.c_int, c.c_int, c.POINTER(c.c_void_p), c.c_void_p,
                                  c.c_size_t, c.c_int, c.c_int, c.c_int, c.c_int]
+        L.orc_reduce_scatter_decision.argtypes = [c.c_int, c.c_size_t]
+        L.orc_reduce_scatter.argtypes = [c.c_int, c.c_int, c.POINTER(c.c_void_p),
+                                         c.POINTER(c.c_void_p), c.POINTER(c.c_size_t), c.c_int,
+                                         c.c_int]
         L.orc_scan.argtypes = [c.c_int, c.c_int, c.POINTER(c.c_void_p), c.POINTER(c.c_void_p),
                                c.c_size_t, c.c_int, c.c_int]
         L.orc_allgather.argtypes =[c.c_int, c.POINTER(c.c_void_p), c.POINTER(c.c_void_p),
@@ -131,6 +135,29 @@ def reduce(sbufs: list[np.ndarray], count: int, op: int, type_code: int, root: i
     if alg < 0:
         raise ValueError(f"oracle reduce failed ({alg})")
     return out, alg
+
+
+RS_TUNED, RS_HALVING, RS_RING = 0, 1, 2
+
+
+def reduce_scatter_decision(n: int, total_bytes: int) -> int:
+    return lib().orc_reduce_scatter_decision(n, total_bytes)
+
+
+def reduce_scatter(sbufs: list[np.ndarray], rcounts: list[int], op: int, type_code: int,
+                   algorithm: int = RS_TUNED) -> tuple[list[np.ndarray], int]:
+    """coll/tuned reduce_scatter: (per-rank results, algorithm run)."""
+    n = len(sbufs)
+    rbufs = [np.zeros(max(1, rc), dtype=sbufs[0].dtype)[:rc] for rc in rcounts]
+    rbufs = [np.ascontiguousarray(r) if r.size else np.zeros(1, dtype=sbufs[0].dtype)
+             for r in rbufs]
+    sp = (ctypes.c_void_p * n)(*[_p(s) for s in sbufs])
+    rp = (ctypes.c_void_p * n)(*[_p(r) for r in rbufs])
+    rc = (ctypes.c_size_t * n)(*rcounts)
+    alg = lib().orc_reduce_scatter(algorithm, n, sp, rp, rc, op, type_code)
+    if alg < 0:
+        raise ValueError(f"oracle reduce_scatter failed ({alg})")
+    return [r[:c] for r, c in zip(rbufs, rcounts)], alg
 
 
 def scan(sbufs: list[np.ndarray], count: int, op: int, type_code: int,

@@ -145,6 +145,36 @@ def case_scan(comm, rank, n, dt, op, count, salt, exclusive=False, inplace=False
     return fields_equal(got, exp[rank].view(dt.np_dtype)), ""
 
 
+def case_rs(comm, rank, n, dt, op, rcounts, salt, inplace=False, kind="R"):
+    total = sum(rcounts)
+    xs = [inputs(dt, total, r, salt, kind) for r in range(n)]
+    exp, _ = orc.reduce_scatter([x.copy() for x in xs], rcounts, op.index, dt.code)
+    s = to_dev(xs[rank], extra=16)
+    if inplace:
+        comm.reduce_scatter(coll.IN_PLACE, s, rcounts, dt, op, blocking=True)
+        out = s
+    else:
+        out = torch.zeros((rcounts[rank] + 1) * dt.extent, dtype=torch.uint8, device="cuda")
+        comm.reduce_scatter(s, out, rcounts, dt, op, blocking=True)
+    got = out.cpu().numpy()[:rcounts[rank] * dt.extent].view(dt.np_dtype)
+    return fields_equal(got, exp[rank].view(dt.np_dtype)), ""
+
+
+def case_regrow(comm, rank, n, salt):
+    """Landing-buffer growth several times in a row (large scans of rising
+    size, an in-place reduce_scatter in between), every result checked."""
+    F = mop.MPI_FLOAT
+    for i, count in enumerate((300001, 1100003, 2500007, 9000011)):
+        ok, msg = case_scan(comm, rank, n, F, mop.MPI_SUM, count, salt + i)
+        if not ok:
+            return False, f"scan {count}: {msg}"
+        ok, msg = case_rs(comm, rank, n, F, mop.MPI_SUM, [count // n + r for r in range(n)],
+                          salt + 10 + i, inplace=True)
+        if not ok:
+            return False, f"rs {count}: {msg}"
+    return True, ""
+
+
 def case_allgather(comm, rank, n, nbytes, salt, inplace=False):
     xs = [np.random.default_rng(SEED + salt + r).integers(0, 256, nbytes, dtype=np.uint8)
           for r in range(n)]
@@ -293,6 +323,21 @@ def main():
         ("rsb_sum_f32_small", lambda: case_rsb(comm, rank, n, F, mop.MPI_SUM, 300, 48)),
         ("rsb_max_f32_mid_specials",
          lambda: case_rsb_kind(comm, rank, n, F, mop.MPI_MAX, 1000, 49, "S")),
+        # reduce_scatter: recursive halving (small / pof2 <= 256 KiB) and ring,
+        # uneven counts with an empty block, staged and zero-copy, in place
+        ("rs_sum_f32_small", lambda: case_rs(comm, rank, n, F, mop.MPI_SUM,
+                                             [300 + 7 * r if r != 1 else 0 for r in range(n)], 56)),
+        ("rs_sum_f32_mid", lambda: case_rs(comm, rank, n, F, mop.MPI_SUM,
+                                           [9000 + 13 * r for r in range(n)], 57)),
+        ("rs_max_f32_specials", lambda: case_rs(comm, rank, n, F, mop.MPI_MAX,
+                                                [5000 + r for r in range(n)], 58, kind="S")),
+        ("rs_sum_f32_big", lambda: case_rs(comm, rank, n, F, mop.MPI_SUM,
+                                           [big // n + 11 * r for r in range(n)], 59)),
+        ("rs_sum_f64_big_inplace", lambda: case_rs(comm, rank, n, D, mop.MPI_SUM,
+                                                   [big // (2 * n) + r for r in range(n)], 70,
+                                                   inplace=True)),
+        ("rsb_sum_f32_big_inplace",
+         lambda: case_rsb(comm, rank, n, F, mop.MPI_SUM, big // 4 + 3, 71, True)),
         # scan / exscan: staged and landing paths, in place
         ("scan_sum_f32_small", lambda: case_scan(comm, rank, n, F, mop.MPI_SUM, 5000, 50)),
         ("scan_sum_f32_big", lambda: case_scan(comm, rank, n, F, mop.MPI_SUM, big + 1, 51)),
@@ -300,6 +345,7 @@ def main():
          lambda: case_scan(comm, rank, n, F, mop.MPI_SUM, big, 52, inplace=True)),
         ("exscan_sum_f64_small", lambda: case_scan(comm, rank, n, D, mop.MPI_SUM, 999, 53, True)),
         ("exscan_max_i32_big", lambda: case_scan(comm, rank, n, I32, mop.MPI_MAX, big, 54, True)),
+        ("landing_regrow", lambda: case_regrow(comm, rank, n, 90)),
         ("exscan_prod_i8_inplace",
          lambda: case_scan(comm, rank, n, I8, mop.MPI_PROD, 70001, 55, True, True)),
     ]

@@ -58,6 +58,9 @@ static int t_allreduce(const void *s, void *r, int c, struct ompi_datatype_t *d,
 static int t_reduce(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
                     int root, struct ompi_communicator_t *cm, mca_coll_base_module_t *m)
 { tuned_calls++; return OMPI_SUCCESS; }
+static int t_rs(const void *s, void *r, const int *c, struct ompi_datatype_t *d,
+                struct ompi_op_t *o, struct ompi_communicator_t *cm, mca_coll_base_module_t *m)
+{ tuned_calls++; return OMPI_SUCCESS; }
 static int t_rsb(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
                  struct ompi_communicator_t *cm, mca_coll_base_module_t *m)
 { tuned_calls++; return OMPI_SUCCESS; }
@@ -77,6 +80,7 @@ static void fill_tuned(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *tm)
 #define SET(fn, f) do { t->coll_##fn = f; t->coll_##fn##_module = tm; OBJ_RETAIN(tm); } while (0)
     SET(allreduce, t_allreduce);
     SET(reduce, t_reduce);
+    SET(reduce_scatter, t_rs);
     SET(reduce_scatter_block, t_rsb);
     SET(scan, t_scan);
     SET(exscan, t_scan);
@@ -90,7 +94,8 @@ static void install(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *m)
 {
 #define INST(fn) if (m->coll_##fn) { OBJ_RELEASE(t->coll_##fn##_module); t->coll_##fn = m->coll_##fn; \
                                       t->coll_##fn##_module = m; OBJ_RETAIN(m); }
-    INST(allreduce) INST(reduce) INST(reduce_scatter_block) INST(scan) INST(exscan)
+    INST(allreduce) INST(reduce) INST(reduce_scatter) INST(reduce_scatter_block) INST(scan)
+    INST(exscan)
     INST(allgather) INST(bcast)
 #undef INST
 }
@@ -99,6 +104,7 @@ static void release_table(mca_coll_base_comm_coll_t *t)
 {
     OBJ_RELEASE(t->coll_allreduce_module);
     OBJ_RELEASE(t->coll_reduce_module);
+    OBJ_RELEASE(t->coll_reduce_scatter_module);
     OBJ_RELEASE(t->coll_reduce_scatter_block_module);
     OBJ_RELEASE(t->coll_scan_module);
     OBJ_RELEASE(t->coll_exscan_module);
@@ -174,7 +180,8 @@ int main(int argc, char **argv)
               (ompi_amd_device_count() > 0), "init_query vs device presence");
     m = mca_coll_rocm_component.super.collm_comm_query(&comm, &prio);
     CHECK(m != NULL && prio == 80, "comm_query on a local intra-communicator");
-    CHECK(m->coll_allreduce && m->coll_reduce && m->coll_reduce_scatter_block && m->coll_scan &&
+    CHECK(m->coll_allreduce && m->coll_reduce && m->coll_reduce_scatter &&
+              m->coll_reduce_scatter_block && m->coll_scan &&
               m->coll_exscan && m->coll_allgather && m->coll_bcast && m->coll_module_enable,
           "module function table");
     {
@@ -199,7 +206,7 @@ int main(int argc, char **argv)
     }
 
     CHECK(m->coll_module_enable(m, &comm) == OMPI_SUCCESS, "enable");
-    CHECK(tm->super.obj_reference_count == 1 + 7 + 7, "enable retains the saved modules (%d)",
+    CHECK(tm->super.obj_reference_count == 1 + 8 + 8, "enable retains the saved modules (%d)",
           tm->super.obj_reference_count);
     install(&table, m);
 
@@ -298,6 +305,33 @@ int main(int argc, char **argv)
                                               table.coll_reduce_scatter_block_module) ==
                   OMPI_SUCCESS, "rsb");
         expect_dev(dr, rb[g_rank], rc * 4, "reduce_scatter_block");
+        harness_dev_free(ds);
+        harness_dev_free(dr);
+        for (int r = 0; r < g_size; ++r) free(rb[r]);
+        free(rb);
+        free_inputs(xs);
+    }
+    /* 4b. reduce_scatter with uneven counts (one rank gets none) */
+    {
+        int rcounts[OMPI_AMD_MAX_RANKS];
+        size_t rcz[OMPI_AMD_MAX_RANKS], n = 0;
+        for (int r = 0; r < g_size; ++r) {
+            rcounts[r] = (r == 1) ? 0 : 700 + 37 * r;
+            rcz[r] = (size_t) rcounts[r];
+            n += rcz[r];
+        }
+        float **xs = all_inputs(n, 45);
+        float **rb = malloc(sizeof(float *) * (size_t) g_size);
+        void *ds, *dr;
+        for (int r = 0; r < g_size; ++r) rb[r] = calloc(rcz[r] + 1, sizeof(float));
+        CHECK(orc_reduce_scatter(ORC_RS_TUNED, g_size, (const void *const *) xs, (void *const *) rb,
+                                 rcz, ORC_OP_SUM, ORC_T_FLOAT) >= 0, "oracle reduce_scatter");
+        ds = dev_of(xs[g_rank], n * 4);
+        dr = dev_of(rb[g_rank], (rcz[g_rank] + 1) * 4);
+        CHECK(table.coll_reduce_scatter(ds, dr, rcounts, &dfloat, &sum, &comm,
+                                        table.coll_reduce_scatter_module) == OMPI_SUCCESS,
+              "reduce_scatter");
+        expect_dev(dr, rb[g_rank], rcz[g_rank] * 4, "reduce_scatter");
         harness_dev_free(ds);
         harness_dev_free(dr);
         for (int r = 0; r < g_size; ++r) free(rb[r]);

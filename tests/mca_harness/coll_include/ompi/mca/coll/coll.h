@@ -24,6 +24,10 @@ typedef int (*mca_coll_base_module_exscan_fn_t)(const void *, void *, int, struc
 typedef int (*mca_coll_base_module_reduce_fn_t)(const void *, void *, int, struct ompi_datatype_t *,
                                                 struct ompi_op_t *, int, struct ompi_communicator_t *,
                                                 HMOD);
+typedef int (*mca_coll_base_module_reduce_scatter_fn_t)(const void *, void *, const int *,
+                                                        struct ompi_datatype_t *,
+                                                        struct ompi_op_t *,
+                                                        struct ompi_communicator_t *, HMOD);
 typedef int (*mca_coll_base_module_reduce_scatter_block_fn_t)(const void *, void *, int,
                                                               struct ompi_datatype_t *,
                                                               struct ompi_op_t *,
@@ -40,6 +44,7 @@ typedef struct mca_coll_base_module_2_3_0_t {
     mca_coll_base_module_bcast_fn_t coll_bcast;
     mca_coll_base_module_exscan_fn_t coll_exscan;
     mca_coll_base_module_reduce_fn_t coll_reduce;
+    mca_coll_base_module_reduce_scatter_fn_t coll_reduce_scatter;
     mca_coll_base_module_reduce_scatter_block_fn_t coll_reduce_scatter_block;
     mca_coll_base_module_scan_fn_t coll_scan;
     void *base_data;
@@ -58,7 +63,8 @@ typedef struct mca_coll_base_component_2_0_0_t {
 /* per-communicator function table (coll.h:608-666 shape) */
 #define HFN(name) mca_coll_base_module_##name##_fn_t coll_##name; mca_coll_base_module_t *coll_##name##_module;
 typedef struct mca_coll_base_comm_coll_t {
-    HFN(allgather) HFN(allreduce) HFN(bcast) HFN(exscan) HFN(reduce) HFN(reduce_scatter_block)
+    HFN(allgather) HFN(allreduce) HFN(bcast) HFN(exscan) HFN(reduce) HFN(reduce_scatter)
+    HFN(reduce_scatter_block)
     HFN(scan)
 } mca_coll_base_comm_coll_t;
 #undef HFN

@@ -163,3 +163,61 @@ def test_scan_linear_order(orc, exclusive):
         nxt = f(orc, SUM, xs[r], acc)          # P_r = f(out = x_r, in = P_(r-1))
         assert np.array_equal(res[r], acc if exclusive else nxt), r
         acc = nxt
+
+
+def halving_fold(orc, op, v, tb):
+    """Python twin of coll_ipc.hip fold() ORDER_HALVING (recursive halving
+    reduce_scatter, coll_base_reduce_scatter.c:132-391) for tmp rank tb."""
+    n = len(v)
+    adj = 1
+    while adj * 2 <= n:
+        adj *= 2
+    remain = n - adj
+    w = [f(orc, op, v[2 * u + 1], v[2 * u]) if u < remain else v[u + remain] for u in range(adj)]
+    m = adj // 2
+    while m >= 1:
+        for u in range(adj):
+            if (u & m) == (tb & m):
+                w[u] = f(orc, op, w[u], w[u ^ m])
+        m //= 2
+    return w[tb]
+
+
+@pytest.mark.parametrize("n", list(range(2, 17)))
+def test_reduce_scatter_closed_forms(orc, n):
+    """Ring (block b folded from x[b+1] around to x[b]) and recursive-halving
+    closed forms against the oracle's message-flow simulations, uneven and
+    zero counts included."""
+    rng = np.random.default_rng(n)
+    rcounts = [int(c) for c in rng.integers(0, 40, n)]
+    rcounts[n // 2] = 0
+    total = sum(rcounts)
+    for op, specials in ((SUM, False), (MAX, True)):
+        xs = _inputs(n, total, 300 + n, specials)
+        disps = np.concatenate([[0], np.cumsum(rcounts)[:-1]]).astype(int)
+        adj = 1
+        while adj * 2 <= n:
+            adj *= 2
+        remain = n - adj
+        for alg in (1, 2):
+            res, ran = orc.reduce_scatter(xs, rcounts, op, F32, algorithm=alg)
+            assert ran == alg
+            for b in range(n):
+                if rcounts[b] == 0:
+                    continue
+                sl = [x[disps[b]:disps[b] + rcounts[b]].copy() for x in xs]
+                if alg == 2:   # ring: v[j] = x[(b + 1 + j) % n], acc = f(v[j], acc)
+                    acc = sl[(b + 1) % n]
+                    for j in range(1, n):
+                        acc = f(orc, op, sl[(b + 1 + j) % n], acc)
+                else:
+                    tb = b // 2 if b < 2 * remain else b - remain
+                    acc = halving_fold(orc, op, sl, tb)
+                assert _bits_equal(res[b], acc), (n, alg, b, op)
+
+
+def test_reduce_scatter_decision(orc):
+    d = orc.reduce_scatter_decision
+    assert d(8, 12 * 1024) == 1 and d(3, 12 * 1024) == 1
+    assert d(8, 256 * 1024) == 1 and d(8, 256 * 1024 + 4) == 2
+    assert d(3, 12 * 1024 + 4) == 2 and d(4, 100000) == 1 and d(6, 100000) == 2
