@@ -41,6 +41,7 @@ extern "C" {
 #define OMPI_AMD_MAX_RANKS 16
 
 typedef struct ompi_amd_comm ompi_amd_comm_t;
+typedef struct ompi_amd_plan ompi_amd_plan_t;
 
 /* Collective over the `size` ranks of one node.  `name` identifies the
  * communicator node-wide and must be unique per job (e.g. "<jobid>.<cid>");
@@ -113,6 +114,18 @@ int ompi_amd_coll_reduce_order(int size, size_t msg_bytes, size_t count, int roo
  * with matching arguments, in the same order. */
 int ompi_amd_allreduce(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
                        size_t count, int type, int op, void *stream);
+/* Persistent allreduce (MPI_Allreduce_init, coll.h:349-352; libnbc's
+ * ompi_coll_libnbc_allreduce_init in the reference).  Collective and
+ * blocking: fixes sbuf/rbuf/count/type/op, picks the path, swaps and pins
+ * the peers' buffer mappings (and sizes the landing buffer for the push
+ * scheme).  ompi_amd_plan_start enqueues one allreduce on `stream` with no
+ * host rendezvous — a truly nonblocking start; every rank must start its
+ * plans in the same order relative to its other collectives.
+ * ompi_amd_plan_free is local; free plans before the communicator. */
+int ompi_amd_allreduce_init(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
+                            size_t count, int type, int op, ompi_amd_plan_t **plan);
+int ompi_amd_plan_start(ompi_amd_plan_t *plan, void *stream);
+int ompi_amd_plan_free(ompi_amd_plan_t *plan);
 /* MPI_Reduce to `root` (coll.h:239-241).  rbuf matters at the root only;
  * the root may pass sbuf = MPI_IN_PLACE.  Every rank folds one block of the
  * vector from every rank's sbuf and stores it into the root's rbuf. */

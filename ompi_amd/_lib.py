@@ -111,6 +111,11 @@ PROTOTYPES = [
       _C.POINTER(_C.c_int)]),
     ("ompi_amd_allreduce", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p]),
+    ("ompi_amd_allreduce_init", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int,
+      _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_plan_start", _C.c_int, [_C.c_void_p, _C.c_void_p]),
+    ("ompi_amd_plan_free", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_reduce", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_int,
       _C.c_void_p]),

@@ -4,6 +4,7 @@ Mirrors the coll framework's entry points this path provides
 (ompi/mca/coll/coll.h:200-250):
 
     coll_allreduce(sbuf, rbuf, count, dtype, op, comm, module)
+    coll_allreduce_init(sbuf, rbuf, count, dtype, op, comm, info, request, module)
     coll_reduce(sbuf, rbuf, count, dtype, op, root, comm, module)
     coll_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, module)
     coll_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, module)
@@ -113,6 +114,15 @@ class Communicator:
                                           op.index, _stream(stream))
         self._finish(rc, f"allreduce({op.name},{datatype.name})", blocking, stream)
 
+    def allreduce_init(self, sbuf, rbuf, count: int, datatype: Datatype, op: Op) -> "Plan":
+        """MPI_Allreduce_init: a persistent allreduce (collective); start()
+        enqueues it without any host rendezvous."""
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.ompi_amd_allreduce_init(self._h, _ptr(sbuf), _ptr(rbuf), count,
+                                                     datatype.code, op.index, ctypes.byref(h)),
+                   f"allreduce_init({op.name},{datatype.name})")
+        return Plan(self, h, f"allreduce({op.name},{datatype.name})")
+
     def reduce(self, sbuf, rbuf, count: int, datatype: Datatype, op: Op, root: int,
                stream=None, blocking: bool = False) -> None:
         """MPI_Reduce; rbuf may be None off the root, sbuf IN_PLACE at the root."""
@@ -158,6 +168,22 @@ class Communicator:
     def __del__(self):
         # destroy is collective; only an explicit free() releases the comm
         pass
+
+
+class Plan:
+    """A persistent collective (ompi_amd_plan_t)."""
+
+    def __init__(self, comm: Communicator, handle, what: str):
+        self._comm, self._h, self._what = comm, handle, what
+
+    def start(self, stream=None, blocking: bool = False) -> None:
+        rc = self._comm._lib.ompi_amd_plan_start(self._h, _stream(stream))
+        self._comm._finish(rc, "start " + self._what, blocking, stream)
+
+    def free(self) -> None:
+        if self._h:
+            _lib.check(self._comm._lib.ompi_amd_plan_free(self._h), "plan_free")
+            self._h = None
 
 
 def block_partition(count: int, nranks: int, block: int) -> tuple[int, int]:

@@ -563,7 +563,7 @@ struct ompi_amd_comm {
     int algorithm = 0;
     // IPC caches
     struct exp_entry { void *base; size_t size; unsigned long long id; hipIpcMemHandle_t h; };
-    struct imp_entry { int peer; hipIpcMemHandle_t h; void *base; uint64_t last_use; };
+    struct imp_entry { int peer; hipIpcMemHandle_t h; void *base; uint64_t last_use; int pins; };
     std::vector<exp_entry> exports;
     std::vector<imp_entry> imports;
     uint64_t use_clock = 0;
@@ -572,6 +572,20 @@ struct ompi_amd_comm {
     int profile = 0;
     std::vector<hipEvent_t> ev_free;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_phase[2];
+};
+
+// A persistent allreduce (MPI_Allreduce_init, coll.h:349-352): buffers,
+// path and peer mappings fixed at init, so a start enqueues device work
+// only — no host rendezvous, no handle swap.
+struct ompi_amd_plan {
+    ompi_amd_comm_t *c = nullptr;
+    const void *src = nullptr;
+    void *rbuf = nullptr;
+    int64_t count = 0;
+    int op = 0, type = 0;
+    int kind = 0;      // 0: small paths (as a plain call), 1 pull, 2 pull+push, 3 push
+    ptr_set sp{}, rp{};
+    void *bases[OMPI_AMD_MAX_RANKS][2] = {};  // pinned peer mappings
 };
 
 namespace ompi_amd {
@@ -636,37 +650,53 @@ static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d) {
     return OMPI_AMD_SUCCESS;
 }
 
-static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const char **out) {
+// pin: the mapping is held by a persistent plan and never evicted until
+// the plan releases it (unpin_import with the returned *base).
+static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const char **out,
+                      bool pin = false, void **base_out = nullptr) {
     *out = nullptr;
+    if (base_out) *base_out = nullptr;
     if (!d.valid) return OMPI_AMD_SUCCESS;
     for (auto &x : c->imports) {
         if (x.peer == peer && memcmp(&x.h, &d.h, sizeof(d.h)) == 0) {
             x.last_use = ++c->use_clock;
+            x.pins += pin ? 1 : 0;
             *out = (const char *)x.base + d.off;
+            if (base_out) *base_out = x.base;
             return OMPI_AMD_SUCCESS;
         }
     }
-    if (c->imports.size() >= 256) {  // evict the least recently used mapping
-        auto it = std::min_element(c->imports.begin(), c->imports.end(),
-                                   [](const ompi_amd_comm::imp_entry &a,
-                                      const ompi_amd_comm::imp_entry &b) {
-                                       return a.last_use < b.last_use;
-                                   });
-        (void)hipIpcCloseMemHandle(it->base);
-        c->imports.erase(it);
+    if (c->imports.size() >= 256) {  // evict the least recently used unpinned mapping
+        auto it = c->imports.end();
+        for (auto jt = c->imports.begin(); jt != c->imports.end(); ++jt)
+            if (jt->pins == 0 && (it == c->imports.end() || jt->last_use < it->last_use)) it = jt;
+        if (it != c->imports.end()) {
+            (void)hipIpcCloseMemHandle(it->base);
+            c->imports.erase(it);
+        }
     }
     void *base = nullptr;
     hipError_t e = hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess);
     if (e != hipSuccess) return record_hip(e, "hipIpcOpenMemHandle");
-    c->imports.push_back({peer, d.h, base, ++c->use_clock});
+    c->imports.push_back({peer, d.h, base, ++c->use_clock, pin ? 1 : 0});
     *out = (const char *)base + d.off;
+    if (base_out) *base_out = base;
     return OMPI_AMD_SUCCESS;
+}
+
+static void unpin_import(ompi_amd_comm_t *c, void *base) {
+    for (auto &x : c->imports)
+        if (x.base == base && x.pins > 0) {
+            --x.pins;
+            return;
+        }
 }
 
 // Swap (sbuf, rbuf) descriptors with every peer and map theirs (either may
 // be NULL: nothing is exported for it).
 static int exchange_bufs(ompi_amd_comm_t *c, const void *sbuf, const void *rbuf, ptr_set *s,
-                         ptr_set *r, uint64_t myflags = 0, uint64_t *allflags = nullptr) {
+                         ptr_set *r, uint64_t myflags = 0, uint64_t *allflags = nullptr,
+                         bool pin = false, void *(*bases)[2] = nullptr) {
     call_blob mine{};
     mine.flags = myflags;
     int rc = export_buf(c, sbuf, &mine.s);
@@ -682,8 +712,13 @@ static int exchange_bufs(ompi_amd_comm_t *c, const void *sbuf, const void *rbuf,
             r->p[p] = (const char *)rbuf;
             continue;
         }
-        if ((rc = import_buf(c, p, all[p].s, &s->p[p])) != OMPI_AMD_SUCCESS) return rc;
-        if ((rc = import_buf(c, p, all[p].r, &r->p[p])) != OMPI_AMD_SUCCESS) return rc;
+        void *b0 = nullptr, *b1 = nullptr;
+        if ((rc = import_buf(c, p, all[p].s, &s->p[p], pin, &b0)) != OMPI_AMD_SUCCESS) return rc;
+        if ((rc = import_buf(c, p, all[p].r, &r->p[p], pin, &b1)) != OMPI_AMD_SUCCESS) return rc;
+        if (bases) {
+            bases[p][0] = b0;
+            bases[p][1] = b1;
+        }
     }
     return OMPI_AMD_SUCCESS;
 }
@@ -1007,13 +1042,12 @@ static int allreduce_staged_two_shot(ompi_amd_comm_t *c, const void *src, void *
     return launch_copy(c, cj, s);
 }
 
-static int allreduce_pull(ompi_amd_comm_t *c, const void *src, void *rbuf, int64_t count,
-                          int op, int type, bool inplace, hipStream_t s) {
+// sp / rp: every rank's input and rbuf as this rank maps them (sp = rp in
+// place); push needs rp only, and the landing buffer sized by push_slot.
+static int allreduce_pull(ompi_amd_comm_t *c, const ptr_set &sp, const ptr_set &rp, void *rbuf,
+                          int64_t count, int op, int type, hipStream_t s) {
     const int n = c->size, mine = (c->rank + 1) % n;
     const int64_t ext = (int64_t)ompi_amd_type_extent(type);
-    ptr_set sp{}, rp{};
-    TRY(exchange_bufs(c, src, rbuf, &sp, &rp));
-    if (inplace) sp = rp;
     TRY(launch_barrier(c, s));
     red_jobs jobs;
     ring_jobs(count, n, &jobs, mine);
@@ -1034,12 +1068,10 @@ static int allreduce_pull(ompi_amd_comm_t *c, const void *src, void *rbuf, int64
     return launch_barrier(c, s);
 }
 
-static int allreduce_pull_push(ompi_amd_comm_t *c, const void *src, void *rbuf, int64_t count,
-                               int op, int type, bool inplace, hipStream_t s) {
+static int allreduce_pull_push(ompi_amd_comm_t *c, const ptr_set &sp, const ptr_set &rp,
+                               int64_t count, int op, int type, hipStream_t s) {
+    // in place, sp = rp: only the owner of a block touches it
     const int n = c->size, mine = (c->rank + 1) % n;
-    ptr_set sp{}, rp{};
-    TRY(exchange_bufs(c, src, rbuf, &sp, &rp));
-    if (inplace) sp = rp;  // only the owner of a block touches it, in place or not
     TRY(launch_barrier(c, s));
     red_jobs jobs;
     ring_jobs(count, n, &jobs, mine);
@@ -1050,18 +1082,21 @@ static int allreduce_pull_push(ompi_amd_comm_t *c, const void *src, void *rbuf, 
     return launch_barrier(c, s);
 }
 
-static int allreduce_push(ompi_amd_comm_t *c, const void *src, void *rbuf, int64_t count,
+// slot r of the owner's landing buffer receives rank r's copy of the
+// owner's block, at the block's own phase mod 16 B
+static size_t push_slot(int64_t count, int n, int type) {
+    int64_t split, early, late;
+    blockcount(count, n, &split, &early, &late);
+    return ((size_t)(early * (int64_t)ompi_amd_type_extent(type)) + 16 + 255) & ~(size_t)255;
+}
+
+static int allreduce_push(ompi_amd_comm_t *c, const void *src, const ptr_set &rp, int64_t count,
                           int op, int type, hipStream_t s) {
     const int n = c->size, mine = (c->rank + 1) % n;
     const int64_t ext = (int64_t)ompi_amd_type_extent(type);
     int64_t split, early, late;
     blockcount(count, n, &split, &early, &late);
-    // slot r of the owner's landing buffer receives rank r's copy of the
-    // owner's block, at the block's own phase mod 16 B
-    const size_t slot = ((size_t)(early * ext) + 16 + 255) & ~(size_t)255;
-    TRY(ensure_landing(c, slot * (size_t)n));
-    ptr_set sp{}, rp{};
-    TRY(exchange_bufs(c, nullptr, rbuf, &sp, &rp));
+    const size_t slot = push_slot(count, n, type);
     cp_jobs cj{};
     for (int b = 0; b < n; ++b) {
         if (b == mine) continue;
@@ -1399,14 +1434,17 @@ int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
         return launch_reduce(c, op, type, sh.peers, n, one_ptr(rbuf), 1,
                              tree ? ORDER_TREE : ORDER_RING, 0, jobs, s);
     }
-    switch (c->algorithm) {
-    case ALG_PULL_PUSH:
-        return allreduce_pull_push(c, src, rbuf, (int64_t)count, op, type, inplace, s);
-    case ALG_PUSH:
-        return allreduce_push(c, src, rbuf, (int64_t)count, op, type, s);
-    default:
-        return allreduce_pull(c, src, rbuf, (int64_t)count, op, type, inplace, s);
+    ptr_set sp{}, rp{};
+    if (c->algorithm == ALG_PUSH) {
+        TRY(ensure_landing(c, push_slot((int64_t)count, n, type) * (size_t)n));
+        TRY(exchange_bufs(c, nullptr, rbuf, &sp, &rp));
+        return allreduce_push(c, src, rp, (int64_t)count, op, type, s);
     }
+    TRY(exchange_bufs(c, src, rbuf, &sp, &rp));
+    if (inplace) sp = rp;
+    if (c->algorithm == ALG_PULL_PUSH)
+        return allreduce_pull_push(c, sp, rp, (int64_t)count, op, type, s);
+    return allreduce_pull(c, sp, rp, rbuf, (int64_t)count, op, type, s);
 }
 
 int ompi_amd_reduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
@@ -1607,6 +1645,71 @@ int ompi_amd_bcast(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, void *
         TRY(launch_copy(c, cj, s));
     }
     return launch_barrier(c, s);
+}
+
+int ompi_amd_allreduce_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count,
+                            int type, int op, ompi_amd_plan_t **out) {
+    if (!c || !rbuf || !out) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
+    TRY(check_sticky(c));
+    TRY(set_dev(c));
+    auto *pl = new (std::nothrow) ompi_amd_plan;
+    if (!pl) return OMPI_AMD_ERR_BAD_PARAM;
+    const size_t bytes = count * ompi_amd_type_extent(type);
+    const bool inplace = in_place(sbuf, rbuf);
+    const int n = c->size;
+    pl->c = c;
+    pl->src = inplace ? rbuf : sbuf;
+    pl->rbuf = rbuf;
+    pl->count = (int64_t)count;
+    pl->op = op;
+    pl->type = type;
+    const bool tree = type_size(type) * count < 10000 || count < (size_t)n;
+    const bool small = n == 1 || count == 0 || (bytes <= c->fused_bytes && bytes <= c->scratch_bytes) ||
+                       bytes <= c->small_bytes || !c->zero_copy || tree;
+    int rc = OMPI_AMD_SUCCESS;
+    if (!small) {
+        pl->kind = c->algorithm == ALG_PUSH ? 3 : c->algorithm == ALG_PULL_PUSH ? 2 : 1;
+        if (pl->kind == 3) rc = ensure_landing(c, push_slot(pl->count, n, type) * (size_t)n);
+        if (rc == OMPI_AMD_SUCCESS)
+            rc = exchange_bufs(c, pl->kind == 3 ? nullptr : pl->src, rbuf, &pl->sp, &pl->rp, 0,
+                               nullptr, true, pl->bases);
+        if (inplace) pl->sp = pl->rp;
+    }
+    if (rc != OMPI_AMD_SUCCESS) {
+        (void)ompi_amd_plan_free(pl);
+        return rc;
+    }
+    *out = pl;
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_plan_start(ompi_amd_plan_t *pl, void *stream) {
+    if (!pl || !pl->c) return OMPI_AMD_ERR_BAD_PARAM;
+    ompi_amd_comm_t *c = pl->c;
+    if (pl->kind == 0)
+        return ompi_amd_allreduce(c, pl->src == pl->rbuf ? (const void *)1 : pl->src, pl->rbuf,
+                                  (size_t)pl->count, pl->type, pl->op, stream);
+    TRY(check_sticky(c));
+    TRY(set_dev(c));
+    hipStream_t s = as_stream(stream);
+    if (pl->kind == 3) {
+        // another call may have grown (and so moved) the landing buffer:
+        // its size only grows, so the slots still fit
+        return allreduce_push(c, pl->src, pl->rp, pl->count, pl->op, pl->type, s);
+    }
+    if (pl->kind == 2) return allreduce_pull_push(c, pl->sp, pl->rp, pl->count, pl->op, pl->type, s);
+    return allreduce_pull(c, pl->sp, pl->rp, pl->rbuf, pl->count, pl->op, pl->type, s);
+}
+
+int ompi_amd_plan_free(ompi_amd_plan_t *pl) {
+    if (!pl) return OMPI_AMD_SUCCESS;
+    if (pl->c)
+        for (int p = 0; p < OMPI_AMD_MAX_RANKS; ++p)
+            for (int k = 0; k < 2; ++k)
+                if (pl->bases[p][k]) unpin_import(pl->c, pl->bases[p][k]);
+    delete pl;
+    return OMPI_AMD_SUCCESS;
 }
 
 }  // extern "C"

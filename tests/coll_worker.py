@@ -175,6 +175,29 @@ def case_regrow(comm, rank, n, salt):
     return True, ""
 
 
+def case_persistent(comm, rank, n, dt, op, count, salt, inplace=False, starts=3):
+    """MPI_Allreduce_init + repeated starts, new data between starts (same
+    buffers), other collectives interleaved, no sync between them."""
+    s = torch.zeros(count * dt.extent, dtype=torch.uint8, device="cuda")
+    out = s if inplace else torch.zeros_like(s)
+    plan = comm.allreduce_init(coll.IN_PLACE if inplace else s, out, count, dt, op)
+    try:
+        for it in range(starts):
+            xs = [inputs(dt, count, r, salt + it) for r in range(n)]
+            exp, _ = orc.allreduce([x.copy() for x in xs], count, op.index, dt.code)
+            s.copy_(torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda())
+            plan.start()
+            other = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+            comm.bcast(other, 4096, it % n)  # an unrelated collective in between
+            torch.cuda.synchronize()
+            got = out.cpu().numpy()[:count * dt.extent].view(dt.np_dtype)
+            if not fields_equal(got, exp[rank]):
+                return False, f"start {it} mismatch"
+        return True, ""
+    finally:
+        plan.free()
+
+
 def case_allgather(comm, rank, n, nbytes, salt, inplace=False):
     xs = [np.random.default_rng(SEED + salt + r).integers(0, 256, nbytes, dtype=np.uint8)
           for r in range(n)]
@@ -349,6 +372,14 @@ def main():
         ("exscan_prod_i8_inplace",
          lambda: case_scan(comm, rank, n, I8, mop.MPI_PROD, 70001, 55, True, True)),
     ]
+    cases += [
+        ("persistent_small", lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, 3001, 80)),
+        ("persistent_mid_inplace",
+         lambda: case_persistent(comm, rank, n, D, mop.MPI_SUM, 70001, 81, inplace=True)),
+        ("persistent_big", lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, big + 3, 82)),
+        ("persistent_big_inplace",
+         lambda: case_persistent(comm, rank, n, F, mop.MPI_MAX, big, 83, inplace=True)),
+    ]
     # zero-copy allreduce under the two push schemes (param "algorithm")
     for alg in (1, 2):
         def with_alg(fn, a=alg):
@@ -373,6 +404,11 @@ def main():
             (f"alg{alg}_ar_max_f32_specials",
              with_alg(lambda: case_allreduce(comm, rank, n, F, mop.MPI_MAX, 300001, 65, "S"))),
             (f"alg{alg}_pipelined_nonblocking", with_alg(lambda: case_pipelined(comm, rank, n, 66))),
+            (f"alg{alg}_persistent_big",
+             with_alg(lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, big + 1, 84))),
+            (f"alg{alg}_persistent_big_inplace",
+             with_alg(lambda: case_persistent(comm, rank, n, D, mop.MPI_SUM, big // 2, 85,
+                                              inplace=True))),
         ]
     only = os.environ.get("COLL_CASES")
     ok_all = True
