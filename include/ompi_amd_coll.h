@@ -73,6 +73,11 @@ int ompi_amd_comm_size(const ompi_amd_comm_t *comm);
  *   "profile"       1: bracket the allreduce's reduce and gather kernels with
  *                   HIP events (read with ompi_amd_comm_phase_ms) */
 int ompi_amd_comm_set_param(ompi_amd_comm_t *comm, const char *key, int64_t value);
+/* Read a parameter above, or a state counter: "landing_bytes" (current
+ * landing-buffer capacity), "landing_alias_retries" (landing growths that
+ * found a peer mapping aliasing an older allocation and retried), "imports"
+ * (cached peer-buffer mappings). */
+int ompi_amd_comm_get_param(const ompi_amd_comm_t *comm, const char *key, int64_t *value);
 
 /* Sticky error of the device side (a barrier that timed out, ...).
  * 0 = none, else an OMPI_AMD_ERR_* code.  Reading it does not sync. */
@@ -125,6 +130,11 @@ int ompi_amd_allreduce(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
 int ompi_amd_allreduce_init(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
                             size_t count, int type, int op, ompi_amd_plan_t **plan);
 int ompi_amd_plan_start(ompi_amd_plan_t *plan, void *stream);
+/* Completion of the last start (the request's MPI_Test / MPI_Wait):
+ * *done = 1 once the device work finished (or nothing was started); a
+ * device-side failure (barrier timeout) is returned as its error code. */
+int ompi_amd_plan_test(ompi_amd_plan_t *plan, int *done);
+int ompi_amd_plan_wait(ompi_amd_plan_t *plan);
 int ompi_amd_plan_free(ompi_amd_plan_t *plan);
 /* MPI_Reduce to `root` (coll.h:239-241).  rbuf matters at the root only;
  * the root may pass sbuf = MPI_IN_PLACE.  Every rank folds one block of the

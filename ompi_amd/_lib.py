@@ -98,6 +98,7 @@ PROTOTYPES = [
     ("ompi_amd_comm_rank", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_comm_size", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_comm_set_param", _C.c_int, [_C.c_void_p, _C.c_char_p, _C.c_int64]),
+    ("ompi_amd_comm_get_param", _C.c_int, [_C.c_void_p, _C.c_char_p, _C.POINTER(_C.c_int64)]),
     ("ompi_amd_comm_error", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_comm_agree", _C.c_int, [_C.c_void_p, _C.c_int, _C.POINTER(_C.c_int)]),
     ("ompi_amd_comm_sync", _C.c_int, [_C.c_void_p, _C.c_void_p]),
@@ -115,6 +116,8 @@ PROTOTYPES = [
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int,
       _C.POINTER(_C.c_void_p)]),
     ("ompi_amd_plan_start", _C.c_int, [_C.c_void_p, _C.c_void_p]),
+    ("ompi_amd_plan_test", _C.c_int, [_C.c_void_p, _C.POINTER(_C.c_int)]),
+    ("ompi_amd_plan_wait", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_plan_free", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_reduce", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_int,

@@ -79,6 +79,12 @@ class Communicator:
         _lib.check(self._lib.ompi_amd_comm_set_param(self._h, key.encode(), int(value)),
                    f"set_param({key})")
 
+    def get_param(self, key: str) -> int:
+        v = ctypes.c_int64()
+        _lib.check(self._lib.ompi_amd_comm_get_param(self._h, key.encode(), ctypes.byref(v)),
+                   f"get_param({key})")
+        return v.value
+
     def error(self) -> int:
         return self._lib.ompi_amd_comm_error(self._h)
 
@@ -179,6 +185,15 @@ class Plan:
     def start(self, stream=None, blocking: bool = False) -> None:
         rc = self._comm._lib.ompi_amd_plan_start(self._h, _stream(stream))
         self._comm._finish(rc, "start " + self._what, blocking, stream)
+
+    def test(self) -> bool:
+        done = ctypes.c_int()
+        _lib.check(self._comm._lib.ompi_amd_plan_test(self._h, ctypes.byref(done)),
+                   "test " + self._what)
+        return bool(done.value)
+
+    def wait(self) -> None:
+        _lib.check(self._comm._lib.ompi_amd_plan_wait(self._h), "wait " + self._what)
 
     def free(self) -> None:
         if self._h:

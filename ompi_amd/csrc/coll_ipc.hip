@@ -47,8 +47,12 @@
 // system-scope release (buffer_wbl2 sc0 sc1).
 #include <hip/hip_runtime.h>
 
+#include <unistd.h>
+
 #include <algorithm>
 #include <array>
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -552,6 +556,8 @@ struct ompi_amd_comm {
     size_t land_bytes = 0;                //   allreduce, large scan/exscan)
     ptr_set peer_land{};
     void *land_opened[kMaxRanks] = {};
+    std::vector<void *> land_rejected;  // aliased landing candidates, freed at destroy
+    int land_alias_retries = 0;
     int *err_host = nullptr, *err_dev = nullptr;
     uint64_t epoch = 0;
     // params
@@ -586,6 +592,8 @@ struct ompi_amd_plan {
     int kind = 0;      // 0: small paths (as a plain call), 1 pull, 2 pull+push, 3 push
     ptr_set sp{}, rp{};
     void *bases[OMPI_AMD_MAX_RANKS][2] = {};  // pinned peer mappings
+    hipEvent_t done = nullptr;                // recorded at the end of every start
+    bool started = false;
 };
 
 namespace ompi_amd {
@@ -760,10 +768,21 @@ static hipError_t alloc_exportable(size_t bytes, char **out, hipIpcMemHandle_t *
     return e;
 }
 
+static uint64_t landing_token(int rank) {
+    static std::atomic<uint64_t> serial{0};
+    uint64_t x = ((uint64_t)getpid() << 32) ^ (++serial << 8) ^ (uint64_t)rank ^
+                 (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+    x ^= x >> 33;  // splitmix finaliser: spread the bits
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    return x | 1;
+}
+
 static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     if (need <= c->land_bytes) return OMPI_AMD_SUCCESS;
-    constexpr size_t kStep = 32u << 20;
-    const size_t want = std::max((need + kStep - 1) / kStep * kStep, 2 * c->land_bytes);
+    constexpr size_t kStep = 32u << 20, kTag = 64;  // the last kTag bytes hold the token
+    const size_t want = std::max((need + kTag + kStep - 1) / kStep * kStep,
+                                 c->land_bytes ? 2 * (c->land_bytes + kTag) : 0);
     int rc = record_hip(hipDeviceSynchronize(), "landing: drain");
     if (rc == OMPI_AMD_SUCCESS) rc = c->boot.barrier();
     if (rc != OMPI_AMD_SUCCESS) return rc;
@@ -772,48 +791,87 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
         c->land_opened[p] = nullptr;
         c->peer_land.p[p] = nullptr;
     }
-    struct { hipIpcMemHandle_t h; int ok; } mine{}, all[kMaxRanks];
-    char *fresh = nullptr;
-    hipError_t e = alloc_exportable(want, &fresh, &mine.h);
-    mine.ok = e == hipSuccess;
-    if (e != hipSuccess) record_hip(e, "landing buffer");
-    rc = c->boot.allgather(&mine, all, sizeof(mine));  // also: nobody maps the old one now
-    if (rc != OMPI_AMD_SUCCESS) {
-        if (fresh) (void)hipFree(fresh);
-        return rc;
-    }
-    if (c->land) (void)hipFree(c->land);
-    c->land = fresh;
-    c->land_bytes = 0;
-    bool ok = true;
-    for (int p = 0; p < c->size; ++p) ok = ok && all[p].ok;
-    for (int p = 0; ok && p < c->size; ++p) {
-        if (p == c->rank) {
-            c->peer_land.p[p] = c->land;
-            continue;
+    // Every rank stamps a fresh token into its new buffer and every importer
+    // reads it back through its mapping.  A mapping that shows another token
+    // aliases an older allocation of that peer (seen on ROCm 7.2 when a new
+    // buffer reuses a freed, previously exported address range): then all
+    // ranks retry with new buffers, keeping the rejected ones alive so the
+    // next ranges differ.
+    bool first = true;
+    for (int attempt = 0; attempt < 3; ++attempt) {
+        struct { hipIpcMemHandle_t h; uint64_t token; int ok; } mine{}, all[kMaxRanks];
+        char *fresh = nullptr;
+        hipError_t e = alloc_exportable(want, &fresh, &mine.h);
+        mine.token = landing_token(c->rank);
+        if (e == hipSuccess)
+            e = hipMemcpy(fresh + want - kTag, &mine.token, sizeof(mine.token),
+                          hipMemcpyHostToDevice);
+        mine.ok = e == hipSuccess;
+        if (e != hipSuccess) record_hip(e, "landing buffer");
+        rc = c->boot.allgather(&mine, all, sizeof(mine));  // also: nobody maps the old one now
+        if (rc != OMPI_AMD_SUCCESS) {
+            if (fresh) (void)hipFree(fresh);
+            return rc;
         }
-        void *m = nullptr;
-        e = hipIpcOpenMemHandle(&m, all[p].h, hipIpcMemLazyEnablePeerAccess);
-        if (e != hipSuccess) {
-            record_hip(e, "hipIpcOpenMemHandle (landing)");
-            ok = false;
-            break;
+        if (first) {
+            if (c->land) (void)hipFree(c->land);
+            c->land = nullptr;
+            c->land_bytes = 0;
+            first = false;
         }
-        c->land_opened[p] = m;
-        c->peer_land.p[p] = (const char *)m;
+        bool ok = true, alias = false;
+        for (int p = 0; p < c->size; ++p) ok = ok && all[p].ok;
+        for (int p = 0; ok && p < c->size; ++p) {
+            if (p == c->rank) continue;
+            void *m = nullptr;
+            e = hipIpcOpenMemHandle(&m, all[p].h, hipIpcMemLazyEnablePeerAccess);
+            if (e != hipSuccess) {
+                record_hip(e, "hipIpcOpenMemHandle (landing)");
+                ok = false;
+                break;
+            }
+            c->land_opened[p] = m;
+            uint64_t seen = 0;
+            e = hipMemcpy(&seen, (char *)m + want - kTag, sizeof(seen), hipMemcpyDeviceToHost);
+            if (e != hipSuccess || seen != all[p].token) {
+                if (e != hipSuccess) record_hip(e, "landing token read");
+                else record_msg("landing buffer of rank %d: the IPC mapping aliases an older "
+                               "allocation (token %016llx, expected %016llx)", p,
+                               (unsigned long long)seen, (unsigned long long)all[p].token);
+                ok = false;
+                alias = e == hipSuccess;
+                break;
+            }
+        }
+        int oks[kMaxRanks], flags = (ok ? 1 : 0) | (alias ? 2 : 0);
+        rc = c->boot.allgather(&flags, oks, sizeof(int));
+        if (rc != OMPI_AMD_SUCCESS) return rc;
+        bool all_ok = true, any_alias = false;
+        for (int p = 0; p < c->size; ++p) {
+            all_ok = all_ok && (oks[p] & 1);
+            any_alias = any_alias || (oks[p] & 2);
+        }
+        if (all_ok) {
+            c->land = fresh;
+            for (int p = 0; p < c->size; ++p)
+                c->peer_land.p[p] = p == c->rank ? c->land : (const char *)c->land_opened[p];
+            c->land_bytes = want - kTag;
+            return OMPI_AMD_SUCCESS;
+        }
+        (void)c->boot.barrier();  // nobody reads the rejected buffers any more
+        for (int p = 0; p < kMaxRanks; ++p) {
+            if (c->land_opened[p]) (void)hipIpcCloseMemHandle(c->land_opened[p]);
+            c->land_opened[p] = nullptr;
+        }
+        if (!any_alias) {
+            if (fresh) (void)hipFree(fresh);
+            return OMPI_AMD_ERR_HIP;
+        }
+        if (fresh) c->land_rejected.push_back(fresh);
+        ++c->land_alias_retries;
+        if (alias) fprintf(stderr, "ompi_amd[%d]: %s; retrying\n", c->rank, ompi_amd_last_error());
     }
-    int all_ok = 0, mine_ok = ok ? 1 : 0, oks[kMaxRanks];
-    rc = c->boot.allgather(&mine_ok, oks, sizeof(int));
-    if (rc != OMPI_AMD_SUCCESS) return rc;
-    all_ok = 1;
-    for (int p = 0; p < c->size; ++p) all_ok &= oks[p];
-    if (!all_ok) {
-        (void)c->boot.barrier();
-        release_landing(c);
-        return OMPI_AMD_ERR_HIP;
-    }
-    c->land_bytes = want;
-    return OMPI_AMD_SUCCESS;
+    return OMPI_AMD_ERR_HIP;
 }
 
 static int launch_barrier(ompi_amd_comm_t *c, hipStream_t s) {
@@ -1287,6 +1345,7 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     if (c->flags) (void)hipFree(c->flags);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->land) (void)hipFree(c->land);
+    for (void *p : c->land_rejected) (void)hipFree(p);
     if (c->err_host) (void)hipHostFree(c->err_host);
     for (int ph = 0; ph < 2; ++ph)
         for (auto &pr : c->ev_phase[ph]) {
@@ -1388,6 +1447,25 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
         if (v < 0 || v >= ALG_COUNT) return OMPI_AMD_ERR_BAD_PARAM;
         c->algorithm = (int)v;
     } else {
+        record_msg("unknown coll param '%s'", key);
+        return OMPI_AMD_ERR_BAD_PARAM;
+    }
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *v) {
+    if (!c || !key || !v) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!strcmp(key, "small_bytes")) *v = (int64_t)c->small_bytes;
+    else if (!strcmp(key, "zero_copy")) *v = c->zero_copy;
+    else if (!strcmp(key, "timeout_ms")) *v = (int64_t)c->timeout_ms;
+    else if (!strcmp(key, "profile")) *v = c->profile;
+    else if (!strcmp(key, "blocks")) *v = c->max_blocks;
+    else if (!strcmp(key, "fused_bytes")) *v = (int64_t)c->fused_bytes;
+    else if (!strcmp(key, "algorithm")) *v = c->algorithm;
+    else if (!strcmp(key, "landing_bytes")) *v = (int64_t)c->land_bytes;
+    else if (!strcmp(key, "landing_alias_retries")) *v = c->land_alias_retries;
+    else if (!strcmp(key, "imports")) *v = (int64_t)c->imports.size();
+    else {
         record_msg("unknown coll param '%s'", key);
         return OMPI_AMD_ERR_BAD_PARAM;
     }
@@ -1676,6 +1754,8 @@ int ompi_amd_allreduce_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, si
                                nullptr, true, pl->bases);
         if (inplace) pl->sp = pl->rp;
     }
+    if (rc == OMPI_AMD_SUCCESS)
+        rc = record_hip(hipEventCreateWithFlags(&pl->done, hipEventDisableTiming), "plan event");
     if (rc != OMPI_AMD_SUCCESS) {
         (void)ompi_amd_plan_free(pl);
         return rc;
@@ -1684,8 +1764,7 @@ int ompi_amd_allreduce_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, si
     return OMPI_AMD_SUCCESS;
 }
 
-int ompi_amd_plan_start(ompi_amd_plan_t *pl, void *stream) {
-    if (!pl || !pl->c) return OMPI_AMD_ERR_BAD_PARAM;
+static int plan_enqueue(ompi_amd_plan_t *pl, void *stream) {
     ompi_amd_comm_t *c = pl->c;
     if (pl->kind == 0)
         return ompi_amd_allreduce(c, pl->src == pl->rbuf ? (const void *)1 : pl->src, pl->rbuf,
@@ -1702,12 +1781,40 @@ int ompi_amd_plan_start(ompi_amd_plan_t *pl, void *stream) {
     return allreduce_pull(c, pl->sp, pl->rp, pl->rbuf, pl->count, pl->op, pl->type, s);
 }
 
+int ompi_amd_plan_start(ompi_amd_plan_t *pl, void *stream) {
+    if (!pl || !pl->c) return OMPI_AMD_ERR_BAD_PARAM;
+    TRY(plan_enqueue(pl, stream));
+    pl->started = true;
+    return record_hip(hipEventRecord(pl->done, as_stream(stream)), "plan completion event");
+}
+
+int ompi_amd_plan_test(ompi_amd_plan_t *pl, int *done) {
+    if (!pl || !done) return OMPI_AMD_ERR_BAD_PARAM;
+    *done = 1;
+    if (!pl->started) return OMPI_AMD_SUCCESS;
+    const hipError_t e = hipEventQuery(pl->done);
+    if (e == hipErrorNotReady) {
+        *done = 0;
+        return OMPI_AMD_SUCCESS;
+    }
+    if (e != hipSuccess) return record_hip(e, "plan test");
+    return check_sticky(pl->c);
+}
+
+int ompi_amd_plan_wait(ompi_amd_plan_t *pl) {
+    if (!pl) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!pl->started) return OMPI_AMD_SUCCESS;
+    TRY(record_hip(hipEventSynchronize(pl->done), "plan wait"));
+    return check_sticky(pl->c);
+}
+
 int ompi_amd_plan_free(ompi_amd_plan_t *pl) {
     if (!pl) return OMPI_AMD_SUCCESS;
     if (pl->c)
         for (int p = 0; p < OMPI_AMD_MAX_RANKS; ++p)
             for (int k = 0; k < 2; ++k)
                 if (pl->bases[p][k]) unpin_import(pl->c, pl->bases[p][k]);
+    if (pl->done) (void)hipEventDestroy(pl->done);
     delete pl;
     return OMPI_AMD_SUCCESS;
 }

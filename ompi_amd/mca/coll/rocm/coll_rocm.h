@@ -4,8 +4,9 @@
  * Drop-in: copy this directory to ompi/mca/coll/rocm/ (INTEGRATION.md §2).
  * The module provides coll_allreduce, coll_reduce, coll_reduce_scatter,
  * coll_reduce_scatter_block,
- * coll_scan, coll_exscan, coll_allgather and coll_bcast
- * (ompi/mca/coll/coll.h:200-250) for device buffers through libompi_amd.so,
+ * coll_scan, coll_exscan, coll_allgather, coll_bcast
+ * (ompi/mca/coll/coll.h:200-250) and the persistent coll_allreduce_init
+ * (coll.h:349-352) for device buffers through libompi_amd.so,
  * and interposes on the previously selected functions (coll/tuned, coll/basic
  * for scan/exscan) for everything else, exactly like coll/cuda does
  * (ompi/mca/coll/cuda/coll_cuda_module.c:120-155).
@@ -19,6 +20,7 @@
 #include "ompi/communicator/communicator.h"
 #include "ompi/mca/coll/base/coll_base_functions.h"
 #include "ompi/mca/coll/coll.h"
+#include "ompi/request/request.h"
 #include "opal/class/opal_object.h"
 
 #include "ompi_amd_coll.h"
@@ -45,6 +47,17 @@ typedef struct mca_coll_rocm_component_t {
 } mca_coll_rocm_component_t;
 
 OMPI_MODULE_DECLSPEC extern mca_coll_rocm_component_t mca_coll_rocm_component;
+
+/* A persistent device collective (MPI_Allreduce_init).  Start enqueues the
+ * plan's kernels; the component's progress callback completes the request
+ * once the plan's completion event has fired. */
+typedef struct mca_coll_rocm_request_t {
+    ompi_request_t super;
+    ompi_amd_plan_t *plan;
+    struct mca_coll_rocm_request_t *next_active; /* started, not yet complete */
+} mca_coll_rocm_request_t;
+
+OBJ_CLASS_DECLARATION(mca_coll_rocm_request_t);
 
 int mca_coll_rocm_init_query(bool enable_progress_threads, bool enable_mpi_threads);
 mca_coll_base_module_t *mca_coll_rocm_comm_query(struct ompi_communicator_t *comm,
@@ -74,6 +87,10 @@ int mca_coll_rocm_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount,
 int mca_coll_rocm_allgather(const void *sbuf, int scount, struct ompi_datatype_t *sdtype,
                             void *rbuf, int rcount, struct ompi_datatype_t *rdtype,
                             struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+int mca_coll_rocm_allreduce_init(const void *sbuf, void *rbuf, int count,
+                                 struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                 struct ompi_communicator_t *comm, struct ompi_info_t *info,
+                                 ompi_request_t **request, mca_coll_base_module_t *module);
 int mca_coll_rocm_bcast(void *buf, int count, struct ompi_datatype_t *dtype, int root,
                         struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
 

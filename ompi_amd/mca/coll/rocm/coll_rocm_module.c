@@ -14,6 +14,14 @@
  * same path — MPI lets buffer residency differ between ranks.  The device
  * path is blocking like every MPI collective: ompi_amd_comm_sync waits for
  * the stream and surfaces a device-side timeout as an MPI error.
+ *
+ * Persistent allreduce (MPI_Allreduce_init) builds a library plan (the
+ * peers' buffer mappings are swapped and pinned once, at init) behind an
+ * ompi_request_t: req_start enqueues the plan's kernels with no host
+ * rendezvous and puts the request on the active list; the progress
+ * callback (registered with opal_progress, as coll/libnbc does,
+ * coll_libnbc_component.c:430-475) completes it when the plan's completion
+ * event has fired, carrying a device-side failure into req_status.
  */
 #include "ompi_config.h"
 
@@ -29,6 +37,8 @@
 #include "ompi/op/op.h"
 #include "ompi/runtime/ompi_rte.h"
 #include "opal/mca/base/mca_base_var.h"
+#include "opal/mca/threads/mutex.h"
+#include "opal/runtime/opal_progress.h"
 
 #include "coll_rocm.h"
 #include "ompi_amd.h"
@@ -107,6 +117,8 @@ static void rocm_module_destruct(mca_coll_rocm_module_t *m)
         OBJ_RELEASE(m->c_coll.coll_reduce_scatter_block_module);
     if (NULL != m->c_coll.coll_allgather_module) OBJ_RELEASE(m->c_coll.coll_allgather_module);
     if (NULL != m->c_coll.coll_bcast_module) OBJ_RELEASE(m->c_coll.coll_bcast_module);
+    if (NULL != m->c_coll.coll_allreduce_init_module)
+        OBJ_RELEASE(m->c_coll.coll_allreduce_init_module);
     if (NULL != m->dev_comm) (void) ompi_amd_comm_destroy(m->dev_comm);
 }
 
@@ -139,6 +151,7 @@ mca_coll_base_module_t *mca_coll_rocm_comm_query(struct ompi_communicator_t *com
     m->super.coll_reduce_scatter_block = mca_coll_rocm_reduce_scatter_block;
     m->super.coll_allgather = mca_coll_rocm_allgather;
     m->super.coll_bcast = mca_coll_rocm_bcast;
+    m->super.coll_allreduce_init = mca_coll_rocm_allreduce_init;
     return &m->super;
 }
 
@@ -163,6 +176,7 @@ int mca_coll_rocm_module_enable(mca_coll_base_module_t *module, struct ompi_comm
     SAVE(reduce_scatter_block);
     SAVE(allgather);
     SAVE(bcast);
+    SAVE(allreduce_init);
 #undef SAVE
 
     /* node-unique segment name: job id + communicator id */
@@ -365,4 +379,154 @@ int mca_coll_rocm_bcast(void *buf, int count, struct ompi_datatype_t *dtype, int
     rc = ompi_amd_bcast(m->dev_comm, buf, size * (size_t) count, root, NULL);
     if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_comm_sync(m->dev_comm, NULL);
     return to_ompi_err(rc);
+}
+
+/* ------------------------------------------------------------- persistent */
+
+static opal_mutex_t rocm_active_lock = OPAL_MUTEX_STATIC_INIT;
+static mca_coll_rocm_request_t *rocm_active; /* started requests, not yet complete */
+static int rocm_progress_registered;
+
+/* opal_progress callback: complete the started requests whose device work
+ * has finished (ompi_amd_plan_test queries the plan's completion event). */
+static int rocm_progress(void)
+{
+    mca_coll_rocm_request_t **pp, *done = NULL;
+    int completed = 0;
+    if (NULL == rocm_active) return 0;
+    OPAL_THREAD_LOCK(&rocm_active_lock);
+    pp = &rocm_active;
+    while (NULL != *pp) {
+        mca_coll_rocm_request_t *r = *pp;
+        int fin = 0;
+        const int rc = ompi_amd_plan_test(r->plan, &fin);
+        if (OMPI_AMD_SUCCESS != rc || fin) {
+            r->super.req_status.MPI_ERROR = to_ompi_err(rc);
+            *pp = r->next_active;
+            r->next_active = done;
+            done = r;
+        } else {
+            pp = &r->next_active;
+        }
+    }
+    OPAL_THREAD_UNLOCK(&rocm_active_lock);
+    while (NULL != done) {
+        mca_coll_rocm_request_t *r = done;
+        done = r->next_active;
+        r->next_active = NULL;
+        ompi_request_complete(&r->super, true);
+        ++completed;
+    }
+    return completed;
+}
+
+static void rocm_unlink_active(mca_coll_rocm_request_t *r)
+{
+    mca_coll_rocm_request_t **pp;
+    OPAL_THREAD_LOCK(&rocm_active_lock);
+    for (pp = &rocm_active; NULL != *pp; pp = &(*pp)->next_active) {
+        if (*pp == r) {
+            *pp = r->next_active;
+            break;
+        }
+    }
+    OPAL_THREAD_UNLOCK(&rocm_active_lock);
+    r->next_active = NULL;
+}
+
+/* MPI_Start / MPI_Startall (ompi/request/request.h:60-77) */
+static int rocm_request_start(size_t count, ompi_request_t **requests)
+{
+    size_t i;
+    for (i = 0; i < count; ++i) {
+        mca_coll_rocm_request_t *r = (mca_coll_rocm_request_t *) requests[i];
+        int rc;
+        if (NULL == r) continue;
+        if (OMPI_REQUEST_ACTIVE == r->super.req_state && !REQUEST_COMPLETE(&r->super)) {
+            return OMPI_ERR_REQUEST; /* started twice without a completion */
+        }
+        r->super.req_complete = REQUEST_PENDING;
+        r->super.req_status.MPI_ERROR = OMPI_SUCCESS;
+        r->super.req_state = OMPI_REQUEST_ACTIVE;
+        rc = ompi_amd_plan_start(r->plan, NULL);
+        if (OMPI_AMD_SUCCESS != rc) {
+            r->super.req_status.MPI_ERROR = to_ompi_err(rc);
+            ompi_request_complete(&r->super, true);
+            return to_ompi_err(rc);
+        }
+        OPAL_THREAD_LOCK(&rocm_active_lock);
+        r->next_active = rocm_active;
+        rocm_active = r;
+        if (!rocm_progress_registered) {
+            rocm_progress_registered = 1;
+            (void) opal_progress_register(rocm_progress);
+        }
+        OPAL_THREAD_UNLOCK(&rocm_active_lock);
+    }
+    return OMPI_SUCCESS;
+}
+
+/* MPI_Request_free: an active request's device work is waited for first —
+ * the plan's peers may still read this rank's buffers through it. */
+static int rocm_request_free(ompi_request_t **rptr)
+{
+    mca_coll_rocm_request_t *r = (mca_coll_rocm_request_t *) *rptr;
+    int rc = OMPI_AMD_SUCCESS;
+    if (NULL != r->next_active) rocm_unlink_active(r);
+    if (NULL != r->plan) {
+        rc = ompi_amd_plan_wait(r->plan);
+        (void) ompi_amd_plan_free(r->plan);
+        r->plan = NULL;
+    }
+    OMPI_REQUEST_FINI(&r->super);
+    OBJ_RELEASE(r);
+    *rptr = MPI_REQUEST_NULL;
+    return to_ompi_err(rc);
+}
+
+static void rocm_request_construct(mca_coll_rocm_request_t *r)
+{
+    r->super.req_type = OMPI_REQUEST_COLL;
+    r->super.req_status._cancelled = 0;
+    r->super.req_start = rocm_request_start;
+    r->super.req_free = rocm_request_free;
+    r->super.req_cancel = NULL;
+    r->plan = NULL;
+    r->next_active = NULL;
+}
+
+OBJ_CLASS_INSTANCE(mca_coll_rocm_request_t, ompi_request_t, rocm_request_construct, NULL);
+
+/* MPI_Allreduce_init (coll.h:349-352).  Collective: the path decision is
+ * agreed like the blocking allreduce's, and on the device path the plan's
+ * init swaps the buffer handles (it synchronises the ranks once). */
+int mca_coll_rocm_allreduce_init(const void *sbuf, void *rbuf, int count,
+                                 struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                 struct ompi_communicator_t *comm, struct ompi_info_t *info,
+                                 ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const int t = type_code(dtype);
+    const int ok = t >= 0 && ompi_op_is_intrinsic(op) &&
+                   ompi_amd_op_supported(op->o_f_to_c_index, t) && dev(sbuf) && dev(rbuf);
+    mca_coll_rocm_request_t *r;
+    ompi_amd_plan_t *plan = NULL;
+    int rc;
+    if (!take_device_path(m, ok)) {
+        return m->c_coll.coll_allreduce_init(sbuf, rbuf, count, dtype, op, comm, info, request,
+                                             m->c_coll.coll_allreduce_init_module);
+    }
+    rc = ompi_amd_allreduce_init(m->dev_comm, MPI_IN_PLACE == sbuf ? rbuf : sbuf, rbuf,
+                                 (size_t) count, t, op->o_f_to_c_index, &plan);
+    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
+    r = OBJ_NEW(mca_coll_rocm_request_t);
+    if (NULL == r) {
+        (void) ompi_amd_plan_free(plan);
+        return OMPI_ERROR;
+    }
+    OMPI_REQUEST_INIT(&r->super, true);
+    r->super.req_mpi_object.comm = comm;
+    r->plan = plan;
+    *request = &r->super;
+    return OMPI_SUCCESS;
 }

@@ -11,7 +11,9 @@
  *   accepts only node-local intra-communicators of 2..16 ranks.
  *   GPU (HARNESS_GPU=1): device buffers run the library and match the CPU
  *   oracle bit for bit; host buffers, mixed residency across ranks and
- *   non-intrinsic ops go to the saved functions on every rank.
+ *   non-intrinsic ops go to the saved functions on every rank.  A
+ *   persistent allreduce request is started and completed through
+ *   opal_progress the way MPI_Start / MPI_Wait drive it.
  *
  * usage: coll_harness <segment-name> <rank> <size>; prints "ok" / "ok gpu".
  */
@@ -25,16 +27,46 @@
 #include "ompi/datatype/ompi_datatype.h"
 #include "ompi/op/op.h"
 #include "ompi/runtime/ompi_rte.h"
+#include "opal/runtime/opal_progress.h"
 #include "../../oracle/oracle.h"
 #include "coll_rocm.h"
 #include "ompi_amd.h"
 
 extern mca_coll_rocm_component_t mca_coll_rocm_component;
 extern int harness_dev_alloc_copy(void **d, const void *h, size_t bytes);
+extern int harness_dev_copy_in(void *d, const void *h, size_t bytes);
 extern int harness_dev_copy_back(void *h, const void *d, size_t bytes);
 extern int harness_dev_free(void *d);
 
 OBJ_CLASS_INSTANCE(mca_coll_base_module_t, opal_object_t, NULL, NULL);
+OBJ_CLASS_INSTANCE(ompi_request_t, opal_object_t, NULL, NULL);
+ompi_request_t harness_request_null;
+
+/* opal_progress: the registered callbacks, polled by the wait loop below */
+static opal_progress_callback_t progress_cbs[8];
+static int n_progress_cbs;
+int opal_progress_register(opal_progress_callback_t cb)
+{
+    progress_cbs[n_progress_cbs++] = cb;
+    return 0;
+}
+int opal_progress_unregister(opal_progress_callback_t cb)
+{
+    for (int i = 0; i < n_progress_cbs; ++i)
+        if (progress_cbs[i] == cb) progress_cbs[i] = progress_cbs[--n_progress_cbs];
+    return 0;
+}
+void opal_progress(void)
+{
+    for (int i = 0; i < n_progress_cbs; ++i) progress_cbs[i]();
+}
+
+/* ompi_request_default_wait for a persistent request (request/req_wait.c) */
+static void harness_wait(ompi_request_t *req)
+{
+    while (!REQUEST_COMPLETE(req)) opal_progress();
+    req->req_state = OMPI_REQUEST_INACTIVE;
+}
 harness_proc_name_t harness_proc_name = {4242, 0};
 int ompi_op_ddt_map[64];
 
@@ -74,6 +106,12 @@ static int t_bcast(void *b, int c, struct ompi_datatype_t *d, int root,
                    struct ompi_communicator_t *cm, mca_coll_base_module_t *m)
 { tuned_calls++; return OMPI_SUCCESS; }
 
+static ompi_request_t t_request;
+static int t_ar_init(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                     struct ompi_communicator_t *cm, struct ompi_info_t *info,
+                     ompi_request_t **req, mca_coll_base_module_t *m)
+{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
+
 static void fill_tuned(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *tm)
 {
     memset(t, 0, sizeof(*t));
@@ -86,6 +124,7 @@ static void fill_tuned(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *tm)
     SET(exscan, t_scan);
     SET(allgather, t_allgather);
     SET(bcast, t_bcast);
+    SET(allreduce_init, t_ar_init);
 #undef SET
 }
 
@@ -96,7 +135,7 @@ static void install(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *m)
                                       t->coll_##fn##_module = m; OBJ_RETAIN(m); }
     INST(allreduce) INST(reduce) INST(reduce_scatter) INST(reduce_scatter_block) INST(scan)
     INST(exscan)
-    INST(allgather) INST(bcast)
+    INST(allgather) INST(bcast) INST(allreduce_init)
 #undef INST
 }
 
@@ -110,6 +149,7 @@ static void release_table(mca_coll_base_comm_coll_t *t)
     OBJ_RELEASE(t->coll_exscan_module);
     OBJ_RELEASE(t->coll_allgather_module);
     OBJ_RELEASE(t->coll_bcast_module);
+    OBJ_RELEASE(t->coll_allreduce_init_module);
 }
 
 /* deterministic per-rank floats in [-1, 1): fp sums depend on order */
@@ -182,7 +222,8 @@ int main(int argc, char **argv)
     CHECK(m != NULL && prio == 80, "comm_query on a local intra-communicator");
     CHECK(m->coll_allreduce && m->coll_reduce && m->coll_reduce_scatter &&
               m->coll_reduce_scatter_block && m->coll_scan &&
-              m->coll_exscan && m->coll_allgather && m->coll_bcast && m->coll_module_enable,
+              m->coll_exscan && m->coll_allgather && m->coll_bcast && m->coll_allreduce_init &&
+              m->coll_module_enable,
           "module function table");
     {
         ompi_communicator_t c1 = comm, ci = comm, cr = comm;
@@ -206,7 +247,7 @@ int main(int argc, char **argv)
     }
 
     CHECK(m->coll_module_enable(m, &comm) == OMPI_SUCCESS, "enable");
-    CHECK(tm->super.obj_reference_count == 1 + 8 + 8, "enable retains the saved modules (%d)",
+    CHECK(tm->super.obj_reference_count == 1 + 9 + 9, "enable retains the saved modules (%d)",
           tm->super.obj_reference_count);
     install(&table, m);
 
@@ -394,6 +435,59 @@ int main(int argc, char **argv)
         harness_dev_free(d2);
         free(h);
         free(h2);
+    }
+    /* 7. persistent allreduce (MPI_Allreduce_init): init once, then three
+     * start / wait rounds with fresh inputs (the plan reads the buffers'
+     * current contents), staged and zero-copy sizes, in place; free */
+    {
+        const size_t counts[3] = {1000, 300001, 300001};
+        for (int k = 0; k < 3; ++k) {
+            const size_t n = counts[k];
+            const int inplace = k == 2;
+            float *zero = calloc(n, sizeof(float));
+            void *ds = dev_of(zero, n * 4), *dr = dev_of(zero, n * 4);
+            ompi_request_t *req = NULL;
+            tuned_calls = 0;
+            CHECK(table.coll_allreduce_init(inplace ? MPI_IN_PLACE : ds, dr, (int) n, &dfloat, &sum,
+                                            &comm, NULL, &req,
+                                            table.coll_allreduce_init_module) == OMPI_SUCCESS,
+                  "allreduce_init");
+            CHECK(tuned_calls == 0 && req != NULL && req->req_persistent &&
+                      REQUEST_COMPLETE(req) && req->req_type == OMPI_REQUEST_COLL,
+                  "allreduce_init request");
+            for (int it = 0; it < 3; ++it) {
+                float **xs = all_inputs(n, 60 + 3 * k + it);
+                float **rb = malloc(sizeof(float *) * (size_t) g_size);
+                for (int r = 0; r < g_size; ++r) rb[r] = calloc(n, sizeof(float));
+                CHECK(orc_allreduce(ORC_AR_TUNED, g_size, (const void *const *) xs,
+                                    (void *const *) rb, n, ORC_OP_SUM, ORC_T_FLOAT, 0) >= 0,
+                      "oracle allreduce");
+                CHECK(harness_dev_copy_in(inplace ? dr : ds, xs[g_rank], n * 4) == 0, "copy in");
+                CHECK(req->req_start(1, &req) == OMPI_SUCCESS, "start");
+                CHECK(req->req_state == OMPI_REQUEST_ACTIVE, "start activates");
+                harness_wait(req);
+                CHECK(req->req_status.MPI_ERROR == OMPI_SUCCESS, "persistent status %d",
+                      req->req_status.MPI_ERROR);
+                expect_dev(dr, rb[g_rank], n * 4, "persistent allreduce");
+                for (int r = 0; r < g_size; ++r) free(rb[r]);
+                free(rb);
+                free_inputs(xs);
+            }
+            CHECK(req->req_free(&req) == OMPI_SUCCESS && req == MPI_REQUEST_NULL, "request free");
+            harness_dev_free(ds);
+            harness_dev_free(dr);
+            free(zero);
+        }
+        /* host buffers: the saved allreduce_init builds the request */
+        {
+            float h[16] = {0}, h2[16] = {0};
+            ompi_request_t *req = NULL;
+            tuned_calls = 0;
+            CHECK(table.coll_allreduce_init(h, h2, 16, &dfloat, &sum, &comm, NULL, &req,
+                                            table.coll_allreduce_init_module) == OMPI_SUCCESS &&
+                      tuned_calls == 1 && req == &t_request,
+                  "host allreduce_init falls back");
+        }
     }
     /* teardown: the table's references, then the module (its destructor
      * releases the saved modules and destroys the device communicator) */

@@ -1,12 +1,14 @@
 /* TEST HARNESS ONLY: the coll framework types the glue uses, with the
  * reference's function signatures (ompi/mca/coll/coll.h:141-143, 200-250,
- * 471-603). */
+ * 349-352, 471-603). */
 #ifndef HARNESS_COLL_H
 #define HARNESS_COLL_H
 #include <stdbool.h>
 #include "ompi/mca/mca.h"
 #include "opal/class/opal_object.h"
+#include "ompi/request/request.h"
 struct ompi_communicator_t;
+struct ompi_info_t;
 struct ompi_datatype_t;
 struct ompi_op_t;
 struct mca_coll_base_module_2_3_0_t;
@@ -34,6 +36,10 @@ typedef int (*mca_coll_base_module_reduce_scatter_block_fn_t)(const void *, void
                                                               struct ompi_communicator_t *, HMOD);
 typedef int (*mca_coll_base_module_scan_fn_t)(const void *, void *, int, struct ompi_datatype_t *,
                                               struct ompi_op_t *, struct ompi_communicator_t *, HMOD);
+typedef int (*mca_coll_base_module_allreduce_init_fn_t)(const void *, void *, int,
+                                                        struct ompi_datatype_t *, struct ompi_op_t *,
+                                                        struct ompi_communicator_t *,
+                                                        struct ompi_info_t *, ompi_request_t **, HMOD);
 typedef int (*mca_coll_base_module_enable_1_1_0_fn_t)(HMOD, struct ompi_communicator_t *);
 #undef HMOD
 typedef struct mca_coll_base_module_2_3_0_t {
@@ -47,6 +53,7 @@ typedef struct mca_coll_base_module_2_3_0_t {
     mca_coll_base_module_reduce_scatter_fn_t coll_reduce_scatter;
     mca_coll_base_module_reduce_scatter_block_fn_t coll_reduce_scatter_block;
     mca_coll_base_module_scan_fn_t coll_scan;
+    mca_coll_base_module_allreduce_init_fn_t coll_allreduce_init;
     void *base_data;
 } mca_coll_base_module_2_3_0_t;
 typedef mca_coll_base_module_2_3_0_t mca_coll_base_module_t;
@@ -65,7 +72,7 @@ typedef struct mca_coll_base_component_2_0_0_t {
 typedef struct mca_coll_base_comm_coll_t {
     HFN(allgather) HFN(allreduce) HFN(bcast) HFN(exscan) HFN(reduce) HFN(reduce_scatter)
     HFN(reduce_scatter_block)
-    HFN(scan)
+    HFN(scan) HFN(allreduce_init)
 } mca_coll_base_comm_coll_t;
 #undef HFN
 #define MCA_COLL_BASE_VERSION_2_0_0 OMPI_MCA_BASE_VERSION_2_1_0("coll", 2, 0, 0)

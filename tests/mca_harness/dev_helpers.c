@@ -8,6 +8,11 @@ int harness_dev_alloc_copy(void **d, const void *h, size_t bytes)
     return hipMemcpy(*d, h, bytes, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
 }
 
+int harness_dev_copy_in(void *d, const void *h, size_t bytes)
+{
+    return hipMemcpy(d, h, bytes, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+
 int harness_dev_copy_back(void *h, const void *d, size_t bytes)
 {
     return hipMemcpy(h, d, bytes, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;

@@ -49,6 +49,12 @@ def run_ranks(n, timeout=600, extra_env=None):
         for p in procs:
             if p.poll() is None:
                 p.kill()
+    logdir = os.environ.get("COLL_LOG_DIR")
+    if logdir:  # raw per-rank output (library diagnostics on stderr)
+        os.makedirs(logdir, exist_ok=True)
+        for r, (_, out) in enumerate(outs):
+            with open(os.path.join(logdir, f"raw_n{n}_rank{r}.txt"), "w") as f:
+                f.write(out or "")
     return outs
 
 
