@@ -42,6 +42,7 @@ extern "C" {
 
 typedef struct ompi_amd_comm ompi_amd_comm_t;
 typedef struct ompi_amd_plan ompi_amd_plan_t;
+typedef struct ompi_amd_request ompi_amd_request_t;
 
 /* Collective over the `size` ranks of one node.  `name` identifies the
  * communicator node-wide and must be unique per job (e.g. "<jobid>.<cid>");
@@ -136,6 +137,26 @@ int ompi_amd_plan_start(ompi_amd_plan_t *plan, void *stream);
 int ompi_amd_plan_test(ompi_amd_plan_t *plan, int *done);
 int ompi_amd_plan_wait(ompi_amd_plan_t *plan);
 int ompi_amd_plan_free(ompi_amd_plan_t *plan);
+/* Nonblocking allreduce (MPI_Iallreduce, coll.h:271-274; libnbc's
+ * ompi_coll_libnbc_iallreduce in the reference).  Returns without waiting
+ * for any peer: sizes without a handle swap (fused / staged paths) are
+ * enqueued on `stream` at once; zero-copy sizes post this rank's half of the
+ * handle swap and are launched by the first ompi_amd_request_test / _wait
+ * (or the next collective call on `comm`) that finds every peer's half.
+ * Deferred calls launch in posting order, and every other collective entry
+ * point launches them first, so device work enters every rank's stream in
+ * the same order.  Up to 7 calls with a handle swap may be outstanding; the
+ * 8th waits for the peers to post the 1st.  Results and errors as
+ * ompi_amd_allreduce once the request completes. */
+int ompi_amd_iallreduce(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf, size_t count,
+                        int type, int op, void *stream, ompi_amd_request_t **request);
+/* *done = 1 once the collective's device work finished; launches deferred
+ * calls whose swap completed (never waits for a peer). */
+int ompi_amd_request_test(ompi_amd_request_t *request, int *done);
+/* Waits for the peers' swap halves (if needed) and for the device work. */
+int ompi_amd_request_wait(ompi_amd_request_t *request);
+/* Completes (waits) and releases the request. */
+int ompi_amd_request_free(ompi_amd_request_t *request);
 /* MPI_Reduce to `root` (coll.h:239-241).  rbuf matters at the root only;
  * the root may pass sbuf = MPI_IN_PLACE.  Every rank folds one block of the
  * vector from every rank's sbuf and stores it into the root's rbuf. */

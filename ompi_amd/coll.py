@@ -4,6 +4,7 @@ Mirrors the coll framework's entry points this path provides
 (ompi/mca/coll/coll.h:200-250):
 
     coll_allreduce(sbuf, rbuf, count, dtype, op, comm, module)
+    coll_iallreduce(sbuf, rbuf, count, dtype, op, comm, request, module)
     coll_allreduce_init(sbuf, rbuf, count, dtype, op, comm, info, request, module)
     coll_reduce(sbuf, rbuf, count, dtype, op, root, comm, module)
     coll_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, module)
@@ -120,6 +121,16 @@ class Communicator:
                                           op.index, _stream(stream))
         self._finish(rc, f"allreduce({op.name},{datatype.name})", blocking, stream)
 
+    def iallreduce(self, sbuf, rbuf, count: int, datatype: Datatype, op: Op,
+                   stream=None) -> "Request":
+        """MPI_Iallreduce: returns without waiting for any peer."""
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.ompi_amd_iallreduce(self._h, _ptr(sbuf), _ptr(rbuf), count,
+                                                 datatype.code, op.index, _stream(stream),
+                                                 ctypes.byref(h)),
+                   f"iallreduce({op.name},{datatype.name})")
+        return Request(self, h, f"iallreduce({op.name},{datatype.name})")
+
     def allreduce_init(self, sbuf, rbuf, count: int, datatype: Datatype, op: Op) -> "Plan":
         """MPI_Allreduce_init: a persistent allreduce (collective); start()
         enqueues it without any host rendezvous."""
@@ -199,6 +210,27 @@ class Plan:
         if self._h:
             _lib.check(self._comm._lib.ompi_amd_plan_free(self._h), "plan_free")
             self._h = None
+
+
+class Request:
+    """A nonblocking collective (ompi_amd_request_t): test / wait / free."""
+
+    def __init__(self, comm: Communicator, handle, what: str):
+        self._comm, self._h, self._what = comm, handle, what
+
+    def test(self) -> bool:
+        done = ctypes.c_int()
+        _lib.check(self._comm._lib.ompi_amd_request_test(self._h, ctypes.byref(done)),
+                   "test " + self._what)
+        return bool(done.value)
+
+    def wait(self) -> None:
+        _lib.check(self._comm._lib.ompi_amd_request_wait(self._h), "wait " + self._what)
+
+    def free(self) -> None:
+        if self._h:
+            h, self._h = self._h, None
+            _lib.check(self._comm._lib.ompi_amd_request_free(h), "free " + self._what)
 
 
 def block_partition(count: int, nranks: int, block: int) -> tuple[int, int]:

@@ -35,9 +35,10 @@ double now_s() {
 }  // namespace
 
 struct ShmBoot::Slot {
-    std::atomic<uint64_t> seq;
-    char pad[56];
-    char blob[2][kBlob];
+    std::atomic<uint64_t> seq;   // last posted ticket
+    std::atomic<uint64_t> done;  // last ticket whose blobs this rank has read
+    char pad[48];
+    char blob[kRing][kBlob];
 };
 
 ShmBoot::Slot *ShmBoot::slot(int r) const {
@@ -106,7 +107,7 @@ int ShmBoot::attach(const char *name, int rank, int size, double timeout_s) {
             return OMPI_AMD_ERR_BOOTSTRAP;
         }
     }
-    seq_ = 0;
+    seq_ = done_ = 0;
     int rc = barrier();  // everyone attached
     if (rc == OMPI_AMD_SUCCESS && rank == 0) {
         shm_unlink(name_);  // the mappings keep it alive; nothing leaks on a crash
@@ -124,29 +125,68 @@ void ShmBoot::detach() {
     unlinked_ = true;
 }
 
-int ShmBoot::allgather(const void *mine, void *all, size_t len) {
+int ShmBoot::post(const void *mine, size_t len, uint64_t *ticket) {
     if (!map_ || len > kBlob) return OMPI_AMD_ERR_BAD_PARAM;
-    const uint64_t s = ++seq_;
+    const uint64_t s = seq_ + 1;
+    // ring slot s % kRing last held ticket s - kRing: every rank must have
+    // read it before it is overwritten
+    const double t0 = now_s();
+    if (s > kRing) {
+        for (int r = 0; r < size_; ++r) {
+            unsigned spins = 0;
+            while (slot(r)->done.load(std::memory_order_acquire) < s - kRing) {
+                if (++spins > 1024) {
+                    if (now_s() - t0 > timeout_s_) {
+                        record_msg("%s: rank %d never consumed rendezvous %llu", name_, r,
+                                   (unsigned long long)(s - kRing));
+                        return OMPI_AMD_ERR_TIMEOUT;
+                    }
+                    sched_yield();
+                }
+            }
+        }
+    }
     Slot *me = slot(rank_);
-    if (len) memcpy(me->blob[s & 1], mine, len);
+    if (len) memcpy(me->blob[s % kRing], mine, len);
     me->seq.store(s, std::memory_order_release);
+    seq_ = s;
+    *ticket = s;
+    return OMPI_AMD_SUCCESS;
+}
+
+int ShmBoot::test(uint64_t ticket, void *all, size_t len, bool block, bool *ready) {
+    *ready = false;
+    if (!map_ || len > kBlob || ticket != done_ + 1 || ticket > seq_) return OMPI_AMD_ERR_BAD_PARAM;
     const double t0 = now_s();
     for (int r = 0; r < size_; ++r) {
         Slot *p = slot(r);
         unsigned spins = 0;
-        while (p->seq.load(std::memory_order_acquire) < s) {
+        while (p->seq.load(std::memory_order_acquire) < ticket) {
+            if (!block) return OMPI_AMD_SUCCESS;
             if (++spins > 1024) {
                 if (now_s() - t0 > timeout_s_) {
                     record_msg("%s: rank %d never reached rendezvous %llu", name_, r,
-                               (unsigned long long)s);
+                               (unsigned long long)ticket);
                     return OMPI_AMD_ERR_TIMEOUT;
                 }
                 sched_yield();
             }
         }
-        if (len) memcpy(static_cast<char *>(all) + (size_t)r * len, p->blob[s & 1], len);
     }
+    for (int r = 0; r < size_ && len; ++r)
+        memcpy(static_cast<char *>(all) + (size_t)r * len, slot(r)->blob[ticket % kRing], len);
+    done_ = ticket;
+    slot(rank_)->done.store(ticket, std::memory_order_release);
+    *ready = true;
     return OMPI_AMD_SUCCESS;
+}
+
+int ShmBoot::allgather(const void *mine, void *all, size_t len) {
+    uint64_t t = 0;
+    bool ready = false;
+    int rc = post(mine, len, &t);
+    if (rc == OMPI_AMD_SUCCESS) rc = test(t, all, len, true, &ready);
+    return rc;
 }
 
 }  // namespace ompi_amd

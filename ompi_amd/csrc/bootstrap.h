@@ -3,9 +3,15 @@
 // The reference bootstraps through PMIx/the runtime and moves every byte
 // through btl/sm's shared segments (opal/mca/btl/sm/btl_sm_component.c).
 // Here the segment carries only control data: each rank's slot holds a
-// sequence word and two exchange blobs (double-buffered by sequence
-// parity), which is enough for an allgather of IPC handles and a host
+// posted-sequence word, a consumed-sequence word and a ring of kRing
+// exchange blobs, which is enough for an allgather of IPC handles and a host
 // barrier.  Payload never goes through it.
+//
+// An allgather can be split: post() publishes this rank's blob and returns
+// its ticket without waiting; test() completes tickets in order once every
+// rank has posted.  Up to kRing - 1 tickets may be outstanding (a post
+// waits only for ring slots every rank has consumed) — the nonblocking
+// collectives post at call time and complete from progress.
 #pragma once
 
 #include <cstddef>
@@ -16,6 +22,7 @@ namespace ompi_amd {
 class ShmBoot {
   public:
     static constexpr size_t kBlob = 2048;
+    static constexpr uint64_t kRing = 8;
 
     ShmBoot() = default;
     ~ShmBoot();
@@ -28,6 +35,14 @@ class ShmBoot {
     // Every rank contributes `len` (<= kBlob) bytes; `all` receives size*len.
     int allgather(const void *mine, void *all, size_t len);
     int barrier() { return allgather(nullptr, nullptr, 0); }
+    // Split allgather.  post(): *ticket = this contribution's sequence.
+    // test(): tickets complete in posting order; *ready = 1 once every rank
+    // posted `ticket` (then `all` holds the blobs), 0 if not yet.  With
+    // block = true it waits (bounded by the attach timeout).
+    int post(const void *mine, size_t len, uint64_t *ticket);
+    int test(uint64_t ticket, void *all, size_t len, bool block, bool *ready);
+    uint64_t posted() const { return seq_; }
+    uint64_t consumed() const { return done_; }
 
   private:
     struct Slot;
@@ -36,7 +51,7 @@ class ShmBoot {
     void *map_ = nullptr;
     size_t bytes_ = 0;
     int rank_ = -1, size_ = 0;
-    uint64_t seq_ = 0;
+    uint64_t seq_ = 0, done_ = 0;
     double timeout_s_ = 60.0;
     bool unlinked_ = false;
 };

@@ -56,6 +56,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <new>
 #include <utility>
 #include <vector>
@@ -538,9 +539,51 @@ static red_order tuned_reduce_order(int n, size_t msg, size_t count, int root, b
     return {ORDER_CHAIN, root, fl};                      // pipeline, 32/64 KiB segments
 }
 
+// What each rank publishes per zero-copy call: its user buffers as
+// (allocation handle, offset).
+struct buf_desc {
+    hipIpcMemHandle_t h;
+    uint64_t off;
+    uint64_t valid;
+};
+struct call_blob {
+    buf_desc s, r;
+    uint64_t flags;  // per-call rank flags (bit 0: MPI_IN_PLACE)
+};
+
+// The parameters a path decision reads, captured when a nonblocking call is
+// posted so that its deferred launch takes the path every rank agreed on.
+struct path_params {
+    size_t small_bytes, fused_bytes;
+    int zero_copy, algorithm;
+};
+
+// A nonblocking collective posted but not launched yet.  Device work must
+// enter every rank's stream in the same order (the epoch barriers pair by
+// count), so deferred calls launch strictly first-in first-out, and every
+// blocking entry point launches the queue first.
+struct pending_op {
+    uint64_t ticket;  // rendezvous ticket of the handle swap (0: none)
+    const void *sbuf;
+    void *rbuf;
+    size_t count;
+    int type, op;
+    hipStream_t stream;
+    path_params pp;
+    ompi_amd_request *req;
+};
+
 }  // namespace ompi_amd
 
 using namespace ompi_amd;
+
+// A nonblocking collective's completion (MPI_Request of MPI_Iallreduce).
+struct ompi_amd_request {
+    ompi_amd_comm_t *c = nullptr;
+    hipEvent_t ev = nullptr;
+    bool launched = false;  // its kernels are on the stream and `ev` recorded after them
+    int rc = OMPI_AMD_SUCCESS;
+};
 
 // ------------------------------------------------------------------ comm
 struct ompi_amd_comm {
@@ -578,6 +621,10 @@ struct ompi_amd_comm {
     int profile = 0;
     std::vector<hipEvent_t> ev_free;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_phase[2];
+    // nonblocking calls not launched yet, and the swapped blobs of the one
+    // being launched (exchange_bufs takes them instead of a rendezvous)
+    std::deque<pending_op> pending;
+    const call_blob *pre = nullptr;
 };
 
 // A persistent allreduce (MPI_Allreduce_init, coll.h:349-352): buffers,
@@ -604,17 +651,6 @@ struct ipc_blob {
     hipIpcMemHandle_t flags, scratch;
 };
 
-// What each rank publishes per zero-copy call: its user buffers as
-// (allocation handle, offset).
-struct buf_desc {
-    hipIpcMemHandle_t h;
-    uint64_t off;
-    uint64_t valid;
-};
-struct call_blob {
-    buf_desc s, r;
-    uint64_t flags;  // per-call rank flags (bit 0: MPI_IN_PLACE)
-};
 
 static int set_dev(ompi_amd_comm_t *c) {
     return record_hip(hipSetDevice(c->device), "hipSetDevice");
@@ -711,8 +747,12 @@ static int exchange_bufs(ompi_amd_comm_t *c, const void *sbuf, const void *rbuf,
     if (rc == OMPI_AMD_SUCCESS) rc = export_buf(c, rbuf, &mine.r);
     if (rc != OMPI_AMD_SUCCESS) return rc;
     call_blob all[kMaxRanks];
-    rc = c->boot.allgather(&mine, all, sizeof(call_blob));
-    if (rc != OMPI_AMD_SUCCESS) return rc;
+    if (c->pre) {  // a deferred nonblocking call: swapped when it was posted
+        memcpy(all, c->pre, sizeof(call_blob) * (size_t)c->size);
+    } else {
+        rc = c->boot.allgather(&mine, all, sizeof(call_blob));
+        if (rc != OMPI_AMD_SUCCESS) return rc;
+    }
     for (int p = 0; p < c->size; ++p) {
         if (allflags) allflags[p] = all[p].flags;
         if (p == c->rank) {
@@ -1258,6 +1298,107 @@ static int scan_common(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
 
 }  // namespace ompi_amd
 
+static path_params params_of(const ompi_amd_comm_t *c) {
+    return {c->small_bytes, c->fused_bytes, c->zero_copy, c->algorithm};
+}
+
+// Whether an allreduce of `count` elements takes a zero-copy path (and so
+// swaps buffer handles): the complement of the fused / staged conditions of
+// allreduce_impl.
+static bool allreduce_swaps(const ompi_amd_comm_t *c, const path_params &pp, size_t count,
+                            int type) {
+    const int n = c->size;
+    if (n == 1 || count == 0) return false;
+    const size_t bytes = count * ompi_amd_type_extent(type);
+    const bool tree = type_size(type) * count < 10000 || count < (size_t)n;
+    if (bytes <= pp.fused_bytes && bytes <= c->scratch_bytes) return false;
+    return !(bytes <= pp.small_bytes || !pp.zero_copy || tree);
+}
+
+static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
+                          int op, hipStream_t s, const path_params &pp);
+
+// Launch deferred nonblocking calls in posting order, each once every rank
+// has posted its handle-swap half; block = wait for them (the blocking entry
+// points do, so their device work follows the deferred calls' on every rank).
+static int progress(ompi_amd_comm_t *c, bool block) {
+    while (!c->pending.empty()) {
+        pending_op o = c->pending.front();
+        call_blob all[kMaxRanks];
+        int rc = OMPI_AMD_SUCCESS;
+        if (o.ticket) {
+            bool ready = false;
+            rc = c->boot.test(o.ticket, all, sizeof(call_blob), block, &ready);
+            if (rc == OMPI_AMD_SUCCESS && !ready) return OMPI_AMD_SUCCESS;
+        }
+        c->pending.pop_front();
+        if (rc == OMPI_AMD_SUCCESS) {
+            c->pre = o.ticket ? all : nullptr;
+            rc = allreduce_impl(c, o.sbuf, o.rbuf, o.count, o.type, o.op, o.stream, o.pp);
+            c->pre = nullptr;
+        }
+        if (rc == OMPI_AMD_SUCCESS)
+            rc = record_hip(hipEventRecord(o.req->ev, o.stream), "request event");
+        o.req->rc = rc;
+        o.req->launched = true;
+        if (rc != OMPI_AMD_SUCCESS) return rc;
+    }
+    return OMPI_AMD_SUCCESS;
+}
+
+static int drain(ompi_amd_comm_t *c) {
+    return c->pending.empty() ? OMPI_AMD_SUCCESS : progress(c, true);
+}
+
+static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
+                          int op, hipStream_t s, const path_params &pp) {
+    if (count == 0) return OMPI_AMD_SUCCESS;  // allreduce.c:104
+    TRY(set_dev(c));
+    const size_t ext = ompi_amd_type_extent(type);
+    const size_t bytes = count * ext;
+    const bool inplace = in_place(sbuf, rbuf);
+    const void *src = inplace ? rbuf : sbuf;
+    const int n = c->size;
+    if (n == 1) {  // coll/self: copy (or nothing in place)
+        if (inplace) return OMPI_AMD_SUCCESS;
+        return record_hip(hipMemcpyAsync(rbuf, src, bytes, hipMemcpyDeviceToDevice, s), "copy");
+    }
+    // order of coll/tuned's fixed decision: < 10000 B recursive doubling
+    const bool tree = type_size(type) * count < 10000 || count < (size_t)n;
+    if (bytes <= pp.fused_bytes && bytes <= c->scratch_bytes)
+        return allreduce_fused(c, src, rbuf, (int64_t)count, op, type, tree, s);
+    if (!tree && (bytes <= pp.small_bytes || !pp.zero_copy) &&
+        two_shot_fits(c, (int64_t)count, ext))
+        return allreduce_staged_two_shot(c, src, rbuf, (int64_t)count, op, type, s);
+    if (bytes <= pp.small_bytes || !pp.zero_copy || tree) {
+        // staged one-shot: my contribution -> my scratch half, barrier,
+        // every rank folds all blocks from all scratches (no trailing
+        // barrier: see next_half)
+        stage_half sh;
+        TRY(stage_in(c, src, bytes, &sh, s));
+        red_jobs jobs;
+        if (tree) {
+            jobs.n = 1;
+            jobs.j[0] = {0, (int64_t)count, 0, 0, -1};
+        } else {
+            ring_jobs((int64_t)count, n, &jobs, -1);
+        }
+        return launch_reduce(c, op, type, sh.peers, n, one_ptr(rbuf), 1,
+                             tree ? ORDER_TREE : ORDER_RING, 0, jobs, s);
+    }
+    ptr_set sp{}, rp{};
+    if (pp.algorithm == ALG_PUSH) {
+        TRY(ensure_landing(c, push_slot((int64_t)count, n, type) * (size_t)n));
+        TRY(exchange_bufs(c, nullptr, rbuf, &sp, &rp));
+        return allreduce_push(c, src, rp, (int64_t)count, op, type, s);
+    }
+    TRY(exchange_bufs(c, src, rbuf, &sp, &rp));
+    if (inplace) sp = rp;
+    if (pp.algorithm == ALG_PULL_PUSH)
+        return allreduce_pull_push(c, sp, rp, (int64_t)count, op, type, s);
+    return allreduce_pull(c, sp, rp, rbuf, (int64_t)count, op, type, s);
+}
+
 extern "C" {
 
 int ompi_amd_comm_create(const char *name, int rank, int size, int device,
@@ -1332,6 +1473,7 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
 int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     if (!c) return OMPI_AMD_SUCCESS;
     (void)hipSetDevice(c->device);
+    (void)drain(c);  // deferred nonblocking calls every peer will also launch
     (void)hipDeviceSynchronize();
     (void)c->boot.barrier();  // nobody still reads our memory
     for (auto &x : c->imports) (void)hipIpcCloseMemHandle(x.base);
@@ -1404,6 +1546,7 @@ int ompi_amd_comm_phase_ms(ompi_amd_comm_t *c, int phase, double *total_ms, int 
 int ompi_amd_comm_agree(ompi_amd_comm_t *c, int local_ok, int *all_ok) {
     if (!c || !all_ok) return OMPI_AMD_ERR_BAD_PARAM;
     int mine = local_ok ? 1 : 0, all[kMaxRanks];
+    TRY(drain(c));
     TRY(c->boot.allgather(&mine, all, sizeof(int)));
     int ok = 1;
     for (int p = 0; p < c->size; ++p) ok &= all[p];
@@ -1414,6 +1557,7 @@ int ompi_amd_comm_agree(ompi_amd_comm_t *c, int local_ok, int *all_ok) {
 int ompi_amd_comm_sync(ompi_amd_comm_t *c, void *stream) {
     if (!c) return OMPI_AMD_ERR_BAD_PARAM;
     TRY(set_dev(c));
+    TRY(drain(c));
     TRY(record_hip(hipStreamSynchronize(as_stream(stream)), "hipStreamSynchronize"));
     return check_sticky(c);
 }
@@ -1472,57 +1616,58 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     return OMPI_AMD_SUCCESS;
 }
 
+
 int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                        int op, void *stream) {
     if (!c || !rbuf) return OMPI_AMD_ERR_BAD_PARAM;
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
     TRY(check_sticky(c));
-    if (count == 0) return OMPI_AMD_SUCCESS;  // allreduce.c:104
+    TRY(drain(c));
+    return allreduce_impl(c, sbuf, rbuf, count, type, op, as_stream(stream), params_of(c));
+}
+
+int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
+                        int op, void *stream, ompi_amd_request_t **out) {
+    if (!c || !rbuf || !out) return OMPI_AMD_ERR_BAD_PARAM;
+    *out = nullptr;
+    if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
+    TRY(check_sticky(c));
     TRY(set_dev(c));
-    hipStream_t s = as_stream(stream);
-    const size_t ext = ompi_amd_type_extent(type);
-    const size_t bytes = count * ext;
+    auto *req = new (std::nothrow) ompi_amd_request;
+    if (!req) return OMPI_AMD_ERR_BAD_PARAM;
+    req->c = c;
+    int rc = record_hip(hipEventCreateWithFlags(&req->ev, hipEventDisableTiming), "request event");
+    if (rc != OMPI_AMD_SUCCESS) {
+        delete req;
+        return rc;
+    }
+    const path_params pp = params_of(c);
     const bool inplace = in_place(sbuf, rbuf);
-    const void *src = inplace ? rbuf : sbuf;
-    const int n = c->size;
-    if (n == 1) {  // coll/self: copy (or nothing in place)
-        if (inplace) return OMPI_AMD_SUCCESS;
-        return record_hip(hipMemcpyAsync(rbuf, src, bytes, hipMemcpyDeviceToDevice, s), "copy");
-    }
-    // order of coll/tuned's fixed decision: < 10000 B recursive doubling
-    const bool tree = type_size(type) * count < 10000 || count < (size_t)n;
-    if (bytes <= c->fused_bytes && bytes <= c->scratch_bytes)
-        return allreduce_fused(c, src, rbuf, (int64_t)count, op, type, tree, s);
-    if (!tree && (bytes <= c->small_bytes || !c->zero_copy) &&
-        two_shot_fits(c, (int64_t)count, ext))
-        return allreduce_staged_two_shot(c, src, rbuf, (int64_t)count, op, type, s);
-    if (bytes <= c->small_bytes || !c->zero_copy || tree) {
-        // staged one-shot: my contribution -> my scratch half, barrier,
-        // every rank folds all blocks from all scratches (no trailing
-        // barrier: see next_half)
-        stage_half sh;
-        TRY(stage_in(c, src, bytes, &sh, s));
-        red_jobs jobs;
-        if (tree) {
-            jobs.n = 1;
-            jobs.j[0] = {0, (int64_t)count, 0, 0, -1};
-        } else {
-            ring_jobs((int64_t)count, n, &jobs, -1);
+    pending_op o{0, inplace ? rbuf : sbuf, rbuf, count, type, op, as_stream(stream), pp, req};
+    if (allreduce_swaps(c, pp, count, type)) {
+        // post this rank's half of the handle swap now; the launch waits for
+        // the peers' halves (progress / the next collective call)
+        const bool push = pp.algorithm == ALG_PUSH;
+        if (push) {
+            const size_t need = push_slot((int64_t)count, c->size, type) * (size_t)c->size;
+            if (need > c->land_bytes) {  // collective growth: every rank decides alike
+                rc = drain(c);
+                if (rc == OMPI_AMD_SUCCESS) rc = ensure_landing(c, need);
+            }
         }
-        return launch_reduce(c, op, type, sh.peers, n, one_ptr(rbuf), 1,
-                             tree ? ORDER_TREE : ORDER_RING, 0, jobs, s);
+        call_blob mine{};
+        if (rc == OMPI_AMD_SUCCESS && !push) rc = export_buf(c, o.sbuf, &mine.s);
+        if (rc == OMPI_AMD_SUCCESS) rc = export_buf(c, rbuf, &mine.r);
+        if (rc == OMPI_AMD_SUCCESS) rc = c->boot.post(&mine, sizeof(mine), &o.ticket);
+        if (rc != OMPI_AMD_SUCCESS) {
+            (void)hipEventDestroy(req->ev);
+            delete req;
+            return rc;
+        }
     }
-    ptr_set sp{}, rp{};
-    if (c->algorithm == ALG_PUSH) {
-        TRY(ensure_landing(c, push_slot((int64_t)count, n, type) * (size_t)n));
-        TRY(exchange_bufs(c, nullptr, rbuf, &sp, &rp));
-        return allreduce_push(c, src, rp, (int64_t)count, op, type, s);
-    }
-    TRY(exchange_bufs(c, src, rbuf, &sp, &rp));
-    if (inplace) sp = rp;
-    if (c->algorithm == ALG_PULL_PUSH)
-        return allreduce_pull_push(c, sp, rp, (int64_t)count, op, type, s);
-    return allreduce_pull(c, sp, rp, rbuf, (int64_t)count, op, type, s);
+    c->pending.push_back(o);
+    *out = req;
+    return progress(c, false);
 }
 
 int ompi_amd_reduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
@@ -1531,6 +1676,7 @@ int ompi_amd_reduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t cou
         return OMPI_AMD_ERR_BAD_PARAM;
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
     TRY(check_sticky(c));
+    TRY(drain(c));
     if (count == 0) return OMPI_AMD_SUCCESS;
     TRY(set_dev(c));
     hipStream_t s = as_stream(stream);
@@ -1583,6 +1729,7 @@ int ompi_amd_reduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *rb
     if (!c || !rbuf) return OMPI_AMD_ERR_BAD_PARAM;
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
     TRY(check_sticky(c));
+    TRY(drain(c));
     if (rcount == 0) return OMPI_AMD_SUCCESS;
     TRY(set_dev(c));
     hipStream_t s = as_stream(stream);
@@ -1626,6 +1773,7 @@ int ompi_amd_reduce_scatter(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
     if (!c || !rbuf || !rcounts) return OMPI_AMD_ERR_BAD_PARAM;
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
     TRY(check_sticky(c));
+    TRY(drain(c));
     const int n = c->size;
     size_t total = 0, off = 0, maxc = 0;
     for (int p = 0; p < n; ++p) {
@@ -1651,11 +1799,13 @@ int ompi_amd_reduce_scatter(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
 
 int ompi_amd_scan(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                   int op, void *stream) {
+    if (c) TRY(drain(c));
     return scan_common(c, sbuf, rbuf, count, type, op, stream, false);
 }
 
 int ompi_amd_exscan(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                     int op, void *stream) {
+    if (c) TRY(drain(c));
     return scan_common(c, sbuf, rbuf, count, type, op, stream, true);
 }
 
@@ -1663,6 +1813,7 @@ int ompi_amd_allgather(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
                        void *stream) {
     if (!c || !rbuf) return OMPI_AMD_ERR_BAD_PARAM;
     TRY(check_sticky(c));
+    TRY(drain(c));
     if (bytes == 0) return OMPI_AMD_SUCCESS;
     TRY(set_dev(c));
     hipStream_t s = as_stream(stream);
@@ -1694,6 +1845,7 @@ int ompi_amd_allgather(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
 int ompi_amd_bcast(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, void *stream) {
     if (!c || !buf || root < 0 || root >= c->size) return OMPI_AMD_ERR_BAD_PARAM;
     TRY(check_sticky(c));
+    TRY(drain(c));
     if (bytes == 0 || c->size == 1) return OMPI_AMD_SUCCESS;
     TRY(set_dev(c));
     hipStream_t s = as_stream(stream);
@@ -1730,6 +1882,7 @@ int ompi_amd_allreduce_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, si
     if (!c || !rbuf || !out) return OMPI_AMD_ERR_BAD_PARAM;
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
     TRY(check_sticky(c));
+    TRY(drain(c));
     TRY(set_dev(c));
     auto *pl = new (std::nothrow) ompi_amd_plan;
     if (!pl) return OMPI_AMD_ERR_BAD_PARAM;
@@ -1783,6 +1936,7 @@ static int plan_enqueue(ompi_amd_plan_t *pl, void *stream) {
 
 int ompi_amd_plan_start(ompi_amd_plan_t *pl, void *stream) {
     if (!pl || !pl->c) return OMPI_AMD_ERR_BAD_PARAM;
+    TRY(drain(pl->c));  // device order: deferred nonblocking calls first
     TRY(plan_enqueue(pl, stream));
     pl->started = true;
     return record_hip(hipEventRecord(pl->done, as_stream(stream)), "plan completion event");
@@ -1817,6 +1971,42 @@ int ompi_amd_plan_free(ompi_amd_plan_t *pl) {
     if (pl->done) (void)hipEventDestroy(pl->done);
     delete pl;
     return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_request_test(ompi_amd_request_t *r, int *done) {
+    if (!r || !done) return OMPI_AMD_ERR_BAD_PARAM;
+    *done = 0;
+    if (!r->launched) {
+        TRY(set_dev(r->c));
+        TRY(progress(r->c, false));
+        if (!r->launched) return OMPI_AMD_SUCCESS;
+    }
+    if (r->rc != OMPI_AMD_SUCCESS) return r->rc;
+    const hipError_t e = hipEventQuery(r->ev);
+    if (e == hipErrorNotReady) return OMPI_AMD_SUCCESS;
+    if (e != hipSuccess) return record_hip(e, "request test");
+    *done = 1;
+    return check_sticky(r->c);
+}
+
+int ompi_amd_request_wait(ompi_amd_request_t *r) {
+    if (!r) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!r->launched) {
+        TRY(set_dev(r->c));
+        TRY(progress(r->c, true));
+    }
+    if (r->rc != OMPI_AMD_SUCCESS) return r->rc;
+    TRY(record_hip(hipEventSynchronize(r->ev), "request wait"));
+    return check_sticky(r->c);
+}
+
+int ompi_amd_request_free(ompi_amd_request_t *r) {
+    if (!r) return OMPI_AMD_SUCCESS;
+    // the peers launch it whatever this rank does: launch and finish it too
+    const int rc = ompi_amd_request_wait(r);
+    if (r->ev) (void)hipEventDestroy(r->ev);
+    delete r;
+    return rc;
 }
 
 }  // extern "C"

@@ -5,8 +5,9 @@
  * The module provides coll_allreduce, coll_reduce, coll_reduce_scatter,
  * coll_reduce_scatter_block,
  * coll_scan, coll_exscan, coll_allgather, coll_bcast
- * (ompi/mca/coll/coll.h:200-250) and the persistent coll_allreduce_init
- * (coll.h:349-352) for device buffers through libompi_amd.so,
+ * (ompi/mca/coll/coll.h:200-250), the nonblocking coll_iallreduce
+ * (coll.h:271-274) and the persistent coll_allreduce_init (coll.h:349-352)
+ * for device buffers through libompi_amd.so,
  * and interposes on the previously selected functions (coll/tuned, coll/basic
  * for scan/exscan) for everything else, exactly like coll/cuda does
  * (ompi/mca/coll/cuda/coll_cuda_module.c:120-155).
@@ -48,12 +49,14 @@ typedef struct mca_coll_rocm_component_t {
 
 OMPI_MODULE_DECLSPEC extern mca_coll_rocm_component_t mca_coll_rocm_component;
 
-/* A persistent device collective (MPI_Allreduce_init).  Start enqueues the
- * plan's kernels; the component's progress callback completes the request
- * once the plan's completion event has fired. */
+/* A device collective's MPI request: persistent (MPI_Allreduce_init: a
+ * library plan, started by req_start) or nonblocking (MPI_Iallreduce: a
+ * library request).  The component's progress callback completes it once
+ * the library reports its device work finished. */
 typedef struct mca_coll_rocm_request_t {
     ompi_request_t super;
-    ompi_amd_plan_t *plan;
+    ompi_amd_plan_t *plan;       /* persistent */
+    ompi_amd_request_t *nbreq;   /* nonblocking */
     struct mca_coll_rocm_request_t *next_active; /* started, not yet complete */
 } mca_coll_rocm_request_t;
 
@@ -87,6 +90,10 @@ int mca_coll_rocm_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount,
 int mca_coll_rocm_allgather(const void *sbuf, int scount, struct ompi_datatype_t *sdtype,
                             void *rbuf, int rcount, struct ompi_datatype_t *rdtype,
                             struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+int mca_coll_rocm_iallreduce(const void *sbuf, void *rbuf, int count,
+                             struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                             struct ompi_communicator_t *comm, ompi_request_t **request,
+                             mca_coll_base_module_t *module);
 int mca_coll_rocm_allreduce_init(const void *sbuf, void *rbuf, int count,
                                  struct ompi_datatype_t *dtype, struct ompi_op_t *op,
                                  struct ompi_communicator_t *comm, struct ompi_info_t *info,

@@ -18,10 +18,13 @@
  * Persistent allreduce (MPI_Allreduce_init) builds a library plan (the
  * peers' buffer mappings are swapped and pinned once, at init) behind an
  * ompi_request_t: req_start enqueues the plan's kernels with no host
- * rendezvous and puts the request on the active list; the progress
- * callback (registered with opal_progress, as coll/libnbc does,
- * coll_libnbc_component.c:430-475) completes it when the plan's completion
- * event has fired, carrying a device-side failure into req_status.
+ * rendezvous and puts the request on the active list.  Nonblocking
+ * allreduce (MPI_Iallreduce) posts a library request (it never waits for a
+ * peer) and goes on the same list.  The progress callback (registered with
+ * opal_progress, as coll/libnbc does, coll_libnbc_component.c:430-475)
+ * completes a request when the library reports its device work finished
+ * (and, for iallreduce, launches deferred work whose handle swap is
+ * complete), carrying a device-side failure into req_status.
  */
 #include "ompi_config.h"
 
@@ -119,6 +122,7 @@ static void rocm_module_destruct(mca_coll_rocm_module_t *m)
     if (NULL != m->c_coll.coll_bcast_module) OBJ_RELEASE(m->c_coll.coll_bcast_module);
     if (NULL != m->c_coll.coll_allreduce_init_module)
         OBJ_RELEASE(m->c_coll.coll_allreduce_init_module);
+    if (NULL != m->c_coll.coll_iallreduce_module) OBJ_RELEASE(m->c_coll.coll_iallreduce_module);
     if (NULL != m->dev_comm) (void) ompi_amd_comm_destroy(m->dev_comm);
 }
 
@@ -151,6 +155,7 @@ mca_coll_base_module_t *mca_coll_rocm_comm_query(struct ompi_communicator_t *com
     m->super.coll_reduce_scatter_block = mca_coll_rocm_reduce_scatter_block;
     m->super.coll_allgather = mca_coll_rocm_allgather;
     m->super.coll_bcast = mca_coll_rocm_bcast;
+    m->super.coll_iallreduce = mca_coll_rocm_iallreduce;
     m->super.coll_allreduce_init = mca_coll_rocm_allreduce_init;
     return &m->super;
 }
@@ -176,6 +181,7 @@ int mca_coll_rocm_module_enable(mca_coll_base_module_t *module, struct ompi_comm
     SAVE(reduce_scatter_block);
     SAVE(allgather);
     SAVE(bcast);
+    SAVE(iallreduce);
     SAVE(allreduce_init);
 #undef SAVE
 
@@ -399,7 +405,8 @@ static int rocm_progress(void)
     while (NULL != *pp) {
         mca_coll_rocm_request_t *r = *pp;
         int fin = 0;
-        const int rc = ompi_amd_plan_test(r->plan, &fin);
+        const int rc = NULL != r->plan ? ompi_amd_plan_test(r->plan, &fin)
+                                       : ompi_amd_request_test(r->nbreq, &fin);
         if (OMPI_AMD_SUCCESS != rc || fin) {
             r->super.req_status.MPI_ERROR = to_ompi_err(rc);
             *pp = r->next_active;
@@ -418,6 +425,18 @@ static int rocm_progress(void)
         ++completed;
     }
     return completed;
+}
+
+static void rocm_link_active(mca_coll_rocm_request_t *r)
+{
+    OPAL_THREAD_LOCK(&rocm_active_lock);
+    r->next_active = rocm_active;
+    rocm_active = r;
+    if (!rocm_progress_registered) {
+        rocm_progress_registered = 1;
+        (void) opal_progress_register(rocm_progress);
+    }
+    OPAL_THREAD_UNLOCK(&rocm_active_lock);
 }
 
 static void rocm_unlink_active(mca_coll_rocm_request_t *r)
@@ -454,20 +473,13 @@ static int rocm_request_start(size_t count, ompi_request_t **requests)
             ompi_request_complete(&r->super, true);
             return to_ompi_err(rc);
         }
-        OPAL_THREAD_LOCK(&rocm_active_lock);
-        r->next_active = rocm_active;
-        rocm_active = r;
-        if (!rocm_progress_registered) {
-            rocm_progress_registered = 1;
-            (void) opal_progress_register(rocm_progress);
-        }
-        OPAL_THREAD_UNLOCK(&rocm_active_lock);
+        rocm_link_active(r);
     }
     return OMPI_SUCCESS;
 }
 
 /* MPI_Request_free: an active request's device work is waited for first —
- * the plan's peers may still read this rank's buffers through it. */
+ * peers may still read this rank's buffers through it. */
 static int rocm_request_free(ompi_request_t **rptr)
 {
     mca_coll_rocm_request_t *r = (mca_coll_rocm_request_t *) *rptr;
@@ -477,6 +489,10 @@ static int rocm_request_free(ompi_request_t **rptr)
         rc = ompi_amd_plan_wait(r->plan);
         (void) ompi_amd_plan_free(r->plan);
         r->plan = NULL;
+    }
+    if (NULL != r->nbreq) {
+        rc = ompi_amd_request_free(r->nbreq);
+        r->nbreq = NULL;
     }
     OMPI_REQUEST_FINI(&r->super);
     OBJ_RELEASE(r);
@@ -492,10 +508,49 @@ static void rocm_request_construct(mca_coll_rocm_request_t *r)
     r->super.req_free = rocm_request_free;
     r->super.req_cancel = NULL;
     r->plan = NULL;
+    r->nbreq = NULL;
     r->next_active = NULL;
 }
 
 OBJ_CLASS_INSTANCE(mca_coll_rocm_request_t, ompi_request_t, rocm_request_construct, NULL);
+
+/* MPI_Iallreduce (coll.h:271-274).  The path agreement is the one host
+ * rendezvous that precedes the call's own (nonblocking) post: every rank
+ * reaches it at the same collective, as for the blocking allreduce. */
+int mca_coll_rocm_iallreduce(const void *sbuf, void *rbuf, int count,
+                             struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                             struct ompi_communicator_t *comm, ompi_request_t **request,
+                             mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const int t = type_code(dtype);
+    const int ok = t >= 0 && ompi_op_is_intrinsic(op) &&
+                   ompi_amd_op_supported(op->o_f_to_c_index, t) && dev(sbuf) && dev(rbuf);
+    mca_coll_rocm_request_t *r;
+    ompi_amd_request_t *nb = NULL;
+    int rc;
+    if (!take_device_path(m, ok)) {
+        return m->c_coll.coll_iallreduce(sbuf, rbuf, count, dtype, op, comm, request,
+                                         m->c_coll.coll_iallreduce_module);
+    }
+    r = OBJ_NEW(mca_coll_rocm_request_t);
+    if (NULL == r) return OMPI_ERROR;
+    rc = ompi_amd_iallreduce(m->dev_comm, MPI_IN_PLACE == sbuf ? rbuf : sbuf, rbuf,
+                             (size_t) count, t, op->o_f_to_c_index, NULL, &nb);
+    if (OMPI_AMD_SUCCESS != rc) {
+        if (NULL != nb) (void) ompi_amd_request_free(nb);
+        OBJ_RELEASE(r);
+        return to_ompi_err(rc);
+    }
+    OMPI_REQUEST_INIT(&r->super, false);
+    r->super.req_state = OMPI_REQUEST_ACTIVE;
+    r->super.req_mpi_object.comm = comm;
+    r->super.req_status.MPI_ERROR = OMPI_SUCCESS;
+    r->nbreq = nb;
+    rocm_link_active(r);
+    *request = &r->super;
+    return OMPI_SUCCESS;
+}
 
 /* MPI_Allreduce_init (coll.h:349-352).  Collective: the path decision is
  * agreed like the blocking allreduce's, and on the device path the plan's

@@ -225,6 +225,56 @@ def case_persistent(comm, rank, n, dt, op, count, salt, inplace=False, starts=3)
         plan.free()
 
 
+def case_iallreduce(comm, rank, n, salt, check_nonblocking=True):
+    """MPI_Iallreduce: the calls return without waiting for any peer (rank 0
+    posts while the others still sleep), five are outstanding at once
+    (fused, staged and zero-copy sizes, one in place), a blocking collective
+    runs in between, completion by test polling and wait; every result
+    checked against the oracle."""
+    import time
+    F, D, I32 = mop.MPI_FLOAT, mop.MPI_DOUBLE, mop.MPI_INT32_T
+    calls = [(F, mop.MPI_SUM, 3001, False), (F, mop.MPI_SUM, 600001, False),
+             (I32, mop.MPI_MAX, 20000, False), (D, mop.MPI_SUM, 300003, True),
+             (F, mop.MPI_SUM, (1 << 20) + 3, False)]
+    prepared = []
+    for i, (dt, op, cnt, ip) in enumerate(calls):
+        xs = [inputs(dt, cnt, r, salt + i) for r in range(n)]
+        exp, _ = orc.allreduce([x.copy() for x in xs], cnt, op.index, dt.code)
+        s = to_dev(xs[rank])
+        out = s if ip else torch.zeros_like(s)
+        prepared.append((dt, op, cnt, ip, s, out, exp[rank]))
+    torch.cuda.synchronize()
+    dist.barrier()
+    if rank != 0:
+        time.sleep(0.5)
+    t0 = time.perf_counter()
+    reqs = [comm.iallreduce(coll.IN_PLACE if ip else s, out, cnt, dt, op)
+            for dt, op, cnt, ip, s, out, _ in prepared]
+    posted = time.perf_counter() - t0
+    msgs = []
+    if rank == 0 and check_nonblocking:
+        t1 = time.perf_counter()
+        early = reqs[1].test()
+        tested = time.perf_counter() - t1
+        if posted > 0.3 or tested > 0.1 or early:
+            msgs.append(f"blocked: post {posted:.3f}s test {tested:.3f}s done-early {early}")
+    other = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    comm.bcast(other, 4096, 0)  # a blocking collective with requests outstanding
+    while not reqs[0].test():
+        pass
+    for r in reqs[1:]:
+        r.wait()
+    torch.cuda.synchronize()
+    for r in reqs:
+        r.free()
+    for i, (dt, op, cnt, ip, s, out, exp) in enumerate(prepared):
+        got = out.cpu().numpy()[:cnt * dt.extent].view(dt.np_dtype)
+        ok, msg = checked(got, exp)
+        if not ok:
+            msgs.append(f"call {i}: {msg}")
+    return not msgs, "; ".join(msgs)
+
+
 def case_allgather(comm, rank, n, nbytes, salt, inplace=False):
     xs = [np.random.default_rng(SEED + salt + r).integers(0, 256, nbytes, dtype=np.uint8)
           for r in range(n)]
@@ -400,6 +450,7 @@ def main():
          lambda: case_scan(comm, rank, n, I8, mop.MPI_PROD, 70001, 55, True, True)),
     ]
     cases += [
+        ("iallreduce_mixed", lambda: case_iallreduce(comm, rank, n, 90)),
         ("persistent_small", lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, 3001, 80)),
         ("persistent_mid_inplace",
          lambda: case_persistent(comm, rank, n, D, mop.MPI_SUM, 70001, 81, inplace=True)),
@@ -431,6 +482,8 @@ def main():
             (f"alg{alg}_ar_max_f32_specials",
              with_alg(lambda: case_allreduce(comm, rank, n, F, mop.MPI_MAX, 300001, 65, "S"))),
             (f"alg{alg}_pipelined_nonblocking", with_alg(lambda: case_pipelined(comm, rank, n, 66))),
+            (f"alg{alg}_iallreduce_mixed",
+             with_alg(lambda: case_iallreduce(comm, rank, n, 91, check_nonblocking=False))),
             (f"alg{alg}_persistent_big",
              with_alg(lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, big + 1, 84))),
             (f"alg{alg}_persistent_big_inplace",

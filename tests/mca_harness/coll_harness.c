@@ -13,7 +13,8 @@
  *   oracle bit for bit; host buffers, mixed residency across ranks and
  *   non-intrinsic ops go to the saved functions on every rank.  A
  *   persistent allreduce request is started and completed through
- *   opal_progress the way MPI_Start / MPI_Wait drive it.
+ *   opal_progress the way MPI_Start / MPI_Wait drive it, and so are
+ *   nonblocking allreduce requests.
  *
  * usage: coll_harness <segment-name> <rank> <size>; prints "ok" / "ok gpu".
  */
@@ -112,6 +113,11 @@ static int t_ar_init(const void *s, void *r, int c, struct ompi_datatype_t *d, s
                      ompi_request_t **req, mca_coll_base_module_t *m)
 { tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
 
+static int t_iallreduce(const void *s, void *r, int c, struct ompi_datatype_t *d,
+                        struct ompi_op_t *o, struct ompi_communicator_t *cm, ompi_request_t **req,
+                        mca_coll_base_module_t *m)
+{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
+
 static void fill_tuned(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *tm)
 {
     memset(t, 0, sizeof(*t));
@@ -124,6 +130,7 @@ static void fill_tuned(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *tm)
     SET(exscan, t_scan);
     SET(allgather, t_allgather);
     SET(bcast, t_bcast);
+    SET(iallreduce, t_iallreduce);
     SET(allreduce_init, t_ar_init);
 #undef SET
 }
@@ -135,7 +142,7 @@ static void install(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *m)
                                       t->coll_##fn##_module = m; OBJ_RETAIN(m); }
     INST(allreduce) INST(reduce) INST(reduce_scatter) INST(reduce_scatter_block) INST(scan)
     INST(exscan)
-    INST(allgather) INST(bcast) INST(allreduce_init)
+    INST(allgather) INST(bcast) INST(iallreduce) INST(allreduce_init)
 #undef INST
 }
 
@@ -149,6 +156,7 @@ static void release_table(mca_coll_base_comm_coll_t *t)
     OBJ_RELEASE(t->coll_exscan_module);
     OBJ_RELEASE(t->coll_allgather_module);
     OBJ_RELEASE(t->coll_bcast_module);
+    OBJ_RELEASE(t->coll_iallreduce_module);
     OBJ_RELEASE(t->coll_allreduce_init_module);
 }
 
@@ -222,7 +230,7 @@ int main(int argc, char **argv)
     CHECK(m != NULL && prio == 80, "comm_query on a local intra-communicator");
     CHECK(m->coll_allreduce && m->coll_reduce && m->coll_reduce_scatter &&
               m->coll_reduce_scatter_block && m->coll_scan &&
-              m->coll_exscan && m->coll_allgather && m->coll_bcast && m->coll_allreduce_init &&
+              m->coll_exscan && m->coll_allgather && m->coll_bcast && m->coll_allreduce_init && m->coll_iallreduce &&
               m->coll_module_enable,
           "module function table");
     {
@@ -247,7 +255,7 @@ int main(int argc, char **argv)
     }
 
     CHECK(m->coll_module_enable(m, &comm) == OMPI_SUCCESS, "enable");
-    CHECK(tm->super.obj_reference_count == 1 + 9 + 9, "enable retains the saved modules (%d)",
+    CHECK(tm->super.obj_reference_count == 1 + 10 + 10, "enable retains the saved modules (%d)",
           tm->super.obj_reference_count);
     install(&table, m);
 
@@ -487,6 +495,53 @@ int main(int argc, char **argv)
                                             table.coll_allreduce_init_module) == OMPI_SUCCESS &&
                       tuned_calls == 1 && req == &t_request,
                   "host allreduce_init falls back");
+        }
+    }
+    /* 8. nonblocking allreduce (MPI_Iallreduce): staged and zero-copy sizes
+     * outstanding together, completed through opal_progress, then freed */
+    {
+        const size_t counts[2] = {1000, 300001};
+        float **xs[2], **rb[2];
+        void *ds[2], *dr[2];
+        ompi_request_t *req[2];
+        tuned_calls = 0;
+        for (int k = 0; k < 2; ++k) {
+            const size_t n = counts[k];
+            xs[k] = all_inputs(n, 70 + k);
+            rb[k] = malloc(sizeof(float *) * (size_t) g_size);
+            for (int r = 0; r < g_size; ++r) rb[k][r] = calloc(n, sizeof(float));
+            CHECK(orc_allreduce(ORC_AR_TUNED, g_size, (const void *const *) xs[k],
+                                (void *const *) rb[k], n, ORC_OP_SUM, ORC_T_FLOAT, 0) >= 0,
+                  "oracle allreduce");
+            ds[k] = dev_of(xs[k][g_rank], n * 4);
+            dr[k] = dev_of(rb[k][g_rank], n * 4);
+            CHECK(harness_dev_copy_in(dr[k], xs[k][(g_rank + 1) % g_size], n * 4) == 0, "junk");
+            CHECK(table.coll_iallreduce(ds[k], dr[k], (int) n, &dfloat, &sum, &comm, &req[k],
+                                        table.coll_iallreduce_module) == OMPI_SUCCESS,
+                  "iallreduce");
+            CHECK(req[k] != NULL && !req[k]->req_persistent &&
+                      req[k]->req_type == OMPI_REQUEST_COLL, "iallreduce request");
+        }
+        CHECK(tuned_calls == 0, "device iallreduce fell back");
+        for (int k = 1; k >= 0; --k) {
+            harness_wait(req[k]);
+            CHECK(req[k]->req_status.MPI_ERROR == OMPI_SUCCESS, "iallreduce status");
+            expect_dev(dr[k], rb[k][g_rank], counts[k] * 4, "iallreduce");
+            CHECK(req[k]->req_free(&req[k]) == OMPI_SUCCESS && req[k] == MPI_REQUEST_NULL,
+                  "iallreduce free");
+            harness_dev_free(ds[k]);
+            harness_dev_free(dr[k]);
+            for (int r = 0; r < g_size; ++r) free(rb[k][r]);
+            free(rb[k]);
+            free_inputs(xs[k]);
+        }
+        {
+            float h[16] = {0}, h2[16] = {0};
+            ompi_request_t *hr = NULL;
+            CHECK(table.coll_iallreduce(h, h2, 16, &dfloat, &sum, &comm, &hr,
+                                        table.coll_iallreduce_module) == OMPI_SUCCESS &&
+                      tuned_calls == 1 && hr == &t_request,
+                  "host iallreduce falls back");
         }
     }
     /* teardown: the table's references, then the module (its destructor
