@@ -133,7 +133,10 @@ int ompi_amd_allreduce_init(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
 int ompi_amd_plan_start(ompi_amd_plan_t *plan, void *stream);
 /* Completion of the last start (the request's MPI_Test / MPI_Wait):
  * *done = 1 once the device work finished (or nothing was started); a
- * device-side failure (barrier timeout) is returned as its error code. */
+ * device-side failure (barrier timeout) is returned as its error code.
+ * The completion point is marked on the start's stream at the first test /
+ * wait after the start (keeping the start itself to kernel launches), so
+ * work queued on that stream in between also has to finish first. */
 int ompi_amd_plan_test(ompi_amd_plan_t *plan, int *done);
 int ompi_amd_plan_wait(ompi_amd_plan_t *plan);
 int ompi_amd_plan_free(ompi_amd_plan_t *plan);
@@ -151,7 +154,8 @@ int ompi_amd_plan_free(ompi_amd_plan_t *plan);
 int ompi_amd_iallreduce(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf, size_t count,
                         int type, int op, void *stream, ompi_amd_request_t **request);
 /* *done = 1 once the collective's device work finished; launches deferred
- * calls whose swap completed (never waits for a peer). */
+ * calls whose swap completed (never waits for a peer).  As for plans, the
+ * completion point is marked at the first test / wait after the launch. */
 int ompi_amd_request_test(ompi_amd_request_t *request, int *done);
 /* Waits for the peers' swap halves (if needed) and for the device work. */
 int ompi_amd_request_wait(ompi_amd_request_t *request);

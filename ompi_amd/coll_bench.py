@@ -154,6 +154,7 @@ def bench_allreduce(args, metric: str, link_gbs: float):
             res["sweep"] = _sweep(comm, dist, torch, mop, world, shared, tdev)
             res["config5"] = _config5(comm, dist, torch, mop, world, rank, tdev)
             res["variants"] = _variants(comm, dist, torch, mop, world, tdev)
+            res["next_rows"] = _next_rows(comm, dist, torch, mop, world, rank, tdev)
         except Exception as e:  # extras never break the headline line
             res["extras_error"] = f"{type(e).__name__}: {e}"
     comm.free()
@@ -276,3 +277,55 @@ def _variants(comm, dist, torch, mop, world, tdev):
     comm.set_param("fused_bytes", 64 << 10)
     comm.set_param("small_bytes", 1 << 20)
     return out
+
+
+def _next_rows(comm, dist, torch, mop, world, rank, tdev):
+    """SURVEY §8f rows 2-3 measured beside the headline: reduce_scatter
+    (uneven counts), scan / exscan, and allreduce as a plain call, a
+    persistent plan start (MPI_Allreduce_init: no handle swap per start)
+    and a nonblocking post + wait (MPI_Iallreduce), per size."""
+    F, SUM = mop.MPI_FLOAT, mop.MPI_SUM
+    res = {}
+    # reduce_scatter, 64 MiB total, rank r gets (1 + r/N) shares
+    weights = [world + r for r in range(world)]
+    total = (64 << 20) // 4
+    rcounts = [total * w // sum(weights) for w in weights]
+    x = torch.ones(sum(rcounts), device="cuda")
+    y = torch.empty(max(rcounts), device="cuda")
+    t = _timed(lambda: comm.reduce_scatter(x, y, rcounts, F, SUM), 10, 3, dist, torch, tdev) / 10
+    S = sum(rcounts) * 4
+    res["reduce_scatter_f32_uneven"] = {"bytes_total": S, "us": round(t * 1e6, 2),
+                                        "busbw": round(S / t * (world - 1) / world / 1e9, 3)}
+    del x, y
+    for name, fn in (("scan", comm.scan), ("exscan", comm.exscan)):
+        n = (16 << 20) // 4
+        x = torch.ones(n, device="cuda")
+        y = torch.empty_like(x)
+        t = _timed(lambda: fn(x, y, n, F, SUM), 10, 3, dist, torch, tdev) / 10
+        res[f"{name}_f32_16MiB"] = {"bytes": n * 4, "us": round(t * 1e6, 2),
+                                    "algbw": round(n * 4 / t / 1e9, 3)}
+        del x, y
+    rows = []
+    for nbytes in (64 << 10, 1 << 20, 16 << 20, 256 << 20):
+        n = nbytes // 4
+        x = torch.ones(n, device="cuda")
+        y = torch.empty_like(x)
+        steps = 20 if nbytes <= (16 << 20) else 5
+        row = {"bytes": nbytes}
+        t = _timed(lambda: comm.allreduce(x, y, n, F, SUM), steps, 3, dist, torch, tdev) / steps
+        row["allreduce_us"] = round(t * 1e6, 2)
+        plan = comm.allreduce_init(x, y, n, F, SUM)
+        t = _timed(lambda: plan.start(), steps, 3, dist, torch, tdev) / steps
+        plan.free()
+        row["persistent_start_us"] = round(t * 1e6, 2)
+
+        def post_wait():
+            r = comm.iallreduce(x, y, n, F, SUM)
+            r.wait()
+            r.free()
+        t = _timed(post_wait, steps, 3, dist, torch, tdev) / steps
+        row["iallreduce_post_wait_us"] = round(t * 1e6, 2)
+        rows.append(row)
+        del x, y
+    res["allreduce_call_kinds"] = rows
+    return res

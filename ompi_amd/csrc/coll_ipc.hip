@@ -581,7 +581,9 @@ using namespace ompi_amd;
 struct ompi_amd_request {
     ompi_amd_comm_t *c = nullptr;
     hipEvent_t ev = nullptr;
-    bool launched = false;  // its kernels are on the stream and `ev` recorded after them
+    hipStream_t stream = nullptr;
+    bool launched = false;  // its kernels are on `stream`
+    bool recorded = false;  // `ev` recorded after them (lazily, at the first test / wait)
     int rc = OMPI_AMD_SUCCESS;
 };
 
@@ -639,8 +641,12 @@ struct ompi_amd_plan {
     int kind = 0;      // 0: small paths (as a plain call), 1 pull, 2 pull+push, 3 push
     ptr_set sp{}, rp{};
     void *bases[OMPI_AMD_MAX_RANKS][2] = {};  // pinned peer mappings
-    hipEvent_t done = nullptr;                // recorded at the end of every start
-    bool started = false;
+    // completion: recorded on the start's stream at the first test / wait
+    // after a start (a later point in the stream, so never early; keeps an
+    // event record out of the start itself)
+    hipEvent_t done = nullptr;
+    hipStream_t stream = nullptr;
+    bool started = false, recorded = false;
 };
 
 namespace ompi_amd {
@@ -1337,8 +1343,7 @@ static int progress(ompi_amd_comm_t *c, bool block) {
             rc = allreduce_impl(c, o.sbuf, o.rbuf, o.count, o.type, o.op, o.stream, o.pp);
             c->pre = nullptr;
         }
-        if (rc == OMPI_AMD_SUCCESS)
-            rc = record_hip(hipEventRecord(o.req->ev, o.stream), "request event");
+        o.req->stream = o.stream;
         o.req->rc = rc;
         o.req->launched = true;
         if (rc != OMPI_AMD_SUCCESS) return rc;
@@ -1939,13 +1944,19 @@ int ompi_amd_plan_start(ompi_amd_plan_t *pl, void *stream) {
     TRY(drain(pl->c));  // device order: deferred nonblocking calls first
     TRY(plan_enqueue(pl, stream));
     pl->started = true;
-    return record_hip(hipEventRecord(pl->done, as_stream(stream)), "plan completion event");
+    pl->recorded = false;
+    pl->stream = as_stream(stream);
+    return OMPI_AMD_SUCCESS;
 }
 
 int ompi_amd_plan_test(ompi_amd_plan_t *pl, int *done) {
     if (!pl || !done) return OMPI_AMD_ERR_BAD_PARAM;
     *done = 1;
     if (!pl->started) return OMPI_AMD_SUCCESS;
+    if (!pl->recorded) {
+        TRY(record_hip(hipEventRecord(pl->done, pl->stream), "plan completion event"));
+        pl->recorded = true;
+    }
     const hipError_t e = hipEventQuery(pl->done);
     if (e == hipErrorNotReady) {
         *done = 0;
@@ -1958,6 +1969,10 @@ int ompi_amd_plan_test(ompi_amd_plan_t *pl, int *done) {
 int ompi_amd_plan_wait(ompi_amd_plan_t *pl) {
     if (!pl) return OMPI_AMD_ERR_BAD_PARAM;
     if (!pl->started) return OMPI_AMD_SUCCESS;
+    if (!pl->recorded) {
+        TRY(record_hip(hipEventRecord(pl->done, pl->stream), "plan completion event"));
+        pl->recorded = true;
+    }
     TRY(record_hip(hipEventSynchronize(pl->done), "plan wait"));
     return check_sticky(pl->c);
 }
@@ -1982,6 +1997,10 @@ int ompi_amd_request_test(ompi_amd_request_t *r, int *done) {
         if (!r->launched) return OMPI_AMD_SUCCESS;
     }
     if (r->rc != OMPI_AMD_SUCCESS) return r->rc;
+    if (!r->recorded) {
+        TRY(record_hip(hipEventRecord(r->ev, r->stream), "request event"));
+        r->recorded = true;
+    }
     const hipError_t e = hipEventQuery(r->ev);
     if (e == hipErrorNotReady) return OMPI_AMD_SUCCESS;
     if (e != hipSuccess) return record_hip(e, "request test");
@@ -1996,6 +2015,10 @@ int ompi_amd_request_wait(ompi_amd_request_t *r) {
         TRY(progress(r->c, true));
     }
     if (r->rc != OMPI_AMD_SUCCESS) return r->rc;
+    if (!r->recorded) {
+        TRY(record_hip(hipEventRecord(r->ev, r->stream), "request event"));
+        r->recorded = true;
+    }
     TRY(record_hip(hipEventSynchronize(r->ev), "request wait"));
     return check_sticky(r->c);
 }
