@@ -1,0 +1,102 @@
+/*
+ * ompi_amd — one-sided communication on device windows of the ranks of one
+ * node.  Replaces, for device memory, osc/sm's module
+ * functions (ompi/mca/osc/sm/osc_sm_comm.c, osc_sm_active_target.c,
+ * osc_sm_passive_target.c) behind the osc framework's module table
+ * (ompi/mca/osc/osc.h):
+ *
+ *   osc_put / osc_get              osc_sm_comm.c:209-268
+ *   osc_accumulate                 osc_sm_comm.c:271-309
+ *   osc_get_accumulate             osc_sm_comm.c:312-360
+ *   osc_compare_and_swap           osc_sm_comm.c:363-400
+ *   osc_fetch_and_op               osc_sm_comm.c:403-441
+ *   osc_fence                      osc_sm_active_target.c:95-115 (a barrier)
+ *   osc_lock / unlock / flush      osc_sm_passive_target.c:57-270 (ticket lock)
+ *
+ * osc/sm computes with ompi_op_reduce on the target's shared segment under
+ * the target's accumulate spinlock (osc_sm_comm.c:130-139, :296-305).  Here
+ * every window is device memory mapped into each peer with
+ * hipIpcOpenMemHandle; the origin rank's GPU runs the operation as kernels
+ * on its stream that load and store the target's memory over xGMI:
+ *   lock kernel   one lane takes the target's accumulate lock (system-scope
+ *                 CAS on a word in the target's fine-grained control page);
+ *   op kernel     target[i] = f(target[i], origin[i]) with op/base's element
+ *                 rule (f(out, in), op_base_functions.c:40-104), preceded by
+ *                 a copy target -> result for the fetching forms;
+ *   unlock kernel release, then stores 0.
+ * All stream-ordered: a call returns after enqueueing; the stream carries
+ * the ordering (MPI's default accumulate_ordering rar,raw,war,waw between
+ * one origin's calls to one target holds).  Results are bit-identical to
+ * osc/sm's for every order of the targets' locks, since each element of the
+ * target is combined by one origin's call at a time with op/base's rule.
+ *
+ * Displacements are in the TARGET's disp_unit (osc_sm_comm.c:289); counts
+ * in elements of `type` (its extent, as op/base: DOUBLE_INT 16 B).  op is an
+ * OMPI_AMD_OP_* code incl. OMPI_AMD_OP_REPLACE and OMPI_AMD_OP_NO_OP.
+ */
+#ifndef OMPI_AMD_OSC_H
+#define OMPI_AMD_OSC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "ompi_amd_coll.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OMPI_AMD_LOCK_EXCLUSIVE 1     /* MPI_LOCK_EXCLUSIVE (mpi.h.in:548) */
+#define OMPI_AMD_LOCK_SHARED    2     /* MPI_LOCK_SHARED (mpi.h.in:549) */
+#define OMPI_AMD_MODE_NOCHECK   1     /* MPI_MODE_NOCHECK (mpi.h.in:542): lock takes no lock */
+
+typedef struct ompi_amd_win ompi_amd_win_t;
+
+/* MPI_Win_create over device memory [base, base + bytes) (collective).
+ * bytes may be 0 (base ignored). */
+int ompi_amd_win_create(ompi_amd_comm_t *comm, void *base, size_t bytes, int disp_unit,
+                        ompi_amd_win_t **win);
+/* MPI_Win_allocate: the window's memory is allocated here (zeroed). */
+int ompi_amd_win_allocate(ompi_amd_comm_t *comm, size_t bytes, int disp_unit, void **base,
+                          ompi_amd_win_t **win);
+/* MPI_Win_free (collective; waits for every rank's outstanding work). */
+int ompi_amd_win_free(ompi_amd_win_t *win);
+/* MPI_Win_fence: a device barrier on `stream` over the window's ranks.
+ * Every RMA call each rank enqueued before its fence (on the same stream)
+ * is complete at every target when the fence completes. */
+int ompi_amd_win_fence(ompi_amd_win_t *win, int assert_, void *stream);
+/* MPI_Win_lock / _unlock (passive target; lock_type as above): the lock
+ * kernel on `stream` waits for the target's ticket lock (FIFO; shared
+ * holders run together).  Unlock releases it after every RMA call the
+ * caller enqueued on `stream` in between. */
+int ompi_amd_win_lock(ompi_amd_win_t *win, int lock_type, int target, int assert_, void *stream);
+int ompi_amd_win_unlock(ompi_amd_win_t *win, int target, void *stream);
+/* MPI_Win_lock_all / unlock_all: shared locks on every rank. */
+int ompi_amd_win_lock_all(ompi_amd_win_t *win, int assert_, void *stream);
+int ompi_amd_win_unlock_all(ompi_amd_win_t *win, void *stream);
+/* MPI_Win_flush: the calls enqueued so far on `stream` are complete at the
+ * target when the host returns (synchronises the stream). */
+int ompi_amd_win_flush(ompi_amd_win_t *win, int target, void *stream);
+
+int ompi_amd_put(ompi_amd_win_t *win, const void *origin, size_t bytes, int target, size_t disp,
+                 void *stream);
+int ompi_amd_get(ompi_amd_win_t *win, void *origin, size_t bytes, int target, size_t disp,
+                 void *stream);
+/* target = op(target, origin) element-wise, under the target's lock. */
+int ompi_amd_accumulate(ompi_amd_win_t *win, const void *origin, size_t count, int type,
+                        int target, size_t disp, int op, void *stream);
+/* result = target, then target = op(target, origin), as one step. */
+int ompi_amd_get_accumulate(ompi_amd_win_t *win, const void *origin, void *result, size_t count,
+                            int type, int target, size_t disp, int op, void *stream);
+/* get_accumulate of one element. */
+int ompi_amd_fetch_and_op(ompi_amd_win_t *win, const void *origin, void *result, int type,
+                          int target, size_t disp, int op, void *stream);
+/* result = target; if target's bytes equal compare's, target = origin. */
+int ompi_amd_compare_and_swap(ompi_amd_win_t *win, const void *origin, const void *compare,
+                              void *result, int type, int target, size_t disp, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OMPI_AMD_OSC_H */

@@ -21,6 +21,7 @@ ERR_HIP = -3
 ERR_TIMEOUT = -4
 ERR_NOT_DEVICE = -5
 ERR_BOOTSTRAP = -6
+ERR_TRUNCATE = -7
 
 _ERRNAMES = {
     ERR_UNSUPPORTED: "unsupported (op,type)",
@@ -29,6 +30,7 @@ _ERRNAMES = {
     ERR_TIMEOUT: "timeout waiting for a peer",
     ERR_NOT_DEVICE: "buffer is not device memory",
     ERR_BOOTSTRAP: "bootstrap failure",
+    ERR_TRUNCATE: "message truncated",
 }
 
 
@@ -60,7 +62,13 @@ class DdtElem(ctypes.Structure):
                 ("stride", ctypes.c_int64), ("disp", ctypes.c_int64)]
 
 
-# (name, restype, argtypes) for every symbol include/ompi_amd.h declares
+class Status(ctypes.Structure):
+    """ompi_amd_status_t (include/ompi_amd_p2p.h)."""
+    _fields_ = [("source", ctypes.c_int), ("tag", ctypes.c_int), ("error", ctypes.c_int),
+                ("bytes", ctypes.c_size_t)]
+
+
+# (name, restype, argtypes) for every symbol include/ompi_amd*.h declares
 _C = ctypes
 PROTOTYPES = [
     ("ompi_amd_version", _C.c_char_p, []),
@@ -141,6 +149,55 @@ PROTOTYPES = [
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p]),
     ("ompi_amd_bcast", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_void_p]),
+    # point-to-point (include/ompi_amd_p2p.h)
+    ("ompi_amd_isend", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_int, _C.c_void_p,
+      _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_irecv", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p,
+      _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_send", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_int, _C.c_void_p]),
+    ("ompi_amd_recv", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p,
+      _C.POINTER(Status)]),
+    ("ompi_amd_sendrecv", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p, _C.c_size_t,
+      _C.c_int, _C.c_int, _C.c_void_p, _C.POINTER(Status)]),
+    ("ompi_amd_p2p_test", _C.c_int, [_C.c_void_p, _C.POINTER(_C.c_int), _C.POINTER(Status)]),
+    ("ompi_amd_p2p_wait", _C.c_int, [_C.c_void_p, _C.POINTER(Status)]),
+    ("ompi_amd_p2p_free", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_iprobe", _C.c_int,
+     [_C.c_void_p, _C.c_int, _C.c_int, _C.POINTER(_C.c_int), _C.POINTER(Status)]),
+    ("ompi_amd_probe", _C.c_int, [_C.c_void_p, _C.c_int, _C.c_int, _C.POINTER(Status)]),
+    # one-sided (include/ompi_amd_osc.h)
+    ("ompi_amd_win_create", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_win_allocate", _C.c_int,
+     [_C.c_void_p, _C.c_size_t, _C.c_int, _C.POINTER(_C.c_void_p), _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_win_free", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_win_fence", _C.c_int, [_C.c_void_p, _C.c_int, _C.c_void_p]),
+    ("ompi_amd_win_lock", _C.c_int, [_C.c_void_p, _C.c_int, _C.c_int, _C.c_int, _C.c_void_p]),
+    ("ompi_amd_win_unlock", _C.c_int, [_C.c_void_p, _C.c_int, _C.c_void_p]),
+    ("ompi_amd_win_lock_all", _C.c_int, [_C.c_void_p, _C.c_int, _C.c_void_p]),
+    ("ompi_amd_win_unlock_all", _C.c_int, [_C.c_void_p, _C.c_void_p]),
+    ("ompi_amd_win_flush", _C.c_int, [_C.c_void_p, _C.c_int, _C.c_void_p]),
+    ("ompi_amd_put", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_size_t, _C.c_void_p]),
+    ("ompi_amd_get", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_size_t, _C.c_void_p]),
+    ("ompi_amd_accumulate", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_size_t, _C.c_int,
+      _C.c_void_p]),
+    ("ompi_amd_get_accumulate", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_size_t,
+      _C.c_int, _C.c_void_p]),
+    ("ompi_amd_fetch_and_op", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_int, _C.c_int, _C.c_size_t, _C.c_int,
+      _C.c_void_p]),
+    ("ompi_amd_compare_and_swap", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_int, _C.c_int, _C.c_size_t,
+      _C.c_void_p]),
 ]
 
 

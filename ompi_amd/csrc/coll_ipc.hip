@@ -63,6 +63,7 @@
 
 #include "../../include/ompi_amd_coll.h"
 #include "bootstrap.h"
+#include "comm_internal.h"
 #include "op_device.h"
 #include "runtime.h"
 
@@ -627,6 +628,8 @@ struct ompi_amd_comm {
     // being launched (exchange_bufs takes them instead of a rendezvous)
     std::deque<pending_op> pending;
     const call_blob *pre = nullptr;
+    // point-to-point mailboxes (p2p.cpp)
+    p2p_state *p2p = nullptr;
 };
 
 // A persistent allreduce (MPI_Allreduce_init, coll.h:349-352): buffers,
@@ -1450,7 +1453,9 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
         ompi_amd_comm_destroy(c);
         return rc;
     }
-    rc = c->boot.allgather(&mine, all, sizeof(ipc_blob));
+    if (rank == 0) rc = p2p_create(c, name, rank, size, 0, &c->p2p);
+    if (rc == OMPI_AMD_SUCCESS) rc = c->boot.allgather(&mine, all, sizeof(ipc_blob));
+    if (rc == OMPI_AMD_SUCCESS && rank != 0) rc = p2p_create(c, name, rank, size, 1, &c->p2p);
     for (int p = 0; rc == OMPI_AMD_SUCCESS && p < size; ++p) {
         if (p == rank) {
             c->peer_flags.p[p] = c->flags;
@@ -1471,6 +1476,7 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
         ompi_amd_comm_destroy(c);
         return rc;
     }
+    if (rank == 0 && c->p2p) p2p_unlink(c->p2p);  // every rank has it mapped
     *out = c;
     return OMPI_AMD_SUCCESS;
 }
@@ -1500,6 +1506,7 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
             (void)hipEventDestroy(pr.second);
         }
     for (auto e : c->ev_free) (void)hipEventDestroy(e);
+    if (c->p2p) p2p_destroy(c->p2p);
     c->boot.detach();
     delete c;
     return OMPI_AMD_SUCCESS;
@@ -2033,3 +2040,54 @@ int ompi_amd_request_free(ompi_amd_request_t *r) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------ services for p2p / osc
+namespace ompi_amd {
+
+static_assert(sizeof(ipc_desc) == sizeof(buf_desc), "ipc_desc mirrors buf_desc");
+
+int comm_rank(const ompi_amd_comm_t *c) { return c->rank; }
+int comm_size(const ompi_amd_comm_t *c) { return c->size; }
+int comm_device(const ompi_amd_comm_t *c) { return c->device; }
+int64_t comm_timeout_ms(const ompi_amd_comm_t *c) { return c->timeout_ms; }
+int *comm_err_dev(ompi_amd_comm_t *c) { return c->err_dev; }
+p2p_state *comm_p2p(ompi_amd_comm_t *c) { return c->p2p; }
+
+int comm_allgather(ompi_amd_comm_t *c, const void *mine, void *all, size_t len) {
+    return c->boot.allgather(mine, all, len);
+}
+
+int comm_export(ompi_amd_comm_t *c, const void *ptr, ipc_desc *d) {
+    buf_desc b{};
+    const int rc = export_buf(c, ptr, &b);
+    memcpy(d, &b, sizeof(b));
+    return rc;
+}
+
+int comm_import(ompi_amd_comm_t *c, int peer, const ipc_desc &d, const char **out, bool pin,
+                void **base) {
+    buf_desc b;
+    memcpy(&b, &d, sizeof(b));
+    return import_buf(c, peer, b, out, pin, base);
+}
+
+void comm_unpin(ompi_amd_comm_t *c, void *base) { unpin_import(c, base); }
+
+int comm_drain(ompi_amd_comm_t *c) { return drain(c); }
+
+int comm_barrier(ompi_amd_comm_t *c, hipStream_t s) {
+    TRY(drain(c));
+    return launch_barrier(c, s);
+}
+
+int comm_sticky(ompi_amd_comm_t *c) { return check_sticky(c); }
+
+int comm_copy(ompi_amd_comm_t *c, const void *src, void *dst, size_t bytes, hipStream_t s) {
+    cp_jobs jobs{};
+    if (bytes == 0) return OMPI_AMD_SUCCESS;
+    jobs.j[0] = {(const char *)src, (char *)dst, (int64_t)bytes};
+    jobs.n = 1;
+    return launch_copy(c, jobs, s);
+}
+
+}  // namespace ompi_amd

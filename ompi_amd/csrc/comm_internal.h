@@ -1,0 +1,57 @@
+// Services of the communicator (coll_ipc.hip) used by the point-to-point
+// (p2p.cpp) and one-sided (osc_ipc.hip) parts of libompi_amd.so.  Internal:
+// not part of the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "../../include/ompi_amd_coll.h"
+
+namespace ompi_amd {
+
+// A device buffer as peers see it: its allocation's IPC handle + offset.
+struct ipc_desc {
+    hipIpcMemHandle_t h;
+    uint64_t off;
+    uint64_t valid;
+};
+
+struct p2p_state;  // p2p.cpp
+
+int comm_rank(const ompi_amd_comm_t *c);
+int comm_size(const ompi_amd_comm_t *c);
+int comm_device(const ompi_amd_comm_t *c);
+int64_t comm_timeout_ms(const ompi_amd_comm_t *c);
+int *comm_err_dev(ompi_amd_comm_t *c);
+// Host rendezvous: every rank contributes len (<= 2048) bytes.
+int comm_allgather(ompi_amd_comm_t *c, const void *mine, void *all, size_t len);
+// Export a device buffer (cached per allocation).
+int comm_export(ompi_amd_comm_t *c, const void *ptr, ipc_desc *d);
+// Map a peer's exported buffer (cached, LRU).  pin: held until comm_unpin.
+int comm_import(ompi_amd_comm_t *c, int peer, const ipc_desc &d, const char **out, bool pin,
+                void **base);
+void comm_unpin(ompi_amd_comm_t *c, void *base);
+// Launch the deferred nonblocking collectives (device work keeps one order).
+int comm_drain(ompi_amd_comm_t *c);
+// Device barrier over every rank of c on stream s (stream-ordered epoch).
+int comm_barrier(ompi_amd_comm_t *c, hipStream_t s);
+// The sticky device error word (a barrier or lock that timed out).
+int comm_sticky(ompi_amd_comm_t *c);
+// Byte copy kernel (16-/4-/1-byte granules by the common phase of src and
+// dst; src or dst may be peer memory), system-scope acquire/release.
+int comm_copy(ompi_amd_comm_t *c, const void *src, void *dst, size_t bytes, hipStream_t s);
+// Point-to-point mailboxes of the communicator (created with it).
+p2p_state *comm_p2p(ompi_amd_comm_t *c);
+
+// p2p.cpp: created by ompi_amd_comm_create in two phases around its first
+// rendezvous (rank 0 creates the segment before it, the others map it
+// after), released by ompi_amd_comm_destroy.
+int p2p_create(ompi_amd_comm_t *c, const char *name, int rank, int size, int phase,
+               p2p_state **out);
+void p2p_unlink(p2p_state *p);
+void p2p_destroy(p2p_state *p);
+
+}  // namespace ompi_amd

@@ -1,0 +1,574 @@
+// One-sided communication on device windows (include/ompi_amd_osc.h).
+//
+// Reference: osc/sm (ompi/mca/osc/sm/).  Its window is one shared segment;
+// an accumulate takes the target's accumulate spinlock and runs
+// ompi_op_reduce(op, origin, target) on the host (osc_sm_comm.c:271-309 ->
+// osc_base_obj_convert.c ompi_osc_base_sndrcv_op); passive-target locks are
+// a ticket lock of three counters per rank (osc_sm_passive_target.c:23-110);
+// a fence is a barrier (osc_sm_active_target.c:95-115).
+//
+// Here each rank's window is device memory that every peer maps with
+// hipIpcOpenMemHandle, plus one fine-grained control page per rank (the
+// accumulate lock word and the ticket-lock counters).  Every operation is
+// kernels on the origin's stream:
+//   lock kernels    one lane; system-scope atomics on the target's control
+//                   page, polled with s_sleep and a wall-clock bound that
+//                   sets the communicator's sticky error word;
+//   acc_kernel      target[i] = f(target[i], origin[i]) with op/base's
+//                   2-buffer element rule (op_device.h), 16-B granules when
+//                   both sides are 16-B aligned; target is peer memory, so
+//                   its loads and stores cross xGMI once each;
+//   copies          put / get / the fetch of get_accumulate: coll_ipc.hip's
+//                   copy kernel.
+// Every transfer workgroup opens with a system-scope acquire and closes
+// with a drained system-scope release, as the collectives do
+// (coll_ipc.hip header): the lock hand-off then orders one origin's
+// stores before the next holder's loads.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cstring>
+#include <new>
+#include <utility>
+
+#include "../../include/ompi_amd_osc.h"
+#include "comm_internal.h"
+#include "op_device.h"
+#include "runtime.h"
+
+namespace ompi_amd {
+
+constexpr int kOscThreads = 256;
+constexpr int kOscMaxRanks = OMPI_AMD_MAX_RANKS;
+
+// control page words (uint32 each)
+enum { CTL_ACC = 0, CTL_COUNTER = 16, CTL_WRITE = 32, CTL_READ = 48, CTL_BYTES = 4096 };
+
+__device__ __forceinline__ void osc_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
+__device__ __forceinline__ void osc_release() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void osc_epilogue() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) osc_release();
+}
+
+__device__ __forceinline__ uint32_t ld_sys(uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Poll until *p == want (or the bound passes: sticky error, give up).
+__device__ __forceinline__ void wait_eq(uint32_t *p, uint32_t want, int *err, uint64_t ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (ld_sys(p) != want) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+            __hip_atomic_store(err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+    }
+}
+
+// kind: 0 accumulate lock, 1 accumulate unlock, 2 start_exclusive,
+// 3 end_exclusive, 4 start_shared, 5 end_shared (osc_sm_passive_target.c:57-110)
+__global__ __launch_bounds__(64) void lock_kernel(uint32_t *ctl, int kind, int *err,
+                                                  uint64_t ticks) {
+    if (threadIdx.x != 0) return;
+    switch (kind) {
+    case 0: {  // opal_atomic_lock: spin on a compare-and-swap 0 -> 1
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            uint32_t expect = 0;
+            if (__hip_atomic_compare_exchange_strong(ctl + CTL_ACC, &expect, 1u, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
+                break;
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+                __hip_atomic_store(err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+        }
+        osc_acquire();
+        break;
+    }
+    case 1:
+        osc_release();
+        __hip_atomic_store(ctl + CTL_ACC, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+    case 2: {  // start_exclusive: take a ticket, wait until every earlier holder ended
+        const uint32_t me = __hip_atomic_fetch_add(ctl + CTL_COUNTER, 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        wait_eq(ctl + CTL_WRITE, me, err, ticks);
+        osc_acquire();
+        break;
+    }
+    case 3:  // end_exclusive
+        osc_release();
+        __hip_atomic_fetch_add(ctl + CTL_WRITE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_fetch_add(ctl + CTL_READ, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+    case 4: {  // start_shared: wait until every earlier ticket has started (shared) or ended
+        const uint32_t me = __hip_atomic_fetch_add(ctl + CTL_COUNTER, 1u, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        wait_eq(ctl + CTL_READ, me, err, ticks);
+        __hip_atomic_fetch_add(ctl + CTL_READ, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        osc_acquire();
+        break;
+    }
+    case 5:  // end_shared
+        osc_release();
+        __hip_atomic_fetch_add(ctl + CTL_WRITE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+    }
+}
+
+// target[i] = f(target[i], origin[i]) — the 2-buffer rule with out = target,
+// in = origin (ompi_osc_base_sndrcv_op -> ompi_op_reduce(op, origin, target)).
+template <typename T, int OP>
+__global__ __launch_bounds__(kOscThreads) void acc_kernel(const T *__restrict__ origin, T *target,
+                                                          int64_t n, int vec) {
+    osc_acquire();
+    const int64_t gs = (int64_t)gridDim.x * kOscThreads;
+    const int64_t tid = (int64_t)blockIdx.x * kOscThreads + threadIdx.x;
+    int64_t done = 0;
+    if constexpr (16 % sizeof(T) == 0) {
+        constexpr int E = 16 / sizeof(T);
+        if (vec) {
+            const int64_t nv = n / E;
+            const u32x4 *o = reinterpret_cast<const u32x4 *>(origin);
+            u32x4 *t = reinterpret_cast<u32x4 *>(target);
+            for (int64_t i = tid; i < nv; i += gs) {
+                vec16<T> a, b;
+                a.v = t[i];
+                b.v = __builtin_nontemporal_load(o + i);
+#pragma unroll
+                for (int e = 0; e < E; ++e) a.e[e] = opfn<OP, false>::f(a.e[e], b.e[e]);
+                t[i] = a.v;
+            }
+            done = nv * E;
+        }
+    }
+    for (int64_t i = done + tid; i < n; i += gs) {
+        const T r = opfn<OP, false>::f(target[i], origin[i]);
+        store_elem(target + i, r);
+    }
+    osc_epilogue();
+}
+
+// Compare-and-swap of one element of `size` data bytes (osc_sm_comm.c:386-396).
+__global__ __launch_bounds__(64) void cas_kernel(const unsigned char *origin,
+                                                 const unsigned char *compare,
+                                                 unsigned char *result, unsigned char *target,
+                                                 int size) {
+    if (threadIdx.x != 0) return;
+    osc_acquire();
+    unsigned char old[16];
+    bool same = true;
+    for (int b = 0; b < size; ++b) {
+        old[b] = target[b];
+        result[b] = old[b];
+        same = same && old[b] == compare[b];
+    }
+    if (same)
+        for (int b = 0; b < size; ++b) target[b] = origin[b];
+    osc_release();
+}
+
+using acc_launch_fn = hipError_t (*)(dim3, const void *, void *, int64_t, int, hipStream_t);
+
+template <int OP, int TYPE>
+static hipError_t acc_launch_slot(dim3 grid, const void *o, void *t, int64_t n, int vec,
+                                  hipStream_t s) {
+    if constexpr (slot_supported(OP, TYPE)) {
+        using T = typename type_of<TYPE>::type;
+        hipLaunchKernelGGL((acc_kernel<T, OP>), grid, dim3(kOscThreads), 0, s,
+                           static_cast<const T *>(o), static_cast<T *>(t), n, vec);
+        return hipGetLastError();
+    } else {
+        return hipErrorInvalidValue;
+    }
+}
+template <int OP, int... T>
+static constexpr std::array<acc_launch_fn, OMPI_AMD_TYPE_COUNT> make_acc_row(
+    std::integer_sequence<int, T...>) {
+    return {{(slot_supported(OP, T) ? &acc_launch_slot<OP, T> : (acc_launch_fn) nullptr)...}};
+}
+template <int... O>
+static constexpr std::array<std::array<acc_launch_fn, OMPI_AMD_TYPE_COUNT>, OMPI_AMD_OP_COUNT>
+make_acc_table(std::integer_sequence<int, O...>) {
+    return {{make_acc_row<O>(std::make_integer_sequence<int, OMPI_AMD_TYPE_COUNT>{})...}};
+}
+static const auto g_acc = make_acc_table(std::make_integer_sequence<int, OMPI_AMD_OP_COUNT>{});
+
+struct win_blob {
+    ipc_desc base, ctl;
+    uint64_t bytes;
+    int64_t disp_unit;
+    int64_t failed;  // this rank could not set up its side
+};
+
+}  // namespace ompi_amd
+
+using namespace ompi_amd;
+
+struct ompi_amd_win {
+    ompi_amd_comm_t *c = nullptr;
+    int rank = 0, size = 0;
+    char *base = nullptr;
+    size_t bytes = 0;
+    bool owns_base = false;
+    uint32_t *ctl = nullptr;
+    char *peer_base[kOscMaxRanks] = {};
+    uint32_t *peer_ctl[kOscMaxRanks] = {};
+    uint64_t peer_bytes[kOscMaxRanks] = {};
+    int64_t peer_disp[kOscMaxRanks] = {};
+    void *pinned[kOscMaxRanks] = {};
+    void *ctl_opened[kOscMaxRanks] = {};
+    int held[kOscMaxRanks] = {};  // outstanding passive lock per target (0 none)
+};
+
+namespace ompi_amd {
+
+enum { HELD_NONE = 0, HELD_EXCLUSIVE = 1, HELD_SHARED = 2, HELD_NOCHECK = 3 };
+
+static uint64_t ticks_of(ompi_amd_win_t *w) {
+    return (uint64_t)comm_timeout_ms(w->c) * 100000ull;  // s_memrealtime: 100 MHz
+}
+
+static int launch_lock(ompi_amd_win_t *w, int target, int kind, hipStream_t s) {
+    hipLaunchKernelGGL(lock_kernel, dim3(1), dim3(64), 0, s, w->peer_ctl[target], kind,
+                       comm_err_dev(w->c), ticks_of(w));
+    return record_hip(hipGetLastError(), "osc lock launch");
+}
+
+// Target address of (target, disp) with room for `bytes`.
+static int target_ptr(ompi_amd_win_t *w, int target, size_t disp, size_t bytes, char **out) {
+    if (target < 0 || target >= w->size) return OMPI_AMD_ERR_BAD_PARAM;
+    const uint64_t off = (uint64_t)disp * (uint64_t)w->peer_disp[target];
+    if (off > w->peer_bytes[target] || bytes > w->peer_bytes[target] - off) {
+        record_msg("osc: target %d range [%llu, +%zu) outside its %llu-byte window", target,
+                   (unsigned long long)off, bytes, (unsigned long long)w->peer_bytes[target]);
+        return OMPI_AMD_ERR_BAD_PARAM;
+    }
+    *out = w->peer_base[target] ? w->peer_base[target] + off : nullptr;
+    return OMPI_AMD_SUCCESS;
+}
+
+static int launch_acc(ompi_amd_win_t *w, int op, int type, const void *origin, void *target,
+                      size_t count, hipStream_t s) {
+    acc_launch_fn f = (op >= 0 && op < OMPI_AMD_OP_COUNT && type >= 0 && type < OMPI_AMD_TYPE_COUNT)
+                          ? g_acc[op][type]
+                          : nullptr;
+    if (!f) {
+        record_msg("osc accumulate: op %d on type %d is not provided", op, type);
+        return OMPI_AMD_ERR_UNSUPPORTED;
+    }
+    const size_t ext = ompi_amd_type_extent(type);
+    const int vec = (16 % ext == 0 && ((uintptr_t)origin & 15) == 0 && ((uintptr_t)target & 15) == 0);
+    const int64_t units = vec ? (int64_t)(count * ext / 16) + 1 : (int64_t)count;
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((units + kOscThreads - 1) / kOscThreads, 2048));
+    return record_hip(f(dim3((unsigned)blocks), origin, target, (int64_t)count, vec, s),
+                      "osc accumulate launch");
+}
+
+#define OSC_TRY(x)                               \
+    do {                                         \
+        int rc_ = (x);                           \
+        if (rc_ != OMPI_AMD_SUCCESS) return rc_; \
+    } while (0)
+
+// accumulate / get_accumulate / fetch_and_op under the accumulate lock
+// (osc_sm_comm.c:296-305, :340-356, :424-438).
+static int rma_op(ompi_amd_win_t *w, const void *origin, void *result, size_t count, int type,
+                  int target, size_t disp, int op, void *stream) {
+    if (!w) return OMPI_AMD_ERR_BAD_PARAM;
+    if (type < 0 || type >= OMPI_AMD_TYPE_COUNT || ompi_amd_type_extent(type) == 0)
+        return OMPI_AMD_ERR_BAD_PARAM;
+    if (op != OMPI_AMD_OP_REPLACE && op != OMPI_AMD_OP_NO_OP &&
+        (op <= 0 || op >= OMPI_AMD_OP_COUNT || !g_acc[op][type])) {
+        record_msg("osc accumulate: op %d on type %d is not provided", op, type);
+        return OMPI_AMD_ERR_UNSUPPORTED;
+    }
+    if (count == 0) return OMPI_AMD_SUCCESS;
+    const size_t bytes = count * ompi_amd_type_extent(type);
+    char *t = nullptr;
+    OSC_TRY(target_ptr(w, target, disp, bytes, &t));
+    hipStream_t s = as_stream(stream);
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    OSC_TRY(launch_lock(w, target, 0, s));
+    int rc = OMPI_AMD_SUCCESS;
+    if (result) rc = comm_copy(w->c, t, result, bytes, s);
+    if (rc == OMPI_AMD_SUCCESS) {
+        if (op == OMPI_AMD_OP_REPLACE) rc = comm_copy(w->c, origin, t, bytes, s);
+        else if (op != OMPI_AMD_OP_NO_OP) rc = launch_acc(w, op, type, origin, t, count, s);
+    }
+    const int urc = launch_lock(w, target, 1, s);  // always release
+    return rc != OMPI_AMD_SUCCESS ? rc : urc;
+}
+
+static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit, bool owns,
+                     ompi_amd_win_t **out) {
+    auto *w = new (std::nothrow) ompi_amd_win;
+    if (!w) return OMPI_AMD_ERR_BAD_PARAM;
+    w->c = c;
+    w->rank = ompi_amd_comm_rank(c);
+    w->size = ompi_amd_comm_size(c);
+    w->base = static_cast<char *>(base);
+    w->bytes = bytes;
+    w->owns_base = owns;
+    int rc = comm_drain(c);  // collective order: deferred nonblocking calls first
+    hipError_t e = hipSuccess;
+    if (rc == OMPI_AMD_SUCCESS) {
+        e = hipExtMallocWithFlags((void **)&w->ctl, CTL_BYTES, hipDeviceMallocUncached);
+        if (e == hipSuccess) e = hipMemset(w->ctl, 0, CTL_BYTES);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        rc = record_hip(e, "osc control page");
+    }
+    win_blob mine{}, all[kOscMaxRanks];
+    mine.bytes = bytes;
+    mine.disp_unit = disp_unit;
+    if (rc == OMPI_AMD_SUCCESS && bytes) rc = comm_export(c, base, &mine.base);
+    if (rc == OMPI_AMD_SUCCESS) {
+        rc = record_hip(hipIpcGetMemHandle(&mine.ctl.h, w->ctl), "hipIpcGetMemHandle (osc)");
+        mine.ctl.valid = 1;
+    }
+    // every rank takes part in the rendezvous, whatever failed locally
+    mine.failed = rc == OMPI_AMD_SUCCESS ? 0 : 1;
+    const int arc = comm_allgather(c, &mine, all, sizeof(win_blob));
+    if (rc == OMPI_AMD_SUCCESS) rc = arc;
+    for (int p = 0; rc == OMPI_AMD_SUCCESS && p < w->size; ++p) {
+        if (all[p].failed) {
+            record_msg("osc window: rank %d failed to set up its window", p);
+            rc = OMPI_AMD_ERR_BOOTSTRAP;
+            break;
+        }
+        w->peer_bytes[p] = all[p].bytes;
+        w->peer_disp[p] = all[p].disp_unit;
+        if (p == w->rank) {
+            w->peer_base[p] = w->base;
+            w->peer_ctl[p] = w->ctl;
+            continue;
+        }
+        if (all[p].bytes) {
+            const char *pb = nullptr;
+            rc = comm_import(c, p, all[p].base, &pb, true, &w->pinned[p]);
+            w->peer_base[p] = const_cast<char *>(pb);
+        }
+        if (rc == OMPI_AMD_SUCCESS) {
+            void *m = nullptr;
+            rc = record_hip(hipIpcOpenMemHandle(&m, all[p].ctl.h, hipIpcMemLazyEnablePeerAccess),
+                            "hipIpcOpenMemHandle (osc control)");
+            w->ctl_opened[p] = m;
+            w->peer_ctl[p] = static_cast<uint32_t *>(m);
+        }
+    }
+    // agree: all mapped (or all give up together)
+    int ok = rc == OMPI_AMD_SUCCESS, all_ok = 0;
+    const int grc = ompi_amd_comm_agree(c, ok, &all_ok);
+    if (rc == OMPI_AMD_SUCCESS && (grc != OMPI_AMD_SUCCESS || !all_ok))
+        rc = grc != OMPI_AMD_SUCCESS ? grc : OMPI_AMD_ERR_BOOTSTRAP;
+    if (rc != OMPI_AMD_SUCCESS) {
+        for (int p = 0; p < w->size; ++p) {
+            if (w->pinned[p]) comm_unpin(c, w->pinned[p]);
+            if (w->ctl_opened[p]) (void)hipIpcCloseMemHandle(w->ctl_opened[p]);
+        }
+        if (w->ctl) (void)hipFree(w->ctl);
+        delete w;
+        return rc;
+    }
+    *out = w;
+    return OMPI_AMD_SUCCESS;
+}
+
+}  // namespace ompi_amd
+
+extern "C" {
+
+int ompi_amd_win_create(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit,
+                        ompi_amd_win_t **out) {
+    if (!c || !out || disp_unit <= 0 || (bytes && !base)) return OMPI_AMD_ERR_BAD_PARAM;
+    if (bytes && !ompi_amd_is_device_pointer(base)) {
+        record_msg("osc window base is not device memory");
+        return OMPI_AMD_ERR_NOT_DEVICE;
+    }
+    int rc = record_hip(hipSetDevice(comm_device(c)), "hipSetDevice");
+    if (rc != OMPI_AMD_SUCCESS) return rc;
+    return win_setup(c, bytes ? base : nullptr, bytes, disp_unit, false, out);
+}
+
+int ompi_amd_win_allocate(ompi_amd_comm_t *c, size_t bytes, int disp_unit, void **base,
+                          ompi_amd_win_t **out) {
+    if (!c || !out || !base || disp_unit <= 0) return OMPI_AMD_ERR_BAD_PARAM;
+    int rc = record_hip(hipSetDevice(comm_device(c)), "hipSetDevice");
+    void *m = nullptr;
+    if (rc == OMPI_AMD_SUCCESS && bytes) {
+        rc = record_hip(hipMalloc(&m, bytes), "hipMalloc (window)");
+        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipMemset(m, 0, bytes), "hipMemset (window)");
+        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    }
+    // a local failure still joins the rendezvous (as a zero-byte window) so
+    // that no peer waits; the collective result reports it
+    if (rc != OMPI_AMD_SUCCESS) {
+        if (m) (void)hipFree(m);
+        ompi_amd_win_t *w = nullptr;
+        if (win_setup(c, nullptr, 0, disp_unit, false, &w) == OMPI_AMD_SUCCESS)
+            (void)ompi_amd_win_free(w);
+        return rc;
+    }
+    rc = win_setup(c, m, bytes, disp_unit, true, out);
+    if (rc != OMPI_AMD_SUCCESS) {
+        if (m) (void)hipFree(m);
+        return rc;
+    }
+    *base = m;
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_win_free(ompi_amd_win_t *w) {
+    if (!w) return OMPI_AMD_SUCCESS;
+    ompi_amd_comm_t *c = w->c;
+    (void)hipSetDevice(comm_device(c));
+    int rc = comm_drain(c);
+    const int src = record_hip(hipDeviceSynchronize(), "hipDeviceSynchronize (win_free)");
+    if (rc == OMPI_AMD_SUCCESS) rc = src;
+    const int brc = comm_allgather(c, nullptr, nullptr, 0);  // nobody still touches the windows
+    if (rc == OMPI_AMD_SUCCESS) rc = brc;
+    for (int p = 0; p < w->size; ++p) {
+        if (w->pinned[p]) comm_unpin(c, w->pinned[p]);
+        if (w->ctl_opened[p]) (void)hipIpcCloseMemHandle(w->ctl_opened[p]);
+    }
+    const int brc2 = comm_allgather(c, nullptr, nullptr, 0);  // mappings closed before frees
+    if (rc == OMPI_AMD_SUCCESS) rc = brc2;
+    if (w->ctl) (void)hipFree(w->ctl);
+    if (w->owns_base && w->base) (void)hipFree(w->base);
+    if (rc == OMPI_AMD_SUCCESS) rc = comm_sticky(c);
+    delete w;
+    return rc;
+}
+
+int ompi_amd_win_fence(ompi_amd_win_t *w, int assert_, void *stream) {
+    if (!w) return OMPI_AMD_ERR_BAD_PARAM;
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    return comm_barrier(w->c, as_stream(stream));
+}
+
+int ompi_amd_win_lock(ompi_amd_win_t *w, int lock_type, int target, int assert_, void *stream) {
+    if (!w || target < 0 || target >= w->size) return OMPI_AMD_ERR_BAD_PARAM;
+    if (lock_type != OMPI_AMD_LOCK_EXCLUSIVE && lock_type != OMPI_AMD_LOCK_SHARED)
+        return OMPI_AMD_ERR_BAD_PARAM;
+    if (w->held[target] != HELD_NONE) {
+        record_msg("osc: target %d is already locked by this rank", target);
+        return OMPI_AMD_ERR_BAD_PARAM;  // MPI_ERR_RMA_SYNC (osc_sm_passive_target.c:122-124)
+    }
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    if (assert_ & OMPI_AMD_MODE_NOCHECK) {
+        w->held[target] = HELD_NOCHECK;
+        return OMPI_AMD_SUCCESS;
+    }
+    const bool excl = lock_type == OMPI_AMD_LOCK_EXCLUSIVE;
+    OSC_TRY(launch_lock(w, target, excl ? 2 : 4, as_stream(stream)));
+    w->held[target] = excl ? HELD_EXCLUSIVE : HELD_SHARED;
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_win_unlock(ompi_amd_win_t *w, int target, void *stream) {
+    if (!w || target < 0 || target >= w->size) return OMPI_AMD_ERR_BAD_PARAM;
+    const int h = w->held[target];
+    if (h == HELD_NONE) {
+        record_msg("osc: target %d is not locked by this rank", target);
+        return OMPI_AMD_ERR_BAD_PARAM;
+    }
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    int rc = OMPI_AMD_SUCCESS;
+    if (h == HELD_EXCLUSIVE) rc = launch_lock(w, target, 3, as_stream(stream));
+    else if (h == HELD_SHARED) rc = launch_lock(w, target, 5, as_stream(stream));
+    w->held[target] = HELD_NONE;
+    return rc;
+}
+
+int ompi_amd_win_lock_all(ompi_amd_win_t *w, int assert_, void *stream) {
+    if (!w) return OMPI_AMD_ERR_BAD_PARAM;
+    for (int p = 0; p < w->size; ++p)  // osc_sm_passive_target.c:191-206
+        OSC_TRY(ompi_amd_win_lock(w, OMPI_AMD_LOCK_SHARED, p, assert_, stream));
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_win_unlock_all(ompi_amd_win_t *w, void *stream) {
+    if (!w) return OMPI_AMD_ERR_BAD_PARAM;
+    for (int p = 0; p < w->size; ++p) OSC_TRY(ompi_amd_win_unlock(w, p, stream));
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_win_flush(ompi_amd_win_t *w, int target, void *stream) {
+    if (!w) return OMPI_AMD_ERR_BAD_PARAM;
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    OSC_TRY(record_hip(hipStreamSynchronize(as_stream(stream)), "hipStreamSynchronize (flush)"));
+    return comm_sticky(w->c);
+}
+
+int ompi_amd_put(ompi_amd_win_t *w, const void *origin, size_t bytes, int target, size_t disp,
+                 void *stream) {
+    if (!w || (bytes && !origin)) return OMPI_AMD_ERR_BAD_PARAM;
+    char *t = nullptr;
+    OSC_TRY(target_ptr(w, target, disp, bytes, &t));
+    if (!bytes) return OMPI_AMD_SUCCESS;
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    return comm_copy(w->c, origin, t, bytes, as_stream(stream));
+}
+
+int ompi_amd_get(ompi_amd_win_t *w, void *origin, size_t bytes, int target, size_t disp,
+                 void *stream) {
+    if (!w || (bytes && !origin)) return OMPI_AMD_ERR_BAD_PARAM;
+    char *t = nullptr;
+    OSC_TRY(target_ptr(w, target, disp, bytes, &t));
+    if (!bytes) return OMPI_AMD_SUCCESS;
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    return comm_copy(w->c, t, origin, bytes, as_stream(stream));
+}
+
+int ompi_amd_accumulate(ompi_amd_win_t *w, const void *origin, size_t count, int type, int target,
+                        size_t disp, int op, void *stream) {
+    if (op == OMPI_AMD_OP_NO_OP) return OMPI_AMD_ERR_BAD_PARAM;  // MPI_Accumulate forbids it
+    if (count && !origin) return OMPI_AMD_ERR_BAD_PARAM;
+    return rma_op(w, origin, nullptr, count, type, target, disp, op, stream);
+}
+
+int ompi_amd_get_accumulate(ompi_amd_win_t *w, const void *origin, void *result, size_t count,
+                            int type, int target, size_t disp, int op, void *stream) {
+    if (count && (!result || (!origin && op != OMPI_AMD_OP_NO_OP))) return OMPI_AMD_ERR_BAD_PARAM;
+    return rma_op(w, origin, result, count, type, target, disp, op, stream);
+}
+
+int ompi_amd_fetch_and_op(ompi_amd_win_t *w, const void *origin, void *result, int type,
+                          int target, size_t disp, int op, void *stream) {
+    return ompi_amd_get_accumulate(w, origin, result, 1, type, target, disp, op, stream);
+}
+
+int ompi_amd_compare_and_swap(ompi_amd_win_t *w, const void *origin, const void *compare,
+                              void *result, int type, int target, size_t disp, void *stream) {
+    if (!w || !origin || !compare || !result) return OMPI_AMD_ERR_BAD_PARAM;
+    if (type < 0 || type >= OMPI_AMD_TYPE_COUNT || ompi_amd_type_extent(type) == 0 ||
+        is_pair_type(type))
+        return OMPI_AMD_ERR_BAD_PARAM;  // integer, logical and byte types (MPI-3.1 §11.3.4)
+    const size_t size = ompi_amd_type_extent(type);  // no gaps in these types
+    char *t = nullptr;
+    OSC_TRY(target_ptr(w, target, disp, size, &t));
+    hipStream_t s = as_stream(stream);
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    OSC_TRY(launch_lock(w, target, 0, s));
+    hipLaunchKernelGGL(cas_kernel, dim3(1), dim3(64), 0, s,
+                       static_cast<const unsigned char *>(origin),
+                       static_cast<const unsigned char *>(compare),
+                       static_cast<unsigned char *>(result), reinterpret_cast<unsigned char *>(t),
+                       (int)size);
+    const int rc = record_hip(hipGetLastError(), "osc compare_and_swap launch");
+    const int urc = launch_lock(w, target, 1, s);
+    return rc != OMPI_AMD_SUCCESS ? rc : urc;
+}
+
+}  // extern "C"

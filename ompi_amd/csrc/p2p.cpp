@@ -1,0 +1,496 @@
+// Point-to-point messages between device buffers (include/ompi_amd_p2p.h).
+//
+// Reference path replaced for device memory: PML ob1's rendezvous for CUDA
+// buffers (pml_ob1_cuda.c:56-101: the sender registers its buffer and sends
+// an RGET header; the receiver "gets" it with btl/smcuda,
+// btl_smcuda.c:1077-1250, which opens the sender's CUDA IPC handle and
+// issues cuMemcpyAsync, then sends a FIN; common_cuda.c:1008-1320).
+//
+// Here:
+//   mailbox  one POSIX shared-memory segment per communicator holding, for
+//            every ordered (src, dst) pair, a ring of kSlots message
+//            descriptors {tag, bytes, IPC handle + offset of the send
+//            buffer} and a published-count word.  Only the sender writes a
+//            descriptor and the count; only the receiver moves a slot from
+//            POSTED to MATCHED to DONE; the sender recycles a DONE slot.
+//   match    on the receiver's host, in MPI order: per source, messages in
+//            sequence order; posted receives in posting order (each takes
+//            the earliest matching message), wildcards allowed.
+//   data     the receiver launches one copy kernel (coll_ipc.hip's
+//            copy_kernel: 16-B granules, system-scope acquire/release) that
+//            loads the sender's buffer through its IPC mapping over xGMI
+//            straight into the receive buffer: one HBM read on the sender's
+//            GPU, one HBM write on the receiver's, no staging.
+//   FIN      the receiver marks the slot DONE once the copy's event has
+//            completed; the send completes when it sees DONE.
+#include <hip/hip_runtime.h>
+
+#include <fcntl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/ompi_amd_p2p.h"
+#include "comm_internal.h"
+#include "runtime.h"
+
+namespace ompi_amd {
+
+constexpr int kSlots = 64;
+
+enum : uint32_t { S_FREE = 0, S_POSTED = 1, S_MATCHED = 2, S_DONE = 3 };
+
+struct alignas(64) msg_slot {
+    std::atomic<uint32_t> state;
+    int32_t tag;
+    uint64_t seq;
+    uint64_t bytes;
+    uint64_t raw;  // the send buffer's address (messages to self)
+    ipc_desc d;    // the send buffer for peers
+};
+
+struct alignas(64) pair_q {
+    std::atomic<uint64_t> posted;  // descriptors published by the sender
+    char pad[56];
+    msg_slot slot[kSlots];
+};
+
+static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory atomics");
+static_assert(std::atomic<uint32_t>::is_always_lock_free, "shared-memory atomics");
+
+struct p2p_state {
+    ompi_amd_comm_t *c = nullptr;
+    int rank = 0, size = 0;
+    char name[256] = {0};
+    pair_q *q = nullptr;
+    size_t bytes = 0;
+    bool unlinked = false;
+    std::vector<uint64_t> scan_from;  // per source: first sequence possibly still POSTED
+    std::deque<ompi_amd_p2p_request *> recvs;  // posted receives not matched yet
+    std::recursive_mutex mu;
+
+    pair_q &pair(int src, int dst) { return q[(size_t)src * (size_t)size + (size_t)dst]; }
+};
+
+}  // namespace ompi_amd
+
+using namespace ompi_amd;
+
+struct ompi_amd_p2p_request {
+    p2p_state *p = nullptr;
+    bool is_send = false;
+    bool done = false;
+    int rc = OMPI_AMD_SUCCESS;
+    // send
+    int peer = 0;
+    uint64_t seq = 0;
+    // receive
+    void *buf = nullptr;
+    size_t cap = 0;
+    int src = OMPI_AMD_ANY_SOURCE, tag = OMPI_AMD_ANY_TAG;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev = nullptr;
+    bool matched = false;
+    msg_slot *slot = nullptr;  // matched message
+    void *pinned = nullptr;    // sender mapping held during the copy
+    ompi_amd_status_t st{};
+};
+
+namespace ompi_amd {
+
+static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+int p2p_create(ompi_amd_comm_t *c, const char *name, int rank, int size, int phase,
+               p2p_state **out) {
+    auto *p = new (std::nothrow) p2p_state;
+    if (!p) return OMPI_AMD_ERR_BOOTSTRAP;
+    p->c = c;
+    p->rank = rank;
+    p->size = size;
+    p->scan_from.assign((size_t)size, 0);
+    snprintf(p->name, sizeof(p->name), "/ompi_amd_%s.p2p", name);
+    for (char *ch = p->name + 1; *ch; ++ch)
+        if (*ch == '/') *ch = '_';
+    p->bytes = sizeof(pair_q) * (size_t)size * (size_t)size;
+    int fd = -1;
+    if (phase == 0) {  // rank 0, before the communicator's first rendezvous
+        shm_unlink(p->name);
+        fd = shm_open(p->name, O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd >= 0 && ftruncate(fd, (off_t)p->bytes) != 0) {
+            close(fd);
+            fd = -1;
+        }
+    } else {  // the others, after it
+        fd = shm_open(p->name, O_RDWR, 0600);
+    }
+    if (fd < 0) {
+        record_msg("p2p mailbox %s: %s", p->name, strerror(errno));
+        delete p;
+        return OMPI_AMD_ERR_BOOTSTRAP;
+    }
+    void *m = mmap(nullptr, p->bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) {
+        record_msg("mmap %s: %s", p->name, strerror(errno));
+        if (phase == 0) shm_unlink(p->name);
+        delete p;
+        return OMPI_AMD_ERR_BOOTSTRAP;
+    }
+    p->q = static_cast<pair_q *>(m);  // zero-filled by ftruncate: all slots FREE
+    *out = p;
+    return OMPI_AMD_SUCCESS;
+}
+
+void p2p_unlink(p2p_state *p) {
+    if (p && !p->unlinked) {
+        shm_unlink(p->name);
+        p->unlinked = true;
+    }
+}
+
+void p2p_destroy(p2p_state *p) {
+    if (!p) return;
+    if (p->q) munmap(p->q, p->bytes);
+    if (p->rank == 0) p2p_unlink(p);
+    delete p;
+}
+
+static bool tag_ok(int want, int have) { return want == OMPI_AMD_ANY_TAG || want == have; }
+
+// The earliest POSTED message from `s` a receive with `tag` matches.
+static msg_slot *find_from(p2p_state *p, int s, int tag) {
+    pair_q &q = p->pair(s, p->rank);
+    const uint64_t posted = q.posted.load(std::memory_order_acquire);
+    uint64_t &from = p->scan_from[(size_t)s];
+    // skip the prefix that is no longer POSTED (matched or recycled)
+    while (from < posted) {
+        msg_slot &m = q.slot[from % kSlots];
+        if (m.state.load(std::memory_order_acquire) == S_POSTED && m.seq == from) break;
+        ++from;
+    }
+    for (uint64_t k = from; k < posted; ++k) {
+        msg_slot &m = q.slot[k % kSlots];
+        if (m.state.load(std::memory_order_acquire) == S_POSTED && m.seq == k && tag_ok(tag, m.tag))
+            return &m;
+    }
+    return nullptr;
+}
+
+static msg_slot *find(p2p_state *p, int src, int tag, int *from_rank) {
+    if (src != OMPI_AMD_ANY_SOURCE) {
+        *from_rank = src;
+        return find_from(p, src, tag);
+    }
+    for (int k = 0; k < p->size; ++k) {
+        const int s = (p->rank + k) % p->size;  // self first, then rank+1, ...
+        if (msg_slot *m = find_from(p, s, tag)) {
+            *from_rank = s;
+            return m;
+        }
+    }
+    return nullptr;
+}
+
+// Claim `m` for receive `r` and launch its copy.
+static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s) {
+    m->state.store(S_MATCHED, std::memory_order_release);
+    r->matched = true;
+    r->slot = m;
+    r->st.source = s;
+    r->st.tag = m->tag;
+    r->st.bytes = m->bytes;
+    size_t n = (size_t)m->bytes;
+    if (n > r->cap) {  // MPI_ERR_TRUNCATE: copy what fits (ob1 does the same)
+        n = r->cap;
+        r->rc = OMPI_AMD_ERR_TRUNCATE;
+        record_msg("p2p receive truncated: message %llu bytes, buffer %zu",
+                   (unsigned long long)m->bytes, r->cap);
+    }
+    r->st.error = r->rc;
+    if (n == 0) return;
+    const char *src = nullptr;
+    int rc = OMPI_AMD_SUCCESS;
+    if (s == p->rank) {
+        src = reinterpret_cast<const char *>(m->raw);
+    } else {
+        rc = comm_import(p->c, s, m->d, &src, true, &r->pinned);
+    }
+    if (rc == OMPI_AMD_SUCCESS) rc = comm_copy(p->c, src, r->buf, n, r->stream);
+    if (rc == OMPI_AMD_SUCCESS) {
+        if (!r->ev) rc = record_hip(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming),
+                                    "hipEventCreate (p2p)");
+        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipEventRecord(r->ev, r->stream), "hipEventRecord (p2p)");
+    }
+    if (rc != OMPI_AMD_SUCCESS) r->rc = r->st.error = rc;
+}
+
+// Match posted receives against published messages, in posting order.
+static void progress(p2p_state *p) {
+    for (auto it = p->recvs.begin(); it != p->recvs.end();) {
+        ompi_amd_p2p_request *r = *it;
+        int s = -1;
+        msg_slot *m = find(p, r->src, r->tag, &s);
+        if (!m) {
+            ++it;
+            continue;
+        }
+        start_recv(p, r, m, s);
+        it = p->recvs.erase(it);
+    }
+}
+
+// Non-blocking completion check of one request.
+static int test_one(ompi_amd_p2p_request *r, bool *done) {
+    p2p_state *p = r->p;
+    std::lock_guard<std::recursive_mutex> g(p->mu);
+    progress(p);
+    if (r->done) {
+        *done = true;
+        return r->rc;
+    }
+    *done = false;
+    if (r->is_send) {
+        msg_slot &m = p->pair(p->rank, r->peer).slot[r->seq % kSlots];
+        if (m.seq != r->seq || m.state.load(std::memory_order_acquire) == S_DONE) r->done = true;
+    } else if (r->matched) {
+        bool copied = true;
+        if (r->ev) {
+            const hipError_t e = hipEventQuery(r->ev);
+            if (e == hipErrorNotReady) {
+                copied = false;
+            } else if (e != hipSuccess) {
+                r->rc = r->st.error = record_hip(e, "p2p copy");
+            }
+        }
+        if (copied) {
+            if (r->pinned) comm_unpin(p->c, r->pinned);
+            r->pinned = nullptr;
+            r->slot->state.store(S_DONE, std::memory_order_release);  // the FIN
+            r->done = true;
+        }
+    }
+    *done = r->done;
+    return r->done ? r->rc : OMPI_AMD_SUCCESS;
+}
+
+static int wait_one(ompi_amd_p2p_request *r) {
+    const double limit = (double)comm_timeout_ms(r->p->c) / 1000.0;
+    const double t0 = now_s();
+    unsigned spins = 0;
+    for (;;) {
+        bool done = false;
+        const int rc = test_one(r, &done);
+        if (done) return rc;
+        if (++spins > 64) sched_yield();
+        if (now_s() - t0 > limit) {
+            record_msg("p2p %s timed out after %.1f s (peer %d, tag %d)",
+                       r->is_send ? "send" : "receive", limit,
+                       r->is_send ? r->peer : r->src, r->is_send ? -1 : r->tag);
+            return OMPI_AMD_ERR_TIMEOUT;
+        }
+    }
+}
+
+static void fill_status(const ompi_amd_p2p_request *r, ompi_amd_status_t *st) {
+    if (!st) return;
+    if (r->is_send) {
+        st->source = r->p->rank;
+        st->tag = 0;
+        st->error = r->rc;
+        st->bytes = 0;
+    } else {
+        *st = r->st;
+    }
+}
+
+}  // namespace ompi_amd
+
+extern "C" {
+
+int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, int tag, int mode,
+                   void *stream, ompi_amd_p2p_request_t **out) {
+    if (!c || !out || tag < 0 || (bytes && !buf)) return OMPI_AMD_ERR_BAD_PARAM;
+    p2p_state *p = comm_p2p(c);
+    if (!p || dst < 0 || dst >= p->size) return OMPI_AMD_ERR_BAD_PARAM;
+    if (mode == OMPI_AMD_SEND_BUFFERED) {
+        record_msg("MPI_Bsend of device buffers is not provided");
+        return OMPI_AMD_ERR_UNSUPPORTED;
+    }
+    if (mode < OMPI_AMD_SEND_SYNCHRONOUS || mode > OMPI_AMD_SEND_STANDARD)
+        return OMPI_AMD_ERR_BAD_PARAM;
+    int rc = record_hip(hipSetDevice(comm_device(c)), "hipSetDevice");
+    // the buffer is read by the receiver at any time from now: its producers must be done
+    if (rc == OMPI_AMD_SUCCESS)
+        rc = record_hip(hipStreamSynchronize(as_stream(stream)), "hipStreamSynchronize (send)");
+    ipc_desc d{};
+    if (rc == OMPI_AMD_SUCCESS && bytes && dst != p->rank) rc = comm_export(c, buf, &d);
+    if (rc != OMPI_AMD_SUCCESS) return rc;
+    auto *r = new (std::nothrow) ompi_amd_p2p_request;
+    if (!r) return OMPI_AMD_ERR_BAD_PARAM;
+    r->p = p;
+    r->is_send = true;
+    r->peer = dst;
+    std::lock_guard<std::recursive_mutex> g(p->mu);
+    pair_q &q = p->pair(p->rank, dst);
+    const uint64_t seq = q.posted.load(std::memory_order_relaxed);
+    msg_slot &m = q.slot[seq % kSlots];
+    // the ring slot must be free: its previous message completed (DONE) or
+    // was never used; wait (bounded) for the receiver otherwise
+    const double limit = (double)comm_timeout_ms(c) / 1000.0, t0 = now_s();
+    for (;;) {
+        const uint32_t s = m.state.load(std::memory_order_acquire);
+        if (s == S_FREE || s == S_DONE) break;
+        progress(p);  // our own receives keep flowing meanwhile
+        sched_yield();
+        if (now_s() - t0 > limit) {
+            record_msg("p2p send to %d: %d messages unmatched for %.1f s", dst, kSlots, limit);
+            delete r;
+            return OMPI_AMD_ERR_TIMEOUT;
+        }
+    }
+    m.tag = tag;
+    m.seq = seq;
+    m.bytes = bytes;
+    m.raw = reinterpret_cast<uint64_t>(buf);
+    m.d = d;
+    m.state.store(S_POSTED, std::memory_order_release);
+    q.posted.store(seq + 1, std::memory_order_release);
+    r->seq = seq;
+    *out = r;
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_irecv(ompi_amd_comm_t *c, void *buf, size_t bytes, int src, int tag, void *stream,
+                   ompi_amd_p2p_request_t **out) {
+    if (!c || !out || (bytes && !buf) || tag < OMPI_AMD_ANY_TAG) return OMPI_AMD_ERR_BAD_PARAM;
+    p2p_state *p = comm_p2p(c);
+    if (!p || src < OMPI_AMD_ANY_SOURCE || src >= p->size) return OMPI_AMD_ERR_BAD_PARAM;
+    const int rc = record_hip(hipSetDevice(comm_device(c)), "hipSetDevice");
+    if (rc != OMPI_AMD_SUCCESS) return rc;
+    auto *r = new (std::nothrow) ompi_amd_p2p_request;
+    if (!r) return OMPI_AMD_ERR_BAD_PARAM;
+    r->p = p;
+    r->buf = buf;
+    r->cap = bytes;
+    r->src = src;
+    r->tag = tag;
+    r->stream = as_stream(stream);
+    std::lock_guard<std::recursive_mutex> g(p->mu);
+    p->recvs.push_back(r);
+    progress(p);
+    *out = r;
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_p2p_test(ompi_amd_p2p_request_t *r, int *done, ompi_amd_status_t *st) {
+    if (!r || !done) return OMPI_AMD_ERR_BAD_PARAM;
+    bool d = false;
+    const int rc = test_one(r, &d);
+    *done = d ? 1 : 0;
+    if (d) fill_status(r, st);
+    return rc;
+}
+
+int ompi_amd_p2p_wait(ompi_amd_p2p_request_t *r, ompi_amd_status_t *st) {
+    if (!r) return OMPI_AMD_ERR_BAD_PARAM;
+    const int rc = wait_one(r);
+    fill_status(r, st);
+    return rc;
+}
+
+int ompi_amd_p2p_free(ompi_amd_p2p_request_t *r) {
+    if (!r) return OMPI_AMD_SUCCESS;
+    int rc = OMPI_AMD_SUCCESS;
+    if (!r->done) rc = wait_one(r);
+    if (!r->done) return rc;  // still referenced by the mailbox: keep it
+    if (r->ev) (void)hipEventDestroy(r->ev);
+    delete r;
+    return rc;
+}
+
+int ompi_amd_send(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, int tag, int mode,
+                  void *stream) {
+    ompi_amd_p2p_request_t *r = nullptr;
+    int rc = ompi_amd_isend(c, buf, bytes, dst, tag, mode, stream, &r);
+    if (rc != OMPI_AMD_SUCCESS) return rc;
+    return ompi_amd_p2p_free(r);
+}
+
+int ompi_amd_recv(ompi_amd_comm_t *c, void *buf, size_t bytes, int src, int tag, void *stream,
+                  ompi_amd_status_t *st) {
+    ompi_amd_p2p_request_t *r = nullptr;
+    int rc = ompi_amd_irecv(c, buf, bytes, src, tag, stream, &r);
+    if (rc != OMPI_AMD_SUCCESS) return rc;
+    rc = wait_one(r);
+    fill_status(r, st);
+    const int frc = ompi_amd_p2p_free(r);
+    return rc != OMPI_AMD_SUCCESS ? rc : frc;
+}
+
+int ompi_amd_sendrecv(ompi_amd_comm_t *c, const void *sbuf, size_t sbytes, int dst, int stag,
+                      void *rbuf, size_t rbytes, int src, int rtag, void *stream,
+                      ompi_amd_status_t *st) {
+    ompi_amd_p2p_request_t *rr = nullptr, *sr = nullptr;
+    int rc = ompi_amd_irecv(c, rbuf, rbytes, src, rtag, stream, &rr);
+    if (rc != OMPI_AMD_SUCCESS) return rc;
+    rc = ompi_amd_isend(c, sbuf, sbytes, dst, stag, OMPI_AMD_SEND_STANDARD, stream, &sr);
+    if (rc != OMPI_AMD_SUCCESS) {
+        (void)ompi_amd_p2p_free(rr);
+        return rc;
+    }
+    const int rrc = wait_one(rr);
+    fill_status(rr, st);
+    const int src_ = wait_one(sr);
+    (void)ompi_amd_p2p_free(rr);
+    (void)ompi_amd_p2p_free(sr);
+    return rrc != OMPI_AMD_SUCCESS ? rrc : src_;
+}
+
+int ompi_amd_iprobe(ompi_amd_comm_t *c, int src, int tag, int *flag, ompi_amd_status_t *st) {
+    if (!c || !flag) return OMPI_AMD_ERR_BAD_PARAM;
+    p2p_state *p = comm_p2p(c);
+    if (!p || src < OMPI_AMD_ANY_SOURCE || src >= p->size) return OMPI_AMD_ERR_BAD_PARAM;
+    std::lock_guard<std::recursive_mutex> g(p->mu);
+    progress(p);  // posted receives match first
+    int s = -1;
+    msg_slot *m = find(p, src, tag, &s);
+    *flag = m ? 1 : 0;
+    if (m && st) {
+        st->source = s;
+        st->tag = m->tag;
+        st->error = OMPI_AMD_SUCCESS;
+        st->bytes = m->bytes;
+    }
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_probe(ompi_amd_comm_t *c, int src, int tag, ompi_amd_status_t *st) {
+    if (!c) return OMPI_AMD_ERR_BAD_PARAM;
+    const double limit = (double)comm_timeout_ms(c) / 1000.0, t0 = now_s();
+    for (;;) {
+        int flag = 0;
+        const int rc = ompi_amd_iprobe(c, src, tag, &flag, st);
+        if (rc != OMPI_AMD_SUCCESS || flag) return rc;
+        sched_yield();
+        if (now_s() - t0 > limit) {
+            record_msg("probe(%d, %d) timed out after %.1f s", src, tag, limit);
+            return OMPI_AMD_ERR_TIMEOUT;
+        }
+    }
+}
+
+}  // extern "C"

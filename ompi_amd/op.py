@@ -48,6 +48,9 @@ MPI_LXOR = Op("MPI_LXOR", 9)
 MPI_BXOR = Op("MPI_BXOR", 10)
 MPI_MAXLOC = Op("MPI_MAXLOC", 11)
 MPI_MINLOC = Op("MPI_MINLOC", 12)
+# one-sided only (MPI_Accumulate / MPI_Get_accumulate, ompi/mca/op/op.h:232-235)
+MPI_REPLACE = Op("MPI_REPLACE", 13)
+MPI_NO_OP = Op("MPI_NO_OP", 14)
 OPS = [MPI_MAX, MPI_MIN, MPI_SUM, MPI_PROD, MPI_LAND, MPI_BAND, MPI_LOR,
        MPI_BOR, MPI_LXOR, MPI_BXOR, MPI_MAXLOC, MPI_MINLOC]
 

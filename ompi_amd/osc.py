@@ -1,0 +1,131 @@
+"""One-sided communication on device windows (the osc surface for device
+memory).
+
+Mirrors osc/sm's module functions (ompi/mca/osc/sm/osc_sm_comm.c,
+osc_sm_active_target.c, osc_sm_passive_target.c):
+
+    put / get                      osc_sm_comm.c:209-268
+    accumulate                     osc_sm_comm.c:271-309
+    get_accumulate                 osc_sm_comm.c:312-360
+    compare_and_swap               osc_sm_comm.c:363-400
+    fetch_and_op                   osc_sm_comm.c:403-441
+    fence                          osc_sm_active_target.c:95-115
+    lock / unlock / lock_all / unlock_all / flush
+                                   osc_sm_passive_target.c:113-270
+
+Displacements are in the target's disp_unit, counts in elements of the
+datatype.  Every call is stream-ordered on the origin's stream; the RMA
+kernels load and store the target's memory over xGMI
+(include/ompi_amd_osc.h).  There is no host fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+
+from . import _lib
+from .coll import Communicator, _ptr, _stream
+from .op import Datatype, Op
+
+LOCK_EXCLUSIVE = 1   # MPI_LOCK_EXCLUSIVE (mpi.h.in:548)
+LOCK_SHARED = 2      # MPI_LOCK_SHARED (mpi.h.in:549)
+MODE_NOCHECK = 1     # MPI_MODE_NOCHECK (mpi.h.in:542)
+
+
+class Window:
+    """MPI_Win over device memory of every rank of `comm`."""
+
+    def __init__(self, comm: Communicator, handle, base_ptr: int, nbytes: int):
+        self.comm, self._h, self.base_ptr, self.nbytes = comm, handle, base_ptr, nbytes
+        self._lib = comm._lib
+
+    @classmethod
+    def create(cls, comm: Communicator, base, nbytes: int | None = None,
+               disp_unit: int = 1) -> "Window":
+        """MPI_Win_create (collective) over a device tensor / pointer."""
+        if nbytes is None:
+            nbytes = base.numel() * base.element_size() if base is not None else 0
+        ptr = _ptr(base) if nbytes else None
+        h = ctypes.c_void_p()
+        _lib.check(comm._lib.ompi_amd_win_create(comm._h, ptr, nbytes, disp_unit,
+                                                 ctypes.byref(h)), "win_create")
+        return cls(comm, h, ptr or 0, nbytes)
+
+    @classmethod
+    def allocate(cls, comm: Communicator, nbytes: int, disp_unit: int = 1) -> "Window":
+        """MPI_Win_allocate (collective): zeroed device memory owned by the
+        window; `base_ptr` is its address."""
+        h, b = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(comm._lib.ompi_amd_win_allocate(comm._h, nbytes, disp_unit, ctypes.byref(b),
+                                                   ctypes.byref(h)), "win_allocate")
+        return cls(comm, h, b.value or 0, nbytes)
+
+    def free(self) -> None:
+        if self._h:
+            h, self._h = self._h, None
+            _lib.check(self._lib.ompi_amd_win_free(h), "win_free")
+
+    # -- synchronisation -----------------------------------------------------
+    def _done(self, rc: int, what: str, blocking: bool, stream) -> None:
+        self.comm._finish(rc, what, blocking, stream)
+
+    def fence(self, assert_: int = 0, stream=None, blocking: bool = False) -> None:
+        self._done(self._lib.ompi_amd_win_fence(self._h, assert_, _stream(stream)), "win_fence",
+                   blocking, stream)
+
+    def lock(self, target: int, lock_type: int = LOCK_EXCLUSIVE, assert_: int = 0,
+             stream=None) -> None:
+        _lib.check(self._lib.ompi_amd_win_lock(self._h, lock_type, target, assert_,
+                                               _stream(stream)), "win_lock")
+
+    def unlock(self, target: int, stream=None, blocking: bool = True) -> None:
+        self._done(self._lib.ompi_amd_win_unlock(self._h, target, _stream(stream)), "win_unlock",
+                   blocking, stream)
+
+    def lock_all(self, assert_: int = 0, stream=None) -> None:
+        _lib.check(self._lib.ompi_amd_win_lock_all(self._h, assert_, _stream(stream)),
+                   "win_lock_all")
+
+    def unlock_all(self, stream=None, blocking: bool = True) -> None:
+        self._done(self._lib.ompi_amd_win_unlock_all(self._h, _stream(stream)), "win_unlock_all",
+                   blocking, stream)
+
+    def flush(self, target: int, stream=None) -> None:
+        _lib.check(self._lib.ompi_amd_win_flush(self._h, target, _stream(stream)), "win_flush")
+
+    # -- communication -------------------------------------------------------
+    def put(self, origin, target: int, disp: int, nbytes: int | None = None, stream=None) -> None:
+        n = origin.numel() * origin.element_size() if nbytes is None else nbytes
+        _lib.check(self._lib.ompi_amd_put(self._h, _ptr(origin), n, target, disp,
+                                          _stream(stream)), "put")
+
+    def get(self, origin, target: int, disp: int, nbytes: int | None = None, stream=None) -> None:
+        n = origin.numel() * origin.element_size() if nbytes is None else nbytes
+        _lib.check(self._lib.ompi_amd_get(self._h, _ptr(origin), n, target, disp,
+                                          _stream(stream)), "get")
+
+    def accumulate(self, origin, count: int, datatype: Datatype, target: int, disp: int, op: Op,
+                   stream=None) -> None:
+        _lib.check(self._lib.ompi_amd_accumulate(self._h, _ptr(origin), count, datatype.code,
+                                                 target, disp, op.index, _stream(stream)),
+                   f"accumulate({op.name}, {datatype.name})")
+
+    def get_accumulate(self, origin, result, count: int, datatype: Datatype, target: int,
+                       disp: int, op: Op, stream=None) -> None:
+        optr = _ptr(origin) if origin is not None else None
+        _lib.check(self._lib.ompi_amd_get_accumulate(self._h, optr, _ptr(result), count,
+                                                     datatype.code, target, disp, op.index,
+                                                     _stream(stream)),
+                   f"get_accumulate({op.name}, {datatype.name})")
+
+    def fetch_and_op(self, origin, result, datatype: Datatype, target: int, disp: int, op: Op,
+                     stream=None) -> None:
+        optr = _ptr(origin) if origin is not None else None
+        _lib.check(self._lib.ompi_amd_fetch_and_op(self._h, optr, _ptr(result), datatype.code,
+                                                   target, disp, op.index, _stream(stream)),
+                   f"fetch_and_op({op.name}, {datatype.name})")
+
+    def compare_and_swap(self, origin, compare, result, datatype: Datatype, target: int,
+                         disp: int, stream=None) -> None:
+        _lib.check(self._lib.ompi_amd_compare_and_swap(self._h, _ptr(origin), _ptr(compare),
+                                                       _ptr(result), datatype.code, target, disp,
+                                                       _stream(stream)), "compare_and_swap")

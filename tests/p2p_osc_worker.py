@@ -1,0 +1,514 @@
+"""One rank of the multi-process point-to-point and one-sided tests
+(tests/test_p2p_osc_gpu.py).
+
+Launched N times with RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT and
+OMPI_AMD_DEVICE.  A gloo group broadcasts the communicator name and
+separates the cases; all data moves through libompi_amd.so on device
+buffers.  Expected results come from the deterministic per-rank inputs and,
+for accumulates, from the CPU oracle's op/base restatement applied in the
+target's order.  One JSON line per case; exit 0 only if all passed.
+"""
+import json
+import os
+import sys
+import traceback
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from ompi_amd import _lib, coll, osc, pml  # noqa: E402
+from ompi_amd import op as mop  # noqa: E402
+from oracle import oracle as orc  # noqa: E402
+
+SEED = 20261015
+STREAM = None  # a dedicated stream (a NULL stream argument means hipStreamPerThread)
+
+
+def payload(rank: int, salt: int, nbytes: int) -> np.ndarray:
+    return np.random.default_rng(SEED + 7919 * salt + rank).integers(0, 256, nbytes, dtype=np.uint8)
+
+
+def dev(a: np.ndarray, extra: int = 0) -> torch.Tensor:
+    raw = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+    t = zeros(raw.nbytes + extra)
+    with torch.cuda.stream(STREAM):
+        t[:raw.nbytes].copy_(torch.from_numpy(raw.copy()))
+    STREAM.synchronize()
+    return t
+
+
+def zeros(nbytes: int) -> torch.Tensor:
+    """A zeroed device buffer, filled before any stream uses it (torch fills
+    on its current stream, which does not order against STREAM)."""
+    t = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    return t
+
+
+def host(t: torch.Tensor) -> np.ndarray:
+    STREAM.synchronize()
+    return t.cpu().numpy()
+
+
+def eq(got: np.ndarray, exp: np.ndarray, what: str):
+    g = np.ascontiguousarray(got).view(np.uint8).reshape(-1)
+    e = np.ascontiguousarray(exp).view(np.uint8).reshape(-1)
+    if g.shape == e.shape and np.array_equal(g, e):
+        return True, ""
+    if g.shape != e.shape:
+        return False, f"{what}: {g.shape} vs {e.shape} bytes"
+    bad = np.flatnonzero(g != e)
+    return False, f"{what}: {bad.size} bytes differ, first at {bad[:4].tolist()}"
+
+
+# ----------------------------------------------------------------- p2p cases
+def case_ring(comm, rank, n, nbytes, salt, soff=0, roff=0):
+    """sendrecv around the ring (MPI_Sendrecv to rank+1 from rank-1), with
+    byte offsets into both buffers."""
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    s = dev(payload(rank, salt, nbytes), extra=soff + 8)
+    if soff:
+        s = dev(np.concatenate([np.zeros(soff, np.uint8), payload(rank, salt, nbytes)]), extra=8)
+    r = zeros(nbytes + roff + 8)
+    st = pml.sendrecv(comm, s[soff:soff + nbytes] if nbytes else s, nxt, 100 + salt,
+                      r[roff:roff + nbytes] if nbytes else r, prv, 100 + salt,
+                      sbytes=nbytes, rbytes=nbytes, stream=STREAM)
+    if (st.source, st.tag, st.bytes) != (prv, 100 + salt, nbytes):
+        return False, f"status {st}"
+    got = host(r)
+    ok, msg = eq(got[roff:roff + nbytes], payload(prv, salt, nbytes), "payload")
+    if ok and (got[:roff].any() or got[roff + nbytes:].any()):
+        return False, "bytes outside the receive window were written"
+    return ok, msg
+
+
+def case_tags_out_of_order(comm, rank, n, salt):
+    """Three sends with tags 5, 6, 7; receives posted as 7, 5, 6."""
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    sizes = {5: 1000, 6: 70001, 7: 3}
+    sends = {t: dev(payload(rank, salt + t, b)) for t, b in sizes.items()}
+    reqs = [pml.isend(comm, sends[t], nxt, t, stream=STREAM) for t in (5, 6, 7)]
+    rbufs = {t: zeros(sizes[t]) for t in sizes}
+    rreqs = {t: pml.irecv(comm, rbufs[t], prv, t, stream=STREAM) for t in (7, 5, 6)}
+    for t, rq in rreqs.items():
+        st = rq.wait()
+        if st.tag != t or st.source != prv or st.bytes != sizes[t]:
+            return False, f"tag {t}: status {st}"
+        ok, msg = eq(host(rbufs[t]), payload(prv, salt + t, sizes[t]), f"tag {t}")
+        if not ok:
+            return ok, msg
+        rq.free()
+    for rq in reqs:
+        rq.wait()
+        rq.free()
+    return True, ""
+
+
+def case_same_tag_order(comm, rank, n, salt, k=40):
+    """k messages with one tag: received in sending order (non-overtaking)."""
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    sends = [dev(payload(rank, salt + i, 257 + i)) for i in range(k)]
+    reqs = [pml.isend(comm, sends[i], nxt, 9, stream=STREAM) for i in range(k)]
+    fails = []
+    for i in range(k):
+        r = zeros(257 + i)
+        st = pml.recv(comm, r, prv, 9, stream=STREAM)
+        if st.bytes != 257 + i:
+            fails.append(f"msg {i}: {st.bytes} bytes")
+            continue
+        ok, msg = eq(host(r), payload(prv, salt + i, 257 + i), f"msg {i}")
+        if not ok:
+            fails.append(msg)
+    for rq in reqs:
+        rq.wait()
+        rq.free()
+    return not fails, "; ".join(fails[:3])
+
+
+def case_any_source(comm, rank, n, salt):
+    """Every rank but 0 sends to 0 with tag = its rank; rank 0 receives with
+    ANY_SOURCE / ANY_TAG and checks each status against the data."""
+    if rank != 0:
+        pml.send(comm, dev(payload(rank, salt, 4096 + rank)), 0, rank, stream=STREAM)
+        return True, ""
+    seen = set()
+    for _ in range(n - 1):
+        r = zeros(8192)
+        st = pml.recv(comm, r, pml.ANY_SOURCE, pml.ANY_TAG, stream=STREAM)
+        if st.tag != st.source or st.bytes != 4096 + st.source or st.source in seen:
+            return False, f"status {st}"
+        seen.add(st.source)
+        ok, msg = eq(host(r)[:st.bytes], payload(st.source, salt, st.bytes), f"from {st.source}")
+        if not ok:
+            return ok, msg
+    return seen == set(range(1, n)), f"sources {sorted(seen)}"
+
+
+def case_probe_truncate(comm, rank, n, salt):
+    """probe reports the size; a short receive raises MPI_ERR_TRUNCATE with
+    the prefix delivered; traffic continues afterwards."""
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    a = dev(payload(rank, salt, 1000))
+    b = dev(payload(rank, salt + 1, 77))
+    r1 = pml.isend(comm, a, nxt, 3, stream=STREAM)
+    r2 = pml.isend(comm, b, nxt, 4, stream=STREAM)
+    st = pml.probe(comm, prv, 3)
+    if (st.source, st.tag, st.bytes) != (prv, 3, 1000):
+        return False, f"probe {st}"
+    if pml.iprobe(comm, prv, 99) is not None:
+        return False, "iprobe matched a tag nobody sent"
+    short = zeros(600)
+    try:
+        pml.recv(comm, short, prv, 3, stream=STREAM)
+        return False, "no truncation error"
+    except _lib.OmpiAmdError as e:
+        if e.code != _lib.ERR_TRUNCATE:
+            return False, f"error {e}"
+    ok, msg = eq(host(short), payload(prv, salt, 1000)[:600], "truncated prefix")
+    if not ok:
+        return ok, msg
+    rb = zeros(77)
+    st = pml.recv(comm, rb, prv, 4, stream=STREAM)
+    for rq in (r1, r2):
+        rq.wait()
+        rq.free()
+    return eq(host(rb), payload(prv, salt + 1, 77), "after truncation")
+
+
+def case_self(comm, rank, n, salt):
+    a = dev(payload(rank, salt, 123457))
+    rq = pml.isend(comm, a, rank, 11, stream=STREAM)
+    r = zeros(123457)
+    st = pml.recv(comm, r, rank, 11, stream=STREAM)
+    rq.wait()
+    rq.free()
+    if st.source != rank:
+        return False, f"status {st}"
+    return eq(host(r), payload(rank, salt, 123457), "self")
+
+
+# ----------------------------------------------------------------- osc cases
+def fp_inputs(dt, count, rank, salt, kind="R"):
+    rng = np.random.default_rng(SEED + 1000 * salt + rank)
+    nd = dt.np_dtype
+    if nd.names:
+        a = np.zeros(count, dtype=nd)
+        a["v"] = np.round(rng.random(count) * 64) / 64
+        a["k"] = rank * count + np.arange(count)
+        return a
+    if nd.kind == "f":
+        if kind == "E":
+            return (rng.integers(-1024, 1025, count) * 2.0 ** -8).astype(nd)
+        a = rng.uniform(-1, 1, count).astype(nd)
+        if kind == "S":
+            idx = rng.integers(0, count, max(1, count // 8))
+            a[idx] = rng.choice(np.array([np.nan, 0.0, -0.0, np.inf, -np.inf], dtype=nd), len(idx))
+        return a
+    info = np.iinfo(nd)
+    lo, hi = (-(1 << 20), 1 << 20) if nd.itemsize >= 4 else (info.min, info.max)
+    return rng.integers(max(lo, info.min), hi, count, dtype=nd, endpoint=True)
+
+
+def case_put_get(comm, rank, n, nbytes, salt):
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    win = osc.Window.allocate(comm, nbytes + 64, disp_unit=1)
+    try:
+        src = dev(payload(rank, salt, nbytes))
+        win.fence(stream=STREAM)
+        win.put(src, nxt, 13, nbytes, stream=STREAM)
+        win.fence(stream=STREAM, blocking=True)
+        local = torch.empty(nbytes + 64, dtype=torch.uint8, device="cuda")
+        win.get(local, rank, 0, stream=STREAM)  # own window through the same path
+        got = host(local)
+        exp = np.zeros(nbytes + 64, np.uint8)
+        exp[13:13 + nbytes] = payload(prv, salt, nbytes)
+        ok, msg = eq(got, exp, "put")
+        if not ok:
+            return ok, msg
+        back = zeros(nbytes)
+        win.get(back, nxt, 13, stream=STREAM)  # next rank's window holds my data
+        win.fence(stream=STREAM, blocking=True)
+        return eq(host(back), payload(rank, salt, nbytes), "get")
+    finally:
+        win.free()
+
+
+def case_acc_disjoint(comm, rank, n, dt, op, count, salt, kind="R"):
+    """Each rank accumulates into the next rank's window (one origin per
+    target): deterministic, bit-exact vs op/base incl. NaN / ±0 selection."""
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    ext = dt.extent
+    win_init = [fp_inputs(dt, count, r, salt, kind) for r in range(n)]
+    origins = [fp_inputs(dt, count, r, salt + 1, kind) for r in range(n)]
+    base = dev(win_init[rank], extra=16)
+    win = osc.Window.create(comm, base, count * ext + 16, disp_unit=ext)
+    try:
+        o = dev(origins[rank])
+        win.fence(stream=STREAM)
+        win.accumulate(o, count, dt, nxt, 0, op, stream=STREAM)
+        win.fence(stream=STREAM, blocking=True)
+        exp = win_init[rank].copy()
+        orc.op_2buff(op.index, dt.code, origins[prv].copy(), exp, count)
+        got = host(base)[:count * ext].view(dt.np_dtype)
+        if dt.np_dtype.names:  # gap bytes carry no data
+            ok1, m1 = eq(got["v"], exp["v"], "v")
+            ok2, m2 = eq(got["k"], exp["k"], "k")
+            return ok1 and ok2, m1 + m2
+        return eq(got, exp, op.name)
+    finally:
+        win.free()
+
+
+def case_acc_concurrent(comm, rank, n, dt, op, count, salt, kind="E"):
+    """Every rank accumulates into the SAME region of rank 0 at once: the
+    accumulate lock serialises them; with exact data every order agrees."""
+    ext = dt.extent
+    init = fp_inputs(dt, count, 99, salt, kind)
+    origins = [fp_inputs(dt, count, r, salt + 1, kind) for r in range(n)]
+    base = dev(init if rank == 0 else np.zeros(0, np.uint8), extra=16)
+    win = osc.Window.create(comm, base, base.numel(), disp_unit=ext)
+    try:
+        o = dev(origins[rank])
+        win.fence(stream=STREAM)
+        for _ in range(2):
+            win.accumulate(o, count, dt, 0, 0, op, stream=STREAM)
+        win.fence(stream=STREAM, blocking=True)
+        if rank != 0:
+            return True, ""
+        exp = init.copy()
+        for r in range(n):
+            for _ in range(2):
+                orc.op_2buff(op.index, dt.code, origins[r].copy(), exp, count)
+        got = host(base)[:count * ext].view(dt.np_dtype)
+        if dt.np_dtype.names:
+            ok1, m1 = eq(got["v"], exp["v"], "v")
+            ok2, m2 = eq(got["k"], exp["k"], "k")
+            return ok1 and ok2, m1 + m2
+        return eq(got, exp, op.name)
+    finally:
+        win.free()
+
+
+def case_get_accumulate(comm, rank, n, salt, count=50001):
+    """result = old target; target = old + origin (fp64, exact data); then
+    REPLACE and NO_OP."""
+    D = mop.MPI_DOUBLE
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    init = [fp_inputs(D, count, r, salt, "E") for r in range(n)]
+    org = [fp_inputs(D, count, r, salt + 1, "E") for r in range(n)]
+    base = dev(init[rank])
+    win = osc.Window.create(comm, base, count * 8, disp_unit=8)
+    try:
+        o = dev(org[rank])
+        res = zeros(count * 8)
+        win.fence(stream=STREAM)
+        win.get_accumulate(o, res, count, D, nxt, 0, mop.MPI_SUM, stream=STREAM)
+        win.fence(stream=STREAM, blocking=True)
+        ok, msg = eq(host(res).view(np.float64), init[nxt], "fetched")
+        if not ok:
+            return ok, msg
+        ok, msg = eq(host(base).view(np.float64), init[rank] + org[prv], "summed")
+        if not ok:
+            return ok, msg
+        comm_barrier()  # every rank checked its window before the next epoch writes it
+        # REPLACE via get_accumulate, then NO_OP fetch
+        win.get_accumulate(o, res, count, D, nxt, 0, mop.MPI_REPLACE, stream=STREAM)
+        win.fence(stream=STREAM, blocking=True)
+        ok, msg = eq(host(res).view(np.float64), init[nxt] + org[rank], "fetched before replace")
+        if not ok:
+            return ok, msg
+        res2 = zeros(count * 8)
+        win.get_accumulate(None, res2, count, D, nxt, 0, mop.MPI_NO_OP, stream=STREAM)
+        win.fence(stream=STREAM, blocking=True)
+        ok, msg = eq(host(res2).view(np.float64), org[rank], "no_op fetch after replace")
+        if not ok:
+            return ok, msg
+        return eq(host(base).view(np.float64), org[prv], "replaced")
+    finally:
+        win.free()
+
+
+def case_fetch_and_op_counter(comm, rank, n, k=25):
+    """Shared counter on rank 0: k fetch_and_op(+1) per rank; the fetched
+    values over all ranks are exactly 0 .. n*k-1 (each increment atomic)."""
+    I64 = mop.MPI_INT64_T
+    win = osc.Window.allocate(comm, 64 if rank == 0 else 0, disp_unit=8)
+    try:
+        one = dev(np.array([1], np.int64))
+        res = zeros(8 * k)
+        win.fence(stream=STREAM)
+        for i in range(k):
+            win.fetch_and_op(one, res[8 * i:8 * i + 8], I64, 0, 0, mop.MPI_SUM, stream=STREAM)
+        win.fence(stream=STREAM, blocking=True)
+        mine = host(res).view(np.int64).tolist()
+        everyone = [None] * n
+        dist.all_gather_object(everyone, mine)
+        allv = sorted(v for lst in everyone for v in lst)
+        if allv != list(range(n * k)):
+            return False, f"fetched values not a permutation: {allv[:10]}..."
+        if rank == 0:
+            t = torch.empty(8, dtype=torch.uint8, device="cuda")
+            win.get(t, 0, 0, stream=STREAM)
+            if int(host(t).view(np.int64)[0]) != n * k:
+                return False, f"counter {host(t).view(np.int64)[0]}"
+        return True, ""
+    finally:
+        win.free()
+
+
+def case_cas(comm, rank, n):
+    """compare_and_swap(-1 -> rank) on rank 0: exactly one winner."""
+    I32 = mop.MPI_INT32_T
+    base = dev(np.array([-1, 0, 0, 0], np.int32))
+    win = osc.Window.create(comm, base, 16, disp_unit=4)
+    try:
+        org = dev(np.array([rank], np.int32))
+        cmp = dev(np.array([-1], np.int32))
+        res = zeros(4)
+        win.fence(stream=STREAM)
+        win.compare_and_swap(org, cmp, res, I32, 0, 0, stream=STREAM)
+        win.fence(stream=STREAM, blocking=True)
+        got = int(host(res).view(np.int32)[0])
+        everyone = [None] * n
+        dist.all_gather_object(everyone, got)
+        winners = [r for r, v in enumerate(everyone) if v == -1]
+        if len(winners) != 1:
+            return False, f"results {everyone}"
+        w = winners[0]
+        if any(v != w for r, v in enumerate(everyone) if r != w):
+            return False, f"losers must see the winner {w}: {everyone}"
+        if rank == 0 and int(host(base).view(np.int32)[0]) != w:
+            return False, f"target holds {host(base).view(np.int32)[0]}, winner {w}"
+        return True, ""
+    finally:
+        win.free()
+
+
+def case_passive_exclusive(comm, rank, n, k=10):
+    """Read-modify-write of a counter under MPI_Win_lock(EXCLUSIVE): get,
+    +1 on the device, put, unlock — k times per rank; final = n*k."""
+    win = osc.Window.allocate(comm, 8 if rank == 0 else 0, disp_unit=8)
+    try:
+        comm_barrier()
+        buf = zeros(8).view(torch.int64)
+        for _ in range(k):
+            win.lock(0, osc.LOCK_EXCLUSIVE, stream=STREAM)
+            win.get(buf, 0, 0, 8, stream=STREAM)
+            with torch.cuda.stream(STREAM):
+                buf.add_(1)
+            win.put(buf, 0, 0, 8, stream=STREAM)
+            win.unlock(0, stream=STREAM, blocking=True)
+        comm_barrier()
+        if rank == 0:
+            win.lock(0, osc.LOCK_SHARED, stream=STREAM)
+            win.get(buf, 0, 0, 8, stream=STREAM)
+            win.unlock(0, stream=STREAM, blocking=True)
+            if int(host(buf)[0]) != n * k:
+                return False, f"counter {int(host(buf)[0])} != {n * k}"
+        return True, ""
+    finally:
+        win.free()
+
+
+def case_lock_all(comm, rank, n, salt, nbytes=100003):
+    """lock_all (shared), get every rank's window, flush, unlock_all."""
+    base = dev(payload(rank, salt, nbytes))
+    win = osc.Window.create(comm, base, nbytes)
+    try:
+        comm_barrier()
+        outs = [zeros(nbytes) for _ in range(n)]
+        win.lock_all(stream=STREAM)
+        for p in range(n):
+            win.get(outs[p], p, 0, stream=STREAM)
+        win.flush(0, stream=STREAM)
+        win.unlock_all(stream=STREAM)
+        for p in range(n):
+            ok, msg = eq(host(outs[p]), payload(p, salt, nbytes), f"rank {p}")
+            if not ok:
+                return ok, msg
+        return True, ""
+    finally:
+        win.free()
+
+
+def comm_barrier():
+    STREAM.synchronize()
+    dist.barrier()
+
+
+def main():
+    global STREAM
+    rank, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    device = int(os.environ.get("OMPI_AMD_DEVICE", "0"))
+    torch.cuda.set_device(device)
+    STREAM = torch.cuda.Stream()
+    dist.init_process_group("gloo", rank=rank, world_size=n)
+    comm = coll.Communicator.from_torch_distributed(device=device)
+    comm.set_param("timeout_ms", 20000)
+    F, D, I32, I64, DI, U8 = (mop.MPI_FLOAT, mop.MPI_DOUBLE, mop.MPI_INT32_T, mop.MPI_INT64_T,
+                              mop.MPI_DOUBLE_INT, mop.MPI_UINT8_T)
+    cases = [
+        ("p2p_ring_0B", lambda: case_ring(comm, rank, n, 0, 1)),
+        ("p2p_ring_1B", lambda: case_ring(comm, rank, n, 1, 2)),
+        ("p2p_ring_4099B_misaligned", lambda: case_ring(comm, rank, n, 4099, 3, soff=3, roff=5)),
+        ("p2p_ring_64MiB", lambda: case_ring(comm, rank, n, 64 << 20, 4)),
+        ("p2p_ring_16MiB_plus_odd", lambda: case_ring(comm, rank, n, (16 << 20) + 13, 5, 16, 16)),
+        ("p2p_tags_out_of_order", lambda: case_tags_out_of_order(comm, rank, n, 6)),
+        ("p2p_same_tag_order", lambda: case_same_tag_order(comm, rank, n, 20)),
+        ("p2p_any_source_any_tag", lambda: case_any_source(comm, rank, n, 70)),
+        ("p2p_probe_truncate", lambda: case_probe_truncate(comm, rank, n, 71)),
+        ("p2p_self", lambda: case_self(comm, rank, n, 72)),
+        ("osc_put_get_small", lambda: case_put_get(comm, rank, n, 1001, 80)),
+        ("osc_put_get_32MiB", lambda: case_put_get(comm, rank, n, 32 << 20, 81)),
+        ("osc_acc_sum_f32", lambda: case_acc_disjoint(comm, rank, n, F, mop.MPI_SUM, 1000003, 82)),
+        ("osc_acc_prod_f64", lambda: case_acc_disjoint(comm, rank, n, D, mop.MPI_PROD, 30001, 83)),
+        ("osc_acc_max_f32_specials",
+         lambda: case_acc_disjoint(comm, rank, n, F, mop.MPI_MAX, 100001, 84, "S")),
+        ("osc_acc_min_f64_specials",
+         lambda: case_acc_disjoint(comm, rank, n, D, mop.MPI_MIN, 20001, 85, "S")),
+        ("osc_acc_band_i64", lambda: case_acc_disjoint(comm, rank, n, I64, mop.MPI_BAND, 7777, 86)),
+        ("osc_acc_bxor_u8_odd", lambda: case_acc_disjoint(comm, rank, n, U8, mop.MPI_BXOR, 1237, 87)),
+        ("osc_acc_maxloc_double_int",
+         lambda: case_acc_disjoint(comm, rank, n, DI, mop.MPI_MAXLOC, 40001, 88)),
+        ("osc_acc_concurrent_sum_f32_exact",
+         lambda: case_acc_concurrent(comm, rank, n, F, mop.MPI_SUM, 262147, 89)),
+        ("osc_acc_concurrent_sum_i32",
+         lambda: case_acc_concurrent(comm, rank, n, I32, mop.MPI_SUM, 65537, 90)),
+        ("osc_acc_concurrent_maxloc",
+         lambda: case_acc_concurrent(comm, rank, n, DI, mop.MPI_MAXLOC, 30001, 91)),
+        ("osc_get_accumulate", lambda: case_get_accumulate(comm, rank, n, 92)),
+        ("osc_fetch_and_op_counter", lambda: case_fetch_and_op_counter(comm, rank, n)),
+        ("osc_compare_and_swap", lambda: case_cas(comm, rank, n)),
+        ("osc_passive_exclusive_rmw", lambda: case_passive_exclusive(comm, rank, n)),
+        ("osc_lock_all_get", lambda: case_lock_all(comm, rank, n, 93)),
+    ]
+    only = os.environ.get("P2P_OSC_ONLY")
+    all_ok = True
+    for name, fn in cases:
+        if only and only not in name:
+            continue
+        comm_barrier()
+        try:
+            ok, msg = fn()
+        except Exception as e:  # noqa: BLE001 - reported per case
+            ok, msg = False, f"{type(e).__name__}: {e}\n{traceback.format_exc()[-1200:]}"
+        all_ok &= bool(ok)
+        print(json.dumps({"rank": rank, "case": name, "ok": bool(ok), "msg": msg}), flush=True)
+        if comm.error():
+            print(json.dumps({"rank": rank, "case": name + "/sticky", "ok": False,
+                              "msg": f"device error {comm.error()}"}), flush=True)
+            all_ok = False
+            break
+    comm_barrier()
+    comm.free()
+    dist.destroy_process_group()
+    sys.exit(0 if all_ok else 1)
+
+
+if __name__ == "__main__":
+    main()

@@ -27,7 +27,7 @@ def free_port():
         return s.getsockname()[1]
 
 
-def run_ranks(n, timeout=600, extra_env=None):
+def run_ranks(n, timeout=600, extra_env=None, worker=WORKER):
     ngpu = torch.cuda.device_count()
     port = free_port()
     procs = []
@@ -38,7 +38,7 @@ def run_ranks(n, timeout=600, extra_env=None):
                     "OMPI_AMD_DEVICE": str(r % ngpu if ngpu >= n else 0),
                     "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
         env.update(extra_env or {})
-        procs.append(subprocess.Popen([sys.executable, WORKER], env=env, stdout=subprocess.PIPE,
+        procs.append(subprocess.Popen([sys.executable, worker], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT, text=True))
     outs = []
     try:

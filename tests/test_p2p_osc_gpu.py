@@ -1,0 +1,27 @@
+"""Multi-process point-to-point and one-sided (§8f row 4)
+tests on device buffers: N ranks run tests/p2p_osc_worker.py.  On a one-GPU
+box all ranks share cuda:0 (IPC mappings, mailboxes, lock words and kernels
+are exercised exactly as across GPUs; only the link differs)."""
+import json
+import os
+
+import pytest
+
+from test_coll_gpu import run_ranks
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKER = os.path.join(ROOT, "tests", "p2p_osc_worker.py")
+
+
+@pytest.mark.parametrize("n", [2, 3, 4])
+def test_p2p_osc_parity(n):
+    outs = run_ranks(n, timeout=300, worker=WORKER)
+    failures = []
+    for r, (rc, out) in enumerate(outs):
+        lines = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+        bad = [ln for ln in lines if not ln["ok"]]
+        if rc != 0 or bad or not lines:
+            failures.append((r, rc, bad[:4], out[-2000:] if not lines or rc not in (0, 1) else ""))
+    assert not failures, failures
