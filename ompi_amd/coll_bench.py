@@ -155,6 +155,7 @@ def bench_allreduce(args, metric: str, link_gbs: float):
             res["config5"] = _config5(comm, dist, torch, mop, world, rank, tdev)
             res["variants"] = _variants(comm, dist, torch, mop, world, tdev)
             res["next_rows"] = _next_rows(comm, dist, torch, mop, world, rank, tdev)
+            res["p2p_osc"] = _p2p_osc_rows(comm, dist, torch, mop, world, rank, tdev)
         except Exception as e:  # extras never break the headline line
             res["extras_error"] = f"{type(e).__name__}: {e}"
     comm.free()
@@ -328,4 +329,61 @@ def _next_rows(comm, dist, torch, mop, world, rank, tdev):
         rows.append(row)
         del x, y
     res["allreduce_call_kinds"] = rows
+    return res
+
+
+def _p2p_osc_rows(comm, dist, torch, mop, world, rank, tdev):
+    """SURVEY §8f rows 1 and 4 beside the headline: device-buffer
+    MPI_Sendrecv around the ring (receiver pulls the sender's buffer over
+    xGMI), and one-sided MPI_Put / MPI_Accumulate(SUM fp32) into the next
+    rank's window per fence epoch, MPI_Fetch_and_op on one shared counter.
+    Rates are bytes per rank over the max-over-ranks time; an accumulate
+    moves 2 bytes over xGMI per window byte (target read + write)."""
+    from ompi_amd import osc, pml
+    res = {}
+    nxt, prv = (rank + 1) % world, (rank - 1) % world
+    rows = []
+    for nbytes in (8, 64 << 10, 16 << 20, 256 << 20):
+        s = torch.ones(max(nbytes, 16), dtype=torch.uint8, device="cuda")
+        r = torch.empty_like(s)
+        steps = 20 if nbytes <= (16 << 20) else 5
+        t = _timed(lambda: pml.sendrecv(comm, s, nxt, 1, r, prv, 1, sbytes=nbytes,
+                                        rbytes=nbytes), steps, 3, dist, torch, tdev) / steps
+        rows.append({"bytes": nbytes, "us": round(t * 1e6, 2),
+                     "gbs_per_rank": round(nbytes / t / 1e9, 3)})
+        del s, r
+    res["sendrecv_ring"] = rows
+    S = 64 << 20
+    win = osc.Window.allocate(comm, S, disp_unit=4)
+    try:
+        x = torch.ones(S // 4, device="cuda")
+        steps = 10
+
+        def put_epoch():
+            win.put(x, nxt, 0, S)
+            win.fence()
+        t = _timed(put_epoch, steps, 2, dist, torch, tdev) / steps
+        res["put_64MiB_fence"] = {"bytes": S, "us": round(t * 1e6, 2),
+                                  "gbs_per_rank": round(S / t / 1e9, 3)}
+
+        def acc_epoch():
+            win.accumulate(x, S // 4, mop.MPI_FLOAT, nxt, 0, mop.MPI_SUM)
+            win.fence()
+        t = _timed(acc_epoch, steps, 2, dist, torch, tdev) / steps
+        res["accumulate_sum_f32_64MiB_fence"] = {
+            "bytes": S, "us": round(t * 1e6, 2), "gbs_per_rank": round(S / t / 1e9, 3),
+            "xgmi_gbs_per_rank": round(2 * S / t / 1e9, 3)}
+        one = torch.ones(1, dtype=torch.int64, device="cuda")
+        out = torch.empty(1, dtype=torch.int64, device="cuda")
+        k = 50
+
+        def fops():
+            for _ in range(k):
+                win.fetch_and_op(one, out, mop.MPI_INT64_T, 0, 0, mop.MPI_SUM)
+            win.fence()
+        t = _timed(fops, 3, 1, dist, torch, tdev) / 3
+        res["fetch_and_op_shared_counter"] = {"ops_per_rank": k, "us_per_op": round(t * 1e6 / k, 2),
+                                              "contenders": world}
+    finally:
+        win.free()
     return res

@@ -43,6 +43,9 @@ int comm_sticky(ompi_amd_comm_t *c);
 // Byte copy kernel (16-/4-/1-byte granules by the common phase of src and
 // dst; src or dst may be peer memory), system-scope acquire/release.
 int comm_copy(ompi_amd_comm_t *c, const void *src, void *dst, size_t bytes, hipStream_t s);
+// osc_ipc.hip: the byte copy of put / get and the p2p receive (persistent
+// grid, one acquire per workgroup; src or dst may be peer memory).
+int xfer_copy(const void *src, void *dst, size_t bytes, hipStream_t s);
 // Point-to-point mailboxes of the communicator (created with it).
 p2p_state *comm_p2p(ompi_amd_comm_t *c);
 

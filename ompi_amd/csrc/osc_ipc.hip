@@ -18,8 +18,11 @@
 //                   2-buffer element rule (op_device.h), 16-B granules when
 //                   both sides are 16-B aligned; target is peer memory, so
 //                   its loads and stores cross xGMI once each;
-//   copies          put / get / the fetch of get_accumulate: coll_ipc.hip's
-//                   copy kernel.
+//   xfer_kernel     put / get / the fetch of get_accumulate (and the p2p
+//                   receive): byte copy, 16-B granules.
+// Grids are persistent (kOscMaxBlocks): a system-scope acquire invalidates
+// the XCD's L2, so paying it once per workgroup in a 65k-workgroup grid
+// cost 7x (tools/osc_probe.py: accumulate 0.89 TB/s uncapped, 6.26 at 256).
 // Every transfer workgroup opens with a system-scope acquire and closes
 // with a drained system-scope release, as the collectives do
 // (coll_ipc.hip header): the lock hand-off then orders one origin's
@@ -28,6 +31,7 @@
 
 #include <algorithm>
 #include <array>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <utility>
@@ -129,33 +133,107 @@ __global__ __launch_bounds__(64) void lock_kernel(uint32_t *ctl, int kind, int *
 
 // target[i] = f(target[i], origin[i]) — the 2-buffer rule with out = target,
 // in = origin (ompi_osc_base_sndrcv_op -> ompi_op_reduce(op, origin, target)).
+// Aligned operands: 4 16-B vectors of each in flight per lane, one chunk
+// per workgroup (the op kernel's tuned shape, op_kernels.hip); the target's
+// loads and stores cross xGMI.  Unaligned: one element per lane.
+constexpr int kOscUnroll = 4;
+// Grid cap: a persistent grid-stride grid, so the per-workgroup L2
+// invalidation of the acquire is paid a bounded number of times
+// (tools/osc_probe.py; env OMPI_AMD_OSC_MAX_BLOCKS overrides).
+constexpr int kOscMaxBlocks = 256;  // one per CU: 6.26 TB/s vs 3.40 at 2048 (256 MiB fp32 SUM)
+
 template <typename T, int OP>
 __global__ __launch_bounds__(kOscThreads) void acc_kernel(const T *__restrict__ origin, T *target,
                                                           int64_t n, int vec) {
-    osc_acquire();
-    const int64_t gs = (int64_t)gridDim.x * kOscThreads;
-    const int64_t tid = (int64_t)blockIdx.x * kOscThreads + threadIdx.x;
+    // one system-scope acquire per workgroup (it invalidates this CU's L1
+    // and the XCD's L2 for every wave of the CU): lane 0, then the barrier
+    if (threadIdx.x == 0) osc_acquire();
+    __syncthreads();
+    using F = opfn<OP, false>;
     int64_t done = 0;
     if constexpr (16 % sizeof(T) == 0) {
         constexpr int E = 16 / sizeof(T);
+        constexpr int64_t chunk = (int64_t)kOscThreads * kOscUnroll;
         if (vec) {
             const int64_t nv = n / E;
             const u32x4 *o = reinterpret_cast<const u32x4 *>(origin);
             u32x4 *t = reinterpret_cast<u32x4 *>(target);
-            for (int64_t i = tid; i < nv; i += gs) {
-                vec16<T> a, b;
-                a.v = t[i];
-                b.v = __builtin_nontemporal_load(o + i);
+            for (int64_t base = (int64_t)blockIdx.x * chunk + threadIdx.x; base < nv;
+                 base += (int64_t)gridDim.x * chunk) {
+                vec16<T> a[kOscUnroll], b[kOscUnroll];
 #pragma unroll
-                for (int e = 0; e < E; ++e) a.e[e] = opfn<OP, false>::f(a.e[e], b.e[e]);
-                t[i] = a.v;
+                for (int u = 0; u < kOscUnroll; ++u) {
+                    const int64_t i = base + (int64_t)u * kOscThreads;
+                    if (i < nv) {
+                        a[u].v = t[i];
+                        b[u].v = __builtin_nontemporal_load(o + i);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kOscUnroll; ++u) {
+                    const int64_t i = base + (int64_t)u * kOscThreads;
+                    if (i < nv) {
+#pragma unroll
+                        for (int e = 0; e < E; ++e) a[u].e[e] = F::f(a[u].e[e], b[u].e[e]);
+                        t[i] = a[u].v;
+                    }
+                }
             }
             done = nv * E;
         }
     }
-    for (int64_t i = done + tid; i < n; i += gs) {
-        const T r = opfn<OP, false>::f(target[i], origin[i]);
+    const int64_t gs = (int64_t)gridDim.x * kOscThreads;
+    for (int64_t i = done + (int64_t)blockIdx.x * kOscThreads + threadIdx.x; i < n; i += gs) {
+        const T r = F::f(target[i], origin[i]);
         store_elem(target + i, r);
+    }
+    osc_epilogue();
+}
+
+// Byte copy for put / get / fetches and the p2p receive: 16-B granules
+// (4 in flight per lane) when src and dst share their phase mod 16, else 4-B
+// or 1-B granules; one acquire per workgroup, persistent grid (as acc_kernel).
+__global__ __launch_bounds__(kOscThreads) void xfer_kernel(const char *src, char *dst,
+                                                           int64_t bytes) {
+    if (threadIdx.x == 0) osc_acquire();
+    __syncthreads();
+    const uintptr_t phase = (uintptr_t)src ^ (uintptr_t)dst;
+    const int g = (phase & 15) == 0 ? 16 : ((phase & 3) == 0 ? 4 : 1);
+    int64_t head = (int64_t)((g - ((uintptr_t)src & (uintptr_t)(g - 1))) & (uintptr_t)(g - 1));
+    if (head > bytes) head = bytes;
+    const int64_t nbody = (bytes - head) / g;
+    const int64_t tid = (int64_t)blockIdx.x * kOscThreads + threadIdx.x;
+    if (g == 16) {
+        const u32x4 *sv = reinterpret_cast<const u32x4 *>(src + head);
+        u32x4 *dv = reinterpret_cast<u32x4 *>(dst + head);
+        constexpr int64_t chunk = (int64_t)kOscThreads * kOscUnroll;
+        for (int64_t base = (int64_t)blockIdx.x * chunk + threadIdx.x; base < nbody;
+             base += (int64_t)gridDim.x * chunk) {
+            u32x4 v[kOscUnroll];
+#pragma unroll
+            for (int u = 0; u < kOscUnroll; ++u) {
+                const int64_t i = base + (int64_t)u * kOscThreads;
+                if (i < nbody) v[u] = __builtin_nontemporal_load(sv + i);
+            }
+#pragma unroll
+            for (int u = 0; u < kOscUnroll; ++u) {
+                const int64_t i = base + (int64_t)u * kOscThreads;
+                if (i < nbody) __builtin_nontemporal_store(v[u], dv + i);
+            }
+        }
+    } else if (g == 4) {
+        const uint32_t *sw = reinterpret_cast<const uint32_t *>(src + head);
+        uint32_t *dw = reinterpret_cast<uint32_t *>(dst + head);
+        for (int64_t i = tid; i < nbody; i += (int64_t)gridDim.x * kOscThreads) dw[i] = sw[i];
+    } else {
+        for (int64_t i = tid; i < nbody; i += (int64_t)gridDim.x * kOscThreads)
+            dst[head + i] = src[head + i];
+    }
+    const int64_t tail0 = head + nbody * g;
+    const int64_t nrest = head + (bytes - tail0);
+    for (int64_t k = tid; k < nrest; k += (int64_t)gridDim.x * kOscThreads) {
+        const int64_t i = k < head ? k : tail0 + (k - head);
+        dst[i] = src[i];
     }
     osc_epilogue();
 }
@@ -259,6 +337,26 @@ static int target_ptr(ompi_amd_win_t *w, int target, size_t disp, size_t bytes, 
     return OMPI_AMD_SUCCESS;
 }
 
+
+static int64_t osc_grid_cap() {
+    static const int64_t cap = [] {
+        const char *e = getenv("OMPI_AMD_OSC_MAX_BLOCKS");
+        return (e && atoll(e) > 0) ? atoll(e) : (int64_t)kOscMaxBlocks;
+    }();
+    return cap;
+}
+
+int xfer_copy(const void *src, void *dst, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return OMPI_AMD_SUCCESS;
+    const int64_t units = (int64_t)(bytes / 16) + 1;
+    const int64_t per = (int64_t)kOscThreads * kOscUnroll;
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((units + per - 1) / per,
+                                                                  osc_grid_cap()));
+    hipLaunchKernelGGL(xfer_kernel, dim3((unsigned)blocks), dim3(kOscThreads), 0, s,
+                       static_cast<const char *>(src), static_cast<char *>(dst), (int64_t)bytes);
+    return record_hip(hipGetLastError(), "xfer copy launch");
+}
+
 static int launch_acc(ompi_amd_win_t *w, int op, int type, const void *origin, void *target,
                       size_t count, hipStream_t s) {
     acc_launch_fn f = (op >= 0 && op < OMPI_AMD_OP_COUNT && type >= 0 && type < OMPI_AMD_TYPE_COUNT)
@@ -270,8 +368,10 @@ static int launch_acc(ompi_amd_win_t *w, int op, int type, const void *origin, v
     }
     const size_t ext = ompi_amd_type_extent(type);
     const int vec = (16 % ext == 0 && ((uintptr_t)origin & 15) == 0 && ((uintptr_t)target & 15) == 0);
-    const int64_t units = vec ? (int64_t)(count * ext / 16) + 1 : (int64_t)count;
-    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((units + kOscThreads - 1) / kOscThreads, 2048));
+    const int64_t per = vec ? (int64_t)kOscThreads * kOscUnroll : (int64_t)kOscThreads;
+    const int64_t units = vec ? (int64_t)(count * ext / 16) : (int64_t)count;
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((units + per - 1) / per,
+                                                                  osc_grid_cap()));
     return record_hip(f(dim3((unsigned)blocks), origin, target, (int64_t)count, vec, s),
                       "osc accumulate launch");
 }
@@ -302,9 +402,9 @@ static int rma_op(ompi_amd_win_t *w, const void *origin, void *result, size_t co
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
     OSC_TRY(launch_lock(w, target, 0, s));
     int rc = OMPI_AMD_SUCCESS;
-    if (result) rc = comm_copy(w->c, t, result, bytes, s);
+    if (result) rc = xfer_copy(t, result, bytes, s);
     if (rc == OMPI_AMD_SUCCESS) {
-        if (op == OMPI_AMD_OP_REPLACE) rc = comm_copy(w->c, origin, t, bytes, s);
+        if (op == OMPI_AMD_OP_REPLACE) rc = xfer_copy(origin, t, bytes, s);
         else if (op != OMPI_AMD_OP_NO_OP) rc = launch_acc(w, op, type, origin, t, count, s);
     }
     const int urc = launch_lock(w, target, 1, s);  // always release
@@ -518,7 +618,7 @@ int ompi_amd_put(ompi_amd_win_t *w, const void *origin, size_t bytes, int target
     OSC_TRY(target_ptr(w, target, disp, bytes, &t));
     if (!bytes) return OMPI_AMD_SUCCESS;
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
-    return comm_copy(w->c, origin, t, bytes, as_stream(stream));
+    return xfer_copy(origin, t, bytes, as_stream(stream));
 }
 
 int ompi_amd_get(ompi_amd_win_t *w, void *origin, size_t bytes, int target, size_t disp,
@@ -528,7 +628,7 @@ int ompi_amd_get(ompi_amd_win_t *w, void *origin, size_t bytes, int target, size
     OSC_TRY(target_ptr(w, target, disp, bytes, &t));
     if (!bytes) return OMPI_AMD_SUCCESS;
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
-    return comm_copy(w->c, t, origin, bytes, as_stream(stream));
+    return xfer_copy(t, origin, bytes, as_stream(stream));
 }
 
 int ompi_amd_accumulate(ompi_amd_win_t *w, const void *origin, size_t count, int type, int target,

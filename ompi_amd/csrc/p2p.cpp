@@ -16,8 +16,8 @@
 //   match    on the receiver's host, in MPI order: per source, messages in
 //            sequence order; posted receives in posting order (each takes
 //            the earliest matching message), wildcards allowed.
-//   data     the receiver launches one copy kernel (coll_ipc.hip's
-//            copy_kernel: 16-B granules, system-scope acquire/release) that
+//   data     the receiver launches one copy kernel (osc_ipc.hip's
+//            xfer_kernel: 16-B granules, system-scope acquire/release) that
 //            loads the sender's buffer through its IPC mapping over xGMI
 //            straight into the receive buffer: one HBM read on the sender's
 //            GPU, one HBM write on the receiver's, no staging.
@@ -229,7 +229,7 @@ static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s
     } else {
         rc = comm_import(p->c, s, m->d, &src, true, &r->pinned);
     }
-    if (rc == OMPI_AMD_SUCCESS) rc = comm_copy(p->c, src, r->buf, n, r->stream);
+    if (rc == OMPI_AMD_SUCCESS) rc = xfer_copy(src, r->buf, n, r->stream);
     if (rc == OMPI_AMD_SUCCESS) {
         if (!r->ev) rc = record_hip(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming),
                                     "hipEventCreate (p2p)");
