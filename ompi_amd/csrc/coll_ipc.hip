@@ -107,6 +107,16 @@ __device__ __forceinline__ void sys_release() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// The workgroup's acquire: lane 0 issues it (it invalidates the CU's L1 and
+// the XCD's L2 for every wave of the CU), the barrier holds the other waves
+// until it completed.  One per workgroup instead of one per wave: in a
+// 1024-workgroup grid the 4 per workgroup cost measurable bandwidth
+// (osc_ipc.hip's grid note).
+__device__ __forceinline__ void acquire_once() {
+    if (threadIdx.x == 0) sys_acquire();
+    __syncthreads();
+}
+
 // Every storing wave drains its stores before the workgroup's single
 // system-scope release (MI355X_MICROARCH.md, inter-workgroup visibility).
 __device__ __forceinline__ void xfer_epilogue() {
@@ -282,7 +292,7 @@ template <typename T, int OP>
 __global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, ptr_set dst, int ndst,
                                                               int n, int order, int flags,
                                                               red_jobs jobs) {
-    sys_acquire();
+    acquire_once();
     const red_job jb = jobs.j[blockIdx.y];
     constexpr int E = 16 / sizeof(T);
     const int64_t gstride = (int64_t)gridDim.x * kXferThreads;
@@ -392,7 +402,7 @@ __global__ __launch_bounds__(kXferThreads) void fused_allreduce_kernel(fused_arg
         }
     }
     __syncthreads();
-    sys_acquire();
+    acquire_once();
     T *dst = reinterpret_cast<T *>(a.dst);
     for (int64_t e = lo + t; e < hi; e += kXferThreads) {
         T v[kMaxRanks];
@@ -405,7 +415,7 @@ __global__ __launch_bounds__(kXferThreads) void fused_allreduce_kernel(fused_arg
 // Byte copy with a peeled head so that the body runs 16 B (or 4 B) per
 // lane whenever src and dst share their alignment phase.
 __global__ __launch_bounds__(kXferThreads) void copy_kernel(cp_jobs jobs) {
-    sys_acquire();
+    acquire_once();
     const cp_job jb = jobs.j[blockIdx.y];
     const int64_t gstride = (int64_t)gridDim.x * kXferThreads;
     const int64_t tid = (int64_t)blockIdx.x * kXferThreads + threadIdx.x;
