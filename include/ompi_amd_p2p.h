@@ -18,11 +18,13 @@
  * are matched in the order they were sent, receives in the order they were
  * posted, MPI_ANY_SOURCE / MPI_ANY_TAG as wildcards.
  *
- * Completion semantics.  A send publishes its buffer after synchronising
- * `stream` (its data must be final) and completes when the receiver's copy
- * has finished — every mode behaves like MPI_Ssend (a valid completion of
- * standard and ready mode; MPI_Bsend is not provided).  A receive completes
- * when the copy into its buffer has finished on the device.  The byte
+ * Completion semantics.  A send synchronises `stream` first (its data must
+ * be final).  Messages of at most 4 KiB (btl/smcuda's eager limit) are
+ * copied into the sender's device eager area and the send completes at
+ * once (ob1's eager protocol); larger ones, and every MPI_Ssend, publish
+ * the user's buffer and complete when the receiver's copy has finished
+ * (rendezvous).  MPI_Bsend is not provided.  A receive completes when the
+ * copy into its buffer has finished on the device.  The byte
  * count is the message size; the MCA glue packs non-contiguous datatypes
  * with the convertor (include/ompi_amd_ddt.h) first.
  */

@@ -23,6 +23,13 @@
 //            GPU, one HBM write on the receiver's, no staging.
 //   FIN      the receiver marks the slot DONE once the copy's event has
 //            completed; the send completes when it sees DONE.
+//   eager    messages of at most kEager bytes (btl/smcuda's 4 KiB eager
+//            limit, btl_smcuda_component.c:197) are first copied into the
+//            sender's device eager area (one kEager cell per ring slot, the
+//            area exported once) and the send completes at once, as ob1's
+//            eager protocol does: MPI_Send of a small message never waits
+//            for the receiver.  The cell is reused only after the slot is
+//            DONE.
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
@@ -48,6 +55,7 @@
 namespace ompi_amd {
 
 constexpr int kSlots = 64;
+constexpr size_t kEager = 4096;
 
 enum : uint32_t { S_FREE = 0, S_POSTED = 1, S_MATCHED = 2, S_DONE = 3 };
 
@@ -79,6 +87,7 @@ struct p2p_state {
     std::vector<uint64_t> scan_from;  // per source: first sequence possibly still POSTED
     std::deque<ompi_amd_p2p_request *> recvs;  // posted receives not matched yet
     std::recursive_mutex mu;
+    char *eager = nullptr;  // [size][kSlots] cells of kEager bytes, allocated at first use
 
     pair_q &pair(int src, int dst) { return q[(size_t)src * (size_t)size + (size_t)dst]; }
 };
@@ -165,6 +174,7 @@ void p2p_unlink(p2p_state *p) {
 void p2p_destroy(p2p_state *p) {
     if (!p) return;
     if (p->q) munmap(p->q, p->bytes);
+    if (p->eager) (void)hipFree(p->eager);
     if (p->rank == 0) p2p_unlink(p);
     delete p;
 }
@@ -333,11 +343,18 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     if (mode < OMPI_AMD_SEND_SYNCHRONOUS || mode > OMPI_AMD_SEND_STANDARD)
         return OMPI_AMD_ERR_BAD_PARAM;
     int rc = record_hip(hipSetDevice(comm_device(c)), "hipSetDevice");
-    // the buffer is read by the receiver at any time from now: its producers must be done
+    const bool eager = bytes <= kEager && mode != OMPI_AMD_SEND_SYNCHRONOUS;  // Ssend: rendezvous
+    std::unique_lock<std::recursive_mutex> alloc_guard(p->mu);
+    if (rc == OMPI_AMD_SUCCESS && eager && !p->eager) {
+        rc = record_hip(hipMalloc((void **)&p->eager, (size_t)p->size * kSlots * kEager),
+                        "hipMalloc (p2p eager area)");
+        if (rc != OMPI_AMD_SUCCESS) p->eager = nullptr;
+    }
+    alloc_guard.unlock();
+    // the buffer is read from now on (by the eager copy or the receiver):
+    // its producers must be done
     if (rc == OMPI_AMD_SUCCESS)
         rc = record_hip(hipStreamSynchronize(as_stream(stream)), "hipStreamSynchronize (send)");
-    ipc_desc d{};
-    if (rc == OMPI_AMD_SUCCESS && bytes && dst != p->rank) rc = comm_export(c, buf, &d);
     if (rc != OMPI_AMD_SUCCESS) return rc;
     auto *r = new (std::nothrow) ompi_amd_p2p_request;
     if (!r) return OMPI_AMD_ERR_BAD_PARAM;
@@ -362,14 +379,29 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
             return OMPI_AMD_ERR_TIMEOUT;
         }
     }
+    const void *src = buf;
+    if (eager && bytes) {  // stage into this slot's cell; the send completes now
+        char *cell = p->eager + ((size_t)dst * kSlots + seq % kSlots) * kEager;
+        rc = xfer_copy(buf, cell, bytes, as_stream(stream));
+        if (rc == OMPI_AMD_SUCCESS)
+            rc = record_hip(hipStreamSynchronize(as_stream(stream)), "hipStreamSynchronize (eager)");
+        src = cell;
+    }
+    ipc_desc d{};
+    if (rc == OMPI_AMD_SUCCESS && bytes && dst != p->rank) rc = comm_export(c, src, &d);
+    if (rc != OMPI_AMD_SUCCESS) {
+        delete r;
+        return rc;
+    }
     m.tag = tag;
     m.seq = seq;
     m.bytes = bytes;
-    m.raw = reinterpret_cast<uint64_t>(buf);
+    m.raw = reinterpret_cast<uint64_t>(src);
     m.d = d;
     m.state.store(S_POSTED, std::memory_order_release);
     q.posted.store(seq + 1, std::memory_order_release);
     r->seq = seq;
+    r->done = eager;  // the user's buffer is free again
     *out = r;
     return OMPI_AMD_SUCCESS;
 }

@@ -192,6 +192,52 @@ def case_self(comm, rank, n, salt):
     return eq(host(r), payload(rank, salt, 123457), "self")
 
 
+def case_eager_send_first(comm, rank, n, salt, k=50):
+    """Every rank first MPI_Sends k small messages (<= 4 KiB, eager) to the
+    next rank, overwriting its buffer after each send returns, and only then
+    receives: completes only because small sends do not wait for the
+    receiver; the data is what the buffer held at the send."""
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    buf = zeros(4096)
+    for i in range(k):
+        nb = 1 + (i * 97) % 4096
+        src = dev(payload(rank, salt + i, nb))
+        with torch.cuda.stream(STREAM):
+            buf[:nb].copy_(src)
+        pml.send(comm, buf, nxt, 20 + i % 3, nbytes=nb, stream=STREAM)
+        with torch.cuda.stream(STREAM):
+            buf.zero_()  # the send already returned: its data was staged
+    fails = []
+    for i in range(k):
+        nb = 1 + (i * 97) % 4096
+        r = zeros(4096)
+        st = pml.recv(comm, r, prv, 20 + i % 3, stream=STREAM)
+        if st.bytes != nb:
+            fails.append(f"msg {i}: {st.bytes} bytes, expected {nb}")
+            continue
+        ok, msg = eq(host(r)[:nb], payload(prv, salt + i, nb), f"msg {i}")
+        if not ok:
+            fails.append(msg)
+    return not fails, "; ".join(fails[:3])
+
+
+def case_ssend_small(comm, rank, n, salt):
+    """MPI_Ssend of a small message takes the rendezvous: the isend is not
+    complete before the receive is posted; data arrives intact."""
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    a = dev(payload(rank, salt, 100))
+    rq = pml.isend(comm, a, nxt, 31, mode=pml.SEND_SYNCHRONOUS, stream=STREAM)
+    early = rq.test()
+    comm_barrier()  # nobody has posted its receive yet
+    r = zeros(100)
+    pml.recv(comm, r, prv, 31, stream=STREAM)
+    rq.wait()
+    rq.free()
+    if early:
+        return False, "synchronous send completed before the receive was posted"
+    return eq(host(r), payload(prv, salt, 100), "ssend")
+
+
 # ----------------------------------------------------------------- osc cases
 def fp_inputs(dt, count, rank, salt, kind="R"):
     rng = np.random.default_rng(SEED + 1000 * salt + rank)
@@ -463,6 +509,8 @@ def main():
         ("p2p_any_source_any_tag", lambda: case_any_source(comm, rank, n, 70)),
         ("p2p_probe_truncate", lambda: case_probe_truncate(comm, rank, n, 71)),
         ("p2p_self", lambda: case_self(comm, rank, n, 72)),
+        ("p2p_eager_send_before_recv", lambda: case_eager_send_first(comm, rank, n, 73)),
+        ("p2p_ssend_small_rendezvous", lambda: case_ssend_small(comm, rank, n, 74)),
         ("osc_put_get_small", lambda: case_put_get(comm, rank, n, 1001, 80)),
         ("osc_put_get_32MiB", lambda: case_put_get(comm, rank, n, 32 << 20, 81)),
         ("osc_acc_sum_f32", lambda: case_acc_disjoint(comm, rank, n, F, mop.MPI_SUM, 1000003, 82)),
