@@ -173,9 +173,11 @@ __global__ __launch_bounds__(kOscThreads) void acc_kernel(const T *__restrict__ 
                 for (int u = 0; u < kOscUnroll; ++u) {
                     const int64_t i = base + (int64_t)u * kOscThreads;
                     if (i < nv) {
+                        vec16<T> r;
+                        r.v = a[u].v;
 #pragma unroll
-                        for (int e = 0; e < E; ++e) a[u].e[e] = F::f(a[u].e[e], b[u].e[e]);
-                        t[i] = a[u].v;
+                        for (int e = 0; e < E; ++e) r.e[e] = F::f(a[u].e[e], b[u].e[e]);
+                        t[i] = r.v;
                     }
                 }
             }
