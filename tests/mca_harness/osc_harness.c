@@ -1,0 +1,200 @@
+/*
+ * TEST HARNESS ONLY: drives ompi_amd/mca/osc/rocm through the osc
+ * framework's selection protocol (ompi_osc_base_select: osc_init,
+ * osc_query per flavor, osc_select) and the module table, one process per
+ * rank (argv: name rank size).  HARNESS_GPU=0: selection checks only (no
+ * device).  HARNESS_GPU=1: windows over device memory; every accumulate is
+ * checked against the oracle's op/base restatement.  Prints "ok" / "ok gpu".
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mpi.h"
+#include "ompi/communicator/communicator.h"
+#include "ompi/constants.h"
+#include "ompi/datatype/ompi_datatype.h"
+#include "ompi/op/op.h"
+#include "ompi/runtime/ompi_rte.h"
+#include "ompi/win/win.h"
+#include "opal/util/info.h"
+#include "../../oracle/oracle.h"
+#include "osc_rocm.h"
+#include "ompi_amd.h"
+
+extern int harness_dev_alloc_copy(void **d, const void *h, size_t bytes);
+extern int harness_dev_copy_in(void *d, const void *h, size_t bytes);
+extern int harness_dev_copy_back(void *h, const void *d, size_t bytes);
+extern int harness_dev_free(void *d);
+
+harness_proc_name_t harness_proc_name = {4242, 0};
+int ompi_op_ddt_map[64];
+
+#define CHECK(c, ...)                                                   \
+    do {                                                                \
+        if (!(c)) {                                                     \
+            fprintf(stderr, "rank %d: FAILED %s: ", g_rank, #c);         \
+            fprintf(stderr, __VA_ARGS__);                               \
+            fprintf(stderr, " (%s)\n", ompi_amd_last_error());          \
+            exit(1);                                                    \
+        }                                                               \
+    } while (0)
+
+static int g_rank, g_size;
+
+/* exact data: k * 2^-8, k in [-1024, 1024] from a per-(rank, salt) LCG */
+static void fill_exact(float *a, size_t n, int rank, int salt)
+{
+    uint64_t x = 0x9E3779B97F4A7C15ull ^ ((uint64_t)(rank + 1) << 20) ^ (uint64_t)salt;
+    for (size_t i = 0; i < n; ++i) {
+        x = x * 6364136223846793005ull + 1442695040888963407ull;
+        a[i] = (float)((int64_t)((x >> 33) % 2049) - 1024) * (1.0f / 256.0f);
+    }
+}
+
+int main(int argc, char **argv)
+{
+    const int use_gpu = getenv("HARNESS_GPU") && atoi(getenv("HARNESS_GPU"));
+    ompi_group_t local = {0}, remote = {1};
+    ompi_communicator_t comm;
+    ompi_datatype_t dfloat = {ORC_T_FLOAT, 4, 1, 1}, dint64 = {ORC_T_INT64, 8, 1, 1};
+    ompi_op_t sum = {OMPI_OP_FLAGS_INTRINSIC, ORC_OP_SUM}, user = {0, ORC_OP_SUM};
+    opal_info_t dev_info = {"ompi_amd_device", "true"};
+    ompi_osc_base_component_t *c = &mca_osc_rocm_component.super;
+    int i;
+
+    if (argc < 4) return 2;
+    harness_proc_name.jobid = (unsigned) strtoul(argv[1], NULL, 16);
+    g_rank = atoi(argv[2]);
+    g_size = atoi(argv[3]);
+    for (i = 0; i < 64; ++i) ompi_op_ddt_map[i] = i;
+    comm = (ompi_communicator_t){g_rank, g_size, 5, 0, &local, NULL};
+    if (c->osc_version.mca_register_component_params)
+        c->osc_version.mca_register_component_params();
+
+    /* selection (ompi_osc_base_select): init, then query per flavor */
+    CHECK((c->osc_init(false, false) == OMPI_SUCCESS) == (ompi_amd_device_count() > 0),
+          "osc_init vs device presence");
+    {
+        ompi_win_t w = {0};
+        float host[4];
+        void *hb = host;
+        ompi_communicator_t ci = comm, cr = comm;
+        ci.inter = 1;
+        cr.c_local_group = &remote;
+        CHECK(c->osc_query(&w, &hb, sizeof(host), 4, &comm, NULL, MPI_WIN_FLAVOR_CREATE) < 0,
+              "host memory is not a device window");
+        CHECK(c->osc_query(&w, &hb, 0, 4, &comm, NULL, MPI_WIN_FLAVOR_ALLOCATE) < 0,
+              "allocate without the device info key");
+        CHECK(c->osc_query(&w, &hb, 0, 4, &ci, &dev_info, MPI_WIN_FLAVOR_ALLOCATE) < 0, "inter");
+        CHECK(c->osc_query(&w, &hb, 0, 4, &cr, &dev_info, MPI_WIN_FLAVOR_ALLOCATE) < 0,
+              "remote peers");
+        CHECK(c->osc_query(&w, &hb, 0, 4, &comm, &dev_info, MPI_WIN_FLAVOR_DYNAMIC) < 0,
+              "dynamic windows");
+    }
+    if (!use_gpu) {
+        printf("ok\n");
+        return 0;
+    }
+
+    const size_t n = 100003;
+    const int nxt = (g_rank + 1) % g_size, prv = (g_rank + g_size - 1) % g_size;
+    float *init = malloc(n * 4), *org = malloc(n * 4), *exp = malloc(n * 4), *got = malloc(n * 4);
+    float *init_nxt = malloc(n * 4), *org_rank = malloc(n * 4);
+    void *dbase = NULL, *dorg = NULL, *dgot = NULL, *abase = NULL;
+    ompi_win_t win = {0}, awin = {0};
+    int model = -1, prio;
+
+    fill_exact(init, n, g_rank, 1);
+    fill_exact(org, n, g_rank, 2);
+    CHECK(harness_dev_alloc_copy(&dbase, init, n * 4) == 0, "device window");
+    CHECK(harness_dev_alloc_copy(&dorg, org, n * 4) == 0, "device origin");
+    CHECK(harness_dev_alloc_copy(&dgot, init, n * 4) == 0, "device result");
+
+    prio = c->osc_query(&win, &dbase, n * 4, 4, &comm, NULL, MPI_WIN_FLAVOR_CREATE);
+    CHECK(prio == 101, "query on device memory: %d", prio);
+    CHECK(c->osc_query(&awin, &abase, 64, 8, &comm, &dev_info, MPI_WIN_FLAVOR_ALLOCATE) == 101,
+          "query allocate with the device info key");
+    CHECK(c->osc_select(&win, &dbase, n * 4, 4, &comm, NULL, MPI_WIN_FLAVOR_CREATE, &model) ==
+              OMPI_SUCCESS && win.w_osc_module && model == MPI_WIN_UNIFIED,
+          "select create");
+    ompi_osc_base_module_t *m = win.w_osc_module;
+
+    /* active target: accumulate SUM into the next rank, bit-exact vs op/base */
+    CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence 1");
+    CHECK(m->osc_accumulate(dorg, (int) n, &dfloat, nxt, 0, (int) n, &dfloat, &sum, &win) ==
+              OMPI_SUCCESS, "accumulate");
+    CHECK(m->osc_accumulate(dorg, 3, &dfloat, nxt, 0, 3, &dfloat, &user, &win) ==
+              OMPI_ERR_NOT_SUPPORTED, "user op refused");
+    CHECK(m->osc_accumulate(dorg, 3, &dfloat, nxt, 0, 3, &dint64, &sum, &win) ==
+              OMPI_ERR_NOT_SUPPORTED, "mismatched datatypes refused");
+    CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence 2");
+    CHECK(harness_dev_copy_back(got, dbase, n * 4) == 0, "copy back");
+    {
+        float *oprv = malloc(n * 4);
+        fill_exact(oprv, n, prv, 2);
+        memcpy(exp, init, n * 4);
+        orc_op_2buff(ORC_OP_SUM, ORC_T_FLOAT, oprv, exp, n);
+        CHECK(0 == memcmp(got, exp, n * 4), "accumulated window");
+        free(oprv);
+    }
+    /* get the next rank's window: its init + my origin */
+    CHECK(m->osc_get(dgot, (int) n, &dfloat, nxt, 0, (int) n, &dfloat, &win) == OMPI_SUCCESS, "get");
+    CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence 3");
+    CHECK(harness_dev_copy_back(got, dgot, n * 4) == 0, "copy back get");
+    fill_exact(init_nxt, n, nxt, 1);
+    memcpy(org_rank, org, n * 4);
+    orc_op_2buff(ORC_OP_SUM, ORC_T_FLOAT, org_rank, init_nxt, n);
+    CHECK(0 == memcmp(got, init_nxt, n * 4), "get of the next window");
+
+    /* passive target: each rank puts its rank id at displacement `rank` of
+     * rank 0's window under an exclusive lock */
+    {
+        float me = (float) g_rank;
+        CHECK(harness_dev_copy_in(dorg, &me, 4) == 0, "origin");
+        CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence 4");
+        CHECK(m->osc_lock(MPI_LOCK_EXCLUSIVE, 0, 0, &win) == OMPI_SUCCESS, "lock");
+        CHECK(m->osc_put(dorg, 1, &dfloat, 0, g_rank, 1, &dfloat, &win) == OMPI_SUCCESS, "put");
+        CHECK(m->osc_unlock(0, &win) == OMPI_SUCCESS, "unlock");
+        CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence 5");
+        if (0 == g_rank) {
+            CHECK(harness_dev_copy_back(got, dbase, 4 * (size_t) g_size) == 0, "copy back");
+            for (i = 0; i < g_size; ++i) CHECK(got[i] == (float) i, "slot %d holds %g", i, got[i]);
+        }
+    }
+    CHECK(m->osc_start(NULL, 0, &win) == OMPI_ERR_NOT_SUPPORTED, "PSCW not provided");
+
+    /* MPI_Win_allocate: a shared counter, fetch_and_op from every rank */
+    CHECK(c->osc_select(&awin, &abase, 0 == g_rank ? 64 : 0, 8, &comm, &dev_info,
+                        MPI_WIN_FLAVOR_ALLOCATE, &model) == OMPI_SUCCESS && awin.w_osc_module,
+          "select allocate");
+    {
+        ompi_osc_base_module_t *a = awin.w_osc_module;
+        int64_t one = 1, seen = -1, total = -1;
+        void *done = NULL, *dres = NULL;
+        const int k = 10;
+        CHECK(harness_dev_alloc_copy(&done, &one, 8) == 0 && harness_dev_alloc_copy(&dres, &one, 8) == 0,
+              "counter buffers");
+        CHECK(a->osc_fence(0, &awin) == OMPI_SUCCESS, "afence 1");
+        for (i = 0; i < k; ++i)
+            CHECK(a->osc_fetch_and_op(done, dres, &dint64, 0, 0, &sum, &awin) == OMPI_SUCCESS,
+                  "fetch_and_op");
+        CHECK(a->osc_fence(0, &awin) == OMPI_SUCCESS, "afence 2");
+        CHECK(harness_dev_copy_back(&seen, dres, 8) == 0, "last fetched");
+        CHECK(seen >= k - 1 && seen < (int64_t) k * g_size, "last fetched value %lld", (long long) seen);
+        if (0 == g_rank) {
+            CHECK(harness_dev_copy_back(&total, abase, 8) == 0, "counter");
+            CHECK(total == (int64_t) k * g_size, "counter %lld", (long long) total);
+        }
+        CHECK(a->osc_free(&awin) == OMPI_SUCCESS && NULL == awin.w_osc_module, "free allocate");
+        harness_dev_free(done);
+        harness_dev_free(dres);
+    }
+    CHECK(m->osc_free(&win) == OMPI_SUCCESS, "free create");
+    harness_dev_free(dbase);
+    harness_dev_free(dorg);
+    harness_dev_free(dgot);
+    printf("ok gpu\n");
+    return 0;
+}

@@ -1,0 +1,15 @@
+/* TEST HARNESS ONLY: the mpi.h constants the osc glue uses
+ * (ompi/include/mpi.h.in:542-557). */
+#ifndef HARNESS_MPI_H
+#define HARNESS_MPI_H
+#define MPI_IN_PLACE ((void *) 1)
+#define MPI_SUCCESS 0
+#define MPI_MODE_NOCHECK 1
+#define MPI_LOCK_EXCLUSIVE 1
+#define MPI_LOCK_SHARED 2
+#define MPI_WIN_FLAVOR_CREATE 1
+#define MPI_WIN_FLAVOR_ALLOCATE 2
+#define MPI_WIN_FLAVOR_DYNAMIC 3
+#define MPI_WIN_FLAVOR_SHARED 4
+#define MPI_WIN_UNIFIED 0
+#endif

@@ -83,3 +83,36 @@ def test_coll_component_device_path(coll_harness, n):
     functions on every rank; release destroys the device communicator."""
     for rc, out, err in _run_coll_harness(coll_harness, n, True, 240):
         assert rc == 0 and out == "ok gpu", (rc, out, err)
+
+
+# ---- osc/rocm (ompi_amd/mca/osc/rocm) through tests/mca_harness/osc_harness.c ----
+
+@pytest.fixture(scope="module")
+def osc_harness(tmp_path_factory):
+    from ompi_amd import _lib
+    from oracle import oracle as orc
+    _lib.load()
+    orc.lib()
+    out = str(tmp_path_factory.mktemp("mca") / "osc_harness")
+    subprocess.run(["bash", os.path.join(ROOT, "tests", "mca_harness", "build_osc.sh"), out],
+                   check=True)
+    return out
+
+
+def test_osc_component_selection(osc_harness):
+    """osc_init refuses without a device; osc_query refuses host memory,
+    allocate without the device info key, inter-communicators, remote peers
+    and dynamic windows (ompi_osc_base_select protocol)."""
+    for rc, out, err in _run_coll_harness(osc_harness, 1, False, 60):
+        assert rc == 0 and out == "ok", (rc, out, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 3])
+def test_osc_component_device_path(osc_harness, n):
+    """MPI_Win_create over device memory and MPI_Win_allocate through the
+    component: fence epochs with accumulate (bit-exact vs op/base) and get,
+    an exclusive-lock put epoch, a fetch_and_op counter, refusal of user ops,
+    mismatched datatypes and PSCW, free."""
+    for rc, out, err in _run_coll_harness(osc_harness, n, True, 180):
+        assert rc == 0 and out == "ok gpu", (rc, out, err)
