@@ -40,7 +40,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--no-extras", action="store_true",
-                   help="N>1: skip the exactness check, size sweep and configs[4] collectives")
+                   help="N>1: skip the exactness check, size sweep and configs[4] collectives; "
+                        "N=1: skip the one-sided / point-to-point rows")
     return p.parse_args()
 
 
@@ -151,6 +152,12 @@ def main():
         res = bench_op(args)
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline_op(args.cpu_seconds)
+        if not args.no_extras:
+            try:  # SURVEY §8f rows 1 / 4 on one GPU; never breaks the headline
+                from ompi_amd import coll_bench
+                res["next_rows_n1"] = coll_bench.single_gpu_rows()
+            except Exception as e:  # noqa: BLE001
+                res["next_rows_n1_error"] = f"{type(e).__name__}: {e}"
     print(json.dumps(res), flush=True)
 
 

@@ -387,3 +387,55 @@ def _p2p_osc_rows(comm, dist, torch, mop, world, rank, tdev):
     finally:
         win.free()
     return res
+
+
+def single_gpu_rows(mib: int = 256):
+    """N=1 leg of SURVEY §8f rows 1 and 4 (bench.py, beside the headline): a
+    communicator of size 1, so the target window and the p2p peer are this
+    GPU and every kernel is HBM-bound exactly like the op kernel.  Event-
+    timed on a dedicated stream; algorithmic HBM bytes per call: accumulate
+    3 x S (read target, read origin, write target), get_accumulate 5 x S
+    (+ fetch copy), put and the p2p receive copy 2 x S."""
+    import torch
+
+    from . import coll, osc, pml
+    from . import op as mop
+
+    S = mib << 20
+    s = torch.cuda.Stream()
+    comm = coll.Communicator(f"n1rows_{os.getpid()}", 0, 1, torch.cuda.current_device())
+    win = osc.Window.allocate(comm, S, disp_unit=4)
+    x = torch.ones(S // 4, device="cuda")
+    r = torch.empty_like(x)
+    torch.cuda.synchronize()
+
+    def timed(fn, iters=10):
+        for _ in range(2):
+            fn()
+        s.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        for _ in range(iters):
+            fn()
+        b.record(s)
+        b.synchronize()
+        return a.elapsed_time(b) / iters / 1e3
+
+    rows = {}
+    try:
+        for name, fn, factor in (
+            ("accumulate_sum_f32", lambda: win.accumulate(x, S // 4, mop.MPI_FLOAT, 0, 0,
+                                                          mop.MPI_SUM, stream=s), 3),
+            ("get_accumulate_sum_f32", lambda: win.get_accumulate(x, r, S // 4, mop.MPI_FLOAT, 0,
+                                                                  0, mop.MPI_SUM, stream=s), 5),
+            ("put", lambda: win.put(x, 0, 0, S, stream=s), 2),
+            ("sendrecv_self", lambda: pml.sendrecv(comm, x, 0, 1, r, 0, 1, stream=s), 2),
+        ):
+            t = timed(fn)
+            gbs = factor * S / t / 1e9
+            rows[name] = {"bytes": S, "ms": round(t * 1e3, 4), "hbm_gbs": round(gbs, 1),
+                          "frac_of_8TBs": round(gbs / 8000.0, 4)}
+    finally:
+        win.free()
+        comm.free()
+    return rows
