@@ -342,6 +342,15 @@ def _p2p_osc_rows(comm, dist, torch, mop, world, rank, tdev):
     from ompi_amd import osc, pml
     res = {}
     nxt, prv = (rank + 1) % world, (rank - 1) % world
+    # a peer lock that never comes must not stall the bench: short bound,
+    # and the rows stop at the first device error
+    comm.set_param("timeout_ms", 5000)
+
+    def check(what):  # collective: every rank stops together
+        e = torch.tensor([abs(comm.error())], dtype=torch.int64, device=tdev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        if int(e.item()):
+            raise RuntimeError(f"device error on some rank after {what}")
     rows = []
     for nbytes in (8, 64 << 10, 16 << 20, 256 << 20):
         s = torch.ones(max(nbytes, 16), dtype=torch.uint8, device="cuda")
@@ -353,6 +362,7 @@ def _p2p_osc_rows(comm, dist, torch, mop, world, rank, tdev):
                      "gbs_per_rank": round(nbytes / t / 1e9, 3)})
         del s, r
     res["sendrecv_ring"] = rows
+    check("sendrecv")
     S = 64 << 20
     win = osc.Window.allocate(comm, S, disp_unit=4)
     try:
@@ -363,6 +373,7 @@ def _p2p_osc_rows(comm, dist, torch, mop, world, rank, tdev):
             win.put(x, nxt, 0, S)
             win.fence()
         t = _timed(put_epoch, steps, 2, dist, torch, tdev) / steps
+        check("put")
         res["put_64MiB_fence"] = {"bytes": S, "us": round(t * 1e6, 2),
                                   "gbs_per_rank": round(S / t / 1e9, 3)}
 
@@ -370,6 +381,7 @@ def _p2p_osc_rows(comm, dist, torch, mop, world, rank, tdev):
             win.accumulate(x, S // 4, mop.MPI_FLOAT, nxt, 0, mop.MPI_SUM)
             win.fence()
         t = _timed(acc_epoch, steps, 2, dist, torch, tdev) / steps
+        check("accumulate")
         res["accumulate_sum_f32_64MiB_fence"] = {
             "bytes": S, "us": round(t * 1e6, 2), "gbs_per_rank": round(S / t / 1e9, 3),
             "xgmi_gbs_per_rank": round(2 * S / t / 1e9, 3)}
@@ -382,6 +394,7 @@ def _p2p_osc_rows(comm, dist, torch, mop, world, rank, tdev):
                 win.fetch_and_op(one, out, mop.MPI_INT64_T, 0, 0, mop.MPI_SUM)
             win.fence()
         t = _timed(fops, 3, 1, dist, torch, tdev) / 3
+        check("fetch_and_op")
         res["fetch_and_op_shared_counter"] = {"ops_per_rank": k, "us_per_op": round(t * 1e6 / k, 2),
                                               "contenders": world}
     finally:

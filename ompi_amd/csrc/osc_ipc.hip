@@ -82,6 +82,11 @@ __device__ __forceinline__ void wait_eq(uint32_t *p, uint32_t want, int *err, ui
 __global__ __launch_bounds__(64) void lock_kernel(uint32_t *ctl, int kind, int *err,
                                                   uint64_t ticks) {
     if (threadIdx.x != 0) return;
+    // fail fast: once a lock or barrier of this communicator timed out, the
+    // later acquisitions do not wait again (the error is already sticky)
+    if ((kind == 0 || kind == 2 || kind == 4) &&
+        __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
+        return;
     switch (kind) {
     case 0: {  // opal_atomic_lock: spin on a compare-and-swap 0 -> 1
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
