@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WORKER = os.path.join(ROOT, "tests", "p2p_osc_worker.py")
 
 
-@pytest.mark.parametrize("n", [2, 3, 4])
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
 def test_p2p_osc_parity(n):
     outs = run_ranks(n, timeout=300, worker=WORKER)
     failures = []
