@@ -65,3 +65,34 @@ def test_type_extents():
     assert lib.ompi_amd_type_extent(38) == 8    # SHORT_INT
     assert lib.ompi_amd_type_extent(15) == 4
     assert lib.ompi_amd_type_extent(14) == 0    # short float: not provided
+
+
+def test_argument_checks_before_any_device_call():
+    """Validation paths that return before touching HIP (CPU-safe): a bad op
+    or type index, an undefined (op, type) slot, NULL buffers with count > 0,
+    and count == 0 (MPI_Reduce_local with count 0 is a no-op even on NULL)."""
+    lib = _lib.load()
+    SUCCESS, UNSUPPORTED, BAD_PARAM = 0, -1, -2
+    assert lib.ompi_amd_op_reduce(99, 15, None, None, 0, None) == BAD_PARAM
+    assert lib.ompi_amd_op_reduce(3, 99, None, None, 0, None) == BAD_PARAM
+    assert lib.ompi_amd_op_reduce(3, 35, None, None, 0, None) == UNSUPPORTED   # SUM DOUBLE_INT
+    assert lib.ompi_amd_op_reduce_3buff(11, 15, None, None, None, 0, None) == UNSUPPORTED
+    assert lib.ompi_amd_op_reduce(3, 15, None, None, 0, None) == SUCCESS
+    assert lib.ompi_amd_op_reduce_3buff(3, 15, None, None, None, 0, None) == SUCCESS
+    assert lib.ompi_amd_op_reduce(3, 15, None, None, 4, None) == BAD_PARAM
+    assert lib.ompi_amd_op_reduce_3buff(3, 15, None, None, None, 4, None) == BAD_PARAM
+    assert lib.ompi_amd_op_supported(3, 15) == 1
+    assert lib.ompi_amd_op_supported(3, 35) == 0
+    assert lib.ompi_amd_op_supported(-1, 15) == 0
+
+
+@pytest.mark.parametrize("count", [0, -5])
+def test_handler_nonpositive_count_is_noop(count):
+    """op/base's loops run `for (i = 0; i < *count; ++i)` (op_base_functions.c:
+    40-51), so count <= 0 touches nothing; the device handler returns before
+    classifying the buffers."""
+    from ompi_amd import op as mop
+    fn = mop.handler(mop.MPI_SUM, mop.MPI_FLOAT)
+    c = ctypes.c_int(count)
+    fn(None, None, ctypes.byref(c), None, None)
+    mop.handler3(mop.MPI_SUM, mop.MPI_FLOAT)(None, None, None, ctypes.byref(c), None, None)
