@@ -363,6 +363,68 @@ __global__ __launch_bounds__(kDdtThreads) void ddt_pack_tile_kernel(ddt_period P
     }
 }
 
+// Staged unpack, the mirror of the tile pack: a workgroup brings the packed
+// bytes of `nper` periods into LDS with 16-B nt loads (coalesced on the
+// contiguous side), then lane t writes packed granules t, t + 256, … of the
+// tile to their typed addresses — adjacent lanes store adjacent granules, so
+// each store instruction covers a contiguous typed stretch.  Only the typed
+// bytes the datatype owns are written (gaps stay untouched).  Per granule
+// the position walks by constant increments (one division per lane per
+// tile) instead of the generic kernel's element search + two divisions.
+template <int G, bool IDENT>
+__global__ __launch_bounds__(kDdtThreads) void ddt_unpack_tile_kernel(ddt_period P,
+                                                                     const char *contig,
+                                                                     char *typed, int64_t start,
+                                                                     int64_t j0, int64_t j1) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    using T = typename granule<G>::t;
+    typedef unsigned int v4 __attribute__((ext_vector_type(4)));
+    const int t = threadIdx.x;
+    uint16_t *map = reinterpret_cast<uint16_t *>(lds);
+    char *data = lds + P.map_bytes;
+    if (!IDENT)
+        for (int64_t i = t; i < P.psize; i += kDdtThreads) map[i] = P.map[i];
+    constexpr int64_t step = (int64_t)G * kDdtThreads;  // packed bytes per lane pass
+    const int64_t st_j = step / P.psize, st_q = step % P.psize;
+    for (int64_t tile = blockIdx.x;; tile += gridDim.x) {
+        const int64_t jt = j0 + tile * P.nper;
+        if (jt >= j1) break;
+        const int64_t nj = min(P.nper, j1 - jt);
+        const int64_t len = nj * P.psize;                    // packed bytes of this tile
+        const char *c0 = contig + (jt * P.psize - start);    // its first packed byte
+        const uintptr_t A0 = (uintptr_t)c0 & ~(uintptr_t)15;
+        const int64_t nv = (int64_t)((((uintptr_t)(c0 + len) + 15) & ~(uintptr_t)15) - A0) / 16;
+        __syncthreads();  // map staged / previous tile's LDS reads done
+        for (int64_t v = t; v < nv; v += kDdtThreads)
+            reinterpret_cast<v4 *>(data)[v] =
+                __builtin_nontemporal_load(reinterpret_cast<const v4 *>(A0) + v);
+        __syncthreads();
+        const char *src = data + ((uintptr_t)c0 - A0);
+        char *t0 = typed + P.base + jt * P.pext;
+        int64_t r = (int64_t)t * G;
+        if (r >= len) continue;
+        int64_t j = r / P.psize, q = r - j * P.psize;
+        constexpr int U = 4;  // granules per lane per pass: U independent stores in flight
+        for (; r < len; r += U * step) {
+            int64_t off[U];
+            T v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                off[u] = j * P.pext + (IDENT ? q : (int64_t)map[q]);
+                q += st_q;
+                j += st_j;
+                if (q >= P.psize) { q -= P.psize; ++j; }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (r + u * step < len) v[u] = *reinterpret_cast<const T *>(src + r + u * step);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (r + u * step < len) *reinterpret_cast<T *>(t0 + off[u]) = v[u];
+        }
+    }
+}
+
 }  // namespace ompi_amd
 
 struct ompi_amd_ddt {
@@ -422,7 +484,7 @@ static hipError_t launch_vec(int G, const ddt_walk &v, const ddt_desc &d, const 
     return hipGetLastError();
 }
 
-// Staged tile pack when the layout is periodic, sub-16-B granular (or
+// Staged tile pack / unpack when the layout is periodic, sub-16-B granular (or
 // multi-element) and dense enough.  Returns false when the
 // generic / walker kernels should run instead.
 constexpr int64_t kTileMaxGap = 128;          // bytes of gap the tile reads through
@@ -446,9 +508,10 @@ static int64_t tile_data_bytes() {
     return v;
 }
 
-static bool tile_pack(const ompi_amd_ddt_t *ddt, size_t count, int G, const char *typed,
-                      char *contig, int64_t start, int64_t end, const ddt_desc &d,
-                      hipStream_t s, hipError_t *err) {
+template <bool UNPACK>
+static bool tile_run(const ompi_amd_ddt_t *ddt, size_t count, int G, char *typed, char *contig,
+                     int64_t start, int64_t end, const ddt_desc &d, hipStream_t s,
+                     hipError_t *err) {
     static const bool off = getenv("OMPI_AMD_DDT_TILE") && atoi(getenv("OMPI_AMD_DDT_TILE")) == 0;
     if (off || end - start < kTileMinWindow) return false;
     ddt_period P{};
@@ -474,6 +537,7 @@ static bool tile_pack(const ompi_amd_ddt_t *ddt, size_t count, int G, const char
         return false;
     }
     if (P.pext < 0 || P.psize % G != 0) return false;
+    if (UNPACK && P.psize > P.pext) return false;  // the tile's packed bytes must fit its LDS
     const int64_t j0 = (start + P.psize - 1) / P.psize, j1 = end / P.psize;
     if (j1 <= j0) return false;
     P.nper = std::max<int64_t>(1, (tile_data_bytes() - P.span) / std::max<int64_t>(P.pext, 1) + 1);
@@ -484,7 +548,13 @@ static bool tile_pack(const ompi_amd_ddt_t *ddt, size_t count, int G, const char
     hipError_t e = hipSuccess;
 #define TILE(GG)                                                                               \
     case GG:                                                                                   \
-        if (ident)                                                                             \
+        if (UNPACK && ident)                                                                   \
+            hipLaunchKernelGGL((ddt_unpack_tile_kernel<GG, true>), dim3(grid),                 \
+                               dim3(kDdtThreads), lds, s, P, contig, typed, start, j0, j1);     \
+        else if (UNPACK)                                                                       \
+            hipLaunchKernelGGL((ddt_unpack_tile_kernel<GG, false>), dim3(grid),                \
+                               dim3(kDdtThreads), lds, s, P, contig, typed, start, j0, j1);     \
+        else if (ident)                                                                        \
             hipLaunchKernelGGL((ddt_pack_tile_kernel<GG, true>), dim3(grid), dim3(kDdtThreads), \
                                lds, s, P, typed, contig, start, j0, j1);                        \
         else                                                                                   \
@@ -505,8 +575,8 @@ static bool tile_pack(const ompi_amd_ddt_t *ddt, size_t count, int G, const char
     // partial periods at the window ends: generic byte mapping
     const ddt_window w{start, start, 0, j0 * P.psize - start, j1 * P.psize, end - j1 * P.psize};
     if (e == hipSuccess && w.head + w.tail > 0) {
-        hipLaunchKernelGGL((ddt_vec_edges<false>), dim3(1), dim3(kDdtThreads), 0, s, d, typed,
-                           contig, w);
+        hipLaunchKernelGGL((ddt_vec_edges<UNPACK>), dim3(1), dim3(kDdtThreads), 0, s, d,
+                           UNPACK ? contig : typed, UNPACK ? typed : contig, w);
         e = hipGetLastError();
     }
     *err = e;
@@ -545,8 +615,8 @@ static int ddt_run(const ompi_amd_ddt_t *ddt, size_t count, const void *typed, v
                       (uint64_t)ddt->max_blen / (uint64_t)G < (1ull << 32) &&
                       (uint64_t)ddt->size / (uint64_t)G < (1ull << 32);
     hipError_t e;
-    if (!UNPACK && tile_pack(ddt, count, G, tsrc, tdst, start, end, d, s, &e)) {
-        // staged LDS tile pack (+ generic bytes for partial periods)
+    if (tile_run<UNPACK>(ddt, count, G, (char *)typed, (char *)contig, start, end, d, s, &e)) {
+        // staged LDS tile pack / unpack (+ generic bytes for partial periods)
     } else if (ddt->host.size() == 1) {
         const ddt_elem &x = ddt->host[0];
         const ddt_walk v{x.count, x.blen / G, x.stride, x.disp, ddt->extent, x.count * (x.blen / G)};
