@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""One staged tile pack (struct {int, double}, 256 MiB packed) x 20, for
-rocprofv3 --kernel-trace --stats: the per-launch duration of
-ddt_pack_tile_kernel against its algorithmic bytes (2 x packed)."""
+"""One staged tile pack and one staged tile unpack (struct {int, double},
+256 MiB packed) x 20 each, for rocprofv3 --kernel-trace --stats: the
+per-launch durations of ddt_pack_tile_kernel / ddt_unpack_tile_kernel
+against their algorithmic bytes (2 x packed)."""
 import os
 import sys
 
@@ -19,5 +20,9 @@ for _ in range(20):
     cv = dd.Convertor()
     cv.prepare_for_send(dt, count, src)
     cv.pack(out, dt.size * count)
+for _ in range(20):
+    cv = dd.Convertor()
+    cv.prepare_for_recv(dt, count, src)
+    cv.unpack(out, dt.size * count)
 torch.cuda.synchronize()
-print("packed", dt.size * count, "bytes x 20")
+print("packed and unpacked", dt.size * count, "bytes x 20")
