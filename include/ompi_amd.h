@@ -50,7 +50,9 @@ enum {
     OMPI_AMD_TYPE_INT32_T = 4, OMPI_AMD_TYPE_UINT32_T = 5,
     OMPI_AMD_TYPE_INT64_T = 6, OMPI_AMD_TYPE_UINT64_T = 7,
     OMPI_AMD_TYPE_FLOAT = 15, OMPI_AMD_TYPE_DOUBLE = 16,
-    OMPI_AMD_TYPE_BOOL = 25, OMPI_AMD_TYPE_BYTE = 30,
+    OMPI_AMD_TYPE_BOOL = 25,
+    OMPI_AMD_TYPE_C_FLOAT_COMPLEX = 27, OMPI_AMD_TYPE_C_DOUBLE_COMPLEX = 28,
+    OMPI_AMD_TYPE_BYTE = 30,
     OMPI_AMD_TYPE_FLOAT_INT = 34, OMPI_AMD_TYPE_DOUBLE_INT = 35,
     OMPI_AMD_TYPE_LONG_INT = 36, OMPI_AMD_TYPE_2INT = 37,
     OMPI_AMD_TYPE_SHORT_INT = 38,

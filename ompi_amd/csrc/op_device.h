@@ -29,6 +29,70 @@ struct two_int_t { int v; int k; };
 struct short_int_t { short v; int k; };
 static_assert(sizeof(double_int_t) == 16 && sizeof(short_int_t) == 8, "pair ABI");
 
+// C complex types (MPI_C_FLOAT_COMPLEX / MPI_C_DOUBLE_COMPLEX): op/base
+// reduces them with C99 `_Complex` arithmetic, OP_FUNC(sum|prod,
+// c_float_complex, float _Complex, +=|*=) (op_base_functions.c:339-340,
+// 408-409) and OP_FUNC_3BUF (:967-968, :1036-1037).  The product is GCC's
+// C99 expansion: x = ac - bd, y = ad + bc in the element type, and only when
+// both are NaN libgcc's __mul?c3 recovers the infinities (ISO C Annex G.5.1).
+template <typename R> struct cplx {
+    R re, im;
+};
+using cfloat_t = cplx<float>;
+using cdouble_t = cplx<double>;
+static_assert(sizeof(cfloat_t) == 8 && sizeof(cdouble_t) == 16, "complex ABI");
+
+template <typename R>
+__device__ __forceinline__ cplx<R> operator+(cplx<R> x, cplx<R> y) {
+    return {x.re + y.re, x.im + y.im};
+}
+
+template <typename R> __device__ __forceinline__ R cp_inf_or_zero(R v) {
+    return __builtin_copysign(__builtin_isinf(v) ? R(1) : R(0), v);
+}
+template <typename R> __device__ __forceinline__ R cp_nan_to_zero(R v) {
+    return __builtin_isnan(v) ? __builtin_copysign(R(0), v) : v;
+}
+
+// (a + ib)(c + id); x = the first operand (2-buffer: out, 3-buffer: in1)
+template <typename R>
+__device__ __forceinline__ cplx<R> operator*(cplx<R> x, cplx<R> y) {
+    R a = x.re, b = x.im, c = y.re, d = y.im;
+    const R ac = a * c, bd = b * d, ad = a * d, bc = b * c;
+    R re = ac - bd, im = ad + bc;
+    if (__builtin_isnan(re) && __builtin_isnan(im)) {
+        bool again = false;
+        if (__builtin_isinf(a) || __builtin_isinf(b)) {
+            a = cp_inf_or_zero(a);
+            b = cp_inf_or_zero(b);
+            c = cp_nan_to_zero(c);
+            d = cp_nan_to_zero(d);
+            again = true;
+        }
+        if (__builtin_isinf(c) || __builtin_isinf(d)) {
+            c = cp_inf_or_zero(c);
+            d = cp_inf_or_zero(d);
+            a = cp_nan_to_zero(a);
+            b = cp_nan_to_zero(b);
+            again = true;
+        }
+        if (!again && (__builtin_isinf(ac) || __builtin_isinf(bd) || __builtin_isinf(ad) ||
+                       __builtin_isinf(bc))) {
+            a = cp_nan_to_zero(a);
+            b = cp_nan_to_zero(b);
+            c = cp_nan_to_zero(c);
+            d = cp_nan_to_zero(d);
+            again = true;
+        }
+        if (again) {
+            const R inf = __builtin_huge_val();
+            re = inf * (a * c - b * d);
+            im = inf * (a * d + b * c);
+        }
+    }
+    return {re, im};
+}
+
 template <typename T> struct is_pair { static constexpr bool value = false; };
 template <> struct is_pair<float_int_t> { static constexpr bool value = true; };
 template <> struct is_pair<double_int_t> { static constexpr bool value = true; };
@@ -55,6 +119,8 @@ template <> struct type_of<OMPI_AMD_TYPE_DOUBLE_INT> { using type = double_int_t
 template <> struct type_of<OMPI_AMD_TYPE_LONG_INT> { using type = long_int_t; };
 template <> struct type_of<OMPI_AMD_TYPE_2INT> { using type = two_int_t; };
 template <> struct type_of<OMPI_AMD_TYPE_SHORT_INT> { using type = short_int_t; };
+template <> struct type_of<OMPI_AMD_TYPE_C_FLOAT_COMPLEX> { using type = cfloat_t; };
+template <> struct type_of<OMPI_AMD_TYPE_C_DOUBLE_COMPLEX> { using type = cdouble_t; };
 
 // Which (op,type) slots exist — the op/base table pattern
 // (op_base_functions.c:1485-1569) restricted to the predefined C types.
@@ -64,8 +130,14 @@ __host__ __device__ constexpr bool is_pair_type(int t) {
     return t == OMPI_AMD_TYPE_FLOAT_INT || t == OMPI_AMD_TYPE_DOUBLE_INT ||
            t == OMPI_AMD_TYPE_LONG_INT || t == OMPI_AMD_TYPE_2INT || t == OMPI_AMD_TYPE_SHORT_INT;
 }
+__host__ __device__ constexpr bool is_c_complex(int t) {
+    return t == OMPI_AMD_TYPE_C_FLOAT_COMPLEX || t == OMPI_AMD_TYPE_C_DOUBLE_COMPLEX;
+}
+// (op/base's COMPLEX(sum|prod) rows, :1509/:1516/:1596/:1603; long double
+// complex stays with op/base: gfx950 has no long double)
 __host__ __device__ constexpr bool slot_supported(int op, int t) {
-    return (op == OMPI_AMD_OP_MAX || op == OMPI_AMD_OP_MIN || op == OMPI_AMD_OP_SUM ||
+    return (op == OMPI_AMD_OP_SUM || op == OMPI_AMD_OP_PROD) && is_c_complex(t) ? true
+         : (op == OMPI_AMD_OP_MAX || op == OMPI_AMD_OP_MIN || op == OMPI_AMD_OP_SUM ||
             op == OMPI_AMD_OP_PROD) ? (is_c_int(t) || is_fp(t))
          : (op == OMPI_AMD_OP_LAND || op == OMPI_AMD_OP_LOR || op == OMPI_AMD_OP_LXOR)
                ? (is_c_int(t) || t == OMPI_AMD_TYPE_BOOL)

@@ -293,6 +293,8 @@ size_t ompi_amd_type_extent(int type) {
     case OMPI_AMD_TYPE_INT16_T: case OMPI_AMD_TYPE_UINT16_T: return 2;
     case OMPI_AMD_TYPE_INT32_T: case OMPI_AMD_TYPE_UINT32_T: case OMPI_AMD_TYPE_FLOAT: return 4;
     case OMPI_AMD_TYPE_INT64_T: case OMPI_AMD_TYPE_UINT64_T: case OMPI_AMD_TYPE_DOUBLE: return 8;
+    case OMPI_AMD_TYPE_C_FLOAT_COMPLEX: return sizeof(cfloat_t);
+    case OMPI_AMD_TYPE_C_DOUBLE_COMPLEX: return sizeof(cdouble_t);
     case OMPI_AMD_TYPE_FLOAT_INT: return sizeof(float_int_t);
     case OMPI_AMD_TYPE_DOUBLE_INT: return sizeof(double_int_t);
     case OMPI_AMD_TYPE_LONG_INT: return sizeof(long_int_t);

@@ -78,6 +78,8 @@ MPI_UINT64_T = Datatype("MPI_UINT64_T", 7, 8, 8, np.dtype(np.uint64))
 MPI_FLOAT = Datatype("MPI_FLOAT", 15, 4, 4, np.dtype(np.float32))
 MPI_DOUBLE = Datatype("MPI_DOUBLE", 16, 8, 8, np.dtype(np.float64))
 MPI_C_BOOL = Datatype("MPI_C_BOOL", 25, 1, 1, np.dtype(np.uint8))
+MPI_C_FLOAT_COMPLEX = Datatype("MPI_C_FLOAT_COMPLEX", 27, 8, 8, np.dtype(np.complex64))
+MPI_C_DOUBLE_COMPLEX = Datatype("MPI_C_DOUBLE_COMPLEX", 28, 16, 16, np.dtype(np.complex128))
 MPI_BYTE = Datatype("MPI_BYTE", 30, 1, 1, np.dtype(np.uint8))
 MPI_FLOAT_INT = Datatype("MPI_FLOAT_INT", 34, 8, 8, _pair(np.float32, 0))
 MPI_DOUBLE_INT = Datatype("MPI_DOUBLE_INT", 35, 12, 16, _pair(np.float64, 4))
@@ -90,7 +92,7 @@ MPI_LONG = MPI_INT64_T
 
 DATATYPES = [MPI_INT8_T, MPI_UINT8_T, MPI_INT16_T, MPI_UINT16_T, MPI_INT32_T,
              MPI_UINT32_T, MPI_INT64_T, MPI_UINT64_T, MPI_FLOAT, MPI_DOUBLE,
-             MPI_C_BOOL, MPI_BYTE, MPI_FLOAT_INT, MPI_DOUBLE_INT, MPI_LONG_INT,
+             MPI_C_BOOL, MPI_C_FLOAT_COMPLEX, MPI_C_DOUBLE_COMPLEX, MPI_BYTE, MPI_FLOAT_INT, MPI_DOUBLE_INT, MPI_LONG_INT,
              MPI_2INT, MPI_SHORT_INT]
 BY_CODE = {d.code: d for d in DATATYPES}
 

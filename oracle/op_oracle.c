@@ -18,12 +18,19 @@
  *     LOC               if (a1.v op a2.v) out = a1; else if equal
  *                       out = {a1.v, min(a2.k, a1.k)}; else out = a2  :709-731
  *
+ *   C complex (float / double _Complex, :339-340, :408-409, :967-968,
+ *   :1036-1037): SUM and PROD only, with C99 `_Complex` arithmetic exactly
+ *   as op/base writes it (`*b *= *a`, `out = in1 * in2`); gcc's expansion
+ *   of the product (x = ac - bd, y = ad + bc, libgcc's __mul?c3 recovery
+ *   when both are NaN, ISO C Annex G.5.1) is what the reference computes.
+ *
  * Note the NaN / signed-zero consequences (pinned in tests/golden):
  * MAX(out=x, in=NaN) = NaN, MAX(out=NaN, in=3) = 3, MAX(out=+0,in=-0) = -0.
  * LOC handlers only write v and k, never the struct padding.
  */
 #include "oracle.h"
 
+#include <complex.h>
 #include <string.h>
 #include <time.h>
 
@@ -45,12 +52,15 @@ size_t orc_type_extent(int type)
     case ORC_T_LONG_INT: return sizeof(orc_long_int_t);
     case ORC_T_2INT: return sizeof(orc_2int_t);
     case ORC_T_SHORT_INT: return sizeof(orc_short_int_t);
+    case ORC_T_C_FLOAT_COMPLEX: return sizeof(float _Complex);
+    case ORC_T_C_DOUBLE_COMPLEX: return sizeof(double _Complex);
     default: return 0;
     }
 }
 
 static int is_c_int(int t) { return t >= ORC_T_INT8 && t <= ORC_T_UINT64; }
 static int is_fp(int t) { return t == ORC_T_FLOAT || t == ORC_T_DOUBLE; }
+static int is_complex(int t) { return t == ORC_T_C_FLOAT_COMPLEX || t == ORC_T_C_DOUBLE_COMPLEX; }
 static int is_loc(int t)
 {
     return t == ORC_T_FLOAT_INT || t == ORC_T_DOUBLE_INT || t == ORC_T_LONG_INT ||
@@ -61,7 +71,9 @@ static int is_loc(int t)
 int orc_op_defined(int op, int type)
 {
     switch (op) {
-    case ORC_OP_MAX: case ORC_OP_MIN: case ORC_OP_SUM: case ORC_OP_PROD:
+    case ORC_OP_SUM: case ORC_OP_PROD:
+        return is_c_int(type) || is_fp(type) || is_complex(type);
+    case ORC_OP_MAX: case ORC_OP_MIN:
         return is_c_int(type) || is_fp(type);
     case ORC_OP_LAND: case ORC_OP_LOR: case ORC_OP_LXOR:
         return is_c_int(type) || type == ORC_T_BOOL;
@@ -167,6 +179,23 @@ ORC_BIT_LOOPS(int64_t) ORC_BIT_LOOPS(uint64_t)
 typedef _Bool orc_bool; typedef char orc_byte;
 ORC_BIT_LOOPS(orc_bool) ORC_BIT_LOOPS(orc_byte)
 
+/* OP_FUNC / OP_FUNC_3BUF over the C complex types: SUM and PROD only */
+#define ORC_COMPLEX_LOOPS(NAME, T)                                             \
+    static void cplx2_##NAME(int op, const T *a, T *b, size_t n)               \
+    {                                                                          \
+        size_t i;                                                              \
+        if (op == ORC_OP_SUM) for (i = 0; i < n; i++) b[i] += a[i];            \
+        else for (i = 0; i < n; i++) b[i] *= a[i];                             \
+    }                                                                          \
+    static void cplx3_##NAME(int op, const T *x, const T *y, T *o, size_t n)   \
+    {                                                                          \
+        size_t i;                                                              \
+        if (op == ORC_OP_SUM) for (i = 0; i < n; i++) o[i] = x[i] + y[i];      \
+        else for (i = 0; i < n; i++) o[i] = x[i] * y[i];                       \
+    }
+ORC_COMPLEX_LOOPS(c32, float _Complex)
+ORC_COMPLEX_LOOPS(c64, double _Complex)
+
 ORC_LOC_LOOPS(orc_float_int_t) ORC_LOC_LOOPS(orc_double_int_t)
 ORC_LOC_LOOPS(orc_long_int_t) ORC_LOC_LOOPS(orc_2int_t)
 ORC_LOC_LOOPS(orc_short_int_t)
@@ -203,6 +232,8 @@ int orc_op_2buff(int op, int type, const void *in, void *inout, size_t count)
         default: return -1;
         }
     }
+    if (type == ORC_T_C_FLOAT_COMPLEX) { cplx2_c32(op, in, inout, count); return 0; }
+    if (type == ORC_T_C_DOUBLE_COMPLEX) { cplx2_c64(op, in, inout, count); return 0; }
     if (is_arith(op)) {
         DISPATCH_INT(arith2, (op, in, inout, count),
                      case ORC_T_FLOAT: arith2_orc_f32(op, in, inout, count); return 0;
@@ -227,6 +258,8 @@ int orc_op_3buff(int op, int type, const void *in1, const void *in2, void *out,
         default: return -1;
         }
     }
+    if (type == ORC_T_C_FLOAT_COMPLEX) { cplx3_c32(op, in1, in2, out, count); return 0; }
+    if (type == ORC_T_C_DOUBLE_COMPLEX) { cplx3_c64(op, in1, in2, out, count); return 0; }
     if (is_arith(op)) {
         DISPATCH_INT(arith3, (op, in1, in2, out, count),
                      case ORC_T_FLOAT: arith3_orc_f32(op, in1, in2, out, count); return 0;

@@ -39,7 +39,8 @@ enum {
 enum {
     ORC_T_INT8 = 0, ORC_T_UINT8 = 1, ORC_T_INT16 = 2, ORC_T_UINT16 = 3,
     ORC_T_INT32 = 4, ORC_T_UINT32 = 5, ORC_T_INT64 = 6, ORC_T_UINT64 = 7,
-    ORC_T_FLOAT = 15, ORC_T_DOUBLE = 16, ORC_T_BOOL = 25, ORC_T_BYTE = 30,
+    ORC_T_FLOAT = 15, ORC_T_DOUBLE = 16, ORC_T_BOOL = 25,
+    ORC_T_C_FLOAT_COMPLEX = 27, ORC_T_C_DOUBLE_COMPLEX = 28, ORC_T_BYTE = 30,
     ORC_T_FLOAT_INT = 34, ORC_T_DOUBLE_INT = 35, ORC_T_LONG_INT = 36,
     ORC_T_2INT = 37, ORC_T_SHORT_INT = 38,
     ORC_T_COUNT = 41

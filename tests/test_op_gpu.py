@@ -55,6 +55,14 @@ def gen(dtype: mop.Datatype, n: int, seed: int) -> np.ndarray:
             if off >= nd.fields["k"][1] + 4:
                 raw[:, off] = rng.integers(0, 255, n)
         return a
+    if nd.kind == "c":
+        # complex: independent real/imaginary parts through the fp generator,
+        # so NaN / inf / ±0 / denormal components meet every recovery branch
+        # of the C99 product (ISO C Annex G.5.1)
+        rd = np.dtype(np.float32 if nd.itemsize == 8 else np.float64)
+        re = gen(Datatype_like(rd), n, seed * 2 + 1)
+        im = gen(Datatype_like(rd), n, seed * 2 + 2)
+        return _cplx(re, im, nd)
     if nd.kind == "f":
         a = (rng.standard_normal(n) * 100).astype(nd)
         specials = np.array([np.nan, -np.nan, 0.0, -0.0, np.inf, -np.inf,
@@ -70,6 +78,22 @@ def gen(dtype: mop.Datatype, n: int, seed: int) -> np.ndarray:
     return a
 
 
+class Datatype_like:
+    """Minimal stand-in carrying a numpy dtype for gen()."""
+    def __init__(self, nd):
+        self.np_dtype = nd
+        self.code = -1
+
+
+def _cplx(re: np.ndarray, im: np.ndarray, nd) -> np.ndarray:
+    # interleave the parts bit-for-bit (re + 1j*im would turn inf*1j into nan)
+    out = np.empty(len(re), dtype=nd)
+    v = out.view(re.dtype).reshape(-1, 2)
+    v[:, 0] = re
+    v[:, 1] = im
+    return out
+
+
 def same_bits(got: np.ndarray, exp: np.ndarray, dtype: mop.Datatype) -> bool:
     nd = dtype.np_dtype
     if nd.names:
@@ -83,9 +107,11 @@ def same_bits(got: np.ndarray, exp: np.ndarray, dtype: mop.Datatype) -> bool:
     e = exp.view(np.uint8)
     if np.array_equal(g, e):
         return True
-    if nd.kind == "f":
-        # NaN payload/sign bits may differ only where both are NaN
-        gv, ev = got.view(nd), exp.view(nd)
+    if nd.kind in "fc":
+        # NaN payload/sign bits may differ only where both are NaN (complex:
+        # per component)
+        rd = nd if nd.kind == "f" else np.dtype(np.float32 if nd.itemsize == 8 else np.float64)
+        gv, ev = got.view(rd), exp.view(rd)
         both_nan = np.isnan(gv) & np.isnan(ev)
         return bool(np.array_equal(gv[~both_nan].view(np.uint8), ev[~both_nan].view(np.uint8)))
     return False
