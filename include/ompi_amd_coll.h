@@ -72,12 +72,22 @@ int ompi_amd_comm_size(const ompi_amd_comm_t *comm);
  *                   buffers, owners reduce locally and store into every
  *                   rbuf).  Env OMPI_AMD_COLL_ALGORITHM sets the default.
  *   "profile"       1: bracket the allreduce's reduce and gather kernels with
- *                   HIP events (read with ompi_amd_comm_phase_ms) */
+ *                   HIP events (read with ompi_amd_comm_phase_ms)
+ *   "force_shadow"  1: zero-copy calls treat every user buffer as one the
+ *                   runtime refused to export and run through the export
+ *                   fallback (a shadow copy of the communicator's own);
+ *                   for tests */
 int ompi_amd_comm_set_param(ompi_amd_comm_t *comm, const char *key, int64_t value);
 /* Read a parameter above, or a state counter: "landing_bytes" (current
- * landing-buffer capacity), "landing_alias_retries" (landing growths that
- * found a peer mapping aliasing an older allocation and retried), "imports"
- * (cached peer-buffer mappings). */
+ * landing-buffer capacity), "stale_closed" (cached peer-buffer mappings
+ * closed because the peer freed that allocation: a newer one of the peer
+ * overlaps its range or reuses its handle under another buffer id),
+ * "stale_same_handle" (of those, how many carried the very handle bytes of
+ * the freed allocation — a cache keyed by handle bytes would have served
+ * the freed memory),
+ * "imports" (cached peer-buffer mappings), "shadowed" (zero-copy calls
+ * that ran through the export fallback because the runtime refused to
+ * export a user buffer). */
 int ompi_amd_comm_get_param(const ompi_amd_comm_t *comm, const char *key, int64_t *value);
 
 /* Sticky error of the device side (a barrier that timed out, ...).

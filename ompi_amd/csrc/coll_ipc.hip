@@ -64,66 +64,17 @@
 #include "../../include/ompi_amd_coll.h"
 #include "bootstrap.h"
 #include "comm_internal.h"
+#include "coll_kernels.h"
 #include "op_device.h"
 #include "runtime.h"
 
 namespace ompi_amd {
 
-constexpr int kMaxRanks = OMPI_AMD_MAX_RANKS;
-constexpr int kXferThreads = 256;
-
-struct ptr_set { const char *p[kMaxRanks]; };
-struct flag_set { uint64_t *p[kMaxRanks]; };
-
-// Operand orders of the reference's reduction algorithms.  Sources are
-// loaded in virtual-rank order v[j] = x[(first + j) % n].
-enum order_t {
-    ORDER_RING = 0,      // ring / ring_segmented block `first`; linear scan (first 0)
-    ORDER_TREE = 1,      // recursive doubling (first 0)
-    ORDER_CHAIN = 2,     // pipeline chain rooted at `first`; basic_linear = chain at 0, no swap
-    ORDER_BINOMIAL = 3,  // in-order binomial tree rooted at `first`
-    ORDER_BINARY = 4,    // binary tree rooted at `first`
-    ORDER_HALVING = 5,   // recursive-halving reduce_scatter, owner tmp rank in flags >> 8
-};
-// The root passed MPI_IN_PLACE: its first combine is f(own, child)
-// (coll_base_reduce.c:170-171, 196-199).
-constexpr int FOLD_ROOT_INPLACE = 1;
-
-// One reduction job: elements [off, off+cnt) of every source, combined in
-// the call's order and written to dst + off_dst (element units).
-struct red_job {
-    int64_t off, cnt, off_dst;
-    int first;  // virtual rank 0 (ring block b, tree root)
-    int head;   // elements before the 16-B aligned body; -1: no common alignment
-};
-struct red_jobs { red_job j[kMaxRanks]; int n; };
-
-struct cp_job { const char *src; char *dst; int64_t bytes; };
-struct cp_jobs { cp_job j[kMaxRanks]; int n; };
-
-__device__ __forceinline__ void sys_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
-__device__ __forceinline__ void sys_release() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
-// The workgroup's acquire: lane 0 issues it (it invalidates the CU's L1 and
-// the XCD's L2 for every wave of the CU), the barrier holds the other waves
-// until it completed.  One per workgroup instead of one per wave: in a
-// 1024-workgroup grid the 4 per workgroup cost measurable bandwidth
-// (osc_ipc.hip's grid note).
-__device__ __forceinline__ void acquire_once() {
-    if (threadIdx.x == 0) sys_acquire();
-    __syncthreads();
-}
-
-// Every storing wave drains its stores before the workgroup's single
-// system-scope release (MI355X_MICROARCH.md, inter-workgroup visibility).
-__device__ __forceinline__ void xfer_epilogue() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) sys_release();
-}
+#define TRY(x)                                   \
+    do {                                         \
+        int rc_ = (x);                           \
+        if (rc_ != OMPI_AMD_SUCCESS) return rc_; \
+    } while (0)
 
 // ---------------------------------------------------------------- barrier
 __global__ __launch_bounds__(64) void barrier_kernel(uint64_t *local, flag_set peers, int rank,
@@ -146,269 +97,6 @@ __global__ __launch_bounds__(64) void barrier_kernel(uint64_t *local, flag_set p
     }
     __syncthreads();
     sys_acquire();
-}
-
-// ---------------------------------------------------------------- reduce
-// Fold v[0..n) (virtual-rank order) with the 2-buffer rule f(out, in).  All
-// array indices are compile-time constants after unrolling; n, order and
-// flags are wave-uniform.
-template <typename T, int OP>
-__device__ __forceinline__ T fold(const T (&v)[kMaxRanks], int n, int order, int flags) {
-    using F = opfn<OP, false>;
-    const bool swap = (flags & FOLD_ROOT_INPLACE) != 0;
-    if (order == ORDER_RING) {
-        // v[j] = x[(b + j) % n]; acc = x[b]; acc = f(x[b+j], acc)
-        T acc = v[0];
-#pragma unroll
-        for (int j = 1; j < kMaxRanks; ++j)
-            if (j < n) acc = F::template f<T>(v[j], acc);
-        return acc;
-    }
-    if (order == ORDER_CHAIN) {
-        // chain fanout 1 (coll_base_topo.c:588-600) under the generic reduce
-        // (coll_base_reduce.c:206-215): node k's only child is k+1,
-        // acc_k = f(acc_(k+1), x_k); basic_linear (:680-721) is the same
-        // expression at first = 0.
-        T acc = v[kMaxRanks - 1];
-#pragma unroll
-        for (int j = kMaxRanks - 1; j >= 0; --j) {
-            if (j == n - 1) acc = v[j];
-            else if (j < n - 1) acc = (j == 0 && swap) ? F::template f<T>(v[0], acc)
-                                                       : F::template f<T>(acc, v[j]);
-        }
-        return acc;
-    }
-    if (order == ORDER_BINOMIAL) {
-        // in-order binomial (coll_base_topo.c:402-458): vrank u's children
-        // are u+1, u+2, u+4, ... while the bit is clear; first child:
-        // acc = f(child, own), later ones acc = f(acc, child).
-        T w[kMaxRanks];
-#pragma unroll
-        for (int i = 0; i < kMaxRanks; ++i) w[i] = v[i];
-#pragma unroll
-        for (int u = 0; u + 1 < kMaxRanks; u += 2)
-            if (u + 1 < n) w[u] = (u == 0 && swap) ? F::template f<T>(w[0], w[1])
-                                                   : F::template f<T>(w[u + 1], w[u]);
-#pragma unroll
-        for (int m = 2; m < kMaxRanks; m <<= 1) {
-#pragma unroll
-            for (int u = 0; u + m < kMaxRanks; u += 2 * m)
-                if (u + m < n) w[u] = F::template f<T>(w[u], w[u + m]);
-        }
-        return w[0];
-    }
-    if (order == ORDER_BINARY) {
-        // build_tree(2) (coll_base_topo.c:77-175): shifted rank s has
-        // children s + d and s + 2d, d = largest power of two <= s + 1;
-        // children have larger s, so descending s sees them finished.
-        T w[kMaxRanks];
-#pragma unroll
-        for (int i = 0; i < kMaxRanks; ++i) w[i] = v[i];
-#pragma unroll
-        for (int s = kMaxRanks - 1; s >= 0; --s) {
-            int d = 1;
-            while (2 * d <= s + 1) d *= 2;
-            const int c0 = s + d, c1 = s + 2 * d;
-            if (c0 < kMaxRanks && c0 < n)
-                w[s] = (s == 0 && swap) ? F::template f<T>(w[0], w[c0])
-                                        : F::template f<T>(w[c0], w[s]);
-            if (c1 < kMaxRanks && c1 < n) w[s] = F::template f<T>(w[s], w[c1]);
-        }
-        return w[0];
-    }
-    if (order == ORDER_HALVING) {
-        // recursive-halving reduce_scatter (coll_base_reduce_scatter.c:
-        // 203-345): the 2*remain lowest ranks fold pairwise (odd keeps:
-        // f(odd, even)), then at every mask from the top the rank holding
-        // the owner's half does f(mine, partner's).  tb = the owner's tmp
-        // rank; holders at mask m agree with tb on bit m, and their
-        // partners never do, so the update can run in place.
-        int adj = 1;
-        while (adj * 2 <= n) adj *= 2;
-        const int remain = n - adj;
-        const int tb = (flags >> 8) & 0xff;
-        T w[kMaxRanks];
-#pragma unroll
-        for (int u = 0; u < kMaxRanks; ++u) {
-            if (2 * u + 1 < kMaxRanks && u < remain) w[u] = F::template f<T>(v[2 * u + 1], v[2 * u]);
-            else if (u < adj) w[u] = v[u + remain];
-        }
-#pragma unroll
-        for (int m = kMaxRanks / 2; m >= 1; m >>= 1) {
-            if (m < adj) {
-#pragma unroll
-                for (int u = 0; u < kMaxRanks; ++u)
-                    if (u < adj && (u & m) == (tb & m)) w[u] = F::template f<T>(w[u], w[u ^ m]);
-            }
-        }
-        T r = w[0];
-#pragma unroll
-        for (int u = 1; u < kMaxRanks; ++u)
-            if (u == tb) r = w[u];
-        return r;
-    }
-    // recursive doubling (coll_base_allreduce.c:184-236): fold the
-    // 2*extra lowest ranks pairwise, then a pairwise tree; every combine is
-    // f(out = higher, in = lower).
-    int adj = 1;
-    while (adj * 2 <= n) adj *= 2;
-    const int extra = n - adj;
-    T w[kMaxRanks];
-#pragma unroll
-    for (int i = 0; i < kMaxRanks; ++i) {
-        if (i < extra) w[i] = F::template f<T>(v[2 * i + 1], v[2 * i]);
-        else if (i < adj) w[i] = v[i + extra];
-    }
-#pragma unroll
-    for (int len = kMaxRanks; len > 1; len >>= 1) {
-        if (len <= adj) {
-#pragma unroll
-            for (int i = 0; i < kMaxRanks / 2; ++i)
-                if (2 * i + 1 < len) w[i] = F::template f<T>(w[2 * i + 1], w[2 * i]);
-        }
-    }
-    return w[0];
-}
-
-// Gather v[j] for element index e of the sources in virtual-rank order.
-template <typename T>
-__device__ __forceinline__ void gather_scalar(T (&v)[kMaxRanks], const ptr_set &src, int n,
-                                              int first, int64_t e) {
-#pragma unroll
-    for (int j = 0; j < kMaxRanks; ++j) {
-        if (j < n) {
-            const int r = (first + j) % n;
-            v[j] = reinterpret_cast<const T *>(src.p[r])[e];
-        }
-    }
-}
-
-// n sources (virtual ranks 0..n), result stored to dst.p[0 .. ndst): ndst =
-// 1 is a plain reduce into one buffer; ndst = size is the fused push of the
-// owner's block into every rank's rbuf (the host orders dst local first,
-// then peers rank+1, rank+2, ... so concurrent owners spread their stores
-// over the links).
-template <typename T, int OP>
-__global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, ptr_set dst, int ndst,
-                                                              int n, int order, int flags,
-                                                              red_jobs jobs) {
-    acquire_once();
-    const red_job jb = jobs.j[blockIdx.y];
-    constexpr int E = 16 / sizeof(T);
-    const int64_t gstride = (int64_t)gridDim.x * kXferThreads;
-    const int64_t tid = (int64_t)blockIdx.x * kXferThreads + threadIdx.x;
-    // vector body [head, head + nvec*E): every source and dst 16-B aligned
-    // there (head < 0: no common alignment, all scalar)
-    const int64_t head = jb.head < 0 ? jb.cnt : jb.head;
-    const int64_t nvec = jb.head < 0 ? 0 : (jb.cnt - head) / E;
-    for (int64_t i = tid; i < nvec; i += gstride) {
-        vec16<T> v[kMaxRanks];
-#pragma unroll
-        for (int j = 0; j < kMaxRanks; ++j) {
-            if (j < n) {
-                const int r = (jb.first + j) % n;
-                const u32x4 *p = reinterpret_cast<const u32x4 *>(
-                    reinterpret_cast<const T *>(src.p[r]) + jb.off + head);
-                v[j].v = __builtin_nontemporal_load(p + i);
-            }
-        }
-        vec16<T> out;
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-            T s[kMaxRanks];
-#pragma unroll
-            for (int j = 0; j < kMaxRanks; ++j) s[j] = v[j].e[e];
-            out.e[e] = fold<T, OP>(s, n, order, flags);
-        }
-#pragma unroll
-        for (int k = 0; k < kMaxRanks; ++k)
-            if (k < ndst)
-                reinterpret_cast<u32x4 *>(reinterpret_cast<T *>(const_cast<char *>(dst.p[k])) +
-                                          jb.off_dst + head)[i] = out.v;
-    }
-    // scalar head [0, head) and tail [head + nvec*E, cnt)
-    const int64_t tail0 = head + nvec * E;
-    const int64_t nscalar = head + (jb.cnt - tail0);
-    for (int64_t k = tid; k < nscalar; k += gstride) {
-        const int64_t e = k < head ? k : tail0 + (k - head);
-        T s[kMaxRanks];
-        gather_scalar<T>(s, src, n, jb.first, jb.off + e);
-        const T r = fold<T, OP>(s, n, order, flags);
-#pragma unroll
-        for (int d = 0; d < kMaxRanks; ++d)
-            if (d < ndst)
-                store_elem<T>(reinterpret_cast<T *>(const_cast<char *>(dst.p[d])) + jb.off_dst + e,
-                              r);
-    }
-    xfer_epilogue();
-}
-
-// ---------------------------------------------------------------- fused small allreduce
-// One launch for small messages (param "fused_bytes"): every workgroup
-// stages its slice of my input in my scratch half, signals the peers on its
-// own flag row, waits for the same slice of every peer and folds it.
-// Workgroup g depends only on the peers' workgroup g (same slice), so there
-// is no grid-wide sync.  Flag slot [g * kMaxRanks + p] of rank r holds the
-// last epoch peer p's workgroup g signalled to r (row 0 doubles as the
-// barrier kernel's row; epochs only grow, so the users never collide).
-constexpr int kFusedMaxGroups = 4096 / (int)sizeof(uint64_t) / kMaxRanks;  // 32 rows
-
-struct fused_args {
-    const char *src;
-    char *dst, *mine;
-    ptr_set peers;
-    uint64_t *flags;
-    flag_set peer_flags;
-    int rank, n, order;
-    int64_t count, split, early, late;
-    uint64_t epoch, timeout_ticks;
-    int *err;
-};
-
-template <typename T, int OP>
-__global__ __launch_bounds__(kXferThreads) void fused_allreduce_kernel(fused_args a) {
-    const int t = threadIdx.x;
-    const int g = blockIdx.y * gridDim.x + blockIdx.x;
-    int64_t off = 0, cnt = a.count;
-    int first = 0;
-    if (a.order == ORDER_RING) {  // grid row y = ring block y
-        const int64_t b = blockIdx.y;
-        off = b < a.split ? b * a.early : b * a.late + a.split;
-        cnt = b < a.split ? a.early : a.late;
-        first = (int)b;
-    }
-    const int64_t per = (cnt + gridDim.x - 1) / gridDim.x;
-    const int64_t lo = off + min(cnt, per * (int64_t)blockIdx.x);
-    const int64_t hi = off + min(cnt, per * (int64_t)(blockIdx.x + 1));
-    const T *src = reinterpret_cast<const T *>(a.src);
-    T *mine = reinterpret_cast<T *>(a.mine);
-    for (int64_t e = lo + t; e < hi; e += kXferThreads) mine[e] = src[e];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) sys_release();
-    __syncthreads();
-    if (t < a.n && t != a.rank) {
-        __hip_atomic_store(a.peer_flags.p[t] + g * kMaxRanks + a.rank, a.epoch, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(a.flags + g * kMaxRanks + t, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_SYSTEM) < a.epoch) {
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
-                __hip_atomic_store(a.err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-                break;
-            }
-        }
-    }
-    __syncthreads();
-    acquire_once();
-    T *dst = reinterpret_cast<T *>(a.dst);
-    for (int64_t e = lo + t; e < hi; e += kXferThreads) {
-        T v[kMaxRanks];
-        gather_scalar<T>(v, a.peers, a.n, first, e);
-        store_elem<T>(dst + e, fold<T, OP>(v, a.n, a.order, 0));
-    }
 }
 
 // ---------------------------------------------------------------- copy
@@ -458,58 +146,24 @@ __global__ __launch_bounds__(kXferThreads) void copy_kernel(cp_jobs jobs) {
 }
 
 // ---------------------------------------------------------------- dispatch
-using red_launch_fn = hipError_t (*)(dim3, const ptr_set &, const ptr_set &, int, int, int, int,
-                                     const red_jobs &, hipStream_t);
-
-template <int OP, int TYPE>
-static hipError_t red_launch_slot(dim3 grid, const ptr_set &src, const ptr_set &dst, int ndst,
-                                  int n, int order, int flags, const red_jobs &jobs,
-                                  hipStream_t s) {
-    if constexpr (slot_supported(OP, TYPE)) {
-        using T = typename type_of<TYPE>::type;
-        hipLaunchKernelGGL((reduce_kernel<T, OP>), grid, dim3(kXferThreads), 0, s, src, dst, ndst,
-                           n, order, flags, jobs);
-        return hipGetLastError();
-    } else {
-        return hipErrorInvalidValue;
+static red_launch_fn red_fn(int op, int type) {
+    if (type < 0 || type >= OMPI_AMD_TYPE_COUNT) return nullptr;
+    switch (op) {
+#define CASE(k) case k: return red_row_##k()[type];
+        OMPI_AMD_COLL_OPS(CASE)
+#undef CASE
+    default: return nullptr;
     }
 }
-
-template <int OP, int... T>
-static constexpr std::array<red_launch_fn, OMPI_AMD_TYPE_COUNT> make_red_row(
-    std::integer_sequence<int, T...>) {
-    return {{(slot_supported(OP, T) ? &red_launch_slot<OP, T> : (red_launch_fn) nullptr)...}};
-}
-template <int... O>
-static constexpr std::array<std::array<red_launch_fn, OMPI_AMD_TYPE_COUNT>, OMPI_AMD_OP_COUNT>
-make_red_table(std::integer_sequence<int, O...>) {
-    return {{make_red_row<O>(std::make_integer_sequence<int, OMPI_AMD_TYPE_COUNT>{})...}};
-}
-static const auto g_red = make_red_table(std::make_integer_sequence<int, OMPI_AMD_OP_COUNT>{});
-
-using fused_launch_fn = hipError_t (*)(dim3, const fused_args &, hipStream_t);
-
-template <int OP, int TYPE>
-static hipError_t fused_launch_slot(dim3 grid, const fused_args &a, hipStream_t s) {
-    if constexpr (slot_supported(OP, TYPE)) {
-        using T = typename type_of<TYPE>::type;
-        hipLaunchKernelGGL((fused_allreduce_kernel<T, OP>), grid, dim3(kXferThreads), 0, s, a);
-        return hipGetLastError();
-    } else {
-        return hipErrorInvalidValue;
+static fused_launch_fn fused_fn(int op, int type) {
+    if (type < 0 || type >= OMPI_AMD_TYPE_COUNT) return nullptr;
+    switch (op) {
+#define CASE(k) case k: return fused_row_##k()[type];
+        OMPI_AMD_COLL_OPS(CASE)
+#undef CASE
+    default: return nullptr;
     }
 }
-template <int OP, int... T>
-static constexpr std::array<fused_launch_fn, OMPI_AMD_TYPE_COUNT> make_fused_row(
-    std::integer_sequence<int, T...>) {
-    return {{(slot_supported(OP, T) ? &fused_launch_slot<OP, T> : (fused_launch_fn) nullptr)...}};
-}
-template <int... O>
-static constexpr std::array<std::array<fused_launch_fn, OMPI_AMD_TYPE_COUNT>, OMPI_AMD_OP_COUNT>
-make_fused_table(std::integer_sequence<int, O...>) {
-    return {{make_fused_row<O>(std::make_integer_sequence<int, OMPI_AMD_TYPE_COUNT>{})...}};
-}
-static const auto g_fused = make_fused_table(std::make_integer_sequence<int, OMPI_AMD_OP_COUNT>{});
 
 // MPI type size (bytes of data) — the tuned decisions use it, not the
 // extent (ompi_datatype_module.c:404-430: DOUBLE_INT size 12 / extent 16).
@@ -556,6 +210,9 @@ struct buf_desc {
     hipIpcMemHandle_t h;
     uint64_t off;
     uint64_t valid;
+    uint64_t id;    // HIP_POINTER_ATTRIBUTE_BUFFER_ID of the allocation in the exporter
+    uint64_t base;  // the allocation's range in the exporter's address space
+    uint64_t size;
 };
 struct call_blob {
     buf_desc s, r;
@@ -567,6 +224,20 @@ struct call_blob {
 struct path_params {
     size_t small_bytes, fused_bytes;
     int zero_copy, algorithm;
+};
+
+// Export fallback.  hipIpcGetMemHandle sometimes refuses a live device
+// allocation (hipErrorInvalidValue on ROCm 7.2, seen for torch tensors after
+// the caching allocator returned and re-took segments; not reproducible in
+// a two-process probe, tools/ipc_alias_probe.hip S7-S12).  A zero-copy call
+// then runs on this rank through a "shadow": an exportable buffer of the
+// communicator that takes the user buffer's place for the peers — the send
+// side is copied in before the call, the receive side copied out after its
+// trailing barrier.  Purely local: the peers just map another allocation.
+struct shadow_set {
+    cp_jobs in{};          // user -> shadow, before the collective
+    cp_job out{};          // shadow -> user rbuf, after its trailing barrier
+    char *mem = nullptr;   // owned shadow memory (nonblocking / persistent calls)
 };
 
 // A nonblocking collective posted but not launched yet.  Device work must
@@ -582,6 +253,7 @@ struct pending_op {
     hipStream_t stream;
     path_params pp;
     ompi_amd_request *req;
+    shadow_set sh;  // export fallback of this call (sbuf / rbuf above are then the shadows)
 };
 
 }  // namespace ompi_amd
@@ -596,6 +268,7 @@ struct ompi_amd_request {
     bool launched = false;  // its kernels are on `stream`
     bool recorded = false;  // `ev` recorded after them (lazily, at the first test / wait)
     int rc = OMPI_AMD_SUCCESS;
+    char *shadow = nullptr;  // export-fallback memory of the call, freed with the request
 };
 
 // ------------------------------------------------------------------ comm
@@ -612,8 +285,18 @@ struct ompi_amd_comm {
     size_t land_bytes = 0;                //   allreduce, large scan/exscan)
     ptr_set peer_land{};
     void *land_opened[kMaxRanks] = {};
-    std::vector<void *> land_rejected;  // aliased landing candidates, freed at destroy
-    int land_alias_retries = 0;
+    int stale_closed = 0;                 // cached peer mappings closed because the peer freed them
+    int stale_same_handle = 0;            //   ... of which the new allocation had the same handle bytes
+    // streams this communicator launched work on: the current one, plus an
+    // event recorded on each earlier one when the calls moved away from it
+    // (quiesce() waits for exactly that work, not for the whole device)
+    bool has_stream = false;
+    hipStream_t cur_stream = nullptr;
+    std::vector<hipEvent_t> stream_evs;
+    char *shadow = nullptr;               // export fallback of blocking calls (shadow_set)
+    size_t shadow_bytes = 0;
+    int shadowed = 0;                     // zero-copy calls that needed it
+    int force_shadow = 0;                 // param "force_shadow": take the fallback always (tests)
     int *err_host = nullptr, *err_dev = nullptr;
     uint64_t epoch = 0;
     // params
@@ -625,7 +308,14 @@ struct ompi_amd_comm {
     int algorithm = 0;
     // IPC caches
     struct exp_entry { void *base; size_t size; unsigned long long id; hipIpcMemHandle_t h; };
-    struct imp_entry { int peer; hipIpcMemHandle_t h; void *base; uint64_t last_use; int pins; };
+    struct imp_entry {
+        int peer;
+        hipIpcMemHandle_t h;
+        uint64_t id, rbase, rsize;  // the allocation in the exporter (buf_desc)
+        void *base;                 // its mapping here
+        uint64_t last_use;
+        int pins;
+    };
     std::vector<exp_entry> exports;
     std::vector<imp_entry> imports;
     uint64_t use_clock = 0;
@@ -660,6 +350,7 @@ struct ompi_amd_plan {
     hipEvent_t done = nullptr;
     hipStream_t stream = nullptr;
     bool started = false, recorded = false;
+    shadow_set sh;  // export fallback (src / rbuf above are then the shadows)
 };
 
 namespace ompi_amd {
@@ -675,8 +366,11 @@ static int set_dev(ompi_amd_comm_t *c) {
     return record_hip(hipSetDevice(c->device), "hipSetDevice");
 }
 
-static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d) {
+// ipc_failed: set when the runtime refused to export a live device
+// allocation (the shadow fallback applies); other failures are errors.
+static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d, bool *ipc_failed = nullptr) {
     memset(d, 0, sizeof(*d));
+    if (ipc_failed) *ipc_failed = false;
     if (!ptr) return OMPI_AMD_SUCCESS;
     void *base = nullptr;
     size_t size = 0;
@@ -688,6 +382,9 @@ static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d) {
         (void)hipGetLastError();
         id = 0;
     }
+    d->id = id;
+    d->base = (uint64_t)(uintptr_t)base;
+    d->size = (uint64_t)size;
     for (auto &x : c->exports) {
         if (x.base == base && x.size == size && x.id == id) {
             d->h = x.h;
@@ -698,7 +395,21 @@ static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d) {
     }
     ompi_amd_comm::exp_entry x{base, size, id, {}};
     e = hipIpcGetMemHandle(&x.h, base);
-    if (e != hipSuccess) return record_hip(e, "hipIpcGetMemHandle");
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        hipPointerAttribute_t at{};
+        const hipError_t ea = hipPointerGetAttributes(&at, ptr);
+        (void)hipGetLastError();
+        const void *imp = nullptr;  // one of this rank's peer mappings overlapping the range?
+        for (auto &m : c->imports)
+            if ((char *)m.base < (char *)base + size && (char *)base < (char *)m.base + m.rsize) imp = m.base;
+        record_msg("hipIpcGetMemHandle: %s (ptr %p in allocation %p + %zu, buffer id %llu, "
+                   "attr rc %d type %d device %d, overlapping peer mapping %p, land %p)",
+                   hipGetErrorString(e), ptr, base, size, (unsigned long long)id, (int)ea,
+                   (int)at.type, at.device, imp, (void *)c->land);
+        if (ipc_failed) *ipc_failed = true;
+        return OMPI_AMD_ERR_HIP;
+    }
     // drop stale entries that overlap this allocation
     c->exports.erase(std::remove_if(c->exports.begin(), c->exports.end(),
                                     [&](const ompi_amd_comm::exp_entry &o) {
@@ -715,13 +426,44 @@ static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d) {
 
 // pin: the mapping is held by a persistent plan and never evicted until
 // the plan releases it (unpin_import with the returned *base).
+// Close every cached mapping of `peer` that cannot be the allocation `d`
+// describes but would collide with it: the same handle bytes or an
+// overlapping exporter range under another buffer id.  The peer has freed
+// those allocations (its live allocations never overlap), and a mapping
+// kept open holds the freed memory alive — opening the new handle next to it
+// is how a stale alias could be handed back, and serving it from the cache
+// would certainly be one.  A pinned mapping (a persistent plan's) of a freed
+// buffer is a program error: report it instead of unmapping under the plan.
+static int drop_stale_imports(ompi_amd_comm_t *c, int peer, const buf_desc &d) {
+    const uint64_t lo = d.base, hi = d.base + d.size;
+    for (auto it = c->imports.begin(); it != c->imports.end();) {
+        const bool same_handle = memcmp(&it->h, &d.h, sizeof(d.h)) == 0;
+        const bool overlap = it->rbase < hi && lo < it->rbase + it->rsize;
+        if (it->peer != peer || it->id == d.id || !(same_handle || overlap)) {
+            ++it;
+            continue;
+        }
+        if (it->pins > 0) {
+            record_msg("rank %d freed a buffer (id %llu) that a persistent collective still maps",
+                       peer, (unsigned long long)it->id);
+            return OMPI_AMD_ERR_BAD_PARAM;
+        }
+        const hipError_t e = hipIpcCloseMemHandle(it->base);
+        if (e != hipSuccess) return record_hip(e, "hipIpcCloseMemHandle (stale peer mapping)");
+        ++c->stale_closed;
+        c->stale_same_handle += same_handle ? 1 : 0;
+        it = c->imports.erase(it);
+    }
+    return OMPI_AMD_SUCCESS;
+}
+
 static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const char **out,
                       bool pin = false, void **base_out = nullptr) {
     *out = nullptr;
     if (base_out) *base_out = nullptr;
     if (!d.valid) return OMPI_AMD_SUCCESS;
     for (auto &x : c->imports) {
-        if (x.peer == peer && memcmp(&x.h, &d.h, sizeof(d.h)) == 0) {
+        if (x.peer == peer && x.id == d.id && memcmp(&x.h, &d.h, sizeof(d.h)) == 0) {
             x.last_use = ++c->use_clock;
             x.pins += pin ? 1 : 0;
             *out = (const char *)x.base + d.off;
@@ -729,6 +471,7 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
             return OMPI_AMD_SUCCESS;
         }
     }
+    TRY(drop_stale_imports(c, peer, d));
     if (c->imports.size() >= 256) {  // evict the least recently used unpinned mapping
         auto it = c->imports.end();
         for (auto jt = c->imports.begin(); jt != c->imports.end(); ++jt)
@@ -741,7 +484,7 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
     void *base = nullptr;
     hipError_t e = hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess);
     if (e != hipSuccess) return record_hip(e, "hipIpcOpenMemHandle");
-    c->imports.push_back({peer, d.h, base, ++c->use_clock, pin ? 1 : 0});
+    c->imports.push_back({peer, d.h, d.id, d.base, d.size, base, ++c->use_clock, pin ? 1 : 0});
     *out = (const char *)base + d.off;
     if (base_out) *base_out = base;
     return OMPI_AMD_SUCCESS;
@@ -790,24 +533,56 @@ static int exchange_bufs(ompi_amd_comm_t *c, const void *sbuf, const void *rbuf,
     return OMPI_AMD_SUCCESS;
 }
 
-static void release_landing(ompi_amd_comm_t *c) {
-    for (int p = 0; p < kMaxRanks; ++p) {
-        if (c->land_opened[p]) (void)hipIpcCloseMemHandle(c->land_opened[p]);
-        c->land_opened[p] = nullptr;
-        c->peer_land.p[p] = nullptr;
+// Work this communicator put on a stream: note the stream; when the calls
+// move to another stream, an event marks the end of the old one's work.
+static void note_stream(ompi_amd_comm_t *c, hipStream_t s) {
+    if (c->has_stream && c->cur_stream == s) return;
+    if (c->has_stream) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) {
+            if (hipEventRecord(e, c->cur_stream) == hipSuccess) c->stream_evs.push_back(e);
+            else (void)hipEventDestroy(e);
+        }
+        // forget marks that have fired
+        for (auto it = c->stream_evs.begin(); c->stream_evs.size() > 8 && it != c->stream_evs.end();) {
+            if (hipEventQuery(*it) == hipSuccess) {
+                (void)hipEventDestroy(*it);
+                it = c->stream_evs.erase(it);
+            } else {
+                ++it;
+            }
+        }
+        (void)hipGetLastError();
     }
-    if (c->land) (void)hipFree(c->land);
-    c->land = nullptr;
-    c->land_bytes = 0;
+    c->cur_stream = s;
+    c->has_stream = true;
+}
+
+// Wait until every kernel this communicator launched has finished (its
+// streams only: an application's unrelated work on the device is not
+// waited for, unlike hipDeviceSynchronize).
+static int quiesce(ompi_amd_comm_t *c) {
+    for (hipEvent_t e : c->stream_evs) {
+        const hipError_t r = hipEventSynchronize(e);
+        (void)hipEventDestroy(e);
+        if (r != hipSuccess) {
+            c->stream_evs.clear();
+            return record_hip(r, "hipEventSynchronize (communicator streams)");
+        }
+    }
+    c->stream_evs.clear();
+    if (c->has_stream)
+        TRY(record_hip(hipStreamSynchronize(c->cur_stream), "hipStreamSynchronize (communicator stream)"));
+    return OMPI_AMD_SUCCESS;
 }
 
 // Collective: every rank reaches it in the same call with the same `need`.
 // Growing waits for all earlier work of every rank (no kernel may still
-// touch the old buffers), then swaps handles of the new one.  The new buffer
-// is allocated (and exported) while the old one is still alive, so it never
-// reuses the old one's address range: on ROCm 7.2 an IPC export of a fresh
-// allocation at a just-freed range failed with hipErrorInvalidValue (seen
-// at 4 ranks, third growth).  Sizes grow geometrically, in 32 MiB steps.
+// touch the old buffers), then swaps descriptors of the new one.  The new
+// buffer is allocated (and exported) while the old one is still alive, so it
+// never reuses the old one's address range: on ROCm 7.2 an IPC export of a
+// fresh allocation at a just-freed range failed with hipErrorInvalidValue
+// (seen at 4 ranks, third growth).  Sizes grow geometrically, in 32 MiB steps.
 static hipError_t alloc_exportable(size_t bytes, char **out, hipIpcMemHandle_t *h) {
     std::vector<void *> failed;
     hipError_t e = hipErrorInvalidValue;
@@ -837,103 +612,112 @@ static uint64_t landing_token(int rank) {
     return x | 1;
 }
 
+// The landing buffers travel as full descriptors (handle + buffer id +
+// exporter range), and before a peer's new landing buffer is mapped every
+// cached mapping of that peer's freed allocations that it could collide
+// with is closed (drop_stale_imports).  Two 8-process runs of round 1 read
+// stale landing data after a growth while such mappings — user buffers the
+// peers had since freed — were still open in the import cache, keyed by
+// handle bytes only; that state no longer exists.  The token the owner
+// stamps into its buffer is still read back through every new mapping, as
+// an assertion: a mismatch fails the call on every rank with the peer and
+// both tokens named (no retry).
 static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     if (need <= c->land_bytes) return OMPI_AMD_SUCCESS;
     constexpr size_t kStep = 32u << 20, kTag = 64;  // the last kTag bytes hold the token
     const size_t want = std::max((need + kTag + kStep - 1) / kStep * kStep,
                                  c->land_bytes ? 2 * (c->land_bytes + kTag) : 0);
-    int rc = record_hip(hipDeviceSynchronize(), "landing: drain");
-    if (rc == OMPI_AMD_SUCCESS) rc = c->boot.barrier();
-    if (rc != OMPI_AMD_SUCCESS) return rc;
+    TRY(quiesce(c));
+    TRY(c->boot.barrier());  // every rank's earlier kernels are done
     for (int p = 0; p < kMaxRanks; ++p) {
         if (c->land_opened[p]) (void)hipIpcCloseMemHandle(c->land_opened[p]);
         c->land_opened[p] = nullptr;
         c->peer_land.p[p] = nullptr;
     }
-    // Every rank stamps a fresh token into its new buffer and every importer
-    // reads it back through its mapping.  A mapping that shows another token
-    // aliases an older allocation of that peer (seen on ROCm 7.2 when a new
-    // buffer reuses a freed, previously exported address range): then all
-    // ranks retry with new buffers, keeping the rejected ones alive so the
-    // next ranges differ.
-    bool first = true;
-    for (int attempt = 0; attempt < 3; ++attempt) {
-        struct { hipIpcMemHandle_t h; uint64_t token; int ok; } mine{}, all[kMaxRanks];
-        char *fresh = nullptr;
-        hipError_t e = alloc_exportable(want, &fresh, &mine.h);
-        mine.token = landing_token(c->rank);
-        if (e == hipSuccess)
-            e = hipMemcpy(fresh + want - kTag, &mine.token, sizeof(mine.token),
-                          hipMemcpyHostToDevice);
-        mine.ok = e == hipSuccess;
-        if (e != hipSuccess) record_hip(e, "landing buffer");
-        rc = c->boot.allgather(&mine, all, sizeof(mine));  // also: nobody maps the old one now
-        if (rc != OMPI_AMD_SUCCESS) {
-            if (fresh) (void)hipFree(fresh);
-            return rc;
-        }
-        if (first) {
-            if (c->land) (void)hipFree(c->land);
-            c->land = nullptr;
-            c->land_bytes = 0;
-            first = false;
-        }
-        bool ok = true, alias = false;
-        for (int p = 0; p < c->size; ++p) ok = ok && all[p].ok;
-        for (int p = 0; ok && p < c->size; ++p) {
-            if (p == c->rank) continue;
-            void *m = nullptr;
-            e = hipIpcOpenMemHandle(&m, all[p].h, hipIpcMemLazyEnablePeerAccess);
-            if (e != hipSuccess) {
-                record_hip(e, "hipIpcOpenMemHandle (landing)");
-                ok = false;
-                break;
-            }
-            c->land_opened[p] = m;
-            uint64_t seen = 0;
-            e = hipMemcpy(&seen, (char *)m + want - kTag, sizeof(seen), hipMemcpyDeviceToHost);
-            if (e != hipSuccess || seen != all[p].token) {
-                if (e != hipSuccess) record_hip(e, "landing token read");
-                else record_msg("landing buffer of rank %d: the IPC mapping aliases an older "
-                               "allocation (token %016llx, expected %016llx)", p,
-                               (unsigned long long)seen, (unsigned long long)all[p].token);
-                ok = false;
-                alias = e == hipSuccess;
-                break;
-            }
-        }
-        int oks[kMaxRanks], flags = (ok ? 1 : 0) | (alias ? 2 : 0);
-        rc = c->boot.allgather(&flags, oks, sizeof(int));
-        if (rc != OMPI_AMD_SUCCESS) return rc;
-        bool all_ok = true, any_alias = false;
-        for (int p = 0; p < c->size; ++p) {
-            all_ok = all_ok && (oks[p] & 1);
-            any_alias = any_alias || (oks[p] & 2);
-        }
-        if (all_ok) {
-            c->land = fresh;
-            for (int p = 0; p < c->size; ++p)
-                c->peer_land.p[p] = p == c->rank ? c->land : (const char *)c->land_opened[p];
-            c->land_bytes = want - kTag;
-            return OMPI_AMD_SUCCESS;
-        }
-        (void)c->boot.barrier();  // nobody reads the rejected buffers any more
-        for (int p = 0; p < kMaxRanks; ++p) {
-            if (c->land_opened[p]) (void)hipIpcCloseMemHandle(c->land_opened[p]);
-            c->land_opened[p] = nullptr;
-        }
-        if (!any_alias) {
-            if (fresh) (void)hipFree(fresh);
-            return OMPI_AMD_ERR_HIP;
-        }
-        if (fresh) c->land_rejected.push_back(fresh);
-        ++c->land_alias_retries;
-        if (alias) fprintf(stderr, "ompi_amd[%d]: %s; retrying\n", c->rank, ompi_amd_last_error());
+    struct land_blob { buf_desc d; uint64_t token; int ok; };
+    land_blob mine{}, all[kMaxRanks];
+    char *fresh = nullptr;
+    hipError_t e = alloc_exportable(want, &fresh, &mine.d.h);
+    mine.token = landing_token(c->rank);
+    if (e == hipSuccess) {
+        unsigned long long id = 0;
+        e = hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)fresh);
+        mine.d.id = id;
+        mine.d.base = (uint64_t)(uintptr_t)fresh;
+        mine.d.size = want;
+        mine.d.valid = 1;
+        if (e != hipSuccess) record_hip(e, "hipPointerGetAttribute (landing buffer id)");
+    } else {
+        record_hip(e, "landing buffer: hipMalloc / hipIpcGetMemHandle");
     }
-    return OMPI_AMD_ERR_HIP;
+    if (e == hipSuccess)
+        e = hipMemcpy(fresh + want - kTag, &mine.token, sizeof(mine.token), hipMemcpyHostToDevice);
+    if (e != hipSuccess && mine.d.valid) record_hip(e, "landing token write");
+    mine.ok = e == hipSuccess;
+    int rc = c->boot.allgather(&mine, all, sizeof(mine));  // also: nobody maps the old one now
+    if (c->land) (void)hipFree(c->land);
+    c->land = nullptr;
+    c->land_bytes = 0;
+    if (rc != OMPI_AMD_SUCCESS) {
+        if (fresh) (void)hipFree(fresh);
+        return rc;
+    }
+    int status = mine.ok ? 0 : 1;  // 0 ok, 1 local HIP failure, 2 token mismatch
+    for (int p = 0; p < c->size && status == 0; ++p) {
+        if (p == c->rank) continue;
+        if (!all[p].ok) {
+            record_msg("landing buffer: rank %d failed to allocate or export its buffer", p);
+            status = 1;
+            break;
+        }
+        rc = drop_stale_imports(c, p, all[p].d);
+        if (rc != OMPI_AMD_SUCCESS) { status = 1; break; }
+        void *m = nullptr;
+        e = hipIpcOpenMemHandle(&m, all[p].d.h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+            record_hip(e, "hipIpcOpenMemHandle (landing)");
+            status = 1;
+            break;
+        }
+        c->land_opened[p] = m;
+        uint64_t seen = 0;
+        e = hipMemcpy(&seen, (char *)m + want - kTag, sizeof(seen), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) {
+            record_hip(e, "landing token read");
+            status = 1;
+        } else if (seen != all[p].token) {
+            record_msg("landing buffer of rank %d (id %llu): the IPC mapping shows token %016llx, "
+                       "expected %016llx (it aliases another allocation)", p,
+                       (unsigned long long)all[p].d.id, (unsigned long long)seen,
+                       (unsigned long long)all[p].token);
+            status = 2;
+        }
+    }
+    int st[kMaxRanks];
+    rc = c->boot.allgather(&status, st, sizeof(int));
+    int worst = 0;
+    for (int p = 0; rc == OMPI_AMD_SUCCESS && p < c->size; ++p) worst = std::max(worst, st[p]);
+    if (rc == OMPI_AMD_SUCCESS && worst == 0) {
+        c->land = fresh;
+        for (int p = 0; p < c->size; ++p)
+            c->peer_land.p[p] = p == c->rank ? c->land : (const char *)c->land_opened[p];
+        c->land_bytes = want - kTag;
+        return OMPI_AMD_SUCCESS;
+    }
+    (void)c->boot.barrier();  // nobody reads the new buffers any more
+    for (int p = 0; p < kMaxRanks; ++p) {
+        if (c->land_opened[p]) (void)hipIpcCloseMemHandle(c->land_opened[p]);
+        c->land_opened[p] = nullptr;
+    }
+    if (fresh) (void)hipFree(fresh);
+    if (rc == OMPI_AMD_SUCCESS && status == 0)
+        record_msg("landing buffer growth failed on another rank (%s)",
+                   worst == 2 ? "stale IPC mapping" : "HIP error");
+    return rc != OMPI_AMD_SUCCESS ? rc : OMPI_AMD_ERR_HIP;
 }
 
 static int launch_barrier(ompi_amd_comm_t *c, hipStream_t s) {
+    note_stream(c, s);
     ++c->epoch;
     const uint64_t ticks = (uint64_t)c->timeout_ms * 100000ull;  // s_memrealtime: 100 MHz
     hipLaunchKernelGGL(barrier_kernel, dim3(1), dim3(64), 0, s, c->flags, c->peer_flags, c->rank,
@@ -943,6 +727,7 @@ static int launch_barrier(ompi_amd_comm_t *c, hipStream_t s) {
 
 static int launch_copy(ompi_amd_comm_t *c, const cp_jobs &jobs, hipStream_t s) {
     if (jobs.n == 0) return OMPI_AMD_SUCCESS;
+    note_stream(c, s);
     int64_t most = 0;
     for (int i = 0; i < jobs.n; ++i) most = std::max(most, jobs.j[i].bytes);
     int64_t blocks = (most / 16 + kXferThreads * 4 - 1) / (kXferThreads * 4);
@@ -950,6 +735,96 @@ static int launch_copy(ompi_amd_comm_t *c, const cp_jobs &jobs, hipStream_t s) {
     hipLaunchKernelGGL(copy_kernel, dim3((unsigned)blocks, (unsigned)jobs.n), dim3(kXferThreads),
                        0, s, jobs);
     return record_hip(hipGetLastError(), "copy launch");
+}
+
+// ---- export fallback (shadow_set) ----
+static int shadow_reserve(ompi_amd_comm_t *c, size_t need, char **out) {
+    if (need <= c->shadow_bytes) {
+        *out = c->shadow;
+        return OMPI_AMD_SUCCESS;
+    }
+    // the old shadow's last readers are the peers of an earlier call, done
+    // once this rank's stream passed that call's trailing barrier
+    TRY(quiesce(c));
+    if (c->shadow) (void)hipFree(c->shadow);
+    c->shadow = nullptr;
+    c->shadow_bytes = 0;
+    const size_t want = (std::max(need, 2 * c->shadow_bytes) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+    hipIpcMemHandle_t h;
+    const hipError_t e = alloc_exportable(want, &c->shadow, &h);
+    if (e != hipSuccess) return record_hip(e, "shadow buffer: hipMalloc / hipIpcGetMemHandle");
+    c->shadow_bytes = want;
+    *out = c->shadow;
+    return OMPI_AMD_SUCCESS;
+}
+
+// Decide the shadows of one zero-copy call and substitute the pointers:
+// *src (sbytes read by peers) and *rbuf (rbytes read or written by peers;
+// rbuf_in: its content is an input).  src == rbuf is in place (one region).
+// owned: fresh memory for this call (post->mem) instead of the
+// communicator's.  Nothing is enqueued here (shadow_in / shadow_out).
+static int shadow_plan(ompi_amd_comm_t *c, const void **src, size_t sbytes, void **rbuf,
+                       size_t rbytes, bool rbuf_in, bool owned, shadow_set *post) {
+    *post = shadow_set{};
+    const bool inplace = *src && *src == (const void *)*rbuf;
+    bool fs = false, fr = false;
+    buf_desc d;
+    if (*src && sbytes) {
+        const int rc = export_buf(c, *src, &d, &fs);
+        if (rc != OMPI_AMD_SUCCESS && !fs) return rc;
+        fs = fs || c->force_shadow;
+    }
+    if (inplace) {
+        fr = fs;
+        fs = false;
+        rbytes = std::max(rbytes, sbytes);
+        rbuf_in = true;
+    } else if (*rbuf && rbytes) {
+        const int rc = export_buf(c, *rbuf, &d, &fr);
+        if (rc != OMPI_AMD_SUCCESS && !fr) return rc;
+        fr = fr || c->force_shadow;
+    }
+    if (!fs && !fr) return OMPI_AMD_SUCCESS;
+    // each region keeps its user pointer's phase mod 256 (the kernels'
+    // vector paths need the sources' and destinations' 16-B phases to agree)
+    const size_t so = fs ? ((uintptr_t)*src & 255) : 0;
+    const size_t rbase = fs ? ((so + sbytes + 255) & ~(size_t)255) : 0;
+    const size_t ro = fr ? rbase + ((uintptr_t)*rbuf & 255) : rbase;
+    const size_t need = (fr ? ro + rbytes : so + sbytes) + 256;
+    char *mem = nullptr;
+    if (owned) {
+        hipIpcMemHandle_t h;
+        const hipError_t e = alloc_exportable(need, &mem, &h);
+        if (e != hipSuccess) return record_hip(e, "shadow buffer: hipMalloc / hipIpcGetMemHandle");
+        post->mem = mem;
+    } else {
+        TRY(shadow_reserve(c, need, &mem));
+    }
+    if (fs) {
+        post->in.j[post->in.n++] = {(const char *)*src, mem + so, (int64_t)sbytes};
+        *src = mem + so;
+    }
+    if (fr) {
+        char *r = mem + ro;
+        if (rbuf_in) post->in.j[post->in.n++] = {(const char *)*rbuf, r, (int64_t)rbytes};
+        post->out = {r, (char *)*rbuf, (int64_t)rbytes};
+        *rbuf = r;
+        if (inplace) *src = r;
+    }
+    ++c->shadowed;
+    return OMPI_AMD_SUCCESS;
+}
+
+static int shadow_in(ompi_amd_comm_t *c, const shadow_set &sh, hipStream_t s) {
+    return launch_copy(c, sh.in, s);
+}
+
+static int shadow_out(ompi_amd_comm_t *c, const shadow_set &sh, hipStream_t s) {
+    if (sh.out.bytes <= 0) return OMPI_AMD_SUCCESS;
+    cp_jobs cj{};
+    cj.j[0] = sh.out;
+    cj.n = 1;
+    return launch_copy(c, cj, s);
 }
 
 static ptr_set one_ptr(const void *p) {
@@ -970,9 +845,10 @@ static ptr_set push_order(const ompi_amd_comm_t *c, const ptr_set &bufs) {
 static int launch_reduce(ompi_amd_comm_t *c, int op, int type, const ptr_set &src, int nsrc,
                          const ptr_set &dst, int ndst, int order, int flags, red_jobs jobs,
                          hipStream_t s) {
-    red_launch_fn f = g_red[op][type];
+    red_launch_fn f = red_fn(op, type);
     if (!f) return OMPI_AMD_ERR_UNSUPPORTED;
     if (jobs.n == 0 || nsrc < 1) return OMPI_AMD_SUCCESS;
+    note_stream(c, s);
     const size_t ext = ompi_amd_type_extent(type);
     int64_t most = 0;
     for (int i = 0; i < jobs.n; ++i) {
@@ -1031,12 +907,6 @@ static int check_sticky(ompi_amd_comm_t *c) {
     return OMPI_AMD_SUCCESS;
 }
 
-#define TRY(x)                                   \
-    do {                                         \
-        int rc_ = (x);                           \
-        if (rc_ != OMPI_AMD_SUCCESS) return rc_; \
-    } while (0)
-
 static bool in_place(const void *sbuf, const void *rbuf) {
     return sbuf == rbuf || sbuf == (const void *)1;
 }
@@ -1092,8 +962,9 @@ static int stage_in(ompi_amd_comm_t *c, const void *src, size_t bytes, stage_hal
 // ---- small allreduce: one fused launch (flags per workgroup) ----
 static int allreduce_fused(ompi_amd_comm_t *c, const void *src, void *rbuf, int64_t count,
                            int op, int type, bool tree, hipStream_t s) {
-    fused_launch_fn f = g_fused[op][type];
+    fused_launch_fn f = fused_fn(op, type);
     if (!f) return OMPI_AMD_ERR_UNSUPPORTED;
+    note_stream(c, s);
     const int n = c->size;
     const stage_half sh = next_half(c);
     fused_args a{};
@@ -1262,6 +1133,10 @@ static int reduce_my_block(ompi_amd_comm_t *c, const void *src, void *rbuf, size
     }
     ptr_set sp{}, rp{};
     uint64_t fl[kMaxRanks] = {};
+    void *none = nullptr;
+    shadow_set sh;  // peers only read src; this rank's result stays local
+    TRY(shadow_plan(c, &src, total_bytes, &none, 0, false, false, &sh));
+    TRY(shadow_in(c, sh, s));
     TRY(exchange_bufs(c, src, nullptr, &sp, &rp, inplace ? 1 : 0, fl));
     bool any_inplace = false;
     for (int p = 0; p < n; ++p) any_inplace = any_inplace || (fl[p] & 1);
@@ -1340,8 +1215,9 @@ static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size
 // Launch deferred nonblocking calls in posting order, each once every rank
 // has posted its handle-swap half; block = wait for them (the blocking entry
 // points do, so their device work follows the deferred calls' on every rank).
-static int progress(ompi_amd_comm_t *c, bool block) {
-    while (!c->pending.empty()) {
+// max_launch: stop after launching that many deferred calls (-1: no limit).
+static int progress(ompi_amd_comm_t *c, bool block, int max_launch = -1) {
+    while (!c->pending.empty() && max_launch-- != 0) {
         pending_op o = c->pending.front();
         call_blob all[kMaxRanks];
         int rc = OMPI_AMD_SUCCESS;
@@ -1353,7 +1229,10 @@ static int progress(ompi_amd_comm_t *c, bool block) {
         c->pending.pop_front();
         if (rc == OMPI_AMD_SUCCESS) {
             c->pre = o.ticket ? all : nullptr;
-            rc = allreduce_impl(c, o.sbuf, o.rbuf, o.count, o.type, o.op, o.stream, o.pp);
+            rc = shadow_in(c, o.sh, o.stream);
+            if (rc == OMPI_AMD_SUCCESS)
+                rc = allreduce_impl(c, o.sbuf, o.rbuf, o.count, o.type, o.op, o.stream, o.pp);
+            if (rc == OMPI_AMD_SUCCESS) rc = shadow_out(c, o.sh, o.stream);
             c->pre = nullptr;
         }
         o.req->stream = o.stream;
@@ -1405,16 +1284,37 @@ static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size
                              tree ? ORDER_TREE : ORDER_RING, 0, jobs, s);
     }
     ptr_set sp{}, rp{};
-    if (pp.algorithm == ALG_PUSH) {
+    // export fallback (shadow_plan); a deferred call substituted its
+    // shadows when it was posted, so these export and plan nothing
+    const bool push = pp.algorithm == ALG_PUSH;
+    const void *xs = push ? nullptr : src;
+    void *xr = rbuf;
+    shadow_set sh;
+    if (c->pre) {
+        // deferred: the posted descriptors are final (progress() runs the
+        // call's own shadow copies around it)
+    } else if (push) {
+        TRY(shadow_plan(c, &xs, 0, &xr, bytes, false, false, &sh));
+    } else {
+        TRY(shadow_plan(c, &xs, bytes, &xr, bytes, inplace, false, &sh));
+        src = xs;
+    }
+    rbuf = xr;
+    TRY(shadow_in(c, sh, s));
+    int rc;
+    if (push) {
         TRY(ensure_landing(c, push_slot((int64_t)count, n, type) * (size_t)n));
         TRY(exchange_bufs(c, nullptr, rbuf, &sp, &rp));
-        return allreduce_push(c, src, rp, (int64_t)count, op, type, s);
+        rc = allreduce_push(c, src, rp, (int64_t)count, op, type, s);
+    } else {
+        TRY(exchange_bufs(c, src, rbuf, &sp, &rp));
+        if (inplace) sp = rp;
+        rc = pp.algorithm == ALG_PULL_PUSH
+                 ? allreduce_pull_push(c, sp, rp, (int64_t)count, op, type, s)
+                 : allreduce_pull(c, sp, rp, rbuf, (int64_t)count, op, type, s);
     }
-    TRY(exchange_bufs(c, src, rbuf, &sp, &rp));
-    if (inplace) sp = rp;
-    if (pp.algorithm == ALG_PULL_PUSH)
-        return allreduce_pull_push(c, sp, rp, (int64_t)count, op, type, s);
-    return allreduce_pull(c, sp, rp, rbuf, (int64_t)count, op, type, s);
+    TRY(rc);
+    return shadow_out(c, sh, s);
 }
 
 extern "C" {
@@ -1444,11 +1344,11 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
     // device resources: fine-grained flags, scratch, pinned error word
     c->scratch_bytes = std::max<size_t>(c->small_bytes, 4 << 20);  // per half
     hipError_t e = hipExtMallocWithFlags((void **)&c->flags, 4096, hipDeviceMallocUncached);
-    if (e == hipSuccess) e = hipMemset(c->flags, 0, 4096);
+    if (e == hipSuccess) e = hipMemsetAsync(c->flags, 0, 4096, nullptr);
     if (e == hipSuccess) e = hipMalloc((void **)&c->scratch, 2 * c->scratch_bytes);
     if (e == hipSuccess) e = hipHostMalloc((void **)&c->err_host, 64, hipHostMallocMapped);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&c->err_dev, c->err_host, 0);
-    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);  // the flag page is zero
     if (e != hipSuccess) {
         rc = record_hip(e, "comm device resources");
         ompi_amd_comm_destroy(c);
@@ -1495,7 +1395,7 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     if (!c) return OMPI_AMD_SUCCESS;
     (void)hipSetDevice(c->device);
     (void)drain(c);  // deferred nonblocking calls every peer will also launch
-    (void)hipDeviceSynchronize();
+    (void)quiesce(c);
     (void)c->boot.barrier();  // nobody still reads our memory
     for (auto &x : c->imports) (void)hipIpcCloseMemHandle(x.base);
     for (int p = 0; p < kMaxRanks; ++p) {
@@ -1508,7 +1408,7 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     if (c->flags) (void)hipFree(c->flags);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->land) (void)hipFree(c->land);
-    for (void *p : c->land_rejected) (void)hipFree(p);
+    if (c->shadow) (void)hipFree(c->shadow);
     if (c->err_host) (void)hipHostFree(c->err_host);
     for (int ph = 0; ph < 2; ++ph)
         for (auto &pr : c->ev_phase[ph]) {
@@ -1612,6 +1512,8 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
     } else if (!strcmp(key, "algorithm")) {
         if (v < 0 || v >= ALG_COUNT) return OMPI_AMD_ERR_BAD_PARAM;
         c->algorithm = (int)v;
+    } else if (!strcmp(key, "force_shadow")) {
+        c->force_shadow = v ? 1 : 0;
     } else {
         record_msg("unknown coll param '%s'", key);
         return OMPI_AMD_ERR_BAD_PARAM;
@@ -1629,7 +1531,10 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "fused_bytes")) *v = (int64_t)c->fused_bytes;
     else if (!strcmp(key, "algorithm")) *v = c->algorithm;
     else if (!strcmp(key, "landing_bytes")) *v = (int64_t)c->land_bytes;
-    else if (!strcmp(key, "landing_alias_retries")) *v = c->land_alias_retries;
+    else if (!strcmp(key, "stale_closed")) *v = c->stale_closed;
+    else if (!strcmp(key, "stale_same_handle")) *v = c->stale_same_handle;
+    else if (!strcmp(key, "shadowed")) *v = c->shadowed;
+    else if (!strcmp(key, "force_shadow")) *v = c->force_shadow;
     else if (!strcmp(key, "imports")) *v = (int64_t)c->imports.size();
     else {
         record_msg("unknown coll param '%s'", key);
@@ -1677,12 +1582,31 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
                 if (rc == OMPI_AMD_SUCCESS) rc = ensure_landing(c, need);
             }
         }
+        // this rank's own posted-but-unlaunched tickets occupy ring slots a
+        // new post would overwrite (ShmBoot::kRing): launch the oldest
+        // deferred calls first (blocking on their peers' posts, which those
+        // peers make before this one)
+        while (rc == OMPI_AMD_SUCCESS && c->boot.posted() - c->boot.consumed() >= ShmBoot::kRing - 1)
+            rc = progress(c, true, 1);
+        // export fallback with memory of its own (several calls may be
+        // outstanding): the posted descriptors are the shadows'
+        const size_t bytes = count * ompi_amd_type_extent(type);
+        if (rc == OMPI_AMD_SUCCESS) {
+            const void *xs = push ? nullptr : o.sbuf;
+            void *xr = o.rbuf;
+            rc = push ? shadow_plan(c, &xs, 0, &xr, bytes, false, true, &o.sh)
+                      : shadow_plan(c, &xs, bytes, &xr, bytes, inplace, true, &o.sh);
+            if (!push) o.sbuf = xs;
+            o.rbuf = xr;
+            req->shadow = o.sh.mem;
+        }
         call_blob mine{};
         if (rc == OMPI_AMD_SUCCESS && !push) rc = export_buf(c, o.sbuf, &mine.s);
-        if (rc == OMPI_AMD_SUCCESS) rc = export_buf(c, rbuf, &mine.r);
+        if (rc == OMPI_AMD_SUCCESS) rc = export_buf(c, o.rbuf, &mine.r);
         if (rc == OMPI_AMD_SUCCESS) rc = c->boot.post(&mine, sizeof(mine), &o.ticket);
         if (rc != OMPI_AMD_SUCCESS) {
             (void)hipEventDestroy(req->ev);
+            if (req->shadow) (void)hipFree(req->shadow);
             delete req;
             return rc;
         }
@@ -1730,7 +1654,11 @@ int ompi_amd_reduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t cou
     // zero-copy: every rank folds one block of the vector from every
     // rank's sbuf and stores it straight into the root's rbuf
     ptr_set sp{}, rp{};
-    TRY(exchange_bufs(c, src, c->rank == root ? rbuf : nullptr, &sp, &rp));
+    void *xr = c->rank == root ? rbuf : nullptr;
+    shadow_set sh;  // peers read src and write the root's rbuf
+    TRY(shadow_plan(c, &src, bytes, &xr, c->rank == root ? bytes : 0, root_inplace, false, &sh));
+    TRY(shadow_in(c, sh, s));
+    TRY(exchange_bufs(c, src, xr, &sp, &rp));
     TRY(launch_barrier(c, s));
     int64_t split, early, late;
     blockcount((int64_t)count, n, &split, &early, &late);
@@ -1743,7 +1671,8 @@ int ompi_amd_reduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t cou
     TRY(timed_phase(c, 0, s, [&] {
         return launch_reduce(c, op, type, sp, n, one_ptr(rp.p[root]), 1, ro.order, ro.flags, jobs, s);
     }));
-    return launch_barrier(c, s);
+    TRY(launch_barrier(c, s));
+    return shadow_out(c, sh, s);
 }
 
 int ompi_amd_reduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
@@ -1854,7 +1783,12 @@ int ompi_amd_allgather(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
         return launch_copy(c, cj, s);
     }
     ptr_set sp{}, rp{};
-    TRY(exchange_bufs(c, inplace ? my_slot : sbuf, nullptr, &sp, &rp));
+    const void *mine = inplace ? my_slot : sbuf;
+    void *none = nullptr;
+    shadow_set sh;
+    TRY(shadow_plan(c, &mine, bytes, &none, 0, false, false, &sh));
+    TRY(shadow_in(c, sh, s));
+    TRY(exchange_bufs(c, mine, nullptr, &sp, &rp));
     TRY(launch_barrier(c, s));
     for (int p = 0; p < n; ++p) {
         if (p == c->rank && inplace) continue;
@@ -1889,7 +1823,12 @@ int ompi_amd_bcast(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, void *
         return OMPI_AMD_SUCCESS;
     }
     ptr_set sp{}, rp{};
-    TRY(exchange_bufs(c, c->rank == root ? buf : nullptr, nullptr, &sp, &rp));
+    const void *mine = c->rank == root ? buf : nullptr;
+    void *none = nullptr;
+    shadow_set sh;
+    TRY(shadow_plan(c, &mine, bytes, &none, 0, false, false, &sh));
+    TRY(shadow_in(c, sh, s));
+    TRY(exchange_bufs(c, mine, nullptr, &sp, &rp));
     TRY(launch_barrier(c, s));
     if (c->rank != root) {
         cj.n = 1;
@@ -1924,8 +1863,15 @@ int ompi_amd_allreduce_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, si
     if (!small) {
         pl->kind = c->algorithm == ALG_PUSH ? 3 : c->algorithm == ALG_PULL_PUSH ? 2 : 1;
         if (pl->kind == 3) rc = ensure_landing(c, push_slot(pl->count, n, type) * (size_t)n);
+        if (rc == OMPI_AMD_SUCCESS) {  // export fallback: shadows of the plan's own
+            const void *xs = pl->kind == 3 ? nullptr : pl->src;
+            void *xr = pl->rbuf;
+            rc = shadow_plan(c, &xs, pl->kind == 3 ? 0 : bytes, &xr, bytes, inplace, true, &pl->sh);
+            if (pl->kind != 3) pl->src = xs;
+            pl->rbuf = xr;
+        }
         if (rc == OMPI_AMD_SUCCESS)
-            rc = exchange_bufs(c, pl->kind == 3 ? nullptr : pl->src, rbuf, &pl->sp, &pl->rp, 0,
+            rc = exchange_bufs(c, pl->kind == 3 ? nullptr : pl->src, pl->rbuf, &pl->sp, &pl->rp, 0,
                                nullptr, true, pl->bases);
         if (inplace) pl->sp = pl->rp;
     }
@@ -1947,13 +1893,19 @@ static int plan_enqueue(ompi_amd_plan_t *pl, void *stream) {
     TRY(check_sticky(c));
     TRY(set_dev(c));
     hipStream_t s = as_stream(stream);
+    TRY(shadow_in(c, pl->sh, s));
+    int rc;
     if (pl->kind == 3) {
         // another call may have grown (and so moved) the landing buffer:
         // its size only grows, so the slots still fit
-        return allreduce_push(c, pl->src, pl->rp, pl->count, pl->op, pl->type, s);
+        rc = allreduce_push(c, pl->src, pl->rp, pl->count, pl->op, pl->type, s);
+    } else if (pl->kind == 2) {
+        rc = allreduce_pull_push(c, pl->sp, pl->rp, pl->count, pl->op, pl->type, s);
+    } else {
+        rc = allreduce_pull(c, pl->sp, pl->rp, pl->rbuf, pl->count, pl->op, pl->type, s);
     }
-    if (pl->kind == 2) return allreduce_pull_push(c, pl->sp, pl->rp, pl->count, pl->op, pl->type, s);
-    return allreduce_pull(c, pl->sp, pl->rp, pl->rbuf, pl->count, pl->op, pl->type, s);
+    TRY(rc);
+    return shadow_out(c, pl->sh, s);
 }
 
 int ompi_amd_plan_start(ompi_amd_plan_t *pl, void *stream) {
@@ -2000,6 +1952,10 @@ int ompi_amd_plan_free(ompi_amd_plan_t *pl) {
         for (int p = 0; p < OMPI_AMD_MAX_RANKS; ++p)
             for (int k = 0; k < 2; ++k)
                 if (pl->bases[p][k]) unpin_import(pl->c, pl->bases[p][k]);
+    if (pl->sh.mem) {  // the plan's last start must be over before its shadow goes
+        if (pl->started && pl->done) (void)ompi_amd_plan_wait(pl);
+        (void)hipFree(pl->sh.mem);
+    }
     if (pl->done) (void)hipEventDestroy(pl->done);
     delete pl;
     return OMPI_AMD_SUCCESS;
@@ -2045,6 +2001,8 @@ int ompi_amd_request_free(ompi_amd_request_t *r) {
     // the peers launch it whatever this rank does: launch and finish it too
     const int rc = ompi_amd_request_wait(r);
     if (r->ev) (void)hipEventDestroy(r->ev);
+    // the call's trailing barrier has passed: no peer reads the shadow any more
+    if (r->shadow) (void)hipFree(r->shadow);
     delete r;
     return rc;
 }

@@ -1,0 +1,352 @@
+// Device side of the xGMI collectives (coll_ipc.hip): the shared job and
+// pointer-set types, the memory-ordering helpers, the reduction fold in the
+// reference algorithms' operand orders, and the reduce / fused-allreduce
+// kernel templates.  The kernels are instantiated per op by coll_kern.hip
+// (one object per op, compiled in parallel) and reached through the
+// per-op launch rows declared at the end.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/ompi_amd_coll.h"
+#include "op_device.h"
+
+namespace ompi_amd {
+
+constexpr int kMaxRanks = OMPI_AMD_MAX_RANKS;
+constexpr int kXferThreads = 256;
+
+struct ptr_set { const char *p[kMaxRanks]; };
+struct flag_set { uint64_t *p[kMaxRanks]; };
+
+// Operand orders of the reference's reduction algorithms.  Sources are
+// loaded in virtual-rank order v[j] = x[(first + j) % n].
+enum order_t {
+    ORDER_RING = 0,      // ring / ring_segmented block `first`; linear scan (first 0)
+    ORDER_TREE = 1,      // recursive doubling (first 0)
+    ORDER_CHAIN = 2,     // pipeline chain rooted at `first`; basic_linear = chain at 0, no swap
+    ORDER_BINOMIAL = 3,  // in-order binomial tree rooted at `first`
+    ORDER_BINARY = 4,    // binary tree rooted at `first`
+    ORDER_HALVING = 5,   // recursive-halving reduce_scatter, owner tmp rank in flags >> 8
+};
+// The root passed MPI_IN_PLACE: its first combine is f(own, child)
+// (coll_base_reduce.c:170-171, 196-199).
+constexpr int FOLD_ROOT_INPLACE = 1;
+
+// One reduction job: elements [off, off+cnt) of every source, combined in
+// the call's order and written to dst + off_dst (element units).
+struct red_job {
+    int64_t off, cnt, off_dst;
+    int first;  // virtual rank 0 (ring block b, tree root)
+    int head;   // elements before the 16-B aligned body; -1: no common alignment
+};
+struct red_jobs { red_job j[kMaxRanks]; int n; };
+
+struct cp_job { const char *src; char *dst; int64_t bytes; };
+struct cp_jobs { cp_job j[kMaxRanks]; int n; };
+
+__device__ __forceinline__ void sys_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
+__device__ __forceinline__ void sys_release() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// The workgroup's acquire: lane 0 issues it (it invalidates the CU's L1 and
+// the XCD's L2 for every wave of the CU), the barrier holds the other waves
+// until it completed.  One per workgroup instead of one per wave: in a
+// 1024-workgroup grid the 4 per workgroup cost measurable bandwidth
+// (osc_ipc.hip's grid note).
+__device__ __forceinline__ void acquire_once() {
+    if (threadIdx.x == 0) sys_acquire();
+    __syncthreads();
+}
+
+// Every storing wave drains its stores before the workgroup's single
+// system-scope release (MI355X_MICROARCH.md, inter-workgroup visibility).
+__device__ __forceinline__ void xfer_epilogue() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) sys_release();
+}
+
+// ---------------------------------------------------------------- reduce
+// Fold v[0..n) (virtual-rank order) with the 2-buffer rule f(out, in).  All
+// array indices are compile-time constants after unrolling; n, order and
+// flags are wave-uniform.
+template <typename T, int OP>
+__device__ __forceinline__ T fold(const T (&v)[kMaxRanks], int n, int order, int flags) {
+    using F = opfn<OP, false>;
+    const bool swap = (flags & FOLD_ROOT_INPLACE) != 0;
+    if (order == ORDER_RING) {
+        // v[j] = x[(b + j) % n]; acc = x[b]; acc = f(x[b+j], acc)
+        T acc = v[0];
+#pragma unroll
+        for (int j = 1; j < kMaxRanks; ++j)
+            if (j < n) acc = F::template f<T>(v[j], acc);
+        return acc;
+    }
+    if (order == ORDER_CHAIN) {
+        // chain fanout 1 (coll_base_topo.c:588-600) under the generic reduce
+        // (coll_base_reduce.c:206-215): node k's only child is k+1,
+        // acc_k = f(acc_(k+1), x_k); basic_linear (:680-721) is the same
+        // expression at first = 0.
+        T acc = v[kMaxRanks - 1];
+#pragma unroll
+        for (int j = kMaxRanks - 1; j >= 0; --j) {
+            if (j == n - 1) acc = v[j];
+            else if (j < n - 1) acc = (j == 0 && swap) ? F::template f<T>(v[0], acc)
+                                                       : F::template f<T>(acc, v[j]);
+        }
+        return acc;
+    }
+    if (order == ORDER_BINOMIAL) {
+        // in-order binomial (coll_base_topo.c:402-458): vrank u's children
+        // are u+1, u+2, u+4, ... while the bit is clear; first child:
+        // acc = f(child, own), later ones acc = f(acc, child).
+        T w[kMaxRanks];
+#pragma unroll
+        for (int i = 0; i < kMaxRanks; ++i) w[i] = v[i];
+#pragma unroll
+        for (int u = 0; u + 1 < kMaxRanks; u += 2)
+            if (u + 1 < n) w[u] = (u == 0 && swap) ? F::template f<T>(w[0], w[1])
+                                                   : F::template f<T>(w[u + 1], w[u]);
+#pragma unroll
+        for (int m = 2; m < kMaxRanks; m <<= 1) {
+#pragma unroll
+            for (int u = 0; u + m < kMaxRanks; u += 2 * m)
+                if (u + m < n) w[u] = F::template f<T>(w[u], w[u + m]);
+        }
+        return w[0];
+    }
+    if (order == ORDER_BINARY) {
+        // build_tree(2) (coll_base_topo.c:77-175): shifted rank s has
+        // children s + d and s + 2d, d = largest power of two <= s + 1;
+        // children have larger s, so descending s sees them finished.
+        T w[kMaxRanks];
+#pragma unroll
+        for (int i = 0; i < kMaxRanks; ++i) w[i] = v[i];
+#pragma unroll
+        for (int s = kMaxRanks - 1; s >= 0; --s) {
+            int d = 1;
+            while (2 * d <= s + 1) d *= 2;
+            const int c0 = s + d, c1 = s + 2 * d;
+            if (c0 < kMaxRanks && c0 < n)
+                w[s] = (s == 0 && swap) ? F::template f<T>(w[0], w[c0])
+                                        : F::template f<T>(w[c0], w[s]);
+            if (c1 < kMaxRanks && c1 < n) w[s] = F::template f<T>(w[s], w[c1]);
+        }
+        return w[0];
+    }
+    if (order == ORDER_HALVING) {
+        // recursive-halving reduce_scatter (coll_base_reduce_scatter.c:
+        // 203-345): the 2*remain lowest ranks fold pairwise (odd keeps:
+        // f(odd, even)), then at every mask from the top the rank holding
+        // the owner's half does f(mine, partner's).  tb = the owner's tmp
+        // rank; holders at mask m agree with tb on bit m, and their
+        // partners never do, so the update can run in place.
+        int adj = 1;
+        while (adj * 2 <= n) adj *= 2;
+        const int remain = n - adj;
+        const int tb = (flags >> 8) & 0xff;
+        T w[kMaxRanks];
+#pragma unroll
+        for (int u = 0; u < kMaxRanks; ++u) {
+            if (2 * u + 1 < kMaxRanks && u < remain) w[u] = F::template f<T>(v[2 * u + 1], v[2 * u]);
+            else if (u < adj) w[u] = v[u + remain];
+        }
+#pragma unroll
+        for (int m = kMaxRanks / 2; m >= 1; m >>= 1) {
+            if (m < adj) {
+#pragma unroll
+                for (int u = 0; u < kMaxRanks; ++u)
+                    if (u < adj && (u & m) == (tb & m)) w[u] = F::template f<T>(w[u], w[u ^ m]);
+            }
+        }
+        T r = w[0];
+#pragma unroll
+        for (int u = 1; u < kMaxRanks; ++u)
+            if (u == tb) r = w[u];
+        return r;
+    }
+    // recursive doubling (coll_base_allreduce.c:184-236): fold the
+    // 2*extra lowest ranks pairwise, then a pairwise tree; every combine is
+    // f(out = higher, in = lower).
+    int adj = 1;
+    while (adj * 2 <= n) adj *= 2;
+    const int extra = n - adj;
+    T w[kMaxRanks];
+#pragma unroll
+    for (int i = 0; i < kMaxRanks; ++i) {
+        if (i < extra) w[i] = F::template f<T>(v[2 * i + 1], v[2 * i]);
+        else if (i < adj) w[i] = v[i + extra];
+    }
+#pragma unroll
+    for (int len = kMaxRanks; len > 1; len >>= 1) {
+        if (len <= adj) {
+#pragma unroll
+            for (int i = 0; i < kMaxRanks / 2; ++i)
+                if (2 * i + 1 < len) w[i] = F::template f<T>(w[2 * i + 1], w[2 * i]);
+        }
+    }
+    return w[0];
+}
+
+// Gather v[j] for element index e of the sources in virtual-rank order.
+template <typename T>
+__device__ __forceinline__ void gather_scalar(T (&v)[kMaxRanks], const ptr_set &src, int n,
+                                              int first, int64_t e) {
+#pragma unroll
+    for (int j = 0; j < kMaxRanks; ++j) {
+        if (j < n) {
+            const int r = (first + j) % n;
+            v[j] = reinterpret_cast<const T *>(src.p[r])[e];
+        }
+    }
+}
+
+// n sources (virtual ranks 0..n), result stored to dst.p[0 .. ndst): ndst =
+// 1 is a plain reduce into one buffer; ndst = size is the fused push of the
+// owner's block into every rank's rbuf (the host orders dst local first,
+// then peers rank+1, rank+2, ... so concurrent owners spread their stores
+// over the links).
+template <typename T, int OP>
+__global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, ptr_set dst, int ndst,
+                                                              int n, int order, int flags,
+                                                              red_jobs jobs) {
+    acquire_once();
+    const red_job jb = jobs.j[blockIdx.y];
+    constexpr int E = 16 / sizeof(T);
+    const int64_t gstride = (int64_t)gridDim.x * kXferThreads;
+    const int64_t tid = (int64_t)blockIdx.x * kXferThreads + threadIdx.x;
+    // vector body [head, head + nvec*E): every source and dst 16-B aligned
+    // there (head < 0: no common alignment, all scalar)
+    const int64_t head = jb.head < 0 ? jb.cnt : jb.head;
+    const int64_t nvec = jb.head < 0 ? 0 : (jb.cnt - head) / E;
+    for (int64_t i = tid; i < nvec; i += gstride) {
+        vec16<T> v[kMaxRanks];
+#pragma unroll
+        for (int j = 0; j < kMaxRanks; ++j) {
+            if (j < n) {
+                const int r = (jb.first + j) % n;
+                const u32x4 *p = reinterpret_cast<const u32x4 *>(
+                    reinterpret_cast<const T *>(src.p[r]) + jb.off + head);
+                v[j].v = __builtin_nontemporal_load(p + i);
+            }
+        }
+        vec16<T> out;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            T s[kMaxRanks];
+#pragma unroll
+            for (int j = 0; j < kMaxRanks; ++j) s[j] = v[j].e[e];
+            out.e[e] = fold<T, OP>(s, n, order, flags);
+        }
+#pragma unroll
+        for (int k = 0; k < kMaxRanks; ++k)
+            if (k < ndst)
+                reinterpret_cast<u32x4 *>(reinterpret_cast<T *>(const_cast<char *>(dst.p[k])) +
+                                          jb.off_dst + head)[i] = out.v;
+    }
+    // scalar head [0, head) and tail [head + nvec*E, cnt)
+    const int64_t tail0 = head + nvec * E;
+    const int64_t nscalar = head + (jb.cnt - tail0);
+    for (int64_t k = tid; k < nscalar; k += gstride) {
+        const int64_t e = k < head ? k : tail0 + (k - head);
+        T s[kMaxRanks];
+        gather_scalar<T>(s, src, n, jb.first, jb.off + e);
+        const T r = fold<T, OP>(s, n, order, flags);
+#pragma unroll
+        for (int d = 0; d < kMaxRanks; ++d)
+            if (d < ndst)
+                store_elem<T>(reinterpret_cast<T *>(const_cast<char *>(dst.p[d])) + jb.off_dst + e,
+                              r);
+    }
+    xfer_epilogue();
+}
+
+// ---------------------------------------------------------------- fused small allreduce
+// One launch for small messages (param "fused_bytes"): every workgroup
+// stages its slice of my input in my scratch half, signals the peers on its
+// own flag row, waits for the same slice of every peer and folds it.
+// Workgroup g depends only on the peers' workgroup g (same slice), so there
+// is no grid-wide sync.  Flag slot [g * kMaxRanks + p] of rank r holds the
+// last epoch peer p's workgroup g signalled to r (row 0 doubles as the
+// barrier kernel's row; epochs only grow, so the users never collide).
+constexpr int kFusedMaxGroups = 4096 / (int)sizeof(uint64_t) / kMaxRanks;  // 32 rows
+
+struct fused_args {
+    const char *src;
+    char *dst, *mine;
+    ptr_set peers;
+    uint64_t *flags;
+    flag_set peer_flags;
+    int rank, n, order;
+    int64_t count, split, early, late;
+    uint64_t epoch, timeout_ticks;
+    int *err;
+};
+
+template <typename T, int OP>
+__global__ __launch_bounds__(kXferThreads) void fused_allreduce_kernel(fused_args a) {
+    const int t = threadIdx.x;
+    const int g = blockIdx.y * gridDim.x + blockIdx.x;
+    int64_t off = 0, cnt = a.count;
+    int first = 0;
+    if (a.order == ORDER_RING) {  // grid row y = ring block y
+        const int64_t b = blockIdx.y;
+        off = b < a.split ? b * a.early : b * a.late + a.split;
+        cnt = b < a.split ? a.early : a.late;
+        first = (int)b;
+    }
+    const int64_t per = (cnt + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = off + min(cnt, per * (int64_t)blockIdx.x);
+    const int64_t hi = off + min(cnt, per * (int64_t)(blockIdx.x + 1));
+    const T *src = reinterpret_cast<const T *>(a.src);
+    T *mine = reinterpret_cast<T *>(a.mine);
+    for (int64_t e = lo + t; e < hi; e += kXferThreads) mine[e] = src[e];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) sys_release();
+    __syncthreads();
+    if (t < a.n && t != a.rank) {
+        __hip_atomic_store(a.peer_flags.p[t] + g * kMaxRanks + a.rank, a.epoch, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(a.flags + g * kMaxRanks + t, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM) < a.epoch) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+                __hip_atomic_store(a.err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    acquire_once();
+    T *dst = reinterpret_cast<T *>(a.dst);
+    for (int64_t e = lo + t; e < hi; e += kXferThreads) {
+        T v[kMaxRanks];
+        gather_scalar<T>(v, a.peers, a.n, first, e);
+        store_elem<T>(dst + e, fold<T, OP>(v, a.n, a.order, 0));
+    }
+}
+
+// ---------------------------------------------------------------- launch rows
+using red_launch_fn = hipError_t (*)(dim3, const ptr_set &, const ptr_set &, int, int, int, int,
+                                     const red_jobs &, hipStream_t);
+using fused_launch_fn = hipError_t (*)(dim3, const fused_args &, hipStream_t);
+
+// Row `op` of the launch tables: OMPI_AMD_TYPE_COUNT entries, NULL where
+// op/base has no handler (slot_supported).  Defined by coll_kern.hip built
+// once per op with -DCOLL_OP=<op>.
+#define OMPI_AMD_COLL_OPS(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
+#define OMPI_AMD_COLL_ROW_DECL(k)          \
+    const red_launch_fn *red_row_##k();    \
+    const fused_launch_fn *fused_row_##k();
+OMPI_AMD_COLL_OPS(OMPI_AMD_COLL_ROW_DECL)
+#undef OMPI_AMD_COLL_ROW_DECL
+
+}  // namespace ompi_amd

@@ -12,11 +12,18 @@
 
 namespace ompi_amd {
 
-// A device buffer as peers see it: its allocation's IPC handle + offset.
+// A device buffer as peers see it: its allocation's IPC handle + offset,
+// plus the allocation's identity in the exporter (HIP buffer id, base
+// address, size).  Importers match cached mappings on (peer, handle, id)
+// and close any cached mapping of that peer whose exporter range overlaps
+// a newer allocation (the peer freed it: live allocations never overlap).
 struct ipc_desc {
     hipIpcMemHandle_t h;
     uint64_t off;
     uint64_t valid;
+    uint64_t id;
+    uint64_t base;
+    uint64_t size;
 };
 
 struct p2p_state;  // p2p.cpp
@@ -45,7 +52,9 @@ int comm_sticky(ompi_amd_comm_t *c);
 int comm_copy(ompi_amd_comm_t *c, const void *src, void *dst, size_t bytes, hipStream_t s);
 // osc_ipc.hip: the byte copy of put / get and the p2p receive (persistent
 // grid, one acquire per workgroup; src or dst may be peer memory).
-int xfer_copy(const void *src, void *dst, size_t bytes, hipStream_t s);
+// gate: a CTL_TAKEN_* word that must read 1 for the copy to run (NULL: none).
+int xfer_copy(const void *src, void *dst, size_t bytes, hipStream_t s,
+              const uint32_t *gate = nullptr);
 // Point-to-point mailboxes of the communicator (created with it).
 p2p_state *comm_p2p(ompi_amd_comm_t *c);
 

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <array>
 #include <utility>
 
@@ -213,22 +214,96 @@ static int buffers_kind(const void *a, const void *b, const void *c) {
     return -1;
 }
 
+// Mixed residency: coll/tuned's ring and segmented ring reduce a malloc'd
+// host bounce buffer into the caller's device rbuf
+// (coll_base_allreduce.c:688-693, 782, 811) whenever coll/rocm declined the
+// call (more than OMPI_AMD_MAX_RANKS ranks, a multi-node comm, ranks
+// disagreeing on residency).  The handler has no error channel and must not
+// abort there: every host operand is staged into a per-thread device
+// scratch, the kernel runs on device memory only, and a host output is
+// copied back — all on the thread's stream, complete before returning.
+struct mixed_scratch {
+    char *p = nullptr;
+    size_t cap = 0;
+};
+static thread_local mixed_scratch tls_scratch;  // grown on demand; freed at regrow only
+
+static char *scratch_bytes(size_t bytes) {
+    if (bytes <= tls_scratch.cap) return tls_scratch.p;
+    const size_t want = std::max(bytes, 2 * tls_scratch.cap);
+    if (tls_scratch.p) (void)hipFree(tls_scratch.p);
+    tls_scratch = {};
+    void *q = nullptr;
+    if (hipMalloc(&q, want) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    tls_scratch = {(char *)q, want};
+    return tls_scratch.p;
+}
+
+// 2-buffer (three = false): in1 = in, out = inout (also the second operand).
+static int reduce_mixed(int op, int type, bool three, const void *in1, const void *in2, void *out,
+                        size_t n, hipStream_t s) {
+    const size_t bytes = n * ompi_amd_type_extent(type);
+    const size_t slot = (bytes + 255) & ~(size_t)255;
+    char *scr = scratch_bytes(3 * slot);
+    if (!scr) {
+        record_msg("op handler: no device scratch for %zu B", 3 * slot);
+        return OMPI_AMD_ERR_HIP;
+    }
+    const void *d1 = in1, *d2 = three ? in2 : out;
+    void *dout = out;
+    auto stage = [&](const void *host, char *dev) {
+        return record_hip(hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, s),
+                          "op handler: stage host operand");
+    };
+    int rc = OMPI_AMD_SUCCESS;
+    if (!ompi_amd_is_device_pointer(in1)) {
+        rc = stage(in1, scr);
+        d1 = scr;
+    }
+    if (rc == OMPI_AMD_SUCCESS && three && !ompi_amd_is_device_pointer(in2)) {
+        rc = stage(in2, scr + slot);
+        d2 = scr + slot;
+    }
+    if (rc == OMPI_AMD_SUCCESS && !ompi_amd_is_device_pointer(out)) {
+        dout = scr + 2 * slot;
+        if (!three) {  // inout is an operand too
+            rc = stage(out, (char *)dout);
+            d2 = dout;
+        }
+    }
+    if (rc == OMPI_AMD_SUCCESS)
+        rc = three ? op_launch(op, type, true, d1, d2, dout, n, s)
+                   : op_launch(op, type, false, d2, d1, dout, n, s);
+    if (rc == OMPI_AMD_SUCCESS && dout != out)
+        rc = record_hip(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, s),
+                        "op handler: result to host");
+    if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipStreamSynchronize(s), "op sync");
+    return rc;
+}
+
 template <int OP, int TYPE>
 static void handler2(const void *in, void *inout, int *count, ompi_datatype_t **dtype,
                      ompi_op_base_module_1_0_0_t *module) {
     if (*count <= 0) return;
     const int kind = buffers_kind(in, inout, nullptr);
-    if (kind == 1) {
-        hipStream_t s = thread_stream();
-        int rc = op_launch(OP, TYPE, false, inout, in, inout, (size_t)*count, s);
-        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipStreamSynchronize(s), "op sync");
-        if (rc != OMPI_AMD_SUCCESS) handler_abort("device reduction failed", OP, TYPE);
+    const fallback_slot &fb = g_fallback[OP][TYPE];
+    if (kind == 0) {
+        if (!fb.fn) handler_abort("host buffers and no fallback registered", OP, TYPE);
+        fb.fn(in, inout, count, dtype, fb.module);
         return;
     }
-    const fallback_slot &fb = g_fallback[OP][TYPE];
-    if (kind == 0 && fb.fn) { fb.fn(in, inout, count, dtype, fb.module); return; }
-    handler_abort(kind == 0 ? "host buffers and no fallback registered"
-                            : "mixed host/device buffers", OP, TYPE);
+    hipStream_t s = thread_stream();
+    int rc;
+    if (kind == 1) {
+        rc = op_launch(OP, TYPE, false, inout, in, inout, (size_t)*count, s);
+        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipStreamSynchronize(s), "op sync");
+    } else {
+        rc = reduce_mixed(OP, TYPE, false, in, nullptr, inout, (size_t)*count, s);
+    }
+    if (rc != OMPI_AMD_SUCCESS) handler_abort("device reduction failed", OP, TYPE);
 }
 
 template <int OP, int TYPE>
@@ -236,17 +311,21 @@ static void handler3(const void *in1, const void *in2, void *out, int *count,
                      ompi_datatype_t **dtype, ompi_op_base_module_1_0_0_t *module) {
     if (*count <= 0) return;
     const int kind = buffers_kind(in1, in2, out);
-    if (kind == 1) {
-        hipStream_t s = thread_stream();
-        int rc = op_launch(OP, TYPE, true, in1, in2, out, (size_t)*count, s);
-        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipStreamSynchronize(s), "op sync");
-        if (rc != OMPI_AMD_SUCCESS) handler_abort("device reduction failed", OP, TYPE);
+    const fallback_slot &fb = g_fallback[OP][TYPE];
+    if (kind == 0) {
+        if (!fb.fn3) handler_abort("host buffers and no fallback registered", OP, TYPE);
+        fb.fn3(in1, in2, out, count, dtype, fb.module3);
         return;
     }
-    const fallback_slot &fb = g_fallback[OP][TYPE];
-    if (kind == 0 && fb.fn3) { fb.fn3(in1, in2, out, count, dtype, fb.module3); return; }
-    handler_abort(kind == 0 ? "host buffers and no fallback registered"
-                            : "mixed host/device buffers", OP, TYPE);
+    hipStream_t s = thread_stream();
+    int rc;
+    if (kind == 1) {
+        rc = op_launch(OP, TYPE, true, in1, in2, out, (size_t)*count, s);
+        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipStreamSynchronize(s), "op sync");
+    } else {
+        rc = reduce_mixed(OP, TYPE, true, in1, in2, out, (size_t)*count, s);
+    }
+    if (rc != OMPI_AMD_SUCCESS) handler_abort("device reduction failed", OP, TYPE);
 }
 
 template <int OP, int... T>

@@ -48,6 +48,13 @@ constexpr int kOscMaxRanks = OMPI_AMD_MAX_RANKS;
 
 // control page words (uint32 each)
 enum { CTL_ACC = 0, CTL_COUNTER = 16, CTL_WRITE = 32, CTL_READ = 48, CTL_BYTES = 4096 };
+// Origin-side words of the rank's own control page: whether this rank's
+// last lock kernel toward target t actually holds the lock — 0 no (skipped
+// after a sticky error, or timed out), 1 yes, 2 a ticket was drawn but never
+// granted.  Unlock kernels and the data kernels of the epoch read them, so a
+// lock that was not taken is never released on someone else's behalf and
+// no data moves without it.
+enum { CTL_TAKEN_ACC = 256, CTL_TAKEN_EPOCH = 512 };
 
 __device__ __forceinline__ void osc_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
 __device__ __forceinline__ void osc_release() {
@@ -65,36 +72,60 @@ __device__ __forceinline__ uint32_t ld_sys(uint32_t *p) {
 }
 
 // Poll until *p == want (or the bound passes: sticky error, give up).
-__device__ __forceinline__ void wait_eq(uint32_t *p, uint32_t want, int *err, uint64_t ticks) {
+__device__ __forceinline__ bool wait_eq(uint32_t *p, uint32_t want, int *err, uint64_t ticks) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (ld_sys(p) != want) {
         __builtin_amdgcn_s_sleep(1);
         if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
             __hip_atomic_store(err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
-            return;
+            return false;
         }
     }
+    return true;
+}
+
+__device__ __forceinline__ void st_sys(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// A data kernel of a locked epoch runs only if its lock was taken
+// (gate = the origin's CTL_TAKEN_* word; NULL: no lock involved).
+__device__ __forceinline__ bool gate_open(const uint32_t *gate) {
+    __shared__ uint32_t open;
+    if (threadIdx.x == 0)
+        open = gate ? __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 1u : 1u;
+    __syncthreads();
+    return open != 0;
 }
 
 // kind: 0 accumulate lock, 1 accumulate unlock, 2 start_exclusive,
 // 3 end_exclusive, 4 start_shared, 5 end_shared (osc_sm_passive_target.c:57-110)
+// taken: this rank's CTL_TAKEN_* word for the target (its own control page).
 __global__ __launch_bounds__(64) void lock_kernel(uint32_t *ctl, int kind, int *err,
-                                                  uint64_t ticks) {
+                                                  uint64_t ticks, uint32_t *taken) {
     if (threadIdx.x != 0) return;
     // fail fast: once a lock or barrier of this communicator timed out, the
     // later acquisitions do not wait again (the error is already sticky)
     if ((kind == 0 || kind == 2 || kind == 4) &&
-        __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
+        __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+        st_sys(taken, 0u);
         return;
+    }
+    // a release of a lock this rank does not hold is a no-op (the unlock
+    // would otherwise free another rank's lock)
+    if ((kind == 1 || kind == 3 || kind == 5) && ld_sys(taken) != 1u) return;
     switch (kind) {
     case 0: {  // opal_atomic_lock: spin on a compare-and-swap 0 -> 1
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t got = 0;
         for (;;) {
             uint32_t expect = 0;
             if (__hip_atomic_compare_exchange_strong(ctl + CTL_ACC, &expect, 1u, __ATOMIC_RELAXED,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+                got = 1;
                 break;
+            }
             __builtin_amdgcn_s_sleep(1);
             if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
                 __hip_atomic_store(err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED,
@@ -102,17 +133,21 @@ __global__ __launch_bounds__(64) void lock_kernel(uint32_t *ctl, int kind, int *
                 break;
             }
         }
+        st_sys(taken, got);
         osc_acquire();
         break;
     }
     case 1:
         osc_release();
         __hip_atomic_store(ctl + CTL_ACC, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        st_sys(taken, 0u);
         break;
     case 2: {  // start_exclusive: take a ticket, wait until every earlier holder ended
         const uint32_t me = __hip_atomic_fetch_add(ctl + CTL_COUNTER, 1u, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_SYSTEM);
-        wait_eq(ctl + CTL_WRITE, me, err, ticks);
+        // a ticket drawn but never granted cannot be given back (the holders
+        // after it wait for it); the communicator's error is sticky by then
+        st_sys(taken, wait_eq(ctl + CTL_WRITE, me, err, ticks) ? 1u : 2u);
         osc_acquire();
         break;
     }
@@ -120,18 +155,22 @@ __global__ __launch_bounds__(64) void lock_kernel(uint32_t *ctl, int kind, int *
         osc_release();
         __hip_atomic_fetch_add(ctl + CTL_WRITE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_fetch_add(ctl + CTL_READ, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        st_sys(taken, 0u);
         break;
     case 4: {  // start_shared: wait until every earlier ticket has started (shared) or ended
         const uint32_t me = __hip_atomic_fetch_add(ctl + CTL_COUNTER, 1u, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_SYSTEM);
-        wait_eq(ctl + CTL_READ, me, err, ticks);
-        __hip_atomic_fetch_add(ctl + CTL_READ, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const bool ok = wait_eq(ctl + CTL_READ, me, err, ticks);
+        if (ok)
+            __hip_atomic_fetch_add(ctl + CTL_READ, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        st_sys(taken, ok ? 1u : 2u);
         osc_acquire();
         break;
     }
     case 5:  // end_shared
         osc_release();
         __hip_atomic_fetch_add(ctl + CTL_WRITE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        st_sys(taken, 0u);
         break;
     }
 }
@@ -149,7 +188,9 @@ constexpr int kOscMaxBlocks = 256;  // one per CU: 6.26 TB/s vs 3.40 at 2048 (25
 
 template <typename T, int OP>
 __global__ __launch_bounds__(kOscThreads) void acc_kernel(const T *__restrict__ origin, T *target,
-                                                          int64_t n, int vec) {
+                                                          int64_t n, int vec,
+                                                          const uint32_t *gate) {
+    if (!gate_open(gate)) return;
     // one system-scope acquire per workgroup (it invalidates this CU's L1
     // and the XCD's L2 for every wave of the CU): lane 0, then the barrier
     if (threadIdx.x == 0) osc_acquire();
@@ -201,7 +242,8 @@ __global__ __launch_bounds__(kOscThreads) void acc_kernel(const T *__restrict__ 
 // (4 in flight per lane) when src and dst share their phase mod 16, else 4-B
 // or 1-B granules; one acquire per workgroup, persistent grid (as acc_kernel).
 __global__ __launch_bounds__(kOscThreads) void xfer_kernel(const char *src, char *dst,
-                                                           int64_t bytes) {
+                                                           int64_t bytes, const uint32_t *gate) {
+    if (!gate_open(gate)) return;
     if (threadIdx.x == 0) osc_acquire();
     __syncthreads();
     const uintptr_t phase = (uintptr_t)src ^ (uintptr_t)dst;
@@ -249,8 +291,9 @@ __global__ __launch_bounds__(kOscThreads) void xfer_kernel(const char *src, char
 __global__ __launch_bounds__(64) void cas_kernel(const unsigned char *origin,
                                                  const unsigned char *compare,
                                                  unsigned char *result, unsigned char *target,
-                                                 int size) {
+                                                 int size, const uint32_t *gate) {
     if (threadIdx.x != 0) return;
+    if (ld_sys(const_cast<uint32_t *>(gate)) != 1u) return;
     osc_acquire();
     unsigned char old[16];
     bool same = true;
@@ -264,15 +307,16 @@ __global__ __launch_bounds__(64) void cas_kernel(const unsigned char *origin,
     osc_release();
 }
 
-using acc_launch_fn = hipError_t (*)(dim3, const void *, void *, int64_t, int, hipStream_t);
+using acc_launch_fn = hipError_t (*)(dim3, const void *, void *, int64_t, int, const uint32_t *,
+                                     hipStream_t);
 
 template <int OP, int TYPE>
 static hipError_t acc_launch_slot(dim3 grid, const void *o, void *t, int64_t n, int vec,
-                                  hipStream_t s) {
+                                  const uint32_t *gate, hipStream_t s) {
     if constexpr (slot_supported(OP, TYPE)) {
         using T = typename type_of<TYPE>::type;
         hipLaunchKernelGGL((acc_kernel<T, OP>), grid, dim3(kOscThreads), 0, s,
-                           static_cast<const T *>(o), static_cast<T *>(t), n, vec);
+                           static_cast<const T *>(o), static_cast<T *>(t), n, vec, gate);
         return hipGetLastError();
     } else {
         return hipErrorInvalidValue;
@@ -325,10 +369,24 @@ static uint64_t ticks_of(ompi_amd_win_t *w) {
     return (uint64_t)comm_timeout_ms(w->c) * 100000ull;  // s_memrealtime: 100 MHz
 }
 
+// The origin's CTL_TAKEN_* word for (lock kind, target).
+static uint32_t *taken_word(ompi_amd_win_t *w, int target, bool acc) {
+    return w->ctl + (acc ? CTL_TAKEN_ACC : CTL_TAKEN_EPOCH) + target;
+}
+
+// The gate of a data kernel toward `target` inside a passive-target epoch
+// this rank locked (NULL: fence / NOCHECK / no epoch — nothing to check).
+static const uint32_t *epoch_gate(ompi_amd_win_t *w, int target);
+
 static int launch_lock(ompi_amd_win_t *w, int target, int kind, hipStream_t s) {
     hipLaunchKernelGGL(lock_kernel, dim3(1), dim3(64), 0, s, w->peer_ctl[target], kind,
-                       comm_err_dev(w->c), ticks_of(w));
+                       comm_err_dev(w->c), ticks_of(w), taken_word(w, target, kind <= 1));
     return record_hip(hipGetLastError(), "osc lock launch");
+}
+
+static const uint32_t *epoch_gate(ompi_amd_win_t *w, int target) {
+    const int h = w->held[target];
+    return (h == HELD_EXCLUSIVE || h == HELD_SHARED) ? taken_word(w, target, false) : nullptr;
 }
 
 // Target address of (target, disp) with room for `bytes`.
@@ -353,19 +411,19 @@ static int64_t osc_grid_cap() {
     return cap;
 }
 
-int xfer_copy(const void *src, void *dst, size_t bytes, hipStream_t s) {
+int xfer_copy(const void *src, void *dst, size_t bytes, hipStream_t s, const uint32_t *gate) {
     if (bytes == 0) return OMPI_AMD_SUCCESS;
     const int64_t units = (int64_t)(bytes / 16) + 1;
     const int64_t per = (int64_t)kOscThreads * kOscUnroll;
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((units + per - 1) / per,
                                                                   osc_grid_cap()));
     hipLaunchKernelGGL(xfer_kernel, dim3((unsigned)blocks), dim3(kOscThreads), 0, s,
-                       static_cast<const char *>(src), static_cast<char *>(dst), (int64_t)bytes);
+                       static_cast<const char *>(src), static_cast<char *>(dst), (int64_t)bytes, gate);
     return record_hip(hipGetLastError(), "xfer copy launch");
 }
 
 static int launch_acc(ompi_amd_win_t *w, int op, int type, const void *origin, void *target,
-                      size_t count, hipStream_t s) {
+                      size_t count, const uint32_t *gate, hipStream_t s) {
     acc_launch_fn f = (op >= 0 && op < OMPI_AMD_OP_COUNT && type >= 0 && type < OMPI_AMD_TYPE_COUNT)
                           ? g_acc[op][type]
                           : nullptr;
@@ -379,7 +437,7 @@ static int launch_acc(ompi_amd_win_t *w, int op, int type, const void *origin, v
     const int64_t units = vec ? (int64_t)(count * ext / 16) : (int64_t)count;
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((units + per - 1) / per,
                                                                   osc_grid_cap()));
-    return record_hip(f(dim3((unsigned)blocks), origin, target, (int64_t)count, vec, s),
+    return record_hip(f(dim3((unsigned)blocks), origin, target, (int64_t)count, vec, gate, s),
                       "osc accumulate launch");
 }
 
@@ -408,11 +466,12 @@ static int rma_op(ompi_amd_win_t *w, const void *origin, void *result, size_t co
     hipStream_t s = as_stream(stream);
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
     OSC_TRY(launch_lock(w, target, 0, s));
+    const uint32_t *gate = taken_word(w, target, true);
     int rc = OMPI_AMD_SUCCESS;
-    if (result) rc = xfer_copy(t, result, bytes, s);
+    if (result) rc = xfer_copy(t, result, bytes, s, gate);
     if (rc == OMPI_AMD_SUCCESS) {
-        if (op == OMPI_AMD_OP_REPLACE) rc = xfer_copy(origin, t, bytes, s);
-        else if (op != OMPI_AMD_OP_NO_OP) rc = launch_acc(w, op, type, origin, t, count, s);
+        if (op == OMPI_AMD_OP_REPLACE) rc = xfer_copy(origin, t, bytes, s, gate);
+        else if (op != OMPI_AMD_OP_NO_OP) rc = launch_acc(w, op, type, origin, t, count, gate, s);
     }
     const int urc = launch_lock(w, target, 1, s);  // always release
     return rc != OMPI_AMD_SUCCESS ? rc : urc;
@@ -625,7 +684,7 @@ int ompi_amd_put(ompi_amd_win_t *w, const void *origin, size_t bytes, int target
     OSC_TRY(target_ptr(w, target, disp, bytes, &t));
     if (!bytes) return OMPI_AMD_SUCCESS;
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
-    return xfer_copy(origin, t, bytes, as_stream(stream));
+    return xfer_copy(origin, t, bytes, as_stream(stream), epoch_gate(w, target));
 }
 
 int ompi_amd_get(ompi_amd_win_t *w, void *origin, size_t bytes, int target, size_t disp,
@@ -635,7 +694,7 @@ int ompi_amd_get(ompi_amd_win_t *w, void *origin, size_t bytes, int target, size
     OSC_TRY(target_ptr(w, target, disp, bytes, &t));
     if (!bytes) return OMPI_AMD_SUCCESS;
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
-    return xfer_copy(t, origin, bytes, as_stream(stream));
+    return xfer_copy(t, origin, bytes, as_stream(stream), epoch_gate(w, target));
 }
 
 int ompi_amd_accumulate(ompi_amd_win_t *w, const void *origin, size_t count, int type, int target,
@@ -672,7 +731,7 @@ int ompi_amd_compare_and_swap(ompi_amd_win_t *w, const void *origin, const void 
                        static_cast<const unsigned char *>(origin),
                        static_cast<const unsigned char *>(compare),
                        static_cast<unsigned char *>(result), reinterpret_cast<unsigned char *>(t),
-                       (int)size);
+                       (int)size, (const uint32_t *)taken_word(w, target, true));
     const int rc = record_hip(hipGetLastError(), "osc compare_and_swap launch");
     const int urc = launch_lock(w, target, 1, s);
     return rc != OMPI_AMD_SUCCESS ? rc : urc;

@@ -315,6 +315,25 @@ static int wait_one(ompi_amd_p2p_request *r) {
     }
 }
 
+// A receive that never matched is taken out of the match list (cancel
+// semantics, after a timeout or at free): a message that arrives later must
+// not be copied into a buffer whose MPI_Recv already returned.  Matched
+// receives (the copy is on the stream) and sends cannot be withdrawn.
+static bool cancel_recv(ompi_amd_p2p_request *r) {
+    p2p_state *p = r->p;
+    std::lock_guard<std::recursive_mutex> g(p->mu);
+    progress(p);  // a message that did arrive by now is still taken
+    if (r->is_send || r->matched || r->done) return false;
+    for (auto it = p->recvs.begin(); it != p->recvs.end(); ++it)
+        if (*it == r) {
+            p->recvs.erase(it);
+            break;
+        }
+    r->done = true;
+    r->rc = r->st.error = OMPI_AMD_ERR_TIMEOUT;
+    return true;
+}
+
 static void fill_status(const ompi_amd_p2p_request *r, ompi_amd_status_t *st) {
     if (!st) return;
     if (r->is_send) {
@@ -447,8 +466,11 @@ int ompi_amd_p2p_wait(ompi_amd_p2p_request_t *r, ompi_amd_status_t *st) {
 int ompi_amd_p2p_free(ompi_amd_p2p_request_t *r) {
     if (!r) return OMPI_AMD_SUCCESS;
     int rc = OMPI_AMD_SUCCESS;
-    if (!r->done) rc = wait_one(r);
-    if (!r->done) return rc;  // still referenced by the mailbox: keep it
+    if (!r->done) {
+        rc = wait_one(r);
+        if (!r->done) cancel_recv(r);
+    }
+    if (!r->done) return rc;  // a matched copy or a send the mailbox still references: keep it
     if (r->ev) (void)hipEventDestroy(r->ev);
     delete r;
     return rc;
@@ -468,6 +490,7 @@ int ompi_amd_recv(ompi_amd_comm_t *c, void *buf, size_t bytes, int src, int tag,
     int rc = ompi_amd_irecv(c, buf, bytes, src, tag, stream, &r);
     if (rc != OMPI_AMD_SUCCESS) return rc;
     rc = wait_one(r);
+    if (rc != OMPI_AMD_SUCCESS && !r->done) cancel_recv(r);  // one timeout, not two
     fill_status(r, st);
     const int frc = ompi_amd_p2p_free(r);
     return rc != OMPI_AMD_SUCCESS ? rc : frc;
@@ -485,6 +508,7 @@ int ompi_amd_sendrecv(ompi_amd_comm_t *c, const void *sbuf, size_t sbytes, int d
         return rc;
     }
     const int rrc = wait_one(rr);
+    if (rrc != OMPI_AMD_SUCCESS && !rr->done) cancel_recv(rr);
     fill_status(rr, st);
     const int src_ = wait_one(sr);
     (void)ompi_amd_p2p_free(rr);

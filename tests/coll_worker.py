@@ -193,10 +193,35 @@ def case_regrow(comm, rank, n, salt):
                           salt + 10 + i, inplace=True)
         if not ok:
             fails.append(f"rs {count}: {msg}")
-    if comm.get_param("landing_alias_retries"):  # informational: the guard fired and recovered
-        print(f"rank {rank}: landing alias retries {comm.get_param('landing_alias_retries')}",
-              file=sys.stderr)
     return not fails, "; ".join(fails)
+
+
+def case_free_realloc(comm, rank, n, count, salt):
+    """Zero-copy allreduce, then every rank frees its buffers (the caching
+    allocator returns the segments: hipFree) and allocates new ones of the
+    same size — normally at the freed addresses — and the allreduce runs
+    again on new data; three rounds, every result checked.  A peer mapping
+    cached from the freed allocation must never serve the new one
+    (common_cuda.c:1008-1150 is the reference's handle
+    contract)."""
+    F = mop.MPI_FLOAT
+    msgs = []
+    for it in range(3):
+        xs = [inputs(F, count, r, salt + it) for r in range(n)]
+        exp, _ = orc.allreduce([x.copy() for x in xs], count, mop.MPI_SUM.index, F.code)
+        s = to_dev(xs[rank])
+        out = torch.zeros_like(s)
+        comm.allreduce(s, out, count, F, mop.MPI_SUM, blocking=True)
+        got = out.cpu().numpy()[:count * F.extent].view(F.np_dtype)
+        if not fields_equal(got, exp[rank]):
+            msgs.append(f"round {it}: {mismatch(got, exp[rank])}")
+        del s, out
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        dist.barrier()  # every rank freed before anyone allocates again
+    msgs.append(f"stale mappings closed so far: {comm.get_param('stale_closed')}, "
+                f"same handle bytes: {comm.get_param('stale_same_handle')}")
+    return len(msgs) == 1, "; ".join(msgs)
 
 
 def case_persistent(comm, rank, n, dt, op, count, salt, inplace=False, starts=3):
@@ -273,6 +298,68 @@ def case_iallreduce(comm, rank, n, salt, check_nonblocking=True):
         if not ok:
             msgs.append(f"call {i}: {msg}")
     return not msgs, "; ".join(msgs)
+
+
+def case_iallreduce_many(comm, rank, n, salt, calls=12):
+    """More zero-copy MPI_Iallreduce calls outstanding than the handle-swap
+    ring holds (ShmBoot::kRing = 8) while the peers still sleep: the posts
+    launch their oldest deferred calls instead of waiting on their own
+    unconsumed tickets, and every result is right."""
+    import time
+    F = mop.MPI_FLOAT
+    cnt = 300007  # 1.2 MB: above small_bytes, so every call swaps handles
+    prepared = []
+    for i in range(calls):
+        xs = [inputs(F, cnt, r, salt + i) for r in range(n)]
+        exp, _ = orc.allreduce([x.copy() for x in xs], cnt, mop.MPI_SUM.index, F.code)
+        s = to_dev(xs[rank])
+        prepared.append((s, torch.zeros_like(s), exp[rank]))
+    torch.cuda.synchronize()
+    dist.barrier()
+    if rank != 0:
+        time.sleep(0.5)
+    reqs = [comm.iallreduce(s, out, cnt, F, mop.MPI_SUM) for s, out, _ in prepared]
+    for r in reqs:
+        r.wait()
+    torch.cuda.synchronize()
+    for r in reqs:
+        r.free()
+    msgs = []
+    for i, (s, out, exp) in enumerate(prepared):
+        ok, msg = checked(out.cpu().numpy()[:cnt * 4].view(np.float32), exp)
+        if not ok:
+            msgs.append(f"call {i}: {msg}")
+    return not msgs, "; ".join(msgs)
+
+
+def headline_input(rank: int, count: int, salt: int) -> np.ndarray:
+    """Dataset E at full size without materialising every rank's vector:
+    x_r[i] = (((i * 2654435761 + r * 40503 + salt) mod 2049) - 1024) * 2^-8,
+    so sums over any order are exact in fp32 and the expected sum is
+    computed rank by rank in int32."""
+    i = np.arange(count, dtype=np.int64)
+    return ((i * 2654435761 + rank * 40503 + salt) % 2049 - 1024).astype(np.int32)
+
+
+def case_headline(comm, rank, n, count, salt, algorithm):
+    """BASELINE's headline point (256 MiB fp32 SUM allreduce) at full size,
+    every element checked exactly (dataset E: exact in any order; the ring
+    operand order itself is checked bit-exact on dataset R at the other
+    sizes)."""
+    F = mop.MPI_FLOAT
+    s = torch.from_numpy(headline_input(rank, count, salt).astype(np.float32) * np.float32(2 ** -8)).cuda()
+    out = torch.empty_like(s)
+    comm.set_param("algorithm", algorithm)
+    try:
+        comm.allreduce(s, out, count, F, mop.MPI_SUM, blocking=True)
+    finally:
+        comm.set_param("algorithm", 0)
+    exp = np.zeros(count, dtype=np.int32)
+    for r in range(n):
+        exp += headline_input(r, count, salt)
+    got = out.cpu().numpy()
+    ok = np.array_equal(got, exp.astype(np.float32) * np.float32(2 ** -8))
+    return ok, "" if ok else mismatch(got, exp.astype(np.float32) * np.float32(2 ** -8))
 
 
 def case_allgather(comm, rank, n, nbytes, salt, inplace=False):
@@ -446,11 +533,13 @@ def main():
         ("exscan_sum_f64_small", lambda: case_scan(comm, rank, n, D, mop.MPI_SUM, 999, 53, True)),
         ("exscan_max_i32_big", lambda: case_scan(comm, rank, n, I32, mop.MPI_MAX, big, 54, True)),
         ("landing_regrow", lambda: case_regrow(comm, rank, n, 90)),
+        ("zero_copy_free_realloc", lambda: case_free_realloc(comm, rank, n, big + 7, 92)),
         ("exscan_prod_i8_inplace",
          lambda: case_scan(comm, rank, n, I8, mop.MPI_PROD, 70001, 55, True, True)),
     ]
     cases += [
         ("iallreduce_mixed", lambda: case_iallreduce(comm, rank, n, 90)),
+        ("iallreduce_many_outstanding", lambda: case_iallreduce_many(comm, rank, n, 94)),
         ("persistent_small", lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, 3001, 80)),
         ("persistent_mid_inplace",
          lambda: case_persistent(comm, rank, n, D, mop.MPI_SUM, 70001, 81, inplace=True)),
@@ -486,9 +575,52 @@ def main():
              with_alg(lambda: case_iallreduce(comm, rank, n, 91, check_nonblocking=False))),
             (f"alg{alg}_persistent_big",
              with_alg(lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, big + 1, 84))),
+            (f"alg{alg}_free_realloc",
+             with_alg(lambda: case_free_realloc(comm, rank, n, big + 9, 93))),
             (f"alg{alg}_persistent_big_inplace",
              with_alg(lambda: case_persistent(comm, rank, n, D, mop.MPI_SUM, big // 2, 85,
                                               inplace=True))),
+        ]
+    if os.environ.get("COLL_HEADLINE"):  # full-size headline only (tests/test_coll_gpu.py)
+        hc = int(os.environ["COLL_HEADLINE"])
+        cases = [(f"headline_alg{a}", lambda a=a: case_headline(comm, rank, n, hc, 95 + a, a))
+                 for a in (0, 1, 2)]
+    # the export fallback (hipIpcGetMemHandle refused): every zero-copy path
+    # through the communicator's shadow buffers ("force_shadow")
+    def shadowed(fn):
+        def run():
+            comm.set_param("force_shadow", 1)
+            try:
+                ok, msg = fn()
+            finally:
+                comm.set_param("force_shadow", 0)
+            return ok, msg
+        return run
+    if not os.environ.get("COLL_HEADLINE"):
+        cases += [
+            ("shadow_ar_pull", shadowed(lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, big + 5, 100))),
+            ("shadow_ar_pull_inplace",
+             shadowed(lambda: case_allreduce(comm, rank, n, D, mop.MPI_SUM, big // 2 + 1, 101, inplace=True))),
+            ("shadow_ar_pullpush", shadowed(with_alg(lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM,
+                                                                            big + 3, 102), 1))),
+            ("shadow_ar_push_inplace", shadowed(with_alg(lambda: case_allreduce(
+                comm, rank, n, F, mop.MPI_SUM, big, 103, inplace=True), 2))),
+            ("shadow_reduce_root_inplace",
+             shadowed(lambda: case_reduce(comm, rank, n, F, mop.MPI_SUM, big + 3, 1, 104, inplace=True))),
+            ("shadow_reduce_root_last",
+             shadowed(lambda: case_reduce(comm, rank, n, DI, mop.MPI_MAXLOC, big // 8 + 7, n - 1, 105))),
+            ("shadow_rsb", shadowed(lambda: case_rsb(comm, rank, n, F, mop.MPI_SUM, big // 4 + 1, 106))),
+            ("shadow_rs_inplace", shadowed(lambda: case_rs(comm, rank, n, D, mop.MPI_SUM,
+                                                           [big // (2 * n) + r for r in range(n)], 107,
+                                                           inplace=True))),
+            ("shadow_allgather_inplace", shadowed(lambda: case_allgather(comm, rank, n, (big * 4) // n + 12,
+                                                                         108, True))),
+            ("shadow_bcast", shadowed(lambda: case_bcast(comm, rank, n, big * 4 + 3, n - 1, 109))),
+            ("shadow_iallreduce", shadowed(lambda: case_iallreduce(comm, rank, n, 110,
+                                                                   check_nonblocking=False))),
+            ("shadow_persistent", shadowed(lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, big + 1, 111))),
+            ("shadow_persistent_push_inplace", shadowed(with_alg(lambda: case_persistent(
+                comm, rank, n, D, mop.MPI_SUM, big // 2, 112, inplace=True), 2))),
         ]
     only = os.environ.get("COLL_CASES")
     ok_all = True
@@ -505,7 +637,7 @@ def main():
         report(rank, n, {"rank": rank, "case": name, "ok": bool(ok), "msg": msg})
         ok_all &= bool(ok)
     # zero-copy disabled: everything staged through the scratch
-    if ok_all and not only:
+    if ok_all and not only and not os.environ.get("COLL_HEADLINE"):
         comm.set_param("zero_copy", 0)
         ok, msg = case_allreduce(comm, rank, n, F, mop.MPI_SUM, 1 << 20, 30)
         report(rank, n, {"rank": rank, "case": "ar_staged_only", "ok": bool(ok), "msg": msg})

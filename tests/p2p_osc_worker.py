@@ -130,6 +130,37 @@ def case_same_tag_order(comm, rank, n, salt, k=40):
     return not fails, "; ".join(fails[:3])
 
 
+def case_recv_timeout_cancel(comm, rank, n, salt):
+    """A receive that times out is withdrawn: the message sent
+    after the timeout is not copied into the abandoned buffer, and the next
+    receive with the same (source, tag) gets it."""
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    nbytes = 70001
+    first = zeros(nbytes)
+    comm.set_param("timeout_ms", 300)
+    timed_out = False
+    try:
+        pml.recv(comm, first, prv, 300 + salt, stream=STREAM)
+    except _lib.OmpiAmdError:
+        timed_out = True
+    finally:
+        comm.set_param("timeout_ms", 20000)
+    comm_barrier()
+    s = dev(payload(rank, salt, nbytes))
+    rq = pml.isend(comm, s, nxt, 300 + salt, stream=STREAM)
+    second = zeros(nbytes)
+    st = pml.recv(comm, second, prv, 300 + salt, stream=STREAM)
+    rq.wait()
+    rq.free()
+    if not timed_out:
+        return False, "the first receive did not time out"
+    if host(first).any():
+        return False, "the withdrawn receive's buffer was written"
+    if st.bytes != nbytes:
+        return False, f"status {st}"
+    return eq(host(second), payload(prv, salt, nbytes), "second receive")
+
+
 def case_any_source(comm, rank, n, salt):
     """Every rank but 0 sends to 0 with tag = its rank; rank 0 receives with
     ANY_SOURCE / ANY_TAG and checks each status against the data."""
@@ -509,6 +540,7 @@ def main():
         ("p2p_any_source_any_tag", lambda: case_any_source(comm, rank, n, 70)),
         ("p2p_probe_truncate", lambda: case_probe_truncate(comm, rank, n, 71)),
         ("p2p_self", lambda: case_self(comm, rank, n, 72)),
+        ("p2p_recv_timeout_cancel", lambda: case_recv_timeout_cancel(comm, rank, n, 75)),
         ("p2p_eager_send_before_recv", lambda: case_eager_send_first(comm, rank, n, 73)),
         ("p2p_ssend_small_rendezvous", lambda: case_ssend_small(comm, rank, n, 74)),
         ("osc_put_get_small", lambda: case_put_get(comm, rank, n, 1001, 80)),
@@ -546,7 +578,12 @@ def main():
         except Exception as e:  # noqa: BLE001 - reported per case
             ok, msg = False, f"{type(e).__name__}: {e}\n{traceback.format_exc()[-1200:]}"
         all_ok &= bool(ok)
-        print(json.dumps({"rank": rank, "case": name, "ok": bool(ok), "msg": msg}), flush=True)
+        line = json.dumps({"rank": rank, "case": name, "ok": bool(ok), "msg": msg})
+        print(line, flush=True)
+        if os.environ.get("COLL_LOG_DIR"):  # progress visible while the test runs
+            os.makedirs(os.environ["COLL_LOG_DIR"], exist_ok=True)
+            with open(os.path.join(os.environ["COLL_LOG_DIR"], f"p2p_osc_n{n}_rank{rank}.jsonl"), "a") as f:
+                f.write(line + "\n")
         if comm.error():
             print(json.dumps({"rank": rank, "case": name + "/sticky", "ok": False,
                               "msg": f"device error {comm.error()}"}), flush=True)

@@ -29,6 +29,11 @@ def free_port():
 
 def run_ranks(n, timeout=600, extra_env=None, worker=WORKER):
     ngpu = torch.cuda.device_count()
+    if "GRAFT_REPO_ROOT" in os.environ and "COLL_LOG_DIR" not in os.environ:
+        # on the gpurun box: per-rank progress files under gpurun_out/ (a hang
+        # names its case, and the progress keeps the silence watchdog off)
+        os.environ["COLL_LOG_DIR"] = os.path.join(os.environ["GRAFT_REPO_ROOT"], "gpurun_out",
+                                                  "coll_logs")
     port = free_port()
     procs = []
     for r in range(n):
@@ -68,4 +73,17 @@ def test_collectives_parity(n):
         bad = [ln for ln in lines if not ln["ok"]]
         if rc != 0 or bad or not lines:
             failures.append((r, rc, bad[:3], out[-1500:] if not lines or rc not in (0, 1) else ""))
+    assert not failures, failures
+
+
+def test_allreduce_headline_size_n8():
+    """256 MiB fp32 SUM allreduce at N = 8 (BASELINE's headline point), all
+    three zero-copy schemes, every element exact (dataset E)."""
+    outs = run_ranks(8, extra_env={"COLL_HEADLINE": str(64 << 20)})
+    failures = []
+    for r, (rc, out) in enumerate(outs):
+        lines = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+        bad = [ln for ln in lines if not ln["ok"]]
+        if rc != 0 or bad or len(lines) != 3:
+            failures.append((r, rc, bad[:3], out[-1500:]))
     assert not failures, failures

@@ -177,6 +177,48 @@ def test_handler_table_path(orc, op, dt):
     assert same_bits(from_dev(to, 0, n * dt.extent).view(dt.np_dtype), exp3, dt)
 
 
+@pytest.mark.parametrize("op,dt", [(mop.MPI_SUM, mop.MPI_FLOAT), (mop.MPI_MAX, mop.MPI_DOUBLE),
+                                   (mop.MPI_MAXLOC, mop.MPI_DOUBLE_INT),
+                                   (mop.MPI_PROD, mop.MPI_C_DOUBLE_COMPLEX)])
+def test_handler_mixed_residency(orc, op, dt):
+    """Host and device operands in one handler call: coll/tuned's ring
+    reduces a malloc'd host inbuf into the device rbuf
+    (coll_base_allreduce.c:688-693) when coll/rocm declines.  The handler
+    stages the host operands on the device and returns the oracle's bits —
+    for every placement of the operands, 2- and 3-buffer."""
+    n = 70001
+    a, b = gen(dt, n, 15), gen(dt, n, 16)
+    ext = dt.extent
+    h2 = mop.handler(op, dt)
+    h3 = mop.handler3(op, dt)
+    cnt = ctypes.c_int(n)
+    for in_dev, inout_dev in ((False, True), (True, False)):
+        ha, hb = a.copy(), b.copy()
+        ta, pa = to_dev(ha)
+        tb, pb = to_dev(hb)
+        src = pa if in_dev else ha.ctypes.data
+        dst = pb if inout_dev else hb.ctypes.data
+        h2(src, dst, ctypes.byref(cnt), None, None)
+        exp = b.copy()
+        orc.op_2buff(op.index, dt.code, a, exp, n)
+        got = from_dev(tb, 0, n * ext).view(dt.np_dtype) if inout_dev else hb
+        assert same_bits(got, exp, dt), ("2buff", in_dev, inout_dev)
+    for mask in range(1, 7):  # not all-device (0 is the plain path), not all-host (7)
+        ha, hb = a.copy(), b.copy()
+        hout = gen(dt, n, 17)
+        ta, pa = to_dev(ha)
+        tb, pb = to_dev(hb)
+        to, po = to_dev(hout)
+        p1 = ha.ctypes.data if mask & 1 else pa
+        p2 = hb.ctypes.data if mask & 2 else pb
+        p3 = hout.ctypes.data if mask & 4 else po
+        h3(p1, p2, p3, ctypes.byref(cnt), None, None)
+        exp3 = gen(dt, n, 17)
+        orc.op_3buff(op.index, dt.code, a, b, exp3, n)
+        got3 = hout if mask & 4 else from_dev(to, 0, n * ext).view(dt.np_dtype)
+        assert same_bits(got3, exp3, dt), ("3buff", mask)
+
+
 def test_handler_host_fallback(orc):
     """Host buffers go to the registered lower-priority handler, never to a
     device kernel (op_example_module_max.c fallback pattern)."""

@@ -193,6 +193,59 @@ static void scenario(int k) {
         alloc(3, 32, 0x63);
         if (eexport(3)) { void *m3 = iopen(3); iclose(m3, "m3"); }
         break;
+    case 7:  // importer keeps the old mapping; a larger allocation takes the freed range
+        printf("S7: import kept open, free 16 MiB, alloc 18 MiB (same start), export\n");
+        alloc(0, 16, 0x70); eexport(0); m0 = iopen(0);
+        efree(0); alloc(1, 18, 0x71);
+        if (eexport(1)) { m1 = iopen(1); iclose(m1, "m1"); }
+        iclose(m0, "stale m0");
+        if (eexport(1)) { m1 = iopen(1); iclose(m1, "m1 after the stale close"); }
+        break;
+    case 8:  // as S7, importer closed before the free
+        printf("S8: import closed, free 16 MiB, alloc 18 MiB, export\n");
+        alloc(0, 16, 0x80); eexport(0); m0 = iopen(0); iclose(m0, "m0");
+        efree(0); alloc(1, 18, 0x81);
+        if (eexport(1)) { m1 = iopen(1); iclose(m1, "m1"); }
+        break;
+    case 9:  // a smaller allocation inside the freed, still-imported range
+        printf("S9: import kept open, free 16 MiB, alloc 8 MiB, export\n");
+        alloc(0, 16, 0x90); eexport(0); m0 = iopen(0);
+        efree(0); alloc(1, 8, 0x91);
+        if (eexport(1)) { m1 = iopen(1); iclose(m1, "m1"); }
+        iclose(m0, "stale m0");
+        break;
+    case 10:  // two freed, still-imported neighbours, one allocation spanning both
+        printf("S10: two imports kept open, both freed, alloc spanning both, export\n");
+        alloc(0, 16, 0xa0); eexport(0); m0 = iopen(0);
+        alloc(1, 16, 0xa1); eexport(1); m1 = iopen(1);
+        efree(0); efree(1); alloc(2, 32, 0xa2);
+        if (eexport(2)) { m2 = iopen(2); iclose(m2, "m2"); }
+        iclose(m0, "stale m0"); iclose(m1, "stale m1");
+        if (eexport(2)) { m2 = iopen(2); iclose(m2, "m2 after the stale closes"); }
+        break;
+    case 11:  // the IMPORTER closes a peer mapping, then allocates and exports its own buffer
+    case 12: {  // as 11, the mapping still open while it allocates
+        printf("S%d: importer %s a peer mapping, then allocates + exports its own 16 MiB\n", k,
+               k == 11 ? "opens and closes" : "keeps open");
+        alloc(0, 16, 0xb0); eexport(0); m0 = iopen(0);
+        if (k == 11) iclose(m0, "m0");
+        for (int rep = 0; rep < 3; ++rep) {
+            void *own = nullptr;
+            hipError_t e = hipMalloc(&own, (size_t)(16 + 2 * rep) << 20);
+            void *base = nullptr;
+            size_t range = 0;
+            hipError_t e2 = hipMemGetAddressRange((hipDeviceptr_t *)&base, &range, (hipDeviceptr_t)own);
+            hipIpcMemHandle_t h;
+            hipError_t e3 = hipIpcGetMemHandle(&h, base ? base : own);
+            printf("  I own alloc %p (rc %d) range %p + %zu (rc %d)%s -> export rc %d %s\n", own, e,
+                   base, range, e2, own == m0 ? "  (the closed mapping's address)" : "", e3,
+                   e3 ? hipGetErrorString(e3) : "");
+            (void)hipGetLastError();
+            (void)hipFree(own);
+        }
+        if (k == 12) iclose(m0, "m0");
+        break;
+    }
     }
     cmd q{3, 0, 0, 0};  // quit: no reply
     wr(c2e[1], &q, sizeof(q));
@@ -201,7 +254,8 @@ static void scenario(int k) {
 
 int main(int argc, char **argv) {
     setvbuf(stdout, nullptr, _IOLBF, 0);
-    for (int k = 1; k <= 6; ++k) {
+    int k0 = argc > 1 ? atoi(argv[1]) : 1;
+    for (int k = k0; k <= 12; ++k) {
         if (pipe(c2e) || pipe(e2c)) return 1;
         fflush(stdout);
         pid_t e = fork();
