@@ -70,6 +70,19 @@ const char *ompi_amd_last_error(void);
  * 1739-1792) used by the convertor and the handlers to pick the path. */
 int ompi_amd_is_device_pointer(const void *ptr);
 
+/* The HIP side of the convertor's GPU function table
+ * (opal_common_cuda_function_table_t, opal/datatype/opal_datatype_cuda.h:
+ * 16-21: gpu_is_gpu_buffer / gpu_cu_memcpy_async / gpu_cu_memcpy /
+ * gpu_memmove; filled by common_cuda.c:1739-1792, :1648-1700).  Any mix of
+ * host and device pointers.  memcpy_async is ordered on `stream` (NULL:
+ * the calling thread's stream); memcpy and memmove complete before they
+ * return; memmove is correct for overlapping ranges. */
+int ompi_amd_memcpy_async(void *dst, const void *src, size_t bytes, void *stream);
+int ompi_amd_memcpy(void *dst, const void *src, size_t bytes);
+int ompi_amd_memmove(void *dst, void *src, size_t bytes);
+/* Wait for `stream` (NULL: the calling thread's stream). */
+int ompi_amd_stream_synchronize(void *stream);
+
 /* ================================================================== */
 /* 1. MPI_Op kernels — replaces op/base's handler loops                */
 /*    ompi/mca/op/base/op_base_functions.c:40-104 (2-buffer),          */
@@ -97,7 +110,10 @@ int ompi_amd_op_reduce_3buff(int op, int type, const void *in1,
  * (the caller sends the result immediately; handlers return void).  When
  * the buffers are host memory they call the fallback registered for the
  * slot (the previous, lower-priority handler — op_example_module_max.c
- * pattern); with no fallback registered they abort loudly. */
+ * pattern); with no fallback registered they abort loudly.  Mixed host and
+ * device operands (coll/tuned's ring reducing a malloc'd bounce buffer
+ * into a device rbuf, coll_base_allreduce.c:688-693) are staged through a
+ * per-thread device scratch and run on the GPU. */
 struct ompi_datatype_t;
 struct ompi_op_base_module_1_0_0_t;
 typedef void (*ompi_amd_op_handler_fn_t)(const void *, void *, int *,

@@ -65,6 +65,34 @@ int ompi_amd_ddt_unpack(const ompi_amd_ddt_t *ddt, size_t count,
                         const void *src, void *dst, size_t offset,
                         size_t bytes, size_t *done, void *stream);
 
+/* An iovec entry, layout-identical to struct iovec (sys/uio.h): the glue
+ * passes the convertor's iovec array straight through. */
+typedef struct {
+    void *iov_base;
+    size_t iov_len;
+} ompi_amd_iovec_t;
+
+/* The convertor's advance step over an iovec array, with the contract of
+ * convertor_advance_fct_t (opal/datatype/opal_convertor.h:64-67) as
+ * opal_generic_simple_pack / _unpack implement it (opal_datatype_pack.c:
+ * 235-370, opal_datatype_unpack.c:245-428): starting at stream byte
+ * `position` (the convertor's bConverted; any byte, mid-element included),
+ * fill (pack) or drain (unpack) iov[0 .. *out_size) in order, each up to its
+ * iov_len; on return iov_len = bytes used per entry, *out_size = entries
+ * used (all, unless the stream ended inside one), *max_data = total bytes.
+ * Returns 1 when the stream is complete, 0 when data remains, a negative
+ * OMPI_AMD_ERR_* on error.  All entries move in ONE kernel launch
+ * (stream-ordered on `stream`; the caller synchronises unless it runs the
+ * convertor asynchronously). */
+int ompi_amd_ddt_pack_iov(const ompi_amd_ddt_t *ddt, size_t count,
+                          const void *typed, size_t position,
+                          ompi_amd_iovec_t *iov, uint32_t *out_size,
+                          size_t *max_data, void *stream);
+int ompi_amd_ddt_unpack_iov(const ompi_amd_ddt_t *ddt, size_t count,
+                            void *typed, size_t position,
+                            ompi_amd_iovec_t *iov, uint32_t *out_size,
+                            size_t *max_data, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

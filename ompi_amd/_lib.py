@@ -57,6 +57,11 @@ class DdtBlock(ctypes.Structure):
     _fields_ = [("disp", ctypes.c_int64), ("len", ctypes.c_int64)]
 
 
+class Iovec(ctypes.Structure):
+    """ompi_amd_iovec_t (layout of struct iovec)."""
+    _fields_ = [("iov_base", ctypes.c_void_p), ("iov_len", ctypes.c_size_t)]
+
+
 class DdtElem(ctypes.Structure):
     _fields_ = [("count", ctypes.c_int64), ("blocklen", ctypes.c_int64),
                 ("stride", ctypes.c_int64), ("disp", ctypes.c_int64)]
@@ -99,7 +104,17 @@ PROTOTYPES = [
     ("ompi_amd_ddt_unpack", _C.c_int,
      [_C.c_void_p, _C.c_size_t, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_size_t,
       _C.POINTER(_C.c_size_t), _C.c_void_p]),
+    ("ompi_amd_ddt_pack_iov", _C.c_int,
+     [_C.c_void_p, _C.c_size_t, _C.c_void_p, _C.c_size_t, _C.c_void_p, _C.POINTER(_C.c_uint32),
+      _C.POINTER(_C.c_size_t), _C.c_void_p]),
+    ("ompi_amd_ddt_unpack_iov", _C.c_int,
+     [_C.c_void_p, _C.c_size_t, _C.c_void_p, _C.c_size_t, _C.c_void_p, _C.POINTER(_C.c_uint32),
+      _C.POINTER(_C.c_size_t), _C.c_void_p]),
     ("ompi_amd_is_device_pointer", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_memcpy_async", _C.c_int, [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p]),
+    ("ompi_amd_memcpy", _C.c_int, [_C.c_void_p, _C.c_void_p, _C.c_size_t]),
+    ("ompi_amd_memmove", _C.c_int, [_C.c_void_p, _C.c_void_p, _C.c_size_t]),
+    ("ompi_amd_stream_synchronize", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_comm_create", _C.c_int,
      [_C.c_char_p, _C.c_int, _C.c_int, _C.c_int, _C.POINTER(_C.c_void_p)]),
     ("ompi_amd_comm_destroy", _C.c_int, [_C.c_void_p]),

@@ -1534,6 +1534,7 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "stale_closed")) *v = c->stale_closed;
     else if (!strcmp(key, "stale_same_handle")) *v = c->stale_same_handle;
     else if (!strcmp(key, "shadowed")) *v = c->shadowed;
+    else if (!strcmp(key, "epoch")) *v = (int64_t)c->epoch;
     else if (!strcmp(key, "force_shadow")) *v = c->force_shadow;
     else if (!strcmp(key, "imports")) *v = (int64_t)c->imports.size();
     else {

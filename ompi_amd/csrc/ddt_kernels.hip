@@ -425,6 +425,75 @@ __global__ __launch_bounds__(kDdtThreads) void ddt_unpack_tile_kernel(ddt_period
     }
 }
 
+// One launch over a whole iovec array (the convertor's fAdvance with
+// out_size > 1): job j is stream window [start, start + len) to or from the
+// contiguous buffer contig (grid row y = job).  The reference fills an iovec
+// array run by run with one memcpy / cuMemcpy each
+// (opal_generic_simple_pack, opal_datatype_pack.c:273-356); here every
+// granule of every iovec is one lane's work in the same launch, so a PML
+// fragment train costs one launch instead of one per fragment.
+struct iov_job {
+    int64_t start, len;
+    char *contig;
+};
+
+template <int G, bool UNPACK>
+__global__ __launch_bounds__(kDdtThreads) void ddt_iov_kernel(ddt_desc d, char *typed,
+                                                              const iov_job *jobs) {
+    __shared__ ddt_elem lds[kDdtLdsElems];
+    const ddt_elem *el = d.elems;
+    if (d.nelem <= kDdtLdsElems) {
+        for (int i = threadIdx.x; i < d.nelem; i += kDdtThreads) lds[i] = d.elems[i];
+        __syncthreads();
+        el = lds;
+    }
+    const iov_job jb = jobs[blockIdx.y];
+    const int64_t start = jb.start, end = jb.start + jb.len;
+    const int64_t body0 = min(end, (start + G - 1) / G * G);
+    const int64_t body1 = max(body0, end / G * G);
+    const int64_t ngran = (body1 - body0) / G;
+    using T = typename granule<G>::t;
+    constexpr int U = kDdtUnroll;
+    const int64_t stride = (int64_t)gridDim.x * kDdtThreads;
+    char *c = jb.contig - start;  // contiguous byte of stream position p: c[p]
+    for (int64_t j0 = (int64_t)blockIdx.x * kDdtThreads + threadIdx.x; j0 < ngran; j0 += stride * U) {
+        int64_t toff[U];
+        T v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = j0 + u * stride;
+            if (j < ngran)
+                toff[u] = typed_offset<uint64_t>(el, d.nelem, (uint64_t)d.size, d.extent,
+                                                 (uint64_t)(body0 + j * G));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = j0 + u * stride;
+            if (j < ngran)
+                v[u] = UNPACK ? *reinterpret_cast<const T *>(c + body0 + j * G)
+                              : *reinterpret_cast<const T *>(typed + toff[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t j = j0 + u * stride;
+            if (j < ngran) {
+                if (UNPACK) *reinterpret_cast<T *>(typed + toff[u]) = v[u];
+                else *reinterpret_cast<T *>(c + body0 + j * G) = v[u];
+            }
+        }
+    }
+    if (blockIdx.x == gridDim.x - 1) {  // the window's bytes off the granule grid
+        const int64_t head = body0 - start, tail = end - body1;
+        for (int64_t k = threadIdx.x; k < head + tail; k += kDdtThreads) {
+            const int64_t p = k < head ? start + k : body1 + (k - head);
+            const int64_t t = typed_offset<uint64_t>(el, d.nelem, (uint64_t)d.size, d.extent,
+                                                     (uint64_t)p);
+            if (UNPACK) typed[t] = c[p];
+            else c[p] = typed[t];
+        }
+    }
+}
+
 }  // namespace ompi_amd
 
 struct ompi_amd_ddt {
@@ -632,11 +701,139 @@ static int ddt_run(const ompi_amd_ddt_t *ddt, size_t count, const void *typed, v
     return OMPI_AMD_SUCCESS;
 }
 
+// Per-thread job table for ddt_iov: pinned host staging + a device copy,
+// reused once the previous call's kernel has read it (event).
+struct iov_table {
+    iov_job *host = nullptr, *dev = nullptr;
+    size_t cap = 0;
+    hipEvent_t used = nullptr;  // after the last kernel that read `dev`
+    bool pending = false;
+};
+static thread_local iov_table tls_iov;
+
+static int iov_reserve(size_t n) {
+    iov_table &t = tls_iov;
+    if (t.pending) {  // the previous launch still reads the table
+        const hipError_t e = hipEventSynchronize(t.used);
+        if (e != hipSuccess) return record_hip(e, "hipEventSynchronize (iov table)");
+        t.pending = false;
+    }
+    if (!t.used && hipEventCreateWithFlags(&t.used, hipEventDisableTiming) != hipSuccess)
+        return record_hip(hipGetLastError(), "hipEventCreate (iov table)");
+    if (n <= t.cap) return OMPI_AMD_SUCCESS;
+    const size_t want = std::max<size_t>(n, 2 * t.cap);
+    if (t.host) (void)hipHostFree(t.host);
+    if (t.dev) (void)hipFree(t.dev);
+    t.host = nullptr;
+    t.dev = nullptr;
+    t.cap = 0;
+    hipError_t e = hipHostMalloc((void **)&t.host, want * sizeof(iov_job), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipMalloc((void **)&t.dev, want * sizeof(iov_job));
+    if (e != hipSuccess) return record_hip(e, "iov job table");
+    t.cap = want;
+    return OMPI_AMD_SUCCESS;
+}
+
+// The fAdvance contract (convertor_advance_fct_t, opal_convertor.h:64-67;
+// opal_generic_simple_pack, opal_datatype_pack.c:273-369): fill (pack) or
+// drain (unpack) iov[0 .. *out_size) in order from stream position
+// `position`, each entry up to its iov_len; iov_len becomes the bytes used,
+// *out_size the entries used (all of them unless the stream ends inside
+// one), *max_data the total.  Returns 1 when the stream is complete, 0 when
+// data remains, a negative OMPI_AMD_ERR_* on error.  One launch for all
+// entries (the single-entry case takes the tuned window kernels).
+template <bool UNPACK>
+static int ddt_iov(const ompi_amd_ddt_t *ddt, size_t count, void *typed, size_t position,
+                   ompi_amd_iovec_t *iov, uint32_t *out_size, size_t *max_data, hipStream_t s) {
+    if (!ddt || !out_size || !max_data || (*out_size && !iov) || (!typed && count))
+        return OMPI_AMD_ERR_BAD_PARAM;
+    const uint64_t total = (uint64_t)ddt->size * count;
+    *max_data = 0;
+    if (position >= total) {
+        *out_size = 0;
+        return 1;
+    }
+    // host pass: assign stream windows to iovecs
+    uint64_t pos = position;
+    uint32_t used = 0;
+    int G = std::min(ddt->gran, pow2_gran((uintptr_t)typed));
+    int64_t most = 0;
+    for (uint32_t i = 0; i < *out_size && pos < total; ++i) {
+        const uint64_t take = std::min<uint64_t>(iov[i].iov_len, total - pos);
+        if (take && !iov[i].iov_base) return OMPI_AMD_ERR_BAD_PARAM;
+        iov[i].iov_len = (size_t)take;
+        if (take) {
+            G = std::min(G, pow2_gran((uint64_t)((uintptr_t)iov[i].iov_base - (uintptr_t)pos)));
+            most = std::max<int64_t>(most, (int64_t)take);
+        }
+        pos += take;
+        used = i + 1;
+    }
+    if (pos < total) used = *out_size;
+    const uint64_t moved = pos - position;
+    int jobs = 0;
+    for (uint32_t i = 0; i < used; ++i) jobs += iov[i].iov_len ? 1 : 0;
+    if (jobs == 1) {  // one window: the tuned kernels (staged tile, walker)
+        for (uint32_t i = 0; i < used; ++i) {
+            if (!iov[i].iov_len) continue;
+            size_t done = 0;
+            const int rc = ddt_run<UNPACK>(ddt, count, typed, iov[i].iov_base, (size_t)position,
+                                           iov[i].iov_len, &done, s);
+            if (rc != OMPI_AMD_SUCCESS) return rc;
+        }
+    } else if (jobs > 1) {
+        int rc = iov_reserve((size_t)jobs);
+        if (rc != OMPI_AMD_SUCCESS) return rc;
+        iov_table &t = tls_iov;
+        uint64_t p = position;
+        int k = 0;
+        for (uint32_t i = 0; i < used; ++i) {
+            if (iov[i].iov_len) t.host[k++] = {(int64_t)p, (int64_t)iov[i].iov_len, (char *)iov[i].iov_base};
+            p += iov[i].iov_len;
+        }
+        hipError_t e = hipMemcpyAsync(t.dev, t.host, (size_t)jobs * sizeof(iov_job),
+                                      hipMemcpyHostToDevice, s);
+        const ddt_desc d{ddt->dev, (int)ddt->host.size(), ddt->size, ddt->extent, {0u, 0u, 0u}};
+        const int64_t per = (int64_t)kDdtThreads * kDdtUnroll * G;
+        const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((most + per - 1) / per, 1024));
+        for (int j0 = 0; e == hipSuccess && j0 < jobs; j0 += 65535) {
+            const dim3 grid(gx, (unsigned)std::min(65535, jobs - j0));
+            const iov_job *tab = t.dev + j0;
+            switch (G) {
+#define IOVK(GG) case GG: hipLaunchKernelGGL((ddt_iov_kernel<GG, UNPACK>), grid, dim3(kDdtThreads), 0, s, d, (char *)typed, tab); break;
+                IOVK(16) IOVK(8) IOVK(4) IOVK(2)
+            default: IOVK(1)
+#undef IOVK
+            }
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = hipEventRecord(t.used, s);
+        if (e != hipSuccess) return record_hip(e, "ddt iovec launch");
+        t.pending = true;
+    }
+    *out_size = used;
+    *max_data = (size_t)moved;
+    return pos == total ? 1 : 0;
+}
+
 }  // namespace ompi_amd
 
 using namespace ompi_amd;
 
 extern "C" {
+
+int ompi_amd_ddt_pack_iov(const ompi_amd_ddt_t *ddt, size_t count, const void *typed,
+                          size_t position, ompi_amd_iovec_t *iov, uint32_t *out_size,
+                          size_t *max_data, void *stream) {
+    return ddt_iov<false>(ddt, count, const_cast<void *>(typed), position, iov, out_size, max_data,
+                          as_stream(stream));
+}
+
+int ompi_amd_ddt_unpack_iov(const ompi_amd_ddt_t *ddt, size_t count, void *typed,
+                            size_t position, ompi_amd_iovec_t *iov, uint32_t *out_size,
+                            size_t *max_data, void *stream) {
+    return ddt_iov<true>(ddt, count, typed, position, iov, out_size, max_data, as_stream(stream));
+}
 
 int ompi_amd_ddt_create_elems(const ompi_amd_ddt_elem_t *elems, int nelems, int64_t extent,
                               ompi_amd_ddt_t **out) {

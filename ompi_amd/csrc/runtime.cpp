@@ -71,4 +71,39 @@ int ompi_amd_is_device_pointer(const void *ptr) {
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
+int ompi_amd_memcpy_async(void *dst, const void *src, size_t bytes, void *stream) {
+    if (bytes == 0) return OMPI_AMD_SUCCESS;
+    if (!dst || !src) return OMPI_AMD_ERR_BAD_PARAM;
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : thread_stream();
+    return record_hip(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s), "hipMemcpyAsync");
+}
+
+int ompi_amd_stream_synchronize(void *stream) {
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : thread_stream();
+    return record_hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+}
+
+int ompi_amd_memcpy(void *dst, const void *src, size_t bytes) {
+    if (bytes == 0) return OMPI_AMD_SUCCESS;
+    if (!dst || !src) return OMPI_AMD_ERR_BAD_PARAM;
+    hipStream_t s = thread_stream();
+    int rc = record_hip(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s), "hipMemcpyAsync");
+    if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+    return rc;
+}
+
+// Overlap-safe: through a temporary device buffer when the ranges overlap
+// (the reference's cuda memmove does the same, common_cuda.c:1715-1737).
+int ompi_amd_memmove(void *dst, void *src, size_t bytes) {
+    if (bytes == 0 || dst == src) return OMPI_AMD_SUCCESS;
+    const char *d = static_cast<const char *>(dst), *s = static_cast<const char *>(src);
+    if (d + bytes <= s || s + bytes <= d) return ompi_amd_memcpy(dst, src, bytes);
+    void *tmp = nullptr;
+    int rc = record_hip(hipMalloc(&tmp, bytes), "hipMalloc (memmove)");
+    if (rc == OMPI_AMD_SUCCESS) rc = ompi_amd_memcpy(tmp, src, bytes);
+    if (rc == OMPI_AMD_SUCCESS) rc = ompi_amd_memcpy(dst, tmp, bytes);
+    if (tmp) (void)hipFree(tmp);
+    return rc;
+}
+
 }  // extern "C"

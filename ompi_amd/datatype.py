@@ -250,6 +250,32 @@ class Convertor:
         self.bConverted += done.value
         return (1 if self.bConverted == self.local_size else 0), done.value
 
+    def _run_iov(self, fn, iovs):
+        """fAdvance over an iovec array (convertor_advance_fct_t,
+        opal_convertor.h:64-67): iovs = [(device address, capacity)...].
+        Returns (completed, [bytes used per entry], entries used, max_data);
+        one kernel launch for all entries."""
+        n = len(iovs)
+        arr = (_lib.Iovec * max(1, n))(*[_lib.Iovec(_addr(b), int(l)) for b, l in iovs])
+        out = ctypes.c_uint32(n)
+        max_data = ctypes.c_size_t(0)
+        sp = None if self.stream is None else (
+            self.stream if isinstance(self.stream, int) else self.stream.cuda_stream)
+        rc = fn(self.datatype._handle, self.count, self.base, self.bConverted, arr,
+                ctypes.byref(out), ctypes.byref(max_data), sp)
+        if rc < 0:
+            _lib.check(rc, "convertor (iovec)")
+        self.bConverted += max_data.value
+        return rc, [arr[i].iov_len for i in range(out.value)], out.value, max_data.value
+
+    def pack_iov(self, iovs):
+        """opal_convertor_pack with an iovec array (packed bytes into each entry)."""
+        return self._run_iov(_lib.load().ompi_amd_ddt_pack_iov, iovs)
+
+    def unpack_iov(self, iovs):
+        """opal_convertor_unpack with an iovec array (packed bytes from each entry)."""
+        return self._run_iov(_lib.load().ompi_amd_ddt_unpack_iov, iovs)
+
     def pack(self, iov, max_data: int):
         """opal_convertor_pack: returns (completed, bytes written into iov)."""
         return self._run(_lib.load().ompi_amd_ddt_pack, self.base, _addr(iov), max_data)

@@ -1,0 +1,50 @@
+/*
+ * The convertor's GPU seam for device buffers through libompi_amd.so.
+ *
+ * Two hook points of the reference (SURVEY.md §8b "convertor offload"):
+ *  - the GPU function table (opal_common_cuda_function_table_t,
+ *    opal/datatype/opal_datatype_cuda.h:16-21), registered with
+ *    opal_cuda_add_initialization_function (opal_datatype_cuda.c:34-36):
+ *    mca_common_rocm_fill_table fills it with HIP implementations;
+ *  - the convertor's advance function (convertor_advance_fct_t,
+ *    opal/datatype/opal_convertor.h:64-67), chosen in
+ *    opal_convertor_prepare_for_send / _recv (opal_convertor.c:565-653):
+ *    opal_rocm_convertor_select replaces the generic pack / unpack by
+ *    opal_rocm_pack / opal_rocm_unpack when the user buffer is device
+ *    memory (CONVERTOR_CUDA, set by mca_cuda_convertor_init through the
+ *    table's gpu_is_gpu_buffer).
+ * INTEGRATION.md §3 shows the two lines a maintainer adds to the
+ * reference's prepare functions.
+ */
+#ifndef OPAL_DATATYPE_ROCM_H
+#define OPAL_DATATYPE_ROCM_H
+
+#include <stdint.h>
+#include <sys/uio.h>
+
+#include "opal/datatype/opal_convertor.h"
+#include "opal/datatype/opal_datatype_cuda.h"
+
+/* opal_cuda_add_initialization_function's callback: fill the GPU table. */
+int mca_common_rocm_fill_table(opal_common_cuda_function_table_t *ftable);
+
+/* After prepare_for_send / _recv chose fAdvance: offload it when the
+ * convertor is a device conversion the library can run.  Returns 1 when
+ * fAdvance now points at opal_rocm_pack / opal_rocm_unpack, 0 when the
+ * reference's choice stays (host buffer, NO_OP contiguous fast path, a
+ * description too irregular to flatten). */
+int opal_rocm_convertor_select(opal_convertor_t *convertor);
+
+/* convertor_advance_fct_t implementations: iov[0 .. *out_size) filled
+ * (pack) or drained (unpack) from bConverted on in one kernel launch;
+ * returns 1 complete, 0 more data pending, -1 error. */
+int32_t opal_rocm_pack(opal_convertor_t *convertor, struct iovec *iov, uint32_t *out_size,
+                       size_t *max_data);
+int32_t opal_rocm_unpack(opal_convertor_t *convertor, struct iovec *iov, uint32_t *out_size,
+                         size_t *max_data);
+
+/* Device programs cached per datatype description (tests / finalize). */
+int opal_rocm_program_cache_size(void);
+void opal_rocm_program_cache_clear(void);
+
+#endif

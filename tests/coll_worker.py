@@ -634,6 +634,8 @@ def main():
             report(rank, n, {"rank": rank, "case": name, "ok": ok, "msg": msg})
             ok_all = False
             break
+        if not ok:  # barrier epochs diverge when ranks launched different device work
+            msg = f"[epoch {comm.get_param('epoch')}] {msg}"
         report(rank, n, {"rank": rank, "case": name, "ok": bool(ok), "msg": msg})
         ok_all &= bool(ok)
     # zero-copy disabled: everything staged through the scratch

@@ -116,3 +116,83 @@ def test_osc_component_device_path(osc_harness, n):
     mismatched datatypes and PSCW, free."""
     for rc, out, err in _run_coll_harness(osc_harness, n, True, 180):
         assert rc == 0 and out == "ok gpu", (rc, out, err)
+
+
+# ---- the convertor seam (ompi_amd/mca/common/rocm) through tests/mca_harness/ddt_harness.c ----
+
+BASIC = {8: 16, 4: 6, 2: 5, 1: 9}  # bytes -> OPAL_DATATYPE_FLOAT8 / INT4 / INT2 / UINT1
+
+
+def _desc_from_runs(runs):
+    """An opt_desc for a typemap: consecutive equal-length runs at a constant
+    stride become one ELEM {count, blocklen, extent, disp} (what
+    opal_datatype_optimize.c produces for vectors / indexed types)."""
+    out, i = [], 0
+    while i < len(runs):
+        d, n = runs[i]
+        j = i + 1
+        st = runs[j][0] - d if j < len(runs) and runs[j][1] == n else None
+        while st is not None and j < len(runs) and runs[j][1] == n and runs[j][0] - runs[j - 1][0] == st:
+            j += 1
+        cnt = j - i
+        bsz = next(b for b in (8, 4, 2, 1) if n % b == 0 and d % b == 0 and (cnt == 1 or st % b == 0))
+        out.append(f"E {BASIC[bsz]} {cnt} {n // bsz} {st if cnt > 1 else n} {d}")
+        i = j
+    return out
+
+
+def _spec(name, count, extent, runs, desc, chunks):
+    size = sum(n for _, n in runs)
+    lines = [f"T {name} {count} {extent} {size}",
+             f"B {len(runs)} " + " ".join(f"{d} {n}" for d, n in runs),
+             f"D {len(desc) + 1}"] + desc + [f"X 1 {size}", f"C {len(chunks)} " + " ".join(map(str, chunks))]
+    return "\n".join(lines)
+
+
+def _ddt_specs(golden):
+    specs = []
+    for t in golden("ddt_kat.json")["types"]:
+        runs = [tuple(b) for b in t["blocks"]]
+        specs.append(_spec(t["name"], t["count"], t["extent"], runs, _desc_from_runs(runs), t["chunks"]))
+    # loop-shaped descriptions (OPAL_DATATYPE_LOOP / END_LOOP), flattened by the glue
+    runs = [(r * 16 + o, n) for r in range(10) for o, n in ((0, 1), (8, 8))]
+    specs.append(_spec("loop_struct_char_double", 450, 160, runs,
+                       ["L 3 10 16", "E 9 1 1 1 0", "E 16 1 1 8 8", "X 3 90"], [12, 956, 65536]))
+    runs = [(a * 256 + b * 24, 8) for a in range(3) for b in range(5)] + [(800, 3)]
+    specs.append(_spec("nested_loops", 97, 1024, runs,
+                       ["L 4 3 256", "L 2 5 24", "E 6 1 2 8 0", "X 2 40", "X 4 120", "E 9 1 3 3 800"],
+                       [12, 956, 65536]))
+    runs = [(r * 96 + k * 32, 8) for r in range(64) for k in range(3)]
+    specs.append(_spec("loop_of_strided", 40, 6144, runs, ["L 2 64 96", "E 16 3 1 32 0", "X 2 1536"],
+                       [12, 4096, 65536]))
+    return "\n".join(specs) + "\n"
+
+
+@pytest.fixture(scope="module")
+def ddt_harness(tmp_path_factory):
+    from ompi_amd import _lib
+    from oracle import oracle as orc
+    _lib.load()
+    orc.lib()
+    out = str(tmp_path_factory.mktemp("mca") / "ddt_harness")
+    subprocess.run(["bash", os.path.join(ROOT, "tests", "mca_harness", "build_ddt.sh"), out], check=True)
+    return out
+
+
+def test_convertor_seam_no_gpu(ddt_harness):
+    """Without a GPU the function table refuses and nothing is offloaded."""
+    r = subprocess.run([ddt_harness], capture_output=True, text=True, timeout=60, input="",
+                       env={**os.environ, "HARNESS_GPU": "0", "HIP_VISIBLE_DEVICES": ""})
+    assert r.returncode == 0 and r.stdout.strip() == "ok cpu", (r.stdout, r.stderr)
+
+
+@pytest.mark.gpu
+def test_convertor_seam_fadvance(ddt_harness, golden):
+    """opal_rocm_pack / _unpack as the convertor's fAdvance, driven like a
+    PML (fragment trains of 1 and 7 iovecs at ddt_test.c's chunk sizes: 12 /
+    82 / 6000 / 36000, blacs 956 / 16K / 64K, upper triangle 48 / 956),
+    resumable at any bConverted, byte-exact against the oracle; gap bytes of
+    the receive buffer untouched."""
+    r = subprocess.run([ddt_harness], capture_output=True, text=True, timeout=300,
+                       input=_ddt_specs(golden), env={**os.environ, "HARNESS_GPU": "1"})
+    assert r.returncode == 0 and "all" in r.stdout, (r.stdout[-3000:], r.stderr[-2000:])
