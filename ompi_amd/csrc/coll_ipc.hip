@@ -57,6 +57,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <mutex>
 #include <new>
 #include <utility>
 #include <vector>
@@ -287,6 +288,8 @@ struct ompi_amd_comm {
     void *land_opened[kMaxRanks] = {};
     int stale_closed = 0;                 // cached peer mappings closed because the peer freed them
     int stale_same_handle = 0;            //   ... of which the new allocation had the same handle bytes
+    int64_t exports_new = 0, imports_new = 0;  // runtime export / open calls made (cache misses)
+    int recycled_exports = 0;             // exports refused: recycled handle bytes (shadowed)
     // streams this communicator launched work on: the current one, plus an
     // event recorded on each earlier one when the calls moved away from it
     // (quiesce() waits for exactly that work, not for the whole device)
@@ -307,7 +310,13 @@ struct ompi_amd_comm {
     int max_blocks = 1024;
     int algorithm = 0;
     // IPC caches
-    struct exp_entry { void *base; size_t size; unsigned long long id; hipIpcMemHandle_t h; };
+    struct exp_entry {
+        void *base;
+        size_t size;
+        unsigned long long id;
+        hipIpcMemHandle_t h;
+        bool recycled;  // the runtime handed this allocation a freed one's handle bytes
+    };
     struct imp_entry {
         int peer;
         hipIpcMemHandle_t h;
@@ -366,8 +375,47 @@ static int set_dev(ompi_amd_comm_t *c) {
     return record_hip(hipSetDevice(c->device), "hipSetDevice");
 }
 
+// Every IPC handle this process has exported, with the allocation it
+// named.  On ROCm 7.2 with dmabuf IPC a new allocation can be handed the
+// very handle bytes of a freed one (profiles/r02_coll_free_realloc*: most
+// re-allocations at a freed address did), and a peer that still maps — or
+// just closed — the freed one may then get the old memory back for the new
+// handle (round 1's stale landing data; round 2's free/realloc push cases
+// with all peer blocks missing).  A handle is therefore never published
+// for a second allocation: export_buf sends such a buffer through its
+// shadow, alloc_exportable retries while holding the colliding allocation.
+struct handle_rec {
+    hipIpcMemHandle_t h;
+    void *base;
+    size_t size;
+    unsigned long long id;
+};
+static std::mutex g_hist_mu;
+static std::vector<handle_rec> g_hist;
+
+// True when h already named another allocation; records it otherwise.
+static bool handle_recycled(const hipIpcMemHandle_t &h, void *base, size_t size,
+                            unsigned long long id) {
+    std::lock_guard<std::mutex> g(g_hist_mu);
+    for (const auto &r : g_hist)
+        if (memcmp(&r.h, &h, sizeof(h)) == 0)
+            return !(r.base == base && r.size == size && r.id == id);
+    g_hist.push_back({h, base, size, id});
+    return false;
+}
+
+static unsigned long long buffer_id(const void *p) {
+    unsigned long long id = 0;
+    if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)p) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return id;
+}
+
 // ipc_failed: set when the runtime refused to export a live device
-// allocation (the shadow fallback applies); other failures are errors.
+// allocation, or handed it recycled handle bytes (the shadow fallback
+// applies); other failures are errors.
 static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d, bool *ipc_failed = nullptr) {
     memset(d, 0, sizeof(*d));
     if (ipc_failed) *ipc_failed = false;
@@ -387,13 +435,19 @@ static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d, bool *ip
     d->size = (uint64_t)size;
     for (auto &x : c->exports) {
         if (x.base == base && x.size == size && x.id == id) {
+            if (x.recycled) {
+                if (ipc_failed) *ipc_failed = true;
+                record_msg("allocation %p + %zu (id %llu) carries a recycled IPC handle", base, size, id);
+                return OMPI_AMD_ERR_HIP;
+            }
             d->h = x.h;
             d->off = (uint64_t)((const char *)ptr - (const char *)base);
             d->valid = 1;
             return OMPI_AMD_SUCCESS;
         }
     }
-    ompi_amd_comm::exp_entry x{base, size, id, {}};
+    ompi_amd_comm::exp_entry x{base, size, id, {}, false};
+    ++c->exports_new;
     e = hipIpcGetMemHandle(&x.h, base);
     if (e != hipSuccess) {
         (void)hipGetLastError();
@@ -417,7 +471,14 @@ static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d, bool *ip
                                                (char *)base < (char *)o.base + o.size;
                                     }),
                      c->exports.end());
+    x.recycled = handle_recycled(x.h, base, size, id);
     c->exports.push_back(x);
+    if (x.recycled) {
+        ++c->recycled_exports;
+        if (ipc_failed) *ipc_failed = true;
+        record_msg("allocation %p + %zu (id %llu) carries a recycled IPC handle", base, size, id);
+        return OMPI_AMD_ERR_HIP;
+    }
     d->h = x.h;
     d->off = (uint64_t)((const char *)ptr - (const char *)base);
     d->valid = 1;
@@ -434,7 +495,9 @@ static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d, bool *ip
 // is how a stale alias could be handed back, and serving it from the cache
 // would certainly be one.  A pinned mapping (a persistent plan's) of a freed
 // buffer is a program error: report it instead of unmapping under the plan.
-static int drop_stale_imports(ompi_amd_comm_t *c, int peer, const buf_desc &d) {
+static int drop_stale_imports(ompi_amd_comm_t *c, int peer, const buf_desc &d,
+                              bool *closed_same = nullptr) {
+    if (closed_same) *closed_same = false;
     const uint64_t lo = d.base, hi = d.base + d.size;
     for (auto it = c->imports.begin(); it != c->imports.end();) {
         const bool same_handle = memcmp(&it->h, &d.h, sizeof(d.h)) == 0;
@@ -452,6 +515,7 @@ static int drop_stale_imports(ompi_amd_comm_t *c, int peer, const buf_desc &d) {
         if (e != hipSuccess) return record_hip(e, "hipIpcCloseMemHandle (stale peer mapping)");
         ++c->stale_closed;
         c->stale_same_handle += same_handle ? 1 : 0;
+        if (closed_same && same_handle) *closed_same = true;
         it = c->imports.erase(it);
     }
     return OMPI_AMD_SUCCESS;
@@ -471,7 +535,8 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
             return OMPI_AMD_SUCCESS;
         }
     }
-    TRY(drop_stale_imports(c, peer, d));
+    bool closed_same = false;
+    TRY(drop_stale_imports(c, peer, d, &closed_same));
     if (c->imports.size() >= 256) {  // evict the least recently used unpinned mapping
         auto it = c->imports.end();
         for (auto jt = c->imports.begin(); jt != c->imports.end(); ++jt)
@@ -482,8 +547,16 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
         }
     }
     void *base = nullptr;
+    ++c->imports_new;
     hipError_t e = hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess);
-    if (e != hipSuccess) return record_hip(e, "hipIpcOpenMemHandle");
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        record_msg("hipIpcOpenMemHandle: %s (peer %d buffer id %llu at %p + %llu%s)",
+                   hipGetErrorString(e), peer, (unsigned long long)d.id, (void *)(uintptr_t)d.base,
+                   (unsigned long long)d.size,
+                   closed_same ? ", after closing its freed predecessor with the same handle" : "");
+        return OMPI_AMD_ERR_HIP;
+    }
     c->imports.push_back({peer, d.h, d.id, d.base, d.size, base, ++c->use_clock, pin ? 1 : 0});
     *out = (const char *)base + d.off;
     if (base_out) *base_out = base;
@@ -583,20 +656,36 @@ static int quiesce(ompi_amd_comm_t *c) {
 // never reuses the old one's address range: on ROCm 7.2 an IPC export of a
 // fresh allocation at a just-freed range failed with hipErrorInvalidValue
 // (seen at 4 ranks, third growth).  Sizes grow geometrically, in 32 MiB steps.
-static hipError_t alloc_exportable(size_t bytes, char **out, hipIpcMemHandle_t *h) {
+// The allocation must also get handle bytes no earlier allocation had
+// (handle_recycled): a colliding one is kept alive while the next is made,
+// so that the runtime cannot hand out the same handle again.
+// uncached: fine-grained memory (flag pages) instead of ordinary device memory.
+static hipError_t alloc_exportable(size_t bytes, char **out, hipIpcMemHandle_t *h,
+                                   bool uncached = false) {
     std::vector<void *> failed;
     hipError_t e = hipErrorInvalidValue;
-    for (int attempt = 0; attempt < 3; ++attempt) {
+    for (int attempt = 0; attempt < 8; ++attempt) {
         void *p = nullptr;
-        e = hipMalloc(&p, bytes + (size_t)attempt * (2u << 20));
+        const size_t sz = bytes + (size_t)attempt * (2u << 20);
+        e = uncached ? hipExtMallocWithFlags(&p, sz, hipDeviceMallocUncached) : hipMalloc(&p, sz);
         if (e != hipSuccess) break;
         e = hipIpcGetMemHandle(h, p);
         if (e == hipSuccess) {
-            *out = (char *)p;
-            break;
+            void *base = nullptr;
+            size_t range = 0;
+            if (hipMemGetAddressRange((hipDeviceptr_t *)&base, &range, (hipDeviceptr_t)p) != hipSuccess) {
+                (void)hipGetLastError();
+                base = p;
+                range = sz;
+            }
+            if (!handle_recycled(*h, base, range, buffer_id(p))) {
+                *out = (char *)p;
+                break;
+            }
+            e = hipErrorInvalidValue;  // recycled handle bytes
         }
         (void)hipGetLastError();
-        failed.push_back(p);  // keep it alive so the next try gets another range
+        failed.push_back(p);  // keep it alive so the next try gets another range and handle
     }
     for (void *p : failed) (void)hipFree(p);
     return e;
@@ -1343,9 +1432,10 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
     if (rc != OMPI_AMD_SUCCESS) { delete c; return rc; }
     // device resources: fine-grained flags, scratch, pinned error word
     c->scratch_bytes = std::max<size_t>(c->small_bytes, 4 << 20);  // per half
-    hipError_t e = hipExtMallocWithFlags((void **)&c->flags, 4096, hipDeviceMallocUncached);
+    ipc_blob mine{}, all[kMaxRanks];
+    hipError_t e = alloc_exportable(4096, (char **)&c->flags, &mine.flags, true);
     if (e == hipSuccess) e = hipMemsetAsync(c->flags, 0, 4096, nullptr);
-    if (e == hipSuccess) e = hipMalloc((void **)&c->scratch, 2 * c->scratch_bytes);
+    if (e == hipSuccess) e = alloc_exportable(2 * c->scratch_bytes, &c->scratch, &mine.scratch);
     if (e == hipSuccess) e = hipHostMalloc((void **)&c->err_host, 64, hipHostMallocMapped);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&c->err_dev, c->err_host, 0);
     if (e == hipSuccess) e = hipStreamSynchronize(nullptr);  // the flag page is zero
@@ -1355,14 +1445,6 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
         return rc;
     }
     *c->err_host = 0;
-    ipc_blob mine{}, all[kMaxRanks];
-    e = hipIpcGetMemHandle(&mine.flags, c->flags);
-    if (e == hipSuccess) e = hipIpcGetMemHandle(&mine.scratch, c->scratch);
-    if (e != hipSuccess) {
-        rc = record_hip(e, "hipIpcGetMemHandle (comm)");
-        ompi_amd_comm_destroy(c);
-        return rc;
-    }
     if (rank == 0) rc = p2p_create(c, name, rank, size, 0, &c->p2p);
     if (rc == OMPI_AMD_SUCCESS) rc = c->boot.allgather(&mine, all, sizeof(ipc_blob));
     if (rc == OMPI_AMD_SUCCESS && rank != 0) rc = p2p_create(c, name, rank, size, 1, &c->p2p);
@@ -1535,6 +1617,9 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "stale_same_handle")) *v = c->stale_same_handle;
     else if (!strcmp(key, "shadowed")) *v = c->shadowed;
     else if (!strcmp(key, "epoch")) *v = (int64_t)c->epoch;
+    else if (!strcmp(key, "exports_new")) *v = c->exports_new;
+    else if (!strcmp(key, "recycled_exports")) *v = c->recycled_exports;
+    else if (!strcmp(key, "imports_new")) *v = c->imports_new;
     else if (!strcmp(key, "force_shadow")) *v = c->force_shadow;
     else if (!strcmp(key, "imports")) *v = (int64_t)c->imports.size();
     else {
@@ -2024,6 +2109,19 @@ p2p_state *comm_p2p(ompi_amd_comm_t *c) { return c->p2p; }
 
 int comm_allgather(ompi_amd_comm_t *c, const void *mine, void *all, size_t len) {
     return c->boot.allgather(mine, all, len);
+}
+
+int comm_alloc_exportable(size_t bytes, bool uncached, void **out, ipc_desc *d) {
+    memset(d, 0, sizeof(*d));
+    char *p = nullptr;
+    const hipError_t e = alloc_exportable(bytes, &p, &d->h, uncached);
+    if (e != hipSuccess) return record_hip(e, "exportable allocation");
+    *out = p;
+    d->valid = 1;
+    d->id = buffer_id(p);
+    d->base = (uint64_t)(uintptr_t)p;
+    d->size = bytes;
+    return OMPI_AMD_SUCCESS;
 }
 
 int comm_export(ompi_amd_comm_t *c, const void *ptr, ipc_desc *d) {

@@ -35,6 +35,9 @@ int64_t comm_timeout_ms(const ompi_amd_comm_t *c);
 int *comm_err_dev(ompi_amd_comm_t *c);
 // Host rendezvous: every rank contributes len (<= 2048) bytes.
 int comm_allgather(ompi_amd_comm_t *c, const void *mine, void *all, size_t len);
+// A fresh device allocation whose IPC handle no earlier allocation of this
+// process had (uncached: fine-grained), described in *d.
+int comm_alloc_exportable(size_t bytes, bool uncached, void **out, ipc_desc *d);
 // Export a device buffer (cached per allocation).
 int comm_export(ompi_amd_comm_t *c, const void *ptr, ipc_desc *d);
 // Map a peer's exported buffer (cached, LRU).  pin: held until comm_unpin.

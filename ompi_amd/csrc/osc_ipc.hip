@@ -489,20 +489,18 @@ static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit
     w->owns_base = owns;
     int rc = comm_drain(c);  // collective order: deferred nonblocking calls first
     hipError_t e = hipSuccess;
+    ipc_desc ctl_desc{};
     if (rc == OMPI_AMD_SUCCESS) {
-        e = hipExtMallocWithFlags((void **)&w->ctl, CTL_BYTES, hipDeviceMallocUncached);
-        if (e == hipSuccess) e = hipMemset(w->ctl, 0, CTL_BYTES);
-        if (e == hipSuccess) e = hipDeviceSynchronize();
-        rc = record_hip(e, "osc control page");
+        rc = comm_alloc_exportable(CTL_BYTES, true, (void **)&w->ctl, &ctl_desc);
+        if (rc == OMPI_AMD_SUCCESS) e = hipMemset(w->ctl, 0, CTL_BYTES);
+        if (rc == OMPI_AMD_SUCCESS && e == hipSuccess) e = hipStreamSynchronize(nullptr);
+        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(e, "osc control page");
     }
     win_blob mine{}, all[kOscMaxRanks];
     mine.bytes = bytes;
     mine.disp_unit = disp_unit;
     if (rc == OMPI_AMD_SUCCESS && bytes) rc = comm_export(c, base, &mine.base);
-    if (rc == OMPI_AMD_SUCCESS) {
-        rc = record_hip(hipIpcGetMemHandle(&mine.ctl.h, w->ctl), "hipIpcGetMemHandle (osc)");
-        mine.ctl.valid = 1;
-    }
+    if (rc == OMPI_AMD_SUCCESS) mine.ctl = ctl_desc;
     // every rank takes part in the rendezvous, whatever failed locally
     mine.failed = rc == OMPI_AMD_SUCCESS ? 0 : 1;
     const int arc = comm_allgather(c, &mine, all, sizeof(win_blob));

@@ -220,7 +220,8 @@ def case_free_realloc(comm, rank, n, count, salt):
         torch.cuda.empty_cache()
         dist.barrier()  # every rank freed before anyone allocates again
     msgs.append(f"stale mappings closed so far: {comm.get_param('stale_closed')}, "
-                f"same handle bytes: {comm.get_param('stale_same_handle')}")
+                f"same handle bytes: {comm.get_param('stale_same_handle')}, "
+                f"recycled handles shadowed: {comm.get_param('recycled_exports')}")
     return len(msgs) == 1, "; ".join(msgs)
 
 
@@ -244,7 +245,12 @@ def case_persistent(comm, rank, n, dt, op, count, salt, inplace=False, starts=3)
             torch.cuda.synchronize()
             got = out.cpu().numpy()[:count * dt.extent].view(dt.np_dtype)
             if not fields_equal(got, exp[rank]):
-                return False, f"start {it} mismatch"
+                blocks = []
+                for b in range(n):  # which ring blocks are wrong, and from whom
+                    off, cnt = coll.block_partition(count, n, b)
+                    if not fields_equal(got[off:off + cnt], exp[rank][off:off + cnt]):
+                        blocks.append(b)
+                return False, f"start {it} mismatch in blocks {blocks}: {mismatch(got, exp[rank])}"
         return True, ""
     finally:
         plan.free()
@@ -630,13 +636,16 @@ def main():
         try:
             ok, msg = fn()
         except Exception as e:  # report and stop: later cases would hang
-            ok, msg = False, f"{type(e).__name__}: {e} {traceback.format_exc()[-400:]}"
+            ok, msg = False, (f"[epoch {comm.get_param('epoch')}] {type(e).__name__}: {e} "
+                              f"{traceback.format_exc()[-400:]}")
             report(rank, n, {"rank": rank, "case": name, "ok": ok, "msg": msg})
             ok_all = False
             break
-        if not ok:  # barrier epochs diverge when ranks launched different device work
-            msg = f"[epoch {comm.get_param('epoch')}] {msg}"
-        report(rank, n, {"rank": rank, "case": name, "ok": bool(ok), "msg": msg})
+        # barrier epochs diverge when ranks launched different device work
+        report(rank, n, {"rank": rank, "case": name, "ok": bool(ok), "msg": msg,
+                         "state": {k: comm.get_param(k) for k in (
+                             "epoch", "shadowed", "recycled_exports", "stale_closed", "exports_new",
+                             "imports_new", "imports", "landing_bytes")}})
         ok_all &= bool(ok)
     # zero-copy disabled: everything staged through the scratch
     if ok_all and not only and not os.environ.get("COLL_HEADLINE"):

@@ -85,6 +85,12 @@ static reply ex(int op, int s, size_t bytes = 0, int fill = 0) {
     rd(e2c[0], &r, sizeof(r));
     return r;
 }
+static unsigned long long hh(const hipIpcMemHandle_t &h) {  // FNV-1a of the handle bytes
+    unsigned long long x = 1469598103934665603ull;
+    for (size_t i = 0; i < sizeof(h); ++i) x = (x ^ (unsigned char)h.reserved[i]) * 1099511628211ull;
+    return x;
+}
+
 static void *exp_ptr[16];
 static int exp_fill[16];
 static reply H[16];
@@ -105,8 +111,8 @@ static void efree(int s) {
 static bool eexport(int s) {
     reply r = ex(2, s);
     H[s] = r;
-    printf("  E export s%d (%p id %llu) -> rc %d %s\n", s, r.ptr, r.id, r.rc,
-           r.rc ? hipGetErrorString((hipError_t)r.rc) : "");
+    printf("  E export s%d (%p id %llu) -> rc %d %s handle %016llx\n", s, r.ptr, r.id, r.rc,
+           r.rc ? hipGetErrorString((hipError_t)r.rc) : "", hh(r.h));
     return r.rc == 0;
 }
 static void *iopen(int s) {
@@ -223,6 +229,24 @@ static void scenario(int k) {
         iclose(m0, "stale m0"); iclose(m1, "stale m1");
         if (eexport(2)) { m2 = iopen(2); iclose(m2, "m2 after the stale closes"); }
         break;
+    case 13: {  // the collective pattern: mapping open, peer frees + reallocates the same
+                // size (same handle bytes?), importer closes the old mapping and opens the
+                // new handle at once; 30 rounds, contents checked every time
+        printf("S13: 30 x (open A; free A; alloc B same size; export B; close A; open B)\n");
+        alloc(0, 16, 0xd0); eexport(0); m0 = iopen(0);
+        for (int rnd = 1; rnd <= 30; ++rnd) {
+            const int a = (rnd - 1) & 1, b = rnd & 1;
+            unsigned long long ha = hh(H[a].h);
+            efree(a);
+            alloc(b, 16, 0xd0 + rnd);
+            eexport(b);
+            printf("  round %d: handle %s\n", rnd, hh(H[b].h) == ha ? "REUSED" : "new");
+            iclose(m0, "old");
+            m0 = iopen(b);
+        }
+        iclose(m0, "last");
+        break;
+    }
     case 11:  // the IMPORTER closes a peer mapping, then allocates and exports its own buffer
     case 12: {  // as 11, the mapping still open while it allocates
         printf("S%d: importer %s a peer mapping, then allocates + exports its own 16 MiB\n", k,
@@ -255,7 +279,7 @@ static void scenario(int k) {
 int main(int argc, char **argv) {
     setvbuf(stdout, nullptr, _IOLBF, 0);
     int k0 = argc > 1 ? atoi(argv[1]) : 1;
-    for (int k = k0; k <= 12; ++k) {
+    for (int k = k0; k <= 13; ++k) {
         if (pipe(c2e) || pipe(e2c)) return 1;
         fflush(stdout);
         pid_t e = fork();
