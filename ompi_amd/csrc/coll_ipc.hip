@@ -222,9 +222,22 @@ struct call_blob {
 
 // The parameters a path decision reads, captured when a nonblocking call is
 // posted so that its deferred launch takes the path every rank agreed on.
+struct fold_plan {
+    int order;   // ORDER_*
+    int first;   // virtual rank 0 of the uniform orders
+    int flags;   // FOLD_ROOT_INPLACE (the reduce of nonoverlapping)
+};
+enum {
+    TUNED_AR_FIXED = 0, TUNED_AR_BASIC_LINEAR = 1, TUNED_AR_NONOVERLAPPING = 2,
+    TUNED_AR_RECURSIVE_DOUBLING = 3, TUNED_AR_RING = 4, TUNED_AR_RING_SEGMENTED = 5,
+    TUNED_AR_RABENSEIFNER = 6, TUNED_AR_COUNT = 7
+};
+
 struct path_params {
     size_t small_bytes, fused_bytes;
     int zero_copy, algorithm;
+    int tuned_alg;      // coll_tuned_allreduce_algorithm the user forced (0: fixed decision)
+    int root0_inplace;  // forced nonoverlapping only: rank 0 passed MPI_IN_PLACE
 };
 
 // Export fallback.  hipIpcGetMemHandle sometimes refuses a live device
@@ -309,6 +322,7 @@ struct ompi_amd_comm {
     int64_t timeout_ms = 30000;
     int max_blocks = 1024;
     int algorithm = 0;
+    int tuned_alg = 0;                    // coll_tuned_allreduce_algorithm (forced), 0 = fixed
     // IPC caches
     struct exp_entry {
         void *base;
@@ -351,6 +365,8 @@ struct ompi_amd_plan {
     int64_t count = 0;
     int op = 0, type = 0;
     int kind = 0;      // 0: small paths (as a plain call), 1 pull, 2 pull+push, 3 push
+    ompi_amd::path_params pp{};  // the parameters (and forced algorithm) fixed at init
+    ompi_amd::fold_plan fp{};
     ptr_set sp{}, rp{};
     void *bases[OMPI_AMD_MAX_RANKS][2] = {};  // pinned peer mappings
     // completion: recorded on the start's stream at the first test / wait
@@ -1033,6 +1049,87 @@ static void ring_jobs(int64_t count, int n, red_jobs *jobs, int only_block) {
     }
 }
 
+// The operand order of one allreduce: the algorithm coll/tuned runs for
+// these arguments — its fixed decision (coll_tuned_decision_fixed.c:45-89)
+// or the one the user forced with coll_tuned_use_dynamic_rules +
+// coll_tuned_allreduce_algorithm (coll_tuned_allreduce_decision.c:37-147),
+// with each algorithm's own fallbacks.  Every path below folds every
+// element in this order, whichever rank computes it.
+static int pof2_floor(int n) {
+    int a = 1;
+    while (a * 2 <= n) a *= 2;
+    return a;
+}
+
+static fold_plan allreduce_fold(int n, int tuned_alg, size_t count, int type, bool root0_inplace) {
+    const size_t msg = type_size(type) * count;
+    const fold_plan tree{ORDER_TREE, 0, 0}, ring{ORDER_RING, 0, 0};
+    // basic_linear: basic linear reduce to 0 (acc = x[n-1]; acc = f(acc, x[i]),
+    // i = n-2 .. 0, coll_base_reduce.c:680-721) + bcast (:881-912)
+    const fold_plan linear{ORDER_CHAIN, 0, 0};
+    switch (tuned_alg) {
+    case TUNED_AR_BASIC_LINEAR: return linear;
+    case TUNED_AR_NONOVERLAPPING: {  // tuned reduce to 0 + bcast (:54-86)
+        const red_order ro = tuned_reduce_order(n, msg, count, 0, root0_inplace);
+        return {ro.order, ro.first, ro.flags};
+    }
+    case TUNED_AR_RECURSIVE_DOUBLING: return tree;
+    case TUNED_AR_RING:               // count < size: recursive doubling (:371-377)
+    case TUNED_AR_RING_SEGMENTED:     // too few segments: ring (:652-656), then as ring
+        return count < (size_t)n ? tree : ring;
+    case TUNED_AR_RABENSEIFNER:       // count < p': basic linear (:988-995)
+        return count < (size_t)pof2_floor(n) ? linear : fold_plan{ORDER_RABEN, 0, 0};
+    default:                          // the fixed decision: < 10000 B recursive doubling
+        return (msg < 10000 || count < (size_t)n) ? tree : ring;
+    }
+}
+
+// Rabenseifner: the piece of the vector vrank o ends up owning — the
+// recursive vector halving of :1122-1171 (the lower vrank of a pair keeps
+// the left floor(w/2) elements of the window).
+static void raben_piece(int64_t count, int n, int o, int64_t *lo, int64_t *cnt) {
+    int64_t l = 0, w = count;
+    for (int m = 1; m < pof2_floor(n); m <<= 1) {
+        const int64_t half = w / 2;
+        if (o & m) { l += half; w -= half; }
+        else w = half;
+    }
+    *lo = l;
+    *cnt = w;
+}
+
+// Jobs folding the elements of ring block `block` (every element: -1)
+// in plan p's order.
+static void fold_jobs(const fold_plan &p, int64_t count, int n, int block, red_jobs *jobs) {
+    if (p.order == ORDER_RING) {
+        ring_jobs(count, n, jobs, block);
+        return;
+    }
+    int64_t lo = 0, hi = count;
+    if (block >= 0) {
+        int64_t split, early, late;
+        blockcount(count, n, &split, &early, &late);
+        lo = block_off(block, split, early, late);
+        hi = lo + block_cnt(block, split, early, late);
+    }
+    jobs->n = 0;
+    if (p.order != ORDER_RABEN) {
+        red_job &j = jobs->j[jobs->n++];
+        j = red_job{lo, hi - lo, lo, p.first, -1};
+        return;
+    }
+    const int adj = pof2_floor(n);
+    for (int o = 0; o < adj; ++o) {  // one job per piece the range meets
+        int64_t plo, pcnt;
+        raben_piece(count, n, o, &plo, &pcnt);
+        const int64_t a = std::max(lo, plo), b = std::min(hi, plo + pcnt);
+        if (a >= b) continue;
+        red_job &j = jobs->j[jobs->n++];
+        j = red_job{a, b - a, a, 0, -1};
+        j.aux = o << 8;
+    }
+}
+
 static int stage_in(ompi_amd_comm_t *c, const void *src, size_t bytes, stage_half *sh,
                     hipStream_t s) {
     if (bytes > c->scratch_bytes) {
@@ -1092,7 +1189,8 @@ static bool two_shot_fits(const ompi_amd_comm_t *c, int64_t count, size_t ext) {
 }
 
 static int allreduce_staged_two_shot(ompi_amd_comm_t *c, const void *src, void *rbuf,
-                                     int64_t count, int op, int type, hipStream_t s) {
+                                     int64_t count, int op, int type, const fold_plan &fp,
+                                     hipStream_t s) {
     const int n = c->size, mine = (c->rank + 1) % n;
     const int64_t ext = (int64_t)ompi_amd_type_extent(type);
     const size_t res = two_shot_result_off((size_t)count * ext);
@@ -1105,8 +1203,8 @@ static int allreduce_staged_two_shot(ompi_amd_comm_t *c, const void *src, void *
     dst.p[0] = (const char *)rbuf;
     dst.p[1] = sh.mine + res + (offm & 15) - offm;
     red_jobs jobs;
-    ring_jobs(count, n, &jobs, mine);
-    TRY(launch_reduce(c, op, type, sh.peers, n, dst, 2, ORDER_RING, 0, jobs, s));
+    fold_jobs(fp, count, n, mine, &jobs);
+    TRY(launch_reduce(c, op, type, sh.peers, n, dst, 2, fp.order, fp.flags, jobs, s));
     TRY(launch_barrier(c, s));
     cp_jobs cj{};
     for (int b = 0; b < n; ++b) {
@@ -1122,14 +1220,14 @@ static int allreduce_staged_two_shot(ompi_amd_comm_t *c, const void *src, void *
 // sp / rp: every rank's input and rbuf as this rank maps them (sp = rp in
 // place); push needs rp only, and the landing buffer sized by push_slot.
 static int allreduce_pull(ompi_amd_comm_t *c, const ptr_set &sp, const ptr_set &rp, void *rbuf,
-                          int64_t count, int op, int type, hipStream_t s) {
+                          int64_t count, int op, int type, const fold_plan &fp, hipStream_t s) {
     const int n = c->size, mine = (c->rank + 1) % n;
     const int64_t ext = (int64_t)ompi_amd_type_extent(type);
     TRY(launch_barrier(c, s));
     red_jobs jobs;
-    ring_jobs(count, n, &jobs, mine);
+    fold_jobs(fp, count, n, mine, &jobs);
     TRY(timed_phase(c, 0, s, [&] {
-        return launch_reduce(c, op, type, sp, n, one_ptr(rbuf), 1, ORDER_RING, 0, jobs, s);
+        return launch_reduce(c, op, type, sp, n, one_ptr(rbuf), 1, fp.order, fp.flags, jobs, s);
     }));
     TRY(launch_barrier(c, s));
     int64_t split, early, late;
@@ -1146,15 +1244,16 @@ static int allreduce_pull(ompi_amd_comm_t *c, const ptr_set &sp, const ptr_set &
 }
 
 static int allreduce_pull_push(ompi_amd_comm_t *c, const ptr_set &sp, const ptr_set &rp,
-                               int64_t count, int op, int type, hipStream_t s) {
+                               int64_t count, int op, int type, const fold_plan &fp,
+                               hipStream_t s) {
     // in place, sp = rp: only the owner of a block touches it
     const int n = c->size, mine = (c->rank + 1) % n;
     TRY(launch_barrier(c, s));
     red_jobs jobs;
-    ring_jobs(count, n, &jobs, mine);
+    fold_jobs(fp, count, n, mine, &jobs);
     const ptr_set dsts = push_order(c, rp);
     TRY(timed_phase(c, 0, s, [&] {
-        return launch_reduce(c, op, type, sp, n, dsts, n, ORDER_RING, 0, jobs, s);
+        return launch_reduce(c, op, type, sp, n, dsts, n, fp.order, fp.flags, jobs, s);
     }));
     return launch_barrier(c, s);
 }
@@ -1168,7 +1267,7 @@ static size_t push_slot(int64_t count, int n, int type) {
 }
 
 static int allreduce_push(ompi_amd_comm_t *c, const void *src, const ptr_set &rp, int64_t count,
-                          int op, int type, hipStream_t s) {
+                          int op, int type, const fold_plan &fp, hipStream_t s) {
     const int n = c->size, mine = (c->rank + 1) % n;
     const int64_t ext = (int64_t)ompi_amd_type_extent(type);
     int64_t split, early, late;
@@ -1192,10 +1291,10 @@ static int allreduce_push(ompi_amd_comm_t *c, const void *src, const ptr_set &rp
         srcs.p[r] = (r == c->rank) ? (const char *)src
                                    : c->land + (size_t)r * slot + (offm & 15) - offm;
     red_jobs jobs;
-    ring_jobs(count, n, &jobs, mine);
+    fold_jobs(fp, count, n, mine, &jobs);
     const ptr_set dsts = push_order(c, rp);
     TRY(timed_phase(c, 0, s, [&] {
-        return launch_reduce(c, op, type, srcs, n, dsts, n, ORDER_RING, 0, jobs, s);
+        return launch_reduce(c, op, type, srcs, n, dsts, n, fp.order, fp.flags, jobs, s);
     }));
     return launch_barrier(c, s);
 }
@@ -1282,7 +1381,7 @@ static int scan_common(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
 }  // namespace ompi_amd
 
 static path_params params_of(const ompi_amd_comm_t *c) {
-    return {c->small_bytes, c->fused_bytes, c->zero_copy, c->algorithm};
+    return {c->small_bytes, c->fused_bytes, c->zero_copy, c->algorithm, c->tuned_alg, 0};
 }
 
 // Whether an allreduce of `count` elements takes a zero-copy path (and so
@@ -1293,13 +1392,27 @@ static bool allreduce_swaps(const ompi_amd_comm_t *c, const path_params &pp, siz
     const int n = c->size;
     if (n == 1 || count == 0) return false;
     const size_t bytes = count * ompi_amd_type_extent(type);
-    const bool tree = type_size(type) * count < 10000 || count < (size_t)n;
-    if (bytes <= pp.fused_bytes && bytes <= c->scratch_bytes) return false;
-    return !(bytes <= pp.small_bytes || !pp.zero_copy || tree);
+    const fold_plan fp = allreduce_fold(n, pp.tuned_alg, count, type, pp.root0_inplace != 0);
+    const bool tree = fp.order == ORDER_TREE;
+    if ((tree || fp.order == ORDER_RING) && bytes <= pp.fused_bytes && bytes <= c->scratch_bytes)
+        return false;
+    return !(bytes <= pp.small_bytes || !pp.zero_copy || (tree && bytes <= c->scratch_bytes));
 }
 
 static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                           int op, hipStream_t s, const path_params &pp);
+
+// Forced nonoverlapping only: every rank must know whether rank 0 passed
+// MPI_IN_PLACE (it changes rank 0's first combine of the reduce,
+// coll_base_allreduce.c:54-86); one host exchange, then in pp.
+static int agree_root0_inplace(ompi_amd_comm_t *c, path_params *pp, bool inplace) {
+    pp->root0_inplace = 0;
+    if (pp->tuned_alg != TUNED_AR_NONOVERLAPPING || c->size == 1) return OMPI_AMD_SUCCESS;
+    int mine = inplace ? 1 : 0, all[kMaxRanks];
+    TRY(c->boot.allgather(&mine, all, sizeof(int)));
+    pp->root0_inplace = all[0];
+    return OMPI_AMD_SUCCESS;
+}
 
 // Launch deferred nonblocking calls in posting order, each once every rank
 // has posted its handle-swap half; block = wait for them (the blocking entry
@@ -1349,28 +1462,23 @@ static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size
         if (inplace) return OMPI_AMD_SUCCESS;
         return record_hip(hipMemcpyAsync(rbuf, src, bytes, hipMemcpyDeviceToDevice, s), "copy");
     }
-    // order of coll/tuned's fixed decision: < 10000 B recursive doubling
-    const bool tree = type_size(type) * count < 10000 || count < (size_t)n;
-    if (bytes <= pp.fused_bytes && bytes <= c->scratch_bytes)
+    // the operand order coll/tuned would use (fixed decision or forced)
+    const fold_plan fp = allreduce_fold(n, pp.tuned_alg, count, type, pp.root0_inplace != 0);
+    const bool tree = fp.order == ORDER_TREE;
+    if ((tree || fp.order == ORDER_RING) && bytes <= pp.fused_bytes && bytes <= c->scratch_bytes)
         return allreduce_fused(c, src, rbuf, (int64_t)count, op, type, tree, s);
     if (!tree && (bytes <= pp.small_bytes || !pp.zero_copy) &&
         two_shot_fits(c, (int64_t)count, ext))
-        return allreduce_staged_two_shot(c, src, rbuf, (int64_t)count, op, type, s);
-    if (bytes <= pp.small_bytes || !pp.zero_copy || tree) {
+        return allreduce_staged_two_shot(c, src, rbuf, (int64_t)count, op, type, fp, s);
+    if (bytes <= pp.small_bytes || !pp.zero_copy || (tree && bytes <= c->scratch_bytes)) {
         // staged one-shot: my contribution -> my scratch half, barrier,
         // every rank folds all blocks from all scratches (no trailing
         // barrier: see next_half)
         stage_half sh;
         TRY(stage_in(c, src, bytes, &sh, s));
         red_jobs jobs;
-        if (tree) {
-            jobs.n = 1;
-            jobs.j[0] = {0, (int64_t)count, 0, 0, -1};
-        } else {
-            ring_jobs((int64_t)count, n, &jobs, -1);
-        }
-        return launch_reduce(c, op, type, sh.peers, n, one_ptr(rbuf), 1,
-                             tree ? ORDER_TREE : ORDER_RING, 0, jobs, s);
+        fold_jobs(fp, (int64_t)count, n, -1, &jobs);
+        return launch_reduce(c, op, type, sh.peers, n, one_ptr(rbuf), 1, fp.order, fp.flags, jobs, s);
     }
     ptr_set sp{}, rp{};
     // export fallback (shadow_plan); a deferred call substituted its
@@ -1394,13 +1502,13 @@ static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size
     if (push) {
         TRY(ensure_landing(c, push_slot((int64_t)count, n, type) * (size_t)n));
         TRY(exchange_bufs(c, nullptr, rbuf, &sp, &rp));
-        rc = allreduce_push(c, src, rp, (int64_t)count, op, type, s);
+        rc = allreduce_push(c, src, rp, (int64_t)count, op, type, fp, s);
     } else {
         TRY(exchange_bufs(c, src, rbuf, &sp, &rp));
         if (inplace) sp = rp;
         rc = pp.algorithm == ALG_PULL_PUSH
-                 ? allreduce_pull_push(c, sp, rp, (int64_t)count, op, type, s)
-                 : allreduce_pull(c, sp, rp, rbuf, (int64_t)count, op, type, s);
+                 ? allreduce_pull_push(c, sp, rp, (int64_t)count, op, type, fp, s)
+                 : allreduce_pull(c, sp, rp, rbuf, (int64_t)count, op, type, fp, s);
     }
     TRY(rc);
     return shadow_out(c, sh, s);
@@ -1423,6 +1531,12 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
     }
     c->device = device;
     if (const char *t = getenv("OMPI_AMD_COLL_TIMEOUT_MS")) c->timeout_ms = atoll(t);
+    // coll/tuned's own forcing variables (coll_tuned_allreduce_decision.c:
+    // 37-101): honoured when dynamic rules are on, as tuned does
+    if (const char *d = getenv("OMPI_MCA_coll_tuned_use_dynamic_rules")) {
+        const char *a = getenv("OMPI_MCA_coll_tuned_allreduce_algorithm");
+        if (atoi(d) && a && atoi(a) >= 0 && atoi(a) < TUNED_AR_COUNT) c->tuned_alg = atoi(a);
+    }
     if (const char *a = getenv("OMPI_AMD_COLL_ALGORITHM")) {
         const int v = atoi(a);
         if (v >= 0 && v < ALG_COUNT) c->algorithm = v;
@@ -1596,6 +1710,9 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
         c->algorithm = (int)v;
     } else if (!strcmp(key, "force_shadow")) {
         c->force_shadow = v ? 1 : 0;
+    } else if (!strcmp(key, "tuned_allreduce_algorithm")) {
+        if (v < 0 || v >= TUNED_AR_COUNT) return OMPI_AMD_ERR_BAD_PARAM;
+        c->tuned_alg = (int)v;
     } else {
         record_msg("unknown coll param '%s'", key);
         return OMPI_AMD_ERR_BAD_PARAM;
@@ -1612,6 +1729,7 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "blocks")) *v = c->max_blocks;
     else if (!strcmp(key, "fused_bytes")) *v = (int64_t)c->fused_bytes;
     else if (!strcmp(key, "algorithm")) *v = c->algorithm;
+    else if (!strcmp(key, "tuned_allreduce_algorithm")) *v = c->tuned_alg;
     else if (!strcmp(key, "landing_bytes")) *v = (int64_t)c->land_bytes;
     else if (!strcmp(key, "stale_closed")) *v = c->stale_closed;
     else if (!strcmp(key, "stale_same_handle")) *v = c->stale_same_handle;
@@ -1636,7 +1754,9 @@ int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
     TRY(check_sticky(c));
     TRY(drain(c));
-    return allreduce_impl(c, sbuf, rbuf, count, type, op, as_stream(stream), params_of(c));
+    path_params pp = params_of(c);
+    TRY(agree_root0_inplace(c, &pp, in_place(sbuf, rbuf)));
+    return allreduce_impl(c, sbuf, rbuf, count, type, op, as_stream(stream), pp);
 }
 
 int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
@@ -1654,8 +1774,17 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
         delete req;
         return rc;
     }
-    const path_params pp = params_of(c);
+    path_params pp = params_of(c);
     const bool inplace = in_place(sbuf, rbuf);
+    if (pp.tuned_alg == TUNED_AR_NONOVERLAPPING) {  // a host exchange, in order with the others
+        rc = drain(c);
+        if (rc == OMPI_AMD_SUCCESS) rc = agree_root0_inplace(c, &pp, inplace);
+        if (rc != OMPI_AMD_SUCCESS) {
+            (void)hipEventDestroy(req->ev);
+            delete req;
+            return rc;
+        }
+    }
     pending_op o{0, inplace ? rbuf : sbuf, rbuf, count, type, op, as_stream(stream), pp, req};
     if (allreduce_swaps(c, pp, count, type)) {
         // post this rank's half of the handle swap now; the launch waits for
@@ -1942,10 +2071,14 @@ int ompi_amd_allreduce_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, si
     pl->count = (int64_t)count;
     pl->op = op;
     pl->type = type;
-    const bool tree = type_size(type) * count < 10000 || count < (size_t)n;
-    const bool small = n == 1 || count == 0 || (bytes <= c->fused_bytes && bytes <= c->scratch_bytes) ||
-                       bytes <= c->small_bytes || !c->zero_copy || tree;
-    int rc = OMPI_AMD_SUCCESS;
+    pl->pp = params_of(c);
+    int rc = agree_root0_inplace(c, &pl->pp, inplace);
+    if (rc != OMPI_AMD_SUCCESS) {
+        delete pl;
+        return rc;
+    }
+    const bool small = n == 1 || count == 0 || !allreduce_swaps(c, pl->pp, count, type);
+    pl->fp = allreduce_fold(n, pl->pp.tuned_alg, count, type, pl->pp.root0_inplace != 0);
     if (!small) {
         pl->kind = c->algorithm == ALG_PUSH ? 3 : c->algorithm == ALG_PULL_PUSH ? 2 : 1;
         if (pl->kind == 3) rc = ensure_landing(c, push_slot(pl->count, n, type) * (size_t)n);
@@ -1973,9 +2106,12 @@ int ompi_amd_allreduce_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, si
 
 static int plan_enqueue(ompi_amd_plan_t *pl, void *stream) {
     ompi_amd_comm_t *c = pl->c;
-    if (pl->kind == 0)
-        return ompi_amd_allreduce(c, pl->src == pl->rbuf ? (const void *)1 : pl->src, pl->rbuf,
-                                  (size_t)pl->count, pl->type, pl->op, stream);
+    if (pl->kind == 0) {  // the small paths: a plain call with the parameters of the init
+        TRY(check_sticky(c));
+        TRY(drain(c));
+        return allreduce_impl(c, pl->src == pl->rbuf ? (const void *)1 : pl->src, pl->rbuf,
+                              (size_t)pl->count, pl->type, pl->op, as_stream(stream), pl->pp);
+    }
     TRY(check_sticky(c));
     TRY(set_dev(c));
     hipStream_t s = as_stream(stream);
@@ -1984,11 +2120,11 @@ static int plan_enqueue(ompi_amd_plan_t *pl, void *stream) {
     if (pl->kind == 3) {
         // another call may have grown (and so moved) the landing buffer:
         // its size only grows, so the slots still fit
-        rc = allreduce_push(c, pl->src, pl->rp, pl->count, pl->op, pl->type, s);
+        rc = allreduce_push(c, pl->src, pl->rp, pl->count, pl->op, pl->type, pl->fp, s);
     } else if (pl->kind == 2) {
-        rc = allreduce_pull_push(c, pl->sp, pl->rp, pl->count, pl->op, pl->type, s);
+        rc = allreduce_pull_push(c, pl->sp, pl->rp, pl->count, pl->op, pl->type, pl->fp, s);
     } else {
-        rc = allreduce_pull(c, pl->sp, pl->rp, pl->rbuf, pl->count, pl->op, pl->type, s);
+        rc = allreduce_pull(c, pl->sp, pl->rp, pl->rbuf, pl->count, pl->op, pl->type, pl->fp, s);
     }
     TRY(rc);
     return shadow_out(c, pl->sh, s);

@@ -30,6 +30,7 @@ enum order_t {
     ORDER_BINOMIAL = 3,  // in-order binomial tree rooted at `first`
     ORDER_BINARY = 4,    // binary tree rooted at `first`
     ORDER_HALVING = 5,   // recursive-halving reduce_scatter, owner tmp rank in flags >> 8
+    ORDER_RABEN = 6,     // Rabenseifner allreduce (redscat_allgather), owner vrank in flags >> 8
 };
 // The root passed MPI_IN_PLACE: its first combine is f(own, child)
 // (coll_base_reduce.c:170-171, 196-199).
@@ -41,8 +42,10 @@ struct red_job {
     int64_t off, cnt, off_dst;
     int first;  // virtual rank 0 (ring block b, tree root)
     int head;   // elements before the 16-B aligned body; -1: no common alignment
+    int aux = 0;  // per-job fold flags, or-ed into the launch's (ORDER_RABEN: owner vrank << 8)
 };
-struct red_jobs { red_job j[kMaxRanks]; int n; };
+// a ring block cut at the Rabenseifner pieces: up to kMaxRanks + 1 jobs
+struct red_jobs { red_job j[2 * kMaxRanks]; int n; };
 
 struct cp_job { const char *src; char *dst; int64_t bytes; };
 struct cp_jobs { cp_job j[kMaxRanks]; int n; };
@@ -138,6 +141,43 @@ __device__ __forceinline__ T fold(const T (&v)[kMaxRanks], int n, int order, int
             if (c1 < kMaxRanks && c1 < n) w[s] = F::template f<T>(w[s], w[c1]);
         }
         return w[0];
+    }
+    if (order == ORDER_RABEN) {
+        // redscat_allgather (coll_base_allreduce.c:970-1243).  Step 1: the
+        // 2*rem lowest ranks pair up; the even one keeps the left half of
+        // the vector as f(even, odd), the odd one the right half as
+        // f(odd, even) (:1031-1080) — the owner's bit 0 says which half
+        // this element is in.  Step 2: recursive halving over the p' vranks
+        // with masks 1, 2, 4, ... (:1122-1171): at every mask the vrank
+        // keeping the element's part does f(mine, partner's).  o = the
+        // vrank the element ends on.
+        int adj = 1;
+        while (adj * 2 <= n) adj *= 2;
+        const int rem = n - adj;
+        const int o = (flags >> 8) & 0xff;
+        const bool right = (o & 1) != 0;
+        T w[kMaxRanks];
+#pragma unroll
+        for (int u = 0; u < kMaxRanks; ++u) {
+            if (2 * u + 1 < kMaxRanks && u < rem)
+                w[u] = right ? F::template f<T>(v[2 * u + 1], v[2 * u])
+                             : F::template f<T>(v[2 * u], v[2 * u + 1]);
+            else if (u < adj)
+                w[u] = v[u + rem < kMaxRanks ? u + rem : 0];
+        }
+#pragma unroll
+        for (int m = 1; m < kMaxRanks; m <<= 1) {
+            if (m < adj) {
+#pragma unroll
+                for (int u = 0; u < kMaxRanks; ++u)
+                    if (u < adj && (u & m) == (o & m)) w[u] = F::template f<T>(w[u], w[u ^ m]);
+            }
+        }
+        T r = w[0];
+#pragma unroll
+        for (int u = 1; u < kMaxRanks; ++u)
+            if (u == o) r = w[u];
+        return r;
     }
     if (order == ORDER_HALVING) {
         // recursive-halving reduce_scatter (coll_base_reduce_scatter.c:
@@ -241,7 +281,7 @@ __global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, ptr_s
             T s[kMaxRanks];
 #pragma unroll
             for (int j = 0; j < kMaxRanks; ++j) s[j] = v[j].e[e];
-            out.e[e] = fold<T, OP>(s, n, order, flags);
+            out.e[e] = fold<T, OP>(s, n, order, flags | jb.aux);
         }
 #pragma unroll
         for (int k = 0; k < kMaxRanks; ++k)
@@ -256,7 +296,7 @@ __global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, ptr_s
         const int64_t e = k < head ? k : tail0 + (k - head);
         T s[kMaxRanks];
         gather_scalar<T>(s, src, n, jb.first, jb.off + e);
-        const T r = fold<T, OP>(s, n, order, flags);
+        const T r = fold<T, OP>(s, n, order, flags | jb.aux);
 #pragma unroll
         for (int d = 0; d < kMaxRanks; ++d)
             if (d < ndst)

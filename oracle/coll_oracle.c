@@ -11,6 +11,10 @@
  *   recursive doubl.  coll_base_allreduce.c:130-274
  *   ring              coll_base_allreduce.c:341-536
  *   ring segmented    coll_base_allreduce.c:618-856
+ *   basic linear      coll_base_allreduce.c:881-912 (linear reduce to 0 + bcast)
+ *   nonoverlapping    coll_base_allreduce.c:54-86 (tuned reduce to 0 + bcast)
+ *   redscat_allgather coll_base_allreduce.c:970-1243 (Rabenseifner)
+ *   forced selection  coll_tuned_allreduce_decision.c:130-150
  *   block partition   coll_base_functions.h:425-431 (COMPUTE_BLOCKCOUNT)
  *   segment count     coll_base_functions.h:407-416 (COMPUTED_SEGCOUNT)
  *
@@ -244,8 +248,125 @@ static int ar_ring_segmented(int n, const void *const *sb, void *const *rb,
     return ORC_AR_RING_SEGMENTED;
 }
 
+/* ---------------- reduce to 0 + bcast ---------------- */
+static int ar_reduce_bcast(int n, const void *const *sb, void *const *rb, size_t count, int op,
+                           int type, int red_alg, int root0_inplace, int ret)
+{
+    const size_t bytes = count * orc_type_extent(type);
+    char *acc = malloc(bytes ? bytes : 1);
+    int r;
+    if (orc_reduce(red_alg, n, sb, acc, count, op, type, 0, root0_inplace) < 0) {
+        free(acc);
+        return -1;
+    }
+    for (r = 0; r < n; r++) memcpy(rb[r], acc, bytes);   /* bcast from 0 */
+    free(acc);
+    return ret;
+}
+
+/* ---------------- Rabenseifner (redscat_allgather) ---------------- */
+static int ar_redscat_allgather(int n, const void *const *sb, void *const *rb, size_t count,
+                                int op, int type)
+{
+    const size_t ext = orc_type_extent(type), bytes = count * ext;
+    int nsteps = 0, p2 = 1, rem, r, step, mask;
+    size_t lh, rh;
+    char **tmp, **msg;
+    int *vrank;
+    size_t *rindex, *sindex, *rcount, *scount, *wsize;
+    while (p2 * 2 <= n) { p2 *= 2; nsteps++; }
+    if (count < (size_t)p2)                                   /* :988-995 */
+        return ar_reduce_bcast(n, sb, rb, count, op, type, ORC_RED_LINEAR, 0,
+                               ORC_AR_BASIC_LINEAR);
+    rem = n - p2;
+    tmp = calloc((size_t)n, sizeof(char *));
+    msg = calloc((size_t)n, sizeof(char *));
+    vrank = calloc((size_t)n, sizeof(int));
+    rindex = calloc((size_t)n * (size_t)(nsteps + 1), sizeof(size_t));
+    sindex = calloc((size_t)n * (size_t)(nsteps + 1), sizeof(size_t));
+    rcount = calloc((size_t)n * (size_t)(nsteps + 1), sizeof(size_t));
+    scount = calloc((size_t)n * (size_t)(nsteps + 1), sizeof(size_t));
+    wsize = calloc((size_t)n, sizeof(size_t));
+    for (r = 0; r < n; r++) {
+        tmp[r] = malloc(bytes ? bytes : 1);
+        msg[r] = malloc(bytes ? bytes : 1);
+        if (sb[r] != rb[r]) memcpy(rb[r], sb[r], bytes);      /* :1006-1010 */
+    }
+    /* step 1 (:1031-1086): even/odd pairs of the 2*rem lowest ranks */
+    lh = count / 2;
+    rh = count - lh;
+    for (r = 0; r < n; r++) memcpy(msg[r], rb[r], bytes);   /* sendrecv: values before the step */
+    for (r = 0; r < 2 * rem; r++) {
+        if (r % 2) {   /* odd: recv the right half from r-1, reduce it */
+            memcpy(tmp[r] + lh * ext, msg[r - 1] + lh * ext, rh * ext);
+            orc_op_2buff(op, type, tmp[r] + lh * ext, (char *)rb[r] + lh * ext, rh);
+        } else {       /* even: recv the left half from r+1, reduce it */
+            memcpy(tmp[r], msg[r + 1], lh * ext);
+            orc_op_2buff(op, type, tmp[r], rb[r], lh);
+        }
+    }
+    for (r = 0; r < 2 * rem; r += 2)  /* the odd rank sends its right half back */
+        memcpy((char *)rb[r] + lh * ext, (char *)rb[r + 1] + lh * ext, rh * ext);
+    for (r = 0; r < n; r++)
+        vrank[r] = r < 2 * rem ? (r % 2 ? -1 : r / 2) : r - rem;
+    /* step 2 (:1104-1171): recursive vector halving, distance doubling */
+    for (r = 0; r < n; r++) wsize[r] = count;
+    for (step = 0, mask = 1; mask < p2; mask <<= 1, step++) {
+        for (r = 0; r < n; r++) memcpy(msg[r], rb[r], bytes);
+        for (r = 0; r < n; r++) {
+            size_t *ri = rindex + (size_t)r * (nsteps + 1), *si = sindex + (size_t)r * (nsteps + 1);
+            size_t *rc = rcount + (size_t)r * (nsteps + 1), *sc = scount + (size_t)r * (nsteps + 1);
+            int vdest, dest;
+            if (vrank[r] < 0) continue;
+            vdest = vrank[r] ^ mask;
+            dest = vdest < rem ? vdest * 2 : vdest + rem;
+            if (r < dest) {
+                rc[step] = wsize[r] / 2;
+                sc[step] = wsize[r] - rc[step];
+                si[step] = ri[step] + rc[step];
+            } else {
+                sc[step] = wsize[r] / 2;
+                rc[step] = wsize[r] - sc[step];
+                ri[step] = si[step] + sc[step];
+            }
+            /* dest sends rbuf[its sindex ..], which is our [rindex ..] */
+            memcpy(tmp[r] + ri[step] * ext, msg[dest] + ri[step] * ext, rc[step] * ext);
+            orc_op_2buff(op, type, tmp[r] + ri[step] * ext, (char *)rb[r] + ri[step] * ext, rc[step]);
+            if (step + 1 < nsteps) {
+                ri[step + 1] = ri[step];
+                si[step + 1] = ri[step];
+                wsize[r] = rc[step];
+            }
+        }
+    }
+    /* step 3 (:1183-1206): allgather, reverse order */
+    for (step = nsteps - 1, mask = p2 >> 1; mask > 0; mask >>= 1, step--) {
+        for (r = 0; r < n; r++) memcpy(msg[r], rb[r], bytes);
+        for (r = 0; r < n; r++) {
+            size_t *si = sindex + (size_t)r * (nsteps + 1), *sc = scount + (size_t)r * (nsteps + 1);
+            int vdest, dest;
+            if (vrank[r] < 0) continue;
+            vdest = vrank[r] ^ mask;
+            dest = vdest < rem ? vdest * 2 : vdest + rem;
+            memcpy((char *)rb[r] + si[step] * ext, msg[dest] + si[step] * ext, sc[step] * ext);
+        }
+    }
+    /* step 4 (:1212-1228): the excluded odd ranks get the result */
+    for (r = 1; r < 2 * rem; r += 2) memcpy(rb[r], rb[r - 1], bytes);
+    for (r = 0; r < n; r++) { free(tmp[r]); free(msg[r]); }
+    free(tmp); free(msg); free(vrank); free(rindex); free(sindex); free(rcount); free(scount);
+    free(wsize);
+    return ORC_AR_REDSCAT_ALLGATHER;
+}
+
 int orc_allreduce(int algorithm, int n, const void *const *sb, void *const *rb,
                   size_t count, int op, int type, size_t segsize)
+{
+    return orc_allreduce_forced(algorithm, n, sb, rb, count, op, type, segsize, 0);
+}
+
+int orc_allreduce_forced(int algorithm, int n, const void *const *sb, void *const *rb,
+                         size_t count, int op, int type, size_t segsize, int root0_inplace)
 {
     const size_t ext = orc_type_extent(type);
     if (n < 1 || ext == 0 || !orc_op_defined(op, type)) return -1;
@@ -270,10 +391,16 @@ int orc_allreduce(int algorithm, int n, const void *const *sb, void *const *rb,
         return -2; /* nonoverlapping: not restated */
     }
     switch (algorithm) {
+    case ORC_AR_BASIC_LINEAR:
+        return ar_reduce_bcast(n, sb, rb, count, op, type, ORC_RED_LINEAR, 0, ORC_AR_BASIC_LINEAR);
+    case ORC_AR_NONOVERLAPPING:
+        return ar_reduce_bcast(n, sb, rb, count, op, type, ORC_RED_TUNED, root0_inplace,
+                               ORC_AR_NONOVERLAPPING);
     case ORC_AR_RECURSIVE_DOUBLING: return ar_recursive_doubling(n, sb, rb, count, op, type);
     case ORC_AR_RING: return ar_ring(n, sb, rb, count, op, type);
     case ORC_AR_RING_SEGMENTED:
         return ar_ring_segmented(n, sb, rb, count, op, type, segsize ? segsize : (1u << 20));
+    case ORC_AR_REDSCAT_ALLGATHER: return ar_redscat_allgather(n, sb, rb, count, op, type);
     default: return -2;
     }
 }

@@ -61,6 +61,8 @@ int    orc_op_3buff(int op, int type, const void *in1, const void *in2,
 /* ---- coll/base allreduce restatement (coll_base_allreduce.c) ---- */
 enum {
     ORC_AR_TUNED = 0,              /* coll_tuned_decision_fixed.c:45-89 */
+    ORC_AR_BASIC_LINEAR = 1,       /* coll_base_allreduce.c:881-912 */
+    ORC_AR_NONOVERLAPPING = 2,     /* coll_base_allreduce.c:54-86 */
     ORC_AR_RECURSIVE_DOUBLING = 3, /* coll_base_allreduce.c:130-274 */
     ORC_AR_RING = 4,               /* coll_base_allreduce.c:341-536 */
     ORC_AR_RING_SEGMENTED = 5,     /* coll_base_allreduce.c:618-856 */
@@ -73,6 +75,14 @@ enum {
 int orc_allreduce(int algorithm, int nranks, const void *const *sbufs,
                   void *const *rbufs, size_t count, int op, int type,
                   size_t segsize);
+
+/* The algorithm a user forced (coll_tuned_use_dynamic_rules +
+ * coll_tuned_allreduce_algorithm, coll_tuned_allreduce_decision.c:130-150,
+ * numbering as above), with each algorithm's fallbacks; root0_inplace: rank
+ * 0 passed MPI_IN_PLACE (changes nonoverlapping's reduce). */
+int orc_allreduce_forced(int algorithm, int nranks, const void *const *sbufs,
+                         void *const *rbufs, size_t count, int op, int type,
+                         size_t segsize, int root0_inplace);
 
 /* Block partition COLL_BASE_COMPUTE_BLOCKCOUNT (coll_base_functions.h:425-431) */
 void orc_blockcount(size_t count, int nblocks, size_t *split,

@@ -18,6 +18,7 @@ LIB_PATH = os.path.join(_HERE, "liboracle.so")
 _lib = None
 
 ALG_TUNED, ALG_RECURSIVE_DOUBLING, ALG_RING, ALG_RING_SEGMENTED = 0, 3, 4, 5
+ALG_BASIC_LINEAR, ALG_NONOVERLAPPING, ALG_REDSCAT_ALLGATHER = 1, 2, 6
 
 
 class Block(ctypes.Structure):
@@ -44,6 +45,9 @@ def lib():
         L.orc_allreduce.argtypes = [c.c_int, c.c_int, c.POINTER(c.c_void_p),
                                     c.POINTER(c.c_void_p), c.c_size_t, c.c_int, c.c_int,
                                     c.c_size_t]
+        L.orc_allreduce_forced.argtypes = [c.c_int, c.c_int, c.POINTER(c.c_void_p),
+                                           c.POINTER(c.c_void_p), c.c_size_t, c.c_int, c.c_int,
+                                           c.c_size_t, c.c_int]
         L.orc_reduce_scatter_block.argtypes = [c.c_int, c.POINTER(c.c_void_p),
                                                c.POINTER(c.c_void_p), c.c_size_t, c.c_int, c.c_int]
         L.orc_reduce_decision.argtypes = [c.c_int, c.c_size_t, c.c_size_t]
@@ -102,6 +106,21 @@ def allreduce(sbufs: list[np.ndarray], count: int, op: int, type_code: int,
     alg = lib().orc_allreduce(algorithm, n, sp, rp, count, op, type_code, segsize)
     if alg < 0:
         raise ValueError(f"oracle allreduce failed ({alg})")
+    return rbufs, alg
+
+
+def allreduce_forced(sbufs: list[np.ndarray], count: int, op: int, type_code: int, algorithm: int,
+                     segsize: int = 0, root0_inplace: bool = False) -> tuple[list[np.ndarray], int]:
+    """coll/tuned allreduce with coll_tuned_allreduce_algorithm forced to
+    `algorithm` (1..6, coll_tuned_allreduce_decision.c:37-47 numbering)."""
+    n = len(sbufs)
+    rbufs = [np.zeros_like(s) for s in sbufs]
+    sp = (ctypes.c_void_p * n)(*[_p(s) for s in sbufs])
+    rp = (ctypes.c_void_p * n)(*[_p(r) for r in rbufs])
+    alg = lib().orc_allreduce_forced(algorithm, n, sp, rp, count, op, type_code, segsize,
+                                     1 if root0_inplace else 0)
+    if alg < 0:
+        raise ValueError(f"oracle allreduce (forced {algorithm}) failed ({alg})")
     return rbufs, alg
 
 

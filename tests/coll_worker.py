@@ -109,6 +109,40 @@ def case_allreduce(comm, rank, n, dt, op, count, salt, kind="R", inplace=False, 
     return True, ""
 
 
+def case_forced(comm, rank, n, alg, dt, op, count, salt, inplace=False, how="blocking"):
+    """MPI_Allreduce with coll_tuned_allreduce_algorithm forced to `alg`
+    (coll_tuned_allreduce_decision.c:37-147): the device result must be the
+    forced algorithm's bits (oracle.allreduce_forced), through the blocking,
+    nonblocking or persistent entry point."""
+    xs = [inputs(dt, count, r, salt) for r in range(n)]
+    exp, _ = orc.allreduce_forced([x.copy() for x in xs], count, op.index, dt.code, alg,
+                                  root0_inplace=inplace)
+    s = to_dev(xs[rank])
+    out = s if inplace else torch.zeros_like(s)
+    src = coll.IN_PLACE if inplace else s
+    comm.set_param("tuned_allreduce_algorithm", alg)
+    try:
+        if how == "blocking":
+            comm.allreduce(src, out, count, dt, op, blocking=True)
+        elif how == "nonblocking":
+            req = comm.iallreduce(src, out, count, dt, op)
+            req.wait()
+            req.free()
+            torch.cuda.synchronize()
+        else:
+            plan = comm.allreduce_init(src, out, count, dt, op)
+            try:
+                plan.start()
+                plan.wait()
+            finally:
+                plan.free()
+            torch.cuda.synchronize()
+    finally:
+        comm.set_param("tuned_allreduce_algorithm", 0)
+    got = out.cpu().numpy()[:count * dt.extent].view(dt.np_dtype)
+    return checked(got, exp[rank])
+
+
 def case_rsb_kind(comm, rank, n, dt, op, rcount, salt, kind):
     return case_rsb(comm, rank, n, dt, op, rcount, salt, kind=kind)
 
@@ -591,6 +625,28 @@ def main():
         hc = int(os.environ["COLL_HEADLINE"])
         cases = [(f"headline_alg{a}", lambda a=a: case_headline(comm, rank, n, hc, 95 + a, a))
                  for a in (0, 1, 2)]
+    # coll/tuned's forced allreduce algorithms (1 basic_linear, 2 nonoverlapping,
+    # 3 recursive doubling, 4 ring, 5 segmented ring, 6 Rabenseifner), every path
+    if not os.environ.get("COLL_HEADLINE"):
+        for alg in range(1, 7):
+            for sz, tag in ((5003, "staged"), (200003, "two_shot"), (big + 3, "zero_copy")):
+                cases.append((f"forced{alg}_sum_f32_{tag}",
+                              lambda a=alg, c=sz: case_forced(comm, rank, n, a, F, mop.MPI_SUM, c, 120 + a)))
+            cases.append((f"forced{alg}_sum_f64_big_inplace",
+                          lambda a=alg: case_forced(comm, rank, n, a, D, mop.MPI_SUM, big // 2 + 1, 130 + a,
+                                                    inplace=True)))
+        cases += [
+            ("forced6_maxloc_pairs", lambda: case_forced(comm, rank, n, 6, DI, mop.MPI_MAXLOC, 70001, 140)),
+            ("forced6_max_specials_tiny", lambda: case_forced(comm, rank, n, 6, F, mop.MPI_MAX, 3, 141)),
+            ("forced6_nonblocking", lambda: case_forced(comm, rank, n, 6, F, mop.MPI_SUM, big + 1, 142,
+                                                        how="nonblocking")),
+            ("forced6_persistent", lambda: case_forced(comm, rank, n, 6, F, mop.MPI_SUM, big + 1, 143,
+                                                       how="persistent")),
+            ("forced2_persistent_inplace", lambda: case_forced(comm, rank, n, 2, F, mop.MPI_SUM, 300001, 144,
+                                                               inplace=True, how="persistent")),
+            ("forced2_nonblocking", lambda: case_forced(comm, rank, n, 2, F, mop.MPI_SUM, big + 1, 145,
+                                                        how="nonblocking")),
+        ]
     # the export fallback (hipIpcGetMemHandle refused): every zero-copy path
     # through the communicator's shadow buffers ("force_shadow")
     def shadowed(fn):

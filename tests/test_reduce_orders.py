@@ -221,3 +221,109 @@ def test_reduce_scatter_decision(orc):
     assert d(8, 12 * 1024) == 1 and d(3, 12 * 1024) == 1
     assert d(8, 256 * 1024) == 1 and d(8, 256 * 1024 + 4) == 2
     assert d(3, 12 * 1024 + 4) == 2 and d(4, 100000) == 1 and d(6, 100000) == 2
+
+
+# ---- forced allreduce algorithms (coll_tuned_allreduce_algorithm) ----
+
+def raben_piece(count, n, o):
+    """Twin of coll_ipc.hip raben_piece: the part of the vector vrank o owns."""
+    adj = 1
+    while adj * 2 <= n:
+        adj *= 2
+    lo, w, m = 0, count, 1
+    while m < adj:
+        half = w // 2
+        if o & m:
+            lo, w = lo + half, w - half
+        else:
+            w = half
+        m *= 2
+    return lo, w
+
+
+def raben_fold(orc, op, v, o):
+    """Twin of coll_ipc.hip fold() ORDER_RABEN for an element owned by vrank o."""
+    n = len(v)
+    adj = 1
+    while adj * 2 <= n:
+        adj *= 2
+    rem = n - adj
+    right = o & 1
+    w = [None] * adj
+    for u in range(adj):
+        if u < rem:
+            w[u] = f(orc, op, v[2 * u + 1], v[2 * u]) if right else f(orc, op, v[2 * u], v[2 * u + 1])
+        else:
+            w[u] = v[u + rem]
+    m = 1
+    while m < adj:
+        for u in range(adj):
+            if (u & m) == (o & m):
+                w[u] = f(orc, op, w[u], w[u ^ m])
+        m *= 2
+    return w[o]
+
+
+@pytest.mark.parametrize("n", list(range(2, 17)))
+def test_rabenseifner_closed_form_matches_message_flow(orc, n):
+    """The device's per-element Rabenseifner fold (pieces by recursive
+    halving, step-1 pair order by half) equals the oracle's message-flow
+    simulation of coll_base_allreduce.c:970-1243, bit for bit, for every
+    comm size 2..16 — including the non-power-of-two fold of step 1."""
+    rng = np.random.default_rng(100 + n)
+    count = 61 * n + 7
+    xs = [rng.uniform(-1, 1, count).astype(np.float32) for _ in range(n)]
+    res, alg = orc.allreduce_forced([x.copy() for x in xs], count, SUM, F32, orc.ALG_REDSCAT_ALLGATHER)
+    assert alg == orc.ALG_REDSCAT_ALLGATHER
+    adj = 1
+    while adj * 2 <= n:
+        adj *= 2
+    exp = np.empty(count, dtype=np.float32)
+    covered = 0
+    for o in range(adj):
+        lo, w = raben_piece(count, n, o)
+        covered += w
+        v = [x[lo:lo + w] for x in xs]
+        exp[lo:lo + w] = raben_fold(orc, SUM, v, o)
+    assert covered == count
+    for r in range(n):
+        assert np.array_equal(res[r].view(np.uint32), exp.view(np.uint32)), (n, r)
+    # and the order matters on this data: the ring's result differs somewhere
+    ring, _ = orc.allreduce([x.copy() for x in xs], count, SUM, F32, orc.ALG_RING)
+    if n > 2:
+        assert not np.array_equal(ring[0].view(np.uint32), exp.view(np.uint32))
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 6, 8])
+def test_forced_small_fallbacks(orc, n):
+    """Each forced algorithm's own fallback: Rabenseifner below p' elements
+    runs basic_linear (:988-995), ring below n elements recursive doubling
+    (:371-377); basic_linear = the linear reduce's chain order."""
+    rng = np.random.default_rng(7 + n)
+    count = n - 1
+    xs = [rng.uniform(-1, 1, count).astype(np.float32) for _ in range(n)]
+    adj = 1
+    while adj * 2 <= n:
+        adj *= 2
+    _, alg = orc.allreduce_forced([x.copy() for x in xs], adj - 1, SUM, F32, orc.ALG_REDSCAT_ALLGATHER)
+    assert alg == orc.ALG_BASIC_LINEAR
+    _, alg = orc.allreduce_forced([x.copy() for x in xs], count, SUM, F32, orc.ALG_RING)
+    assert alg == orc.ALG_RECURSIVE_DOUBLING
+    res, _ = orc.allreduce_forced([x.copy() for x in xs], count, SUM, F32, orc.ALG_BASIC_LINEAR)
+    assert np.array_equal(res[0].view(np.uint32), fold(orc, SUM, xs, CHAIN, False).view(np.uint32))
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 7])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_forced_nonoverlapping_is_tuned_reduce_then_bcast(orc, n, inplace):
+    """nonoverlapping = tuned reduce to rank 0 (with rank 0's MPI_IN_PLACE)
+    + bcast (:54-86): every rank gets the reduce's result."""
+    rng = np.random.default_rng(11 + n)
+    count = 3001
+    xs = [rng.uniform(-1, 1, count).astype(np.float32) for _ in range(n)]
+    res, alg = orc.allreduce_forced([x.copy() for x in xs], count, SUM, F32, orc.ALG_NONOVERLAPPING,
+                                    root0_inplace=inplace)
+    assert alg == orc.ALG_NONOVERLAPPING
+    red, _ = orc.reduce([x.copy() for x in xs], count, SUM, F32, 0, inplace)
+    for r in range(n):
+        assert np.array_equal(res[r].view(np.uint32), red.view(np.uint32))
