@@ -45,7 +45,20 @@ def _ptr(buf) -> int:
 
 
 def _stream(stream):
+    """The stream a call is ordered on: None means torch's current stream, so
+    a collective runs after the torch work that produced its buffers (the
+    library's own NULL default is the per-thread stream, which is not
+    ordered after torch's stream)."""
     if stream is None:
+        try:
+            import torch
+            if torch.cuda.is_available():
+                # torch's default stream is the legacy null stream (handle 0),
+                # which the C ABI spells hipStreamLegacy (1): NULL there means
+                # the per-thread stream
+                return torch.cuda.current_stream().cuda_stream or 1
+        except ImportError:
+            pass
         return None
     if isinstance(stream, int):
         return stream

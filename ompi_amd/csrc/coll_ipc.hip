@@ -324,13 +324,6 @@ struct ompi_amd_comm {
     int algorithm = 0;
     int tuned_alg = 0;                    // coll_tuned_allreduce_algorithm (forced), 0 = fixed
     // IPC caches
-    struct exp_entry {
-        void *base;
-        size_t size;
-        unsigned long long id;
-        hipIpcMemHandle_t h;
-        bool recycled;  // the runtime handed this allocation a freed one's handle bytes
-    };
     struct imp_entry {
         int peer;
         hipIpcMemHandle_t h;
@@ -339,7 +332,6 @@ struct ompi_amd_comm {
         uint64_t last_use;
         int pins;
     };
-    std::vector<exp_entry> exports;
     std::vector<imp_entry> imports;
     uint64_t use_clock = 0;
     void *opened[kMaxRanks][2] = {};      // flags / scratch mappings of peers
@@ -400,24 +392,45 @@ static int set_dev(ompi_amd_comm_t *c) {
 // with all peer blocks missing).  A handle is therefore never published
 // for a second allocation: export_buf sends such a buffer through its
 // shadow, alloc_exportable retries while holding the colliding allocation.
-struct handle_rec {
-    hipIpcMemHandle_t h;
+// The process's IPC exports, one per allocation (base, size, HIP buffer
+// id): every export — user buffers, shadows, landing, scratch, flag pages
+// — goes through export_alloc, so an allocation is exported once and its
+// handle stays the one peers already know (a second hipIpcGetMemHandle on
+// the same allocation can return other bytes).  Records of freed
+// allocations are kept as the handle history: an allocation whose handle
+// bytes equal an older record's is "recycled" and never published.
+struct export_rec {
     void *base;
     size_t size;
     unsigned long long id;
+    hipIpcMemHandle_t h;
+    bool recycled;
 };
-static std::mutex g_hist_mu;
-static std::vector<handle_rec> g_hist;
+static std::mutex g_exp_mu;
+static std::vector<export_rec> g_exp;
 
-// True when h already named another allocation; records it otherwise.
-static bool handle_recycled(const hipIpcMemHandle_t &h, void *base, size_t size,
-                            unsigned long long id) {
-    std::lock_guard<std::mutex> g(g_hist_mu);
-    for (const auto &r : g_hist)
-        if (memcmp(&r.h, &h, sizeof(h)) == 0)
-            return !(r.base == base && r.size == size && r.id == id);
-    g_hist.push_back({h, base, size, id});
-    return false;
+// 0: *h exported (fresh if *fresh), 1: recycled handle bytes, <0: the
+// runtime refused (*e).
+static int export_alloc(void *base, size_t size, unsigned long long id, hipIpcMemHandle_t *h,
+                        hipError_t *e, bool *fresh) {
+    std::lock_guard<std::mutex> g(g_exp_mu);
+    *fresh = false;
+    *e = hipSuccess;
+    for (const auto &r : g_exp)
+        if (r.base == base && r.size == size && r.id == id) {
+            *h = r.h;
+            return r.recycled ? 1 : 0;
+        }
+    *e = hipIpcGetMemHandle(h, base);
+    if (*e != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    *fresh = true;
+    bool recycled = false;
+    for (const auto &r : g_exp) recycled = recycled || memcmp(&r.h, h, sizeof(*h)) == 0;
+    g_exp.push_back({base, size, id, *h, recycled});
+    return recycled ? 1 : 0;
 }
 
 static unsigned long long buffer_id(const void *p) {
@@ -449,60 +462,33 @@ static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d, bool *ip
     d->id = id;
     d->base = (uint64_t)(uintptr_t)base;
     d->size = (uint64_t)size;
-    for (auto &x : c->exports) {
-        if (x.base == base && x.size == size && x.id == id) {
-            if (x.recycled) {
-                if (ipc_failed) *ipc_failed = true;
-                record_msg("allocation %p + %zu (id %llu) carries a recycled IPC handle", base, size, id);
-                return OMPI_AMD_ERR_HIP;
-            }
-            d->h = x.h;
-            d->off = (uint64_t)((const char *)ptr - (const char *)base);
-            d->valid = 1;
-            return OMPI_AMD_SUCCESS;
-        }
-    }
-    ompi_amd_comm::exp_entry x{base, size, id, {}, false};
-    ++c->exports_new;
-    e = hipIpcGetMemHandle(&x.h, base);
-    if (e != hipSuccess) {
-        (void)hipGetLastError();
+    hipIpcMemHandle_t h;
+    bool fresh = false;
+    const int rc = export_alloc(base, size, id, &h, &e, &fresh);
+    c->exports_new += fresh ? 1 : 0;
+    if (rc < 0) {
         hipPointerAttribute_t at{};
         const hipError_t ea = hipPointerGetAttributes(&at, ptr);
         (void)hipGetLastError();
-        const void *imp = nullptr;  // one of this rank's peer mappings overlapping the range?
-        for (auto &m : c->imports)
-            if ((char *)m.base < (char *)base + size && (char *)base < (char *)m.base + m.rsize) imp = m.base;
         record_msg("hipIpcGetMemHandle: %s (ptr %p in allocation %p + %zu, buffer id %llu, "
-                   "attr rc %d type %d device %d, overlapping peer mapping %p, land %p)",
+                   "attr rc %d type %d device %d)",
                    hipGetErrorString(e), ptr, base, size, (unsigned long long)id, (int)ea,
-                   (int)at.type, at.device, imp, (void *)c->land);
+                   (int)at.type, at.device);
         if (ipc_failed) *ipc_failed = true;
         return OMPI_AMD_ERR_HIP;
     }
-    // drop stale entries that overlap this allocation
-    c->exports.erase(std::remove_if(c->exports.begin(), c->exports.end(),
-                                    [&](const ompi_amd_comm::exp_entry &o) {
-                                        return (char *)o.base < (char *)base + size &&
-                                               (char *)base < (char *)o.base + o.size;
-                                    }),
-                     c->exports.end());
-    x.recycled = handle_recycled(x.h, base, size, id);
-    c->exports.push_back(x);
-    if (x.recycled) {
-        ++c->recycled_exports;
+    if (rc == 1) {
+        c->recycled_exports += fresh ? 1 : 0;
         if (ipc_failed) *ipc_failed = true;
         record_msg("allocation %p + %zu (id %llu) carries a recycled IPC handle", base, size, id);
         return OMPI_AMD_ERR_HIP;
     }
-    d->h = x.h;
+    d->h = h;
     d->off = (uint64_t)((const char *)ptr - (const char *)base);
     d->valid = 1;
     return OMPI_AMD_SUCCESS;
 }
 
-// pin: the mapping is held by a persistent plan and never evicted until
-// the plan releases it (unpin_import with the returned *base).
 // Close every cached mapping of `peer` that cannot be the allocation `d`
 // describes but would collide with it: the same handle bytes or an
 // overlapping exporter range under another buffer id.  The peer has freed
@@ -673,7 +659,7 @@ static int quiesce(ompi_amd_comm_t *c) {
 // fresh allocation at a just-freed range failed with hipErrorInvalidValue
 // (seen at 4 ranks, third growth).  Sizes grow geometrically, in 32 MiB steps.
 // The allocation must also get handle bytes no earlier allocation had
-// (handle_recycled): a colliding one is kept alive while the next is made,
+// (export_alloc): a colliding one is kept alive while the next is made,
 // so that the runtime cannot hand out the same handle again.
 // uncached: fine-grained memory (flag pages) instead of ordinary device memory.
 static hipError_t alloc_exportable(size_t bytes, char **out, hipIpcMemHandle_t *h,
@@ -685,21 +671,20 @@ static hipError_t alloc_exportable(size_t bytes, char **out, hipIpcMemHandle_t *
         const size_t sz = bytes + (size_t)attempt * (2u << 20);
         e = uncached ? hipExtMallocWithFlags(&p, sz, hipDeviceMallocUncached) : hipMalloc(&p, sz);
         if (e != hipSuccess) break;
-        e = hipIpcGetMemHandle(h, p);
-        if (e == hipSuccess) {
-            void *base = nullptr;
-            size_t range = 0;
-            if (hipMemGetAddressRange((hipDeviceptr_t *)&base, &range, (hipDeviceptr_t)p) != hipSuccess) {
-                (void)hipGetLastError();
-                base = p;
-                range = sz;
-            }
-            if (!handle_recycled(*h, base, range, buffer_id(p))) {
-                *out = (char *)p;
-                break;
-            }
-            e = hipErrorInvalidValue;  // recycled handle bytes
+        void *base = nullptr;
+        size_t range = 0;
+        if (hipMemGetAddressRange((hipDeviceptr_t *)&base, &range, (hipDeviceptr_t)p) != hipSuccess) {
+            (void)hipGetLastError();
+            base = p;
+            range = sz;
         }
+        bool fresh = false;
+        const int rc = export_alloc(base, range, buffer_id(p), h, &e, &fresh);
+        if (rc == 0) {
+            *out = (char *)p;
+            break;
+        }
+        if (rc == 1) e = hipErrorInvalidValue;  // recycled handle bytes
         (void)hipGetLastError();
         failed.push_back(p);  // keep it alive so the next try gets another range and handle
     }

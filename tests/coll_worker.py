@@ -492,6 +492,8 @@ def main():
     dist.init_process_group("gloo", rank=rank, world_size=n)
     comm = coll.Communicator.from_torch_distributed(device=device)
     comm.set_param("timeout_ms", 20000)
+    if os.environ.get("OMPI_AMD_TEST_FORCE_SHADOW") == "1":  # every zero-copy call through shadows
+        comm.set_param("force_shadow", 1)
     big = int(os.environ.get("COLL_BIG", 1 << 22))
     F, D, I32, I64, I8, DI = (mop.MPI_FLOAT, mop.MPI_DOUBLE, mop.MPI_INT32_T, mop.MPI_INT64_T,
                               mop.MPI_INT8_T, mop.MPI_DOUBLE_INT)
@@ -646,6 +648,12 @@ def main():
                                                                inplace=True, how="persistent")),
             ("forced2_nonblocking", lambda: case_forced(comm, rank, n, 2, F, mop.MPI_SUM, big + 1, 145,
                                                         how="nonblocking")),
+            ("forced2_blocking_inplace_f32", lambda: case_forced(comm, rank, n, 2, F, mop.MPI_SUM, 300001,
+                                                                 144, inplace=True)),
+            ("forced4_persistent_inplace", lambda: case_forced(comm, rank, n, 4, F, mop.MPI_SUM, 300001, 144,
+                                                               inplace=True, how="persistent")),
+            ("persistent_inplace_sum_f32", lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, 300001, 146,
+                                                                   inplace=True)),
         ]
     # the export fallback (hipIpcGetMemHandle refused): every zero-copy path
     # through the communicator's shadow buffers ("force_shadow")
