@@ -82,6 +82,10 @@ int ompi_amd_memcpy(void *dst, const void *src, size_t bytes);
 int ompi_amd_memmove(void *dst, void *src, size_t bytes);
 /* Wait for `stream` (NULL: the calling thread's stream). */
 int ompi_amd_stream_synchronize(void *stream);
+/* Device memory for callers that stage host operands (coll/rocm's
+ * residency staging): hipMalloc / hipFree.  bytes == 0 gives NULL. */
+int ompi_amd_device_alloc(void **ptr, size_t bytes);
+int ompi_amd_device_free(void *ptr);
 
 /* ================================================================== */
 /* 1. MPI_Op kernels — replaces op/base's handler loops                */

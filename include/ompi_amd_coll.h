@@ -99,6 +99,12 @@ int ompi_amd_comm_error(const ompi_amd_comm_t *comm);
  * glue uses it so that all ranks take the device path or all fall back to
  * the saved tuned functions (buffer residency may differ across ranks). */
 int ompi_amd_comm_agree(ompi_amd_comm_t *comm, int local_ok, int *all_ok);
+/* The same rendezvous, counting: *n_yes = number of ranks that passed
+ * local_yes != 0 (all ranks get the same count).  coll/rocm's residency
+ * vote: size = all device, 0 = all host, else mixed.  Each call (agree,
+ * vote, and every host-side handle swap) adds one to get_param
+ * "boot_calls". */
+int ompi_amd_comm_vote(ompi_amd_comm_t *comm, int local_yes, int *n_yes);
 
 /* Wait for `stream` (NULL = per-thread) and report a sticky device error:
  * the blocking completion the MPI entry points need. */

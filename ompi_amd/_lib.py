@@ -114,6 +114,8 @@ PROTOTYPES = [
     ("ompi_amd_memcpy_async", _C.c_int, [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p]),
     ("ompi_amd_memcpy", _C.c_int, [_C.c_void_p, _C.c_void_p, _C.c_size_t]),
     ("ompi_amd_memmove", _C.c_int, [_C.c_void_p, _C.c_void_p, _C.c_size_t]),
+    ("ompi_amd_device_alloc", _C.c_int, [_C.POINTER(_C.c_void_p), _C.c_size_t]),
+    ("ompi_amd_device_free", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_stream_synchronize", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_comm_create", _C.c_int,
      [_C.c_char_p, _C.c_int, _C.c_int, _C.c_int, _C.POINTER(_C.c_void_p)]),
@@ -124,6 +126,7 @@ PROTOTYPES = [
     ("ompi_amd_comm_get_param", _C.c_int, [_C.c_void_p, _C.c_char_p, _C.POINTER(_C.c_int64)]),
     ("ompi_amd_comm_error", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_comm_agree", _C.c_int, [_C.c_void_p, _C.c_int, _C.POINTER(_C.c_int)]),
+    ("ompi_amd_comm_vote", _C.c_int, [_C.c_void_p, _C.c_int, _C.POINTER(_C.c_int)]),
     ("ompi_amd_comm_sync", _C.c_int, [_C.c_void_p, _C.c_void_p]),
     ("ompi_amd_comm_phase_ms", _C.c_int,
      [_C.c_void_p, _C.c_int, _C.POINTER(_C.c_double), _C.POINTER(_C.c_int)]),

@@ -148,6 +148,12 @@ def bench_allreduce(args, metric: str, link_gbs: float):
         "shared_gpu_rehearsal": shared,
         "device_error": err,
     }
+    if not getattr(args, "no_cpu_baseline", False):
+        # every rank waits while rank 0 runs the CPU ring on `world` cores
+        dist.barrier()
+        if rank == 0:
+            res["cpu_baseline"] = cpu_baseline_ring(world, S, factor)
+        dist.barrier()
     if not args.no_extras:
         try:
             res["check"] = _check_exact(comm, dist, torch, mop, n, rank, shared)
@@ -162,6 +168,32 @@ def bench_allreduce(args, metric: str, link_gbs: float):
     dist.barrier()
     dist.destroy_process_group()
     return res if rank == 0 else None
+
+
+def cpu_baseline_ring(world: int, nbytes: int, factor: float, seconds: float = 10.0) -> dict:
+    """The reference's CPU path for this metric, restated: coll/tuned's
+    ring_segmented allreduce (coll_base_allreduce.c:618-856) with op/base's
+    loop as the reduction, `world` host processes over POSIX shared memory
+    (tools/cpu_ring_baseline.c, linked against the oracle), on the same
+    message size.  A bounded sample of about `seconds` of ring time."""
+    import json as _json
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tools", "cpu_ring_baseline")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(root, "tools"), "cpu_ring_baseline"],
+                       check=True, capture_output=True)
+    est = nbytes / 1.5e9  # seconds per iteration at the ~1.7 GB/s algbw seen in round 1
+    iters = max(5, min(200, int(seconds / max(est, 1e-6))))
+    out = subprocess.run([exe, str(world), str(nbytes), "2", str(iters)], check=True,
+                         capture_output=True, text=True, timeout=600)
+    line = _json.loads(out.stdout.strip().splitlines()[-1])
+    return {"value": line["busbw_GBps"], "unit": "GB/s", "cores": world, "kind": "port",
+            "sample": f"ring_segmented restatement (tools/cpu_ring_baseline.c, oracle op/base "
+                      f"loop), {world} processes x 1 core over POSIX shm, {nbytes} B per rank, "
+                      f"{iters} timed iterations (median {line['median_s']:.4f} s); value is "
+                      f"busBW = S/t x {factor:.3f}"}
 
 
 ALGORITHMS = ((0, "pull"), (1, "pull_push"), (2, "push"))

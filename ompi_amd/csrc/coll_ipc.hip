@@ -53,6 +53,7 @@
 #include <array>
 #include <atomic>
 #include <chrono>
+#include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -301,6 +302,7 @@ struct ompi_amd_comm {
     void *land_opened[kMaxRanks] = {};
     int stale_closed = 0;                 // cached peer mappings closed because the peer freed them
     int stale_same_handle = 0;            //   ... of which the new allocation had the same handle bytes
+    int aliased_opens = 0;                // opens the runtime answered with a mapping we already hold
     int64_t exports_new = 0, imports_new = 0;  // runtime export / open calls made (cache misses)
     int recycled_exports = 0;             // exports refused: recycled handle bytes (shadowed)
     // streams this communicator launched work on: the current one, plus an
@@ -411,6 +413,29 @@ static std::vector<export_rec> g_exp;
 
 // 0: *h exported (fresh if *fresh), 1: recycled handle bytes, <0: the
 // runtime refused (*e).
+// OMPI_AMD_IPC_TRACE=1: one stderr line per new export and per new import
+// (handle words 0-15), for diagnosing mapping mix-ups after the fact.
+static bool ipc_trace() {
+    static const bool on = [] {
+        const char *v = getenv("OMPI_AMD_IPC_TRACE");
+        return v && *v == '1';
+    }();
+    return on;
+}
+
+static void trace_handle(const char *what, const hipIpcMemHandle_t &h, const char *fmt, ...) {
+    if (!ipc_trace()) return;
+    char head[256];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(head, sizeof(head), fmt, ap);
+    va_end(ap);
+    unsigned w[16];
+    memcpy(w, &h, sizeof(w));
+    fprintf(stderr, "[ipc pid %d] %s %s h=", (int)getpid(), what, head);
+    for (int i = 0; i < 16; ++i) fprintf(stderr, "%08x%s", w[i], i == 15 ? "\n" : ".");
+}
+
 static int export_alloc(void *base, size_t size, unsigned long long id, hipIpcMemHandle_t *h,
                         hipError_t *e, bool *fresh) {
     std::lock_guard<std::mutex> g(g_exp_mu);
@@ -429,6 +454,7 @@ static int export_alloc(void *base, size_t size, unsigned long long id, hipIpcMe
     *fresh = true;
     bool recycled = false;
     for (const auto &r : g_exp) recycled = recycled || memcmp(&r.h, h, sizeof(*h)) == 0;
+    trace_handle("export", *h, "%p+%zu id %llu%s", base, size, id, recycled ? " RECYCLED" : "");
     g_exp.push_back({base, size, id, *h, recycled});
     return recycled ? 1 : 0;
 }
@@ -513,6 +539,8 @@ static int drop_stale_imports(ompi_amd_comm_t *c, int peer, const buf_desc &d,
                        peer, (unsigned long long)it->id);
             return OMPI_AMD_ERR_BAD_PARAM;
         }
+        trace_handle("close-stale", it->h, "peer %d id %llu -> %p", it->peer,
+                     (unsigned long long)it->id, it->base);
         const hipError_t e = hipIpcCloseMemHandle(it->base);
         if (e != hipSuccess) return record_hip(e, "hipIpcCloseMemHandle (stale peer mapping)");
         ++c->stale_closed;
@@ -521,6 +549,37 @@ static int drop_stale_imports(ompi_amd_comm_t *c, int peer, const buf_desc &d,
         it = c->imports.erase(it);
     }
     return OMPI_AMD_SUCCESS;
+}
+
+// Is `base` (just returned by hipIpcOpenMemHandle for a handle we do not
+// hold) inside a mapping this communicator already holds?  Then the runtime
+// answered a new handle with an existing mapping of another allocation.
+static const char *mapped_already(const ompi_amd_comm_t *c, const void *base) {
+    static thread_local char what[160];
+    const char *b = (const char *)base;
+    for (const auto &x : c->imports)
+        if (b >= (const char *)x.base && b < (const char *)x.base + x.rsize) {
+            snprintf(what, sizeof(what), "peer %d buffer id %llu (%p + %llu)", x.peer,
+                     (unsigned long long)x.id, (void *)(uintptr_t)x.rbase,
+                     (unsigned long long)x.rsize);
+            return what;
+        }
+    for (int p = 0; p < kMaxRanks; ++p) {
+        if (c->opened[p][0] && b == (const char *)c->opened[p][0]) {
+            snprintf(what, sizeof(what), "peer %d's flag page", p);
+            return what;
+        }
+        if (c->opened[p][1] && b >= (const char *)c->opened[p][1] &&
+            b < (const char *)c->opened[p][1] + c->scratch_bytes) {
+            snprintf(what, sizeof(what), "peer %d's scratch", p);
+            return what;
+        }
+        if (c->land_opened[p] && b == (const char *)c->land_opened[p]) {
+            snprintf(what, sizeof(what), "peer %d's landing buffer", p);
+            return what;
+        }
+    }
+    return nullptr;
 }
 
 static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const char **out,
@@ -557,6 +616,18 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
                    hipGetErrorString(e), peer, (unsigned long long)d.id, (void *)(uintptr_t)d.base,
                    (unsigned long long)d.size,
                    closed_same ? ", after closing its freed predecessor with the same handle" : "");
+        return OMPI_AMD_ERR_HIP;
+    }
+    trace_handle("open", d.h, "peer %d id %llu %p+%llu -> %p", peer, (unsigned long long)d.id,
+                 (void *)(uintptr_t)d.base, (unsigned long long)d.size, base);
+    if (const char *what = mapped_already(c, base)) {
+        unsigned hw[16];
+        memcpy(hw, &d.h, sizeof(hw));
+        record_msg("hipIpcOpenMemHandle returned %p for peer %d buffer id %llu (%p + %llu, handle "
+                   "word7 %08x), which is already this process's mapping of %s",
+                   base, peer, (unsigned long long)d.id, (void *)(uintptr_t)d.base,
+                   (unsigned long long)d.size, hw[7], what);
+        ++c->aliased_opens;
         return OMPI_AMD_ERR_HIP;
     }
     c->imports.push_back({peer, d.h, d.id, d.base, d.size, base, ++c->use_clock, pin ? 1 : 0});
@@ -740,8 +811,14 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     } else {
         record_hip(e, "landing buffer: hipMalloc / hipIpcGetMemHandle");
     }
+    // hipMemcpy from pageable memory may return once the bytes are staged,
+    // before they reach the device: a peer reading through its mapping right
+    // after the rendezvous below would see whatever the memory held before
+    // (round 2 saw exactly that as a "token mismatch").  Wait for the copy.
     if (e == hipSuccess)
-        e = hipMemcpy(fresh + want - kTag, &mine.token, sizeof(mine.token), hipMemcpyHostToDevice);
+        e = hipMemcpyAsync(fresh + want - kTag, &mine.token, sizeof(mine.token),
+                           hipMemcpyHostToDevice, nullptr);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
     if (e != hipSuccess && mine.d.valid) record_hip(e, "landing token write");
     mine.ok = e == hipSuccess;
     int rc = c->boot.allgather(&mine, all, sizeof(mine));  // also: nobody maps the old one now
@@ -767,6 +844,13 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
         if (e != hipSuccess) {
             record_hip(e, "hipIpcOpenMemHandle (landing)");
             status = 1;
+            break;
+        }
+        if (const char *what = mapped_already(c, m)) {
+            record_msg("landing buffer of rank %d: hipIpcOpenMemHandle returned %p, already this "
+                       "process's mapping of %s", p, m, what);
+            ++c->aliased_opens;
+            status = 2;
             break;
         }
         c->land_opened[p] = m;
@@ -1657,6 +1741,17 @@ int ompi_amd_comm_agree(ompi_amd_comm_t *c, int local_ok, int *all_ok) {
     return OMPI_AMD_SUCCESS;
 }
 
+int ompi_amd_comm_vote(ompi_amd_comm_t *c, int local_yes, int *n_yes) {
+    if (!c || !n_yes) return OMPI_AMD_ERR_BAD_PARAM;
+    int mine = local_yes ? 1 : 0, all[kMaxRanks];
+    TRY(drain(c));
+    TRY(c->boot.allgather(&mine, all, sizeof(int)));
+    int k = 0;
+    for (int p = 0; p < c->size; ++p) k += all[p];
+    *n_yes = k;
+    return OMPI_AMD_SUCCESS;
+}
+
 int ompi_amd_comm_sync(ompi_amd_comm_t *c, void *stream) {
     if (!c) return OMPI_AMD_ERR_BAD_PARAM;
     TRY(set_dev(c));
@@ -1716,8 +1811,10 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "algorithm")) *v = c->algorithm;
     else if (!strcmp(key, "tuned_allreduce_algorithm")) *v = c->tuned_alg;
     else if (!strcmp(key, "landing_bytes")) *v = (int64_t)c->land_bytes;
+    else if (!strcmp(key, "boot_calls")) *v = (int64_t)c->boot.posted();
     else if (!strcmp(key, "stale_closed")) *v = c->stale_closed;
     else if (!strcmp(key, "stale_same_handle")) *v = c->stale_same_handle;
+    else if (!strcmp(key, "aliased_opens")) *v = c->aliased_opens;
     else if (!strcmp(key, "shadowed")) *v = c->shadowed;
     else if (!strcmp(key, "epoch")) *v = (int64_t)c->epoch;
     else if (!strcmp(key, "exports_new")) *v = c->exports_new;

@@ -573,7 +573,8 @@ int ompi_amd_win_allocate(ompi_amd_comm_t *c, size_t bytes, int disp_unit, void 
     if (rc == OMPI_AMD_SUCCESS && bytes) {
         rc = record_hip(hipMalloc(&m, bytes), "hipMalloc (window)");
         if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipMemset(m, 0, bytes), "hipMemset (window)");
-        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipDeviceSynchronize(), "hipDeviceSynchronize");
+        if (rc == OMPI_AMD_SUCCESS)
+            rc = record_hip(hipStreamSynchronize(nullptr), "hipStreamSynchronize (window memset)");
     }
     // a local failure still joins the rendezvous (as a zero-byte window) so
     // that no peer waits; the collective result reports it

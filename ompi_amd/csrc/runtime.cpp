@@ -106,4 +106,16 @@ int ompi_amd_memmove(void *dst, void *src, size_t bytes) {
     return rc;
 }
 
+int ompi_amd_device_alloc(void **ptr, size_t bytes) {
+    if (!ptr) return OMPI_AMD_ERR_BAD_PARAM;
+    *ptr = nullptr;
+    if (bytes == 0) return OMPI_AMD_SUCCESS;
+    return record_hip(hipMalloc(ptr, bytes), "hipMalloc");
+}
+
+int ompi_amd_device_free(void *ptr) {
+    if (!ptr) return OMPI_AMD_SUCCESS;
+    return record_hip(hipFree(ptr), "hipFree");
+}
+
 }  // extern "C"

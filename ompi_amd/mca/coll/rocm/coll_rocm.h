@@ -34,7 +34,21 @@ typedef struct mca_coll_rocm_module_t {
     mca_coll_base_comm_coll_t c_coll;
     /* libompi_amd communicator (IPC mappings, flags, epoch) */
     ompi_amd_comm_t *dev_comm;
+    /* residency policy (coll_rocm_residency): which path a blocking call
+     * takes.  AUTO votes per call; after coll_rocm_residency_lock unanimous
+     * votes in a row the module locks to DEVICE or HOST and stops voting
+     * (a rank whose operands sit elsewhere stages them); every
+     * coll_rocm_residency_recheck locked calls one vote asks whether any
+     * rank staged, and unlocks if so. */
+    int mode;
+    int forced;                  /* mode set by the parameter: never unlocks */
+    int streak_dev, streak_host; /* consecutive unanimous votes (AUTO) */
+    int since_check, mismatched; /* locked: calls since the last recheck, own stagings */
+    void *dstage[2], *hstage[2]; /* grow-only staging per operand slot */
+    size_t dstage_bytes[2], hstage_bytes[2];
 } mca_coll_rocm_module_t;
+
+enum { ROCM_RES_AUTO = 0, ROCM_RES_DEVICE = 1, ROCM_RES_HOST = 2 };
 
 OBJ_CLASS_DECLARATION(mca_coll_rocm_module_t);
 
@@ -45,6 +59,9 @@ typedef struct mca_coll_rocm_component_t {
     int zero_copy;       /* coll_rocm_zero_copy */
     int timeout_ms;      /* coll_rocm_timeout_ms */
     int algorithm;       /* coll_rocm_allreduce_algorithm (0 pull, 1 pull+push, 2 push) */
+    int residency;       /* coll_rocm_residency: 0 auto, 1 device, 2 host */
+    int residency_lock;  /* coll_rocm_residency_lock: unanimous votes before locking (0 never) */
+    int residency_recheck; /* coll_rocm_residency_recheck: locked calls per recheck vote (0 never) */
 } mca_coll_rocm_component_t;
 
 OMPI_MODULE_DECLSPEC extern mca_coll_rocm_component_t mca_coll_rocm_component;

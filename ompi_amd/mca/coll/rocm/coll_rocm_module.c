@@ -29,6 +29,7 @@
 #include "ompi_config.h"
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "mpi.h"
@@ -68,6 +69,9 @@ mca_coll_rocm_component_t mca_coll_rocm_component = {
     .zero_copy = 1,
     .timeout_ms = 30000,
     .algorithm = 0,
+    .residency = ROCM_RES_AUTO,
+    .residency_lock = 8,
+    .residency_recheck = 256,
 };
 
 static int rocm_register(void)
@@ -97,6 +101,24 @@ static int rocm_register(void)
                                            MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_coll_rocm_component.algorithm);
+    (void) mca_base_component_var_register(c, "residency",
+                                           "Where blocking collectives run: 0 vote per call until the ranks "
+                                           "agree coll_rocm_residency_lock times in a row, 1 device (host "
+                                           "operands are staged), 2 host (the saved functions; device "
+                                           "operands are staged)",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_coll_rocm_component.residency);
+    (void) mca_base_component_var_register(c, "residency_lock",
+                                           "Unanimous residency votes in a row before the vote stops (0: never)",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_coll_rocm_component.residency_lock);
+    (void) mca_base_component_var_register(c, "residency_recheck",
+                                           "Locked calls between two votes on whether any rank staged (0: never)",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_coll_rocm_component.residency_recheck);
     return OMPI_SUCCESS;
 }
 
@@ -106,6 +128,14 @@ static void rocm_module_construct(mca_coll_rocm_module_t *m)
 {
     memset(&m->c_coll, 0, sizeof(m->c_coll));
     m->dev_comm = NULL;
+    m->mode = ROCM_RES_AUTO;
+    m->forced = 0;
+    m->streak_dev = m->streak_host = 0;
+    m->since_check = m->mismatched = 0;
+    for (int k = 0; k < 2; ++k) {
+        m->dstage[k] = m->hstage[k] = NULL;
+        m->dstage_bytes[k] = m->hstage_bytes[k] = 0;
+    }
 }
 
 static void rocm_module_destruct(mca_coll_rocm_module_t *m)
@@ -124,6 +154,10 @@ static void rocm_module_destruct(mca_coll_rocm_module_t *m)
         OBJ_RELEASE(m->c_coll.coll_allreduce_init_module);
     if (NULL != m->c_coll.coll_iallreduce_module) OBJ_RELEASE(m->c_coll.coll_iallreduce_module);
     if (NULL != m->dev_comm) (void) ompi_amd_comm_destroy(m->dev_comm);
+    for (int k = 0; k < 2; ++k) {
+        (void) ompi_amd_device_free(m->dstage[k]);
+        free(m->hstage[k]);
+    }
 }
 
 OBJ_CLASS_INSTANCE(mca_coll_rocm_module_t, mca_coll_base_module_t, rocm_module_construct,
@@ -194,6 +228,11 @@ int mca_coll_rocm_module_enable(mca_coll_base_module_t *module, struct ompi_comm
     (void) ompi_amd_comm_set_param(m->dev_comm, "zero_copy", mca_coll_rocm_component.zero_copy);
     (void) ompi_amd_comm_set_param(m->dev_comm, "timeout_ms", mca_coll_rocm_component.timeout_ms);
     (void) ompi_amd_comm_set_param(m->dev_comm, "algorithm", mca_coll_rocm_component.algorithm);
+    if (ROCM_RES_DEVICE == mca_coll_rocm_component.residency ||
+        ROCM_RES_HOST == mca_coll_rocm_component.residency) {
+        m->mode = mca_coll_rocm_component.residency;
+        m->forced = 1;
+    }
     return OMPI_SUCCESS;
 }
 
@@ -222,7 +261,8 @@ static int dev(const void *p)
     return MPI_IN_PLACE == p || ompi_amd_is_device_pointer(p);
 }
 
-/* every rank must answer the same way (buffer residency may differ) */
+/* every rank must answer the same way (buffer residency may differ): the
+ * per-call vote the nonblocking and persistent entry points keep */
 static bool take_device_path(mca_coll_rocm_module_t *m, int local_ok)
 {
     int all_ok = 0;
@@ -230,25 +270,220 @@ static bool take_device_path(mca_coll_rocm_module_t *m, int local_ok)
     return all_ok != 0;
 }
 
+/* ------------------------------------------------------------- residency */
+
+enum { ROCM_SAVED = 0, ROCM_DEVICE = 1, ROCM_SAVED_HOST = 2 };
+
+/*
+ * The path of one blocking call, the same on every rank without a message
+ * once the module is locked.
+ *
+ * uniform_ok is what every rank computes alike: a reduction's count,
+ * datatype and op are the same on all ranks (MPI-4.1 §6.9.1), so "predefined
+ * type, intrinsic op with a device kernel" needs no agreement.  local_dev is
+ * this rank's operand residency, which MPI lets differ.
+ *
+ * AUTO votes on local_dev (one shared-memory rendezvous, as every call did
+ * before): all device -> the device path, otherwise the saved function with
+ * the operands as they are.  After residency_lock unanimous votes in a row
+ * the module locks to DEVICE or HOST and stops voting.  Locked, a rank whose
+ * operands are not where the locked path runs stages them (rocm_stage):
+ * host operands into device memory for the device path, device operands
+ * into host memory for the saved host path (coll/cuda's approach,
+ * coll_cuda_allreduce.c:42-72).  Every residency_recheck locked calls one
+ * vote asks whether any rank staged since the last one; if so the module
+ * returns to AUTO.  Calls are counted per module in call order, which every
+ * rank shares, so every rank votes at the same calls.
+ */
+static int rocm_path(mca_coll_rocm_module_t *m, int uniform_ok, int local_dev)
+{
+    const int size = ompi_amd_comm_size(m->dev_comm);
+    const int lock = mca_coll_rocm_component.residency_lock;
+    const int recheck = mca_coll_rocm_component.residency_recheck;
+    int n_yes = 0;
+    if (!uniform_ok) return ROCM_SAVED;
+    if (ROCM_RES_AUTO != m->mode) {
+        const int device = ROCM_RES_DEVICE == m->mode;
+        if (!local_dev != !device) m->mismatched++;
+        if (!m->forced && recheck > 0 && ++m->since_check >= recheck) {
+            if (OMPI_AMD_SUCCESS == ompi_amd_comm_vote(m->dev_comm, m->mismatched > 0, &n_yes) &&
+                n_yes > 0) {
+                m->mode = ROCM_RES_AUTO;
+                m->streak_dev = m->streak_host = 0;
+            }
+            m->since_check = m->mismatched = 0;
+        }
+        return device ? ROCM_DEVICE : ROCM_SAVED_HOST;
+    }
+    if (OMPI_AMD_SUCCESS != ompi_amd_comm_vote(m->dev_comm, local_dev, &n_yes)) return ROCM_SAVED;
+    if (n_yes == size) {
+        m->streak_dev++;
+        m->streak_host = 0;
+    } else if (0 == n_yes) {
+        m->streak_host++;
+        m->streak_dev = 0;
+    } else {
+        m->streak_dev = m->streak_host = 0;
+    }
+    if (lock > 0 && (m->streak_dev >= lock || m->streak_host >= lock)) {
+        m->mode = m->streak_dev >= lock ? ROCM_RES_DEVICE : ROCM_RES_HOST;
+        m->since_check = m->mismatched = 0;
+    }
+    return n_yes == size ? ROCM_DEVICE : ROCM_SAVED;
+}
+
+/* One operand of a collective: the caller's buffer (NULL or MPI_IN_PLACE:
+ * nothing to stage), count elements of dtype, and whether the collective
+ * reads / writes it.  rocm_stage fills in what the collective gets. */
+typedef struct {
+    void *user;
+    size_t count;
+    struct ompi_datatype_t *dtype;
+    int in, out;
+    void *use;
+    int how;        /* 0 as is, 1 byte copy of the typed span, 2 packed */
+    ptrdiff_t gap;  /* true lower bound of the span */
+    size_t bytes;
+} rocm_operand_t;
+
+/* grow-only staging memory of one operand slot */
+static char *stage_buf(mca_coll_rocm_module_t *m, int slot, int on_dev, size_t bytes)
+{
+    void **p = on_dev ? &m->dstage[slot] : &m->hstage[slot];
+    size_t *have = on_dev ? &m->dstage_bytes[slot] : &m->hstage_bytes[slot];
+    if (bytes > *have) {
+        const size_t want = bytes > 2 * *have ? bytes : 2 * *have;
+        if (on_dev) {
+            (void) ompi_amd_device_free(*p);
+            *p = NULL;
+            if (OMPI_AMD_SUCCESS != ompi_amd_device_alloc(p, want)) *p = NULL;
+        } else {
+            free(*p);
+            *p = malloc(want);
+        }
+        *have = NULL == *p ? 0 : want;
+    }
+    return (char *) *p;
+}
+
+/* Put every operand where the chosen path runs: device memory (packed when
+ * its layout is not contiguous, since the device path moves bytes) or host
+ * memory (the typed span as it is, for the saved function). */
+static int rocm_stage(mca_coll_rocm_module_t *m, rocm_operand_t *o, int n, int to_dev)
+{
+    for (int i = 0; i < n; ++i) {
+        rocm_operand_t *x = &o[i];
+        int is_dev, contig;
+        x->use = x->user;
+        x->how = 0;
+        if (NULL == x->user || MPI_IN_PLACE == x->user || 0 == x->count) continue;
+        is_dev = ompi_amd_is_device_pointer(x->user);
+        contig = ompi_datatype_is_contiguous_memory_layout(x->dtype, (int) x->count);
+        if (to_dev ? (is_dev && contig) : !is_dev) continue;
+        if (to_dev && !contig) {
+            size_t size = 0;
+            char *h, *d;
+            (void) ompi_datatype_type_size(x->dtype, &size);
+            x->bytes = size * x->count;
+            h = stage_buf(m, i, 0, x->bytes);
+            d = stage_buf(m, i, 1, x->bytes);
+            if (NULL == h || NULL == d) return OMPI_ERR_OUT_OF_RESOURCE;
+            if (x->in) {
+                if (MPI_SUCCESS != ompi_datatype_sndrcv(x->user, (int) x->count, x->dtype, h,
+                                                        (int) x->bytes, MPI_BYTE) ||
+                    OMPI_AMD_SUCCESS != ompi_amd_memcpy(d, h, x->bytes)) {
+                    return OMPI_ERROR;
+                }
+            }
+            x->use = d;
+            x->how = 2;
+        } else {
+            ptrdiff_t lb, ext, tlb, text;
+            char *b;
+            (void) ompi_datatype_get_extent(x->dtype, &lb, &ext);
+            (void) ompi_datatype_get_true_extent(x->dtype, &tlb, &text);
+            x->bytes = (x->count - 1) * (size_t) ext + (size_t) text;
+            x->gap = tlb;
+            b = stage_buf(m, i, to_dev, x->bytes);
+            if (NULL == b) return OMPI_ERR_OUT_OF_RESOURCE;
+            /* an output's gaps must survive the copy back */
+            if ((x->in || (x->out && !contig)) &&
+                OMPI_AMD_SUCCESS != ompi_amd_memcpy(b, (char *) x->user + tlb, x->bytes)) {
+                return OMPI_ERROR;
+            }
+            x->use = b - tlb;
+            x->how = 1;
+        }
+    }
+    return OMPI_SUCCESS;
+}
+
+/* copy staged outputs back to the caller's buffers */
+static int rocm_unstage(mca_coll_rocm_module_t *m, const rocm_operand_t *o, int n, int rc)
+{
+    for (int i = 0; OMPI_SUCCESS == rc && i < n; ++i) {
+        const rocm_operand_t *x = &o[i];
+        if (!x->out || 0 == x->how) continue;
+        if (1 == x->how) {
+            if (OMPI_AMD_SUCCESS != ompi_amd_memcpy((char *) x->user + x->gap,
+                                                    (char *) x->use + x->gap, x->bytes)) {
+                rc = OMPI_ERROR;
+            }
+        } else if (OMPI_AMD_SUCCESS != ompi_amd_memcpy(m->hstage[i], x->use, x->bytes) ||
+                   MPI_SUCCESS != ompi_datatype_sndrcv(m->hstage[i], (int) x->bytes, MPI_BYTE,
+                                                       x->user, (int) x->count, x->dtype)) {
+            rc = OMPI_ERROR;
+        }
+    }
+    return rc;
+}
+
+/* decide, and stage for the decision: *path is ROCM_DEVICE or a saved path */
+static int rocm_begin(mca_coll_rocm_module_t *m, int uniform_ok, int local_dev,
+                      rocm_operand_t *o, int n, int *path)
+{
+    *path = rocm_path(m, uniform_ok, local_dev);
+    for (int i = 0; i < n; ++i) {
+        o[i].use = o[i].user;
+        o[i].how = 0;
+    }
+    if (ROCM_SAVED == *path) return OMPI_SUCCESS;
+    return rocm_stage(m, o, n, ROCM_DEVICE == *path);
+}
+
+static int rocm_dev_finish(mca_coll_rocm_module_t *m, const rocm_operand_t *o, int n, int rc)
+{
+    if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_comm_sync(m->dev_comm, NULL);
+    return rocm_unstage(m, o, n, to_ompi_err(rc));
+}
+
 /* ------------------------------------------------------------- collectives */
+
+static int reduction_ok(struct ompi_datatype_t *dtype, struct ompi_op_t *op)
+{
+    const int t = type_code(dtype);
+    return t >= 0 && ompi_op_is_intrinsic(op) && ompi_amd_op_supported(op->o_f_to_c_index, t);
+}
 
 int mca_coll_rocm_allreduce(const void *sbuf, void *rbuf, int count,
                             struct ompi_datatype_t *dtype, struct ompi_op_t *op,
                             struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
 {
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
-    const int t = type_code(dtype);
-    const int ok = t >= 0 && ompi_op_is_intrinsic(op) &&
-                   ompi_amd_op_supported(op->o_f_to_c_index, t) && dev(sbuf) && dev(rbuf);
-    int rc;
-    if (!take_device_path(m, ok)) {
-        return m->c_coll.coll_allreduce(sbuf, rbuf, count, dtype, op, comm,
-                                        m->c_coll.coll_allreduce_module);
+    const int inplace = MPI_IN_PLACE == sbuf;
+    rocm_operand_t o[2] = {{(void *) sbuf, (size_t) count, dtype, 1, 0},
+                           {rbuf, (size_t) count, dtype, inplace, 1}};
+    int path, rc;
+    rc = rocm_begin(m, reduction_ok(dtype, op), dev(sbuf) && dev(rbuf), o, 2, &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
+        rc = m->c_coll.coll_allreduce(o[0].use, o[1].use, count, dtype, op, comm,
+                                      m->c_coll.coll_allreduce_module);
+        return rocm_unstage(m, o, 2, rc);
     }
-    rc = ompi_amd_allreduce(m->dev_comm, MPI_IN_PLACE == sbuf ? rbuf : sbuf, rbuf,
-                            (size_t) count, t, op->o_f_to_c_index, NULL);
-    if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_comm_sync(m->dev_comm, NULL);
-    return to_ompi_err(rc);
+    rc = ompi_amd_allreduce(m->dev_comm, inplace ? o[1].use : o[0].use, o[1].use, (size_t) count,
+                            type_code(dtype), op->o_f_to_c_index, NULL);
+    return rocm_dev_finish(m, o, 2, rc);
 }
 
 /* MPI_Reduce: rbuf is significant at the root only (MPI-3.1 §5.9.1), so
@@ -258,20 +493,21 @@ int mca_coll_rocm_reduce(const void *sbuf, void *rbuf, int count, struct ompi_da
                          mca_coll_base_module_t *module)
 {
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
-    const int t = type_code(dtype);
     const int is_root = ompi_comm_rank(comm) == root;
-    const int ok = t >= 0 && ompi_op_is_intrinsic(op) &&
-                   ompi_amd_op_supported(op->o_f_to_c_index, t) &&
-                   (is_root ? dev(rbuf) && dev(sbuf) : ompi_amd_is_device_pointer(sbuf));
-    int rc;
-    if (!take_device_path(m, ok)) {
-        return m->c_coll.coll_reduce(sbuf, rbuf, count, dtype, op, root, comm,
-                                     m->c_coll.coll_reduce_module);
+    rocm_operand_t o[2] = {{(void *) sbuf, (size_t) count, dtype, 1, 0},
+                           {is_root ? rbuf : NULL, (size_t) count, dtype, MPI_IN_PLACE == sbuf, 1}};
+    int path, rc;
+    rc = rocm_begin(m, reduction_ok(dtype, op),
+                    is_root ? dev(rbuf) && dev(sbuf) : ompi_amd_is_device_pointer(sbuf), o, 2, &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
+        rc = m->c_coll.coll_reduce(o[0].use, is_root ? o[1].use : rbuf, count, dtype, op, root, comm,
+                                   m->c_coll.coll_reduce_module);
+        return rocm_unstage(m, o, 2, rc);
     }
-    rc = ompi_amd_reduce(m->dev_comm, sbuf, is_root ? rbuf : NULL, (size_t) count, t,
-                         op->o_f_to_c_index, root, NULL);
-    if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_comm_sync(m->dev_comm, NULL);
-    return to_ompi_err(rc);
+    rc = ompi_amd_reduce(m->dev_comm, o[0].use, is_root ? o[1].use : NULL, (size_t) count,
+                         type_code(dtype), op->o_f_to_c_index, root, NULL);
+    return rocm_dev_finish(m, o, 2, rc);
 }
 
 static int rocm_scan_common(const void *sbuf, void *rbuf, int count,
@@ -279,20 +515,22 @@ static int rocm_scan_common(const void *sbuf, void *rbuf, int count,
                             struct ompi_communicator_t *comm, mca_coll_rocm_module_t *m,
                             int exclusive)
 {
-    const int t = type_code(dtype);
-    const int ok = t >= 0 && ompi_op_is_intrinsic(op) &&
-                   ompi_amd_op_supported(op->o_f_to_c_index, t) && dev(sbuf) && dev(rbuf);
-    int rc;
-    if (!take_device_path(m, ok)) {
-        return exclusive ? m->c_coll.coll_exscan(sbuf, rbuf, count, dtype, op, comm,
-                                                 m->c_coll.coll_exscan_module)
-                         : m->c_coll.coll_scan(sbuf, rbuf, count, dtype, op, comm,
-                                               m->c_coll.coll_scan_module);
+    rocm_operand_t o[2] = {{(void *) sbuf, (size_t) count, dtype, 1, 0},
+                           {rbuf, (size_t) count, dtype, MPI_IN_PLACE == sbuf, 1}};
+    int path, rc;
+    rc = rocm_begin(m, reduction_ok(dtype, op), dev(sbuf) && dev(rbuf), o, 2, &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
+        rc = exclusive ? m->c_coll.coll_exscan(o[0].use, o[1].use, count, dtype, op, comm,
+                                               m->c_coll.coll_exscan_module)
+                       : m->c_coll.coll_scan(o[0].use, o[1].use, count, dtype, op, comm,
+                                             m->c_coll.coll_scan_module);
+        return rocm_unstage(m, o, 2, rc);
     }
-    rc = (exclusive ? ompi_amd_exscan : ompi_amd_scan)(m->dev_comm, sbuf, rbuf, (size_t) count, t,
+    rc = (exclusive ? ompi_amd_exscan : ompi_amd_scan)(m->dev_comm, o[0].use, o[1].use,
+                                                       (size_t) count, type_code(dtype),
                                                        op->o_f_to_c_index, NULL);
-    if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_comm_sync(m->dev_comm, NULL);
-    return to_ompi_err(rc);
+    return rocm_dev_finish(m, o, 2, rc);
 }
 
 int mca_coll_rocm_scan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
@@ -314,21 +552,26 @@ int mca_coll_rocm_reduce_scatter(const void *sbuf, void *rbuf, const int *rcount
                                  struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
 {
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
-    const int t = type_code(dtype);
-    const int n = ompi_comm_size(comm);
-    const int ok = t >= 0 && ompi_op_is_intrinsic(op) &&
-                   ompi_amd_op_supported(op->o_f_to_c_index, t) && dev(sbuf) && dev(rbuf);
-    size_t counts[OMPI_AMD_MAX_RANKS];
-    int rc, i;
-    if (!take_device_path(m, ok)) {
-        return m->c_coll.coll_reduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm,
-                                             m->c_coll.coll_reduce_scatter_module);
+    const int n = ompi_comm_size(comm), inplace = MPI_IN_PLACE == sbuf;
+    size_t counts[OMPI_AMD_MAX_RANKS], total = 0;
+    int path, rc, i;
+    for (i = 0; i < n; ++i) total += (size_t) rcounts[i];
+    {
+        rocm_operand_t o[2] = {{(void *) sbuf, total, dtype, 1, 0},
+                               {rbuf, inplace ? total : (size_t) rcounts[ompi_comm_rank(comm)],
+                                dtype, inplace, 1}};
+        rc = rocm_begin(m, reduction_ok(dtype, op), dev(sbuf) && dev(rbuf), o, 2, &path);
+        if (OMPI_SUCCESS != rc) return rc;
+        if (ROCM_DEVICE != path) {
+            rc = m->c_coll.coll_reduce_scatter(o[0].use, o[1].use, rcounts, dtype, op, comm,
+                                               m->c_coll.coll_reduce_scatter_module);
+            return rocm_unstage(m, o, 2, rc);
+        }
+        for (i = 0; i < n; ++i) counts[i] = (size_t) rcounts[i];
+        rc = ompi_amd_reduce_scatter(m->dev_comm, inplace ? o[1].use : o[0].use, o[1].use, counts,
+                                     type_code(dtype), op->o_f_to_c_index, NULL);
+        return rocm_dev_finish(m, o, 2, rc);
     }
-    for (i = 0; i < n; ++i) counts[i] = (size_t) rcounts[i];
-    rc = ompi_amd_reduce_scatter(m->dev_comm, MPI_IN_PLACE == sbuf ? rbuf : sbuf, rbuf, counts, t,
-                                 op->o_f_to_c_index, NULL);
-    if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_comm_sync(m->dev_comm, NULL);
-    return to_ompi_err(rc);
 }
 
 int mca_coll_rocm_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount,
@@ -337,54 +580,70 @@ int mca_coll_rocm_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount,
                                        mca_coll_base_module_t *module)
 {
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
-    const int t = type_code(dtype);
-    const int ok = t >= 0 && ompi_op_is_intrinsic(op) &&
-                   ompi_amd_op_supported(op->o_f_to_c_index, t) && dev(sbuf) && dev(rbuf);
-    int rc;
-    if (!take_device_path(m, ok)) {
-        return m->c_coll.coll_reduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm,
-                                                   m->c_coll.coll_reduce_scatter_block_module);
+    const size_t all = (size_t) rcount * (size_t) ompi_comm_size(comm);
+    const int inplace = MPI_IN_PLACE == sbuf;
+    rocm_operand_t o[2] = {{(void *) sbuf, all, dtype, 1, 0},
+                           {rbuf, inplace ? all : (size_t) rcount, dtype, inplace, 1}};
+    int path, rc;
+    rc = rocm_begin(m, reduction_ok(dtype, op), dev(sbuf) && dev(rbuf), o, 2, &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
+        rc = m->c_coll.coll_reduce_scatter_block(o[0].use, o[1].use, rcount, dtype, op, comm,
+                                                 m->c_coll.coll_reduce_scatter_block_module);
+        return rocm_unstage(m, o, 2, rc);
     }
-    rc = ompi_amd_reduce_scatter_block(m->dev_comm, MPI_IN_PLACE == sbuf ? rbuf : sbuf, rbuf,
-                                       (size_t) rcount, t, op->o_f_to_c_index, NULL);
-    if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_comm_sync(m->dev_comm, NULL);
-    return to_ompi_err(rc);
+    rc = ompi_amd_reduce_scatter_block(m->dev_comm, inplace ? o[1].use : o[0].use, o[1].use,
+                                       (size_t) rcount, type_code(dtype), op->o_f_to_c_index, NULL);
+    return rocm_dev_finish(m, o, 2, rc);
 }
 
+/* allgather / bcast move bytes: any datatype qualifies (a rank whose layout
+ * is not contiguous packs when the device path runs), so the uniform part
+ * is always true and the vote covers residency and layout. */
 int mca_coll_rocm_allgather(const void *sbuf, int scount, struct ompi_datatype_t *sdtype,
                             void *rbuf, int rcount, struct ompi_datatype_t *rdtype,
                             struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
 {
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const int inplace = MPI_IN_PLACE == sbuf;
+    const size_t all = (size_t) rcount * (size_t) ompi_comm_size(comm);
+    rocm_operand_t o[2] = {{(void *) sbuf, (size_t) scount, sdtype, 1, 0},
+                           {rbuf, all, rdtype, inplace, 1}};
     size_t rsize = 0;
-    int rc, ok;
+    int path, rc, ok;
     (void) ompi_datatype_type_size(rdtype, &rsize);
-    /* contiguous, gap-free receive type: the gather is a byte copy */
-    ok = ompi_datatype_is_contiguous_memory_layout(rdtype, rcount) && dev(rbuf) && dev(sbuf) &&
-         (MPI_IN_PLACE == sbuf || ompi_datatype_is_contiguous_memory_layout(sdtype, scount));
-    if (!take_device_path(m, ok)) {
-        return m->c_coll.coll_allgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm,
-                                        m->c_coll.coll_allgather_module);
+    ok = ompi_datatype_is_contiguous_memory_layout(rdtype, (int) all) && dev(rbuf) && dev(sbuf) &&
+         (inplace || ompi_datatype_is_contiguous_memory_layout(sdtype, scount));
+    rc = rocm_begin(m, 1, ok, o, 2, &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
+        rc = m->c_coll.coll_allgather(o[0].use, scount, sdtype, o[1].use, rcount, rdtype, comm,
+                                      m->c_coll.coll_allgather_module);
+        return rocm_unstage(m, o, 2, rc);
     }
-    rc = ompi_amd_allgather(m->dev_comm, MPI_IN_PLACE == sbuf ? (const void *) 1 : sbuf, rbuf,
+    rc = ompi_amd_allgather(m->dev_comm, inplace ? (const void *) 1 : o[0].use, o[1].use,
                             rsize * (size_t) rcount, NULL);
-    if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_comm_sync(m->dev_comm, NULL);
-    return to_ompi_err(rc);
+    return rocm_dev_finish(m, o, 2, rc);
 }
 
 int mca_coll_rocm_bcast(void *buf, int count, struct ompi_datatype_t *dtype, int root,
                         struct ompi_communicator_t *comm, mca_coll_base_module_t *module)
 {
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const int is_root = ompi_comm_rank(comm) == root;
+    rocm_operand_t o[1] = {{buf, (size_t) count, dtype, is_root, !is_root}};
     size_t size = 0;
-    int rc;
+    int path, rc;
     (void) ompi_datatype_type_size(dtype, &size);
-    if (!take_device_path(m, ompi_datatype_is_contiguous_memory_layout(dtype, count) && dev(buf))) {
-        return m->c_coll.coll_bcast(buf, count, dtype, root, comm, m->c_coll.coll_bcast_module);
+    rc = rocm_begin(m, 1, ompi_datatype_is_contiguous_memory_layout(dtype, count) && dev(buf), o, 1,
+                    &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
+        rc = m->c_coll.coll_bcast(o[0].use, count, dtype, root, comm, m->c_coll.coll_bcast_module);
+        return rocm_unstage(m, o, 1, rc);
     }
-    rc = ompi_amd_bcast(m->dev_comm, buf, size * (size_t) count, root, NULL);
-    if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_comm_sync(m->dev_comm, NULL);
-    return to_ompi_err(rc);
+    rc = ompi_amd_bcast(m->dev_comm, o[0].use, size * (size_t) count, root, NULL);
+    return rocm_dev_finish(m, o, 1, rc);
 }
 
 /* ------------------------------------------------------------- persistent */

@@ -697,6 +697,8 @@ def main():
     for name, fn in cases:
         if only and name not in only.split(","):
             continue
+        if os.environ.get("OMPI_AMD_IPC_TRACE") == "1":
+            print(f"[case {name}] epoch {comm.get_param('epoch')}", file=sys.stderr, flush=True)
         try:
             ok, msg = fn()
         except Exception as e:  # report and stop: later cases would hang
@@ -709,7 +711,7 @@ def main():
         report(rank, n, {"rank": rank, "case": name, "ok": bool(ok), "msg": msg,
                          "state": {k: comm.get_param(k) for k in (
                              "epoch", "shadowed", "recycled_exports", "stale_closed", "exports_new",
-                             "imports_new", "imports", "landing_bytes")}})
+                             "imports_new", "imports", "landing_bytes", "aliased_opens", "boot_calls")}})
         ok_all &= bool(ok)
     # zero-copy disabled: everything staged through the scratch
     if ok_all and not only and not os.environ.get("COLL_HEADLINE"):

@@ -6,7 +6,7 @@ set -e
 H=$(cd "$(dirname "$0")" && pwd)
 R=$(cd "$H/../.." && pwd)
 OUT=${1:-$H/coll_harness}
-gcc -std=gnu11 -O1 -Wall -Wextra -Wno-unused-parameter -Wno-missing-field-initializers \
+gcc -std=gnu11 -O1 -DHARNESS_COLL -Wall -Wextra -Wno-unused-parameter -Wno-missing-field-initializers \
     -I"$H/coll_include" -I"$H/include" -I"$R/include" -I"$R/ompi_amd/mca/coll/rocm" \
     -I/opt/rocm/include \
     "$R/ompi_amd/mca/coll/rocm/coll_rocm_module.c" "$H/coll_harness.c" "$H/dev_helpers.c" \

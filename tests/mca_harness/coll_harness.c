@@ -83,11 +83,22 @@ int ompi_op_ddt_map[64];
 
 static int g_rank, g_size;
 static int tuned_calls;
+static int t_sdev = -1, t_rdev = -1; /* residency of the last saved allreduce's buffers */
+struct ompi_datatype_t harness_mpi_byte = {ORC_T_BYTE, 1, 1, 1};
 
 /* ---- the previously selected functions ("tuned"): count and succeed ---- */
+/* allreduce also records where its buffers live and, into a host rbuf,
+ * writes a marker the caller can look for after a staged copy back */
 static int t_allreduce(const void *s, void *r, int c, struct ompi_datatype_t *d,
                        struct ompi_op_t *o, struct ompi_communicator_t *cm,
-                       mca_coll_base_module_t *m) { tuned_calls++; return OMPI_SUCCESS; }
+                       mca_coll_base_module_t *m)
+{
+    tuned_calls++;
+    t_sdev = MPI_IN_PLACE == s ? -1 : ompi_amd_is_device_pointer(s);
+    t_rdev = ompi_amd_is_device_pointer(r);
+    if (!t_rdev && c > 0) ((float *) r)[0] = 42.f;
+    return OMPI_SUCCESS;
+}
 static int t_reduce(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
                     int root, struct ompi_communicator_t *cm, mca_coll_base_module_t *m)
 { tuned_calls++; return OMPI_SUCCESS; }
@@ -258,6 +269,8 @@ int main(int argc, char **argv)
     CHECK(tm->super.obj_reference_count == 1 + 10 + 10, "enable retains the saved modules (%d)",
           tm->super.obj_reference_count);
     install(&table, m);
+    /* sections 1-8: the per-call residency vote (never locks) */
+    mca_coll_rocm_component.residency_lock = 0;
 
     /* 1. allreduce: staged (1000) and zero-copy (300001) sizes */
     {
@@ -543,6 +556,126 @@ int main(int argc, char **argv)
                       tuned_calls == 1 && hr == &t_request,
                   "host iallreduce falls back");
         }
+    }
+    /* 9. residency policy: unanimous votes lock the module, a locked call
+     * makes no bootstrap call, a rank whose buffers sit elsewhere stages
+     * them, and a recheck vote unlocks after such a call */
+    {
+        mca_coll_rocm_module_t *rm = (mca_coll_rocm_module_t *) m;
+        const size_t n = 1000;
+        float **xs = all_inputs(n, 90);
+        float **rb = malloc(sizeof(float *) * (size_t) g_size);
+        float *h = malloc(n * 4), *h2 = calloc(n, 4), *got = malloc(n * 4);
+        void *d, *d2;
+        int64_t b0 = 0, b1 = 0;
+        for (int r = 0; r < g_size; ++r) rb[r] = calloc(n, sizeof(float));
+        CHECK(orc_allreduce(ORC_AR_TUNED, g_size, (const void *const *) xs, (void *const *) rb, n,
+                            ORC_OP_SUM, ORC_T_FLOAT, 0) >= 0, "oracle allreduce");
+        memcpy(h, xs[g_rank], n * 4);
+        d = dev_of(h, n * 4);
+        d2 = dev_of(h2, n * 4);
+#define BOOT(v) CHECK(ompi_amd_comm_get_param(rm->dev_comm, "boot_calls", &(v)) == 0, "boot_calls")
+        mca_coll_rocm_component.residency_lock = 3;
+        mca_coll_rocm_component.residency_recheck = 4;
+        CHECK(rm->mode == ROCM_RES_AUTO, "auto before the votes");
+        rm->streak_dev = rm->streak_host = 0; /* sections 1-8 voted too */
+        /* (a) three unanimous host votes lock HOST */
+        tuned_calls = 0;
+        BOOT(b0);
+        for (int k = 0; k < 3; ++k)
+            CHECK(table.coll_allreduce(h, h2, (int) n, &dfloat, &sum, &comm,
+                                       table.coll_allreduce_module) == OMPI_SUCCESS, "host vote");
+        BOOT(b1);
+        CHECK(b1 - b0 == 3 && tuned_calls == 3 && rm->mode == ROCM_RES_HOST,
+              "3 votes lock HOST (boot %lld, tuned %d, mode %d)", (long long) (b1 - b0), tuned_calls,
+              rm->mode);
+        /* (b) locked: a host-buffer allreduce makes no bootstrap call */
+        BOOT(b0);
+        CHECK(table.coll_allreduce(h, h2, (int) n, &dfloat, &sum, &comm,
+                                   table.coll_allreduce_module) == OMPI_SUCCESS, "locked host");
+        BOOT(b1);
+        CHECK(b1 == b0 && tuned_calls == 4 && t_sdev == 0 && t_rdev == 0,
+              "locked host call: %lld bootstrap calls", (long long) (b1 - b0));
+        /* (c) rank 0 brings device buffers: it stages them to the host, the
+         * saved function sees host memory on every rank, and the marker it
+         * wrote comes back into rank 0's device rbuf */
+        CHECK(table.coll_allreduce(g_rank == 0 ? d : (void *) h, g_rank == 0 ? d2 : (void *) h2,
+                                   (int) n, &dfloat, &sum, &comm,
+                                   table.coll_allreduce_module) == OMPI_SUCCESS, "staged to host");
+        CHECK(tuned_calls == 5 && t_sdev == 0 && t_rdev == 0, "saved function got host buffers");
+        if (g_rank == 0) {
+            CHECK(harness_dev_copy_back(got, d2, 4) == 0 && got[0] == 42.f,
+                  "staged rbuf copied back (%g)", (double) got[0]);
+        }
+        /* (d) the 4th locked call is a recheck vote: rank 0 staged, so AUTO */
+        BOOT(b0);
+        for (int k = 0; k < 2; ++k)
+            CHECK(table.coll_allreduce(h, h2, (int) n, &dfloat, &sum, &comm,
+                                       table.coll_allreduce_module) == OMPI_SUCCESS, "recheck");
+        BOOT(b1);
+        CHECK(b1 - b0 == 1 && rm->mode == ROCM_RES_AUTO, "recheck unlocks (boot %lld mode %d)",
+              (long long) (b1 - b0), rm->mode);
+        /* (e) three unanimous device votes lock DEVICE (results exact) */
+        tuned_calls = 0;
+        for (int k = 0; k < 3; ++k) {
+            CHECK(table.coll_allreduce(d, d2, (int) n, &dfloat, &sum, &comm,
+                                       table.coll_allreduce_module) == OMPI_SUCCESS, "dev vote");
+            expect_dev(d2, rb[g_rank], n * 4, "allreduce while voting");
+        }
+        CHECK(rm->mode == ROCM_RES_DEVICE && tuned_calls == 0, "DEVICE lock (mode %d)", rm->mode);
+        /* (f) rank 0 brings host buffers: it stages them to the device, the
+         * device path runs on every rank with no bootstrap call (staged size) */
+        memset(h2, 0, n * 4);
+        BOOT(b0);
+        CHECK(table.coll_allreduce(g_rank == 0 ? (void *) h : d, g_rank == 0 ? (void *) h2 : d2,
+                                   (int) n, &dfloat, &sum, &comm,
+                                   table.coll_allreduce_module) == OMPI_SUCCESS, "staged to device");
+        BOOT(b1);
+        CHECK(b1 == b0 && tuned_calls == 0, "locked device call: %lld bootstrap calls, tuned %d",
+              (long long) (b1 - b0), tuned_calls);
+        if (g_rank == 0) CHECK(memcmp(h2, rb[0], n * 4) == 0, "host rbuf after device staging");
+        else expect_dev(d2, rb[g_rank], n * 4, "allreduce beside a staging rank");
+        /* (g) rank 0 receives an allgather into a non-contiguous type: it
+         * packs through the datatype engine; its gaps stay untouched */
+        {
+            const size_t b = 64, elems = b / 4 * (size_t) g_size, span = elems * 8 - 4;
+            ompi_datatype_t gap4 = {ORC_T_FLOAT, 4, 0, 0};
+            unsigned char *mine = malloc(b), *all = malloc(b * (size_t) g_size), *t = malloc(span);
+            void *ds, *dr;
+            for (int r = 0; r < g_size; ++r)
+                for (size_t k = 0; k < b; ++k) all[(size_t) r * b + k] = (unsigned char) (r * 29 + k);
+            memcpy(mine, all + (size_t) g_rank * b, b);
+            memset(t, 0x5A, span);
+            ds = dev_of(mine, b);
+            dr = dev_of(t, g_rank == 0 ? span : b * (size_t) g_size);
+            CHECK(table.coll_allgather(ds, (int) b, &dbyte, dr, g_rank == 0 ? (int) (b / 4) : (int) b,
+                                       g_rank == 0 ? &gap4 : &dbyte, &comm,
+                                       table.coll_allgather_module) == OMPI_SUCCESS, "allgather");
+            CHECK(tuned_calls == 0, "packed allgather stayed on the device path");
+            if (g_rank == 0) {
+                CHECK(harness_dev_copy_back(t, dr, span) == 0, "copy back");
+                for (size_t e = 0; e < elems; ++e) {
+                    CHECK(memcmp(t + e * 8, all + e * 4, 4) == 0, "packed element %zu", e);
+                    if (e + 1 < elems) CHECK(t[e * 8 + 4] == 0x5A, "gap %zu overwritten", e);
+                }
+            } else {
+                expect_dev(dr, all, b * (size_t) g_size, "allgather beside a packing rank");
+            }
+            harness_dev_free(ds);
+            harness_dev_free(dr);
+            free(mine);
+            free(all);
+            free(t);
+        }
+#undef BOOT
+        harness_dev_free(d);
+        harness_dev_free(d2);
+        for (int r = 0; r < g_size; ++r) free(rb[r]);
+        free(rb);
+        free(h);
+        free(h2);
+        free(got);
+        free_inputs(xs);
     }
     /* teardown: the table's references, then the module (its destructor
      * releases the saved modules and destroys the device communicator) */

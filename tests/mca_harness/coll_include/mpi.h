@@ -3,4 +3,7 @@
 #define HARNESS_MPI_H
 #define MPI_IN_PLACE ((void *) 1)
 #define MPI_SUCCESS 0
+struct ompi_datatype_t;
+extern struct ompi_datatype_t harness_mpi_byte;
+#define MPI_BYTE (&harness_mpi_byte)
 #endif
