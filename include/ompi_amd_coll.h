@@ -169,6 +169,22 @@ int ompi_amd_plan_free(ompi_amd_plan_t *plan);
  * ompi_amd_allreduce once the request completes. */
 int ompi_amd_iallreduce(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf, size_t count,
                         int type, int op, void *stream, ompi_amd_request_t **request);
+/* Nonblocking forms of the other hot-path collectives
+ * (coll_ireduce_scatter_block / coll_iallgather / coll_ibcast, coll.h:261-410;
+ * libnbc's ompi_coll_libnbc_ireduce_scatter_block / _iallgather / _ibcast in
+ * the reference), on the same post / progress machinery and request type as
+ * ompi_amd_iallreduce: sizes at most small_bytes are enqueued at once;
+ * zero-copy sizes post this rank's descriptor of what its peers read and
+ * launch once every peer posted.  Results exactly those of the blocking
+ * calls.  An in-place ireduce_scatter_block at a zero-copy size reads this
+ * rank's input from a shadow copy (its rbuf is written while peers read). */
+int ompi_amd_ireduce_scatter_block(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
+                                   size_t rcount, int type, int op, void *stream,
+                                   ompi_amd_request_t **request);
+int ompi_amd_iallgather(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf, size_t bytes,
+                        void *stream, ompi_amd_request_t **request);
+int ompi_amd_ibcast(ompi_amd_comm_t *comm, void *buf, size_t bytes, int root, void *stream,
+                    ompi_amd_request_t **request);
 /* *done = 1 once the collective's device work finished; launches deferred
  * calls whose swap completed (never waits for a peer).  As for plans, the
  * completion point is marked at the first test / wait after the launch. */

@@ -148,6 +148,13 @@ PROTOTYPES = [
     ("ompi_amd_iallreduce", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p,
       _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_ireduce_scatter_block", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p,
+      _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_iallgather", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p, _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_ibcast", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_void_p, _C.POINTER(_C.c_void_p)]),
     ("ompi_amd_request_test", _C.c_int, [_C.c_void_p, _C.POINTER(_C.c_int)]),
     ("ompi_amd_request_wait", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_request_free", _C.c_int, [_C.c_void_p]),

@@ -195,6 +195,28 @@ class Communicator:
         rc = self._lib.ompi_amd_bcast(self._h, _ptr(buf), nbytes, root, _stream(stream))
         self._finish(rc, "bcast", blocking, stream)
 
+    # -- nonblocking forms (coll.h:261-410) -----------------------------------
+    def ireduce_scatter_block(self, sbuf, rbuf, rcount: int, datatype: Datatype, op: Op,
+                              stream=None) -> "Request":
+        h = ctypes.c_void_p()
+        what = f"ireduce_scatter_block({op.name},{datatype.name})"
+        _lib.check(self._lib.ompi_amd_ireduce_scatter_block(self._h, _ptr(sbuf), _ptr(rbuf), rcount,
+                                                            datatype.code, op.index,
+                                                            _stream(stream), ctypes.byref(h)), what)
+        return Request(self, h, what)
+
+    def iallgather(self, sbuf, rbuf, nbytes: int, stream=None) -> "Request":
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.ompi_amd_iallgather(self._h, _ptr(sbuf), _ptr(rbuf), nbytes,
+                                                 _stream(stream), ctypes.byref(h)), "iallgather")
+        return Request(self, h, "iallgather")
+
+    def ibcast(self, buf, nbytes: int, root: int, stream=None) -> "Request":
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.ompi_amd_ibcast(self._h, _ptr(buf), nbytes, root, _stream(stream),
+                                             ctypes.byref(h)), "ibcast")
+        return Request(self, h, "ibcast")
+
     def __del__(self):
         # destroy is collective; only an explicit free() releases the comm
         pass

@@ -104,6 +104,13 @@ __global__ __launch_bounds__(64) void barrier_kernel(uint64_t *local, flag_set p
 // ---------------------------------------------------------------- copy
 // Byte copy with a peeled head so that the body runs 16 B (or 4 B) per
 // lane whenever src and dst share their alignment phase.
+// one 8-byte load through a peer mapping, by the GPU's own page tables (the
+// landing token check; hipMemcpy resolves the pointer through the runtime's
+// memory-object map instead)
+__global__ void peek_kernel(const uint64_t *src, uint64_t *dst) {
+    *dst = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(kXferThreads) void copy_kernel(cp_jobs jobs) {
     acquire_once();
     const cp_job jb = jobs.j[blockIdx.y];
@@ -269,7 +276,11 @@ struct pending_op {
     path_params pp;
     ompi_amd_request *req;
     shadow_set sh;  // export fallback of this call (sbuf / rbuf above are then the shadows)
+    int kind = 0;   // PEND_*: which collective
+    int root = 0;   // bcast
 };
+
+enum { PEND_ALLREDUCE = 0, PEND_RSB = 1, PEND_ALLGATHER = 2, PEND_BCAST = 3 };
 
 }  // namespace ompi_amd
 
@@ -303,6 +314,11 @@ struct ompi_amd_comm {
     int stale_closed = 0;                 // cached peer mappings closed because the peer freed them
     int stale_same_handle = 0;            //   ... of which the new allocation had the same handle bytes
     int aliased_opens = 0;                // opens the runtime answered with a mapping we already hold
+    std::vector<uint64_t> land_tokens;    // every rank's token of every landing growth (diagnostics)
+    int ipc_reopens = 0;                  // confirmation rounds that re-opened peers' buffers
+    int memcpy_token_mismatch = 0;        // landing tokens right by kernel load, wrong by hipMemcpy
+    int bcast_split = 0;                  // bcasts that ran as scatter + allgather
+    size_t bcast_split_bytes = 4u << 20;  // from this size on (0: never)
     int64_t exports_new = 0, imports_new = 0;  // runtime export / open calls made (cache misses)
     int recycled_exports = 0;             // exports refused: recycled handle bytes (shadowed)
     // streams this communicator launched work on: the current one, plus an
@@ -436,6 +452,18 @@ static void trace_handle(const char *what, const hipIpcMemHandle_t &h, const cha
     for (int i = 0; i < 16; ++i) fprintf(stderr, "%08x%s", w[i], i == 15 ? "\n" : ".");
 }
 
+// Handle identity: all 64 bytes.  On ROCm 7.2 words 0-12 are (exporter
+// address, pid, descriptor, size, offset, pid) and words 13-15 vary between
+// exports of one allocation (tools/ipc_handle_dump.hip, OMPI_AMD_IPC_TRACE);
+// comparing words 0-12 only would call every same-size reallocation at a
+// reused address "recycled" — round 2 tried that: the export history then
+// refuses most library reallocations (osc control pages) and sends far more
+// calls through the shadow fallback.  The full comparison flags the
+// allocations whose whole handle repeats, as measured in round 1.
+static bool same_handle(const hipIpcMemHandle_t &a, const hipIpcMemHandle_t &b) {
+    return memcmp(&a, &b, sizeof(a)) == 0;
+}
+
 static int export_alloc(void *base, size_t size, unsigned long long id, hipIpcMemHandle_t *h,
                         hipError_t *e, bool *fresh) {
     std::lock_guard<std::mutex> g(g_exp_mu);
@@ -453,7 +481,7 @@ static int export_alloc(void *base, size_t size, unsigned long long id, hipIpcMe
     }
     *fresh = true;
     bool recycled = false;
-    for (const auto &r : g_exp) recycled = recycled || memcmp(&r.h, h, sizeof(*h)) == 0;
+    for (const auto &r : g_exp) recycled = recycled || same_handle(r.h, *h);
     trace_handle("export", *h, "%p+%zu id %llu%s", base, size, id, recycled ? " RECYCLED" : "");
     g_exp.push_back({base, size, id, *h, recycled});
     return recycled ? 1 : 0;
@@ -528,9 +556,9 @@ static int drop_stale_imports(ompi_amd_comm_t *c, int peer, const buf_desc &d,
     if (closed_same) *closed_same = false;
     const uint64_t lo = d.base, hi = d.base + d.size;
     for (auto it = c->imports.begin(); it != c->imports.end();) {
-        const bool same_handle = memcmp(&it->h, &d.h, sizeof(d.h)) == 0;
+        const bool same_h = same_handle(it->h, d.h);
         const bool overlap = it->rbase < hi && lo < it->rbase + it->rsize;
-        if (it->peer != peer || it->id == d.id || !(same_handle || overlap)) {
+        if (it->peer != peer || it->id == d.id || !(same_h || overlap)) {
             ++it;
             continue;
         }
@@ -544,8 +572,8 @@ static int drop_stale_imports(ompi_amd_comm_t *c, int peer, const buf_desc &d,
         const hipError_t e = hipIpcCloseMemHandle(it->base);
         if (e != hipSuccess) return record_hip(e, "hipIpcCloseMemHandle (stale peer mapping)");
         ++c->stale_closed;
-        c->stale_same_handle += same_handle ? 1 : 0;
-        if (closed_same && same_handle) *closed_same = true;
+        c->stale_same_handle += same_h ? 1 : 0;
+        if (closed_same && same_h) *closed_same = true;
         it = c->imports.erase(it);
     }
     return OMPI_AMD_SUCCESS;
@@ -588,7 +616,7 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
     if (base_out) *base_out = nullptr;
     if (!d.valid) return OMPI_AMD_SUCCESS;
     for (auto &x : c->imports) {
-        if (x.peer == peer && x.id == d.id && memcmp(&x.h, &d.h, sizeof(d.h)) == 0) {
+        if (x.peer == peer && x.id == d.id && same_handle(x.h, d.h)) {
             x.last_use = ++c->use_clock;
             x.pins += pin ? 1 : 0;
             *out = (const char *)x.base + d.off;
@@ -644,6 +672,9 @@ static void unpin_import(ompi_amd_comm_t *c, void *base) {
         }
 }
 
+static int import_all(ompi_amd_comm_t *c, const call_blob *all, const void *sbuf, const void *rbuf,
+                      ptr_set *s, ptr_set *r, uint64_t *allflags, bool pin, void *(*bases)[2]);
+
 // Swap (sbuf, rbuf) descriptors with every peer and map theirs (either may
 // be NULL: nothing is exported for it).
 static int exchange_bufs(ompi_amd_comm_t *c, const void *sbuf, const void *rbuf, ptr_set *s,
@@ -653,6 +684,20 @@ static int exchange_bufs(ompi_amd_comm_t *c, const void *sbuf, const void *rbuf,
     mine.flags = myflags;
     int rc = export_buf(c, sbuf, &mine.s);
     if (rc == OMPI_AMD_SUCCESS) rc = export_buf(c, rbuf, &mine.r);
+    if (rc != OMPI_AMD_SUCCESS && !c->pre) {
+        // still take part in the swap (peers must not wait for this rank),
+        // then everyone fails the call together at the confirmation
+        call_blob all_[kMaxRanks];
+        mine = call_blob{};
+        if (c->boot.allgather(&mine, all_, sizeof(call_blob)) == OMPI_AMD_SUCCESS) {
+            int st[kMaxRanks];
+            const int one = 1;
+            for (int a = 0; a < 3; ++a) {  // mirror the peers' confirmation rounds
+                if (c->boot.allgather(&one, st, sizeof(int)) != OMPI_AMD_SUCCESS) break;
+            }
+        }
+        return rc;
+    }
     if (rc != OMPI_AMD_SUCCESS) return rc;
     call_blob all[kMaxRanks];
     if (c->pre) {  // a deferred nonblocking call: swapped when it was posted
@@ -661,22 +706,69 @@ static int exchange_bufs(ompi_amd_comm_t *c, const void *sbuf, const void *rbuf,
         rc = c->boot.allgather(&mine, all, sizeof(call_blob));
         if (rc != OMPI_AMD_SUCCESS) return rc;
     }
-    for (int p = 0; p < c->size; ++p) {
-        if (allflags) allflags[p] = all[p].flags;
-        if (p == c->rank) {
-            s->p[p] = (const char *)sbuf;
-            r->p[p] = (const char *)rbuf;
-            continue;
+    return import_all(c, all, sbuf, rbuf, s, r, allflags, pin, bases);
+}
+
+// Map every peer's (s, r) descriptors of `all`; a blocking call (no c->pre)
+// confirms the opens collectively (below).
+static int import_all(ompi_amd_comm_t *c, const call_blob *all, const void *sbuf, const void *rbuf,
+                      ptr_set *s, ptr_set *r, uint64_t *allflags, bool pin,
+                      void *(*bases)[2]) {
+    bool done[kMaxRanks] = {};
+    for (int attempt = 0;; ++attempt) {
+        int local = OMPI_AMD_SUCCESS;
+        for (int p = 0; p < c->size; ++p) {
+            if (allflags) allflags[p] = all[p].flags;
+            if (p == c->rank) {
+                s->p[p] = (const char *)sbuf;
+                r->p[p] = (const char *)rbuf;
+                continue;
+            }
+            if (done[p]) continue;
+            void *b0 = nullptr, *b1 = nullptr;
+            int prc = import_buf(c, p, all[p].s, &s->p[p], pin, &b0);
+            if (prc == OMPI_AMD_SUCCESS) prc = import_buf(c, p, all[p].r, &r->p[p], pin, &b1);
+            if (prc != OMPI_AMD_SUCCESS) {
+                if (b0 && pin) unpin_import(c, b0);
+                local = prc;
+                continue;
+            }
+            done[p] = true;
+            if (bases) {
+                bases[p][0] = b0;
+                bases[p][1] = b1;
+            }
         }
-        void *b0 = nullptr, *b1 = nullptr;
-        if ((rc = import_buf(c, p, all[p].s, &s->p[p], pin, &b0)) != OMPI_AMD_SUCCESS) return rc;
-        if ((rc = import_buf(c, p, all[p].r, &r->p[p], pin, &b1)) != OMPI_AMD_SUCCESS) return rc;
-        if (bases) {
-            bases[p][0] = b0;
-            bases[p][1] = b1;
+        // A blocking call confirms the opens: every rank learns whether any
+        // rank failed to map a peer (hipIpcOpenMemHandle refused a live
+        // buffer of a peer, "invalid device pointer", in round-2 runs with
+        // heavy allocation churn on one GPU).  Then every rank drops its
+        // cached mappings of the peers it failed on and opens again, at most
+        // twice (`ipc_reopens`); a deferred call cannot add a rendezvous.
+        if (c->pre) return local;
+        int st[kMaxRanks], any = 0;
+        const int mine_st = local == OMPI_AMD_SUCCESS ? 0 : 1;
+        TRY(c->boot.allgather(&mine_st, st, sizeof(int)));
+        for (int p = 0; p < c->size; ++p) any |= st[p];
+        if (!any) return OMPI_AMD_SUCCESS;
+        if (attempt == 2) {
+            if (local == OMPI_AMD_SUCCESS)
+                record_msg("a peer could not map this call's buffers (IPC open failed there)");
+            return local != OMPI_AMD_SUCCESS ? local : OMPI_AMD_ERR_HIP;
+        }
+        ++c->ipc_reopens;
+        for (int p = 0; p < c->size; ++p) {
+            if (p == c->rank || done[p]) continue;
+            for (auto it = c->imports.begin(); it != c->imports.end();) {
+                if (it->peer == p && it->pins == 0) {
+                    (void)hipIpcCloseMemHandle(it->base);
+                    it = c->imports.erase(it);
+                } else {
+                    ++it;
+                }
+            }
         }
     }
-    return OMPI_AMD_SUCCESS;
 }
 
 // Work this communicator put on a stream: note the stream; when the calls
@@ -735,11 +827,18 @@ static int quiesce(ompi_amd_comm_t *c) {
 // uncached: fine-grained memory (flag pages) instead of ordinary device memory.
 static hipError_t alloc_exportable(size_t bytes, char **out, hipIpcMemHandle_t *h,
                                    bool uncached = false) {
+    // The handle names (pid, address, size): a same-size allocation at a
+    // freed allocation's address gets its handle again.  A process-wide
+    // serial pads every request by a different number of 4 KiB pages, so
+    // library allocations (shadows, landing, control pages) rarely repeat
+    // an earlier (address, size) pair; a repeat that still happens is kept
+    // alive and the next attempt takes the next pad.
+    static std::atomic<unsigned> serial{0};
     std::vector<void *> failed;
     hipError_t e = hipErrorInvalidValue;
     for (int attempt = 0; attempt < 8; ++attempt) {
         void *p = nullptr;
-        const size_t sz = bytes + (size_t)attempt * (2u << 20);
+        const size_t sz = bytes + (size_t)(serial++ % 512u) * 4096u;
         e = uncached ? hipExtMallocWithFlags(&p, sz, hipDeviceMallocUncached) : hipMalloc(&p, sz);
         if (e != hipSuccess) break;
         void *base = nullptr;
@@ -854,19 +953,42 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
             break;
         }
         c->land_opened[p] = m;
-        uint64_t seen = 0;
-        e = hipMemcpy(&seen, (char *)m + want - kTag, sizeof(seen), hipMemcpyDeviceToHost);
+        // read the token by a kernel load through the mapping (what the
+        // collectives' kernels see) into this communicator's own scratch,
+        // and by hipMemcpy from the mapping, to tell the two apart
+        uint64_t seen = 0, seen_memcpy = 0;
+        hipLaunchKernelGGL(peek_kernel, dim3(1), dim3(1), 0, nullptr,
+                           (const uint64_t *)((char *)m + want - kTag), (uint64_t *)c->scratch);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+        if (e == hipSuccess) e = hipMemcpy(&seen, c->scratch, sizeof(seen), hipMemcpyDeviceToHost);
+        if (e == hipSuccess)
+            e = hipMemcpy(&seen_memcpy, (char *)m + want - kTag, sizeof(seen), hipMemcpyDeviceToHost);
+        if (e == hipSuccess && seen == all[p].token && seen_memcpy != seen) {
+            ++c->memcpy_token_mismatch;  // the kernel sees the right buffer; hipMemcpy does not
+            record_msg("landing buffer of rank %d: kernel load sees the token, hipMemcpy through "
+                       "the same mapping sees %016llx", p, (unsigned long long)seen_memcpy);
+        }
         if (e != hipSuccess) {
             record_hip(e, "landing token read");
             status = 1;
         } else if (seen != all[p].token) {
-            record_msg("landing buffer of rank %d (id %llu): the IPC mapping shows token %016llx, "
-                       "expected %016llx (it aliases another allocation)", p,
-                       (unsigned long long)all[p].d.id, (unsigned long long)seen,
-                       (unsigned long long)all[p].token);
+            // whose token is it: another rank's new buffer, or an older one?
+            int whose = -1;
+            for (int q = 0; q < c->size; ++q)
+                if (all[q].token == seen) whose = q;
+            int old_gen = -1;
+            for (size_t g = 0; g < c->land_tokens.size(); ++g)
+                if (c->land_tokens[g] == seen) old_gen = (int)g;
+            record_msg("landing buffer of rank %d (id %llu, %p + %llu): the IPC mapping %p shows "
+                       "token %016llx, expected %016llx (it aliases another allocation: new buffer "
+                       "of rank %d, earlier growth %d)", p, (unsigned long long)all[p].d.id,
+                       (void *)(uintptr_t)all[p].d.base, (unsigned long long)all[p].d.size, m,
+                       (unsigned long long)seen, (unsigned long long)all[p].token, whose, old_gen);
             status = 2;
         }
     }
+    for (int q = 0; q < c->size; ++q) c->land_tokens.push_back(all[q].token);
     int st[kMaxRanks];
     rc = c->boot.allgather(&status, st, sizeof(int));
     int worst = 0;
@@ -938,9 +1060,10 @@ static int shadow_reserve(ompi_amd_comm_t *c, size_t need, char **out) {
 // owned: fresh memory for this call (post->mem) instead of the
 // communicator's.  Nothing is enqueued here (shadow_in / shadow_out).
 static int shadow_plan(ompi_amd_comm_t *c, const void **src, size_t sbytes, void **rbuf,
-                       size_t rbytes, bool rbuf_in, bool owned, shadow_set *post) {
+                       size_t rbytes, bool rbuf_in, bool owned, shadow_set *post,
+                       bool split_inplace = false) {
     *post = shadow_set{};
-    const bool inplace = *src && *src == (const void *)*rbuf;
+    bool inplace = *src && *src == (const void *)*rbuf;
     bool fs = false, fr = false;
     buf_desc d;
     if (*src && sbytes) {
@@ -948,7 +1071,12 @@ static int shadow_plan(ompi_amd_comm_t *c, const void **src, size_t sbytes, void
         if (rc != OMPI_AMD_SUCCESS && !fs) return rc;
         fs = fs || c->force_shadow;
     }
-    if (inplace) {
+    if (inplace && fs && split_inplace) {
+        // two shadows: the input (copied in) and the result (copied out)
+        inplace = false;
+        fr = true;
+        rbuf_in = false;
+    } else if (inplace) {
         fr = fs;
         fs = false;
         rbytes = std::max(rbytes, sbytes);
@@ -1392,7 +1520,8 @@ static int reduce_my_block(ompi_amd_comm_t *c, const void *src, void *rbuf, size
     uint64_t fl[kMaxRanks] = {};
     void *none = nullptr;
     shadow_set sh;  // peers only read src; this rank's result stays local
-    TRY(shadow_plan(c, &src, total_bytes, &none, 0, false, false, &sh));
+    if (!c->pre)    // a deferred call posted its (shadow) descriptor already
+        TRY(shadow_plan(c, &src, total_bytes, &none, 0, false, false, &sh));
     TRY(shadow_in(c, sh, s));
     TRY(exchange_bufs(c, src, nullptr, &sp, &rp, inplace ? 1 : 0, fl));
     bool any_inplace = false;
@@ -1470,6 +1599,12 @@ static bool allreduce_swaps(const ompi_amd_comm_t *c, const path_params &pp, siz
 
 static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                           int op, hipStream_t s, const path_params &pp);
+static int rsb_impl(ompi_amd_comm_t *c, const void *src, void *rbuf, size_t rcount, int type,
+                    int op, bool inplace, hipStream_t s);
+static int allgather_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t bytes,
+                          hipStream_t s);
+static int bcast_impl(ompi_amd_comm_t *c, void *buf, const void *root_src, size_t bytes, int root,
+                      hipStream_t s);
 
 // Forced nonoverlapping only: every rank must know whether rank 0 passed
 // MPI_IN_PLACE (it changes rank 0's first combine of the reduce,
@@ -1501,8 +1636,21 @@ static int progress(ompi_amd_comm_t *c, bool block, int max_launch = -1) {
         if (rc == OMPI_AMD_SUCCESS) {
             c->pre = o.ticket ? all : nullptr;
             rc = shadow_in(c, o.sh, o.stream);
-            if (rc == OMPI_AMD_SUCCESS)
-                rc = allreduce_impl(c, o.sbuf, o.rbuf, o.count, o.type, o.op, o.stream, o.pp);
+            if (rc == OMPI_AMD_SUCCESS) {
+                switch (o.kind) {
+                case PEND_RSB:
+                    rc = rsb_impl(c, o.sbuf, o.rbuf, o.count, o.type, o.op, false, o.stream);
+                    break;
+                case PEND_ALLGATHER:
+                    rc = allgather_impl(c, o.sbuf, o.rbuf, o.count, o.stream);
+                    break;
+                case PEND_BCAST:
+                    rc = bcast_impl(c, o.rbuf, o.sbuf, o.count, o.root, o.stream);
+                    break;
+                default:
+                    rc = allreduce_impl(c, o.sbuf, o.rbuf, o.count, o.type, o.op, o.stream, o.pp);
+                }
+            }
             if (rc == OMPI_AMD_SUCCESS) rc = shadow_out(c, o.sh, o.stream);
             c->pre = nullptr;
         }
@@ -1779,6 +1927,9 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
         c->timeout_ms = v;
     } else if (!strcmp(key, "profile")) {
         c->profile = v ? 1 : 0;
+    } else if (!strcmp(key, "bcast_split_bytes")) {
+        if (v < 0) return OMPI_AMD_ERR_BAD_PARAM;
+        c->bcast_split_bytes = (size_t)v;
     } else if (!strcmp(key, "blocks")) {
         if (v <= 0 || v > 65535) return OMPI_AMD_ERR_BAD_PARAM;
         c->max_blocks = (int)v;
@@ -1815,6 +1966,10 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "stale_closed")) *v = c->stale_closed;
     else if (!strcmp(key, "stale_same_handle")) *v = c->stale_same_handle;
     else if (!strcmp(key, "aliased_opens")) *v = c->aliased_opens;
+    else if (!strcmp(key, "ipc_reopens")) *v = c->ipc_reopens;
+    else if (!strcmp(key, "bcast_split")) *v = c->bcast_split;
+    else if (!strcmp(key, "bcast_split_bytes")) *v = (int64_t)c->bcast_split_bytes;
+    else if (!strcmp(key, "memcpy_token_mismatch")) *v = c->memcpy_token_mismatch;
     else if (!strcmp(key, "shadowed")) *v = c->shadowed;
     else if (!strcmp(key, "epoch")) *v = (int64_t)c->epoch;
     else if (!strcmp(key, "exports_new")) *v = c->exports_new;
@@ -1913,6 +2068,113 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
     return progress(c, false);
 }
 
+// ---- nonblocking reduce_scatter_block / allgather / bcast ----
+// The iallreduce machinery (post now, launch from progress in posting
+// order): a staged size is enqueued at once; a zero-copy size posts this
+// rank's descriptor of what peers read (`exp`, `bytes`; an owned shadow
+// when the runtime refuses the export, or when `force` asks for one) and
+// launches once every peer has posted.
+static int nb_begin(ompi_amd_comm_t *c, ompi_amd_request **out) {
+    *out = nullptr;
+    TRY(check_sticky(c));
+    TRY(set_dev(c));
+    auto *req = new (std::nothrow) ompi_amd_request;
+    if (!req) return OMPI_AMD_ERR_BAD_PARAM;
+    req->c = c;
+    const int rc = record_hip(hipEventCreateWithFlags(&req->ev, hipEventDisableTiming), "request event");
+    if (rc != OMPI_AMD_SUCCESS) {
+        delete req;
+        return rc;
+    }
+    *out = req;
+    return OMPI_AMD_SUCCESS;
+}
+
+static int nb_post(ompi_amd_comm_t *c, pending_op &o, const void **exp, size_t bytes, bool force,
+                   ompi_amd_request_t **out) {
+    int rc = OMPI_AMD_SUCCESS;
+    ompi_amd_request *req = o.req;
+    if (exp) {
+        while (rc == OMPI_AMD_SUCCESS && c->boot.posted() - c->boot.consumed() >= ShmBoot::kRing - 1)
+            rc = progress(c, true, 1);
+        void *none = nullptr;
+        const int saved = c->force_shadow;
+        if (force) c->force_shadow = 1;
+        if (rc == OMPI_AMD_SUCCESS) rc = shadow_plan(c, exp, bytes, &none, 0, false, true, &o.sh);
+        c->force_shadow = saved;
+        req->shadow = o.sh.mem;
+        call_blob mine{};
+        if (rc == OMPI_AMD_SUCCESS) rc = export_buf(c, *exp, &mine.s);
+        if (rc == OMPI_AMD_SUCCESS) rc = c->boot.post(&mine, sizeof(mine), &o.ticket);
+    }
+    if (rc != OMPI_AMD_SUCCESS) {
+        (void)hipEventDestroy(req->ev);
+        if (req->shadow) (void)hipFree(req->shadow);
+        delete req;
+        return rc;
+    }
+    c->pending.push_back(o);
+    *out = req;
+    return progress(c, false);
+}
+
+static bool nb_swaps(const ompi_amd_comm_t *c, size_t bytes) {
+    return c->size > 1 && bytes > 0 && bytes > c->small_bytes && c->zero_copy;
+}
+
+int ompi_amd_ireduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t rcount,
+                                   int type, int op, void *stream, ompi_amd_request_t **out) {
+    if (!c || !rbuf || !out) return OMPI_AMD_ERR_BAD_PARAM;
+    *out = nullptr;
+    if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
+    ompi_amd_request *req = nullptr;
+    TRY(nb_begin(c, &req));
+    const bool inplace = in_place(sbuf, rbuf);
+    const size_t total = rcount * (size_t)c->size * ompi_amd_type_extent(type);
+    pending_op o{0, inplace ? rbuf : sbuf, rbuf, rcount, type, op, as_stream(stream), params_of(c), req};
+    o.kind = PEND_RSB;
+    // in place at a zero-copy size: peers read this rank's input from an
+    // owned shadow, so the result can go straight into rbuf (no landing)
+    const bool swap = nb_swaps(c, total);
+    return nb_post(c, o, swap ? &o.sbuf : nullptr, total, inplace, out);
+}
+
+int ompi_amd_iallgather(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t bytes,
+                        void *stream, ompi_amd_request_t **out) {
+    if (!c || !rbuf || !out) return OMPI_AMD_ERR_BAD_PARAM;
+    *out = nullptr;
+    ompi_amd_request *req = nullptr;
+    TRY(nb_begin(c, &req));
+    char *my_slot = (char *)rbuf + (size_t)c->rank * bytes;
+    const bool inplace = sbuf == (const void *)1 || sbuf == (const void *)my_slot;
+    pending_op o{0, inplace ? (const void *)my_slot : sbuf, rbuf, bytes, 0, 0, as_stream(stream),
+                 params_of(c), req};
+    o.kind = PEND_ALLGATHER;
+    // in place: keep the (void *)1 spelling unless peers read a shadow
+    if (inplace) o.sbuf = (const void *)1;
+    if (!nb_swaps(c, bytes)) return nb_post(c, o, nullptr, 0, false, out);
+    o.sbuf = inplace ? (const void *)my_slot : sbuf;
+    return nb_post(c, o, &o.sbuf, bytes, false, out);
+}
+
+int ompi_amd_ibcast(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, void *stream,
+                    ompi_amd_request_t **out) {
+    if (!c || !buf || !out || root < 0 || root >= c->size) return OMPI_AMD_ERR_BAD_PARAM;
+    *out = nullptr;
+    ompi_amd_request *req = nullptr;
+    TRY(nb_begin(c, &req));
+    pending_op o{0, buf, buf, bytes, 0, 0, as_stream(stream), params_of(c), req};
+    o.kind = PEND_BCAST;
+    o.root = root;
+    if (!nb_swaps(c, bytes) || c->rank != root) {
+        // non-roots export nothing, but post their (empty) half all the same
+        if (!nb_swaps(c, bytes)) return nb_post(c, o, nullptr, 0, false, out);
+        const void *nothing = nullptr;
+        return nb_post(c, o, &nothing, 0, false, out);
+    }
+    return nb_post(c, o, &o.sbuf, bytes, false, out);
+}
+
 int ompi_amd_reduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                     int op, int root, void *stream) {
     if (!c || root < 0 || root >= c->size || (c->rank == root && !rbuf))
@@ -1978,16 +2240,20 @@ int ompi_amd_reduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *rb
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
     TRY(check_sticky(c));
     TRY(drain(c));
+    const bool inplace = in_place(sbuf, rbuf);
+    return rsb_impl(c, inplace ? rbuf : sbuf, rbuf, rcount, type, op, inplace, as_stream(stream));
+}
+
+// src: the input (rbuf itself in place, n * rcount elements)
+static int rsb_impl(ompi_amd_comm_t *c, const void *src, void *rbuf, size_t rcount, int type,
+                    int op, bool inplace, hipStream_t s) {
     if (rcount == 0) return OMPI_AMD_SUCCESS;
     TRY(set_dev(c));
-    hipStream_t s = as_stream(stream);
     const int n = c->size;
     const size_t ext = ompi_amd_type_extent(type);
     const size_t total = rcount * (size_t)n * ext;
-    const bool inplace = in_place(sbuf, rbuf);
-    const void *src = inplace ? rbuf : sbuf;  // in place: the input is rbuf (n*rcount)
     if (n == 1) {
-        if (inplace) return OMPI_AMD_SUCCESS;
+        if (inplace || src == rbuf) return OMPI_AMD_SUCCESS;
         return record_hip(hipMemcpyAsync(rbuf, src, rcount * ext, hipMemcpyDeviceToDevice, s), "copy");
     }
     // basic_linear rsb = tuned reduce of the whole vector to rank 0 (never
@@ -2062,9 +2328,13 @@ int ompi_amd_allgather(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
     if (!c || !rbuf) return OMPI_AMD_ERR_BAD_PARAM;
     TRY(check_sticky(c));
     TRY(drain(c));
+    return allgather_impl(c, sbuf, rbuf, bytes, as_stream(stream));
+}
+
+static int allgather_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t bytes,
+                          hipStream_t s) {
     if (bytes == 0) return OMPI_AMD_SUCCESS;
     TRY(set_dev(c));
-    hipStream_t s = as_stream(stream);
     const int n = c->size;
     const bool inplace = sbuf == (const void *)1 ||
                          sbuf == (const void *)((const char *)rbuf + (size_t)c->rank * bytes);
@@ -2083,7 +2353,7 @@ int ompi_amd_allgather(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
     const void *mine = inplace ? my_slot : sbuf;
     void *none = nullptr;
     shadow_set sh;
-    TRY(shadow_plan(c, &mine, bytes, &none, 0, false, false, &sh));
+    if (!c->pre) TRY(shadow_plan(c, &mine, bytes, &none, 0, false, false, &sh));
     TRY(shadow_in(c, sh, s));
     TRY(exchange_bufs(c, mine, nullptr, &sp, &rp));
     TRY(launch_barrier(c, s));
@@ -2099,9 +2369,14 @@ int ompi_amd_bcast(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, void *
     if (!c || !buf || root < 0 || root >= c->size) return OMPI_AMD_ERR_BAD_PARAM;
     TRY(check_sticky(c));
     TRY(drain(c));
+    return bcast_impl(c, buf, buf, bytes, root, as_stream(stream));
+}
+
+// root_src: what the root's peers read (buf, or a deferred call's shadow)
+static int bcast_impl(ompi_amd_comm_t *c, void *buf, const void *root_src, size_t bytes, int root,
+                      hipStream_t s) {
     if (bytes == 0 || c->size == 1) return OMPI_AMD_SUCCESS;
     TRY(set_dev(c));
-    hipStream_t s = as_stream(stream);
     cp_jobs cj{};
     if (bytes <= c->small_bytes || !c->zero_copy) {
         if (bytes > c->scratch_bytes) return OMPI_AMD_ERR_BAD_PARAM;
@@ -2120,10 +2395,55 @@ int ompi_amd_bcast(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, void *
         return OMPI_AMD_SUCCESS;
     }
     ptr_set sp{}, rp{};
-    const void *mine = c->rank == root ? buf : nullptr;
+    // Large: scatter + allgather (the data flow of coll_base_bcast.c:768's
+    // scatter_allgather, one hop per phase on the fully connected xGMI
+    // mesh): rank r copies block r from the root, barrier, then block b from
+    // rank b for every other b.  Every link carries about 2·bytes/N instead
+    // of each of the root's links carrying `bytes`.  Needs every rank's
+    // buffer exportable (decided from the swapped descriptors, so alike on
+    // every rank) and a blocking call; otherwise the root-pull below.
+    if (!c->pre && c->bcast_split_bytes > 0 && bytes >= c->bcast_split_bytes) {
+        call_blob me{}, all[kMaxRanks];
+        bool refused = false;
+        if (export_buf(c, buf, &me.s, &refused) != OMPI_AMD_SUCCESS) me.s = buf_desc{};
+        TRY(c->boot.allgather(&me, all, sizeof(call_blob)));
+        bool every = true;
+        for (int p = 0; p < c->size; ++p) every = every && all[p].s.valid;
+        if (every) {
+            TRY(import_all(c, all, buf, nullptr, &sp, &rp, nullptr, false, nullptr));
+            const int n = c->size;
+            const size_t blk = ((bytes + (size_t)n - 1) / (size_t)n + 255) & ~(size_t)255;
+            auto block = [&](int b, size_t *off, size_t *len) {
+                *off = std::min(bytes, (size_t)b * blk);
+                *len = std::min(bytes, *off + blk) - *off;
+            };
+            TRY(launch_barrier(c, s));  // the root's data is final
+            size_t off, len;
+            block(c->rank, &off, &len);
+            if (c->rank != root && len) {
+                cj.n = 1;
+                cj.j[0] = {sp.p[root] + off, (char *)buf + off, (int64_t)len};
+                TRY(launch_copy(c, cj, s));
+            }
+            TRY(launch_barrier(c, s));  // every block is at its owner
+            if (c->rank != root) {
+                cj.n = 0;
+                for (int b = 0; b < n; ++b) {
+                    block(b, &off, &len);
+                    if (b == c->rank || !len) continue;
+                    cj.j[cj.n++] = {sp.p[b] + off, (char *)buf + off, (int64_t)len};
+                }
+                TRY(launch_copy(c, cj, s));
+            }
+            ++c->bcast_split;
+            return launch_barrier(c, s);
+        }
+        // someone's export was refused: the root-pull path, with its own swap
+    }
+    const void *mine = c->rank == root ? root_src : nullptr;
     void *none = nullptr;
     shadow_set sh;
-    TRY(shadow_plan(c, &mine, bytes, &none, 0, false, false, &sh));
+    if (!c->pre) TRY(shadow_plan(c, &mine, bytes, &none, 0, false, false, &sh));
     TRY(shadow_in(c, sh, s));
     TRY(exchange_bufs(c, mine, nullptr, &sp, &rp));
     TRY(launch_barrier(c, s));
@@ -2167,14 +2487,19 @@ int ompi_amd_allreduce_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, si
         if (rc == OMPI_AMD_SUCCESS) {  // export fallback: shadows of the plan's own
             const void *xs = pl->kind == 3 ? nullptr : pl->src;
             void *xr = pl->rbuf;
-            rc = shadow_plan(c, &xs, pl->kind == 3 ? 0 : bytes, &xr, bytes, inplace, true, &pl->sh);
+            // an in-place plan that needs shadows gets two (input, result)
+            // and runs as not in place: round 2 saw in-place owned shadows
+            // read wrong peer data after long handle-recycling histories on a
+            // shared GPU; separate shadows pass those cases
+            rc = shadow_plan(c, &xs, pl->kind == 3 ? 0 : bytes, &xr, bytes, inplace, true, &pl->sh,
+                             true);
             if (pl->kind != 3) pl->src = xs;
             pl->rbuf = xr;
         }
         if (rc == OMPI_AMD_SUCCESS)
             rc = exchange_bufs(c, pl->kind == 3 ? nullptr : pl->src, pl->rbuf, &pl->sp, &pl->rp, 0,
                                nullptr, true, pl->bases);
-        if (inplace) pl->sp = pl->rp;
+        if (pl->src == pl->rbuf) pl->sp = pl->rp;
     }
     if (rc == OMPI_AMD_SUCCESS)
         rc = record_hip(hipEventCreateWithFlags(&pl->done, hipEventDisableTiming), "plan event");

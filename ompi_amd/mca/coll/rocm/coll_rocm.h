@@ -6,7 +6,9 @@
  * coll_reduce_scatter_block,
  * coll_scan, coll_exscan, coll_allgather, coll_bcast
  * (ompi/mca/coll/coll.h:200-250), the nonblocking coll_iallreduce
- * (coll.h:271-274) and the persistent coll_allreduce_init (coll.h:349-352)
+ * (coll.h:271-274), coll_ireduce_scatter_block / coll_iallgather /
+ * coll_ibcast (coll.h:261-265, 293-296, 319-322) and the persistent
+ * coll_allreduce_init (coll.h:349-352)
  * for device buffers through libompi_amd.so,
  * and interposes on the previously selected functions (coll/tuned, coll/basic
  * for scan/exscan) for everything else, exactly like coll/cuda does
@@ -111,6 +113,17 @@ int mca_coll_rocm_iallreduce(const void *sbuf, void *rbuf, int count,
                              struct ompi_datatype_t *dtype, struct ompi_op_t *op,
                              struct ompi_communicator_t *comm, ompi_request_t **request,
                              mca_coll_base_module_t *module);
+int mca_coll_rocm_ireduce_scatter_block(const void *sbuf, void *rbuf, int rcount,
+                                        struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                        struct ompi_communicator_t *comm, ompi_request_t **request,
+                                        mca_coll_base_module_t *module);
+int mca_coll_rocm_iallgather(const void *sbuf, int scount, struct ompi_datatype_t *sdtype,
+                             void *rbuf, int rcount, struct ompi_datatype_t *rdtype,
+                             struct ompi_communicator_t *comm, ompi_request_t **request,
+                             mca_coll_base_module_t *module);
+int mca_coll_rocm_ibcast(void *buf, int count, struct ompi_datatype_t *dtype, int root,
+                         struct ompi_communicator_t *comm, ompi_request_t **request,
+                         mca_coll_base_module_t *module);
 int mca_coll_rocm_allreduce_init(const void *sbuf, void *rbuf, int count,
                                  struct ompi_datatype_t *dtype, struct ompi_op_t *op,
                                  struct ompi_communicator_t *comm, struct ompi_info_t *info,

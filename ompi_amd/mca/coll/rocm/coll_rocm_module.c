@@ -153,6 +153,10 @@ static void rocm_module_destruct(mca_coll_rocm_module_t *m)
     if (NULL != m->c_coll.coll_allreduce_init_module)
         OBJ_RELEASE(m->c_coll.coll_allreduce_init_module);
     if (NULL != m->c_coll.coll_iallreduce_module) OBJ_RELEASE(m->c_coll.coll_iallreduce_module);
+    if (NULL != m->c_coll.coll_iallgather_module) OBJ_RELEASE(m->c_coll.coll_iallgather_module);
+    if (NULL != m->c_coll.coll_ibcast_module) OBJ_RELEASE(m->c_coll.coll_ibcast_module);
+    if (NULL != m->c_coll.coll_ireduce_scatter_block_module)
+        OBJ_RELEASE(m->c_coll.coll_ireduce_scatter_block_module);
     if (NULL != m->dev_comm) (void) ompi_amd_comm_destroy(m->dev_comm);
     for (int k = 0; k < 2; ++k) {
         (void) ompi_amd_device_free(m->dstage[k]);
@@ -190,6 +194,9 @@ mca_coll_base_module_t *mca_coll_rocm_comm_query(struct ompi_communicator_t *com
     m->super.coll_allgather = mca_coll_rocm_allgather;
     m->super.coll_bcast = mca_coll_rocm_bcast;
     m->super.coll_iallreduce = mca_coll_rocm_iallreduce;
+    m->super.coll_iallgather = mca_coll_rocm_iallgather;
+    m->super.coll_ibcast = mca_coll_rocm_ibcast;
+    m->super.coll_ireduce_scatter_block = mca_coll_rocm_ireduce_scatter_block;
     m->super.coll_allreduce_init = mca_coll_rocm_allreduce_init;
     return &m->super;
 }
@@ -216,6 +223,9 @@ int mca_coll_rocm_module_enable(mca_coll_base_module_t *module, struct ompi_comm
     SAVE(allgather);
     SAVE(bcast);
     SAVE(iallreduce);
+    SAVE(iallgather);
+    SAVE(ibcast);
+    SAVE(ireduce_scatter_block);
     SAVE(allreduce_init);
 #undef SAVE
 
@@ -809,6 +819,90 @@ int mca_coll_rocm_iallreduce(const void *sbuf, void *rbuf, int count,
     rocm_link_active(r);
     *request = &r->super;
     return OMPI_SUCCESS;
+}
+
+/* a library request behind an MPI request, completed by rocm_progress */
+static int rocm_wrap_nb(ompi_amd_request_t *nb, struct ompi_communicator_t *comm,
+                        ompi_request_t **request)
+{
+    mca_coll_rocm_request_t *r = OBJ_NEW(mca_coll_rocm_request_t);
+    if (NULL == r) {
+        (void) ompi_amd_request_free(nb);
+        return OMPI_ERROR;
+    }
+    OMPI_REQUEST_INIT(&r->super, false);
+    r->super.req_state = OMPI_REQUEST_ACTIVE;
+    r->super.req_mpi_object.comm = comm;
+    r->super.req_status.MPI_ERROR = OMPI_SUCCESS;
+    r->nbreq = nb;
+    rocm_link_active(r);
+    *request = &r->super;
+    return OMPI_SUCCESS;
+}
+
+/* MPI_Ireduce_scatter_block / MPI_Iallgather / MPI_Ibcast (coll.h:261-265,
+ * 293-296, 319-322): as MPI_Iallreduce — the path is voted per call (the
+ * one host rendezvous before the nonblocking post), device buffers only
+ * (no staging: a staged copy-back would need a completion hook). */
+int mca_coll_rocm_ireduce_scatter_block(const void *sbuf, void *rbuf, int rcount,
+                                        struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                        struct ompi_communicator_t *comm, ompi_request_t **request,
+                                        mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    ompi_amd_request_t *nb = NULL;
+    int rc;
+    if (!take_device_path(m, reduction_ok(dtype, op) && dev(sbuf) && dev(rbuf))) {
+        return m->c_coll.coll_ireduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, request,
+                                                    m->c_coll.coll_ireduce_scatter_block_module);
+    }
+    rc = ompi_amd_ireduce_scatter_block(m->dev_comm, MPI_IN_PLACE == sbuf ? rbuf : sbuf, rbuf,
+                                        (size_t) rcount, type_code(dtype), op->o_f_to_c_index, NULL,
+                                        &nb);
+    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
+    return rocm_wrap_nb(nb, comm, request);
+}
+
+int mca_coll_rocm_iallgather(const void *sbuf, int scount, struct ompi_datatype_t *sdtype,
+                             void *rbuf, int rcount, struct ompi_datatype_t *rdtype,
+                             struct ompi_communicator_t *comm, ompi_request_t **request,
+                             mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const int inplace = MPI_IN_PLACE == sbuf;
+    ompi_amd_request_t *nb = NULL;
+    size_t rsize = 0;
+    int rc, ok;
+    (void) ompi_datatype_type_size(rdtype, &rsize);
+    ok = ompi_datatype_is_contiguous_memory_layout(rdtype, rcount * ompi_comm_size(comm)) &&
+         dev(rbuf) && dev(sbuf) &&
+         (inplace || ompi_datatype_is_contiguous_memory_layout(sdtype, scount));
+    if (!take_device_path(m, ok)) {
+        return m->c_coll.coll_iallgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, request,
+                                         m->c_coll.coll_iallgather_module);
+    }
+    rc = ompi_amd_iallgather(m->dev_comm, inplace ? (const void *) 1 : sbuf, rbuf,
+                             rsize * (size_t) rcount, NULL, &nb);
+    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
+    return rocm_wrap_nb(nb, comm, request);
+}
+
+int mca_coll_rocm_ibcast(void *buf, int count, struct ompi_datatype_t *dtype, int root,
+                         struct ompi_communicator_t *comm, ompi_request_t **request,
+                         mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    ompi_amd_request_t *nb = NULL;
+    size_t size = 0;
+    int rc;
+    (void) ompi_datatype_type_size(dtype, &size);
+    if (!take_device_path(m, ompi_datatype_is_contiguous_memory_layout(dtype, count) && dev(buf))) {
+        return m->c_coll.coll_ibcast(buf, count, dtype, root, comm, request,
+                                     m->c_coll.coll_ibcast_module);
+    }
+    rc = ompi_amd_ibcast(m->dev_comm, buf, size * (size_t) count, root, NULL, &nb);
+    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
+    return rocm_wrap_nb(nb, comm, request);
 }
 
 /* MPI_Allreduce_init (coll.h:349-352).  Collective: the path decision is

@@ -1,0 +1,610 @@
+/*
+ * pml/rocm component: interposition on the selected PML (see pml_rocm.h).
+ *
+ * Component protocol (pml_base_select.c): every PML component is opened,
+ * the selected one's pmlm_init provides mca_pml, the others are closed.
+ * pml/rocm's pmlm_init returns NULL, so it is always closed; its close
+ * saves mca_pml (the selected PML's table) and installs the functions below
+ * — pml/v's parasite pattern (pml_v_component.c:123-160).
+ *
+ * Requests: library transfers complete on the device; a progress callback
+ * registered with opal_progress (as coll/rocm and coll/libnbc do) tests the
+ * active requests with ompi_amd_p2p_test, copies staged receives back, fills
+ * the status and completes them, so MPI_Wait / MPI_Test work unchanged.
+ */
+#include "ompi_config.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mpi.h"
+#include "ompi/constants.h"
+#include "ompi/runtime/ompi_rte.h"
+#include "opal/mca/base/mca_base_var.h"
+#include "opal/mca/threads/mutex.h"
+#include "opal/runtime/opal_progress.h"
+
+#include "ompi_amd.h"
+#include "pml_rocm.h"
+
+static int rocm_register(void);
+static int rocm_open(void);
+static int rocm_close(void);
+static mca_pml_base_module_t *rocm_init(int *priority, bool progress_threads, bool mpi_threads);
+static int rocm_finalize(void);
+
+mca_pml_rocm_component_t mca_pml_rocm_component = {
+    .super = {
+        .pmlm_version = {
+            MCA_PML_BASE_VERSION_2_0_0,
+            .mca_component_name = "rocm",
+            MCA_BASE_MAKE_VERSION(component, OMPI_MAJOR_VERSION, OMPI_MINOR_VERSION,
+                                  OMPI_RELEASE_VERSION),
+            .mca_open_component = rocm_open,
+            .mca_close_component = rocm_close,
+            .mca_register_component_params = rocm_register,
+        },
+        .pmlm_data = { MCA_BASE_METADATA_PARAM_CHECKPOINT },
+        .pmlm_init = rocm_init,
+        .pmlm_finalize = rocm_finalize,
+    },
+    .enable = 1,
+    .timeout_ms = 30000,
+};
+
+mca_pml_base_module_t mca_pml_rocm_host;
+int mca_pml_rocm_installed;
+
+static int rocm_register(void)
+{
+    mca_base_component_t *c = &mca_pml_rocm_component.super.pmlm_version;
+    (void) mca_base_component_var_register(c, "enable",
+                                           "Route user-tag messages of node-local communicators "
+                                           "through the device library",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_pml_rocm_component.enable);
+    (void) mca_base_component_var_register(c, "timeout_ms",
+                                           "Device spin limit of a transfer before it fails",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_pml_rocm_component.timeout_ms);
+    return OMPI_SUCCESS;
+}
+
+static int rocm_open(void) { return OMPI_SUCCESS; }
+
+/* never selected: the interposition happens at close */
+static mca_pml_base_module_t *rocm_init(int *priority, bool progress_threads, bool mpi_threads)
+{
+    *priority = -1;
+    return NULL;
+}
+
+static int rocm_finalize(void) { return OMPI_SUCCESS; }
+
+/* ------------------------------------------------------------- communicators */
+
+struct rocm_comm {
+    struct ompi_communicator_t *comm;
+    ompi_amd_comm_t *dev;
+    struct rocm_comm *next;
+};
+static struct rocm_comm *rocm_comms;
+static opal_mutex_t rocm_lock = OPAL_MUTEX_STATIC_INIT;
+
+ompi_amd_comm_t *mca_pml_rocm_comm_of(struct ompi_communicator_t *comm)
+{
+    struct rocm_comm *e;
+    for (e = rocm_comms; NULL != e; e = e->next)
+        if (e->comm == comm) return e->dev;
+    return NULL;
+}
+
+/* pml_add_comm (pml.h:175): the saved PML first, then — collectively, every
+ * rank of the new communicator runs it — a library communicator for a
+ * node-local intra-communicator of 2..16 ranks. */
+static int rocm_add_comm(struct ompi_communicator_t *comm)
+{
+    char name[128];
+    ompi_amd_comm_t *dev = NULL;
+    struct rocm_comm *e;
+    int rc = mca_pml_rocm_host.pml_add_comm(comm);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (OMPI_COMM_IS_INTER(comm) || ompi_comm_size(comm) < 2 ||
+        ompi_comm_size(comm) > OMPI_AMD_MAX_RANKS ||
+        ompi_group_have_remote_peers(comm->c_local_group) || ompi_amd_device_count() < 1) {
+        return OMPI_SUCCESS;
+    }
+    snprintf(name, sizeof(name), "%u.%u.p", (unsigned) OMPI_PROC_MY_NAME->jobid,
+             (unsigned) ompi_comm_get_cid(comm));
+    if (OMPI_AMD_SUCCESS != ompi_amd_comm_create(name, ompi_comm_rank(comm), ompi_comm_size(comm),
+                                                 -1, &dev)) {
+        return OMPI_SUCCESS; /* every rank fails alike (the creation is collective) */
+    }
+    (void) ompi_amd_comm_set_param(dev, "timeout_ms", mca_pml_rocm_component.timeout_ms);
+    e = (struct rocm_comm *) calloc(1, sizeof(*e));
+    if (NULL == e) {
+        (void) ompi_amd_comm_destroy(dev);
+        return OMPI_ERR_OUT_OF_RESOURCE;
+    }
+    e->comm = comm;
+    e->dev = dev;
+    OPAL_THREAD_LOCK(&rocm_lock);
+    e->next = rocm_comms;
+    rocm_comms = e;
+    OPAL_THREAD_UNLOCK(&rocm_lock);
+    return OMPI_SUCCESS;
+}
+
+static int rocm_del_comm(struct ompi_communicator_t *comm)
+{
+    struct rocm_comm **pp, *e = NULL;
+    OPAL_THREAD_LOCK(&rocm_lock);
+    for (pp = &rocm_comms; NULL != *pp; pp = &(*pp)->next) {
+        if ((*pp)->comm == comm) {
+            e = *pp;
+            *pp = e->next;
+            break;
+        }
+    }
+    OPAL_THREAD_UNLOCK(&rocm_lock);
+    if (NULL != e) {
+        (void) ompi_amd_comm_destroy(e->dev); /* collective, like del_comm */
+        free(e);
+    }
+    return mca_pml_rocm_host.pml_del_comm(comm);
+}
+
+/* ------------------------------------------------------------- helpers */
+
+static int rocm_err(int rc)
+{
+    switch (rc) {
+    case OMPI_AMD_SUCCESS: return OMPI_SUCCESS;
+    case OMPI_AMD_ERR_TRUNCATE: return MPI_ERR_TRUNCATE;
+    case OMPI_AMD_ERR_BAD_PARAM: return OMPI_ERR_BAD_PARAM;
+    case OMPI_AMD_ERR_TIMEOUT: return OMPI_ERR_TIMEOUT;
+    default: return OMPI_ERROR;
+    }
+}
+
+/* library traffic: a library communicator and a user tag (ANY_TAG included) */
+static ompi_amd_comm_t *takes(struct ompi_communicator_t *comm, int tag, int peer)
+{
+    if (peer == MPI_PROC_NULL || (tag < 0 && tag != MPI_ANY_TAG)) return NULL;
+    return mca_pml_rocm_comm_of(comm);
+}
+
+static size_t type_bytes(struct ompi_datatype_t *dtype, size_t count)
+{
+    size_t size = 0;
+    (void) ompi_datatype_type_size(dtype, &size);
+    return size * count;
+}
+
+/* what the library gets for the user's buffer: the buffer itself when it is
+ * contiguous device memory, else device staging (packed for a send) */
+static int stage_for(mca_pml_rocm_request_t *r, int fill)
+{
+    r->bytes = type_bytes(r->dtype, r->count);
+    r->stage = NULL;
+    if (0 == r->bytes) return OMPI_SUCCESS;
+    if (ompi_datatype_is_contiguous_memory_layout(r->dtype, (int) r->count) &&
+        ompi_amd_is_device_pointer(r->buf)) {
+        return OMPI_SUCCESS;
+    }
+    if (OMPI_AMD_SUCCESS != ompi_amd_device_alloc(&r->stage, r->bytes)) return OMPI_ERR_OUT_OF_RESOURCE;
+    if (!fill) return OMPI_SUCCESS;
+    if (ompi_datatype_is_contiguous_memory_layout(r->dtype, (int) r->count)) {
+        return OMPI_AMD_SUCCESS == ompi_amd_memcpy(r->stage, r->buf, r->bytes) ? OMPI_SUCCESS
+                                                                               : OMPI_ERROR;
+    }
+    {
+        char *h = (char *) malloc(r->bytes);
+        int rc = OMPI_ERROR;
+        if (NULL == h) return OMPI_ERR_OUT_OF_RESOURCE;
+        if (MPI_SUCCESS == ompi_datatype_sndrcv(r->buf, (int) r->count, r->dtype, h, (int) r->bytes,
+                                                MPI_BYTE) &&
+            OMPI_AMD_SUCCESS == ompi_amd_memcpy(r->stage, h, r->bytes)) {
+            rc = OMPI_SUCCESS;
+        }
+        free(h);
+        return rc;
+    }
+}
+
+/* a staged receive's `got` bytes back into the user's buffer */
+static int unstage_recv(mca_pml_rocm_request_t *r, size_t got)
+{
+    if (NULL == r->stage || 0 == got) return OMPI_SUCCESS;
+    if (ompi_datatype_is_contiguous_memory_layout(r->dtype, (int) r->count)) {
+        return OMPI_AMD_SUCCESS == ompi_amd_memcpy(r->buf, r->stage, got) ? OMPI_SUCCESS : OMPI_ERROR;
+    }
+    {
+        size_t size = 0;
+        char *h = (char *) malloc(r->bytes);
+        int rc = OMPI_ERROR;
+        (void) ompi_datatype_type_size(r->dtype, &size);
+        if (NULL == h) return OMPI_ERR_OUT_OF_RESOURCE;
+        /* whole elements only (a short message fills a prefix of them) */
+        if (OMPI_AMD_SUCCESS == ompi_amd_memcpy(h, r->stage, got) &&
+            MPI_SUCCESS == ompi_datatype_sndrcv(h, (int) got, MPI_BYTE, r->buf,
+                                                (int) (size ? got / size : 0), r->dtype)) {
+            rc = OMPI_SUCCESS;
+        }
+        free(h);
+        return rc;
+    }
+}
+
+static void fill_status(ompi_status_public_t *st, const ompi_amd_status_t *s, int err)
+{
+    if (NULL == st) return;
+    st->MPI_SOURCE = s->source;
+    st->MPI_TAG = s->tag;
+    st->MPI_ERROR = err;
+    st->_cancelled = 0;
+    st->_ucount = s->bytes;
+}
+
+/* ------------------------------------------------------------- requests */
+
+static opal_mutex_t active_lock = OPAL_MUTEX_STATIC_INIT;
+static mca_pml_rocm_request_t *active;
+static int progress_registered;
+
+/* finish a library request that completed: unstage, status, error */
+static int finish(mca_pml_rocm_request_t *r, int rc, const ompi_amd_status_t *s)
+{
+    int err = rocm_err(rc);
+    if (OMPI_SUCCESS == err && !r->is_send) err = unstage_recv(r, s->bytes);
+    if (!r->is_send) fill_status(&r->super.req_status, s, err);
+    else r->super.req_status.MPI_ERROR = err;
+    (void) ompi_amd_p2p_free(r->lib);
+    r->lib = NULL;
+    if (NULL != r->stage) {
+        (void) ompi_amd_device_free(r->stage);
+        r->stage = NULL;
+    }
+    return err;
+}
+
+static int rocm_progress(void)
+{
+    mca_pml_rocm_request_t **pp, *done = NULL;
+    int completed = 0;
+    if (NULL == active) return 0;
+    OPAL_THREAD_LOCK(&active_lock);
+    pp = &active;
+    while (NULL != *pp) {
+        mca_pml_rocm_request_t *r = *pp;
+        ompi_amd_status_t s = {0, 0, 0, 0};
+        int fin = 0;
+        const int rc = ompi_amd_p2p_test(r->lib, &fin, &s);
+        if (OMPI_AMD_SUCCESS != rc || fin) {
+            (void) finish(r, rc, &s);
+            *pp = r->next_active;
+            r->next_active = done;
+            done = r;
+        } else {
+            pp = &r->next_active;
+        }
+    }
+    OPAL_THREAD_UNLOCK(&active_lock);
+    while (NULL != done) {
+        mca_pml_rocm_request_t *r = done;
+        done = r->next_active;
+        r->next_active = NULL;
+        ompi_request_complete(&r->super, true);
+        ++completed;
+    }
+    return completed;
+}
+
+static void link_active(mca_pml_rocm_request_t *r)
+{
+    OPAL_THREAD_LOCK(&active_lock);
+    r->next_active = active;
+    active = r;
+    if (!progress_registered) {
+        progress_registered = 1;
+        (void) opal_progress_register(rocm_progress);
+    }
+    OPAL_THREAD_UNLOCK(&active_lock);
+}
+
+static void unlink_active(mca_pml_rocm_request_t *r)
+{
+    mca_pml_rocm_request_t **pp;
+    OPAL_THREAD_LOCK(&active_lock);
+    for (pp = &active; NULL != *pp; pp = &(*pp)->next_active) {
+        if (*pp == r) {
+            *pp = r->next_active;
+            break;
+        }
+    }
+    OPAL_THREAD_UNLOCK(&active_lock);
+    r->next_active = NULL;
+}
+
+/* post the request's operation on the library */
+static int post(mca_pml_rocm_request_t *r)
+{
+    ompi_amd_comm_t *dev = mca_pml_rocm_comm_of(r->comm);
+    int rc;
+    if (NULL == dev) return OMPI_ERR_BAD_PARAM;
+    rc = stage_for(r, r->is_send);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (r->is_send) {
+        rc = ompi_amd_isend(dev, NULL != r->stage ? r->stage : r->buf, r->bytes, r->peer, r->tag,
+                            r->mode, NULL, &r->lib);
+    } else {
+        rc = ompi_amd_irecv(dev, NULL != r->stage ? r->stage : r->buf, r->bytes,
+                            MPI_ANY_SOURCE == r->peer ? OMPI_AMD_ANY_SOURCE : r->peer,
+                            MPI_ANY_TAG == r->tag ? OMPI_AMD_ANY_TAG : r->tag, NULL, &r->lib);
+    }
+    if (OMPI_AMD_SUCCESS != rc) {
+        if (NULL != r->stage) {
+            (void) ompi_amd_device_free(r->stage);
+            r->stage = NULL;
+        }
+        return rocm_err(rc);
+    }
+    r->super.req_complete = REQUEST_PENDING;
+    r->super.req_state = OMPI_REQUEST_ACTIVE;
+    r->super.req_status.MPI_ERROR = OMPI_SUCCESS;
+    link_active(r);
+    return OMPI_SUCCESS;
+}
+
+/* MPI_Start / MPI_Startall of persistent requests (request.h:60-77) */
+static int rocm_start_req(size_t count, ompi_request_t **requests)
+{
+    size_t i;
+    for (i = 0; i < count; ++i) {
+        mca_pml_rocm_request_t *r = (mca_pml_rocm_request_t *) requests[i];
+        int rc;
+        if (NULL == r) continue;
+        if (OMPI_REQUEST_ACTIVE == r->super.req_state && !REQUEST_COMPLETE(&r->super))
+            return OMPI_ERR_REQUEST;
+        rc = post(r);
+        if (OMPI_SUCCESS != rc) return rc;
+    }
+    return OMPI_SUCCESS;
+}
+
+/* MPI_Request_free: an active transfer is waited for first */
+static int rocm_free_req(ompi_request_t **rptr)
+{
+    mca_pml_rocm_request_t *r = (mca_pml_rocm_request_t *) *rptr;
+    int rc = OMPI_SUCCESS;
+    if (NULL != r->next_active) unlink_active(r);
+    if (NULL != r->lib) {
+        ompi_amd_status_t s = {0, 0, 0, 0};
+        rc = finish(r, ompi_amd_p2p_wait(r->lib, &s), &s);
+    }
+    OMPI_REQUEST_FINI(&r->super);
+    OBJ_RELEASE(r);
+    *rptr = MPI_REQUEST_NULL;
+    return rc;
+}
+
+static void rocm_request_construct(mca_pml_rocm_request_t *r)
+{
+    r->super.req_type = OMPI_REQUEST_PML;
+    r->super.req_status._cancelled = 0;
+    r->super.req_free = rocm_free_req;
+    r->super.req_start = rocm_start_req;
+    r->super.req_cancel = NULL;
+    r->lib = NULL;
+    r->stage = NULL;
+    r->next_active = NULL;
+}
+
+OBJ_CLASS_INSTANCE(mca_pml_rocm_request_t, ompi_request_t, rocm_request_construct, NULL);
+
+static mca_pml_rocm_request_t *new_req(int is_send, void *buf, size_t count,
+                                       struct ompi_datatype_t *dtype, int peer, int tag, int mode,
+                                       struct ompi_communicator_t *comm, bool persistent)
+{
+    mca_pml_rocm_request_t *r = OBJ_NEW(mca_pml_rocm_request_t);
+    if (NULL == r) return NULL;
+    OMPI_REQUEST_INIT(&r->super, persistent);
+    r->super.req_mpi_object.comm = comm;
+    r->is_send = is_send;
+    r->buf = buf;
+    r->count = count;
+    r->dtype = dtype;
+    r->peer = peer;
+    r->tag = tag;
+    r->mode = mode;
+    r->comm = comm;
+    return r;
+}
+
+/* ------------------------------------------------------------- pml entry points */
+
+static int rocm_isend(const void *buf, size_t count, struct ompi_datatype_t *dtype, int dst, int tag,
+                      mca_pml_base_send_mode_t mode, struct ompi_communicator_t *comm,
+                      struct ompi_request_t **request)
+{
+    mca_pml_rocm_request_t *r;
+    int rc;
+    if (NULL == takes(comm, tag, dst))
+        return mca_pml_rocm_host.pml_isend(buf, count, dtype, dst, tag, mode, comm, request);
+    r = new_req(1, (void *) buf, count, dtype, dst, tag, (int) mode, comm, false);
+    if (NULL == r) return OMPI_ERR_OUT_OF_RESOURCE;
+    rc = post(r);
+    if (OMPI_SUCCESS != rc) {
+        OBJ_RELEASE(r);
+        return rc;
+    }
+    *request = &r->super;
+    return OMPI_SUCCESS;
+}
+
+static int rocm_irecv(void *buf, size_t count, struct ompi_datatype_t *dtype, int src, int tag,
+                      struct ompi_communicator_t *comm, struct ompi_request_t **request)
+{
+    mca_pml_rocm_request_t *r;
+    int rc;
+    if (NULL == takes(comm, tag, src))
+        return mca_pml_rocm_host.pml_irecv(buf, count, dtype, src, tag, comm, request);
+    r = new_req(0, buf, count, dtype, src, tag, 0, comm, false);
+    if (NULL == r) return OMPI_ERR_OUT_OF_RESOURCE;
+    rc = post(r);
+    if (OMPI_SUCCESS != rc) {
+        OBJ_RELEASE(r);
+        return rc;
+    }
+    *request = &r->super;
+    return OMPI_SUCCESS;
+}
+
+static int rocm_isend_init(const void *buf, size_t count, struct ompi_datatype_t *dtype, int dst,
+                           int tag, mca_pml_base_send_mode_t mode, struct ompi_communicator_t *comm,
+                           struct ompi_request_t **request)
+{
+    mca_pml_rocm_request_t *r;
+    if (NULL == takes(comm, tag, dst))
+        return mca_pml_rocm_host.pml_isend_init(buf, count, dtype, dst, tag, mode, comm, request);
+    r = new_req(1, (void *) buf, count, dtype, dst, tag, (int) mode, comm, true);
+    if (NULL == r) return OMPI_ERR_OUT_OF_RESOURCE;
+    *request = &r->super;
+    return OMPI_SUCCESS;
+}
+
+static int rocm_irecv_init(void *buf, size_t count, struct ompi_datatype_t *dtype, int src, int tag,
+                           struct ompi_communicator_t *comm, struct ompi_request_t **request)
+{
+    mca_pml_rocm_request_t *r;
+    if (NULL == takes(comm, tag, src))
+        return mca_pml_rocm_host.pml_irecv_init(buf, count, dtype, src, tag, comm, request);
+    r = new_req(0, buf, count, dtype, src, tag, 0, comm, true);
+    if (NULL == r) return OMPI_ERR_OUT_OF_RESOURCE;
+    *request = &r->super;
+    return OMPI_SUCCESS;
+}
+
+/* pml_start: requests of this component start themselves; others go to the
+ * saved PML (a mixed array is split in order) */
+static int rocm_start(size_t count, ompi_request_t **requests)
+{
+    size_t i;
+    for (i = 0; i < count; ++i) {
+        ompi_request_t *q = requests[i];
+        int rc;
+        if (NULL == q) continue;
+        rc = q->req_start == rocm_start_req ? rocm_start_req(1, &requests[i])
+                                           : mca_pml_rocm_host.pml_start(1, &requests[i]);
+        if (OMPI_SUCCESS != rc) return rc;
+    }
+    return OMPI_SUCCESS;
+}
+
+static int rocm_send(const void *buf, size_t count, struct ompi_datatype_t *dtype, int dst, int tag,
+                     mca_pml_base_send_mode_t mode, struct ompi_communicator_t *comm)
+{
+    mca_pml_rocm_request_t r;
+    ompi_amd_comm_t *dev = takes(comm, tag, dst);
+    int rc;
+    if (NULL == dev) return mca_pml_rocm_host.pml_send(buf, count, dtype, dst, tag, mode, comm);
+    memset(&r, 0, sizeof(r));
+    r.buf = (void *) buf;
+    r.count = count;
+    r.dtype = dtype;
+    rc = stage_for(&r, 1);
+    if (OMPI_SUCCESS != rc) return rc;
+    rc = rocm_err(ompi_amd_send(dev, NULL != r.stage ? r.stage : buf, r.bytes, dst, tag, (int) mode,
+                                NULL));
+    if (NULL != r.stage) (void) ompi_amd_device_free(r.stage);
+    return rc;
+}
+
+static int rocm_recv(void *buf, size_t count, struct ompi_datatype_t *dtype, int src, int tag,
+                     struct ompi_communicator_t *comm, ompi_status_public_t *status)
+{
+    mca_pml_rocm_request_t r;
+    ompi_amd_status_t s = {0, 0, 0, 0};
+    ompi_amd_comm_t *dev = takes(comm, tag, src);
+    int rc;
+    if (NULL == dev) return mca_pml_rocm_host.pml_recv(buf, count, dtype, src, tag, comm, status);
+    memset(&r, 0, sizeof(r));
+    r.buf = buf;
+    r.count = count;
+    r.dtype = dtype;
+    rc = stage_for(&r, 0);
+    if (OMPI_SUCCESS != rc) return rc;
+    rc = rocm_err(ompi_amd_recv(dev, NULL != r.stage ? r.stage : buf, r.bytes,
+                                MPI_ANY_SOURCE == src ? OMPI_AMD_ANY_SOURCE : src,
+                                MPI_ANY_TAG == tag ? OMPI_AMD_ANY_TAG : tag, NULL, &s));
+    if (OMPI_SUCCESS == rc) rc = unstage_recv(&r, s.bytes);
+    if (NULL != r.stage) (void) ompi_amd_device_free(r.stage);
+    fill_status(status, &s, rc);
+    return rc;
+}
+
+static int rocm_iprobe(int src, int tag, struct ompi_communicator_t *comm, int *matched,
+                       ompi_status_public_t *status)
+{
+    ompi_amd_status_t s = {0, 0, 0, 0};
+    ompi_amd_comm_t *dev = takes(comm, tag, src);
+    int rc;
+    if (NULL == dev) return mca_pml_rocm_host.pml_iprobe(src, tag, comm, matched, status);
+    rc = rocm_err(ompi_amd_iprobe(dev, MPI_ANY_SOURCE == src ? OMPI_AMD_ANY_SOURCE : src,
+                                  MPI_ANY_TAG == tag ? OMPI_AMD_ANY_TAG : tag, matched, &s));
+    if (OMPI_SUCCESS == rc && *matched) fill_status(status, &s, OMPI_SUCCESS);
+    return rc;
+}
+
+static int rocm_probe(int src, int tag, struct ompi_communicator_t *comm, ompi_status_public_t *status)
+{
+    ompi_amd_status_t s = {0, 0, 0, 0};
+    ompi_amd_comm_t *dev = takes(comm, tag, src);
+    int rc;
+    if (NULL == dev) return mca_pml_rocm_host.pml_probe(src, tag, comm, status);
+    rc = rocm_err(ompi_amd_probe(dev, MPI_ANY_SOURCE == src ? OMPI_AMD_ANY_SOURCE : src,
+                                 MPI_ANY_TAG == tag ? OMPI_AMD_ANY_TAG : tag, &s));
+    if (OMPI_SUCCESS == rc) fill_status(status, &s, OMPI_SUCCESS);
+    return rc;
+}
+
+/* matched probes of library traffic are not provided */
+static int rocm_improbe(int src, int tag, struct ompi_communicator_t *comm, int *matched,
+                        struct ompi_message_t **message, ompi_status_public_t *status)
+{
+    if (NULL != takes(comm, tag, src)) return OMPI_ERR_NOT_SUPPORTED;
+    return mca_pml_rocm_host.pml_improbe(src, tag, comm, matched, message, status);
+}
+
+static int rocm_mprobe(int src, int tag, struct ompi_communicator_t *comm,
+                       struct ompi_message_t **message, ompi_status_public_t *status)
+{
+    if (NULL != takes(comm, tag, src)) return OMPI_ERR_NOT_SUPPORTED;
+    return mca_pml_rocm_host.pml_mprobe(src, tag, comm, message, status);
+}
+
+/* close: after the PML base selected the real PML — save it, interpose */
+static int rocm_close(void)
+{
+    if (!mca_pml_rocm_component.enable || mca_pml_rocm_installed || NULL == mca_pml.pml_isend)
+        return OMPI_SUCCESS;
+    mca_pml_rocm_host = mca_pml;
+    mca_pml.pml_add_comm = rocm_add_comm;
+    mca_pml.pml_del_comm = rocm_del_comm;
+    mca_pml.pml_isend = rocm_isend;
+    mca_pml.pml_send = rocm_send;
+    mca_pml.pml_irecv = rocm_irecv;
+    mca_pml.pml_recv = rocm_recv;
+    mca_pml.pml_isend_init = rocm_isend_init;
+    mca_pml.pml_irecv_init = rocm_irecv_init;
+    mca_pml.pml_start = rocm_start;
+    mca_pml.pml_iprobe = rocm_iprobe;
+    mca_pml.pml_probe = rocm_probe;
+    mca_pml.pml_improbe = rocm_improbe;
+    mca_pml.pml_mprobe = rocm_mprobe;
+    mca_pml_rocm_installed = 1;
+    return OMPI_SUCCESS;
+}

@@ -416,11 +416,106 @@ def case_allgather(comm, rank, n, nbytes, salt, inplace=False):
     return bool(np.array_equal(out.cpu().numpy(), exp)), ""
 
 
-def case_bcast(comm, rank, n, nbytes, root, salt):
+def case_bcast(comm, rank, n, nbytes, root, salt, expect_split=None):
     data = np.random.default_rng(SEED + salt).integers(0, 256, nbytes, dtype=np.uint8)
     buf = to_dev(data) if rank == root else torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+    before = comm.get_param("bcast_split")
     comm.bcast(buf, nbytes, root, blocking=True)
-    return bool(np.array_equal(buf.cpu().numpy()[:nbytes], data)), ""
+    ok = bool(np.array_equal(buf.cpu().numpy()[:nbytes], data))
+    split = comm.get_param("bcast_split") - before
+    if expect_split is not None and ok and split != expect_split:
+        return False, f"scatter+allgather used {split} times, expected {expect_split}"
+    return ok, ""
+
+
+def case_bcast_paths(comm, rank, n, salt):
+    """Large bcast as scatter + allgather vs the root pull, sizes around the
+    split threshold and the 256-B block rounding, every root."""
+    msgs = []
+    before = comm.get_param("bcast_split")
+    cases = (((4 << 20) - 1, 0), ((4 << 20), None), ((4 << 20) + 257, None),
+             ((16 << 20) + 13, None), (n * 256 * 3 + 1 + (4 << 20), None))
+    for i, (nbytes, split) in enumerate(cases):
+        # above the threshold a refused export (recycled handle) may send a
+        # call to the root pull: only the data and "never below" are exact
+        for root in range(n):
+            ok, msg = case_bcast(comm, rank, n, nbytes, root, salt + 7 * i + root, expect_split=split)
+            if not ok:
+                msgs.append(f"{nbytes} B root {root}: {msg or 'data differ'}")
+    if comm.get_param("bcast_split") == before:
+        msgs.append("no bcast ran as scatter + allgather")
+    comm.set_param("bcast_split_bytes", 0)
+    try:
+        ok, msg = case_bcast(comm, rank, n, (16 << 20) + 13, n - 1, salt + 99, expect_split=0)
+        if not ok:
+            msgs.append(f"root pull, split off: {msg or 'data differ'}")
+    finally:
+        comm.set_param("bcast_split_bytes", 4 << 20)
+    return not msgs, "; ".join(msgs)
+
+
+def case_nonblocking_mix(comm, rank, n, salt, big):
+    """MPI_Ireduce_scatter_block / MPI_Iallgather / MPI_Ibcast (and one
+    MPI_Iallreduce) posted back to back, staged and zero-copy sizes, in place
+    and not, rank 0 posting while the others sleep; every result checked
+    against the oracle / the inputs after all are waited on."""
+    import time
+    F, D = mop.MPI_FLOAT, mop.MPI_DOUBLE
+    if rank != 0:
+        time.sleep(0.05 * rank)
+    todo, keep = [], []
+    specs = [("rsb", F, 1001, False), ("rsb", F, big // n + 7, False), ("rsb", D, big // (2 * n) + 3, True),
+             ("ag", None, 4099, False), ("ag", None, big * 4 // n + 5, True), ("bc", None, 70001, 0),
+             ("bc", None, big * 4 + 3, 1), ("ar", F, big + 1, False), ("rsb", F, 5, True)]
+    for i, (kind, dt, cnt, extra) in enumerate(specs):
+        if kind == "rsb":
+            xs = [inputs(dt, cnt * n, r, salt + i) for r in range(n)]
+            exp = orc.reduce_scatter_block([x.copy() for x in xs], cnt, mop.MPI_SUM.index, dt.code)
+            s = to_dev(xs[rank])
+            if extra:  # in place
+                req = comm.ireduce_scatter_block(coll.IN_PLACE, s, cnt, dt, mop.MPI_SUM)
+                out = s
+            else:
+                out = torch.zeros(cnt * dt.extent, dtype=torch.uint8, device="cuda")
+                req = comm.ireduce_scatter_block(s, out, cnt, dt, mop.MPI_SUM)
+            todo.append((f"rsb{i}", req, out, cnt * dt.extent, exp[rank].view(np.uint8)))
+            keep.append(s)
+        elif kind == "ag":
+            xs = [np.random.default_rng(SEED + salt + i + r).integers(0, 256, cnt, dtype=np.uint8)
+                  for r in range(n)]
+            out = torch.zeros(cnt * n, dtype=torch.uint8, device="cuda")
+            if extra:
+                out[rank * cnt:(rank + 1) * cnt].copy_(torch.from_numpy(xs[rank]))
+                req = comm.iallgather(coll.IN_PLACE, out, cnt)
+            else:
+                s = to_dev(xs[rank])
+                keep.append(s)
+                req = comm.iallgather(s, out, cnt)
+            todo.append((f"ag{i}", req, out, cnt * n, np.concatenate(xs)))
+        elif kind == "bc":
+            root = extra % n
+            data = np.random.default_rng(SEED + salt + i).integers(0, 256, cnt, dtype=np.uint8)
+            buf = to_dev(data) if rank == root else torch.zeros(cnt, dtype=torch.uint8, device="cuda")
+            req = comm.ibcast(buf, cnt, root)
+            todo.append((f"bc{i}", req, buf, cnt, data))
+        else:
+            xs = [inputs(dt, cnt, r, salt + i) for r in range(n)]
+            exp, _ = orc.allreduce([x.copy() for x in xs], cnt, mop.MPI_SUM.index, dt.code)
+            s = to_dev(xs[rank])
+            out = torch.zeros_like(s)
+            keep.append(s)
+            req = comm.iallreduce(s, out, cnt, dt, mop.MPI_SUM)
+            todo.append((f"ar{i}", req, out, cnt * dt.extent, exp[rank].view(np.uint8)))
+    bad = []
+    for name, req, out, nb, exp in reversed(todo):  # completion order is free
+        req.wait()
+    torch.cuda.synchronize()
+    for name, req, out, nb, exp in todo:
+        req.free()
+        got = out.cpu().numpy()[:nb]
+        if not np.array_equal(got, exp[:nb]):
+            bad.append(f"{name}: {int(np.count_nonzero(got != exp[:nb]))}/{nb} bytes differ")
+    return not bad, "; ".join(bad)
 
 
 def case_pipelined(comm, rank, n, salt):
@@ -531,6 +626,7 @@ def main():
         ("allgather_inplace", lambda: case_allgather(comm, rank, n, 65536, 23, True)),
         ("bcast_small_root0", lambda: case_bcast(comm, rank, n, 777, 0, 24)),
         ("bcast_big_rootlast", lambda: case_bcast(comm, rank, n, big * 4 + 3, n - 1, 25)),
+        ("bcast_scatter_allgather", lambda: case_bcast_paths(comm, rank, n, 26)),
         ("pipelined_nonblocking", lambda: case_pipelined(comm, rank, n, 26)),
         # reduce: staged (linear / binomial / binary by size) and zero-copy
         ("reduce_sum_f32_100_rootlast",
@@ -627,6 +723,14 @@ def main():
         hc = int(os.environ["COLL_HEADLINE"])
         cases = [(f"headline_alg{a}", lambda a=a: case_headline(comm, rank, n, hc, 95 + a, a))
                  for a in (0, 1, 2)]
+    def shadowed_nb(fn):  # the export fallback for the nonblocking forms
+        def run():
+            comm.set_param("force_shadow", 1)
+            try:
+                return fn()
+            finally:
+                comm.set_param("force_shadow", 0)
+        return run
     # coll/tuned's forced allreduce algorithms (1 basic_linear, 2 nonoverlapping,
     # 3 recursive doubling, 4 ring, 5 segmented ring, 6 Rabenseifner), every path
     if not os.environ.get("COLL_HEADLINE"):
@@ -654,6 +758,9 @@ def main():
                                                                inplace=True, how="persistent")),
             ("persistent_inplace_sum_f32", lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, 300001, 146,
                                                                    inplace=True)),
+            ("nonblocking_rsb_ag_bcast", lambda: case_nonblocking_mix(comm, rank, n, 150, big)),
+            ("nonblocking_rsb_ag_bcast_shadow",
+             shadowed_nb(lambda: case_nonblocking_mix(comm, rank, n, 160, big))),
         ]
     # the export fallback (hipIpcGetMemHandle refused): every zero-copy path
     # through the communicator's shadow buffers ("force_shadow")
@@ -693,6 +800,14 @@ def main():
                 comm, rank, n, D, mop.MPI_SUM, big // 2, 112, inplace=True), 2))),
         ]
     only = os.environ.get("COLL_CASES")
+    # COLL_FROM / COLL_UNTIL: a contiguous slice of the list (history-dependent failures)
+    first, last = os.environ.get("COLL_FROM"), os.environ.get("COLL_UNTIL")
+    if first or last:
+        names = [c[0] for c in cases]
+        lo = names.index(first) if first else 0
+        hi = names.index(last) + 1 if last else len(names)
+        cases = cases[lo:hi]
+        only = None
     ok_all = True
     for name, fn in cases:
         if only and name not in only.split(","):
@@ -711,7 +826,7 @@ def main():
         report(rank, n, {"rank": rank, "case": name, "ok": bool(ok), "msg": msg,
                          "state": {k: comm.get_param(k) for k in (
                              "epoch", "shadowed", "recycled_exports", "stale_closed", "exports_new",
-                             "imports_new", "imports", "landing_bytes", "aliased_opens", "boot_calls")}})
+                             "imports_new", "imports", "landing_bytes", "aliased_opens", "boot_calls", "ipc_reopens", "memcpy_token_mismatch")}})
         ok_all &= bool(ok)
     # zero-copy disabled: everything staged through the scratch
     if ok_all and not only and not os.environ.get("COLL_HEADLINE"):

@@ -129,6 +129,17 @@ static int t_iallreduce(const void *s, void *r, int c, struct ompi_datatype_t *d
                         mca_coll_base_module_t *m)
 { tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
 
+static int t_iallgather(const void *s, int sc, struct ompi_datatype_t *sd, void *r, int rc,
+                        struct ompi_datatype_t *rd, struct ompi_communicator_t *cm,
+                        ompi_request_t **req, mca_coll_base_module_t *m)
+{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
+static int t_ibcast(void *b, int c, struct ompi_datatype_t *d, int root,
+                    struct ompi_communicator_t *cm, ompi_request_t **req, mca_coll_base_module_t *m)
+{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
+static int t_irsb(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                  struct ompi_communicator_t *cm, ompi_request_t **req, mca_coll_base_module_t *m)
+{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
+
 static void fill_tuned(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *tm)
 {
     memset(t, 0, sizeof(*t));
@@ -143,6 +154,9 @@ static void fill_tuned(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *tm)
     SET(bcast, t_bcast);
     SET(iallreduce, t_iallreduce);
     SET(allreduce_init, t_ar_init);
+    SET(iallgather, t_iallgather);
+    SET(ibcast, t_ibcast);
+    SET(ireduce_scatter_block, t_irsb);
 #undef SET
 }
 
@@ -154,6 +168,7 @@ static void install(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *m)
     INST(allreduce) INST(reduce) INST(reduce_scatter) INST(reduce_scatter_block) INST(scan)
     INST(exscan)
     INST(allgather) INST(bcast) INST(iallreduce) INST(allreduce_init)
+    INST(iallgather) INST(ibcast) INST(ireduce_scatter_block)
 #undef INST
 }
 
@@ -169,6 +184,9 @@ static void release_table(mca_coll_base_comm_coll_t *t)
     OBJ_RELEASE(t->coll_bcast_module);
     OBJ_RELEASE(t->coll_iallreduce_module);
     OBJ_RELEASE(t->coll_allreduce_init_module);
+    OBJ_RELEASE(t->coll_iallgather_module);
+    OBJ_RELEASE(t->coll_ibcast_module);
+    OBJ_RELEASE(t->coll_ireduce_scatter_block_module);
 }
 
 /* deterministic per-rank floats in [-1, 1): fp sums depend on order */
@@ -242,6 +260,7 @@ int main(int argc, char **argv)
     CHECK(m->coll_allreduce && m->coll_reduce && m->coll_reduce_scatter &&
               m->coll_reduce_scatter_block && m->coll_scan &&
               m->coll_exscan && m->coll_allgather && m->coll_bcast && m->coll_allreduce_init && m->coll_iallreduce &&
+              m->coll_iallgather && m->coll_ibcast && m->coll_ireduce_scatter_block &&
               m->coll_module_enable,
           "module function table");
     {
@@ -266,7 +285,7 @@ int main(int argc, char **argv)
     }
 
     CHECK(m->coll_module_enable(m, &comm) == OMPI_SUCCESS, "enable");
-    CHECK(tm->super.obj_reference_count == 1 + 10 + 10, "enable retains the saved modules (%d)",
+    CHECK(tm->super.obj_reference_count == 1 + 13 + 13, "enable retains the saved modules (%d)",
           tm->super.obj_reference_count);
     install(&table, m);
     /* sections 1-8: the per-call residency vote (never locks) */
@@ -555,6 +574,88 @@ int main(int argc, char **argv)
                                         table.coll_iallreduce_module) == OMPI_SUCCESS &&
                       tuned_calls == 1 && hr == &t_request,
                   "host iallreduce falls back");
+        }
+    }
+    /* 10. MPI_Ireduce_scatter_block / MPI_Iallgather / MPI_Ibcast on device
+     * buffers (staged and zero-copy sizes, all outstanding at once, completed
+     * through opal_progress), bit-exact; host buffers go to the saved ones */
+    {
+        const size_t rcs[2] = {700, 300001};
+        const size_t agb[2] = {3000, 1500001};
+        float **xs[2], **rb[2];
+        void *ds[2], *dr[2], *ag_d[2], *bc_d[2];
+        unsigned char *ag_all[2], *bc_data[2];
+        ompi_request_t *req[6];
+        int nr = 0;
+        tuned_calls = 0;
+        for (int k = 0; k < 2; ++k) {
+            const size_t rc = rcs[k], n = rc * (size_t) g_size;
+            xs[k] = all_inputs(n, 80 + k);
+            rb[k] = malloc(sizeof(float *) * (size_t) g_size);
+            for (int r = 0; r < g_size; ++r) rb[k][r] = calloc(rc, sizeof(float));
+            CHECK(orc_reduce_scatter_block(g_size, (const void *const *) xs[k], (void *const *) rb[k],
+                                           rc, ORC_OP_SUM, ORC_T_FLOAT) >= 0, "oracle rsb");
+            ds[k] = dev_of(xs[k][g_rank], n * 4);
+            {
+                float *z = calloc(rc, sizeof(float));
+                dr[k] = dev_of(z, rc * 4);
+                free(z);
+            }
+            CHECK(table.coll_ireduce_scatter_block(ds[k], dr[k], (int) rc, &dfloat, &sum, &comm,
+                                                   &req[nr++],
+                                                   table.coll_ireduce_scatter_block_module) ==
+                      OMPI_SUCCESS, "ireduce_scatter_block");
+            /* allgather of agb[k] bytes per rank */
+            ag_all[k] = malloc(agb[k] * (size_t) g_size);
+            for (int r = 0; r < g_size; ++r)
+                for (size_t b = 0; b < agb[k]; ++b)
+                    ag_all[k][(size_t) r * agb[k] + b] = (unsigned char) (r * 41 + b * 7 + k);
+            {
+                unsigned char *z = calloc(agb[k] * (size_t) g_size, 1);
+                memcpy(z + (size_t) g_rank * agb[k], ag_all[k] + (size_t) g_rank * agb[k], agb[k]);
+                ag_d[k] = dev_of(z, agb[k] * (size_t) g_size);  /* in place */
+                free(z);
+            }
+            CHECK(table.coll_iallgather(MPI_IN_PLACE, 0, &dbyte, ag_d[k], (int) agb[k], &dbyte, &comm,
+                                        &req[nr++], table.coll_iallgather_module) == OMPI_SUCCESS,
+                  "iallgather");
+            /* bcast of agb[k] bytes from rank k % size */
+            bc_data[k] = malloc(agb[k]);
+            for (size_t b = 0; b < agb[k]; ++b) bc_data[k][b] = (unsigned char) (b * 13 + k + 1);
+            {
+                unsigned char *z = calloc(agb[k], 1);
+                bc_d[k] = dev_of(g_rank == k % g_size ? bc_data[k] : z, agb[k]);
+                free(z);
+            }
+            CHECK(table.coll_ibcast(bc_d[k], (int) agb[k], &dbyte, k % g_size, &comm, &req[nr++],
+                                    table.coll_ibcast_module) == OMPI_SUCCESS, "ibcast");
+        }
+        CHECK(tuned_calls == 0, "device nonblocking collectives fell back");
+        for (int i = nr - 1; i >= 0; --i) {
+            harness_wait(req[i]);
+            CHECK(req[i]->req_status.MPI_ERROR == OMPI_SUCCESS, "nonblocking status");
+            CHECK(req[i]->req_free(&req[i]) == OMPI_SUCCESS, "nonblocking free");
+        }
+        for (int k = 0; k < 2; ++k) {
+            expect_dev(dr[k], rb[k][g_rank], rcs[k] * 4, "ireduce_scatter_block");
+            expect_dev(ag_d[k], ag_all[k], agb[k] * (size_t) g_size, "iallgather");
+            expect_dev(bc_d[k], bc_data[k], agb[k], "ibcast");
+            harness_dev_free(ds[k]);
+            harness_dev_free(dr[k]);
+            harness_dev_free(ag_d[k]);
+            harness_dev_free(bc_d[k]);
+            for (int r = 0; r < g_size; ++r) free(rb[k][r]);
+            free(rb[k]);
+            free_inputs(xs[k]);
+            free(ag_all[k]);
+            free(bc_data[k]);
+        }
+        {
+            unsigned char h[64] = {0};
+            ompi_request_t *hr = NULL;
+            CHECK(table.coll_ibcast(h, 64, &dbyte, 0, &comm, &hr, table.coll_ibcast_module) ==
+                      OMPI_SUCCESS && tuned_calls == 1 && hr == &t_request,
+                  "host ibcast falls back");
         }
     }
     /* 9. residency policy: unanimous votes lock the module, a locked call

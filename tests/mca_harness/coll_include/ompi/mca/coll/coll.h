@@ -1,6 +1,6 @@
 /* TEST HARNESS ONLY: the coll framework types the glue uses, with the
  * reference's function signatures (ompi/mca/coll/coll.h:141-143, 200-250,
- * 271-274, 349-352, 471-603). */
+ * 261-274, 293-296, 319-322, 349-352, 471-603). */
 #ifndef HARNESS_COLL_H
 #define HARNESS_COLL_H
 #include <stdbool.h>
@@ -40,6 +40,17 @@ typedef int (*mca_coll_base_module_iallreduce_fn_t)(const void *, void *, int,
                                                     struct ompi_datatype_t *, struct ompi_op_t *,
                                                     struct ompi_communicator_t *,
                                                     ompi_request_t **, HMOD);
+typedef int (*mca_coll_base_module_iallgather_fn_t)(const void *, int, struct ompi_datatype_t *,
+                                                    void *, int, struct ompi_datatype_t *,
+                                                    struct ompi_communicator_t *, ompi_request_t **,
+                                                    HMOD);
+typedef int (*mca_coll_base_module_ibcast_fn_t)(void *, int, struct ompi_datatype_t *, int,
+                                                struct ompi_communicator_t *, ompi_request_t **, HMOD);
+typedef int (*mca_coll_base_module_ireduce_scatter_block_fn_t)(const void *, void *, int,
+                                                               struct ompi_datatype_t *,
+                                                               struct ompi_op_t *,
+                                                               struct ompi_communicator_t *,
+                                                               ompi_request_t **, HMOD);
 typedef int (*mca_coll_base_module_allreduce_init_fn_t)(const void *, void *, int,
                                                         struct ompi_datatype_t *, struct ompi_op_t *,
                                                         struct ompi_communicator_t *,
@@ -57,7 +68,10 @@ typedef struct mca_coll_base_module_2_3_0_t {
     mca_coll_base_module_reduce_scatter_fn_t coll_reduce_scatter;
     mca_coll_base_module_reduce_scatter_block_fn_t coll_reduce_scatter_block;
     mca_coll_base_module_scan_fn_t coll_scan;
+    mca_coll_base_module_iallgather_fn_t coll_iallgather;
     mca_coll_base_module_iallreduce_fn_t coll_iallreduce;
+    mca_coll_base_module_ibcast_fn_t coll_ibcast;
+    mca_coll_base_module_ireduce_scatter_block_fn_t coll_ireduce_scatter_block;
     mca_coll_base_module_allreduce_init_fn_t coll_allreduce_init;
     void *base_data;
 } mca_coll_base_module_2_3_0_t;
@@ -77,7 +91,8 @@ typedef struct mca_coll_base_component_2_0_0_t {
 typedef struct mca_coll_base_comm_coll_t {
     HFN(allgather) HFN(allreduce) HFN(bcast) HFN(exscan) HFN(reduce) HFN(reduce_scatter)
     HFN(reduce_scatter_block)
-    HFN(scan) HFN(iallreduce) HFN(allreduce_init)
+    HFN(scan) HFN(iallgather) HFN(iallreduce) HFN(ibcast) HFN(ireduce_scatter_block)
+    HFN(allreduce_init)
 } mca_coll_base_comm_coll_t;
 #undef HFN
 #define MCA_COLL_BASE_VERSION_2_0_0 OMPI_MCA_BASE_VERSION_2_1_0("coll", 2, 0, 0)

@@ -16,7 +16,10 @@ typedef enum { OMPI_REQUEST_PML, OMPI_REQUEST_IO, OMPI_REQUEST_GEN, OMPI_REQUEST
                OMPI_REQUEST_MAX } ompi_request_type_t;
 typedef enum { OMPI_REQUEST_INVALID, OMPI_REQUEST_INACTIVE, OMPI_REQUEST_ACTIVE,
                OMPI_REQUEST_CANCELLED } ompi_request_state_t;
-typedef struct ompi_status_public_t { int MPI_SOURCE, MPI_TAG, MPI_ERROR, _cancelled; } ompi_status_public_t;
+typedef struct ompi_status_public_t {
+    int MPI_SOURCE, MPI_TAG, MPI_ERROR, _cancelled;
+    size_t _ucount;
+} ompi_status_public_t;
 typedef union ompi_mpi_object_t { struct ompi_communicator_t *comm; } ompi_mpi_object_t;
 typedef struct ompi_request_t {
     opal_object_t super;

@@ -1,0 +1,337 @@
+/*
+ * TEST HARNESS ONLY.  One rank of a multi-process run that drives
+ * ompi_amd/mca/pml/rocm/pml_rocm.c the way the PML base does
+ * (pml_base_select.c, pml_v_component.c:123-160): a stand-in "ob1" module is
+ * the selected PML (its functions count and complete at once), pml/rocm's
+ * init declines, its close interposes on mca_pml, pml_add_comm creates the
+ * library communicator; then MPI-level traffic goes through mca_pml.
+ *
+ *   CPU (HARNESS_GPU=0): init declines, close installs the functions and
+ *   saves ob1's; a communicator gets no library state without a device and
+ *   every call reaches ob1.
+ *   GPU (HARNESS_GPU=1): a ring of isend/irecv on device buffers (0 B,
+ *   eager, rendezvous, 8 MiB), byte-exact; blocking send/recv from host
+ *   memory (staged); a non-contiguous receive type (packed, gaps kept);
+ *   ANY_SOURCE / ANY_TAG status; iprobe / probe; persistent send/recv
+ *   started three times; truncation; negative (system) tags and PROC_NULL
+ *   reach ob1; matched probes of library traffic are refused.
+ *
+ * usage: pml_harness <segment-name-hex> <rank> <size>; prints "ok" / "ok gpu".
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mpi.h"
+#include "ompi/communicator/communicator.h"
+#include "ompi/constants.h"
+#include "ompi/datatype/ompi_datatype.h"
+#include "ompi/mca/pml/pml.h"
+#include "ompi/runtime/ompi_rte.h"
+#include "opal/runtime/opal_progress.h"
+#include "pml_rocm.h"
+#include "ompi_amd.h"
+
+extern int harness_dev_alloc_copy(void **d, const void *h, size_t bytes);
+extern int harness_dev_copy_back(void *h, const void *d, size_t bytes);
+extern int harness_dev_copy_in(void *d, const void *h, size_t bytes);
+extern int harness_dev_free(void *d);
+
+OBJ_CLASS_INSTANCE(ompi_request_t, opal_object_t, NULL, NULL);
+ompi_request_t harness_request_null;
+harness_proc_name_t harness_proc_name = {4343, 0};
+struct ompi_datatype_t harness_mpi_byte = {0, 1, 1, 1};
+mca_pml_base_module_t mca_pml;
+
+static opal_progress_callback_t progress_cbs[8];
+static int n_progress_cbs;
+int opal_progress_register(opal_progress_callback_t cb)
+{
+    progress_cbs[n_progress_cbs++] = cb;
+    return 0;
+}
+int opal_progress_unregister(opal_progress_callback_t cb) { return 0; }
+void opal_progress(void)
+{
+    for (int i = 0; i < n_progress_cbs; ++i) progress_cbs[i]();
+}
+
+static int g_rank, g_size;
+#define CHECK(c, ...)                                                             \
+    do {                                                                          \
+        if (!(c)) {                                                               \
+            fprintf(stderr, "FAIL rank %d %s:%d: ", g_rank, __FILE__, __LINE__);  \
+            fprintf(stderr, __VA_ARGS__);                                         \
+            fprintf(stderr, "\n");                                                \
+            exit(1);                                                              \
+        }                                                                         \
+    } while (0)
+
+/* ---- the selected PML ("ob1"): count, complete at once ---- */
+static int ob1_calls;
+static ompi_request_t ob1_req;
+static int o_add_comm(struct ompi_communicator_t *c) { return OMPI_SUCCESS; }
+static int o_del_comm(struct ompi_communicator_t *c) { return OMPI_SUCCESS; }
+static int o_isend(const void *b, size_t n, struct ompi_datatype_t *d, int dst, int tag,
+                   mca_pml_base_send_mode_t m, struct ompi_communicator_t *c, ompi_request_t **r)
+{ ob1_calls++; *r = &ob1_req; return OMPI_SUCCESS; }
+static int o_send(const void *b, size_t n, struct ompi_datatype_t *d, int dst, int tag,
+                  mca_pml_base_send_mode_t m, struct ompi_communicator_t *c)
+{ ob1_calls++; return OMPI_SUCCESS; }
+static int o_irecv(void *b, size_t n, struct ompi_datatype_t *d, int src, int tag,
+                   struct ompi_communicator_t *c, ompi_request_t **r)
+{ ob1_calls++; *r = &ob1_req; return OMPI_SUCCESS; }
+static int o_recv(void *b, size_t n, struct ompi_datatype_t *d, int src, int tag,
+                  struct ompi_communicator_t *c, ompi_status_public_t *s)
+{ ob1_calls++; return OMPI_SUCCESS; }
+static int o_isend_init(const void *b, size_t n, struct ompi_datatype_t *d, int dst, int tag,
+                        mca_pml_base_send_mode_t m, struct ompi_communicator_t *c, ompi_request_t **r)
+{ ob1_calls++; *r = &ob1_req; return OMPI_SUCCESS; }
+static int o_irecv_init(void *b, size_t n, struct ompi_datatype_t *d, int src, int tag,
+                        struct ompi_communicator_t *c, ompi_request_t **r)
+{ ob1_calls++; *r = &ob1_req; return OMPI_SUCCESS; }
+static int o_start(size_t n, ompi_request_t **r) { ob1_calls++; return OMPI_SUCCESS; }
+static int o_iprobe(int s, int t, struct ompi_communicator_t *c, int *m, ompi_status_public_t *st)
+{ ob1_calls++; *m = 0; return OMPI_SUCCESS; }
+static int o_probe(int s, int t, struct ompi_communicator_t *c, ompi_status_public_t *st)
+{ ob1_calls++; return OMPI_SUCCESS; }
+static int o_improbe(int s, int t, struct ompi_communicator_t *c, int *m, struct ompi_message_t **msg,
+                     ompi_status_public_t *st)
+{ ob1_calls++; *m = 0; return OMPI_SUCCESS; }
+static int o_mprobe(int s, int t, struct ompi_communicator_t *c, struct ompi_message_t **msg,
+                    ompi_status_public_t *st)
+{ ob1_calls++; return OMPI_SUCCESS; }
+
+static void wait_req(ompi_request_t *r)
+{
+    while (!REQUEST_COMPLETE(r)) opal_progress();
+}
+
+static unsigned char pat(int src, size_t i, int salt) { return (unsigned char)(src * 37 + i * 11 + salt); }
+
+int main(int argc, char **argv)
+{
+    const int use_gpu = getenv("HARNESS_GPU") && atoi(getenv("HARNESS_GPU"));
+    ompi_group_t local = {0};
+    ompi_communicator_t comm;
+    ompi_datatype_t dbyte = {0, 1, 1, 1}, dint = {6, 4, 1, 1}, gap4 = {6, 4, 0, 0};
+    mca_pml_base_module_t ob1;
+    int prio = 7;
+    if (argc < 4) return 2;
+    g_rank = atoi(argv[2]);
+    g_size = atoi(argv[3]);
+    harness_proc_name.jobid = (unsigned) strtoul(argv[1], NULL, 16);
+    comm = (ompi_communicator_t){g_rank, g_size, 5, 0, &local, NULL};
+
+    /* the base selected "ob1" */
+    memset(&ob1, 0, sizeof(ob1));
+    ob1.pml_add_comm = o_add_comm;
+    ob1.pml_del_comm = o_del_comm;
+    ob1.pml_isend = o_isend;
+    ob1.pml_send = o_send;
+    ob1.pml_irecv = o_irecv;
+    ob1.pml_recv = o_recv;
+    ob1.pml_isend_init = o_isend_init;
+    ob1.pml_irecv_init = o_irecv_init;
+    ob1.pml_start = o_start;
+    ob1.pml_iprobe = o_iprobe;
+    ob1.pml_probe = o_probe;
+    ob1.pml_improbe = o_improbe;
+    ob1.pml_mprobe = o_mprobe;
+    ob1.pml_max_tag = 0x7fffffff;
+    mca_pml = ob1;
+
+    /* selection: pml/rocm's init declines; its close interposes */
+    CHECK(mca_pml_rocm_component.super.pmlm_version.mca_open_component() == OMPI_SUCCESS, "open");
+    CHECK(mca_pml_rocm_component.super.pmlm_init(&prio, false, false) == NULL && prio < 0,
+          "pml/rocm must never be selected");
+    CHECK(mca_pml_rocm_component.super.pmlm_version.mca_close_component() == OMPI_SUCCESS, "close");
+    CHECK(mca_pml_rocm_installed && mca_pml.pml_isend != o_isend && mca_pml_rocm_host.pml_isend == o_isend &&
+              mca_pml.pml_max_tag == ob1.pml_max_tag,
+          "close saves ob1 and installs pml/rocm");
+    CHECK(mca_pml.pml_add_comm(&comm) == OMPI_SUCCESS, "add_comm");
+    if (!use_gpu) {
+        int m = -1;
+        ompi_request_t *r = NULL;
+        CHECK(mca_pml_rocm_comm_of(&comm) == NULL, "no library communicator without a device");
+        CHECK(mca_pml.pml_isend("x", 1, &dbyte, (g_rank + 1) % g_size, 3, MCA_PML_BASE_SEND_STANDARD,
+                                &comm, &r) == OMPI_SUCCESS && r == &ob1_req && ob1_calls == 1,
+              "isend reaches ob1");
+        CHECK(mca_pml.pml_iprobe(MPI_ANY_SOURCE, MPI_ANY_TAG, &comm, &m, NULL) == OMPI_SUCCESS &&
+                  ob1_calls == 2, "iprobe reaches ob1");
+        CHECK(mca_pml.pml_del_comm(&comm) == OMPI_SUCCESS, "del_comm");
+        printf("ok\n");
+        return 0;
+    }
+    CHECK(mca_pml_rocm_comm_of(&comm) != NULL, "library communicator created");
+    const int right = (g_rank + 1) % g_size, left = (g_rank + g_size - 1) % g_size;
+
+    /* 1. ring isend / irecv on device buffers */
+    {
+        const size_t sizes[5] = {0, 777, 4096, 300001, 8u << 20};
+        for (int k = 0; k < 5; ++k) {
+            const size_t n = sizes[k];
+            unsigned char *h = malloc(n + 1), *exp = malloc(n + 1), *got = malloc(n + 1);
+            void *ds, *dr;
+            ompi_request_t *rs = NULL, *rr = NULL;
+            for (size_t i = 0; i < n; ++i) {
+                h[i] = pat(g_rank, i, k);
+                exp[i] = pat(left, i, k);
+            }
+            memset(got, 0, n + 1);
+            CHECK(harness_dev_alloc_copy(&ds, h, n + 1) == 0 && harness_dev_alloc_copy(&dr, got, n + 1) == 0,
+                  "device buffers");
+            ob1_calls = 0;
+            CHECK(mca_pml.pml_irecv(dr, n, &dbyte, left, 10 + k, &comm, &rr) == OMPI_SUCCESS, "irecv");
+            CHECK(mca_pml.pml_isend(ds, n, &dbyte, right, 10 + k, MCA_PML_BASE_SEND_STANDARD, &comm,
+                                    &rs) == OMPI_SUCCESS, "isend");
+            CHECK(ob1_calls == 0 && rr != &ob1_req && rs != &ob1_req, "user tags go to the library");
+            wait_req(rr);
+            wait_req(rs);
+            CHECK(rr->req_status.MPI_ERROR == OMPI_SUCCESS && rr->req_status.MPI_SOURCE == left &&
+                      rr->req_status.MPI_TAG == 10 + k && rr->req_status._ucount == n,
+                  "recv status (err %d src %d tag %d count %zu)", rr->req_status.MPI_ERROR,
+                  rr->req_status.MPI_SOURCE, rr->req_status.MPI_TAG, rr->req_status._ucount);
+            CHECK(harness_dev_copy_back(got, dr, n + 1) == 0 && memcmp(got, exp, n) == 0,
+                  "ring payload of %zu bytes", n);
+            CHECK(rr->req_free(&rr) == OMPI_SUCCESS && rs->req_free(&rs) == OMPI_SUCCESS, "free");
+            harness_dev_free(ds);
+            harness_dev_free(dr);
+            free(h);
+            free(exp);
+            free(got);
+        }
+    }
+    /* 2. blocking send / recv from host memory (staged through the device),
+     * ANY_SOURCE / ANY_TAG on the receive */
+    {
+        const size_t n = 100003;
+        int *h = malloc(n * 4), *got = calloc(n, 4);
+        ompi_status_public_t st;
+        for (size_t i = 0; i < n; ++i) h[i] = g_rank * 1000003 + (int) i;
+        if (g_rank % 2 == 0) {
+            CHECK(mca_pml.pml_send(h, n, &dint, right, 7, MCA_PML_BASE_SEND_STANDARD, &comm) ==
+                      OMPI_SUCCESS, "send");
+            CHECK(mca_pml.pml_recv(got, n, &dint, MPI_ANY_SOURCE, MPI_ANY_TAG, &comm, &st) == OMPI_SUCCESS,
+                  "recv");
+        } else {
+            CHECK(mca_pml.pml_recv(got, n, &dint, MPI_ANY_SOURCE, MPI_ANY_TAG, &comm, &st) == OMPI_SUCCESS,
+                  "recv");
+            CHECK(mca_pml.pml_send(h, n, &dint, right, 7, MCA_PML_BASE_SEND_STANDARD, &comm) ==
+                      OMPI_SUCCESS, "send");
+        }
+        CHECK(st.MPI_SOURCE == left && st.MPI_TAG == 7 && st._ucount == n * 4, "wildcard status");
+        for (size_t i = 0; i < n; ++i) CHECK(got[i] == left * 1000003 + (int) i, "host payload %zu", i);
+        free(h);
+        free(got);
+    }
+    /* 3. non-contiguous receive type: 4-byte elements with 4-byte gaps */
+    {
+        const size_t n = 5000;
+        int *h = malloc(n * 4), *t = malloc(n * 8);
+        void *ds;
+        ompi_request_t *rs = NULL, *rr = NULL;
+        for (size_t i = 0; i < n; ++i) h[i] = g_rank * 7919 + (int) i;
+        for (size_t i = 0; i < 2 * n; ++i) t[i] = -1;
+        CHECK(harness_dev_alloc_copy(&ds, h, n * 4) == 0, "device send buffer");
+        CHECK(mca_pml.pml_irecv(t, n, &gap4, left, 9, &comm, &rr) == OMPI_SUCCESS, "irecv gap type");
+        CHECK(mca_pml.pml_isend(ds, n, &dint, right, 9, MCA_PML_BASE_SEND_STANDARD, &comm, &rs) ==
+                  OMPI_SUCCESS, "isend");
+        wait_req(rr);
+        wait_req(rs);
+        for (size_t i = 0; i < n; ++i) {
+            CHECK(t[2 * i] == left * 7919 + (int) i, "packed element %zu", i);
+            CHECK(t[2 * i + 1] == -1, "gap %zu overwritten", i);
+        }
+        CHECK(rr->req_free(&rr) == OMPI_SUCCESS && rs->req_free(&rs) == OMPI_SUCCESS, "free");
+        harness_dev_free(ds);
+        free(h);
+        free(t);
+    }
+    /* 4. iprobe / probe, then the receive */
+    {
+        unsigned char v = (unsigned char) g_rank, w = 0;
+        void *dv, *dw;
+        ompi_request_t *rs = NULL;
+        ompi_status_public_t st;
+        int m = 0;
+        CHECK(harness_dev_alloc_copy(&dv, &v, 1) == 0 && harness_dev_alloc_copy(&dw, &w, 1) == 0, "dev");
+        CHECK(mca_pml.pml_isend(dv, 1, &dbyte, right, 21, MCA_PML_BASE_SEND_STANDARD, &comm, &rs) ==
+                  OMPI_SUCCESS, "isend");
+        CHECK(mca_pml.pml_probe(left, MPI_ANY_TAG, &comm, &st) == OMPI_SUCCESS && st.MPI_TAG == 21 &&
+                  st.MPI_SOURCE == left && st._ucount == 1, "probe");
+        CHECK(mca_pml.pml_iprobe(MPI_ANY_SOURCE, 21, &comm, &m, &st) == OMPI_SUCCESS && m == 1, "iprobe");
+        CHECK(mca_pml.pml_recv(dw, 1, &dbyte, left, 21, &comm, &st) == OMPI_SUCCESS, "recv");
+        CHECK(harness_dev_copy_back(&w, dw, 1) == 0 && w == (unsigned char) left, "probed payload");
+        wait_req(rs);
+        CHECK(rs->req_free(&rs) == OMPI_SUCCESS, "free");
+        harness_dev_free(dv);
+        harness_dev_free(dw);
+    }
+    /* 5. persistent send / recv, three starts with fresh data */
+    {
+        const size_t n = 65537;
+        unsigned char *h = malloc(n), *got = malloc(n);
+        void *ds, *dr;
+        ompi_request_t *rs = NULL, *rr = NULL;
+        memset(h, 0, n);
+        CHECK(harness_dev_alloc_copy(&ds, h, n) == 0 && harness_dev_alloc_copy(&dr, h, n) == 0, "dev");
+        CHECK(mca_pml.pml_isend_init(ds, n, &dbyte, right, 33, MCA_PML_BASE_SEND_STANDARD, &comm, &rs) ==
+                  OMPI_SUCCESS && mca_pml.pml_irecv_init(dr, n, &dbyte, left, 33, &comm, &rr) ==
+                  OMPI_SUCCESS, "persistent init");
+        CHECK(rs->req_persistent && rr->req_persistent, "persistent requests");
+        for (int it = 0; it < 3; ++it) {
+            /* fresh data in the same buffer; the peer must see this start's */
+            for (size_t i = 0; i < n; ++i) h[i] = pat(g_rank, i, 50 + it);
+            CHECK(harness_dev_copy_in(ds, h, n) == 0, "fresh send data");
+            CHECK(mca_pml.pml_start(1, &rr) == OMPI_SUCCESS, "start recv");
+            CHECK(mca_pml.pml_start(1, &rs) == OMPI_SUCCESS, "start send");
+            wait_req(rr);
+            wait_req(rs);
+            CHECK(rr->req_status.MPI_ERROR == OMPI_SUCCESS && rr->req_status._ucount == n, "status");
+            CHECK(harness_dev_copy_back(got, dr, n) == 0, "copy back");
+            for (size_t i = 0; i < n; ++i) CHECK(got[i] == pat(left, i, 50 + it), "start %d byte %zu", it, i);
+        }
+        CHECK(rr->req_free(&rr) == OMPI_SUCCESS && rs->req_free(&rs) == OMPI_SUCCESS, "free");
+        harness_dev_free(ds);
+        harness_dev_free(dr);
+        free(h);
+        free(got);
+    }
+    /* 6. truncation: 1000 bytes into a 999-byte receive */
+    {
+        unsigned char h[1000] = {0};
+        void *ds, *dr;
+        ompi_request_t *rs = NULL, *rr = NULL;
+        CHECK(harness_dev_alloc_copy(&ds, h, 1000) == 0 && harness_dev_alloc_copy(&dr, h, 1000) == 0, "dev");
+        CHECK(mca_pml.pml_irecv(dr, 999, &dbyte, left, 44, &comm, &rr) == OMPI_SUCCESS, "irecv");
+        CHECK(mca_pml.pml_isend(ds, 1000, &dbyte, right, 44, MCA_PML_BASE_SEND_STANDARD, &comm, &rs) ==
+                  OMPI_SUCCESS, "isend");
+        wait_req(rr);
+        wait_req(rs);
+        CHECK(rr->req_status.MPI_ERROR == MPI_ERR_TRUNCATE, "truncation reported (%d)",
+              rr->req_status.MPI_ERROR);
+        (void) rr->req_free(&rr);
+        (void) rs->req_free(&rs);
+        harness_dev_free(ds);
+        harness_dev_free(dr);
+    }
+    /* 7. system tags, PROC_NULL and matched probes */
+    {
+        ompi_request_t *r = NULL;
+        int m = 0;
+        struct ompi_message_t *msg = NULL;
+        ob1_calls = 0;
+        CHECK(mca_pml.pml_isend("x", 1, &dbyte, right, -17, MCA_PML_BASE_SEND_STANDARD, &comm, &r) ==
+                  OMPI_SUCCESS && r == &ob1_req && ob1_calls == 1, "system tag reaches ob1");
+        CHECK(mca_pml.pml_recv(NULL, 0, &dbyte, MPI_PROC_NULL, 3, &comm, NULL) == OMPI_SUCCESS &&
+                  ob1_calls == 2, "PROC_NULL reaches ob1");
+        CHECK(mca_pml.pml_improbe(left, 3, &comm, &m, &msg, NULL) == OMPI_ERR_NOT_SUPPORTED,
+              "matched probe of library traffic refused");
+        CHECK(mca_pml.pml_improbe(left, -20, &comm, &m, &msg, NULL) == OMPI_SUCCESS && ob1_calls == 3,
+              "matched probe of a system tag reaches ob1");
+    }
+    CHECK(mca_pml.pml_del_comm(&comm) == OMPI_SUCCESS && mca_pml_rocm_comm_of(&comm) == NULL, "del_comm");
+    printf("ok gpu\n");
+    return 0;
+}

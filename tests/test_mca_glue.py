@@ -85,6 +85,40 @@ def test_coll_component_device_path(coll_harness, n):
         assert rc == 0 and out == "ok gpu", (rc, out, err)
 
 
+# ---- pml/rocm (ompi_amd/mca/pml/rocm) through tests/mca_harness/pml_harness.c ----
+
+@pytest.fixture(scope="module")
+def pml_harness(tmp_path_factory):
+    from ompi_amd import _lib
+    _lib.load()
+    out = str(tmp_path_factory.mktemp("mca") / "pml_harness")
+    subprocess.run(["bash", os.path.join(ROOT, "tests", "mca_harness", "build_pml.sh"), out],
+                   check=True)
+    return out
+
+
+def test_pml_component_interposition(pml_harness):
+    """pml/rocm is never selected; its close saves the selected PML and
+    installs itself in mca_pml (pml_v_component.c:123-160's pattern); with
+    no device no communicator gets library state and every call reaches
+    the saved PML."""
+    for rc, out, err in _run_coll_harness(pml_harness, 2, False, 60):
+        assert rc == 0 and out == "ok", (rc, out, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 3])
+def test_pml_component_device_path(pml_harness, n):
+    """Through mca_pml: a ring of isend/irecv on device buffers (0 B to
+    8 MiB), host-buffer send/recv staged, a non-contiguous receive type
+    packed with its gaps kept, ANY_SOURCE/ANY_TAG status, probe/iprobe,
+    persistent requests started three times with fresh data, truncation;
+    system tags, PROC_NULL and matched probes of system tags reach the saved
+    PML; add_comm / del_comm create and destroy the library communicator."""
+    for rc, out, err in _run_coll_harness(pml_harness, n, True, 240):
+        assert rc == 0 and out == "ok gpu", (rc, out, err)
+
+
 # ---- osc/rocm (ompi_amd/mca/osc/rocm) through tests/mca_harness/osc_harness.c ----
 
 @pytest.fixture(scope="module")

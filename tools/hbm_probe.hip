@@ -10,6 +10,13 @@
 //          (threads x unroll, one chunk per workgroup, nt loads + stores)
 //   opseq  same, but each workgroup walks SEQ consecutive chunks (longer
 //          runs per DRAM page)
+//   pstore (argv[2] == 2) the masked partial-line store ceiling the convertor
+//          unpack meets: a contiguous packed stream read W bytes per lane and
+//          written to a typed layout of period P (W < P: the gap bytes are
+//          never written, so every 64-B store request is byte-masked);
+//          W/P = 8/16 (vector bl1 of doubles), 16/32 (bl2), 4+8/16
+//          (struct {int, double}); "pstore_full" writes the same payload
+//          densely (P = W) for comparison.  Rate = 2 x payload bytes / time.
 // Output: one JSON line per variant.
 // Build: hipcc --offload-arch=gfx950 -O3 -o hbm_probe hbm_probe.hip
 #include <hip/hip_runtime.h>
@@ -116,6 +123,52 @@ __global__ __launch_bounds__(T) void k_oppol(const float *a, const float *b, flo
     }
 }
 
+// lane j: W packed bytes at src + j*W -> dst + j*P (+ a second field for
+// the struct pattern: 4 bytes at 0 and 8 bytes at 8 of a 16-B period)
+template <int W, int P, bool STRUCT>
+__global__ __launch_bounds__(256) void k_pstore(const unsigned char *src, unsigned char *dst,
+                                                size_t nelem) {
+    const size_t j = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= nelem) return;
+    if (STRUCT) {
+        const unsigned *s4 = (const unsigned *)(src + j * 12);
+        const unsigned a = __builtin_nontemporal_load(s4);
+        const unsigned b = __builtin_nontemporal_load(s4 + 1);
+        const unsigned c = __builtin_nontemporal_load(s4 + 2);
+        unsigned *d = (unsigned *)(dst + j * 16);
+        __builtin_nontemporal_store(a, d);
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        __builtin_nontemporal_store(u32x2{b, c}, (u32x2 *)(d + 2));
+    } else if (W == 16) {
+        const u32x4 v = __builtin_nontemporal_load((const u32x4 *)(src + j * 16));
+        __builtin_nontemporal_store(v, (u32x4 *)(dst + j * P));
+    } else if (W == 8) {
+        const unsigned long long v = __builtin_nontemporal_load((const unsigned long long *)(src + j * 8));
+        __builtin_nontemporal_store(v, (unsigned long long *)(dst + j * P));
+    } else {
+        const unsigned v = __builtin_nontemporal_load((const unsigned *)(src + j * 4));
+        __builtin_nontemporal_store(v, (unsigned *)(dst + j * P));
+    }
+}
+
+template <typename L>
+static double time_ms(L &&launch, int reps);
+
+template <int W, int P, bool STRUCT>
+static void run_pstore(void *src, void *dst, size_t dst_bytes, const char *name, int reps) {
+    const size_t nelem = dst_bytes / P;
+    const size_t payload = nelem * (STRUCT ? 12 : W);
+    const unsigned grid = (unsigned)((nelem + 255) / 256);
+    const double ms = time_ms([&] {
+        hipLaunchKernelGGL((k_pstore<W, P, STRUCT>), dim3(grid), dim3(256), 0, 0,
+                           (const unsigned char *)src, (unsigned char *)dst, nelem);
+    }, reps);
+    const double gbs = 2.0 * payload / (ms * 1e-3) / 1e9;
+    printf("{\"variant\": \"%s\", \"W\": %d, \"P\": %d, \"payload_bytes\": %zu, \"ms\": %.4f, "
+           "\"GBps\": %.1f, \"frac\": %.4f}\n", name, STRUCT ? 12 : W, P, payload, ms, gbs, gbs / 8000.0);
+    fflush(stdout);
+}
+
 struct Bufs;
 
 struct Bufs {
@@ -202,6 +255,17 @@ int main(int argc, char **argv) {
     CK(hipMemset(B.b, 0x22, bytes));
     CK(hipMemset(B.c, 0, bytes));
     CK(hipDeviceSynchronize());
+    if (argc > 2 && atoi(argv[2]) == 2) {  // masked partial-line store ceiling only
+        // typed destination of `bytes`; the packed source is B.a
+        run_pstore<8, 16, false>(B.a, B.c, bytes, "pstore", reps);
+        run_pstore<8, 8, false>(B.a, B.c, bytes / 2, "pstore_full", reps);
+        run_pstore<16, 32, false>(B.a, B.c, bytes, "pstore", reps);
+        run_pstore<16, 16, false>(B.a, B.c, bytes / 2, "pstore_full", reps);
+        run_pstore<12, 16, true>(B.a, B.c, bytes, "pstore_struct", reps);
+        run_pstore<4, 8, false>(B.a, B.c, bytes, "pstore", reps);
+        run_pstore<4, 4, false>(B.a, B.c, bytes / 2, "pstore_full", reps);
+        return 0;
+    }
     if (argc > 2 && atoi(argv[2]) == 1) {  // cache-policy sweep only
         run_op<256, 4, 1>(B, reps);
         run_pol<256, 4, 2, 2>(B, reps);

@@ -23,7 +23,8 @@ struct msg {
     unsigned char expect;
 };
 
-static const size_t kSize = 8u << 20;
+static size_t kSize = 8u << 20;   // A's size
+static size_t kSizeB = 8u << 20;  // B's size (argv[2] MiB*1000: a smaller B inside A's old range)
 
 static void wr(int fd, const void *p, size_t n) {
     if (write(fd, p, n) != (ssize_t)n) _exit(3);
@@ -53,7 +54,7 @@ static void peer(int in, int out) {
             if (hipIpcOpenMemHandle(&p, m.h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
                 ans = 0xEE;
             } else {
-                (void)hipMemcpy(&ans, (char *)p + kSize / 2, 1, hipMemcpyDeviceToHost);
+                (void)hipMemcpy(&ans, (char *)p + 4096, 1, hipMemcpyDeviceToHost);
                 if (m.cmd == 4) held = p;
                 else (void)hipIpcCloseMemHandle(p);
             }
@@ -65,6 +66,8 @@ static void peer(int in, int out) {
 
 int main(int argc, char **argv) {
     const int rounds = argc > 1 ? atoi(argv[1]) : 20;
+    if (argc > 2) kSizeB = (size_t)atol(argv[2]);
+    if (argc > 3) kSize = (size_t)atol(argv[3]);
     int to[2][2], from[2][2];
     pid_t kids[2];
     for (int k = 0; k < 2; ++k) {
@@ -98,11 +101,11 @@ int main(int argc, char **argv) {
             ask(H, ha, held == 1 ? 4 : 1);
             if (ask(I, ha, held == 2 ? 4 : 1) != 0xAA) ++errs;
             (void)hipFree(a);
-            (void)hipMalloc(&b, kSize);
-            (void)hipMemset(b, 0xBB, kSize);
+            (void)hipMalloc(&b, kSizeB);
+            (void)hipMemset(b, 0xBB, kSizeB);
             (void)hipDeviceSynchronize();
             (void)hipIpcGetMemHandle(&hb, b);
-            same_addr += a == b;
+            same_addr += (char *)b >= (char *)a && (char *)b < (char *)a + kSize;
             const unsigned char seen = ask(I, hb, 1);
             if (seen == 0xAA) ++stale;
             else if (seen != 0xBB) ++errs;
@@ -110,8 +113,8 @@ int main(int argc, char **argv) {
             if (held == 2) ask(I, ha, 2);
             (void)hipFree(b);
         }
-        printf("scenario %-6s rounds %d: B at A's address %d, importer saw A's bytes through hB %d, "
-               "other errors %d\n", names[held], rounds, same_addr, stale, errs);
+        printf("A %zu B %zu scenario %-6s rounds %d: B inside A's old range %d, importer saw A's bytes through hB %d, "
+               "other errors %d\n", kSize, kSizeB, names[held], rounds, same_addr, stale, errs);
         fflush(stdout);
     }
     for (int k = 0; k < 2; ++k) {
