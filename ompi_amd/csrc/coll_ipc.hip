@@ -429,6 +429,8 @@ static std::vector<export_rec> g_exp;
 
 // 0: *h exported (fresh if *fresh), 1: recycled handle bytes, <0: the
 // runtime refused (*e).
+static int quiesce(ompi_amd_comm_t *c);
+
 // OMPI_AMD_IPC_TRACE=1: one stderr line per new export and per new import
 // (handle words 0-15), for diagnosing mapping mix-ups after the fact.
 static bool ipc_trace() {
@@ -551,14 +553,20 @@ static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d, bool *ip
 // is how a stale alias could be handed back, and serving it from the cache
 // would certainly be one.  A pinned mapping (a persistent plan's) of a freed
 // buffer is a program error: report it instead of unmapping under the plan.
+// which: 0 = only mappings under the same handle bytes (they must go before
+// the new handle is opened: the runtime could answer with them), 1 = only
+// the other overlapping ones — closed after the new mapping is open, so
+// that the new one does not take over their just-unmapped addresses (a
+// page-translation reuse hazard this ordering removes), 2 = both.
 static int drop_stale_imports(ompi_amd_comm_t *c, int peer, const buf_desc &d,
-                              bool *closed_same = nullptr) {
+                              bool *closed_same = nullptr, int which = 2) {
     if (closed_same) *closed_same = false;
     const uint64_t lo = d.base, hi = d.base + d.size;
     for (auto it = c->imports.begin(); it != c->imports.end();) {
         const bool same_h = same_handle(it->h, d.h);
         const bool overlap = it->rbase < hi && lo < it->rbase + it->rsize;
-        if (it->peer != peer || it->id == d.id || !(same_h || overlap)) {
+        const bool pick = which == 2 ? (same_h || overlap) : which == 0 ? same_h : (overlap && !same_h);
+        if (it->peer != peer || it->id == d.id || !pick) {
             ++it;
             continue;
         }
@@ -625,12 +633,13 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
         }
     }
     bool closed_same = false;
-    TRY(drop_stale_imports(c, peer, d, &closed_same));
+    TRY(drop_stale_imports(c, peer, d, &closed_same, 0));
     if (c->imports.size() >= 256) {  // evict the least recently used unpinned mapping
         auto it = c->imports.end();
         for (auto jt = c->imports.begin(); jt != c->imports.end(); ++jt)
             if (jt->pins == 0 && (it == c->imports.end() || jt->last_use < it->last_use)) it = jt;
         if (it != c->imports.end()) {
+            TRY(quiesce(c));  // an earlier call's kernel may still read it
             (void)hipIpcCloseMemHandle(it->base);
             c->imports.erase(it);
         }
@@ -658,10 +667,13 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
         ++c->aliased_opens;
         return OMPI_AMD_ERR_HIP;
     }
+    // now the peer's freed allocations that overlap this one (their
+    // mappings stayed open across the open above, see drop_stale_imports)
+    const int drc = drop_stale_imports(c, peer, d, nullptr, 1);
     c->imports.push_back({peer, d.h, d.id, d.base, d.size, base, ++c->use_clock, pin ? 1 : 0});
     *out = (const char *)base + d.off;
     if (base_out) *base_out = base;
-    return OMPI_AMD_SUCCESS;
+    return drc;
 }
 
 static void unpin_import(ompi_amd_comm_t *c, void *base) {
@@ -757,6 +769,7 @@ static int import_all(ompi_amd_comm_t *c, const call_blob *all, const void *sbuf
             return local != OMPI_AMD_SUCCESS ? local : OMPI_AMD_ERR_HIP;
         }
         ++c->ipc_reopens;
+        TRY(quiesce(c));  // no earlier kernel of this communicator still reads a mapping closed below
         for (int p = 0; p < c->size; ++p) {
             if (p == c->rank || done[p]) continue;
             for (auto it = c->imports.begin(); it != c->imports.end();) {
@@ -889,11 +902,18 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
                                  c->land_bytes ? 2 * (c->land_bytes + kTag) : 0);
     TRY(quiesce(c));
     TRY(c->boot.barrier());  // every rank's earlier kernels are done
+    // the old mappings stay open until the new ones are (so the new ones
+    // get fresh addresses in this process), then close
+    void *old_land[kMaxRanks];
     for (int p = 0; p < kMaxRanks; ++p) {
-        if (c->land_opened[p]) (void)hipIpcCloseMemHandle(c->land_opened[p]);
+        old_land[p] = c->land_opened[p];
         c->land_opened[p] = nullptr;
         c->peer_land.p[p] = nullptr;
     }
+    auto close_old = [&] {
+        for (int p = 0; p < kMaxRanks; ++p)
+            if (old_land[p]) (void)hipIpcCloseMemHandle(old_land[p]);
+    };
     struct land_blob { buf_desc d; uint64_t token; int ok; };
     land_blob mine{}, all[kMaxRanks];
     char *fresh = nullptr;
@@ -920,11 +940,12 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
     if (e != hipSuccess && mine.d.valid) record_hip(e, "landing token write");
     mine.ok = e == hipSuccess;
-    int rc = c->boot.allgather(&mine, all, sizeof(mine));  // also: nobody maps the old one now
-    if (c->land) (void)hipFree(c->land);
+    int rc = c->boot.allgather(&mine, all, sizeof(mine));  // also: nobody uses the old one now
+    if (c->land) (void)hipFree(c->land);  // peers' mappings keep it alive until they close them
     c->land = nullptr;
     c->land_bytes = 0;
     if (rc != OMPI_AMD_SUCCESS) {
+        close_old();
         if (fresh) (void)hipFree(fresh);
         return rc;
     }
@@ -936,10 +957,15 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
             status = 1;
             break;
         }
-        rc = drop_stale_imports(c, p, all[p].d);
+        rc = drop_stale_imports(c, p, all[p].d, nullptr, 0);
         if (rc != OMPI_AMD_SUCCESS) { status = 1; break; }
         void *m = nullptr;
         e = hipIpcOpenMemHandle(&m, all[p].d.h, hipIpcMemLazyEnablePeerAccess);
+        if (e == hipSuccess && drop_stale_imports(c, p, all[p].d, nullptr, 1) != OMPI_AMD_SUCCESS) {
+            (void)hipIpcCloseMemHandle(m);
+            status = 1;
+            break;
+        }
         if (e != hipSuccess) {
             record_hip(e, "hipIpcOpenMemHandle (landing)");
             status = 1;
@@ -988,6 +1014,7 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
             status = 2;
         }
     }
+    close_old();
     for (int q = 0; q < c->size; ++q) c->land_tokens.push_back(all[q].token);
     int st[kMaxRanks];
     rc = c->boot.allgather(&status, st, sizeof(int));

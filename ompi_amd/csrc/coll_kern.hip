@@ -21,8 +21,12 @@ hipError_t red_launch_slot(dim3 grid, const ptr_set &src, const ptr_set &dst, in
                            int order, int flags, const red_jobs &jobs, hipStream_t s) {
     if constexpr (slot_supported(OP, TYPE)) {
         using T = typename type_of<TYPE>::type;
-        hipLaunchKernelGGL((reduce_kernel<T, OP>), grid, dim3(kXferThreads), 0, s, src, dst, ndst,
-                           n, order, flags, jobs);
+        if (n <= 8)
+            hipLaunchKernelGGL((reduce_kernel<T, OP, 8>), grid, dim3(kXferThreads), 0, s, src, dst,
+                               ndst, n, order, flags, jobs);
+        else
+            hipLaunchKernelGGL((reduce_kernel<T, OP, kMaxRanks>), grid, dim3(kXferThreads), 0, s,
+                               src, dst, ndst, n, order, flags, jobs);
         return hipGetLastError();
     } else {
         return hipErrorInvalidValue;

@@ -78,15 +78,15 @@ __device__ __forceinline__ void xfer_epilogue() {
 // Fold v[0..n) (virtual-rank order) with the 2-buffer rule f(out, in).  All
 // array indices are compile-time constants after unrolling; n, order and
 // flags are wave-uniform.
-template <typename T, int OP>
-__device__ __forceinline__ T fold(const T (&v)[kMaxRanks], int n, int order, int flags) {
+template <typename T, int OP, int NM = kMaxRanks>
+__device__ __forceinline__ T fold(const T (&v)[NM], int n, int order, int flags) {
     using F = opfn<OP, false>;
     const bool swap = (flags & FOLD_ROOT_INPLACE) != 0;
     if (order == ORDER_RING) {
         // v[j] = x[(b + j) % n]; acc = x[b]; acc = f(x[b+j], acc)
         T acc = v[0];
 #pragma unroll
-        for (int j = 1; j < kMaxRanks; ++j)
+        for (int j = 1; j < NM; ++j)
             if (j < n) acc = F::template f<T>(v[j], acc);
         return acc;
     }
@@ -95,9 +95,9 @@ __device__ __forceinline__ T fold(const T (&v)[kMaxRanks], int n, int order, int
         // (coll_base_reduce.c:206-215): node k's only child is k+1,
         // acc_k = f(acc_(k+1), x_k); basic_linear (:680-721) is the same
         // expression at first = 0.
-        T acc = v[kMaxRanks - 1];
+        T acc = v[NM - 1];
 #pragma unroll
-        for (int j = kMaxRanks - 1; j >= 0; --j) {
+        for (int j = NM - 1; j >= 0; --j) {
             if (j == n - 1) acc = v[j];
             else if (j < n - 1) acc = (j == 0 && swap) ? F::template f<T>(v[0], acc)
                                                        : F::template f<T>(acc, v[j]);
@@ -108,17 +108,17 @@ __device__ __forceinline__ T fold(const T (&v)[kMaxRanks], int n, int order, int
         // in-order binomial (coll_base_topo.c:402-458): vrank u's children
         // are u+1, u+2, u+4, ... while the bit is clear; first child:
         // acc = f(child, own), later ones acc = f(acc, child).
-        T w[kMaxRanks];
+        T w[NM];
 #pragma unroll
-        for (int i = 0; i < kMaxRanks; ++i) w[i] = v[i];
+        for (int i = 0; i < NM; ++i) w[i] = v[i];
 #pragma unroll
-        for (int u = 0; u + 1 < kMaxRanks; u += 2)
+        for (int u = 0; u + 1 < NM; u += 2)
             if (u + 1 < n) w[u] = (u == 0 && swap) ? F::template f<T>(w[0], w[1])
                                                    : F::template f<T>(w[u + 1], w[u]);
 #pragma unroll
-        for (int m = 2; m < kMaxRanks; m <<= 1) {
+        for (int m = 2; m < NM; m <<= 1) {
 #pragma unroll
-            for (int u = 0; u + m < kMaxRanks; u += 2 * m)
+            for (int u = 0; u + m < NM; u += 2 * m)
                 if (u + m < n) w[u] = F::template f<T>(w[u], w[u + m]);
         }
         return w[0];
@@ -127,18 +127,18 @@ __device__ __forceinline__ T fold(const T (&v)[kMaxRanks], int n, int order, int
         // build_tree(2) (coll_base_topo.c:77-175): shifted rank s has
         // children s + d and s + 2d, d = largest power of two <= s + 1;
         // children have larger s, so descending s sees them finished.
-        T w[kMaxRanks];
+        T w[NM];
 #pragma unroll
-        for (int i = 0; i < kMaxRanks; ++i) w[i] = v[i];
+        for (int i = 0; i < NM; ++i) w[i] = v[i];
 #pragma unroll
-        for (int s = kMaxRanks - 1; s >= 0; --s) {
+        for (int s = NM - 1; s >= 0; --s) {
             int d = 1;
             while (2 * d <= s + 1) d *= 2;
             const int c0 = s + d, c1 = s + 2 * d;
-            if (c0 < kMaxRanks && c0 < n)
+            if (c0 < NM && c0 < n)
                 w[s] = (s == 0 && swap) ? F::template f<T>(w[0], w[c0])
                                         : F::template f<T>(w[c0], w[s]);
-            if (c1 < kMaxRanks && c1 < n) w[s] = F::template f<T>(w[s], w[c1]);
+            if (c1 < NM && c1 < n) w[s] = F::template f<T>(w[s], w[c1]);
         }
         return w[0];
     }
@@ -156,26 +156,26 @@ __device__ __forceinline__ T fold(const T (&v)[kMaxRanks], int n, int order, int
         const int rem = n - adj;
         const int o = (flags >> 8) & 0xff;
         const bool right = (o & 1) != 0;
-        T w[kMaxRanks];
+        T w[NM];
 #pragma unroll
-        for (int u = 0; u < kMaxRanks; ++u) {
-            if (2 * u + 1 < kMaxRanks && u < rem)
+        for (int u = 0; u < NM; ++u) {
+            if (2 * u + 1 < NM && u < rem)
                 w[u] = right ? F::template f<T>(v[2 * u + 1], v[2 * u])
                              : F::template f<T>(v[2 * u], v[2 * u + 1]);
             else if (u < adj)
-                w[u] = v[u + rem < kMaxRanks ? u + rem : 0];
+                w[u] = v[u + rem < NM ? u + rem : 0];
         }
 #pragma unroll
-        for (int m = 1; m < kMaxRanks; m <<= 1) {
+        for (int m = 1; m < NM; m <<= 1) {
             if (m < adj) {
 #pragma unroll
-                for (int u = 0; u < kMaxRanks; ++u)
+                for (int u = 0; u < NM; ++u)
                     if (u < adj && (u & m) == (o & m)) w[u] = F::template f<T>(w[u], w[u ^ m]);
             }
         }
         T r = w[0];
 #pragma unroll
-        for (int u = 1; u < kMaxRanks; ++u)
+        for (int u = 1; u < NM; ++u)
             if (u == o) r = w[u];
         return r;
     }
@@ -190,23 +190,23 @@ __device__ __forceinline__ T fold(const T (&v)[kMaxRanks], int n, int order, int
         while (adj * 2 <= n) adj *= 2;
         const int remain = n - adj;
         const int tb = (flags >> 8) & 0xff;
-        T w[kMaxRanks];
+        T w[NM];
 #pragma unroll
-        for (int u = 0; u < kMaxRanks; ++u) {
-            if (2 * u + 1 < kMaxRanks && u < remain) w[u] = F::template f<T>(v[2 * u + 1], v[2 * u]);
+        for (int u = 0; u < NM; ++u) {
+            if (2 * u + 1 < NM && u < remain) w[u] = F::template f<T>(v[2 * u + 1], v[2 * u]);
             else if (u < adj) w[u] = v[u + remain];
         }
 #pragma unroll
-        for (int m = kMaxRanks / 2; m >= 1; m >>= 1) {
+        for (int m = NM / 2; m >= 1; m >>= 1) {
             if (m < adj) {
 #pragma unroll
-                for (int u = 0; u < kMaxRanks; ++u)
+                for (int u = 0; u < NM; ++u)
                     if (u < adj && (u & m) == (tb & m)) w[u] = F::template f<T>(w[u], w[u ^ m]);
             }
         }
         T r = w[0];
 #pragma unroll
-        for (int u = 1; u < kMaxRanks; ++u)
+        for (int u = 1; u < NM; ++u)
             if (u == tb) r = w[u];
         return r;
     }
@@ -216,17 +216,17 @@ __device__ __forceinline__ T fold(const T (&v)[kMaxRanks], int n, int order, int
     int adj = 1;
     while (adj * 2 <= n) adj *= 2;
     const int extra = n - adj;
-    T w[kMaxRanks];
+    T w[NM];
 #pragma unroll
-    for (int i = 0; i < kMaxRanks; ++i) {
+    for (int i = 0; i < NM; ++i) {
         if (i < extra) w[i] = F::template f<T>(v[2 * i + 1], v[2 * i]);
         else if (i < adj) w[i] = v[i + extra];
     }
 #pragma unroll
-    for (int len = kMaxRanks; len > 1; len >>= 1) {
+    for (int len = NM; len > 1; len >>= 1) {
         if (len <= adj) {
 #pragma unroll
-            for (int i = 0; i < kMaxRanks / 2; ++i)
+            for (int i = 0; i < NM / 2; ++i)
                 if (2 * i + 1 < len) w[i] = F::template f<T>(w[2 * i + 1], w[2 * i]);
         }
     }
@@ -234,11 +234,11 @@ __device__ __forceinline__ T fold(const T (&v)[kMaxRanks], int n, int order, int
 }
 
 // Gather v[j] for element index e of the sources in virtual-rank order.
-template <typename T>
-__device__ __forceinline__ void gather_scalar(T (&v)[kMaxRanks], const ptr_set &src, int n,
+template <typename T, int NM = kMaxRanks>
+__device__ __forceinline__ void gather_scalar(T (&v)[NM], const ptr_set &src, int n,
                                               int first, int64_t e) {
 #pragma unroll
-    for (int j = 0; j < kMaxRanks; ++j) {
+    for (int j = 0; j < NM; ++j) {
         if (j < n) {
             const int r = (first + j) % n;
             v[j] = reinterpret_cast<const T *>(src.p[r])[e];
@@ -246,12 +246,15 @@ __device__ __forceinline__ void gather_scalar(T (&v)[kMaxRanks], const ptr_set &
     }
 }
 
+// NM: the register arrays' size, a compile-time bound >= n (8 for up to 8
+// ranks, else 16: at N <= 8 the kernel holds half the vectors, 109 -> fewer
+// VGPRs and more waves per SIMD).
 // n sources (virtual ranks 0..n), result stored to dst.p[0 .. ndst): ndst =
 // 1 is a plain reduce into one buffer; ndst = size is the fused push of the
 // owner's block into every rank's rbuf (the host orders dst local first,
 // then peers rank+1, rank+2, ... so concurrent owners spread their stores
 // over the links).
-template <typename T, int OP>
+template <typename T, int OP, int NM = kMaxRanks>
 __global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, ptr_set dst, int ndst,
                                                               int n, int order, int flags,
                                                               red_jobs jobs) {
@@ -265,9 +268,9 @@ __global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, ptr_s
     const int64_t head = jb.head < 0 ? jb.cnt : jb.head;
     const int64_t nvec = jb.head < 0 ? 0 : (jb.cnt - head) / E;
     for (int64_t i = tid; i < nvec; i += gstride) {
-        vec16<T> v[kMaxRanks];
+        vec16<T> v[NM];
 #pragma unroll
-        for (int j = 0; j < kMaxRanks; ++j) {
+        for (int j = 0; j < NM; ++j) {
             if (j < n) {
                 const int r = (jb.first + j) % n;
                 const u32x4 *p = reinterpret_cast<const u32x4 *>(
@@ -278,13 +281,13 @@ __global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, ptr_s
         vec16<T> out;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            T s[kMaxRanks];
+            T s[NM];
 #pragma unroll
-            for (int j = 0; j < kMaxRanks; ++j) s[j] = v[j].e[e];
-            out.e[e] = fold<T, OP>(s, n, order, flags | jb.aux);
+            for (int j = 0; j < NM; ++j) s[j] = v[j].e[e];
+            out.e[e] = fold<T, OP, NM>(s, n, order, flags | jb.aux);
         }
 #pragma unroll
-        for (int k = 0; k < kMaxRanks; ++k)
+        for (int k = 0; k < NM; ++k)
             if (k < ndst)
                 reinterpret_cast<u32x4 *>(reinterpret_cast<T *>(const_cast<char *>(dst.p[k])) +
                                           jb.off_dst + head)[i] = out.v;
@@ -294,11 +297,11 @@ __global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, ptr_s
     const int64_t nscalar = head + (jb.cnt - tail0);
     for (int64_t k = tid; k < nscalar; k += gstride) {
         const int64_t e = k < head ? k : tail0 + (k - head);
-        T s[kMaxRanks];
-        gather_scalar<T>(s, src, n, jb.first, jb.off + e);
-        const T r = fold<T, OP>(s, n, order, flags | jb.aux);
+        T s[NM];
+        gather_scalar<T, NM>(s, src, n, jb.first, jb.off + e);
+        const T r = fold<T, OP, NM>(s, n, order, flags | jb.aux);
 #pragma unroll
-        for (int d = 0; d < kMaxRanks; ++d)
+        for (int d = 0; d < NM; ++d)
             if (d < ndst)
                 store_elem<T>(reinterpret_cast<T *>(const_cast<char *>(dst.p[d])) + jb.off_dst + e,
                               r);
