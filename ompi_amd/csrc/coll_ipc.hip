@@ -58,6 +58,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <map>
 #include <mutex>
 #include <new>
 #include <utility>
@@ -79,26 +80,36 @@ namespace ompi_amd {
     } while (0)
 
 // ---------------------------------------------------------------- barrier
+// A rank that fails a call its peers may already have launched (a deferred
+// nonblocking call whose IPC open was refused) raises every peer's abort
+// word, so their waits give up within ~1 ms instead of timing out.
+__global__ void abort_kernel(flag_set peers, int rank, int size) {
+    const int t = threadIdx.x;
+    if (t < size && t != rank)
+        __hip_atomic_store(peers.p[t] + kAbortWord, (uint64_t)1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    sys_release();
+}
+
+// dbg (OMPI_AMD_DEBUG_PROGRESS=1, else null; host-mapped): [0] the last
+// epoch whose barrier started, [1] the last that ended, [2 + p] peer p's
+// flag as last seen by a wait still running (a hang names the missing peer).
 __global__ __launch_bounds__(64) void barrier_kernel(uint64_t *local, flag_set peers, int rank,
                                                      int size, uint64_t epoch, int *err,
-                                                     uint64_t timeout_ticks) {
+                                                     uint64_t timeout_ticks, uint64_t *dbg) {
     const int t = threadIdx.x;
+    if (dbg && t == 0)
+        __hip_atomic_store(dbg, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     sys_release();
     if (t < size && t != rank)
         __hip_atomic_store(peers.p[t] + rank, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (t < size && t != rank) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(local + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > timeout_ticks) {
-                __hip_atomic_store(err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-                break;
-            }
-        }
-    }
+    if (t < size && t != rank)
+        (void)wait_epoch(local + t, epoch, err, timeout_ticks, local + kAbortWord,
+                         dbg ? dbg + 2 + t : nullptr);
     __syncthreads();
     sys_acquire();
+    if (dbg && t == 0)
+        __hip_atomic_store(dbg + 1, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------- copy
@@ -316,6 +327,8 @@ struct ompi_amd_comm {
     int aliased_opens = 0;                // opens the runtime answered with a mapping we already hold
     std::vector<uint64_t> land_tokens;    // every rank's token of every landing growth (diagnostics)
     int ipc_reopens = 0;                  // confirmation rounds that re-opened peers' buffers
+    int ipc_local_reopens = 0;            // opens retried after closing the peer's cached mappings
+    int size_mismatch_opens = 0;          // opens whose mapping had another allocation's range
     int memcpy_token_mismatch = 0;        // landing tokens right by kernel load, wrong by hipMemcpy
     int bcast_split = 0;                  // bcasts that ran as scatter + allgather
     size_t bcast_split_bytes = 4u << 20;  // from this size on (0: never)
@@ -329,9 +342,32 @@ struct ompi_amd_comm {
     std::vector<hipEvent_t> stream_evs;
     char *shadow = nullptr;               // export fallback of blocking calls (shadow_set)
     size_t shadow_bytes = 0;
+    // Shadow arena: every shadow (blocking, nonblocking, persistent) is a
+    // range of a chunk that is exported once and freed only with the
+    // communicator, so peers map each chunk once and no exported address is
+    // ever freed and handed out again (the churn behind the runtime's stale
+    // import answers).
+    struct arena_chunk {
+        char *base;
+        size_t size;
+        std::map<size_t, size_t> free;  // offset -> bytes, coalesced
+        std::map<size_t, size_t> used;  // offset -> bytes
+    };
+    std::mutex arena_mu;
+    std::vector<arena_chunk> arena;
+    size_t arena_bytes = 0;
     int shadowed = 0;                     // zero-copy calls that needed it
     int force_shadow = 0;                 // param "force_shadow": take the fallback always (tests)
+    // param "user_ipc" (env OMPI_AMD_USER_IPC): export the caller's buffers
+    // to peers (zero-copy).  Off by default: every zero-copy-size call stages
+    // through the shadow arena (exported once, never freed), because on ROCm
+    // 7.2 an IPC mapping of an application buffer names (pid, address), not
+    // the allocation — after the application frees and reallocates, cached
+    // or freshly opened mappings were seen to reach other memory (DESIGN.md
+    // §4.6: wrong blocks, illegal-address faults, refused opens).
+    int user_ipc = 0;
     int *err_host = nullptr, *err_dev = nullptr;
+    uint64_t *dbg_host = nullptr, *dbg_dev = nullptr;  // OMPI_AMD_DEBUG_PROGRESS=1 (barrier_kernel)
     uint64_t epoch = 0;
     // params
     size_t small_bytes = 1 << 20;
@@ -548,25 +584,24 @@ static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d, bool *ip
 // Close every cached mapping of `peer` that cannot be the allocation `d`
 // describes but would collide with it: the same handle bytes or an
 // overlapping exporter range under another buffer id.  The peer has freed
-// those allocations (its live allocations never overlap), and a mapping
-// kept open holds the freed memory alive — opening the new handle next to it
-// is how a stale alias could be handed back, and serving it from the cache
-// would certainly be one.  A pinned mapping (a persistent plan's) of a freed
-// buffer is a program error: report it instead of unmapping under the plan.
-// which: 0 = only mappings under the same handle bytes (they must go before
-// the new handle is opened: the runtime could answer with them), 1 = only
-// the other overlapping ones — closed after the new mapping is open, so
-// that the new one does not take over their just-unmapped addresses (a
-// page-translation reuse hazard this ordering removes), 2 = both.
+// those allocations (its live allocations never overlap).  They must be
+// closed BEFORE the new handle is opened: ROCm 7.2's hipIpcOpenMemHandle
+// answers a handle whose exporter address this process already maps with
+// that existing mapping, even when the size differs (measured in round 2:
+// peer 1's buffer id 347 at 0x763d73200000 + 16818488 came back as this
+// process's still-open mapping of its freed buffer id 329 at 0x763d73200000
+// + 16814384 — caught by mapped_already — after an ordering that closed
+// overlapping mappings only after the open).  A pinned mapping (a persistent
+// plan's) of a freed buffer is a program error: report it instead of
+// unmapping under the plan.
 static int drop_stale_imports(ompi_amd_comm_t *c, int peer, const buf_desc &d,
-                              bool *closed_same = nullptr, int which = 2) {
+                              bool *closed_same = nullptr) {
     if (closed_same) *closed_same = false;
     const uint64_t lo = d.base, hi = d.base + d.size;
     for (auto it = c->imports.begin(); it != c->imports.end();) {
         const bool same_h = same_handle(it->h, d.h);
         const bool overlap = it->rbase < hi && lo < it->rbase + it->rsize;
-        const bool pick = which == 2 ? (same_h || overlap) : which == 0 ? same_h : (overlap && !same_h);
-        if (it->peer != peer || it->id == d.id || !pick) {
+        if (it->peer != peer || it->id == d.id || !(same_h || overlap)) {
             ++it;
             continue;
         }
@@ -633,7 +668,7 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
         }
     }
     bool closed_same = false;
-    TRY(drop_stale_imports(c, peer, d, &closed_same, 0));
+    TRY(drop_stale_imports(c, peer, d, &closed_same));
     if (c->imports.size() >= 256) {  // evict the least recently used unpinned mapping
         auto it = c->imports.end();
         for (auto jt = c->imports.begin(); jt != c->imports.end(); ++jt)
@@ -645,35 +680,95 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
         }
     }
     void *base = nullptr;
-    ++c->imports_new;
-    hipError_t e = hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess);
-    if (e != hipSuccess) {
+    // Two attempts.  After heavy allocation churn on a shared GPU the runtime
+    // has refused a live peer buffer ("invalid device pointer") or answered
+    // with a mapping this process already holds; both went away once every
+    // cached mapping of that peer was closed (the blocking calls' confirmation
+    // round measured it, ipc_reopens).  The second attempt does that here,
+    // so a deferred nonblocking call — which has no confirmation round —
+    // recovers the same way: wait for this communicator's kernels (one may
+    // still read a mapping about to close), close the peer's unpinned
+    // mappings, open again.
+    for (int attempt = 0;; ++attempt) {
+        ++c->imports_new;
+        hipError_t e = hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess);
+        const char *what = nullptr;
+        if (e == hipSuccess) {
+            trace_handle("open", d.h, "peer %d id %llu %p+%llu -> %p", peer, (unsigned long long)d.id,
+                         (void *)(uintptr_t)d.base, (unsigned long long)d.size, base);
+            what = mapped_already(c, base);
+            if (!what) {
+                // the mapping must be the advertised allocation: the range
+                // the runtime reports for it has the exporter's base (offset
+                // 0) and size.  A stale answer — an earlier allocation at the
+                // same exporter address — has its own size (round 2: pushes
+                // into a peer's rbuf landed elsewhere after churn).
+                void *mb = nullptr;
+                size_t ms = 0;
+                const hipError_t er = hipMemGetAddressRange((hipDeviceptr_t *)&mb, &ms,
+                                                            (hipDeviceptr_t)base);
+                if (er != hipSuccess) (void)hipGetLastError();
+                // (the runtime may round the mapping up to its page size)
+                const uint64_t up = (d.size + (2u << 20) - 1) & ~(uint64_t)((2u << 20) - 1);
+                if (ipc_trace())
+                    fprintf(stderr, "[ipc pid %d] open-range %p+%zu advertised %llu\n", (int)getpid(),
+                            mb, ms, (unsigned long long)d.size);
+                if (er != hipSuccess || (mb == base && ms >= d.size && ms <= up)) break;
+                static thread_local char why[128];
+                snprintf(why, sizeof(why), "a mapping of %zu bytes at %p (advertised %llu at offset 0)",
+                         ms, mb, (unsigned long long)d.size);
+                what = why;
+                ++c->size_mismatch_opens;
+                // treated as an alias: the just-opened reference is closed below
+                c->imports.push_back({peer, d.h, d.id, d.base, d.size, base, ++c->use_clock, 0});
+            } else {
+                ++c->aliased_opens;
+            }
+        } else {
+            (void)hipGetLastError();
+        }
+        if (attempt == 1) {
+            if (what) {
+                unsigned hw[16];
+                memcpy(hw, &d.h, sizeof(hw));
+                record_msg("hipIpcOpenMemHandle returned %p for peer %d buffer id %llu (%p + %llu, "
+                           "handle word7 %08x), which is already this process's mapping of %s",
+                           base, peer, (unsigned long long)d.id, (void *)(uintptr_t)d.base,
+                           (unsigned long long)d.size, hw[7], what);
+            } else {
+                record_msg("hipIpcOpenMemHandle: %s (peer %d buffer id %llu at %p + %llu%s)",
+                           hipGetErrorString(e), peer, (unsigned long long)d.id,
+                           (void *)(uintptr_t)d.base, (unsigned long long)d.size,
+                           closed_same ? ", after closing its freed predecessor with the same handle"
+                                       : "");
+            }
+            return OMPI_AMD_ERR_HIP;
+        }
+        TRY(quiesce(c));
+        ++c->ipc_local_reopens;
+        bool closed_base = false;
+        for (auto it = c->imports.begin(); it != c->imports.end();) {
+            if (it->peer == peer && it->pins == 0) {
+                closed_base = closed_base || ((const char *)base >= (const char *)it->base &&
+                                              (const char *)base < (const char *)it->base + it->rsize);
+                (void)hipIpcCloseMemHandle(it->base);
+                it = c->imports.erase(it);
+            } else {
+                ++it;
+            }
+        }
+        // an alias answer into one of the mappings just closed may be a
+        // second reference to it (a refcounting runtime): drop that too;
+        // never close into a mapping still in use (another peer's, the
+        // communicator's own pages)
+        if (what && closed_base) (void)hipIpcCloseMemHandle(base);
         (void)hipGetLastError();
-        record_msg("hipIpcOpenMemHandle: %s (peer %d buffer id %llu at %p + %llu%s)",
-                   hipGetErrorString(e), peer, (unsigned long long)d.id, (void *)(uintptr_t)d.base,
-                   (unsigned long long)d.size,
-                   closed_same ? ", after closing its freed predecessor with the same handle" : "");
-        return OMPI_AMD_ERR_HIP;
+        base = nullptr;
     }
-    trace_handle("open", d.h, "peer %d id %llu %p+%llu -> %p", peer, (unsigned long long)d.id,
-                 (void *)(uintptr_t)d.base, (unsigned long long)d.size, base);
-    if (const char *what = mapped_already(c, base)) {
-        unsigned hw[16];
-        memcpy(hw, &d.h, sizeof(hw));
-        record_msg("hipIpcOpenMemHandle returned %p for peer %d buffer id %llu (%p + %llu, handle "
-                   "word7 %08x), which is already this process's mapping of %s",
-                   base, peer, (unsigned long long)d.id, (void *)(uintptr_t)d.base,
-                   (unsigned long long)d.size, hw[7], what);
-        ++c->aliased_opens;
-        return OMPI_AMD_ERR_HIP;
-    }
-    // now the peer's freed allocations that overlap this one (their
-    // mappings stayed open across the open above, see drop_stale_imports)
-    const int drc = drop_stale_imports(c, peer, d, nullptr, 1);
     c->imports.push_back({peer, d.h, d.id, d.base, d.size, base, ++c->use_clock, pin ? 1 : 0});
     *out = (const char *)base + d.off;
     if (base_out) *base_out = base;
-    return drc;
+    return OMPI_AMD_SUCCESS;
 }
 
 static void unpin_import(ompi_amd_comm_t *c, void *base) {
@@ -957,15 +1052,10 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
             status = 1;
             break;
         }
-        rc = drop_stale_imports(c, p, all[p].d, nullptr, 0);
+        rc = drop_stale_imports(c, p, all[p].d);
         if (rc != OMPI_AMD_SUCCESS) { status = 1; break; }
         void *m = nullptr;
         e = hipIpcOpenMemHandle(&m, all[p].d.h, hipIpcMemLazyEnablePeerAccess);
-        if (e == hipSuccess && drop_stale_imports(c, p, all[p].d, nullptr, 1) != OMPI_AMD_SUCCESS) {
-            (void)hipIpcCloseMemHandle(m);
-            status = 1;
-            break;
-        }
         if (e != hipSuccess) {
             record_hip(e, "hipIpcOpenMemHandle (landing)");
             status = 1;
@@ -1044,7 +1134,7 @@ static int launch_barrier(ompi_amd_comm_t *c, hipStream_t s) {
     ++c->epoch;
     const uint64_t ticks = (uint64_t)c->timeout_ms * 100000ull;  // s_memrealtime: 100 MHz
     hipLaunchKernelGGL(barrier_kernel, dim3(1), dim3(64), 0, s, c->flags, c->peer_flags, c->rank,
-                       c->size, c->epoch, c->err_dev, ticks);
+                       c->size, c->epoch, c->err_dev, ticks, c->dbg_dev);
     return record_hip(hipGetLastError(), "barrier launch");
 }
 
@@ -1060,6 +1150,69 @@ static int launch_copy(ompi_amd_comm_t *c, const cp_jobs &jobs, hipStream_t s) {
     return record_hip(hipGetLastError(), "copy launch");
 }
 
+// ---- shadow arena ----
+// First fit over the chunks (256-B granules, never across a chunk: peers map
+// each chunk separately); a new chunk of max(need, 64 MiB, everything so
+// far) when none fits.
+static int arena_alloc(ompi_amd_comm_t *c, size_t need, char **out) {
+    const size_t n = (std::max<size_t>(need, 1) + 255) & ~(size_t)255;
+    std::lock_guard<std::mutex> g(c->arena_mu);
+    for (auto &ch : c->arena) {
+        for (auto it = ch.free.begin(); it != ch.free.end(); ++it) {
+            if (it->second < n) continue;
+            const size_t off = it->first, left = it->second - n;
+            ch.free.erase(it);
+            if (left) ch.free[off + n] = left;
+            ch.used[off] = n;
+            *out = ch.base + off;
+            return OMPI_AMD_SUCCESS;
+        }
+    }
+    const size_t want = (std::max({n, (size_t)64 << 20, c->arena_bytes}) + (2u << 20) - 1) &
+                        ~(size_t)((2u << 20) - 1);
+    char *mem = nullptr;
+    hipIpcMemHandle_t h;
+    const hipError_t e = alloc_exportable(want, &mem, &h);
+    if (e != hipSuccess) return record_hip(e, "shadow arena: hipMalloc / hipIpcGetMemHandle");
+    c->arena.push_back({mem, want, {}, {}});
+    auto &ch = c->arena.back();
+    if (want > n) ch.free[n] = want - n;
+    ch.used[0] = n;
+    c->arena_bytes += want;
+    *out = mem;
+    return OMPI_AMD_SUCCESS;
+}
+
+// The caller guarantees no peer still reads the range (the call that used it
+// passed its trailing barrier on this rank's stream).
+static void arena_free(ompi_amd_comm_t *c, char *p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> g(c->arena_mu);
+    for (auto &ch : c->arena) {
+        if (p < ch.base || p >= ch.base + ch.size) continue;
+        const size_t off = (size_t)(p - ch.base);
+        auto u = ch.used.find(off);
+        if (u == ch.used.end()) return;
+        size_t lo = off, len = u->second;
+        ch.used.erase(u);
+        auto nx = ch.free.lower_bound(off);
+        if (nx != ch.free.end() && nx->first == off + len) {  // merge the next free range
+            len += nx->second;
+            nx = ch.free.erase(nx);
+        }
+        if (nx != ch.free.begin()) {  // and the previous one
+            auto pv = std::prev(nx);
+            if (pv->first + pv->second == lo) {
+                lo = pv->first;
+                len += pv->second;
+                ch.free.erase(pv);
+            }
+        }
+        ch.free[lo] = len;
+        return;
+    }
+}
+
 // ---- export fallback (shadow_set) ----
 static int shadow_reserve(ompi_amd_comm_t *c, size_t need, char **out) {
     if (need <= c->shadow_bytes) {
@@ -1069,13 +1222,11 @@ static int shadow_reserve(ompi_amd_comm_t *c, size_t need, char **out) {
     // the old shadow's last readers are the peers of an earlier call, done
     // once this rank's stream passed that call's trailing barrier
     TRY(quiesce(c));
-    if (c->shadow) (void)hipFree(c->shadow);
+    arena_free(c, c->shadow);
+    const size_t want = std::max(need, 2 * c->shadow_bytes);
     c->shadow = nullptr;
     c->shadow_bytes = 0;
-    const size_t want = (std::max(need, 2 * c->shadow_bytes) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
-    hipIpcMemHandle_t h;
-    const hipError_t e = alloc_exportable(want, &c->shadow, &h);
-    if (e != hipSuccess) return record_hip(e, "shadow buffer: hipMalloc / hipIpcGetMemHandle");
+    TRY(arena_alloc(c, want, &c->shadow));
     c->shadow_bytes = want;
     *out = c->shadow;
     return OMPI_AMD_SUCCESS;
@@ -1094,9 +1245,12 @@ static int shadow_plan(ompi_amd_comm_t *c, const void **src, size_t sbytes, void
     bool fs = false, fr = false;
     buf_desc d;
     if (*src && sbytes) {
-        const int rc = export_buf(c, *src, &d, &fs);
-        if (rc != OMPI_AMD_SUCCESS && !fs) return rc;
-        fs = fs || c->force_shadow;
+        if (c->force_shadow || !c->user_ipc) {
+            fs = true;
+        } else {
+            const int rc = export_buf(c, *src, &d, &fs);
+            if (rc != OMPI_AMD_SUCCESS && !fs) return rc;
+        }
     }
     if (inplace && fs && split_inplace) {
         // two shadows: the input (copied in) and the result (copied out)
@@ -1109,9 +1263,12 @@ static int shadow_plan(ompi_amd_comm_t *c, const void **src, size_t sbytes, void
         rbytes = std::max(rbytes, sbytes);
         rbuf_in = true;
     } else if (*rbuf && rbytes) {
-        const int rc = export_buf(c, *rbuf, &d, &fr);
-        if (rc != OMPI_AMD_SUCCESS && !fr) return rc;
-        fr = fr || c->force_shadow;
+        if (c->force_shadow || !c->user_ipc) {
+            fr = true;
+        } else {
+            const int rc = export_buf(c, *rbuf, &d, &fr);
+            if (rc != OMPI_AMD_SUCCESS && !fr) return rc;
+        }
     }
     if (!fs && !fr) return OMPI_AMD_SUCCESS;
     // each region keeps its user pointer's phase mod 256 (the kernels'
@@ -1122,9 +1279,7 @@ static int shadow_plan(ompi_amd_comm_t *c, const void **src, size_t sbytes, void
     const size_t need = (fr ? ro + rbytes : so + sbytes) + 256;
     char *mem = nullptr;
     if (owned) {
-        hipIpcMemHandle_t h;
-        const hipError_t e = alloc_exportable(need, &mem, &h);
-        if (e != hipSuccess) return record_hip(e, "shadow buffer: hipMalloc / hipIpcGetMemHandle");
+        TRY(arena_alloc(c, need, &mem));
         post->mem = mem;
     } else {
         TRY(shadow_reserve(c, need, &mem));
@@ -1645,6 +1800,24 @@ static int agree_root0_inplace(ompi_amd_comm_t *c, path_params *pp, bool inplace
     return OMPI_AMD_SUCCESS;
 }
 
+// This rank failed a call its peers may have launched: make the failure
+// sticky here and raise every peer's abort word (their barrier waits then
+// give up within ~1 ms and their calls fail with OMPI_AMD_ERR_TIMEOUT).
+static void abort_peers(ompi_amd_comm_t *c, int rc) {
+    int expect = 0;
+    (void)__atomic_compare_exchange_n(c->err_host, &expect, rc, false, __ATOMIC_ACQ_REL,
+                                      __ATOMIC_ACQUIRE);
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        return;
+    }
+    hipLaunchKernelGGL(abort_kernel, dim3(1), dim3(64), 0, s, c->peer_flags, c->rank, c->size);
+    if (hipGetLastError() == hipSuccess) (void)hipStreamSynchronize(s);
+    (void)hipGetLastError();
+    (void)hipStreamDestroy(s);
+}
+
 // Launch deferred nonblocking calls in posting order, each once every rank
 // has posted its handle-swap half; block = wait for them (the blocking entry
 // points do, so their device work follows the deferred calls' on every rank).
@@ -1684,7 +1857,12 @@ static int progress(ompi_amd_comm_t *c, bool block, int max_launch = -1) {
         o.req->stream = o.stream;
         o.req->rc = rc;
         o.req->launched = true;
-        if (rc != OMPI_AMD_SUCCESS) return rc;
+        if (rc != OMPI_AMD_SUCCESS) {
+            // peers launch this call from their own progress and would wait
+            // for this rank's device work until their timeout
+            abort_peers(c, rc);
+            return rc;
+        }
     }
     return OMPI_AMD_SUCCESS;
 }
@@ -1781,6 +1959,7 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
         const char *a = getenv("OMPI_MCA_coll_tuned_allreduce_algorithm");
         if (atoi(d) && a && atoi(a) >= 0 && atoi(a) < TUNED_AR_COUNT) c->tuned_alg = atoi(a);
     }
+    if (const char *u = getenv("OMPI_AMD_USER_IPC")) c->user_ipc = atoi(u) ? 1 : 0;
     if (const char *a = getenv("OMPI_AMD_COLL_ALGORITHM")) {
         const int v = atoi(a);
         if (v >= 0 && v < ALG_COUNT) c->algorithm = v;
@@ -1791,11 +1970,18 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
     // device resources: fine-grained flags, scratch, pinned error word
     c->scratch_bytes = std::max<size_t>(c->small_bytes, 4 << 20);  // per half
     ipc_blob mine{}, all[kMaxRanks];
-    hipError_t e = alloc_exportable(4096, (char **)&c->flags, &mine.flags, true);
-    if (e == hipSuccess) e = hipMemsetAsync(c->flags, 0, 4096, nullptr);
+    hipError_t e = alloc_exportable(kFlagPageBytes, (char **)&c->flags, &mine.flags, true);
+    if (e == hipSuccess) e = hipMemsetAsync(c->flags, 0, kFlagPageBytes, nullptr);
     if (e == hipSuccess) e = alloc_exportable(2 * c->scratch_bytes, &c->scratch, &mine.scratch);
     if (e == hipSuccess) e = hipHostMalloc((void **)&c->err_host, 64, hipHostMallocMapped);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&c->err_dev, c->err_host, 0);
+    if (e == hipSuccess && getenv("OMPI_AMD_DEBUG_PROGRESS") && atoi(getenv("OMPI_AMD_DEBUG_PROGRESS"))) {
+        e = hipHostMalloc((void **)&c->dbg_host, (2 + kMaxRanks) * sizeof(uint64_t), hipHostMallocMapped);
+        if (e == hipSuccess) {
+            memset(c->dbg_host, 0, (2 + kMaxRanks) * sizeof(uint64_t));
+            e = hipHostGetDevicePointer((void **)&c->dbg_dev, c->dbg_host, 0);
+        }
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(nullptr);  // the flag page is zero
     if (e != hipSuccess) {
         rc = record_hip(e, "comm device resources");
@@ -1848,8 +2034,10 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     if (c->flags) (void)hipFree(c->flags);
     if (c->scratch) (void)hipFree(c->scratch);
     if (c->land) (void)hipFree(c->land);
-    if (c->shadow) (void)hipFree(c->shadow);
+    for (auto &ch : c->arena) (void)hipFree(ch.base);  // shadows included
+    c->arena.clear();
     if (c->err_host) (void)hipHostFree(c->err_host);
+    if (c->dbg_host) (void)hipHostFree(c->dbg_host);
     for (int ph = 0; ph < 2; ++ph)
         for (auto &pr : c->ev_phase[ph]) {
             (void)hipEventDestroy(pr.first);
@@ -1968,6 +2156,8 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
         c->algorithm = (int)v;
     } else if (!strcmp(key, "force_shadow")) {
         c->force_shadow = v ? 1 : 0;
+    } else if (!strcmp(key, "user_ipc")) {
+        c->user_ipc = v ? 1 : 0;
     } else if (!strcmp(key, "tuned_allreduce_algorithm")) {
         if (v < 0 || v >= TUNED_AR_COUNT) return OMPI_AMD_ERR_BAD_PARAM;
         c->tuned_alg = (int)v;
@@ -1999,10 +2189,21 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "memcpy_token_mismatch")) *v = c->memcpy_token_mismatch;
     else if (!strcmp(key, "shadowed")) *v = c->shadowed;
     else if (!strcmp(key, "epoch")) *v = (int64_t)c->epoch;
+    else if (!strcmp(key, "ipc_local_reopens")) *v = c->ipc_local_reopens;
+    else if (!strcmp(key, "size_mismatch_opens")) *v = c->size_mismatch_opens;
+    else if (!strncmp(key, "dbg_", 4) && c->dbg_host) {  // dbg_entered / dbg_left / dbg_seenP
+        volatile uint64_t *d = c->dbg_host;
+        if (!strcmp(key, "dbg_entered")) *v = (int64_t)d[0];
+        else if (!strcmp(key, "dbg_left")) *v = (int64_t)d[1];
+        else if (!strncmp(key, "dbg_seen", 8) && atoi(key + 8) >= 0 && atoi(key + 8) < kMaxRanks)
+            *v = (int64_t)d[2 + atoi(key + 8)];
+        else return OMPI_AMD_ERR_BAD_PARAM;
+    }
     else if (!strcmp(key, "exports_new")) *v = c->exports_new;
     else if (!strcmp(key, "recycled_exports")) *v = c->recycled_exports;
     else if (!strcmp(key, "imports_new")) *v = c->imports_new;
     else if (!strcmp(key, "force_shadow")) *v = c->force_shadow;
+    else if (!strcmp(key, "user_ipc")) *v = c->user_ipc;
     else if (!strcmp(key, "imports")) *v = (int64_t)c->imports.size();
     else {
         record_msg("unknown coll param '%s'", key);
@@ -2085,7 +2286,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
         if (rc == OMPI_AMD_SUCCESS) rc = c->boot.post(&mine, sizeof(mine), &o.ticket);
         if (rc != OMPI_AMD_SUCCESS) {
             (void)hipEventDestroy(req->ev);
-            if (req->shadow) (void)hipFree(req->shadow);
+            arena_free(c, req->shadow);
             delete req;
             return rc;
         }
@@ -2136,7 +2337,7 @@ static int nb_post(ompi_amd_comm_t *c, pending_op &o, const void **exp, size_t b
     }
     if (rc != OMPI_AMD_SUCCESS) {
         (void)hipEventDestroy(req->ev);
-        if (req->shadow) (void)hipFree(req->shadow);
+        arena_free(c, req->shadow);
         delete req;
         return rc;
     }
@@ -2426,18 +2627,34 @@ static int bcast_impl(ompi_amd_comm_t *c, void *buf, const void *root_src, size_
     // scatter_allgather, one hop per phase on the fully connected xGMI
     // mesh): rank r copies block r from the root, barrier, then block b from
     // rank b for every other b.  Every link carries about 2·bytes/N instead
-    // of each of the root's links carrying `bytes`.  Needs every rank's
-    // buffer exportable (decided from the swapped descriptors, so alike on
-    // every rank) and a blocking call; otherwise the root-pull below.
+    // of each of the root's links carrying `bytes`.  What peers read is
+    // every rank's buffer itself (user_ipc, when every export succeeds) or
+    // every rank's communicator shadow (the root copies its buffer in; rank
+    // r keeps block r there too); a blocking call only, else the root-pull.
     if (!c->pre && c->bcast_split_bytes > 0 && bytes >= c->bcast_split_bytes) {
-        call_blob me{}, all[kMaxRanks];
-        bool refused = false;
-        if (export_buf(c, buf, &me.s, &refused) != OMPI_AMD_SUCCESS) me.s = buf_desc{};
-        TRY(c->boot.allgather(&me, all, sizeof(call_blob)));
-        bool every = true;
-        for (int p = 0; p < c->size; ++p) every = every && all[p].s.valid;
+        bool every = false;
+        char *mine_sh = nullptr;  // staged: this rank's shadow (buf's phase mod 256)
+        if (c->user_ipc) {
+            call_blob me{}, all[kMaxRanks];
+            bool refused = false;
+            if (export_buf(c, buf, &me.s, &refused) != OMPI_AMD_SUCCESS) me.s = buf_desc{};
+            TRY(c->boot.allgather(&me, all, sizeof(call_blob)));
+            every = true;
+            for (int p = 0; p < c->size; ++p) every = every && all[p].s.valid;
+            if (every) TRY(import_all(c, all, buf, nullptr, &sp, &rp, nullptr, false, nullptr));
+        } else {
+            char *base = nullptr;
+            TRY(shadow_reserve(c, bytes + 256, &base));
+            mine_sh = base + ((uintptr_t)buf & 255);
+            if (c->rank == root) {
+                cj.n = 1;
+                cj.j[0] = {(const char *)buf, mine_sh, (int64_t)bytes};
+                TRY(launch_copy(c, cj, s));
+            }
+            TRY(exchange_bufs(c, mine_sh, nullptr, &sp, &rp));
+            every = true;
+        }
         if (every) {
-            TRY(import_all(c, all, buf, nullptr, &sp, &rp, nullptr, false, nullptr));
             const int n = c->size;
             const size_t blk = ((bytes + (size_t)n - 1) / (size_t)n + 255) & ~(size_t)255;
             auto block = [&](int b, size_t *off, size_t *len) {
@@ -2448,8 +2665,9 @@ static int bcast_impl(ompi_amd_comm_t *c, void *buf, const void *root_src, size_
             size_t off, len;
             block(c->rank, &off, &len);
             if (c->rank != root && len) {
-                cj.n = 1;
-                cj.j[0] = {sp.p[root] + off, (char *)buf + off, (int64_t)len};
+                cj.n = 0;
+                cj.j[cj.n++] = {sp.p[root] + off, (char *)buf + off, (int64_t)len};
+                if (mine_sh) cj.j[cj.n++] = {sp.p[root] + off, mine_sh + off, (int64_t)len};
                 TRY(launch_copy(c, cj, s));
             }
             TRY(launch_barrier(c, s));  // every block is at its owner
@@ -2610,7 +2828,7 @@ int ompi_amd_plan_free(ompi_amd_plan_t *pl) {
                 if (pl->bases[p][k]) unpin_import(pl->c, pl->bases[p][k]);
     if (pl->sh.mem) {  // the plan's last start must be over before its shadow goes
         if (pl->started && pl->done) (void)ompi_amd_plan_wait(pl);
-        (void)hipFree(pl->sh.mem);
+        arena_free(pl->c, pl->sh.mem);
     }
     if (pl->done) (void)hipEventDestroy(pl->done);
     delete pl;
@@ -2658,7 +2876,7 @@ int ompi_amd_request_free(ompi_amd_request_t *r) {
     const int rc = ompi_amd_request_wait(r);
     if (r->ev) (void)hipEventDestroy(r->ev);
     // the call's trailing barrier has passed: no peer reads the shadow any more
-    if (r->shadow) (void)hipFree(r->shadow);
+    arena_free(r->c, r->shadow);
     delete r;
     return rc;
 }

@@ -66,6 +66,52 @@ __device__ __forceinline__ void acquire_once() {
     __syncthreads();
 }
 
+// Wait until *flag >= epoch (a peer's barrier store).  Bounded: past
+// `ticks` (s_memrealtime, 100 MHz) the communicator's sticky error word is
+// set; and every ~1 ms of waiting the word is read, so once any wait of this
+// communicator has given up, every later one gives up within 1 ms.  A rank
+// whose peer failed a call before launching it (e.g. an IPC open refused in
+// a deferred nonblocking call) thus drains its queued collectives in one
+// timeout instead of one per barrier, and reaches the host rendezvous of
+// comm_destroy while that peer is still there to keep its memory alive.
+// Returns false when the wait gave up.
+// The flag page: 32 rows x 16 ranks of epochs (4 KiB), then the abort word a
+// failing peer sets (abort_peers) — read by the same ~1 ms check.
+constexpr int kAbortWord = 512;               // uint64 index in the flag page
+constexpr size_t kFlagPageBytes = 8192;
+
+// seen (debug, OMPI_AMD_DEBUG_PROGRESS=1; else null): the flag value read
+// at every ~1 ms check, in host-mapped memory a watchdog can print.
+__device__ __forceinline__ bool wait_epoch(const uint64_t *flag, uint64_t epoch, int *err,
+                                           uint64_t ticks, const uint64_t *abort_word,
+                                           uint64_t *seen = nullptr) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t check = t0 + 100000;  // 1 ms
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+        __builtin_amdgcn_s_sleep(1);
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (now - t0 > ticks) {
+            __hip_atomic_store(err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            return false;
+        }
+        if (now >= check) {
+            if (seen)
+                __hip_atomic_store(seen, __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
+                return false;
+            if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+                __hip_atomic_store(err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                return false;
+            }
+            check = now + 100000;
+        }
+    }
+    return true;
+}
+
 // Every storing wave drains its stores before the workgroup's single
 // system-scope release (MI355X_MICROARCH.md, inter-workgroup visibility).
 __device__ __forceinline__ void xfer_epilogue() {
@@ -353,21 +399,18 @@ __global__ __launch_bounds__(kXferThreads) void fused_allreduce_kernel(fused_arg
     __syncthreads();
     if (t == 0) sys_release();
     __syncthreads();
+    __shared__ int gave_up;
+    if (t == 0) gave_up = 0;
+    __syncthreads();
     if (t < a.n && t != a.rank) {
         __hip_atomic_store(a.peer_flags.p[t] + g * kMaxRanks + a.rank, a.epoch, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(a.flags + g * kMaxRanks + t, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_SYSTEM) < a.epoch) {
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
-                __hip_atomic_store(a.err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-                break;
-            }
-        }
+        if (!wait_epoch(a.flags + g * kMaxRanks + t, a.epoch, a.err, a.timeout_ticks,
+                        a.flags + kAbortWord))
+            gave_up = 1;
     }
     __syncthreads();
+    if (gave_up) return;  // a peer never arrived: its scratch is not ours to read
     acquire_once();
     T *dst = reinterpret_cast<T *>(a.dst);
     for (int64_t e = lo + t; e < hi; e += kXferThreads) {

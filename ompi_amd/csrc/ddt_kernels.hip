@@ -281,6 +281,11 @@ __global__ void ddt_vec_edges(ddt_desc d, const char *src, char *dst, ddt_window
 // type's granule and stores them with one dwordx4 each.  Sub-16-B runs
 // (struct{int,double}, blacs indexed, vector of single doubles) thus move
 // with 16-B global accesses on both sides instead of 4- or 8-B granules.
+struct iov_job {
+    int64_t start, len;
+    char *contig;
+};
+
 struct ddt_period {
     int64_t psize;      // packed bytes per period
     int64_t pext;       // typed bytes between consecutive periods
@@ -291,22 +296,19 @@ struct ddt_period {
     const uint16_t *map;  // psize entries: typed offset - lowest, per packed byte
 };
 
+// Tiles tile0, tile0 + tstep, ... of the periods [j0, j1) of one window
+// (contig = the window's first packed byte, stream position start); the map
+// is staged in LDS by the caller.
 template <int G, bool IDENT>
-__global__ __launch_bounds__(kDdtThreads) void ddt_pack_tile_kernel(ddt_period P,
-                                                                   const char *typed,
-                                                                   char *contig, int64_t start,
-                                                                   int64_t j0, int64_t j1) {
-    extern __shared__ __attribute__((aligned(16))) char lds[];
+__device__ __forceinline__ void pack_tiles(const ddt_period &P, const char *typed, char *contig,
+                                           int64_t start, int64_t j0, int64_t j1, int64_t tile0,
+                                           int64_t tstep, const uint16_t *map, char *data) {
     using T = typename granule<G>::t;
     typedef unsigned int v4 __attribute__((ext_vector_type(4)));
     const int t = threadIdx.x;
-    uint16_t *map = reinterpret_cast<uint16_t *>(lds);
-    char *data = lds + P.map_bytes;
-    if (!IDENT)
-        for (int64_t i = t; i < P.psize; i += kDdtThreads) map[i] = P.map[i];
     constexpr int64_t step = 16 * kDdtThreads;  // packed bytes per lane pass
     const int64_t st_j = step / P.psize, st_q = step % P.psize;
-    for (int64_t tile = blockIdx.x;; tile += gridDim.x) {
+    for (int64_t tile = tile0;; tile += tstep) {
         const int64_t jt = j0 + tile * P.nper;
         if (jt >= j1) break;
         const int64_t nj = min(P.nper, j1 - jt);
@@ -363,6 +365,26 @@ __global__ __launch_bounds__(kDdtThreads) void ddt_pack_tile_kernel(ddt_period P
     }
 }
 
+// LDS: the period's byte map (unless IDENT), then the tile's data
+template <bool IDENT>
+__device__ __forceinline__ uint16_t *stage_map(const ddt_period &P, char *lds) {
+    uint16_t *map = reinterpret_cast<uint16_t *>(lds);
+    if (!IDENT)
+        for (int64_t i = threadIdx.x; i < P.psize; i += kDdtThreads) map[i] = P.map[i];
+    return map;
+}
+
+template <int G, bool IDENT>
+__global__ __launch_bounds__(kDdtThreads) void ddt_pack_tile_kernel(ddt_period P,
+                                                                   const char *typed,
+                                                                   char *contig, int64_t start,
+                                                                   int64_t j0, int64_t j1) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const uint16_t *map = stage_map<IDENT>(P, lds);
+    pack_tiles<G, IDENT>(P, typed, contig, start, j0, j1, blockIdx.x, gridDim.x, map,
+                         lds + P.map_bytes);
+}
+
 // Staged unpack, the mirror of the tile pack: a workgroup brings the packed
 // bytes of `nper` periods into LDS with 16-B nt loads (coalesced on the
 // contiguous side), then lane t writes packed granules t, t + 256, … of the
@@ -372,21 +394,15 @@ __global__ __launch_bounds__(kDdtThreads) void ddt_pack_tile_kernel(ddt_period P
 // the position walks by constant increments (one division per lane per
 // tile) instead of the generic kernel's element search + two divisions.
 template <int G, bool IDENT>
-__global__ __launch_bounds__(kDdtThreads) void ddt_unpack_tile_kernel(ddt_period P,
-                                                                     const char *contig,
-                                                                     char *typed, int64_t start,
-                                                                     int64_t j0, int64_t j1) {
-    extern __shared__ __attribute__((aligned(16))) char lds[];
+__device__ __forceinline__ void unpack_tiles(const ddt_period &P, const char *contig, char *typed,
+                                             int64_t start, int64_t j0, int64_t j1, int64_t tile0,
+                                             int64_t tstep, const uint16_t *map, char *data) {
     using T = typename granule<G>::t;
     typedef unsigned int v4 __attribute__((ext_vector_type(4)));
     const int t = threadIdx.x;
-    uint16_t *map = reinterpret_cast<uint16_t *>(lds);
-    char *data = lds + P.map_bytes;
-    if (!IDENT)
-        for (int64_t i = t; i < P.psize; i += kDdtThreads) map[i] = P.map[i];
     constexpr int64_t step = (int64_t)G * kDdtThreads;  // packed bytes per lane pass
     const int64_t st_j = step / P.psize, st_q = step % P.psize;
-    for (int64_t tile = blockIdx.x;; tile += gridDim.x) {
+    for (int64_t tile = tile0;; tile += tstep) {
         const int64_t jt = j0 + tile * P.nper;
         if (jt >= j1) break;
         const int64_t nj = min(P.nper, j1 - jt);
@@ -425,6 +441,17 @@ __global__ __launch_bounds__(kDdtThreads) void ddt_unpack_tile_kernel(ddt_period
     }
 }
 
+template <int G, bool IDENT>
+__global__ __launch_bounds__(kDdtThreads) void ddt_unpack_tile_kernel(ddt_period P,
+                                                                     const char *contig,
+                                                                     char *typed, int64_t start,
+                                                                     int64_t j0, int64_t j1) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const uint16_t *map = stage_map<IDENT>(P, lds);
+    unpack_tiles<G, IDENT>(P, contig, typed, start, j0, j1, blockIdx.x, gridDim.x, map,
+                           lds + P.map_bytes);
+}
+
 // One launch over a whole iovec array (the convertor's fAdvance with
 // out_size > 1): job j is stream window [start, start + len) to or from the
 // contiguous buffer contig (grid row y = job).  The reference fills an iovec
@@ -432,10 +459,6 @@ __global__ __launch_bounds__(kDdtThreads) void ddt_unpack_tile_kernel(ddt_period
 // (opal_generic_simple_pack, opal_datatype_pack.c:273-356); here every
 // granule of every iovec is one lane's work in the same launch, so a PML
 // fragment train costs one launch instead of one per fragment.
-struct iov_job {
-    int64_t start, len;
-    char *contig;
-};
 
 template <int G, bool UNPACK>
 __global__ __launch_bounds__(kDdtThreads) void ddt_iov_kernel(ddt_desc d, char *typed,
@@ -490,6 +513,39 @@ __global__ __launch_bounds__(kDdtThreads) void ddt_iov_kernel(ddt_desc d, char *
                                                      (uint64_t)p);
             if (UNPACK) typed[t] = c[p];
             else c[p] = typed[t];
+        }
+    }
+}
+
+// The staged tile kernels over an iovec array (periodic layouts): grid row
+// y = job, x = tiles of that job's whole periods; the last x-block also moves
+// the job's partial periods at both ends byte by byte (a 64 KiB PML fragment
+// rarely starts or ends on a period boundary).
+template <int G, bool IDENT, bool UNPACK>
+__global__ __launch_bounds__(kDdtThreads) void ddt_iov_tile_kernel(ddt_period P, ddt_desc d,
+                                                                   char *typed,
+                                                                   const iov_job *jobs) {
+    extern __shared__ __attribute__((aligned(16))) char lds[];
+    const uint16_t *map = stage_map<IDENT>(P, lds);
+    const iov_job jb = jobs[blockIdx.y];
+    const int64_t start = jb.start, end = jb.start + jb.len;
+    const int64_t j0 = (start + P.psize - 1) / P.psize, j1 = end / P.psize;
+    if (j1 > j0) {
+        if (UNPACK)
+            unpack_tiles<G, IDENT>(P, jb.contig, typed, start, j0, j1, blockIdx.x, gridDim.x, map,
+                                   lds + P.map_bytes);
+        else
+            pack_tiles<G, IDENT>(P, typed, jb.contig, start, j0, j1, blockIdx.x, gridDim.x, map,
+                                 lds + P.map_bytes);
+    }
+    if (blockIdx.x == gridDim.x - 1) {
+        const int64_t h1 = min(end, j0 * P.psize);     // head [start, h1)
+        const int64_t t0 = max(h1, j1 * P.psize);      // tail [t0, end)
+        const int64_t head = h1 - start, tail = end - t0;
+        for (int64_t k = threadIdx.x; k < head + tail; k += kDdtThreads) {
+            const int64_t p = k < head ? start + k : t0 + (k - head);
+            if (UNPACK) move_byte<true>(d.elems, d, jb.contig, typed, p, start);
+            else move_byte<false>(d.elems, d, typed, jb.contig, p, start);
         }
     }
 }
@@ -577,12 +633,16 @@ static int64_t tile_data_bytes() {
     return v;
 }
 
-template <bool UNPACK>
-static bool tile_run(const ompi_amd_ddt_t *ddt, size_t count, int G, char *typed, char *contig,
-                     int64_t start, int64_t end, const ddt_desc &d, hipStream_t s,
-                     hipError_t *err) {
-    static const bool off = getenv("OMPI_AMD_DDT_TILE") && atoi(getenv("OMPI_AMD_DDT_TILE")) == 0;
-    if (off || end - start < kTileMinWindow) return false;
+static bool tile_off() {
+    static const bool v = getenv("OMPI_AMD_DDT_TILE") && atoi(getenv("OMPI_AMD_DDT_TILE")) == 0;
+    return v;
+}
+
+// The period of the staged tile kernels for this layout (false: not
+// periodic enough, or a gap too wide to read through); *lds = dynamic LDS.
+static bool tile_period(const ompi_amd_ddt_t *ddt, size_t count, int G, bool unpack,
+                        ddt_period *out, bool *ident_out, size_t *lds) {
+    if (tile_off()) return false;
     ddt_period P{};
     bool ident = false;
     const ddt_elem &x = ddt->host[0];
@@ -606,14 +666,27 @@ static bool tile_run(const ompi_amd_ddt_t *ddt, size_t count, int G, char *typed
         return false;
     }
     if (P.pext < 0 || P.psize % G != 0) return false;
-    if (UNPACK && P.psize > P.pext) return false;  // the tile's packed bytes must fit its LDS
+    if (unpack && P.psize > P.pext) return false;  // the tile's packed bytes must fit its LDS
+    P.nper = std::max<int64_t>(1, (tile_data_bytes() - P.span) / std::max<int64_t>(P.pext, 1) + 1);
+    *lds = (size_t)P.map_bytes + (size_t)(((P.nper - 1) * P.pext + P.span + 15) & ~(int64_t)15) + 32;
+    *out = P;
+    *ident_out = ident;
+    return true;
+}
+
+template <bool UNPACK>
+static bool tile_run(const ompi_amd_ddt_t *ddt, size_t count, int G, char *typed, char *contig,
+                     int64_t start, int64_t end, const ddt_desc &d, hipStream_t s,
+                     hipError_t *err) {
+    if (end - start < kTileMinWindow) return false;
+    ddt_period P{};
+    bool ident = false;
+    size_t lds = 0;
+    if (!tile_period(ddt, count, G, UNPACK, &P, &ident, &lds)) return false;
     const int64_t j0 = (start + P.psize - 1) / P.psize, j1 = end / P.psize;
     if (j1 <= j0) return false;
-    P.nper = std::max<int64_t>(1, (tile_data_bytes() - P.span) / std::max<int64_t>(P.pext, 1) + 1);
     const int64_t tiles = (j1 - j0 + P.nper - 1) / P.nper;
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(tiles, 2048));
-    const size_t lds = (size_t)P.map_bytes +
-                       (size_t)(((P.nper - 1) * P.pext + P.span + 15) & ~(int64_t)15) + 32;
     hipError_t e = hipSuccess;
 #define TILE(GG)                                                                               \
     case GG:                                                                                   \
@@ -796,14 +869,44 @@ static int ddt_iov(const ompi_amd_ddt_t *ddt, size_t count, void *typed, size_t 
         const ddt_desc d{ddt->dev, (int)ddt->host.size(), ddt->size, ddt->extent, {0u, 0u, 0u}};
         const int64_t per = (int64_t)kDdtThreads * kDdtUnroll * G;
         const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((most + per - 1) / per, 1024));
+        // periodic layouts: the staged tile kernels per job (LDS-staged
+        // 16-B accesses on both sides instead of per-granule searches)
+        ddt_period P{};
+        bool ident = false;
+        size_t lds = 0;
+        const bool tiled = tile_period(ddt, count, G, UNPACK, &P, &ident, &lds);
+        // whole periods of the longest job, in tiles (+1: a job need not start
+        // on a period boundary)
+        const unsigned tgx = tiled ? (unsigned)std::max<int64_t>(
+                                         1, std::min<int64_t>((most / std::max<int64_t>(P.psize, 1) +
+                                                               P.nper) / P.nper, 2048))
+                                   : 1u;
         for (int j0 = 0; e == hipSuccess && j0 < jobs; j0 += 65535) {
             const dim3 grid(gx, (unsigned)std::min(65535, jobs - j0));
             const iov_job *tab = t.dev + j0;
-            switch (G) {
+            if (tiled) {
+                const dim3 tgrid(tgx, grid.y);
+#define IOVT(GG)                                                                                \
+    case GG:                                                                                    \
+        if (ident)                                                                              \
+            hipLaunchKernelGGL((ddt_iov_tile_kernel<GG, true, UNPACK>), tgrid, dim3(kDdtThreads), \
+                               lds, s, P, d, (char *)typed, tab);                               \
+        else                                                                                    \
+            hipLaunchKernelGGL((ddt_iov_tile_kernel<GG, false, UNPACK>), tgrid, dim3(kDdtThreads), \
+                               lds, s, P, d, (char *)typed, tab);                               \
+        break;
+                switch (G) {
+                    IOVT(16) IOVT(8) IOVT(4) IOVT(2)
+                default: IOVT(1)
+                }
+#undef IOVT
+            } else {
+                switch (G) {
 #define IOVK(GG) case GG: hipLaunchKernelGGL((ddt_iov_kernel<GG, UNPACK>), grid, dim3(kDdtThreads), 0, s, d, (char *)typed, tab); break;
-                IOVK(16) IOVK(8) IOVK(4) IOVK(2)
-            default: IOVK(1)
+                    IOVK(16) IOVK(8) IOVK(4) IOVK(2)
+                default: IOVK(1)
 #undef IOVK
+                }
             }
             e = hipGetLastError();
         }

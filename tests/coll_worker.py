@@ -582,6 +582,10 @@ def report(rank, n, obj):
 
 def main():
     rank, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    import faulthandler
+    # a rank stuck for a minute prints every thread's stack (then again each
+    # minute): a hang names the call it sits in
+    faulthandler.dump_traceback_later(60, repeat=True, file=sys.stderr)
     device = int(os.environ.get("OMPI_AMD_DEVICE", "0"))
     torch.cuda.set_device(device)
     dist.init_process_group("gloo", rank=rank, world_size=n)
@@ -592,7 +596,27 @@ def main():
     big = int(os.environ.get("COLL_BIG", 1 << 22))
     F, D, I32, I64, I8, DI = (mop.MPI_FLOAT, mop.MPI_DOUBLE, mop.MPI_INT32_T, mop.MPI_INT64_T,
                               mop.MPI_INT8_T, mop.MPI_DOUBLE_INT)
+    def user_ipc(fn, alg=0):  # zero-copy on the caller's own buffers (param "user_ipc")
+        def run():
+            comm.set_param("user_ipc", 1)
+            comm.set_param("algorithm", alg)
+            try:
+                return fn()
+            finally:
+                comm.set_param("user_ipc", 0)
+                comm.set_param("algorithm", 0)
+        return run
     cases = [
+        # user_ipc first, before any allocation churn
+        ("user_ipc_ar_pull", user_ipc(lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, big + 5, 160,
+                                                             repeat=2))),
+        ("user_ipc_ar_pullpush_inplace", user_ipc(lambda: case_allreduce(
+            comm, rank, n, F, mop.MPI_SUM, big, 161, inplace=True), 1)),
+        ("user_ipc_ar_push", user_ipc(lambda: case_allreduce(comm, rank, n, D, mop.MPI_SUM, big // 2 + 3,
+                                                             162), 2)),
+        ("user_ipc_rsb_allgather", user_ipc(lambda: (lambda a, b: (a[0] and b[0], a[1] + b[1]))(
+            case_rsb(comm, rank, n, DI, mop.MPI_MAXLOC, big // 8, 163),
+            case_allgather(comm, rank, n, (big * 4) // n + 12, 164)))),
         ("ar_sum_f32_1", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, 1, 1)),
         ("ar_sum_f32_7", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, 7, 2)),
         ("ar_sum_f32_2499_tree", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, 2499, 3)),
@@ -808,12 +832,32 @@ def main():
         hi = names.index(last) + 1 if last else len(names)
         cases = cases[lo:hi]
         only = None
+    import threading
+    cur = {"name": None, "t0": 0.0}
+
+    def watchdog():  # a case running long prints the barrier progress record
+        import time
+        while True:
+            time.sleep(20)
+            name, t0 = cur["name"], cur["t0"]
+            if name is None or time.time() - t0 < 40:
+                continue
+            try:
+                keys = ["epoch", "dbg_entered", "dbg_left"] + [f"dbg_seen{p}" for p in range(n)]
+                vals = {k: comm.get_param(k) for k in keys}
+            except Exception as e:  # noqa: BLE001 (debug record off)
+                vals = {"error": str(e)}
+            print(f"[watchdog] case {name} running {time.time() - t0:.0f} s: {vals}",
+                  file=sys.stderr, flush=True)
+
+    threading.Thread(target=watchdog, daemon=True).start()
     ok_all = True
     for name, fn in cases:
         if only and name not in only.split(","):
             continue
-        if os.environ.get("OMPI_AMD_IPC_TRACE") == "1":
-            print(f"[case {name}] epoch {comm.get_param('epoch')}", file=sys.stderr, flush=True)
+        print(f"[case {name}] epoch {comm.get_param('epoch')}", file=sys.stderr, flush=True)
+        import time as _t
+        cur["name"], cur["t0"] = name, _t.time()
         try:
             ok, msg = fn()
         except Exception as e:  # report and stop: later cases would hang
@@ -826,7 +870,8 @@ def main():
         report(rank, n, {"rank": rank, "case": name, "ok": bool(ok), "msg": msg,
                          "state": {k: comm.get_param(k) for k in (
                              "epoch", "shadowed", "recycled_exports", "stale_closed", "exports_new",
-                             "imports_new", "imports", "landing_bytes", "aliased_opens", "boot_calls", "ipc_reopens", "memcpy_token_mismatch")}})
+                             "imports_new", "imports", "landing_bytes", "aliased_opens", "boot_calls", "ipc_reopens", "memcpy_token_mismatch",
+                             "ipc_local_reopens", "size_mismatch_opens")}})
         ok_all &= bool(ok)
     # zero-copy disabled: everything staged through the scratch
     if ok_all and not only and not os.environ.get("COLL_HEADLINE"):

@@ -35,7 +35,10 @@ def run_ranks(n, timeout=600, extra_env=None, worker=WORKER):
         os.environ["COLL_LOG_DIR"] = os.path.join(os.environ["GRAFT_REPO_ROOT"], "gpurun_out",
                                                   "coll_logs")
     port = free_port()
-    procs = []
+    logdir = os.environ.get("COLL_LOG_DIR")
+    if logdir:
+        os.makedirs(logdir, exist_ok=True)
+    procs, files = [], []
     for r in range(n):
         env = dict(os.environ)
         env.update({"RANK": str(r), "WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
@@ -43,23 +46,26 @@ def run_ranks(n, timeout=600, extra_env=None, worker=WORKER):
                     "OMPI_AMD_DEVICE": str(r % ngpu if ngpu >= n else 0),
                     "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
         env.update(extra_env or {})
-        procs.append(subprocess.Popen([sys.executable, worker], env=env, stdout=subprocess.PIPE,
+        # raw per-rank output (library diagnostics on stderr) goes straight to
+        # a file, so that it survives a run killed at its time limit
+        path = os.path.join(logdir, f"raw_n{n}_rank{r}.txt") if logdir else None
+        f = open(path, "w+") if path else subprocess.PIPE
+        files.append(f)
+        procs.append(subprocess.Popen([sys.executable, worker], env=env, stdout=f,
                                       stderr=subprocess.STDOUT, text=True))
     outs = []
     try:
-        for p in procs:
+        for p, f in zip(procs, files):
             out, _ = p.communicate(timeout=timeout)
+            if f is not subprocess.PIPE:
+                f.seek(0)
+                out = f.read()
+                f.close()
             outs.append((p.returncode, out))
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
-    logdir = os.environ.get("COLL_LOG_DIR")
-    if logdir:  # raw per-rank output (library diagnostics on stderr)
-        os.makedirs(logdir, exist_ok=True)
-        for r, (_, out) in enumerate(outs):
-            with open(os.path.join(logdir, f"raw_n{n}_rank{r}.txt"), "w") as f:
-                f.write(out or "")
     return outs
 
 

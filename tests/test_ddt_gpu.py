@@ -232,3 +232,88 @@ def test_tile_unpack_layouts(orc, layout):
         got = dst.cpu().numpy()
         assert np.array_equal(got, exp), (layout, chunk, src_off,
                                           int(np.flatnonzero(got != exp)[:1].sum()))
+
+
+def tile_layout(layout, count_cap=None):
+    i32, f64 = dd.predefined("MPI_INT"), dd.predefined("MPI_DOUBLE")
+    lens = [13, 13, 13, 13, 13, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1]
+    disps = [286, 308, 330, 352, 374, 396, 419, 442, 465, 488, 511, 534, 557, 580, 603,
+             626, 649, 672]
+    mk = {
+        "struct_int_double": (lambda c: dd.type_struct([1, 1], [0, 8], [i32, f64]), 200003, True),
+        "blacs": (lambda c: dd.type_indexed(lens, disps, i32), 4001, True),
+        "vector_bl1_single": (lambda c: dd.type_vector(c, 1, 2, f64), 300007, False),
+        "vector_bl8_single": (lambda c: dd.type_vector(c, 8, 16, f64), 40009, False),
+        "vector5_bl1_tiled": (lambda c: dd.type_vector(5, 1, 2, f64), 50001, True),
+        "struct_neg_lb": (lambda c: dd.type_struct([1, 2], [-8, 4], [f64, i32]), 70001, True),
+        "contig_resized": (lambda c: dd.type_struct([3], [4], [i32]), 100001, True),
+    }
+    fn, count, tiled_count = mk[layout]
+    if count_cap:
+        count = max(3, min(count, count_cap))
+    if tiled_count:
+        return fn(None), count
+    return fn(count), 1
+
+
+IOV_LAYOUTS = ["struct_int_double", "blacs", "vector_bl1_single", "vector_bl8_single",
+               "vector5_bl1_tiled", "struct_neg_lb", "contig_resized"]
+
+
+@pytest.mark.parametrize("layout", IOV_LAYOUTS)
+@pytest.mark.parametrize("frag", [65536, 4099, 12])
+def test_iov_train_layouts(orc, layout, frag):
+    """fAdvance over iovec trains (ompi_amd_ddt_pack_iov / _unpack_iov, one
+    launch per call; periodic layouts run the staged tile kernels per iovec,
+    partial periods at each fragment's ends byte by byte): the stream in
+    `frag`-byte fragments at odd offsets (64 KiB ones aligned) of one device buffer, several calls
+    of up to 97 iovecs each, resumed at bConverted.  Pack byte-exact vs the
+    oracle; unpack into a pre-filled typed buffer byte-exact vs the oracle's
+    unpack into the same buffer (gap bytes untouched)."""
+    probe, _ = tile_layout(layout)
+    cap = None if frag >= 4096 else max(3, (frag * 6000) // probe.size)
+    dt, count = tile_layout(layout, cap)
+    total = dt.size * count
+    lb = min(d for d, _ in dt.runs)
+    shift = max(0, -lb)
+    runs = [(d + shift, n) for d, n in dt.runs]
+    span = span_of(dt, count) + shift
+    src = dev_bytes(span, seed=21)
+    exp = orc.pack(runs, dt.extent, count, src.cpu().numpy()[:span].copy(), 0, total)
+    nfrag = (total + frag - 1) // frag
+    # 64 KiB fragments 16-B aligned (the type's own granule), the others at
+    # odd offsets (byte granules)
+    off, pitch = (0, frag + 16) if frag == 65536 else (1, frag + 3)
+    packed = dev_bytes(nfrag * pitch + 16, seed=22)
+    base = packed.data_ptr() + off
+    iovs = [(base + i * pitch, frag) for i in range(nfrag)]
+    per_call = 97
+    conv = dd.Convertor()
+    conv.prepare_for_send(dt, count, src.data_ptr() + shift)
+    pos = 0
+    for c0 in range(0, nfrag, per_call):
+        rc, lens, used, moved = conv.pack_iov(iovs[c0:c0 + per_call])
+        want = min(per_call * frag, total - pos)
+        assert moved == want and sum(lens) == want, (layout, frag, c0)
+        pos += moved
+        assert rc == (1 if pos == total else 0)
+    torch.cuda.synchronize()
+    got_all = packed.cpu().numpy()
+    got = np.concatenate([got_all[off + i * pitch:off + i * pitch + min(frag, total - i * frag)]
+                          for i in range(nfrag)])
+    assert np.array_equal(got, exp), (layout, frag, int(np.flatnonzero(got != exp)[:1].sum()))
+    # unpack the same fragments into a pre-filled typed buffer
+    fill = dev_bytes(span, seed=23)
+    want_typed = fill.cpu().numpy().copy()
+    orc.unpack(runs, dt.extent, count, exp.copy(), want_typed, 0)
+    conv = dd.Convertor()
+    conv.prepare_for_recv(dt, count, fill.data_ptr() + shift)
+    pos = 0
+    for c0 in range(0, nfrag, per_call):
+        rc, lens, used, moved = conv.unpack_iov(iovs[c0:c0 + per_call])
+        pos += moved
+        assert rc == (1 if pos == total else 0)
+    torch.cuda.synchronize()
+    out = fill.cpu().numpy()
+    assert np.array_equal(out, want_typed), (layout, frag, "unpack",
+                                             int(np.flatnonzero(out != want_typed)[:1].sum()))
