@@ -16,6 +16,14 @@ import os
 import time
 
 
+def _progress(rank, what):
+    """One stderr line per bench phase on rank 0 (a long multi-rank run shows
+    where it is; the GPU box's watchdog takes a silent run for a hung one)."""
+    if rank == 0:
+        import sys
+        print(f"[bench] {time.strftime('%H:%M:%S')} {what}", file=sys.stderr, flush=True)
+
+
 def _timed(fn, steps, warmup, dist, torch, dev="cuda"):
     for _ in range(warmup):
         fn()
@@ -71,23 +79,33 @@ def bench_allreduce(args, metric: str, link_gbs: float):
     # times, so they agree.
     S = n * 4
     factor = 2.0 * (world - 1) / world
+    # ipc "staged": peers read this rank's shadow (the library default,
+    # user_ipc = 0); "user": peers map the caller's x / y directly (param
+    # user_ipc = 1; these buffers live for the whole run, so no mapping goes
+    # stale).  Both are MCA-settable; the line names the one that ran.
     schemes = {}
-    for a, name in ALGORITHMS:
-        comm.set_param("algorithm", a)
-        comm.set_param("blocks", 1024)
-        exact = _exact_ok(comm, dist, torch, mop, n, rank, shared)
-        for blocks in BLOCKS:
-            comm.set_param("blocks", blocks)
-            ta = _timed(ours, 5, 2, dist, torch, tdev) / 5
-            schemes[f"{name}/{blocks}"] = {"algorithm": a, "blocks": blocks, "bit_exact": exact,
-                                           "us": round(ta * 1e6, 2),
-                                           "busbw": round(S / ta * factor / 1e9, 2)}
+    for ipc in ("staged", "user"):
+        comm.set_param("user_ipc", 1 if ipc == "user" else 0)
+        for a, name in ALGORITHMS:
+            comm.set_param("algorithm", a)
+            comm.set_param("blocks", 1024)
+            _progress(rank, f"scheme {name}/{ipc}: exactness check")
+            exact = _exact_ok(comm, dist, torch, mop, n, rank, shared)
+            _progress(rank, f"scheme {name}/{ipc}: bit_exact={exact}, timing {len(BLOCKS)} grids")
+            for blocks in BLOCKS:
+                comm.set_param("blocks", blocks)
+                ta = _timed(ours, 5, 2, dist, torch, tdev) / 5
+                schemes[f"{name}/{ipc}/{blocks}"] = {
+                    "algorithm": a, "ipc": ipc, "blocks": blocks, "bit_exact": exact,
+                    "us": round(ta * 1e6, 2), "busbw": round(S / ta * factor / 1e9, 2)}
     usable = [v for v in schemes.values() if v["bit_exact"] is not False]
     best = min(usable or schemes.values(), key=lambda v: v["us"])
+    comm.set_param("user_ipc", 1 if best["ipc"] == "user" else 0)
     comm.set_param("algorithm", best["algorithm"])
     comm.set_param("blocks", best["blocks"])
     best_name = next(k for k, v in schemes.items() if v is best)
 
+    _progress(rank, f"headline: {best_name}")
     t = _timed(ours, args.steps, args.warmup, dist, torch, tdev)
     err = comm.error()
     # per-phase kernel time over one more profiled pass of K steps
@@ -152,15 +170,24 @@ def bench_allreduce(args, metric: str, link_gbs: float):
         # every rank waits while rank 0 runs the CPU ring on `world` cores
         dist.barrier()
         if rank == 0:
+            _progress(rank, "cpu baseline (CPU ring restatement)")
             res["cpu_baseline"] = cpu_baseline_ring(world, S, factor)
         dist.barrier()
     if not args.no_extras:
+        # the extras allocate buffers per size: the library default (staged)
+        comm.set_param("user_ipc", 0)
         try:
+            _progress(rank, "extras: check")
             res["check"] = _check_exact(comm, dist, torch, mop, n, rank, shared)
+            _progress(rank, "extras: sweep")
             res["sweep"] = _sweep(comm, dist, torch, mop, world, shared, tdev)
+            _progress(rank, "extras: config5")
             res["config5"] = _config5(comm, dist, torch, mop, world, rank, tdev)
+            _progress(rank, "extras: variants")
             res["variants"] = _variants(comm, dist, torch, mop, world, tdev)
+            _progress(rank, "extras: next_rows")
             res["next_rows"] = _next_rows(comm, dist, torch, mop, world, rank, tdev)
+            _progress(rank, "extras: p2p_osc")
             res["p2p_osc"] = _p2p_osc_rows(comm, dist, torch, mop, world, rank, tdev)
         except Exception as e:  # extras never break the headline line
             res["extras_error"] = f"{type(e).__name__}: {e}"

@@ -1622,6 +1622,41 @@ static int allreduce_pull(ompi_amd_comm_t *c, const ptr_set &sp, const ptr_set &
     return launch_barrier(c, s);
 }
 
+// The pull scheme staged through this rank's shadow `sh` (user_ipc off):
+// peers read only shadows.  The caller copied the input into `sh` and
+// swapped shadows (sp[r] = rank r's).  The owner of block b folds it from
+// every shadow and stores the result into its rbuf AND into block b of its
+// own shadow (nobody else reads that block of it during the fold), so the
+// gather phase pulls results from the shadows: one local copy of the input
+// is the whole price of staging (no result shadow, no copy out).
+static int allreduce_pull_staged(ompi_amd_comm_t *c, const ptr_set &sp, char *sh, void *rbuf,
+                                 int64_t count, int op, int type, const fold_plan &fp,
+                                 hipStream_t s) {
+    const int n = c->size, mine = (c->rank + 1) % n;
+    const int64_t ext = (int64_t)ompi_amd_type_extent(type);
+    TRY(launch_barrier(c, s));
+    red_jobs jobs;
+    fold_jobs(fp, count, n, mine, &jobs);
+    ptr_set dsts{};
+    dsts.p[0] = (const char *)rbuf;
+    dsts.p[1] = sh;
+    TRY(timed_phase(c, 0, s, [&] {
+        return launch_reduce(c, op, type, sp, n, dsts, 2, fp.order, fp.flags, jobs, s);
+    }));
+    TRY(launch_barrier(c, s));
+    int64_t split, early, late;
+    blockcount(count, n, &split, &early, &late);
+    cp_jobs cj{};
+    for (int b = 0; b < n; ++b) {
+        if (b == mine) continue;
+        const int owner = (b + n - 1) % n;
+        const int64_t off = block_off(b, split, early, late) * ext;
+        cj.j[cj.n++] = {sp.p[owner] + off, (char *)rbuf + off, block_cnt(b, split, early, late) * ext};
+    }
+    TRY(timed_phase(c, 1, s, [&] { return launch_copy(c, cj, s); }));
+    return launch_barrier(c, s);
+}
+
 static int allreduce_pull_push(ompi_amd_comm_t *c, const ptr_set &sp, const ptr_set &rp,
                                int64_t count, int op, int type, const fold_plan &fp,
                                hipStream_t s) {
@@ -1903,6 +1938,20 @@ static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size
         return launch_reduce(c, op, type, sh.peers, n, one_ptr(rbuf), 1, fp.order, fp.flags, jobs, s);
     }
     ptr_set sp{}, rp{};
+    if (!c->pre && pp.algorithm == ALG_PULL && !c->user_ipc && !c->force_shadow) {
+        // staged pull: the input into this rank's shadow (rbuf's phase mod
+        // 256, so results and shadows line up for 16-B vectors), swap
+        // shadows, fold / gather through them
+        char *base = nullptr;
+        TRY(shadow_reserve(c, bytes + 256, &base));
+        char *sh = base + ((uintptr_t)rbuf & 255);
+        cp_jobs cj{};
+        cj.n = 1;
+        cj.j[0] = {(const char *)src, sh, (int64_t)bytes};
+        TRY(launch_copy(c, cj, s));
+        TRY(exchange_bufs(c, sh, nullptr, &sp, &rp));
+        return allreduce_pull_staged(c, sp, sh, rbuf, (int64_t)count, op, type, fp, s);
+    }
     // export fallback (shadow_plan); a deferred call substituted its
     // shadows when it was posted, so these export and plan nothing
     const bool push = pp.algorithm == ALG_PUSH;
