@@ -60,8 +60,15 @@ int ompi_amd_comm_size(const ompi_amd_comm_t *comm);
  *   "small_bytes"   messages up to this size go through the staged path
  *                   (copy into the IPC scratch, no host rendezvous);
  *                   default 1 MiB, capped at the scratch size
- *   "zero_copy"     1 (default): large messages read peers' user buffers
- *                   directly; 0: always stage through the scratch
+ *   "zero_copy"     1 (default): large messages move peer to peer (through
+ *                   shadows, or the caller's buffers with user_ipc);
+ *                   0: always stage through the scratch
+ *   "user_ipc"      0 (default): every large call stages what peers read
+ *                   into the communicator's shadow arena (exported once,
+ *                   freed only with the communicator); 1: peers map the
+ *                   caller's buffers directly (env OMPI_AMD_USER_IPC) —
+ *                   only for buffers that are not freed and reallocated
+ *                   while the communicator lives
  *   "timeout_ms"    device spin limit per barrier (default 30000)
  *   "blocks"        grid cap of the transfer kernels (default 1024)
  *   "algorithm"     data movement of zero-copy allreduces (all ranks alike):

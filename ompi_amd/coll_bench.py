@@ -16,12 +16,40 @@ import os
 import time
 
 
+_PHASE = {"what": None, "t0": 0.0}
+
+
 def _progress(rank, what):
     """One stderr line per bench phase on rank 0 (a long multi-rank run shows
     where it is; the GPU box's watchdog takes a silent run for a hung one)."""
+    _PHASE["what"], _PHASE["t0"] = what, time.time()
     if rank == 0:
         import sys
         print(f"[bench] {time.strftime('%H:%M:%S')} {what}", file=sys.stderr, flush=True)
+
+
+def _watchdog(comm, rank, world):
+    """Every rank: a phase running over 30 s prints the communicator's epoch
+    and (OMPI_AMD_DEBUG_PROGRESS=1) its barrier progress record."""
+    import sys
+    import threading
+
+    def run():
+        while True:
+            time.sleep(15)
+            what, t0 = _PHASE["what"], _PHASE["t0"]
+            if what is None or time.time() - t0 < 30:
+                continue
+            vals = {}
+            for k in ["epoch", "dbg_entered", "dbg_left"] + [f"dbg_seen{p}" for p in range(world)]:
+                try:
+                    vals[k] = comm.get_param(k)
+                except Exception:  # noqa: BLE001 (debug record off)
+                    pass
+            print(f"[bench watchdog rank {rank}] {what} running {time.time() - t0:.0f} s: {vals}",
+                  file=sys.stderr, flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
 
 
 def _timed(fn, steps, warmup, dist, torch, dev="cuda"):
@@ -62,6 +90,7 @@ def bench_allreduce(args, metric: str, link_gbs: float):
     tdev = "cpu" if shared else "cuda"
     rank, world = dist.get_rank(), dist.get_world_size()
     comm = coll.Communicator.from_torch_distributed(device=local)
+    _watchdog(comm, dist.get_rank(), dist.get_world_size())
 
     n = args.ar_bytes // 4
     g = torch.Generator(device="cuda").manual_seed(20261015 + rank)
@@ -261,6 +290,7 @@ def _sweep(comm, dist, torch, mop, world, shared, tdev):
     out = []
     factor = 2.0 * (world - 1) / world
     for nbytes in (8, 1024, 65536, 1 << 20, 16 << 20, 64 << 20, 256 << 20, 1 << 30):
+        _progress(dist.get_rank(), f"sweep {nbytes} B")
         n = max(1, nbytes // 4)
         x = torch.ones(n, device="cuda")
         y = torch.empty_like(x)

@@ -69,6 +69,7 @@ mca_coll_rocm_component_t mca_coll_rocm_component = {
     .zero_copy = 1,
     .timeout_ms = 30000,
     .algorithm = 0,
+    .user_ipc = 0,
     .residency = ROCM_RES_AUTO,
     .residency_lock = 8,
     .residency_recheck = 256,
@@ -87,7 +88,7 @@ static int rocm_register(void)
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_coll_rocm_component.small_bytes);
     (void) mca_base_component_var_register(c, "zero_copy",
-                                           "Read peers' user buffers directly for large messages",
+                                           "Large messages peer to peer (through shadows, or the caller's buffers with user_ipc)",
                                            MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_coll_rocm_component.zero_copy);
@@ -101,6 +102,12 @@ static int rocm_register(void)
                                            MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_coll_rocm_component.algorithm);
+    (void) mca_base_component_var_register(c, "user_ipc",
+                                           "Let peers map the caller's buffers (zero-copy); 0 stages every "
+                                           "large call through the communicator's exported shadow arena",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_coll_rocm_component.user_ipc);
     (void) mca_base_component_var_register(c, "residency",
                                            "Where blocking collectives run: 0 vote per call until the ranks "
                                            "agree coll_rocm_residency_lock times in a row, 1 device (host "
@@ -238,6 +245,7 @@ int mca_coll_rocm_module_enable(mca_coll_base_module_t *module, struct ompi_comm
     (void) ompi_amd_comm_set_param(m->dev_comm, "zero_copy", mca_coll_rocm_component.zero_copy);
     (void) ompi_amd_comm_set_param(m->dev_comm, "timeout_ms", mca_coll_rocm_component.timeout_ms);
     (void) ompi_amd_comm_set_param(m->dev_comm, "algorithm", mca_coll_rocm_component.algorithm);
+    (void) ompi_amd_comm_set_param(m->dev_comm, "user_ipc", mca_coll_rocm_component.user_ipc);
     if (ROCM_RES_DEVICE == mca_coll_rocm_component.residency ||
         ROCM_RES_HOST == mca_coll_rocm_component.residency) {
         m->mode = mca_coll_rocm_component.residency;
