@@ -289,7 +289,10 @@ def _sweep(comm, dist, torch, mop, world, shared, tdev):
     and RCCL side by side."""
     out = []
     factor = 2.0 * (world - 1) / world
-    for nbytes in (8, 1024, 65536, 1 << 20, 16 << 20, 64 << 20, 256 << 20, 1 << 30):
+    sizes = (8, 1024, 65536, 1 << 20, 16 << 20, 64 << 20, 256 << 20, 1 << 30)
+    if os.environ.get("OMPI_AMD_BENCH_SWEEP"):  # e.g. "1073741824": a subset (rehearsals)
+        sizes = tuple(int(v) for v in os.environ["OMPI_AMD_BENCH_SWEEP"].split(","))
+    for nbytes in sizes:
         _progress(dist.get_rank(), f"sweep {nbytes} B")
         n = max(1, nbytes // 4)
         x = torch.ones(n, device="cuda")

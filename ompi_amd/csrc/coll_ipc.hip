@@ -79,14 +79,22 @@ namespace ompi_amd {
         if (rc_ != OMPI_AMD_SUCCESS) return rc_; \
     } while (0)
 
+// Largest allocation the library exports or maps: on ROCm 7.2
+// hipIpcOpenMemHandle of a 2 GiB + 2 MiB allocation never returned (four
+// ranks on one MI355X, OMPI_AMD_TRACE=1); 1 GiB opened in < 1 ms.
+constexpr size_t kMaxIpcBytes = (2ull << 30) - (4u << 20);
+
 // ---------------------------------------------------------------- barrier
 // A rank that fails a call its peers may already have launched (a deferred
 // nonblocking call whose IPC open was refused) raises every peer's abort
 // word, so their waits give up within ~1 ms instead of timing out.
-__global__ void abort_kernel(flag_set peers, int rank, int size) {
+__global__ void abort_kernel(flag_set peers, uint64_t *local, int rank, int size) {
     const int t = threadIdx.x;
     if (t < size && t != rank)
         __hip_atomic_store(peers.p[t] + kAbortWord, (uint64_t)1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t == rank)
+        __hip_atomic_store(local + kAbortWord, (uint64_t)1, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
     sys_release();
 }
@@ -271,6 +279,7 @@ struct shadow_set {
     cp_jobs in{};          // user -> shadow, before the collective
     cp_job out{};          // shadow -> user rbuf, after its trailing barrier
     char *mem = nullptr;   // owned shadow memory (nonblocking / persistent calls)
+    char *mem2 = nullptr;  //   its result region when input + result exceed one allocation
 };
 
 // A nonblocking collective posted but not launched yet.  Device work must
@@ -306,6 +315,7 @@ struct ompi_amd_request {
     bool recorded = false;  // `ev` recorded after them (lazily, at the first test / wait)
     int rc = OMPI_AMD_SUCCESS;
     char *shadow = nullptr;  // export-fallback memory of the call, freed with the request
+    char *shadow2 = nullptr; //   and its separate result region, if any
 };
 
 // ------------------------------------------------------------------ comm
@@ -342,6 +352,8 @@ struct ompi_amd_comm {
     std::vector<hipEvent_t> stream_evs;
     char *shadow = nullptr;               // export fallback of blocking calls (shadow_set)
     size_t shadow_bytes = 0;
+    char *shadow2 = nullptr;              //   its result region when both exceed one allocation
+    size_t shadow2_bytes = 0;
     // Shadow arena: every shadow (blocking, nonblocking, persistent) is a
     // range of a chunk that is exported once and freed only with the
     // communicator, so peers map each chunk once and no exported address is
@@ -477,6 +489,31 @@ static bool ipc_trace() {
     return on;
 }
 
+// OMPI_AMD_TRACE=1: one stderr line before and after each host step that
+// can block (allocations, exports, opens, rendezvous, stream drains), with
+// its duration — a stuck rank names the step it sits in.
+static bool host_trace() {
+    static const bool on = [] {
+        const char *v = getenv("OMPI_AMD_TRACE");
+        return v && *v == '1';
+    }();
+    return on;
+}
+
+struct host_step {
+    const char *what;
+    size_t arg;
+    std::chrono::steady_clock::time_point t0;
+    host_step(const char *w, size_t a = 0) : what(w), arg(a), t0(std::chrono::steady_clock::now()) {
+        if (host_trace()) fprintf(stderr, "[trace pid %d] %s %zu ...\n", (int)getpid(), what, arg);
+    }
+    ~host_step() {
+        if (!host_trace()) return;
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        fprintf(stderr, "[trace pid %d] %s %zu done %.3f ms\n", (int)getpid(), what, arg, ms);
+    }
+};
+
 static void trace_handle(const char *what, const hipIpcMemHandle_t &h, const char *fmt, ...) {
     if (!ipc_trace()) return;
     char head[256];
@@ -512,7 +549,10 @@ static int export_alloc(void *base, size_t size, unsigned long long id, hipIpcMe
             *h = r.h;
             return r.recycled ? 1 : 0;
         }
-    *e = hipIpcGetMemHandle(h, base);
+    {
+        host_step st("hipIpcGetMemHandle", size);
+        *e = hipIpcGetMemHandle(h, base);
+    }
     if (*e != hipSuccess) {
         (void)hipGetLastError();
         return -1;
@@ -554,6 +594,12 @@ static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d, bool *ip
     d->id = id;
     d->base = (uint64_t)(uintptr_t)base;
     d->size = (uint64_t)size;
+    if (size > kMaxIpcBytes) {  // peers could not open it: the shadow path
+        if (ipc_failed) *ipc_failed = true;
+        record_msg("allocation %p + %zu exceeds the %zu-byte IPC mapping limit", base, size,
+                   kMaxIpcBytes);
+        return OMPI_AMD_ERR_HIP;
+    }
     hipIpcMemHandle_t h;
     bool fresh = false;
     const int rc = export_alloc(base, size, id, &h, &e, &fresh);
@@ -691,7 +737,11 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
     // mappings, open again.
     for (int attempt = 0;; ++attempt) {
         ++c->imports_new;
-        hipError_t e = hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess);
+        hipError_t e;
+        {
+            host_step st("hipIpcOpenMemHandle", (size_t)d.size);
+            e = hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess);
+        }
         const char *what = nullptr;
         if (e == hipSuccess) {
             trace_handle("open", d.h, "peer %d id %llu %p+%llu -> %p", peer, (unsigned long long)d.id,
@@ -810,6 +860,7 @@ static int exchange_bufs(ompi_amd_comm_t *c, const void *sbuf, const void *rbuf,
     if (c->pre) {  // a deferred nonblocking call: swapped when it was posted
         memcpy(all, c->pre, sizeof(call_blob) * (size_t)c->size);
     } else {
+        host_step st("exchange allgather");
         rc = c->boot.allgather(&mine, all, sizeof(call_blob));
         if (rc != OMPI_AMD_SUCCESS) return rc;
     }
@@ -908,6 +959,7 @@ static void note_stream(ompi_amd_comm_t *c, hipStream_t s) {
 // streams only: an application's unrelated work on the device is not
 // waited for, unlike hipDeviceSynchronize).
 static int quiesce(ompi_amd_comm_t *c) {
+    host_step st("quiesce");
     for (hipEvent_t e : c->stream_evs) {
         const hipError_t r = hipEventSynchronize(e);
         (void)hipEventDestroy(e);
@@ -947,7 +999,10 @@ static hipError_t alloc_exportable(size_t bytes, char **out, hipIpcMemHandle_t *
     for (int attempt = 0; attempt < 8; ++attempt) {
         void *p = nullptr;
         const size_t sz = bytes + (size_t)(serial++ % 512u) * 4096u;
-        e = uncached ? hipExtMallocWithFlags(&p, sz, hipDeviceMallocUncached) : hipMalloc(&p, sz);
+        {
+            host_step st("hipMalloc", sz);
+            e = uncached ? hipExtMallocWithFlags(&p, sz, hipDeviceMallocUncached) : hipMalloc(&p, sz);
+        }
         if (e != hipSuccess) break;
         void *base = nullptr;
         size_t range = 0;
@@ -994,7 +1049,12 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     if (need <= c->land_bytes) return OMPI_AMD_SUCCESS;
     constexpr size_t kStep = 32u << 20, kTag = 64;  // the last kTag bytes hold the token
     const size_t want = std::max((need + kTag + kStep - 1) / kStep * kStep,
-                                 c->land_bytes ? 2 * (c->land_bytes + kTag) : 0);
+                                 c->land_bytes ? std::min(2 * (c->land_bytes + kTag), kMaxIpcBytes) : 0);
+    if (want > kMaxIpcBytes) {  // every rank decides alike (same need)
+        record_msg("landing buffer of %zu bytes exceeds the %zu-byte IPC mapping limit", want,
+                   kMaxIpcBytes);
+        return OMPI_AMD_ERR_UNSUPPORTED;
+    }
     TRY(quiesce(c));
     TRY(c->boot.barrier());  // every rank's earlier kernels are done
     // the old mappings stay open until the new ones are (so the new ones
@@ -1151,10 +1211,12 @@ static int launch_copy(ompi_amd_comm_t *c, const cp_jobs &jobs, hipStream_t s) {
 }
 
 // ---- shadow arena ----
+
 // First fit over the chunks (256-B granules, never across a chunk: peers map
 // each chunk separately); a new chunk of max(need, 64 MiB, everything so
 // far) when none fits.
 static int arena_alloc(ompi_amd_comm_t *c, size_t need, char **out) {
+    host_step st("arena_alloc", need);
     const size_t n = (std::max<size_t>(need, 1) + 255) & ~(size_t)255;
     std::lock_guard<std::mutex> g(c->arena_mu);
     for (auto &ch : c->arena) {
@@ -1168,8 +1230,13 @@ static int arena_alloc(ompi_amd_comm_t *c, size_t need, char **out) {
             return OMPI_AMD_SUCCESS;
         }
     }
-    const size_t want = (std::max({n, (size_t)64 << 20, c->arena_bytes}) + (2u << 20) - 1) &
-                        ~(size_t)((2u << 20) - 1);
+    if (n > kMaxIpcBytes) {
+        record_msg("shadow of %zu bytes exceeds the %zu-byte IPC allocation limit", n, kMaxIpcBytes);
+        return OMPI_AMD_ERR_UNSUPPORTED;
+    }
+    const size_t want = std::min(kMaxIpcBytes,
+                                 (std::max({n, (size_t)64 << 20, c->arena_bytes}) + (2u << 20) - 1) &
+                                     ~(size_t)((2u << 20) - 1));
     char *mem = nullptr;
     hipIpcMemHandle_t h;
     const hipError_t e = alloc_exportable(want, &mem, &h);
@@ -1214,21 +1281,25 @@ static void arena_free(ompi_amd_comm_t *c, char *p) {
 }
 
 // ---- export fallback (shadow_set) ----
-static int shadow_reserve(ompi_amd_comm_t *c, size_t need, char **out) {
-    if (need <= c->shadow_bytes) {
-        *out = c->shadow;
+// k: the communicator's shadow k (0, and 1 for a result region that does
+// not fit beside the input in one IPC allocation).
+static int shadow_reserve(ompi_amd_comm_t *c, size_t need, char **out, int k = 0) {
+    char *&sh = k ? c->shadow2 : c->shadow;
+    size_t &bytes = k ? c->shadow2_bytes : c->shadow_bytes;
+    if (need <= bytes) {
+        *out = sh;
         return OMPI_AMD_SUCCESS;
     }
     // the old shadow's last readers are the peers of an earlier call, done
     // once this rank's stream passed that call's trailing barrier
     TRY(quiesce(c));
-    arena_free(c, c->shadow);
-    const size_t want = std::max(need, 2 * c->shadow_bytes);
-    c->shadow = nullptr;
-    c->shadow_bytes = 0;
-    TRY(arena_alloc(c, want, &c->shadow));
-    c->shadow_bytes = want;
-    *out = c->shadow;
+    arena_free(c, sh);
+    const size_t want = std::max(need, std::min(2 * bytes, kMaxIpcBytes));
+    sh = nullptr;
+    bytes = 0;
+    TRY(arena_alloc(c, want, &sh));
+    bytes = want;
+    *out = sh;
     return OMPI_AMD_SUCCESS;
 }
 
@@ -1276,20 +1347,29 @@ static int shadow_plan(ompi_amd_comm_t *c, const void **src, size_t sbytes, void
     const size_t so = fs ? ((uintptr_t)*src & 255) : 0;
     const size_t rbase = fs ? ((so + sbytes + 255) & ~(size_t)255) : 0;
     const size_t ro = fr ? rbase + ((uintptr_t)*rbuf & 255) : rbase;
-    const size_t need = (fr ? ro + rbytes : so + sbytes) + 256;
-    char *mem = nullptr;
+    size_t need = (fr ? ro + rbytes : so + sbytes) + 256;
+    // input and result in separate allocations when together they pass the
+    // IPC size limit (the result region then starts at offset 0 of its own)
+    const bool split2 = fs && fr && need > kMaxIpcBytes;
+    if (split2) need = so + sbytes + 256;
+    char *mem = nullptr, *mem2 = nullptr;
     if (owned) {
         TRY(arena_alloc(c, need, &mem));
         post->mem = mem;
+        if (split2) {
+            TRY(arena_alloc(c, ((uintptr_t)*rbuf & 255) + rbytes + 256, &mem2));
+            post->mem2 = mem2;
+        }
     } else {
         TRY(shadow_reserve(c, need, &mem));
+        if (split2) TRY(shadow_reserve(c, ((uintptr_t)*rbuf & 255) + rbytes + 256, &mem2, 1));
     }
     if (fs) {
         post->in.j[post->in.n++] = {(const char *)*src, mem + so, (int64_t)sbytes};
         *src = mem + so;
     }
     if (fr) {
-        char *r = mem + ro;
+        char *r = split2 ? mem2 + ((uintptr_t)*rbuf & 255) : mem + ro;
         if (rbuf_in) post->in.j[post->in.n++] = {(const char *)*rbuf, r, (int64_t)rbytes};
         post->out = {r, (char *)*rbuf, (int64_t)rbytes};
         *rbuf = r;
@@ -1847,7 +1927,8 @@ static void abort_peers(ompi_amd_comm_t *c, int rc) {
         (void)hipGetLastError();
         return;
     }
-    hipLaunchKernelGGL(abort_kernel, dim3(1), dim3(64), 0, s, c->peer_flags, c->rank, c->size);
+    hipLaunchKernelGGL(abort_kernel, dim3(1), dim3(64), 0, s, c->peer_flags, c->flags, c->rank,
+                       c->size);
     if (hipGetLastError() == hipSuccess) (void)hipStreamSynchronize(s);
     (void)hipGetLastError();
     (void)hipStreamDestroy(s);
@@ -2328,6 +2409,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
             if (!push) o.sbuf = xs;
             o.rbuf = xr;
             req->shadow = o.sh.mem;
+            req->shadow2 = o.sh.mem2;
         }
         call_blob mine{};
         if (rc == OMPI_AMD_SUCCESS && !push) rc = export_buf(c, o.sbuf, &mine.s);
@@ -2336,6 +2418,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
         if (rc != OMPI_AMD_SUCCESS) {
             (void)hipEventDestroy(req->ev);
             arena_free(c, req->shadow);
+        arena_free(c, req->shadow2);
             delete req;
             return rc;
         }
@@ -2380,6 +2463,7 @@ static int nb_post(ompi_amd_comm_t *c, pending_op &o, const void **exp, size_t b
         if (rc == OMPI_AMD_SUCCESS) rc = shadow_plan(c, exp, bytes, &none, 0, false, true, &o.sh);
         c->force_shadow = saved;
         req->shadow = o.sh.mem;
+            req->shadow2 = o.sh.mem2;
         call_blob mine{};
         if (rc == OMPI_AMD_SUCCESS) rc = export_buf(c, *exp, &mine.s);
         if (rc == OMPI_AMD_SUCCESS) rc = c->boot.post(&mine, sizeof(mine), &o.ticket);
@@ -2387,6 +2471,7 @@ static int nb_post(ompi_amd_comm_t *c, pending_op &o, const void **exp, size_t b
     if (rc != OMPI_AMD_SUCCESS) {
         (void)hipEventDestroy(req->ev);
         arena_free(c, req->shadow);
+        arena_free(c, req->shadow2);
         delete req;
         return rc;
     }
@@ -2875,9 +2960,10 @@ int ompi_amd_plan_free(ompi_amd_plan_t *pl) {
         for (int p = 0; p < OMPI_AMD_MAX_RANKS; ++p)
             for (int k = 0; k < 2; ++k)
                 if (pl->bases[p][k]) unpin_import(pl->c, pl->bases[p][k]);
-    if (pl->sh.mem) {  // the plan's last start must be over before its shadow goes
+    if (pl->sh.mem || pl->sh.mem2) {  // the plan's last start must be over before its shadow goes
         if (pl->started && pl->done) (void)ompi_amd_plan_wait(pl);
         arena_free(pl->c, pl->sh.mem);
+        arena_free(pl->c, pl->sh.mem2);
     }
     if (pl->done) (void)hipEventDestroy(pl->done);
     delete pl;
@@ -2926,6 +3012,7 @@ int ompi_amd_request_free(ompi_amd_request_t *r) {
     if (r->ev) (void)hipEventDestroy(r->ev);
     // the call's trailing barrier has passed: no peer reads the shadow any more
     arena_free(r->c, r->shadow);
+    arena_free(r->c, r->shadow2);
     delete r;
     return rc;
 }

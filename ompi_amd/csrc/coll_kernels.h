@@ -67,23 +67,24 @@ __device__ __forceinline__ void acquire_once() {
 }
 
 // Wait until *flag >= epoch (a peer's barrier store).  Bounded: past
-// `ticks` (s_memrealtime, 100 MHz) the communicator's sticky error word is
-// set; and every ~1 ms of waiting the word is read, so once any wait of this
-// communicator has given up, every later one gives up within 1 ms.  A rank
-// whose peer failed a call before launching it (e.g. an IPC open refused in
-// a deferred nonblocking call) thus drains its queued collectives in one
-// timeout instead of one per barrier, and reaches the host rendezvous of
-// comm_destroy while that peer is still there to keep its memory alive.
+// `ticks` (s_memrealtime, 100 MHz) the communicator's sticky error word (host
+// memory, written only — a spinning wave never reads host memory) is set and
+// the communicator's abort word (in its own flag page, device memory) is
+// raised.  Every ~1 ms of waiting the abort word is read, so once any wait
+// of this communicator has given up — or a failing peer raised the word
+// (abort_peers) — every later wait gives up within 1 ms: a rank whose peer
+// failed a call it had already launched drains its queued collectives in one
+// timeout instead of one per barrier, and reaches comm_destroy's host
+// rendezvous while that peer is still there to keep its memory alive.
 // Returns false when the wait gave up.
-// The flag page: 32 rows x 16 ranks of epochs (4 KiB), then the abort word a
-// failing peer sets (abort_peers) — read by the same ~1 ms check.
+// The flag page: 32 rows x 16 ranks of epochs (4 KiB), then the abort word.
 constexpr int kAbortWord = 512;               // uint64 index in the flag page
 constexpr size_t kFlagPageBytes = 8192;
 
 // seen (debug, OMPI_AMD_DEBUG_PROGRESS=1; else null): the flag value read
 // at every ~1 ms check, in host-mapped memory a watchdog can print.
 __device__ __forceinline__ bool wait_epoch(const uint64_t *flag, uint64_t epoch, int *err,
-                                           uint64_t ticks, const uint64_t *abort_word,
+                                           uint64_t ticks, uint64_t *abort_word,
                                            uint64_t *seen = nullptr) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t check = t0 + 100000;  // 1 ms
@@ -93,14 +94,13 @@ __device__ __forceinline__ bool wait_epoch(const uint64_t *flag, uint64_t epoch,
         if (now - t0 > ticks) {
             __hip_atomic_store(err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(abort_word, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             return false;
         }
         if (now >= check) {
             if (seen)
                 __hip_atomic_store(seen, __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)
-                return false;
             if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
                 __hip_atomic_store(err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
