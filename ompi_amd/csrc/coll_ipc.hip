@@ -721,7 +721,7 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
             if (jt->pins == 0 && (it == c->imports.end() || jt->last_use < it->last_use)) it = jt;
         if (it != c->imports.end()) {
             TRY(quiesce(c));  // an earlier call's kernel may still read it
-            (void)hipIpcCloseMemHandle(it->base);
+            hip_ignore(hipIpcCloseMemHandle(it->base));
             c->imports.erase(it);
         }
     }
@@ -801,7 +801,7 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
             if (it->peer == peer && it->pins == 0) {
                 closed_base = closed_base || ((const char *)base >= (const char *)it->base &&
                                               (const char *)base < (const char *)it->base + it->rsize);
-                (void)hipIpcCloseMemHandle(it->base);
+                hip_ignore(hipIpcCloseMemHandle(it->base));
                 it = c->imports.erase(it);
             } else {
                 ++it;
@@ -811,7 +811,7 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
         // second reference to it (a refcounting runtime): drop that too;
         // never close into a mapping still in use (another peer's, the
         // communicator's own pages)
-        if (what && closed_base) (void)hipIpcCloseMemHandle(base);
+        if (what && closed_base) hip_ignore(hipIpcCloseMemHandle(base));
         (void)hipGetLastError();
         base = nullptr;
     }
@@ -920,7 +920,7 @@ static int import_all(ompi_amd_comm_t *c, const call_blob *all, const void *sbuf
             if (p == c->rank || done[p]) continue;
             for (auto it = c->imports.begin(); it != c->imports.end();) {
                 if (it->peer == p && it->pins == 0) {
-                    (void)hipIpcCloseMemHandle(it->base);
+                    hip_ignore(hipIpcCloseMemHandle(it->base));
                     it = c->imports.erase(it);
                 } else {
                     ++it;
@@ -938,12 +938,12 @@ static void note_stream(ompi_amd_comm_t *c, hipStream_t s) {
         hipEvent_t e = nullptr;
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) {
             if (hipEventRecord(e, c->cur_stream) == hipSuccess) c->stream_evs.push_back(e);
-            else (void)hipEventDestroy(e);
+            else hip_ignore(hipEventDestroy(e));
         }
         // forget marks that have fired
         for (auto it = c->stream_evs.begin(); c->stream_evs.size() > 8 && it != c->stream_evs.end();) {
             if (hipEventQuery(*it) == hipSuccess) {
-                (void)hipEventDestroy(*it);
+                hip_ignore(hipEventDestroy(*it));
                 it = c->stream_evs.erase(it);
             } else {
                 ++it;
@@ -962,7 +962,7 @@ static int quiesce(ompi_amd_comm_t *c) {
     host_step st("quiesce");
     for (hipEvent_t e : c->stream_evs) {
         const hipError_t r = hipEventSynchronize(e);
-        (void)hipEventDestroy(e);
+        hip_ignore(hipEventDestroy(e));
         if (r != hipSuccess) {
             c->stream_evs.clear();
             return record_hip(r, "hipEventSynchronize (communicator streams)");
@@ -1021,7 +1021,7 @@ static hipError_t alloc_exportable(size_t bytes, char **out, hipIpcMemHandle_t *
         (void)hipGetLastError();
         failed.push_back(p);  // keep it alive so the next try gets another range and handle
     }
-    for (void *p : failed) (void)hipFree(p);
+    for (void *p : failed) hip_ignore(hipFree(p));
     return e;
 }
 
@@ -1067,7 +1067,7 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     }
     auto close_old = [&] {
         for (int p = 0; p < kMaxRanks; ++p)
-            if (old_land[p]) (void)hipIpcCloseMemHandle(old_land[p]);
+            if (old_land[p]) hip_ignore(hipIpcCloseMemHandle(old_land[p]));
     };
     struct land_blob { buf_desc d; uint64_t token; int ok; };
     land_blob mine{}, all[kMaxRanks];
@@ -1096,12 +1096,12 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     if (e != hipSuccess && mine.d.valid) record_hip(e, "landing token write");
     mine.ok = e == hipSuccess;
     int rc = c->boot.allgather(&mine, all, sizeof(mine));  // also: nobody uses the old one now
-    if (c->land) (void)hipFree(c->land);  // peers' mappings keep it alive until they close them
+    if (c->land) hip_ignore(hipFree(c->land));  // peers' mappings keep it alive until they close them
     c->land = nullptr;
     c->land_bytes = 0;
     if (rc != OMPI_AMD_SUCCESS) {
         close_old();
-        if (fresh) (void)hipFree(fresh);
+        if (fresh) hip_ignore(hipFree(fresh));
         return rc;
     }
     int status = mine.ok ? 0 : 1;  // 0 ok, 1 local HIP failure, 2 token mismatch
@@ -1179,10 +1179,10 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     }
     (void)c->boot.barrier();  // nobody reads the new buffers any more
     for (int p = 0; p < kMaxRanks; ++p) {
-        if (c->land_opened[p]) (void)hipIpcCloseMemHandle(c->land_opened[p]);
+        if (c->land_opened[p]) hip_ignore(hipIpcCloseMemHandle(c->land_opened[p]));
         c->land_opened[p] = nullptr;
     }
-    if (fresh) (void)hipFree(fresh);
+    if (fresh) hip_ignore(hipFree(fresh));
     if (rc == OMPI_AMD_SUCCESS && status == 0)
         record_msg("landing buffer growth failed on another rank (%s)",
                    worst == 2 ? "stale IPC mapping" : "HIP error");
@@ -1454,9 +1454,9 @@ template <typename F>
 static int timed_phase(ompi_amd_comm_t *c, int phase, hipStream_t s, F &&launch) {
     if (!c->profile) return launch();
     hipEvent_t a = prof_event(c), b = prof_event(c);
-    if (a) (void)hipEventRecord(a, s);
+    if (a) hip_ignore(hipEventRecord(a, s));
     const int rc = launch();
-    if (b) (void)hipEventRecord(b, s);
+    if (b) hip_ignore(hipEventRecord(b, s));
     if (a && b) c->ev_phase[phase].emplace_back(a, b);
     return rc;
 }
@@ -1929,9 +1929,9 @@ static void abort_peers(ompi_amd_comm_t *c, int rc) {
     }
     hipLaunchKernelGGL(abort_kernel, dim3(1), dim3(64), 0, s, c->peer_flags, c->flags, c->rank,
                        c->size);
-    if (hipGetLastError() == hipSuccess) (void)hipStreamSynchronize(s);
+    if (hipGetLastError() == hipSuccess) hip_ignore(hipStreamSynchronize(s));
     (void)hipGetLastError();
-    (void)hipStreamDestroy(s);
+    hip_ignore(hipStreamDestroy(s));
 }
 
 // Launch deferred nonblocking calls in posting order, each once every rank
@@ -2149,31 +2149,31 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
 
 int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     if (!c) return OMPI_AMD_SUCCESS;
-    (void)hipSetDevice(c->device);
+    hip_ignore(hipSetDevice(c->device));
     (void)drain(c);  // deferred nonblocking calls every peer will also launch
     (void)quiesce(c);
     (void)c->boot.barrier();  // nobody still reads our memory
-    for (auto &x : c->imports) (void)hipIpcCloseMemHandle(x.base);
+    for (auto &x : c->imports) hip_ignore(hipIpcCloseMemHandle(x.base));
     for (int p = 0; p < kMaxRanks; ++p) {
         for (int k = 0; k < 2; ++k)
-            if (c->opened[p][k]) (void)hipIpcCloseMemHandle(c->opened[p][k]);
-        if (c->land_opened[p]) (void)hipIpcCloseMemHandle(c->land_opened[p]);
+            if (c->opened[p][k]) hip_ignore(hipIpcCloseMemHandle(c->opened[p][k]));
+        if (c->land_opened[p]) hip_ignore(hipIpcCloseMemHandle(c->land_opened[p]));
         c->land_opened[p] = nullptr;
     }
     (void)c->boot.barrier();
-    if (c->flags) (void)hipFree(c->flags);
-    if (c->scratch) (void)hipFree(c->scratch);
-    if (c->land) (void)hipFree(c->land);
-    for (auto &ch : c->arena) (void)hipFree(ch.base);  // shadows included
+    if (c->flags) hip_ignore(hipFree(c->flags));
+    if (c->scratch) hip_ignore(hipFree(c->scratch));
+    if (c->land) hip_ignore(hipFree(c->land));
+    for (auto &ch : c->arena) hip_ignore(hipFree(ch.base));  // shadows included
     c->arena.clear();
-    if (c->err_host) (void)hipHostFree(c->err_host);
-    if (c->dbg_host) (void)hipHostFree(c->dbg_host);
+    if (c->err_host) hip_ignore(hipHostFree(c->err_host));
+    if (c->dbg_host) hip_ignore(hipHostFree(c->dbg_host));
     for (int ph = 0; ph < 2; ++ph)
         for (auto &pr : c->ev_phase[ph]) {
-            (void)hipEventDestroy(pr.first);
-            (void)hipEventDestroy(pr.second);
+            hip_ignore(hipEventDestroy(pr.first));
+            hip_ignore(hipEventDestroy(pr.second));
         }
-    for (auto e : c->ev_free) (void)hipEventDestroy(e);
+    for (auto e : c->ev_free) hip_ignore(hipEventDestroy(e));
     if (c->p2p) p2p_destroy(c->p2p);
     c->boot.detach();
     delete c;
@@ -2375,7 +2375,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
         rc = drain(c);
         if (rc == OMPI_AMD_SUCCESS) rc = agree_root0_inplace(c, &pp, inplace);
         if (rc != OMPI_AMD_SUCCESS) {
-            (void)hipEventDestroy(req->ev);
+            hip_ignore(hipEventDestroy(req->ev));
             delete req;
             return rc;
         }
@@ -2416,7 +2416,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
         if (rc == OMPI_AMD_SUCCESS) rc = export_buf(c, o.rbuf, &mine.r);
         if (rc == OMPI_AMD_SUCCESS) rc = c->boot.post(&mine, sizeof(mine), &o.ticket);
         if (rc != OMPI_AMD_SUCCESS) {
-            (void)hipEventDestroy(req->ev);
+            hip_ignore(hipEventDestroy(req->ev));
             arena_free(c, req->shadow);
         arena_free(c, req->shadow2);
             delete req;
@@ -2469,7 +2469,7 @@ static int nb_post(ompi_amd_comm_t *c, pending_op &o, const void **exp, size_t b
         if (rc == OMPI_AMD_SUCCESS) rc = c->boot.post(&mine, sizeof(mine), &o.ticket);
     }
     if (rc != OMPI_AMD_SUCCESS) {
-        (void)hipEventDestroy(req->ev);
+        hip_ignore(hipEventDestroy(req->ev));
         arena_free(c, req->shadow);
         arena_free(c, req->shadow2);
         delete req;
@@ -2965,7 +2965,7 @@ int ompi_amd_plan_free(ompi_amd_plan_t *pl) {
         arena_free(pl->c, pl->sh.mem);
         arena_free(pl->c, pl->sh.mem2);
     }
-    if (pl->done) (void)hipEventDestroy(pl->done);
+    if (pl->done) hip_ignore(hipEventDestroy(pl->done));
     delete pl;
     return OMPI_AMD_SUCCESS;
 }
@@ -3009,7 +3009,7 @@ int ompi_amd_request_free(ompi_amd_request_t *r) {
     if (!r) return OMPI_AMD_SUCCESS;
     // the peers launch it whatever this rank does: launch and finish it too
     const int rc = ompi_amd_request_wait(r);
-    if (r->ev) (void)hipEventDestroy(r->ev);
+    if (r->ev) hip_ignore(hipEventDestroy(r->ev));
     // the call's trailing barrier has passed: no peer reads the shadow any more
     arena_free(r->c, r->shadow);
     arena_free(r->c, r->shadow2);

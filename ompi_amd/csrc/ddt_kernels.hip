@@ -795,8 +795,8 @@ static int iov_reserve(size_t n) {
         return record_hip(hipGetLastError(), "hipEventCreate (iov table)");
     if (n <= t.cap) return OMPI_AMD_SUCCESS;
     const size_t want = std::max<size_t>(n, 2 * t.cap);
-    if (t.host) (void)hipHostFree(t.host);
-    if (t.dev) (void)hipFree(t.dev);
+    if (t.host) hip_ignore(hipHostFree(t.host));
+    if (t.dev) hip_ignore(hipFree(t.dev));
     t.host = nullptr;
     t.dev = nullptr;
     t.cap = 0;
@@ -1004,8 +1004,8 @@ int ompi_amd_ddt_create_elems(const ompi_amd_ddt_elem_t *elems, int nelems, int6
     }
     if (err != hipSuccess) {
         int rc = record_hip(err, "ddt descriptor upload");
-        if (d->dev) (void)hipFree(d->dev);
-        if (d->dmap) (void)hipFree(d->dmap);
+        if (d->dev) hip_ignore(hipFree(d->dev));
+        if (d->dmap) hip_ignore(hipFree(d->dmap));
         delete d;
         return rc;
     }
@@ -1045,8 +1045,8 @@ int ompi_amd_ddt_create(const ompi_amd_ddt_block_t *blocks, int nblocks, int64_t
 
 int ompi_amd_ddt_destroy(ompi_amd_ddt_t *ddt) {
     if (!ddt) return OMPI_AMD_SUCCESS;
-    if (ddt->dev) (void)hipFree(ddt->dev);
-    if (ddt->dmap) (void)hipFree(ddt->dmap);
+    if (ddt->dev) hip_ignore(hipFree(ddt->dev));
+    if (ddt->dmap) hip_ignore(hipFree(ddt->dmap));
     delete ddt;
     return OMPI_AMD_SUCCESS;
 }

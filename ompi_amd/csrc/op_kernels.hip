@@ -231,7 +231,7 @@ static thread_local mixed_scratch tls_scratch;  // grown on demand; freed at reg
 static char *scratch_bytes(size_t bytes) {
     if (bytes <= tls_scratch.cap) return tls_scratch.p;
     const size_t want = std::max(bytes, 2 * tls_scratch.cap);
-    if (tls_scratch.p) (void)hipFree(tls_scratch.p);
+    if (tls_scratch.p) hip_ignore(hipFree(tls_scratch.p));
     tls_scratch = {};
     void *q = nullptr;
     if (hipMalloc(&q, want) != hipSuccess) {

@@ -539,9 +539,9 @@ static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit
     if (rc != OMPI_AMD_SUCCESS) {
         for (int p = 0; p < w->size; ++p) {
             if (w->pinned[p]) comm_unpin(c, w->pinned[p]);
-            if (w->ctl_opened[p]) (void)hipIpcCloseMemHandle(w->ctl_opened[p]);
+            if (w->ctl_opened[p]) hip_ignore(hipIpcCloseMemHandle(w->ctl_opened[p]));
         }
-        if (w->ctl) (void)hipFree(w->ctl);
+        if (w->ctl) hip_ignore(hipFree(w->ctl));
         delete w;
         return rc;
     }
@@ -579,7 +579,7 @@ int ompi_amd_win_allocate(ompi_amd_comm_t *c, size_t bytes, int disp_unit, void 
     // a local failure still joins the rendezvous (as a zero-byte window) so
     // that no peer waits; the collective result reports it
     if (rc != OMPI_AMD_SUCCESS) {
-        if (m) (void)hipFree(m);
+        if (m) hip_ignore(hipFree(m));
         ompi_amd_win_t *w = nullptr;
         if (win_setup(c, nullptr, 0, disp_unit, false, &w) == OMPI_AMD_SUCCESS)
             (void)ompi_amd_win_free(w);
@@ -587,7 +587,7 @@ int ompi_amd_win_allocate(ompi_amd_comm_t *c, size_t bytes, int disp_unit, void 
     }
     rc = win_setup(c, m, bytes, disp_unit, true, out);
     if (rc != OMPI_AMD_SUCCESS) {
-        if (m) (void)hipFree(m);
+        if (m) hip_ignore(hipFree(m));
         return rc;
     }
     *base = m;
@@ -597,7 +597,7 @@ int ompi_amd_win_allocate(ompi_amd_comm_t *c, size_t bytes, int disp_unit, void 
 int ompi_amd_win_free(ompi_amd_win_t *w) {
     if (!w) return OMPI_AMD_SUCCESS;
     ompi_amd_comm_t *c = w->c;
-    (void)hipSetDevice(comm_device(c));
+    hip_ignore(hipSetDevice(comm_device(c)));
     int rc = comm_drain(c);
     const int src = record_hip(hipDeviceSynchronize(), "hipDeviceSynchronize (win_free)");
     if (rc == OMPI_AMD_SUCCESS) rc = src;
@@ -605,12 +605,12 @@ int ompi_amd_win_free(ompi_amd_win_t *w) {
     if (rc == OMPI_AMD_SUCCESS) rc = brc;
     for (int p = 0; p < w->size; ++p) {
         if (w->pinned[p]) comm_unpin(c, w->pinned[p]);
-        if (w->ctl_opened[p]) (void)hipIpcCloseMemHandle(w->ctl_opened[p]);
+        if (w->ctl_opened[p]) hip_ignore(hipIpcCloseMemHandle(w->ctl_opened[p]));
     }
     const int brc2 = comm_allgather(c, nullptr, nullptr, 0);  // mappings closed before frees
     if (rc == OMPI_AMD_SUCCESS) rc = brc2;
-    if (w->ctl) (void)hipFree(w->ctl);
-    if (w->owns_base && w->base) (void)hipFree(w->base);
+    if (w->ctl) hip_ignore(hipFree(w->ctl));
+    if (w->owns_base && w->base) hip_ignore(hipFree(w->base));
     if (rc == OMPI_AMD_SUCCESS) rc = comm_sticky(c);
     delete w;
     return rc;

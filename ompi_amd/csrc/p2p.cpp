@@ -174,7 +174,7 @@ void p2p_unlink(p2p_state *p) {
 void p2p_destroy(p2p_state *p) {
     if (!p) return;
     if (p->q) munmap(p->q, p->bytes);
-    if (p->eager) (void)hipFree(p->eager);
+    if (p->eager) hip_ignore(hipFree(p->eager));
     if (p->rank == 0) p2p_unlink(p);
     delete p;
 }
@@ -471,7 +471,7 @@ int ompi_amd_p2p_free(ompi_amd_p2p_request_t *r) {
         if (!r->done) cancel_recv(r);
     }
     if (!r->done) return rc;  // a matched copy or a send the mailbox still references: keep it
-    if (r->ev) (void)hipEventDestroy(r->ev);
+    if (r->ev) hip_ignore(hipEventDestroy(r->ev));
     delete r;
     return rc;
 }

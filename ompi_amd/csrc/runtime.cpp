@@ -12,6 +12,7 @@ static thread_local hipStream_t tls_stream = nullptr;
 
 int record_hip(hipError_t e, const char *what) {
     if (e == hipSuccess) return OMPI_AMD_SUCCESS;
+    (void)hipGetLastError();  // reported through the status: not left for the application's checks
     snprintf(tls_err, sizeof(tls_err), "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
     return OMPI_AMD_ERR_HIP;
 }

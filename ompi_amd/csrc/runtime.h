@@ -11,6 +11,10 @@ namespace ompi_amd {
 int record_hip(hipError_t e, const char *what);
 // Record a non-HIP failure message.
 void record_msg(const char *fmt, ...);
+// A HIP call whose failure is tolerated: also clear the thread's last-error
+// slot, so that the application's next error check (torch reads
+// hipGetLastError after its own launches) does not inherit it.
+inline void hip_ignore(hipError_t) { (void)hipGetLastError(); }
 
 // The stream handlers of this thread run on (ompi_amd_set_thread_stream).
 hipStream_t thread_stream();
