@@ -1793,6 +1793,61 @@ static int allreduce_push(ompi_amd_comm_t *c, const void *src, const ptr_set &rp
     return launch_barrier(c, s);
 }
 
+// The push scheme with a gather instead of remote result stores: nothing
+// of the caller's is exported (the default, user_ipc = 0).  Scatter: block b
+// of my input into slot [me] of its owner's landing buffer (remote stores,
+// library memory).  Barrier.  The owner folds its block from its own input
+// and its landing slots (local reads) into its rbuf and into its landing
+// result slot [n].  Barrier.  Every rank pulls the other blocks from their
+// owners' result slots into its rbuf.  Barrier.  Same xGMI bytes as the
+// zero-copy pull ((N-1)/N·S out, (N-1)/N·S in), no staging copy.
+static int allreduce_push_gather(ompi_amd_comm_t *c, const void *src, void *rbuf, int64_t count,
+                                 int op, int type, const fold_plan &fp, hipStream_t s) {
+    const int n = c->size, mine = (c->rank + 1) % n;
+    const int64_t ext = (int64_t)ompi_amd_type_extent(type);
+    int64_t split, early, late;
+    blockcount(count, n, &split, &early, &late);
+    const size_t slot = push_slot(count, n, type);
+    TRY(ensure_landing(c, slot * (size_t)(n + 1)));
+    cp_jobs cj{};
+    for (int b = 0; b < n; ++b) {
+        if (b == mine) continue;
+        const int owner = (b + n - 1) % n;
+        const int64_t off = block_off(b, split, early, late) * ext;
+        char *dst = const_cast<char *>(c->peer_land.p[owner]) + (size_t)c->rank * slot + (off & 15);
+        cj.j[cj.n++] = {(const char *)src + off, dst, block_cnt(b, split, early, late) * ext};
+    }
+    // the owner's reads of its slots and the peers' reads of its result slot
+    // from the previous landing call ended before that call's trailing
+    // barrier, so the scatter needs no leading one
+    TRY(timed_phase(c, 1, s, [&] { return launch_copy(c, cj, s); }));
+    TRY(launch_barrier(c, s));
+    const int64_t offm = block_off(mine, split, early, late) * ext;
+    ptr_set srcs{};
+    for (int r = 0; r < n; ++r)
+        srcs.p[r] = (r == c->rank) ? (const char *)src
+                                   : c->land + (size_t)r * slot + (offm & 15) - offm;
+    red_jobs jobs;
+    fold_jobs(fp, count, n, mine, &jobs);
+    ptr_set dsts{};
+    dsts.p[0] = (const char *)rbuf;
+    dsts.p[1] = c->land + (size_t)n * slot + (offm & 15) - offm;
+    TRY(timed_phase(c, 0, s, [&] {
+        return launch_reduce(c, op, type, srcs, n, dsts, 2, fp.order, fp.flags, jobs, s);
+    }));
+    TRY(launch_barrier(c, s));
+    cj = cp_jobs{};
+    for (int b = 0; b < n; ++b) {
+        if (b == mine) continue;
+        const int owner = (b + n - 1) % n;
+        const int64_t off = block_off(b, split, early, late) * ext;
+        const char *res = c->peer_land.p[owner] + (size_t)n * slot + (off & 15);
+        cj.j[cj.n++] = {res, (char *)rbuf + off, block_cnt(b, split, early, late) * ext};
+    }
+    TRY(launch_copy(c, cj, s));
+    return launch_barrier(c, s);
+}
+
 // reduce_scatter_block / reduce_scatter: my block [off, off + cnt) of the
 // full vector folded from every rank's input into rbuf[0, cnt).
 // Staged: inputs in the scratch halves.  Zero-copy: peers' inputs read in
@@ -2019,6 +2074,8 @@ static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size
         return launch_reduce(c, op, type, sh.peers, n, one_ptr(rbuf), 1, fp.order, fp.flags, jobs, s);
     }
     ptr_set sp{}, rp{};
+    if (!c->pre && pp.algorithm == ALG_PUSH && !c->user_ipc && !c->force_shadow)
+        return allreduce_push_gather(c, src, rbuf, (int64_t)count, op, type, fp, s);
     if (!c->pre && pp.algorithm == ALG_PULL && !c->user_ipc && !c->force_shadow) {
         // staged pull: the input into this rank's shadow (rbuf's phase mod
         // 256, so results and shadows line up for 16-B vectors), swap
