@@ -72,12 +72,15 @@ int ompi_amd_comm_size(const ompi_amd_comm_t *comm);
  *   "timeout_ms"    device spin limit per barrier (default 30000)
  *   "blocks"        grid cap of the transfer kernels (default 1024)
  *   "algorithm"     data movement of zero-copy allreduces (all ranks alike):
- *                   0 pull (default: reduce own block from peers' sbufs,
- *                   then pull the other blocks), 1 pull+push (reduce own
- *                   block and store it into every rbuf in the same pass),
- *                   2 push (scatter blocks into the owners' landing
- *                   buffers, owners reduce locally and store into every
- *                   rbuf).  Env OMPI_AMD_COLL_ALGORITHM sets the default.
+ *                   0 pull (reduce own block from peers' inputs, then pull
+ *                   the other blocks), 1 pull+push (reduce own block and
+ *                   store it into every rbuf in the same pass), 2 push
+ *                   (default: scatter blocks into the owners' landing
+ *                   buffers, owners reduce locally; with user_ipc 0 the
+ *                   results are gathered from the owners' landing result
+ *                   slots — no staging copy, nothing of the caller's
+ *                   exported — with user_ipc 1 stored into every rbuf).
+ *                   Env OMPI_AMD_COLL_ALGORITHM sets the default.
  *   "profile"       1: bracket the allreduce's reduce and gather kernels with
  *                   HIP events (read with ompi_amd_comm_phase_ms)
  *   "force_shadow"  1: zero-copy calls treat every user buffer as one the

@@ -387,7 +387,7 @@ struct ompi_amd_comm {
     int zero_copy = 1;
     int64_t timeout_ms = 30000;
     int max_blocks = 1024;
-    int algorithm = 0;
+    int algorithm = 2;                    // push: push-gather in the staged mode (no staging copy)
     int tuned_alg = 0;                    // coll_tuned_allreduce_algorithm (forced), 0 = fixed
     // IPC caches
     struct imp_entry {

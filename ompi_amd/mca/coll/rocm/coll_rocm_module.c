@@ -68,7 +68,7 @@ mca_coll_rocm_component_t mca_coll_rocm_component = {
     .small_bytes = 1 << 20,
     .zero_copy = 1,
     .timeout_ms = 30000,
-    .algorithm = 0,
+    .algorithm = 2,
     .user_ipc = 0,
     .residency = ROCM_RES_AUTO,
     .residency_lock = 8,
@@ -98,7 +98,8 @@ static int rocm_register(void)
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_coll_rocm_component.timeout_ms);
     (void) mca_base_component_var_register(c, "allreduce_algorithm",
-                                           "Large-message allreduce data movement: 0 pull, 1 pull+push, 2 push",
+                                           "Large-message allreduce data movement: 0 pull, 1 pull+push, 2 push (default; push-gather "
+                                           "through the landing buffers when user_ipc is 0)",
                                            MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_coll_rocm_component.algorithm);

@@ -393,7 +393,7 @@ def case_headline(comm, rank, n, count, salt, algorithm):
     try:
         comm.allreduce(s, out, count, F, mop.MPI_SUM, blocking=True)
     finally:
-        comm.set_param("algorithm", 0)
+        comm.set_param("algorithm", DEFAULT_ALG[0])
     exp = np.zeros(count, dtype=np.int32)
     for r in range(n):
         exp += headline_input(r, count, salt)
@@ -567,6 +567,9 @@ def case_pipelined(comm, rank, n, salt):
     return True, ""
 
 
+DEFAULT_ALG = [0]  # the communicator's "algorithm" at creation (set in main)
+
+
 def report(rank, n, obj):
     """One JSON line per case on stdout (read by the test) and, when
     COLL_LOG_DIR is set, appended to a per-rank file there (progress that a
@@ -591,6 +594,7 @@ def main():
     dist.init_process_group("gloo", rank=rank, world_size=n)
     comm = coll.Communicator.from_torch_distributed(device=device)
     comm.set_param("timeout_ms", 20000)
+    DEFAULT_ALG[0] = comm.get_param("algorithm")
     if os.environ.get("OMPI_AMD_TEST_FORCE_SHADOW") == "1":  # every zero-copy call through shadows
         comm.set_param("force_shadow", 1)
     big = int(os.environ.get("COLL_BIG", 1 << 22))
@@ -604,7 +608,7 @@ def main():
                 return fn()
             finally:
                 comm.set_param("user_ipc", 0)
-                comm.set_param("algorithm", 0)
+                comm.set_param("algorithm", DEFAULT_ALG[0])
         return run
     cases = [
         # user_ipc first, before any allocation churn
@@ -710,14 +714,15 @@ def main():
          lambda: case_persistent(comm, rank, n, F, mop.MPI_MAX, big, 83, inplace=True)),
     ]
     # zero-copy allreduce under the two push schemes (param "algorithm")
-    for alg in (1, 2):
+    # the schemes other than the library default (which every unscoped case runs)
+    for alg in [a for a in (0, 1, 2) if a != DEFAULT_ALG[0]]:
         def with_alg(fn, a=alg):
             def run():
                 comm.set_param("algorithm", a)
                 try:
                     return fn()
                 finally:
-                    comm.set_param("algorithm", 0)
+                    comm.set_param("algorithm", DEFAULT_ALG[0])
             return run
         cases += [
             (f"alg{alg}_ar_sum_f32_big",
