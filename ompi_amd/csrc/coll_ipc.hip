@@ -265,6 +265,7 @@ struct path_params {
     int zero_copy, algorithm;
     int tuned_alg;      // coll_tuned_allreduce_algorithm the user forced (0: fixed decision)
     int root0_inplace;  // forced nonoverlapping only: rank 0 passed MPI_IN_PLACE
+    int push_gather;    // push scheme, staged (user_ipc 0): no handle swap at all
 };
 
 // Export fallback.  hipIpcGetMemHandle sometimes refuses a live device
@@ -1931,7 +1932,8 @@ static int scan_common(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
 }  // namespace ompi_amd
 
 static path_params params_of(const ompi_amd_comm_t *c) {
-    return {c->small_bytes, c->fused_bytes, c->zero_copy, c->algorithm, c->tuned_alg, 0};
+    return {c->small_bytes, c->fused_bytes, c->zero_copy, c->algorithm, c->tuned_alg, 0,
+            c->algorithm == ALG_PUSH && !c->user_ipc && !c->force_shadow ? 1 : 0};
 }
 
 // Whether an allreduce of `count` elements takes a zero-copy path (and so
@@ -1947,6 +1949,14 @@ static bool allreduce_swaps(const ompi_amd_comm_t *c, const path_params &pp, siz
     if ((tree || fp.order == ORDER_RING) && bytes <= pp.fused_bytes && bytes <= c->scratch_bytes)
         return false;
     return !(bytes <= pp.small_bytes || !pp.zero_copy || (tree && bytes <= c->scratch_bytes));
+}
+
+// A zero-copy-size allreduce that runs push-gather: no handle swap (so a
+// nonblocking or persistent one needs no host rendezvous), only a landing
+// buffer of n + 1 slots, grown beforehand (growth is collective).
+static bool allreduce_push_gathers(const ompi_amd_comm_t *c, const path_params &pp, size_t count,
+                                   int type) {
+    return pp.push_gather && allreduce_swaps(c, pp, count, type);
 }
 
 static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
@@ -2074,7 +2084,7 @@ static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size
         return launch_reduce(c, op, type, sh.peers, n, one_ptr(rbuf), 1, fp.order, fp.flags, jobs, s);
     }
     ptr_set sp{}, rp{};
-    if (!c->pre && pp.algorithm == ALG_PUSH && !c->user_ipc && !c->force_shadow)
+    if (!c->pre && pp.push_gather)
         return allreduce_push_gather(c, src, rbuf, (int64_t)count, op, type, fp, s);
     if (!c->pre && pp.algorithm == ALG_PULL && !c->user_ipc && !c->force_shadow) {
         // staged pull: the input into this rank's shadow (rbuf's phase mod
@@ -2438,7 +2448,20 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
         }
     }
     pending_op o{0, inplace ? rbuf : sbuf, rbuf, count, type, op, as_stream(stream), pp, req};
-    if (allreduce_swaps(c, pp, count, type)) {
+    if (allreduce_push_gathers(c, pp, count, type)) {
+        // no swap: only the landing buffer must be big enough before the
+        // launch (growing is collective and blocking: every rank here alike)
+        const size_t need = push_slot((int64_t)count, c->size, type) * (size_t)(c->size + 1);
+        if (need > c->land_bytes) {
+            rc = drain(c);
+            if (rc == OMPI_AMD_SUCCESS) rc = ensure_landing(c, need);
+            if (rc != OMPI_AMD_SUCCESS) {
+                hip_ignore(hipEventDestroy(req->ev));
+                delete req;
+                return rc;
+            }
+        }
+    } else if (allreduce_swaps(c, pp, count, type)) {
         // post this rank's half of the handle swap now; the launch waits for
         // the peers' halves (progress / the next collective call)
         const bool push = pp.algorithm == ALG_PUSH;
@@ -2916,6 +2939,8 @@ int ompi_amd_allreduce_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, si
         return rc;
     }
     const bool small = n == 1 || count == 0 || !allreduce_swaps(c, pl->pp, count, type);
+    if (rc == OMPI_AMD_SUCCESS && allreduce_push_gathers(c, pl->pp, count, type))  // kind 0: re-run
+        rc = ensure_landing(c, push_slot((int64_t)count, n, type) * (size_t)(n + 1));
     pl->fp = allreduce_fold(n, pl->pp.tuned_alg, count, type, pl->pp.root0_inplace != 0);
     if (!small) {
         pl->kind = c->algorithm == ALG_PUSH ? 3 : c->algorithm == ALG_PULL_PUSH ? 2 : 1;
