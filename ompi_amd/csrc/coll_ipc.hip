@@ -1856,9 +1856,12 @@ static int allreduce_push_gather(ompi_amd_comm_t *c, const void *src, void *rbuf
 // peer may still read its own block there), so every rank learns the
 // in-place flags with the handle swap and in-place ranks fold into their
 // landing buffer and copy after the trailing barrier.
+// rcounts: every rank's block length (reduce_scatter), or null for equal
+// blocks of cnt (reduce_scatter_block).
 static int reduce_my_block(ompi_amd_comm_t *c, const void *src, void *rbuf, size_t total_bytes,
                            int64_t off, int64_t cnt, int64_t max_cnt, int op, int type,
-                           red_order ro, bool inplace, hipStream_t s) {
+                           red_order ro, bool inplace, hipStream_t s,
+                           const size_t *rcounts = nullptr) {
     red_jobs jobs;
     jobs.n = 1;
     jobs.j[0] = {off, cnt, 0, ro.first, -1};
@@ -1868,6 +1871,47 @@ static int reduce_my_block(ompi_amd_comm_t *c, const void *src, void *rbuf, size
         stage_half sh;
         TRY(stage_in(c, src, total_bytes, &sh, s));
         return launch_reduce(c, op, type, sh.peers, n, one_ptr(rbuf), 1, ro.order, ro.flags, jobs, s);
+    }
+    if (!c->pre && !c->user_ipc && !c->force_shadow) {
+        // Staged push (nothing of the caller's exported, no staging copy):
+        // block b of my input into slot [me] of rank b's landing buffer
+        // (at its own phase mod 16), barrier, fold my block from my input
+        // and my landing slots, barrier (peers then may reuse the slots).
+        // In place, the result goes through landing slot [n] (it may
+        // overlap my own block of the input, reduce_scatter's uneven counts).
+        const size_t slot = ((size_t)max_cnt * ext + 16 + 255) & ~(size_t)255;
+        TRY(ensure_landing(c, slot * (size_t)(n + 1)));
+        cp_jobs cj{};
+        int64_t ob = 0;
+        for (int b = 0; b < n; ++b) {
+            const int64_t cb = rcounts ? (int64_t)rcounts[b] : cnt;
+            if (b != c->rank && cb > 0) {
+                const int64_t bytes_off = ob * (int64_t)ext;
+                char *dst = const_cast<char *>(c->peer_land.p[b]) + (size_t)c->rank * slot + (bytes_off & 15);
+                cj.j[cj.n++] = {(const char *)src + bytes_off, dst, cb * (int64_t)ext};
+            }
+            ob += cb;
+        }
+        // the previous landing call's trailing barrier ended every reader of
+        // these slots: no leading barrier
+        TRY(launch_copy(c, cj, s));
+        TRY(launch_barrier(c, s));
+        const int64_t offb = off * (int64_t)ext;
+        ptr_set srcs{};
+        for (int r = 0; r < n; ++r)
+            srcs.p[r] = (r == c->rank) ? (const char *)src
+                                       : c->land + (size_t)r * slot + (offb & 15) - offb;
+        char *res = inplace ? c->land + (size_t)n * slot + (offb & 15) : (char *)rbuf;
+        jobs.j[0].off_dst = 0;
+        if (cnt > 0)
+            TRY(launch_reduce(c, op, type, srcs, n, one_ptr(res), 1, ro.order, ro.flags, jobs, s));
+        if (inplace && cnt > 0) {
+            cj = cp_jobs{};
+            cj.n = 1;
+            cj.j[0] = {res, (char *)rbuf, cnt * (int64_t)ext};
+            TRY(launch_copy(c, cj, s));
+        }
+        return launch_barrier(c, s);
     }
     ptr_set sp{}, rp{};
     uint64_t fl[kMaxRanks] = {};
@@ -2750,7 +2794,7 @@ int ompi_amd_reduce_scatter(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
     }
     const red_order ro = tuned_reduce_scatter_order(n, total * type_size(type), c->rank);
     return reduce_my_block(c, src, rbuf, total * ext, (int64_t)off, (int64_t)rcounts[c->rank],
-                           (int64_t)maxc, op, type, ro, inplace, s);
+                           (int64_t)maxc, op, type, ro, inplace, s, rcounts);
 }
 
 int ompi_amd_scan(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
