@@ -621,6 +621,11 @@ def main():
         ("user_ipc_rsb_allgather", user_ipc(lambda: (lambda a, b: (a[0] and b[0], a[1] + b[1]))(
             case_rsb(comm, rank, n, DI, mop.MPI_MAXLOC, big // 8, 163),
             case_allgather(comm, rank, n, (big * 4) // n + 12, 164)))),
+        # VERDICT r1 item 1 under user_ipc: every rank frees its buffers
+        # (hipFree through empty_cache) and reallocates them between calls
+        ("user_ipc_free_realloc", user_ipc(lambda: case_free_realloc(comm, rank, n, big + 11, 165))),
+        ("user_ipc_free_realloc_push", user_ipc(lambda: case_free_realloc(comm, rank, n, big + 13, 166),
+                                                2)),
         ("ar_sum_f32_1", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, 1, 1)),
         ("ar_sum_f32_7", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, 7, 2)),
         ("ar_sum_f32_2499_tree", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, 2499, 3)),
