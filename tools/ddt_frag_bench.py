@@ -57,7 +57,8 @@ def main():
         base = packed.data_ptr()
         iovs = (_lib.Iovec * nfrag)(*[_lib.Iovec(base + k * FRAG, FRAG) for k in range(nfrag)])
         for kind in ("pack", "unpack"):
-            for mode in ("per_call", "per_call_async", "iov_batch"):
+            modes = os.environ.get("FRAG_MODES", "per_call,per_call_async,iov_batch").split(",")
+            for mode in modes:
                 def run():
                     cv = dd.Convertor()
                     (cv.prepare_for_send if kind == "pack" else cv.prepare_for_recv)(
