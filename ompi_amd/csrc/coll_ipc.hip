@@ -2696,6 +2696,53 @@ int ompi_amd_reduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t cou
         jobs.j[0] = {0, (int64_t)count, 0, ro.first, -1};
         return launch_reduce(c, op, type, sh.peers, n, one_ptr(rbuf), 1, ro.order, ro.flags, jobs, s);
     }
+    int64_t split, early, late;
+    blockcount((int64_t)count, n, &split, &early, &late);
+    if (!c->user_ipc && !c->force_shadow) {
+        // Staged push (nothing of the caller's exported, no staging copy on
+        // the non-roots): block b of my input into slot [me] of rank b's
+        // landing buffer, barrier, rank b folds block b locally and stores
+        // it into the root's landing result area, barrier, the root copies
+        // the result into rbuf, barrier (the next landing call's scatter
+        // may land where this result area was).
+        const int64_t ext = (int64_t)ompi_amd_type_extent(type);
+        const size_t slot = ((size_t)early * (size_t)ext + 16 + 255) & ~(size_t)255;
+        const size_t res_off = slot * (size_t)n;
+        TRY(ensure_landing(c, res_off + ((bytes + 255) & ~(size_t)255)));
+        cp_jobs cj{};
+        for (int b = 0; b < n; ++b) {
+            const int64_t off = block_off(b, split, early, late) * ext, cb = block_cnt(b, split, early, late);
+            if (b == c->rank || cb == 0) continue;
+            char *dst = const_cast<char *>(c->peer_land.p[b]) + (size_t)c->rank * slot + (off & 15);
+            cj.j[cj.n++] = {(const char *)src + off, dst, cb * ext};
+        }
+        TRY(launch_copy(c, cj, s));
+        TRY(launch_barrier(c, s));
+        const int64_t offm = block_off(c->rank, split, early, late) * ext;
+        ptr_set srcs{};
+        for (int r = 0; r < n; ++r)
+            srcs.p[r] = (r == c->rank) ? (const char *)src
+                                       : c->land + (size_t)r * slot + (offm & 15) - offm;
+        jobs.n = 1;
+        jobs.j[0].off = block_off(c->rank, split, early, late);
+        jobs.j[0].cnt = block_cnt(c->rank, split, early, late);
+        jobs.j[0].off_dst = jobs.j[0].off;
+        jobs.j[0].first = ro.first;
+        jobs.j[0].head = -1;
+        const char *res = c->peer_land.p[root] + res_off;  // my own landing when I am the root
+        if (jobs.j[0].cnt > 0)
+            TRY(timed_phase(c, 0, s, [&] {
+                return launch_reduce(c, op, type, srcs, n, one_ptr(res), 1, ro.order, ro.flags, jobs, s);
+            }));
+        TRY(launch_barrier(c, s));
+        if (c->rank == root) {
+            cj = cp_jobs{};
+            cj.n = 1;
+            cj.j[0] = {c->land + res_off, (char *)rbuf, (int64_t)bytes};
+            TRY(launch_copy(c, cj, s));
+        }
+        return launch_barrier(c, s);
+    }
     // zero-copy: every rank folds one block of the vector from every
     // rank's sbuf and stores it straight into the root's rbuf
     ptr_set sp{}, rp{};
@@ -2705,8 +2752,6 @@ int ompi_amd_reduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t cou
     TRY(shadow_in(c, sh, s));
     TRY(exchange_bufs(c, src, xr, &sp, &rp));
     TRY(launch_barrier(c, s));
-    int64_t split, early, late;
-    blockcount((int64_t)count, n, &split, &early, &late);
     jobs.n = 1;
     jobs.j[0].off = block_off(c->rank, split, early, late);
     jobs.j[0].cnt = block_cnt(c->rank, split, early, late);
