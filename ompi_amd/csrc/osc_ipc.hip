@@ -35,6 +35,7 @@
 #include <cstring>
 #include <new>
 #include <utility>
+#include <vector>
 
 #include "../../include/ompi_amd_osc.h"
 #include "comm_internal.h"
@@ -358,6 +359,7 @@ struct ompi_amd_win {
     int64_t peer_disp[kOscMaxRanks] = {};
     void *pinned[kOscMaxRanks] = {};
     void *ctl_opened[kOscMaxRanks] = {};
+    std::vector<hipStream_t> streams;  // every stream an epoch or RMA call ran on (win_free waits)
     int held[kOscMaxRanks] = {};  // outstanding passive lock per target (0 none)
 };
 
@@ -447,6 +449,14 @@ static int launch_acc(ompi_amd_win_t *w, int op, int type, const void *origin, v
         if (rc_ != OMPI_AMD_SUCCESS) return rc_; \
     } while (0)
 
+// The stream of a window call, remembered so that win_free waits for this
+// window's work only (not for every stream of the device).
+static hipStream_t win_stream(ompi_amd_win_t *w, void *stream) {
+    const hipStream_t s = as_stream(stream);
+    if (std::find(w->streams.begin(), w->streams.end(), s) == w->streams.end()) w->streams.push_back(s);
+    return s;
+}
+
 // accumulate / get_accumulate / fetch_and_op under the accumulate lock
 // (osc_sm_comm.c:296-305, :340-356, :424-438).
 static int rma_op(ompi_amd_win_t *w, const void *origin, void *result, size_t count, int type,
@@ -463,7 +473,7 @@ static int rma_op(ompi_amd_win_t *w, const void *origin, void *result, size_t co
     const size_t bytes = count * ompi_amd_type_extent(type);
     char *t = nullptr;
     OSC_TRY(target_ptr(w, target, disp, bytes, &t));
-    hipStream_t s = as_stream(stream);
+    hipStream_t s = win_stream(w, stream);
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
     OSC_TRY(launch_lock(w, target, 0, s));
     const uint32_t *gate = taken_word(w, target, true);
@@ -599,8 +609,10 @@ int ompi_amd_win_free(ompi_amd_win_t *w) {
     ompi_amd_comm_t *c = w->c;
     hip_ignore(hipSetDevice(comm_device(c)));
     int rc = comm_drain(c);
-    const int src = record_hip(hipDeviceSynchronize(), "hipDeviceSynchronize (win_free)");
-    if (rc == OMPI_AMD_SUCCESS) rc = src;
+    for (hipStream_t s : w->streams) {  // this window's epochs and RMA kernels
+        const int src = record_hip(hipStreamSynchronize(s), "hipStreamSynchronize (win_free)");
+        if (rc == OMPI_AMD_SUCCESS) rc = src;
+    }
     const int brc = comm_allgather(c, nullptr, nullptr, 0);  // nobody still touches the windows
     if (rc == OMPI_AMD_SUCCESS) rc = brc;
     for (int p = 0; p < w->size; ++p) {
@@ -619,7 +631,7 @@ int ompi_amd_win_free(ompi_amd_win_t *w) {
 int ompi_amd_win_fence(ompi_amd_win_t *w, int assert_, void *stream) {
     if (!w) return OMPI_AMD_ERR_BAD_PARAM;
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
-    return comm_barrier(w->c, as_stream(stream));
+    return comm_barrier(w->c, win_stream(w, stream));
 }
 
 int ompi_amd_win_lock(ompi_amd_win_t *w, int lock_type, int target, int assert_, void *stream) {
@@ -636,7 +648,7 @@ int ompi_amd_win_lock(ompi_amd_win_t *w, int lock_type, int target, int assert_,
         return OMPI_AMD_SUCCESS;
     }
     const bool excl = lock_type == OMPI_AMD_LOCK_EXCLUSIVE;
-    OSC_TRY(launch_lock(w, target, excl ? 2 : 4, as_stream(stream)));
+    OSC_TRY(launch_lock(w, target, excl ? 2 : 4, win_stream(w, stream)));
     w->held[target] = excl ? HELD_EXCLUSIVE : HELD_SHARED;
     return OMPI_AMD_SUCCESS;
 }
@@ -650,8 +662,8 @@ int ompi_amd_win_unlock(ompi_amd_win_t *w, int target, void *stream) {
     }
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
     int rc = OMPI_AMD_SUCCESS;
-    if (h == HELD_EXCLUSIVE) rc = launch_lock(w, target, 3, as_stream(stream));
-    else if (h == HELD_SHARED) rc = launch_lock(w, target, 5, as_stream(stream));
+    if (h == HELD_EXCLUSIVE) rc = launch_lock(w, target, 3, win_stream(w, stream));
+    else if (h == HELD_SHARED) rc = launch_lock(w, target, 5, win_stream(w, stream));
     w->held[target] = HELD_NONE;
     return rc;
 }
@@ -672,7 +684,7 @@ int ompi_amd_win_unlock_all(ompi_amd_win_t *w, void *stream) {
 int ompi_amd_win_flush(ompi_amd_win_t *w, int target, void *stream) {
     if (!w) return OMPI_AMD_ERR_BAD_PARAM;
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
-    OSC_TRY(record_hip(hipStreamSynchronize(as_stream(stream)), "hipStreamSynchronize (flush)"));
+    OSC_TRY(record_hip(hipStreamSynchronize(win_stream(w, stream)), "hipStreamSynchronize (flush)"));
     return comm_sticky(w->c);
 }
 
@@ -683,7 +695,7 @@ int ompi_amd_put(ompi_amd_win_t *w, const void *origin, size_t bytes, int target
     OSC_TRY(target_ptr(w, target, disp, bytes, &t));
     if (!bytes) return OMPI_AMD_SUCCESS;
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
-    return xfer_copy(origin, t, bytes, as_stream(stream), epoch_gate(w, target));
+    return xfer_copy(origin, t, bytes, win_stream(w, stream), epoch_gate(w, target));
 }
 
 int ompi_amd_get(ompi_amd_win_t *w, void *origin, size_t bytes, int target, size_t disp,
@@ -693,7 +705,7 @@ int ompi_amd_get(ompi_amd_win_t *w, void *origin, size_t bytes, int target, size
     OSC_TRY(target_ptr(w, target, disp, bytes, &t));
     if (!bytes) return OMPI_AMD_SUCCESS;
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
-    return xfer_copy(t, origin, bytes, as_stream(stream), epoch_gate(w, target));
+    return xfer_copy(t, origin, bytes, win_stream(w, stream), epoch_gate(w, target));
 }
 
 int ompi_amd_accumulate(ompi_amd_win_t *w, const void *origin, size_t count, int type, int target,
@@ -723,7 +735,7 @@ int ompi_amd_compare_and_swap(ompi_amd_win_t *w, const void *origin, const void 
     const size_t size = ompi_amd_type_extent(type);  // no gaps in these types
     char *t = nullptr;
     OSC_TRY(target_ptr(w, target, disp, size, &t));
-    hipStream_t s = as_stream(stream);
+    hipStream_t s = win_stream(w, stream);
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
     OSC_TRY(launch_lock(w, target, 0, s));
     hipLaunchKernelGGL(cas_kernel, dim3(1), dim3(64), 0, s,
