@@ -299,6 +299,7 @@ struct pending_op {
     shadow_set sh;  // export fallback of this call (sbuf / rbuf above are then the shadows)
     int kind = 0;   // PEND_*: which collective
     int root = 0;   // bcast
+    bool inplace = false;  // rsb without a swap (staged push): MPI_IN_PLACE
 };
 
 enum { PEND_ALLREDUCE = 0, PEND_RSB = 1, PEND_ALLGATHER = 2, PEND_BCAST = 3 };
@@ -2064,7 +2065,7 @@ static int progress(ompi_amd_comm_t *c, bool block, int max_launch = -1) {
             if (rc == OMPI_AMD_SUCCESS) {
                 switch (o.kind) {
                 case PEND_RSB:
-                    rc = rsb_impl(c, o.sbuf, o.rbuf, o.count, o.type, o.op, false, o.stream);
+                    rc = rsb_impl(c, o.sbuf, o.rbuf, o.count, o.type, o.op, o.inplace, o.stream);
                     break;
                 case PEND_ALLGATHER:
                     rc = allgather_impl(c, o.sbuf, o.rbuf, o.count, o.stream);
@@ -2619,9 +2620,27 @@ int ompi_amd_ireduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *r
     const size_t total = rcount * (size_t)c->size * ompi_amd_type_extent(type);
     pending_op o{0, inplace ? rbuf : sbuf, rbuf, rcount, type, op, as_stream(stream), params_of(c), req};
     o.kind = PEND_RSB;
+    const bool swap = nb_swaps(c, total);
+    if (swap && !c->user_ipc && !c->force_shadow) {
+        // staged push (reduce_my_block): no swap, so no host rendezvous at
+        // launch; only the landing buffer must be big enough beforehand
+        // (its growth is collective: every rank posts this call alike)
+        const size_t slot = (rcount * ompi_amd_type_extent(type) + 16 + 255) & ~(size_t)255;
+        int rc = OMPI_AMD_SUCCESS;
+        if (slot * (size_t)(c->size + 1) > c->land_bytes) {
+            rc = drain(c);
+            if (rc == OMPI_AMD_SUCCESS) rc = ensure_landing(c, slot * (size_t)(c->size + 1));
+        }
+        if (rc != OMPI_AMD_SUCCESS) {
+            hip_ignore(hipEventDestroy(req->ev));
+            delete req;
+            return rc;
+        }
+        o.inplace = inplace;
+        return nb_post(c, o, nullptr, 0, false, out);
+    }
     // in place at a zero-copy size: peers read this rank's input from an
     // owned shadow, so the result can go straight into rbuf (no landing)
-    const bool swap = nb_swaps(c, total);
     return nb_post(c, o, swap ? &o.sbuf : nullptr, total, inplace, out);
 }
 
