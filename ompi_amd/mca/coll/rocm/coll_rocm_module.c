@@ -478,11 +478,20 @@ static int rocm_dev_finish(mca_coll_rocm_module_t *m, const rocm_operand_t *o, i
 
 /* ------------------------------------------------------------- collectives */
 
-static int reduction_ok(struct ompi_datatype_t *dtype, struct ompi_op_t *op)
+/* The device path moves at most this many bytes of vector per call: every
+ * peer-visible region is one IPC allocation, capped below 2 GiB on ROCm 7.2
+ * (DESIGN.md §4.6), and the push schemes need (N + 1) / N of the vector in
+ * one landing buffer.  Larger reductions go to the saved functions (count,
+ * datatype and op agree on every rank, so every rank decides alike). */
+#define ROCM_MAX_DEVICE_BYTES ((size_t) 1 << 30)
+
+static int reduction_ok_n(struct ompi_datatype_t *dtype, struct ompi_op_t *op, size_t elems)
 {
     const int t = type_code(dtype);
-    return t >= 0 && ompi_op_is_intrinsic(op) && ompi_amd_op_supported(op->o_f_to_c_index, t);
+    return t >= 0 && ompi_op_is_intrinsic(op) && ompi_amd_op_supported(op->o_f_to_c_index, t) &&
+           elems * ompi_amd_type_extent(t) <= ROCM_MAX_DEVICE_BYTES;
 }
+
 
 int mca_coll_rocm_allreduce(const void *sbuf, void *rbuf, int count,
                             struct ompi_datatype_t *dtype, struct ompi_op_t *op,
@@ -493,7 +502,7 @@ int mca_coll_rocm_allreduce(const void *sbuf, void *rbuf, int count,
     rocm_operand_t o[2] = {{(void *) sbuf, (size_t) count, dtype, 1, 0},
                            {rbuf, (size_t) count, dtype, inplace, 1}};
     int path, rc;
-    rc = rocm_begin(m, reduction_ok(dtype, op), dev(sbuf) && dev(rbuf), o, 2, &path);
+    rc = rocm_begin(m, reduction_ok_n(dtype, op, (size_t) count), dev(sbuf) && dev(rbuf), o, 2, &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
         rc = m->c_coll.coll_allreduce(o[0].use, o[1].use, count, dtype, op, comm,
@@ -516,7 +525,7 @@ int mca_coll_rocm_reduce(const void *sbuf, void *rbuf, int count, struct ompi_da
     rocm_operand_t o[2] = {{(void *) sbuf, (size_t) count, dtype, 1, 0},
                            {is_root ? rbuf : NULL, (size_t) count, dtype, MPI_IN_PLACE == sbuf, 1}};
     int path, rc;
-    rc = rocm_begin(m, reduction_ok(dtype, op),
+    rc = rocm_begin(m, reduction_ok_n(dtype, op, (size_t) count),
                     is_root ? dev(rbuf) && dev(sbuf) : ompi_amd_is_device_pointer(sbuf), o, 2, &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
@@ -537,7 +546,7 @@ static int rocm_scan_common(const void *sbuf, void *rbuf, int count,
     rocm_operand_t o[2] = {{(void *) sbuf, (size_t) count, dtype, 1, 0},
                            {rbuf, (size_t) count, dtype, MPI_IN_PLACE == sbuf, 1}};
     int path, rc;
-    rc = rocm_begin(m, reduction_ok(dtype, op), dev(sbuf) && dev(rbuf), o, 2, &path);
+    rc = rocm_begin(m, reduction_ok_n(dtype, op, (size_t) count), dev(sbuf) && dev(rbuf), o, 2, &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
         rc = exclusive ? m->c_coll.coll_exscan(o[0].use, o[1].use, count, dtype, op, comm,
@@ -579,7 +588,7 @@ int mca_coll_rocm_reduce_scatter(const void *sbuf, void *rbuf, const int *rcount
         rocm_operand_t o[2] = {{(void *) sbuf, total, dtype, 1, 0},
                                {rbuf, inplace ? total : (size_t) rcounts[ompi_comm_rank(comm)],
                                 dtype, inplace, 1}};
-        rc = rocm_begin(m, reduction_ok(dtype, op), dev(sbuf) && dev(rbuf), o, 2, &path);
+        rc = rocm_begin(m, reduction_ok_n(dtype, op, total), dev(sbuf) && dev(rbuf), o, 2, &path);
         if (OMPI_SUCCESS != rc) return rc;
         if (ROCM_DEVICE != path) {
             rc = m->c_coll.coll_reduce_scatter(o[0].use, o[1].use, rcounts, dtype, op, comm,
@@ -604,7 +613,7 @@ int mca_coll_rocm_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount,
     rocm_operand_t o[2] = {{(void *) sbuf, all, dtype, 1, 0},
                            {rbuf, inplace ? all : (size_t) rcount, dtype, inplace, 1}};
     int path, rc;
-    rc = rocm_begin(m, reduction_ok(dtype, op), dev(sbuf) && dev(rbuf), o, 2, &path);
+    rc = rocm_begin(m, reduction_ok_n(dtype, op, all), dev(sbuf) && dev(rbuf), o, 2, &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
         rc = m->c_coll.coll_reduce_scatter_block(o[0].use, o[1].use, rcount, dtype, op, comm,
@@ -802,8 +811,7 @@ int mca_coll_rocm_iallreduce(const void *sbuf, void *rbuf, int count,
 {
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
     const int t = type_code(dtype);
-    const int ok = t >= 0 && ompi_op_is_intrinsic(op) &&
-                   ompi_amd_op_supported(op->o_f_to_c_index, t) && dev(sbuf) && dev(rbuf);
+    const int ok = reduction_ok_n(dtype, op, (size_t) count) && dev(sbuf) && dev(rbuf);
     mca_coll_rocm_request_t *r;
     ompi_amd_request_t *nb = NULL;
     int rc;
@@ -861,7 +869,8 @@ int mca_coll_rocm_ireduce_scatter_block(const void *sbuf, void *rbuf, int rcount
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
     ompi_amd_request_t *nb = NULL;
     int rc;
-    if (!take_device_path(m, reduction_ok(dtype, op) && dev(sbuf) && dev(rbuf))) {
+    if (!take_device_path(m, reduction_ok_n(dtype, op, (size_t) rcount * (size_t) ompi_comm_size(comm)) &&
+                                 dev(sbuf) && dev(rbuf))) {
         return m->c_coll.coll_ireduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, request,
                                                     m->c_coll.coll_ireduce_scatter_block_module);
     }
@@ -924,8 +933,7 @@ int mca_coll_rocm_allreduce_init(const void *sbuf, void *rbuf, int count,
 {
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
     const int t = type_code(dtype);
-    const int ok = t >= 0 && ompi_op_is_intrinsic(op) &&
-                   ompi_amd_op_supported(op->o_f_to_c_index, t) && dev(sbuf) && dev(rbuf);
+    const int ok = reduction_ok_n(dtype, op, (size_t) count) && dev(sbuf) && dev(rbuf);
     mca_coll_rocm_request_t *r;
     ompi_amd_plan_t *plan = NULL;
     int rc;
