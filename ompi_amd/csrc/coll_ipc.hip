@@ -3254,6 +3254,20 @@ int comm_import(ompi_amd_comm_t *c, int peer, const ipc_desc &d, const char **ou
 
 void comm_unpin(ompi_amd_comm_t *c, void *base) { unpin_import(c, base); }
 
+int comm_drop_peer_mappings(ompi_amd_comm_t *c, int peer) {
+    TRY(quiesce(c));
+    ++c->ipc_local_reopens;
+    for (auto it = c->imports.begin(); it != c->imports.end();) {
+        if (it->peer == peer && it->pins == 0) {
+            hip_ignore(hipIpcCloseMemHandle(it->base));
+            it = c->imports.erase(it);
+        } else {
+            ++it;
+        }
+    }
+    return OMPI_AMD_SUCCESS;
+}
+
 int comm_drain(ompi_amd_comm_t *c) { return drain(c); }
 
 int comm_barrier(ompi_amd_comm_t *c, hipStream_t s) {

@@ -44,6 +44,10 @@ int comm_export(ompi_amd_comm_t *c, const void *ptr, ipc_desc *d);
 int comm_import(ompi_amd_comm_t *c, int peer, const ipc_desc &d, const char **out, bool pin,
                 void **base);
 void comm_unpin(ompi_amd_comm_t *c, void *base);
+// After a refused IPC open of one of `peer`'s allocations: drain this
+// communicator's kernels and close every unpinned cached mapping of that
+// peer (the runtime then answers a fresh open).
+int comm_drop_peer_mappings(ompi_amd_comm_t *c, int peer);
 // Launch the deferred nonblocking collectives (device work keeps one order).
 int comm_drain(ompi_amd_comm_t *c);
 // Device barrier over every rank of c on stream s (stream-ordered epoch).

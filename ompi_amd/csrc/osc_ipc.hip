@@ -535,8 +535,14 @@ static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit
         }
         if (rc == OMPI_AMD_SUCCESS) {
             void *m = nullptr;
-            rc = record_hip(hipIpcOpenMemHandle(&m, all[p].ctl.h, hipIpcMemLazyEnablePeerAccess),
-                            "hipIpcOpenMemHandle (osc control)");
+            hipError_t e = hipIpcOpenMemHandle(&m, all[p].ctl.h, hipIpcMemLazyEnablePeerAccess);
+            if (e != hipSuccess) {  // once more after closing the peer's cached mappings
+                hip_ignore(e);
+                rc = comm_drop_peer_mappings(c, p);
+                if (rc == OMPI_AMD_SUCCESS)
+                    e = hipIpcOpenMemHandle(&m, all[p].ctl.h, hipIpcMemLazyEnablePeerAccess);
+            }
+            if (rc == OMPI_AMD_SUCCESS) rc = record_hip(e, "hipIpcOpenMemHandle (osc control)");
             w->ctl_opened[p] = m;
             w->peer_ctl[p] = static_cast<uint32_t *>(m);
         }

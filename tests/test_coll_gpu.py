@@ -27,7 +27,7 @@ def free_port():
         return s.getsockname()[1]
 
 
-def run_ranks(n, timeout=600, extra_env=None, worker=WORKER):
+def run_ranks(n, timeout=600, extra_env=None, worker=WORKER, tag="n"):
     ngpu = torch.cuda.device_count()
     if "GRAFT_REPO_ROOT" in os.environ and "COLL_LOG_DIR" not in os.environ:
         # on the gpurun box: per-rank progress files under gpurun_out/ (a hang
@@ -48,7 +48,7 @@ def run_ranks(n, timeout=600, extra_env=None, worker=WORKER):
         env.update(extra_env or {})
         # raw per-rank output (library diagnostics on stderr) goes straight to
         # a file, so that it survives a run killed at its time limit
-        path = os.path.join(logdir, f"raw_n{n}_rank{r}.txt") if logdir else None
+        path = os.path.join(logdir, f"raw_{tag}{n}_rank{r}.txt") if logdir else None
         f = open(path, "w+") if path else subprocess.PIPE
         files.append(f)
         procs.append(subprocess.Popen([sys.executable, worker], env=env, stdout=f,

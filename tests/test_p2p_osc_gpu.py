@@ -17,11 +17,13 @@ WORKER = os.path.join(ROOT, "tests", "p2p_osc_worker.py")
 
 @pytest.mark.parametrize("n", [2, 3, 4, 8])
 def test_p2p_osc_parity(n):
-    outs = run_ranks(n, timeout=300, worker=WORKER)
-    failures = []
+    outs = run_ranks(n, timeout=300, worker=WORKER, tag="p2p_osc_n")
+    failures, first = [], []
     for r, (rc, out) in enumerate(outs):
         lines = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
         bad = [ln for ln in lines if not ln["ok"]]
         if rc != 0 or bad or not lines:
             failures.append((r, rc, bad[:4], out[-2000:] if not lines or rc not in (0, 1) else ""))
-    assert not failures, failures
+            if bad:  # every failing rank's first message, short (the rank that failed first shows)
+                first.append(f"rank {r}: {bad[0]['case']}: {bad[0]['msg'][:300]}")
+    assert not failures, ("\n".join(first), failures)
