@@ -25,6 +25,12 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# Deployment requirement: the peers' IPC mappings need
+# the HSA runtime's dmabuf IPC mode.  Set before torch or the library touch
+# the GPU, unless the environment already chose (the library's load-time
+# constructor applies the same default to an mpirun job).
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 XGMI_LINK_GBS = 153.0          # per-link, R(N) = (N-1) x 153
 METRIC = "Allreduce busBW GB/s @256MiB fp32 SUM at 2/4/8 GPUs; MPI_Op HBM GB/s"
@@ -45,6 +51,25 @@ def parse():
     return p.parse_args()
 
 
+def host_cpu() -> dict:
+    """The host the CPU baseline ran on (BASELINE.md §5 asks for nproc and
+    the CPU model beside the core count used)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = None
+    return {"nproc": os.cpu_count(), "cpus_allowed": allowed, "cpu_model": model}
+
+
 def cpu_baseline_op(seconds: float) -> dict:
     """The oracle's op/base restatement (scalar C loop, 1 thread) on a
     bounded sample of the same workload: 3-buffer fp32 SUM, 64 MiB/buffer."""
@@ -63,7 +88,7 @@ def cpu_baseline_op(seconds: float) -> dict:
         total += orc.time_op_3buff(3, 15, a, b, out, n, 4)
         iters += 4
     gbs = 3.0 * n * 4 * iters / total / 1e9
-    return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+    return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port", **host_cpu(),
             "sample": f"oracle op/base restatement, 3-buffer fp32 SUM, 64 MiB/buffer, "
                       f"{iters} iterations in {total:.1f} s, 1 thread"}
 

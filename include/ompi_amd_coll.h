@@ -81,8 +81,8 @@ int ompi_amd_comm_size(const ompi_amd_comm_t *comm);
  *                   slots — no staging copy, nothing of the caller's
  *                   exported — with user_ipc 1 stored into every rbuf).
  *                   Env OMPI_AMD_COLL_ALGORITHM sets the default.
- *   "profile"       1: bracket the allreduce's reduce and gather kernels with
- *                   HIP events (read with ompi_amd_comm_phase_ms)
+ *   "profile"       1: bracket the allreduce's fold, gather and scatter
+ *                   kernels with HIP events (read with ompi_amd_comm_phase_ms)
  *   "force_shadow"  1: zero-copy calls treat every user buffer as one the
  *                   runtime refused to export and run through the export
  *                   fallback (a shadow copy of the communicator's own);
@@ -121,8 +121,9 @@ int ompi_amd_comm_vote(ompi_amd_comm_t *comm, int local_yes, int *n_yes);
 int ompi_amd_comm_sync(ompi_amd_comm_t *comm, void *stream);
 
 /* Kernel time of the profiled allreduce phases since the last read:
- * phase 0 = the fused peer-load reduction, 1 = the peer gather.  Waits for
- * the recorded events. */
+ * phase 0 = the reduction (fold), 1 = the peer gather of finished blocks,
+ * 2 = the scatter of input blocks into the owners' landing slots (push
+ * schemes).  Waits for the recorded events. */
 int ompi_amd_comm_phase_ms(ompi_amd_comm_t *comm, int phase, double *total_ms, int *calls);
 
 /* The ring block partition and ownership the allreduce uses (host-only,
@@ -166,6 +167,11 @@ int ompi_amd_plan_start(ompi_amd_plan_t *plan, void *stream);
 int ompi_amd_plan_test(ompi_amd_plan_t *plan, int *done);
 int ompi_amd_plan_wait(ompi_amd_plan_t *plan);
 int ompi_amd_plan_free(ompi_amd_plan_t *plan);
+/* Which path a plan's starts take (diagnostics / tests): 0 = the plain call
+ * re-run (fused / staged sizes, and the default push-gather scheme at any
+ * size: no handle swap), 1 pull, 2 pull+push, 3 push with the caller's
+ * buffers mapped (user_ipc); -1 for NULL. */
+int ompi_amd_plan_kind(const ompi_amd_plan_t *plan);
 /* Nonblocking allreduce (MPI_Iallreduce, coll.h:271-274; libnbc's
  * ompi_coll_libnbc_iallreduce in the reference).  Returns without waiting
  * for any peer: sizes without a handle swap (fused / staged paths) are

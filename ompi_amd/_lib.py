@@ -145,6 +145,7 @@ PROTOTYPES = [
     ("ompi_amd_plan_test", _C.c_int, [_C.c_void_p, _C.POINTER(_C.c_int)]),
     ("ompi_amd_plan_wait", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_plan_free", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_plan_kind", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_iallreduce", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p,
       _C.POINTER(_C.c_void_p)]),

@@ -241,6 +241,12 @@ class Plan:
     def wait(self) -> None:
         _lib.check(self._comm._lib.ompi_amd_plan_wait(self._h), "wait " + self._what)
 
+    @property
+    def kind(self) -> int:
+        """0 re-run of the plain call (fused / staged / push-gather), 1 pull,
+        2 pull+push, 3 push on the caller's mapped buffers."""
+        return self._comm._lib.ompi_amd_plan_kind(self._h)
+
     def free(self) -> None:
         if self._h:
             _lib.check(self._comm._lib.ompi_amd_plan_free(self._h), "plan_free")

@@ -406,7 +406,7 @@ struct ompi_amd_comm {
     // per-phase kernel timing (param "profile"): event pairs per call
     int profile = 0;
     std::vector<hipEvent_t> ev_free;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_phase[2];
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_phase[3];  // fold, gather, scatter
     // nonblocking calls not launched yet, and the swapped blobs of the one
     // being launched (exchange_bufs takes them instead of a rendezvous)
     std::deque<pending_op> pending;
@@ -1779,7 +1779,7 @@ static int allreduce_push(ompi_amd_comm_t *c, const void *src, const ptr_set &rp
     }
     // the owner's previous reads of its landing ended before the previous
     // push call's trailing barrier, so the scatter needs no leading one
-    TRY(timed_phase(c, 1, s, [&] { return launch_copy(c, cj, s); }));
+    TRY(timed_phase(c, 2, s, [&] { return launch_copy(c, cj, s); }));
     TRY(launch_barrier(c, s));
     const int64_t offm = block_off(mine, split, early, late) * ext;
     ptr_set srcs{};
@@ -1822,7 +1822,7 @@ static int allreduce_push_gather(ompi_amd_comm_t *c, const void *src, void *rbuf
     // the owner's reads of its slots and the peers' reads of its result slot
     // from the previous landing call ended before that call's trailing
     // barrier, so the scatter needs no leading one
-    TRY(timed_phase(c, 1, s, [&] { return launch_copy(c, cj, s); }));
+    TRY(timed_phase(c, 2, s, [&] { return launch_copy(c, cj, s); }));
     TRY(launch_barrier(c, s));
     const int64_t offm = block_off(mine, split, early, late) * ext;
     ptr_set srcs{};
@@ -1846,7 +1846,7 @@ static int allreduce_push_gather(ompi_amd_comm_t *c, const void *src, void *rbuf
         const char *res = c->peer_land.p[owner] + (size_t)n * slot + (off & 15);
         cj.j[cj.n++] = {res, (char *)rbuf + off, block_cnt(b, split, early, late) * ext};
     }
-    TRY(launch_copy(c, cj, s));
+    TRY(timed_phase(c, 1, s, [&] { return launch_copy(c, cj, s); }));
     return launch_barrier(c, s);
 }
 
@@ -2280,7 +2280,7 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     c->arena.clear();
     if (c->err_host) hip_ignore(hipHostFree(c->err_host));
     if (c->dbg_host) hip_ignore(hipHostFree(c->dbg_host));
-    for (int ph = 0; ph < 2; ++ph)
+    for (int ph = 0; ph < 3; ++ph)
         for (auto &pr : c->ev_phase[ph]) {
             hip_ignore(hipEventDestroy(pr.first));
             hip_ignore(hipEventDestroy(pr.second));
@@ -2316,7 +2316,7 @@ int ompi_amd_coll_reduce_order(int size, size_t msg_bytes, size_t count, int roo
 }
 
 int ompi_amd_comm_phase_ms(ompi_amd_comm_t *c, int phase, double *total_ms, int *calls) {
-    if (!c || phase < 0 || phase > 1 || !total_ms || !calls) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!c || phase < 0 || phase > 2 || !total_ms || !calls) return OMPI_AMD_ERR_BAD_PARAM;
     double tot = 0.0;
     int n = 0;
     for (auto &pr : c->ev_phase[phase]) {
@@ -2447,6 +2447,8 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "force_shadow")) *v = c->force_shadow;
     else if (!strcmp(key, "user_ipc")) *v = c->user_ipc;
     else if (!strcmp(key, "imports")) *v = (int64_t)c->imports.size();
+    else if (!strcmp(key, "ipc_mode_legacy_env")) *v = ipc_mode_env_at_load();
+    else if (!strcmp(key, "ipc_mode_legacy")) *v = *ipc_mode_env_now() ? atoi(ipc_mode_env_now()) : -1;
     else {
         record_msg("unknown coll param '%s'", key);
         return OMPI_AMD_ERR_BAD_PARAM;
@@ -3046,8 +3048,13 @@ int ompi_amd_allreduce_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, si
         delete pl;
         return rc;
     }
-    const bool small = n == 1 || count == 0 || !allreduce_swaps(c, pl->pp, count, type);
-    if (rc == OMPI_AMD_SUCCESS && allreduce_push_gathers(c, pl->pp, count, type))  // kind 0: re-run
+    // kind 0 (a start re-runs the plain call): the fused / staged sizes, and
+    // the push-gather scheme at any size — it swaps no handles (library
+    // landing buffers only), so a re-run has no host rendezvous once the
+    // landing buffer is sized here for its n + 1 slots
+    const bool push_gather = allreduce_push_gathers(c, pl->pp, count, type);
+    const bool small = n == 1 || count == 0 || !allreduce_swaps(c, pl->pp, count, type) || push_gather;
+    if (rc == OMPI_AMD_SUCCESS && push_gather)
         rc = ensure_landing(c, push_slot((int64_t)count, n, type) * (size_t)(n + 1));
     pl->fp = allreduce_fold(n, pl->pp.tuned_alg, count, type, pl->pp.root0_inplace != 0);
     if (!small) {
@@ -3105,6 +3112,8 @@ static int plan_enqueue(ompi_amd_plan_t *pl, void *stream) {
     TRY(rc);
     return shadow_out(c, pl->sh, s);
 }
+
+int ompi_amd_plan_kind(const ompi_amd_plan_t *pl) { return pl ? pl->kind : -1; }
 
 int ompi_amd_plan_start(ompi_amd_plan_t *pl, void *stream) {
     if (!pl || !pl->c) return OMPI_AMD_ERR_BAD_PARAM;

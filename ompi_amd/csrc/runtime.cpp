@@ -3,6 +3,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 namespace ompi_amd {
@@ -25,6 +26,30 @@ void record_msg(const char *fmt, ...) {
 }
 
 hipStream_t thread_stream() { return tls_stream ? tls_stream : hipStreamPerThread; }
+
+// Deployment requirement: peers map each other's memory
+// with hipIpcOpenMemHandle, which on this driver stack works only in the
+// dmabuf IPC mode (HSA_ENABLE_IPC_MODE_LEGACY=0; the legacy mode fails with
+// "hipIpcGetMemHandle: invalid argument").  The HSA runtime reads the
+// variable once, when it initialises, so the library sets it when it is
+// loaded unless the environment already says otherwise — before any HIP
+// call this library makes.  A process whose GPU was initialised before
+// the library was loaded keeps the mode it started with; the communicator
+// reports both (param "ipc_mode_legacy_env").
+static int g_ipc_env_at_load = -2;
+
+__attribute__((constructor)) static void ipc_mode_default() {
+    const char *v = getenv("HSA_ENABLE_IPC_MODE_LEGACY");
+    g_ipc_env_at_load = v ? atoi(v) : -1;
+    if (!v) setenv("HSA_ENABLE_IPC_MODE_LEGACY", "0", 0);
+}
+
+int ipc_mode_env_at_load() { return g_ipc_env_at_load; }
+
+const char *ipc_mode_env_now() {
+    const char *v = getenv("HSA_ENABLE_IPC_MODE_LEGACY");
+    return v ? v : "";
+}
 
 }  // namespace ompi_amd
 

@@ -11,10 +11,19 @@ namespace ompi_amd {
 int record_hip(hipError_t e, const char *what);
 // Record a non-HIP failure message.
 void record_msg(const char *fmt, ...);
-// A HIP call whose failure is tolerated: also clear the thread's last-error
-// slot, so that the application's next error check (torch reads
-// hipGetLastError after its own launches) does not inherit it.
-inline void hip_ignore(hipError_t) { (void)hipGetLastError(); }
+// A HIP call whose failure is tolerated: clear the thread's last-error slot
+// when (and only when) it failed, so that the application's next error check
+// (torch reads hipGetLastError after its own launches) does not inherit our
+// failure — and an error the application left pending is not wiped.
+inline void hip_ignore(hipError_t e) {
+    if (e != hipSuccess) (void)hipGetLastError();
+}
+
+// The HSA IPC mode this process runs under: HSA_ENABLE_IPC_MODE_LEGACY as
+// the library found it when it was loaded (-1: unset, then set to 0 by the
+// library's constructor, before any HIP call of its own).
+int ipc_mode_env_at_load();
+const char *ipc_mode_env_now();
 
 // The stream handlers of this thread run on (ompi_amd_set_thread_stream).
 hipStream_t thread_stream();

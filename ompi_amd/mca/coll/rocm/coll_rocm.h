@@ -65,6 +65,7 @@ typedef struct mca_coll_rocm_component_t {
     int residency;       /* coll_rocm_residency: 0 auto, 1 device, 2 host */
     int residency_lock;  /* coll_rocm_residency_lock: unanimous votes before locking (0 never) */
     int residency_recheck; /* coll_rocm_residency_recheck: locked calls per recheck vote (0 never) */
+    int max_device_mib;  /* coll_rocm_max_device_mib: larger calls go to the saved functions */
 } mca_coll_rocm_component_t;
 
 OMPI_MODULE_DECLSPEC extern mca_coll_rocm_component_t mca_coll_rocm_component;

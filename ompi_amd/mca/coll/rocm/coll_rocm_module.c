@@ -73,6 +73,7 @@ mca_coll_rocm_component_t mca_coll_rocm_component = {
     .residency = ROCM_RES_AUTO,
     .residency_lock = 8,
     .residency_recheck = 256,
+    .max_device_mib = 1024,
 };
 
 static int rocm_register(void)
@@ -127,6 +128,13 @@ static int rocm_register(void)
                                            MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_coll_rocm_component.residency_recheck);
+    (void) mca_base_component_var_register(c, "max_device_mib",
+                                           "Largest vector (reductions) or per-rank block (allgather, "
+                                           "bcast) the device path takes, in MiB; larger calls go to "
+                                           "the saved functions",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_coll_rocm_component.max_device_mib);
     return OMPI_SUCCESS;
 }
 
@@ -478,18 +486,24 @@ static int rocm_dev_finish(mca_coll_rocm_module_t *m, const rocm_operand_t *o, i
 
 /* ------------------------------------------------------------- collectives */
 
-/* The device path moves at most this many bytes of vector per call: every
- * peer-visible region is one IPC allocation, capped below 2 GiB on ROCm 7.2
- * (DESIGN.md §4.6), and the push schemes need (N + 1) / N of the vector in
- * one landing buffer.  Larger reductions go to the saved functions (count,
- * datatype and op agree on every rank, so every rank decides alike). */
-#define ROCM_MAX_DEVICE_BYTES ((size_t) 1 << 30)
+/* The device path moves at most coll_rocm_max_device_mib (1 GiB) of vector
+ * per call: every peer-visible region is one IPC allocation, capped below
+ * 2 GiB on ROCm 7.2, the push schemes need (N + 1) / N of
+ * the vector in one landing buffer, and allgather / bcast stage a rank's
+ * block (the root's whole buffer) in one shadow.  Larger calls go to the
+ * saved functions.  The sizes tested are ones every rank computes alike
+ * (a reduction's count, datatype and op; allgather's and bcast's type
+ * signatures must match, MPI-4.1 §6.4), so every rank decides alike. */
+static int bytes_ok(size_t bytes)
+{
+    return bytes <= ((size_t) mca_coll_rocm_component.max_device_mib << 20);
+}
 
 static int reduction_ok_n(struct ompi_datatype_t *dtype, struct ompi_op_t *op, size_t elems)
 {
     const int t = type_code(dtype);
     return t >= 0 && ompi_op_is_intrinsic(op) && ompi_amd_op_supported(op->o_f_to_c_index, t) &&
-           elems * ompi_amd_type_extent(t) <= ROCM_MAX_DEVICE_BYTES;
+           bytes_ok(elems * ompi_amd_type_extent(t));
 }
 
 
@@ -642,7 +656,7 @@ int mca_coll_rocm_allgather(const void *sbuf, int scount, struct ompi_datatype_t
     (void) ompi_datatype_type_size(rdtype, &rsize);
     ok = ompi_datatype_is_contiguous_memory_layout(rdtype, (int) all) && dev(rbuf) && dev(sbuf) &&
          (inplace || ompi_datatype_is_contiguous_memory_layout(sdtype, scount));
-    rc = rocm_begin(m, 1, ok, o, 2, &path);
+    rc = rocm_begin(m, bytes_ok(rsize * (size_t) rcount), ok, o, 2, &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
         rc = m->c_coll.coll_allgather(o[0].use, scount, sdtype, o[1].use, rcount, rdtype, comm,
@@ -663,8 +677,8 @@ int mca_coll_rocm_bcast(void *buf, int count, struct ompi_datatype_t *dtype, int
     size_t size = 0;
     int path, rc;
     (void) ompi_datatype_type_size(dtype, &size);
-    rc = rocm_begin(m, 1, ompi_datatype_is_contiguous_memory_layout(dtype, count) && dev(buf), o, 1,
-                    &path);
+    rc = rocm_begin(m, bytes_ok(size * (size_t) count),
+                    ompi_datatype_is_contiguous_memory_layout(dtype, count) && dev(buf), o, 1, &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
         rc = m->c_coll.coll_bcast(o[0].use, count, dtype, root, comm, m->c_coll.coll_bcast_module);
@@ -771,7 +785,9 @@ static int rocm_request_free(ompi_request_t **rptr)
 {
     mca_coll_rocm_request_t *r = (mca_coll_rocm_request_t *) *rptr;
     int rc = OMPI_AMD_SUCCESS;
-    if (NULL != r->next_active) rocm_unlink_active(r);
+    /* always: the oldest active request is the list's tail (next_active
+     * NULL) and must leave the list too (a no-op when it is not on it) */
+    rocm_unlink_active(r);
     if (NULL != r->plan) {
         rc = ompi_amd_plan_wait(r->plan);
         (void) ompi_amd_plan_free(r->plan);
@@ -892,7 +908,8 @@ int mca_coll_rocm_iallgather(const void *sbuf, int scount, struct ompi_datatype_
     size_t rsize = 0;
     int rc, ok;
     (void) ompi_datatype_type_size(rdtype, &rsize);
-    ok = ompi_datatype_is_contiguous_memory_layout(rdtype, rcount * ompi_comm_size(comm)) &&
+    ok = bytes_ok(rsize * (size_t) rcount) &&
+         ompi_datatype_is_contiguous_memory_layout(rdtype, rcount * ompi_comm_size(comm)) &&
          dev(rbuf) && dev(sbuf) &&
          (inplace || ompi_datatype_is_contiguous_memory_layout(sdtype, scount));
     if (!take_device_path(m, ok)) {
@@ -914,7 +931,8 @@ int mca_coll_rocm_ibcast(void *buf, int count, struct ompi_datatype_t *dtype, in
     size_t size = 0;
     int rc;
     (void) ompi_datatype_type_size(dtype, &size);
-    if (!take_device_path(m, ompi_datatype_is_contiguous_memory_layout(dtype, count) && dev(buf))) {
+    if (!take_device_path(m, bytes_ok(size * (size_t) count) &&
+                                 ompi_datatype_is_contiguous_memory_layout(dtype, count) && dev(buf))) {
         return m->c_coll.coll_ibcast(buf, count, dtype, root, comm, request,
                                      m->c_coll.coll_ibcast_module);
     }

@@ -109,6 +109,30 @@ def case_allreduce(comm, rank, n, dt, op, count, salt, kind="R", inplace=False, 
     return True, ""
 
 
+def case_ring_segmented_R(comm, rank, n, count, salt, algorithm=None):
+    """coll/tuned's ring_segmented decision (bytes > N x 1 MiB,
+    coll_tuned_decision_fixed.c:72-86) on order-sensitive data (dataset R):
+    the device result must be the oracle's ring_segmented bits.  Sized past
+    N x 1 MiB at every N (at N = 8 the general cases' COLL_BIG is below it)."""
+    assert count * 4 > n * (1 << 20), "not in the ring_segmented range"
+    xs = [inputs(mop.MPI_FLOAT, count, r, salt, "R") for r in range(n)]
+    exp, alg = orc.allreduce([x.copy() for x in xs], count, mop.MPI_SUM.index, mop.MPI_FLOAT.code)
+    if alg != orc.ALG_RING_SEGMENTED:
+        return False, f"oracle decision {alg}, expected ring_segmented"
+    s = to_dev(xs[rank])
+    out = torch.zeros_like(s)
+    if algorithm is not None:
+        comm.set_param("algorithm", algorithm)
+    try:
+        comm.allreduce(s, out, count, mop.MPI_FLOAT, mop.MPI_SUM, blocking=True)
+    finally:
+        if algorithm is not None:
+            comm.set_param("algorithm", DEFAULT_ALG[0])
+    got = out.cpu().numpy()[:count * 4].view(np.float32)
+    ok = fields_equal(got, exp[rank])
+    return ok, "" if ok else mismatch(got, exp[rank])
+
+
 def case_forced(comm, rank, n, alg, dt, op, count, salt, inplace=False, how="blocking"):
     """MPI_Allreduce with coll_tuned_allreduce_algorithm forced to `alg`
     (coll_tuned_allreduce_decision.c:37-147): the device result must be the
@@ -259,13 +283,16 @@ def case_free_realloc(comm, rank, n, count, salt):
     return len(msgs) == 1, "; ".join(msgs)
 
 
-def case_persistent(comm, rank, n, dt, op, count, salt, inplace=False, starts=3):
+def case_persistent(comm, rank, n, dt, op, count, salt, inplace=False, starts=3, expect_kind=None):
     """MPI_Allreduce_init + repeated starts, new data between starts (same
-    buffers), other collectives interleaved, no sync between them."""
+    buffers), other collectives interleaved, no sync between them.
+    expect_kind: the path the plan must have taken (Plan.kind)."""
     s = torch.zeros(count * dt.extent, dtype=torch.uint8, device="cuda")
     out = s if inplace else torch.zeros_like(s)
     plan = comm.allreduce_init(coll.IN_PLACE if inplace else s, out, count, dt, op)
     try:
+        if expect_kind is not None and plan.kind != expect_kind:
+            return False, f"plan kind {plan.kind}, expected {expect_kind}"
         for it in range(starts):
             xs = [inputs(dt, count, r, salt + it) for r in range(n)]
             exp, _ = orc.allreduce([x.copy() for x in xs], count, op.index, dt.code)
@@ -598,6 +625,11 @@ def main():
     if os.environ.get("OMPI_AMD_TEST_FORCE_SHADOW") == "1":  # every zero-copy call through shadows
         comm.set_param("force_shadow", 1)
     big = int(os.environ.get("COLL_BIG", 1 << 22))
+    # the HSA IPC mode this rank runs under (not forced by the test: the
+    # environment's, else the library's load-time default)
+    report(rank, n, {"rank": rank, "case": "ipc_mode", "ok": True, "msg": "",
+                     "env_at_load": comm.get_param("ipc_mode_legacy_env"),
+                     "legacy": comm.get_param("ipc_mode_legacy")})
     F, D, I32, I64, I8, DI = (mop.MPI_FLOAT, mop.MPI_DOUBLE, mop.MPI_INT32_T, mop.MPI_INT64_T,
                               mop.MPI_INT8_T, mop.MPI_DOUBLE_INT)
     def user_ipc(fn, alg=0):  # zero-copy on the caller's own buffers (param "user_ipc")
@@ -632,6 +664,14 @@ def main():
         ("ar_sum_f32_2500_ring", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, 2500, 4)),
         ("ar_sum_f32_12345_staged", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, 12345, 5)),
         ("ar_sum_f32_big_odd", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, big + 5, 6)),
+        # ring_segmented on dataset R at every N, past N x 1 MiB (12 MiB + 20 B
+        # at N <= 8), under the default scheme and the two others
+        ("ar_ring_segmented_R", lambda: case_ring_segmented_R(comm, rank, n,
+                                                              max(3 << 20, n << 18) + 5, 170)),
+        ("ar_ring_segmented_R_pull", lambda: case_ring_segmented_R(comm, rank, n,
+                                                                   max(3 << 20, n << 18) + 9, 171, 0)),
+        ("ar_ring_segmented_R_pullpush", lambda: case_ring_segmented_R(
+            comm, rank, n, max(3 << 20, n << 18) + 13, 172, 1)),
         ("ar_sum_f32_big", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, big, 7, repeat=3)),
         ("ar_sum_f32_big_inplace",
          lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, big, 8, inplace=True)),
@@ -714,7 +754,10 @@ def main():
         ("persistent_small", lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, 3001, 80)),
         ("persistent_mid_inplace",
          lambda: case_persistent(comm, rank, n, D, mop.MPI_SUM, 70001, 81, inplace=True)),
-        ("persistent_big", lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, big + 3, 82)),
+        ("persistent_big", lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, big + 3, 82,
+                                                   expect_kind=0 if DEFAULT_ALG[0] == 2 else None)),
+        ("user_ipc_persistent_push_kind", user_ipc(lambda: case_persistent(
+            comm, rank, n, F, mop.MPI_SUM, big + 3, 86, expect_kind=3), 2)),
         ("persistent_big_inplace",
          lambda: case_persistent(comm, rank, n, F, mop.MPI_MAX, big, 83, inplace=True)),
     ]

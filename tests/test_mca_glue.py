@@ -51,8 +51,9 @@ def coll_harness(tmp_path_factory):
 def _run_coll_harness(exe, n, gpu, timeout):
     import secrets
     name = secrets.token_hex(3)
-    env = {**os.environ, "HARNESS_GPU": "1" if gpu else "0", "HSA_ENABLE_IPC_MODE_LEGACY": "0",
-           "OMPI_AMD_COLL_TIMEOUT_MS": "20000"}
+    # the HSA IPC mode is inherited (the library's load-time default when
+    # unset), as an mpirun job gets it: INTEGRATION.md §6
+    env = {**os.environ, "HARNESS_GPU": "1" if gpu else "0", "OMPI_AMD_COLL_TIMEOUT_MS": "20000"}
     procs = [subprocess.Popen([exe, name, str(r), str(n)], stdout=subprocess.PIPE,
                               stderr=subprocess.PIPE, text=True, env=env) for r in range(n)]
     outs = []
