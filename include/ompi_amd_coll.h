@@ -89,15 +89,17 @@ int ompi_amd_comm_size(const ompi_amd_comm_t *comm);
  *                   for tests */
 int ompi_amd_comm_set_param(ompi_amd_comm_t *comm, const char *key, int64_t value);
 /* Read a parameter above, or a state counter: "landing_bytes" (current
- * landing-buffer capacity), "stale_closed" (cached peer-buffer mappings
- * closed because the peer freed that allocation: a newer one of the peer
- * overlaps its range or reuses its handle under another buffer id),
- * "stale_same_handle" (of those, how many carried the very handle bytes of
- * the freed allocation — a cache keyed by handle bytes would have served
- * the freed memory),
- * "imports" (cached peer-buffer mappings), "shadowed" (zero-copy calls
- * that ran through the export fallback because the runtime refused to
- * export a user buffer). */
+ * landing-buffer capacity), "imports" (this communicator's references to
+ * peer mappings), "shadowed" (zero-copy calls that ran through the export
+ * fallback), and the process-wide IPC registry's counters (mappings are
+ * shared by every communicator, window and message of the process and
+ * closed with their last reference): "ipc_opens" / "ipc_closes" (runtime
+ * open / close calls made), "ipc_shared" (maps answered from a mapping the
+ * process already held), "ipc_retired" (mappings closed because the
+ * exporter freed the allocation), "ipc_live", "ipc_refs"; "ipc_mode_legacy"
+ * (HSA_ENABLE_IPC_MODE_LEGACY in effect, -1 unset) and
+ * "ipc_mode_legacy_env" (its value when the library was loaded, -1 unset:
+ * the library then defaulted it to 0). */
 int ompi_amd_comm_get_param(const ompi_amd_comm_t *comm, const char *key, int64_t *value);
 
 /* Sticky error of the device side (a barrier that timed out, ...).

@@ -21,13 +21,22 @@
  * Completion semantics.  A send synchronises `stream` first (its data must
  * be final).  Messages of at most 4 KiB (btl/smcuda's eager limit) are
  * copied into the sender's device eager area and the send completes at
- * once (ob1's eager protocol); larger ones, and every MPI_Ssend, publish
- * the user's buffer and complete when the receiver's copy has finished
- * (rendezvous).  MPI_Bsend is not provided.  A receive completes when the
- * copy into its buffer has finished on the device.  The byte
- * count is the message size; the MCA glue packs non-contiguous datatypes
- * with the convertor (include/ompi_amd_ddt.h) first.
- */
+ * once (ob1's eager protocol).  Larger ones are copied into a library-owned
+ * send stage (a pool of exported device buffers that live as long as the
+ * communicator) and the send completes once staged — the receiver pulls
+ * from the stage, so no peer ever maps an application buffer; MPI_Ssend
+ * completes at the receiver's FIN.  Past the pool's cap (param
+ * "p2p_stage_mib", default 1024) or with param "p2p_user_ipc" = 1 the
+ * receiver maps the send buffer itself (rendezvous).  Host (pageable or
+ * pinned) buffers are accepted on both sides: a host send always goes
+ * through a stage, a host receive lands in a device receive stage and is
+ * copied out before it completes.  MPI_Bsend is not provided.  A receive
+ * completes when its data is in its buffer.  Host-side waits (a full
+ * 64-slot ring, wait, probe) are bounded by param "p2p_timeout_ms" (-1: the
+ * communicator's timeout_ms, the default; 0: no limit — the PML glue's
+ * setting, MPI semantics).  The byte count is the message size; the MCA
+ * glue packs non-contiguous datatypes first.
+  */
 #ifndef OMPI_AMD_P2P_H
 #define OMPI_AMD_P2P_H
 
@@ -61,13 +70,13 @@ typedef struct {
     size_t bytes;
 } ompi_amd_status_t;
 
-/* Nonblocking send of `bytes` from device buffer `buf` to rank `dst`.
- * tag >= 0.  Up to 64 sends to one destination may be unmatched at a time;
- * the 65th waits (bounded by the communicator's timeout) for one to
+/* Nonblocking send of `bytes` from `buf` (device or host memory) to rank
+ * `dst`.  tag >= 0.  Up to 64 sends to one destination may be unmatched at
+ * a time; the 65th waits (bounded by p2p_timeout_ms) for one to
  * complete. */
 int ompi_amd_isend(ompi_amd_comm_t *comm, const void *buf, size_t bytes, int dst, int tag,
                    int mode, void *stream, ompi_amd_p2p_request_t **request);
-/* Nonblocking receive into device buffer `buf` of capacity `bytes` from
+/* Nonblocking receive into `buf` (device or host) of capacity `bytes` from
  * `src` (or OMPI_AMD_ANY_SOURCE) with `tag` (or OMPI_AMD_ANY_TAG).  The
  * copy runs on `stream` once the message is matched. */
 int ompi_amd_irecv(ompi_amd_comm_t *comm, void *buf, size_t bytes, int src, int tag,

@@ -68,6 +68,7 @@
 #include "bootstrap.h"
 #include "comm_internal.h"
 #include "coll_kernels.h"
+#include "ipc_registry.h"
 #include "op_device.h"
 #include "runtime.h"
 
@@ -241,6 +242,7 @@ struct buf_desc {
     uint64_t id;    // HIP_POINTER_ATTRIBUTE_BUFFER_ID of the allocation in the exporter
     uint64_t base;  // the allocation's range in the exporter's address space
     uint64_t size;
+    uint64_t pid;   // the exporter process (the registry's key, ipc_registry.h)
 };
 struct call_blob {
     buf_desc s, r;
@@ -333,14 +335,8 @@ struct ompi_amd_comm {
     char *land = nullptr;                 // grow-on-demand landing buffer (push
     size_t land_bytes = 0;                //   allreduce, large scan/exscan)
     ptr_set peer_land{};
-    void *land_opened[kMaxRanks] = {};
-    int stale_closed = 0;                 // cached peer mappings closed because the peer freed them
-    int stale_same_handle = 0;            //   ... of which the new allocation had the same handle bytes
-    int aliased_opens = 0;                // opens the runtime answered with a mapping we already hold
+    ipc_ref *land_ref[kMaxRanks] = {};   // peers' landing buffers (IPC registry references)
     std::vector<uint64_t> land_tokens;    // every rank's token of every landing growth (diagnostics)
-    int ipc_reopens = 0;                  // confirmation rounds that re-opened peers' buffers
-    int ipc_local_reopens = 0;            // opens retried after closing the peer's cached mappings
-    int size_mismatch_opens = 0;          // opens whose mapping had another allocation's range
     int memcpy_token_mismatch = 0;        // landing tokens right by kernel load, wrong by hipMemcpy
     int bcast_split = 0;                  // bcasts that ran as scatter + allgather
     size_t bcast_split_bytes = 4u << 20;  // from this size on (0: never)
@@ -391,18 +387,21 @@ struct ompi_amd_comm {
     int max_blocks = 1024;
     int algorithm = 2;                    // push: push-gather in the staged mode (no staging copy)
     int tuned_alg = 0;                    // coll_tuned_allreduce_algorithm (forced), 0 = fixed
-    // IPC caches
+    // this communicator's references to peer mappings (the mappings
+    // themselves are process-wide: ipc_registry.h), least recently used
+    // evicted past 256
     struct imp_entry {
         int peer;
         hipIpcMemHandle_t h;
         uint64_t id, rbase, rsize;  // the allocation in the exporter (buf_desc)
+        ipc_ref *ref;
         void *base;                 // its mapping here
         uint64_t last_use;
         int pins;
     };
     std::vector<imp_entry> imports;
     uint64_t use_clock = 0;
-    void *opened[kMaxRanks][2] = {};      // flags / scratch mappings of peers
+    ipc_ref *opened[kMaxRanks][2] = {};   // peers' flag pages / scratch
     // per-phase kernel timing (param "profile"): event pairs per call
     int profile = 0;
     std::vector<hipEvent_t> ev_free;
@@ -443,7 +442,7 @@ namespace ompi_amd {
 enum { ALG_PULL = 0, ALG_PULL_PUSH = 1, ALG_PUSH = 2, ALG_COUNT = 3 };
 
 struct ipc_blob {
-    hipIpcMemHandle_t flags, scratch;
+    buf_desc flags, scratch;
 };
 
 
@@ -576,6 +575,23 @@ static unsigned long long buffer_id(const void *p) {
     return id;
 }
 
+// The descriptor peers map an exported library allocation by (the handle
+// is already in d->h): the allocation's real range, buffer id and process.
+static void describe_alloc(void *p, buf_desc *d) {
+    void *ab = p;
+    size_t as = 0;
+    if (hipMemGetAddressRange((hipDeviceptr_t *)&ab, &as, (hipDeviceptr_t)p) != hipSuccess) {
+        (void)hipGetLastError();
+        ab = p;
+    }
+    d->off = (uint64_t)((char *)p - (char *)ab);
+    d->valid = 1;
+    d->id = buffer_id(p);
+    d->base = (uint64_t)(uintptr_t)ab;
+    d->size = as;
+    d->pid = (uint64_t)getpid();
+}
+
 // ipc_failed: set when the runtime refused to export a live device
 // allocation, or handed it recycled handle bytes (the shadow fallback
 // applies); other failures are errors.
@@ -626,198 +642,92 @@ static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d, bool *ip
     d->h = h;
     d->off = (uint64_t)((const char *)ptr - (const char *)base);
     d->valid = 1;
+    d->pid = (uint64_t)getpid();
     return OMPI_AMD_SUCCESS;
 }
 
-// Close every cached mapping of `peer` that cannot be the allocation `d`
-// describes but would collide with it: the same handle bytes or an
-// overlapping exporter range under another buffer id.  The peer has freed
-// those allocations (its live allocations never overlap).  They must be
-// closed BEFORE the new handle is opened: ROCm 7.2's hipIpcOpenMemHandle
-// answers a handle whose exporter address this process already maps with
-// that existing mapping, even when the size differs (measured in round 2:
-// peer 1's buffer id 347 at 0x763d73200000 + 16818488 came back as this
-// process's still-open mapping of its freed buffer id 329 at 0x763d73200000
-// + 16814384 — caught by mapped_already — after an ordering that closed
-// overlapping mappings only after the open).  A pinned mapping (a persistent
-// plan's) of a freed buffer is a program error: report it instead of
-// unmapping under the plan.
-static int drop_stale_imports(ompi_amd_comm_t *c, int peer, const buf_desc &d,
-                              bool *closed_same = nullptr) {
-    if (closed_same) *closed_same = false;
-    const uint64_t lo = d.base, hi = d.base + d.size;
+static ipc_alloc alloc_of(const buf_desc &d) { return ipc_alloc{d.h, d.pid, d.id, d.base, d.size}; }
+
+// This rank failed a call its peers may have launched: make the failure
+// sticky here and raise every peer's abort word (their barrier waits then
+// give up within ~1 ms and their calls fail with OMPI_AMD_ERR_TIMEOUT).
+static void abort_peers(ompi_amd_comm_t *c, int rc) {
+    int expect = 0;
+    (void)__atomic_compare_exchange_n(c->err_host, &expect, rc, false, __ATOMIC_ACQ_REL,
+                                      __ATOMIC_ACQUIRE);
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();
+        return;
+    }
+    hipLaunchKernelGGL(abort_kernel, dim3(1), dim3(64), 0, s, c->peer_flags, c->flags, c->rank,
+                       c->size);
+    if (hipGetLastError() == hipSuccess) hip_ignore(hipStreamSynchronize(s));
+    (void)hipGetLastError();
+    hip_ignore(hipStreamDestroy(s));
+}
+
+// Drop this communicator's references to mappings the registry retired
+// (their exporter freed the allocation).  A pinned one is reported: a
+// persistent operation of this communicator still uses it.
+static int drop_retired(ompi_amd_comm_t *c) {
     for (auto it = c->imports.begin(); it != c->imports.end();) {
-        const bool same_h = same_handle(it->h, d.h);
-        const bool overlap = it->rbase < hi && lo < it->rbase + it->rsize;
-        if (it->peer != peer || it->id == d.id || !(same_h || overlap)) {
+        if (!ipc_retired(it->ref)) {
             ++it;
             continue;
         }
         if (it->pins > 0) {
             record_msg("rank %d freed a buffer (id %llu) that a persistent collective still maps",
-                       peer, (unsigned long long)it->id);
+                       it->peer, (unsigned long long)it->id);
             return OMPI_AMD_ERR_BAD_PARAM;
         }
-        trace_handle("close-stale", it->h, "peer %d id %llu -> %p", it->peer,
-                     (unsigned long long)it->id, it->base);
-        const hipError_t e = hipIpcCloseMemHandle(it->base);
-        if (e != hipSuccess) return record_hip(e, "hipIpcCloseMemHandle (stale peer mapping)");
-        ++c->stale_closed;
-        c->stale_same_handle += same_h ? 1 : 0;
-        if (closed_same && same_h) *closed_same = true;
+        ipc_unmap(it->ref);
         it = c->imports.erase(it);
     }
     return OMPI_AMD_SUCCESS;
 }
 
-// Is `base` (just returned by hipIpcOpenMemHandle for a handle we do not
-// hold) inside a mapping this communicator already holds?  Then the runtime
-// answered a new handle with an existing mapping of another allocation.
-static const char *mapped_already(const ompi_amd_comm_t *c, const void *base) {
-    static thread_local char what[160];
-    const char *b = (const char *)base;
-    for (const auto &x : c->imports)
-        if (b >= (const char *)x.base && b < (const char *)x.base + x.rsize) {
-            snprintf(what, sizeof(what), "peer %d buffer id %llu (%p + %llu)", x.peer,
-                     (unsigned long long)x.id, (void *)(uintptr_t)x.rbase,
-                     (unsigned long long)x.rsize);
-            return what;
-        }
-    for (int p = 0; p < kMaxRanks; ++p) {
-        if (c->opened[p][0] && b == (const char *)c->opened[p][0]) {
-            snprintf(what, sizeof(what), "peer %d's flag page", p);
-            return what;
-        }
-        if (c->opened[p][1] && b >= (const char *)c->opened[p][1] &&
-            b < (const char *)c->opened[p][1] + c->scratch_bytes) {
-            snprintf(what, sizeof(what), "peer %d's scratch", p);
-            return what;
-        }
-        if (c->land_opened[p] && b == (const char *)c->land_opened[p]) {
-            snprintf(what, sizeof(what), "peer %d's landing buffer", p);
-            return what;
-        }
-    }
-    return nullptr;
-}
-
+// Map peer `peer`'s buffer `d` (cached per communicator; the mapping itself
+// is the process's, shared through the IPC registry).  One attempt: a
+// refused or wrong answer from the runtime is an error, never retried.
 static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const char **out,
                       bool pin = false, void **base_out = nullptr) {
     *out = nullptr;
     if (base_out) *base_out = nullptr;
     if (!d.valid) return OMPI_AMD_SUCCESS;
+    TRY(drop_retired(c));
     for (auto &x : c->imports) {
-        if (x.peer == peer && x.id == d.id && same_handle(x.h, d.h)) {
+        if (x.peer == peer && x.id == d.id && x.rbase == d.base && x.rsize == d.size &&
+            same_handle(x.h, d.h)) {
             x.last_use = ++c->use_clock;
-            x.pins += pin ? 1 : 0;
+            if (pin) {
+                ++x.pins;
+                ipc_pin(x.ref, 1);
+            }
             *out = (const char *)x.base + d.off;
             if (base_out) *base_out = x.base;
             return OMPI_AMD_SUCCESS;
         }
     }
-    bool closed_same = false;
-    TRY(drop_stale_imports(c, peer, d, &closed_same));
-    if (c->imports.size() >= 256) {  // evict the least recently used unpinned mapping
+    if (c->imports.size() >= 256) {  // evict the least recently used unpinned reference
         auto it = c->imports.end();
         for (auto jt = c->imports.begin(); jt != c->imports.end(); ++jt)
             if (jt->pins == 0 && (it == c->imports.end() || jt->last_use < it->last_use)) it = jt;
         if (it != c->imports.end()) {
             TRY(quiesce(c));  // an earlier call's kernel may still read it
-            hip_ignore(hipIpcCloseMemHandle(it->base));
+            ipc_unmap(it->ref);
             c->imports.erase(it);
         }
     }
+    ipc_ref *ref = nullptr;
     void *base = nullptr;
-    // Two attempts.  After heavy allocation churn on a shared GPU the runtime
-    // has refused a live peer buffer ("invalid device pointer") or answered
-    // with a mapping this process already holds; both went away once every
-    // cached mapping of that peer was closed (the blocking calls' confirmation
-    // round measured it, ipc_reopens).  The second attempt does that here,
-    // so a deferred nonblocking call — which has no confirmation round —
-    // recovers the same way: wait for this communicator's kernels (one may
-    // still read a mapping about to close), close the peer's unpinned
-    // mappings, open again.
-    for (int attempt = 0;; ++attempt) {
-        ++c->imports_new;
-        hipError_t e;
-        {
-            host_step st("hipIpcOpenMemHandle", (size_t)d.size);
-            e = hipIpcOpenMemHandle(&base, d.h, hipIpcMemLazyEnablePeerAccess);
-        }
-        const char *what = nullptr;
-        if (e == hipSuccess) {
-            trace_handle("open", d.h, "peer %d id %llu %p+%llu -> %p", peer, (unsigned long long)d.id,
-                         (void *)(uintptr_t)d.base, (unsigned long long)d.size, base);
-            what = mapped_already(c, base);
-            if (!what) {
-                // the mapping must be the advertised allocation: the range
-                // the runtime reports for it has the exporter's base (offset
-                // 0) and size.  A stale answer — an earlier allocation at the
-                // same exporter address — has its own size (round 2: pushes
-                // into a peer's rbuf landed elsewhere after churn).
-                void *mb = nullptr;
-                size_t ms = 0;
-                const hipError_t er = hipMemGetAddressRange((hipDeviceptr_t *)&mb, &ms,
-                                                            (hipDeviceptr_t)base);
-                if (er != hipSuccess) (void)hipGetLastError();
-                // (the runtime may round the mapping up to its page size)
-                const uint64_t up = (d.size + (2u << 20) - 1) & ~(uint64_t)((2u << 20) - 1);
-                if (ipc_trace())
-                    fprintf(stderr, "[ipc pid %d] open-range %p+%zu advertised %llu\n", (int)getpid(),
-                            mb, ms, (unsigned long long)d.size);
-                if (er != hipSuccess || (mb == base && ms >= d.size && ms <= up)) break;
-                static thread_local char why[128];
-                snprintf(why, sizeof(why), "a mapping of %zu bytes at %p (advertised %llu at offset 0)",
-                         ms, mb, (unsigned long long)d.size);
-                what = why;
-                ++c->size_mismatch_opens;
-                // treated as an alias: the just-opened reference is closed below
-                c->imports.push_back({peer, d.h, d.id, d.base, d.size, base, ++c->use_clock, 0});
-            } else {
-                ++c->aliased_opens;
-            }
-        } else {
-            (void)hipGetLastError();
-        }
-        if (attempt == 1) {
-            if (what) {
-                unsigned hw[16];
-                memcpy(hw, &d.h, sizeof(hw));
-                record_msg("hipIpcOpenMemHandle returned %p for peer %d buffer id %llu (%p + %llu, "
-                           "handle word7 %08x), which is already this process's mapping of %s",
-                           base, peer, (unsigned long long)d.id, (void *)(uintptr_t)d.base,
-                           (unsigned long long)d.size, hw[7], what);
-            } else {
-                record_msg("hipIpcOpenMemHandle: %s (peer %d buffer id %llu at %p + %llu%s)",
-                           hipGetErrorString(e), peer, (unsigned long long)d.id,
-                           (void *)(uintptr_t)d.base, (unsigned long long)d.size,
-                           closed_same ? ", after closing its freed predecessor with the same handle"
-                                       : "");
-            }
-            return OMPI_AMD_ERR_HIP;
-        }
-        TRY(quiesce(c));
-        ++c->ipc_local_reopens;
-        bool closed_base = false;
-        for (auto it = c->imports.begin(); it != c->imports.end();) {
-            if (it->peer == peer && it->pins == 0) {
-                closed_base = closed_base || ((const char *)base >= (const char *)it->base &&
-                                              (const char *)base < (const char *)it->base + it->rsize);
-                hip_ignore(hipIpcCloseMemHandle(it->base));
-                it = c->imports.erase(it);
-            } else {
-                ++it;
-            }
-        }
-        // an alias answer into one of the mappings just closed may be a
-        // second reference to it (a refcounting runtime): drop that too;
-        // never close into a mapping still in use (another peer's, the
-        // communicator's own pages)
-        if (what && closed_base) hip_ignore(hipIpcCloseMemHandle(base));
-        (void)hipGetLastError();
-        base = nullptr;
+    {
+        host_step st("ipc_map", (size_t)d.size);
+        TRY(ipc_map(alloc_of(d), &ref, &base));
     }
-    c->imports.push_back({peer, d.h, d.id, d.base, d.size, base, ++c->use_clock, pin ? 1 : 0});
+    ++c->imports_new;
+    if (pin) ipc_pin(ref, 1);
+    c->imports.push_back({peer, d.h, d.id, d.base, d.size, ref, base, ++c->use_clock, pin ? 1 : 0});
     *out = (const char *)base + d.off;
     if (base_out) *base_out = base;
     return OMPI_AMD_SUCCESS;
@@ -827,6 +737,7 @@ static void unpin_import(ompi_amd_comm_t *c, void *base) {
     for (auto &x : c->imports)
         if (x.base == base && x.pins > 0) {
             --x.pins;
+            ipc_pin(x.ref, -1);
             return;
         }
 }
@@ -844,17 +755,12 @@ static int exchange_bufs(ompi_amd_comm_t *c, const void *sbuf, const void *rbuf,
     int rc = export_buf(c, sbuf, &mine.s);
     if (rc == OMPI_AMD_SUCCESS) rc = export_buf(c, rbuf, &mine.r);
     if (rc != OMPI_AMD_SUCCESS && !c->pre) {
-        // still take part in the swap (peers must not wait for this rank),
-        // then everyone fails the call together at the confirmation
+        // still take part in the swap (peers must not wait for this rank at
+        // the rendezvous), then stop their device work
         call_blob all_[kMaxRanks];
         mine = call_blob{};
-        if (c->boot.allgather(&mine, all_, sizeof(call_blob)) == OMPI_AMD_SUCCESS) {
-            int st[kMaxRanks];
-            const int one = 1;
-            for (int a = 0; a < 3; ++a) {  // mirror the peers' confirmation rounds
-                if (c->boot.allgather(&one, st, sizeof(int)) != OMPI_AMD_SUCCESS) break;
-            }
-        }
+        (void)c->boot.allgather(&mine, all_, sizeof(call_blob));
+        abort_peers(c, rc);
         return rc;
     }
     if (rc != OMPI_AMD_SUCCESS) return rc;
@@ -869,67 +775,32 @@ static int exchange_bufs(ompi_amd_comm_t *c, const void *sbuf, const void *rbuf,
     return import_all(c, all, sbuf, rbuf, s, r, allflags, pin, bases);
 }
 
-// Map every peer's (s, r) descriptors of `all`; a blocking call (no c->pre)
-// confirms the opens collectively (below).
+// Map every peer's (s, r) descriptors of `all`.  A failure is final for
+// this communicator: the peers' device work of the call is stopped through
+// their abort words (abort_peers) instead of a confirmation rendezvous.
 static int import_all(ompi_amd_comm_t *c, const call_blob *all, const void *sbuf, const void *rbuf,
                       ptr_set *s, ptr_set *r, uint64_t *allflags, bool pin,
                       void *(*bases)[2]) {
-    bool done[kMaxRanks] = {};
-    for (int attempt = 0;; ++attempt) {
-        int local = OMPI_AMD_SUCCESS;
-        for (int p = 0; p < c->size; ++p) {
-            if (allflags) allflags[p] = all[p].flags;
-            if (p == c->rank) {
-                s->p[p] = (const char *)sbuf;
-                r->p[p] = (const char *)rbuf;
-                continue;
-            }
-            if (done[p]) continue;
-            void *b0 = nullptr, *b1 = nullptr;
-            int prc = import_buf(c, p, all[p].s, &s->p[p], pin, &b0);
-            if (prc == OMPI_AMD_SUCCESS) prc = import_buf(c, p, all[p].r, &r->p[p], pin, &b1);
-            if (prc != OMPI_AMD_SUCCESS) {
-                if (b0 && pin) unpin_import(c, b0);
-                local = prc;
-                continue;
-            }
-            done[p] = true;
-            if (bases) {
-                bases[p][0] = b0;
-                bases[p][1] = b1;
-            }
+    int rc = OMPI_AMD_SUCCESS;
+    for (int p = 0; p < c->size; ++p) {
+        if (allflags) allflags[p] = all[p].flags;
+        if (p == c->rank) {
+            s->p[p] = (const char *)sbuf;
+            r->p[p] = (const char *)rbuf;
+            continue;
         }
-        // A blocking call confirms the opens: every rank learns whether any
-        // rank failed to map a peer (hipIpcOpenMemHandle refused a live
-        // buffer of a peer, "invalid device pointer", in round-2 runs with
-        // heavy allocation churn on one GPU).  Then every rank drops its
-        // cached mappings of the peers it failed on and opens again, at most
-        // twice (`ipc_reopens`); a deferred call cannot add a rendezvous.
-        if (c->pre) return local;
-        int st[kMaxRanks], any = 0;
-        const int mine_st = local == OMPI_AMD_SUCCESS ? 0 : 1;
-        TRY(c->boot.allgather(&mine_st, st, sizeof(int)));
-        for (int p = 0; p < c->size; ++p) any |= st[p];
-        if (!any) return OMPI_AMD_SUCCESS;
-        if (attempt == 2) {
-            if (local == OMPI_AMD_SUCCESS)
-                record_msg("a peer could not map this call's buffers (IPC open failed there)");
-            return local != OMPI_AMD_SUCCESS ? local : OMPI_AMD_ERR_HIP;
-        }
-        ++c->ipc_reopens;
-        TRY(quiesce(c));  // no earlier kernel of this communicator still reads a mapping closed below
-        for (int p = 0; p < c->size; ++p) {
-            if (p == c->rank || done[p]) continue;
-            for (auto it = c->imports.begin(); it != c->imports.end();) {
-                if (it->peer == p && it->pins == 0) {
-                    hip_ignore(hipIpcCloseMemHandle(it->base));
-                    it = c->imports.erase(it);
-                } else {
-                    ++it;
-                }
-            }
+        if (rc != OMPI_AMD_SUCCESS) continue;
+        void *b0 = nullptr, *b1 = nullptr;
+        rc = import_buf(c, p, all[p].s, &s->p[p], pin, &b0);
+        if (rc == OMPI_AMD_SUCCESS) rc = import_buf(c, p, all[p].r, &r->p[p], pin, &b1);
+        if (rc != OMPI_AMD_SUCCESS && b0 && pin) unpin_import(c, b0);
+        if (rc == OMPI_AMD_SUCCESS && bases) {
+            bases[p][0] = b0;
+            bases[p][1] = b1;
         }
     }
+    if (rc != OMPI_AMD_SUCCESS) abort_peers(c, rc);
+    return rc;
 }
 
 // Work this communicator put on a stream: note the stream; when the calls
@@ -960,6 +831,8 @@ static void note_stream(ompi_amd_comm_t *c, hipStream_t s) {
 // Wait until every kernel this communicator launched has finished (its
 // streams only: an application's unrelated work on the device is not
 // waited for, unlike hipDeviceSynchronize).
+static int quiesce_user(void *c) { return quiesce(static_cast<ompi_amd_comm_t *>(c)); }
+
 static int quiesce(ompi_amd_comm_t *c) {
     host_step st("quiesce");
     for (hipEvent_t e : c->stream_evs) {
@@ -1037,16 +910,13 @@ static uint64_t landing_token(int rank) {
     return x | 1;
 }
 
-// The landing buffers travel as full descriptors (handle + buffer id +
-// exporter range), and before a peer's new landing buffer is mapped every
-// cached mapping of that peer's freed allocations that it could collide
-// with is closed (drop_stale_imports).  Two 8-process runs of round 1 read
-// stale landing data after a growth while such mappings — user buffers the
-// peers had since freed — were still open in the import cache, keyed by
-// handle bytes only; that state no longer exists.  The token the owner
-// stamps into its buffer is still read back through every new mapping, as
-// an assertion: a mismatch fails the call on every rank with the peer and
-// both tokens named (no retry).
+// The landing buffers travel as full descriptors (process, handle, buffer
+// id, exporter range) and are mapped through the IPC registry, which
+// retires any mapping of the peer's freed allocations that the new one
+// could collide with before opening it.  The token the owner stamps into
+// its buffer is read back through every new mapping, as an assertion: a
+// mismatch fails the growth on every rank with the peer and both tokens
+// named (no retry).
 static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     if (need <= c->land_bytes) return OMPI_AMD_SUCCESS;
     constexpr size_t kStep = 32u << 20, kTag = 64;  // the last kTag bytes hold the token
@@ -1061,15 +931,14 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     TRY(c->boot.barrier());  // every rank's earlier kernels are done
     // the old mappings stay open until the new ones are (so the new ones
     // get fresh addresses in this process), then close
-    void *old_land[kMaxRanks];
+    ipc_ref *old_land[kMaxRanks];
     for (int p = 0; p < kMaxRanks; ++p) {
-        old_land[p] = c->land_opened[p];
-        c->land_opened[p] = nullptr;
+        old_land[p] = c->land_ref[p];
+        c->land_ref[p] = nullptr;
         c->peer_land.p[p] = nullptr;
     }
     auto close_old = [&] {
-        for (int p = 0; p < kMaxRanks; ++p)
-            if (old_land[p]) hip_ignore(hipIpcCloseMemHandle(old_land[p]));
+        for (int p = 0; p < kMaxRanks; ++p) ipc_unmap(old_land[p]);
     };
     struct land_blob { buf_desc d; uint64_t token; int ok; };
     land_blob mine{}, all[kMaxRanks];
@@ -1077,13 +946,20 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     hipError_t e = alloc_exportable(want, &fresh, &mine.d.h);
     mine.token = landing_token(c->rank);
     if (e == hipSuccess) {
-        unsigned long long id = 0;
-        e = hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)fresh);
-        mine.d.id = id;
+        mine.d.id = buffer_id(fresh);
         mine.d.base = (uint64_t)(uintptr_t)fresh;
         mine.d.size = want;
+        mine.d.pid = (uint64_t)getpid();
         mine.d.valid = 1;
-        if (e != hipSuccess) record_hip(e, "hipPointerGetAttribute (landing buffer id)");
+        // the registry keys on the allocation's real range (alloc_exportable pads it)
+        void *ab = nullptr;
+        size_t as = 0;
+        if (hipMemGetAddressRange((hipDeviceptr_t *)&ab, &as, (hipDeviceptr_t)fresh) == hipSuccess) {
+            mine.d.base = (uint64_t)(uintptr_t)ab;
+            mine.d.size = as;
+        } else {
+            (void)hipGetLastError();
+        }
     } else {
         record_hip(e, "landing buffer: hipMalloc / hipIpcGetMemHandle");
     }
@@ -1114,24 +990,13 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
             status = 1;
             break;
         }
-        rc = drop_stale_imports(c, p, all[p].d);
-        if (rc != OMPI_AMD_SUCCESS) { status = 1; break; }
         void *m = nullptr;
-        e = hipIpcOpenMemHandle(&m, all[p].d.h, hipIpcMemLazyEnablePeerAccess);
-        if (e != hipSuccess) {
-            record_hip(e, "hipIpcOpenMemHandle (landing)");
+        if (ipc_map(alloc_of(all[p].d), &c->land_ref[p], &m) != OMPI_AMD_SUCCESS) {
             status = 1;
             break;
         }
-        if (const char *what = mapped_already(c, m)) {
-            record_msg("landing buffer of rank %d: hipIpcOpenMemHandle returned %p, already this "
-                       "process's mapping of %s", p, m, what);
-            ++c->aliased_opens;
-            status = 2;
-            break;
-        }
-        c->land_opened[p] = m;
-        // read the token by a kernel load through the mapping (what the
+        // the token sits `want` - kTag bytes from the allocation's start
+        // (alloc_exportable's pointer is the allocation's base); read it by a kernel load through the mapping (what the
         // collectives' kernels see) into this communicator's own scratch,
         // and by hipMemcpy from the mapping, to tell the two apart
         uint64_t seen = 0, seen_memcpy = 0;
@@ -1175,14 +1040,14 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     if (rc == OMPI_AMD_SUCCESS && worst == 0) {
         c->land = fresh;
         for (int p = 0; p < c->size; ++p)
-            c->peer_land.p[p] = p == c->rank ? c->land : (const char *)c->land_opened[p];
+            c->peer_land.p[p] = p == c->rank ? c->land : (const char *)ipc_ref_base(c->land_ref[p]);
         c->land_bytes = want - kTag;
         return OMPI_AMD_SUCCESS;
     }
     (void)c->boot.barrier();  // nobody reads the new buffers any more
     for (int p = 0; p < kMaxRanks; ++p) {
-        if (c->land_opened[p]) hip_ignore(hipIpcCloseMemHandle(c->land_opened[p]));
-        c->land_opened[p] = nullptr;
+        ipc_unmap(c->land_ref[p]);
+        c->land_ref[p] = nullptr;
     }
     if (fresh) hip_ignore(hipFree(fresh));
     if (rc == OMPI_AMD_SUCCESS && status == 0)
@@ -2025,25 +1890,6 @@ static int agree_root0_inplace(ompi_amd_comm_t *c, path_params *pp, bool inplace
     return OMPI_AMD_SUCCESS;
 }
 
-// This rank failed a call its peers may have launched: make the failure
-// sticky here and raise every peer's abort word (their barrier waits then
-// give up within ~1 ms and their calls fail with OMPI_AMD_ERR_TIMEOUT).
-static void abort_peers(ompi_amd_comm_t *c, int rc) {
-    int expect = 0;
-    (void)__atomic_compare_exchange_n(c->err_host, &expect, rc, false, __ATOMIC_ACQ_REL,
-                                      __ATOMIC_ACQUIRE);
-    hipStream_t s = nullptr;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
-        (void)hipGetLastError();
-        return;
-    }
-    hipLaunchKernelGGL(abort_kernel, dim3(1), dim3(64), 0, s, c->peer_flags, c->flags, c->rank,
-                       c->size);
-    if (hipGetLastError() == hipSuccess) hip_ignore(hipStreamSynchronize(s));
-    (void)hipGetLastError();
-    hip_ignore(hipStreamDestroy(s));
-}
-
 // Launch deferred nonblocking calls in posting order, each once every rank
 // has posted its handle-swap half; block = wait for them (the blocking entry
 // points do, so their device work follows the deferred calls' on every rank).
@@ -2212,9 +2058,9 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
     // device resources: fine-grained flags, scratch, pinned error word
     c->scratch_bytes = std::max<size_t>(c->small_bytes, 4 << 20);  // per half
     ipc_blob mine{}, all[kMaxRanks];
-    hipError_t e = alloc_exportable(kFlagPageBytes, (char **)&c->flags, &mine.flags, true);
+    hipError_t e = alloc_exportable(kFlagPageBytes, (char **)&c->flags, &mine.flags.h, true);
     if (e == hipSuccess) e = hipMemsetAsync(c->flags, 0, kFlagPageBytes, nullptr);
-    if (e == hipSuccess) e = alloc_exportable(2 * c->scratch_bytes, &c->scratch, &mine.scratch);
+    if (e == hipSuccess) e = alloc_exportable(2 * c->scratch_bytes, &c->scratch, &mine.scratch.h);
     if (e == hipSuccess) e = hipHostMalloc((void **)&c->err_host, 64, hipHostMallocMapped);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&c->err_dev, c->err_host, 0);
     if (e == hipSuccess && getenv("OMPI_AMD_DEBUG_PROGRESS") && atoi(getenv("OMPI_AMD_DEBUG_PROGRESS"))) {
@@ -2230,7 +2076,10 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
         ompi_amd_comm_destroy(c);
         return rc;
     }
+    describe_alloc(c->flags, &mine.flags);
+    describe_alloc(c->scratch, &mine.scratch);
     *c->err_host = 0;
+    ipc_add_user(c, quiesce_user);
     if (rank == 0) rc = p2p_create(c, name, rank, size, 0, &c->p2p);
     if (rc == OMPI_AMD_SUCCESS) rc = c->boot.allgather(&mine, all, sizeof(ipc_blob));
     if (rc == OMPI_AMD_SUCCESS && rank != 0) rc = p2p_create(c, name, rank, size, 1, &c->p2p);
@@ -2241,11 +2090,9 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
             continue;
         }
         void *f = nullptr, *s = nullptr;
-        e = hipIpcOpenMemHandle(&f, all[p].flags, hipIpcMemLazyEnablePeerAccess);
-        if (e == hipSuccess) e = hipIpcOpenMemHandle(&s, all[p].scratch, hipIpcMemLazyEnablePeerAccess);
-        if (e != hipSuccess) { rc = record_hip(e, "hipIpcOpenMemHandle (comm)"); break; }
-        c->opened[p][0] = f;
-        c->opened[p][1] = s;
+        rc = ipc_map(alloc_of(all[p].flags), &c->opened[p][0], &f);
+        if (rc == OMPI_AMD_SUCCESS) rc = ipc_map(alloc_of(all[p].scratch), &c->opened[p][1], &s);
+        if (rc != OMPI_AMD_SUCCESS) break;
         c->peer_flags.p[p] = (uint64_t *)f;
         c->peer_scratch.p[p] = (const char *)s;
     }
@@ -2265,12 +2112,13 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     (void)drain(c);  // deferred nonblocking calls every peer will also launch
     (void)quiesce(c);
     (void)c->boot.barrier();  // nobody still reads our memory
-    for (auto &x : c->imports) hip_ignore(hipIpcCloseMemHandle(x.base));
+    ipc_remove_user(c);
+    for (auto &x : c->imports) ipc_unmap(x.ref);  // the process's mapping stays while others hold it
+    c->imports.clear();
     for (int p = 0; p < kMaxRanks; ++p) {
-        for (int k = 0; k < 2; ++k)
-            if (c->opened[p][k]) hip_ignore(hipIpcCloseMemHandle(c->opened[p][k]));
-        if (c->land_opened[p]) hip_ignore(hipIpcCloseMemHandle(c->land_opened[p]));
-        c->land_opened[p] = nullptr;
+        for (int k = 0; k < 2; ++k) ipc_unmap(c->opened[p][k]);
+        ipc_unmap(c->land_ref[p]);
+        c->land_ref[p] = nullptr;
     }
     (void)c->boot.barrier();
     if (c->flags) hip_ignore(hipFree(c->flags));
@@ -2403,6 +2251,8 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
     } else if (!strcmp(key, "tuned_allreduce_algorithm")) {
         if (v < 0 || v >= TUNED_AR_COUNT) return OMPI_AMD_ERR_BAD_PARAM;
         c->tuned_alg = (int)v;
+    } else if (!strncmp(key, "p2p_", 4) && p2p_set_param(c->p2p, key, v) != OMPI_AMD_ERR_UNSUPPORTED) {
+        return p2p_set_param(c->p2p, key, v);
     } else {
         record_msg("unknown coll param '%s'", key);
         return OMPI_AMD_ERR_BAD_PARAM;
@@ -2422,17 +2272,17 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "tuned_allreduce_algorithm")) *v = c->tuned_alg;
     else if (!strcmp(key, "landing_bytes")) *v = (int64_t)c->land_bytes;
     else if (!strcmp(key, "boot_calls")) *v = (int64_t)c->boot.posted();
-    else if (!strcmp(key, "stale_closed")) *v = c->stale_closed;
-    else if (!strcmp(key, "stale_same_handle")) *v = c->stale_same_handle;
-    else if (!strcmp(key, "aliased_opens")) *v = c->aliased_opens;
-    else if (!strcmp(key, "ipc_reopens")) *v = c->ipc_reopens;
+    else if (!strcmp(key, "ipc_opens")) *v = ipc_get_stats().opens;
+    else if (!strcmp(key, "ipc_closes")) *v = ipc_get_stats().closes;
+    else if (!strcmp(key, "ipc_shared")) *v = ipc_get_stats().shared;
+    else if (!strcmp(key, "ipc_retired")) *v = ipc_get_stats().retired;
+    else if (!strcmp(key, "ipc_live")) *v = ipc_get_stats().live;
+    else if (!strcmp(key, "ipc_refs")) *v = ipc_get_stats().refs;
     else if (!strcmp(key, "bcast_split")) *v = c->bcast_split;
     else if (!strcmp(key, "bcast_split_bytes")) *v = (int64_t)c->bcast_split_bytes;
     else if (!strcmp(key, "memcpy_token_mismatch")) *v = c->memcpy_token_mismatch;
     else if (!strcmp(key, "shadowed")) *v = c->shadowed;
     else if (!strcmp(key, "epoch")) *v = (int64_t)c->epoch;
-    else if (!strcmp(key, "ipc_local_reopens")) *v = c->ipc_local_reopens;
-    else if (!strcmp(key, "size_mismatch_opens")) *v = c->size_mismatch_opens;
     else if (!strncmp(key, "dbg_", 4) && c->dbg_host) {  // dbg_entered / dbg_left / dbg_seenP
         volatile uint64_t *d = c->dbg_host;
         if (!strcmp(key, "dbg_entered")) *v = (int64_t)d[0];
@@ -2447,6 +2297,7 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "force_shadow")) *v = c->force_shadow;
     else if (!strcmp(key, "user_ipc")) *v = c->user_ipc;
     else if (!strcmp(key, "imports")) *v = (int64_t)c->imports.size();
+    else if (!strncmp(key, "p2p_", 4) && p2p_get_param(c->p2p, key, v) == OMPI_AMD_SUCCESS) return OMPI_AMD_SUCCESS;
     else if (!strcmp(key, "ipc_mode_legacy_env")) *v = ipc_mode_env_at_load();
     else if (!strcmp(key, "ipc_mode_legacy")) *v = *ipc_mode_env_now() ? atoi(ipc_mode_env_now()) : -1;
     else {
@@ -3240,10 +3091,10 @@ int comm_alloc_exportable(size_t bytes, bool uncached, void **out, ipc_desc *d) 
     const hipError_t e = alloc_exportable(bytes, &p, &d->h, uncached);
     if (e != hipSuccess) return record_hip(e, "exportable allocation");
     *out = p;
-    d->valid = 1;
-    d->id = buffer_id(p);
-    d->base = (uint64_t)(uintptr_t)p;
-    d->size = bytes;
+    buf_desc b{};
+    b.h = d->h;
+    describe_alloc(p, &b);
+    memcpy(d, &b, sizeof(b));
     return OMPI_AMD_SUCCESS;
 }
 
@@ -3262,20 +3113,6 @@ int comm_import(ompi_amd_comm_t *c, int peer, const ipc_desc &d, const char **ou
 }
 
 void comm_unpin(ompi_amd_comm_t *c, void *base) { unpin_import(c, base); }
-
-int comm_drop_peer_mappings(ompi_amd_comm_t *c, int peer) {
-    TRY(quiesce(c));
-    ++c->ipc_local_reopens;
-    for (auto it = c->imports.begin(); it != c->imports.end();) {
-        if (it->peer == peer && it->pins == 0) {
-            hip_ignore(hipIpcCloseMemHandle(it->base));
-            it = c->imports.erase(it);
-        } else {
-            ++it;
-        }
-    }
-    return OMPI_AMD_SUCCESS;
-}
 
 int comm_drain(ompi_amd_comm_t *c) { return drain(c); }
 

@@ -13,10 +13,10 @@
 namespace ompi_amd {
 
 // A device buffer as peers see it: its allocation's IPC handle + offset,
-// plus the allocation's identity in the exporter (HIP buffer id, base
-// address, size).  Importers match cached mappings on (peer, handle, id)
-// and close any cached mapping of that peer whose exporter range overlaps
-// a newer allocation (the peer freed it: live allocations never overlap).
+// plus the allocation's identity in the exporter (process, HIP buffer id,
+// base address, size).  Mappings are shared process-wide through the IPC
+// registry (ipc_registry.h), which retires a mapping once the exporter's
+// newer allocation overlaps its range (live allocations never overlap).
 struct ipc_desc {
     hipIpcMemHandle_t h;
     uint64_t off;
@@ -24,6 +24,7 @@ struct ipc_desc {
     uint64_t id;
     uint64_t base;
     uint64_t size;
+    uint64_t pid;
 };
 
 struct p2p_state;  // p2p.cpp
@@ -44,10 +45,6 @@ int comm_export(ompi_amd_comm_t *c, const void *ptr, ipc_desc *d);
 int comm_import(ompi_amd_comm_t *c, int peer, const ipc_desc &d, const char **out, bool pin,
                 void **base);
 void comm_unpin(ompi_amd_comm_t *c, void *base);
-// After a refused IPC open of one of `peer`'s allocations: drain this
-// communicator's kernels and close every unpinned cached mapping of that
-// peer (the runtime then answers a fresh open).
-int comm_drop_peer_mappings(ompi_amd_comm_t *c, int peer);
 // Launch the deferred nonblocking collectives (device work keeps one order).
 int comm_drain(ompi_amd_comm_t *c);
 // Device barrier over every rank of c on stream s (stream-ordered epoch).
@@ -71,6 +68,10 @@ p2p_state *comm_p2p(ompi_amd_comm_t *c);
 int p2p_create(ompi_amd_comm_t *c, const char *name, int rank, int size, int phase,
                p2p_state **out);
 void p2p_unlink(p2p_state *p);
+// Point-to-point parameters / counters ("p2p_*" keys of comm set/get_param);
+// OMPI_AMD_ERR_UNSUPPORTED for a key that is not one of them.
+int p2p_set_param(p2p_state *p, const char *key, int64_t v);
+int p2p_get_param(p2p_state *p, const char *key, int64_t *v);
 void p2p_destroy(p2p_state *p);
 
 }  // namespace ompi_amd

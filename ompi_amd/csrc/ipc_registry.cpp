@@ -1,0 +1,209 @@
+// Process-wide IPC mapping registry (ipc_registry.h).
+#include "ipc_registry.h"
+
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "runtime.h"
+
+namespace ompi_amd {
+
+struct ipc_ref {
+    ipc_alloc a;
+    int device;
+    void *base;      // the mapping in this process
+    int refs = 0;
+    int pins = 0;
+    bool retired = false;  // closed: the exporter freed the allocation
+};
+
+namespace {
+
+std::mutex g_mu;
+std::vector<ipc_ref *> g_live;  // open mappings
+struct user { void *owner; int (*quiesce)(void *); };
+std::vector<user> g_users;
+ipc_stats g_st{};
+
+bool same_handle(const hipIpcMemHandle_t &x, const hipIpcMemHandle_t &y) {
+    return memcmp(&x, &y, sizeof(x)) == 0;
+}
+
+bool same_alloc(const ipc_alloc &x, const ipc_alloc &y) {
+    return x.pid == y.pid && x.id == y.id && x.base == y.base && x.size == y.size &&
+           same_handle(x.h, y.h);
+}
+
+bool trace() {
+    static const bool on = [] {
+        const char *v = getenv("OMPI_AMD_IPC_TRACE");
+        return v && *v == '1';
+    }();
+    return on;
+}
+
+void close_mapping(ipc_ref *r) {
+    const hipError_t e = hipIpcCloseMemHandle(r->base);
+    hip_ignore(e);
+    ++g_st.closes;
+    --g_st.live;
+    if (trace())
+        fprintf(stderr, "[ipc pid %d] close pid %llu id %llu %p+%llu -> %p%s\n", (int)getpid(),
+                (unsigned long long)r->a.pid, (unsigned long long)r->a.id,
+                (void *)(uintptr_t)r->a.base, (unsigned long long)r->a.size, r->base,
+                r->retired ? " (retired)" : "");
+}
+
+}  // namespace
+
+int ipc_map(const ipc_alloc &a, ipc_ref **ref, void **base) {
+    *ref = nullptr;
+    *base = nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return record_hip(hipErrorInvalidDevice, "hipGetDevice (ipc_map)");
+    std::lock_guard<std::mutex> g(g_mu);
+    for (ipc_ref *r : g_live)
+        if (r->device == dev && same_alloc(r->a, a)) {
+            ++r->refs;
+            ++g_st.refs;
+            ++g_st.shared;
+            *ref = r;
+            *base = r->base;
+            return OMPI_AMD_SUCCESS;
+        }
+    // The exporter's live allocations never overlap and never share handle
+    // bytes: a mapping that does either belongs to an allocation it freed.
+    // It must be closed BEFORE the new handle is opened (the runtime would
+    // answer the open with it).  A pinned one is a program error.
+    std::vector<ipc_ref *> stale;
+    for (ipc_ref *r : g_live) {
+        if (r->device != dev || r->a.pid != a.pid) continue;
+        const bool overlap = r->a.base < a.base + a.size && a.base < r->a.base + r->a.size;
+        if (overlap || same_handle(r->a.h, a.h)) stale.push_back(r);
+    }
+    for (ipc_ref *r : stale)
+        if (r->pins > 0) {
+            record_msg("process %llu freed a device buffer (id %llu, %p + %llu) that a persistent "
+                       "operation of this process still maps", (unsigned long long)a.pid,
+                       (unsigned long long)r->a.id, (void *)(uintptr_t)r->a.base,
+                       (unsigned long long)r->a.size);
+            return OMPI_AMD_ERR_BAD_PARAM;
+        }
+    if (!stale.empty()) {
+        // earlier work of any user may still read through these mappings
+        for (const user &u : g_users) {
+            const int rc = u.quiesce(u.owner);
+            if (rc != OMPI_AMD_SUCCESS) return rc;
+        }
+        for (ipc_ref *r : stale) {
+            r->retired = true;
+            close_mapping(r);
+            ++g_st.retired;
+            g_live.erase(std::find(g_live.begin(), g_live.end(), r));
+            if (r->refs == 0) delete r;  // else freed by its last holder's ipc_unmap
+        }
+    }
+    void *m = nullptr;
+    ++g_st.opens;
+    const hipError_t e = hipIpcOpenMemHandle(&m, a.h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        record_msg("hipIpcOpenMemHandle: %s (process %llu buffer id %llu at %p + %llu)",
+                   hipGetErrorString(e), (unsigned long long)a.pid, (unsigned long long)a.id,
+                   (void *)(uintptr_t)a.base, (unsigned long long)a.size);
+        return OMPI_AMD_ERR_HIP;
+    }
+    // The answer must be a new mapping of the advertised allocation: not
+    // inside one the process holds, with the exporter's base and size (the
+    // runtime rounds the mapping up to its 2 MiB page).
+    for (ipc_ref *r : g_live)
+        if ((const char *)m >= (const char *)r->base &&
+            (const char *)m < (const char *)r->base + r->a.size) {
+            // not closed: that could unmap the live mapping it aliases
+            record_msg("hipIpcOpenMemHandle returned %p for process %llu buffer id %llu, which is "
+                       "this process's mapping of buffer id %llu of process %llu",
+                       m, (unsigned long long)a.pid, (unsigned long long)a.id,
+                       (unsigned long long)r->a.id, (unsigned long long)r->a.pid);
+            return OMPI_AMD_ERR_HIP;
+        }
+    void *mb = nullptr;
+    size_t ms = 0;
+    if (hipMemGetAddressRange((hipDeviceptr_t *)&mb, &ms, (hipDeviceptr_t)m) == hipSuccess) {
+        const uint64_t up = (a.size + (2u << 20) - 1) & ~(uint64_t)((2u << 20) - 1);
+        if (mb != m || ms < a.size || ms > up) {
+            hip_ignore(hipIpcCloseMemHandle(m));
+            ++g_st.closes;
+            record_msg("hipIpcOpenMemHandle for process %llu buffer id %llu (%llu bytes) returned "
+                       "a mapping of %zu bytes at %p", (unsigned long long)a.pid,
+                       (unsigned long long)a.id, (unsigned long long)a.size, ms, mb);
+            return OMPI_AMD_ERR_HIP;
+        }
+    } else {
+        (void)hipGetLastError();
+    }
+    auto *r = new ipc_ref;
+    r->a = a;
+    r->device = dev;
+    r->base = m;
+    r->refs = 1;
+    g_live.push_back(r);
+    ++g_st.live;
+    ++g_st.refs;
+    if (trace())
+        fprintf(stderr, "[ipc pid %d] open pid %llu id %llu %p+%llu -> %p\n", (int)getpid(),
+                (unsigned long long)a.pid, (unsigned long long)a.id, (void *)(uintptr_t)a.base,
+                (unsigned long long)a.size, m);
+    *ref = r;
+    *base = m;
+    return OMPI_AMD_SUCCESS;
+}
+
+void ipc_unmap(ipc_ref *r) {
+    if (!r) return;
+    std::lock_guard<std::mutex> g(g_mu);
+    --g_st.refs;
+    if (--r->refs > 0) return;
+    if (!r->retired) {
+        close_mapping(r);
+        g_live.erase(std::find(g_live.begin(), g_live.end(), r));
+    }
+    delete r;
+}
+
+void ipc_pin(ipc_ref *r, int delta) {
+    if (!r) return;
+    std::lock_guard<std::mutex> g(g_mu);
+    r->pins += delta;
+}
+
+bool ipc_retired(const ipc_ref *r) {
+    std::lock_guard<std::mutex> g(g_mu);
+    return r && r->retired;
+}
+
+void *ipc_ref_base(const ipc_ref *r) { return r ? r->base : nullptr; }
+
+void ipc_add_user(void *owner, int (*quiesce)(void *)) {
+    std::lock_guard<std::mutex> g(g_mu);
+    g_users.push_back({owner, quiesce});
+}
+
+void ipc_remove_user(void *owner) {
+    std::lock_guard<std::mutex> g(g_mu);
+    g_users.erase(std::remove_if(g_users.begin(), g_users.end(),
+                                 [&](const user &u) { return u.owner == owner; }),
+                  g_users.end());
+}
+
+ipc_stats ipc_get_stats() {
+    std::lock_guard<std::mutex> g(g_mu);
+    return g_st;
+}
+
+}  // namespace ompi_amd

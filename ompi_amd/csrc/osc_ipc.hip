@@ -39,6 +39,7 @@
 
 #include "../../include/ompi_amd_osc.h"
 #include "comm_internal.h"
+#include "ipc_registry.h"
 #include "op_device.h"
 #include "runtime.h"
 
@@ -358,7 +359,7 @@ struct ompi_amd_win {
     uint64_t peer_bytes[kOscMaxRanks] = {};
     int64_t peer_disp[kOscMaxRanks] = {};
     void *pinned[kOscMaxRanks] = {};
-    void *ctl_opened[kOscMaxRanks] = {};
+    ipc_ref *ctl_ref[kOscMaxRanks] = {};  // peers' control pages (IPC registry references)
     std::vector<hipStream_t> streams;  // every stream an epoch or RMA call ran on (win_free waits)
     int held[kOscMaxRanks] = {};  // outstanding passive lock per target (0 none)
 };
@@ -533,18 +534,11 @@ static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit
             rc = comm_import(c, p, all[p].base, &pb, true, &w->pinned[p]);
             w->peer_base[p] = const_cast<char *>(pb);
         }
-        if (rc == OMPI_AMD_SUCCESS) {
+        if (rc == OMPI_AMD_SUCCESS) {  // one attempt (a refused open is an error)
             void *m = nullptr;
-            hipError_t e = hipIpcOpenMemHandle(&m, all[p].ctl.h, hipIpcMemLazyEnablePeerAccess);
-            if (e != hipSuccess) {  // once more after closing the peer's cached mappings
-                hip_ignore(e);
-                rc = comm_drop_peer_mappings(c, p);
-                if (rc == OMPI_AMD_SUCCESS)
-                    e = hipIpcOpenMemHandle(&m, all[p].ctl.h, hipIpcMemLazyEnablePeerAccess);
-            }
-            if (rc == OMPI_AMD_SUCCESS) rc = record_hip(e, "hipIpcOpenMemHandle (osc control)");
-            w->ctl_opened[p] = m;
-            w->peer_ctl[p] = static_cast<uint32_t *>(m);
+            const ipc_desc &d = all[p].ctl;
+            rc = ipc_map(ipc_alloc{d.h, d.pid, d.id, d.base, d.size}, &w->ctl_ref[p], &m);
+            w->peer_ctl[p] = reinterpret_cast<uint32_t *>(static_cast<char *>(m) + d.off);
         }
     }
     // agree: all mapped (or all give up together)
@@ -555,7 +549,7 @@ static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit
     if (rc != OMPI_AMD_SUCCESS) {
         for (int p = 0; p < w->size; ++p) {
             if (w->pinned[p]) comm_unpin(c, w->pinned[p]);
-            if (w->ctl_opened[p]) hip_ignore(hipIpcCloseMemHandle(w->ctl_opened[p]));
+            ipc_unmap(w->ctl_ref[p]);
         }
         if (w->ctl) hip_ignore(hipFree(w->ctl));
         delete w;
@@ -623,7 +617,7 @@ int ompi_amd_win_free(ompi_amd_win_t *w) {
     if (rc == OMPI_AMD_SUCCESS) rc = brc;
     for (int p = 0; p < w->size; ++p) {
         if (w->pinned[p]) comm_unpin(c, w->pinned[p]);
-        if (w->ctl_opened[p]) hip_ignore(hipIpcCloseMemHandle(w->ctl_opened[p]));
+        ipc_unmap(w->ctl_ref[p]);  // the process's mapping stays while others hold it
     }
     const int brc2 = comm_allgather(c, nullptr, nullptr, 0);  // mappings closed before frees
     if (rc == OMPI_AMD_SUCCESS) rc = brc2;

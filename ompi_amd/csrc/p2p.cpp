@@ -30,6 +30,20 @@
 //            eager protocol does: MPI_Send of a small message never waits
 //            for the receiver.  The cell is reused only after the slot is
 //            DONE.
+//   staged   larger messages are copied into a library-owned send stage
+//            (a pool of exported device buffers, never freed while the
+//            communicator lives) and the receiver pulls from there, so no
+//            peer ever maps an application buffer — the (process, address)
+//            identity of an IPC handle cannot go stale under the
+//            application's frees.  A standard send
+//            completes once staged (ob1 may buffer a standard send too);
+//            MPI_Ssend still completes at the receiver's FIN.  Past the
+//            pool's cap (param p2p_stage_mib), or with p2p_user_ipc = 1, the
+//            receiver maps the send buffer itself (rendezvous, as before).
+//   host     host send buffers always go through a stage (eager cell or
+//            pool: the copy kernel cannot read pageable memory); a receive
+//            into host memory lands in a device receive stage first and is
+//            copied out before it completes.
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
@@ -77,8 +91,24 @@ struct alignas(64) pair_q {
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory atomics");
 static_assert(std::atomic<uint32_t>::is_always_lock_free, "shared-memory atomics");
 
+// A library-owned device buffer of the send-stage pool (exported once) or
+// of the receive-stage pool (local only).
+struct stage {
+    char *buf = nullptr;
+    size_t cap = 0;
+    ipc_desc d{};
+};
+
 struct p2p_state {
     ompi_amd_comm_t *c = nullptr;
+    int64_t timeout_ms = -1;  // param p2p_timeout_ms: -1 the communicator's, 0 none
+    int user_ipc = 0;         // param p2p_user_ipc: large sends map the caller's buffer
+    size_t stage_cap = 1ull << 30;  // param p2p_stage_mib: send-stage pool limit
+    size_t stage_bytes = 0;         //   allocated so far
+    std::vector<stage> send_free, recv_free;
+    struct inflight { int dst; uint64_t seq; stage st; };
+    std::deque<inflight> staged;  // sends whose stage the receiver may still read
+    int64_t staged_sends = 0, direct_sends = 0, host_sends = 0, host_recvs = 0;
     int rank = 0, size = 0;
     char name[256] = {0};
     pair_q *q = nullptr;
@@ -114,6 +144,9 @@ struct ompi_amd_p2p_request {
     msg_slot *slot = nullptr;  // matched message
     void *pinned = nullptr;    // sender mapping held during the copy
     ompi_amd_status_t st{};
+    void *host_dst = nullptr;  // a host receive buffer: the copy lands in `rstage` first
+    stage rstage{};
+    bool has_rstage = false;
 };
 
 namespace ompi_amd {
@@ -121,6 +154,38 @@ namespace ompi_amd {
 static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch())
         .count();
+}
+
+int p2p_set_param(p2p_state *p, const char *key, int64_t v) {
+    if (!p) return OMPI_AMD_ERR_BAD_PARAM;
+    std::lock_guard<std::recursive_mutex> g(p->mu);
+    if (!strcmp(key, "p2p_timeout_ms")) {
+        if (v < -1) return OMPI_AMD_ERR_BAD_PARAM;
+        p->timeout_ms = v;
+    } else if (!strcmp(key, "p2p_user_ipc")) {
+        p->user_ipc = v ? 1 : 0;
+    } else if (!strcmp(key, "p2p_stage_mib")) {
+        if (v < 0) return OMPI_AMD_ERR_BAD_PARAM;
+        p->stage_cap = (size_t)v << 20;
+    } else {
+        return OMPI_AMD_ERR_UNSUPPORTED;  // not a p2p key
+    }
+    return OMPI_AMD_SUCCESS;
+}
+
+int p2p_get_param(p2p_state *p, const char *key, int64_t *v) {
+    if (!p) return OMPI_AMD_ERR_BAD_PARAM;
+    std::lock_guard<std::recursive_mutex> g(p->mu);
+    if (!strcmp(key, "p2p_timeout_ms")) *v = p->timeout_ms;
+    else if (!strcmp(key, "p2p_user_ipc")) *v = p->user_ipc;
+    else if (!strcmp(key, "p2p_stage_mib")) *v = (int64_t)(p->stage_cap >> 20);
+    else if (!strcmp(key, "p2p_stage_bytes")) *v = (int64_t)p->stage_bytes;
+    else if (!strcmp(key, "p2p_staged_sends")) *v = p->staged_sends;
+    else if (!strcmp(key, "p2p_direct_sends")) *v = p->direct_sends;
+    else if (!strcmp(key, "p2p_host_sends")) *v = p->host_sends;
+    else if (!strcmp(key, "p2p_host_recvs")) *v = p->host_recvs;
+    else return OMPI_AMD_ERR_UNSUPPORTED;
+    return OMPI_AMD_SUCCESS;
 }
 
 int p2p_create(ompi_amd_comm_t *c, const char *name, int rank, int size, int phase,
@@ -175,9 +240,76 @@ void p2p_destroy(p2p_state *p) {
     if (!p) return;
     if (p->q) munmap(p->q, p->bytes);
     if (p->eager) hip_ignore(hipFree(p->eager));
+    // the communicator's final rendezvous has passed: no peer reads a stage
+    for (auto &f : p->staged) hip_ignore(hipFree(f.st.buf));
+    for (auto &st : p->send_free) hip_ignore(hipFree(st.buf));
+    for (auto &st : p->recv_free) hip_ignore(hipFree(st.buf));
     if (p->rank == 0) p2p_unlink(p);
     delete p;
 }
+
+// Seconds a host wait may last (0: no limit; the PML glue's blocking calls
+// never time out, MPI semantics).
+static double limit_s(const p2p_state *p) {
+    const int64_t ms = p->timeout_ms < 0 ? comm_timeout_ms(p->c) : p->timeout_ms;
+    return ms == 0 ? 0.0 : (double)ms / 1000.0;
+}
+
+static bool over(const p2p_state *p, double t0) {
+    const double l = limit_s(p);
+    return l > 0 && now_s() - t0 > l;
+}
+
+// size classes: powers of two from 64 KiB (2 MiB multiples past 1 GiB)
+static size_t stage_class(size_t bytes) {
+    if (bytes > (1ull << 30)) return (bytes + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+    size_t c = 64u << 10;
+    while (c < bytes) c <<= 1;
+    return c;
+}
+
+// Send stages whose message the receiver finished (slot DONE or recycled)
+// go back to the pool.  Under p->mu.
+static void reclaim(p2p_state *p) {
+    for (auto it = p->staged.begin(); it != p->staged.end();) {
+        msg_slot &m = p->pair(p->rank, it->dst).slot[it->seq % kSlots];
+        if (m.seq != it->seq || m.state.load(std::memory_order_acquire) == S_DONE) {
+            p->send_free.push_back(it->st);
+            it = p->staged.erase(it);
+        } else {
+            ++it;
+        }
+    }
+}
+
+// The smallest free stage of `pool` that holds `bytes`, or a new one
+// (exported when `exported`); false past the send pool's cap.  Under p->mu.
+static bool take_stage(p2p_state *p, std::vector<stage> &pool, size_t bytes, bool exported,
+                       stage *out) {
+    auto best = pool.end();
+    for (auto it = pool.begin(); it != pool.end(); ++it)
+        if (it->cap >= bytes && (best == pool.end() || it->cap < best->cap)) best = it;
+    if (best != pool.end()) {
+        *out = *best;
+        pool.erase(best);
+        return true;
+    }
+    const size_t cls = stage_class(bytes);
+    if (exported && p->stage_bytes + cls > p->stage_cap) return false;
+    stage st;
+    st.cap = cls;
+    if (exported) {
+        if (comm_alloc_exportable(cls, false, (void **)&st.buf, &st.d) != OMPI_AMD_SUCCESS) return false;
+        p->stage_bytes += cls;
+    } else if (hipMalloc((void **)&st.buf, cls) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    *out = st;
+    return true;
+}
+
+static bool is_device(const void *ptr) { return ompi_amd_is_device_pointer(ptr) != 0; }
 
 static bool tag_ok(int want, int have) { return want == OMPI_AMD_ANY_TAG || want == have; }
 
@@ -239,7 +371,19 @@ static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s
     } else {
         rc = comm_import(p->c, s, m->d, &src, true, &r->pinned);
     }
-    if (rc == OMPI_AMD_SUCCESS) rc = xfer_copy(src, r->buf, n, r->stream);
+    char *dst = static_cast<char *>(r->buf);
+    if (rc == OMPI_AMD_SUCCESS && r->host_dst) {  // lands in a device stage, then to host
+        if (take_stage(p, p->recv_free, n, false, &r->rstage)) {
+            r->has_rstage = true;
+            dst = r->rstage.buf;
+        } else {
+            rc = record_hip(hipErrorOutOfMemory, "p2p receive stage");
+        }
+    }
+    if (rc == OMPI_AMD_SUCCESS) rc = xfer_copy(src, dst, n, r->stream);
+    if (rc == OMPI_AMD_SUCCESS && r->host_dst)
+        rc = record_hip(hipMemcpyAsync(r->host_dst, dst, n, hipMemcpyDeviceToHost, r->stream),
+                        "hipMemcpyAsync (p2p receive to host)");
     if (rc == OMPI_AMD_SUCCESS) {
         if (!r->ev) rc = record_hip(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming),
                                     "hipEventCreate (p2p)");
@@ -289,6 +433,10 @@ static int test_one(ompi_amd_p2p_request *r, bool *done) {
         if (copied) {
             if (r->pinned) comm_unpin(p->c, r->pinned);
             r->pinned = nullptr;
+            if (r->has_rstage) {
+                p->recv_free.push_back(r->rstage);
+                r->has_rstage = false;
+            }
             r->slot->state.store(S_DONE, std::memory_order_release);  // the FIN
             r->done = true;
         }
@@ -298,7 +446,6 @@ static int test_one(ompi_amd_p2p_request *r, bool *done) {
 }
 
 static int wait_one(ompi_amd_p2p_request *r) {
-    const double limit = (double)comm_timeout_ms(r->p->c) / 1000.0;
     const double t0 = now_s();
     unsigned spins = 0;
     for (;;) {
@@ -306,9 +453,9 @@ static int wait_one(ompi_amd_p2p_request *r) {
         const int rc = test_one(r, &done);
         if (done) return rc;
         if (++spins > 64) sched_yield();
-        if (now_s() - t0 > limit) {
+        if (over(r->p, t0)) {
             record_msg("p2p %s timed out after %.1f s (peer %d, tag %d)",
-                       r->is_send ? "send" : "receive", limit,
+                       r->is_send ? "send" : "receive", limit_s(r->p),
                        r->is_send ? r->peer : r->src, r->is_send ? -1 : r->tag);
             return OMPI_AMD_ERR_TIMEOUT;
         }
@@ -362,6 +509,8 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     if (mode < OMPI_AMD_SEND_SYNCHRONOUS || mode > OMPI_AMD_SEND_STANDARD)
         return OMPI_AMD_ERR_BAD_PARAM;
     int rc = record_hip(hipSetDevice(comm_device(c)), "hipSetDevice");
+    const hipStream_t s = as_stream(stream);
+    const bool host = bytes && !is_device(buf);
     const bool eager = bytes <= kEager && mode != OMPI_AMD_SEND_SYNCHRONOUS;  // Ssend: rendezvous
     std::unique_lock<std::recursive_mutex> alloc_guard(p->mu);
     if (rc == OMPI_AMD_SUCCESS && eager && !p->eager) {
@@ -370,10 +519,10 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
         if (rc != OMPI_AMD_SUCCESS) p->eager = nullptr;
     }
     alloc_guard.unlock();
-    // the buffer is read from now on (by the eager copy or the receiver):
+    // the buffer is read from now on (by a staging copy or the receiver):
     // its producers must be done
-    if (rc == OMPI_AMD_SUCCESS)
-        rc = record_hip(hipStreamSynchronize(as_stream(stream)), "hipStreamSynchronize (send)");
+    if (rc == OMPI_AMD_SUCCESS && !host)
+        rc = record_hip(hipStreamSynchronize(s), "hipStreamSynchronize (send)");
     if (rc != OMPI_AMD_SUCCESS) return rc;
     auto *r = new (std::nothrow) ompi_amd_p2p_request;
     if (!r) return OMPI_AMD_ERR_BAD_PARAM;
@@ -385,29 +534,74 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     const uint64_t seq = q.posted.load(std::memory_order_relaxed);
     msg_slot &m = q.slot[seq % kSlots];
     // the ring slot must be free: its previous message completed (DONE) or
-    // was never used; wait (bounded) for the receiver otherwise
-    const double limit = (double)comm_timeout_ms(c) / 1000.0, t0 = now_s();
+    // was never used; wait for the receiver otherwise (bounded only by
+    // p2p_timeout_ms)
+    const double t0 = now_s();
     for (;;) {
-        const uint32_t s = m.state.load(std::memory_order_acquire);
-        if (s == S_FREE || s == S_DONE) break;
+        const uint32_t st = m.state.load(std::memory_order_acquire);
+        if (st == S_FREE || st == S_DONE) break;
         progress(p);  // our own receives keep flowing meanwhile
         sched_yield();
-        if (now_s() - t0 > limit) {
-            record_msg("p2p send to %d: %d messages unmatched for %.1f s", dst, kSlots, limit);
+        if (over(p, t0)) {
+            record_msg("p2p send to %d: %d messages unmatched for %.1f s", dst, kSlots, limit_s(p));
             delete r;
             return OMPI_AMD_ERR_TIMEOUT;
         }
     }
+    reclaim(p);
     const void *src = buf;
+    ipc_desc d{};
+    bool staged = false;
+    auto copy_in = [&](char *to) {
+        const int crc = host ? record_hip(hipMemcpyAsync(to, buf, bytes, hipMemcpyHostToDevice, s),
+                                          "hipMemcpyAsync (p2p send stage)")
+                             : xfer_copy(buf, to, bytes, s);
+        return crc == OMPI_AMD_SUCCESS ? record_hip(hipStreamSynchronize(s), "hipStreamSynchronize (stage)")
+                                       : crc;
+    };
     if (eager && bytes) {  // stage into this slot's cell; the send completes now
         char *cell = p->eager + ((size_t)dst * kSlots + seq % kSlots) * kEager;
-        rc = xfer_copy(buf, cell, bytes, as_stream(stream));
-        if (rc == OMPI_AMD_SUCCESS)
-            rc = record_hip(hipStreamSynchronize(as_stream(stream)), "hipStreamSynchronize (eager)");
+        rc = copy_in(cell);
         src = cell;
+    } else if (bytes && (host || (dst != p->rank && !p->user_ipc))) {
+        stage st;
+        bool got = take_stage(p, p->send_free, bytes, true, &st);
+        if (!got && host) {  // a host buffer cannot be mapped: wait for a stage
+            const double t1 = now_s();
+            while (!got) {
+                progress(p);
+                reclaim(p);
+                got = take_stage(p, p->send_free, bytes, true, &st);
+                if (!got && p->staged.empty()) {  // nothing to wait for: past the cap once
+                    const size_t cap = p->stage_cap;
+                    p->stage_cap = p->stage_bytes + stage_class(bytes);
+                    got = take_stage(p, p->send_free, bytes, true, &st);
+                    p->stage_cap = cap;
+                    if (!got) break;
+                }
+                if (!got) sched_yield();
+                if (!got && over(p, t1)) break;
+            }
+            if (!got) rc = record_hip(hipErrorOutOfMemory, "p2p send stage (host buffer)");
+        }
+        if (got) {
+            rc = copy_in(st.buf);
+            if (rc == OMPI_AMD_SUCCESS) {
+                src = st.buf;
+                d = st.d;
+                staged = true;
+                p->staged.push_back({dst, seq, st});
+                ++p->staged_sends;
+            } else {
+                p->send_free.push_back(st);
+            }
+        }
     }
-    ipc_desc d{};
-    if (rc == OMPI_AMD_SUCCESS && bytes && dst != p->rank) rc = comm_export(c, src, &d);
+    if (host) ++p->host_sends;
+    if (rc == OMPI_AMD_SUCCESS && bytes && dst != p->rank && !staged) {
+        rc = comm_export(c, src, &d);
+        if (!eager) ++p->direct_sends;
+    }
     if (rc != OMPI_AMD_SUCCESS) {
         delete r;
         return rc;
@@ -420,7 +614,8 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     m.state.store(S_POSTED, std::memory_order_release);
     q.posted.store(seq + 1, std::memory_order_release);
     r->seq = seq;
-    r->done = eager;  // the user's buffer is free again
+    // the user's buffer is free again once staged (Ssend: at the FIN)
+    r->done = eager || (staged && mode != OMPI_AMD_SEND_SYNCHRONOUS);
     *out = r;
     return OMPI_AMD_SUCCESS;
 }
@@ -436,6 +631,10 @@ int ompi_amd_irecv(ompi_amd_comm_t *c, void *buf, size_t bytes, int src, int tag
     if (!r) return OMPI_AMD_ERR_BAD_PARAM;
     r->p = p;
     r->buf = buf;
+    if (bytes && !is_device(buf)) {
+        r->host_dst = buf;
+        ++p->host_recvs;
+    }
     r->cap = bytes;
     r->src = src;
     r->tag = tag;
@@ -535,15 +734,15 @@ int ompi_amd_iprobe(ompi_amd_comm_t *c, int src, int tag, int *flag, ompi_amd_st
 }
 
 int ompi_amd_probe(ompi_amd_comm_t *c, int src, int tag, ompi_amd_status_t *st) {
-    if (!c) return OMPI_AMD_ERR_BAD_PARAM;
-    const double limit = (double)comm_timeout_ms(c) / 1000.0, t0 = now_s();
+    if (!c || !comm_p2p(c)) return OMPI_AMD_ERR_BAD_PARAM;
+    const double t0 = now_s();
     for (;;) {
         int flag = 0;
         const int rc = ompi_amd_iprobe(c, src, tag, &flag, st);
         if (rc != OMPI_AMD_SUCCESS || flag) return rc;
         sched_yield();
-        if (now_s() - t0 > limit) {
-            record_msg("probe(%d, %d) timed out after %.1f s", src, tag, limit);
+        if (over(comm_p2p(c), t0)) {
+            record_msg("probe(%d, %d) timed out after %.1f s", src, tag, limit_s(comm_p2p(c)));
             return OMPI_AMD_ERR_TIMEOUT;
         }
     }

@@ -50,7 +50,8 @@ mca_pml_rocm_component_t mca_pml_rocm_component = {
         .pmlm_finalize = rocm_finalize,
     },
     .enable = 1,
-    .timeout_ms = 30000,
+    .timeout_ms = 0,
+    .host_path = 0,
 };
 
 mca_pml_base_module_t mca_pml_rocm_host;
@@ -66,10 +67,18 @@ static int rocm_register(void)
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_pml_rocm_component.enable);
     (void) mca_base_component_var_register(c, "timeout_ms",
-                                           "Device spin limit of a transfer before it fails",
+                                           "Host wait limit of a library transfer (0: none, MPI "
+                                           "semantics)",
                                            MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_pml_rocm_component.timeout_ms);
+    (void) mca_base_component_var_register(c, "host_path",
+                                           "1: host-buffer operations go to the saved PML (the "
+                                           "application never mixes host and device buffers in "
+                                           "one message)",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_pml_rocm_component.host_path);
     return OMPI_SUCCESS;
 }
 
@@ -123,7 +132,8 @@ static int rocm_add_comm(struct ompi_communicator_t *comm)
                                                  -1, &dev)) {
         return OMPI_SUCCESS; /* every rank fails alike (the creation is collective) */
     }
-    (void) ompi_amd_comm_set_param(dev, "timeout_ms", mca_pml_rocm_component.timeout_ms);
+    /* host waits follow MPI: no limit unless the parameter sets one */
+    (void) ompi_amd_comm_set_param(dev, "p2p_timeout_ms", mca_pml_rocm_component.timeout_ms);
     e = (struct rocm_comm *) calloc(1, sizeof(*e));
     if (NULL == e) {
         (void) ompi_amd_comm_destroy(dev);
@@ -177,6 +187,19 @@ static ompi_amd_comm_t *takes(struct ompi_communicator_t *comm, int tag, int pee
     return mca_pml_rocm_comm_of(comm);
 }
 
+/* takes(), and with pml_rocm_host_path the buffer is device memory (a
+ * zero-byte operation counts as host: nothing to move) */
+static ompi_amd_comm_t *takes_buf(struct ompi_communicator_t *comm, int tag, int peer,
+                                  const void *buf, size_t count)
+{
+    ompi_amd_comm_t *dev = takes(comm, tag, peer);
+    if (NULL != dev && mca_pml_rocm_component.host_path &&
+        (0 == count || !ompi_amd_is_device_pointer(buf))) {
+        return NULL;
+    }
+    return dev;
+}
+
 static size_t type_bytes(struct ompi_datatype_t *dtype, size_t count)
 {
     size_t size = 0;
@@ -184,58 +207,52 @@ static size_t type_bytes(struct ompi_datatype_t *dtype, size_t count)
     return size * count;
 }
 
-/* what the library gets for the user's buffer: the buffer itself when it is
- * contiguous device memory, else device staging (packed for a send) */
+/* what the library gets for the user's buffer: the buffer itself when its
+ * layout is contiguous (host or device: the library stages host memory in
+ * its own pooled device buffers), else a host buffer with the packed bytes
+ * (packed here for a send) */
 static int stage_for(mca_pml_rocm_request_t *r, int fill)
 {
     r->bytes = type_bytes(r->dtype, r->count);
     r->stage = NULL;
-    if (0 == r->bytes) return OMPI_SUCCESS;
-    if (ompi_datatype_is_contiguous_memory_layout(r->dtype, (int) r->count) &&
-        ompi_amd_is_device_pointer(r->buf)) {
+    if (0 == r->bytes || ompi_datatype_is_contiguous_memory_layout(r->dtype, (int) r->count))
         return OMPI_SUCCESS;
+    r->stage = malloc(r->bytes);
+    if (NULL == r->stage) return OMPI_ERR_OUT_OF_RESOURCE;
+    if (fill && MPI_SUCCESS != ompi_datatype_sndrcv(r->buf, (int) r->count, r->dtype, r->stage,
+                                                    (int) r->bytes, MPI_BYTE)) {
+        free(r->stage);
+        r->stage = NULL;
+        return OMPI_ERROR;
     }
-    if (OMPI_AMD_SUCCESS != ompi_amd_device_alloc(&r->stage, r->bytes)) return OMPI_ERR_OUT_OF_RESOURCE;
-    if (!fill) return OMPI_SUCCESS;
-    if (ompi_datatype_is_contiguous_memory_layout(r->dtype, (int) r->count)) {
-        return OMPI_AMD_SUCCESS == ompi_amd_memcpy(r->stage, r->buf, r->bytes) ? OMPI_SUCCESS
-                                                                               : OMPI_ERROR;
-    }
-    {
-        char *h = (char *) malloc(r->bytes);
-        int rc = OMPI_ERROR;
-        if (NULL == h) return OMPI_ERR_OUT_OF_RESOURCE;
-        if (MPI_SUCCESS == ompi_datatype_sndrcv(r->buf, (int) r->count, r->dtype, h, (int) r->bytes,
-                                                MPI_BYTE) &&
-            OMPI_AMD_SUCCESS == ompi_amd_memcpy(r->stage, h, r->bytes)) {
-            rc = OMPI_SUCCESS;
-        }
-        free(h);
-        return rc;
-    }
+    return OMPI_SUCCESS;
 }
 
-/* a staged receive's `got` bytes back into the user's buffer */
+/* a packed receive's `got` bytes back into the user's layout (whole
+ * elements: a short message fills a prefix of them) */
 static int unstage_recv(mca_pml_rocm_request_t *r, size_t got)
 {
+    size_t size = 0;
     if (NULL == r->stage || 0 == got) return OMPI_SUCCESS;
-    if (ompi_datatype_is_contiguous_memory_layout(r->dtype, (int) r->count)) {
-        return OMPI_AMD_SUCCESS == ompi_amd_memcpy(r->buf, r->stage, got) ? OMPI_SUCCESS : OMPI_ERROR;
-    }
-    {
-        size_t size = 0;
-        char *h = (char *) malloc(r->bytes);
-        int rc = OMPI_ERROR;
-        (void) ompi_datatype_type_size(r->dtype, &size);
-        if (NULL == h) return OMPI_ERR_OUT_OF_RESOURCE;
-        /* whole elements only (a short message fills a prefix of them) */
-        if (OMPI_AMD_SUCCESS == ompi_amd_memcpy(h, r->stage, got) &&
-            MPI_SUCCESS == ompi_datatype_sndrcv(h, (int) got, MPI_BYTE, r->buf,
-                                                (int) (size ? got / size : 0), r->dtype)) {
-            rc = OMPI_SUCCESS;
-        }
-        free(h);
-        return rc;
+    (void) ompi_datatype_type_size(r->dtype, &size);
+    return MPI_SUCCESS == ompi_datatype_sndrcv(r->stage, (int) got, MPI_BYTE, r->buf,
+                                               (int) (size ? got / size : 0), r->dtype)
+               ? OMPI_SUCCESS
+               : OMPI_ERROR;
+}
+
+static void *lib_buf(mca_pml_rocm_request_t *r) { return NULL != r->stage ? r->stage : r->buf; }
+
+/* Wait for a library request without a time limit, driving opal_progress
+ * (other PML traffic, e.g. the system-tag messages of a collective the peer
+ * is inside, must keep moving: ob1's blocking calls do the same). */
+static int wait_lib(ompi_amd_p2p_request_t *lib, ompi_amd_status_t *s)
+{
+    for (;;) {
+        int fin = 0;
+        const int rc = ompi_amd_p2p_test(lib, &fin, s);
+        if (OMPI_AMD_SUCCESS != rc || fin) return rc;
+        opal_progress();
     }
 }
 
@@ -264,10 +281,8 @@ static int finish(mca_pml_rocm_request_t *r, int rc, const ompi_amd_status_t *s)
     else r->super.req_status.MPI_ERROR = err;
     (void) ompi_amd_p2p_free(r->lib);
     r->lib = NULL;
-    if (NULL != r->stage) {
-        (void) ompi_amd_device_free(r->stage);
-        r->stage = NULL;
-    }
+    free(r->stage);
+    r->stage = NULL;
     return err;
 }
 
@@ -301,6 +316,15 @@ static int rocm_progress(void)
         ++completed;
     }
     return completed;
+}
+
+int mca_pml_rocm_active_count(void)
+{
+    int n = 0;
+    OPAL_THREAD_LOCK(&active_lock);
+    for (mca_pml_rocm_request_t *r = active; NULL != r; r = r->next_active) ++n;
+    OPAL_THREAD_UNLOCK(&active_lock);
+    return n;
 }
 
 static void link_active(mca_pml_rocm_request_t *r)
@@ -338,18 +362,15 @@ static int post(mca_pml_rocm_request_t *r)
     rc = stage_for(r, r->is_send);
     if (OMPI_SUCCESS != rc) return rc;
     if (r->is_send) {
-        rc = ompi_amd_isend(dev, NULL != r->stage ? r->stage : r->buf, r->bytes, r->peer, r->tag,
-                            r->mode, NULL, &r->lib);
+        rc = ompi_amd_isend(dev, lib_buf(r), r->bytes, r->peer, r->tag, r->mode, NULL, &r->lib);
     } else {
-        rc = ompi_amd_irecv(dev, NULL != r->stage ? r->stage : r->buf, r->bytes,
+        rc = ompi_amd_irecv(dev, lib_buf(r), r->bytes,
                             MPI_ANY_SOURCE == r->peer ? OMPI_AMD_ANY_SOURCE : r->peer,
                             MPI_ANY_TAG == r->tag ? OMPI_AMD_ANY_TAG : r->tag, NULL, &r->lib);
     }
     if (OMPI_AMD_SUCCESS != rc) {
-        if (NULL != r->stage) {
-            (void) ompi_amd_device_free(r->stage);
-            r->stage = NULL;
-        }
+        free(r->stage);
+        r->stage = NULL;
         return rocm_err(rc);
     }
     r->super.req_complete = REQUEST_PENDING;
@@ -375,15 +396,17 @@ static int rocm_start_req(size_t count, ompi_request_t **requests)
     return OMPI_SUCCESS;
 }
 
-/* MPI_Request_free: an active transfer is waited for first */
+/* MPI_Request_free: an active transfer is waited for first (no time limit) */
 static int rocm_free_req(ompi_request_t **rptr)
 {
     mca_pml_rocm_request_t *r = (mca_pml_rocm_request_t *) *rptr;
     int rc = OMPI_SUCCESS;
-    if (NULL != r->next_active) unlink_active(r);
+    /* always: the oldest active request is the list's tail (next_active
+     * NULL) and must leave the list before it is released */
+    unlink_active(r);
     if (NULL != r->lib) {
         ompi_amd_status_t s = {0, 0, 0, 0};
-        rc = finish(r, ompi_amd_p2p_wait(r->lib, &s), &s);
+        rc = finish(r, wait_lib(r->lib, &s), &s);
     }
     OMPI_REQUEST_FINI(&r->super);
     OBJ_RELEASE(r);
@@ -432,7 +455,7 @@ static int rocm_isend(const void *buf, size_t count, struct ompi_datatype_t *dty
 {
     mca_pml_rocm_request_t *r;
     int rc;
-    if (NULL == takes(comm, tag, dst))
+    if (NULL == takes_buf(comm, tag, dst, buf, count))
         return mca_pml_rocm_host.pml_isend(buf, count, dtype, dst, tag, mode, comm, request);
     r = new_req(1, (void *) buf, count, dtype, dst, tag, (int) mode, comm, false);
     if (NULL == r) return OMPI_ERR_OUT_OF_RESOURCE;
@@ -450,7 +473,7 @@ static int rocm_irecv(void *buf, size_t count, struct ompi_datatype_t *dtype, in
 {
     mca_pml_rocm_request_t *r;
     int rc;
-    if (NULL == takes(comm, tag, src))
+    if (NULL == takes_buf(comm, tag, src, buf, count))
         return mca_pml_rocm_host.pml_irecv(buf, count, dtype, src, tag, comm, request);
     r = new_req(0, buf, count, dtype, src, tag, 0, comm, false);
     if (NULL == r) return OMPI_ERR_OUT_OF_RESOURCE;
@@ -468,7 +491,7 @@ static int rocm_isend_init(const void *buf, size_t count, struct ompi_datatype_t
                            struct ompi_request_t **request)
 {
     mca_pml_rocm_request_t *r;
-    if (NULL == takes(comm, tag, dst))
+    if (NULL == takes_buf(comm, tag, dst, buf, count))
         return mca_pml_rocm_host.pml_isend_init(buf, count, dtype, dst, tag, mode, comm, request);
     r = new_req(1, (void *) buf, count, dtype, dst, tag, (int) mode, comm, true);
     if (NULL == r) return OMPI_ERR_OUT_OF_RESOURCE;
@@ -480,7 +503,7 @@ static int rocm_irecv_init(void *buf, size_t count, struct ompi_datatype_t *dtyp
                            struct ompi_communicator_t *comm, struct ompi_request_t **request)
 {
     mca_pml_rocm_request_t *r;
-    if (NULL == takes(comm, tag, src))
+    if (NULL == takes_buf(comm, tag, src, buf, count))
         return mca_pml_rocm_host.pml_irecv_init(buf, count, dtype, src, tag, comm, request);
     r = new_req(0, buf, count, dtype, src, tag, 0, comm, true);
     if (NULL == r) return OMPI_ERR_OUT_OF_RESOURCE;
@@ -508,7 +531,9 @@ static int rocm_send(const void *buf, size_t count, struct ompi_datatype_t *dtyp
                      mca_pml_base_send_mode_t mode, struct ompi_communicator_t *comm)
 {
     mca_pml_rocm_request_t r;
-    ompi_amd_comm_t *dev = takes(comm, tag, dst);
+    ompi_amd_comm_t *dev = takes_buf(comm, tag, dst, buf, count);
+    ompi_amd_p2p_request_t *lib = NULL;
+    ompi_amd_status_t s = {0, 0, 0, 0};
     int rc;
     if (NULL == dev) return mca_pml_rocm_host.pml_send(buf, count, dtype, dst, tag, mode, comm);
     memset(&r, 0, sizeof(r));
@@ -517,9 +542,12 @@ static int rocm_send(const void *buf, size_t count, struct ompi_datatype_t *dtyp
     r.dtype = dtype;
     rc = stage_for(&r, 1);
     if (OMPI_SUCCESS != rc) return rc;
-    rc = rocm_err(ompi_amd_send(dev, NULL != r.stage ? r.stage : buf, r.bytes, dst, tag, (int) mode,
-                                NULL));
-    if (NULL != r.stage) (void) ompi_amd_device_free(r.stage);
+    rc = rocm_err(ompi_amd_isend(dev, lib_buf(&r), r.bytes, dst, tag, (int) mode, NULL, &lib));
+    if (OMPI_SUCCESS == rc) {
+        rc = rocm_err(wait_lib(lib, &s));
+        (void) ompi_amd_p2p_free(lib);
+    }
+    free(r.stage);
     return rc;
 }
 
@@ -528,7 +556,8 @@ static int rocm_recv(void *buf, size_t count, struct ompi_datatype_t *dtype, int
 {
     mca_pml_rocm_request_t r;
     ompi_amd_status_t s = {0, 0, 0, 0};
-    ompi_amd_comm_t *dev = takes(comm, tag, src);
+    ompi_amd_comm_t *dev = takes_buf(comm, tag, src, buf, count);
+    ompi_amd_p2p_request_t *lib = NULL;
     int rc;
     if (NULL == dev) return mca_pml_rocm_host.pml_recv(buf, count, dtype, src, tag, comm, status);
     memset(&r, 0, sizeof(r));
@@ -537,15 +566,21 @@ static int rocm_recv(void *buf, size_t count, struct ompi_datatype_t *dtype, int
     r.dtype = dtype;
     rc = stage_for(&r, 0);
     if (OMPI_SUCCESS != rc) return rc;
-    rc = rocm_err(ompi_amd_recv(dev, NULL != r.stage ? r.stage : buf, r.bytes,
-                                MPI_ANY_SOURCE == src ? OMPI_AMD_ANY_SOURCE : src,
-                                MPI_ANY_TAG == tag ? OMPI_AMD_ANY_TAG : tag, NULL, &s));
+    rc = rocm_err(ompi_amd_irecv(dev, lib_buf(&r), r.bytes,
+                                 MPI_ANY_SOURCE == src ? OMPI_AMD_ANY_SOURCE : src,
+                                 MPI_ANY_TAG == tag ? OMPI_AMD_ANY_TAG : tag, NULL, &lib));
+    if (OMPI_SUCCESS == rc) {
+        rc = rocm_err(wait_lib(lib, &s));
+        (void) ompi_amd_p2p_free(lib);
+    }
     if (OMPI_SUCCESS == rc) rc = unstage_recv(&r, s.bytes);
-    if (NULL != r.stage) (void) ompi_amd_device_free(r.stage);
+    free(r.stage);
     fill_status(status, &s, rc);
     return rc;
 }
 
+/* With pml_rocm_host_path a message may arrive on either engine: a probe
+ * asks the library first, then the saved PML. */
 static int rocm_iprobe(int src, int tag, struct ompi_communicator_t *comm, int *matched,
                        ompi_status_public_t *status)
 {
@@ -556,33 +591,37 @@ static int rocm_iprobe(int src, int tag, struct ompi_communicator_t *comm, int *
     rc = rocm_err(ompi_amd_iprobe(dev, MPI_ANY_SOURCE == src ? OMPI_AMD_ANY_SOURCE : src,
                                   MPI_ANY_TAG == tag ? OMPI_AMD_ANY_TAG : tag, matched, &s));
     if (OMPI_SUCCESS == rc && *matched) fill_status(status, &s, OMPI_SUCCESS);
+    if (OMPI_SUCCESS == rc && !*matched && mca_pml_rocm_component.host_path)
+        return mca_pml_rocm_host.pml_iprobe(src, tag, comm, matched, status);
     return rc;
 }
 
+/* no time limit: iprobe + opal_progress until a message is there */
 static int rocm_probe(int src, int tag, struct ompi_communicator_t *comm, ompi_status_public_t *status)
 {
-    ompi_amd_status_t s = {0, 0, 0, 0};
-    ompi_amd_comm_t *dev = takes(comm, tag, src);
-    int rc;
-    if (NULL == dev) return mca_pml_rocm_host.pml_probe(src, tag, comm, status);
-    rc = rocm_err(ompi_amd_probe(dev, MPI_ANY_SOURCE == src ? OMPI_AMD_ANY_SOURCE : src,
-                                 MPI_ANY_TAG == tag ? OMPI_AMD_ANY_TAG : tag, &s));
-    if (OMPI_SUCCESS == rc) fill_status(status, &s, OMPI_SUCCESS);
-    return rc;
+    if (NULL == takes(comm, tag, src)) return mca_pml_rocm_host.pml_probe(src, tag, comm, status);
+    for (;;) {
+        int matched = 0;
+        const int rc = rocm_iprobe(src, tag, comm, &matched, status);
+        if (OMPI_SUCCESS != rc || matched) return rc;
+        opal_progress();
+    }
 }
 
 /* matched probes of library traffic are not provided */
 static int rocm_improbe(int src, int tag, struct ompi_communicator_t *comm, int *matched,
                         struct ompi_message_t **message, ompi_status_public_t *status)
 {
-    if (NULL != takes(comm, tag, src)) return OMPI_ERR_NOT_SUPPORTED;
+    if (NULL != takes(comm, tag, src) && !mca_pml_rocm_component.host_path)
+        return OMPI_ERR_NOT_SUPPORTED;
     return mca_pml_rocm_host.pml_improbe(src, tag, comm, matched, message, status);
 }
 
 static int rocm_mprobe(int src, int tag, struct ompi_communicator_t *comm,
                        struct ompi_message_t **message, ompi_status_public_t *status)
 {
-    if (NULL != takes(comm, tag, src)) return OMPI_ERR_NOT_SUPPORTED;
+    if (NULL != takes(comm, tag, src) && !mca_pml_rocm_component.host_path)
+        return OMPI_ERR_NOT_SUPPORTED;
     return mca_pml_rocm_host.pml_mprobe(src, tag, comm, message, status);
 }
 

@@ -11,14 +11,20 @@
  *
  * What goes through the library: user-tag traffic (tag >= 0, and
  * MPI_ANY_TAG receives / probes) on a node-local intra-communicator of 2..16
- * ranks for which pml_add_comm created a library communicator.  The rule
- * depends on the communicator and the tag only — never on buffer residency,
- * which MPI lets differ between sender and receiver — so both ends of every
- * message take the same path: host buffers and non-contiguous datatypes are
- * staged (packed with ompi_datatype_sndrcv) into device memory.  Negative
+ * ranks for which pml_add_comm created a library communicator.  By default
+ * the rule depends on the communicator and the tag only — never on buffer
+ * residency, which MPI lets differ between sender and receiver — so both
+ * ends of every message meet in one matching engine.  The library takes
+ * host buffers itself (pooled device stages, no allocation or export per
+ * message); non-contiguous datatypes are packed on the host first.
+ * pml_rocm_host_path = 1 sends every host-buffer operation to the saved PML
+ * instead (zero library calls for host traffic) for applications whose
+ * senders and receivers always agree on residency: a host-buffer send
+ * matched by a device-buffer receive would then never meet it.  Negative
  * (system) tags, used by the collectives' own messages, and MPI_PROC_NULL
  * stay on the saved PML.  Matched probes (improbe / mprobe / imrecv / mrecv)
- * of library traffic are refused (OMPI_ERR_NOT_SUPPORTED).
+ * of library traffic are refused (OMPI_ERR_NOT_SUPPORTED).  Blocking calls
+ * never time out (they drive opal_progress while they wait, as ob1 does).
  */
 #ifndef MCA_PML_ROCM_H
 #define MCA_PML_ROCM_H
@@ -38,7 +44,8 @@ BEGIN_C_DECLS
 typedef struct mca_pml_rocm_component_t {
     mca_pml_base_component_2_0_0_t super;
     int enable;          /* pml_rocm_enable (1): interpose at close */
-    int timeout_ms;      /* pml_rocm_timeout_ms: device spin limit of a transfer */
+    int timeout_ms;      /* pml_rocm_timeout_ms: host wait limit (0, the default: none) */
+    int host_path;       /* pml_rocm_host_path: 1 = host buffers to the saved PML */
 } mca_pml_rocm_component_t;
 
 OMPI_MODULE_DECLSPEC extern mca_pml_rocm_component_t mca_pml_rocm_component;
@@ -60,7 +67,8 @@ typedef struct mca_pml_rocm_request_t {
     struct ompi_datatype_t *dtype;
     int peer, tag, mode;
     struct ompi_communicator_t *comm;
-    /* staging (NULL: the user buffer itself goes to the library) */
+    /* host packing of a non-contiguous datatype (NULL: the user buffer
+     * itself goes to the library, host or device) */
     void *stage;
     size_t bytes;
     struct mca_pml_rocm_request_t *next_active;
@@ -70,6 +78,8 @@ OBJ_CLASS_DECLARATION(mca_pml_rocm_request_t);
 
 /* library communicator of `comm`, or NULL when pml/rocm does not take it */
 ompi_amd_comm_t *mca_pml_rocm_comm_of(struct ompi_communicator_t *comm);
+/* requests on the active list (started, not yet completed; diagnostics) */
+int mca_pml_rocm_active_count(void);
 
 END_C_DECLS
 

@@ -277,8 +277,7 @@ def case_free_realloc(comm, rank, n, count, salt):
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
         dist.barrier()  # every rank freed before anyone allocates again
-    msgs.append(f"stale mappings closed so far: {comm.get_param('stale_closed')}, "
-                f"same handle bytes: {comm.get_param('stale_same_handle')}, "
+    msgs.append(f"mappings retired so far (exporter freed them): {comm.get_param('ipc_retired')}, "
                 f"recycled handles shadowed: {comm.get_param('recycled_exports')}")
     return len(msgs) == 1, "; ".join(msgs)
 
@@ -922,9 +921,9 @@ def main():
         # barrier epochs diverge when ranks launched different device work
         report(rank, n, {"rank": rank, "case": name, "ok": bool(ok), "msg": msg,
                          "state": {k: comm.get_param(k) for k in (
-                             "epoch", "shadowed", "recycled_exports", "stale_closed", "exports_new",
-                             "imports_new", "imports", "landing_bytes", "aliased_opens", "boot_calls", "ipc_reopens", "memcpy_token_mismatch",
-                             "ipc_local_reopens", "size_mismatch_opens")}})
+                             "epoch", "shadowed", "recycled_exports", "exports_new", "imports_new",
+                             "imports", "landing_bytes", "boot_calls", "memcpy_token_mismatch",
+                             "ipc_opens", "ipc_closes", "ipc_shared", "ipc_retired", "ipc_live")}})
         ok_all &= bool(ok)
     # zero-copy disabled: everything staged through the scratch
     if ok_all and not only and not os.environ.get("COLL_HEADLINE"):

@@ -11,10 +11,15 @@
  *   every call reaches ob1.
  *   GPU (HARNESS_GPU=1): a ring of isend/irecv on device buffers (0 B,
  *   eager, rendezvous, 8 MiB), byte-exact; blocking send/recv from host
- *   memory (staged); a non-contiguous receive type (packed, gaps kept);
- *   ANY_SOURCE / ANY_TAG status; iprobe / probe; persistent send/recv
- *   started three times; truncation; negative (system) tags and PROC_NULL
- *   reach ob1; matched probes of library traffic are refused.
+ *   memory (the library's pooled stages: no allocation per message); a
+ *   non-contiguous receive type (packed, gaps kept); ANY_SOURCE / ANY_TAG
+ *   status; iprobe / probe; persistent send/recv started three times;
+ *   truncation; negative (system) tags and PROC_NULL reach ob1; matched
+ *   probes of library traffic are refused; MPI_Request_free of an in-flight
+ *   Ssend and irecv leaves no request on the active list; a sender that
+ *   frees and reallocates its device buffer between messages (staged
+ *   default and p2p_user_ipc = 1) stays byte-exact; pml_rocm_host_path = 1
+ *   sends host-buffer traffic to ob1 with zero library calls.
  *
  * usage: pml_harness <segment-name-hex> <rank> <size>; prints "ok" / "ok gpu".
  */
@@ -330,6 +335,117 @@ int main(int argc, char **argv)
               "matched probe of library traffic refused");
         CHECK(mca_pml.pml_improbe(left, -20, &comm, &m, &msg, NULL) == OMPI_SUCCESS && ob1_calls == 3,
               "matched probe of a system tag reaches ob1");
+    }
+    /* 8. MPI_Request_free of active requests (the oldest active request is
+     * the list's tail): an in-flight Ssend and irecv, freed, leave the list */
+    {
+        const size_t n = 65536;
+        unsigned char *h = malloc(n), *got = malloc(n);
+        void *ds, *dr;
+        ompi_request_t *rs = NULL, *rr = NULL;
+        for (size_t i = 0; i < n; ++i) h[i] = pat(g_rank, i, 60);
+        memset(got, 0, n);
+        CHECK(harness_dev_alloc_copy(&ds, h, n) == 0 && harness_dev_alloc_copy(&dr, got, n) == 0, "dev");
+        CHECK(mca_pml.pml_irecv(dr, n, &dbyte, left, 60, &comm, &rr) == OMPI_SUCCESS, "irecv");
+        CHECK(mca_pml.pml_isend(ds, n, &dbyte, right, 60, MCA_PML_BASE_SEND_SYNCHRONOUS, &comm, &rs) ==
+                  OMPI_SUCCESS, "issend");
+        CHECK(mca_pml_rocm_active_count() == 2, "two active requests (%d)", mca_pml_rocm_active_count());
+        CHECK(rr->req_free(&rr) == OMPI_SUCCESS, "free active irecv");
+        CHECK(rs->req_free(&rs) == OMPI_SUCCESS, "free active issend");
+        CHECK(mca_pml_rocm_active_count() == 0, "freed requests left on the active list (%d)",
+              mca_pml_rocm_active_count());
+        opal_progress();
+        CHECK(harness_dev_copy_back(got, dr, n) == 0, "copy back");
+        for (size_t i = 0; i < n; ++i) CHECK(got[i] == pat(left, i, 60), "freed irecv byte %zu", i);
+        harness_dev_free(ds);
+        harness_dev_free(dr);
+        free(h);
+        free(got);
+    }
+    /* 9. the sender frees and reallocates its device buffer between
+     * messages: staged (default: the receiver reads library memory) and
+     * p2p_user_ipc = 1 (the receiver maps the send buffer; the IPC registry
+     * retires the freed allocation's mapping) */
+    {
+        ompi_amd_comm_t *dev = mca_pml_rocm_comm_of(&comm);
+        const size_t n = 8u << 20;
+        unsigned char *h = malloc(n), *got = malloc(n);
+        int64_t staged0 = 0, staged1 = 0;
+        for (int mode = 0; mode < 2; ++mode) {
+            CHECK(ompi_amd_comm_set_param(dev, "p2p_user_ipc", mode) == OMPI_AMD_SUCCESS, "p2p_user_ipc");
+            (void) ompi_amd_comm_get_param(dev, "p2p_staged_sends", &staged0);
+            for (int it = 0; it < 3; ++it) {
+                void *ds, *dr;
+                ompi_status_public_t st;
+                for (size_t i = 0; i < n; i += 4099) h[i] = pat(g_rank, i, 70 + it + 3 * mode);
+                memset(got, 0, n);
+                CHECK(harness_dev_alloc_copy(&ds, h, n) == 0 && harness_dev_alloc_copy(&dr, got, n) == 0,
+                      "dev");
+                if (g_rank % 2 == 0) {
+                    CHECK(mca_pml.pml_send(ds, n, &dbyte, right, 70, MCA_PML_BASE_SEND_STANDARD, &comm) ==
+                              OMPI_SUCCESS, "send");
+                    CHECK(mca_pml.pml_recv(dr, n, &dbyte, left, 70, &comm, &st) == OMPI_SUCCESS, "recv");
+                } else {
+                    CHECK(mca_pml.pml_recv(dr, n, &dbyte, left, 70, &comm, &st) == OMPI_SUCCESS, "recv");
+                    CHECK(mca_pml.pml_send(ds, n, &dbyte, right, 70, MCA_PML_BASE_SEND_STANDARD, &comm) ==
+                              OMPI_SUCCESS, "send");
+                }
+                CHECK(harness_dev_copy_back(got, dr, n) == 0, "copy back");
+                for (size_t i = 0; i < n; i += 4099)
+                    CHECK(got[i] == pat(left, i, 70 + it + 3 * mode), "mode %d round %d byte %zu", mode, it, i);
+                harness_dev_free(ds);  /* freed while the peer may still hold a mapping of it */
+                harness_dev_free(dr);
+            }
+            (void) ompi_amd_comm_get_param(dev, "p2p_staged_sends", &staged1);
+            CHECK(mode == 0 ? staged1 - staged0 == 3 : staged1 == staged0,
+                  "mode %d: %lld staged sends", mode, (long long) (staged1 - staged0));
+        }
+        (void) ompi_amd_comm_set_param(dev, "p2p_user_ipc", 0);
+        free(h);
+        free(got);
+    }
+    /* 10. pml_rocm_host_path = 1: host-buffer operations reach ob1 and make
+     * no library call; device buffers still go to the library */
+    {
+        ompi_amd_comm_t *dev = mca_pml_rocm_comm_of(&comm);
+        int64_t hs0 = 0, hs1 = 0, hr0 = 0, hr1 = 0;
+        int x = g_rank, y = -1, m = 0;
+        ompi_request_t *r = NULL;
+        mca_pml_rocm_component.host_path = 1;
+        (void) ompi_amd_comm_get_param(dev, "p2p_host_sends", &hs0);
+        (void) ompi_amd_comm_get_param(dev, "p2p_host_recvs", &hr0);
+        ob1_calls = 0;
+        CHECK(mca_pml.pml_send(&x, 1, &dint, right, 80, MCA_PML_BASE_SEND_STANDARD, &comm) == OMPI_SUCCESS,
+              "host send");
+        CHECK(mca_pml.pml_recv(&y, 1, &dint, left, 80, &comm, NULL) == OMPI_SUCCESS, "host recv");
+        CHECK(mca_pml.pml_isend(&x, 1, &dint, right, 81, MCA_PML_BASE_SEND_STANDARD, &comm, &r) ==
+                  OMPI_SUCCESS && r == &ob1_req, "host isend");
+        CHECK(ob1_calls == 3, "host traffic reaches ob1 (%d calls)", ob1_calls);
+        (void) ompi_amd_comm_get_param(dev, "p2p_host_sends", &hs1);
+        (void) ompi_amd_comm_get_param(dev, "p2p_host_recvs", &hr1);
+        CHECK(hs1 == hs0 && hr1 == hr0, "library calls for host traffic");
+        CHECK(mca_pml.pml_iprobe(left, 99, &comm, &m, NULL) == OMPI_SUCCESS && m == 0 && ob1_calls == 4,
+              "probe asks both engines");
+        {
+            void *dv, *dw;
+            unsigned char v = (unsigned char) (g_rank + 1), w = 0;
+            CHECK(harness_dev_alloc_copy(&dv, &v, 1) == 0 && harness_dev_alloc_copy(&dw, &w, 1) == 0, "dev");
+            ob1_calls = 0;
+            if (g_rank % 2 == 0) {
+                CHECK(mca_pml.pml_send(dv, 1, &dbyte, right, 82, MCA_PML_BASE_SEND_STANDARD, &comm) ==
+                          OMPI_SUCCESS, "device send");
+                CHECK(mca_pml.pml_recv(dw, 1, &dbyte, left, 82, &comm, NULL) == OMPI_SUCCESS, "device recv");
+            } else {
+                CHECK(mca_pml.pml_recv(dw, 1, &dbyte, left, 82, &comm, NULL) == OMPI_SUCCESS, "device recv");
+                CHECK(mca_pml.pml_send(dv, 1, &dbyte, right, 82, MCA_PML_BASE_SEND_STANDARD, &comm) ==
+                          OMPI_SUCCESS, "device send");
+            }
+            CHECK(ob1_calls == 0, "device traffic stays on the library under host_path");
+            CHECK(harness_dev_copy_back(&w, dw, 1) == 0 && w == (unsigned char) (left + 1), "device payload");
+            harness_dev_free(dv);
+            harness_dev_free(dw);
+        }
+        mca_pml_rocm_component.host_path = 0;
     }
     CHECK(mca_pml.pml_del_comm(&comm) == OMPI_SUCCESS && mca_pml_rocm_comm_of(&comm) == NULL, "del_comm");
     printf("ok gpu\n");
