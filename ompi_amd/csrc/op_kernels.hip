@@ -207,8 +207,8 @@ static fallback_slot g_fallback[OMPI_AMD_OP_COUNT][OMPI_AMD_TYPE_COUNT];
 
 // kind: 1 = all device, 0 = all host, -1 = mixed
 static int buffers_kind(const void *a, const void *b, const void *c) {
-    const int da = ompi_amd_is_device_pointer(a), db = ompi_amd_is_device_pointer(b);
-    const int dc = c ? ompi_amd_is_device_pointer(c) : db;
+    const int da = device_pointer_cached(a), db = device_pointer_cached(b);
+    const int dc = c ? device_pointer_cached(c) : db;
     if (da && db && dc) return 1;
     if (!da && !db && !dc) return 0;
     return -1;

@@ -97,6 +97,34 @@ int ompi_amd_is_device_pointer(const void *ptr) {
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
+}  // extern "C"
+
+namespace ompi_amd {
+
+// The op handlers classify every operand on every call (ompi_op_reduce has
+// no residency hint).  A pure-host reduction (op/avx or op/base underneath)
+// should not pay a runtime pointer query per operand per call: each thread
+// remembers the last 8 host regions it classified, at 2 MiB granularity.
+// Device allocations live in the GPU's own virtual-address aperture, never
+// in a range that was host memory, so a granule once seen as host stays
+// host; device pointers are always queried (the device path's cost is the
+// kernel anyway).
+int device_pointer_cached(const void *p) {
+    static thread_local uintptr_t host_gran[8];  // granule + 1 (0 = empty)
+    static thread_local unsigned next;
+    if (!p) return 0;
+    const uintptr_t g = ((uintptr_t)p >> 21) + 1;
+    for (uintptr_t h : host_gran)
+        if (h == g) return 0;
+    const int d = ompi_amd_is_device_pointer(p);
+    if (!d) host_gran[next++ & 7] = g;
+    return d;
+}
+
+}  // namespace ompi_amd
+
+extern "C" {
+
 int ompi_amd_memcpy_async(void *dst, const void *src, size_t bytes, void *stream) {
     if (bytes == 0) return OMPI_AMD_SUCCESS;
     if (!dst || !src) return OMPI_AMD_ERR_BAD_PARAM;

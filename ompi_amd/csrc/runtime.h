@@ -33,6 +33,10 @@ inline hipStream_t as_stream(void *s) {
 }
 
 int op_set_max_blocks(int64_t v);
+// ompi_amd_is_device_pointer with a per-thread cache of host regions (op
+// handlers: a pure-host call makes no runtime query once its buffers' 2 MiB
+// granules are known)
+int device_pointer_cached(const void *p);
 int op_launch(int op, int type, bool three, const void *x, const void *y, void *dst,
               size_t n, hipStream_t s);
 

@@ -6,10 +6,13 @@
  * For each intrinsic MPI_Op the query builds one module whose slot i is
  * libompi_amd's handler when BOTH op/base and the library have slot i
  * (op_base_op_select.c:182-204 requires the NULL pattern to stay op/base's;
- * NULL = keep the lower-priority handler).  The slot's current handler —
- * op/base's, installed before any component is queried
- * (op_base_op_select.c:113-122) — is registered with the library as the
- * host-buffer fallback.
+ * NULL = keep the lower-priority handler).  The host-buffer fallback of a
+ * slot is captured in the module's opm_enable, not in the query: the base
+ * queries every component first (check_components, :133) and then enables
+ * and installs them in ascending priority (:137-178), so at op/rocm's
+ * enable the slot already holds whatever a lower-priority component (op/avx
+ * at 50) installed over op/base — host reductions keep that handler and
+ * its semantics.
  */
 #include "ompi_config.h"
 
@@ -97,6 +100,29 @@ static int rocm_component_init_query(bool enable_progress_threads,
     return OMPI_SUCCESS;
 }
 
+/* opm_enable (op_base_op_select.c:142-150): the slots this module takes
+ * hold the handler the lower-priority components left there; that handler
+ * (and its module, retained for as long as the library may call it) is
+ * what host buffers go to. */
+static int rocm_module_enable(struct ompi_op_base_module_1_0_0_t *module, struct ompi_op_t *op)
+{
+    int i;
+    for (i = 0; i < OMPI_OP_BASE_TYPE_MAX; ++i) {
+        ompi_op_base_module_t *m2, *m3;
+        if (NULL == module->opm_fns[i] && NULL == module->opm_3buff_fns[i]) continue;
+        m2 = op->o_func.intrinsic.modules[i];
+        m3 = op->o_3buff_intrinsic.modules[i];
+        if (NULL != m2) OBJ_RETAIN(m2);
+        if (NULL != m3) OBJ_RETAIN(m3);
+        (void) ompi_amd_op_set_fallback(op->o_f_to_c_index, i,
+                                        (ompi_amd_op_handler_fn_t) op->o_func.intrinsic.fns[i],
+                                        (struct ompi_op_base_module_1_0_0_t *) m2,
+                                        (ompi_amd_op_3buff_handler_fn_t) op->o_3buff_intrinsic.fns[i],
+                                        (struct ompi_op_base_module_1_0_0_t *) m3);
+    }
+    return OMPI_SUCCESS;
+}
+
 static struct ompi_op_base_module_1_0_0_t *
 rocm_component_op_query(struct ompi_op_t *op, int *priority)
 {
@@ -128,19 +154,8 @@ rocm_component_op_query(struct ompi_op_t *op, int *priority)
             module->opm_3buff_fns[i] = (ompi_op_base_3buff_handler_fn_t) row3[i];
             ++used;
         }
-        if (NULL != module->opm_fns[i] || NULL != module->opm_3buff_fns[i]) {
-            /* host buffers in this slot go back to op/base */
-            ompi_op_base_module_t *m2 = op->o_func.intrinsic.modules[i];
-            ompi_op_base_module_t *m3 = op->o_3buff_intrinsic.modules[i];
-            if (NULL != m2) OBJ_RETAIN(m2);
-            if (NULL != m3) OBJ_RETAIN(m3);
-            (void) ompi_amd_op_set_fallback(op->o_f_to_c_index, i,
-                                            (ompi_amd_op_handler_fn_t) base2,
-                                            (struct ompi_op_base_module_1_0_0_t *) m2,
-                                            (ompi_amd_op_3buff_handler_fn_t) base3,
-                                            (struct ompi_op_base_module_1_0_0_t *) m3);
-        }
     }
+    module->opm_enable = rocm_module_enable;
     if (0 == used) {
         OBJ_RELEASE(module);
         return NULL;

@@ -1,20 +1,26 @@
 /*
  * TEST HARNESS ONLY.  Drives ompi_amd/mca/op/rocm/op_rocm_component.c the
  * way the op framework does (op_base_op_select.c:90-211): install op/base's
- * handlers, query the component, copy every non-NULL slot of its module over
- * them, run the NULL-pattern sanity check, then reduce through the
- * resulting op->o_func table like ompi_op_reduce (op.h:585-587).
+ * handlers, query EVERY component (an op/avx stand-in at priority 50 and
+ * op/rocm at 60) before enabling any, then in ascending priority call each
+ * module's opm_enable and copy its non-NULL slots over the table, run the
+ * NULL-pattern sanity check, and reduce through the resulting op->o_func
+ * table like ompi_op_reduce (op.h:585-587).
  *
  * op/base is played by the CPU oracle (oracle/liboracle.so, the C
- * restatement of op_base_functions.c).  Host buffers must come back through
- * the registered fallback; with HARNESS_GPU=1 device buffers must run the
- * HIP handler.  Results are compared with the oracle.  Prints "ok".
+ * restatement of op_base_functions.c); the op/avx stand-in installs its own
+ * SUM FLOAT handler (also the oracle, counted apart).  Host buffers must come
+ * back through the handler op/avx installed (op/rocm's fallback is captured
+ * at enable, after op/avx's slots went in), never op/base's; with
+ * HARNESS_GPU=1 device buffers must run the HIP handler.  Results are
+ * compared with the oracle.  Prints "ok".
  */
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include "ompi/constants.h"
 #include "ompi/op/op.h"
 #include "../../oracle/oracle.h"
 #include "ompi_amd.h"
@@ -48,11 +54,37 @@ extern ompi_op_base_component_1_0_0_t mca_op_rocm_component;
         base_calls++;                                                             \
         orc_op_3buff(OPC, T, a, b, o, (size_t) *n);                               \
     }
-static int base_calls = 0;
+static int base_calls = 0, avx_calls = 0;
 BASE2(ORC_OP_SUM, ORC_T_FLOAT, base_sum_float)
 BASE3(ORC_OP_SUM, ORC_T_FLOAT, base3_sum_float)
 BASE2(ORC_OP_MAXLOC, ORC_T_DOUBLE_INT, base_maxloc_double_int)
 BASE3(ORC_OP_MAXLOC, ORC_T_DOUBLE_INT, base3_maxloc_double_int)
+
+/* the op/avx stand-in's SUM FLOAT handlers (priority 50, below op/rocm) */
+static void avx_sum_float(const void *in, void *inout, int *n, struct ompi_datatype_t **d,
+                          ompi_op_base_module_t *m)
+{
+    (void) d; (void) m;
+    avx_calls++;
+    orc_op_2buff(ORC_OP_SUM, ORC_T_FLOAT, in, inout, (size_t) *n);
+}
+static void avx3_sum_float(const void *a, const void *b, void *o, int *n,
+                           struct ompi_datatype_t **d, ompi_op_base_module_t *m)
+{
+    (void) d; (void) m;
+    avx_calls++;
+    orc_op_3buff(ORC_OP_SUM, ORC_T_FLOAT, a, b, o, (size_t) *n);
+}
+static ompi_op_base_module_t *avx_query(ompi_op_t *op, int *prio)
+{
+    ompi_op_base_module_t *m;
+    if (op->o_f_to_c_index != ORC_OP_SUM) return NULL;
+    m = OBJ_NEW(ompi_op_base_module_t);
+    m->opm_fns[ORC_T_FLOAT] = avx_sum_float;
+    m->opm_3buff_fns[ORC_T_FLOAT] = avx3_sum_float;
+    *prio = 50;
+    return m;
+}
 
 /* present in op/base but never expected to be called here */
 static void base_other(const void *a, void *b, int *n, struct ompi_datatype_t **d,
@@ -102,18 +134,31 @@ static void select_op(ompi_op_t *op, int opidx, ompi_op_base_module_t *base)
         op->o_func.intrinsic.fns[ORC_T_DOUBLE_INT] = base_maxloc_double_int;
         op->o_3buff_intrinsic.fns[ORC_T_DOUBLE_INT] = base3_maxloc_double_int;
     }
-    m = mca_op_rocm_component.opc_op_query(op, &prio);
-    CHECK(m != NULL && prio == 60, "query op %d", opidx);
-    /* op_base_op_select.c:137-178: copy non-NULL slots */
-    for (i = 0; i < OMPI_OP_BASE_TYPE_MAX; ++i) {
-        if (m->opm_fns[i]) {
-            op->o_func.intrinsic.fns[i] = m->opm_fns[i];
-            op->o_func.intrinsic.modules[i] = m;
+    /* check_components (:133): every component is queried first */
+    {
+        int pa = -1;
+        ompi_op_base_module_t *ma = avx_query(op, &pa), *order[2];
+        int k, nm = 0;
+        m = mca_op_rocm_component.opc_op_query(op, &prio);
+        CHECK(m != NULL && prio == 60, "query op %d", opidx);
+        if (ma) order[nm++] = ma;  /* ascending priority: avx (50), rocm (60) */
+        order[nm++] = m;
+        /* op_base_op_select.c:137-178: enable, then copy non-NULL slots */
+        for (k = 0; k < nm; ++k) {
+            ompi_op_base_module_t *mk = order[k];
+            if (mk->opm_enable) CHECK(mk->opm_enable(mk, op) == OMPI_SUCCESS, "enable");
+            for (i = 0; i < OMPI_OP_BASE_TYPE_MAX; ++i) {
+                if (mk->opm_fns[i]) {
+                    op->o_func.intrinsic.fns[i] = mk->opm_fns[i];
+                    op->o_func.intrinsic.modules[i] = mk;
+                }
+                if (mk->opm_3buff_fns[i]) {
+                    op->o_3buff_intrinsic.fns[i] = mk->opm_3buff_fns[i];
+                    op->o_3buff_intrinsic.modules[i] = mk;
+                }
+            }
         }
-        if (m->opm_3buff_fns[i]) {
-            op->o_3buff_intrinsic.fns[i] = m->opm_3buff_fns[i];
-            op->o_3buff_intrinsic.modules[i] = m;
-        }
+        CHECK(m->opm_enable != NULL, "op/rocm captures its fallback at enable");
     }
     /* op_base_op_select.c:182-204: NULL pattern must stay op/base's */
     for (i = 0; i < OMPI_OP_BASE_TYPE_MAX; ++i) {
@@ -151,10 +196,23 @@ int main(void)
     }
     orc_op_2buff(ORC_OP_SUM, ORC_T_FLOAT, a, e, (size_t) n);
     cnt = n;
-    base_calls = 0;
+    base_calls = avx_calls = 0;
     sum.o_func.intrinsic.fns[ORC_T_FLOAT](a, b, &cnt, NULL, sum.o_func.intrinsic.modules[ORC_T_FLOAT]);
-    CHECK(base_calls == 1, "host SUM did not fall back (%d)", base_calls);
+    CHECK(avx_calls == 1 && base_calls == 0,
+          "host SUM must reach the op/avx stand-in's handler (avx %d, base %d)", avx_calls, base_calls);
     CHECK(memcmp(b, e, n * sizeof(float)) == 0, "host SUM result");
+    {   /* 3-buffer too */
+        float *o = malloc(n * sizeof(float)), *x = malloc(n * sizeof(float));
+        for (i = 0; i < n; ++i) x[i] = 1.0f + (float) i;
+        orc_op_3buff(ORC_OP_SUM, ORC_T_FLOAT, a, x, e, (size_t) n);
+        avx_calls = 0;
+        sum.o_3buff_intrinsic.fns[ORC_T_FLOAT](a, x, o, &cnt, NULL, NULL);
+        CHECK(avx_calls == 1 && base_calls == 0, "host 3buff SUM fallback (avx %d)", avx_calls);
+        CHECK(memcmp(o, e, n * sizeof(float)) == 0, "host 3buff SUM result");
+        free(o);
+        free(x);
+    }
+
 
     if (use_gpu) {
         void *da, *db;
