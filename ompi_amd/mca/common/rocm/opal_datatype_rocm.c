@@ -17,7 +17,9 @@
 
 #include "opal/datatype/opal_convertor.h"
 #include "opal/datatype/opal_datatype.h"
+#if OPAL_CUDA_SUPPORT
 #include "opal/datatype/opal_datatype_cuda.h"
+#endif
 #include "opal/datatype/opal_datatype_internal.h"
 
 #include "ompi_amd.h"
@@ -29,6 +31,20 @@ _Static_assert(sizeof(struct iovec) == sizeof(ompi_amd_iovec_t) &&
                    offsetof(struct iovec, iov_len) == offsetof(ompi_amd_iovec_t, iov_len),
                "ompi_amd_iovec_t mirrors struct iovec");
 
+/* The convertor's stream exists only in an OPAL_CUDA_SUPPORT build
+ * (opal_convertor.h:120-123); otherwise the calling thread's library
+ * stream (ompi_amd_set_thread_stream, NULL = the per-thread default). */
+static void *conv_stream(const opal_convertor_t *c)
+{
+#if OPAL_CUDA_SUPPORT
+    return c->stream;
+#else
+    (void) c;
+    return NULL;
+#endif
+}
+
+#if OPAL_CUDA_SUPPORT
 /* ------------------------------------------------- GPU function table */
 
 /* mca_common_cuda_is_gpu_buffer (common_cuda.c:1739-1792) */
@@ -42,7 +58,7 @@ static int rocm_is_gpu_buffer(const void *buf, opal_convertor_t *convertor)
  * convertor's stream */
 static int rocm_memcpy_async(void *dst, const void *src, size_t n, opal_convertor_t *convertor)
 {
-    return ompi_amd_memcpy_async(dst, src, n, convertor ? convertor->stream : NULL) == 0 ? 0 : -1;
+    return ompi_amd_memcpy_async(dst, src, n, convertor ? conv_stream(convertor) : NULL) == 0 ? 0 : -1;
 }
 
 static int rocm_memcpy(void *dst, const void *src, size_t n)
@@ -64,6 +80,7 @@ int mca_common_rocm_fill_table(opal_common_cuda_function_table_t *ftable)
     ftable->gpu_memmove = &rocm_memmove;
     return 0;
 }
+#endif /* OPAL_CUDA_SUPPORT */
 
 /* ------------------------------------------ opt_desc -> device program */
 
@@ -272,14 +289,14 @@ static int32_t advance(opal_convertor_t *conv, struct iovec *iov, uint32_t *out_
     if (!prog) return -1;
     const int rc = unpack
         ? ompi_amd_ddt_unpack_iov(prog, conv->count, conv->pBaseBuf, conv->bConverted,
-                                  (ompi_amd_iovec_t *)iov, out_size, max_data, conv->stream)
+                                  (ompi_amd_iovec_t *)iov, out_size, max_data, conv_stream(conv))
         : ompi_amd_ddt_pack_iov(prog, conv->count, conv->pBaseBuf, conv->bConverted,
-                                (ompi_amd_iovec_t *)iov, out_size, max_data, conv->stream);
+                                (ompi_amd_iovec_t *)iov, out_size, max_data, conv_stream(conv));
     if (rc < 0) return -1;
     /* synchronous unless the PML runs the convertor asynchronously and
-     * waits on its stream itself (CONVERTOR_CUDA_ASYNC,
-     * opal_cuda_set_copy_function_async) */
-    if (!(conv->flags & CONVERTOR_CUDA_ASYNC) && ompi_amd_stream_synchronize(conv->stream) != 0)
+     * waits on its stream itself (CONVERTOR_CUDA_ASYNC, set only by a CUDA
+     * build's opal_cuda_set_copy_function_async) */
+    if (!(conv->flags & CONVERTOR_CUDA_ASYNC) && ompi_amd_stream_synchronize(conv_stream(conv)) != 0)
         return -1;
     conv->bConverted += *max_data;
     if (rc == 1) conv->flags |= CONVERTOR_COMPLETED;
@@ -298,13 +315,92 @@ int32_t opal_rocm_unpack(opal_convertor_t *convertor, struct iovec *iov, uint32_
     return advance(convertor, iov, out_size, max_data, 1);
 }
 
+/* The first byte the conversion touches is device memory (the reference's
+ * mca_cuda_convertor_init asks the same of pUserBuf, opal_datatype_cuda.c:
+ * 44-60; the true lower bound keeps a type with a negative lb inside the
+ * allocation). */
+static int device_buffer(const opal_convertor_t *c)
+{
+    if (NULL == c->pBaseBuf || NULL == c->pDesc) return 0;
+    return ompi_amd_is_device_pointer(c->pBaseBuf + c->pDesc->true_lb);
+}
+
 int opal_rocm_convertor_select(opal_convertor_t *convertor)
 {
     const uint32_t f = convertor->flags;
-    if (!(f & CONVERTOR_CUDA) || (f & (CONVERTOR_NO_OP | CONVERTOR_COMPLETED)) ||
+    if ((f & (CONVERTOR_NO_OP | CONVERTOR_COMPLETED | CONVERTOR_SKIP_CUDA_INIT)) ||
         !(f & CONVERTOR_HOMOGENEOUS) || (f & CONVERTOR_WITH_CHECKSUM))
         return 0;
+#if OPAL_CUDA_SUPPORT
+    /* a CUDA-support build flagged device buffers already (mca_cuda_convertor_init) */
+    if (!(f & CONVERTOR_CUDA)) return 0;
+#else
+    /* a ROCm-only build: this seam asks the runtime itself */
+    if (!device_buffer(convertor)) return 0;
+#endif
     if (!program_of(convertor->pDesc, 1)) return 0;
     convertor->fAdvance = (f & CONVERTOR_SEND) ? opal_rocm_pack : opal_rocm_unpack;
     return 1;
+}
+
+int opal_rocm_convertor_owns(const opal_convertor_t *convertor)
+{
+    return convertor->fAdvance == opal_rocm_pack || convertor->fAdvance == opal_rocm_unpack;
+}
+
+/* Packed offset, within desc[i0, i1) (r bytes into its packed stream), of
+ * the start of the predefined element that holds byte r. */
+static size_t snap_in(const dt_elem_desc_t *d, uint32_t i0, uint32_t i1, size_t r, int depth)
+{
+    size_t at = 0;
+    for (uint32_t i = i0; i < i1 && depth < 16;) {
+        const uint16_t type = d[i].elem.common.type;
+        if (type == OPAL_DATATYPE_LOOP) {
+            const uint32_t items = d[i].loop.items;
+            if (items < 1 || i + items >= i1) return at;
+            const size_t body = d[i + items].end_loop.size, total = body * d[i].loop.loops;
+            if (body && r < at + total) {
+                const size_t k = (r - at) / body;
+                return at + k * body + snap_in(d, i + 1, i + items, (r - at) - k * body, depth + 1);
+            }
+            at += total;
+            i += items + 1;
+        } else if (type == OPAL_DATATYPE_END_LOOP) {
+            ++i;
+        } else if ((d[i].elem.common.flags & OPAL_DATATYPE_FLAG_DATA) &&
+                   type < OPAL_DATATYPE_MAX_PREDEFINED && opal_datatype_basicDatatypes[type]) {
+            const size_t bsz = opal_datatype_basicDatatypes[type]->size;
+            const size_t bytes = (size_t)d[i].elem.count * d[i].elem.blocklen * bsz;
+            if (bsz && r < at + bytes) return at + (r - at) / bsz * bsz;
+            at += bytes;
+            ++i;
+        } else {
+            ++i;
+        }
+    }
+    return at;
+}
+
+/* opal_convertor_set_position_nocheck for an offloaded convertor.  The
+ * device program resumes at any byte from bConverted alone, so the
+ * reference's stack (pStack / stack_pos / partial_length: the host walk's
+ * state) is not needed: a receive goes to exactly `*position` (a partial
+ * element is unpacked byte for byte); a send of a non-contiguous type
+ * moves back to the start of the predefined element holding it, as the
+ * reference does (opal_convertor.c:433-443: "don't allow it to move in the
+ * middle of a predefined datatype"). */
+int32_t opal_rocm_set_position(opal_convertor_t *convertor, size_t *position)
+{
+    const opal_datatype_t *dt = convertor->pDesc;
+    size_t pos = *position;
+    if ((convertor->flags & CONVERTOR_SEND) && !(dt->flags & OPAL_DATATYPE_FLAG_CONTIGUOUS) &&
+        dt->size > 0) {
+        const size_t inst = pos / dt->size;
+        pos = inst * dt->size +
+              snap_in(dt->opt_desc.desc, 0, (uint32_t)dt->opt_desc.used, pos - inst * dt->size, 0);
+    }
+    convertor->bConverted = pos;
+    convertor->partial_length = 0;
+    *position = pos;
+    return 0;
 }

@@ -13,8 +13,12 @@
  *    opal_rocm_pack / opal_rocm_unpack when the user buffer is device
  *    memory (CONVERTOR_CUDA, set by mca_cuda_convertor_init through the
  *    table's gpu_is_gpu_buffer).
- * INTEGRATION.md §3 shows the two lines a maintainer adds to the
- * reference's prepare functions.
+ * Nothing here depends on OPAL_CUDA_SUPPORT except the function table and
+ * the convertor's stream field, which exist only in such a build
+ * (opal_convertor.h:120-123): a ROCm-only build compiles the seam with
+ * OPAL_CUDA_SUPPORT 0 and gets the offload through the select / set-
+ * position hooks alone.  INTEGRATION.md §3 shows the lines a maintainer
+ * adds to the reference's prepare and set-position functions.
  */
 #ifndef OPAL_DATATYPE_ROCM_H
 #define OPAL_DATATYPE_ROCM_H
@@ -23,17 +27,31 @@
 #include <sys/uio.h>
 
 #include "opal/datatype/opal_convertor.h"
+#if OPAL_CUDA_SUPPORT
 #include "opal/datatype/opal_datatype_cuda.h"
 
-/* opal_cuda_add_initialization_function's callback: fill the GPU table. */
+/* opal_cuda_add_initialization_function's callback: fill the GPU table
+ * (a CUDA-support build only: the table exists nowhere else). */
 int mca_common_rocm_fill_table(opal_common_cuda_function_table_t *ftable);
+#endif
 
 /* After prepare_for_send / _recv chose fAdvance: offload it when the
  * convertor is a device conversion the library can run.  Returns 1 when
  * fAdvance now points at opal_rocm_pack / opal_rocm_unpack, 0 when the
  * reference's choice stays (host buffer, NO_OP contiguous fast path, a
- * description too irregular to flatten). */
+ * description too irregular to flatten).  Device residency: CONVERTOR_CUDA
+ * in an OPAL_CUDA_SUPPORT build; otherwise this seam's own pointer query
+ * (so a ROCm-only build, where nothing sets CONVERTOR_CUDA, offloads too). */
 int opal_rocm_convertor_select(opal_convertor_t *convertor);
+
+/* The convertor runs on this seam (its fAdvance is ours). */
+int opal_rocm_convertor_owns(const opal_convertor_t *convertor);
+
+/* opal_convertor_set_position_nocheck for an owned convertor (the third
+ * hook line): bConverted = *position for a receive, the
+ * start of the enclosing predefined element for a non-contiguous send, as
+ * the reference; *position updated.  Returns 0. */
+int32_t opal_rocm_set_position(opal_convertor_t *convertor, size_t *position);
 
 /* convertor_advance_fct_t implementations: iov[0 .. *out_size) filled
  * (pack) or drained (unpack) from bConverted on in one kernel launch;

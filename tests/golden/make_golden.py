@@ -16,6 +16,11 @@ Sources (all restated, nothing executed from /root/reference):
   x[b-1] + (x[b-2] + (... + (x[b+1] + x[b]))); recursive doubling (pof2) =
   pairwise tree.  Evaluated here in numpy float32, independently of the C
   oracle, on inputs chosen so the two orders round differently.
+* unpack_ooo.json — test/datatype/unpack_ooo.c: the struct of strided int
+  and double vectors (:167-266) over struct foo_t (:30-33), the packed
+  input pbar and the receive buffer bar as the test initialises them
+  (:80-92), the expected result it checks (:125-131), and its four
+  fragment tables of (bytes, offset) pairs (:199-250), as data.
 * ddt_kat.json — the datatypes of test/datatype/ddt_lib.c / ddt_test.c
   (vector(450,10,11) of double :479-493; blacs indexed :273-300; upper
   triangular(100) :130-144; struct{char,double} :230-245; vector(2,2,5)
@@ -219,9 +224,55 @@ def ddt_kat():
     return {"types": types}
 
 
+def unpack_ooo():
+    """unpack_ooo.c's fixture.  N = 331 elements (:27).  struct foo_t {int
+    i[3]; double d[3];} puts i at 0/4/8 and d at 16/24/32 (extent 40); the
+    type is struct{vector(2,1,2,MPI_INT) at &foo.i[0], vector(2,1,2,
+    MPI_DOUBLE) at &foo.d[0]} (:167-266), so each element's typemap is
+    i[0], i[2], d[0], d[2]: 24 bytes packed, the layout of struct pfoo_t
+    {int i[2]; double d[2];} (:35-38)."""
+    n = 331
+    pbar = np.zeros(n, dtype=[("i", "<i4", 2), ("d", "<f8", 2)])
+    j = np.arange(n)
+    pbar["i"][:, 0] = 123 + j          # :81-84
+    pbar["i"][:, 1] = 789 + j
+    pbar["d"][:, 0] = 123.456 + j
+    pbar["d"][:, 1] = 789.123 + j
+    foo = np.dtype({"names": ["i", "pad", "d"], "formats": [("<i4", 3), "<u4", ("<f8", 3)],
+                    "offsets": [0, 12, 16], "itemsize": 40})
+    bar = np.zeros(n, dtype=foo)
+    raw = bar.view(np.uint8).reshape(n, 40)
+    for off, ln in ((0, 4), (8, 4), (16, 8), (32, 8)):   # :85-91: 0xFF over the data fields
+        raw[:, off:off + ln] = 0xFF
+    bar["i"][:, 1] = 0
+    bar["d"][:, 1] = 0.0
+    bar["pad"] = 0x5A5A5A5A  # malloc'd padding in the reference: here a pattern that must survive
+    exp = bar.copy()
+    exp["i"][:, 0] = pbar["i"][:, 0]   # :125-131
+    exp["i"][:, 2] = pbar["i"][:, 1]
+    exp["d"][:, 0] = pbar["d"][:, 0]
+    exp["d"][:, 2] = pbar["d"][:, 1]
+    tables = {  # :199-250
+        "test1": [[992, 0], [1325, 992], [992, 2317], [992, 3309], [992, 4301], [992, 5293],
+                  [992, 6285], [667, 7277]],
+        "test2": [[992, 0], [992, 2317], [992, 3309], [992, 4301], [992, 5293], [992, 6285],
+                  [1325, 992], [667, 7277]],
+        "test3": [[992, 0], [4960, 2317], [1325, 992], [667, 7277]],
+        "test4": [[992, 0], [992, 2976], [992, 1984], [992, 992], [3976, 3968]],
+    }
+    return {"ref": "test/datatype/unpack_ooo.c", "count": n, "extent": 40, "size": 24,
+            "blocks": [[0, 4], [8, 4], [16, 8], [32, 8]],
+            "desc": ["E 6 2 1 8 0", "E 16 2 1 16 16"],
+            "tables": tables,
+            "packed_hex": pbar.tobytes().hex(),
+            "bar_init_hex": bar.tobytes().hex(),
+            "expected_hex": exp.tobytes().hex()}
+
+
 def main():
     for name, fn in (("op_kat.json", op_kat), ("op_edge.json", op_edge),
-                     ("ring_closed_form.json", ring_closed_form), ("ddt_kat.json", ddt_kat)):
+                     ("ring_closed_form.json", ring_closed_form), ("ddt_kat.json", ddt_kat),
+                     ("unpack_ooo.json", unpack_ooo)):
         with open(os.path.join(HERE, name), "w") as f:
             json.dump(fn(), f, indent=1, sort_keys=True)
             f.write("\n")

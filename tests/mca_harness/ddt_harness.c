@@ -22,7 +22,9 @@
 
 #include "opal/datatype/opal_convertor.h"
 #include "opal/datatype/opal_datatype.h"
+#if OPAL_CUDA_SUPPORT
 #include "opal/datatype/opal_datatype_cuda.h"
+#endif
 #include "opal/datatype/opal_datatype_internal.h"
 
 #include "../../oracle/oracle.h"
@@ -38,8 +40,9 @@ int harness_dev_free(void *d);
 static opal_datatype_t basic[OPAL_DATATYPE_MAX_PREDEFINED];
 const opal_datatype_t *opal_datatype_basicDatatypes[OPAL_DATATYPE_MAX_PREDEFINED];
 
-static opal_common_cuda_function_table_t ftable;
 static int gpu_enabled;
+#if OPAL_CUDA_SUPPORT
+static opal_common_cuda_function_table_t ftable;
 
 void opal_cuda_add_initialization_function(int (*fptr)(opal_common_cuda_function_table_t *))
 {
@@ -51,6 +54,7 @@ void mca_cuda_convertor_init(opal_convertor_t *convertor, const void *pUserBuf)
 {
     if (gpu_enabled && ftable.gpu_is_gpu_buffer(pUserBuf, convertor)) convertor->flags |= CONVERTOR_CUDA;
 }
+#endif
 
 /* prepare_for_send / _recv reduced to what this test needs: homogeneous,
  * non-contiguous; then the two lines INTEGRATION.md §3 adds to the
@@ -60,16 +64,36 @@ static int32_t prepare(opal_convertor_t *c, const opal_datatype_t *dt, size_t co
 {
     memset(c, 0, sizeof(*c));
     c->flags = dir | CONVERTOR_HOMOGENEOUS;
+#if OPAL_CUDA_SUPPORT
     mca_cuda_convertor_init(c, buf);
+#endif
     c->local_size = count * dt->size;
     c->pBaseBuf = (unsigned char *)buf;
     c->count = count;
     c->pDesc = dt;
     c->use_desc = &dt->opt_desc;
+    c->pStack = c->static_stack;
+    c->stack_size = DT_STATIC_STACK_SIZE;
     c->fAdvance = NULL;  /* the reference's generic functions are not built here */
     if (count == 0 || dt->size == 0) c->flags |= CONVERTOR_COMPLETED;
     opal_rocm_convertor_select(c);
     return 0;
+}
+
+/* opal_convertor_set_position (opal_convertor.h:313-346) restated; the
+ * nocheck step of an offloaded convertor is the seam's hook */
+int32_t opal_convertor_set_position(opal_convertor_t *c, size_t *position)
+{
+    if (c->local_size <= *position) {
+        c->flags |= CONVERTOR_COMPLETED;
+        c->bConverted = c->local_size;
+        *position = c->bConverted;
+        return 0;
+    }
+    if (*position == c->bConverted) return 0;
+    c->flags &= ~CONVERTOR_COMPLETED;
+    if (!opal_rocm_convertor_owns(c)) return -1;  /* the host walk is not built here */
+    return opal_rocm_set_position(c, position);
 }
 
 int32_t opal_convertor_prepare_for_send(opal_convertor_t *c, const struct opal_datatype_t *dt,
@@ -110,6 +134,7 @@ int32_t opal_convertor_unpack(opal_convertor_t *c, struct iovec *iov, uint32_t *
 
 /* ---- the test ---- */
 typedef struct {
+    char kind;  /* 'T' fragment trains, 'U' out-of-order unpack, 'P' position.c replay */
     char name[64];
     size_t count;
     int64_t extent;
@@ -120,7 +145,30 @@ typedef struct {
     dt_elem_desc_t *desc;
     int nchunks;
     size_t chunks[16];
+    int nfrag;                /* U: the fragment table (bytes, offset) */
+    size_t frags[32][2];
+    unsigned char *init, *packed, *expect;  /* U: typed initial, packed stream, typed expected */
+    size_t ninit, npacked, nexpect;
+    size_t seg;               /* P: segment length */
 } spec_t;
+
+static int read_hex(FILE *f, unsigned char **out, size_t *n)
+{
+    size_t len = 0;
+    if (fscanf(f, "%zu", &len) != 1) return -1;
+    unsigned char *b = malloc(len + 1);
+    for (size_t i = 0; i < len; ++i) {
+        unsigned v;
+        if (fscanf(f, "%2x", &v) != 1) {
+            free(b);
+            return -1;
+        }
+        b[i] = (unsigned char) v;
+    }
+    *out = b;
+    *n = len;
+    return 0;
+}
 
 static uint64_t rng_state = 0x9e3779b97f4a7c15ull;
 static uint8_t rnd8(void)
@@ -136,8 +184,10 @@ static int read_spec(FILE *f, spec_t *s)
     char tag[4];
     memset(s, 0, sizeof(*s));
     if (fscanf(f, "%3s", tag) != 1) return 0;
-    if (strcmp(tag, "T") || fscanf(f, "%63s %zu %ld %zu", s->name, &s->count, &s->extent, &s->size) != 4)
+    if ((strcmp(tag, "T") && strcmp(tag, "U") && strcmp(tag, "P")) ||
+        fscanf(f, "%63s %zu %ld %zu", s->name, &s->count, &s->extent, &s->size) != 4)
         return -1;
+    s->kind = tag[0];
     if (fscanf(f, "%3s %d", tag, &s->nb) != 2 || strcmp(tag, "B")) return -1;
     s->blocks = calloc((size_t)s->nb, sizeof(orc_block_t));
     for (int i = 0; i < s->nb; ++i)
@@ -176,6 +226,19 @@ static int read_spec(FILE *f, spec_t *s)
         } else {
             return -1;
         }
+    }
+    if (s->kind == 'U') {
+        if (fscanf(f, "%3s %d", tag, &s->nfrag) != 2 || strcmp(tag, "F") || s->nfrag > 32) return -1;
+        for (int i = 0; i < s->nfrag; ++i)
+            if (fscanf(f, "%zu %zu", &s->frags[i][0], &s->frags[i][1]) != 2) return -1;
+        if (fscanf(f, "%3s", tag) != 1 || strcmp(tag, "I") || read_hex(f, &s->init, &s->ninit)) return -1;
+        if (fscanf(f, "%3s", tag) != 1 || strcmp(tag, "P") || read_hex(f, &s->packed, &s->npacked)) return -1;
+        if (fscanf(f, "%3s", tag) != 1 || strcmp(tag, "E") || read_hex(f, &s->expect, &s->nexpect)) return -1;
+        return 1;
+    }
+    if (s->kind == 'P') {
+        if (fscanf(f, "%3s %zu", tag, &s->seg) != 2 || strcmp(tag, "S") || s->seg == 0) return -1;
+        return 1;
     }
     if (fscanf(f, "%3s %d", tag, &s->nchunks) != 2 || strcmp(tag, "C") || s->nchunks > 16) return -1;
     for (int i = 0; i < s->nchunks; ++i)
@@ -301,18 +364,184 @@ static int test_type(const spec_t *s)
     return fails;
 }
 
+static void type_of_spec(const spec_t *s, opal_datatype_t *dt)
+{
+    memset(dt, 0, sizeof(*dt));
+    dt->size = s->size;
+    dt->lb = dt->true_lb = 0;
+    dt->ub = dt->true_ub = s->extent;
+    dt->opt_desc.length = dt->opt_desc.used = (size_t)s->nd;
+    dt->opt_desc.desc = s->desc;
+}
+
+/* unpack_ooo.c:75-131: a receive convertor over the typed buffer; every
+ * fragment (bytes, offset) of the table unpacked after set_position, out of
+ * order; the whole typed buffer must equal the expected bytes */
+static int test_unpack_ooo(const spec_t *s)
+{
+    opal_datatype_t dt;
+    opal_convertor_t c;
+    void *dtyped = NULL, *dpacked = NULL;
+    unsigned char *got = malloc(s->ninit);
+    int fails = 0;
+    type_of_spec(s, &dt);
+    if (s->ninit != s->nexpect || s->npacked != s->size * s->count ||
+        harness_dev_alloc_copy(&dtyped, s->init, s->ninit) ||
+        harness_dev_alloc_copy(&dpacked, s->packed, s->npacked)) {
+        printf("FAIL %s: fixture sizes / device allocation\n", s->name);
+        return 1;
+    }
+    opal_convertor_prepare_for_recv(&c, &dt, s->count, dtyped);
+    if (c.fAdvance != opal_rocm_unpack) {
+        printf("FAIL %s: unpack not offloaded (flags %x)\n", s->name, c.flags);
+        return 1;
+    }
+    for (int i = 0; i < s->nfrag && !fails; ++i) {
+        size_t pos = s->frags[i][1], max = s->frags[i][0];
+        struct iovec iov = {(char *) dpacked + s->frags[i][1], s->frags[i][0]};
+        uint32_t n = 1;
+        opal_convertor_set_position(&c, &pos);
+        if (pos != s->frags[i][1]) {
+            printf("FAIL %s: set_position(%zu) gave %zu\n", s->name, s->frags[i][1], pos);
+            ++fails;
+            break;
+        }
+        const int32_t rc = opal_convertor_unpack(&c, &iov, &n, &max);
+        if (rc < 0 || max != s->frags[i][0] || c.bConverted != s->frags[i][1] + s->frags[i][0]) {
+            printf("FAIL %s: fragment %d (%zu at %zu): rc %d max %zu bConverted %zu: %s\n", s->name, i,
+                   s->frags[i][0], s->frags[i][1], rc, max, c.bConverted, ompi_amd_last_error());
+            ++fails;
+        }
+    }
+    if (!fails && (harness_dev_copy_back(got, dtyped, s->ninit) || memcmp(got, s->expect, s->ninit))) {
+        size_t bad = 0;
+        while (bad < s->ninit && got[bad] == s->expect[bad]) ++bad;
+        printf("FAIL %s: typed buffer differs from the expected at byte %zu (element %zu, offset %zu)\n",
+               s->name, bad, bad / (size_t) s->extent, bad % (size_t) s->extent);
+        ++fails;
+    }
+    harness_dev_free(dtyped);
+    harness_dev_free(dpacked);
+    free(got);
+    if (!fails) printf("ok %s\n", s->name);
+    return fails;
+}
+
+/* position.c:90-250 replayed on device buffers: create_segments (a send
+ * convertor's set_position finds each segment's end), shuffle_segments
+ * (every other pair from the ends swapped), pack_segments and
+ * unpack_segments in that order; packed segments must equal the oracle's
+ * stream at their positions and the received typed buffer the sent one
+ * (gaps untouched) */
+static int test_position(const spec_t *s)
+{
+    opal_datatype_t dt;
+    opal_convertor_t c;
+    const size_t total = s->size * s->count, tbytes = (size_t) s->extent * s->count;
+    size_t nseg = 0, pos = 0;
+    size_t (*segs)[2] = malloc(sizeof(*segs) * (total + 1));
+    char *typed = malloc(tbytes), *bg = malloc(tbytes), *stream = malloc(total), *got = malloc(tbytes);
+    char *exp = malloc(tbytes), *pk = malloc(total);
+    void *dsend = NULL, *drecv = NULL, *dseg = NULL;
+    int fails = 0;
+    type_of_spec(s, &dt);
+    for (size_t i = 0; i < tbytes; ++i) typed[i] = (char) rnd8();
+    for (size_t i = 0; i < tbytes; ++i) bg[i] = (char) rnd8();
+    orc_pack(s->blocks, s->nb, s->extent, s->count, typed, stream, 0, total);
+    memcpy(exp, bg, tbytes);
+    orc_unpack(s->blocks, s->nb, s->extent, s->count, stream, exp, 0, total);
+    if (harness_dev_alloc_copy(&dsend, typed, tbytes) || harness_dev_alloc_copy(&drecv, bg, tbytes) ||
+        harness_dev_alloc_copy(&dseg, stream, total)) {
+        printf("FAIL %s: device allocation\n", s->name);
+        return 1;
+    }
+    /* create_segments: a send convertor's set_position snaps each end */
+    opal_convertor_prepare_for_send(&c, &dt, s->count, dsend);
+    if (c.fAdvance != opal_rocm_pack) {
+        printf("FAIL %s: pack not offloaded\n", s->name);
+        return 1;
+    }
+    while (pos < total) {
+        size_t end = pos + s->seg;
+        opal_convertor_set_position(&c, &end);
+        if (end <= pos) {
+            printf("FAIL %s: set_position made no progress at %zu\n", s->name, pos);
+            return 1;
+        }
+        segs[nseg][0] = pos;
+        segs[nseg][1] = end - pos;
+        ++nseg;
+        pos = end;
+    }
+    /* shuffle_segments (position.c:96-107) */
+    for (size_t i = 0; i < nseg / 2; i += 2) {
+        size_t t0 = segs[i][0], t1 = segs[i][1];
+        segs[i][0] = segs[nseg - i - 1][0];
+        segs[i][1] = segs[nseg - i - 1][1];
+        segs[nseg - i - 1][0] = t0;
+        segs[nseg - i - 1][1] = t1;
+    }
+    /* pack_segments: fresh convertor, set_position + pack per segment */
+    opal_convertor_prepare_for_send(&c, &dt, s->count, dsend);
+    for (size_t i = 0; i < nseg && !fails; ++i) {
+        size_t p = segs[i][0], max = segs[i][1];
+        struct iovec iov = {(char *) dseg + segs[i][0], segs[i][1]};
+        uint32_t n = 1;
+        opal_convertor_set_position(&c, &p);
+        if (p != segs[i][0] || opal_convertor_pack(&c, &iov, &n, &max) < 0 || max != segs[i][1]) {
+            printf("FAIL %s: pack segment %zu (%zu at %zu): position %zu, max %zu\n", s->name, i,
+                   segs[i][1], segs[i][0], p, max);
+            ++fails;
+        }
+    }
+    if (!fails && (harness_dev_copy_back(pk, dseg, total) || memcmp(pk, stream, total))) {
+        size_t bad = 0;
+        while (bad < total && pk[bad] == stream[bad]) ++bad;
+        printf("FAIL %s: packed segments differ from the oracle's stream at byte %zu\n", s->name, bad);
+        ++fails;
+    }
+    /* unpack_segments: fresh receive convertor, same order */
+    opal_convertor_prepare_for_recv(&c, &dt, s->count, drecv);
+    for (size_t i = 0; i < nseg && !fails; ++i) {
+        size_t p = segs[i][0], max = segs[i][1];
+        struct iovec iov = {(char *) dseg + segs[i][0], segs[i][1]};
+        uint32_t n = 1;
+        opal_convertor_set_position(&c, &p);
+        if (p != segs[i][0] || opal_convertor_unpack(&c, &iov, &n, &max) < 0 || max != segs[i][1]) {
+            printf("FAIL %s: unpack segment %zu\n", s->name, i);
+            ++fails;
+        }
+    }
+    if (!fails && (harness_dev_copy_back(got, drecv, tbytes) || memcmp(got, exp, tbytes))) {
+        size_t bad = 0;
+        while (bad < tbytes && got[bad] == exp[bad]) ++bad;
+        printf("FAIL %s: received typed buffer differs at byte %zu\n", s->name, bad);
+        ++fails;
+    }
+    if (!fails) printf("ok %s (%zu segments)\n", s->name, nseg);
+    harness_dev_free(dsend);
+    harness_dev_free(drecv);
+    harness_dev_free(dseg);
+    free(segs); free(typed); free(bg); free(stream); free(got); free(exp); free(pk);
+    return fails;
+}
+
 int main(void)
 {
     static const struct { int type; size_t size; } sizes[] = {
         {OPAL_DATATYPE_INT1, 1}, {OPAL_DATATYPE_INT2, 2}, {OPAL_DATATYPE_INT4, 4},
         {OPAL_DATATYPE_INT8, 8}, {OPAL_DATATYPE_UINT1, 1}, {OPAL_DATATYPE_FLOAT4, 4},
-        {OPAL_DATATYPE_FLOAT8, 8}};
+        {OPAL_DATATYPE_FLOAT8, 8}, {OPAL_DATATYPE_FLOAT16, 16}};
     for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]); ++i) {
         basic[sizes[i].type].size = sizes[i].size;
         opal_datatype_basicDatatypes[sizes[i].type] = &basic[sizes[i].type];
     }
     const int gpu = getenv("HARNESS_GPU") && atoi(getenv("HARNESS_GPU"));
+#if OPAL_CUDA_SUPPORT
     opal_cuda_add_initialization_function(mca_common_rocm_fill_table);
+#else
+    gpu_enabled = gpu;  /* nothing to register: the seam asks the runtime itself */
+#endif
     if (!gpu) {
         /* no GPU: the table must refuse, nothing may be offloaded */
         static char host_buf[64];
@@ -326,27 +555,45 @@ int main(void)
             printf("FAIL: offload selected without a GPU\n");
             return 1;
         }
-        printf("ok cpu\n");
+        printf("ok cpu (OPAL_CUDA_SUPPORT %d)\n", OPAL_CUDA_SUPPORT);
         return 0;
     }
+#if OPAL_CUDA_SUPPORT
     if (!gpu_enabled) {
         printf("FAIL: mca_common_rocm_fill_table refused on a GPU host\n");
         return 1;
+    }
+#endif
+    {   /* a host buffer is never offloaded (either build) */
+        static char host_buf[64];
+        opal_datatype_t dt;
+        opal_convertor_t c;
+        memset(&dt, 0, sizeof(dt));
+        dt.size = 8;
+        dt.ub = 16;
+        opal_convertor_prepare_for_send(&c, &dt, 2, host_buf);
+        if (c.fAdvance) {
+            printf("FAIL: a host buffer was offloaded\n");
+            return 1;
+        }
     }
     int fails = 0, types = 0;
     spec_t s;
     int r;
     while ((r = read_spec(stdin, &s)) == 1) {
-        fails += test_type(&s) ? 1 : 0;
+        fails += (s.kind == 'U' ? test_unpack_ooo(&s) : s.kind == 'P' ? test_position(&s) : test_type(&s)) ? 1 : 0;
         ++types;
         free(s.blocks);
         free(s.desc);
+        free(s.init);
+        free(s.packed);
+        free(s.expect);
     }
     if (r < 0) {
         printf("FAIL: bad spec after %d types\n", types);
         return 1;
     }
-    printf("programs cached %d\n", opal_rocm_program_cache_size());
+    printf("programs cached %d (OPAL_CUDA_SUPPORT %d)\n", opal_rocm_program_cache_size(), OPAL_CUDA_SUPPORT);
     opal_rocm_program_cache_clear();
     if (fails) printf("FAILED %d of %d\n", fails, types);
     else printf("all %d ok\n", types);

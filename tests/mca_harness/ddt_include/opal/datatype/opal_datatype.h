@@ -1,5 +1,6 @@
 /* TEST HARNESS ONLY: opal_datatype_t's fields the convertor seam reads
- * (opal/datatype/opal_datatype.h:55-145), restated. */
+ * (opal/datatype/opal_datatype.h:55-145), restated with the reference's
+ * field list and order. */
 #ifndef HARNESS_OPAL_DATATYPE_H
 #define HARNESS_OPAL_DATATYPE_H
 #include <stddef.h>
@@ -21,6 +22,9 @@ typedef struct dt_type_desc_t {
     dt_elem_desc_t *desc;
 } dt_type_desc_t;
 
+#define OPAL_MAX_OBJECT_NAME 64
+
+/* the reference's field list and order (opal_datatype.h:97-134) */
 typedef struct opal_datatype_t {
     opal_object_t super;
     uint16_t flags;
@@ -30,8 +34,10 @@ typedef struct opal_datatype_t {
     ptrdiff_t true_lb, true_ub, lb, ub;
     size_t nbElems;
     uint32_t align, loops;
+    char name[OPAL_MAX_OBJECT_NAME];
     dt_type_desc_t desc;
     dt_type_desc_t opt_desc;
+    size_t *ptypes;
 } opal_datatype_t;
 
 extern const opal_datatype_t *opal_datatype_basicDatatypes[OPAL_DATATYPE_MAX_PREDEFINED];

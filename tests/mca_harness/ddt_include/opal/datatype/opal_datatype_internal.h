@@ -17,6 +17,7 @@
 #define OPAL_DATATYPE_UINT1 9
 #define OPAL_DATATYPE_FLOAT4 15
 #define OPAL_DATATYPE_FLOAT8 16
+#define OPAL_DATATYPE_FLOAT16 18
 
 typedef struct ddt_elem_id_description {
     uint16_t flags;

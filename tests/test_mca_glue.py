@@ -203,14 +203,38 @@ def _ddt_specs(golden):
     return "\n".join(specs) + "\n"
 
 
-@pytest.fixture(scope="module")
-def ddt_harness(tmp_path_factory):
+def _ooo_specs(golden):
+    """unpack_ooo.c's four fragment tables (tests/golden/unpack_ooo.json) as
+    harness "U" blocks, and position.c's segment replay as a "P" block
+    (MPI_LONG_DOUBLE_INT: long double + int, size 20, extent 32, 2048
+    elements, 113-byte segments, position.c:23-24 / :236)."""
+    u = golden("unpack_ooo.json")
+    specs = []
+    for name, tab in sorted(u["tables"].items()):
+        lines = [f"U unpack_ooo_{name} {u['count']} {u['extent']} {u['size']}",
+                 f"B {len(u['blocks'])} " + " ".join(f"{d} {n}" for d, n in u["blocks"]),
+                 f"D {len(u['desc']) + 1}"] + u["desc"] + [f"X 1 {u['size']}",
+                 f"F {len(tab)} " + " ".join(f"{b} {o}" for b, o in tab)]
+        for tag, key in (("I", "bar_init_hex"), ("P", "packed_hex"), ("E", "expected_hex")):
+            lines.append(f"{tag} {len(u[key]) // 2} {u[key]}")
+        specs.append("\n".join(lines))
+    specs.append("\n".join(["P position_long_double_int 2048 32 20", "B 2 0 16 16 4",
+                            "D 3", "E 18 1 1 16 0", "E 6 1 1 4 16", "X 1 20", "S 113"]))
+    return "\n".join(specs) + "\n"
+
+
+@pytest.fixture(scope="module", params=[1, 0], ids=["cuda_support_build", "rocm_only_build"])
+def ddt_harness(request, tmp_path_factory):
+    """The seam compiled as in an OPAL_CUDA_SUPPORT build (function table,
+    convertor->stream) and as in a ROCm-only build (neither field exists;
+    residency asked by the seam itself)."""
     from ompi_amd import _lib
     from oracle import oracle as orc
     _lib.load()
     orc.lib()
-    out = str(tmp_path_factory.mktemp("mca") / "ddt_harness")
-    subprocess.run(["bash", os.path.join(ROOT, "tests", "mca_harness", "build_ddt.sh"), out], check=True)
+    out = str(tmp_path_factory.mktemp("mca") / f"ddt_harness_{request.param}")
+    subprocess.run(["bash", os.path.join(ROOT, "tests", "mca_harness", "build_ddt.sh"), out,
+                    str(request.param)], check=True)
     return out
 
 
@@ -218,7 +242,7 @@ def test_convertor_seam_no_gpu(ddt_harness):
     """Without a GPU the function table refuses and nothing is offloaded."""
     r = subprocess.run([ddt_harness], capture_output=True, text=True, timeout=60, input="",
                        env={**os.environ, "HARNESS_GPU": "0", "HIP_VISIBLE_DEVICES": ""})
-    assert r.returncode == 0 and r.stdout.strip() == "ok cpu", (r.stdout, r.stderr)
+    assert r.returncode == 0 and r.stdout.strip().startswith("ok cpu"), (r.stdout, r.stderr)
 
 
 @pytest.mark.gpu
@@ -227,7 +251,15 @@ def test_convertor_seam_fadvance(ddt_harness, golden):
     PML (fragment trains of 1 and 7 iovecs at ddt_test.c's chunk sizes: 12 /
     82 / 6000 / 36000, blacs 956 / 16K / 64K, upper triangle 48 / 956),
     resumable at any bConverted, byte-exact against the oracle; gap bytes of
-    the receive buffer untouched."""
+    the receive buffer untouched.  Then the reference's own out-of-order
+    fixtures: unpack_ooo.c's four (bytes, offset) tables through
+    opal_convertor_set_position + unpack, byte-exact against the expected
+    layout the test checks (:125-131, gaps and padding untouched), and
+    position.c's reversed-segment replay."""
     r = subprocess.run([ddt_harness], capture_output=True, text=True, timeout=300,
-                       input=_ddt_specs(golden), env={**os.environ, "HARNESS_GPU": "1"})
+                       input=_ddt_specs(golden) + _ooo_specs(golden),
+                       env={**os.environ, "HARNESS_GPU": "1"})
     assert r.returncode == 0 and "all" in r.stdout, (r.stdout[-3000:], r.stderr[-2000:])
+    for t in ("unpack_ooo_test1", "unpack_ooo_test2", "unpack_ooo_test3", "unpack_ooo_test4",
+              "position_long_double_int"):
+        assert f"ok {t}" in r.stdout, r.stdout[-3000:]

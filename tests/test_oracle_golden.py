@@ -252,3 +252,21 @@ def test_datatype_builders_match_reference_types(golden):
         assert dt.runs == [tuple(b) for b in t["blocks"]], name
         assert dt.size == t["size"] and dt.extent == t["extent"], name
         assert len(dt.elems) == nel, (name, dt.elems[:4])
+
+
+@pytest.mark.parametrize("table", ["test1", "test2", "test3", "test4"])
+def test_oracle_unpack_out_of_order_fixture(orc, golden, table):
+    """The oracle's unpack restatement against the reference's own
+    out-of-order fixture (test/datatype/unpack_ooo.c, tests/golden/
+    unpack_ooo.json): every (bytes, offset) fragment of the table unpacked at
+    its offset, in the table's order, gives exactly the layout the test
+    checks (:125-131) — gaps (i[1], d[1]) and padding untouched."""
+    u = golden("unpack_ooo.json")
+    packed = np.frombuffer(bytes.fromhex(u["packed_hex"]), dtype=np.uint8)
+    typed = np.frombuffer(bytes.fromhex(u["bar_init_hex"]), dtype=np.uint8).copy()
+    expected = np.frombuffer(bytes.fromhex(u["expected_hex"]), dtype=np.uint8)
+    assert sum(b for b, _ in u["tables"][table]) == packed.nbytes == u["size"] * u["count"]
+    for nbytes, off in u["tables"][table]:
+        frag = packed[off:off + nbytes].copy()
+        assert orc.unpack(u["blocks"], u["extent"], u["count"], frag, typed, off) == nbytes
+    assert np.array_equal(typed, expected)
