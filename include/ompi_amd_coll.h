@@ -169,10 +169,25 @@ int ompi_amd_plan_start(ompi_amd_plan_t *plan, void *stream);
 int ompi_amd_plan_test(ompi_amd_plan_t *plan, int *done);
 int ompi_amd_plan_wait(ompi_amd_plan_t *plan);
 int ompi_amd_plan_free(ompi_amd_plan_t *plan);
+/* Persistent reduce_scatter_block / allgather / bcast (MPI-4
+ * MPI_Reduce_scatter_block_init / MPI_Allgather_init / MPI_Bcast_init;
+ * coll.h:545-566 coll_*_init).  Local (nothing is exchanged at init); every
+ * ompi_amd_plan_start posts the nonblocking call with the init's arguments
+ * on `stream` (it never waits for a peer) and ompi_amd_plan_test / _wait /
+ * _free follow that call's request; a start waits for the previous one to
+ * have completed (MPI requires it anyway).  Same argument rules as the
+ * blocking calls (rbuf / buf, MPI_IN_PLACE = (void *)1). */
+int ompi_amd_reduce_scatter_block_init(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
+                                       size_t rcount, int type, int op, ompi_amd_plan_t **plan);
+int ompi_amd_allgather_init(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf, size_t bytes,
+                            ompi_amd_plan_t **plan);
+int ompi_amd_bcast_init(ompi_amd_comm_t *comm, void *buf, size_t bytes, int root,
+                        ompi_amd_plan_t **plan);
 /* Which path a plan's starts take (diagnostics / tests): 0 = the plain call
  * re-run (fused / staged sizes, and the default push-gather scheme at any
  * size: no handle swap), 1 pull, 2 pull+push, 3 push with the caller's
- * buffers mapped (user_ipc); -1 for NULL. */
+ * buffers mapped (user_ipc), 4 a persistent reduce_scatter_block /
+ * allgather / bcast; -1 for NULL. */
 int ompi_amd_plan_kind(const ompi_amd_plan_t *plan);
 /* Nonblocking allreduce (MPI_Iallreduce, coll.h:271-274; libnbc's
  * ompi_coll_libnbc_iallreduce in the reference).  Returns without waiting
@@ -203,6 +218,24 @@ int ompi_amd_iallgather(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf, siz
                         void *stream, ompi_amd_request_t **request);
 int ompi_amd_ibcast(ompi_amd_comm_t *comm, void *buf, size_t bytes, int root, void *stream,
                     ompi_amd_request_t **request);
+/* Nonblocking reduce / scan / exscan / reduce_scatter (coll_ireduce,
+ * coll_iscan, coll_iexscan, coll_ireduce_scatter: coll.h:276-300; libnbc's
+ * in the reference).  Results exactly those of the blocking calls (the same
+ * operand orders).  They post no buffer descriptors: every size launches on
+ * the staged or landing paths, in posting order, with no handle swap (a
+ * zero-copy size grows the landing buffer at post time if it must —
+ * collective, as for ompi_amd_iallreduce).  ompi_amd_ireduce posts one
+ * ticket carrying the root's MPI_IN_PLACE choice and launches once every
+ * peer posted it. */
+int ompi_amd_ireduce(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type,
+                     int op, int root, void *stream, ompi_amd_request_t **request);
+int ompi_amd_iscan(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type,
+                   int op, void *stream, ompi_amd_request_t **request);
+int ompi_amd_iexscan(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf, size_t count, int type,
+                     int op, void *stream, ompi_amd_request_t **request);
+int ompi_amd_ireduce_scatter(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
+                             const size_t *rcounts, int type, int op, void *stream,
+                             ompi_amd_request_t **request);
 /* *done = 1 once the collective's device work finished; launches deferred
  * calls whose swap completed (never waits for a peer).  As for plans, the
  * completion point is marked at the first test / wait after the launch. */

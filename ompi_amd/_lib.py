@@ -156,6 +156,24 @@ PROTOTYPES = [
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p, _C.POINTER(_C.c_void_p)]),
     ("ompi_amd_ibcast", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_void_p, _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_ireduce", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_int, _C.c_void_p,
+      _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_iscan", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p,
+      _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_iexscan", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p,
+      _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_ireduce_scatter", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.POINTER(_C.c_size_t), _C.c_int, _C.c_int, _C.c_void_p,
+      _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_reduce_scatter_block_init", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_allgather_init", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_bcast_init", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.POINTER(_C.c_void_p)]),
     ("ompi_amd_request_test", _C.c_int, [_C.c_void_p, _C.POINTER(_C.c_int)]),
     ("ompi_amd_request_wait", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_request_free", _C.c_int, [_C.c_void_p]),

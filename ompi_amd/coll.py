@@ -217,6 +217,57 @@ class Communicator:
                                              ctypes.byref(h)), "ibcast")
         return Request(self, h, "ibcast")
 
+    def ireduce(self, sbuf, rbuf, count: int, datatype: Datatype, op: Op, root: int,
+                stream=None) -> "Request":
+        """MPI_Ireduce (rbuf may be None off the root, sbuf IN_PLACE at it)."""
+        h = ctypes.c_void_p()
+        what = f"ireduce({op.name},{datatype.name},root={root})"
+        _lib.check(self._lib.ompi_amd_ireduce(self._h, _ptr(sbuf), _ptr(rbuf) if rbuf is not None else None,
+                                              count, datatype.code, op.index, root, _stream(stream),
+                                              ctypes.byref(h)), what)
+        return Request(self, h, what)
+
+    def iscan(self, sbuf, rbuf, count: int, datatype: Datatype, op: Op, stream=None,
+              exclusive: bool = False) -> "Request":
+        """MPI_Iscan (exclusive: MPI_Iexscan)."""
+        h = ctypes.c_void_p()
+        fn = self._lib.ompi_amd_iexscan if exclusive else self._lib.ompi_amd_iscan
+        what = f"{'iexscan' if exclusive else 'iscan'}({op.name},{datatype.name})"
+        _lib.check(fn(self._h, _ptr(sbuf), _ptr(rbuf), count, datatype.code, op.index, _stream(stream),
+                      ctypes.byref(h)), what)
+        return Request(self, h, what)
+
+    def ireduce_scatter(self, sbuf, rbuf, rcounts, datatype: Datatype, op: Op,
+                        stream=None) -> "Request":
+        h = ctypes.c_void_p()
+        arr = (ctypes.c_size_t * self.size)(*[int(c) for c in rcounts])
+        what = f"ireduce_scatter({op.name},{datatype.name})"
+        _lib.check(self._lib.ompi_amd_ireduce_scatter(self._h, _ptr(sbuf), _ptr(rbuf), arr,
+                                                      datatype.code, op.index, _stream(stream),
+                                                      ctypes.byref(h)), what)
+        return Request(self, h, what)
+
+    # -- persistent forms (MPI-4 *_init, coll.h:545-566) ----------------------
+    def reduce_scatter_block_init(self, sbuf, rbuf, rcount: int, datatype: Datatype,
+                                  op: Op) -> "Plan":
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.ompi_amd_reduce_scatter_block_init(self._h, _ptr(sbuf), _ptr(rbuf), rcount,
+                                                                datatype.code, op.index, ctypes.byref(h)),
+                   "reduce_scatter_block_init")
+        return Plan(self, h, f"reduce_scatter_block({op.name},{datatype.name})")
+
+    def allgather_init(self, sbuf, rbuf, nbytes: int) -> "Plan":
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.ompi_amd_allgather_init(self._h, _ptr(sbuf), _ptr(rbuf), nbytes,
+                                                     ctypes.byref(h)), "allgather_init")
+        return Plan(self, h, "allgather")
+
+    def bcast_init(self, buf, nbytes: int, root: int) -> "Plan":
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.ompi_amd_bcast_init(self._h, _ptr(buf), nbytes, root, ctypes.byref(h)),
+                   "bcast_init")
+        return Plan(self, h, "bcast")
+
     def __del__(self):
         # destroy is collective; only an explicit free() releases the comm
         pass

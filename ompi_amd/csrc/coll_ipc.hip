@@ -300,11 +300,14 @@ struct pending_op {
     ompi_amd_request *req;
     shadow_set sh;  // export fallback of this call (sbuf / rbuf above are then the shadows)
     int kind = 0;   // PEND_*: which collective
-    int root = 0;   // bcast
+    int root = 0;   // bcast, reduce
     bool inplace = false;  // rsb without a swap (staged push): MPI_IN_PLACE
+    bool exclusive = false;        // scan: exscan
+    std::vector<size_t> rcounts;   // reduce_scatter
 };
 
-enum { PEND_ALLREDUCE = 0, PEND_RSB = 1, PEND_ALLGATHER = 2, PEND_BCAST = 3 };
+enum { PEND_ALLREDUCE = 0, PEND_RSB = 1, PEND_ALLGATHER = 2, PEND_BCAST = 3, PEND_REDUCE = 4,
+       PEND_SCAN = 5, PEND_RS = 6 };
 
 }  // namespace ompi_amd
 
@@ -435,6 +438,13 @@ struct ompi_amd_plan {
     hipStream_t stream = nullptr;
     bool started = false, recorded = false;
     shadow_set sh;  // export fallback (src / rbuf above are then the shadows)
+    // kind 4: a persistent reduce_scatter_block / allgather / bcast — every
+    // start posts the nonblocking call with the init's arguments (PEND_*
+    // below), whose request the plan's test / wait / free follow
+    int nb_kind = -1;
+    int root = 0;
+    size_t bytes = 0;
+    ompi_amd_request *req = nullptr;
 };
 
 namespace ompi_amd {
@@ -1877,6 +1887,10 @@ static int allgather_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size
                           hipStream_t s);
 static int bcast_impl(ompi_amd_comm_t *c, void *buf, const void *root_src, size_t bytes, int root,
                       hipStream_t s);
+static int reduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
+                       int op, int root, bool root_inplace, hipStream_t s);
+static int rs_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, const size_t *rcounts,
+                   int type, int op, hipStream_t s);
 
 // Forced nonoverlapping only: every rank must know whether rank 0 passed
 // MPI_IN_PLACE (it changes rank 0's first combine of the reduce,
@@ -1919,6 +1933,26 @@ static int progress(ompi_amd_comm_t *c, bool block, int max_launch = -1) {
                 case PEND_BCAST:
                     rc = bcast_impl(c, o.rbuf, o.sbuf, o.count, o.root, o.stream);
                     break;
+                case PEND_REDUCE:
+                case PEND_SCAN:
+                case PEND_RS: {
+                    // these post no buffer descriptors: they launch on the
+                    // staged / landing paths only (no handle swap at launch)
+                    const int ui = c->user_ipc, fs = c->force_shadow;
+                    c->user_ipc = 0;
+                    c->force_shadow = 0;
+                    if (o.kind == PEND_REDUCE)
+                        rc = reduce_impl(c, o.sbuf, o.rbuf, o.count, o.type, o.op, o.root,
+                                         o.ticket && (all[o.root].flags & 1), o.stream);
+                    else if (o.kind == PEND_SCAN)
+                        rc = scan_common(c, o.sbuf, o.rbuf, o.count, o.type, o.op, o.stream,
+                                         o.exclusive);
+                    else
+                        rc = rs_impl(c, o.sbuf, o.rbuf, o.rcounts.data(), o.type, o.op, o.stream);
+                    c->user_ipc = ui;
+                    c->force_shadow = fs;
+                    break;
+                }
                 default:
                     rc = allreduce_impl(c, o.sbuf, o.rbuf, o.count, o.type, o.op, o.stream, o.pp);
                 }
@@ -2533,6 +2567,113 @@ int ompi_amd_ibcast(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, void 
     return nb_post(c, o, &o.sbuf, bytes, false, out);
 }
 
+// ---- nonblocking reduce / scan / exscan / reduce_scatter ----
+// They post no buffer descriptors and launch (in posting order, from
+// progress) on the staged or landing paths, which need no handle swap; the
+// landing buffer is grown at post time when a zero-copy size needs it
+// (collective and blocking, as for iallreduce: every rank posts alike).
+// ireduce posts one ticket carrying the root's MPI_IN_PLACE flag (it
+// changes the root's first combine, coll_base_reduce.c:170-171), so no
+// rank waits for a peer at post time.
+static int nb_landing(ompi_amd_comm_t *c, size_t need, ompi_amd_request *req) {
+    int rc = OMPI_AMD_SUCCESS;
+    if (need > c->land_bytes) {
+        rc = drain(c);
+        if (rc == OMPI_AMD_SUCCESS) rc = ensure_landing(c, need);
+    }
+    if (rc != OMPI_AMD_SUCCESS) {
+        hip_ignore(hipEventDestroy(req->ev));
+        delete req;
+    }
+    return rc;
+}
+
+int ompi_amd_ireduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
+                     int op, int root, void *stream, ompi_amd_request_t **out) {
+    if (!c || !out || root < 0 || root >= c->size || (c->rank == root && !rbuf))
+        return OMPI_AMD_ERR_BAD_PARAM;
+    *out = nullptr;
+    if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
+    ompi_amd_request *req = nullptr;
+    TRY(nb_begin(c, &req));
+    const int n = c->size;
+    const size_t bytes = count * ompi_amd_type_extent(type);
+    pending_op o{0, sbuf, rbuf, count, type, op, as_stream(stream), params_of(c), req};
+    o.kind = PEND_REDUCE;
+    o.root = root;
+    if (n > 1 && count > 0 && bytes > c->small_bytes && c->zero_copy) {
+        int64_t split, early, late;
+        blockcount((int64_t)count, n, &split, &early, &late);
+        const size_t slot = ((size_t)early * ompi_amd_type_extent(type) + 16 + 255) & ~(size_t)255;
+        TRY(nb_landing(c, slot * (size_t)n + ((bytes + 255) & ~(size_t)255), req));
+    }
+    if (n == 1 || count == 0) return nb_post(c, o, nullptr, 0, false, out);
+    int rc = OMPI_AMD_SUCCESS;
+    while (rc == OMPI_AMD_SUCCESS && c->boot.posted() - c->boot.consumed() >= ShmBoot::kRing - 1)
+        rc = progress(c, true, 1);
+    call_blob mine{};
+    mine.flags = (c->rank == root && in_place(sbuf, rbuf)) ? 1 : 0;
+    if (rc == OMPI_AMD_SUCCESS) rc = c->boot.post(&mine, sizeof(mine), &o.ticket);
+    if (rc != OMPI_AMD_SUCCESS) {
+        hip_ignore(hipEventDestroy(req->ev));
+        delete req;
+        return rc;
+    }
+    c->pending.push_back(o);
+    *out = req;
+    return progress(c, false);
+}
+
+static int iscan_common(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
+                        int op, void *stream, bool exclusive, ompi_amd_request_t **out) {
+    if (!c || !rbuf || !out) return OMPI_AMD_ERR_BAD_PARAM;
+    *out = nullptr;
+    if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
+    ompi_amd_request *req = nullptr;
+    TRY(nb_begin(c, &req));
+    const size_t bytes = count * ompi_amd_type_extent(type);
+    pending_op o{0, sbuf, rbuf, count, type, op, as_stream(stream), params_of(c), req};
+    o.kind = PEND_SCAN;
+    o.exclusive = exclusive;
+    if (c->size > 1 && count > 0 && bytes > c->small_bytes && c->zero_copy)
+        TRY(nb_landing(c, bytes + 256, req));
+    return nb_post(c, o, nullptr, 0, false, out);
+}
+
+int ompi_amd_iscan(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
+                   int op, void *stream, ompi_amd_request_t **out) {
+    return iscan_common(c, sbuf, rbuf, count, type, op, stream, false, out);
+}
+
+int ompi_amd_iexscan(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
+                     int op, void *stream, ompi_amd_request_t **out) {
+    return iscan_common(c, sbuf, rbuf, count, type, op, stream, true, out);
+}
+
+int ompi_amd_ireduce_scatter(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
+                             const size_t *rcounts, int type, int op, void *stream,
+                             ompi_amd_request_t **out) {
+    if (!c || !rbuf || !rcounts || !out) return OMPI_AMD_ERR_BAD_PARAM;
+    *out = nullptr;
+    if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
+    ompi_amd_request *req = nullptr;
+    TRY(nb_begin(c, &req));
+    const size_t ext = ompi_amd_type_extent(type);
+    pending_op o{0, sbuf, rbuf, 0, type, op, as_stream(stream), params_of(c), req};
+    o.kind = PEND_RS;
+    o.rcounts.assign(rcounts, rcounts + c->size);
+    size_t total = 0, maxc = 0;
+    for (size_t v : o.rcounts) {
+        total += v;
+        maxc = std::max(maxc, v);
+    }
+    if (c->size > 1 && total * ext > c->small_bytes && c->zero_copy) {  // reduce_my_block's staged push
+        const size_t slot = (maxc * ext + 16 + 255) & ~(size_t)255;
+        TRY(nb_landing(c, slot * (size_t)(c->size + 1), req));
+    }
+    return nb_post(c, o, nullptr, 0, false, out);
+}
+
 int ompi_amd_reduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                     int op, int root, void *stream) {
     if (!c || root < 0 || root >= c->size || (c->rank == root && !rbuf))
@@ -2541,8 +2682,20 @@ int ompi_amd_reduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t cou
     TRY(check_sticky(c));
     TRY(drain(c));
     if (count == 0) return OMPI_AMD_SUCCESS;
+    // the in-place flag only changes the root's first combine; every rank
+    // must fold the same expression, so the root's choice is made known
+    const bool root_inplace = c->rank == root && in_place(sbuf, rbuf);
+    int flag = root_inplace ? 1 : 0, flags_all[kMaxRanks];
+    if (c->size > 1) TRY(c->boot.allgather(&flag, flags_all, sizeof(int)));
+    return reduce_impl(c, sbuf, rbuf, count, type, op, root, c->size > 1 ? flags_all[root] != 0 : root_inplace,
+                       as_stream(stream));
+}
+
+// root_inplace_all: whether the root passed MPI_IN_PLACE (known to every rank)
+static int reduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
+                       int op, int root, bool root_inplace_all, hipStream_t s) {
+    if (count == 0) return OMPI_AMD_SUCCESS;
     TRY(set_dev(c));
-    hipStream_t s = as_stream(stream);
     const int n = c->size;
     const size_t bytes = count * ompi_amd_type_extent(type);
     const bool root_inplace = c->rank == root && in_place(sbuf, rbuf);
@@ -2552,12 +2705,7 @@ int ompi_amd_reduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t cou
         if (root_inplace) return OMPI_AMD_SUCCESS;
         return record_hip(hipMemcpyAsync(rbuf, src, bytes, hipMemcpyDeviceToDevice, s), "copy");
     }
-    // the in-place flag only changes the root's first combine; every rank
-    // must fold the same expression, so the root's choice is made known
-    int flag = root_inplace ? 1 : 0, flags_all[kMaxRanks];
-    TRY(c->boot.allgather(&flag, flags_all, sizeof(int)));
-    const red_order ro = tuned_reduce_order(n, type_size(type) * count, count, root,
-                                            flags_all[root] != 0);
+    const red_order ro = tuned_reduce_order(n, type_size(type) * count, count, root, root_inplace_all);
     red_jobs jobs;
     if (bytes <= c->small_bytes || !c->zero_copy) {
         // staged: everyone stages, the root folds everything
@@ -2691,6 +2839,11 @@ int ompi_amd_reduce_scatter(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
     TRY(check_sticky(c));
     TRY(drain(c));
+    return rs_impl(c, sbuf, rbuf, rcounts, type, op, as_stream(stream));
+}
+
+static int rs_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, const size_t *rcounts,
+                   int type, int op, hipStream_t s) {
     const int n = c->size;
     size_t total = 0, off = 0, maxc = 0;
     for (int p = 0; p < n; ++p) {
@@ -2700,7 +2853,6 @@ int ompi_amd_reduce_scatter(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
     }
     if (total == 0) return OMPI_AMD_SUCCESS;
     TRY(set_dev(c));
-    hipStream_t s = as_stream(stream);
     const size_t ext = ompi_amd_type_extent(type);
     const bool inplace = in_place(sbuf, rbuf);
     const void *src = inplace ? rbuf : sbuf;
@@ -2966,8 +3118,72 @@ static int plan_enqueue(ompi_amd_plan_t *pl, void *stream) {
 
 int ompi_amd_plan_kind(const ompi_amd_plan_t *pl) { return pl ? pl->kind : -1; }
 
+static int plan_nb_post(ompi_amd_plan_t *pl, void *stream) {
+    ompi_amd_comm_t *c = pl->c;
+    if (pl->req) {  // MPI: a start follows the completion of the previous one
+        const int frc = ompi_amd_request_free(pl->req);
+        pl->req = nullptr;
+        TRY(frc);
+    }
+    switch (pl->nb_kind) {
+    case PEND_RSB:
+        return ompi_amd_ireduce_scatter_block(c, pl->src, pl->rbuf, (size_t)pl->count, pl->type, pl->op,
+                                              stream, &pl->req);
+    case PEND_ALLGATHER:
+        return ompi_amd_iallgather(c, pl->src, pl->rbuf, pl->bytes, stream, &pl->req);
+    case PEND_BCAST:
+        return ompi_amd_ibcast(c, pl->rbuf, pl->bytes, pl->root, stream, &pl->req);
+    default:
+        return OMPI_AMD_ERR_BAD_PARAM;
+    }
+}
+
+static int plan_nb_new(ompi_amd_comm_t *c, int nb_kind, const void *src, void *rbuf, size_t count,
+                       int type, int op, int root, size_t bytes, ompi_amd_plan_t **out) {
+    *out = nullptr;
+    TRY(check_sticky(c));
+    auto *pl = new (std::nothrow) ompi_amd_plan;
+    if (!pl) return OMPI_AMD_ERR_BAD_PARAM;
+    pl->c = c;
+    pl->kind = 4;
+    pl->nb_kind = nb_kind;
+    pl->src = src;
+    pl->rbuf = rbuf;
+    pl->count = (int64_t)count;
+    pl->type = type;
+    pl->op = op;
+    pl->root = root;
+    pl->bytes = bytes;
+    *out = pl;
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_reduce_scatter_block_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
+                                       size_t rcount, int type, int op, ompi_amd_plan_t **out) {
+    if (!c || !rbuf || !out) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
+    return plan_nb_new(c, PEND_RSB, sbuf, rbuf, rcount, type, op, 0, 0, out);
+}
+
+int ompi_amd_allgather_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t bytes,
+                            ompi_amd_plan_t **out) {
+    if (!c || !rbuf || !out) return OMPI_AMD_ERR_BAD_PARAM;
+    return plan_nb_new(c, PEND_ALLGATHER, sbuf, rbuf, 0, 0, 0, 0, bytes, out);
+}
+
+int ompi_amd_bcast_init(ompi_amd_comm_t *c, void *buf, size_t bytes, int root,
+                        ompi_amd_plan_t **out) {
+    if (!c || !buf || !out || root < 0 || root >= c->size) return OMPI_AMD_ERR_BAD_PARAM;
+    return plan_nb_new(c, PEND_BCAST, buf, buf, 0, 0, 0, root, bytes, out);
+}
+
 int ompi_amd_plan_start(ompi_amd_plan_t *pl, void *stream) {
     if (!pl || !pl->c) return OMPI_AMD_ERR_BAD_PARAM;
+    if (pl->kind == 4) {  // posts a nonblocking call: never waits for a peer
+        TRY(plan_nb_post(pl, stream));
+        pl->started = true;
+        return OMPI_AMD_SUCCESS;
+    }
     TRY(drain(pl->c));  // device order: deferred nonblocking calls first
     TRY(plan_enqueue(pl, stream));
     pl->started = true;
@@ -2980,6 +3196,7 @@ int ompi_amd_plan_test(ompi_amd_plan_t *pl, int *done) {
     if (!pl || !done) return OMPI_AMD_ERR_BAD_PARAM;
     *done = 1;
     if (!pl->started) return OMPI_AMD_SUCCESS;
+    if (pl->kind == 4) return pl->req ? ompi_amd_request_test(pl->req, done) : OMPI_AMD_SUCCESS;
     if (!pl->recorded) {
         TRY(record_hip(hipEventRecord(pl->done, pl->stream), "plan completion event"));
         pl->recorded = true;
@@ -2996,6 +3213,7 @@ int ompi_amd_plan_test(ompi_amd_plan_t *pl, int *done) {
 int ompi_amd_plan_wait(ompi_amd_plan_t *pl) {
     if (!pl) return OMPI_AMD_ERR_BAD_PARAM;
     if (!pl->started) return OMPI_AMD_SUCCESS;
+    if (pl->kind == 4) return pl->req ? ompi_amd_request_wait(pl->req) : OMPI_AMD_SUCCESS;
     if (!pl->recorded) {
         TRY(record_hip(hipEventRecord(pl->done, pl->stream), "plan completion event"));
         pl->recorded = true;
@@ -3006,6 +3224,11 @@ int ompi_amd_plan_wait(ompi_amd_plan_t *pl) {
 
 int ompi_amd_plan_free(ompi_amd_plan_t *pl) {
     if (!pl) return OMPI_AMD_SUCCESS;
+    if (pl->kind == 4) {
+        const int rc = pl->req ? ompi_amd_request_free(pl->req) : OMPI_AMD_SUCCESS;
+        delete pl;
+        return rc;
+    }
     if (pl->c)
         for (int p = 0; p < OMPI_AMD_MAX_RANKS; ++p)
             for (int k = 0; k < 2; ++k)

@@ -7,8 +7,10 @@
  * coll_scan, coll_exscan, coll_allgather, coll_bcast
  * (ompi/mca/coll/coll.h:200-250), the nonblocking coll_iallreduce
  * (coll.h:271-274), coll_ireduce_scatter_block / coll_iallgather /
- * coll_ibcast (coll.h:261-265, 293-296, 319-322) and the persistent
- * coll_allreduce_init (coll.h:349-352)
+ * coll_ibcast, coll_ireduce, coll_iscan, coll_iexscan, coll_ireduce_scatter
+ * (coll.h:261-326) and the persistent coll_allreduce_init,
+ * coll_reduce_scatter_block_init, coll_allgather_init and coll_bcast_init
+ * (coll.h:339-400)
  * for device buffers through libompi_amd.so,
  * and interposes on the previously selected functions (coll/tuned, coll/basic
  * for scan/exscan) for everything else, exactly like coll/cuda does
@@ -132,6 +134,31 @@ int mca_coll_rocm_allreduce_init(const void *sbuf, void *rbuf, int count,
                                  ompi_request_t **request, mca_coll_base_module_t *module);
 int mca_coll_rocm_bcast(void *buf, int count, struct ompi_datatype_t *dtype, int root,
                         struct ompi_communicator_t *comm, mca_coll_base_module_t *module);
+int mca_coll_rocm_ireduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                          struct ompi_op_t *op, int root, struct ompi_communicator_t *comm,
+                          ompi_request_t **request, mca_coll_base_module_t *module);
+int mca_coll_rocm_iscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                        struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                        ompi_request_t **request, mca_coll_base_module_t *module);
+int mca_coll_rocm_iexscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                          struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                          ompi_request_t **request, mca_coll_base_module_t *module);
+int mca_coll_rocm_ireduce_scatter(const void *sbuf, void *rbuf, const int *rcounts,
+                                  struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                  struct ompi_communicator_t *comm, ompi_request_t **request,
+                                  mca_coll_base_module_t *module);
+int mca_coll_rocm_reduce_scatter_block_init(const void *sbuf, void *rbuf, int rcount,
+                                            struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                            struct ompi_communicator_t *comm,
+                                            struct ompi_info_t *info, ompi_request_t **request,
+                                            mca_coll_base_module_t *module);
+int mca_coll_rocm_allgather_init(const void *sbuf, int scount, struct ompi_datatype_t *sdtype,
+                                 void *rbuf, int rcount, struct ompi_datatype_t *rdtype,
+                                 struct ompi_communicator_t *comm, struct ompi_info_t *info,
+                                 ompi_request_t **request, mca_coll_base_module_t *module);
+int mca_coll_rocm_bcast_init(void *buf, int count, struct ompi_datatype_t *dtype, int root,
+                             struct ompi_communicator_t *comm, struct ompi_info_t *info,
+                             ompi_request_t **request, mca_coll_base_module_t *module);
 
 END_C_DECLS
 

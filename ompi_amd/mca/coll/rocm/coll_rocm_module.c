@@ -173,6 +173,16 @@ static void rocm_module_destruct(mca_coll_rocm_module_t *m)
     if (NULL != m->c_coll.coll_ibcast_module) OBJ_RELEASE(m->c_coll.coll_ibcast_module);
     if (NULL != m->c_coll.coll_ireduce_scatter_block_module)
         OBJ_RELEASE(m->c_coll.coll_ireduce_scatter_block_module);
+    if (NULL != m->c_coll.coll_ireduce_module) OBJ_RELEASE(m->c_coll.coll_ireduce_module);
+    if (NULL != m->c_coll.coll_iscan_module) OBJ_RELEASE(m->c_coll.coll_iscan_module);
+    if (NULL != m->c_coll.coll_iexscan_module) OBJ_RELEASE(m->c_coll.coll_iexscan_module);
+    if (NULL != m->c_coll.coll_ireduce_scatter_module)
+        OBJ_RELEASE(m->c_coll.coll_ireduce_scatter_module);
+    if (NULL != m->c_coll.coll_reduce_scatter_block_init_module)
+        OBJ_RELEASE(m->c_coll.coll_reduce_scatter_block_init_module);
+    if (NULL != m->c_coll.coll_allgather_init_module)
+        OBJ_RELEASE(m->c_coll.coll_allgather_init_module);
+    if (NULL != m->c_coll.coll_bcast_init_module) OBJ_RELEASE(m->c_coll.coll_bcast_init_module);
     if (NULL != m->dev_comm) (void) ompi_amd_comm_destroy(m->dev_comm);
     for (int k = 0; k < 2; ++k) {
         (void) ompi_amd_device_free(m->dstage[k]);
@@ -214,6 +224,13 @@ mca_coll_base_module_t *mca_coll_rocm_comm_query(struct ompi_communicator_t *com
     m->super.coll_ibcast = mca_coll_rocm_ibcast;
     m->super.coll_ireduce_scatter_block = mca_coll_rocm_ireduce_scatter_block;
     m->super.coll_allreduce_init = mca_coll_rocm_allreduce_init;
+    m->super.coll_ireduce = mca_coll_rocm_ireduce;
+    m->super.coll_iscan = mca_coll_rocm_iscan;
+    m->super.coll_iexscan = mca_coll_rocm_iexscan;
+    m->super.coll_ireduce_scatter = mca_coll_rocm_ireduce_scatter;
+    m->super.coll_reduce_scatter_block_init = mca_coll_rocm_reduce_scatter_block_init;
+    m->super.coll_allgather_init = mca_coll_rocm_allgather_init;
+    m->super.coll_bcast_init = mca_coll_rocm_bcast_init;
     return &m->super;
 }
 
@@ -243,6 +260,13 @@ int mca_coll_rocm_module_enable(mca_coll_base_module_t *module, struct ompi_comm
     SAVE(ibcast);
     SAVE(ireduce_scatter_block);
     SAVE(allreduce_init);
+    SAVE(ireduce);
+    SAVE(iscan);
+    SAVE(iexscan);
+    SAVE(ireduce_scatter);
+    SAVE(reduce_scatter_block_init);
+    SAVE(allgather_init);
+    SAVE(bcast_init);
 #undef SAVE
 
     /* node-unique segment name: job id + communicator id */
@@ -972,4 +996,169 @@ int mca_coll_rocm_allreduce_init(const void *sbuf, void *rbuf, int count,
     r->plan = plan;
     *request = &r->super;
     return OMPI_SUCCESS;
+}
+
+/* MPI_Ireduce / MPI_Iscan / MPI_Iexscan / MPI_Ireduce_scatter (coll.h:
+ * 297-326): the per-call vote, then the library posts the call (no handle
+ * swap; ompi_amd_ireduce posts the root's in-place choice) and the glue
+ * returns a request on the active list; otherwise the saved (libnbc)
+ * functions.  MPI_Ireduce's rbuf matters at the root only. */
+int mca_coll_rocm_ireduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                          struct ompi_op_t *op, int root, struct ompi_communicator_t *comm,
+                          ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const int is_root = ompi_comm_rank(comm) == root;
+    ompi_amd_request_t *nb = NULL;
+    int rc;
+    if (!take_device_path(m, reduction_ok_n(dtype, op, (size_t) count) &&
+                                 (is_root ? dev(rbuf) && dev(sbuf) : ompi_amd_is_device_pointer(sbuf)))) {
+        return m->c_coll.coll_ireduce(sbuf, rbuf, count, dtype, op, root, comm, request,
+                                      m->c_coll.coll_ireduce_module);
+    }
+    rc = ompi_amd_ireduce(m->dev_comm, sbuf, is_root ? rbuf : NULL, (size_t) count, type_code(dtype),
+                          op->o_f_to_c_index, root, NULL, &nb);
+    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
+    return rocm_wrap_nb(nb, comm, request);
+}
+
+static int rocm_iscan_common(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                             struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                             ompi_request_t **request, mca_coll_rocm_module_t *m, int exclusive)
+{
+    ompi_amd_request_t *nb = NULL;
+    int rc;
+    if (!take_device_path(m, reduction_ok_n(dtype, op, (size_t) count) && dev(sbuf) && dev(rbuf))) {
+        return exclusive ? m->c_coll.coll_iexscan(sbuf, rbuf, count, dtype, op, comm, request,
+                                                  m->c_coll.coll_iexscan_module)
+                         : m->c_coll.coll_iscan(sbuf, rbuf, count, dtype, op, comm, request,
+                                                m->c_coll.coll_iscan_module);
+    }
+    rc = (exclusive ? ompi_amd_iexscan : ompi_amd_iscan)(m->dev_comm, sbuf, rbuf, (size_t) count,
+                                                         type_code(dtype), op->o_f_to_c_index, NULL,
+                                                         &nb);
+    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
+    return rocm_wrap_nb(nb, comm, request);
+}
+
+int mca_coll_rocm_iscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                        struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                        ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    return rocm_iscan_common(sbuf, rbuf, count, dtype, op, comm, request,
+                             (mca_coll_rocm_module_t *) module, 0);
+}
+
+int mca_coll_rocm_iexscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                          struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                          ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    return rocm_iscan_common(sbuf, rbuf, count, dtype, op, comm, request,
+                             (mca_coll_rocm_module_t *) module, 1);
+}
+
+int mca_coll_rocm_ireduce_scatter(const void *sbuf, void *rbuf, const int *rcounts,
+                                  struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                  struct ompi_communicator_t *comm, ompi_request_t **request,
+                                  mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const int n = ompi_comm_size(comm);
+    size_t counts[OMPI_AMD_MAX_RANKS], total = 0;
+    ompi_amd_request_t *nb = NULL;
+    int rc, i;
+    for (i = 0; i < n; ++i) total += (size_t) rcounts[i];
+    if (!take_device_path(m, reduction_ok_n(dtype, op, total) && dev(sbuf) && dev(rbuf))) {
+        return m->c_coll.coll_ireduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, request,
+                                              m->c_coll.coll_ireduce_scatter_module);
+    }
+    for (i = 0; i < n; ++i) counts[i] = (size_t) rcounts[i];
+    rc = ompi_amd_ireduce_scatter(m->dev_comm, sbuf, rbuf, counts, type_code(dtype),
+                                  op->o_f_to_c_index, NULL, &nb);
+    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
+    return rocm_wrap_nb(nb, comm, request);
+}
+
+/* MPI_Reduce_scatter_block_init / MPI_Allgather_init / MPI_Bcast_init
+ * (coll.h:339-400): the same agreement as the blocking calls; on the device
+ * path a library plan behind a persistent request (its start posts the
+ * nonblocking call, completion through the progress callback), otherwise
+ * the saved (libnbc) functions build the request. */
+static int rocm_wrap_plan(ompi_amd_plan_t *plan, struct ompi_communicator_t *comm,
+                          ompi_request_t **request)
+{
+    mca_coll_rocm_request_t *r = OBJ_NEW(mca_coll_rocm_request_t);
+    if (NULL == r) {
+        (void) ompi_amd_plan_free(plan);
+        return OMPI_ERROR;
+    }
+    OMPI_REQUEST_INIT(&r->super, true);
+    r->super.req_mpi_object.comm = comm;
+    r->plan = plan;
+    *request = &r->super;
+    return OMPI_SUCCESS;
+}
+
+int mca_coll_rocm_reduce_scatter_block_init(const void *sbuf, void *rbuf, int rcount,
+                                            struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                            struct ompi_communicator_t *comm,
+                                            struct ompi_info_t *info, ompi_request_t **request,
+                                            mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    ompi_amd_plan_t *plan = NULL;
+    int rc;
+    if (!take_device_path(m, reduction_ok_n(dtype, op, (size_t) rcount * (size_t) ompi_comm_size(comm)) &&
+                                 dev(sbuf) && dev(rbuf))) {
+        return m->c_coll.coll_reduce_scatter_block_init(sbuf, rbuf, rcount, dtype, op, comm, info,
+                                                        request,
+                                                        m->c_coll.coll_reduce_scatter_block_init_module);
+    }
+    rc = ompi_amd_reduce_scatter_block_init(m->dev_comm, sbuf, rbuf, (size_t) rcount,
+                                            type_code(dtype), op->o_f_to_c_index, &plan);
+    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
+    return rocm_wrap_plan(plan, comm, request);
+}
+
+int mca_coll_rocm_allgather_init(const void *sbuf, int scount, struct ompi_datatype_t *sdtype,
+                                 void *rbuf, int rcount, struct ompi_datatype_t *rdtype,
+                                 struct ompi_communicator_t *comm, struct ompi_info_t *info,
+                                 ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const int inplace = MPI_IN_PLACE == sbuf;
+    ompi_amd_plan_t *plan = NULL;
+    size_t rsize = 0;
+    int rc, ok;
+    (void) ompi_datatype_type_size(rdtype, &rsize);
+    ok = bytes_ok(rsize * (size_t) rcount) &&
+         ompi_datatype_is_contiguous_memory_layout(rdtype, rcount * ompi_comm_size(comm)) &&
+         dev(rbuf) && dev(sbuf) && (inplace || ompi_datatype_is_contiguous_memory_layout(sdtype, scount));
+    if (!take_device_path(m, ok)) {
+        return m->c_coll.coll_allgather_init(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, info,
+                                             request, m->c_coll.coll_allgather_init_module);
+    }
+    rc = ompi_amd_allgather_init(m->dev_comm, inplace ? (const void *) 1 : sbuf, rbuf,
+                                 rsize * (size_t) rcount, &plan);
+    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
+    return rocm_wrap_plan(plan, comm, request);
+}
+
+int mca_coll_rocm_bcast_init(void *buf, int count, struct ompi_datatype_t *dtype, int root,
+                             struct ompi_communicator_t *comm, struct ompi_info_t *info,
+                             ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    ompi_amd_plan_t *plan = NULL;
+    size_t size = 0;
+    int rc;
+    (void) ompi_datatype_type_size(dtype, &size);
+    if (!take_device_path(m, bytes_ok(size * (size_t) count) &&
+                                 ompi_datatype_is_contiguous_memory_layout(dtype, count) && dev(buf))) {
+        return m->c_coll.coll_bcast_init(buf, count, dtype, root, comm, info, request,
+                                         m->c_coll.coll_bcast_init_module);
+    }
+    rc = ompi_amd_bcast_init(m->dev_comm, buf, size * (size_t) count, root, &plan);
+    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
+    return rocm_wrap_plan(plan, comm, request);
 }

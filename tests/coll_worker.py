@@ -238,6 +238,132 @@ def case_rs(comm, rank, n, dt, op, rcounts, salt, inplace=False, kind="R"):
     return checked(got, exp[rank].view(dt.np_dtype))
 
 
+def case_nb_reduce_scan_rs(comm, rank, n, salt, big):
+    """MPI_Ireduce / MPI_Iscan / MPI_Iexscan / MPI_Ireduce_scatter (coll.h:
+    276-300): eight calls outstanding at once — staged and landing sizes,
+    the root in place, uneven reduce_scatter counts with an empty block and
+    in place — with a blocking allreduce posted in between and rank 0
+    posting while its peers sleep; every result bit-exact against the
+    oracle's order of the blocking call."""
+    import time
+    F, D, I32 = mop.MPI_FLOAT, mop.MPI_DOUBLE, mop.MPI_INT32_T
+    SUM, MAX = mop.MPI_SUM, mop.MPI_MAX
+    checks, reqs = [], []
+    if rank != 0:
+        time.sleep(0.3)  # rank 0 posts everything before its peers arrive
+
+    def ireduce(dt, op, count, root, inplace, sl):
+        root %= n
+        xs = [inputs(dt, count, r, sl) for r in range(n)]
+        exp, _ = orc.reduce([x.copy() for x in xs], count, op.index, dt.code, root, inplace)
+        s = to_dev(xs[rank])
+        out = None
+        if rank == root:
+            out = s if inplace else torch.zeros_like(s)
+            reqs.append(comm.ireduce(coll.IN_PLACE if inplace else s, out, count, dt, op, root))
+            checks.append((f"ireduce {count} root {root}", out, count, dt, exp))
+        else:
+            reqs.append(comm.ireduce(s, None, count, dt, op, root))
+        checks.append(("keep", s, 0, dt, None))
+
+    def iscan(dt, op, count, exclusive, inplace, sl):
+        xs = [inputs(dt, count, r, sl) for r in range(n)]
+        exp = orc.scan([x.copy() for x in xs], count, op.index, dt.code, exclusive)
+        s = to_dev(xs[rank])
+        out = s if inplace else torch.zeros_like(s)
+        reqs.append(comm.iscan(coll.IN_PLACE if inplace else s, out, count, dt, op,
+                               exclusive=exclusive))
+        if not (exclusive and rank == 0):
+            checks.append((f"{'iexscan' if exclusive else 'iscan'} {count}", out, count, dt, exp[rank]))
+        checks.append(("keep", s, 0, dt, None))
+
+    def irs(dt, op, rcounts, inplace, sl):
+        total = sum(rcounts)
+        xs = [inputs(dt, total, r, sl) for r in range(n)]
+        exp, _ = orc.reduce_scatter([x.copy() for x in xs], rcounts, op.index, dt.code)
+        s = to_dev(xs[rank], extra=16)
+        out = s if inplace else torch.zeros((rcounts[rank] + 1) * dt.extent, dtype=torch.uint8,
+                                            device="cuda")
+        reqs.append(comm.ireduce_scatter(coll.IN_PLACE if inplace else s, out, rcounts, dt, op))
+        checks.append((f"ireduce_scatter {total}", out, rcounts[rank], dt, exp[rank]))
+        checks.append(("keep", s, 0, dt, None))
+
+    ireduce(F, SUM, 3001, n - 1, False, salt)
+    ireduce(D, SUM, big // 2 + 3, 1, True, salt + 1)
+    iscan(F, SUM, big + 7, False, False, salt + 2)
+    iscan(I32, MAX, 5000, True, True, salt + 3)
+    irs(F, SUM, [big // n + 5 * r if r != 1 else 0 for r in range(n)], False, salt + 4)
+    # a blocking collective between the posts (it launches the deferred ones first)
+    ok_b, msg_b = case_allreduce(comm, rank, n, F, SUM, 12345, salt + 5)
+    irs(D, SUM, [big // (2 * n) + r for r in range(n)], True, salt + 6)
+    ireduce(F, MAX, big + 11, 0, False, salt + 7)
+    iscan(D, SUM, 999, True, False, salt + 8)
+    for r in reqs:
+        r.wait()
+        r.free()
+    torch.cuda.synchronize()
+    msgs = [] if ok_b else [f"allreduce in between: {msg_b}"]
+    for name, out, count, dt, exp in checks:
+        if exp is None:
+            continue
+        got = out.cpu().numpy()[:count * dt.extent].view(dt.np_dtype)
+        ok, msg = checked(got, np.asarray(exp).view(dt.np_dtype)[:count])
+        if not ok:
+            msgs.append(f"{name}: {msg}")
+    return not msgs, "; ".join(msgs)
+
+
+def case_persistent_rsb_ag_bcast(comm, rank, n, salt, big):
+    """MPI_Reduce_scatter_block_init / MPI_Allgather_init / MPI_Bcast_init
+    (coll.h:545-566): three starts each with fresh data in the same buffers,
+    staged and zero-copy sizes, in place, every result checked against the
+    oracle / the expected bytes; the three plans started back to back before
+    any wait."""
+    DI, F = mop.MPI_DOUBLE_INT, mop.MPI_FLOAT
+    msgs = []
+    for size_tag, rc_di, ag_bytes, bc_bytes in (("staged", 1000, 5000, 4097),
+                                                ("zero_copy", big // 8 + 3, (big * 4) // n + 20,
+                                                 big * 4 + 13)):
+        sb = torch.zeros(rc_di * n * DI.extent, dtype=torch.uint8, device="cuda")
+        rb = torch.zeros(rc_di * DI.extent, dtype=torch.uint8, device="cuda")
+        agin = torch.zeros(ag_bytes, dtype=torch.uint8, device="cuda")
+        agout = torch.zeros(ag_bytes * n, dtype=torch.uint8, device="cuda")
+        bc = torch.zeros(bc_bytes, dtype=torch.uint8, device="cuda")
+        root = (salt + len(size_tag)) % n
+        p_rsb = comm.reduce_scatter_block_init(sb, rb, rc_di, DI, mop.MPI_MAXLOC)
+        p_ag = comm.allgather_init(agin, agout, ag_bytes)
+        p_bc = comm.bcast_init(bc, bc_bytes, root)
+        try:
+            for it in range(3):
+                xs = [inputs(DI, rc_di * n, r, salt + it) for r in range(n)]
+                exp = orc.reduce_scatter_block([x.copy() for x in xs], rc_di, mop.MPI_MAXLOC.index, DI.code)
+                sb.copy_(torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda())
+                pays = [np.random.default_rng(SEED + 77 * it + r).integers(0, 256, ag_bytes, dtype=np.uint8)
+                        for r in range(n)]
+                agin.copy_(torch.from_numpy(pays[rank]).cuda())
+                bpay = np.random.default_rng(SEED + 99 * it).integers(0, 256, bc_bytes, dtype=np.uint8)
+                bc.copy_(torch.from_numpy(bpay if rank == root else np.zeros(bc_bytes, np.uint8)).cuda())
+                torch.cuda.synchronize()
+                p_rsb.start()
+                p_ag.start()
+                p_bc.start()
+                for p in (p_rsb, p_ag, p_bc):
+                    p.wait()
+                torch.cuda.synchronize()
+                got = rb.cpu().numpy().view(DI.np_dtype)
+                ok, msg = checked(got, exp[rank].view(DI.np_dtype))
+                if not ok:
+                    msgs.append(f"{size_tag} start {it} rsb: {msg}")
+                if not np.array_equal(agout.cpu().numpy(), np.concatenate(pays)):
+                    msgs.append(f"{size_tag} start {it} allgather differs")
+                if not np.array_equal(bc.cpu().numpy(), bpay):
+                    msgs.append(f"{size_tag} start {it} bcast differs")
+        finally:
+            for p in (p_rsb, p_ag, p_bc):
+                p.free()
+    return not msgs, "; ".join(msgs)
+
+
 def case_regrow(comm, rank, n, salt):
     """Landing-buffer growth several times in a row (large scans of rising
     size, an in-place reduce_scatter in between), every result checked."""
@@ -835,6 +961,8 @@ def main():
             ("persistent_inplace_sum_f32", lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, 300001, 146,
                                                                    inplace=True)),
             ("nonblocking_rsb_ag_bcast", lambda: case_nonblocking_mix(comm, rank, n, 150, big)),
+            ("nonblocking_reduce_scan_rs", lambda: case_nb_reduce_scan_rs(comm, rank, n, 180, big)),
+            ("persistent_rsb_allgather_bcast", lambda: case_persistent_rsb_ag_bcast(comm, rank, n, 190, big)),
             ("nonblocking_rsb_ag_bcast_shadow",
              shadowed_nb(lambda: case_nonblocking_mix(comm, rank, n, 160, big))),
         ]

@@ -140,6 +140,28 @@ static int t_irsb(const void *s, void *r, int c, struct ompi_datatype_t *d, stru
                   struct ompi_communicator_t *cm, ompi_request_t **req, mca_coll_base_module_t *m)
 { tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
 
+static int t_ireduce(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                     int root, struct ompi_communicator_t *cm, ompi_request_t **req,
+                     mca_coll_base_module_t *m)
+{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
+static int t_iscan(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                   struct ompi_communicator_t *cm, ompi_request_t **req, mca_coll_base_module_t *m)
+{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
+static int t_irs(const void *s, void *r, const int *c, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                 struct ompi_communicator_t *cm, ompi_request_t **req, mca_coll_base_module_t *m)
+{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
+static int t_rsb_init(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
+                      struct ompi_communicator_t *cm, struct ompi_info_t *info, ompi_request_t **req,
+                      mca_coll_base_module_t *m)
+{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
+static int t_ag_init(const void *s, int sc, struct ompi_datatype_t *sd, void *r, int rc,
+                     struct ompi_datatype_t *rd, struct ompi_communicator_t *cm,
+                     struct ompi_info_t *info, ompi_request_t **req, mca_coll_base_module_t *m)
+{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
+static int t_bc_init(void *b, int c, struct ompi_datatype_t *d, int root, struct ompi_communicator_t *cm,
+                     struct ompi_info_t *info, ompi_request_t **req, mca_coll_base_module_t *m)
+{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
+
 static void fill_tuned(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *tm)
 {
     memset(t, 0, sizeof(*t));
@@ -157,6 +179,13 @@ static void fill_tuned(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *tm)
     SET(iallgather, t_iallgather);
     SET(ibcast, t_ibcast);
     SET(ireduce_scatter_block, t_irsb);
+    SET(ireduce, t_ireduce);
+    SET(iscan, t_iscan);
+    SET(iexscan, t_iscan);
+    SET(ireduce_scatter, t_irs);
+    SET(reduce_scatter_block_init, t_rsb_init);
+    SET(allgather_init, t_ag_init);
+    SET(bcast_init, t_bc_init);
 #undef SET
 }
 
@@ -169,6 +198,8 @@ static void install(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *m)
     INST(exscan)
     INST(allgather) INST(bcast) INST(iallreduce) INST(allreduce_init)
     INST(iallgather) INST(ibcast) INST(ireduce_scatter_block)
+    INST(ireduce) INST(iscan) INST(iexscan) INST(ireduce_scatter)
+    INST(reduce_scatter_block_init) INST(allgather_init) INST(bcast_init)
 #undef INST
 }
 
@@ -187,6 +218,13 @@ static void release_table(mca_coll_base_comm_coll_t *t)
     OBJ_RELEASE(t->coll_iallgather_module);
     OBJ_RELEASE(t->coll_ibcast_module);
     OBJ_RELEASE(t->coll_ireduce_scatter_block_module);
+    OBJ_RELEASE(t->coll_ireduce_module);
+    OBJ_RELEASE(t->coll_iscan_module);
+    OBJ_RELEASE(t->coll_iexscan_module);
+    OBJ_RELEASE(t->coll_ireduce_scatter_module);
+    OBJ_RELEASE(t->coll_reduce_scatter_block_init_module);
+    OBJ_RELEASE(t->coll_allgather_init_module);
+    OBJ_RELEASE(t->coll_bcast_init_module);
 }
 
 /* deterministic per-rank floats in [-1, 1): fp sums depend on order */
@@ -261,6 +299,8 @@ int main(int argc, char **argv)
               m->coll_reduce_scatter_block && m->coll_scan &&
               m->coll_exscan && m->coll_allgather && m->coll_bcast && m->coll_allreduce_init && m->coll_iallreduce &&
               m->coll_iallgather && m->coll_ibcast && m->coll_ireduce_scatter_block &&
+              m->coll_ireduce && m->coll_iscan && m->coll_iexscan && m->coll_ireduce_scatter &&
+              m->coll_reduce_scatter_block_init && m->coll_allgather_init && m->coll_bcast_init &&
               m->coll_module_enable,
           "module function table");
     {
@@ -285,7 +325,7 @@ int main(int argc, char **argv)
     }
 
     CHECK(m->coll_module_enable(m, &comm) == OMPI_SUCCESS, "enable");
-    CHECK(tm->super.obj_reference_count == 1 + 13 + 13, "enable retains the saved modules (%d)",
+    CHECK(tm->super.obj_reference_count == 1 + 20 + 20, "enable retains the saved modules (%d)",
           tm->super.obj_reference_count);
     install(&table, m);
     /* sections 1-8: the per-call residency vote (never locks) */
@@ -656,6 +696,161 @@ int main(int argc, char **argv)
             CHECK(table.coll_ibcast(h, 64, &dbyte, 0, &comm, &hr, table.coll_ibcast_module) ==
                       OMPI_SUCCESS && tuned_calls == 1 && hr == &t_request,
                   "host ibcast falls back");
+        }
+    }
+    /* 11. MPI_Ireduce / MPI_Iscan / MPI_Iexscan / MPI_Ireduce_scatter and the
+     * persistent MPI_Reduce_scatter_block_init / MPI_Allgather_init /
+     * MPI_Bcast_init through the communicator's table, on device buffers,
+     * all outstanding at once, every result against the oracle; host
+     * buffers go to the saved functions */
+    {
+        const size_t counts[2] = {1500, 300001};
+        ompi_request_t *req[16];
+        int nr = 0;
+        void *d_in[2], *d_red[2], *d_scan[2], *d_exs[2], *d_rs[2], *d_rsbi[2], *d_rsbo[2];
+        float **xs[2], *redexp[2], **scanexp[2], **exsexp[2], **rsexp[2], **rsbexp[2];
+        float **rsbin[2];
+        int rcounts[2][OMPI_AMD_MAX_RANKS];
+        size_t rcz[2][OMPI_AMD_MAX_RANKS];
+        tuned_calls = 0;
+        for (int k = 0; k < 2; ++k) {
+            const size_t n = counts[k];
+            size_t total = 0;
+            const int root = (k + 1) % g_size;
+            xs[k] = all_inputs(n, 110 + k);
+            redexp[k] = calloc(n, 4);
+            scanexp[k] = malloc(sizeof(float *) * (size_t) g_size);
+            exsexp[k] = malloc(sizeof(float *) * (size_t) g_size);
+            rsexp[k] = malloc(sizeof(float *) * (size_t) g_size);
+            for (int r = 0; r < g_size; ++r) {
+                scanexp[k][r] = calloc(n, 4);
+                exsexp[k][r] = calloc(n, 4);
+                rcounts[k][r] = (int) (n / (size_t) g_size) + (r == 1 ? -7 : 3 * r);
+                rcz[k][r] = (size_t) rcounts[k][r];
+                total += rcz[k][r];
+            }
+            for (int r = 0; r < g_size; ++r) rsexp[k][r] = calloc(rcz[k][r] + 1, 4);
+            CHECK(total <= n, "rs total");
+            CHECK(orc_reduce(ORC_RED_TUNED, g_size, (const void *const *) xs[k], redexp[k], n, ORC_OP_SUM,
+                             ORC_T_FLOAT, root, 0) >= 0, "oracle reduce");
+            CHECK(orc_scan(0, g_size, (const void *const *) xs[k], (void *const *) scanexp[k], n, ORC_OP_SUM,
+                           ORC_T_FLOAT) >= 0, "oracle scan");
+            CHECK(orc_scan(1, g_size, (const void *const *) xs[k], (void *const *) exsexp[k], n, ORC_OP_SUM,
+                           ORC_T_FLOAT) >= 0, "oracle exscan");
+            CHECK(orc_reduce_scatter(ORC_RS_TUNED, g_size, (const void *const *) xs[k], (void *const *) rsexp[k],
+                                     rcz[k], ORC_OP_SUM, ORC_T_FLOAT) >= 0, "oracle reduce_scatter");
+            d_in[k] = dev_of(xs[k][g_rank], n * 4);
+            {
+                float *z = calloc(n + 1, 4);
+                d_red[k] = dev_of(z, n * 4);
+                d_scan[k] = dev_of(z, n * 4);
+                d_exs[k] = dev_of(z, n * 4);
+                d_rs[k] = dev_of(z, (rcz[k][g_rank] + 1) * 4);
+                free(z);
+            }
+            CHECK(table.coll_ireduce(d_in[k], g_rank == root ? d_red[k] : NULL, (int) n, &dfloat, &sum, root,
+                                     &comm, &req[nr++], table.coll_ireduce_module) == OMPI_SUCCESS,
+                  "ireduce");
+            CHECK(table.coll_iscan(d_in[k], d_scan[k], (int) n, &dfloat, &sum, &comm, &req[nr++],
+                                   table.coll_iscan_module) == OMPI_SUCCESS, "iscan");
+            CHECK(table.coll_iexscan(d_in[k], d_exs[k], (int) n, &dfloat, &sum, &comm, &req[nr++],
+                                     table.coll_iexscan_module) == OMPI_SUCCESS, "iexscan");
+            CHECK(table.coll_ireduce_scatter(d_in[k], d_rs[k], rcounts[k], &dfloat, &sum, &comm, &req[nr++],
+                                             table.coll_ireduce_scatter_module) == OMPI_SUCCESS,
+                  "ireduce_scatter");
+        }
+        CHECK(tuned_calls == 0, "device ireduce / iscan / ireduce_scatter fell back");
+        for (int i = 0; i < nr; ++i) {
+            harness_wait(req[i]);
+            CHECK(req[i]->req_status.MPI_ERROR == OMPI_SUCCESS, "status");
+            CHECK(req[i]->req_free(&req[i]) == OMPI_SUCCESS, "free");
+        }
+        for (int k = 0; k < 2; ++k) {
+            const size_t n = counts[k];
+            if (g_rank == (k + 1) % g_size) expect_dev(d_red[k], redexp[k], n * 4, "ireduce");
+            expect_dev(d_scan[k], scanexp[k][g_rank], n * 4, "iscan");
+            if (g_rank > 0) expect_dev(d_exs[k], exsexp[k][g_rank], n * 4, "iexscan");
+            expect_dev(d_rs[k], rsexp[k][g_rank], rcz[k][g_rank] * 4, "ireduce_scatter");
+        }
+        /* persistent: three starts of each, fresh data every time */
+        for (int k = 0; k < 2; ++k) {
+            const size_t rc = counts[k] / (size_t) g_size;
+            ompi_request_t *pr[3];
+            unsigned char *ag_all = malloc(rc * 4 * (size_t) g_size), *bc_data = malloc(rc * 4);
+            void *ag_d, *bc_d;
+            rsbin[k] = all_inputs(rc * (size_t) g_size, 120 + k);
+            rsbexp[k] = malloc(sizeof(float *) * (size_t) g_size);
+            for (int r = 0; r < g_size; ++r) rsbexp[k][r] = calloc(rc, 4);
+            d_rsbi[k] = dev_of(rsbin[k][g_rank], rc * 4 * (size_t) g_size);
+            {
+                float *z = calloc(rc + 1, 4);
+                d_rsbo[k] = dev_of(z, rc * 4);
+                free(z);
+                unsigned char *zb = calloc(rc * 4 * (size_t) g_size, 1);
+                ag_d = dev_of(zb, rc * 4 * (size_t) g_size);
+                bc_d = dev_of(zb, rc * 4);
+                free(zb);
+            }
+            CHECK(table.coll_reduce_scatter_block_init(d_rsbi[k], d_rsbo[k], (int) rc, &dfloat, &sum, &comm,
+                                                       NULL, &pr[0],
+                                                       table.coll_reduce_scatter_block_init_module) ==
+                      OMPI_SUCCESS && pr[0]->req_persistent, "reduce_scatter_block_init");
+            CHECK(table.coll_allgather_init(MPI_IN_PLACE, 0, &dbyte, ag_d, (int) (rc * 4), &dbyte, &comm, NULL,
+                                            &pr[1], table.coll_allgather_init_module) == OMPI_SUCCESS &&
+                      pr[1]->req_persistent, "allgather_init");
+            CHECK(table.coll_bcast_init(bc_d, (int) (rc * 4), &dbyte, k % g_size, &comm, NULL, &pr[2],
+                                        table.coll_bcast_init_module) == OMPI_SUCCESS &&
+                      pr[2]->req_persistent, "bcast_init");
+            CHECK(tuned_calls == 0, "device persistent inits fell back");
+            for (int it = 0; it < 3; ++it) {
+                for (int r = 0; r < g_size; ++r) gen(rsbin[k][r], rc * (size_t) g_size, r, 130 + 10 * k + it);
+                CHECK(orc_reduce_scatter_block(g_size, (const void *const *) rsbin[k], (void *const *) rsbexp[k],
+                                               rc, ORC_OP_SUM, ORC_T_FLOAT) >= 0, "oracle rsb");
+                CHECK(harness_dev_copy_in(d_rsbi[k], rsbin[k][g_rank], rc * 4 * (size_t) g_size) == 0, "in");
+                for (int r = 0; r < g_size; ++r)
+                    for (size_t b = 0; b < rc * 4; ++b) ag_all[(size_t) r * rc * 4 + b] = (unsigned char) (r * 7 + b + it);
+                for (size_t b = 0; b < rc * 4; ++b) bc_data[b] = (unsigned char) (b * 3 + it + k);
+                {
+                    unsigned char *zb = calloc(rc * 4 * (size_t) g_size, 1);
+                    memcpy(zb + (size_t) g_rank * rc * 4, ag_all + (size_t) g_rank * rc * 4, rc * 4);
+                    CHECK(harness_dev_copy_in(ag_d, zb, rc * 4 * (size_t) g_size) == 0, "ag in");
+                    CHECK(harness_dev_copy_in(bc_d, g_rank == k % g_size ? bc_data : zb, rc * 4) == 0, "bc in");
+                    free(zb);
+                }
+                for (int i = 0; i < 3; ++i)  /* MPI_Startall (request.h:60-77) */
+                    CHECK(pr[i]->req_start(1, &pr[i]) == OMPI_SUCCESS, "start");
+                for (int i = 0; i < 3; ++i) {
+                    harness_wait(pr[i]);
+                    CHECK(pr[i]->req_status.MPI_ERROR == OMPI_SUCCESS, "persistent status");
+                }
+                expect_dev(d_rsbo[k], rsbexp[k][g_rank], rc * 4, "reduce_scatter_block_init start");
+                expect_dev(ag_d, ag_all, rc * 4 * (size_t) g_size, "allgather_init start");
+                expect_dev(bc_d, bc_data, rc * 4, "bcast_init start");
+            }
+            for (int i = 0; i < 3; ++i) CHECK(pr[i]->req_free(&pr[i]) == OMPI_SUCCESS, "persistent free");
+            harness_dev_free(ag_d);
+            harness_dev_free(bc_d);
+            free(ag_all);
+            free(bc_data);
+        }
+        for (int k = 0; k < 2; ++k) {
+            harness_dev_free(d_in[k]); harness_dev_free(d_red[k]); harness_dev_free(d_scan[k]);
+            harness_dev_free(d_exs[k]); harness_dev_free(d_rs[k]); harness_dev_free(d_rsbi[k]);
+            harness_dev_free(d_rsbo[k]);
+            for (int r = 0; r < g_size; ++r) {
+                free(scanexp[k][r]); free(exsexp[k][r]); free(rsexp[k][r]); free(rsbexp[k][r]);
+            }
+            free(scanexp[k]); free(exsexp[k]); free(rsexp[k]); free(rsbexp[k]); free(redexp[k]);
+            free_inputs(xs[k]);
+            free_inputs(rsbin[k]);
+        }
+        {
+            float h[16] = {0}, h2[16] = {0};
+            ompi_request_t *hr = NULL;
+            CHECK(table.coll_iscan(h, h2, 16, &dfloat, &sum, &comm, &hr, table.coll_iscan_module) ==
+                      OMPI_SUCCESS && tuned_calls == 1 && hr == &t_request, "host iscan falls back");
+            CHECK(table.coll_bcast_init(h, 16, &dbyte, 0, &comm, NULL, &hr, table.coll_bcast_init_module) ==
+                      OMPI_SUCCESS && tuned_calls == 2 && hr == &t_request, "host bcast_init falls back");
         }
     }
     /* 9. residency policy: unanimous votes lock the module, a locked call
