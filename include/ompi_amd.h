@@ -28,6 +28,7 @@ extern "C" {
 #define OMPI_AMD_ERR_TIMEOUT       (-4)  /* a peer never reached a flag    */
 #define OMPI_AMD_ERR_NOT_DEVICE    (-5)  /* buffer is not device memory    */
 #define OMPI_AMD_ERR_BOOTSTRAP     (-6)  /* shared-memory rendezvous failed */
+#define OMPI_AMD_ERR_RMA_SYNC      (-7)  /* RMA epoch call out of order (OMPI_ERR_RMA_SYNC) */
 
 /* ------------------------------------------------------------------ */
 /* Op and type codes — numerically identical to the reference enums so */

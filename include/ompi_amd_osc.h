@@ -51,6 +51,7 @@ extern "C" {
 #define OMPI_AMD_MODE_NOCHECK   1     /* MPI_MODE_NOCHECK (mpi.h.in:542): lock takes no lock */
 
 typedef struct ompi_amd_win ompi_amd_win_t;
+typedef struct ompi_amd_rma_request ompi_amd_rma_request_t;
 
 /* MPI_Win_create over device memory [base, base + bytes) (collective).
  * bytes may be 0 (base ignored). */
@@ -94,6 +95,39 @@ int ompi_amd_fetch_and_op(ompi_amd_win_t *win, const void *origin, void *result,
 /* result = target; if target's bytes equal compare's, target = origin. */
 int ompi_amd_compare_and_swap(ompi_amd_win_t *win, const void *origin, const void *compare,
                               void *result, int type, int target, size_t disp, void *stream);
+
+/* General active target synchronisation (MPI_Win_post / _start /
+ * _complete / _wait / _test; osc.h:366-372, osc/sm's
+ * osc_sm_active_target.c:126-330).  ranks: the group's members as ranks of
+ * the window's communicator.  Stream-ordered like fence: post releases this
+ * rank's window and tells each origin; start waits (on the device) until
+ * every target of its group posted this epoch; complete releases the
+ * epoch's RMA and tells each target; wait waits (on the device) until every
+ * origin of the post group completed.  test is host-side and never blocks
+ * (*flag = 1 ends the exposure epoch).  The glue syncs the stream where MPI
+ * blocks (wait, complete). */
+int ompi_amd_win_post(ompi_amd_win_t *win, const int *ranks, int n, int assert_, void *stream);
+int ompi_amd_win_start(ompi_amd_win_t *win, const int *ranks, int n, int assert_, void *stream);
+int ompi_amd_win_complete(ompi_amd_win_t *win, void *stream);
+int ompi_amd_win_wait(ompi_amd_win_t *win, void *stream);
+int ompi_amd_win_test(ompi_amd_win_t *win, int *flag);
+
+/* Request-based RMA (MPI_Rput / _Rget / _Raccumulate / _Rget_accumulate,
+ * osc.h:384-393): the call as above plus a request that completes when its
+ * kernels have finished on `stream` (local and remote completion at once). */
+int ompi_amd_rput(ompi_amd_win_t *win, const void *origin, size_t bytes, int target, size_t disp,
+                  void *stream, ompi_amd_rma_request_t **request);
+int ompi_amd_rget(ompi_amd_win_t *win, void *origin, size_t bytes, int target, size_t disp,
+                  void *stream, ompi_amd_rma_request_t **request);
+int ompi_amd_raccumulate(ompi_amd_win_t *win, const void *origin, size_t count, int type,
+                         int target, size_t disp, int op, void *stream,
+                         ompi_amd_rma_request_t **request);
+int ompi_amd_rget_accumulate(ompi_amd_win_t *win, const void *origin, void *result, size_t count,
+                             int type, int target, size_t disp, int op, void *stream,
+                             ompi_amd_rma_request_t **request);
+int ompi_amd_rma_test(ompi_amd_rma_request_t *request, int *done);
+int ompi_amd_rma_wait(ompi_amd_rma_request_t *request);
+int ompi_amd_rma_free(ompi_amd_rma_request_t *request);
 
 #ifdef __cplusplus
 }

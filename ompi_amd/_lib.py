@@ -21,6 +21,7 @@ ERR_HIP = -3
 ERR_TIMEOUT = -4
 ERR_NOT_DEVICE = -5
 ERR_BOOTSTRAP = -6
+ERR_RMA_SYNC = -7
 ERR_TRUNCATE = -7
 
 _ERRNAMES = {
@@ -30,6 +31,7 @@ _ERRNAMES = {
     ERR_TIMEOUT: "timeout waiting for a peer",
     ERR_NOT_DEVICE: "buffer is not device memory",
     ERR_BOOTSTRAP: "bootstrap failure",
+    ERR_RMA_SYNC: "RMA synchronisation call out of order",
     ERR_TRUNCATE: "message truncated",
 }
 
@@ -242,6 +244,28 @@ PROTOTYPES = [
     ("ompi_amd_compare_and_swap", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_int, _C.c_int, _C.c_size_t,
       _C.c_void_p]),
+    ("ompi_amd_win_post", _C.c_int,
+     [_C.c_void_p, _C.POINTER(_C.c_int), _C.c_int, _C.c_int, _C.c_void_p]),
+    ("ompi_amd_win_start", _C.c_int,
+     [_C.c_void_p, _C.POINTER(_C.c_int), _C.c_int, _C.c_int, _C.c_void_p]),
+    ("ompi_amd_win_complete", _C.c_int, [_C.c_void_p, _C.c_void_p]),
+    ("ompi_amd_win_wait", _C.c_int, [_C.c_void_p, _C.c_void_p]),
+    ("ompi_amd_win_test", _C.c_int, [_C.c_void_p, _C.POINTER(_C.c_int)]),
+    ("ompi_amd_rput", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_size_t, _C.c_void_p,
+      _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_rget", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_size_t, _C.c_void_p,
+      _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_raccumulate", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_size_t, _C.c_int,
+      _C.c_void_p, _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_rget_accumulate", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_size_t,
+      _C.c_int, _C.c_void_p, _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_rma_test", _C.c_int, [_C.c_void_p, _C.POINTER(_C.c_int)]),
+    ("ompi_amd_rma_wait", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_rma_free", _C.c_int, [_C.c_void_p]),
 ]
 
 

@@ -57,16 +57,19 @@ __device__ __forceinline__ void st16(u32x4 *p, u32x4 v) {
 
 // dst[i] = f(x[i], y[i]).  2-buffer: x = dst = inout, y = in.
 // 3-buffer: x = in1, y = in2, dst = out.  x/dst may alias, so no restrict;
-// every lane loads all its vectors before storing any.
+// every lane loads all its vectors before storing any.  The 16-B vectors
+// start at element `head` (the operands share their offset within 16 B:
+// the head elements before the first boundary and the tail after the last
+// whole vector go element by element, in workgroup 0).
 template <typename T, int OP, bool THREE>
 __global__ __launch_bounds__(kOpThreads) void op_vec_kernel(const T *x, const T *y, T *dst,
-                                                            size_t nvec, size_t n) {
+                                                            size_t nvec, size_t n, int head) {
     using F = opfn<OP, THREE>;
     constexpr int E = 16 / sizeof(T);
     constexpr size_t chunk = (size_t)kOpThreads * kOpUnroll;
-    const u32x4 *xv = reinterpret_cast<const u32x4 *>(x);
-    const u32x4 *yv = reinterpret_cast<const u32x4 *>(y);
-    u32x4 *dv = reinterpret_cast<u32x4 *>(dst);
+    const u32x4 *xv = reinterpret_cast<const u32x4 *>(x + head);
+    const u32x4 *yv = reinterpret_cast<const u32x4 *>(y + head);
+    u32x4 *dv = reinterpret_cast<u32x4 *>(dst + head);
     const size_t stride = (size_t)gridDim.x * chunk;
 
     for (size_t base = (size_t)blockIdx.x * chunk + threadIdx.x; base < nvec; base += stride) {
@@ -91,21 +94,43 @@ __global__ __launch_bounds__(kOpThreads) void op_vec_kernel(const T *x, const T 
             }
         }
     }
-    // scalar tail: elements past the last whole 16-B vector
     if (blockIdx.x == 0) {
-        for (size_t i = nvec * E + threadIdx.x; i < n; i += kOpThreads)
+        if ((int)threadIdx.x < head) {  // head: before the first 16-B boundary
+            const size_t i = threadIdx.x;
+            store_elem<T>(dst + i, F::template f<T>(x[i], y[i]));
+        }
+        // tail: elements past the last whole 16-B vector
+        for (size_t i = (size_t)head + nvec * E + threadIdx.x; i < n; i += kOpThreads)
             store_elem<T>(dst + i, F::template f<T>(x[i], y[i]));
     }
 }
 
-// Unaligned operands: one element per lane, grid-stride.
+// Operands at different offsets within 16 B: elements, kOpUnroll*E per lane
+// per pass (coalesced across lanes, every load of a pass issued before its
+// stores, so as many bytes are in flight per lane as in op_vec_kernel).
 template <typename T, int OP, bool THREE>
 __global__ __launch_bounds__(kOpThreads) void op_scalar_kernel(const T *x, const T *y, T *dst,
                                                                size_t n) {
     using F = opfn<OP, THREE>;
-    const size_t stride = (size_t)gridDim.x * kOpThreads;
-    for (size_t i = (size_t)blockIdx.x * kOpThreads + threadIdx.x; i < n; i += stride)
-        store_elem<T>(dst + i, F::template f<T>(x[i], y[i]));
+    constexpr int K = kOpUnroll * (16 / sizeof(T) < 4 ? 16 / sizeof(T) : 4);
+    constexpr size_t chunk = (size_t)kOpThreads * K;
+    const size_t stride = (size_t)gridDim.x * chunk;
+    for (size_t base = (size_t)blockIdx.x * chunk + threadIdx.x; base < n; base += stride) {
+        T a[K], b[K];
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            const size_t i = base + (size_t)u * kOpThreads;
+            if (i < n) {
+                a[u] = x[i];
+                b[u] = y[i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            const size_t i = base + (size_t)u * kOpThreads;
+            if (i < n) store_elem<T>(dst + i, F::template f<T>(a[u], b[u]));
+        }
+    }
 }
 
 static int g_max_blocks = -1;
@@ -131,18 +156,24 @@ template <typename T, int OP, bool THREE>
 static hipError_t launch_typed(const void *x, const void *y, void *dst, size_t n,
                                hipStream_t s) {
     constexpr int E = 16 / sizeof(T);
-    const bool aligned = ((((uintptr_t)x) | ((uintptr_t)y) | ((uintptr_t)dst)) & 15) == 0;
+    const uintptr_t px = (uintptr_t)x & 15, py = (uintptr_t)y & 15, pd = (uintptr_t)dst & 15;
     const size_t max_blocks = (size_t)op_max_blocks();
-    if (aligned) {
-        const size_t nvec = n / E;
+    // same offset within 16 B (aligned, or e.g. all three displaced by the
+    // same element count): peel the head, vectors after it
+    if (px == py && px == pd && px % sizeof(T) == 0) {
+        size_t head = px ? (16 - px) / sizeof(T) : 0;
+        if (head > n) head = n;
+        const size_t nvec = (n - head) / E;
         const size_t chunk = (size_t)kOpThreads * kOpUnroll;
         size_t blocks = (nvec + chunk - 1) / chunk;
         if (blocks == 0) blocks = 1;
         if (blocks > max_blocks) blocks = max_blocks;
         hipLaunchKernelGGL((op_vec_kernel<T, OP, THREE>), dim3((unsigned)blocks), dim3(kOpThreads),
-                           0, s, (const T *)x, (const T *)y, (T *)dst, nvec, n);
+                           0, s, (const T *)x, (const T *)y, (T *)dst, nvec, n, (int)head);
     } else {
-        size_t blocks = (n + kOpThreads - 1) / kOpThreads;
+        constexpr size_t chunk = (size_t)kOpThreads * kOpUnroll * (E < 4 ? E : 4);
+        size_t blocks = (n + chunk - 1) / chunk;
+        if (blocks == 0) blocks = 1;
         if (blocks > max_blocks) blocks = max_blocks;
         hipLaunchKernelGGL((op_scalar_kernel<T, OP, THREE>), dim3((unsigned)blocks),
                            dim3(kOpThreads), 0, s, (const T *)x, (const T *)y, (T *)dst, n);

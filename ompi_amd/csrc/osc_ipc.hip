@@ -57,6 +57,20 @@ enum { CTL_ACC = 0, CTL_COUNTER = 16, CTL_WRITE = 32, CTL_READ = 48, CTL_BYTES =
 // lock that was not taken is never released on someone else's behalf and
 // no data moves without it.
 enum { CTL_TAKEN_ACC = 256, CTL_TAKEN_EPOCH = 512 };
+// General active target synchronisation (osc_sm_active_target.c:126-330):
+// word CTL_POST + 16 p of a rank's control page counts the exposure epochs
+// rank p opened toward it (MPI_Win_post; osc/sm's posts[] bit per rank, a
+// counter here so that repeated epochs need no clearing); CTL_COMPLETE
+// counts the access epochs origins closed toward it (MPI_Win_complete;
+// osc/sm's complete_count).  Each on its own 64-B line.
+enum { CTL_POST = 640, CTL_COMPLETE = 960 };
+constexpr int kPscwLane = 16;  // words between two CTL_POST counters
+static_assert(CTL_POST + kPscwLane * OMPI_AMD_MAX_RANKS <= CTL_COMPLETE, "pscw words overlap");
+
+// the peers' control pages, by value (a kernel argument)
+struct peer_ctl_set {
+    uint32_t *p[OMPI_AMD_MAX_RANKS];
+};
 
 __device__ __forceinline__ void osc_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
 __device__ __forceinline__ void osc_release() {
@@ -175,6 +189,48 @@ __global__ __launch_bounds__(64) void lock_kernel(uint32_t *ctl, int kind, int *
         st_sys(taken, 0u);
         break;
     }
+}
+
+// PSCW on the stream (one lane per group member):
+//   0 post      release this rank's window; +1 on CTL_POST[me] of each origin
+//   1 start     wait until each target's CTL_POST[target] here reached the
+//               epoch's count, then acquire
+//   2 complete  release (the epoch's RMA kernels precede on the stream); +1
+//               on CTL_COMPLETE of each target
+//   3 wait      wait until CTL_COMPLETE here reached the count, then acquire
+struct pscw_group {
+    int n;
+    int rank[kOscMaxRanks];
+    uint32_t want[kOscMaxRanks];  // start: per target; wait: want[0]
+};
+
+__global__ __launch_bounds__(64) void pscw_kernel(uint32_t *own, peer_ctl_set peers, pscw_group g,
+                                                  int kind, int me, int *err, uint64_t ticks) {
+    const int t = threadIdx.x;
+    if (kind == 0 || kind == 2) {
+        if (t == 0) osc_release();
+        __syncthreads();
+        if (t < g.n)
+            __hip_atomic_fetch_add(peers.p[g.rank[t]] + (kind == 0 ? CTL_POST + kPscwLane * me : CTL_COMPLETE),
+                                   1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
+    const int lanes = kind == 1 ? g.n : 1;
+    if (t < lanes) {
+        uint32_t *w = kind == 1 ? own + CTL_POST + kPscwLane * g.rank[t] : own + CTL_COMPLETE;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while ((int32_t)(ld_sys(w) - g.want[t]) < 0) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+                __hip_atomic_store(err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    if (t == 0) osc_acquire();
 }
 
 // target[i] = f(target[i], origin[i]) — the 2-buffer rule with out = target,
@@ -347,6 +403,13 @@ struct win_blob {
 
 using namespace ompi_amd;
 
+// A request-based RMA call (MPI_Rput / _Rget / _Raccumulate /
+// _Rget_accumulate): an event recorded after the call's kernels.
+struct ompi_amd_rma_request {
+    hipEvent_t ev = nullptr;
+    ompi_amd_win_t *w = nullptr;
+};
+
 struct ompi_amd_win {
     ompi_amd_comm_t *c = nullptr;
     int rank = 0, size = 0;
@@ -362,6 +425,12 @@ struct ompi_amd_win {
     ipc_ref *ctl_ref[kOscMaxRanks] = {};  // peers' control pages (IPC registry references)
     std::vector<hipStream_t> streams;  // every stream an epoch or RMA call ran on (win_free waits)
     int held[kOscMaxRanks] = {};  // outstanding passive lock per target (0 none)
+    // general active target synchronisation (host side of the counters)
+    bool posted = false, started = false;
+    uint32_t post_seen[kOscMaxRanks] = {};  // exposure epochs of rank t this rank started toward
+    uint32_t complete_want = 0;             // access epochs origins must have closed here
+    std::vector<int> start_group;
+    hipStream_t query = nullptr;  // MPI_Win_test's counter reads
 };
 
 namespace ompi_amd {
@@ -581,7 +650,10 @@ int ompi_amd_win_allocate(ompi_amd_comm_t *c, size_t bytes, int disp_unit, void 
     int rc = record_hip(hipSetDevice(comm_device(c)), "hipSetDevice");
     void *m = nullptr;
     if (rc == OMPI_AMD_SUCCESS && bytes) {
-        rc = record_hip(hipMalloc(&m, bytes), "hipMalloc (window)");
+        // library-owned: exported once, padded so that its handle is not a
+        // freed window's again (peers may still cache that one; §4.6)
+        ipc_desc d;
+        rc = comm_alloc_exportable(bytes, false, &m, &d);
         if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipMemset(m, 0, bytes), "hipMemset (window)");
         if (rc == OMPI_AMD_SUCCESS)
             rc = record_hip(hipStreamSynchronize(nullptr), "hipStreamSynchronize (window memset)");
@@ -621,6 +693,7 @@ int ompi_amd_win_free(ompi_amd_win_t *w) {
     }
     const int brc2 = comm_allgather(c, nullptr, nullptr, 0);  // mappings closed before frees
     if (rc == OMPI_AMD_SUCCESS) rc = brc2;
+    if (w->query) hip_ignore(hipStreamDestroy(w->query));
     if (w->ctl) hip_ignore(hipFree(w->ctl));
     if (w->owns_base && w->base) hip_ignore(hipFree(w->base));
     if (rc == OMPI_AMD_SUCCESS) rc = comm_sticky(c);
@@ -746,6 +819,195 @@ int ompi_amd_compare_and_swap(ompi_amd_win_t *w, const void *origin, const void 
     const int rc = record_hip(hipGetLastError(), "osc compare_and_swap launch");
     const int urc = launch_lock(w, target, 1, s);
     return rc != OMPI_AMD_SUCCESS ? rc : urc;
+}
+
+// ---- general active target synchronisation (osc_sm_active_target.c) ----
+
+static int pscw_launch(ompi_amd_win_t *w, int kind, const pscw_group &g, hipStream_t s) {
+    peer_ctl_set peers{};
+    for (int p = 0; p < w->size; ++p) peers.p[p] = w->peer_ctl[p];
+    hipLaunchKernelGGL(pscw_kernel, dim3(1), dim3(64), 0, s, w->ctl, peers, g, kind, w->rank,
+                       comm_err_dev(w->c), ticks_of(w));
+    return record_hip(hipGetLastError(), "osc pscw launch");
+}
+
+static int pscw_group_of(ompi_amd_win_t *w, const int *ranks, int n, pscw_group *g) {
+    if (n < 0 || n > w->size || (n && !ranks)) return OMPI_AMD_ERR_BAD_PARAM;
+    *g = pscw_group{};
+    g->n = n;
+    for (int i = 0; i < n; ++i) {
+        if (ranks[i] < 0 || ranks[i] >= w->size) return OMPI_AMD_ERR_BAD_PARAM;
+        g->rank[i] = ranks[i];
+    }
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_win_post(ompi_amd_win_t *w, const int *ranks, int n, int assert_, void *stream) {
+    if (!w) return OMPI_AMD_ERR_BAD_PARAM;
+    if (w->posted) {  // osc_sm_active_target.c:230-233
+        record_msg("osc: MPI_Win_post while an exposure epoch is open");
+        return OMPI_AMD_ERR_RMA_SYNC;
+    }
+    pscw_group g;
+    OSC_TRY(pscw_group_of(w, ranks, n, &g));
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    // MPI_MODE_NOCHECK: the origins start without waiting for this post
+    // (osc_sm_active_target.c:239); the window is still released
+    if (assert_ & OMPI_AMD_MODE_NOCHECK) g.n = 0;
+    OSC_TRY(pscw_launch(w, 0, g, win_stream(w, stream)));
+    w->posted = true;
+    w->complete_want += (uint32_t)n;  // every origin of the group completes once
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_win_start(ompi_amd_win_t *w, const int *ranks, int n, int assert_, void *stream) {
+    if (!w) return OMPI_AMD_ERR_BAD_PARAM;
+    if (w->started) {  // osc_sm_active_target.c:137-140
+        record_msg("osc: MPI_Win_start while an access epoch is open");
+        return OMPI_AMD_ERR_RMA_SYNC;
+    }
+    pscw_group g;
+    OSC_TRY(pscw_group_of(w, ranks, n, &g));
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    // MPI_MODE_NOCHECK: the targets' posts are not waited for (nor counted:
+    // they posted with NOCHECK too, osc_sm_active_target.c:142)
+    if (!(assert_ & OMPI_AMD_MODE_NOCHECK)) {
+        for (int i = 0; i < n; ++i) g.want[i] = w->post_seen[ranks[i]] + 1;
+        OSC_TRY(pscw_launch(w, 1, g, win_stream(w, stream)));
+        for (int i = 0; i < n; ++i) ++w->post_seen[ranks[i]];
+    }
+    w->started = true;
+    w->start_group.assign(ranks, ranks + n);
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_win_complete(ompi_amd_win_t *w, void *stream) {
+    if (!w) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!w->started) {
+        record_msg("osc: MPI_Win_complete without MPI_Win_start");
+        return OMPI_AMD_ERR_RMA_SYNC;
+    }
+    pscw_group g;
+    OSC_TRY(pscw_group_of(w, w->start_group.data(), (int)w->start_group.size(), &g));
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    OSC_TRY(pscw_launch(w, 2, g, win_stream(w, stream)));
+    w->started = false;
+    w->start_group.clear();
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_win_wait(ompi_amd_win_t *w, void *stream) {
+    if (!w) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!w->posted) {
+        record_msg("osc: MPI_Win_wait without MPI_Win_post");
+        return OMPI_AMD_ERR_RMA_SYNC;
+    }
+    pscw_group g{};
+    g.want[0] = w->complete_want;
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    OSC_TRY(pscw_launch(w, 3, g, win_stream(w, stream)));
+    w->posted = false;
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_win_test(ompi_amd_win_t *w, int *flag) {
+    if (!w || !flag) return OMPI_AMD_ERR_BAD_PARAM;
+    *flag = 0;
+    if (!w->posted) {
+        record_msg("osc: MPI_Win_test without MPI_Win_post");
+        return OMPI_AMD_ERR_RMA_SYNC;
+    }
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    // read the counter on a stream of its own: this rank's streams may hold
+    // a start kernel that waits for a peer (and the legacy stream would
+    // order the read behind it)
+    if (!w->query) OSC_TRY(record_hip(hipStreamCreateWithFlags(&w->query, hipStreamNonBlocking),
+                                      "osc test stream"));
+    uint32_t seen = 0;
+    OSC_TRY(record_hip(hipMemcpyAsync(&seen, w->ctl + CTL_COMPLETE, sizeof(seen),
+                                      hipMemcpyDeviceToHost, w->query), "osc test (complete counter)"));
+    OSC_TRY(record_hip(hipStreamSynchronize(w->query), "osc test (complete counter)"));
+    if ((int32_t)(seen - w->complete_want) >= 0) {
+        // the exposure epoch ends (osc_sm_active_target.c:320-330); the wait
+        // kernel (already satisfied) acquires what the origins released
+        pscw_group g{};
+        g.want[0] = w->complete_want;
+        OSC_TRY(pscw_launch(w, 3, g, win_stream(w, nullptr)));
+        *flag = 1;
+        w->posted = false;
+    }
+    return comm_sticky(w->c);
+}
+
+// ---- request-based RMA (osc.h:384-393) ----
+
+static int rma_request(ompi_amd_win_t *w, void *stream, int rc, ompi_amd_rma_request_t **out) {
+    *out = nullptr;
+    if (rc != OMPI_AMD_SUCCESS) return rc;
+    auto *r = new (std::nothrow) ompi_amd_rma_request;
+    if (!r) return OMPI_AMD_ERR_BAD_PARAM;
+    r->w = w;
+    rc = record_hip(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming), "rma request event");
+    if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipEventRecord(r->ev, win_stream(w, stream)), "rma request record");
+    if (rc != OMPI_AMD_SUCCESS) {
+        if (r->ev) hip_ignore(hipEventDestroy(r->ev));
+        delete r;
+        return rc;
+    }
+    *out = r;
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_rput(ompi_amd_win_t *w, const void *origin, size_t bytes, int target, size_t disp,
+                  void *stream, ompi_amd_rma_request_t **req) {
+    if (!req) return OMPI_AMD_ERR_BAD_PARAM;
+    return rma_request(w, stream, ompi_amd_put(w, origin, bytes, target, disp, stream), req);
+}
+
+int ompi_amd_rget(ompi_amd_win_t *w, void *origin, size_t bytes, int target, size_t disp,
+                  void *stream, ompi_amd_rma_request_t **req) {
+    if (!req) return OMPI_AMD_ERR_BAD_PARAM;
+    return rma_request(w, stream, ompi_amd_get(w, origin, bytes, target, disp, stream), req);
+}
+
+int ompi_amd_raccumulate(ompi_amd_win_t *w, const void *origin, size_t count, int type, int target,
+                         size_t disp, int op, void *stream, ompi_amd_rma_request_t **req) {
+    if (!req) return OMPI_AMD_ERR_BAD_PARAM;
+    return rma_request(w, stream,
+                       ompi_amd_accumulate(w, origin, count, type, target, disp, op, stream), req);
+}
+
+int ompi_amd_rget_accumulate(ompi_amd_win_t *w, const void *origin, void *result, size_t count,
+                             int type, int target, size_t disp, int op, void *stream,
+                             ompi_amd_rma_request_t **req) {
+    if (!req) return OMPI_AMD_ERR_BAD_PARAM;
+    return rma_request(w, stream,
+                       ompi_amd_get_accumulate(w, origin, result, count, type, target, disp, op,
+                                               stream), req);
+}
+
+int ompi_amd_rma_test(ompi_amd_rma_request_t *r, int *done) {
+    if (!r || !done) return OMPI_AMD_ERR_BAD_PARAM;
+    const hipError_t e = hipEventQuery(r->ev);
+    *done = 0;
+    if (e == hipErrorNotReady) return OMPI_AMD_SUCCESS;
+    if (e != hipSuccess) return record_hip(e, "rma request test");
+    *done = 1;
+    return comm_sticky(r->w->c);
+}
+
+int ompi_amd_rma_wait(ompi_amd_rma_request_t *r) {
+    if (!r) return OMPI_AMD_ERR_BAD_PARAM;
+    OSC_TRY(record_hip(hipEventSynchronize(r->ev), "rma request wait"));
+    return comm_sticky(r->w->c);
+}
+
+int ompi_amd_rma_free(ompi_amd_rma_request_t *r) {
+    if (!r) return OMPI_AMD_SUCCESS;
+    const int rc = ompi_amd_rma_wait(r);
+    hip_ignore(hipEventDestroy(r->ev));
+    delete r;
+    return rc;
 }
 
 }  // extern "C"

@@ -15,6 +15,7 @@
 
 #include "mpi.h"
 #include "ompi/mca/osc/osc.h"
+#include "ompi/request/request.h"
 
 #include "ompi_amd_coll.h"
 #include "ompi_amd_osc.h"
@@ -28,6 +29,15 @@ typedef struct ompi_osc_rocm_module_t {
     struct ompi_communicator_t *comm;
     int size;
 } ompi_osc_rocm_module_t;
+
+/* the MPI request of MPI_Rput / _Rget / _Raccumulate / _Rget_accumulate
+ * over the library's (completed from opal_progress) */
+typedef struct ompi_osc_rocm_request_t {
+    ompi_request_t super;
+    ompi_amd_rma_request_t *rma;
+    struct ompi_osc_rocm_request_t *next_active;
+} ompi_osc_rocm_request_t;
+OBJ_CLASS_DECLARATION(ompi_osc_rocm_request_t);
 
 typedef struct ompi_osc_rocm_component_t {
     ompi_osc_base_component_t super;

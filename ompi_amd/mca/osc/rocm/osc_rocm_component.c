@@ -4,7 +4,12 @@
  * Mirrors osc/sm's module functions (ompi/mca/osc/sm/osc_sm_comm.c,
  * osc_sm_active_target.c, osc_sm_passive_target.c) one call each; the
  * data moves by kernels on the origin's GPU over the peers' IPC mappings
- * (include/ompi_amd_osc.h).  Predefined datatypes with equal origin and
+ * (include/ompi_amd_osc.h).  General active target synchronisation
+ * (post / start / complete / wait / test) runs on the device too: start and
+ * wait are kernels that wait for the peers' counters, so MPI's blocking
+ * calls return once the stream got there (complete and wait synchronise).
+ * Request-based RMA completes its request from the opal_progress callback
+ * once the call's kernels have run.  Predefined datatypes with equal origin and
  * target signatures; everything else returns OMPI_ERR_NOT_SUPPORTED, as
  * osc/sm rejects what it cannot do.  Blocking MPI semantics come from the
  * stream synchronisation in fence / unlock / flush (ompi_amd_comm_sync,
@@ -21,11 +26,15 @@
 #include "ompi/constants.h"
 #include "ompi/communicator/communicator.h"
 #include "ompi/datatype/ompi_datatype.h"
+#include "ompi/group/group.h"
 #include "ompi/mca/osc/osc.h"
 #include "ompi/op/op.h"
+#include "ompi/request/request.h"
 #include "ompi/runtime/ompi_rte.h"
 #include "ompi/win/win.h"
 #include "opal/mca/base/mca_base_var.h"
+#include "opal/mca/threads/mutex.h"
+#include "opal/runtime/opal_progress.h"
 #include "opal/util/info.h"
 
 #include "ompi_amd.h"
@@ -89,6 +98,7 @@ static int to_ompi_err(int rc)
     case OMPI_AMD_ERR_UNSUPPORTED: return OMPI_ERR_NOT_SUPPORTED;
     case OMPI_AMD_ERR_BAD_PARAM: return OMPI_ERR_BAD_PARAM;
     case OMPI_AMD_ERR_TIMEOUT: return OMPI_ERR_TIMEOUT;
+    case OMPI_AMD_ERR_RMA_SYNC: return OMPI_ERR_RMA_SYNC;
     default: return OMPI_ERROR;
     }
 }
@@ -250,30 +260,229 @@ static int rocm_free(struct ompi_win_t *win)
     return to_ompi_err(rc);
 }
 
-/* PSCW, dynamic / shared windows and request-based RMA: not provided (the
- * framework reports MPI_ERR_UNSUPPORTED_OPERATION) */
+/* ------------------------------------------------- general active target */
+
+/* the members of `group` as ranks of the window's communicator
+ * (osc_sm_active_target.c:63-90); NULL when one is not a member */
+static int *group_ranks(ompi_osc_rocm_module_t *m, ompi_group_t *group, int *n)
+{
+    int i, *r1, *r2;
+    *n = ompi_group_size(group);
+    r1 = malloc(sizeof(int) * (size_t) (*n + 1));
+    r2 = malloc(sizeof(int) * (size_t) (*n + 1));
+    if (NULL == r1 || NULL == r2) goto fail;
+    for (i = 0; i < *n; ++i) r1[i] = i;
+    if (OMPI_SUCCESS != ompi_group_translate_ranks(group, *n, r1, m->comm->c_local_group, r2))
+        goto fail;
+    for (i = 0; i < *n; ++i)
+        if (r2[i] < 0 || r2[i] >= m->size) goto fail;
+    free(r1);
+    return r2;
+fail:
+    free(r1);
+    free(r2);
+    return NULL;
+}
+
+static int rocm_start(struct ompi_group_t *group, int assert_, struct ompi_win_t *win)
+{
+    ompi_osc_rocm_module_t *m = mod(win);
+    int n, rc, *ranks = group_ranks(m, group, &n);
+    if (NULL == ranks) return OMPI_ERR_OUT_OF_RESOURCE;
+    rc = ompi_amd_win_start(m->dev_win, ranks, n, assert_, NULL);
+    free(ranks);
+    return to_ompi_err(rc);
+}
+
+static int rocm_post(struct ompi_group_t *group, int assert_, struct ompi_win_t *win)
+{
+    ompi_osc_rocm_module_t *m = mod(win);
+    int n, rc, *ranks = group_ranks(m, group, &n);
+    if (NULL == ranks) return OMPI_ERR_OUT_OF_RESOURCE;
+    rc = ompi_amd_win_post(m->dev_win, ranks, n, assert_, NULL);
+    free(ranks);
+    return to_ompi_err(rc);
+}
+
+/* MPI_Win_complete returns when the access epoch's RMA is done everywhere
+ * it goes (osc_sm_active_target.c:180-213): the stream is synchronised */
+static int rocm_complete(struct ompi_win_t *win)
+{
+    ompi_osc_rocm_module_t *m = mod(win);
+    return complete(m, ompi_amd_win_complete(m->dev_win, NULL));
+}
+
+static int rocm_wait(struct ompi_win_t *win)
+{
+    ompi_osc_rocm_module_t *m = mod(win);
+    return complete(m, ompi_amd_win_wait(m->dev_win, NULL));
+}
+
+static int rocm_test(struct ompi_win_t *win, int *flag)
+{
+    ompi_osc_rocm_module_t *m = mod(win);
+    const int rc = ompi_amd_win_test(m->dev_win, flag);
+    if (OMPI_AMD_SUCCESS != rc || !*flag) return to_ompi_err(rc);
+    return complete(m, rc);  /* the acquire the library queued has run */
+}
+
+/* ------------------------------------------------------ request-based RMA */
+
+static opal_mutex_t rma_active_lock = OPAL_MUTEX_STATIC_INIT;
+static ompi_osc_rocm_request_t *rma_active;
+static int rma_progress_registered;
+
+/* opal_progress callback: complete the requests whose kernels finished */
+static int rma_progress(void)
+{
+    ompi_osc_rocm_request_t **pp, *done = NULL;
+    int completed = 0;
+    if (NULL == rma_active) return 0;
+    OPAL_THREAD_LOCK(&rma_active_lock);
+    pp = &rma_active;
+    while (NULL != *pp) {
+        ompi_osc_rocm_request_t *r = *pp;
+        int fin = 0;
+        const int rc = ompi_amd_rma_test(r->rma, &fin);
+        if (OMPI_AMD_SUCCESS != rc || fin) {
+            r->super.req_status.MPI_ERROR = to_ompi_err(rc);
+            *pp = r->next_active;
+            r->next_active = done;
+            done = r;
+        } else {
+            pp = &r->next_active;
+        }
+    }
+    OPAL_THREAD_UNLOCK(&rma_active_lock);
+    while (NULL != done) {
+        ompi_osc_rocm_request_t *r = done;
+        done = r->next_active;
+        r->next_active = NULL;
+        ompi_request_complete(&r->super, true);
+        ++completed;
+    }
+    return completed;
+}
+
+static int rma_request_free(ompi_request_t **rptr)
+{
+    ompi_osc_rocm_request_t *r = (ompi_osc_rocm_request_t *) *rptr, **pp;
+    int rc;
+    OPAL_THREAD_LOCK(&rma_active_lock);
+    for (pp = &rma_active; NULL != *pp; pp = &(*pp)->next_active) {
+        if (*pp == r) {
+            *pp = r->next_active;
+            break;
+        }
+    }
+    OPAL_THREAD_UNLOCK(&rma_active_lock);
+    rc = ompi_amd_rma_free(r->rma);  /* waits for the kernels first */
+    OMPI_REQUEST_FINI(&r->super);
+    OBJ_RELEASE(r);
+    *rptr = MPI_REQUEST_NULL;
+    return to_ompi_err(rc);
+}
+
+static void rma_request_construct(ompi_osc_rocm_request_t *r)
+{
+    r->super.req_type = OMPI_REQUEST_WIN;
+    r->super.req_status._cancelled = 0;
+    r->super.req_free = rma_request_free;
+    r->super.req_cancel = NULL;
+    r->rma = NULL;
+    r->next_active = NULL;
+}
+
+OBJ_CLASS_INSTANCE(ompi_osc_rocm_request_t, ompi_request_t, rma_request_construct, NULL);
+
+/* an MPI request over the library request of a call that returned rc */
+static int rma_wrap(int rc, ompi_amd_rma_request_t *rma, struct ompi_win_t *win,
+                    ompi_request_t **request)
+{
+    ompi_osc_rocm_request_t *r;
+    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
+    r = OBJ_NEW(ompi_osc_rocm_request_t);
+    if (NULL == r) {
+        (void) ompi_amd_rma_free(rma);
+        return OMPI_ERR_OUT_OF_RESOURCE;
+    }
+    OMPI_REQUEST_INIT(&r->super, false);
+    r->super.req_state = OMPI_REQUEST_ACTIVE;
+    r->super.req_status.MPI_ERROR = OMPI_SUCCESS;
+    r->rma = rma;
+    OPAL_THREAD_LOCK(&rma_active_lock);
+    r->next_active = rma_active;
+    rma_active = r;
+    if (!rma_progress_registered) {
+        rma_progress_registered = 1;
+        (void) opal_progress_register(rma_progress);
+    }
+    OPAL_THREAD_UNLOCK(&rma_active_lock);
+    *request = &r->super;
+    return OMPI_SUCCESS;
+}
+
+/* a zero-count call completes at once (osc_sm_comm.c:54-57 hands back
+ * ompi_request_empty); here a library request over no kernels does */
+static int rocm_rput(const void *origin, int ocount, struct ompi_datatype_t *odt, int target,
+                     ptrdiff_t disp, int tcount, struct ompi_datatype_t *tdt,
+                     struct ompi_win_t *win, ompi_request_t **request)
+{
+    ompi_amd_rma_request_t *rma = NULL;
+    const size_t bytes = span(odt, ocount);
+    if (0 != ocount && (0 == bytes || bytes != span(tdt, tcount) || disp < 0))
+        return OMPI_ERR_NOT_SUPPORTED;
+    return rma_wrap(ompi_amd_rput(mod(win)->dev_win, origin, bytes, target, (size_t) disp, NULL,
+                                  &rma), rma, win, request);
+}
+
+static int rocm_rget(void *origin, int ocount, struct ompi_datatype_t *odt, int target,
+                     ptrdiff_t disp, int tcount, struct ompi_datatype_t *tdt,
+                     struct ompi_win_t *win, ompi_request_t **request)
+{
+    ompi_amd_rma_request_t *rma = NULL;
+    const size_t bytes = span(odt, ocount);
+    if (0 != ocount && (0 == bytes || bytes != span(tdt, tcount) || disp < 0))
+        return OMPI_ERR_NOT_SUPPORTED;
+    return rma_wrap(ompi_amd_rget(mod(win)->dev_win, origin, bytes, target, (size_t) disp, NULL,
+                                  &rma), rma, win, request);
+}
+
+static int rocm_raccumulate(const void *origin, int ocount, struct ompi_datatype_t *odt,
+                            int target, ptrdiff_t disp, int tcount, struct ompi_datatype_t *tdt,
+                            struct ompi_op_t *op, struct ompi_win_t *win, ompi_request_t **request)
+{
+    ompi_amd_rma_request_t *rma = NULL;
+    if (0 != ocount && (!acc_ok(odt, ocount, tdt, tcount, op) || disp < 0))
+        return OMPI_ERR_NOT_SUPPORTED;
+    return rma_wrap(ompi_amd_raccumulate(mod(win)->dev_win, origin, (size_t) ocount,
+                                         0 != ocount ? type_code(tdt) : 0, target, (size_t) disp,
+                                         op->o_f_to_c_index, NULL, &rma), rma, win, request);
+}
+
+static int rocm_rget_accumulate(const void *origin, int ocount, struct ompi_datatype_t *odt,
+                                void *result, int rcount, struct ompi_datatype_t *rdt, int target,
+                                ptrdiff_t disp, int tcount, struct ompi_datatype_t *tdt,
+                                struct ompi_op_t *op, struct ompi_win_t *win,
+                                ompi_request_t **request)
+{
+    ompi_amd_rma_request_t *rma = NULL;
+    const int no_op = ompi_op_is_intrinsic(op) && OMPI_AMD_OP_NO_OP == op->o_f_to_c_index;
+    if (0 != tcount && (rdt->id != tdt->id || rcount != tcount || disp < 0 ||
+                        !acc_ok(no_op ? tdt : odt, no_op ? tcount : ocount, tdt, tcount, op)))
+        return OMPI_ERR_NOT_SUPPORTED;
+    return rma_wrap(ompi_amd_rget_accumulate(mod(win)->dev_win, no_op ? NULL : origin, result,
+                                             (size_t) tcount, 0 != tcount ? type_code(tdt) : 0,
+                                             target, (size_t) disp, op->o_f_to_c_index, NULL,
+                                             &rma), rma, win, request);
+}
+
+/* dynamic and shared windows: not provided (selection leaves those flavors
+ * to osc/sm and osc/rdma, rocm_query) */
 static int ns_shared_query(struct ompi_win_t *w, int r, size_t *s, int *d, void *b)
 { return OMPI_ERR_NOT_SUPPORTED; }
 static int ns_attach(struct ompi_win_t *w, void *b, size_t s) { return OMPI_ERR_NOT_SUPPORTED; }
 static int ns_detach(struct ompi_win_t *w, const void *b) { return OMPI_ERR_NOT_SUPPORTED; }
-static int ns_group(struct ompi_group_t *g, int a, struct ompi_win_t *w) { return OMPI_ERR_NOT_SUPPORTED; }
-static int ns_win(struct ompi_win_t *w) { return OMPI_ERR_NOT_SUPPORTED; }
-static int ns_test(struct ompi_win_t *w, int *f) { return OMPI_ERR_NOT_SUPPORTED; }
-static int ns_rput(const void *o, int oc, struct ompi_datatype_t *od, int t, ptrdiff_t d, int tc,
-                   struct ompi_datatype_t *td, struct ompi_win_t *w, ompi_request_t **r)
-{ return OMPI_ERR_NOT_SUPPORTED; }
-static int ns_rget(void *o, int oc, struct ompi_datatype_t *od, int t, ptrdiff_t d, int tc,
-                   struct ompi_datatype_t *td, struct ompi_win_t *w, ompi_request_t **r)
-{ return OMPI_ERR_NOT_SUPPORTED; }
-static int ns_racc(const void *o, int oc, struct ompi_datatype_t *od, int t, ptrdiff_t d, int tc,
-                   struct ompi_datatype_t *td, struct ompi_op_t *op, struct ompi_win_t *w,
-                   ompi_request_t **r)
-{ return OMPI_ERR_NOT_SUPPORTED; }
-static int ns_rgacc(const void *o, int oc, struct ompi_datatype_t *od, void *res, int rc,
-                    struct ompi_datatype_t *rd, int t, ptrdiff_t d, int tc,
-                    struct ompi_datatype_t *td, struct ompi_op_t *op, struct ompi_win_t *w,
-                    ompi_request_t **r)
-{ return OMPI_ERR_NOT_SUPPORTED; }
 
 static const ompi_osc_base_module_t rocm_module_template = {
     .osc_win_shared_query = ns_shared_query,
@@ -286,16 +495,16 @@ static const ompi_osc_base_module_t rocm_module_template = {
     .osc_compare_and_swap = rocm_compare_and_swap,
     .osc_fetch_and_op = rocm_fetch_and_op,
     .osc_get_accumulate = rocm_get_accumulate,
-    .osc_rput = ns_rput,
-    .osc_rget = ns_rget,
-    .osc_raccumulate = ns_racc,
-    .osc_rget_accumulate = ns_rgacc,
+    .osc_rput = rocm_rput,
+    .osc_rget = rocm_rget,
+    .osc_raccumulate = rocm_raccumulate,
+    .osc_rget_accumulate = rocm_rget_accumulate,
     .osc_fence = rocm_fence,
-    .osc_start = ns_group,
-    .osc_complete = ns_win,
-    .osc_post = ns_group,
-    .osc_wait = ns_win,
-    .osc_test = ns_test,
+    .osc_start = rocm_start,
+    .osc_complete = rocm_complete,
+    .osc_post = rocm_post,
+    .osc_wait = rocm_wait,
+    .osc_test = rocm_test,
     .osc_lock = rocm_lock,
     .osc_unlock = rocm_unlock,
     .osc_lock_all = rocm_lock_all,

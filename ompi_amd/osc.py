@@ -10,6 +10,10 @@ osc_sm_active_target.c, osc_sm_passive_target.c):
     compare_and_swap               osc_sm_comm.c:363-400
     fetch_and_op                   osc_sm_comm.c:403-441
     fence                          osc_sm_active_target.c:95-115
+    post / start / complete / wait / test
+                                   osc_sm_active_target.c:126-335
+    rput / rget / raccumulate / rget_accumulate
+                                   osc_sm_comm.c:23-206
     lock / unlock / lock_all / unlock_all / flush
                                    osc_sm_passive_target.c:113-270
 
@@ -29,6 +33,32 @@ from .op import Datatype, Op
 LOCK_EXCLUSIVE = 1   # MPI_LOCK_EXCLUSIVE (mpi.h.in:548)
 LOCK_SHARED = 2      # MPI_LOCK_SHARED (mpi.h.in:549)
 MODE_NOCHECK = 1     # MPI_MODE_NOCHECK (mpi.h.in:542)
+
+
+class RmaRequest:
+    """The request of MPI_Rput / _Rget / _Raccumulate / _Rget_accumulate:
+    complete when the call's kernels have finished."""
+
+    def __init__(self, lib, handle):
+        self._lib, self._h = lib, handle
+
+    def test(self) -> bool:
+        done = ctypes.c_int(0)
+        _lib.check(self._lib.ompi_amd_rma_test(self._h, ctypes.byref(done)), "rma_test")
+        return bool(done.value)
+
+    def wait(self) -> None:
+        _lib.check(self._lib.ompi_amd_rma_wait(self._h), "rma_wait")
+
+    def free(self) -> None:
+        if self._h:
+            h, self._h = self._h, None
+            _lib.check(self._lib.ompi_amd_rma_free(h), "rma_free")
+
+
+def _ranks(ranks):
+    ranks = list(ranks)
+    return (ctypes.c_int * max(1, len(ranks)))(*ranks), len(ranks)
 
 
 class Window:
@@ -92,6 +122,32 @@ class Window:
     def flush(self, target: int, stream=None) -> None:
         _lib.check(self._lib.ompi_amd_win_flush(self._h, target, _stream(stream)), "win_flush")
 
+    def post(self, ranks, assert_: int = 0, stream=None) -> None:
+        """MPI_Win_post: open an exposure epoch to the origins `ranks`."""
+        arr, n = _ranks(ranks)
+        _lib.check(self._lib.ompi_amd_win_post(self._h, arr, n, assert_, _stream(stream)),
+                   "win_post")
+
+    def start(self, ranks, assert_: int = 0, stream=None) -> None:
+        """MPI_Win_start: open an access epoch to the targets `ranks`
+        (the stream waits until each of them posted)."""
+        arr, n = _ranks(ranks)
+        _lib.check(self._lib.ompi_amd_win_start(self._h, arr, n, assert_, _stream(stream)),
+                   "win_start")
+
+    def complete(self, stream=None, blocking: bool = False) -> None:
+        self._done(self._lib.ompi_amd_win_complete(self._h, _stream(stream)), "win_complete",
+                   blocking, stream)
+
+    def wait(self, stream=None, blocking: bool = False) -> None:
+        self._done(self._lib.ompi_amd_win_wait(self._h, _stream(stream)), "win_wait",
+                   blocking, stream)
+
+    def test(self) -> bool:
+        flag = ctypes.c_int(0)
+        _lib.check(self._lib.ompi_amd_win_test(self._h, ctypes.byref(flag)), "win_test")
+        return bool(flag.value)
+
     # -- communication -------------------------------------------------------
     def put(self, origin, target: int, disp: int, nbytes: int | None = None, stream=None) -> None:
         n = origin.numel() * origin.element_size() if nbytes is None else nbytes
@@ -129,3 +185,33 @@ class Window:
         _lib.check(self._lib.ompi_amd_compare_and_swap(self._h, _ptr(origin), _ptr(compare),
                                                        _ptr(result), datatype.code, target, disp,
                                                        _stream(stream)), "compare_and_swap")
+
+    # -- request-based communication ------------------------------------------
+    def _req(self, fn, what, *args) -> RmaRequest:
+        h = ctypes.c_void_p()
+        _lib.check(fn(self._h, *args, ctypes.byref(h)), what)
+        return RmaRequest(self._lib, h)
+
+    def rput(self, origin, target: int, disp: int, nbytes: int | None = None,
+             stream=None) -> RmaRequest:
+        n = origin.numel() * origin.element_size() if nbytes is None else nbytes
+        return self._req(self._lib.ompi_amd_rput, "rput", _ptr(origin), n, target, disp,
+                         _stream(stream))
+
+    def rget(self, origin, target: int, disp: int, nbytes: int | None = None,
+             stream=None) -> RmaRequest:
+        n = origin.numel() * origin.element_size() if nbytes is None else nbytes
+        return self._req(self._lib.ompi_amd_rget, "rget", _ptr(origin), n, target, disp,
+                         _stream(stream))
+
+    def raccumulate(self, origin, count: int, datatype: Datatype, target: int, disp: int,
+                    op: Op, stream=None) -> RmaRequest:
+        return self._req(self._lib.ompi_amd_raccumulate, f"raccumulate({op.name})", _ptr(origin),
+                         count, datatype.code, target, disp, op.index, _stream(stream))
+
+    def rget_accumulate(self, origin, result, count: int, datatype: Datatype, target: int,
+                        disp: int, op: Op, stream=None) -> RmaRequest:
+        optr = _ptr(origin) if origin is not None else None
+        return self._req(self._lib.ompi_amd_rget_accumulate, f"rget_accumulate({op.name})", optr,
+                         _ptr(result), count, datatype.code, target, disp, op.index,
+                         _stream(stream))

@@ -9,6 +9,6 @@ OUT=${1:-$H/osc_harness}
 gcc -std=gnu11 -O1 -Wall -Wextra -Wno-unused-parameter -Wno-missing-field-initializers \
     -I"$H/osc_include" -I"$H/coll_include" -I"$H/include" -I"$R/include" \
     -I"$R/ompi_amd/mca/osc/rocm" -I/opt/rocm/include \
-    "$R/ompi_amd/mca/osc/rocm/osc_rocm_component.c" "$H/osc_harness.c" "$H/dev_helpers.c" \
+    "$R/ompi_amd/mca/osc/rocm/osc_rocm_component.c" "$H/osc_harness.c" "$H/dev_helpers.c" "$H/progress_stub.c" \
     -L"$R/ompi_amd" -lompi_amd -L"$R/oracle" -loracle -L/opt/rocm/lib -lamdhip64 \
     -Wl,-rpath,"$R/ompi_amd" -Wl,-rpath,"$R/oracle" -Wl,-rpath,/opt/rocm/lib -o "$OUT"

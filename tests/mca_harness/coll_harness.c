@@ -40,27 +40,6 @@ extern int harness_dev_copy_back(void *h, const void *d, size_t bytes);
 extern int harness_dev_free(void *d);
 
 OBJ_CLASS_INSTANCE(mca_coll_base_module_t, opal_object_t, NULL, NULL);
-OBJ_CLASS_INSTANCE(ompi_request_t, opal_object_t, NULL, NULL);
-ompi_request_t harness_request_null;
-
-/* opal_progress: the registered callbacks, polled by the wait loop below */
-static opal_progress_callback_t progress_cbs[8];
-static int n_progress_cbs;
-int opal_progress_register(opal_progress_callback_t cb)
-{
-    progress_cbs[n_progress_cbs++] = cb;
-    return 0;
-}
-int opal_progress_unregister(opal_progress_callback_t cb)
-{
-    for (int i = 0; i < n_progress_cbs; ++i)
-        if (progress_cbs[i] == cb) progress_cbs[i] = progress_cbs[--n_progress_cbs];
-    return 0;
-}
-void opal_progress(void)
-{
-    for (int i = 0; i < n_progress_cbs; ++i) progress_cbs[i]();
-}
 
 /* ompi_request_default_wait for a persistent request (request/req_wait.c) */
 static void harness_wait(ompi_request_t *req)

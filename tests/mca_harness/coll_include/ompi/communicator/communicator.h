@@ -2,7 +2,7 @@
 #ifndef HARNESS_COMMUNICATOR_H
 #define HARNESS_COMMUNICATOR_H
 #include "ompi/mca/coll/coll.h"
-typedef struct ompi_group_t { int remote_peers; } ompi_group_t;
+#include "ompi/group/group.h"
 typedef struct ompi_communicator_t {
     int rank, size, cid, inter;
     ompi_group_t *c_local_group;
@@ -12,5 +12,4 @@ typedef struct ompi_communicator_t {
 static inline int ompi_comm_rank(const ompi_communicator_t *c) { return c->rank; }
 static inline int ompi_comm_size(const ompi_communicator_t *c) { return c->size; }
 static inline int ompi_comm_get_cid(const ompi_communicator_t *c) { return c->cid; }
-static inline int ompi_group_have_remote_peers(const ompi_group_t *g) { return g->remote_peers; }
 #endif

@@ -17,7 +17,9 @@
 #include "ompi/datatype/ompi_datatype.h"
 #include "ompi/op/op.h"
 #include "ompi/runtime/ompi_rte.h"
+#include "ompi/request/request.h"
 #include "ompi/win/win.h"
+#include "opal/runtime/opal_progress.h"
 #include "opal/util/info.h"
 #include "../../oracle/oracle.h"
 #include "osc_rocm.h"
@@ -69,6 +71,7 @@ int main(int argc, char **argv)
     g_rank = atoi(argv[2]);
     g_size = atoi(argv[3]);
     for (i = 0; i < 64; ++i) ompi_op_ddt_map[i] = i;
+    local.grp_proc_count = g_size;
     comm = (ompi_communicator_t){g_rank, g_size, 5, 0, &local, NULL};
     if (c->osc_version.mca_register_component_params)
         c->osc_version.mca_register_component_params();
@@ -163,7 +166,97 @@ int main(int argc, char **argv)
             for (i = 0; i < g_size; ++i) CHECK(got[i] == (float) i, "slot %d holds %g", i, got[i]);
         }
     }
-    CHECK(m->osc_start(NULL, 0, &win) == OMPI_ERR_NOT_SUPPORTED, "PSCW not provided");
+
+    /* general active target (osc_sm_active_target.c:126-335): expose to the
+     * previous rank, access the next; two epochs closed by wait, one by test */
+    {
+        const int wprv = prv, wnxt = nxt;
+        ompi_group_t gprv = {0, 1, &wprv}, gnxt = {0, 1, &wnxt}, gnone = {0, 0, NULL};
+        const int k = 4099;
+        int flag = 0, e;
+        CHECK(m->osc_complete(&win) == OMPI_ERR_RMA_SYNC, "complete without start");
+        CHECK(m->osc_wait(&win) == OMPI_ERR_RMA_SYNC, "wait without post");
+        CHECK(m->osc_test(&win, &flag) == OMPI_ERR_RMA_SYNC, "test without post");
+        CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence before pscw");
+        for (e = 0; e < 3; ++e) {
+            float *mine = malloc(k * 4), *theirs = malloc(k * 4);
+            long spins = 0;
+            fill_exact(mine, k, g_rank, 10 + e);
+            fill_exact(theirs, k, prv, 10 + e);
+            CHECK(harness_dev_copy_in(dorg, mine, k * 4) == 0, "origin");
+            CHECK(m->osc_post(&gprv, 0, &win) == OMPI_SUCCESS, "post %d", e);
+            CHECK(m->osc_post(&gprv, 0, &win) == OMPI_ERR_RMA_SYNC, "second post");
+            CHECK(m->osc_start(&gnxt, 0, &win) == OMPI_SUCCESS, "start %d", e);
+            CHECK(m->osc_start(&gnxt, 0, &win) == OMPI_ERR_RMA_SYNC, "second start");
+            CHECK(m->osc_put(dorg, k, &dfloat, nxt, 0, k, &dfloat, &win) == OMPI_SUCCESS, "pscw put");
+            CHECK(m->osc_complete(&win) == OMPI_SUCCESS, "complete %d", e);
+            if (e < 2) {
+                CHECK(m->osc_wait(&win) == OMPI_SUCCESS, "wait %d", e);
+            } else {
+                do {
+                    CHECK(m->osc_test(&win, &flag) == OMPI_SUCCESS, "test");
+                } while (!flag && ++spins < 100000000L);
+                CHECK(flag, "MPI_Win_test never completed");
+            }
+            CHECK(harness_dev_copy_back(got, dbase, k * 4) == 0, "copy back");
+            CHECK(0 == memcmp(got, theirs, k * 4), "pscw epoch %d window", e);
+            /* everyone checked before the next epoch overwrites: an empty
+             * epoch of a fence does it */
+            CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence after epoch");
+            free(mine);
+            free(theirs);
+        }
+        /* the empty group and MPI_MODE_NOCHECK pass through */
+        CHECK(m->osc_post(&gnone, MPI_MODE_NOCHECK, &win) == OMPI_SUCCESS &&
+                  m->osc_start(&gnone, MPI_MODE_NOCHECK, &win) == OMPI_SUCCESS &&
+                  m->osc_complete(&win) == OMPI_SUCCESS && m->osc_wait(&win) == OMPI_SUCCESS,
+              "empty epoch");
+    }
+
+    /* request-based RMA under lock_all: MPI_Wait = opal_progress until the
+     * request completes; then the window holds the put and the sum */
+    {
+        const int k = 5003;
+        float *mine = malloc(k * 4), *theirs = malloc(k * 4), *fetched = malloc(k * 4);
+        ompi_request_t *r1 = NULL, *r2 = NULL, *r3 = NULL;
+        fill_exact(mine, k, g_rank, 20);
+        fill_exact(theirs, k, prv, 20);
+        CHECK(harness_dev_copy_in(dorg, mine, k * 4) == 0, "origin");
+        CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence before requests");
+        CHECK(harness_dev_copy_back(exp, dbase, n * 4) == 0, "window before");
+        CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence before requests 2");
+        CHECK(m->osc_lock_all(0, &win) == OMPI_SUCCESS, "lock_all");
+        CHECK(m->osc_rput(dorg, k, &dfloat, nxt, 0, k, &dfloat, &win, &r1) == OMPI_SUCCESS && r1,
+              "rput");
+        CHECK(m->osc_raccumulate(dorg, k, &dfloat, nxt, 2 * k, k, &dfloat, &sum, &win, &r2) ==
+                  OMPI_SUCCESS && r2, "raccumulate");
+        CHECK(m->osc_rget(dgot, k, &dfloat, nxt, 4 * k, k, &dfloat, &win, &r3) == OMPI_SUCCESS && r3,
+              "rget");
+        CHECK(m->osc_raccumulate(dorg, 3, &dfloat, nxt, 0, 3, &dfloat, &user, &win, &r3) ==
+                  OMPI_ERR_NOT_SUPPORTED, "user op refused (request)");
+        while (!REQUEST_COMPLETE(r1) || !REQUEST_COMPLETE(r2)) opal_progress();
+        CHECK(r1->req_status.MPI_ERROR == OMPI_SUCCESS && r2->req_status.MPI_ERROR == OMPI_SUCCESS,
+              "request status");
+        CHECK(r1->req_free(&r1) == OMPI_SUCCESS && r1 == MPI_REQUEST_NULL, "free r1");
+        CHECK(r2->req_free(&r2) == OMPI_SUCCESS, "free r2");
+        CHECK(r3->req_free(&r3) == OMPI_SUCCESS, "free r3 (waits)");
+        CHECK(m->osc_unlock_all(&win) == OMPI_SUCCESS, "unlock_all");
+        CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence after requests");
+        CHECK(harness_dev_copy_back(got, dbase, n * 4) == 0, "window after");
+        CHECK(0 == memcmp(got, theirs, k * 4), "rput landed");
+        memcpy(init_nxt, exp + 2 * k, k * 4);
+        orc_op_2buff(ORC_OP_SUM, ORC_T_FLOAT, theirs, init_nxt, k);
+        CHECK(0 == memcmp(got + 2 * k, init_nxt, k * 4), "raccumulate landed");
+        /* rget read [4k, 5k) of the next window: its init + my first accumulate */
+        fill_exact(init_nxt, n, nxt, 1);
+        memcpy(org_rank, org, n * 4);
+        orc_op_2buff(ORC_OP_SUM, ORC_T_FLOAT, org_rank, init_nxt, n);
+        CHECK(harness_dev_copy_back(fetched, dgot, k * 4) == 0, "rget back");
+        CHECK(0 == memcmp(fetched, init_nxt + 4 * k, k * 4), "rget fetched");
+        free(mine);
+        free(theirs);
+        free(fetched);
+    }
 
     /* MPI_Win_allocate: a shared counter, fetch_and_op from every rank */
     CHECK(c->osc_select(&awin, &abase, 0 == g_rank ? 64 : 0, 8, &comm, &dev_info,

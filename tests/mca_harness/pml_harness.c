@@ -42,24 +42,9 @@ extern int harness_dev_copy_back(void *h, const void *d, size_t bytes);
 extern int harness_dev_copy_in(void *d, const void *h, size_t bytes);
 extern int harness_dev_free(void *d);
 
-OBJ_CLASS_INSTANCE(ompi_request_t, opal_object_t, NULL, NULL);
-ompi_request_t harness_request_null;
 harness_proc_name_t harness_proc_name = {4343, 0};
 struct ompi_datatype_t harness_mpi_byte = {0, 1, 1, 1};
 mca_pml_base_module_t mca_pml;
-
-static opal_progress_callback_t progress_cbs[8];
-static int n_progress_cbs;
-int opal_progress_register(opal_progress_callback_t cb)
-{
-    progress_cbs[n_progress_cbs++] = cb;
-    return 0;
-}
-int opal_progress_unregister(opal_progress_callback_t cb) { return 0; }
-void opal_progress(void)
-{
-    for (int i = 0; i < n_progress_cbs; ++i) progress_cbs[i]();
-}
 
 static int g_rank, g_size;
 #define CHECK(c, ...)                                                             \

@@ -513,6 +513,153 @@ def case_lock_all(comm, rank, n, salt, nbytes=100003):
         win.free()
 
 
+def case_pscw_ring(comm, rank, n, salt, nbytes=200003, epochs=3, use_test=False):
+    """General active target (osc_sm_active_target.c:126-335): each rank
+    exposes its window to the previous rank (post [prv]) and accesses the
+    next one (start [nxt]), puts, completes and waits; `epochs` epochs in a
+    row (the counters are cumulative), the last one closed by MPI_Win_test
+    when use_test."""
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    base = zeros(nbytes)
+    win = osc.Window.create(comm, base, nbytes)
+    try:
+        for e in range(epochs):
+            src = dev(payload(rank, salt + e, nbytes))
+            win.post([prv], stream=STREAM)
+            win.start([nxt], stream=STREAM)
+            win.put(src, nxt, 0, nbytes, stream=STREAM)
+            win.complete(stream=STREAM)
+            if use_test and e == epochs - 1:
+                STREAM.synchronize()
+                import time
+                t0, done = time.time(), False
+                while not done and time.time() - t0 < 20:
+                    done = win.test()
+                if not done:
+                    return False, "MPI_Win_test never saw the origin complete"
+                torch.cuda.synchronize()
+            else:
+                win.wait(stream=STREAM, blocking=True)
+            ok, msg = eq(host(base), payload(prv, salt + e, nbytes), f"epoch {e}")
+            if not ok:
+                return ok, msg
+            comm_barrier()  # the next epoch overwrites what was just checked
+        return True, ""
+    finally:
+        win.free()
+
+
+def case_pscw_all_to_one(comm, rank, n, salt, count=100003):
+    """Rank 0 posts to every other rank; each origin accumulates (SUM, exact
+    data) into its own slice of rank 0's window, then rank 0 waits: every
+    slice is bit-exact vs op/base, with rank 0 reading right after wait."""
+    F = mop.MPI_FLOAT
+    init = fp_inputs(F, count * n, 99, salt, "E")
+    org = [fp_inputs(F, count, r, salt + 1, "E") for r in range(n)]
+    base = dev(init if rank == 0 else np.zeros(0, np.float32), extra=16)
+    win = osc.Window.create(comm, base, base.numel(), disp_unit=4)
+    try:
+        if rank == 0:
+            win.post(range(1, n), stream=STREAM)
+            win.wait(stream=STREAM, blocking=True)
+            exp = init.copy()
+            for r in range(1, n):
+                sl = exp[r * count:(r + 1) * count]
+                orc.op_2buff(mop.MPI_SUM.index, F.code, org[r].copy(), sl, count)
+            return eq(host(base)[:count * n * 4].view(np.float32), exp, "slices")
+        o = dev(org[rank])
+        win.start([0], stream=STREAM)
+        win.accumulate(o, count, F, 0, rank * count, mop.MPI_SUM, stream=STREAM)
+        win.complete(stream=STREAM, blocking=True)
+        return True, ""
+    finally:
+        win.free()
+
+
+def case_pscw_errors(comm, rank, n):
+    """Epoch calls out of order return OMPI_AMD_ERR_RMA_SYNC
+    (osc_sm_active_target.c:137-140, 191-193, 230-233, 279-282, 314-317)."""
+    win = osc.Window.allocate(comm, 64, disp_unit=1)
+    bad = []
+    try:
+        for what, fn in (("complete without start", lambda: win.complete(stream=STREAM)),
+                         ("wait without post", lambda: win.wait(stream=STREAM)),
+                         ("test without post", lambda: win.test())):
+            try:
+                fn()
+                bad.append(what + " accepted")
+            except _lib.OmpiAmdError as e:
+                if e.code != _lib.ERR_RMA_SYNC:
+                    bad.append(f"{what}: code {e.code}")
+        # an epoch of the empty group: post / start / complete / wait pass
+        win.post([], stream=STREAM)
+        try:
+            win.post([], stream=STREAM)
+            bad.append("second post accepted")
+        except _lib.OmpiAmdError as e:
+            if e.code != _lib.ERR_RMA_SYNC:
+                bad.append(f"second post: code {e.code}")
+        win.start([], stream=STREAM)
+        win.complete(stream=STREAM)
+        win.wait(stream=STREAM, blocking=True)
+        return not bad, "; ".join(bad)
+    finally:
+        win.free()
+
+
+def case_request_rma(comm, rank, n, salt, count=65537):
+    """MPI_Rput / _Raccumulate / _Rget / _Rget_accumulate under lock_all:
+    each request completes (test / wait) once its kernels ran; the windows
+    then hold exactly the puts and the op/base sums."""
+    F = mop.MPI_FLOAT
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    init = [fp_inputs(F, 3 * count, r, salt, "E") for r in range(n)]
+    org = [fp_inputs(F, count, r, salt + 1, "E") for r in range(n)]
+    org2 = [fp_inputs(F, count, r, salt + 2, "E") for r in range(n)]
+    src = [fp_inputs(F, count, r, salt + 3, "E") for r in range(n)]
+    base = dev(init[rank])
+    win = osc.Window.create(comm, base, 3 * count * 4, disp_unit=4)
+    try:
+        comm_barrier()
+        s, o, o2 = dev(src[rank]), dev(org[rank]), dev(org2[rank])
+        back, res = zeros(count * 4), zeros(count * 4)
+        win.lock_all(stream=STREAM)
+        r1 = win.rput(s, nxt, 0, count * 4, stream=STREAM)
+        r2 = win.raccumulate(o, count, F, nxt, count, mop.MPI_SUM, stream=STREAM)
+        r3 = win.rget(back, nxt, 2 * count, count * 4, stream=STREAM)
+        r4 = win.rget_accumulate(o2, res, count, F, nxt, count, mop.MPI_SUM, stream=STREAM)
+        import time
+        t0, done = time.time(), False
+        while not done and time.time() - t0 < 20:
+            done = r1.test()
+        for r in (r2, r3, r4):
+            r.wait()
+        if not (done and r2.test() and r3.test() and r4.test()):
+            return False, "a request never completed"
+        for r in (r1, r2, r3, r4):
+            r.free()
+        win.unlock_all(stream=STREAM)
+        comm_barrier()
+        mine = host(base).view(np.float32)
+        ok, msg = eq(mine[:count], src[prv], "rput")
+        if not ok:
+            return ok, msg
+        b = init[rank][count:2 * count].copy()
+        orc.op_2buff(mop.MPI_SUM.index, F.code, org[prv].copy(), b, count)
+        exp_res = init[nxt][count:2 * count].copy()
+        orc.op_2buff(mop.MPI_SUM.index, F.code, org[rank].copy(), exp_res, count)
+        orc.op_2buff(mop.MPI_SUM.index, F.code, org2[prv].copy(), b, count)
+        ok, msg = eq(mine[count:2 * count], b, "raccumulate + rget_accumulate")
+        if not ok:
+            return ok, msg
+        ok, msg = eq(host(back).view(np.float32), init[nxt][2 * count:], "rget")
+        if not ok:
+            return ok, msg
+        return eq(host(res).view(np.float32), exp_res, "rget_accumulate fetched")
+    finally:
+        win.free()
+
+
 def comm_barrier():
     STREAM.synchronize()
     dist.barrier()
@@ -566,6 +713,11 @@ def main():
         ("osc_compare_and_swap", lambda: case_cas(comm, rank, n)),
         ("osc_passive_exclusive_rmw", lambda: case_passive_exclusive(comm, rank, n)),
         ("osc_lock_all_get", lambda: case_lock_all(comm, rank, n, 93)),
+        ("osc_pscw_ring", lambda: case_pscw_ring(comm, rank, n, 94)),
+        ("osc_pscw_ring_test", lambda: case_pscw_ring(comm, rank, n, 95, epochs=2, use_test=True)),
+        ("osc_pscw_all_to_one_acc", lambda: case_pscw_all_to_one(comm, rank, n, 96)),
+        ("osc_pscw_errors", lambda: case_pscw_errors(comm, rank, n)),
+        ("osc_request_rma", lambda: case_request_rma(comm, rank, n, 97)),
     ]
     only = os.environ.get("P2P_OSC_ONLY")
     all_ok = True

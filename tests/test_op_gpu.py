@@ -277,3 +277,43 @@ def test_large_buffer_sum_float(orc):
     exp = np.empty_like(a)
     orc.op_3buff(3, 15, a, b, exp, n)
     assert np.array_equal(out.cpu().numpy().view(np.uint32), exp.view(np.uint32))
+
+
+MISALIGNED = [(mop.MPI_SUM, mop.MPI_FLOAT), (mop.MPI_MAX, mop.MPI_DOUBLE),
+              (mop.MPI_BXOR, mop.MPI_UINT8_T), (mop.MPI_PROD, mop.MPI_INT16_T),
+              (mop.MPI_MAXLOC, mop.MPI_FLOAT_INT)]
+
+
+@pytest.mark.parametrize("op,dt", MISALIGNED, ids=[f"{o.name}-{d.name}" for o, d in MISALIGNED])
+def test_misaligned_operands(orc, op, dt):
+    """Operands displaced inside their 16-B vectors: all by the same amount
+    (head peeled, vectors after it) and by different amounts (element path),
+    sizes around the head / tail boundaries; the bytes around the result stay
+    untouched."""
+    ext = dt.extent
+    for n in (1, 3, 5, 17, 1000, 65537, 1 << 20):
+        for offs in ((ext, ext, ext), (3 * ext, 3 * ext, 3 * ext), (ext, 0, ext), (0, 2 * ext, ext)):
+            a = gen(dt, n, 400 + n % 97)
+            b = gen(dt, n, 500 + n % 89)
+            out0 = gen(dt, n + 8, 600)
+            xo, yo, do = offs
+            ta, pa = to_dev(a, xo)
+            tb, pb = to_dev(b, yo)
+            raw_out = np.ascontiguousarray(out0).view(np.uint8)
+            to, po = to_dev(out0, do)  # guard bytes: the rest of out0 after n elements
+            mop.reduce_local_3buff_async(pa, pb, po, n, dt, op)
+            torch.cuda.synchronize()
+            exp3 = out0[:n].copy()
+            orc.op_3buff(op.index, dt.code, a, b, exp3, n)
+            got = from_dev(to, do, raw_out.nbytes)
+            assert same_bits(got[:n * ext].view(dt.np_dtype), exp3, dt), (op.name, dt.name, n, offs)
+            assert np.array_equal(got[n * ext:], raw_out[n * ext:]), ("guard bytes", n, offs)
+            # 2-buffer (inout shares the in operand's offset or not)
+            ta, pa = to_dev(a, xo)
+            tb, pb = to_dev(b, do)
+            mop.reduce_local_async(pa, pb, n, dt, op)
+            torch.cuda.synchronize()
+            exp = b.copy()
+            orc.op_2buff(op.index, dt.code, a, exp, n)
+            got2 = from_dev(tb, do, n * ext).view(dt.np_dtype)
+            assert same_bits(got2, exp, dt), (op.name, dt.name, n, offs, "2buff")
