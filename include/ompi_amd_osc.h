@@ -96,6 +96,22 @@ int ompi_amd_fetch_and_op(ompi_amd_win_t *win, const void *origin, void *result,
 int ompi_amd_compare_and_swap(ompi_amd_win_t *win, const void *origin, const void *compare,
                               void *result, int type, int target, size_t disp, void *stream);
 
+/* MPI_Win_allocate_shared (osc_sm_component.c:244-360): rank 0 allocates
+ * one exportable device allocation holding every rank's segment back to
+ * back (each `bytes`, or rounded up to 4 KiB with noncontig =
+ * alloc_shared_noncontig), every other rank maps it once, so the segments
+ * are contiguous in every process and kernels may load / store any of them
+ * directly.  *base = this rank's segment.  Zero-filled.  Collective. */
+int ompi_amd_win_allocate_shared(ompi_amd_comm_t *comm, size_t bytes, int disp_unit, int noncontig,
+                                 void **base, ompi_amd_win_t **win);
+/* MPI_Win_shared_query (osc_sm_component.c:455-485): size, disp_unit and
+ * this process's address of `rank`'s segment; rank < 0 (MPI_PROC_NULL) =
+ * the first segment of nonzero size.  Windows not made by
+ * ompi_amd_win_allocate_shared: OMPI_AMD_ERR_UNSUPPORTED (osc/sm's
+ * MPI_ERR_WIN). */
+int ompi_amd_win_shared_query(ompi_amd_win_t *win, int rank, size_t *size, int *disp_unit,
+                              void **baseptr);
+
 /* General active target synchronisation (MPI_Win_post / _start /
  * _complete / _wait / _test; osc.h:366-372, osc/sm's
  * osc_sm_active_target.c:126-330).  ranks: the group's members as ranks of

@@ -244,6 +244,12 @@ PROTOTYPES = [
     ("ompi_amd_compare_and_swap", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_int, _C.c_int, _C.c_size_t,
       _C.c_void_p]),
+    ("ompi_amd_win_allocate_shared", _C.c_int,
+     [_C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.POINTER(_C.c_void_p),
+      _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_win_shared_query", _C.c_int,
+     [_C.c_void_p, _C.c_int, _C.POINTER(_C.c_size_t), _C.POINTER(_C.c_int),
+      _C.POINTER(_C.c_void_p)]),
     ("ompi_amd_win_post", _C.c_int,
      [_C.c_void_p, _C.POINTER(_C.c_int), _C.c_int, _C.c_int, _C.c_void_p]),
     ("ompi_amd_win_start", _C.c_int,

@@ -297,10 +297,12 @@ __global__ __launch_bounds__(kOscThreads) void acc_kernel(const T *__restrict__ 
 }
 
 // Byte copy for put / get / fetches and the p2p receive: 16-B granules
-// (4 in flight per lane) when src and dst share their phase mod 16, else 4-B
-// or 1-B granules; one acquire per workgroup, persistent grid (as acc_kernel).
-__global__ __launch_bounds__(kOscThreads) void xfer_kernel(const char *src, char *dst,
-                                                           int64_t bytes, const uint32_t *gate) {
+// (UNROLL in flight per lane) when src and dst share their phase mod 16,
+// else 4-B or 1-B granules; one acquire per workgroup, persistent grid (as
+// acc_kernel).
+template <int THREADS, int UNROLL>
+__global__ __launch_bounds__(THREADS) void xfer_kernel(const char *src, char *dst, int64_t bytes,
+                                                       const uint32_t *gate) {
     if (!gate_open(gate)) return;
     if (threadIdx.x == 0) osc_acquire();
     __syncthreads();
@@ -309,36 +311,36 @@ __global__ __launch_bounds__(kOscThreads) void xfer_kernel(const char *src, char
     int64_t head = (int64_t)((g - ((uintptr_t)src & (uintptr_t)(g - 1))) & (uintptr_t)(g - 1));
     if (head > bytes) head = bytes;
     const int64_t nbody = (bytes - head) / g;
-    const int64_t tid = (int64_t)blockIdx.x * kOscThreads + threadIdx.x;
+    const int64_t tid = (int64_t)blockIdx.x * THREADS + threadIdx.x;
     if (g == 16) {
         const u32x4 *sv = reinterpret_cast<const u32x4 *>(src + head);
         u32x4 *dv = reinterpret_cast<u32x4 *>(dst + head);
-        constexpr int64_t chunk = (int64_t)kOscThreads * kOscUnroll;
+        constexpr int64_t chunk = (int64_t)THREADS * UNROLL;
         for (int64_t base = (int64_t)blockIdx.x * chunk + threadIdx.x; base < nbody;
              base += (int64_t)gridDim.x * chunk) {
-            u32x4 v[kOscUnroll];
+            u32x4 v[UNROLL];
 #pragma unroll
-            for (int u = 0; u < kOscUnroll; ++u) {
-                const int64_t i = base + (int64_t)u * kOscThreads;
+            for (int u = 0; u < UNROLL; ++u) {
+                const int64_t i = base + (int64_t)u * THREADS;
                 if (i < nbody) v[u] = __builtin_nontemporal_load(sv + i);
             }
 #pragma unroll
-            for (int u = 0; u < kOscUnroll; ++u) {
-                const int64_t i = base + (int64_t)u * kOscThreads;
+            for (int u = 0; u < UNROLL; ++u) {
+                const int64_t i = base + (int64_t)u * THREADS;
                 if (i < nbody) __builtin_nontemporal_store(v[u], dv + i);
             }
         }
     } else if (g == 4) {
         const uint32_t *sw = reinterpret_cast<const uint32_t *>(src + head);
         uint32_t *dw = reinterpret_cast<uint32_t *>(dst + head);
-        for (int64_t i = tid; i < nbody; i += (int64_t)gridDim.x * kOscThreads) dw[i] = sw[i];
+        for (int64_t i = tid; i < nbody; i += (int64_t)gridDim.x * THREADS) dw[i] = sw[i];
     } else {
-        for (int64_t i = tid; i < nbody; i += (int64_t)gridDim.x * kOscThreads)
+        for (int64_t i = tid; i < nbody; i += (int64_t)gridDim.x * THREADS)
             dst[head + i] = src[head + i];
     }
     const int64_t tail0 = head + nbody * g;
     const int64_t nrest = head + (bytes - tail0);
-    for (int64_t k = tid; k < nrest; k += (int64_t)gridDim.x * kOscThreads) {
+    for (int64_t k = tid; k < nrest; k += (int64_t)gridDim.x * THREADS) {
         const int64_t i = k < head ? k : tail0 + (k - head);
         dst[i] = src[i];
     }
@@ -431,6 +433,11 @@ struct ompi_amd_win {
     uint32_t complete_want = 0;             // access epochs origins must have closed here
     std::vector<int> start_group;
     hipStream_t query = nullptr;  // MPI_Win_test's counter reads
+    // MPI_Win_allocate_shared: one allocation on rank 0 holds every rank's
+    // segment back to back; the others map it once
+    bool shared = false;
+    char *shared_seg = nullptr;   // rank 0: the allocation; others: their mapping
+    ipc_ref *shared_ref = nullptr;
 };
 
 namespace ompi_amd {
@@ -483,14 +490,20 @@ static int64_t osc_grid_cap() {
     return cap;
 }
 
+// Copy shape: 256 threads x 4 16-B vectors per lane.  256x8, 256x16, 512x8,
+// 1024x4 and 1024x8 measured within noise of it (put 5.26-5.59 TB/s,
+// profiles/r03_xfer_shape_sweep.txt): bytes in flight are not the limit.
+constexpr int kXferThreads = 256, kXferUnroll = 4;
+
 int xfer_copy(const void *src, void *dst, size_t bytes, hipStream_t s, const uint32_t *gate) {
     if (bytes == 0) return OMPI_AMD_SUCCESS;
     const int64_t units = (int64_t)(bytes / 16) + 1;
-    const int64_t per = (int64_t)kOscThreads * kOscUnroll;
+    const int64_t per = (int64_t)kXferThreads * kXferUnroll;
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((units + per - 1) / per,
                                                                   osc_grid_cap()));
-    hipLaunchKernelGGL(xfer_kernel, dim3((unsigned)blocks), dim3(kOscThreads), 0, s,
-                       static_cast<const char *>(src), static_cast<char *>(dst), (int64_t)bytes, gate);
+    hipLaunchKernelGGL((xfer_kernel<kXferThreads, kXferUnroll>), dim3((unsigned)blocks),
+                       dim3(kXferThreads), 0, s, static_cast<const char *>(src),
+                       static_cast<char *>(dst), (int64_t)bytes, gate);
     return record_hip(hipGetLastError(), "xfer copy launch");
 }
 
@@ -557,8 +570,10 @@ static int rma_op(ompi_amd_win_t *w, const void *origin, void *result, size_t co
     return rc != OMPI_AMD_SUCCESS ? rc : urc;
 }
 
+// shared: every rank's base as this process maps it (MPI_Win_allocate_shared),
+// so nothing is exported or imported for the bases.
 static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit, bool owns,
-                     ompi_amd_win_t **out) {
+                     ompi_amd_win_t **out, char *const *shared = nullptr) {
     auto *w = new (std::nothrow) ompi_amd_win;
     if (!w) return OMPI_AMD_ERR_BAD_PARAM;
     w->c = c;
@@ -579,7 +594,7 @@ static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit
     win_blob mine{}, all[kOscMaxRanks];
     mine.bytes = bytes;
     mine.disp_unit = disp_unit;
-    if (rc == OMPI_AMD_SUCCESS && bytes) rc = comm_export(c, base, &mine.base);
+    if (rc == OMPI_AMD_SUCCESS && bytes && !shared) rc = comm_export(c, base, &mine.base);
     if (rc == OMPI_AMD_SUCCESS) mine.ctl = ctl_desc;
     // every rank takes part in the rendezvous, whatever failed locally
     mine.failed = rc == OMPI_AMD_SUCCESS ? 0 : 1;
@@ -598,7 +613,9 @@ static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit
             w->peer_ctl[p] = w->ctl;
             continue;
         }
-        if (all[p].bytes) {
+        if (shared) {
+            w->peer_base[p] = shared[p];
+        } else if (all[p].bytes) {
             const char *pb = nullptr;
             rc = comm_import(c, p, all[p].base, &pb, true, &w->pinned[p]);
             w->peer_base[p] = const_cast<char *>(pb);
@@ -691,8 +708,10 @@ int ompi_amd_win_free(ompi_amd_win_t *w) {
         if (w->pinned[p]) comm_unpin(c, w->pinned[p]);
         ipc_unmap(w->ctl_ref[p]);  // the process's mapping stays while others hold it
     }
+    ipc_unmap(w->shared_ref);
     const int brc2 = comm_allgather(c, nullptr, nullptr, 0);  // mappings closed before frees
     if (rc == OMPI_AMD_SUCCESS) rc = brc2;
+    if (w->shared && !w->shared_ref && w->shared_seg) hip_ignore(hipFree(w->shared_seg));
     if (w->query) hip_ignore(hipStreamDestroy(w->query));
     if (w->ctl) hip_ignore(hipFree(w->ctl));
     if (w->owns_base && w->base) hip_ignore(hipFree(w->base));
@@ -819,6 +838,94 @@ int ompi_amd_compare_and_swap(ompi_amd_win_t *w, const void *origin, const void 
     const int rc = record_hip(hipGetLastError(), "osc compare_and_swap launch");
     const int urc = launch_lock(w, target, 1, s);
     return rc != OMPI_AMD_SUCCESS ? rc : urc;
+}
+
+// ---- shared windows (osc_sm_component.c:244-360, 455-485) ----
+
+int ompi_amd_win_allocate_shared(ompi_amd_comm_t *c, size_t bytes, int disp_unit, int noncontig,
+                                 void **base, ompi_amd_win_t **out) {
+    if (!c || !out || !base || disp_unit <= 0) return OMPI_AMD_ERR_BAD_PARAM;
+    const int me = ompi_amd_comm_rank(c), n = ompi_amd_comm_size(c);
+    int rc = record_hip(hipSetDevice(comm_device(c)), "hipSetDevice");
+    if (rc == OMPI_AMD_SUCCESS) rc = comm_drain(c);
+    // segment sizes: exact, or whole pages with alloc_shared_noncontig
+    // (osc_sm_component.c:265-268)
+    uint64_t seg = noncontig ? (bytes + 4095) / 4096 * 4096 : bytes, segs[kOscMaxRanks] = {};
+    const int src = comm_allgather(c, &seg, segs, sizeof(seg));
+    if (rc == OMPI_AMD_SUCCESS) rc = src;
+    uint64_t prefix[kOscMaxRanks + 1] = {};
+    for (int p = 0; p < n; ++p) prefix[p + 1] = prefix[p] + segs[p];
+    // rank 0 allocates the whole window; everyone learns its descriptor
+    struct seg_blob {
+        ipc_desc d;
+        int64_t failed;
+    } mine{}, all[kOscMaxRanks];
+    char *m = nullptr;
+    if (me == 0 && rc == OMPI_AMD_SUCCESS) {
+        rc = comm_alloc_exportable(prefix[n] ? prefix[n] : 1, false, (void **)&m, &mine.d);
+        if (rc == OMPI_AMD_SUCCESS && prefix[n])
+            rc = record_hip(hipMemset(m, 0, prefix[n]), "hipMemset (shared window)");
+        if (rc == OMPI_AMD_SUCCESS)
+            rc = record_hip(hipStreamSynchronize(nullptr), "hipStreamSynchronize (shared window)");
+    }
+    mine.failed = rc == OMPI_AMD_SUCCESS ? 0 : 1;
+    const int arc = comm_allgather(c, &mine, all, sizeof(seg_blob));
+    if (rc == OMPI_AMD_SUCCESS) rc = arc;
+    if (rc == OMPI_AMD_SUCCESS && all[0].failed) {
+        record_msg("osc shared window: rank 0 could not allocate %llu bytes",
+                   (unsigned long long)prefix[n]);
+        rc = OMPI_AMD_ERR_BOOTSTRAP;
+    }
+    ipc_ref *ref = nullptr;
+    if (rc == OMPI_AMD_SUCCESS && me != 0) {
+        void *mb = nullptr;
+        const ipc_desc &d = all[0].d;
+        rc = ipc_map(ipc_alloc{d.h, d.pid, d.id, d.base, d.size}, &ref, &mb);
+        if (rc == OMPI_AMD_SUCCESS) m = static_cast<char *>(mb) + d.off;
+    }
+    int all_ok = 0;
+    const int grc = ompi_amd_comm_agree(c, rc == OMPI_AMD_SUCCESS, &all_ok);
+    if (rc == OMPI_AMD_SUCCESS && (grc != OMPI_AMD_SUCCESS || !all_ok))
+        rc = grc != OMPI_AMD_SUCCESS ? grc : OMPI_AMD_ERR_BOOTSTRAP;
+    char *bases[kOscMaxRanks] = {};
+    for (int p = 0; p < n && m; ++p) bases[p] = m + prefix[p];
+    ompi_amd_win_t *w = nullptr;
+    if (rc == OMPI_AMD_SUCCESS) rc = win_setup(c, bases[me], bytes, disp_unit, false, &w, bases);
+    if (rc != OMPI_AMD_SUCCESS) {
+        ipc_unmap(ref);
+        (void)comm_allgather(c, nullptr, nullptr, 0);  // every mapping closed before the free
+        if (me == 0 && m) hip_ignore(hipFree(m));
+        return rc;
+    }
+    for (int p = 0; p < n; ++p) w->peer_bytes[p] = segs[p];  // queried sizes (padded if noncontig)
+    w->bytes = segs[me];
+    w->shared = true;
+    w->shared_seg = m;
+    w->shared_ref = ref;
+    *base = bases[me];
+    *out = w;
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_win_shared_query(ompi_amd_win_t *w, int rank, size_t *size, int *disp_unit,
+                              void **baseptr) {
+    if (!w || !size || !disp_unit || !baseptr) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!w->shared) {  // osc_sm_component.c:460-462
+        record_msg("osc: MPI_Win_shared_query on a window not made by MPI_Win_allocate_shared");
+        return OMPI_AMD_ERR_UNSUPPORTED;
+    }
+    if (rank >= w->size) return OMPI_AMD_ERR_BAD_PARAM;
+    *size = 0;
+    *disp_unit = 0;
+    *baseptr = nullptr;
+    for (int p = rank < 0 ? 0 : rank; p < (rank < 0 ? w->size : rank + 1); ++p) {
+        if (rank < 0 && w->peer_bytes[p] == 0) continue;  // MPI_PROC_NULL: first nonzero segment
+        *size = w->peer_bytes[p];
+        *disp_unit = (int)w->peer_disp[p];
+        *baseptr = w->peer_base[p];
+        break;
+    }
+    return OMPI_AMD_SUCCESS;
 }
 
 // ---- general active target synchronisation (osc_sm_active_target.c) ----

@@ -80,6 +80,7 @@ typedef struct mca_coll_rocm_request_t {
     ompi_request_t super;
     ompi_amd_plan_t *plan;       /* persistent */
     ompi_amd_request_t *nbreq;   /* nonblocking */
+    struct rocm_nb_stage *stage; /* nonblocking: this rank's staged operands */
     struct mca_coll_rocm_request_t *next_active; /* started, not yet complete */
 } mca_coll_rocm_request_t;
 

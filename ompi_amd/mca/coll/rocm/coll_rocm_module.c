@@ -395,11 +395,26 @@ typedef struct {
     int how;        /* 0 as is, 1 byte copy of the typed span, 2 packed */
     ptrdiff_t gap;  /* true lower bound of the span */
     size_t bytes;
+    char *hbuf;     /* packed: the host side of the pack / unpack */
 } rocm_operand_t;
 
+/* Staging memory of one operand slot: the module's grow-only buffers for
+ * blocking calls, a nonblocking request's own for its lifetime. */
+typedef char *(*rocm_buf_fn)(void *ctx, int slot, int on_dev, size_t bytes);
+
+/* a nonblocking call's staged operands (rocm_nb_begin), copied back and
+ * freed when its request completes */
+struct rocm_nb_stage {
+    rocm_operand_t o[2];
+    int n;
+    void *dev[2], *host[2];
+};
+static void nb_stage_free(struct rocm_nb_stage *st);
+
 /* grow-only staging memory of one operand slot */
-static char *stage_buf(mca_coll_rocm_module_t *m, int slot, int on_dev, size_t bytes)
+static char *stage_buf(void *ctx, int slot, int on_dev, size_t bytes)
 {
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) ctx;
     void **p = on_dev ? &m->dstage[slot] : &m->hstage[slot];
     size_t *have = on_dev ? &m->dstage_bytes[slot] : &m->hstage_bytes[slot];
     if (bytes > *have) {
@@ -420,13 +435,14 @@ static char *stage_buf(mca_coll_rocm_module_t *m, int slot, int on_dev, size_t b
 /* Put every operand where the chosen path runs: device memory (packed when
  * its layout is not contiguous, since the device path moves bytes) or host
  * memory (the typed span as it is, for the saved function). */
-static int rocm_stage(mca_coll_rocm_module_t *m, rocm_operand_t *o, int n, int to_dev)
+static int rocm_stage_with(rocm_buf_fn get, void *ctx, rocm_operand_t *o, int n, int to_dev)
 {
     for (int i = 0; i < n; ++i) {
         rocm_operand_t *x = &o[i];
         int is_dev, contig;
         x->use = x->user;
         x->how = 0;
+        x->hbuf = NULL;
         if (NULL == x->user || MPI_IN_PLACE == x->user || 0 == x->count) continue;
         is_dev = ompi_amd_is_device_pointer(x->user);
         contig = ompi_datatype_is_contiguous_memory_layout(x->dtype, (int) x->count);
@@ -436,8 +452,8 @@ static int rocm_stage(mca_coll_rocm_module_t *m, rocm_operand_t *o, int n, int t
             char *h, *d;
             (void) ompi_datatype_type_size(x->dtype, &size);
             x->bytes = size * x->count;
-            h = stage_buf(m, i, 0, x->bytes);
-            d = stage_buf(m, i, 1, x->bytes);
+            h = get(ctx, i, 0, x->bytes);
+            d = get(ctx, i, 1, x->bytes);
             if (NULL == h || NULL == d) return OMPI_ERR_OUT_OF_RESOURCE;
             if (x->in) {
                 if (MPI_SUCCESS != ompi_datatype_sndrcv(x->user, (int) x->count, x->dtype, h,
@@ -447,6 +463,7 @@ static int rocm_stage(mca_coll_rocm_module_t *m, rocm_operand_t *o, int n, int t
                 }
             }
             x->use = d;
+            x->hbuf = h;
             x->how = 2;
         } else {
             ptrdiff_t lb, ext, tlb, text;
@@ -455,7 +472,7 @@ static int rocm_stage(mca_coll_rocm_module_t *m, rocm_operand_t *o, int n, int t
             (void) ompi_datatype_get_true_extent(x->dtype, &tlb, &text);
             x->bytes = (x->count - 1) * (size_t) ext + (size_t) text;
             x->gap = tlb;
-            b = stage_buf(m, i, to_dev, x->bytes);
+            b = get(ctx, i, to_dev, x->bytes);
             if (NULL == b) return OMPI_ERR_OUT_OF_RESOURCE;
             /* an output's gaps must survive the copy back */
             if ((x->in || (x->out && !contig)) &&
@@ -469,8 +486,13 @@ static int rocm_stage(mca_coll_rocm_module_t *m, rocm_operand_t *o, int n, int t
     return OMPI_SUCCESS;
 }
 
+static int rocm_stage(mca_coll_rocm_module_t *m, rocm_operand_t *o, int n, int to_dev)
+{
+    return rocm_stage_with(stage_buf, m, o, n, to_dev);
+}
+
 /* copy staged outputs back to the caller's buffers */
-static int rocm_unstage(mca_coll_rocm_module_t *m, const rocm_operand_t *o, int n, int rc)
+static int rocm_unstage_ops(const rocm_operand_t *o, int n, int rc)
 {
     for (int i = 0; OMPI_SUCCESS == rc && i < n; ++i) {
         const rocm_operand_t *x = &o[i];
@@ -480,13 +502,19 @@ static int rocm_unstage(mca_coll_rocm_module_t *m, const rocm_operand_t *o, int 
                                                     (char *) x->use + x->gap, x->bytes)) {
                 rc = OMPI_ERROR;
             }
-        } else if (OMPI_AMD_SUCCESS != ompi_amd_memcpy(m->hstage[i], x->use, x->bytes) ||
-                   MPI_SUCCESS != ompi_datatype_sndrcv(m->hstage[i], (int) x->bytes, MPI_BYTE,
+        } else if (OMPI_AMD_SUCCESS != ompi_amd_memcpy(x->hbuf, x->use, x->bytes) ||
+                   MPI_SUCCESS != ompi_datatype_sndrcv(x->hbuf, (int) x->bytes, MPI_BYTE,
                                                        x->user, (int) x->count, x->dtype)) {
             rc = OMPI_ERROR;
         }
     }
     return rc;
+}
+
+static int rocm_unstage(mca_coll_rocm_module_t *m, const rocm_operand_t *o, int n, int rc)
+{
+    (void) m;
+    return rocm_unstage_ops(o, n, rc);
 }
 
 /* decide, and stage for the decision: *path is ROCM_DEVICE or a saved path */
@@ -497,6 +525,7 @@ static int rocm_begin(mca_coll_rocm_module_t *m, int uniform_ok, int local_dev,
     for (int i = 0; i < n; ++i) {
         o[i].use = o[i].user;
         o[i].how = 0;
+        o[i].hbuf = NULL;
     }
     if (ROCM_SAVED == *path) return OMPI_SUCCESS;
     return rocm_stage(m, o, n, ROCM_DEVICE == *path);
@@ -746,6 +775,12 @@ static int rocm_progress(void)
         mca_coll_rocm_request_t *r = done;
         done = r->next_active;
         r->next_active = NULL;
+        if (NULL != r->stage) {  /* staged outputs back to the caller's buffers */
+            r->super.req_status.MPI_ERROR =
+                rocm_unstage_ops(r->stage->o, r->stage->n, r->super.req_status.MPI_ERROR);
+            nb_stage_free(r->stage);
+            r->stage = NULL;
+        }
         ompi_request_complete(&r->super, true);
         ++completed;
     }
@@ -818,9 +853,11 @@ static int rocm_request_free(ompi_request_t **rptr)
         r->plan = NULL;
     }
     if (NULL != r->nbreq) {
-        rc = ompi_amd_request_free(r->nbreq);
+        rc = ompi_amd_request_free(r->nbreq);  /* waits for the device work */
         r->nbreq = NULL;
     }
+    nb_stage_free(r->stage);  /* freed before completion: outputs are undefined */
+    r->stage = NULL;
     OMPI_REQUEST_FINI(&r->super);
     OBJ_RELEASE(r);
     *rptr = MPI_REQUEST_NULL;
@@ -836,55 +873,89 @@ static void rocm_request_construct(mca_coll_rocm_request_t *r)
     r->super.req_cancel = NULL;
     r->plan = NULL;
     r->nbreq = NULL;
+    r->stage = NULL;
     r->next_active = NULL;
 }
 
 OBJ_CLASS_INSTANCE(mca_coll_rocm_request_t, ompi_request_t, rocm_request_construct, NULL);
 
-/* MPI_Iallreduce (coll.h:271-274).  The path agreement is the one host
- * rendezvous that precedes the call's own (nonblocking) post: every rank
- * reaches it at the same collective, as for the blocking allreduce. */
-int mca_coll_rocm_iallreduce(const void *sbuf, void *rbuf, int count,
-                             struct ompi_datatype_t *dtype, struct ompi_op_t *op,
-                             struct ompi_communicator_t *comm, ompi_request_t **request,
-                             mca_coll_base_module_t *module)
+/* ------------------------------------------------------------ nonblocking */
+
+/* a nonblocking request's own staging memory, exact size, freed with it */
+static char *nb_buf(void *ctx, int slot, int on_dev, size_t bytes)
 {
-    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
-    const int t = type_code(dtype);
-    const int ok = reduction_ok_n(dtype, op, (size_t) count) && dev(sbuf) && dev(rbuf);
-    mca_coll_rocm_request_t *r;
-    ompi_amd_request_t *nb = NULL;
+    struct rocm_nb_stage *st = (struct rocm_nb_stage *) ctx;
+    void **p = on_dev ? &st->dev[slot] : &st->host[slot];
+    if (NULL == *p) {
+        if (!on_dev) {
+            *p = malloc(bytes ? bytes : 1);
+        } else if (OMPI_AMD_SUCCESS != ompi_amd_device_alloc(p, bytes ? bytes : 1)) {
+            *p = NULL;
+        }
+    }
+    return (char *) *p;
+}
+
+static void nb_stage_free(struct rocm_nb_stage *st)
+{
+    if (NULL == st) return;
+    for (int k = 0; k < 2; ++k) {
+        (void) ompi_amd_device_free(st->dev[k]);
+        free(st->host[k]);
+    }
+    free(st);
+}
+
+/* The path of one nonblocking call.  What every rank computes alike comes
+ * first (no rendezvous when it fails).  A module locked to DEVICE (§3.2 of
+ * every rank locks at the same blocking call) takes the device
+ * path with no vote at all; a rank whose operands are not device-contiguous
+ * stages them into memory of the request — inputs now, outputs back when
+ * the request completes (rocm_progress), as coll/cuda stages for its
+ * blocking calls (coll_cuda_allreduce.c:42-72) — and counts the mismatch
+ * for the next recheck vote.  Otherwise the per-call vote. */
+static int rocm_nb_begin(mca_coll_rocm_module_t *m, int uniform_ok, int local_ok,
+                         rocm_operand_t *o, int n, struct rocm_nb_stage **stage, int *path)
+{
+    struct rocm_nb_stage *st;
     int rc;
-    if (!take_device_path(m, ok)) {
-        return m->c_coll.coll_iallreduce(sbuf, rbuf, count, dtype, op, comm, request,
-                                         m->c_coll.coll_iallreduce_module);
+    *stage = NULL;
+    for (int i = 0; i < n; ++i) {
+        o[i].use = o[i].user;
+        o[i].how = 0;
+        o[i].hbuf = NULL;
     }
-    r = OBJ_NEW(mca_coll_rocm_request_t);
-    if (NULL == r) return OMPI_ERROR;
-    rc = ompi_amd_iallreduce(m->dev_comm, MPI_IN_PLACE == sbuf ? rbuf : sbuf, rbuf,
-                             (size_t) count, t, op->o_f_to_c_index, NULL, &nb);
-    if (OMPI_AMD_SUCCESS != rc) {
-        if (NULL != nb) (void) ompi_amd_request_free(nb);
-        OBJ_RELEASE(r);
-        return to_ompi_err(rc);
+    *path = ROCM_SAVED;
+    if (!uniform_ok) return OMPI_SUCCESS;
+    if (ROCM_RES_DEVICE != m->mode) {
+        *path = take_device_path(m, local_ok) ? ROCM_DEVICE : ROCM_SAVED;
+        return OMPI_SUCCESS;
     }
-    OMPI_REQUEST_INIT(&r->super, false);
-    r->super.req_state = OMPI_REQUEST_ACTIVE;
-    r->super.req_mpi_object.comm = comm;
-    r->super.req_status.MPI_ERROR = OMPI_SUCCESS;
-    r->nbreq = nb;
-    rocm_link_active(r);
-    *request = &r->super;
+    *path = ROCM_DEVICE;
+    if (local_ok) return OMPI_SUCCESS;
+    m->mismatched++;
+    st = calloc(1, sizeof(*st));
+    if (NULL == st) return OMPI_ERR_OUT_OF_RESOURCE;
+    rc = rocm_stage_with(nb_buf, st, o, n, 1);
+    if (OMPI_SUCCESS != rc) {
+        nb_stage_free(st);
+        return rc;
+    }
+    memcpy(st->o, o, (size_t) n * sizeof(*o));
+    st->n = n;
+    *stage = st;
     return OMPI_SUCCESS;
 }
 
-/* a library request behind an MPI request, completed by rocm_progress */
-static int rocm_wrap_nb(ompi_amd_request_t *nb, struct ompi_communicator_t *comm,
-                        ompi_request_t **request)
+/* a library request (and the call's staged operands) behind an MPI
+ * request, completed by rocm_progress */
+static int rocm_wrap_nb(ompi_amd_request_t *nb, struct rocm_nb_stage *stage,
+                        struct ompi_communicator_t *comm, ompi_request_t **request)
 {
     mca_coll_rocm_request_t *r = OBJ_NEW(mca_coll_rocm_request_t);
     if (NULL == r) {
         (void) ompi_amd_request_free(nb);
+        nb_stage_free(stage);
         return OMPI_ERROR;
     }
     OMPI_REQUEST_INIT(&r->super, false);
@@ -892,33 +963,75 @@ static int rocm_wrap_nb(ompi_amd_request_t *nb, struct ompi_communicator_t *comm
     r->super.req_mpi_object.comm = comm;
     r->super.req_status.MPI_ERROR = OMPI_SUCCESS;
     r->nbreq = nb;
+    r->stage = stage;
     rocm_link_active(r);
     *request = &r->super;
     return OMPI_SUCCESS;
 }
 
+/* the library's answer to a nonblocking post: a request, or the error (the
+ * staged operands go with it) */
+static int rocm_nb_post(int rc, ompi_amd_request_t *nb, struct rocm_nb_stage *stage,
+                        struct ompi_communicator_t *comm, ompi_request_t **request)
+{
+    if (OMPI_AMD_SUCCESS != rc) {
+        if (NULL != nb) (void) ompi_amd_request_free(nb);
+        nb_stage_free(stage);
+        return to_ompi_err(rc);
+    }
+    return rocm_wrap_nb(nb, stage, comm, request);
+}
+
+/* MPI_Iallreduce (coll.h:271-274) */
+int mca_coll_rocm_iallreduce(const void *sbuf, void *rbuf, int count,
+                             struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                             struct ompi_communicator_t *comm, ompi_request_t **request,
+                             mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const int inplace = MPI_IN_PLACE == sbuf;
+    rocm_operand_t o[2] = {{(void *) sbuf, (size_t) count, dtype, 1, 0},
+                           {rbuf, (size_t) count, dtype, inplace, 1}};
+    struct rocm_nb_stage *st = NULL;
+    ompi_amd_request_t *nb = NULL;
+    int path, rc;
+    rc = rocm_nb_begin(m, reduction_ok_n(dtype, op, (size_t) count), dev(sbuf) && dev(rbuf), o, 2,
+                       &st, &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
+        return m->c_coll.coll_iallreduce(sbuf, rbuf, count, dtype, op, comm, request,
+                                         m->c_coll.coll_iallreduce_module);
+    }
+    rc = ompi_amd_iallreduce(m->dev_comm, inplace ? o[1].use : o[0].use, o[1].use,
+                             (size_t) count, type_code(dtype), op->o_f_to_c_index, NULL, &nb);
+    return rocm_nb_post(rc, nb, st, comm, request);
+}
+
 /* MPI_Ireduce_scatter_block / MPI_Iallgather / MPI_Ibcast (coll.h:261-265,
- * 293-296, 319-322): as MPI_Iallreduce — the path is voted per call (the
- * one host rendezvous before the nonblocking post), device buffers only
- * (no staging: a staged copy-back would need a completion hook). */
+ * 293-296, 319-322): as MPI_Iallreduce. */
 int mca_coll_rocm_ireduce_scatter_block(const void *sbuf, void *rbuf, int rcount,
                                         struct ompi_datatype_t *dtype, struct ompi_op_t *op,
                                         struct ompi_communicator_t *comm, ompi_request_t **request,
                                         mca_coll_base_module_t *module)
 {
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const size_t all = (size_t) rcount * (size_t) ompi_comm_size(comm);
+    const int inplace = MPI_IN_PLACE == sbuf;
+    rocm_operand_t o[2] = {{(void *) sbuf, all, dtype, 1, 0},
+                           {rbuf, inplace ? all : (size_t) rcount, dtype, inplace, 1}};
+    struct rocm_nb_stage *st = NULL;
     ompi_amd_request_t *nb = NULL;
-    int rc;
-    if (!take_device_path(m, reduction_ok_n(dtype, op, (size_t) rcount * (size_t) ompi_comm_size(comm)) &&
-                                 dev(sbuf) && dev(rbuf))) {
+    int path, rc;
+    rc = rocm_nb_begin(m, reduction_ok_n(dtype, op, all), dev(sbuf) && dev(rbuf), o, 2, &st, &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
         return m->c_coll.coll_ireduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, request,
                                                     m->c_coll.coll_ireduce_scatter_block_module);
     }
-    rc = ompi_amd_ireduce_scatter_block(m->dev_comm, MPI_IN_PLACE == sbuf ? rbuf : sbuf, rbuf,
+    rc = ompi_amd_ireduce_scatter_block(m->dev_comm, inplace ? o[1].use : o[0].use, o[1].use,
                                         (size_t) rcount, type_code(dtype), op->o_f_to_c_index, NULL,
                                         &nb);
-    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
-    return rocm_wrap_nb(nb, comm, request);
+    return rocm_nb_post(rc, nb, st, comm, request);
 }
 
 int mca_coll_rocm_iallgather(const void *sbuf, int scount, struct ompi_datatype_t *sdtype,
@@ -928,22 +1041,25 @@ int mca_coll_rocm_iallgather(const void *sbuf, int scount, struct ompi_datatype_
 {
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
     const int inplace = MPI_IN_PLACE == sbuf;
+    const size_t all = (size_t) rcount * (size_t) ompi_comm_size(comm);
+    rocm_operand_t o[2] = {{(void *) sbuf, (size_t) scount, sdtype, 1, 0},
+                           {rbuf, all, rdtype, inplace, 1}};
+    struct rocm_nb_stage *st = NULL;
     ompi_amd_request_t *nb = NULL;
     size_t rsize = 0;
-    int rc, ok;
+    int path, rc, ok;
     (void) ompi_datatype_type_size(rdtype, &rsize);
-    ok = bytes_ok(rsize * (size_t) rcount) &&
-         ompi_datatype_is_contiguous_memory_layout(rdtype, rcount * ompi_comm_size(comm)) &&
-         dev(rbuf) && dev(sbuf) &&
+    ok = ompi_datatype_is_contiguous_memory_layout(rdtype, (int) all) && dev(rbuf) && dev(sbuf) &&
          (inplace || ompi_datatype_is_contiguous_memory_layout(sdtype, scount));
-    if (!take_device_path(m, ok)) {
+    rc = rocm_nb_begin(m, bytes_ok(rsize * (size_t) rcount), ok, o, 2, &st, &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
         return m->c_coll.coll_iallgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, request,
                                          m->c_coll.coll_iallgather_module);
     }
-    rc = ompi_amd_iallgather(m->dev_comm, inplace ? (const void *) 1 : sbuf, rbuf,
+    rc = ompi_amd_iallgather(m->dev_comm, inplace ? (const void *) 1 : o[0].use, o[1].use,
                              rsize * (size_t) rcount, NULL, &nb);
-    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
-    return rocm_wrap_nb(nb, comm, request);
+    return rocm_nb_post(rc, nb, st, comm, request);
 }
 
 int mca_coll_rocm_ibcast(void *buf, int count, struct ompi_datatype_t *dtype, int root,
@@ -951,18 +1067,23 @@ int mca_coll_rocm_ibcast(void *buf, int count, struct ompi_datatype_t *dtype, in
                          mca_coll_base_module_t *module)
 {
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const int is_root = ompi_comm_rank(comm) == root;
+    rocm_operand_t o[1] = {{buf, (size_t) count, dtype, is_root, !is_root}};
+    struct rocm_nb_stage *st = NULL;
     ompi_amd_request_t *nb = NULL;
     size_t size = 0;
-    int rc;
+    int path, rc;
     (void) ompi_datatype_type_size(dtype, &size);
-    if (!take_device_path(m, bytes_ok(size * (size_t) count) &&
-                                 ompi_datatype_is_contiguous_memory_layout(dtype, count) && dev(buf))) {
+    rc = rocm_nb_begin(m, bytes_ok(size * (size_t) count),
+                       ompi_datatype_is_contiguous_memory_layout(dtype, count) && dev(buf), o, 1, &st,
+                       &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
         return m->c_coll.coll_ibcast(buf, count, dtype, root, comm, request,
                                      m->c_coll.coll_ibcast_module);
     }
-    rc = ompi_amd_ibcast(m->dev_comm, buf, size * (size_t) count, root, NULL, &nb);
-    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
-    return rocm_wrap_nb(nb, comm, request);
+    rc = ompi_amd_ibcast(m->dev_comm, o[0].use, size * (size_t) count, root, NULL, &nb);
+    return rocm_nb_post(rc, nb, st, comm, request);
 }
 
 /* MPI_Allreduce_init (coll.h:349-352).  Collective: the path decision is
@@ -999,46 +1120,55 @@ int mca_coll_rocm_allreduce_init(const void *sbuf, void *rbuf, int count,
 }
 
 /* MPI_Ireduce / MPI_Iscan / MPI_Iexscan / MPI_Ireduce_scatter (coll.h:
- * 297-326): the per-call vote, then the library posts the call (no handle
- * swap; ompi_amd_ireduce posts the root's in-place choice) and the glue
- * returns a request on the active list; otherwise the saved (libnbc)
- * functions.  MPI_Ireduce's rbuf matters at the root only. */
+ * 297-326): rocm_nb_begin, then the library posts the call (no handle
+ * swap; ompi_amd_ireduce posts the root's in-place choice); otherwise the
+ * saved (libnbc) functions.  MPI_Ireduce's rbuf matters at the root only. */
 int mca_coll_rocm_ireduce(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
                           struct ompi_op_t *op, int root, struct ompi_communicator_t *comm,
                           ompi_request_t **request, mca_coll_base_module_t *module)
 {
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
     const int is_root = ompi_comm_rank(comm) == root;
+    rocm_operand_t o[2] = {{(void *) sbuf, (size_t) count, dtype, 1, 0},
+                           {is_root ? rbuf : NULL, (size_t) count, dtype, MPI_IN_PLACE == sbuf, 1}};
+    struct rocm_nb_stage *st = NULL;
     ompi_amd_request_t *nb = NULL;
-    int rc;
-    if (!take_device_path(m, reduction_ok_n(dtype, op, (size_t) count) &&
-                                 (is_root ? dev(rbuf) && dev(sbuf) : ompi_amd_is_device_pointer(sbuf)))) {
+    int path, rc;
+    rc = rocm_nb_begin(m, reduction_ok_n(dtype, op, (size_t) count),
+                       is_root ? dev(rbuf) && dev(sbuf) : ompi_amd_is_device_pointer(sbuf), o, 2,
+                       &st, &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
         return m->c_coll.coll_ireduce(sbuf, rbuf, count, dtype, op, root, comm, request,
                                       m->c_coll.coll_ireduce_module);
     }
-    rc = ompi_amd_ireduce(m->dev_comm, sbuf, is_root ? rbuf : NULL, (size_t) count, type_code(dtype),
-                          op->o_f_to_c_index, root, NULL, &nb);
-    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
-    return rocm_wrap_nb(nb, comm, request);
+    rc = ompi_amd_ireduce(m->dev_comm, o[0].use, is_root ? o[1].use : NULL, (size_t) count,
+                          type_code(dtype), op->o_f_to_c_index, root, NULL, &nb);
+    return rocm_nb_post(rc, nb, st, comm, request);
 }
 
 static int rocm_iscan_common(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
                              struct ompi_op_t *op, struct ompi_communicator_t *comm,
                              ompi_request_t **request, mca_coll_rocm_module_t *m, int exclusive)
 {
+    rocm_operand_t o[2] = {{(void *) sbuf, (size_t) count, dtype, 1, 0},
+                           {rbuf, (size_t) count, dtype, MPI_IN_PLACE == sbuf, 1}};
+    struct rocm_nb_stage *st = NULL;
     ompi_amd_request_t *nb = NULL;
-    int rc;
-    if (!take_device_path(m, reduction_ok_n(dtype, op, (size_t) count) && dev(sbuf) && dev(rbuf))) {
+    int path, rc;
+    rc = rocm_nb_begin(m, reduction_ok_n(dtype, op, (size_t) count), dev(sbuf) && dev(rbuf), o, 2,
+                       &st, &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
         return exclusive ? m->c_coll.coll_iexscan(sbuf, rbuf, count, dtype, op, comm, request,
                                                   m->c_coll.coll_iexscan_module)
                          : m->c_coll.coll_iscan(sbuf, rbuf, count, dtype, op, comm, request,
                                                 m->c_coll.coll_iscan_module);
     }
-    rc = (exclusive ? ompi_amd_iexscan : ompi_amd_iscan)(m->dev_comm, sbuf, rbuf, (size_t) count,
-                                                         type_code(dtype), op->o_f_to_c_index, NULL,
-                                                         &nb);
-    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
-    return rocm_wrap_nb(nb, comm, request);
+    rc = (exclusive ? ompi_amd_iexscan : ompi_amd_iscan)(m->dev_comm, o[0].use, o[1].use,
+                                                         (size_t) count, type_code(dtype),
+                                                         op->o_f_to_c_index, NULL, &nb);
+    return rocm_nb_post(rc, nb, st, comm, request);
 }
 
 int mca_coll_rocm_iscan(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
@@ -1063,20 +1193,28 @@ int mca_coll_rocm_ireduce_scatter(const void *sbuf, void *rbuf, const int *rcoun
                                   mca_coll_base_module_t *module)
 {
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
-    const int n = ompi_comm_size(comm);
+    const int n = ompi_comm_size(comm), inplace = MPI_IN_PLACE == sbuf;
     size_t counts[OMPI_AMD_MAX_RANKS], total = 0;
+    struct rocm_nb_stage *st = NULL;
     ompi_amd_request_t *nb = NULL;
-    int rc, i;
+    int path, rc, i;
     for (i = 0; i < n; ++i) total += (size_t) rcounts[i];
-    if (!take_device_path(m, reduction_ok_n(dtype, op, total) && dev(sbuf) && dev(rbuf))) {
-        return m->c_coll.coll_ireduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, request,
-                                              m->c_coll.coll_ireduce_scatter_module);
+    {
+        rocm_operand_t o[2] = {{(void *) sbuf, total, dtype, 1, 0},
+                               {rbuf, inplace ? total : (size_t) rcounts[ompi_comm_rank(comm)],
+                                dtype, inplace, 1}};
+        rc = rocm_nb_begin(m, reduction_ok_n(dtype, op, total), dev(sbuf) && dev(rbuf), o, 2, &st,
+                           &path);
+        if (OMPI_SUCCESS != rc) return rc;
+        if (ROCM_DEVICE != path) {
+            return m->c_coll.coll_ireduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, request,
+                                                  m->c_coll.coll_ireduce_scatter_module);
+        }
+        for (i = 0; i < n; ++i) counts[i] = (size_t) rcounts[i];
+        rc = ompi_amd_ireduce_scatter(m->dev_comm, inplace ? o[1].use : o[0].use, o[1].use, counts,
+                                      type_code(dtype), op->o_f_to_c_index, NULL, &nb);
+        return rocm_nb_post(rc, nb, st, comm, request);
     }
-    for (i = 0; i < n; ++i) counts[i] = (size_t) rcounts[i];
-    rc = ompi_amd_ireduce_scatter(m->dev_comm, sbuf, rbuf, counts, type_code(dtype),
-                                  op->o_f_to_c_index, NULL, &nb);
-    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
-    return rocm_wrap_nb(nb, comm, request);
 }
 
 /* MPI_Reduce_scatter_block_init / MPI_Allgather_init / MPI_Bcast_init

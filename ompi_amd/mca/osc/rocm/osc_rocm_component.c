@@ -9,7 +9,9 @@
  * wait are kernels that wait for the peers' counters, so MPI's blocking
  * calls return once the stream got there (complete and wait synchronise).
  * Request-based RMA completes its request from the opal_progress callback
- * once the call's kernels have run.  Predefined datatypes with equal origin and
+ * once the call's kernels have run.  MPI_Win_allocate_shared windows keep
+ * every rank's segment in one device allocation that all ranks map
+ * (MPI_Win_shared_query hands out the addresses).  Predefined datatypes with equal origin and
  * target signatures; everything else returns OMPI_ERR_NOT_SUPPORTED, as
  * osc/sm rejects what it cannot do.  Blocking MPI semantics come from the
  * stream synchronisation in fence / unlock / flush (ompi_amd_comm_sync,
@@ -396,9 +398,10 @@ static void rma_request_construct(ompi_osc_rocm_request_t *r)
 OBJ_CLASS_INSTANCE(ompi_osc_rocm_request_t, ompi_request_t, rma_request_construct, NULL);
 
 /* an MPI request over the library request of a call that returned rc */
-static int rma_wrap(int rc, ompi_amd_rma_request_t *rma, struct ompi_win_t *win,
+static int rma_wrap(int rc, ompi_amd_rma_request_t *const *rmap, struct ompi_win_t *win,
                     ompi_request_t **request)
 {
+    ompi_amd_rma_request_t *rma = *rmap;  /* read after the call that set it */
     ompi_osc_rocm_request_t *r;
     if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
     r = OBJ_NEW(ompi_osc_rocm_request_t);
@@ -433,7 +436,7 @@ static int rocm_rput(const void *origin, int ocount, struct ompi_datatype_t *odt
     if (0 != ocount && (0 == bytes || bytes != span(tdt, tcount) || disp < 0))
         return OMPI_ERR_NOT_SUPPORTED;
     return rma_wrap(ompi_amd_rput(mod(win)->dev_win, origin, bytes, target, (size_t) disp, NULL,
-                                  &rma), rma, win, request);
+                                  &rma), &rma, win, request);
 }
 
 static int rocm_rget(void *origin, int ocount, struct ompi_datatype_t *odt, int target,
@@ -445,7 +448,7 @@ static int rocm_rget(void *origin, int ocount, struct ompi_datatype_t *odt, int 
     if (0 != ocount && (0 == bytes || bytes != span(tdt, tcount) || disp < 0))
         return OMPI_ERR_NOT_SUPPORTED;
     return rma_wrap(ompi_amd_rget(mod(win)->dev_win, origin, bytes, target, (size_t) disp, NULL,
-                                  &rma), rma, win, request);
+                                  &rma), &rma, win, request);
 }
 
 static int rocm_raccumulate(const void *origin, int ocount, struct ompi_datatype_t *odt,
@@ -457,7 +460,7 @@ static int rocm_raccumulate(const void *origin, int ocount, struct ompi_datatype
         return OMPI_ERR_NOT_SUPPORTED;
     return rma_wrap(ompi_amd_raccumulate(mod(win)->dev_win, origin, (size_t) ocount,
                                          0 != ocount ? type_code(tdt) : 0, target, (size_t) disp,
-                                         op->o_f_to_c_index, NULL, &rma), rma, win, request);
+                                         op->o_f_to_c_index, NULL, &rma), &rma, win, request);
 }
 
 static int rocm_rget_accumulate(const void *origin, int ocount, struct ompi_datatype_t *odt,
@@ -474,20 +477,29 @@ static int rocm_rget_accumulate(const void *origin, int ocount, struct ompi_data
     return rma_wrap(ompi_amd_rget_accumulate(mod(win)->dev_win, no_op ? NULL : origin, result,
                                              (size_t) tcount, 0 != tcount ? type_code(tdt) : 0,
                                              target, (size_t) disp, op->o_f_to_c_index, NULL,
-                                             &rma), rma, win, request);
+                                             &rma), &rma, win, request);
 }
 
-/* dynamic and shared windows: not provided (selection leaves those flavors
- * to osc/sm and osc/rdma, rocm_query) */
-static int ns_shared_query(struct ompi_win_t *w, int r, size_t *s, int *d, void *b)
-{ return OMPI_ERR_NOT_SUPPORTED; }
-static int ns_attach(struct ompi_win_t *w, void *b, size_t s) { return OMPI_ERR_NOT_SUPPORTED; }
-static int ns_detach(struct ompi_win_t *w, const void *b) { return OMPI_ERR_NOT_SUPPORTED; }
+/* MPI_Win_shared_query (osc_sm_component.c:455-485): baseptr points to a
+ * void *; MPI_PROC_NULL asks for the first segment of nonzero size */
+static int rocm_shared_query(struct ompi_win_t *win, int rank, size_t *size, int *disp_unit,
+                             void *baseptr)
+{
+    const int rc = ompi_amd_win_shared_query(mod(win)->dev_win, MPI_PROC_NULL == rank ? -1 : rank,
+                                             size, disp_unit, (void **) baseptr);
+    return OMPI_AMD_ERR_UNSUPPORTED == rc ? MPI_ERR_WIN : to_ompi_err(rc);
+}
+
+/* MPI_Win_attach / MPI_Win_detach: this component makes no dynamic windows
+ * (rocm_query leaves that flavor to osc/rdma), so as osc/sm for its own
+ * flavors (osc_sm_component.c:488-511) */
+static int rocm_attach(struct ompi_win_t *w, void *b, size_t s) { return MPI_ERR_RMA_ATTACH; }
+static int rocm_detach(struct ompi_win_t *w, const void *b) { return MPI_ERR_RMA_ATTACH; }
 
 static const ompi_osc_base_module_t rocm_module_template = {
-    .osc_win_shared_query = ns_shared_query,
-    .osc_win_attach = ns_attach,
-    .osc_win_detach = ns_detach,
+    .osc_win_shared_query = rocm_shared_query,
+    .osc_win_attach = rocm_attach,
+    .osc_win_detach = rocm_detach,
     .osc_free = rocm_free,
     .osc_put = rocm_put,
     .osc_get = rocm_get,
@@ -530,11 +542,11 @@ static int rocm_query(struct ompi_win_t *win, void **base, size_t size, int disp
     if (MPI_WIN_FLAVOR_CREATE == flavor)
         return (0 == size || 1 == ompi_amd_is_device_pointer(*base)) ? mca_osc_rocm_component.priority
                                                                       : -1;
-    if (MPI_WIN_FLAVOR_ALLOCATE == flavor) {
+    if (MPI_WIN_FLAVOR_ALLOCATE == flavor || MPI_WIN_FLAVOR_SHARED == flavor) {
         (void) opal_info_get_bool(info, "ompi_amd_device", &dev, &flag);
         return (flag && dev) ? mca_osc_rocm_component.priority : -1;
     }
-    return -1;  /* dynamic / shared windows stay with osc/sm, osc/rdma */
+    return -1;  /* dynamic windows stay with osc/rdma */
 }
 
 static int rocm_select(struct ompi_win_t *win, void **base, size_t size, int disp_unit,
@@ -559,11 +571,19 @@ static int rocm_select(struct ompi_win_t *win, void **base, size_t size, int dis
     }
     (void) ompi_amd_comm_set_param(m->dev_comm, "timeout_ms", mca_osc_rocm_component.timeout_ms);
     /* residency may differ between ranks (query is local): decide together */
-    local_ok = MPI_WIN_FLAVOR_ALLOCATE == flavor || 0 == size ||
+    local_ok = MPI_WIN_FLAVOR_CREATE != flavor || 0 == size ||
                1 == ompi_amd_is_device_pointer(*base);
     rc = ompi_amd_comm_agree(m->dev_comm, local_ok, &all_ok);
     if (OMPI_AMD_SUCCESS == rc && !all_ok) rc = OMPI_AMD_ERR_UNSUPPORTED;
-    if (OMPI_AMD_SUCCESS == rc) {
+    if (OMPI_AMD_SUCCESS == rc && MPI_WIN_FLAVOR_SHARED == flavor) {
+        /* one allocation, segments back to back unless alloc_shared_noncontig
+         * (osc_sm_component.c:259-268) */
+        bool noncontig = false;
+        int nflag = 0;
+        (void) opal_info_get_bool(info, "alloc_shared_noncontig", &noncontig, &nflag);
+        rc = ompi_amd_win_allocate_shared(m->dev_comm, size, disp_unit, nflag && noncontig, base,
+                                          &m->dev_win);
+    } else if (OMPI_AMD_SUCCESS == rc) {
         rc = MPI_WIN_FLAVOR_ALLOCATE == flavor
                  ? ompi_amd_win_allocate(m->dev_comm, size, disp_unit, base, &m->dev_win)
                  : ompi_amd_win_create(m->dev_comm, *base, size, disp_unit, &m->dev_win);

@@ -9,6 +9,7 @@ osc_sm_active_target.c, osc_sm_passive_target.c):
     get_accumulate                 osc_sm_comm.c:312-360
     compare_and_swap               osc_sm_comm.c:363-400
     fetch_and_op                   osc_sm_comm.c:403-441
+    allocate_shared / shared_query osc_sm_component.c:244-360, 455-485
     fence                          osc_sm_active_target.c:95-115
     post / start / complete / wait / test
                                    osc_sm_active_target.c:126-335
@@ -49,6 +50,27 @@ class RmaRequest:
 
     def wait(self) -> None:
         _lib.check(self._lib.ompi_amd_rma_wait(self._h), "rma_wait")
+
+    @classmethod
+    def allocate_shared(cls, comm: Communicator, nbytes: int, disp_unit: int = 1,
+                        noncontig: bool = False) -> "Window":
+        """MPI_Win_allocate_shared (collective): every rank's segment in one
+        device allocation of rank 0, contiguous in every process unless
+        `noncontig`; `base_ptr` is this rank's segment."""
+        h, b = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(comm._lib.ompi_amd_win_allocate_shared(comm._h, nbytes, disp_unit,
+                                                          int(noncontig), ctypes.byref(b),
+                                                          ctypes.byref(h)), "win_allocate_shared")
+        return cls(comm, h, b.value or 0, nbytes)
+
+    def shared_query(self, rank: int):
+        """MPI_Win_shared_query: (size, disp_unit, address in this process)
+        of `rank`'s segment; rank < 0 (MPI_PROC_NULL) = the first nonzero one."""
+        size, du, base = ctypes.c_size_t(), ctypes.c_int(), ctypes.c_void_p()
+        _lib.check(self._lib.ompi_amd_win_shared_query(self._h, rank, ctypes.byref(size),
+                                                       ctypes.byref(du), ctypes.byref(base)),
+                   "win_shared_query")
+        return size.value, du.value, base.value or 0
 
     def free(self) -> None:
         if self._h:

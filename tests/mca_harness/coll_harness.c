@@ -490,6 +490,38 @@ int main(int argc, char **argv)
         CHECK(table.coll_reduce(h, g_rank == 0 ? h2 : NULL, (int) n, &dfloat, &sum, 0, &comm,
                                 table.coll_reduce_module) == OMPI_SUCCESS && tuned_calls == 5,
               "host reduce falls back");
+        /* past coll_rocm_max_device_mib (here lowered to 1 MiB): device
+         * buffers of every size-capped slot go to the saved functions on
+         * every rank alike (count, datatype and root agree) */
+        {
+            const int saved_mib = mca_coll_rocm_component.max_device_mib;
+            const size_t big = (1u << 20) + 64;
+            void *b1 = NULL, *b2 = NULL;
+            ompi_request_t *rq = NULL;
+            unsigned char *zero = calloc(big * (size_t) g_size, 1);
+            b1 = dev_of(zero, big);
+            b2 = dev_of(zero, big * (size_t) g_size);
+            free(zero);
+            mca_coll_rocm_component.max_device_mib = 1;
+            tuned_calls = 0;
+            CHECK(table.coll_allreduce(b1, b2, (int) (big / 4), &dfloat, &sum, &comm,
+                                       table.coll_allreduce_module) == OMPI_SUCCESS &&
+                      tuned_calls == 1, "allreduce past the cap");
+            CHECK(table.coll_bcast(b1, (int) big, &dbyte, 0, &comm, table.coll_bcast_module) ==
+                      OMPI_SUCCESS && tuned_calls == 2, "bcast past the cap");
+            CHECK(table.coll_allgather(b1, (int) big, &dbyte, b2, (int) big, &dbyte, &comm,
+                                       table.coll_allgather_module) == OMPI_SUCCESS &&
+                      tuned_calls == 3, "allgather past the cap");
+            CHECK(table.coll_ibcast(b1, (int) big, &dbyte, 0, &comm, &rq,
+                                    table.coll_ibcast_module) == OMPI_SUCCESS &&
+                      tuned_calls == 4 && rq == &t_request, "ibcast past the cap");
+            CHECK(table.coll_iallgather(b1, (int) big, &dbyte, b2, (int) big, &dbyte, &comm, &rq,
+                                        table.coll_iallgather_module) == OMPI_SUCCESS &&
+                      tuned_calls == 5 && rq == &t_request, "iallgather past the cap");
+            mca_coll_rocm_component.max_device_mib = saved_mib;
+            harness_dev_free(b1);
+            harness_dev_free(b2);
+        }
         harness_dev_free(d);
         harness_dev_free(d2);
         free(h);
@@ -941,6 +973,63 @@ int main(int argc, char **argv)
             free(mine);
             free(all);
             free(t);
+        }
+        /* (h) nonblocking calls under the DEVICE lock: no vote (zero
+         * bootstrap calls); rank 0's host buffers go into its request's own
+         * device memory and its output comes back when the request
+         * completes (from opal_progress), counted as a mismatch for the
+         * next recheck */
+        {
+            ompi_request_t *rq = NULL;
+            const int mism0 = rm->mismatched;
+            BOOT(b0);
+            CHECK(table.coll_iallreduce(d, d2, (int) n, &dfloat, &sum, &comm, &rq,
+                                        table.coll_iallreduce_module) == OMPI_SUCCESS,
+                  "locked iallreduce");
+            harness_wait(rq);
+            CHECK(rq->req_status.MPI_ERROR == OMPI_SUCCESS && rq->req_free(&rq) == OMPI_SUCCESS,
+                  "locked iallreduce completes");
+            BOOT(b1);
+            CHECK(b1 == b0 && tuned_calls == 0, "locked nonblocking call: %lld bootstrap calls",
+                  (long long) (b1 - b0));
+            expect_dev(d2, rb[g_rank], n * 4, "locked iallreduce");
+            memset(h2, 0, n * 4);
+            BOOT(b0);
+            CHECK(table.coll_iallreduce(g_rank == 0 ? (void *) h : d, g_rank == 0 ? (void *) h2 : d2,
+                                        (int) n, &dfloat, &sum, &comm, &rq,
+                                        table.coll_iallreduce_module) == OMPI_SUCCESS,
+                  "staged iallreduce");
+            harness_wait(rq);
+            CHECK(rq->req_status.MPI_ERROR == OMPI_SUCCESS && rq->req_free(&rq) == OMPI_SUCCESS,
+                  "staged iallreduce completes");
+            BOOT(b1);
+            CHECK(b1 == b0 && tuned_calls == 0, "staged nonblocking call: %lld bootstrap calls",
+                  (long long) (b1 - b0));
+            if (g_rank == 0) {
+                CHECK(memcmp(h2, rb[0], n * 4) == 0, "host rbuf after nonblocking staging");
+                CHECK(rm->mismatched == mism0 + 1, "the staged call counts as a mismatch");
+            } else {
+                expect_dev(d2, rb[g_rank], n * 4, "iallreduce beside a staging rank");
+            }
+            /* MPI_Ibcast from the last rank, whose buffer is host memory */
+            {
+                const int root = g_size - 1;
+                unsigned char *hb = malloc(777), *want = malloc(777);
+                void *db;
+                for (int k = 0; k < 777; ++k) want[k] = (unsigned char) (k * 7 + 3);
+                memcpy(hb, g_rank == root ? want : (unsigned char *) h, 777);
+                db = dev_of(hb, 777);
+                CHECK(table.coll_ibcast(g_rank == root ? (void *) hb : db, 777, &dbyte, root, &comm,
+                                        &rq, table.coll_ibcast_module) == OMPI_SUCCESS, "ibcast");
+                harness_wait(rq);
+                CHECK(rq->req_status.MPI_ERROR == OMPI_SUCCESS && rq->req_free(&rq) == OMPI_SUCCESS,
+                      "ibcast completes");
+                CHECK(tuned_calls == 0, "staged ibcast stayed on the device path");
+                if (g_rank != root) expect_dev(db, want, 777, "ibcast from a host-buffer root");
+                harness_dev_free(db);
+                free(hb);
+                free(want);
+            }
         }
 #undef BOOT
         harness_dev_free(d);

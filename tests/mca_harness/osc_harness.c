@@ -62,7 +62,7 @@ int main(int argc, char **argv)
     ompi_communicator_t comm;
     ompi_datatype_t dfloat = {ORC_T_FLOAT, 4, 1, 1}, dint64 = {ORC_T_INT64, 8, 1, 1};
     ompi_op_t sum = {OMPI_OP_FLAGS_INTRINSIC, ORC_OP_SUM}, user = {0, ORC_OP_SUM};
-    opal_info_t dev_info = {"ompi_amd_device", "true"};
+    opal_info_t dev_info = {"ompi_amd_device", "true", NULL};
     ompi_osc_base_component_t *c = &mca_osc_rocm_component.super;
     int i;
 
@@ -95,6 +95,8 @@ int main(int argc, char **argv)
               "remote peers");
         CHECK(c->osc_query(&w, &hb, 0, 4, &comm, &dev_info, MPI_WIN_FLAVOR_DYNAMIC) < 0,
               "dynamic windows");
+        CHECK(c->osc_query(&w, &hb, 0, 4, &comm, NULL, MPI_WIN_FLAVOR_SHARED) < 0,
+              "shared without the device info key");
     }
     if (!use_gpu) {
         printf("ok\n");
@@ -195,7 +197,7 @@ int main(int argc, char **argv)
             } else {
                 do {
                     CHECK(m->osc_test(&win, &flag) == OMPI_SUCCESS, "test");
-                } while (!flag && ++spins < 100000000L);
+                } while (!flag && ++spins < 2000000L);
                 CHECK(flag, "MPI_Win_test never completed");
             }
             CHECK(harness_dev_copy_back(got, dbase, k * 4) == 0, "copy back");
@@ -256,6 +258,50 @@ int main(int argc, char **argv)
         free(mine);
         free(theirs);
         free(fetched);
+    }
+
+    /* MPI_Win_allocate_shared: segments of (rank + 1) * 1000 floats back to
+     * back in one device allocation; each rank fills its own, reads every
+     * peer's through MPI_Win_shared_query's address */
+    {
+        opal_info_t contig = {"alloc_shared_noncontig", "false", NULL};
+        opal_info_t sinfo = {"ompi_amd_device", "true", &contig};
+        ompi_win_t swin = {0};
+        void *sbase = NULL, *qbase = NULL, *prev_end = NULL;
+        const size_t mine_n = 1000 * (size_t)(g_rank + 1);
+        float *buf = malloc(1000 * (size_t) g_size * 4), *ref = malloc(1000 * (size_t) g_size * 4);
+        size_t qsize = 0;
+        int qdu = 0, p;
+        CHECK(c->osc_query(&swin, &sbase, mine_n * 4, 4, &comm, &sinfo, MPI_WIN_FLAVOR_SHARED) ==
+                  101, "query shared with the device info key");
+        CHECK(c->osc_select(&swin, &sbase, mine_n * 4, 4, &comm, &sinfo, MPI_WIN_FLAVOR_SHARED,
+                            &model) == OMPI_SUCCESS && swin.w_osc_module && sbase,
+              "select shared");
+        ompi_osc_base_module_t *sm = swin.w_osc_module;
+        fill_exact(buf, mine_n, g_rank, 30);
+        CHECK(harness_dev_copy_in(sbase, buf, mine_n * 4) == 0, "own segment");
+        CHECK(sm->osc_fence(0, &swin) == OMPI_SUCCESS, "shared fence");
+        for (p = 0; p < g_size; ++p) {
+            CHECK(sm->osc_win_shared_query(&swin, p, &qsize, &qdu, &qbase) == OMPI_SUCCESS,
+                  "shared_query %d", p);
+            CHECK(qsize == 1000 * (size_t)(p + 1) * 4 && qdu == 4, "segment %d size %zu", p, qsize);
+            CHECK(p != g_rank || qbase == sbase, "own segment address");
+            CHECK(p == 0 || qbase == prev_end, "segment %d not contiguous", p);
+            prev_end = (char *) qbase + qsize;
+            CHECK(harness_dev_copy_back(buf, qbase, qsize) == 0, "read segment %d", p);
+            fill_exact(ref, qsize / 4, p, 30);
+            CHECK(0 == memcmp(buf, ref, qsize), "segment %d bytes", p);
+        }
+        CHECK(sm->osc_win_shared_query(&swin, MPI_PROC_NULL, &qsize, &qdu, &qbase) == OMPI_SUCCESS &&
+                  qsize == 4000 && qdu == 4, "MPI_PROC_NULL query");
+        CHECK(m->osc_win_shared_query(&win, 0, &qsize, &qdu, &qbase) == MPI_ERR_WIN,
+              "shared_query on an MPI_Win_create window");
+        CHECK(m->osc_win_attach(&win, dorg, 64) == MPI_ERR_RMA_ATTACH &&
+                  m->osc_win_detach(&win, dorg) == MPI_ERR_RMA_ATTACH, "attach / detach refused");
+        CHECK(sm->osc_fence(0, &swin) == OMPI_SUCCESS, "shared fence 2");
+        CHECK(sm->osc_free(&swin) == OMPI_SUCCESS, "free shared");
+        free(buf);
+        free(ref);
     }
 
     /* MPI_Win_allocate: a shared counter, fetch_and_op from every rank */

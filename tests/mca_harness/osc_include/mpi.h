@@ -1,5 +1,5 @@
 /* TEST HARNESS ONLY: the mpi.h constants the osc glue uses
- * (ompi/include/mpi.h.in:542-557). */
+ * (ompi/include/mpi.h.in:542-557, 640, 656). */
 #ifndef HARNESS_MPI_H
 #define HARNESS_MPI_H
 #define MPI_IN_PLACE ((void *) 1)
@@ -12,4 +12,7 @@
 #define MPI_WIN_FLAVOR_DYNAMIC 3
 #define MPI_WIN_FLAVOR_SHARED 4
 #define MPI_WIN_UNIFIED 0
+#define MPI_PROC_NULL (-2)
+#define MPI_ERR_WIN 53
+#define MPI_ERR_RMA_ATTACH 69
 #endif

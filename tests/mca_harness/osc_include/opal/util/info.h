@@ -3,15 +3,19 @@
 #ifndef HARNESS_OPAL_INFO_H
 #define HARNESS_OPAL_INFO_H
 #include <stdbool.h>
+#include <stddef.h>
 #include <string.h>
 typedef struct opal_info_t {
-    const char *key;   /* one entry is enough for the harness */
+    const char *key;
     const char *value;
+    const struct opal_info_t *next;  /* further entries (NULL: none) */
 } opal_info_t;
 static inline int opal_info_get_bool(opal_info_t *info, const char *key, bool *value, int *flag)
 {
-    *flag = info && info->key && 0 == strcmp(info->key, key);
-    if (*flag) *value = 0 == strcmp(info->value, "true") || 0 == strcmp(info->value, "1");
+    const opal_info_t *e = info;
+    while (e && !(e->key && 0 == strcmp(e->key, key))) e = e->next;
+    *flag = NULL != e;
+    if (*flag) *value = 0 == strcmp(e->value, "true") || 0 == strcmp(e->value, "1");
     return 0;
 }
 #endif

@@ -660,6 +660,77 @@ def case_request_rma(comm, rank, n, salt, count=65537):
         win.free()
 
 
+def case_shared_window(comm, rank, n, salt, noncontig=False):
+    """MPI_Win_allocate_shared (osc_sm_component.c:244-360): segments of
+    different sizes (one empty), each written by its owner with plain
+    device copies and read by every rank through MPI_Win_shared_query's
+    address; contiguous unless noncontig; MPI_PROC_NULL = the first
+    nonzero segment; put into a shared window; shared_query on a window of
+    another flavor is refused."""
+    lib = _lib.load()
+    sizes = [0 if (n > 2 and r == 1) else 1000 * (r + 1) + 3 * (r % 2) for r in range(n)]
+    seg = [((z + 4095) // 4096 * 4096 if noncontig else z) for z in sizes]
+    win = osc.Window.allocate_shared(comm, sizes[rank], disp_unit=1, noncontig=noncontig)
+    try:
+        mine = payload(rank, salt, sizes[rank])
+        if sizes[rank]:
+            _lib.check(lib.ompi_amd_memcpy(win.base_ptr, mine.ctypes.data, sizes[rank]), "memcpy")
+        comm_barrier()
+        addrs = []
+        for p in range(n):
+            size, du, addr = win.shared_query(p)
+            if size != seg[p] or du != 1:
+                return False, f"rank {p}: size {size} disp {du}, expected {seg[p]} / 1"
+            if p == rank and addr != win.base_ptr:
+                return False, "own segment address differs from the allocation's base"
+            addrs.append(addr)
+            if sizes[p]:
+                got = np.empty(sizes[p], np.uint8)
+                _lib.check(lib.ompi_amd_memcpy(got.ctypes.data, addr, sizes[p]), "memcpy back")
+                ok, msg = eq(got, payload(p, salt, sizes[p]), f"segment {p}")
+                if not ok:
+                    return ok, msg
+        for p in range(n - 1):
+            if addrs[p + 1] != addrs[p] + seg[p]:
+                return False, f"segments {p}, {p + 1} not back to back"
+        first = next(p for p in range(n) if sizes[p])
+        if win.shared_query(-1) != (seg[first], 1, addrs[first]):
+            return False, f"MPI_PROC_NULL query {win.shared_query(-1)}"
+        # RMA into the shared window: put into the next nonempty segment
+        tgt = next(p for p in [(rank + k) % n for k in range(1, n + 1)] if sizes[p])
+        src_rank = [r for r in range(n) if next(p for p in [(r + k) % n for k in range(1, n + 1)]
+                                                 if sizes[p]) == rank]
+        m = min(sizes[tgt], 512)
+        src = dev(payload(rank, salt + 1, m))
+        win.fence(stream=STREAM)
+        if m:
+            win.put(src, tgt, 0, m, stream=STREAM)
+        win.fence(stream=STREAM, blocking=True)
+        if sizes[rank] and src_rank:
+            got = np.empty(sizes[rank], np.uint8)
+            _lib.check(lib.ompi_amd_memcpy(got.ctypes.data, win.base_ptr, sizes[rank]), "memcpy")
+            w = max(src_rank)  # several writers: the last fence orders nothing among them
+            if len(src_rank) == 1:
+                mm = min(sizes[rank], 512)
+                exp = mine.copy()
+                exp[:mm] = payload(w, salt + 1, mm)
+                ok, msg = eq(got, exp, "put into the shared window")
+                if not ok:
+                    return ok, msg
+        other = osc.Window.allocate(comm, 64, disp_unit=1)
+        try:
+            other.shared_query(0)
+            return False, "shared_query on an MPI_Win_allocate window accepted"
+        except _lib.OmpiAmdError as e:
+            if e.code != _lib.ERR_UNSUPPORTED:
+                return False, f"shared_query on another flavor: code {e.code}"
+        finally:
+            other.free()
+        return True, ""
+    finally:
+        win.free()
+
+
 def comm_barrier():
     STREAM.synchronize()
     dist.barrier()
@@ -718,6 +789,8 @@ def main():
         ("osc_pscw_all_to_one_acc", lambda: case_pscw_all_to_one(comm, rank, n, 96)),
         ("osc_pscw_errors", lambda: case_pscw_errors(comm, rank, n)),
         ("osc_request_rma", lambda: case_request_rma(comm, rank, n, 97)),
+        ("osc_shared_window", lambda: case_shared_window(comm, rank, n, 98)),
+        ("osc_shared_window_noncontig", lambda: case_shared_window(comm, rank, n, 99, noncontig=True)),
     ]
     only = os.environ.get("P2P_OSC_ONLY")
     all_ok = True
