@@ -396,6 +396,7 @@ typedef struct {
     ptrdiff_t gap;  /* true lower bound of the span */
     size_t bytes;
     char *hbuf;     /* packed: the host side of the pack / unpack */
+    int contig;
 } rocm_operand_t;
 
 /* Staging memory of one operand slot: the module's grow-only buffers for
@@ -435,6 +436,25 @@ static char *stage_buf(void *ctx, int slot, int on_dev, size_t bytes)
 /* Put every operand where the chosen path runs: device memory (packed when
  * its layout is not contiguous, since the device path moves bytes) or host
  * memory (the typed span as it is, for the saved function). */
+/* the caller's input into a staged operand (again at every persistent start) */
+static int stage_copy_in(const rocm_operand_t *x)
+{
+    if (2 == x->how) {
+        if (x->in && (MPI_SUCCESS != ompi_datatype_sndrcv(x->user, (int) x->count, x->dtype,
+                                                          x->hbuf, (int) x->bytes, MPI_BYTE) ||
+                      OMPI_AMD_SUCCESS != ompi_amd_memcpy(x->use, x->hbuf, x->bytes))) {
+            return OMPI_ERROR;
+        }
+    } else if (1 == x->how && (x->in || (x->out && !x->contig))) {
+        /* an output's gaps must survive the copy back */
+        if (OMPI_AMD_SUCCESS != ompi_amd_memcpy((char *) x->use + x->gap,
+                                                (char *) x->user + x->gap, x->bytes)) {
+            return OMPI_ERROR;
+        }
+    }
+    return OMPI_SUCCESS;
+}
+
 static int rocm_stage_with(rocm_buf_fn get, void *ctx, rocm_operand_t *o, int n, int to_dev)
 {
     for (int i = 0; i < n; ++i) {
@@ -447,23 +467,14 @@ static int rocm_stage_with(rocm_buf_fn get, void *ctx, rocm_operand_t *o, int n,
         is_dev = ompi_amd_is_device_pointer(x->user);
         contig = ompi_datatype_is_contiguous_memory_layout(x->dtype, (int) x->count);
         if (to_dev ? (is_dev && contig) : !is_dev) continue;
+        x->contig = contig;
         if (to_dev && !contig) {
             size_t size = 0;
-            char *h, *d;
             (void) ompi_datatype_type_size(x->dtype, &size);
             x->bytes = size * x->count;
-            h = get(ctx, i, 0, x->bytes);
-            d = get(ctx, i, 1, x->bytes);
-            if (NULL == h || NULL == d) return OMPI_ERR_OUT_OF_RESOURCE;
-            if (x->in) {
-                if (MPI_SUCCESS != ompi_datatype_sndrcv(x->user, (int) x->count, x->dtype, h,
-                                                        (int) x->bytes, MPI_BYTE) ||
-                    OMPI_AMD_SUCCESS != ompi_amd_memcpy(d, h, x->bytes)) {
-                    return OMPI_ERROR;
-                }
-            }
-            x->use = d;
-            x->hbuf = h;
+            x->hbuf = get(ctx, i, 0, x->bytes);
+            x->use = get(ctx, i, 1, x->bytes);
+            if (NULL == x->hbuf || NULL == x->use) return OMPI_ERR_OUT_OF_RESOURCE;
             x->how = 2;
         } else {
             ptrdiff_t lb, ext, tlb, text;
@@ -474,14 +485,10 @@ static int rocm_stage_with(rocm_buf_fn get, void *ctx, rocm_operand_t *o, int n,
             x->gap = tlb;
             b = get(ctx, i, to_dev, x->bytes);
             if (NULL == b) return OMPI_ERR_OUT_OF_RESOURCE;
-            /* an output's gaps must survive the copy back */
-            if ((x->in || (x->out && !contig)) &&
-                OMPI_AMD_SUCCESS != ompi_amd_memcpy(b, (char *) x->user + tlb, x->bytes)) {
-                return OMPI_ERROR;
-            }
             x->use = b - tlb;
             x->how = 1;
         }
+        if (OMPI_SUCCESS != stage_copy_in(x)) return OMPI_ERROR;
     }
     return OMPI_SUCCESS;
 }
@@ -778,8 +785,10 @@ static int rocm_progress(void)
         if (NULL != r->stage) {  /* staged outputs back to the caller's buffers */
             r->super.req_status.MPI_ERROR =
                 rocm_unstage_ops(r->stage->o, r->stage->n, r->super.req_status.MPI_ERROR);
-            nb_stage_free(r->stage);
-            r->stage = NULL;
+            if (!r->super.req_persistent) {  /* a persistent request keeps it for its starts */
+                nb_stage_free(r->stage);
+                r->stage = NULL;
+            }
         }
         ompi_request_complete(&r->super, true);
         ++completed;
@@ -827,7 +836,11 @@ static int rocm_request_start(size_t count, ompi_request_t **requests)
         r->super.req_complete = REQUEST_PENDING;
         r->super.req_status.MPI_ERROR = OMPI_SUCCESS;
         r->super.req_state = OMPI_REQUEST_ACTIVE;
-        rc = ompi_amd_plan_start(r->plan, NULL);
+        rc = OMPI_AMD_SUCCESS;
+        for (int k = 0; NULL != r->stage && k < r->stage->n; ++k) {  /* this start's inputs */
+            if (OMPI_SUCCESS != stage_copy_in(&r->stage->o[k])) rc = OMPI_AMD_ERR_HIP;
+        }
+        if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_plan_start(r->plan, NULL);
         if (OMPI_AMD_SUCCESS != rc) {
             r->super.req_status.MPI_ERROR = to_ompi_err(rc);
             ompi_request_complete(&r->super, true);
@@ -1086,8 +1099,13 @@ int mca_coll_rocm_ibcast(void *buf, int count, struct ompi_datatype_t *dtype, in
     return rocm_nb_post(rc, nb, st, comm, request);
 }
 
+static int rocm_wrap_plan(int rc, ompi_amd_plan_t *plan, struct rocm_nb_stage *stage,
+                          struct ompi_communicator_t *comm, ompi_request_t **request);
+
 /* MPI_Allreduce_init (coll.h:349-352).  Collective: the path decision is
- * agreed like the blocking allreduce's, and on the device path the plan's
+ * rocm_nb_begin's (no vote under the DEVICE lock; a rank with host operands
+ * gets staging memory owned by the request, refilled at every start and
+ * copied back at every completion), and on the device path the plan's
  * init swaps the buffer handles (it synchronises the ranks once). */
 int mca_coll_rocm_allreduce_init(const void *sbuf, void *rbuf, int count,
                                  struct ompi_datatype_t *dtype, struct ompi_op_t *op,
@@ -1095,28 +1113,22 @@ int mca_coll_rocm_allreduce_init(const void *sbuf, void *rbuf, int count,
                                  ompi_request_t **request, mca_coll_base_module_t *module)
 {
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
-    const int t = type_code(dtype);
-    const int ok = reduction_ok_n(dtype, op, (size_t) count) && dev(sbuf) && dev(rbuf);
-    mca_coll_rocm_request_t *r;
+    const int inplace = MPI_IN_PLACE == sbuf;
+    rocm_operand_t o[2] = {{(void *) sbuf, (size_t) count, dtype, 1, 0},
+                           {rbuf, (size_t) count, dtype, inplace, 1}};
+    struct rocm_nb_stage *st = NULL;
     ompi_amd_plan_t *plan = NULL;
-    int rc;
-    if (!take_device_path(m, ok)) {
+    int path, rc;
+    rc = rocm_nb_begin(m, reduction_ok_n(dtype, op, (size_t) count), dev(sbuf) && dev(rbuf), o, 2,
+                       &st, &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
         return m->c_coll.coll_allreduce_init(sbuf, rbuf, count, dtype, op, comm, info, request,
                                              m->c_coll.coll_allreduce_init_module);
     }
-    rc = ompi_amd_allreduce_init(m->dev_comm, MPI_IN_PLACE == sbuf ? rbuf : sbuf, rbuf,
-                                 (size_t) count, t, op->o_f_to_c_index, &plan);
-    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
-    r = OBJ_NEW(mca_coll_rocm_request_t);
-    if (NULL == r) {
-        (void) ompi_amd_plan_free(plan);
-        return OMPI_ERROR;
-    }
-    OMPI_REQUEST_INIT(&r->super, true);
-    r->super.req_mpi_object.comm = comm;
-    r->plan = plan;
-    *request = &r->super;
-    return OMPI_SUCCESS;
+    rc = ompi_amd_allreduce_init(m->dev_comm, inplace ? o[1].use : o[0].use, o[1].use,
+                                 (size_t) count, type_code(dtype), op->o_f_to_c_index, &plan);
+    return rocm_wrap_plan(rc, plan, st, comm, request);
 }
 
 /* MPI_Ireduce / MPI_Iscan / MPI_Iexscan / MPI_Ireduce_scatter (coll.h:
@@ -1218,21 +1230,24 @@ int mca_coll_rocm_ireduce_scatter(const void *sbuf, void *rbuf, const int *rcoun
 }
 
 /* MPI_Reduce_scatter_block_init / MPI_Allgather_init / MPI_Bcast_init
- * (coll.h:339-400): the same agreement as the blocking calls; on the device
+ * (coll.h:339-400): the same decision as MPI_Allreduce_init; on the device
  * path a library plan behind a persistent request (its start posts the
  * nonblocking call, completion through the progress callback), otherwise
  * the saved (libnbc) functions build the request. */
-static int rocm_wrap_plan(ompi_amd_plan_t *plan, struct ompi_communicator_t *comm,
-                          ompi_request_t **request)
+static int rocm_wrap_plan(int rc, ompi_amd_plan_t *plan, struct rocm_nb_stage *stage,
+                          struct ompi_communicator_t *comm, ompi_request_t **request)
 {
-    mca_coll_rocm_request_t *r = OBJ_NEW(mca_coll_rocm_request_t);
+    mca_coll_rocm_request_t *r = NULL;
+    if (OMPI_AMD_SUCCESS == rc) r = OBJ_NEW(mca_coll_rocm_request_t);
     if (NULL == r) {
-        (void) ompi_amd_plan_free(plan);
-        return OMPI_ERROR;
+        if (NULL != plan) (void) ompi_amd_plan_free(plan);
+        nb_stage_free(stage);
+        return OMPI_AMD_SUCCESS != rc ? to_ompi_err(rc) : OMPI_ERROR;
     }
     OMPI_REQUEST_INIT(&r->super, true);
     r->super.req_mpi_object.comm = comm;
     r->plan = plan;
+    r->stage = stage;
     *request = &r->super;
     return OMPI_SUCCESS;
 }
@@ -1244,18 +1259,24 @@ int mca_coll_rocm_reduce_scatter_block_init(const void *sbuf, void *rbuf, int rc
                                             mca_coll_base_module_t *module)
 {
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const size_t all = (size_t) rcount * (size_t) ompi_comm_size(comm);
+    const int inplace = MPI_IN_PLACE == sbuf;
+    rocm_operand_t o[2] = {{(void *) sbuf, all, dtype, 1, 0},
+                           {rbuf, inplace ? all : (size_t) rcount, dtype, inplace, 1}};
+    struct rocm_nb_stage *st = NULL;
     ompi_amd_plan_t *plan = NULL;
-    int rc;
-    if (!take_device_path(m, reduction_ok_n(dtype, op, (size_t) rcount * (size_t) ompi_comm_size(comm)) &&
-                                 dev(sbuf) && dev(rbuf))) {
+    int path, rc;
+    rc = rocm_nb_begin(m, reduction_ok_n(dtype, op, all), dev(sbuf) && dev(rbuf), o, 2, &st, &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
         return m->c_coll.coll_reduce_scatter_block_init(sbuf, rbuf, rcount, dtype, op, comm, info,
                                                         request,
                                                         m->c_coll.coll_reduce_scatter_block_init_module);
     }
-    rc = ompi_amd_reduce_scatter_block_init(m->dev_comm, sbuf, rbuf, (size_t) rcount,
-                                            type_code(dtype), op->o_f_to_c_index, &plan);
-    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
-    return rocm_wrap_plan(plan, comm, request);
+    rc = ompi_amd_reduce_scatter_block_init(m->dev_comm, inplace ? MPI_IN_PLACE : o[0].use,
+                                            o[1].use, (size_t) rcount, type_code(dtype),
+                                            op->o_f_to_c_index, &plan);
+    return rocm_wrap_plan(rc, plan, st, comm, request);
 }
 
 int mca_coll_rocm_allgather_init(const void *sbuf, int scount, struct ompi_datatype_t *sdtype,
@@ -1265,21 +1286,25 @@ int mca_coll_rocm_allgather_init(const void *sbuf, int scount, struct ompi_datat
 {
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
     const int inplace = MPI_IN_PLACE == sbuf;
+    const size_t all = (size_t) rcount * (size_t) ompi_comm_size(comm);
+    rocm_operand_t o[2] = {{(void *) sbuf, (size_t) scount, sdtype, 1, 0},
+                           {rbuf, all, rdtype, inplace, 1}};
+    struct rocm_nb_stage *st = NULL;
     ompi_amd_plan_t *plan = NULL;
     size_t rsize = 0;
-    int rc, ok;
+    int path, rc, ok;
     (void) ompi_datatype_type_size(rdtype, &rsize);
-    ok = bytes_ok(rsize * (size_t) rcount) &&
-         ompi_datatype_is_contiguous_memory_layout(rdtype, rcount * ompi_comm_size(comm)) &&
-         dev(rbuf) && dev(sbuf) && (inplace || ompi_datatype_is_contiguous_memory_layout(sdtype, scount));
-    if (!take_device_path(m, ok)) {
+    ok = ompi_datatype_is_contiguous_memory_layout(rdtype, (int) all) && dev(rbuf) && dev(sbuf) &&
+         (inplace || ompi_datatype_is_contiguous_memory_layout(sdtype, scount));
+    rc = rocm_nb_begin(m, bytes_ok(rsize * (size_t) rcount), ok, o, 2, &st, &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
         return m->c_coll.coll_allgather_init(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, info,
                                              request, m->c_coll.coll_allgather_init_module);
     }
-    rc = ompi_amd_allgather_init(m->dev_comm, inplace ? (const void *) 1 : sbuf, rbuf,
+    rc = ompi_amd_allgather_init(m->dev_comm, inplace ? (const void *) 1 : o[0].use, o[1].use,
                                  rsize * (size_t) rcount, &plan);
-    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
-    return rocm_wrap_plan(plan, comm, request);
+    return rocm_wrap_plan(rc, plan, st, comm, request);
 }
 
 int mca_coll_rocm_bcast_init(void *buf, int count, struct ompi_datatype_t *dtype, int root,
@@ -1287,16 +1312,21 @@ int mca_coll_rocm_bcast_init(void *buf, int count, struct ompi_datatype_t *dtype
                              ompi_request_t **request, mca_coll_base_module_t *module)
 {
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const int is_root = ompi_comm_rank(comm) == root;
+    rocm_operand_t o[1] = {{buf, (size_t) count, dtype, is_root, !is_root}};
+    struct rocm_nb_stage *st = NULL;
     ompi_amd_plan_t *plan = NULL;
     size_t size = 0;
-    int rc;
+    int path, rc;
     (void) ompi_datatype_type_size(dtype, &size);
-    if (!take_device_path(m, bytes_ok(size * (size_t) count) &&
-                                 ompi_datatype_is_contiguous_memory_layout(dtype, count) && dev(buf))) {
+    rc = rocm_nb_begin(m, bytes_ok(size * (size_t) count),
+                       ompi_datatype_is_contiguous_memory_layout(dtype, count) && dev(buf), o, 1, &st,
+                       &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
         return m->c_coll.coll_bcast_init(buf, count, dtype, root, comm, info, request,
                                          m->c_coll.coll_bcast_init_module);
     }
-    rc = ompi_amd_bcast_init(m->dev_comm, buf, size * (size_t) count, root, &plan);
-    if (OMPI_AMD_SUCCESS != rc) return to_ompi_err(rc);
-    return rocm_wrap_plan(plan, comm, request);
+    rc = ompi_amd_bcast_init(m->dev_comm, o[0].use, size * (size_t) count, root, &plan);
+    return rocm_wrap_plan(rc, plan, st, comm, request);
 }

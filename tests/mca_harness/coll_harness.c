@@ -1030,6 +1030,35 @@ int main(int argc, char **argv)
                 free(hb);
                 free(want);
             }
+            /* (i) MPI_Allreduce_init under the lock, rank 0 on host buffers:
+             * every start refills its staged input, every completion
+             * copies its output back */
+            for (int round = 0; round < 2; ++round) {
+                float **xs2 = all_inputs(n, 95 + round);
+                float **rb2 = malloc(sizeof(float *) * (size_t) g_size);
+                for (int r = 0; r < g_size; ++r) rb2[r] = calloc(n, sizeof(float));
+                CHECK(orc_allreduce(ORC_AR_TUNED, g_size, (const void *const *) xs2,
+                                    (void *const *) rb2, n, ORC_OP_SUM, ORC_T_FLOAT, 0) >= 0,
+                      "oracle allreduce");
+                if (0 == round) {
+                    CHECK(table.coll_allreduce_init(g_rank == 0 ? (void *) h : d,
+                                                    g_rank == 0 ? (void *) h2 : d2, (int) n, &dfloat,
+                                                    &sum, &comm, NULL, &rq,
+                                                    table.coll_allreduce_init_module) == OMPI_SUCCESS,
+                          "allreduce_init under the lock");
+                }
+                if (g_rank == 0) memcpy(h, xs2[0], n * 4);
+                else CHECK(harness_dev_copy_in(d, xs2[g_rank], n * 4) == 0, "input");
+                CHECK(rq->req_start(1, &rq) == OMPI_SUCCESS, "start %d", round);
+                harness_wait(rq);
+                CHECK(rq->req_status.MPI_ERROR == OMPI_SUCCESS, "persistent status");
+                if (g_rank == 0) CHECK(memcmp(h2, rb2[0], n * 4) == 0, "staged persistent result %d", round);
+                else expect_dev(d2, rb2[g_rank], n * 4, "persistent beside a staging rank");
+                for (int r = 0; r < g_size; ++r) free(rb2[r]);
+                free(rb2);
+                free_inputs(xs2);
+            }
+            CHECK(rq->req_free(&rq) == OMPI_SUCCESS && tuned_calls == 0, "persistent free");
         }
 #undef BOOT
         harness_dev_free(d);
