@@ -415,6 +415,10 @@ struct ompi_amd_comm {
     const call_blob *pre = nullptr;
     // point-to-point mailboxes (p2p.cpp)
     p2p_state *p2p = nullptr;
+    // per-communicator state of the one-sided part (osc_ipc.hip): released
+    // by destroy in two phases (comm_internal.h comm_set_osc_state)
+    void *osc_state = nullptr;
+    void (*osc_release)(void *, int) = nullptr;
 };
 
 // A persistent allreduce (MPI_Allreduce_init, coll.h:349-352): buffers,
@@ -2149,12 +2153,14 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     ipc_remove_user(c);
     for (auto &x : c->imports) ipc_unmap(x.ref);  // the process's mapping stays while others hold it
     c->imports.clear();
+    if (c->osc_release) c->osc_release(c->osc_state, 0);  // its peer mappings
     for (int p = 0; p < kMaxRanks; ++p) {
         for (int k = 0; k < 2; ++k) ipc_unmap(c->opened[p][k]);
         ipc_unmap(c->land_ref[p]);
         c->land_ref[p] = nullptr;
     }
     (void)c->boot.barrier();
+    if (c->osc_release) c->osc_release(c->osc_state, 1);  // its own memory
     if (c->flags) hip_ignore(hipFree(c->flags));
     if (c->scratch) hip_ignore(hipFree(c->scratch));
     if (c->land) hip_ignore(hipFree(c->land));
@@ -3303,6 +3309,13 @@ int comm_device(const ompi_amd_comm_t *c) { return c->device; }
 int64_t comm_timeout_ms(const ompi_amd_comm_t *c) { return c->timeout_ms; }
 int *comm_err_dev(ompi_amd_comm_t *c) { return c->err_dev; }
 p2p_state *comm_p2p(ompi_amd_comm_t *c) { return c->p2p; }
+
+void *comm_osc_state(ompi_amd_comm_t *c) { return c->osc_state; }
+
+void comm_set_osc_state(ompi_amd_comm_t *c, void *state, void (*release)(void *, int)) {
+    c->osc_state = state;
+    c->osc_release = release;
+}
 
 int comm_allgather(ompi_amd_comm_t *c, const void *mine, void *all, size_t len) {
     return c->boot.allgather(mine, all, len);

@@ -61,6 +61,13 @@ int xfer_copy(const void *src, void *dst, size_t bytes, hipStream_t s,
               const uint32_t *gate = nullptr);
 // Point-to-point mailboxes of the communicator (created with it).
 p2p_state *comm_p2p(ompi_amd_comm_t *c);
+// The one-sided part's per-communicator state (NULL until it sets one).
+// ompi_amd_comm_destroy calls release(state, 0) after its first barrier
+// (nobody reads this rank's memory any more: drop peer mappings) and
+// release(state, 1) after its second (every peer dropped its mappings:
+// free this rank's memory).
+void *comm_osc_state(ompi_amd_comm_t *c);
+void comm_set_osc_state(ompi_amd_comm_t *c, void *state, void (*release)(void *, int));
 
 // p2p.cpp: created by ompi_amd_comm_create in two phases around its first
 // rendezvous (rank 0 creates the segment before it, the others map it

@@ -395,7 +395,7 @@ make_acc_table(std::integer_sequence<int, O...>) {
 static const auto g_acc = make_acc_table(std::make_integer_sequence<int, OMPI_AMD_OP_COUNT>{});
 
 struct win_blob {
-    ipc_desc base, ctl;
+    ipc_desc base;
     uint64_t bytes;
     int64_t disp_unit;
     int64_t failed;  // this rank could not set up its side
@@ -424,7 +424,7 @@ struct ompi_amd_win {
     uint64_t peer_bytes[kOscMaxRanks] = {};
     int64_t peer_disp[kOscMaxRanks] = {};
     void *pinned[kOscMaxRanks] = {};
-    ipc_ref *ctl_ref[kOscMaxRanks] = {};  // peers' control pages (IPC registry references)
+    int ctl_slot = -1;  // this window's page in the communicator's control arena
     std::vector<hipStream_t> streams;  // every stream an epoch or RMA call ran on (win_free waits)
     int held[kOscMaxRanks] = {};  // outstanding passive lock per target (0 none)
     // general active target synchronisation (host side of the counters)
@@ -570,6 +570,126 @@ static int rma_op(ompi_amd_win_t *w, const void *origin, void *result, size_t co
     return rc != OMPI_AMD_SUCCESS ? rc : urc;
 }
 
+// ---- control pages: one arena per communicator ----
+// Every window needs a control page that every peer maps.  One exportable
+// allocation per window meant one IPC open per peer per window, and opens
+// of freshly recycled exporter ranges are what ROCm 7.2 refused ("invalid
+// device pointer").  The pages come instead from an arena
+// of the communicator — kCtlPerChunk pages per exportable, fine-grained
+// allocation, mapped by every peer once, released with the communicator.
+// Windows are created and freed collectively, in one order, so every rank
+// takes the same slot; a freed window's page is zeroed before its slot is
+// reused.
+constexpr int kCtlPerChunk = 64;
+constexpr size_t kCtlWords = CTL_BYTES / sizeof(uint32_t);
+
+struct ctl_chunk {
+    uint32_t *mine = nullptr;
+    uint32_t *peer[kOscMaxRanks] = {};
+    ipc_ref *ref[kOscMaxRanks] = {};
+};
+
+struct ctl_arena {
+    std::vector<ctl_chunk> chunks;
+    std::vector<char> used;  // per slot
+};
+
+static void ctl_arena_release(void *state, int phase) {
+    auto *a = static_cast<ctl_arena *>(state);
+    if (!a) return;
+    if (phase == 0) {  // nobody reads our pages any more: drop the peers' mappings
+        for (auto &ch : a->chunks)
+            for (auto &r : ch.ref) {
+                ipc_unmap(r);
+                r = nullptr;
+            }
+        return;
+    }
+    for (auto &ch : a->chunks)  // every peer dropped its mappings of ours
+        if (ch.mine) hip_ignore(hipFree(ch.mine));
+    delete a;
+}
+
+// The lowest free slot (every rank alike), growing the arena by one chunk —
+// a collective step every rank reaches at the same window — when none is
+// free.  rc_in: this rank's state so far (it joins the rendezvous anyway).
+static int ctl_take(ompi_amd_comm_t *c, int rc_in, int *slot) {
+    *slot = -1;
+    auto *a = static_cast<ctl_arena *>(comm_osc_state(c));
+    if (!a) {
+        a = new (std::nothrow) ctl_arena;
+        if (!a) return OMPI_AMD_ERR_BAD_PARAM;  // every rank: the same allocation failure
+        comm_set_osc_state(c, a, ctl_arena_release);
+    }
+    for (size_t k = 0; k < a->used.size(); ++k)
+        if (!a->used[k]) {
+            a->used[k] = 1;
+            *slot = (int)k;
+            return rc_in;
+        }
+    const int me = comm_rank(c), n = comm_size(c);
+    struct chunk_blob {
+        ipc_desc d;
+        int64_t failed;
+    } mine{}, all[kOscMaxRanks];
+    ctl_chunk ch;
+    int rc = rc_in;
+    if (rc == OMPI_AMD_SUCCESS) {
+        rc = comm_alloc_exportable(CTL_BYTES * kCtlPerChunk, true, (void **)&ch.mine, &mine.d);
+        if (rc == OMPI_AMD_SUCCESS)
+            rc = record_hip(hipMemset(ch.mine, 0, CTL_BYTES * kCtlPerChunk), "osc control arena");
+        if (rc == OMPI_AMD_SUCCESS)
+            rc = record_hip(hipStreamSynchronize(nullptr), "osc control arena");
+    }
+    mine.failed = rc == OMPI_AMD_SUCCESS ? 0 : 1;
+    const int arc = comm_allgather(c, &mine, all, sizeof(chunk_blob));
+    if (rc == OMPI_AMD_SUCCESS) rc = arc;
+    for (int p = 0; rc == OMPI_AMD_SUCCESS && p < n; ++p) {
+        if (all[p].failed) {
+            record_msg("osc control arena: rank %d could not allocate its chunk", p);
+            rc = OMPI_AMD_ERR_BOOTSTRAP;
+        } else if (p == me) {
+            ch.peer[p] = ch.mine;
+        } else {  // one attempt (a refused open is an error)
+            void *m = nullptr;
+            const ipc_desc &d = all[p].d;
+            rc = ipc_map(ipc_alloc{d.h, d.pid, d.id, d.base, d.size}, &ch.ref[p], &m);
+            ch.peer[p] = reinterpret_cast<uint32_t *>(static_cast<char *>(m) + d.off);
+        }
+    }
+    int all_ok = 0;  // the chunk joins the arena on every rank or on none
+    const int grc = ompi_amd_comm_agree(c, rc == OMPI_AMD_SUCCESS, &all_ok);
+    if (rc == OMPI_AMD_SUCCESS && (grc != OMPI_AMD_SUCCESS || !all_ok))
+        rc = grc != OMPI_AMD_SUCCESS ? grc : OMPI_AMD_ERR_BOOTSTRAP;
+    if (rc != OMPI_AMD_SUCCESS) {
+        for (auto &r : ch.ref) ipc_unmap(r);
+        (void)comm_allgather(c, nullptr, nullptr, 0);  // every mapping closed before the free
+        if (ch.mine) hip_ignore(hipFree(ch.mine));
+        return rc;
+    }
+    *slot = (int)a->used.size();
+    a->chunks.push_back(ch);
+    a->used.resize(a->used.size() + kCtlPerChunk, 0);
+    a->used[(size_t)*slot] = 1;
+    return OMPI_AMD_SUCCESS;
+}
+
+// rank p's control page of slot `slot` as this process maps it
+static uint32_t *ctl_page(ompi_amd_comm_t *c, int slot, int p) {
+    auto *a = static_cast<ctl_arena *>(comm_osc_state(c));
+    return a->chunks[(size_t)slot / kCtlPerChunk].peer[p] + (size_t)(slot % kCtlPerChunk) * kCtlWords;
+}
+
+// after the window's last use everywhere: zero this rank's page, free the slot
+static int ctl_give(ompi_amd_comm_t *c, int slot) {
+    if (slot < 0) return OMPI_AMD_SUCCESS;
+    auto *a = static_cast<ctl_arena *>(comm_osc_state(c));
+    int rc = record_hip(hipMemset(ctl_page(c, slot, comm_rank(c)), 0, CTL_BYTES), "osc control page reset");
+    if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipStreamSynchronize(nullptr), "osc control page reset");
+    a->used[(size_t)slot] = 0;
+    return rc;
+}
+
 // shared: every rank's base as this process maps it (MPI_Win_allocate_shared),
 // so nothing is exported or imported for the bases.
 static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit, bool owns,
@@ -583,19 +703,12 @@ static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit
     w->bytes = bytes;
     w->owns_base = owns;
     int rc = comm_drain(c);  // collective order: deferred nonblocking calls first
-    hipError_t e = hipSuccess;
-    ipc_desc ctl_desc{};
-    if (rc == OMPI_AMD_SUCCESS) {
-        rc = comm_alloc_exportable(CTL_BYTES, true, (void **)&w->ctl, &ctl_desc);
-        if (rc == OMPI_AMD_SUCCESS) e = hipMemset(w->ctl, 0, CTL_BYTES);
-        if (rc == OMPI_AMD_SUCCESS && e == hipSuccess) e = hipStreamSynchronize(nullptr);
-        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(e, "osc control page");
-    }
+    rc = ctl_take(c, rc, &w->ctl_slot);
+    if (rc == OMPI_AMD_SUCCESS) w->ctl = ctl_page(c, w->ctl_slot, w->rank);
     win_blob mine{}, all[kOscMaxRanks];
     mine.bytes = bytes;
     mine.disp_unit = disp_unit;
     if (rc == OMPI_AMD_SUCCESS && bytes && !shared) rc = comm_export(c, base, &mine.base);
-    if (rc == OMPI_AMD_SUCCESS) mine.ctl = ctl_desc;
     // every rank takes part in the rendezvous, whatever failed locally
     mine.failed = rc == OMPI_AMD_SUCCESS ? 0 : 1;
     const int arc = comm_allgather(c, &mine, all, sizeof(win_blob));
@@ -620,12 +733,7 @@ static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit
             rc = comm_import(c, p, all[p].base, &pb, true, &w->pinned[p]);
             w->peer_base[p] = const_cast<char *>(pb);
         }
-        if (rc == OMPI_AMD_SUCCESS) {  // one attempt (a refused open is an error)
-            void *m = nullptr;
-            const ipc_desc &d = all[p].ctl;
-            rc = ipc_map(ipc_alloc{d.h, d.pid, d.id, d.base, d.size}, &w->ctl_ref[p], &m);
-            w->peer_ctl[p] = reinterpret_cast<uint32_t *>(static_cast<char *>(m) + d.off);
-        }
+        w->peer_ctl[p] = ctl_page(c, w->ctl_slot, p);
     }
     // agree: all mapped (or all give up together)
     int ok = rc == OMPI_AMD_SUCCESS, all_ok = 0;
@@ -633,11 +741,9 @@ static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit
     if (rc == OMPI_AMD_SUCCESS && (grc != OMPI_AMD_SUCCESS || !all_ok))
         rc = grc != OMPI_AMD_SUCCESS ? grc : OMPI_AMD_ERR_BOOTSTRAP;
     if (rc != OMPI_AMD_SUCCESS) {
-        for (int p = 0; p < w->size; ++p) {
+        for (int p = 0; p < w->size; ++p)
             if (w->pinned[p]) comm_unpin(c, w->pinned[p]);
-            ipc_unmap(w->ctl_ref[p]);
-        }
-        if (w->ctl) hip_ignore(hipFree(w->ctl));
+        (void)ctl_give(c, w->ctl_slot);  // nobody used it: every rank failed here together
         delete w;
         return rc;
     }
@@ -704,16 +810,15 @@ int ompi_amd_win_free(ompi_amd_win_t *w) {
     }
     const int brc = comm_allgather(c, nullptr, nullptr, 0);  // nobody still touches the windows
     if (rc == OMPI_AMD_SUCCESS) rc = brc;
-    for (int p = 0; p < w->size; ++p) {
+    for (int p = 0; p < w->size; ++p)
         if (w->pinned[p]) comm_unpin(c, w->pinned[p]);
-        ipc_unmap(w->ctl_ref[p]);  // the process's mapping stays while others hold it
-    }
+    const int crc = ctl_give(c, w->ctl_slot);  // the peers' last kernels on it are done
+    if (rc == OMPI_AMD_SUCCESS) rc = crc;
     ipc_unmap(w->shared_ref);
     const int brc2 = comm_allgather(c, nullptr, nullptr, 0);  // mappings closed before frees
     if (rc == OMPI_AMD_SUCCESS) rc = brc2;
     if (w->shared && !w->shared_ref && w->shared_seg) hip_ignore(hipFree(w->shared_seg));
     if (w->query) hip_ignore(hipStreamDestroy(w->query));
-    if (w->ctl) hip_ignore(hipFree(w->ctl));
     if (w->owns_base && w->base) hip_ignore(hipFree(w->base));
     if (rc == OMPI_AMD_SUCCESS) rc = comm_sticky(c);
     delete w;

@@ -17,6 +17,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "mpi.h"
 #include "ompi/constants.h"
@@ -246,13 +247,24 @@ static void *lib_buf(mca_pml_rocm_request_t *r) { return NULL != r->stage ? r->s
 /* Wait for a library request without a time limit, driving opal_progress
  * (other PML traffic, e.g. the system-tag messages of a collective the peer
  * is inside, must keep moving: ob1's blocking calls do the same). */
+/* Wait for a library request while driving opal_progress.  No limit by
+ * default (MPI semantics); pml_rocm_timeout_ms > 0 bounds it (diagnostics:
+ * a lost message becomes OMPI_ERR_TIMEOUT instead of a hang). */
 static int wait_lib(ompi_amd_p2p_request_t *lib, ompi_amd_status_t *s)
 {
-    for (;;) {
+    const int limit_ms = mca_pml_rocm_component.timeout_ms;
+    struct timespec t0, t;
+    (void) clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (unsigned k = 0;; ++k) {
         int fin = 0;
         const int rc = ompi_amd_p2p_test(lib, &fin, s);
         if (OMPI_AMD_SUCCESS != rc || fin) return rc;
         opal_progress();
+        if (limit_ms > 0 && 0 == (k & 1023)) {
+            (void) clock_gettime(CLOCK_MONOTONIC, &t);
+            if ((t.tv_sec - t0.tv_sec) * 1000 + (t.tv_nsec - t0.tv_nsec) / 1000000 > limit_ms)
+                return OMPI_AMD_ERR_TIMEOUT;
+        }
     }
 }
 

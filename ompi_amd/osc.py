@@ -51,27 +51,6 @@ class RmaRequest:
     def wait(self) -> None:
         _lib.check(self._lib.ompi_amd_rma_wait(self._h), "rma_wait")
 
-    @classmethod
-    def allocate_shared(cls, comm: Communicator, nbytes: int, disp_unit: int = 1,
-                        noncontig: bool = False) -> "Window":
-        """MPI_Win_allocate_shared (collective): every rank's segment in one
-        device allocation of rank 0, contiguous in every process unless
-        `noncontig`; `base_ptr` is this rank's segment."""
-        h, b = ctypes.c_void_p(), ctypes.c_void_p()
-        _lib.check(comm._lib.ompi_amd_win_allocate_shared(comm._h, nbytes, disp_unit,
-                                                          int(noncontig), ctypes.byref(b),
-                                                          ctypes.byref(h)), "win_allocate_shared")
-        return cls(comm, h, b.value or 0, nbytes)
-
-    def shared_query(self, rank: int):
-        """MPI_Win_shared_query: (size, disp_unit, address in this process)
-        of `rank`'s segment; rank < 0 (MPI_PROC_NULL) = the first nonzero one."""
-        size, du, base = ctypes.c_size_t(), ctypes.c_int(), ctypes.c_void_p()
-        _lib.check(self._lib.ompi_amd_win_shared_query(self._h, rank, ctypes.byref(size),
-                                                       ctypes.byref(du), ctypes.byref(base)),
-                   "win_shared_query")
-        return size.value, du.value, base.value or 0
-
     def free(self) -> None:
         if self._h:
             h, self._h = self._h, None
@@ -110,6 +89,27 @@ class Window:
         _lib.check(comm._lib.ompi_amd_win_allocate(comm._h, nbytes, disp_unit, ctypes.byref(b),
                                                    ctypes.byref(h)), "win_allocate")
         return cls(comm, h, b.value or 0, nbytes)
+
+    @classmethod
+    def allocate_shared(cls, comm: Communicator, nbytes: int, disp_unit: int = 1,
+                        noncontig: bool = False) -> "Window":
+        """MPI_Win_allocate_shared (collective): every rank's segment in one
+        device allocation of rank 0, contiguous in every process unless
+        `noncontig`; `base_ptr` is this rank's segment."""
+        h, b = ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(comm._lib.ompi_amd_win_allocate_shared(comm._h, nbytes, disp_unit,
+                                                          int(noncontig), ctypes.byref(b),
+                                                          ctypes.byref(h)), "win_allocate_shared")
+        return cls(comm, h, b.value or 0, nbytes)
+
+    def shared_query(self, rank: int):
+        """MPI_Win_shared_query: (size, disp_unit, address in this process)
+        of `rank`'s segment; rank < 0 (MPI_PROC_NULL) = the first nonzero one."""
+        size, du, base = ctypes.c_size_t(), ctypes.c_int(), ctypes.c_void_p()
+        _lib.check(self._lib.ompi_amd_win_shared_query(self._h, rank, ctypes.byref(size),
+                                                       ctypes.byref(du), ctypes.byref(base)),
+                   "win_shared_query")
+        return size.value, du.value, base.value or 0
 
     def free(self) -> None:
         if self._h:

@@ -364,6 +364,46 @@ def case_persistent_rsb_ag_bcast(comm, rank, n, salt, big):
     return not msgs, "; ".join(msgs)
 
 
+def case_zero_counts(comm, rank, n, salt):
+    """Zero elements / bytes in every entry point — blocking, nonblocking and
+    persistent — (MPI filters count 0 above coll only for some calls,
+    allreduce.c:104): every call succeeds on every rank, nothing is written
+    (sentinel bytes stay), and the communicator's epochs stay paired (a
+    normal allreduce right after is bit-exact)."""
+    F, SUM = mop.MPI_FLOAT, mop.MPI_SUM
+    sent = np.full(64, 0xA5, np.uint8)
+    a, b = to_dev(sent), to_dev(sent)
+    comm.allreduce(a, b, 0, F, SUM)
+    comm.reduce(a, b, 0, F, SUM, n - 1)
+    comm.scan(a, b, 0, F, SUM)
+    comm.exscan(a, b, 0, F, SUM)
+    comm.reduce_scatter_block(a, b, 0, F, SUM)
+    comm.reduce_scatter(a, b, [0] * n, F, SUM)
+    comm.allgather(a, b, 0)
+    comm.bcast(b, 0, 0)
+    reqs = [comm.iallreduce(a, b, 0, F, SUM), comm.ireduce(a, b, 0, F, SUM, 0),
+            comm.iscan(a, b, 0, F, SUM), comm.iscan(a, b, 0, F, SUM, exclusive=True),
+            comm.ireduce_scatter_block(a, b, 0, F, SUM), comm.ireduce_scatter(a, b, [0] * n, F, SUM),
+            comm.iallgather(a, b, 0), comm.ibcast(b, 0, n - 1)]
+    for r in reqs:
+        r.wait()
+        r.free()
+    plans = [comm.allreduce_init(a, b, 0, F, SUM), comm.reduce_scatter_block_init(a, b, 0, F, SUM),
+             comm.allgather_init(a, b, 0), comm.bcast_init(b, 0, 0)]
+    for _ in range(2):
+        for p in plans:
+            p.start()
+        for p in plans:
+            p.wait()
+    for p in plans:
+        p.free()
+    torch.cuda.synchronize()
+    for t, what in ((a, "sbuf"), (b, "rbuf")):
+        if not np.array_equal(t.cpu().numpy(), sent):
+            return False, f"a zero-count call wrote into {what}"
+    return case_allreduce(comm, rank, n, F, SUM, 4099, salt)
+
+
 def case_regrow(comm, rank, n, salt):
     """Landing-buffer growth several times in a row (large scans of rising
     size, an in-place reduce_scatter in between), every result checked."""
@@ -874,6 +914,7 @@ def main():
          lambda: case_scan(comm, rank, n, I8, mop.MPI_PROD, 70001, 55, True, True)),
     ]
     cases += [
+        ("zero_counts_every_entry_point", lambda: case_zero_counts(comm, rank, n, 96)),
         ("iallreduce_mixed", lambda: case_iallreduce(comm, rank, n, 90)),
         ("iallreduce_many_outstanding", lambda: case_iallreduce_many(comm, rank, n, 94)),
         ("persistent_small", lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, 3001, 80)),

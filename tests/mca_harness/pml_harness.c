@@ -47,6 +47,8 @@ struct ompi_datatype_t harness_mpi_byte = {0, 1, 1, 1};
 mca_pml_base_module_t mca_pml;
 
 static int g_rank, g_size;
+/* where a rank is (stderr, shown when the test fails or hangs) */
+#define SECTION(k) (fprintf(stderr, "rank %d: section %d\n", g_rank, (k)), fflush(stderr))
 #define CHECK(c, ...)                                                             \
     do {                                                                          \
         if (!(c)) {                                                               \
@@ -139,6 +141,8 @@ int main(int argc, char **argv)
     CHECK(mca_pml_rocm_installed && mca_pml.pml_isend != o_isend && mca_pml_rocm_host.pml_isend == o_isend &&
               mca_pml.pml_max_tag == ob1.pml_max_tag,
           "close saves ob1 and installs pml/rocm");
+    /* a lost message ends the run with a CHECK message instead of a hang */
+    if (use_gpu) mca_pml_rocm_component.timeout_ms = 60000;
     CHECK(mca_pml.pml_add_comm(&comm) == OMPI_SUCCESS, "add_comm");
     if (!use_gpu) {
         int m = -1;
@@ -156,6 +160,7 @@ int main(int argc, char **argv)
     CHECK(mca_pml_rocm_comm_of(&comm) != NULL, "library communicator created");
     const int right = (g_rank + 1) % g_size, left = (g_rank + g_size - 1) % g_size;
 
+    SECTION(1);
     /* 1. ring isend / irecv on device buffers */
     {
         const size_t sizes[5] = {0, 777, 4096, 300001, 8u << 20};
@@ -192,6 +197,7 @@ int main(int argc, char **argv)
             free(got);
         }
     }
+    SECTION(2);
     /* 2. blocking send / recv from host memory (staged through the device),
      * ANY_SOURCE / ANY_TAG on the receive */
     {
@@ -215,6 +221,7 @@ int main(int argc, char **argv)
         free(h);
         free(got);
     }
+    SECTION(3);
     /* 3. non-contiguous receive type: 4-byte elements with 4-byte gaps */
     {
         const size_t n = 5000;
@@ -238,6 +245,7 @@ int main(int argc, char **argv)
         free(h);
         free(t);
     }
+    SECTION(4);
     /* 4. iprobe / probe, then the receive */
     {
         unsigned char v = (unsigned char) g_rank, w = 0;
@@ -258,6 +266,7 @@ int main(int argc, char **argv)
         harness_dev_free(dv);
         harness_dev_free(dw);
     }
+    SECTION(5);
     /* 5. persistent send / recv, three starts with fresh data */
     {
         const size_t n = 65537;
@@ -288,6 +297,7 @@ int main(int argc, char **argv)
         free(h);
         free(got);
     }
+    SECTION(6);
     /* 6. truncation: 1000 bytes into a 999-byte receive */
     {
         unsigned char h[1000] = {0};
@@ -306,6 +316,7 @@ int main(int argc, char **argv)
         harness_dev_free(ds);
         harness_dev_free(dr);
     }
+    SECTION(7);
     /* 7. system tags, PROC_NULL and matched probes */
     {
         ompi_request_t *r = NULL;
@@ -321,6 +332,7 @@ int main(int argc, char **argv)
         CHECK(mca_pml.pml_improbe(left, -20, &comm, &m, &msg, NULL) == OMPI_SUCCESS && ob1_calls == 3,
               "matched probe of a system tag reaches ob1");
     }
+    SECTION(8);
     /* 8. MPI_Request_free of active requests (the oldest active request is
      * the list's tail): an in-flight Ssend and irecv, freed, leave the list */
     {
@@ -347,6 +359,7 @@ int main(int argc, char **argv)
         free(h);
         free(got);
     }
+    SECTION(9);
     /* 9. the sender frees and reallocates its device buffer between
      * messages: staged (default: the receiver reads library memory) and
      * p2p_user_ipc = 1 (the receiver maps the send buffer; the IPC registry
@@ -389,6 +402,7 @@ int main(int argc, char **argv)
         free(h);
         free(got);
     }
+    SECTION(10);
     /* 10. pml_rocm_host_path = 1: host-buffer operations reach ob1 and make
      * no library call; device buffers still go to the library */
     {

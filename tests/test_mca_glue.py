@@ -4,6 +4,7 @@ tests/mca_harness: slot ownership, the NULL-pattern check, host-buffer
 fallback to op/base (CPU) and the device path (GPU)."""
 import os
 import subprocess
+import time
 
 import pytest
 
@@ -56,10 +57,17 @@ def _run_coll_harness(exe, n, gpu, timeout):
     env = {**os.environ, "HARNESS_GPU": "1" if gpu else "0", "OMPI_AMD_COLL_TIMEOUT_MS": "20000"}
     procs = [subprocess.Popen([exe, name, str(r), str(n)], stdout=subprocess.PIPE,
                               stderr=subprocess.PIPE, text=True, env=env) for r in range(n)]
-    outs = []
+    outs, deadline = [], time.time() + timeout
     try:
         for p in procs:
-            out, err = p.communicate(timeout=timeout)
+            try:
+                out, err = p.communicate(timeout=max(1.0, deadline - time.time()))
+            except subprocess.TimeoutExpired:  # report every rank's last words
+                for q in procs:
+                    if q.poll() is None:
+                        q.kill()
+                tails = [(q.returncode, *(x[-1500:] for x in q.communicate())) for q in procs]
+                raise AssertionError(f"harness timed out after {timeout} s: {tails}")
             outs.append((p.returncode, out.strip(), err[-2000:]))
     finally:
         for p in procs:
@@ -82,7 +90,7 @@ def test_coll_component_device_path(coll_harness, n):
     through the communicator's table runs on device buffers and matches the
     oracle bit for bit; host / mixed / user-op calls go to the saved
     functions on every rank; release destroys the device communicator."""
-    for rc, out, err in _run_coll_harness(coll_harness, n, True, 240):
+    for rc, out, err in _run_coll_harness(coll_harness, n, True, 150):
         assert rc == 0 and out == "ok gpu", (rc, out, err)
 
 
@@ -116,7 +124,7 @@ def test_pml_component_device_path(pml_harness, n):
     persistent requests started three times with fresh data, truncation;
     system tags, PROC_NULL and matched probes of system tags reach the saved
     PML; add_comm / del_comm create and destroy the library communicator."""
-    for rc, out, err in _run_coll_harness(pml_harness, n, True, 240):
+    for rc, out, err in _run_coll_harness(pml_harness, n, True, 150):
         assert rc == 0 and out == "ok gpu", (rc, out, err)
 
 
@@ -149,7 +157,7 @@ def test_osc_component_device_path(osc_harness, n):
     component: fence epochs with accumulate (bit-exact vs op/base) and get,
     an exclusive-lock put epoch, a fetch_and_op counter, refusal of user ops,
     mismatched datatypes and PSCW, free."""
-    for rc, out, err in _run_coll_harness(osc_harness, n, True, 180):
+    for rc, out, err in _run_coll_harness(osc_harness, n, True, 150):
         assert rc == 0 and out == "ok gpu", (rc, out, err)
 
 
