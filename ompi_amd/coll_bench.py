@@ -101,12 +101,13 @@ def bench_allreduce(args, metric: str, link_gbs: float):
     def ours():
         comm.allreduce(x, y, n, mop.MPI_FLOAT, mop.MPI_SUM, stream=stream)
 
-    # The headline runs the library DEFAULT (what coll/rocm ships:
-    # coll_rocm_allreduce_algorithm / coll_rocm_user_ipc at their defaults,
-    # coll_rocm_module.c) — never a scheme picked per run.  The other
-    # schemes are measured beside it (each first checked bit-exact on
-    # dataset E at this size) and reported only under config.schemes, as
-    # the evidence a change of default would rest on.
+    # The headline runs what coll/rocm ships (coll_rocm_module.c): staged
+    # (coll_rocm_user_ipc 0) with coll_rocm_autotune 1 — the library itself
+    # measures its staged schemes x grids on the first calls of a size and
+    # keeps the fastest (ompi_amd_allreduce); the bench
+    # never picks.  Every scheme, user-IPC ones included, is also measured
+    # beside it (each first checked bit-exact on dataset E at this size)
+    # and reported under config.schemes only.
     S = n * 4
     factor = 2.0 * (world - 1) / world
     default = {"algorithm": comm.get_param("algorithm"), "user_ipc": comm.get_param("user_ipc"),
@@ -138,6 +139,30 @@ def bench_allreduce(args, metric: str, link_gbs: float):
     comm.set_param("blocks", default["blocks"])
     best = {"algorithm": default["algorithm"]}
     best_name = default_name
+    # coll/rocm ships coll_rocm_autotune = 1 (setting a scheme above turned
+    # it off, as it does in the library): the first calls of this size try
+    # the candidates, every rank then runs the one whose slowest rank was
+    # fastest — what an MPI job gets from its first allreduces of this size
+    autotune = None
+    if not os.environ.get("OMPI_AMD_BENCH_NO_AUTOTUNE"):
+        comm.set_param("autotune", 1)
+        _progress(rank, "autotune: one call per candidate")
+        calls = 0
+        while calls < 12:
+            ours()
+            torch.cuda.synchronize()
+            calls += 1
+            if comm.get_param("autotune_state") == 2:
+                break
+        if comm.get_param("autotune_state") == 2:
+            a_c, b_c = comm.get_param("autotune_algorithm"), comm.get_param("autotune_blocks")
+            best = {"algorithm": a_c}
+            best_name = f"{dict(ALGORITHMS)[a_c]}/staged/{b_c}"
+            autotune = {"choice": best_name, "calls": calls,
+                        "worst_rank_us": {
+                            f"{dict(ALGORITHMS)[comm.get_param(f'autotune_alg{k}')]}/staged/"
+                            f"{comm.get_param(f'autotune_grid{k}')}": comm.get_param(f"autotune_us{k}")
+                            for k in range(6)}}
 
     _progress(rank, f"headline: {best_name}")
     t = _timed(ours, args.steps, args.warmup, dist, torch, tdev)
@@ -205,6 +230,7 @@ def bench_allreduce(args, metric: str, link_gbs: float):
                    "count": n, "bytes": S, "op": "MPI_SUM", "datatype": "MPI_FLOAT",
                    "parallelism": f"{world} ranks, 1 GPU each", "busbw_factor": factor,
                    "algorithm": best_name, "algorithm_is_library_default": True,
+                   "library_default_scheme": default_name, "autotune": autotune,
                    "bit_exact_dataset_E": default_exact,
                    "ipc_mode_legacy": comm.get_param("ipc_mode_legacy"),
                    "schemes": schemes},

@@ -326,6 +326,28 @@ struct ompi_amd_request {
 };
 
 // ------------------------------------------------------------------ comm
+// Autotuning of large staged allreduces (param "autotune"): the first
+// kTuneCands blocking calls of a size bucket run one candidate (scheme x
+// grid) each, timed with events on the call's stream; at the last one the
+// ranks allgather their times and every rank takes the candidate whose
+// slowest rank was fastest — the same choice everywhere, since every rank
+// makes the same calls.  coll/tuned's dynamic rules pick from a table;
+// this picks from measurements on the machine it runs on (xGMI loads vs
+// stores and the grid that saturates the links are not knowable offline).
+constexpr int kTuneCands = 6;
+struct tune_cand {
+    int algorithm, blocks;
+};
+static const tune_cand kTune[kTuneCands] = {{2, 1024}, {2, 512}, {2, 256},
+                                            {0, 1024}, {0, 512}, {0, 256}};
+struct tune_bucket {
+    int next = 0;
+    bool done = false;
+    int choice = 0;
+    hipEvent_t ev[2 * kTuneCands] = {};
+    float worst_ms[kTuneCands] = {};
+};
+
 struct ompi_amd_comm {
     int rank = 0, size = 0, device = 0;
     ShmBoot boot;
@@ -389,6 +411,12 @@ struct ompi_amd_comm {
     int64_t timeout_ms = 30000;
     int max_blocks = 1024;
     int algorithm = 2;                    // push: push-gather in the staged mode (no staging copy)
+    // param "autotune" (0 here; coll/rocm turns it on): large blocking
+    // allreduces pick their scheme and grid by measurement (tune_bucket)
+    int autotune = 0;
+    std::map<int, struct tune_bucket> tune;  // by floor(log2(bytes))
+    int tune_last = 0;                       // last bucket touched: 0 none, 1 tuning, 2 decided
+    int tune_last_key = -1;
     int tuned_alg = 0;                    // coll_tuned_allreduce_algorithm (forced), 0 = fixed
     // this communicator's references to peer mappings (the mappings
     // themselves are process-wide: ipc_registry.h), least recently used
@@ -2174,6 +2202,9 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
             hip_ignore(hipEventDestroy(pr.second));
         }
     for (auto e : c->ev_free) hip_ignore(hipEventDestroy(e));
+    for (auto &kv : c->tune)
+        for (auto e : kv.second.ev)
+            if (e) hip_ignore(hipEventDestroy(e));
     if (c->p2p) p2p_destroy(c->p2p);
     c->boot.detach();
     delete c;
@@ -2278,16 +2309,21 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
     } else if (!strcmp(key, "blocks")) {
         if (v <= 0 || v > 65535) return OMPI_AMD_ERR_BAD_PARAM;
         c->max_blocks = (int)v;
+        c->autotune = 0;  // an explicit grid is not second-guessed
+    } else if (!strcmp(key, "autotune")) {
+        c->autotune = v ? 1 : 0;
     } else if (!strcmp(key, "fused_bytes")) {
         if (v < 0) return OMPI_AMD_ERR_BAD_PARAM;
         c->fused_bytes = std::min<size_t>((size_t)v, c->scratch_bytes);
     } else if (!strcmp(key, "algorithm")) {
         if (v < 0 || v >= ALG_COUNT) return OMPI_AMD_ERR_BAD_PARAM;
         c->algorithm = (int)v;
+        c->autotune = 0;  // an explicit scheme is not second-guessed
     } else if (!strcmp(key, "force_shadow")) {
         c->force_shadow = v ? 1 : 0;
     } else if (!strcmp(key, "user_ipc")) {
         c->user_ipc = v ? 1 : 0;
+        c->autotune = 0;
     } else if (!strcmp(key, "tuned_allreduce_algorithm")) {
         if (v < 0 || v >= TUNED_AR_COUNT) return OMPI_AMD_ERR_BAD_PARAM;
         c->tuned_alg = (int)v;
@@ -2309,6 +2345,22 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "blocks")) *v = c->max_blocks;
     else if (!strcmp(key, "fused_bytes")) *v = (int64_t)c->fused_bytes;
     else if (!strcmp(key, "algorithm")) *v = c->algorithm;
+    else if (!strcmp(key, "autotune")) *v = c->autotune;
+    else if (!strcmp(key, "autotune_state")) *v = c->tune_last;
+    else if (!strncmp(key, "autotune_", 9) && c->tune_last_key >= 0 &&
+             c->tune.count(c->tune_last_key) && c->tune.at(c->tune_last_key).done) {
+        // the last decided bucket: its choice and every candidate's worst rank
+        const tune_bucket &tb = c->tune.at(c->tune_last_key);
+        if (!strcmp(key, "autotune_algorithm")) *v = kTune[tb.choice].algorithm;
+        else if (!strcmp(key, "autotune_blocks")) *v = kTune[tb.choice].blocks;
+        else if (!strncmp(key, "autotune_us", 11) && atoi(key + 11) >= 0 && atoi(key + 11) < kTuneCands)
+            *v = (int64_t)(tb.worst_ms[atoi(key + 11)] * 1000.f);
+        else if (!strncmp(key, "autotune_alg", 12) && atoi(key + 12) >= 0 && atoi(key + 12) < kTuneCands)
+            *v = kTune[atoi(key + 12)].algorithm;
+        else if (!strncmp(key, "autotune_grid", 13) && atoi(key + 13) >= 0 && atoi(key + 13) < kTuneCands)
+            *v = kTune[atoi(key + 13)].blocks;
+        else return OMPI_AMD_ERR_BAD_PARAM;
+    }
     else if (!strcmp(key, "tuned_allreduce_algorithm")) *v = c->tuned_alg;
     else if (!strcmp(key, "landing_bytes")) *v = (int64_t)c->land_bytes;
     else if (!strcmp(key, "boot_calls")) *v = (int64_t)c->boot.posted();
@@ -2356,7 +2408,62 @@ int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
     TRY(drain(c));
     path_params pp = params_of(c);
     TRY(agree_root0_inplace(c, &pp, in_place(sbuf, rbuf)));
-    return allreduce_impl(c, sbuf, rbuf, count, type, op, as_stream(stream), pp);
+    const hipStream_t s = as_stream(stream);
+    tune_bucket *tb = nullptr;
+    int cand = -1;
+    const int save_alg = c->algorithm, save_blocks = c->max_blocks;
+    if (c->autotune && pp.tuned_alg == 0 && !c->user_ipc && !c->force_shadow &&
+        allreduce_swaps(c, pp, count, type)) {
+        const size_t bytes = count * ompi_amd_type_extent(type);
+        const int key = 63 - __builtin_clzll((unsigned long long)bytes);
+        tb = &c->tune[key];
+        c->tune_last_key = key;
+        cand = tb->done ? -1 : tb->next;
+        const tune_cand &tc = kTune[tb->done ? tb->choice : cand];
+        c->algorithm = tc.algorithm;
+        c->max_blocks = tc.blocks;
+        pp = params_of(c);
+        if (cand >= 0) {
+            for (int k = 0; k < 2; ++k)
+                if (!tb->ev[2 * cand + k])
+                    TRY(record_hip(hipEventCreate(&tb->ev[2 * cand + k]), "autotune event"));
+            TRY(record_hip(hipEventRecord(tb->ev[2 * cand], s), "autotune event"));
+        }
+    }
+    int rc = allreduce_impl(c, sbuf, rbuf, count, type, op, s, pp);
+    c->algorithm = save_alg;
+    c->max_blocks = save_blocks;
+    if (cand >= 0) {
+        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipEventRecord(tb->ev[2 * cand + 1], s), "autotune event");
+        if (++tb->next == kTuneCands) {  // every rank is at this call: decide together
+            float mine[kTuneCands], all[kMaxRanks][kTuneCands];
+            for (int k = 0; k < kTuneCands; ++k) {
+                mine[k] = 1e30f;
+                if (rc == OMPI_AMD_SUCCESS && hipEventSynchronize(tb->ev[2 * k + 1]) == hipSuccess &&
+                    hipEventElapsedTime(&mine[k], tb->ev[2 * k], tb->ev[2 * k + 1]) != hipSuccess)
+                    mine[k] = 1e30f;
+                (void)hipGetLastError();
+            }
+            const int arc = comm_allgather(c, mine, all, sizeof(mine));
+            if (rc == OMPI_AMD_SUCCESS) rc = arc;
+            int best = 0;
+            for (int k = 0; k < kTuneCands; ++k) {
+                float w = 0.f;
+                for (int p = 0; p < c->size; ++p) w = std::max(w, arc == OMPI_AMD_SUCCESS ? all[p][k] : 0.f);
+                tb->worst_ms[k] = w;
+                if (w < tb->worst_ms[best]) best = k;
+            }
+            tb->choice = arc == OMPI_AMD_SUCCESS ? best : 0;  // a failed rendezvous fails every rank
+            tb->done = true;
+            for (auto &e : tb->ev)
+                if (e) {
+                    hip_ignore(hipEventDestroy(e));
+                    e = nullptr;
+                }
+        }
+    }
+    if (tb) c->tune_last = tb->done ? 2 : 1;
+    return rc;
 }
 
 int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,

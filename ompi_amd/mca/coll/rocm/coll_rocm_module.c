@@ -70,6 +70,7 @@ mca_coll_rocm_component_t mca_coll_rocm_component = {
     .timeout_ms = 30000,
     .algorithm = 2,
     .user_ipc = 0,
+    .autotune = 1,
     .residency = ROCM_RES_AUTO,
     .residency_lock = 8,
     .residency_recheck = 256,
@@ -110,6 +111,14 @@ static int rocm_register(void)
                                            MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_coll_rocm_component.user_ipc);
+    (void) mca_base_component_var_register(c, "autotune",
+                                           "Large staged allreduces pick their scheme (push-gather or "
+                                           "pull) and grid by measurement: the first six calls of a size "
+                                           "bucket try one each, all ranks then take the fastest; 0 keeps "
+                                           "coll_rocm_allreduce_algorithm",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_coll_rocm_component.autotune);
     (void) mca_base_component_var_register(c, "residency",
                                            "Where blocking collectives run: 0 vote per call until the ranks "
                                            "agree coll_rocm_residency_lock times in a row, 1 device (host "
@@ -279,6 +288,8 @@ int mca_coll_rocm_module_enable(mca_coll_base_module_t *module, struct ompi_comm
     (void) ompi_amd_comm_set_param(m->dev_comm, "timeout_ms", mca_coll_rocm_component.timeout_ms);
     (void) ompi_amd_comm_set_param(m->dev_comm, "algorithm", mca_coll_rocm_component.algorithm);
     (void) ompi_amd_comm_set_param(m->dev_comm, "user_ipc", mca_coll_rocm_component.user_ipc);
+    /* last: setting the scheme turns autotuning off */
+    (void) ompi_amd_comm_set_param(m->dev_comm, "autotune", mca_coll_rocm_component.autotune);
     if (ROCM_RES_DEVICE == mca_coll_rocm_component.residency ||
         ROCM_RES_HOST == mca_coll_rocm_component.residency) {
         m->mode = mca_coll_rocm_component.residency;

@@ -404,6 +404,47 @@ def case_zero_counts(comm, rank, n, salt):
     return case_allreduce(comm, rank, n, F, SUM, 4099, salt)
 
 
+def case_autotune(comm, rank, n, salt, big):
+    """param "autotune" (coll/rocm's default): the first six large blocking
+    allreduces of a size bucket run one candidate each (push-gather and
+    staged pull x 1024 / 512 / 256 blocks), the sixth decides — on every
+    rank alike — and later calls run the choice; every result bit-exact
+    against the oracle on dataset R (the fold order is the same whatever
+    the scheme), in place too, and a nonblocking allreduce of the same size
+    posted meanwhile keeps the default scheme."""
+    F, SUM = mop.MPI_FLOAT, mop.MPI_SUM
+    count = big + 11
+    comm.set_param("autotune", 1)
+    try:
+        for i in range(9):
+            if i == 3:  # a nonblocking call in the middle of the tuning
+                xs = [inputs(F, count, r, salt + 50) for r in range(n)]
+                exp, _ = orc.allreduce([x.copy() for x in xs], count, SUM.index, F.code)
+                sb = to_dev(xs[rank])
+                ob = torch.zeros_like(sb)
+                req = comm.iallreduce(sb, ob, count, F, SUM)
+                req.wait()
+                req.free()
+                got = ob.cpu().numpy().view(np.float32)
+                if not np.array_equal(got.view(np.uint32), exp[rank].view(np.uint32)):
+                    return False, "iallreduce during the tuning differs"
+            ok, msg = case_allreduce(comm, rank, n, F, SUM, count, salt + i, inplace=(i % 3 == 2))
+            if not ok:
+                return False, f"call {i}: {msg}"
+            state = comm.get_param("autotune_state")
+            if state != (1 if i < 5 else 2):
+                return False, f"call {i}: autotune_state {state}"
+        choice = (comm.get_param("autotune_algorithm"), comm.get_param("autotune_blocks"))
+        times = [comm.get_param(f"autotune_us{k}") for k in range(6)]
+        everyone = [None] * n
+        dist.all_gather_object(everyone, (choice, times))
+        if any(e != everyone[0] for e in everyone):
+            return False, f"ranks chose differently: {everyone}"
+        return True, f"choice {choice}, worst-rank us per candidate {times}"
+    finally:
+        comm.set_param("autotune", 0)
+
+
 def case_regrow(comm, rank, n, salt):
     """Landing-buffer growth several times in a row (large scans of rising
     size, an in-place reduce_scatter in between), every result checked."""
@@ -766,6 +807,10 @@ def report(rank, n, obj):
     """One JSON line per case on stdout (read by the test) and, when
     COLL_LOG_DIR is set, appended to a per-rank file there (progress that a
     watchdog on the GPU box can see while the test still runs)."""
+    try:  # process resources after the case (diagnostics for IPC open failures)
+        obj.setdefault("fds", len(os.listdir("/proc/self/fd")))
+    except OSError:
+        pass
     line = json.dumps(obj)
     print(line, flush=True)
     d = os.environ.get("COLL_LOG_DIR")
@@ -915,6 +960,7 @@ def main():
     ]
     cases += [
         ("zero_counts_every_entry_point", lambda: case_zero_counts(comm, rank, n, 96)),
+        ("autotune_large_allreduce", lambda: case_autotune(comm, rank, n, 97, big)),
         ("iallreduce_mixed", lambda: case_iallreduce(comm, rank, n, 90)),
         ("iallreduce_many_outstanding", lambda: case_iallreduce_many(comm, rank, n, 94)),
         ("persistent_small", lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, 3001, 80)),

@@ -803,7 +803,14 @@ def main():
         except Exception as e:  # noqa: BLE001 - reported per case
             ok, msg = False, f"{type(e).__name__}: {e}\n{traceback.format_exc()[-1200:]}"
         all_ok &= bool(ok)
-        line = json.dumps({"rank": rank, "case": name, "ok": bool(ok), "msg": msg})
+        # process resources after the case (diagnostics for IPC open failures)
+        try:
+            fds = len(os.listdir("/proc/self/fd"))
+        except OSError:
+            fds = -1
+        line = json.dumps({"rank": rank, "case": name, "ok": bool(ok), "msg": msg, "fds": fds,
+                           "ipc_live": comm.get_param("ipc_live"),
+                           "ipc_opens": comm.get_param("ipc_opens")})
         print(line, flush=True)
         if os.environ.get("COLL_LOG_DIR"):  # progress visible while the test runs
             os.makedirs(os.environ["COLL_LOG_DIR"], exist_ok=True)
