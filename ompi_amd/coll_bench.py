@@ -16,7 +16,12 @@ import os
 import time
 
 
-_PHASE = {"what": None, "t0": 0.0}
+_PHASE = {"what": None, "t0": 0.0, "pending": None}
+# An extras phase (after the headline was measured) that runs longer than
+# this is taken as stuck: every rank's watchdog ends its process, and rank 0
+# first prints the headline line it already holds, so a hang in a side row
+# never costs the driver the headline.
+EXTRAS_PHASE_LIMIT_S = float(os.environ.get("OMPI_AMD_BENCH_EXTRAS_LIMIT_S", "240"))
 
 
 def _progress(rank, what):
@@ -30,7 +35,10 @@ def _progress(rank, what):
 
 def _watchdog(comm, rank, world):
     """Every rank: a phase running over 30 s prints the communicator's epoch
-    and (OMPI_AMD_DEBUG_PROGRESS=1) its barrier progress record."""
+    and (OMPI_AMD_DEBUG_PROGRESS=1) its barrier progress record; an extras
+    phase past EXTRAS_PHASE_LIMIT_S ends the process (rank 0 prints the
+    headline line first)."""
+    import json
     import sys
     import threading
 
@@ -48,6 +56,14 @@ def _watchdog(comm, rank, world):
                     pass
             print(f"[bench watchdog rank {rank}] {what} running {time.time() - t0:.0f} s: {vals}",
                   file=sys.stderr, flush=True)
+            pending = _PHASE["pending"]
+            if pending is not None and time.time() - t0 > EXTRAS_PHASE_LIMIT_S:
+                if rank == 0:
+                    pending["extras_error"] = (f"watchdog: '{what}' still running after "
+                                               f"{time.time() - t0:.0f} s; extras abandoned")
+                    print(json.dumps(dict(pending)), flush=True)
+                sys.stderr.flush()
+                os._exit(0)
 
     threading.Thread(target=run, daemon=True).start()
 
@@ -105,42 +121,19 @@ def bench_allreduce(args, metric: str, link_gbs: float):
     # (coll_rocm_user_ipc 0) with coll_rocm_autotune 1 — the library itself
     # measures its staged schemes x grids on the first calls of a size and
     # keeps the fastest (ompi_amd_allreduce); the bench
-    # never picks.  Every scheme, user-IPC ones included, is also measured
-    # beside it (each first checked bit-exact on dataset E at this size)
-    # and reported under config.schemes only.
+    # never picks.  Every scheme, user-IPC ones included, is measured after
+    # the headline, among the extras (each first checked bit-exact on
+    # dataset E at this size), and reported under config.schemes only.
     S = n * 4
     factor = 2.0 * (world - 1) / world
     default = {"algorithm": comm.get_param("algorithm"), "user_ipc": comm.get_param("user_ipc"),
                "blocks": comm.get_param("blocks")}
     default_name = (f"{dict(ALGORITHMS)[default['algorithm']]}/"
                     f"{'user' if default['user_ipc'] else 'staged'}/{default['blocks']}")
-    schemes = {}
-    if not os.environ.get("OMPI_AMD_BENCH_NO_SCHEMES"):
-        # ipc "staged": peers read library-owned memory (shadow arena /
-        # landing buffers; the default, user_ipc = 0); "user": peers map the
-        # caller's x / y directly (user_ipc = 1; these buffers live for the
-        # whole run, so no mapping goes stale)
-        for ipc in ("staged", "user"):
-            comm.set_param("user_ipc", 1 if ipc == "user" else 0)
-            for a, name in ALGORITHMS:
-                comm.set_param("algorithm", a)
-                comm.set_param("blocks", default["blocks"])
-                _progress(rank, f"scheme {name}/{ipc}: exactness check")
-                exact = _exact_ok(comm, dist, torch, mop, n, rank, shared)
-                _progress(rank, f"scheme {name}/{ipc}: bit_exact={exact}, timing {len(BLOCKS)} grids")
-                for blocks in BLOCKS:
-                    comm.set_param("blocks", blocks)
-                    ta = _timed(ours, 5, 2, dist, torch, tdev) / 5
-                    schemes[f"{name}/{ipc}/{blocks}"] = {
-                        "algorithm": a, "ipc": ipc, "blocks": blocks, "bit_exact": exact,
-                        "us": round(ta * 1e6, 2), "busbw": round(S / ta * factor / 1e9, 2)}
-    comm.set_param("user_ipc", default["user_ipc"])
-    comm.set_param("algorithm", default["algorithm"])
-    comm.set_param("blocks", default["blocks"])
     best = {"algorithm": default["algorithm"]}
     best_name = default_name
-    # coll/rocm ships coll_rocm_autotune = 1 (setting a scheme above turned
-    # it off, as it does in the library): the first calls of this size try
+    # coll/rocm ships coll_rocm_autotune = 1 (a communicator built outside
+    # the MCA glue starts with it off): the first calls of this size try
     # the candidates, every rank then runs the one whose slowest rank was
     # fastest — what an MPI job gets from its first allreduces of this size
     autotune = None
@@ -233,7 +226,7 @@ def bench_allreduce(args, metric: str, link_gbs: float):
                    "library_default_scheme": default_name, "autotune": autotune,
                    "bit_exact_dataset_E": default_exact,
                    "ipc_mode_legacy": comm.get_param("ipc_mode_legacy"),
-                   "schemes": schemes},
+                   "schemes": {}},
         "roofline": {"bound": "xgmi", "achieved": red_gbs,
                      "peak": roof, "unit": "GB/s",
                      "frac": round(red_gbs / roof, 4) if red_gbs else None,
@@ -258,8 +251,12 @@ def bench_allreduce(args, metric: str, link_gbs: float):
         dist.barrier()
     if not args.no_extras:
         # the extras allocate buffers per size: the library default (staged)
-        comm.set_param("user_ipc", 0)
+        _PHASE["pending"] = res
         try:
+            if not os.environ.get("OMPI_AMD_BENCH_NO_SCHEMES"):
+                res["config"]["schemes"] = _schemes(comm, dist, torch, mop, n, rank, shared,
+                                                    tdev, ours, default)
+            comm.set_param("user_ipc", 0)
             _progress(rank, "extras: check")
             res["check"] = _check_exact(comm, dist, torch, mop, n, rank, shared)
             _progress(rank, "extras: sweep")
@@ -274,10 +271,44 @@ def bench_allreduce(args, metric: str, link_gbs: float):
             res["p2p_osc"] = _p2p_osc_rows(comm, dist, torch, mop, world, rank, tdev)
         except Exception as e:  # extras never break the headline line
             res["extras_error"] = f"{type(e).__name__}: {e}"
+        _PHASE["pending"] = None
     comm.free()
     dist.barrier()
     dist.destroy_process_group()
     return res if rank == 0 else None
+
+
+def _schemes(comm, dist, torch, mop, n, rank, shared, tdev, ours, default):
+    """Every data-movement scheme x transfer grid, measured after the
+    headline (config.schemes only; the headline is the library default).
+    ipc "staged": peers read library-owned memory (shadow arena / landing
+    buffers; the default, user_ipc = 0); "user": peers map the caller's
+    x / y directly (user_ipc = 1; these buffers live for the whole run, so
+    no mapping goes stale).  Each scheme is first checked bit-exact on
+    dataset E at this size."""
+    S = n * 4
+    world = dist.get_world_size()
+    factor = 2.0 * (world - 1) / world
+    schemes = {}
+    for ipc in ("staged", "user"):
+        comm.set_param("user_ipc", 1 if ipc == "user" else 0)
+        for a, name in ALGORITHMS:
+            comm.set_param("algorithm", a)
+            comm.set_param("blocks", default["blocks"])
+            _progress(rank, f"extras: scheme {name}/{ipc}: exactness check")
+            exact = _exact_ok(comm, dist, torch, mop, n, rank, shared)
+            _progress(rank, f"extras: scheme {name}/{ipc}: bit_exact={exact}, "
+                            f"timing {len(BLOCKS)} grids")
+            for blocks in BLOCKS:
+                comm.set_param("blocks", blocks)
+                ta = _timed(ours, 5, 2, dist, torch, tdev) / 5
+                schemes[f"{name}/{ipc}/{blocks}"] = {
+                    "algorithm": a, "ipc": ipc, "blocks": blocks, "bit_exact": exact,
+                    "us": round(ta * 1e6, 2), "busbw": round(S / ta * factor / 1e9, 2)}
+    comm.set_param("user_ipc", default["user_ipc"])
+    comm.set_param("algorithm", default["algorithm"])
+    comm.set_param("blocks", default["blocks"])
+    return schemes
 
 
 def cpu_baseline_ring(world: int, nbytes: int, factor: float, seconds: float = 10.0) -> dict:
