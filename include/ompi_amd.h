@@ -50,8 +50,13 @@ enum {
     OMPI_AMD_TYPE_INT16_T = 2, OMPI_AMD_TYPE_UINT16_T = 3,
     OMPI_AMD_TYPE_INT32_T = 4, OMPI_AMD_TYPE_UINT32_T = 5,
     OMPI_AMD_TYPE_INT64_T = 6, OMPI_AMD_TYPE_UINT64_T = 7,
+    /* short float = opal_short_float_t (_Float16 wherever the compiler has
+     * it, config/opal_check_alt_short_float.m4:27-35); its complex is
+     * opal_short_float_t[2] (MPIX_C_FLOAT16 / MPIX_C_FLOAT16_COMPLEX) */
+    OMPI_AMD_TYPE_SHORT_FLOAT = 14,
     OMPI_AMD_TYPE_FLOAT = 15, OMPI_AMD_TYPE_DOUBLE = 16,
     OMPI_AMD_TYPE_BOOL = 25,
+    OMPI_AMD_TYPE_C_SHORT_FLOAT_COMPLEX = 26,
     OMPI_AMD_TYPE_C_FLOAT_COMPLEX = 27, OMPI_AMD_TYPE_C_DOUBLE_COMPLEX = 28,
     OMPI_AMD_TYPE_BYTE = 30,
     OMPI_AMD_TYPE_FLOAT_INT = 34, OMPI_AMD_TYPE_DOUBLE_INT = 35,

@@ -93,6 +93,36 @@ __device__ __forceinline__ cplx<R> operator*(cplx<R> x, cplx<R> y) {
     return {re, im};
 }
 
+// Short float (opal_short_float_t = _Float16, the MPIX_C_FLOAT16 extension)
+// and its complex, opal_short_float_t[2]: op/base has no `short float
+// _Complex`, so it reduces the pair with COMPLEX_SUM_FUNC / COMPLEX_PROD_FUNC
+// (op_base_functions.c:112-147, 3-buffer :739-775):
+//   sum   re = x.re + y.re, im = x.im + y.im
+//   prod  re = y.re*x.re - y.im*x.im, im = y.re*x.im + y.im*x.re
+// (y = in / in2 on the left as the reference writes it; every term below is
+// commutative bit for bit).  On the x86-64 hosts MI355X nodes run, gcc and
+// clang evaluate _Float16 expressions in float (excess precision, rounded
+// once at the assignment): the products of two halves are exact in float
+// (11 + 11 significant bits), the sum or difference rounds once to float,
+// then to half.  The device does exactly that, so the result is the x86
+// reference's bit for bit.  Real short float +, * and the compares are
+// correctly rounded either way (float's 24 bits >= 2 x 11 + 2: rounding to
+// float and then to half equals rounding to half once), so v_add_f16 /
+// v_mul_f16 give the same bits as the host's float evaluation.
+using half_t = _Float16;
+struct chalf_t {
+    half_t re, im;
+};
+static_assert(sizeof(chalf_t) == 4, "short float complex ABI");
+__device__ __forceinline__ chalf_t operator+(chalf_t x, chalf_t y) {
+    return {(half_t)(x.re + y.re), (half_t)(x.im + y.im)};
+}
+__device__ __forceinline__ chalf_t operator*(chalf_t x, chalf_t y) {
+    const float a = (float)x.re, b = (float)x.im, c = (float)y.re, d = (float)y.im;
+    // exact products: contraction into an fma cannot change the result
+    return {(half_t)(c * a - d * b), (half_t)(c * b + d * a)};
+}
+
 template <typename T> struct is_pair { static constexpr bool value = false; };
 template <> struct is_pair<float_int_t> { static constexpr bool value = true; };
 template <> struct is_pair<double_int_t> { static constexpr bool value = true; };
@@ -110,6 +140,7 @@ template <> struct type_of<OMPI_AMD_TYPE_INT32_T> { using type = int32_t; };
 template <> struct type_of<OMPI_AMD_TYPE_UINT32_T> { using type = uint32_t; };
 template <> struct type_of<OMPI_AMD_TYPE_INT64_T> { using type = int64_t; };
 template <> struct type_of<OMPI_AMD_TYPE_UINT64_T> { using type = uint64_t; };
+template <> struct type_of<OMPI_AMD_TYPE_SHORT_FLOAT> { using type = half_t; };
 template <> struct type_of<OMPI_AMD_TYPE_FLOAT> { using type = float; };
 template <> struct type_of<OMPI_AMD_TYPE_DOUBLE> { using type = double; };
 template <> struct type_of<OMPI_AMD_TYPE_BOOL> { using type = bool; };
@@ -119,22 +150,28 @@ template <> struct type_of<OMPI_AMD_TYPE_DOUBLE_INT> { using type = double_int_t
 template <> struct type_of<OMPI_AMD_TYPE_LONG_INT> { using type = long_int_t; };
 template <> struct type_of<OMPI_AMD_TYPE_2INT> { using type = two_int_t; };
 template <> struct type_of<OMPI_AMD_TYPE_SHORT_INT> { using type = short_int_t; };
+template <> struct type_of<OMPI_AMD_TYPE_C_SHORT_FLOAT_COMPLEX> { using type = chalf_t; };
 template <> struct type_of<OMPI_AMD_TYPE_C_FLOAT_COMPLEX> { using type = cfloat_t; };
 template <> struct type_of<OMPI_AMD_TYPE_C_DOUBLE_COMPLEX> { using type = cdouble_t; };
 
 // Which (op,type) slots exist — the op/base table pattern
 // (op_base_functions.c:1485-1569) restricted to the predefined C types.
 __host__ __device__ constexpr bool is_c_int(int t) { return t >= 0 && t <= 7; }
-__host__ __device__ constexpr bool is_fp(int t) { return t == OMPI_AMD_TYPE_FLOAT || t == OMPI_AMD_TYPE_DOUBLE; }
+__host__ __device__ constexpr bool is_fp(int t) {
+    return t == OMPI_AMD_TYPE_SHORT_FLOAT || t == OMPI_AMD_TYPE_FLOAT || t == OMPI_AMD_TYPE_DOUBLE;
+}
 __host__ __device__ constexpr bool is_pair_type(int t) {
     return t == OMPI_AMD_TYPE_FLOAT_INT || t == OMPI_AMD_TYPE_DOUBLE_INT ||
            t == OMPI_AMD_TYPE_LONG_INT || t == OMPI_AMD_TYPE_2INT || t == OMPI_AMD_TYPE_SHORT_INT;
 }
 __host__ __device__ constexpr bool is_c_complex(int t) {
-    return t == OMPI_AMD_TYPE_C_FLOAT_COMPLEX || t == OMPI_AMD_TYPE_C_DOUBLE_COMPLEX;
+    return t == OMPI_AMD_TYPE_C_SHORT_FLOAT_COMPLEX || t == OMPI_AMD_TYPE_C_FLOAT_COMPLEX ||
+           t == OMPI_AMD_TYPE_C_DOUBLE_COMPLEX;
 }
-// (op/base's COMPLEX(sum|prod) rows, :1509/:1516/:1596/:1603; long double
-// complex stays with op/base: gfx950 has no long double)
+// (op/base's FLOATING_POINT and COMPLEX(sum|prod) rows,
+// op_base_functions.c:1400-1406, 1432-1436, as filled when configure finds
+// _Float16; long double and its complex stay with op/base: gfx950 has no
+// long double)
 __host__ __device__ constexpr bool slot_supported(int op, int t) {
     return (op == OMPI_AMD_OP_SUM || op == OMPI_AMD_OP_PROD) && is_c_complex(t) ? true
          : (op == OMPI_AMD_OP_MAX || op == OMPI_AMD_OP_MIN || op == OMPI_AMD_OP_SUM ||

@@ -400,8 +400,11 @@ size_t ompi_amd_type_extent(int type) {
     switch (type) {
     case OMPI_AMD_TYPE_INT8_T: case OMPI_AMD_TYPE_UINT8_T: case OMPI_AMD_TYPE_BOOL:
     case OMPI_AMD_TYPE_BYTE: return 1;
-    case OMPI_AMD_TYPE_INT16_T: case OMPI_AMD_TYPE_UINT16_T: return 2;
-    case OMPI_AMD_TYPE_INT32_T: case OMPI_AMD_TYPE_UINT32_T: case OMPI_AMD_TYPE_FLOAT: return 4;
+    case OMPI_AMD_TYPE_INT16_T: case OMPI_AMD_TYPE_UINT16_T: case OMPI_AMD_TYPE_SHORT_FLOAT:
+        return 2;
+    case OMPI_AMD_TYPE_INT32_T: case OMPI_AMD_TYPE_UINT32_T: case OMPI_AMD_TYPE_FLOAT:
+    case OMPI_AMD_TYPE_C_SHORT_FLOAT_COMPLEX:
+        return 4;
     case OMPI_AMD_TYPE_INT64_T: case OMPI_AMD_TYPE_UINT64_T: case OMPI_AMD_TYPE_DOUBLE: return 8;
     case OMPI_AMD_TYPE_C_FLOAT_COMPLEX: return sizeof(cfloat_t);
     case OMPI_AMD_TYPE_C_DOUBLE_COMPLEX: return sizeof(cdouble_t);

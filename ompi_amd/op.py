@@ -75,6 +75,11 @@ MPI_INT32_T = Datatype("MPI_INT32_T", 4, 4, 4, np.dtype(np.int32))
 MPI_UINT32_T = Datatype("MPI_UINT32_T", 5, 4, 4, np.dtype(np.uint32))
 MPI_INT64_T = Datatype("MPI_INT64_T", 6, 8, 8, np.dtype(np.int64))
 MPI_UINT64_T = Datatype("MPI_UINT64_T", 7, 8, 8, np.dtype(np.uint64))
+# MPIX_C_FLOAT16 (opal_short_float_t = _Float16) and its complex,
+# opal_short_float_t[2] (no numpy complex32: a (re, im) record of halves)
+MPIX_C_FLOAT16 = Datatype("MPIX_C_FLOAT16", 14, 2, 2, np.dtype(np.float16))
+MPIX_C_FLOAT16_COMPLEX = Datatype("MPIX_C_FLOAT16_COMPLEX", 26, 4, 4,
+                                  np.dtype([("re", np.float16), ("im", np.float16)]))
 MPI_FLOAT = Datatype("MPI_FLOAT", 15, 4, 4, np.dtype(np.float32))
 MPI_DOUBLE = Datatype("MPI_DOUBLE", 16, 8, 8, np.dtype(np.float64))
 MPI_C_BOOL = Datatype("MPI_C_BOOL", 25, 1, 1, np.dtype(np.uint8))
@@ -91,8 +96,8 @@ MPI_INT = MPI_INT32_T
 MPI_LONG = MPI_INT64_T
 
 DATATYPES = [MPI_INT8_T, MPI_UINT8_T, MPI_INT16_T, MPI_UINT16_T, MPI_INT32_T,
-             MPI_UINT32_T, MPI_INT64_T, MPI_UINT64_T, MPI_FLOAT, MPI_DOUBLE,
-             MPI_C_BOOL, MPI_C_FLOAT_COMPLEX, MPI_C_DOUBLE_COMPLEX, MPI_BYTE, MPI_FLOAT_INT, MPI_DOUBLE_INT, MPI_LONG_INT,
+             MPI_UINT32_T, MPI_INT64_T, MPI_UINT64_T, MPIX_C_FLOAT16, MPI_FLOAT, MPI_DOUBLE,
+             MPI_C_BOOL, MPIX_C_FLOAT16_COMPLEX, MPI_C_FLOAT_COMPLEX, MPI_C_DOUBLE_COMPLEX, MPI_BYTE, MPI_FLOAT_INT, MPI_DOUBLE_INT, MPI_LONG_INT,
              MPI_2INT, MPI_SHORT_INT]
 BY_CODE = {d.code: d for d in DATATYPES}
 

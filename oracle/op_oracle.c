@@ -24,6 +24,19 @@
  *   of the product (x = ac - bd, y = ad + bc, libgcc's __mul?c3 recovery
  *   when both are NaN, ISO C Annex G.5.1) is what the reference computes.
  *
+ *   Short float (opal_short_float_t = _Float16 wherever configure finds
+ *   it, config/opal_check_alt_short_float.m4:27-35): SUM/PROD/MAX/MIN
+ *   (:184-187, :247-250, :307-310, :376-379, 3-buffer :813-815, :876-878,
+ *   :936-938, :1005-1007) and its complex, opal_short_float_t[2], SUM/PROD
+ *   through COMPLEX_SUM_FUNC / COMPLEX_PROD_FUNC (:112-147, :334-337,
+ *   :403-406, 3-buffer :739-775, :963-965, :1032-1034):
+ *     re = a.re*b.re - a.im*b.im, im = a.re*b.im + a.im*b.re  (a = in)
+ *   An x86-64 gcc/clang build evaluates _Float16 expressions in float and
+ *   rounds once at the assignment (no native half arithmetic below
+ *   AVX512-FP16); restated here with explicit float arithmetic and
+ *   orc_f2h.  For a single +, * that equals rounding to half directly
+ *   (24 >= 2*11 + 2 bits), for the complex product it is the x86 result.
+ *
  * Note the NaN / signed-zero consequences (pinned in tests/golden):
  * MAX(out=x, in=NaN) = NaN, MAX(out=NaN, in=3) = 3, MAX(out=+0,in=-0) = -0.
  * LOC handlers only write v and k, never the struct padding.
@@ -44,8 +57,8 @@ size_t orc_type_extent(int type)
 {
     switch (type) {
     case ORC_T_INT8: case ORC_T_UINT8: case ORC_T_BOOL: case ORC_T_BYTE: return 1;
-    case ORC_T_INT16: case ORC_T_UINT16: return 2;
-    case ORC_T_INT32: case ORC_T_UINT32: case ORC_T_FLOAT: return 4;
+    case ORC_T_INT16: case ORC_T_UINT16: case ORC_T_SHORT_FLOAT: return 2;
+    case ORC_T_INT32: case ORC_T_UINT32: case ORC_T_FLOAT: case ORC_T_C_SHORT_FLOAT_COMPLEX: return 4;
     case ORC_T_INT64: case ORC_T_UINT64: case ORC_T_DOUBLE: return 8;
     case ORC_T_FLOAT_INT: return sizeof(orc_float_int_t);
     case ORC_T_DOUBLE_INT: return sizeof(orc_double_int_t);
@@ -59,8 +72,61 @@ size_t orc_type_extent(int type)
 }
 
 static int is_c_int(int t) { return t >= ORC_T_INT8 && t <= ORC_T_UINT64; }
-static int is_fp(int t) { return t == ORC_T_FLOAT || t == ORC_T_DOUBLE; }
-static int is_complex(int t) { return t == ORC_T_C_FLOAT_COMPLEX || t == ORC_T_C_DOUBLE_COMPLEX; }
+static int is_fp(int t) { return t == ORC_T_SHORT_FLOAT || t == ORC_T_FLOAT || t == ORC_T_DOUBLE; }
+static int is_complex(int t)
+{
+    return t == ORC_T_C_SHORT_FLOAT_COMPLEX || t == ORC_T_C_FLOAT_COMPLEX || t == ORC_T_C_DOUBLE_COMPLEX;
+}
+
+/* ---- binary16 ---- */
+float orc_h2f(uint16_t h)
+{
+    uint32_t s = (uint32_t)(h & 0x8000u) << 16, e = (h >> 10) & 0x1fu, m = h & 0x3ffu, x;
+    float f;
+    if (e == 0) {
+        if (m == 0) {
+            x = s;
+        } else { /* subnormal half: normalise into a float */
+            uint32_t sh = 0;
+            while (!(m & 0x400u)) { m <<= 1; sh++; }
+            x = s | ((113u - sh) << 23) | ((m & 0x3ffu) << 13);
+        }
+    } else if (e == 31) {
+        x = s | 0x7f800000u | (m << 13);
+    } else {
+        x = s | ((e + 112u) << 23) | (m << 13);
+    }
+    memcpy(&f, &x, 4);
+    return f;
+}
+
+uint16_t orc_f2h(float f)
+{
+    uint32_t x, ax, sign, e, m, q, rem, half;
+    int shift;
+    memcpy(&x, &f, 4);
+    sign = (x >> 16) & 0x8000u;
+    ax = x & 0x7fffffffu;
+    if (ax >= 0x7f800000u) /* inf; NaN stays NaN (quiet, top payload bits) */
+        return (uint16_t)(sign | (ax == 0x7f800000u ? 0x7c00u : 0x7e00u | ((ax >> 13) & 0x3ffu)));
+    if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u); /* >= 65520: inf */
+    if (ax >= 0x38800000u) { /* normal half: drop 13 bits, nearest even */
+        q = (ax - 0x38000000u) >> 13;
+        rem = ax & 0x1fffu;
+        q += (rem > 0x1000u || (rem == 0x1000u && (q & 1u))) ? 1u : 0u;
+        return (uint16_t)(sign | q);
+    }
+    e = ax >> 23;
+    if (e == 0) return (uint16_t)sign; /* float subnormal: far below 2^-25 */
+    m = (ax & 0x7fffffu) | 0x800000u;  /* value = m * 2^(e-150) = (m * 2^(e-126)) * 2^-24 */
+    shift = 126 - (int)e;
+    if (shift > 24) return (uint16_t)sign;
+    q = m >> shift;
+    rem = m & ((1u << shift) - 1u);
+    half = 1u << (shift - 1);
+    q += (rem > half || (rem == half && (q & 1u))) ? 1u : 0u;
+    return (uint16_t)(sign | q);
+}
 static int is_loc(int t)
 {
     return t == ORC_T_FLOAT_INT || t == ORC_T_DOUBLE_INT || t == ORC_T_LONG_INT ||
@@ -179,6 +245,55 @@ ORC_BIT_LOOPS(int64_t) ORC_BIT_LOOPS(uint64_t)
 typedef _Bool orc_bool; typedef char orc_byte;
 ORC_BIT_LOOPS(orc_bool) ORC_BIT_LOOPS(orc_byte)
 
+/* short float: float evaluation, one rounding (see the header comment) */
+static uint16_t h_arith(int op, uint16_t x, uint16_t y) /* x = out / in1, y = in / in2 */
+{
+    const float fx = orc_h2f(x), fy = orc_h2f(y);
+    switch (op) {
+    case ORC_OP_SUM: return orc_f2h(fx + fy);
+    case ORC_OP_PROD: return orc_f2h(fx * fy);
+    case ORC_OP_MAX: return (fx > fy) ? x : y;
+    default: return (fx < fy) ? x : y; /* MIN */
+    }
+}
+static void arith2_half(int op, const uint16_t *a, uint16_t *b, size_t n)
+{
+    size_t i;
+    for (i = 0; i < n; i++) b[i] = h_arith(op, b[i], a[i]);
+}
+static void arith3_half(int op, const uint16_t *x, const uint16_t *y, uint16_t *o, size_t n)
+{
+    size_t i;
+    for (i = 0; i < n; i++) o[i] = h_arith(op, x[i], y[i]);
+}
+/* opal_short_float_t[2]: COMPLEX_SUM_FUNC / COMPLEX_PROD_FUNC; a = in (2buff)
+ * or in1 (3buff), b = out (2buff) or in2 (3buff), written as the reference
+ * writes them */
+static void chalf(int op, const uint16_t *a, const uint16_t *b, uint16_t *o)
+{
+    const float a0 = orc_h2f(a[0]), a1 = orc_h2f(a[1]), b0 = orc_h2f(b[0]), b1 = orc_h2f(b[1]);
+    uint16_t r0, r1;
+    if (op == ORC_OP_SUM) {
+        r0 = orc_f2h(b0 + a0);
+        r1 = orc_f2h(b1 + a1);
+    } else {
+        r0 = orc_f2h(a0 * b0 - a1 * b1);
+        r1 = orc_f2h(a0 * b1 + a1 * b0);
+    }
+    o[0] = r0;
+    o[1] = r1;
+}
+static void cplx2_c16(int op, const uint16_t *a, uint16_t *b, size_t n)
+{
+    size_t i;
+    for (i = 0; i < n; i++) chalf(op, a + 2 * i, b + 2 * i, b + 2 * i);
+}
+static void cplx3_c16(int op, const uint16_t *x, const uint16_t *y, uint16_t *o, size_t n)
+{
+    size_t i;
+    for (i = 0; i < n; i++) chalf(op, x + 2 * i, y + 2 * i, o + 2 * i);
+}
+
 /* OP_FUNC / OP_FUNC_3BUF over the C complex types: SUM and PROD only */
 #define ORC_COMPLEX_LOOPS(NAME, T)                                             \
     static void cplx2_##NAME(int op, const T *a, T *b, size_t n)               \
@@ -232,6 +347,8 @@ int orc_op_2buff(int op, int type, const void *in, void *inout, size_t count)
         default: return -1;
         }
     }
+    if (type == ORC_T_C_SHORT_FLOAT_COMPLEX) { cplx2_c16(op, in, inout, count); return 0; }
+    if (type == ORC_T_SHORT_FLOAT) { arith2_half(op, in, inout, count); return 0; }
     if (type == ORC_T_C_FLOAT_COMPLEX) { cplx2_c32(op, in, inout, count); return 0; }
     if (type == ORC_T_C_DOUBLE_COMPLEX) { cplx2_c64(op, in, inout, count); return 0; }
     if (is_arith(op)) {
@@ -258,6 +375,8 @@ int orc_op_3buff(int op, int type, const void *in1, const void *in2, void *out,
         default: return -1;
         }
     }
+    if (type == ORC_T_C_SHORT_FLOAT_COMPLEX) { cplx3_c16(op, in1, in2, out, count); return 0; }
+    if (type == ORC_T_SHORT_FLOAT) { arith3_half(op, in1, in2, out, count); return 0; }
     if (type == ORC_T_C_FLOAT_COMPLEX) { cplx3_c32(op, in1, in2, out, count); return 0; }
     if (type == ORC_T_C_DOUBLE_COMPLEX) { cplx3_c64(op, in1, in2, out, count); return 0; }
     if (is_arith(op)) {

@@ -39,8 +39,9 @@ enum {
 enum {
     ORC_T_INT8 = 0, ORC_T_UINT8 = 1, ORC_T_INT16 = 2, ORC_T_UINT16 = 3,
     ORC_T_INT32 = 4, ORC_T_UINT32 = 5, ORC_T_INT64 = 6, ORC_T_UINT64 = 7,
+    ORC_T_SHORT_FLOAT = 14,
     ORC_T_FLOAT = 15, ORC_T_DOUBLE = 16, ORC_T_BOOL = 25,
-    ORC_T_C_FLOAT_COMPLEX = 27, ORC_T_C_DOUBLE_COMPLEX = 28, ORC_T_BYTE = 30,
+    ORC_T_C_SHORT_FLOAT_COMPLEX = 26, ORC_T_C_FLOAT_COMPLEX = 27, ORC_T_C_DOUBLE_COMPLEX = 28, ORC_T_BYTE = 30,
     ORC_T_FLOAT_INT = 34, ORC_T_DOUBLE_INT = 35, ORC_T_LONG_INT = 36,
     ORC_T_2INT = 37, ORC_T_SHORT_INT = 38,
     ORC_T_COUNT = 41
@@ -57,6 +58,11 @@ int    orc_op_2buff(int op, int type, const void *in, void *inout, size_t count)
 /* 3-buffer: out[i] = in1[i] (op) in2[i]      (*_3BUF macros) */
 int    orc_op_3buff(int op, int type, const void *in1, const void *in2,
                     void *out, size_t count);
+/* IEEE binary16 <-> binary32 (round to nearest even), the conversions an
+ * x86-64 build of op/base performs around its float evaluation of
+ * opal_short_float_t (_Float16) expressions */
+float    orc_h2f(uint16_t h);
+uint16_t orc_f2h(float f);
 
 /* ---- coll/base allreduce restatement (coll_base_allreduce.c) ---- */
 enum {

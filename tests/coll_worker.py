@@ -842,6 +842,7 @@ def main():
                      "legacy": comm.get_param("ipc_mode_legacy")})
     F, D, I32, I64, I8, DI = (mop.MPI_FLOAT, mop.MPI_DOUBLE, mop.MPI_INT32_T, mop.MPI_INT64_T,
                               mop.MPI_INT8_T, mop.MPI_DOUBLE_INT)
+    H = mop.MPIX_C_FLOAT16
     def user_ipc(fn, alg=0):  # zero-copy on the caller's own buffers (param "user_ipc")
         def run():
             comm.set_param("user_ipc", 1)
@@ -897,6 +898,13 @@ def main():
         ("ar_min_f32_specials_tree", lambda: case_allreduce(comm, rank, n, F, mop.MPI_MIN, 999, 11, "S")),
         ("ar_sum_f64_big", lambda: case_allreduce(comm, rank, n, D, mop.MPI_SUM, big // 2 + 3, 12)),
         ("ar_sum_i32", lambda: case_allreduce(comm, rank, n, I32, mop.MPI_SUM, 1000003, 13)),
+        # MPIX_C_FLOAT16 (opal_short_float_t): ring order at the zero-copy size,
+        # the fused path, MAX on specials
+        ("ar_sum_f16_big", lambda: case_allreduce(comm, rank, n, H, mop.MPI_SUM, 2 * big + 3, 180)),
+        ("ar_sum_f16_fused", lambda: case_allreduce(comm, rank, n, H, mop.MPI_SUM, 3001, 181)),
+        ("ar_max_f16_specials", lambda: case_allreduce(comm, rank, n, H, mop.MPI_MAX, 70001, 182, "S")),
+        ("reduce_sum_f16_big_root1",
+         lambda: case_reduce(comm, rank, n, H, mop.MPI_SUM, big + 1, 1 % n, 183)),
         ("ar_band_i64", lambda: case_allreduce(comm, rank, n, I64, mop.MPI_BAND, 77777, 14)),
         ("ar_prod_i8", lambda: case_allreduce(comm, rank, n, I8, mop.MPI_PROD, 50001, 15)),
         ("ar_maxloc_double_int", lambda: case_allreduce(comm, rank, n, DI, mop.MPI_MAXLOC, 262147, 16)),

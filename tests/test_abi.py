@@ -64,7 +64,9 @@ def test_type_extents():
     assert lib.ompi_amd_type_extent(35) == 16   # DOUBLE_INT
     assert lib.ompi_amd_type_extent(38) == 8    # SHORT_INT
     assert lib.ompi_amd_type_extent(15) == 4
-    assert lib.ompi_amd_type_extent(14) == 0    # short float: not provided
+    assert lib.ompi_amd_type_extent(14) == 2    # short float (_Float16)
+    assert lib.ompi_amd_type_extent(26) == 4    # short float complex (_Float16[2])
+    assert lib.ompi_amd_type_extent(24) == 0    # long double: not provided
 
 
 def test_argument_checks_before_any_device_call():

@@ -37,6 +37,9 @@ def from_dev(t, offset, nbytes) -> np.ndarray:
 def gen(dtype: mop.Datatype, n: int, seed: int) -> np.ndarray:
     rng = np.random.default_rng(seed)
     nd = dtype.np_dtype
+    if nd.names == ("re", "im"):  # short float complex: a record of two halves
+        h = np.dtype(np.float16)
+        return _cplx(gen(Datatype_like(h), n, seed * 2 + 1), gen(Datatype_like(h), n, seed * 2 + 2), nd)
     if nd.names:  # pair
         a = np.zeros(n, dtype=nd)
         vt = nd.fields["v"][0]
@@ -96,6 +99,8 @@ def _cplx(re: np.ndarray, im: np.ndarray, nd) -> np.ndarray:
 
 def same_bits(got: np.ndarray, exp: np.ndarray, dtype: mop.Datatype) -> bool:
     nd = dtype.np_dtype
+    if nd.names == ("re", "im"):
+        return same_bits(got.view(np.float16), exp.view(np.float16), Datatype_like(np.dtype(np.float16)))
     if nd.names:
         # pair types: compare the value and index bytes.  Padding bytes of a
         # struct take unspecified values when a member is stored (C11

@@ -270,3 +270,40 @@ def test_oracle_unpack_out_of_order_fixture(orc, golden, table):
         frag = packed[off:off + nbytes].copy()
         assert orc.unpack(u["blocks"], u["extent"], u["count"], frag, typed, off) == nbytes
     assert np.array_equal(typed, expected)
+
+
+def test_short_float_restatement(orc):
+    """binary16 in the oracle (MPIX_C_FLOAT16 / opal_short_float_t): the
+    half <-> float conversions equal numpy's IEEE ones (every half, and
+    floats around every half's midpoints), and SUM / PROD equal the exact
+    double result rounded once to half — so the x86 float evaluation the
+    oracle restates is correctly rounded for one +, *."""
+    import ctypes
+    L = orc.lib()
+    L.orc_h2f.restype, L.orc_h2f.argtypes = ctypes.c_float, [ctypes.c_uint16]
+    L.orc_f2h.restype, L.orc_f2h.argtypes = ctypes.c_uint16, [ctypes.c_float]
+    allh = np.arange(65536, dtype=np.uint16)
+    ref = allh.view(np.float16).astype(np.float32)
+    got = np.array([L.orc_h2f(int(h)) for h in allh], dtype=np.float32)
+    nan = np.isnan(ref)
+    assert np.array_equal(ref[~nan].view(np.uint32), got[~nan].view(np.uint32))
+    assert np.isnan(got[nan]).all()
+    rng = np.random.default_rng(14)
+    near = (ref[~nan][::7].view(np.uint32).astype(np.int64)[:, None] + np.arange(-2, 3)[None, :])
+    fs = np.concatenate([rng.integers(0, 2**32, 20000, dtype=np.uint64).astype(np.uint32),
+                         (near.ravel() & 0xffffffff).astype(np.uint32)]).view(np.float32)
+    fs = fs[~np.isnan(fs)]
+    with np.errstate(over="ignore"):
+        exp = fs.astype(np.float16).view(np.uint16)
+    assert np.array_equal(np.array([L.orc_f2h(float(f)) for f in fs], dtype=np.uint16), exp)
+    a = rng.integers(0, 65536, 50000, dtype=np.uint64).astype(np.uint16)
+    b = rng.integers(0, 65536, 50000, dtype=np.uint64).astype(np.uint16)
+    for op, fn in ((SUM, np.add), (PROD, np.multiply)):
+        out = b.copy()
+        orc.op_2buff(op, 14, a, out, len(a))
+        with np.errstate(over="ignore", invalid="ignore"):
+            e = fn(b.view(np.float16).astype(np.float64),
+                   a.view(np.float16).astype(np.float64)).astype(np.float16)
+        ok = ~np.isnan(e)
+        assert np.array_equal(out[ok], e.view(np.uint16)[ok]), op
+        assert np.isnan(out.view(np.float16)[~ok]).all()
