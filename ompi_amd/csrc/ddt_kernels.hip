@@ -316,12 +316,29 @@ __device__ __forceinline__ void pack_tiles(const ddt_period &P, const char *type
         const uintptr_t a0 = (uintptr_t)t0 & ~(uintptr_t)15;
         const uintptr_t a1 = ((uintptr_t)(t0 + (nj - 1) * P.pext + P.span) + 15) & ~(uintptr_t)15;
         const int64_t nv = (int64_t)(a1 - a0) / 16;
-        __syncthreads();  // map staged / previous tile's LDS reads done
-        for (int64_t v = t; v < nv; v += kDdtThreads)
-            reinterpret_cast<v4 *>(data)[v] =
-                __builtin_nontemporal_load(reinterpret_cast<const v4 *>(a0) + v);
-        __syncthreads();
         const int64_t toff = (int64_t)((uintptr_t)t0 - a0);
+        __syncthreads();  // map staged / previous tile's LDS reads done
+        if (IDENT && P.pext - P.psize >= 64) {
+            // a run per period with gaps of 64 B or more: only the 16-B
+            // vectors holding run bytes are read (the gap lines are never
+            // fetched; the LDS bytes under them are never assembled).  r =
+            // the vector's offset from the tile's first run, ph its phase in
+            // the period; it meets run k if ph < blen, run k+1 if it crosses
+            // the period end (pext <= 4096, so 32-bit arithmetic).
+            const uint32_t pe = (uint32_t)P.pext, bl = (uint32_t)P.psize;
+            for (int64_t v = t; v < nv; v += kDdtThreads) {
+                const int64_t r = 16 * v - toff;
+                const uint32_t ph = r < 0 ? 0u : (uint32_t)r % pe;
+                if (ph < bl || ph + 16 > pe)
+                    reinterpret_cast<v4 *>(data)[v] =
+                        __builtin_nontemporal_load(reinterpret_cast<const v4 *>(a0) + v);
+            }
+        } else {
+            for (int64_t v = t; v < nv; v += kDdtThreads)
+                reinterpret_cast<v4 *>(data)[v] =
+                    __builtin_nontemporal_load(reinterpret_cast<const v4 *>(a0) + v);
+        }
+        __syncthreads();
         const int64_t len = nj * P.psize;               // packed bytes of this tile
         char *c0 = contig + (jt * P.psize - start);     // its first packed byte
         const uintptr_t A0 = (uintptr_t)c0 & ~(uintptr_t)15;

@@ -95,6 +95,30 @@ def test_vector_config3(orc, bl):
         assert np.array_equal(packed[:dt.size].cpu().numpy(), exp), (bl, chunk)
 
 
+@pytest.mark.parametrize("bl,stride,shift", [(8, 16, 0), (8, 16, 8), (9, 19, 8), (16, 32, 24),
+                                             (5, 13, 4)])
+def test_vector_gapped_tile_pack(orc, bl, stride, shift):
+    """The staged pack skips the 16-B vectors of gaps of 64 B or more
+    (gap lines are never read): run phases that drift across 16 B (stride
+    19 / 13 doubles), a typed base off 16-B alignment by `shift` bytes, and
+    a 64 KiB-fragment train whose windows start mid-period; the gap bytes
+    hold random data that must never reach the packed stream."""
+    d = dd.predefined("MPI_DOUBLE")
+    count = (512 * 1024) // (8 * bl) + 3
+    dt = dd.type_vector(count, bl, stride, d)
+    span = span_of(dt, 1)
+    src = dev_bytes(span + shift, seed=stride)
+    src_np = src.cpu().numpy()[shift:shift + span]
+    exp = orc.pack(dt.runs, dt.extent, 1, src_np, 0, dt.size)
+    for chunk in (dt.size, 65536 + 8):
+        packed = dev_bytes(dt.size)
+        conv = dd.Convertor()
+        conv.prepare_for_send(dt, 1, src.data_ptr() + shift)
+        chunked(conv, conv.pack, packed.data_ptr(), dt.size, chunk)
+        torch.cuda.synchronize()
+        assert np.array_equal(packed[:dt.size].cpu().numpy(), exp), (bl, stride, shift, chunk)
+
+
 def test_struct_int_double_offsets(orc):
     i32, f64 = dd.predefined("MPI_INT"), dd.predefined("MPI_DOUBLE")
     dt = dd.type_struct([1, 1], [0, 8], [i32, f64])
