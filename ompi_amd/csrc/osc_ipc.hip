@@ -300,7 +300,7 @@ __global__ __launch_bounds__(kOscThreads) void acc_kernel(const T *__restrict__ 
 // (UNROLL in flight per lane) when src and dst share their phase mod 16,
 // else 4-B or 1-B granules; one acquire per workgroup, persistent grid (as
 // acc_kernel).
-template <int THREADS, int UNROLL, bool PIPE>
+template <int THREADS, int UNROLL>
 __global__ __launch_bounds__(THREADS) void xfer_kernel(const char *src, char *dst, int64_t bytes,
                                                        const uint32_t *gate) {
     if (!gate_open(gate)) return;
@@ -312,40 +312,7 @@ __global__ __launch_bounds__(THREADS) void xfer_kernel(const char *src, char *ds
     if (head > bytes) head = bytes;
     const int64_t nbody = (bytes - head) / g;
     const int64_t tid = (int64_t)blockIdx.x * THREADS + threadIdx.x;
-    if (g == 16 && PIPE) {
-        // software-pipelined: the loads of pass k+1 are issued before the
-        // stores of pass k, so no wave waits for its own store
-        // acknowledgements before its next loads (vmcnt counts both in
-        // order on gfx9)
-        const u32x4 *sv = reinterpret_cast<const u32x4 *>(src + head);
-        u32x4 *dv = reinterpret_cast<u32x4 *>(dst + head);
-        constexpr int64_t chunk = (int64_t)THREADS * UNROLL;
-        const int64_t stride = (int64_t)gridDim.x * chunk;
-        int64_t base = (int64_t)blockIdx.x * chunk + threadIdx.x;
-        u32x4 cur[UNROLL];
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            const int64_t i = base + (int64_t)u * THREADS;
-            if (i < nbody) cur[u] = __builtin_nontemporal_load(sv + i);
-        }
-        while (base < nbody) {
-            const int64_t nb = base + stride;
-            u32x4 nxt[UNROLL];
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                const int64_t i = nb + (int64_t)u * THREADS;
-                if (i < nbody) nxt[u] = __builtin_nontemporal_load(sv + i);
-            }
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) {
-                const int64_t i = base + (int64_t)u * THREADS;
-                if (i < nbody) __builtin_nontemporal_store(cur[u], dv + i);
-            }
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) cur[u] = nxt[u];
-            base = nb;
-        }
-    } else if (g == 16) {
+    if (g == 16) {
         const u32x4 *sv = reinterpret_cast<const u32x4 *>(src + head);
         u32x4 *dv = reinterpret_cast<u32x4 *>(dst + head);
         constexpr int64_t chunk = (int64_t)THREADS * UNROLL;
@@ -525,7 +492,12 @@ static int64_t osc_grid_cap() {
 
 // Copy shape: 256 threads x 4 16-B vectors per lane.  256x8, 256x16, 512x8,
 // 1024x4 and 1024x8 measured within noise of it (put 5.26-5.59 TB/s,
-// profiles/r03_xfer_shape_sweep.txt): bytes in flight are not the limit.
+// profiles/r03_xfer_shape_sweep.txt): bytes in flight are not the limit,
+// and neither is the store-acknowledgement wait (a software-pipelined body,
+// loads of pass k+1 before stores of pass k, measured the same: 0.726 vs
+// 0.722 of 8 TB/s, profiles/r03_xfer_probe.jsonl).  The limit is the grid:
+// one chunk per workgroup reaches 0.775 without an acquire but 0.456 with
+// one per workgroup, so the persistent grid (one acquire per CU) stays.
 constexpr int kXferThreads = 256, kXferUnroll = 4;
 
 int xfer_copy(const void *src, void *dst, size_t bytes, hipStream_t s, const uint32_t *gate) {
@@ -534,16 +506,9 @@ int xfer_copy(const void *src, void *dst, size_t bytes, hipStream_t s, const uin
     const int64_t per = (int64_t)kXferThreads * kXferUnroll;
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((units + per - 1) / per,
                                                                   osc_grid_cap()));
-    // OMPI_AMD_XFER_PIPE=1: the software-pipelined body (A/B measurement)
-    static const bool pipe = getenv("OMPI_AMD_XFER_PIPE") && atoi(getenv("OMPI_AMD_XFER_PIPE")) == 1;
-    if (pipe)
-        hipLaunchKernelGGL((xfer_kernel<kXferThreads, kXferUnroll, true>), dim3((unsigned)blocks),
-                           dim3(kXferThreads), 0, s, static_cast<const char *>(src),
-                           static_cast<char *>(dst), (int64_t)bytes, gate);
-    else
-        hipLaunchKernelGGL((xfer_kernel<kXferThreads, kXferUnroll, false>), dim3((unsigned)blocks),
-                           dim3(kXferThreads), 0, s, static_cast<const char *>(src),
-                           static_cast<char *>(dst), (int64_t)bytes, gate);
+    hipLaunchKernelGGL((xfer_kernel<kXferThreads, kXferUnroll>), dim3((unsigned)blocks),
+                       dim3(kXferThreads), 0, s, static_cast<const char *>(src),
+                       static_cast<char *>(dst), (int64_t)bytes, gate);
     return record_hip(hipGetLastError(), "xfer copy launch");
 }
 
