@@ -630,6 +630,21 @@ static hipError_t launch_vec(int G, const ddt_walk &v, const ddt_desc &d, const 
 // multi-element) and dense enough.  Returns false when the
 // generic / walker kernels should run instead.
 constexpr int64_t kTileMaxGap = 128;          // bytes of gap the tile reads through
+// Run periods (vector-like layouts), unpack: the tile never touches the
+// typed gaps (it reads the packed side and writes runs only), so a gap
+// costs nothing but LDS — vector bl64 (512-B runs, 512-B gaps) unpacks at
+// 5.10 TB/s through the tile vs 4.06 through the per-granule kernel.  The
+// pack keeps kTileMaxGap: its gap-skipping loads mask half the lanes, and
+// bl64 packed slower staged (3.74 vs 4.00 TB/s,
+// profiles/r03_ddt_run_maxgap_ab.jsonl).  OMPI_AMD_DDT_RUN_MAXGAP overrides
+// the unpack bound (128 = the round-2 behaviour).
+static int64_t run_max_gap() {
+    static const int64_t v = [] {
+        const char *e = getenv("OMPI_AMD_DDT_RUN_MAXGAP");
+        return e ? std::max<int64_t>(0, atoll(e)) : (int64_t)4096;
+    }();
+    return v;
+}
 constexpr int64_t kTileDataDefault = 16 << 10;  // LDS data bytes per workgroup (tuned)
 constexpr int64_t kTileMinWindow = 256 << 10;   // smaller windows: one generic launch
 
@@ -665,7 +680,8 @@ static bool tile_period(const ompi_amd_ddt_t *ddt, size_t count, int G, bool unp
     const ddt_elem &x = ddt->host[0];
     if (ddt->host.size() == 1 && x.count > 1 && (G < 16 || tile_wide()) &&
         (count == 1 || ddt->extent == x.count * x.stride) && x.stride > 0 &&
-        x.stride - x.blen <= kTileMaxGap && x.stride <= tile_data_bytes() / 4) {
+        x.stride - x.blen <= (unpack ? run_max_gap() : kTileMaxGap) &&
+        x.stride <= tile_data_bytes() / 4) {
         ident = true;  // period = one run
         P.psize = x.blen;
         P.pext = x.stride;
