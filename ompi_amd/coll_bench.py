@@ -135,13 +135,14 @@ def bench_allreduce(args, metric: str, link_gbs: float):
     # coll/rocm ships coll_rocm_autotune = 1 (a communicator built outside
     # the MCA glue starts with it off): the first calls of this size try
     # the candidates, every rank then runs the one whose slowest rank was
-    # fastest — what an MPI job gets from its first allreduces of this size
+    # fastest (each candidate's best of two rounds) — what an MPI job gets
+    # from its first allreduces of this size
     autotune = None
     if not os.environ.get("OMPI_AMD_BENCH_NO_AUTOTUNE"):
         comm.set_param("autotune", 1)
         _progress(rank, "autotune: one call per candidate")
         calls = 0
-        while calls < 12:
+        while calls < 16:  # 6 candidates x 2 rounds decide at the 12th
             ours()
             torch.cuda.synchronize()
             calls += 1

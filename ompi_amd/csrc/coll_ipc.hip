@@ -327,24 +327,27 @@ struct ompi_amd_request {
 
 // ------------------------------------------------------------------ comm
 // Autotuning of large staged allreduces (param "autotune"): the first
-// kTuneCands blocking calls of a size bucket run one candidate (scheme x
-// grid) each, timed with events on the call's stream; at the last one the
+// kTuneRounds x kTuneCands blocking calls of a size bucket run the
+// candidates (scheme x grid) in turn, each call timed with events on its
+// stream; a candidate's time is its best round (the bucket's first call
+// also pays the one-time setup — landing growth, peer mappings — and any
+// call may include host skew between the ranks).  At the last call the
 // ranks allgather their times and every rank takes the candidate whose
 // slowest rank was fastest — the same choice everywhere, since every rank
 // makes the same calls.  coll/tuned's dynamic rules pick from a table;
 // this picks from measurements on the machine it runs on (xGMI loads vs
 // stores and the grid that saturates the links are not knowable offline).
-constexpr int kTuneCands = 6;
+constexpr int kTuneCands = 6, kTuneRounds = 2, kTuneCalls = kTuneCands * kTuneRounds;
 struct tune_cand {
     int algorithm, blocks;
 };
 static const tune_cand kTune[kTuneCands] = {{2, 1024}, {2, 512}, {2, 256},
                                             {0, 1024}, {0, 512}, {0, 256}};
 struct tune_bucket {
-    int next = 0;
+    int next = 0;  // calls made so far; call k runs candidate k % kTuneCands
     bool done = false;
     int choice = 0;
-    hipEvent_t ev[2 * kTuneCands] = {};
+    hipEvent_t ev[2 * kTuneCalls] = {};
     float worst_ms[kTuneCands] = {};
 };
 
@@ -2418,8 +2421,8 @@ int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
         const int key = 63 - __builtin_clzll((unsigned long long)bytes);
         tb = &c->tune[key];
         c->tune_last_key = key;
-        cand = tb->done ? -1 : tb->next;
-        const tune_cand &tc = kTune[tb->done ? tb->choice : cand];
+        cand = tb->done ? -1 : tb->next;  // the call's slot; candidate cand % kTuneCands
+        const tune_cand &tc = kTune[tb->done ? tb->choice : cand % kTuneCands];
         c->algorithm = tc.algorithm;
         c->max_blocks = tc.blocks;
         pp = params_of(c);
@@ -2435,14 +2438,16 @@ int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
     c->max_blocks = save_blocks;
     if (cand >= 0) {
         if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipEventRecord(tb->ev[2 * cand + 1], s), "autotune event");
-        if (++tb->next == kTuneCands) {  // every rank is at this call: decide together
+        if (++tb->next == kTuneCalls) {  // every rank is at this call: decide together
             float mine[kTuneCands], all[kMaxRanks][kTuneCands];
-            for (int k = 0; k < kTuneCands; ++k) {
-                mine[k] = 1e30f;
-                if (rc == OMPI_AMD_SUCCESS && hipEventSynchronize(tb->ev[2 * k + 1]) == hipSuccess &&
-                    hipEventElapsedTime(&mine[k], tb->ev[2 * k], tb->ev[2 * k + 1]) != hipSuccess)
-                    mine[k] = 1e30f;
+            for (int k = 0; k < kTuneCands; ++k) mine[k] = 1e30f;
+            for (int call = 0; call < kTuneCalls; ++call) {
+                float ms = 1e30f;
+                if (rc == OMPI_AMD_SUCCESS && hipEventSynchronize(tb->ev[2 * call + 1]) == hipSuccess &&
+                    hipEventElapsedTime(&ms, tb->ev[2 * call], tb->ev[2 * call + 1]) != hipSuccess)
+                    ms = 1e30f;
                 (void)hipGetLastError();
+                mine[call % kTuneCands] = std::min(mine[call % kTuneCands], ms);
             }
             const int arc = comm_allgather(c, mine, all, sizeof(mine));
             if (rc == OMPI_AMD_SUCCESS) rc = arc;

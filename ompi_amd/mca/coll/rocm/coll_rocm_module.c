@@ -113,8 +113,9 @@ static int rocm_register(void)
                                            &mca_coll_rocm_component.user_ipc);
     (void) mca_base_component_var_register(c, "autotune",
                                            "Large staged allreduces pick their scheme (push-gather or "
-                                           "pull) and grid by measurement: the first six calls of a size "
-                                           "bucket try one each, all ranks then take the fastest; 0 keeps "
+                                           "pull) and grid by measurement: the first twelve calls of a size "
+                                           "bucket try each of six candidates twice, all ranks then take the "
+                                           "fastest; 0 keeps "
                                            "coll_rocm_allreduce_algorithm",
                                            MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
                                            MCA_BASE_VAR_SCOPE_READONLY,

@@ -405,10 +405,11 @@ def case_zero_counts(comm, rank, n, salt):
 
 
 def case_autotune(comm, rank, n, salt, big):
-    """param "autotune" (coll/rocm's default): the first six large blocking
-    allreduces of a size bucket run one candidate each (push-gather and
-    staged pull x 1024 / 512 / 256 blocks), the sixth decides — on every
-    rank alike — and later calls run the choice; every result bit-exact
+    """param "autotune" (coll/rocm's default): the first twelve large
+    blocking allreduces of a size bucket run the six candidates twice each
+    (push-gather and staged pull x 1024 / 512 / 256 blocks; a candidate
+    counts its best round), the twelfth decides — on every rank alike — and
+    later calls run the choice; every result bit-exact
     against the oracle on dataset R (the fold order is the same whatever
     the scheme), in place too, and a nonblocking allreduce of the same size
     posted meanwhile keeps the default scheme."""
@@ -416,7 +417,7 @@ def case_autotune(comm, rank, n, salt, big):
     count = big + 11
     comm.set_param("autotune", 1)
     try:
-        for i in range(9):
+        for i in range(15):
             if i == 3:  # a nonblocking call in the middle of the tuning
                 xs = [inputs(F, count, r, salt + 50) for r in range(n)]
                 exp, _ = orc.allreduce([x.copy() for x in xs], count, SUM.index, F.code)
@@ -432,7 +433,7 @@ def case_autotune(comm, rank, n, salt, big):
             if not ok:
                 return False, f"call {i}: {msg}"
             state = comm.get_param("autotune_state")
-            if state != (1 if i < 5 else 2):
+            if state != (1 if i < 11 else 2):
                 return False, f"call {i}: autotune_state {state}"
         choice = (comm.get_param("autotune_algorithm"), comm.get_param("autotune_blocks"))
         times = [comm.get_param(f"autotune_us{k}") for k in range(6)]
