@@ -329,9 +329,10 @@ struct ompi_amd_request {
 // Autotuning of large staged allreduces (param "autotune"): the first
 // kTuneRounds x kTuneCands blocking calls of a size bucket run the
 // candidates (scheme x grid) in turn, each call timed with events on its
-// stream; a candidate's time is its best round (the bucket's first call
-// also pays the one-time setup — landing growth, peer mappings — and any
-// call may include host skew between the ranks).  At the last call the
+// stream after a device barrier (host skew between the ranks is not
+// timed); a candidate's time is its best round (the bucket's first call
+// also pays the one-time setup — landing growth, peer mappings).  At the
+// last call the
 // ranks allgather their times and every rank takes the candidate whose
 // slowest rank was fastest — the same choice everywhere, since every rank
 // makes the same calls.  coll/tuned's dynamic rules pick from a table;
@@ -2430,6 +2431,11 @@ int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
             for (int k = 0; k < 2; ++k)
                 if (!tb->ev[2 * cand + k])
                     TRY(record_hip(hipEventCreate(&tb->ev[2 * cand + k]), "autotune event"));
+            // a device barrier first, so the timed region starts with every
+            // rank present: host skew between the ranks' calls is not
+            // charged to the candidate (every rank makes this call)
+            TRY(set_dev(c));
+            TRY(launch_barrier(c, s));
             TRY(record_hip(hipEventRecord(tb->ev[2 * cand], s), "autotune event"));
         }
     }
