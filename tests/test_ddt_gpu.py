@@ -98,8 +98,8 @@ def test_vector_config3(orc, bl):
 @pytest.mark.parametrize("bl,stride,shift", [(8, 16, 0), (8, 16, 8), (9, 19, 8), (16, 32, 24),
                                              (5, 13, 4)])
 def test_vector_gapped_tile_pack(orc, bl, stride, shift):
-    """The staged pack skips the 16-B vectors of gaps of 64 B or more
-    (gap lines are never read): run phases that drift across 16 B (stride
+    """The staged tile pack of vector runs with gaps of 64-128 B (read
+    through into LDS, batched): run phases that drift across 16 B (stride
     19 / 13 doubles), a typed base off 16-B alignment by `shift` bytes, and
     a 64 KiB-fragment train whose windows start mid-period; the gap bytes
     hold random data that must never reach the packed stream."""
