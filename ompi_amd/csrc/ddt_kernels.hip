@@ -643,8 +643,8 @@ constexpr int64_t kTileMaxGap = 128;          // bytes of gap the tile reads thr
 // typed gaps (it reads the packed side and writes runs only), so a gap
 // costs nothing but LDS — vector bl64 (512-B runs, 512-B gaps) unpacks at
 // 5.10 TB/s through the tile vs 4.06 through the per-granule kernel.  The
-// pack keeps kTileMaxGap: its gap-skipping loads mask half the lanes, and
-// bl64 packed slower staged (3.74 vs 4.00 TB/s,
+// pack keeps kTileMaxGap: it stages the typed span gaps included, so wide
+// gaps multiply its reads (bl64 packed slower staged, 3.74 vs 4.00 TB/s,
 // profiles/r03_ddt_run_maxgap_ab.jsonl).  OMPI_AMD_DDT_RUN_MAXGAP overrides
 // the unpack bound (128 = the round-2 behaviour).
 static int64_t run_max_gap() {
