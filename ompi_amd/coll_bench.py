@@ -142,7 +142,7 @@ def bench_allreduce(args, metric: str, link_gbs: float):
         comm.set_param("autotune", 1)
         _progress(rank, "autotune: one call per candidate")
         calls = 0
-        while calls < 16:  # 6 candidates x 2 rounds decide at the 12th
+        while calls < 24:  # 9 candidates x 2 rounds decide at the 18th
             ours()
             torch.cuda.synchronize()
             calls += 1
@@ -156,7 +156,7 @@ def bench_allreduce(args, metric: str, link_gbs: float):
                         "worst_rank_us": {
                             f"{dict(ALGORITHMS)[comm.get_param(f'autotune_alg{k}')]}/staged/"
                             f"{comm.get_param(f'autotune_grid{k}')}": comm.get_param(f"autotune_us{k}")
-                            for k in range(6)}}
+                            for k in range(9)}}
 
     _progress(rank, f"headline: {best_name}")
     t = _timed(ours, args.steps, args.warmup, dist, torch, tdev)
@@ -192,9 +192,13 @@ def bench_allreduce(args, metric: str, link_gbs: float):
     #   scatter the peers' input blocks pushed into this rank's landing slots
     alg, user = best["algorithm"], bool(comm.get_param("user_ipc"))
     part = (world - 1) / world * S
-    fold_bytes = {0: part, 1: 2 * part, 2: part if user else 0.0}[alg]
-    xgmi = {"fold": fold_bytes, "gather": part if alg in (0, 2) and not (alg == 2 and user) else 0.0,
-            "scatter": part if alg == 2 else 0.0}
+    # push-land (3): the fold stores its result into every peer's landing
+    # buffer (part out), the second phase is a local copy; with user_ipc it
+    # is the push scheme
+    fold_bytes = {0: part, 1: 2 * part, 2: part if user else 0.0, 3: part}[alg]
+    xgmi = {"fold": fold_bytes,
+            "gather": part if alg in (0, 2) and not (alg == 2 and user) else 0.0,
+            "scatter": part if alg in (2, 3) else 0.0}
     ph = {}
     for k, name in enumerate(("fold", "gather", "scatter")):
         ms, calls = phases[k]
@@ -340,7 +344,7 @@ def cpu_baseline_ring(world: int, nbytes: int, factor: float, seconds: float = 1
                       f"busBW = S/t x {factor:.3f}"}
 
 
-ALGORITHMS = ((0, "pull"), (1, "pull_push"), (2, "push"))
+ALGORITHMS = ((0, "pull"), (1, "pull_push"), (2, "push"), (3, "push_land"))
 BLOCKS = (256, 512, 1024, 2048)  # grid cap of the transfer kernels
 
 

@@ -31,7 +31,12 @@
 //   2 push       every rank stores block b of its sbuf into the owner's
 //                landing slot (writes only over xGMI), barrier, the owner
 //                reduces from local memory and stores the result into every
-//                rank's rbuf, barrier
+//                rank's rbuf, barrier (staged, user_ipc 0: push-gather — the
+//                owner keeps its result, every rank then pulls the others)
+//   3 push-land  staged push whose second phase stores too: the owner
+//                stores its result into every rank's landing buffer,
+//                barrier, each rank copies the results into its rbuf
+//                locally, barrier (with user_ipc: as 2)
 // Below `small_bytes` every rank stages its input in IPC scratch and folds
 // all blocks itself (one barrier, no host rendezvous).
 //
@@ -267,7 +272,7 @@ struct path_params {
     int zero_copy, algorithm;
     int tuned_alg;      // coll_tuned_allreduce_algorithm the user forced (0: fixed decision)
     int root0_inplace;  // forced nonoverlapping only: rank 0 passed MPI_IN_PLACE
-    int push_gather;    // push scheme, staged (user_ipc 0): no handle swap at all
+    int push_gather;    // push / push-land scheme, staged (user_ipc 0): no handle swap at all
 };
 
 // Export fallback.  hipIpcGetMemHandle sometimes refuses a live device
@@ -338,11 +343,12 @@ struct ompi_amd_request {
 // makes the same calls.  coll/tuned's dynamic rules pick from a table;
 // this picks from measurements on the machine it runs on (xGMI loads vs
 // stores and the grid that saturates the links are not knowable offline).
-constexpr int kTuneCands = 6, kTuneRounds = 2, kTuneCalls = kTuneCands * kTuneRounds;
+constexpr int kTuneCands = 9, kTuneRounds = 2, kTuneCalls = kTuneCands * kTuneRounds;
 struct tune_cand {
     int algorithm, blocks;
 };
 static const tune_cand kTune[kTuneCands] = {{2, 1024}, {2, 512}, {2, 256},
+                                            {3, 1024}, {3, 512}, {3, 256},
                                             {0, 1024}, {0, 512}, {0, 256}};
 struct tune_bucket {
     int next = 0;  // calls made so far; call k runs candidate k % kTuneCands
@@ -485,7 +491,11 @@ struct ompi_amd_plan {
 
 namespace ompi_amd {
 
-enum { ALG_PULL = 0, ALG_PULL_PUSH = 1, ALG_PUSH = 2, ALG_COUNT = 3 };
+enum { ALG_PULL = 0, ALG_PULL_PUSH = 1, ALG_PUSH = 2, ALG_PUSH_LAND = 3, ALG_COUNT = 4 };
+// push-land is the staged push whose second phase also stores (the owners
+// push their results into every rank's landing buffer) instead of loading;
+// with user_ipc it is the push scheme (results stored into the rbufs)
+static inline bool is_push(int alg) { return alg == ALG_PUSH || alg == ALG_PUSH_LAND; }
 
 struct ipc_blob {
     buf_desc flags, scratch;
@@ -1706,6 +1716,17 @@ static int allreduce_push(ompi_amd_comm_t *c, const void *src, const ptr_set &rp
     return launch_barrier(c, s);
 }
 
+// Landing bytes of the staged push schemes: push-gather needs n input slots
+// and its result slot [n]; push-land n input slots and n result slots (one
+// per block).  Push-land falls back to push-gather when its 2n slots would
+// pass the IPC size limit (every rank computes the same for the same count).
+static size_t staged_push_landing(int n, int algorithm, int64_t count, int type, bool *land) {
+    const size_t slot = push_slot(count, n, type);
+    const bool l = algorithm == ALG_PUSH_LAND && slot * (size_t)(2 * n) <= kMaxIpcBytes;
+    if (land) *land = l;
+    return slot * (size_t)(l ? 2 * n : n + 1);
+}
+
 // The push scheme with a gather instead of remote result stores: nothing
 // of the caller's is exported (the default, user_ipc = 0).  Scatter: block b
 // of my input into slot [me] of its owner's landing buffer (remote stores,
@@ -1714,14 +1735,26 @@ static int allreduce_push(ompi_amd_comm_t *c, const void *src, const ptr_set &rp
 // result slot [n].  Barrier.  Every rank pulls the other blocks from their
 // owners' result slots into its rbuf.  Barrier.  Same xGMI bytes as the
 // zero-copy pull ((N-1)/N·S out, (N-1)/N·S in), no staging copy.
+//
+// Push-land (algorithm 3): the same scatter and barrier; then the owner
+// folds its block into its rbuf AND stores the result into slot [n + b] of
+// every peer's landing buffer in the same pass (remote stores, spread over
+// the links: local first, then rank+1, rank+2, ...).  Barrier.  Every rank
+// copies the other blocks from its own result slots into its rbuf (local
+// HBM).  Barrier (every landing call ends with one: the next landing call of
+// any collective may scatter into these bytes without a leading barrier).
+// Both xGMI phases store; the price is one local copy of (N-1)/N of the
+// vector.
 static int allreduce_push_gather(ompi_amd_comm_t *c, const void *src, void *rbuf, int64_t count,
-                                 int op, int type, const fold_plan &fp, hipStream_t s) {
+                                 int op, int type, const fold_plan &fp, hipStream_t s,
+                                 int algorithm) {
     const int n = c->size, mine = (c->rank + 1) % n;
     const int64_t ext = (int64_t)ompi_amd_type_extent(type);
     int64_t split, early, late;
     blockcount(count, n, &split, &early, &late);
     const size_t slot = push_slot(count, n, type);
-    TRY(ensure_landing(c, slot * (size_t)(n + 1)));
+    bool land = false;
+    TRY(ensure_landing(c, staged_push_landing(n, algorithm, count, type, &land)));
     cp_jobs cj{};
     for (int b = 0; b < n; ++b) {
         if (b == mine) continue;
@@ -1744,6 +1777,25 @@ static int allreduce_push_gather(ompi_amd_comm_t *c, const void *src, void *rbuf
     fold_jobs(fp, count, n, mine, &jobs);
     ptr_set dsts{};
     dsts.p[0] = (const char *)rbuf;
+    if (land) {
+        for (int k = 1; k < n; ++k) {
+            const int q = (c->rank + k) % n;
+            dsts.p[k] = c->peer_land.p[q] + (size_t)(n + mine) * slot + (offm & 15) - offm;
+        }
+        TRY(timed_phase(c, 0, s, [&] {
+            return launch_reduce(c, op, type, srcs, n, dsts, n, fp.order, fp.flags, jobs, s);
+        }));
+        TRY(launch_barrier(c, s));
+        cj = cp_jobs{};
+        for (int b = 0; b < n; ++b) {
+            if (b == mine) continue;
+            const int64_t off = block_off(b, split, early, late) * ext;
+            cj.j[cj.n++] = {c->land + (size_t)(n + b) * slot + (off & 15), (char *)rbuf + off,
+                            block_cnt(b, split, early, late) * ext};
+        }
+        TRY(timed_phase(c, 1, s, [&] { return launch_copy(c, cj, s); }));
+        return launch_barrier(c, s);
+    }
     dsts.p[1] = c->land + (size_t)n * slot + (offm & 15) - offm;
     TRY(timed_phase(c, 0, s, [&] {
         return launch_reduce(c, op, type, srcs, n, dsts, 2, fp.order, fp.flags, jobs, s);
@@ -1889,7 +1941,7 @@ static int scan_common(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
 
 static path_params params_of(const ompi_amd_comm_t *c) {
     return {c->small_bytes, c->fused_bytes, c->zero_copy, c->algorithm, c->tuned_alg, 0,
-            c->algorithm == ALG_PUSH && !c->user_ipc && !c->force_shadow ? 1 : 0};
+            is_push(c->algorithm) && !c->user_ipc && !c->force_shadow ? 1 : 0};
 }
 
 // Whether an allreduce of `count` elements takes a zero-copy path (and so
@@ -2046,7 +2098,7 @@ static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size
     }
     ptr_set sp{}, rp{};
     if (!c->pre && pp.push_gather)
-        return allreduce_push_gather(c, src, rbuf, (int64_t)count, op, type, fp, s);
+        return allreduce_push_gather(c, src, rbuf, (int64_t)count, op, type, fp, s, pp.algorithm);
     if (!c->pre && pp.algorithm == ALG_PULL && !c->user_ipc && !c->force_shadow) {
         // staged pull: the input into this rank's shadow (rbuf's phase mod
         // 256, so results and shadows line up for 16-B vectors), swap
@@ -2063,7 +2115,7 @@ static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size
     }
     // export fallback (shadow_plan); a deferred call substituted its
     // shadows when it was posted, so these export and plan nothing
-    const bool push = pp.algorithm == ALG_PUSH;
+    const bool push = is_push(pp.algorithm);
     const void *xs = push ? nullptr : src;
     void *xr = rbuf;
     shadow_set sh;
@@ -2507,7 +2559,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
     if (allreduce_push_gathers(c, pp, count, type)) {
         // no swap: only the landing buffer must be big enough before the
         // launch (growing is collective and blocking: every rank here alike)
-        const size_t need = push_slot((int64_t)count, c->size, type) * (size_t)(c->size + 1);
+        const size_t need = staged_push_landing(c->size, pp.algorithm, (int64_t)count, type, nullptr);
         if (need > c->land_bytes) {
             rc = drain(c);
             if (rc == OMPI_AMD_SUCCESS) rc = ensure_landing(c, need);
@@ -2520,7 +2572,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
     } else if (allreduce_swaps(c, pp, count, type)) {
         // post this rank's half of the handle swap now; the launch waits for
         // the peers' halves (progress / the next collective call)
-        const bool push = pp.algorithm == ALG_PUSH;
+        const bool push = is_push(pp.algorithm);
         if (push) {
             const size_t need = push_slot((int64_t)count, c->size, type) * (size_t)c->size;
             if (need > c->land_bytes) {  // collective growth: every rank decides alike
@@ -3182,10 +3234,10 @@ int ompi_amd_allreduce_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, si
     const bool push_gather = allreduce_push_gathers(c, pl->pp, count, type);
     const bool small = n == 1 || count == 0 || !allreduce_swaps(c, pl->pp, count, type) || push_gather;
     if (rc == OMPI_AMD_SUCCESS && push_gather)
-        rc = ensure_landing(c, push_slot((int64_t)count, n, type) * (size_t)(n + 1));
+        rc = ensure_landing(c, staged_push_landing(n, pl->pp.algorithm, (int64_t)count, type, nullptr));
     pl->fp = allreduce_fold(n, pl->pp.tuned_alg, count, type, pl->pp.root0_inplace != 0);
     if (!small) {
-        pl->kind = c->algorithm == ALG_PUSH ? 3 : c->algorithm == ALG_PULL_PUSH ? 2 : 1;
+        pl->kind = is_push(c->algorithm) ? 3 : c->algorithm == ALG_PULL_PUSH ? 2 : 1;
         if (pl->kind == 3) rc = ensure_landing(c, push_slot(pl->count, n, type) * (size_t)n);
         if (rc == OMPI_AMD_SUCCESS) {  // export fallback: shadows of the plan's own
             const void *xs = pl->kind == 3 ? nullptr : pl->src;

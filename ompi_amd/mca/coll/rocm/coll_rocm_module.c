@@ -101,7 +101,9 @@ static int rocm_register(void)
                                            &mca_coll_rocm_component.timeout_ms);
     (void) mca_base_component_var_register(c, "allreduce_algorithm",
                                            "Large-message allreduce data movement: 0 pull, 1 pull+push, 2 push (default; push-gather "
-                                           "through the landing buffers when user_ipc is 0)",
+                                           "through the landing buffers when user_ipc is 0), 3 push-land "
+                                           "(results stored into every rank's landing buffer, then a local "
+                                           "copy; push when user_ipc is 1)",
                                            MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_coll_rocm_component.algorithm);
@@ -113,9 +115,9 @@ static int rocm_register(void)
                                            &mca_coll_rocm_component.user_ipc);
     (void) mca_base_component_var_register(c, "autotune",
                                            "Large staged allreduces pick their scheme (push-gather or "
-                                           "pull) and grid by measurement: the first twelve calls of a size "
-                                           "bucket try each of six candidates twice, all ranks then take the "
-                                           "fastest; 0 keeps "
+                                           "push-land or pull) and grid by measurement: the first eighteen calls "
+                                           "of a size bucket try each of nine candidates twice, all ranks then "
+                                           "take the fastest; 0 keeps "
                                            "coll_rocm_allreduce_algorithm",
                                            MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
                                            MCA_BASE_VAR_SCOPE_READONLY,

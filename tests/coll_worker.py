@@ -405,11 +405,11 @@ def case_zero_counts(comm, rank, n, salt):
 
 
 def case_autotune(comm, rank, n, salt, big):
-    """param "autotune" (coll/rocm's default): the first twelve large
-    blocking allreduces of a size bucket run the six candidates twice each
-    (push-gather and staged pull x 1024 / 512 / 256 blocks; a candidate
-    counts its best round), the twelfth decides — on every rank alike — and
-    later calls run the choice; every result bit-exact
+    """param "autotune" (coll/rocm's default): the first eighteen large
+    blocking allreduces of a size bucket run the nine candidates twice each
+    (push-gather, push-land and staged pull x 1024 / 512 / 256 blocks; a
+    candidate counts its best round), the eighteenth decides — on every
+    rank alike — and later calls run the choice; every result bit-exact
     against the oracle on dataset R (the fold order is the same whatever
     the scheme), in place too, and a nonblocking allreduce of the same size
     posted meanwhile keeps the default scheme."""
@@ -417,7 +417,7 @@ def case_autotune(comm, rank, n, salt, big):
     count = big + 11
     comm.set_param("autotune", 1)
     try:
-        for i in range(15):
+        for i in range(21):
             if i == 3:  # a nonblocking call in the middle of the tuning
                 xs = [inputs(F, count, r, salt + 50) for r in range(n)]
                 exp, _ = orc.allreduce([x.copy() for x in xs], count, SUM.index, F.code)
@@ -433,10 +433,10 @@ def case_autotune(comm, rank, n, salt, big):
             if not ok:
                 return False, f"call {i}: {msg}"
             state = comm.get_param("autotune_state")
-            if state != (1 if i < 11 else 2):
+            if state != (1 if i < 17 else 2):
                 return False, f"call {i}: autotune_state {state}"
         choice = (comm.get_param("autotune_algorithm"), comm.get_param("autotune_blocks"))
-        times = [comm.get_param(f"autotune_us{k}") for k in range(6)]
+        times = [comm.get_param(f"autotune_us{k}") for k in range(9)]
         everyone = [None] * n
         dist.all_gather_object(everyone, (choice, times))
         if any(e != everyone[0] for e in everyone):
@@ -884,6 +884,8 @@ def main():
                                                                    max(3 << 20, n << 18) + 9, 171, 0)),
         ("ar_ring_segmented_R_pullpush", lambda: case_ring_segmented_R(
             comm, rank, n, max(3 << 20, n << 18) + 13, 172, 1)),
+        ("ar_ring_segmented_R_pushland", lambda: case_ring_segmented_R(
+            comm, rank, n, max(3 << 20, n << 18) + 17, 173, 3)),
         ("ar_sum_f32_big", lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, big, 7, repeat=3)),
         ("ar_sum_f32_big_inplace",
          lambda: case_allreduce(comm, rank, n, F, mop.MPI_SUM, big, 8, inplace=True)),
@@ -984,7 +986,7 @@ def main():
     ]
     # zero-copy allreduce under the two push schemes (param "algorithm")
     # the schemes other than the library default (which every unscoped case runs)
-    for alg in [a for a in (0, 1, 2) if a != DEFAULT_ALG[0]]:
+    for alg in [a for a in (0, 1, 2, 3) if a != DEFAULT_ALG[0]]:
         def with_alg(fn, a=alg):
             def run():
                 comm.set_param("algorithm", a)
@@ -1020,7 +1022,7 @@ def main():
     if os.environ.get("COLL_HEADLINE"):  # full-size headline only (tests/test_coll_gpu.py)
         hc = int(os.environ["COLL_HEADLINE"])
         cases = [(f"headline_alg{a}", lambda a=a: case_headline(comm, rank, n, hc, 95 + a, a))
-                 for a in (0, 1, 2)]
+                 for a in (0, 1, 2, 3)]
     def shadowed_nb(fn):  # the export fallback for the nonblocking forms
         def run():
             comm.set_param("force_shadow", 1)
