@@ -3504,6 +3504,15 @@ int comm_alloc_exportable(size_t bytes, bool uncached, void **out, ipc_desc *d) 
     return OMPI_AMD_SUCCESS;
 }
 
+int comm_arena_alloc(ompi_amd_comm_t *c, size_t bytes, void **out) {
+    char *p = nullptr;
+    const int rc = arena_alloc(c, bytes, &p);
+    *out = p;
+    return rc;
+}
+
+void comm_arena_free(ompi_amd_comm_t *c, void *p) { arena_free(c, static_cast<char *>(p)); }
+
 int comm_export(ompi_amd_comm_t *c, const void *ptr, ipc_desc *d) {
     buf_desc b{};
     const int rc = export_buf(c, ptr, &b);

@@ -39,6 +39,12 @@ int comm_allgather(ompi_amd_comm_t *c, const void *mine, void *all, size_t len);
 // A fresh device allocation whose IPC handle no earlier allocation of this
 // process had (uncached: fine-grained), described in *d.
 int comm_alloc_exportable(size_t bytes, bool uncached, void **out, ipc_desc *d);
+// Device memory from the communicator's exported arena (the shadow arena:
+// chunks exported once, mapped by each peer once, freed at comm_destroy),
+// so a peer maps nothing new per buffer.  comm_arena_free: once no peer
+// touches the range any more.
+int comm_arena_alloc(ompi_amd_comm_t *c, size_t bytes, void **out);
+void comm_arena_free(ompi_amd_comm_t *c, void *p);
 // Export a device buffer (cached per allocation).
 int comm_export(ompi_amd_comm_t *c, const void *ptr, ipc_desc *d);
 // Map a peer's exported buffer (cached, LRU).  pin: held until comm_unpin.

@@ -417,7 +417,8 @@ struct ompi_amd_win {
     int rank = 0, size = 0;
     char *base = nullptr;
     size_t bytes = 0;
-    bool owns_base = false;
+    bool owns_base = false;   // hipMalloc'd by win_allocate (past the arena's limit)
+    bool arena_base = false;  // from the communicator's exported arena
     uint32_t *ctl = nullptr;
     char *peer_base[kOscMaxRanks] = {};
     uint32_t *peer_ctl[kOscMaxRanks] = {};
@@ -437,7 +438,9 @@ struct ompi_amd_win {
     // segment back to back; the others map it once
     bool shared = false;
     char *shared_seg = nullptr;   // rank 0: the allocation; others: their mapping
-    ipc_ref *shared_ref = nullptr;
+    void *shared_pin = nullptr;   // others: the pinned import of rank 0's allocation
+    bool shared_owner = false;    // rank 0: frees shared_seg (arena or hipFree)
+    bool shared_arena = false;
 };
 
 namespace ompi_amd {
@@ -777,29 +780,45 @@ int ompi_amd_win_allocate(ompi_amd_comm_t *c, size_t bytes, int disp_unit, void 
     if (!c || !out || !base || disp_unit <= 0) return OMPI_AMD_ERR_BAD_PARAM;
     int rc = record_hip(hipSetDevice(comm_device(c)), "hipSetDevice");
     void *m = nullptr;
+    bool arena = false;
     if (rc == OMPI_AMD_SUCCESS && bytes) {
-        // library-owned: exported once, padded so that its handle is not a
-        // freed window's again (peers may still cache that one; §4.6)
-        ipc_desc d;
-        rc = comm_alloc_exportable(bytes, false, &m, &d);
+        // library-owned, from the communicator's exported arena: its chunks
+        // are exported once and every peer maps each chunk once, so a new
+        // window costs no IPC open at all (each open of a fresh small
+        // allocation was a chance for ROCm 7.2's "invalid device pointer"
+        // refusal).  Past the arena's IPC size limit: an
+        // allocation of its own, padded so that its handle is not a freed
+        // window's again.
+        rc = comm_arena_alloc(c, bytes, &m);
+        arena = rc == OMPI_AMD_SUCCESS;
+        if (rc == OMPI_AMD_ERR_UNSUPPORTED) {
+            ipc_desc d;
+            rc = comm_alloc_exportable(bytes, false, &m, &d);
+        }
         if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipMemset(m, 0, bytes), "hipMemset (window)");
         if (rc == OMPI_AMD_SUCCESS)
             rc = record_hip(hipStreamSynchronize(nullptr), "hipStreamSynchronize (window memset)");
     }
+    auto release = [&] {
+        if (!m) return;
+        if (arena) comm_arena_free(c, m);
+        else hip_ignore(hipFree(m));
+    };
     // a local failure still joins the rendezvous (as a zero-byte window) so
     // that no peer waits; the collective result reports it
     if (rc != OMPI_AMD_SUCCESS) {
-        if (m) hip_ignore(hipFree(m));
+        release();
         ompi_amd_win_t *w = nullptr;
         if (win_setup(c, nullptr, 0, disp_unit, false, &w) == OMPI_AMD_SUCCESS)
             (void)ompi_amd_win_free(w);
         return rc;
     }
-    rc = win_setup(c, m, bytes, disp_unit, true, out);
+    rc = win_setup(c, m, bytes, disp_unit, !arena, out);
     if (rc != OMPI_AMD_SUCCESS) {
-        if (m) hip_ignore(hipFree(m));
+        release();
         return rc;
     }
+    (*out)->arena_base = arena;
     *base = m;
     return OMPI_AMD_SUCCESS;
 }
@@ -819,12 +838,16 @@ int ompi_amd_win_free(ompi_amd_win_t *w) {
         if (w->pinned[p]) comm_unpin(c, w->pinned[p]);
     const int crc = ctl_give(c, w->ctl_slot);  // the peers' last kernels on it are done
     if (rc == OMPI_AMD_SUCCESS) rc = crc;
-    ipc_unmap(w->shared_ref);
-    const int brc2 = comm_allgather(c, nullptr, nullptr, 0);  // mappings closed before frees
+    if (w->shared_pin) comm_unpin(c, w->shared_pin);
+    const int brc2 = comm_allgather(c, nullptr, nullptr, 0);  // mappings released before frees
     if (rc == OMPI_AMD_SUCCESS) rc = brc2;
-    if (w->shared && !w->shared_ref && w->shared_seg) hip_ignore(hipFree(w->shared_seg));
+    if (w->shared_owner && w->shared_seg) {
+        if (w->shared_arena) comm_arena_free(c, w->shared_seg);
+        else hip_ignore(hipFree(w->shared_seg));
+    }
     if (w->query) hip_ignore(hipStreamDestroy(w->query));
     if (w->owns_base && w->base) hip_ignore(hipFree(w->base));
+    if (w->arena_base && w->base) comm_arena_free(c, w->base);  // nobody maps it per window
     if (rc == OMPI_AMD_SUCCESS) rc = comm_sticky(c);
     delete w;
     return rc;
@@ -971,8 +994,15 @@ int ompi_amd_win_allocate_shared(ompi_amd_comm_t *c, size_t bytes, int disp_unit
         int64_t failed;
     } mine{}, all[kOscMaxRanks];
     char *m = nullptr;
+    bool arena = false;
     if (me == 0 && rc == OMPI_AMD_SUCCESS) {
-        rc = comm_alloc_exportable(prefix[n] ? prefix[n] : 1, false, (void **)&m, &mine.d);
+        // from rank 0's exported arena (peers map its chunk once, §4.6), or
+        // an allocation of its own past the arena's IPC size limit
+        rc = comm_arena_alloc(c, prefix[n] ? prefix[n] : 1, (void **)&m);
+        arena = rc == OMPI_AMD_SUCCESS;
+        if (arena) rc = comm_export(c, m, &mine.d);
+        else if (rc == OMPI_AMD_ERR_UNSUPPORTED)
+            rc = comm_alloc_exportable(prefix[n] ? prefix[n] : 1, false, (void **)&m, &mine.d);
         if (rc == OMPI_AMD_SUCCESS && prefix[n])
             rc = record_hip(hipMemset(m, 0, prefix[n]), "hipMemset (shared window)");
         if (rc == OMPI_AMD_SUCCESS)
@@ -986,13 +1016,17 @@ int ompi_amd_win_allocate_shared(ompi_amd_comm_t *c, size_t bytes, int disp_unit
                    (unsigned long long)prefix[n]);
         rc = OMPI_AMD_ERR_BOOTSTRAP;
     }
-    ipc_ref *ref = nullptr;
+    void *pin = nullptr;
     if (rc == OMPI_AMD_SUCCESS && me != 0) {
-        void *mb = nullptr;
-        const ipc_desc &d = all[0].d;
-        rc = ipc_map(ipc_alloc{d.h, d.pid, d.id, d.base, d.size}, &ref, &mb);
-        if (rc == OMPI_AMD_SUCCESS) m = static_cast<char *>(mb) + d.off;
+        const char *mb = nullptr;
+        rc = comm_import(c, 0, all[0].d, &mb, true, &pin);
+        if (rc == OMPI_AMD_SUCCESS) m = const_cast<char *>(mb);
     }
+    auto release_owner = [&] {
+        if (me != 0 || !m) return;
+        if (arena) comm_arena_free(c, m);
+        else hip_ignore(hipFree(m));
+    };
     int all_ok = 0;
     const int grc = ompi_amd_comm_agree(c, rc == OMPI_AMD_SUCCESS, &all_ok);
     if (rc == OMPI_AMD_SUCCESS && (grc != OMPI_AMD_SUCCESS || !all_ok))
@@ -1002,16 +1036,18 @@ int ompi_amd_win_allocate_shared(ompi_amd_comm_t *c, size_t bytes, int disp_unit
     ompi_amd_win_t *w = nullptr;
     if (rc == OMPI_AMD_SUCCESS) rc = win_setup(c, bases[me], bytes, disp_unit, false, &w, bases);
     if (rc != OMPI_AMD_SUCCESS) {
-        ipc_unmap(ref);
-        (void)comm_allgather(c, nullptr, nullptr, 0);  // every mapping closed before the free
-        if (me == 0 && m) hip_ignore(hipFree(m));
+        if (pin) comm_unpin(c, pin);
+        (void)comm_allgather(c, nullptr, nullptr, 0);  // every mapping released before the free
+        release_owner();
         return rc;
     }
     for (int p = 0; p < n; ++p) w->peer_bytes[p] = segs[p];  // queried sizes (padded if noncontig)
     w->bytes = segs[me];
     w->shared = true;
     w->shared_seg = m;
-    w->shared_ref = ref;
+    w->shared_pin = pin;
+    w->shared_owner = me == 0;
+    w->shared_arena = arena;
     *base = bases[me];
     *out = w;
     return OMPI_AMD_SUCCESS;
