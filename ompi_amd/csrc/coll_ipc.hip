@@ -1136,9 +1136,11 @@ static int launch_copy(ompi_amd_comm_t *c, const cp_jobs &jobs, hipStream_t s) {
 // ---- shadow arena ----
 
 // First fit over the chunks (256-B granules, never across a chunk: peers map
-// each chunk separately); a new chunk of max(need, 64 MiB, everything so
-// far) when none fits.
-static int arena_alloc(ompi_amd_comm_t *c, size_t need, char **out) {
+// each chunk separately); a new chunk of max(need, min_chunk, everything so
+// far) when none fits (64 MiB for collective shadows; windows ask for 2 MiB:
+// the osc component gives every window a communicator of its own).
+static int arena_alloc(ompi_amd_comm_t *c, size_t need, char **out,
+                       size_t min_chunk = (size_t)64 << 20) {
     host_step st("arena_alloc", need);
     const size_t n = (std::max<size_t>(need, 1) + 255) & ~(size_t)255;
     std::lock_guard<std::mutex> g(c->arena_mu);
@@ -1158,7 +1160,7 @@ static int arena_alloc(ompi_amd_comm_t *c, size_t need, char **out) {
         return OMPI_AMD_ERR_UNSUPPORTED;
     }
     const size_t want = std::min(kMaxIpcBytes,
-                                 (std::max({n, (size_t)64 << 20, c->arena_bytes}) + (2u << 20) - 1) &
+                                 (std::max({n, min_chunk, c->arena_bytes}) + (2u << 20) - 1) &
                                      ~(size_t)((2u << 20) - 1));
     char *mem = nullptr;
     hipIpcMemHandle_t h;
@@ -3506,7 +3508,7 @@ int comm_alloc_exportable(size_t bytes, bool uncached, void **out, ipc_desc *d) 
 
 int comm_arena_alloc(ompi_amd_comm_t *c, size_t bytes, void **out) {
     char *p = nullptr;
-    const int rc = arena_alloc(c, bytes, &p);
+    const int rc = arena_alloc(c, bytes, &p, (size_t)2 << 20);
     *out = p;
     return rc;
 }
