@@ -103,13 +103,24 @@ static int rocm_component_init_query(bool enable_progress_threads,
 /* opm_enable (op_base_op_select.c:142-150): the slots this module takes
  * hold the handler the lower-priority components left there; that handler
  * (and its module, retained for as long as the library may call it) is
- * what host buffers go to. */
+ * what host buffers go to.
+ *
+ * Reference counts: the copy loop that follows enable retains this module
+ * once per slot it takes, but its 3-buffer branch releases the slot's
+ * 2-BUFFER module (op_base_op_select.c:163-164) — this module itself when
+ * it took both slots of the type, as it just stored itself there.  The op
+ * destructor later releases both arrays (op.c:500-507), so without help
+ * this module would end with half the references its slots hold and be
+ * released past zero at MPI_Finalize.  One extra retain per type whose
+ * 2- and 3-buffer slots it takes balances that (a framework with the
+ * release fixed would leak the module instead of freeing it twice). */
 static int rocm_module_enable(struct ompi_op_base_module_1_0_0_t *module, struct ompi_op_t *op)
 {
     int i;
     for (i = 0; i < OMPI_OP_BASE_TYPE_MAX; ++i) {
         ompi_op_base_module_t *m2, *m3;
         if (NULL == module->opm_fns[i] && NULL == module->opm_3buff_fns[i]) continue;
+        if (NULL != module->opm_fns[i] && NULL != module->opm_3buff_fns[i]) OBJ_RETAIN(module);
         m2 = op->o_func.intrinsic.modules[i];
         m3 = op->o_3buff_intrinsic.modules[i];
         if (NULL != m2) OBJ_RETAIN(m2);

@@ -143,22 +143,43 @@ static void select_op(ompi_op_t *op, int opidx, ompi_op_base_module_t *base)
         CHECK(m != NULL && prio == 60, "query op %d", opidx);
         if (ma) order[nm++] = ma;  /* ascending priority: avx (50), rocm (60) */
         order[nm++] = m;
-        /* op_base_op_select.c:137-178: enable, then copy non-NULL slots */
+        /* op_base_op_select.c:137-178: enable, then copy non-NULL slots with
+         * the reference's reference counting as written — including its
+         * 3-buffer branch releasing the slot's 2-buffer module (:163-164) —
+         * then release the query's reference (:174) */
         for (k = 0; k < nm; ++k) {
             ompi_op_base_module_t *mk = order[k];
             if (mk->opm_enable) CHECK(mk->opm_enable(mk, op) == OMPI_SUCCESS, "enable");
             for (i = 0; i < OMPI_OP_BASE_TYPE_MAX; ++i) {
                 if (mk->opm_fns[i]) {
+                    OBJ_RELEASE(op->o_func.intrinsic.modules[i]);
                     op->o_func.intrinsic.fns[i] = mk->opm_fns[i];
                     op->o_func.intrinsic.modules[i] = mk;
+                    OBJ_RETAIN(mk);
                 }
                 if (mk->opm_3buff_fns[i]) {
+                    OBJ_RELEASE(op->o_func.intrinsic.modules[i]);  /* sic: the 2-buffer module */
                     op->o_3buff_intrinsic.fns[i] = mk->opm_3buff_fns[i];
                     op->o_3buff_intrinsic.modules[i] = mk;
+                    OBJ_RETAIN(mk);
                 }
             }
+            OBJ_RELEASE(mk);
         }
         CHECK(m->opm_enable != NULL, "op/rocm captures its fallback at enable");
+        /* the op destructor releases every 2- and 3-buffer slot's module
+         * once (op.c:500-507): op/rocm's count must equal the slots that
+         * hold it, so it reaches zero exactly at the last one */
+        {
+            int held = 0;
+            for (i = 0; i < OMPI_OP_BASE_TYPE_MAX; ++i) {
+                held += op->o_func.intrinsic.modules[i] == m;
+                held += op->o_3buff_intrinsic.modules[i] == m;
+            }
+            CHECK(held > 0 && m->super.obj_reference_count == held,
+                  "op %d: op/rocm module references %d, slots holding it %d", opidx,
+                  (int) m->super.obj_reference_count, held);
+        }
     }
     /* op_base_op_select.c:182-204: NULL pattern must stay op/base's */
     for (i = 0; i < OMPI_OP_BASE_TYPE_MAX; ++i) {
@@ -178,6 +199,9 @@ int main(void)
 {
     const int use_gpu = getenv("HARNESS_GPU") && atoi(getenv("HARNESS_GPU"));
     ompi_op_base_module_t *base = OBJ_NEW(ompi_op_base_module_t);
+    /* op/base's module: one reference per slot of every op (never freed in
+     * the harness; the reference's select loop releases it per slot) */
+    base->super.obj_reference_count = 1 << 20;
     ompi_op_t sum, maxloc, band;
     int n = 1000, i, cnt;
     float *a, *b, *e;
