@@ -810,7 +810,8 @@ def main():
             fds = -1
         line = json.dumps({"rank": rank, "case": name, "ok": bool(ok), "msg": msg, "fds": fds,
                            "ipc_live": comm.get_param("ipc_live"),
-                           "ipc_opens": comm.get_param("ipc_opens")})
+                           "ipc_opens": comm.get_param("ipc_opens"),
+                           "ipc_refusals": comm.get_param("ipc_refusals")})
         print(line, flush=True)
         if os.environ.get("COLL_LOG_DIR"):  # progress visible while the test runs
             os.makedirs(os.environ["COLL_LOG_DIR"], exist_ok=True)
