@@ -764,6 +764,11 @@ def main():
         ("osc_put_get_small", lambda: case_put_get(comm, rank, n, 1001, 80)),
         ("osc_put_get_32MiB", lambda: case_put_get(comm, rank, n, 32 << 20, 81)),
         ("osc_acc_sum_f32", lambda: case_acc_disjoint(comm, rank, n, F, mop.MPI_SUM, 1000003, 82)),
+        # MPIX_C_FLOAT16 accumulates (acc_kernel<_Float16>): 8 halves per 16-B vector
+        ("osc_acc_sum_f16", lambda: case_acc_disjoint(comm, rank, n, mop.MPIX_C_FLOAT16, mop.MPI_SUM,
+                                                      100003, 140)),
+        ("osc_acc_max_f16_specials",
+         lambda: case_acc_disjoint(comm, rank, n, mop.MPIX_C_FLOAT16, mop.MPI_MAX, 70001, 141, "S")),
         ("osc_acc_prod_f64", lambda: case_acc_disjoint(comm, rank, n, D, mop.MPI_PROD, 30001, 83)),
         ("osc_acc_max_f32_specials",
          lambda: case_acc_disjoint(comm, rank, n, F, mop.MPI_MAX, 100001, 84, "S")),
