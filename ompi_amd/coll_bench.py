@@ -84,6 +84,20 @@ def _timed(fn, steps, warmup, dist, torch, dev="cuda"):
     return float(t.item())
 
 
+def _settle(comm, fn, torch, limit=24):
+    """Run a blocking allreduce until the library's autotune of its size
+    bucket has decided (autotune_state 2), or it does not tune this size
+    (state stays 0 or a settled bucket's 2): the first kTuneCalls = 18
+    calls of a new large size try every candidate, slow grids included, and
+    must not land inside a timed region (coll_ipc.hip, ompi_amd_allreduce).
+    Every rank makes the same calls, so every rank stops at the same one."""
+    for _ in range(limit):
+        fn()
+        torch.cuda.synchronize()
+        if comm.get_param("autotune_state") != 1:
+            return
+
+
 def bench_allreduce(args, metric: str, link_gbs: float):
     import torch
     import torch.distributed as dist
@@ -262,6 +276,11 @@ def bench_allreduce(args, metric: str, link_gbs: float):
                 res["config"]["schemes"] = _schemes(comm, dist, torch, mop, n, rank, shared,
                                                     tdev, ours, default)
             comm.set_param("user_ipc", 0)
+            # the scheme sweep set explicit schemes (which turns autotune
+            # off); the rows below measure what the library ships: autotune
+            # on, each new size settled (_settle) before its timed region
+            # (the headline bucket keeps its choice)
+            comm.set_param("autotune", 0 if os.environ.get("OMPI_AMD_BENCH_NO_AUTOTUNE") else 1)
             _progress(rank, "extras: check")
             res["check"] = _check_exact(comm, dist, torch, mop, n, rank, shared)
             _progress(rank, "extras: sweep")
@@ -390,6 +409,7 @@ def _sweep(comm, dist, torch, mop, world, shared, tdev):
         x = torch.ones(n, device="cuda")
         y = torch.empty_like(x)
         steps = 20 if nbytes <= (64 << 20) else 5
+        _settle(comm, lambda: comm.allreduce(x, y, n, mop.MPI_FLOAT, mop.MPI_SUM), torch)
         t = _timed(lambda: comm.allreduce(x, y, n, mop.MPI_FLOAT, mop.MPI_SUM), steps, 3,
                    dist, torch, tdev) / steps
         row = {"bytes": n * 4, "us": round(t * 1e6, 2),
@@ -454,6 +474,7 @@ def _variants(comm, dist, torch, mop, world, tdev):
         for name, fused, small in paths:
             comm.set_param("fused_bytes", fused)
             comm.set_param("small_bytes", small)
+            _settle(comm, lambda: comm.allreduce(x, y, n, mop.MPI_FLOAT, mop.MPI_SUM), torch)
             t = _timed(lambda: comm.allreduce(x, y, n, mop.MPI_FLOAT, mop.MPI_SUM), 20, 3,
                        dist, torch, tdev) / 20
             row[name + "_us"] = round(t * 1e6, 2)
@@ -497,6 +518,7 @@ def _next_rows(comm, dist, torch, mop, world, rank, tdev):
         y = torch.empty_like(x)
         steps = 20 if nbytes <= (16 << 20) else 5
         row = {"bytes": nbytes}
+        _settle(comm, lambda: comm.allreduce(x, y, n, F, SUM), torch)
         t = _timed(lambda: comm.allreduce(x, y, n, F, SUM), steps, 3, dist, torch, tdev) / steps
         row["allreduce_us"] = round(t * 1e6, 2)
         plan = comm.allreduce_init(x, y, n, F, SUM)
