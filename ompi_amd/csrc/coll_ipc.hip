@@ -273,6 +273,7 @@ struct path_params {
     int tuned_alg;      // coll_tuned_allreduce_algorithm the user forced (0: fixed decision)
     int root0_inplace;  // forced nonoverlapping only: rank 0 passed MPI_IN_PLACE
     int push_gather;    // push / push-land scheme, staged (user_ipc 0): no handle swap at all
+    int blocks = 0;     // transfer grid of a deferred call (nb_tuned); 0: the communicator's
 };
 
 // Export fallback.  hipIpcGetMemHandle sometimes refuses a live device
@@ -427,6 +428,9 @@ struct ompi_amd_comm {
     std::map<int, struct tune_bucket> tune;  // by floor(log2(bytes))
     int tune_last = 0;                       // last bucket touched: 0 none, 1 tuning, 2 decided
     int tune_last_key = -1;
+    // the scheme / grid the last nonblocking or persistent allreduce of an
+    // autotuned size took (nb_tuned; -1: none yet)
+    int nb_tuned_alg = -1, nb_tuned_blocks = -1;
     int tuned_alg = 0;                    // coll_tuned_allreduce_algorithm (forced), 0 = fixed
     // this communicator's references to peer mappings (the mappings
     // themselves are process-wide: ipc_registry.h), least recently used
@@ -1943,7 +1947,7 @@ static int scan_common(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
 
 static path_params params_of(const ompi_amd_comm_t *c) {
     return {c->small_bytes, c->fused_bytes, c->zero_copy, c->algorithm, c->tuned_alg, 0,
-            is_push(c->algorithm) && !c->user_ipc && !c->force_shadow ? 1 : 0};
+            is_push(c->algorithm) && !c->user_ipc && !c->force_shadow ? 1 : 0, 0};
 }
 
 // Whether an allreduce of `count` elements takes a zero-copy path (and so
@@ -1967,6 +1971,34 @@ static bool allreduce_swaps(const ompi_amd_comm_t *c, const path_params &pp, siz
 static bool allreduce_push_gathers(const ompi_amd_comm_t *c, const path_params &pp, size_t count,
                                    int type) {
     return pp.push_gather && allreduce_swaps(c, pp, count, type);
+}
+
+// Nonblocking and persistent allreduces of a size bucket the autotune has
+// decided take the fastest measured candidate among the schemes that swap
+// no handles (push-gather, push-land: the deferred launch needs no host
+// rendezvous) with its grid; a bucket that chose the staged pull (which
+// swaps) still gives its best push-type candidate.  Before the bucket is
+// decided they keep the communicator's scheme.  Every rank made the same
+// blocking calls before this one (MPI orders collectives alike on every
+// rank), so every rank finds the same bucket state and takes the same path.
+static void nb_tuned(ompi_amd_comm_t *c, path_params *pp, size_t count, int type) {
+    if (!c->autotune || pp->tuned_alg != 0 || c->user_ipc || c->force_shadow ||
+        !allreduce_swaps(c, *pp, count, type))
+        return;
+    const size_t bytes = count * ompi_amd_type_extent(type);
+    const auto it = c->tune.find(63 - __builtin_clzll((unsigned long long)bytes));
+    if (it == c->tune.end() || !it->second.done) return;
+    int best = -1;
+    for (int k = 0; k < kTuneCands; ++k)
+        if (is_push(kTune[k].algorithm) &&
+            (best < 0 || it->second.worst_ms[k] < it->second.worst_ms[best]))
+            best = k;
+    if (best < 0) return;
+    pp->algorithm = kTune[best].algorithm;
+    pp->blocks = kTune[best].blocks;
+    pp->push_gather = 1;
+    c->nb_tuned_alg = pp->algorithm;
+    c->nb_tuned_blocks = pp->blocks;
 }
 
 static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
@@ -2071,6 +2103,13 @@ static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size
                           int op, hipStream_t s, const path_params &pp) {
     if (count == 0) return OMPI_AMD_SUCCESS;  // allreduce.c:104
     TRY(set_dev(c));
+    // a deferred call's own grid (nb_tuned) for the launches below
+    struct grid_scope {
+        ompi_amd_comm_t *c;
+        int saved;
+        ~grid_scope() { c->max_blocks = saved; }
+    } grid{c, c->max_blocks};
+    if (pp.blocks > 0) c->max_blocks = pp.blocks;
     const size_t ext = ompi_amd_type_extent(type);
     const size_t bytes = count * ext;
     const bool inplace = in_place(sbuf, rbuf);
@@ -2405,6 +2444,8 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "algorithm")) *v = c->algorithm;
     else if (!strcmp(key, "autotune")) *v = c->autotune;
     else if (!strcmp(key, "autotune_state")) *v = c->tune_last;
+    else if (!strcmp(key, "nb_tuned_algorithm")) *v = c->nb_tuned_alg;
+    else if (!strcmp(key, "nb_tuned_blocks")) *v = c->nb_tuned_blocks;
     else if (!strncmp(key, "autotune_", 9) && c->tune_last_key >= 0 &&
              c->tune.count(c->tune_last_key) && c->tune.at(c->tune_last_key).done) {
         // the last decided bucket: its choice and every candidate's worst rank
@@ -2548,6 +2589,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
         return rc;
     }
     path_params pp = params_of(c);
+    nb_tuned(c, &pp, count, type);
     const bool inplace = in_place(sbuf, rbuf);
     if (pp.tuned_alg == TUNED_AR_NONOVERLAPPING) {  // a host exchange, in order with the others
         rc = drain(c);
@@ -2609,7 +2651,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
         if (rc != OMPI_AMD_SUCCESS) {
             hip_ignore(hipEventDestroy(req->ev));
             arena_free(c, req->shadow);
-        arena_free(c, req->shadow2);
+            arena_free(c, req->shadow2);
             delete req;
             return rc;
         }
@@ -3225,6 +3267,7 @@ int ompi_amd_allreduce_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, si
     pl->op = op;
     pl->type = type;
     pl->pp = params_of(c);
+    nb_tuned(c, &pl->pp, count, type);
     int rc = agree_root0_inplace(c, &pl->pp, inplace);
     if (rc != OMPI_AMD_SUCCESS) {
         delete pl;

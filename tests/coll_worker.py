@@ -412,7 +412,9 @@ def case_autotune(comm, rank, n, salt, big):
     rank alike — and later calls run the choice; every result bit-exact
     against the oracle on dataset R (the fold order is the same whatever
     the scheme), in place too, and a nonblocking allreduce of the same size
-    posted meanwhile keeps the default scheme."""
+    posted meanwhile keeps the default scheme; once decided, a nonblocking
+    and a persistent allreduce of that size take the fastest candidate that
+    swaps no handles (push-gather / push-land) with its grid."""
     F, SUM = mop.MPI_FLOAT, mop.MPI_SUM
     count = big + 11
     comm.set_param("autotune", 1)
@@ -437,11 +439,42 @@ def case_autotune(comm, rank, n, salt, big):
                 return False, f"call {i}: autotune_state {state}"
         choice = (comm.get_param("autotune_algorithm"), comm.get_param("autotune_blocks"))
         times = [comm.get_param(f"autotune_us{k}") for k in range(9)]
+        # decided: a nonblocking and a persistent allreduce of this size take
+        # the fastest push-type candidate (no handle swap) with its grid
+        algs = [comm.get_param(f"autotune_alg{k}") for k in range(9)]
+        grids = [comm.get_param(f"autotune_grid{k}") for k in range(9)]
+        push = [k for k in range(9) if algs[k] in (2, 3)]
+        # (times are whole microseconds: a tie may hide a sub-microsecond order)
+        fastest = min(times[k] for k in push)
+        wanted = {(algs[k], grids[k]) for k in push if times[k] == fastest}
+        xs = [inputs(F, count, r, salt + 60) for r in range(n)]
+        exp, _ = orc.allreduce([x.copy() for x in xs], count, SUM.index, F.code)
+        sb = to_dev(xs[rank])
+        ob = torch.zeros_like(sb)
+        req = comm.iallreduce(sb, ob, count, F, SUM)
+        req.wait()
+        req.free()
+        took_nb = (comm.get_param("nb_tuned_algorithm"), comm.get_param("nb_tuned_blocks"))
+        if not np.array_equal(ob.cpu().numpy().view(np.uint32), exp[rank].view(np.uint32)):
+            return False, f"iallreduce after the tuning ({took_nb}) differs"
+        ob.zero_()
+        plan = comm.allreduce_init(sb, ob, count, F, SUM)
+        for _ in range(2):
+            plan.start()
+            plan.wait()
+        plan.free()
+        took_plan = (comm.get_param("nb_tuned_algorithm"), comm.get_param("nb_tuned_blocks"))
+        if not np.array_equal(ob.cpu().numpy().view(np.uint32), exp[rank].view(np.uint32)):
+            return False, f"persistent allreduce after the tuning ({took_plan}) differs"
+        if took_nb not in wanted or took_plan != took_nb:
+            return False, (f"deferred calls took {took_nb} / {took_plan}, expected the fastest "
+                           f"push-type candidate {wanted}")
         everyone = [None] * n
-        dist.all_gather_object(everyone, (choice, times))
+        dist.all_gather_object(everyone, (choice, times, took_nb))
         if any(e != everyone[0] for e in everyone):
             return False, f"ranks chose differently: {everyone}"
-        return True, f"choice {choice}, worst-rank us per candidate {times}"
+        return True, (f"choice {choice}, deferred calls {took_nb}, worst-rank us per "
+                      f"candidate {times}")
     finally:
         comm.set_param("autotune", 0)
 
