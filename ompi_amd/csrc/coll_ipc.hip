@@ -309,6 +309,7 @@ struct pending_op {
     int root = 0;   // bcast, reduce
     bool inplace = false;  // rsb without a swap (staged push): MPI_IN_PLACE
     bool exclusive = false;        // scan: exscan
+    bool land = false;             // allgather / bcast through the landing buffers (no swap)
     std::vector<size_t> rcounts;   // reduce_scatter
 };
 
@@ -431,6 +432,7 @@ struct ompi_amd_comm {
     // the scheme / grid the last nonblocking or persistent allreduce of an
     // autotuned size took (nb_tuned; -1: none yet)
     int nb_tuned_alg = -1, nb_tuned_blocks = -1;
+    int64_t land_deferred = 0;  // allgathers / bcasts run through the landing buffers
     int tuned_alg = 0;                    // coll_tuned_allreduce_algorithm (forced), 0 = fixed
     // this communicator's references to peer mappings (the mappings
     // themselves are process-wide: ipc_registry.h), least recently used
@@ -2009,6 +2011,11 @@ static int allgather_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size
                           hipStream_t s);
 static int bcast_impl(ompi_amd_comm_t *c, void *buf, const void *root_src, size_t bytes, int root,
                       hipStream_t s);
+static int allgather_land(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t bytes,
+                          hipStream_t s);
+static int bcast_land(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, hipStream_t s);
+static size_t ag_landing_need(const ompi_amd_comm_t *c, size_t bytes);
+static size_t bcast_landing_need(const ompi_amd_comm_t *c, size_t bytes);
 static int reduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                        int op, int root, bool root_inplace, hipStream_t s);
 static int rs_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, const size_t *rcounts,
@@ -2050,10 +2057,12 @@ static int progress(ompi_amd_comm_t *c, bool block, int max_launch = -1) {
                     rc = rsb_impl(c, o.sbuf, o.rbuf, o.count, o.type, o.op, o.inplace, o.stream);
                     break;
                 case PEND_ALLGATHER:
-                    rc = allgather_impl(c, o.sbuf, o.rbuf, o.count, o.stream);
+                    rc = o.land ? allgather_land(c, o.sbuf, o.rbuf, o.count, o.stream)
+                                : allgather_impl(c, o.sbuf, o.rbuf, o.count, o.stream);
                     break;
                 case PEND_BCAST:
-                    rc = bcast_impl(c, o.rbuf, o.sbuf, o.count, o.root, o.stream);
+                    rc = o.land ? bcast_land(c, o.rbuf, o.count, o.root, o.stream)
+                                : bcast_impl(c, o.rbuf, o.sbuf, o.count, o.root, o.stream);
                     break;
                 case PEND_REDUCE:
                 case PEND_SCAN:
@@ -2446,6 +2455,7 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "autotune_state")) *v = c->tune_last;
     else if (!strcmp(key, "nb_tuned_algorithm")) *v = c->nb_tuned_alg;
     else if (!strcmp(key, "nb_tuned_blocks")) *v = c->nb_tuned_blocks;
+    else if (!strcmp(key, "landing_deferred")) *v = c->land_deferred;
     else if (!strncmp(key, "autotune_", 9) && c->tune_last_key >= 0 &&
              c->tune.count(c->tune_last_key) && c->tune.at(c->tune_last_key).done) {
         // the last decided bucket: its choice and every candidate's worst rank
@@ -2696,7 +2706,7 @@ static int nb_post(ompi_amd_comm_t *c, pending_op &o, const void **exp, size_t b
         if (rc == OMPI_AMD_SUCCESS) rc = shadow_plan(c, exp, bytes, &none, 0, false, true, &o.sh);
         c->force_shadow = saved;
         req->shadow = o.sh.mem;
-            req->shadow2 = o.sh.mem2;
+        req->shadow2 = o.sh.mem2;
         call_blob mine{};
         if (rc == OMPI_AMD_SUCCESS) rc = export_buf(c, *exp, &mine.s);
         if (rc == OMPI_AMD_SUCCESS) rc = c->boot.post(&mine, sizeof(mine), &o.ticket);
@@ -2715,6 +2725,22 @@ static int nb_post(ompi_amd_comm_t *c, pending_op &o, const void **exp, size_t b
 
 static bool nb_swaps(const ompi_amd_comm_t *c, size_t bytes) {
     return c->size > 1 && bytes > 0 && bytes > c->small_bytes && c->zero_copy;
+}
+
+// A deferred call's landing buffer grown at post time (growth is collective
+// and blocking: every rank posts the same call alike); on failure the
+// request is released.
+static int nb_grow_landing(ompi_amd_comm_t *c, size_t need, ompi_amd_request *req) {
+    int rc = OMPI_AMD_SUCCESS;
+    if (need > c->land_bytes) {
+        rc = drain(c);
+        if (rc == OMPI_AMD_SUCCESS) rc = ensure_landing(c, need);
+    }
+    if (rc != OMPI_AMD_SUCCESS) {
+        hip_ignore(hipEventDestroy(req->ev));
+        delete req;
+    }
+    return rc;
 }
 
 int ompi_amd_ireduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t rcount,
@@ -2766,6 +2792,11 @@ int ompi_amd_iallgather(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
     // in place: keep the (void *)1 spelling unless peers read a shadow
     if (inplace) o.sbuf = (const void *)1;
     if (!nb_swaps(c, bytes)) return nb_post(c, o, nullptr, 0, false, out);
+    if (const size_t need = ag_landing_need(c, bytes)) {
+        TRY(nb_grow_landing(c, need, req));
+        o.land = true;  // stores into the peers' landing buffers: nothing to post
+        return nb_post(c, o, nullptr, 0, false, out);
+    }
     o.sbuf = inplace ? (const void *)my_slot : sbuf;
     return nb_post(c, o, &o.sbuf, bytes, false, out);
 }
@@ -2779,6 +2810,13 @@ int ompi_amd_ibcast(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, void 
     pending_op o{0, buf, buf, bytes, 0, 0, as_stream(stream), params_of(c), req};
     o.kind = PEND_BCAST;
     o.root = root;
+    if (nb_swaps(c, bytes)) {
+        if (const size_t need = bcast_landing_need(c, bytes)) {
+            TRY(nb_grow_landing(c, need, req));
+            o.land = true;  // stores into the peers' landing buffers: nothing to post
+            return nb_post(c, o, nullptr, 0, false, out);
+        }
+    }
     if (!nb_swaps(c, bytes) || c->rank != root) {
         // non-roots export nothing, but post their (empty) half all the same
         if (!nb_swaps(c, bytes)) return nb_post(c, o, nullptr, 0, false, out);
@@ -3243,6 +3281,135 @@ static int bcast_impl(ompi_amd_comm_t *c, void *buf, const void *root_src, size_
     if (c->rank != root) {
         cj.n = 1;
         cj.j[0] = {sp.p[root], (char *)buf, (int64_t)bytes};
+        TRY(launch_copy(c, cj, s));
+    }
+    return launch_barrier(c, s);
+}
+
+// ---- allgather / bcast through the landing buffers (deferred calls) ----
+// Nonblocking and persistent allgathers and bcasts of a zero-copy size in
+// the staged mode move their data by remote STORES into the peers' landing
+// buffers (library memory, mapped once), so they post no buffer descriptor:
+// no host rendezvous at post or at launch, the same as the push-gather
+// allreduce.  Landing layout: the allgather puts rank p's block in slot p;
+// the bcast mirrors the buffer (offset o of the buffer at offset o).  Data
+// sits at the phase mod 16 the receiver's rbuf offset has when rbuf itself
+// is 16-B aligned (the copies stay 16-B vectors for aligned buffers).
+// Every landing call ends with a barrier (the next landing call of any
+// collective may store into these bytes without a leading one).
+static size_t ag_land_slot(size_t bytes) { return (bytes + 16 + 255) & ~(size_t)255; }
+
+// Landing bytes a deferred allgather (bcast) needs, or 0 when it does not
+// take the landing path (user_ipc / force_shadow, a staged size, or past
+// the IPC size limit); every rank computes the same for the same call.
+static size_t ag_landing_need(const ompi_amd_comm_t *c, size_t bytes) {
+    if (c->user_ipc || c->force_shadow || c->size == 1 || bytes <= c->small_bytes || !c->zero_copy)
+        return 0;
+    const size_t need = ag_land_slot(bytes) * (size_t)c->size;
+    return need + (64u << 20) <= kMaxIpcBytes ? need : 0;
+}
+static size_t bcast_landing_need(const ompi_amd_comm_t *c, size_t bytes) {
+    if (c->user_ipc || c->force_shadow || c->size == 1 || bytes <= c->small_bytes || !c->zero_copy)
+        return 0;
+    const size_t need = ((bytes + 255) & ~(size_t)255) + 256;
+    return need + (64u << 20) <= kMaxIpcBytes ? need : 0;
+}
+
+// Store my block into slot [me] of every peer's landing buffer (local rbuf
+// first, then peers rank+1, rank+2, ... so concurrent ranks spread over the
+// links), barrier, copy the peers' slots of my landing buffer into rbuf,
+// barrier.  xGMI bytes as the pull ((N-1)·B out and in per rank); the price
+// is one local copy of (N-1)·B.
+static int allgather_land(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t bytes,
+                          hipStream_t s) {
+    if (bytes == 0) return OMPI_AMD_SUCCESS;
+    TRY(set_dev(c));
+    const int n = c->size;
+    const size_t slot = ag_land_slot(bytes);
+    TRY(ensure_landing(c, slot * (size_t)n));  // grown at post time: a no-op here
+    ++c->land_deferred;
+    char *my_slot = (char *)rbuf + (size_t)c->rank * bytes;
+    const bool inplace = sbuf == (const void *)1 || sbuf == (const void *)my_slot;
+    const char *mine = inplace ? my_slot : (const char *)sbuf;
+    const size_t ph_me = ((size_t)c->rank * bytes) & 15;
+    cp_jobs cj{};
+    if (!inplace) cj.j[cj.n++] = {mine, my_slot, (int64_t)bytes};
+    for (int k = 1; k < n; ++k) {
+        const int q = (c->rank + k) % n;
+        cj.j[cj.n++] = {mine, const_cast<char *>(c->peer_land.p[q]) + (size_t)c->rank * slot + ph_me,
+                        (int64_t)bytes};
+    }
+    TRY(launch_copy(c, cj, s));
+    TRY(launch_barrier(c, s));
+    cj = cp_jobs{};
+    for (int p = 0; p < n; ++p) {
+        if (p == c->rank) continue;
+        const size_t ph = ((size_t)p * bytes) & 15;
+        cj.j[cj.n++] = {c->land + (size_t)p * slot + ph, (char *)rbuf + (size_t)p * bytes,
+                        (int64_t)bytes};
+    }
+    TRY(launch_copy(c, cj, s));
+    return launch_barrier(c, s);
+}
+
+// Scatter + allgather by stores (the data flow of the blocking split bcast,
+// coll_base_bcast.c:768's scatter_allgather): the root stores block b into
+// rank b's landing buffer and its own block into every peer's; barrier;
+// every other rank stores its block from its landing buffer into every
+// non-root peer's and copies it into its buffer; barrier; every non-root
+// copies the other blocks from its landing buffer; barrier.  The root's
+// links carry about 2·bytes/N each instead of `bytes`.
+static int bcast_land(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, hipStream_t s) {
+    if (bytes == 0 || c->size == 1) return OMPI_AMD_SUCCESS;
+    TRY(set_dev(c));
+    const int n = c->size, me = c->rank;
+    TRY(ensure_landing(c, ((bytes + 255) & ~(size_t)255) + 256));
+    ++c->land_deferred;
+    const size_t blk = ((bytes + (size_t)n - 1) / (size_t)n + 255) & ~(size_t)255;
+    auto block = [&](int b, size_t *off, size_t *len) {
+        *off = std::min(bytes, (size_t)b * blk);
+        *len = std::min(bytes, *off + blk) - *off;
+    };
+    size_t off, len;
+    cp_jobs cj{};
+    if (me == root) {
+        for (int k = 1; k < n; ++k) {  // block b to its distributor b
+            const int b = (me + k) % n;
+            block(b, &off, &len);
+            if (len) cj.j[cj.n++] = {(const char *)buf + off, const_cast<char *>(c->peer_land.p[b]) + off,
+                                     (int64_t)len};
+        }
+        TRY(launch_copy(c, cj, s));
+        cj = cp_jobs{};
+        block(root, &off, &len);  // the root distributes its own block
+        for (int k = 1; k < n && len; ++k) {
+            const int q = (me + k) % n;
+            cj.j[cj.n++] = {(const char *)buf + off, const_cast<char *>(c->peer_land.p[q]) + off,
+                            (int64_t)len};
+        }
+        TRY(launch_copy(c, cj, s));
+    }
+    TRY(launch_barrier(c, s));  // block b is in rank b's landing buffer
+    if (me != root) {
+        block(me, &off, &len);
+        if (len) {
+            cj.j[cj.n++] = {c->land + off, (char *)buf + off, (int64_t)len};
+            for (int k = 1; k < n; ++k) {
+                const int q = (me + k) % n;
+                if (q == root) continue;
+                cj.j[cj.n++] = {c->land + off, const_cast<char *>(c->peer_land.p[q]) + off, (int64_t)len};
+            }
+        }
+        TRY(launch_copy(c, cj, s));
+    }
+    TRY(launch_barrier(c, s));  // every block is in every non-root's landing buffer
+    if (me != root) {
+        cj = cp_jobs{};
+        for (int b = 0; b < n; ++b) {
+            block(b, &off, &len);
+            if (b == me || !len) continue;
+            cj.j[cj.n++] = {c->land + off, (char *)buf + off, (int64_t)len};
+        }
         TRY(launch_copy(c, cj, s));
     }
     return launch_barrier(c, s);

@@ -731,6 +731,7 @@ def case_nonblocking_mix(comm, rank, n, salt, big):
     if rank != 0:
         time.sleep(0.05 * rank)
     todo, keep = [], []
+    landed0 = comm.get_param("landing_deferred")
     specs = [("rsb", F, 1001, False), ("rsb", F, big // n + 7, False), ("rsb", D, big // (2 * n) + 3, True),
              ("ag", None, 4099, False), ("ag", None, big * 4 // n + 5, True), ("bc", None, 70001, 0),
              ("bc", None, big * 4 + 3, 1), ("ar", F, big + 1, False), ("rsb", F, 5, True)]
@@ -777,6 +778,13 @@ def case_nonblocking_mix(comm, rank, n, salt, big):
     for name, req, out, nb, exp in reversed(todo):  # completion order is free
         req.wait()
     torch.cuda.synchronize()
+    # the zero-copy-size iallgather and ibcast stored into the landing
+    # buffers (no descriptor posted, no host rendezvous) in the staged mode
+    landed = comm.get_param("landing_deferred") - landed0
+    small = comm.get_param("small_bytes")
+    want = sum(1 for kind, _, cnt, _ in specs if kind in ("ag", "bc") and cnt > small)
+    if not comm.get_param("user_ipc") and landed != want:
+        bad.append(f"{landed} deferred allgather / bcast calls took the landing path, expected {want}")
     for name, req, out, nb, exp in todo:
         req.free()
         got = out.cpu().numpy()[:nb]
