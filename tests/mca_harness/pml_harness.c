@@ -430,14 +430,17 @@ int main(int argc, char **argv)
             unsigned char v = (unsigned char) (g_rank + 1), w = 0;
             CHECK(harness_dev_alloc_copy(&dv, &v, 1) == 0 && harness_dev_alloc_copy(&dw, &w, 1) == 0, "dev");
             ob1_calls = 0;
+            int src_rc = OMPI_SUCCESS, rcv_rc = OMPI_SUCCESS;
             if (g_rank % 2 == 0) {
-                CHECK(mca_pml.pml_send(dv, 1, &dbyte, right, 82, MCA_PML_BASE_SEND_STANDARD, &comm) ==
-                          OMPI_SUCCESS, "device send");
-                CHECK(mca_pml.pml_recv(dw, 1, &dbyte, left, 82, &comm, NULL) == OMPI_SUCCESS, "device recv");
+                src_rc = mca_pml.pml_send(dv, 1, &dbyte, right, 82, MCA_PML_BASE_SEND_STANDARD, &comm);
+                CHECK(src_rc == OMPI_SUCCESS, "device send: %d (%s)", src_rc, ompi_amd_last_error());
+                rcv_rc = mca_pml.pml_recv(dw, 1, &dbyte, left, 82, &comm, NULL);
+                CHECK(rcv_rc == OMPI_SUCCESS, "device recv: %d (%s)", rcv_rc, ompi_amd_last_error());
             } else {
-                CHECK(mca_pml.pml_recv(dw, 1, &dbyte, left, 82, &comm, NULL) == OMPI_SUCCESS, "device recv");
-                CHECK(mca_pml.pml_send(dv, 1, &dbyte, right, 82, MCA_PML_BASE_SEND_STANDARD, &comm) ==
-                          OMPI_SUCCESS, "device send");
+                rcv_rc = mca_pml.pml_recv(dw, 1, &dbyte, left, 82, &comm, NULL);
+                CHECK(rcv_rc == OMPI_SUCCESS, "device recv: %d (%s)", rcv_rc, ompi_amd_last_error());
+                src_rc = mca_pml.pml_send(dv, 1, &dbyte, right, 82, MCA_PML_BASE_SEND_STANDARD, &comm);
+                CHECK(src_rc == OMPI_SUCCESS, "device send: %d (%s)", src_rc, ompi_amd_last_error());
             }
             CHECK(ob1_calls == 0, "device traffic stays on the library under host_path");
             CHECK(harness_dev_copy_back(&w, dw, 1) == 0 && w == (unsigned char) (left + 1), "device payload");
