@@ -1901,10 +1901,15 @@ static int reduce_my_block(ompi_amd_comm_t *c, const void *src, void *rbuf, size
     void *dst = inplace ? (void *)c->land : rbuf;
     TRY(launch_reduce(c, op, type, sp, n, one_ptr(dst), 1, ro.order, ro.flags, jobs, s));
     TRY(launch_barrier(c, s));
+    if (!any_inplace) return OMPI_AMD_SUCCESS;
+    // the result leaves the landing buffer after the barrier (peers may read
+    // this rank's input in rbuf until then); one more barrier keeps the
+    // peers' next landing call from storing into it while the copy runs
+    // (every rank sees the same flags, so every rank takes it)
     if (inplace && cnt > 0)
-        return record_hip(hipMemcpyAsync(rbuf, c->land, (size_t)cnt * ext, hipMemcpyDeviceToDevice, s),
-                          "in-place result copy");
-    return OMPI_AMD_SUCCESS;
+        TRY(record_hip(hipMemcpyAsync(rbuf, c->land, (size_t)cnt * ext, hipMemcpyDeviceToDevice, s),
+                       "in-place result copy"));
+    return launch_barrier(c, s);
 }
 
 // scan (exclusive = false) / exscan: rank r folds ranks 0..r (0..r-1) in
