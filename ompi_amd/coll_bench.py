@@ -446,6 +446,19 @@ def _config5(comm, dist, torch, mop, world, rank, tdev):
     t = _timed(lambda: comm.bcast(b, b.numel(), 0), 10, 3, dist, torch, tdev) / 10
     res["bcast"] = {"bytes": b.numel(), "us": round(t * 1e6, 2),
                     "busbw": round(b.numel() / t / 1e9, 3)}
+    # A/B: the same two calls through the landing
+    # buffers (stores, no per-call descriptor swap, one more local copy) —
+    # what the nonblocking / persistent forms always take
+    comm.set_param("land_blocking", 1)
+    try:
+        t = _timed(lambda: comm.allgather(src, dst, per), 10, 3, dist, torch, tdev) / 10
+        res["allgather_landing"] = {"bytes_total": per * world, "us": round(t * 1e6, 2),
+                                    "busbw": round(per * world / t * (world - 1) / world / 1e9, 3)}
+        t = _timed(lambda: comm.bcast(b, b.numel(), 0), 10, 3, dist, torch, tdev) / 10
+        res["bcast_landing"] = {"bytes": b.numel(), "us": round(t * 1e6, 2),
+                                "busbw": round(b.numel() / t / 1e9, 3)}
+    finally:
+        comm.set_param("land_blocking", 0)
     # MPI_Reduce fp32 SUM 64 MiB to root 0 (tuned pipeline order); every
     # rank reduces 1/N of the vector and stores it into the root's rbuf
     nf = (64 << 20) // 4

@@ -432,7 +432,10 @@ struct ompi_amd_comm {
     // the scheme / grid the last nonblocking or persistent allreduce of an
     // autotuned size took (nb_tuned; -1: none yet)
     int nb_tuned_alg = -1, nb_tuned_blocks = -1;
-    int64_t land_deferred = 0;  // allgathers / bcasts run through the landing buffers
+    int64_t land_ag_bcast = 0;  // allgathers / bcasts run through the landing buffers
+    // param "land_blocking" (0): blocking allgather / bcast of a zero-copy
+    // size take the landing path too (an A/B the 8-GPU bench measures)
+    int land_blocking = 0;
     int tuned_alg = 0;                    // coll_tuned_allreduce_algorithm (forced), 0 = fixed
     // this communicator's references to peer mappings (the mappings
     // themselves are process-wide: ipc_registry.h), least recently used
@@ -2423,6 +2426,8 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
         c->autotune = 0;  // an explicit grid is not second-guessed
     } else if (!strcmp(key, "autotune")) {
         c->autotune = v ? 1 : 0;
+    } else if (!strcmp(key, "land_blocking")) {
+        c->land_blocking = v ? 1 : 0;
     } else if (!strcmp(key, "fused_bytes")) {
         if (v < 0) return OMPI_AMD_ERR_BAD_PARAM;
         c->fused_bytes = std::min<size_t>((size_t)v, c->scratch_bytes);
@@ -2460,7 +2465,8 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "autotune_state")) *v = c->tune_last;
     else if (!strcmp(key, "nb_tuned_algorithm")) *v = c->nb_tuned_alg;
     else if (!strcmp(key, "nb_tuned_blocks")) *v = c->nb_tuned_blocks;
-    else if (!strcmp(key, "landing_deferred")) *v = c->land_deferred;
+    else if (!strcmp(key, "landing_ag_bcast")) *v = c->land_ag_bcast;
+    else if (!strcmp(key, "land_blocking")) *v = c->land_blocking;
     else if (!strncmp(key, "autotune_", 9) && c->tune_last_key >= 0 &&
              c->tune.count(c->tune_last_key) && c->tune.at(c->tune_last_key).done) {
         // the last decided bucket: its choice and every candidate's worst rank
@@ -3147,6 +3153,8 @@ int ompi_amd_allgather(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
     if (!c || !rbuf) return OMPI_AMD_ERR_BAD_PARAM;
     TRY(check_sticky(c));
     TRY(drain(c));
+    if (c->land_blocking && ag_landing_need(c, bytes))  // grown here: collective, every rank alike
+        return allgather_land(c, sbuf, rbuf, bytes, as_stream(stream));
     return allgather_impl(c, sbuf, rbuf, bytes, as_stream(stream));
 }
 
@@ -3188,6 +3196,8 @@ int ompi_amd_bcast(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, void *
     if (!c || !buf || root < 0 || root >= c->size) return OMPI_AMD_ERR_BAD_PARAM;
     TRY(check_sticky(c));
     TRY(drain(c));
+    if (c->land_blocking && bcast_landing_need(c, bytes))
+        return bcast_land(c, buf, bytes, root, as_stream(stream));
     return bcast_impl(c, buf, buf, bytes, root, as_stream(stream));
 }
 
@@ -3332,7 +3342,7 @@ static int allgather_land(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size
     const int n = c->size;
     const size_t slot = ag_land_slot(bytes);
     TRY(ensure_landing(c, slot * (size_t)n));  // grown at post time: a no-op here
-    ++c->land_deferred;
+    ++c->land_ag_bcast;
     char *my_slot = (char *)rbuf + (size_t)c->rank * bytes;
     const bool inplace = sbuf == (const void *)1 || sbuf == (const void *)my_slot;
     const char *mine = inplace ? my_slot : (const char *)sbuf;
@@ -3369,7 +3379,7 @@ static int bcast_land(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, hip
     TRY(set_dev(c));
     const int n = c->size, me = c->rank;
     TRY(ensure_landing(c, ((bytes + 255) & ~(size_t)255) + 256));
-    ++c->land_deferred;
+    ++c->land_ag_bcast;
     const size_t blk = ((bytes + (size_t)n - 1) / (size_t)n + 255) & ~(size_t)255;
     auto block = [&](int b, size_t *off, size_t *len) {
         *off = std::min(bytes, (size_t)b * blk);

@@ -721,6 +721,39 @@ def case_bcast_paths(comm, rank, n, salt):
     return not msgs, "; ".join(msgs)
 
 
+def case_land_blocking(comm, rank, n, salt, big):
+    """param land_blocking = 1 (the 8-GPU bench's A/B): blocking allgather
+    and bcast of zero-copy sizes through the landing buffers (stores into the
+    peers' landing slots, no descriptor swap) — unaligned block sizes, in
+    place, every root — byte-exact, and every such call counted."""
+    msgs = []
+    small = comm.get_param("small_bytes")
+    before = comm.get_param("landing_ag_bcast")
+    want = 0
+    comm.set_param("land_blocking", 1)
+    try:
+        for i, (nbytes, inplace) in enumerate((((big * 4) // n + 12, False), ((big * 4) // n + 5, True),
+                                               (small + 16 * n + 3, False))):
+            ok, msg = case_allgather(comm, rank, n, nbytes, salt + i, inplace)
+            want += 1 if nbytes > small else 0
+            if not ok:
+                msgs.append(f"allgather {nbytes} B{' in place' if inplace else ''}: {msg or 'data differ'}")
+        for root in range(n):
+            for j, nbytes in enumerate((big * 4 + 3, small + 1, n * 256 * 3 + 1 + small)):
+                ok, msg = case_bcast(comm, rank, n, nbytes, root, salt + 10 + 3 * root + j)
+                want += 1 if nbytes > small else 0
+                if not ok:
+                    msgs.append(f"bcast {nbytes} B root {root}: {msg or 'data differ'}")
+    finally:
+        comm.set_param("land_blocking", 0)
+    landed = comm.get_param("landing_ag_bcast") - before
+    if comm.get_param("user_ipc") or comm.get_param("force_shadow"):
+        want = 0
+    if landed != want:
+        msgs.append(f"{landed} calls took the landing path, expected {want}")
+    return not msgs, "; ".join(msgs)
+
+
 def case_nonblocking_mix(comm, rank, n, salt, big):
     """MPI_Ireduce_scatter_block / MPI_Iallgather / MPI_Ibcast (and one
     MPI_Iallreduce) posted back to back, staged and zero-copy sizes, in place
@@ -731,7 +764,7 @@ def case_nonblocking_mix(comm, rank, n, salt, big):
     if rank != 0:
         time.sleep(0.05 * rank)
     todo, keep = [], []
-    landed0 = comm.get_param("landing_deferred")
+    landed0 = comm.get_param("landing_ag_bcast")
     specs = [("rsb", F, 1001, False), ("rsb", F, big // n + 7, False), ("rsb", D, big // (2 * n) + 3, True),
              ("ag", None, 4099, False), ("ag", None, big * 4 // n + 5, True), ("bc", None, 70001, 0),
              ("bc", None, big * 4 + 3, 1), ("ar", F, big + 1, False), ("rsb", F, 5, True)]
@@ -780,7 +813,7 @@ def case_nonblocking_mix(comm, rank, n, salt, big):
     torch.cuda.synchronize()
     # the zero-copy-size iallgather and ibcast stored into the landing
     # buffers (no descriptor posted, no host rendezvous) in the staged mode
-    landed = comm.get_param("landing_deferred") - landed0
+    landed = comm.get_param("landing_ag_bcast") - landed0
     small = comm.get_param("small_bytes")
     want = sum(1 for kind, _, cnt, _ in specs if kind in ("ag", "bc") and cnt > small)
     if comm.get_param("user_ipc") or comm.get_param("force_shadow"):
@@ -964,6 +997,7 @@ def main():
         ("bcast_small_root0", lambda: case_bcast(comm, rank, n, 777, 0, 24)),
         ("bcast_big_rootlast", lambda: case_bcast(comm, rank, n, big * 4 + 3, n - 1, 25)),
         ("bcast_scatter_allgather", lambda: case_bcast_paths(comm, rank, n, 26)),
+        ("allgather_bcast_land_blocking", lambda: case_land_blocking(comm, rank, n, 27, big)),
         ("pipelined_nonblocking", lambda: case_pipelined(comm, rank, n, 26)),
         # reduce: staged (linear / binomial / binary by size) and zero-copy
         ("reduce_sum_f32_100_rootlast",
