@@ -289,6 +289,8 @@ def bench_allreduce(args, metric: str, link_gbs: float):
             res["config5"] = _config5(comm, dist, torch, mop, world, rank, tdev)
             _progress(rank, "extras: variants")
             res["variants"] = _variants(comm, dist, torch, mop, world, tdev)
+            _progress(rank, "extras: copy_nt")
+            res["copy_nt"] = _copy_nt(comm, dist, torch, mop, world, tdev, args.ar_bytes)
             _progress(rank, "extras: next_rows")
             res["next_rows"] = _next_rows(comm, dist, torch, mop, world, rank, tdev)
             _progress(rank, "extras: p2p_osc")
@@ -496,6 +498,38 @@ def _variants(comm, dist, torch, mop, world, tdev):
     comm.set_param("fused_bytes", 64 << 10)
     comm.set_param("small_bytes", 1 << 20)
     return out
+
+
+def _copy_nt(comm, dist, torch, mop, world, tdev, nbytes):
+    """A/B of the copy kernels' stores (param copy_nt: plain vs
+    non-temporal) on the headline allreduce as the library runs it
+    (autotuned scheme), with the per-phase kernel time of each."""
+    n = nbytes // 4
+    x = torch.ones(n, device="cuda")
+    y = torch.empty_like(x)
+    res = {}
+    try:
+        for nt in (0, 1):
+            comm.set_param("copy_nt", nt)
+            fn = lambda: comm.allreduce(x, y, n, mop.MPI_FLOAT, mop.MPI_SUM)  # noqa: E731
+            _settle(comm, fn, torch)
+            t = _timed(fn, 10, 3, dist, torch, tdev) / 10
+            comm.set_param("profile", 1)
+            for _ in range(5):
+                fn()
+            torch.cuda.synchronize()
+            comm.set_param("profile", 0)
+            ph = {}
+            for k, name in enumerate(("fold", "gather", "scatter")):
+                tot, calls = comm.phase_ms(k)  # read once: it resets the phase's record
+                if calls:
+                    ph[name] = round(tot / calls, 4)
+            res["nt" if nt else "plain"] = {"us": round(t * 1e6, 2),
+                                           "busbw": round(nbytes / t * 2 * (world - 1) / world / 1e9, 3),
+                                           "phase_kernel_ms": ph}
+    finally:
+        comm.set_param("copy_nt", 0)
+    return res
 
 
 def _next_rows(comm, dist, torch, mop, world, rank, tdev):

@@ -136,6 +136,9 @@ __global__ void peek_kernel(const uint64_t *src, uint64_t *dst) {
     *dst = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// NT: non-temporal stores (streaming cache policy) — param "copy_nt", an
+// A/B the 8-GPU bench measures for the remote stores of the scatter phases
+template <bool NT>
 __global__ __launch_bounds__(kXferThreads) void copy_kernel(cp_jobs jobs) {
     acquire_once();
     const cp_job jb = jobs.j[blockIdx.y];
@@ -157,12 +160,22 @@ __global__ __launch_bounds__(kXferThreads) void copy_kernel(cp_jobs jobs) {
             const u32x4 b = __builtin_nontemporal_load(s + i + gstride);
             const u32x4 c = __builtin_nontemporal_load(s + i + 2 * gstride);
             const u32x4 e = __builtin_nontemporal_load(s + i + 3 * gstride);
-            d[i] = a;
-            d[i + gstride] = b;
-            d[i + 2 * gstride] = c;
-            d[i + 3 * gstride] = e;
+            if constexpr (NT) {
+                __builtin_nontemporal_store(a, d + i);
+                __builtin_nontemporal_store(b, d + i + gstride);
+                __builtin_nontemporal_store(c, d + i + 2 * gstride);
+                __builtin_nontemporal_store(e, d + i + 3 * gstride);
+            } else {
+                d[i] = a;
+                d[i + gstride] = b;
+                d[i + 2 * gstride] = c;
+                d[i + 3 * gstride] = e;
+            }
         }
-        for (; i < nbody; i += gstride) d[i] = __builtin_nontemporal_load(s + i);
+        for (; i < nbody; i += gstride) {
+            if constexpr (NT) __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
+            else d[i] = __builtin_nontemporal_load(s + i);
+        }
     } else if (g == 4) {
         const uint32_t *s = reinterpret_cast<const uint32_t *>(sb);
         uint32_t *d = reinterpret_cast<uint32_t *>(db);
@@ -436,6 +449,7 @@ struct ompi_amd_comm {
     // param "land_blocking" (0): blocking allgather / bcast of a zero-copy
     // size take the landing path too (an A/B the 8-GPU bench measures)
     int land_blocking = 0;
+    int copy_nt = 0;  // param "copy_nt": the copy kernels store non-temporally
     int tuned_alg = 0;                    // coll_tuned_allreduce_algorithm (forced), 0 = fixed
     // this communicator's references to peer mappings (the mappings
     // themselves are process-wide: ipc_registry.h), least recently used
@@ -1137,8 +1151,12 @@ static int launch_copy(ompi_amd_comm_t *c, const cp_jobs &jobs, hipStream_t s) {
     for (int i = 0; i < jobs.n; ++i) most = std::max(most, jobs.j[i].bytes);
     int64_t blocks = (most / 16 + kXferThreads * 4 - 1) / (kXferThreads * 4);
     blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, std::max(1, c->max_blocks / jobs.n)));
-    hipLaunchKernelGGL(copy_kernel, dim3((unsigned)blocks, (unsigned)jobs.n), dim3(kXferThreads),
-                       0, s, jobs);
+    if (c->copy_nt)
+        hipLaunchKernelGGL(copy_kernel<true>, dim3((unsigned)blocks, (unsigned)jobs.n),
+                           dim3(kXferThreads), 0, s, jobs);
+    else
+        hipLaunchKernelGGL(copy_kernel<false>, dim3((unsigned)blocks, (unsigned)jobs.n),
+                           dim3(kXferThreads), 0, s, jobs);
     return record_hip(hipGetLastError(), "copy launch");
 }
 
@@ -2428,6 +2446,8 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
         c->autotune = v ? 1 : 0;
     } else if (!strcmp(key, "land_blocking")) {
         c->land_blocking = v ? 1 : 0;
+    } else if (!strcmp(key, "copy_nt")) {
+        c->copy_nt = v ? 1 : 0;
     } else if (!strcmp(key, "fused_bytes")) {
         if (v < 0) return OMPI_AMD_ERR_BAD_PARAM;
         c->fused_bytes = std::min<size_t>((size_t)v, c->scratch_bytes);
@@ -2467,6 +2487,7 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "nb_tuned_blocks")) *v = c->nb_tuned_blocks;
     else if (!strcmp(key, "landing_ag_bcast")) *v = c->land_ag_bcast;
     else if (!strcmp(key, "land_blocking")) *v = c->land_blocking;
+    else if (!strcmp(key, "copy_nt")) *v = c->copy_nt;
     else if (!strncmp(key, "autotune_", 9) && c->tune_last_key >= 0 &&
              c->tune.count(c->tune_last_key) && c->tune.at(c->tune_last_key).done) {
         // the last decided bucket: its choice and every candidate's worst rank

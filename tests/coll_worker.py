@@ -721,6 +721,29 @@ def case_bcast_paths(comm, rank, n, salt):
     return not msgs, "; ".join(msgs)
 
 
+def case_copy_nt(comm, rank, n, salt, big):
+    """param copy_nt = 1 (non-temporal stores in the copy kernels, the
+    8-GPU bench's A/B): a zero-copy allreduce on dataset R bit-exact against
+    the oracle, in place too, and a byte-exact allgather and bcast."""
+    F, SUM = mop.MPI_FLOAT, mop.MPI_SUM
+    msgs = []
+    comm.set_param("copy_nt", 1)
+    try:
+        for i, inplace in enumerate((False, True)):
+            ok, msg = case_allreduce(comm, rank, n, F, SUM, big + 13, salt + i, inplace=inplace)
+            if not ok:
+                msgs.append(f"allreduce{' in place' if inplace else ''}: {msg}")
+        ok, msg = case_allgather(comm, rank, n, (big * 4) // n + 9, salt + 5)
+        if not ok:
+            msgs.append(f"allgather: {msg or 'data differ'}")
+        ok, msg = case_bcast(comm, rank, n, big * 4 + 7, n - 1, salt + 6)
+        if not ok:
+            msgs.append(f"bcast: {msg or 'data differ'}")
+    finally:
+        comm.set_param("copy_nt", 0)
+    return not msgs, "; ".join(msgs)
+
+
 def case_land_blocking(comm, rank, n, salt, big):
     """param land_blocking = 1 (the 8-GPU bench's A/B): blocking allgather
     and bcast of zero-copy sizes through the landing buffers (stores into the
@@ -998,6 +1021,7 @@ def main():
         ("bcast_big_rootlast", lambda: case_bcast(comm, rank, n, big * 4 + 3, n - 1, 25)),
         ("bcast_scatter_allgather", lambda: case_bcast_paths(comm, rank, n, 26)),
         ("allgather_bcast_land_blocking", lambda: case_land_blocking(comm, rank, n, 27, big)),
+        ("copy_nt_stores", lambda: case_copy_nt(comm, rank, n, 28, big)),
         ("pipelined_nonblocking", lambda: case_pipelined(comm, rank, n, 26)),
         # reduce: staged (linear / binomial / binary by size) and zero-copy
         ("reduce_sum_f32_100_rootlast",
