@@ -65,6 +65,8 @@ typedef struct mca_coll_rocm_component_t {
     int algorithm;       /* coll_rocm_allreduce_algorithm (0 pull, 1 pull+push, 2 push) */
     int user_ipc;        /* coll_rocm_user_ipc: peers map the caller's buffers (else staged) */
     int autotune;        /* coll_rocm_autotune: measure the large-allreduce scheme and grid */
+    int land_blocking;   /* coll_rocm_land_blocking: blocking allgather / bcast by landing stores */
+    int copy_nt;         /* coll_rocm_copy_nt: non-temporal stores in the copy kernels */
     int residency;       /* coll_rocm_residency: 0 auto, 1 device, 2 host */
     int residency_lock;  /* coll_rocm_residency_lock: unanimous votes before locking (0 never) */
     int residency_recheck; /* coll_rocm_residency_recheck: locked calls per recheck vote (0 never) */

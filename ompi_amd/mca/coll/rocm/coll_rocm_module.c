@@ -71,6 +71,8 @@ mca_coll_rocm_component_t mca_coll_rocm_component = {
     .algorithm = 2,
     .user_ipc = 0,
     .autotune = 1,
+    .land_blocking = 0,
+    .copy_nt = 0,
     .residency = ROCM_RES_AUTO,
     .residency_lock = 8,
     .residency_recheck = 256,
@@ -122,6 +124,19 @@ static int rocm_register(void)
                                            MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_coll_rocm_component.autotune);
+    (void) mca_base_component_var_register(c, "land_blocking",
+                                           "1: blocking allgather / bcast of zero-copy sizes store into the "
+                                           "peers' landing buffers (as the nonblocking and persistent forms "
+                                           "always do) instead of pulling from the peers' shadows",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_coll_rocm_component.land_blocking);
+    (void) mca_base_component_var_register(c, "copy_nt",
+                                           "1: the collectives' copy kernels store non-temporally "
+                                           "(streaming cache policy)",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_coll_rocm_component.copy_nt);
     (void) mca_base_component_var_register(c, "residency",
                                            "Where blocking collectives run: 0 vote per call until the ranks "
                                            "agree coll_rocm_residency_lock times in a row, 1 device (host "
@@ -291,6 +306,8 @@ int mca_coll_rocm_module_enable(mca_coll_base_module_t *module, struct ompi_comm
     (void) ompi_amd_comm_set_param(m->dev_comm, "timeout_ms", mca_coll_rocm_component.timeout_ms);
     (void) ompi_amd_comm_set_param(m->dev_comm, "algorithm", mca_coll_rocm_component.algorithm);
     (void) ompi_amd_comm_set_param(m->dev_comm, "user_ipc", mca_coll_rocm_component.user_ipc);
+    (void) ompi_amd_comm_set_param(m->dev_comm, "land_blocking", mca_coll_rocm_component.land_blocking);
+    (void) ompi_amd_comm_set_param(m->dev_comm, "copy_nt", mca_coll_rocm_component.copy_nt);
     /* last: setting the scheme turns autotuning off */
     (void) ompi_amd_comm_set_param(m->dev_comm, "autotune", mca_coll_rocm_component.autotune);
     if (ROCM_RES_DEVICE == mca_coll_rocm_component.residency ||
