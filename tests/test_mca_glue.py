@@ -228,6 +228,13 @@ def _ooo_specs(golden):
         specs.append("\n".join(lines))
     specs.append("\n".join(["P position_long_double_int 2048 32 20", "B 2 0 16 16 4",
                             "D 3", "E 18 1 1 16 0", "E 6 1 1 4 16", "X 1 20", "S 113"]))
+    # position_noncontig.c (:33, :218-236): MPI_Type_vector(150, 1, 2, MPI_INT)
+    # of NELT = 300 ints, 113-byte segments (ints split across segments),
+    # shuffled, packed and unpacked out of order; the odd ints of the
+    # receive buffer stay untouched (:238-245)
+    specs.append("\n".join(["P position_noncontig_vector_int 1 1196 600",
+                            "B 150 " + " ".join(f"{8 * i} 4" for i in range(150)),
+                            "D 2", "E 6 150 1 8 0", "X 1 600", "S 113"]))
     return "\n".join(specs) + "\n"
 
 
@@ -263,11 +270,11 @@ def test_convertor_seam_fadvance(ddt_harness, golden):
     fixtures: unpack_ooo.c's four (bytes, offset) tables through
     opal_convertor_set_position + unpack, byte-exact against the expected
     layout the test checks (:125-131, gaps and padding untouched), and
-    position.c's reversed-segment replay."""
+    position.c's and position_noncontig.c's shuffled-segment replays."""
     r = subprocess.run([ddt_harness], capture_output=True, text=True, timeout=300,
                        input=_ddt_specs(golden) + _ooo_specs(golden),
                        env={**os.environ, "HARNESS_GPU": "1"})
     assert r.returncode == 0 and "all" in r.stdout, (r.stdout[-3000:], r.stderr[-2000:])
     for t in ("unpack_ooo_test1", "unpack_ooo_test2", "unpack_ooo_test3", "unpack_ooo_test4",
-              "position_long_double_int"):
+              "position_long_double_int", "position_noncontig_vector_int"):
         assert f"ok {t}" in r.stdout, r.stdout[-3000:]
