@@ -136,8 +136,9 @@ __global__ void peek_kernel(const uint64_t *src, uint64_t *dst) {
     *dst = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// NT: non-temporal stores (streaming cache policy) — param "copy_nt", an
-// A/B the 8-GPU bench measures for the remote stores of the scatter phases
+// NT: non-temporal stores (streaming cache policy) — param "copy_nt" (which
+// also sets the fold kernels' FOLD_NT_STORE), an A/B the 8-GPU bench
+// measures for the remote stores of the scatter and push phases
 template <bool NT>
 __global__ __launch_bounds__(kXferThreads) void copy_kernel(cp_jobs jobs) {
     acquire_once();
@@ -1386,7 +1387,7 @@ static int launch_reduce(ompi_amd_comm_t *c, int op, int type, const ptr_set &sr
     int64_t blocks = (most + per - 1) / per;
     blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, std::max(1, c->max_blocks / jobs.n)));
     return record_hip(f(dim3((unsigned)blocks, (unsigned)jobs.n), src, dst, ndst, nsrc, order,
-                        flags, jobs, s),
+                        flags | (c->copy_nt ? FOLD_NT_STORE : 0), jobs, s),
                       "reduce launch");
 }
 

@@ -35,6 +35,9 @@ enum order_t {
 // The root passed MPI_IN_PLACE: its first combine is f(own, child)
 // (coll_base_reduce.c:170-171, 196-199).
 constexpr int FOLD_ROOT_INPLACE = 1;
+// Launch flag, not a fold rule: the vector body stores non-temporally
+// (param "copy_nt", the 8-GPU bench's A/B; fold() never reads bit 16).
+constexpr int FOLD_NT_STORE = 1 << 16;
 
 // One reduction job: elements [off, off+cnt) of every source, combined in
 // the call's order and written to dst + off_dst (element units).
@@ -332,11 +335,20 @@ __global__ __launch_bounds__(kXferThreads) void reduce_kernel(ptr_set src, ptr_s
             for (int j = 0; j < NM; ++j) s[j] = v[j].e[e];
             out.e[e] = fold<T, OP, NM>(s, n, order, flags | jb.aux);
         }
+        if (flags & FOLD_NT_STORE) {
 #pragma unroll
-        for (int k = 0; k < NM; ++k)
-            if (k < ndst)
-                reinterpret_cast<u32x4 *>(reinterpret_cast<T *>(const_cast<char *>(dst.p[k])) +
-                                          jb.off_dst + head)[i] = out.v;
+            for (int k = 0; k < NM; ++k)
+                if (k < ndst)
+                    __builtin_nontemporal_store(
+                        out.v, reinterpret_cast<u32x4 *>(reinterpret_cast<T *>(const_cast<char *>(dst.p[k])) +
+                                                         jb.off_dst + head) + i);
+        } else {
+#pragma unroll
+            for (int k = 0; k < NM; ++k)
+                if (k < ndst)
+                    reinterpret_cast<u32x4 *>(reinterpret_cast<T *>(const_cast<char *>(dst.p[k])) +
+                                              jb.off_dst + head)[i] = out.v;
+        }
     }
     // scalar head [0, head) and tail [head + nvec*E, cnt)
     const int64_t tail0 = head + nvec * E;
