@@ -508,6 +508,7 @@ def _copy_nt(comm, dist, torch, mop, world, tdev, nbytes):
     x = torch.ones(n, device="cuda")
     y = torch.empty_like(x)
     res = {}
+    saved = comm.get_param("copy_nt")
     try:
         for nt in (0, 1):
             comm.set_param("copy_nt", nt)
@@ -528,7 +529,7 @@ def _copy_nt(comm, dist, torch, mop, world, tdev, nbytes):
                                            "busbw": round(nbytes / t * 2 * (world - 1) / world / 1e9, 3),
                                            "phase_kernel_ms": ph}
     finally:
-        comm.set_param("copy_nt", 0)
+        comm.set_param("copy_nt", saved)
     return res
 
 

@@ -72,7 +72,7 @@ mca_coll_rocm_component_t mca_coll_rocm_component = {
     .user_ipc = 0,
     .autotune = 1,
     .land_blocking = 0,
-    .copy_nt = 0,
+    .copy_nt = 1,
     .residency = ROCM_RES_AUTO,
     .residency_lock = 8,
     .residency_recheck = 256,
@@ -132,8 +132,8 @@ static int rocm_register(void)
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_coll_rocm_component.land_blocking);
     (void) mca_base_component_var_register(c, "copy_nt",
-                                           "1: the collectives' copy kernels store non-temporally "
-                                           "(streaming cache policy)",
+                                           "1 (default): the collectives' copy and fold kernels store "
+                                           "non-temporally (streaming cache policy); 0: plain stores",
                                            MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_coll_rocm_component.copy_nt);

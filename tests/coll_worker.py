@@ -722,12 +722,14 @@ def case_bcast_paths(comm, rank, n, salt):
 
 
 def case_copy_nt(comm, rank, n, salt, big):
-    """param copy_nt = 1 (non-temporal stores in the copy kernels, the
-    8-GPU bench's A/B): a zero-copy allreduce on dataset R bit-exact against
-    the oracle, in place too, and a byte-exact allgather and bcast."""
+    """param copy_nt flipped from its default (non-temporal vs plain stores
+    in the copy and fold kernels, the 8-GPU bench's A/B): a zero-copy
+    allreduce on dataset R bit-exact against the oracle, in place too, and a
+    byte-exact allgather and bcast."""
     F, SUM = mop.MPI_FLOAT, mop.MPI_SUM
     msgs = []
-    comm.set_param("copy_nt", 1)
+    saved = comm.get_param("copy_nt")
+    comm.set_param("copy_nt", 1 - saved)  # the non-default store kind (the default runs everywhere else)
     try:
         for i, inplace in enumerate((False, True)):
             ok, msg = case_allreduce(comm, rank, n, F, SUM, big + 13, salt + i, inplace=inplace)
@@ -740,7 +742,7 @@ def case_copy_nt(comm, rank, n, salt, big):
         if not ok:
             msgs.append(f"bcast: {msg or 'data differ'}")
     finally:
-        comm.set_param("copy_nt", 0)
+        comm.set_param("copy_nt", saved)
     return not msgs, "; ".join(msgs)
 
 
