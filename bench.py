@@ -154,8 +154,28 @@ def load_traffic(key: str):
         return None
 
 
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` started without a launcher: run the same command
+    as N ranks under torch.distributed.run (one process per GPU, rendezvous
+    on 127.0.0.1) and return its exit status.  Called before anything here
+    touches the GPU; the ranks are children, so nothing is exec'd."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] no WORLD_SIZE: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd).returncode
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 or args.gpus > 1:
         from ompi_amd import coll_bench

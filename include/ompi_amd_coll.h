@@ -183,11 +183,26 @@ int ompi_amd_allgather_init(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
                             ompi_amd_plan_t **plan);
 int ompi_amd_bcast_init(ompi_amd_comm_t *comm, void *buf, size_t bytes, int root,
                         ompi_amd_plan_t **plan);
+/* Persistent reduce / reduce_scatter / scan / exscan (MPI-4 MPI_Reduce_init,
+ * MPI_Reduce_scatter_init, MPI_Scan_init, MPI_Exscan_init; coll.h:561-567
+ * coll_reduce_init / coll_reduce_scatter_init / coll_scan_init /
+ * coll_exscan_init).  Plans of kind 4, as above: local at init, every start
+ * posts ompi_amd_ireduce / _ireduce_scatter / _iscan / _iexscan with the
+ * init's arguments (rcounts is copied at init).  Results exactly those of
+ * the blocking calls. */
+int ompi_amd_reduce_init(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf, size_t count,
+                         int type, int op, int root, ompi_amd_plan_t **plan);
+int ompi_amd_reduce_scatter_init(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf,
+                                 const size_t *rcounts, int type, int op, ompi_amd_plan_t **plan);
+int ompi_amd_scan_init(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf, size_t count,
+                       int type, int op, ompi_amd_plan_t **plan);
+int ompi_amd_exscan_init(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf, size_t count,
+                         int type, int op, ompi_amd_plan_t **plan);
 /* Which path a plan's starts take (diagnostics / tests): 0 = the plain call
  * re-run (fused / staged sizes, and the default push-gather scheme at any
  * size: no handle swap), 1 pull, 2 pull+push, 3 push with the caller's
  * buffers mapped (user_ipc), 4 a persistent reduce_scatter_block /
- * allgather / bcast; -1 for NULL. */
+ * allgather / bcast / reduce / reduce_scatter / scan / exscan; -1 for NULL. */
 int ompi_amd_plan_kind(const ompi_amd_plan_t *plan);
 /* Nonblocking allreduce (MPI_Iallreduce, coll.h:271-274; libnbc's
  * ompi_coll_libnbc_iallreduce in the reference).  Returns without waiting

@@ -176,6 +176,16 @@ PROTOTYPES = [
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.POINTER(_C.c_void_p)]),
     ("ompi_amd_bcast_init", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_reduce_init", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_int,
+      _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_reduce_scatter_init", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.POINTER(_C.c_size_t), _C.c_int, _C.c_int,
+      _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_scan_init", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_exscan_init", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.POINTER(_C.c_void_p)]),
     ("ompi_amd_request_test", _C.c_int, [_C.c_void_p, _C.POINTER(_C.c_int)]),
     ("ompi_amd_request_wait", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_request_free", _C.c_int, [_C.c_void_p]),

@@ -268,6 +268,36 @@ class Communicator:
                    "bcast_init")
         return Plan(self, h, "bcast")
 
+    def reduce_init(self, sbuf, rbuf, count: int, datatype: Datatype, op: Op, root: int) -> "Plan":
+        """MPI_Reduce_init (coll.h:561 coll_reduce_init): every start posts ireduce."""
+        h = ctypes.c_void_p()
+        what = f"reduce({op.name},{datatype.name},root={root})"
+        _lib.check(self._lib.ompi_amd_reduce_init(self._h, _ptr(sbuf),
+                                                  _ptr(rbuf) if rbuf is not None else None, count,
+                                                  datatype.code, op.index, root, ctypes.byref(h)),
+                   what + "_init")
+        return Plan(self, h, what)
+
+    def reduce_scatter_init(self, sbuf, rbuf, rcounts, datatype: Datatype, op: Op) -> "Plan":
+        """MPI_Reduce_scatter_init (coll.h:562 coll_reduce_scatter_init)."""
+        h = ctypes.c_void_p()
+        arr = (ctypes.c_size_t * self.size)(*[int(c) for c in rcounts])
+        what = f"reduce_scatter({op.name},{datatype.name})"
+        _lib.check(self._lib.ompi_amd_reduce_scatter_init(self._h, _ptr(sbuf), _ptr(rbuf), arr,
+                                                          datatype.code, op.index, ctypes.byref(h)),
+                   what + "_init")
+        return Plan(self, h, what)
+
+    def scan_init(self, sbuf, rbuf, count: int, datatype: Datatype, op: Op,
+                  exclusive: bool = False) -> "Plan":
+        """MPI_Scan_init / MPI_Exscan_init (coll.h:558, 564)."""
+        h = ctypes.c_void_p()
+        fn = self._lib.ompi_amd_exscan_init if exclusive else self._lib.ompi_amd_scan_init
+        what = f"{'exscan' if exclusive else 'scan'}({op.name},{datatype.name})"
+        _lib.check(fn(self._h, _ptr(sbuf), _ptr(rbuf), count, datatype.code, op.index, ctypes.byref(h)),
+                   what + "_init")
+        return Plan(self, h, what)
+
     def __del__(self):
         # destroy is collective; only an explicit free() releases the comm
         pass

@@ -18,9 +18,10 @@ import time
 
 _PHASE = {"what": None, "t0": 0.0, "pending": None}
 # An extras phase (after the headline was measured) that runs longer than
-# this is taken as stuck: every rank's watchdog ends its process, and rank 0
-# first prints the headline line it already holds, so a hang in a side row
-# never costs the driver the headline.
+# this is taken as stuck: every rank's watchdog ends its process with exit
+# status 3, and rank 0 first prints the headline line it already holds, so a
+# hang in a side row never costs the driver the headline and never passes
+# for a clean run.
 EXTRAS_PHASE_LIMIT_S = float(os.environ.get("OMPI_AMD_BENCH_EXTRAS_LIMIT_S", "240"))
 
 
@@ -63,7 +64,7 @@ def _watchdog(comm, rank, world):
                                                f"{time.time() - t0:.0f} s; extras abandoned")
                     print(json.dumps(dict(pending)), flush=True)
                 sys.stderr.flush()
-                os._exit(0)
+                os._exit(3)  # the headline line is out; the run still failed
 
     threading.Thread(target=run, daemon=True).start()
 
@@ -84,10 +85,10 @@ def _timed(fn, steps, warmup, dist, torch, dev="cuda"):
     return float(t.item())
 
 
-def _settle(comm, fn, torch, limit=24):
+def _settle(comm, fn, torch, limit=48):
     """Run a blocking allreduce until the library's autotune of its size
     bucket has decided (autotune_state 2), or it does not tune this size
-    (state stays 0 or a settled bucket's 2): the first kTuneCalls = 18
+    (state stays 0 or a settled bucket's 2): the first kTuneCalls = 36
     calls of a new large size try every candidate, slow grids included, and
     must not land inside a timed region (coll_ipc.hip, ompi_amd_allreduce).
     Every rank makes the same calls, so every rank stops at the same one."""
@@ -156,7 +157,7 @@ def bench_allreduce(args, metric: str, link_gbs: float):
         comm.set_param("autotune", 1)
         _progress(rank, "autotune: one call per candidate")
         calls = 0
-        while calls < 24:  # 9 candidates x 2 rounds decide at the 18th
+        while calls < 48:  # 18 candidates (9 with copy_nt fixed) x 2 rounds decide at the 36th
             ours()
             torch.cuda.synchronize()
             calls += 1
@@ -164,13 +165,16 @@ def bench_allreduce(args, metric: str, link_gbs: float):
                 break
         if comm.get_param("autotune_state") == 2:
             a_c, b_c = comm.get_param("autotune_algorithm"), comm.get_param("autotune_blocks")
+            nt_c = comm.get_param("autotune_copy_nt")
             best = {"algorithm": a_c}
-            best_name = f"{dict(ALGORITHMS)[a_c]}/staged/{b_c}"
+            best_name = f"{dict(ALGORITHMS)[a_c]}/staged/{b_c}/{'nt' if nt_c else 'plain'}"
             autotune = {"choice": best_name, "calls": calls,
                         "worst_rank_us": {
                             f"{dict(ALGORITHMS)[comm.get_param(f'autotune_alg{k}')]}/staged/"
-                            f"{comm.get_param(f'autotune_grid{k}')}": comm.get_param(f"autotune_us{k}")
-                            for k in range(9)}}
+                            f"{comm.get_param(f'autotune_grid{k}')}/"
+                            f"{'nt' if comm.get_param(f'autotune_nt{k}') else 'plain'}":
+                            comm.get_param(f"autotune_us{k}")
+                            for k in range(comm.get_param("autotune_ncand"))}}
 
     _progress(rank, f"headline: {best_name}")
     t = _timed(ours, args.steps, args.warmup, dist, torch, tdev)
@@ -272,6 +276,9 @@ def bench_allreduce(args, metric: str, link_gbs: float):
         # the extras allocate buffers per size: the library default (staged)
         _PHASE["pending"] = res
         try:
+            if os.environ.get("OMPI_AMD_BENCH_TEST_HANG"):  # the watchdog's own test
+                _progress(rank, "extras: forced hang")
+                time.sleep(1e9)
             if not os.environ.get("OMPI_AMD_BENCH_NO_SCHEMES"):
                 res["config"]["schemes"] = _schemes(comm, dist, torch, mop, n, rank, shared,
                                                     tdev, ours, default)
@@ -508,7 +515,7 @@ def _copy_nt(comm, dist, torch, mop, world, tdev, nbytes):
     x = torch.ones(n, device="cuda")
     y = torch.empty_like(x)
     res = {}
-    saved = comm.get_param("copy_nt")
+    saved = comm.get_param("copy_nt") if comm.get_param("copy_nt_fixed") else -1
     try:
         for nt in (0, 1):
             comm.set_param("copy_nt", nt)

@@ -288,6 +288,7 @@ struct path_params {
     int root0_inplace;  // forced nonoverlapping only: rank 0 passed MPI_IN_PLACE
     int push_gather;    // push / push-land scheme, staged (user_ipc 0): no handle swap at all
     int blocks = 0;     // transfer grid of a deferred call (nb_tuned); 0: the communicator's
+    int copy_nt = -1;   // store kind of the copy / fold kernels (autotune); -1: the communicator's
 };
 
 // Export fallback.  hipIpcGetMemHandle sometimes refuses a live device
@@ -359,15 +360,23 @@ struct ompi_amd_request {
 // makes the same calls.  coll/tuned's dynamic rules pick from a table;
 // this picks from measurements on the machine it runs on (xGMI loads vs
 // stores and the grid that saturates the links are not knowable offline).
-constexpr int kTuneCands = 9, kTuneRounds = 2, kTuneCalls = kTuneCands * kTuneRounds;
+// The store kind of the copy and fold kernels (non-temporal or plain) is a
+// third dimension unless param copy_nt fixed it: remote xGMI stores may
+// prefer either, and one GPU cannot tell — 18 candidates
+// then, 9 with it fixed.
+constexpr int kTuneGrid = 9, kTuneCands = 2 * kTuneGrid, kTuneRounds = 2,
+              kTuneCalls = kTuneCands * kTuneRounds;
 struct tune_cand {
-    int algorithm, blocks;
+    int algorithm, blocks, nt;  // nt: 1 non-temporal stores, 0 plain
 };
-static const tune_cand kTune[kTuneCands] = {{2, 1024}, {2, 512}, {2, 256},
-                                            {3, 1024}, {3, 512}, {3, 256},
-                                            {0, 1024}, {0, 512}, {0, 256}};
+static const tune_cand kTune[kTuneCands] = {
+    {2, 1024, 1}, {2, 512, 1}, {2, 256, 1}, {3, 1024, 1}, {3, 512, 1}, {3, 256, 1},
+    {0, 1024, 1}, {0, 512, 1}, {0, 256, 1},
+    {2, 1024, 0}, {2, 512, 0}, {2, 256, 0}, {3, 1024, 0}, {3, 512, 0}, {3, 256, 0},
+    {0, 1024, 0}, {0, 512, 0}, {0, 256, 0}};
 struct tune_bucket {
-    int next = 0;  // calls made so far; call k runs candidate k % kTuneCands
+    int ncand = kTuneCands;  // candidates tried: kTuneGrid when copy_nt is fixed
+    int next = 0;            // calls made so far; call k runs candidate k % ncand
     bool done = false;
     int choice = 0;
     hipEvent_t ev[2 * kTuneCalls] = {};
@@ -445,15 +454,17 @@ struct ompi_amd_comm {
     int tune_last_key = -1;
     // the scheme / grid the last nonblocking or persistent allreduce of an
     // autotuned size took (nb_tuned; -1: none yet)
-    int nb_tuned_alg = -1, nb_tuned_blocks = -1;
+    int nb_tuned_alg = -1, nb_tuned_blocks = -1, nb_tuned_nt = -1;
     int64_t land_ag_bcast = 0;  // allgathers / bcasts run through the landing buffers
     // param "land_blocking" (0): blocking allgather / bcast of a zero-copy
     // size take the landing path too (an A/B the 8-GPU bench measures)
     int land_blocking = 0;
-    // param "copy_nt" (1): the copy and fold kernels store non-temporally —
+    // param "copy_nt": 1 the copy and fold kernels store non-temporally —
     // measured no slower on one GPU at N = 2 / 4 / 8 (scatter, gather and fold
-    // kernels 1-5 % faster); 0 restores plain stores
+    // kernels 1-5 % faster) — 0 plain stores; -1 (default)
+    // non-temporal, and the autotune measures both (copy_nt_fixed 0)
     int copy_nt = 1;
+    int copy_nt_fixed = 0;
     int tuned_alg = 0;                    // coll_tuned_allreduce_algorithm (forced), 0 = fixed
     // this communicator's references to peer mappings (the mappings
     // themselves are process-wide: ipc_registry.h), least recently used
@@ -513,6 +524,8 @@ struct ompi_amd_plan {
     int nb_kind = -1;
     int root = 0;
     size_t bytes = 0;
+    bool exclusive = false;        // PEND_SCAN: exscan
+    std::vector<size_t> rcounts;   // PEND_RS: the init's counts
     ompi_amd_request *req = nullptr;
 };
 
@@ -2021,16 +2034,18 @@ static void nb_tuned(ompi_amd_comm_t *c, path_params *pp, size_t count, int type
     const auto it = c->tune.find(63 - __builtin_clzll((unsigned long long)bytes));
     if (it == c->tune.end() || !it->second.done) return;
     int best = -1;
-    for (int k = 0; k < kTuneCands; ++k)
+    for (int k = 0; k < it->second.ncand; ++k)
         if (is_push(kTune[k].algorithm) &&
             (best < 0 || it->second.worst_ms[k] < it->second.worst_ms[best]))
             best = k;
     if (best < 0) return;
     pp->algorithm = kTune[best].algorithm;
     pp->blocks = kTune[best].blocks;
+    if (it->second.ncand == kTuneCands) pp->copy_nt = kTune[best].nt;
     pp->push_gather = 1;
     c->nb_tuned_alg = pp->algorithm;
     c->nb_tuned_blocks = pp->blocks;
+    c->nb_tuned_nt = pp->copy_nt >= 0 ? pp->copy_nt : c->copy_nt;
 }
 
 static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
@@ -2145,10 +2160,14 @@ static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size
     // a deferred call's own grid (nb_tuned) for the launches below
     struct grid_scope {
         ompi_amd_comm_t *c;
-        int saved;
-        ~grid_scope() { c->max_blocks = saved; }
-    } grid{c, c->max_blocks};
+        int saved, saved_nt;
+        ~grid_scope() {
+            c->max_blocks = saved;
+            c->copy_nt = saved_nt;
+        }
+    } grid{c, c->max_blocks, c->copy_nt};
     if (pp.blocks > 0) c->max_blocks = pp.blocks;
+    if (pp.copy_nt >= 0) c->copy_nt = pp.copy_nt;
     const size_t ext = ompi_amd_type_extent(type);
     const size_t bytes = count * ext;
     const bool inplace = in_place(sbuf, rbuf);
@@ -2451,7 +2470,8 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
     } else if (!strcmp(key, "land_blocking")) {
         c->land_blocking = v ? 1 : 0;
     } else if (!strcmp(key, "copy_nt")) {
-        c->copy_nt = v ? 1 : 0;
+        c->copy_nt_fixed = v >= 0;
+        c->copy_nt = v != 0 ? 1 : 0;
     } else if (!strcmp(key, "fused_bytes")) {
         if (v < 0) return OMPI_AMD_ERR_BAD_PARAM;
         c->fused_bytes = std::min<size_t>((size_t)v, c->scratch_bytes);
@@ -2476,6 +2496,11 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
     return OMPI_AMD_SUCCESS;
 }
 
+// the store kind candidate k of a bucket ran with (a fixed copy_nt: that)
+static int tune_nt(const ompi_amd_comm_t *c, const tune_bucket &tb, int k) {
+    return tb.ncand == kTuneCands ? kTune[k].nt : c->copy_nt;
+}
+
 int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *v) {
     if (!c || !key || !v) return OMPI_AMD_ERR_BAD_PARAM;
     if (!strcmp(key, "small_bytes")) *v = (int64_t)c->small_bytes;
@@ -2489,21 +2514,28 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "autotune_state")) *v = c->tune_last;
     else if (!strcmp(key, "nb_tuned_algorithm")) *v = c->nb_tuned_alg;
     else if (!strcmp(key, "nb_tuned_blocks")) *v = c->nb_tuned_blocks;
+    else if (!strcmp(key, "nb_tuned_copy_nt")) *v = c->nb_tuned_nt;
     else if (!strcmp(key, "landing_ag_bcast")) *v = c->land_ag_bcast;
     else if (!strcmp(key, "land_blocking")) *v = c->land_blocking;
     else if (!strcmp(key, "copy_nt")) *v = c->copy_nt;
+    else if (!strcmp(key, "copy_nt_fixed")) *v = c->copy_nt_fixed;
     else if (!strncmp(key, "autotune_", 9) && c->tune_last_key >= 0 &&
              c->tune.count(c->tune_last_key) && c->tune.at(c->tune_last_key).done) {
         // the last decided bucket: its choice and every candidate's worst rank
         const tune_bucket &tb = c->tune.at(c->tune_last_key);
+        const auto idx = [&](int at) { return atoi(key + at) >= 0 && atoi(key + at) < tb.ncand; };
         if (!strcmp(key, "autotune_algorithm")) *v = kTune[tb.choice].algorithm;
         else if (!strcmp(key, "autotune_blocks")) *v = kTune[tb.choice].blocks;
-        else if (!strncmp(key, "autotune_us", 11) && atoi(key + 11) >= 0 && atoi(key + 11) < kTuneCands)
+        else if (!strcmp(key, "autotune_copy_nt")) *v = tune_nt(c, tb, tb.choice);
+        else if (!strcmp(key, "autotune_ncand")) *v = tb.ncand;
+        else if (!strncmp(key, "autotune_us", 11) && idx(11))
             *v = (int64_t)(tb.worst_ms[atoi(key + 11)] * 1000.f);
-        else if (!strncmp(key, "autotune_alg", 12) && atoi(key + 12) >= 0 && atoi(key + 12) < kTuneCands)
+        else if (!strncmp(key, "autotune_alg", 12) && idx(12))
             *v = kTune[atoi(key + 12)].algorithm;
-        else if (!strncmp(key, "autotune_grid", 13) && atoi(key + 13) >= 0 && atoi(key + 13) < kTuneCands)
+        else if (!strncmp(key, "autotune_grid", 13) && idx(13))
             *v = kTune[atoi(key + 13)].blocks;
+        else if (!strncmp(key, "autotune_nt", 11) && idx(11))
+            *v = tune_nt(c, tb, atoi(key + 11));
         else return OMPI_AMD_ERR_BAD_PARAM;
     }
     else if (!strcmp(key, "tuned_allreduce_algorithm")) *v = c->tuned_alg;
@@ -2562,13 +2594,16 @@ int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
         allreduce_swaps(c, pp, count, type)) {
         const size_t bytes = count * ompi_amd_type_extent(type);
         const int key = 63 - __builtin_clzll((unsigned long long)bytes);
+        const bool fresh = !c->tune.count(key);
         tb = &c->tune[key];
+        if (fresh) tb->ncand = c->copy_nt_fixed ? kTuneGrid : kTuneCands;
         c->tune_last_key = key;
-        cand = tb->done ? -1 : tb->next;  // the call's slot; candidate cand % kTuneCands
-        const tune_cand &tc = kTune[tb->done ? tb->choice : cand % kTuneCands];
+        cand = tb->done ? -1 : tb->next;  // the call's slot; candidate cand % ncand
+        const tune_cand &tc = kTune[tb->done ? tb->choice : cand % tb->ncand];
         c->algorithm = tc.algorithm;
         c->max_blocks = tc.blocks;
         pp = params_of(c);
+        if (tb->ncand == kTuneCands) pp.copy_nt = tc.nt;
         if (cand >= 0) {
             for (int k = 0; k < 2; ++k)
                 if (!tb->ev[2 * cand + k])
@@ -2586,21 +2621,21 @@ int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
     c->max_blocks = save_blocks;
     if (cand >= 0) {
         if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipEventRecord(tb->ev[2 * cand + 1], s), "autotune event");
-        if (++tb->next == kTuneCalls) {  // every rank is at this call: decide together
+        if (++tb->next == tb->ncand * kTuneRounds) {  // every rank is at this call: decide together
             float mine[kTuneCands], all[kMaxRanks][kTuneCands];
             for (int k = 0; k < kTuneCands; ++k) mine[k] = 1e30f;
-            for (int call = 0; call < kTuneCalls; ++call) {
+            for (int call = 0; call < tb->ncand * kTuneRounds; ++call) {
                 float ms = 1e30f;
                 if (rc == OMPI_AMD_SUCCESS && hipEventSynchronize(tb->ev[2 * call + 1]) == hipSuccess &&
                     hipEventElapsedTime(&ms, tb->ev[2 * call], tb->ev[2 * call + 1]) != hipSuccess)
                     ms = 1e30f;
                 (void)hipGetLastError();
-                mine[call % kTuneCands] = std::min(mine[call % kTuneCands], ms);
+                mine[call % tb->ncand] = std::min(mine[call % tb->ncand], ms);
             }
             const int arc = comm_allgather(c, mine, all, sizeof(mine));
             if (rc == OMPI_AMD_SUCCESS) rc = arc;
             int best = 0;
-            for (int k = 0; k < kTuneCands; ++k) {
+            for (int k = 0; k < tb->ncand; ++k) {
                 float w = 0.f;
                 for (int p = 0; p < c->size; ++p) w = std::max(w, arc == OMPI_AMD_SUCCESS ? all[p][k] : 0.f);
                 tb->worst_ms[k] = w;
@@ -3562,6 +3597,15 @@ static int plan_nb_post(ompi_amd_plan_t *pl, void *stream) {
         return ompi_amd_iallgather(c, pl->src, pl->rbuf, pl->bytes, stream, &pl->req);
     case PEND_BCAST:
         return ompi_amd_ibcast(c, pl->rbuf, pl->bytes, pl->root, stream, &pl->req);
+    case PEND_REDUCE:
+        return ompi_amd_ireduce(c, pl->src, pl->rbuf, (size_t)pl->count, pl->type, pl->op, pl->root,
+                                stream, &pl->req);
+    case PEND_SCAN:
+        return (pl->exclusive ? ompi_amd_iexscan : ompi_amd_iscan)(c, pl->src, pl->rbuf, (size_t)pl->count,
+                                                                   pl->type, pl->op, stream, &pl->req);
+    case PEND_RS:
+        return ompi_amd_ireduce_scatter(c, pl->src, pl->rbuf, pl->rcounts.data(), pl->type, pl->op, stream,
+                                        &pl->req);
     default:
         return OMPI_AMD_ERR_BAD_PARAM;
     }
@@ -3604,6 +3648,42 @@ int ompi_amd_bcast_init(ompi_amd_comm_t *c, void *buf, size_t bytes, int root,
                         ompi_amd_plan_t **out) {
     if (!c || !buf || !out || root < 0 || root >= c->size) return OMPI_AMD_ERR_BAD_PARAM;
     return plan_nb_new(c, PEND_BCAST, buf, buf, 0, 0, 0, root, bytes, out);
+}
+
+int ompi_amd_reduce_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
+                         int op, int root, ompi_amd_plan_t **out) {
+    if (!c || !out || root < 0 || root >= c->size || (c->rank == root && !rbuf))
+        return OMPI_AMD_ERR_BAD_PARAM;
+    if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
+    return plan_nb_new(c, PEND_REDUCE, sbuf, rbuf, count, type, op, root, 0, out);
+}
+
+int ompi_amd_reduce_scatter_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
+                                 const size_t *rcounts, int type, int op, ompi_amd_plan_t **out) {
+    if (!c || !rbuf || !rcounts || !out) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
+    TRY(plan_nb_new(c, PEND_RS, sbuf, rbuf, 0, type, op, 0, 0, out));
+    (*out)->rcounts.assign(rcounts, rcounts + c->size);
+    return OMPI_AMD_SUCCESS;
+}
+
+static int scan_init_common(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
+                            int op, bool exclusive, ompi_amd_plan_t **out) {
+    if (!c || !rbuf || !out) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
+    TRY(plan_nb_new(c, PEND_SCAN, sbuf, rbuf, count, type, op, 0, 0, out));
+    (*out)->exclusive = exclusive;
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_scan_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op,
+                       ompi_amd_plan_t **out) {
+    return scan_init_common(c, sbuf, rbuf, count, type, op, false, out);
+}
+
+int ompi_amd_exscan_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
+                         int op, ompi_amd_plan_t **out) {
+    return scan_init_common(c, sbuf, rbuf, count, type, op, true, out);
 }
 
 int ompi_amd_plan_start(ompi_amd_plan_t *pl, void *stream) {

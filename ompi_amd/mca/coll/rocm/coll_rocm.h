@@ -66,7 +66,7 @@ typedef struct mca_coll_rocm_component_t {
     int user_ipc;        /* coll_rocm_user_ipc: peers map the caller's buffers (else staged) */
     int autotune;        /* coll_rocm_autotune: measure the large-allreduce scheme and grid */
     int land_blocking;   /* coll_rocm_land_blocking: blocking allgather / bcast by landing stores */
-    int copy_nt;         /* coll_rocm_copy_nt: non-temporal stores in the copy kernels */
+    int copy_nt;         /* coll_rocm_copy_nt: non-temporal stores in the copy kernels (-1 autotuned) */
     int residency;       /* coll_rocm_residency: 0 auto, 1 device, 2 host */
     int residency_lock;  /* coll_rocm_residency_lock: unanimous votes before locking (0 never) */
     int residency_recheck; /* coll_rocm_residency_recheck: locked calls per recheck vote (0 never) */
@@ -83,7 +83,10 @@ typedef struct mca_coll_rocm_request_t {
     ompi_request_t super;
     ompi_amd_plan_t *plan;       /* persistent */
     ompi_amd_request_t *nbreq;   /* nonblocking */
-    struct rocm_nb_stage *stage; /* nonblocking: this rank's staged operands */
+    /* the saved (libnbc) function's request when it runs on host copies of
+     * this rank's device operands (nonblocking or persistent) */
+    ompi_request_t *inner;
+    struct rocm_nb_stage *stage; /* this rank's staged operands */
     struct mca_coll_rocm_request_t *next_active; /* started, not yet complete */
 } mca_coll_rocm_request_t;
 
@@ -163,6 +166,22 @@ int mca_coll_rocm_allgather_init(const void *sbuf, int scount, struct ompi_datat
 int mca_coll_rocm_bcast_init(void *buf, int count, struct ompi_datatype_t *dtype, int root,
                              struct ompi_communicator_t *comm, struct ompi_info_t *info,
                              ompi_request_t **request, mca_coll_base_module_t *module);
+int mca_coll_rocm_reduce_init(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                              struct ompi_op_t *op, int root, struct ompi_communicator_t *comm,
+                              struct ompi_info_t *info, ompi_request_t **request,
+                              mca_coll_base_module_t *module);
+int mca_coll_rocm_reduce_scatter_init(const void *sbuf, void *rbuf, const int *rcounts,
+                                      struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                      struct ompi_communicator_t *comm, struct ompi_info_t *info,
+                                      ompi_request_t **request, mca_coll_base_module_t *module);
+int mca_coll_rocm_scan_init(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                            struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                            struct ompi_info_t *info, ompi_request_t **request,
+                            mca_coll_base_module_t *module);
+int mca_coll_rocm_exscan_init(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                              struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                              struct ompi_info_t *info, ompi_request_t **request,
+                              mca_coll_base_module_t *module);
 
 END_C_DECLS
 

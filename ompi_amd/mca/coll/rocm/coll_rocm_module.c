@@ -72,7 +72,7 @@ mca_coll_rocm_component_t mca_coll_rocm_component = {
     .user_ipc = 0,
     .autotune = 1,
     .land_blocking = 0,
-    .copy_nt = 1,
+    .copy_nt = -1,
     .residency = ROCM_RES_AUTO,
     .residency_lock = 8,
     .residency_recheck = 256,
@@ -132,8 +132,10 @@ static int rocm_register(void)
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_coll_rocm_component.land_blocking);
     (void) mca_base_component_var_register(c, "copy_nt",
-                                           "1 (default): the collectives' copy and fold kernels store "
-                                           "non-temporally (streaming cache policy); 0: plain stores",
+                                           "1: the collectives' copy and fold kernels store "
+                                           "non-temporally (streaming cache policy); 0: plain stores; "
+                                           "-1 (default): non-temporal, and the large-allreduce "
+                                           "autotune measures both kinds",
                                            MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_coll_rocm_component.copy_nt);
@@ -210,6 +212,11 @@ static void rocm_module_destruct(mca_coll_rocm_module_t *m)
     if (NULL != m->c_coll.coll_allgather_init_module)
         OBJ_RELEASE(m->c_coll.coll_allgather_init_module);
     if (NULL != m->c_coll.coll_bcast_init_module) OBJ_RELEASE(m->c_coll.coll_bcast_init_module);
+    if (NULL != m->c_coll.coll_reduce_init_module) OBJ_RELEASE(m->c_coll.coll_reduce_init_module);
+    if (NULL != m->c_coll.coll_reduce_scatter_init_module)
+        OBJ_RELEASE(m->c_coll.coll_reduce_scatter_init_module);
+    if (NULL != m->c_coll.coll_scan_init_module) OBJ_RELEASE(m->c_coll.coll_scan_init_module);
+    if (NULL != m->c_coll.coll_exscan_init_module) OBJ_RELEASE(m->c_coll.coll_exscan_init_module);
     if (NULL != m->dev_comm) (void) ompi_amd_comm_destroy(m->dev_comm);
     for (int k = 0; k < 2; ++k) {
         (void) ompi_amd_device_free(m->dstage[k]);
@@ -258,6 +265,10 @@ mca_coll_base_module_t *mca_coll_rocm_comm_query(struct ompi_communicator_t *com
     m->super.coll_reduce_scatter_block_init = mca_coll_rocm_reduce_scatter_block_init;
     m->super.coll_allgather_init = mca_coll_rocm_allgather_init;
     m->super.coll_bcast_init = mca_coll_rocm_bcast_init;
+    m->super.coll_reduce_init = mca_coll_rocm_reduce_init;
+    m->super.coll_reduce_scatter_init = mca_coll_rocm_reduce_scatter_init;
+    m->super.coll_scan_init = mca_coll_rocm_scan_init;
+    m->super.coll_exscan_init = mca_coll_rocm_exscan_init;
     return &m->super;
 }
 
@@ -294,6 +305,10 @@ int mca_coll_rocm_module_enable(mca_coll_base_module_t *module, struct ompi_comm
     SAVE(reduce_scatter_block_init);
     SAVE(allgather_init);
     SAVE(bcast_init);
+    SAVE(reduce_init);
+    SAVE(reduce_scatter_init);
+    SAVE(scan_init);
+    SAVE(exscan_init);
 #undef SAVE
 
     /* node-unique segment name: job id + communicator id */
@@ -555,7 +570,14 @@ static int rocm_unstage(mca_coll_rocm_module_t *m, const rocm_operand_t *o, int 
     return rocm_unstage_ops(o, n, rc);
 }
 
-/* decide, and stage for the decision: *path is ROCM_DEVICE or a saved path */
+/* Decide, and stage for the decision: *path is ROCM_DEVICE or a saved path.
+ * The saved functions (coll/tuned, coll/basic) run on the host: whatever
+ * the reason the device path is not taken — a user op, a derived datatype,
+ * a slot without a device kernel, a vector past max_device_mib, or peers
+ * whose operands are host memory — this rank's device operands are copied
+ * to host memory first and its outputs back after, as coll/cuda does for
+ * every call it wraps (coll_cuda_allreduce.c:42-72).  Host operands go as
+ * they are. */
 static int rocm_begin(mca_coll_rocm_module_t *m, int uniform_ok, int local_dev,
                       rocm_operand_t *o, int n, int *path)
 {
@@ -565,7 +587,6 @@ static int rocm_begin(mca_coll_rocm_module_t *m, int uniform_ok, int local_dev,
         o[i].how = 0;
         o[i].hbuf = NULL;
     }
-    if (ROCM_SAVED == *path) return OMPI_SUCCESS;
     return rocm_stage(m, o, n, ROCM_DEVICE == *path);
 }
 
@@ -796,11 +817,16 @@ static int rocm_progress(void)
     pp = &rocm_active;
     while (NULL != *pp) {
         mca_coll_rocm_request_t *r = *pp;
-        int fin = 0;
-        const int rc = NULL != r->plan ? ompi_amd_plan_test(r->plan, &fin)
-                                       : ompi_amd_request_test(r->nbreq, &fin);
+        int fin = 0, rc = OMPI_AMD_SUCCESS;
+        if (NULL != r->inner) {  /* the saved function's request (host copies) */
+            fin = REQUEST_COMPLETE(r->inner);
+        } else {
+            rc = NULL != r->plan ? ompi_amd_plan_test(r->plan, &fin)
+                                 : ompi_amd_request_test(r->nbreq, &fin);
+        }
         if (OMPI_AMD_SUCCESS != rc || fin) {
-            r->super.req_status.MPI_ERROR = to_ompi_err(rc);
+            r->super.req_status.MPI_ERROR = NULL != r->inner ? r->inner->req_status.MPI_ERROR
+                                                             : to_ompi_err(rc);
             *pp = r->next_active;
             r->next_active = done;
             done = r;
@@ -813,6 +839,14 @@ static int rocm_progress(void)
         mca_coll_rocm_request_t *r = done;
         done = r->next_active;
         r->next_active = NULL;
+        if (NULL != r->inner) {
+            if (r->super.req_persistent) {
+                r->inner->req_state = OMPI_REQUEST_INACTIVE;  /* as MPI_Wait leaves it */
+            } else {
+                (void) ompi_request_free(&r->inner);
+                r->inner = NULL;
+            }
+        }
         if (NULL != r->stage) {  /* staged outputs back to the caller's buffers */
             r->super.req_status.MPI_ERROR =
                 rocm_unstage_ops(r->stage->o, r->stage->n, r->super.req_status.MPI_ERROR);
@@ -867,15 +901,18 @@ static int rocm_request_start(size_t count, ompi_request_t **requests)
         r->super.req_complete = REQUEST_PENDING;
         r->super.req_status.MPI_ERROR = OMPI_SUCCESS;
         r->super.req_state = OMPI_REQUEST_ACTIVE;
-        rc = OMPI_AMD_SUCCESS;
+        rc = OMPI_SUCCESS;
         for (int k = 0; NULL != r->stage && k < r->stage->n; ++k) {  /* this start's inputs */
-            if (OMPI_SUCCESS != stage_copy_in(&r->stage->o[k])) rc = OMPI_AMD_ERR_HIP;
+            if (OMPI_SUCCESS != stage_copy_in(&r->stage->o[k])) rc = OMPI_ERROR;
         }
-        if (OMPI_AMD_SUCCESS == rc) rc = ompi_amd_plan_start(r->plan, NULL);
-        if (OMPI_AMD_SUCCESS != rc) {
-            r->super.req_status.MPI_ERROR = to_ompi_err(rc);
+        if (OMPI_SUCCESS == rc) {
+            rc = NULL != r->inner ? r->inner->req_start(1, &r->inner)
+                                  : to_ompi_err(ompi_amd_plan_start(r->plan, NULL));
+        }
+        if (OMPI_SUCCESS != rc) {
+            r->super.req_status.MPI_ERROR = rc;
             ompi_request_complete(&r->super, true);
-            return to_ompi_err(rc);
+            return rc;
         }
         rocm_link_active(r);
     }
@@ -900,12 +937,21 @@ static int rocm_request_free(ompi_request_t **rptr)
         rc = ompi_amd_request_free(r->nbreq);  /* waits for the device work */
         r->nbreq = NULL;
     }
+    rc = to_ompi_err(rc);
+    if (NULL != r->inner) {  /* the host copies must outlive the saved call */
+        while (OMPI_REQUEST_ACTIVE == r->inner->req_state && !REQUEST_COMPLETE(r->inner)) {
+            opal_progress();
+        }
+        if (OMPI_SUCCESS == rc) rc = ompi_request_free(&r->inner);
+        else (void) ompi_request_free(&r->inner);
+        r->inner = NULL;
+    }
     nb_stage_free(r->stage);  /* freed before completion: outputs are undefined */
     r->stage = NULL;
     OMPI_REQUEST_FINI(&r->super);
     OBJ_RELEASE(r);
     *rptr = MPI_REQUEST_NULL;
-    return to_ompi_err(rc);
+    return rc;
 }
 
 static void rocm_request_construct(mca_coll_rocm_request_t *r)
@@ -917,6 +963,7 @@ static void rocm_request_construct(mca_coll_rocm_request_t *r)
     r->super.req_cancel = NULL;
     r->plan = NULL;
     r->nbreq = NULL;
+    r->inner = NULL;
     r->stage = NULL;
     r->next_active = NULL;
 }
@@ -950,14 +997,30 @@ static void nb_stage_free(struct rocm_nb_stage *st)
     free(st);
 }
 
-/* The path of one nonblocking call.  What every rank computes alike comes
- * first (no rendezvous when it fails).  A module locked to DEVICE (§3.2 of
- * every rank locks at the same blocking call) takes the device
- * path with no vote at all; a rank whose operands are not device-contiguous
- * stages them into memory of the request — inputs now, outputs back when
- * the request completes (rocm_progress), as coll/cuda stages for its
- * blocking calls (coll_cuda_allreduce.c:42-72) — and counts the mismatch
- * for the next recheck vote.  Otherwise the per-call vote. */
+/* does any of this rank's operands live in device memory? */
+static int any_device(const rocm_operand_t *o, int n)
+{
+    for (int i = 0; i < n; ++i) {
+        if (NULL != o[i].user && MPI_IN_PLACE != o[i].user && 0 != o[i].count &&
+            ompi_amd_is_device_pointer(o[i].user)) {
+            return 1;
+        }
+    }
+    return 0;
+}
+
+/* The path of one nonblocking or persistent call.  What every rank computes
+ * alike comes first (no rendezvous when it fails).  A module locked to
+ * DEVICE (§3.2 of DESIGN.md: every rank locks at the same blocking call)
+ * takes the device path with no vote at all; a rank whose operands are not
+ * device-contiguous stages them into memory of the request — inputs now
+ * (and at every persistent start), outputs back when the request completes
+ * (rocm_progress) — and counts the mismatch for the next recheck vote.
+ * Otherwise the per-call vote.  When the saved (libnbc) function runs
+ * instead, this rank's device operands go to it as host copies owned by a
+ * request that wraps the saved one (rocm_saved_post), the blocking calls'
+ * coll/cuda pattern (coll_cuda_allreduce.c:42-72) stretched over the
+ * request's life. */
 static int rocm_nb_begin(mca_coll_rocm_module_t *m, int uniform_ok, int local_ok,
                          rocm_operand_t *o, int n, struct rocm_nb_stage **stage, int *path)
 {
@@ -970,17 +1033,19 @@ static int rocm_nb_begin(mca_coll_rocm_module_t *m, int uniform_ok, int local_ok
         o[i].hbuf = NULL;
     }
     *path = ROCM_SAVED;
-    if (!uniform_ok) return OMPI_SUCCESS;
-    if (ROCM_RES_DEVICE != m->mode) {
-        *path = take_device_path(m, local_ok) ? ROCM_DEVICE : ROCM_SAVED;
-        return OMPI_SUCCESS;
+    if (uniform_ok) {
+        *path = ROCM_RES_DEVICE == m->mode || take_device_path(m, local_ok) ? ROCM_DEVICE
+                                                                            : ROCM_SAVED;
     }
-    *path = ROCM_DEVICE;
-    if (local_ok) return OMPI_SUCCESS;
-    m->mismatched++;
+    if (ROCM_DEVICE == *path) {
+        if (local_ok) return OMPI_SUCCESS;
+        m->mismatched++;  /* locked to DEVICE: this rank's operands go to the device */
+    } else if (!any_device(o, n)) {
+        return OMPI_SUCCESS;  /* the saved function takes host operands as they are */
+    }
     st = calloc(1, sizeof(*st));
     if (NULL == st) return OMPI_ERR_OUT_OF_RESOURCE;
-    rc = rocm_stage_with(nb_buf, st, o, n, 1);
+    rc = rocm_stage_with(nb_buf, st, o, n, ROCM_DEVICE == *path);
     if (OMPI_SUCCESS != rc) {
         nb_stage_free(st);
         return rc;
@@ -1026,6 +1091,37 @@ static int rocm_nb_post(int rc, ompi_amd_request_t *nb, struct rocm_nb_stage *st
     return rocm_wrap_nb(nb, stage, comm, request);
 }
 
+/* The saved function's answer: with nothing staged its request is the
+ * caller's; otherwise a request of ours wraps it, completes when it does
+ * (rocm_progress copies the staged outputs back first) and, persistent,
+ * refills the staged inputs before every start of it. */
+static int rocm_saved_post(int rc, ompi_request_t *inner, struct rocm_nb_stage *stage,
+                           struct ompi_communicator_t *comm, ompi_request_t **request)
+{
+    mca_coll_rocm_request_t *r = NULL;
+    if (NULL == stage) {
+        *request = inner;
+        return rc;
+    }
+    if (OMPI_SUCCESS == rc) r = OBJ_NEW(mca_coll_rocm_request_t);
+    if (NULL == r) {
+        if (OMPI_SUCCESS == rc && NULL != inner) (void) ompi_request_free(&inner);
+        nb_stage_free(stage);
+        return OMPI_SUCCESS != rc ? rc : OMPI_ERROR;
+    }
+    OMPI_REQUEST_INIT(&r->super, inner->req_persistent);
+    r->super.req_mpi_object.comm = comm;
+    r->super.req_status.MPI_ERROR = OMPI_SUCCESS;
+    r->inner = inner;
+    r->stage = stage;
+    *request = &r->super;
+    if (!inner->req_persistent) {
+        r->super.req_state = OMPI_REQUEST_ACTIVE;
+        rocm_link_active(r);
+    }
+    return OMPI_SUCCESS;
+}
+
 /* MPI_Iallreduce (coll.h:271-274) */
 int mca_coll_rocm_iallreduce(const void *sbuf, void *rbuf, int count,
                              struct ompi_datatype_t *dtype, struct ompi_op_t *op,
@@ -1038,13 +1134,15 @@ int mca_coll_rocm_iallreduce(const void *sbuf, void *rbuf, int count,
                            {rbuf, (size_t) count, dtype, inplace, 1}};
     struct rocm_nb_stage *st = NULL;
     ompi_amd_request_t *nb = NULL;
+    ompi_request_t *inner = NULL;
     int path, rc;
     rc = rocm_nb_begin(m, reduction_ok_n(dtype, op, (size_t) count), dev(sbuf) && dev(rbuf), o, 2,
                        &st, &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
-        return m->c_coll.coll_iallreduce(sbuf, rbuf, count, dtype, op, comm, request,
-                                         m->c_coll.coll_iallreduce_module);
+        rc = m->c_coll.coll_iallreduce(o[0].use, o[1].use, count, dtype, op, comm, &inner,
+                                       m->c_coll.coll_iallreduce_module);
+        return rocm_saved_post(rc, inner, st, comm, request);
     }
     rc = ompi_amd_iallreduce(m->dev_comm, inplace ? o[1].use : o[0].use, o[1].use,
                              (size_t) count, type_code(dtype), op->o_f_to_c_index, NULL, &nb);
@@ -1065,12 +1163,14 @@ int mca_coll_rocm_ireduce_scatter_block(const void *sbuf, void *rbuf, int rcount
                            {rbuf, inplace ? all : (size_t) rcount, dtype, inplace, 1}};
     struct rocm_nb_stage *st = NULL;
     ompi_amd_request_t *nb = NULL;
+    ompi_request_t *inner = NULL;
     int path, rc;
     rc = rocm_nb_begin(m, reduction_ok_n(dtype, op, all), dev(sbuf) && dev(rbuf), o, 2, &st, &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
-        return m->c_coll.coll_ireduce_scatter_block(sbuf, rbuf, rcount, dtype, op, comm, request,
-                                                    m->c_coll.coll_ireduce_scatter_block_module);
+        rc = m->c_coll.coll_ireduce_scatter_block(o[0].use, o[1].use, rcount, dtype, op, comm, &inner,
+                                                  m->c_coll.coll_ireduce_scatter_block_module);
+        return rocm_saved_post(rc, inner, st, comm, request);
     }
     rc = ompi_amd_ireduce_scatter_block(m->dev_comm, inplace ? o[1].use : o[0].use, o[1].use,
                                         (size_t) rcount, type_code(dtype), op->o_f_to_c_index, NULL,
@@ -1090,6 +1190,7 @@ int mca_coll_rocm_iallgather(const void *sbuf, int scount, struct ompi_datatype_
                            {rbuf, all, rdtype, inplace, 1}};
     struct rocm_nb_stage *st = NULL;
     ompi_amd_request_t *nb = NULL;
+    ompi_request_t *inner = NULL;
     size_t rsize = 0;
     int path, rc, ok;
     (void) ompi_datatype_type_size(rdtype, &rsize);
@@ -1098,8 +1199,9 @@ int mca_coll_rocm_iallgather(const void *sbuf, int scount, struct ompi_datatype_
     rc = rocm_nb_begin(m, bytes_ok(rsize * (size_t) rcount), ok, o, 2, &st, &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
-        return m->c_coll.coll_iallgather(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, request,
-                                         m->c_coll.coll_iallgather_module);
+        rc = m->c_coll.coll_iallgather(o[0].use, scount, sdtype, o[1].use, rcount, rdtype, comm, &inner,
+                                       m->c_coll.coll_iallgather_module);
+        return rocm_saved_post(rc, inner, st, comm, request);
     }
     rc = ompi_amd_iallgather(m->dev_comm, inplace ? (const void *) 1 : o[0].use, o[1].use,
                              rsize * (size_t) rcount, NULL, &nb);
@@ -1115,6 +1217,7 @@ int mca_coll_rocm_ibcast(void *buf, int count, struct ompi_datatype_t *dtype, in
     rocm_operand_t o[1] = {{buf, (size_t) count, dtype, is_root, !is_root}};
     struct rocm_nb_stage *st = NULL;
     ompi_amd_request_t *nb = NULL;
+    ompi_request_t *inner = NULL;
     size_t size = 0;
     int path, rc;
     (void) ompi_datatype_type_size(dtype, &size);
@@ -1123,8 +1226,9 @@ int mca_coll_rocm_ibcast(void *buf, int count, struct ompi_datatype_t *dtype, in
                        &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
-        return m->c_coll.coll_ibcast(buf, count, dtype, root, comm, request,
-                                     m->c_coll.coll_ibcast_module);
+        rc = m->c_coll.coll_ibcast(o[0].use, count, dtype, root, comm, &inner,
+                                   m->c_coll.coll_ibcast_module);
+        return rocm_saved_post(rc, inner, st, comm, request);
     }
     rc = ompi_amd_ibcast(m->dev_comm, o[0].use, size * (size_t) count, root, NULL, &nb);
     return rocm_nb_post(rc, nb, st, comm, request);
@@ -1149,13 +1253,15 @@ int mca_coll_rocm_allreduce_init(const void *sbuf, void *rbuf, int count,
                            {rbuf, (size_t) count, dtype, inplace, 1}};
     struct rocm_nb_stage *st = NULL;
     ompi_amd_plan_t *plan = NULL;
+    ompi_request_t *inner = NULL;
     int path, rc;
     rc = rocm_nb_begin(m, reduction_ok_n(dtype, op, (size_t) count), dev(sbuf) && dev(rbuf), o, 2,
                        &st, &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
-        return m->c_coll.coll_allreduce_init(sbuf, rbuf, count, dtype, op, comm, info, request,
-                                             m->c_coll.coll_allreduce_init_module);
+        rc = m->c_coll.coll_allreduce_init(o[0].use, o[1].use, count, dtype, op, comm, info, &inner,
+                                           m->c_coll.coll_allreduce_init_module);
+        return rocm_saved_post(rc, inner, st, comm, request);
     }
     rc = ompi_amd_allreduce_init(m->dev_comm, inplace ? o[1].use : o[0].use, o[1].use,
                                  (size_t) count, type_code(dtype), op->o_f_to_c_index, &plan);
@@ -1176,14 +1282,16 @@ int mca_coll_rocm_ireduce(const void *sbuf, void *rbuf, int count, struct ompi_d
                            {is_root ? rbuf : NULL, (size_t) count, dtype, MPI_IN_PLACE == sbuf, 1}};
     struct rocm_nb_stage *st = NULL;
     ompi_amd_request_t *nb = NULL;
+    ompi_request_t *inner = NULL;
     int path, rc;
     rc = rocm_nb_begin(m, reduction_ok_n(dtype, op, (size_t) count),
                        is_root ? dev(rbuf) && dev(sbuf) : ompi_amd_is_device_pointer(sbuf), o, 2,
                        &st, &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
-        return m->c_coll.coll_ireduce(sbuf, rbuf, count, dtype, op, root, comm, request,
-                                      m->c_coll.coll_ireduce_module);
+        rc = m->c_coll.coll_ireduce(o[0].use, is_root ? o[1].use : rbuf, count, dtype, op, root, comm,
+                                    &inner, m->c_coll.coll_ireduce_module);
+        return rocm_saved_post(rc, inner, st, comm, request);
     }
     rc = ompi_amd_ireduce(m->dev_comm, o[0].use, is_root ? o[1].use : NULL, (size_t) count,
                           type_code(dtype), op->o_f_to_c_index, root, NULL, &nb);
@@ -1198,15 +1306,17 @@ static int rocm_iscan_common(const void *sbuf, void *rbuf, int count, struct omp
                            {rbuf, (size_t) count, dtype, MPI_IN_PLACE == sbuf, 1}};
     struct rocm_nb_stage *st = NULL;
     ompi_amd_request_t *nb = NULL;
+    ompi_request_t *inner = NULL;
     int path, rc;
     rc = rocm_nb_begin(m, reduction_ok_n(dtype, op, (size_t) count), dev(sbuf) && dev(rbuf), o, 2,
                        &st, &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
-        return exclusive ? m->c_coll.coll_iexscan(sbuf, rbuf, count, dtype, op, comm, request,
-                                                  m->c_coll.coll_iexscan_module)
-                         : m->c_coll.coll_iscan(sbuf, rbuf, count, dtype, op, comm, request,
-                                                m->c_coll.coll_iscan_module);
+        rc = exclusive ? m->c_coll.coll_iexscan(o[0].use, o[1].use, count, dtype, op, comm, &inner,
+                                                m->c_coll.coll_iexscan_module)
+                       : m->c_coll.coll_iscan(o[0].use, o[1].use, count, dtype, op, comm, &inner,
+                                              m->c_coll.coll_iscan_module);
+        return rocm_saved_post(rc, inner, st, comm, request);
     }
     rc = (exclusive ? ompi_amd_iexscan : ompi_amd_iscan)(m->dev_comm, o[0].use, o[1].use,
                                                          (size_t) count, type_code(dtype),
@@ -1240,6 +1350,7 @@ int mca_coll_rocm_ireduce_scatter(const void *sbuf, void *rbuf, const int *rcoun
     size_t counts[OMPI_AMD_MAX_RANKS], total = 0;
     struct rocm_nb_stage *st = NULL;
     ompi_amd_request_t *nb = NULL;
+    ompi_request_t *inner = NULL;
     int path, rc, i;
     for (i = 0; i < n; ++i) total += (size_t) rcounts[i];
     {
@@ -1250,8 +1361,9 @@ int mca_coll_rocm_ireduce_scatter(const void *sbuf, void *rbuf, const int *rcoun
                            &path);
         if (OMPI_SUCCESS != rc) return rc;
         if (ROCM_DEVICE != path) {
-            return m->c_coll.coll_ireduce_scatter(sbuf, rbuf, rcounts, dtype, op, comm, request,
-                                                  m->c_coll.coll_ireduce_scatter_module);
+            rc = m->c_coll.coll_ireduce_scatter(o[0].use, o[1].use, rcounts, dtype, op, comm, &inner,
+                                                m->c_coll.coll_ireduce_scatter_module);
+            return rocm_saved_post(rc, inner, st, comm, request);
         }
         for (i = 0; i < n; ++i) counts[i] = (size_t) rcounts[i];
         rc = ompi_amd_ireduce_scatter(m->dev_comm, inplace ? o[1].use : o[0].use, o[1].use, counts,
@@ -1296,13 +1408,15 @@ int mca_coll_rocm_reduce_scatter_block_init(const void *sbuf, void *rbuf, int rc
                            {rbuf, inplace ? all : (size_t) rcount, dtype, inplace, 1}};
     struct rocm_nb_stage *st = NULL;
     ompi_amd_plan_t *plan = NULL;
+    ompi_request_t *inner = NULL;
     int path, rc;
     rc = rocm_nb_begin(m, reduction_ok_n(dtype, op, all), dev(sbuf) && dev(rbuf), o, 2, &st, &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
-        return m->c_coll.coll_reduce_scatter_block_init(sbuf, rbuf, rcount, dtype, op, comm, info,
-                                                        request,
-                                                        m->c_coll.coll_reduce_scatter_block_init_module);
+        rc = m->c_coll.coll_reduce_scatter_block_init(o[0].use, o[1].use, rcount, dtype, op, comm, info,
+                                                      &inner,
+                                                      m->c_coll.coll_reduce_scatter_block_init_module);
+        return rocm_saved_post(rc, inner, st, comm, request);
     }
     rc = ompi_amd_reduce_scatter_block_init(m->dev_comm, inplace ? MPI_IN_PLACE : o[0].use,
                                             o[1].use, (size_t) rcount, type_code(dtype),
@@ -1322,6 +1436,7 @@ int mca_coll_rocm_allgather_init(const void *sbuf, int scount, struct ompi_datat
                            {rbuf, all, rdtype, inplace, 1}};
     struct rocm_nb_stage *st = NULL;
     ompi_amd_plan_t *plan = NULL;
+    ompi_request_t *inner = NULL;
     size_t rsize = 0;
     int path, rc, ok;
     (void) ompi_datatype_type_size(rdtype, &rsize);
@@ -1330,8 +1445,9 @@ int mca_coll_rocm_allgather_init(const void *sbuf, int scount, struct ompi_datat
     rc = rocm_nb_begin(m, bytes_ok(rsize * (size_t) rcount), ok, o, 2, &st, &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
-        return m->c_coll.coll_allgather_init(sbuf, scount, sdtype, rbuf, rcount, rdtype, comm, info,
-                                             request, m->c_coll.coll_allgather_init_module);
+        rc = m->c_coll.coll_allgather_init(o[0].use, scount, sdtype, o[1].use, rcount, rdtype, comm,
+                                           info, &inner, m->c_coll.coll_allgather_init_module);
+        return rocm_saved_post(rc, inner, st, comm, request);
     }
     rc = ompi_amd_allgather_init(m->dev_comm, inplace ? (const void *) 1 : o[0].use, o[1].use,
                                  rsize * (size_t) rcount, &plan);
@@ -1347,6 +1463,7 @@ int mca_coll_rocm_bcast_init(void *buf, int count, struct ompi_datatype_t *dtype
     rocm_operand_t o[1] = {{buf, (size_t) count, dtype, is_root, !is_root}};
     struct rocm_nb_stage *st = NULL;
     ompi_amd_plan_t *plan = NULL;
+    ompi_request_t *inner = NULL;
     size_t size = 0;
     int path, rc;
     (void) ompi_datatype_type_size(dtype, &size);
@@ -1355,9 +1472,120 @@ int mca_coll_rocm_bcast_init(void *buf, int count, struct ompi_datatype_t *dtype
                        &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
-        return m->c_coll.coll_bcast_init(buf, count, dtype, root, comm, info, request,
-                                         m->c_coll.coll_bcast_init_module);
+        rc = m->c_coll.coll_bcast_init(o[0].use, count, dtype, root, comm, info, &inner,
+                                       m->c_coll.coll_bcast_init_module);
+        return rocm_saved_post(rc, inner, st, comm, request);
     }
     rc = ompi_amd_bcast_init(m->dev_comm, o[0].use, size * (size_t) count, root, &plan);
     return rocm_wrap_plan(rc, plan, st, comm, request);
+}
+
+/* MPI_Reduce_init / MPI_Reduce_scatter_init / MPI_Scan_init / MPI_Exscan_init
+ * (coll.h:555-567 coll_reduce_init, coll_reduce_scatter_init,
+ * coll_scan_init, coll_exscan_init; libnbc's in the reference): the same
+ * decision as MPI_Allreduce_init; on the device path a library plan whose
+ * every start posts the nonblocking call with the init's arguments.
+ * MPI_Reduce_init's rbuf matters at the root only. */
+int mca_coll_rocm_reduce_init(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                              struct ompi_op_t *op, int root, struct ompi_communicator_t *comm,
+                              struct ompi_info_t *info, ompi_request_t **request,
+                              mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const int is_root = ompi_comm_rank(comm) == root;
+    rocm_operand_t o[2] = {{(void *) sbuf, (size_t) count, dtype, 1, 0},
+                           {is_root ? rbuf : NULL, (size_t) count, dtype, MPI_IN_PLACE == sbuf, 1}};
+    struct rocm_nb_stage *st = NULL;
+    ompi_amd_plan_t *plan = NULL;
+    ompi_request_t *inner = NULL;
+    int path, rc;
+    rc = rocm_nb_begin(m, reduction_ok_n(dtype, op, (size_t) count),
+                       is_root ? dev(rbuf) && dev(sbuf) : ompi_amd_is_device_pointer(sbuf), o, 2,
+                       &st, &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
+        rc = m->c_coll.coll_reduce_init(o[0].use, is_root ? o[1].use : rbuf, count, dtype, op, root,
+                                        comm, info, &inner, m->c_coll.coll_reduce_init_module);
+        return rocm_saved_post(rc, inner, st, comm, request);
+    }
+    rc = ompi_amd_reduce_init(m->dev_comm, o[0].use, is_root ? o[1].use : NULL, (size_t) count,
+                              type_code(dtype), op->o_f_to_c_index, root, &plan);
+    return rocm_wrap_plan(rc, plan, st, comm, request);
+}
+
+int mca_coll_rocm_reduce_scatter_init(const void *sbuf, void *rbuf, const int *rcounts,
+                                      struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                      struct ompi_communicator_t *comm, struct ompi_info_t *info,
+                                      ompi_request_t **request, mca_coll_base_module_t *module)
+{
+    mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) module;
+    const int n = ompi_comm_size(comm), inplace = MPI_IN_PLACE == sbuf;
+    size_t counts[OMPI_AMD_MAX_RANKS], total = 0;
+    struct rocm_nb_stage *st = NULL;
+    ompi_amd_plan_t *plan = NULL;
+    ompi_request_t *inner = NULL;
+    int path, rc, i;
+    for (i = 0; i < n; ++i) total += (size_t) rcounts[i];
+    {
+        rocm_operand_t o[2] = {{(void *) sbuf, total, dtype, 1, 0},
+                               {rbuf, inplace ? total : (size_t) rcounts[ompi_comm_rank(comm)],
+                                dtype, inplace, 1}};
+        rc = rocm_nb_begin(m, reduction_ok_n(dtype, op, total), dev(sbuf) && dev(rbuf), o, 2, &st,
+                           &path);
+        if (OMPI_SUCCESS != rc) return rc;
+        if (ROCM_DEVICE != path) {
+            rc = m->c_coll.coll_reduce_scatter_init(o[0].use, o[1].use, rcounts, dtype, op, comm, info,
+                                                    &inner, m->c_coll.coll_reduce_scatter_init_module);
+            return rocm_saved_post(rc, inner, st, comm, request);
+        }
+        for (i = 0; i < n; ++i) counts[i] = (size_t) rcounts[i];
+        rc = ompi_amd_reduce_scatter_init(m->dev_comm, inplace ? o[1].use : o[0].use, o[1].use,
+                                          counts, type_code(dtype), op->o_f_to_c_index, &plan);
+        return rocm_wrap_plan(rc, plan, st, comm, request);
+    }
+}
+
+static int rocm_scan_init_common(const void *sbuf, void *rbuf, int count,
+                                 struct ompi_datatype_t *dtype, struct ompi_op_t *op,
+                                 struct ompi_communicator_t *comm, struct ompi_info_t *info,
+                                 ompi_request_t **request, mca_coll_rocm_module_t *m, int exclusive)
+{
+    rocm_operand_t o[2] = {{(void *) sbuf, (size_t) count, dtype, 1, 0},
+                           {rbuf, (size_t) count, dtype, MPI_IN_PLACE == sbuf, 1}};
+    struct rocm_nb_stage *st = NULL;
+    ompi_amd_plan_t *plan = NULL;
+    ompi_request_t *inner = NULL;
+    int path, rc;
+    rc = rocm_nb_begin(m, reduction_ok_n(dtype, op, (size_t) count), dev(sbuf) && dev(rbuf), o, 2,
+                       &st, &path);
+    if (OMPI_SUCCESS != rc) return rc;
+    if (ROCM_DEVICE != path) {
+        rc = exclusive ? m->c_coll.coll_exscan_init(o[0].use, o[1].use, count, dtype, op, comm, info,
+                                                    &inner, m->c_coll.coll_exscan_init_module)
+                       : m->c_coll.coll_scan_init(o[0].use, o[1].use, count, dtype, op, comm, info,
+                                                  &inner, m->c_coll.coll_scan_init_module);
+        return rocm_saved_post(rc, inner, st, comm, request);
+    }
+    rc = (exclusive ? ompi_amd_exscan_init : ompi_amd_scan_init)(m->dev_comm, o[0].use, o[1].use,
+                                                                 (size_t) count, type_code(dtype),
+                                                                 op->o_f_to_c_index, &plan);
+    return rocm_wrap_plan(rc, plan, st, comm, request);
+}
+
+int mca_coll_rocm_scan_init(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                            struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                            struct ompi_info_t *info, ompi_request_t **request,
+                            mca_coll_base_module_t *module)
+{
+    return rocm_scan_init_common(sbuf, rbuf, count, dtype, op, comm, info, request,
+                                 (mca_coll_rocm_module_t *) module, 0);
+}
+
+int mca_coll_rocm_exscan_init(const void *sbuf, void *rbuf, int count, struct ompi_datatype_t *dtype,
+                              struct ompi_op_t *op, struct ompi_communicator_t *comm,
+                              struct ompi_info_t *info, ompi_request_t **request,
+                              mca_coll_base_module_t *module)
+{
+    return rocm_scan_init_common(sbuf, rbuf, count, dtype, op, comm, info, request,
+                                 (mca_coll_rocm_module_t *) module, 1);
 }

@@ -364,6 +364,73 @@ def case_persistent_rsb_ag_bcast(comm, rank, n, salt, big):
     return not msgs, "; ".join(msgs)
 
 
+def case_persistent_reduce_scan_rs(comm, rank, n, salt, big):
+    """MPI_Reduce_init / MPI_Scan_init / MPI_Exscan_init /
+    MPI_Reduce_scatter_init (coll.h:561-567 coll_reduce_init,
+    coll_scan_init, coll_exscan_init, coll_reduce_scatter_init): three starts
+    each with fresh data in the same buffers, staged and landing sizes, the
+    reduce root in place, uneven reduce_scatter counts with an empty block,
+    the four plans started back to back before any wait; every result
+    bit-exact against the oracle's order of the blocking call."""
+    F, D, I32 = mop.MPI_FLOAT, mop.MPI_DOUBLE, mop.MPI_INT32_T
+    SUM, MAX = mop.MPI_SUM, mop.MPI_MAX
+    msgs = []
+    for tag, count, dt, op in (("staged", 3001, F, SUM), ("landing", big + 7, D, SUM),
+                               ("landing_max", big // 2 + 5, I32, MAX)):
+        root = (salt + count) % n
+        root_inplace = tag == "landing"
+        rcounts = [count // n + 3 * r if r != 1 else 0 for r in range(n)]
+        ext = dt.extent
+        sb = torch.zeros(count * ext, dtype=torch.uint8, device="cuda")
+        rd = torch.zeros(count * ext, dtype=torch.uint8, device="cuda")
+        sc = torch.zeros(count * ext, dtype=torch.uint8, device="cuda")
+        ex = torch.zeros(count * ext, dtype=torch.uint8, device="cuda")
+        rs = torch.zeros((rcounts[rank] + 1) * ext, dtype=torch.uint8, device="cuda")
+        rsin = torch.zeros(sum(rcounts) * ext, dtype=torch.uint8, device="cuda")
+        if rank == root:
+            p_red = comm.reduce_init(coll.IN_PLACE if root_inplace else sb, rd, count, dt, op, root)
+        else:
+            p_red = comm.reduce_init(sb, None, count, dt, op, root)
+        p_scan = comm.scan_init(sb, sc, count, dt, op)
+        p_ex = comm.scan_init(sb, ex, count, dt, op, exclusive=True)
+        p_rs = comm.reduce_scatter_init(rsin, rs, rcounts, dt, op)
+        plans = (p_red, p_scan, p_ex, p_rs)
+        try:
+            for it in range(3):
+                xs = [inputs(dt, count, r, salt + 10 * it) for r in range(n)]
+                ys = [inputs(dt, sum(rcounts), r, salt + 10 * it + 5) for r in range(n)]
+                red, _ = orc.reduce([x.copy() for x in xs], count, op.index, dt.code, root,
+                                    root_inplace)
+                scan = orc.scan([x.copy() for x in xs], count, op.index, dt.code, False)
+                exs = orc.scan([x.copy() for x in xs], count, op.index, dt.code, True)
+                rse, _ = orc.reduce_scatter([y.copy() for y in ys], rcounts, op.index, dt.code)
+                mine = torch.from_numpy(xs[rank].view(np.uint8).copy()).cuda()
+                sb.copy_(mine)
+                if rank == root and root_inplace:
+                    rd.copy_(mine)
+                rsin.copy_(torch.from_numpy(ys[rank].view(np.uint8).copy()).cuda())
+                torch.cuda.synchronize()
+                for p in plans:
+                    p.start()
+                for p in plans:
+                    p.wait()
+                torch.cuda.synchronize()
+                want = [("scan", sc, count, scan[rank]), ("reduce_scatter", rs, rcounts[rank], rse[rank])]
+                if rank == root:
+                    want.append(("reduce", rd, count, red))
+                if rank > 0:
+                    want.append(("exscan", ex, count, exs[rank]))
+                for name, buf, c, e in want:
+                    got = buf.cpu().numpy()[:c * ext].view(dt.np_dtype)
+                    ok, msg = checked(got, np.asarray(e).view(dt.np_dtype)[:c])
+                    if not ok:
+                        msgs.append(f"{tag} start {it} {name}: {msg}")
+        finally:
+            for p in plans:
+                p.free()
+    return not msgs, "; ".join(msgs)
+
+
 def case_zero_counts(comm, rank, n, salt):
     """Zero elements / bytes in every entry point — blocking, nonblocking and
     persistent — (MPI filters count 0 above coll only for some calls,
@@ -405,10 +472,11 @@ def case_zero_counts(comm, rank, n, salt):
 
 
 def case_autotune(comm, rank, n, salt, big):
-    """param "autotune" (coll/rocm's default): the first eighteen large
-    blocking allreduces of a size bucket run the nine candidates twice each
-    (push-gather, push-land and staged pull x 1024 / 512 / 256 blocks; a
-    candidate counts its best round), the eighteenth decides — on every
+    """param "autotune" (coll/rocm's default): the first 36 large blocking
+    allreduces of a size bucket run the 18 candidates twice each
+    (push-gather, push-land and staged pull x 1024 / 512 / 256 blocks x
+    non-temporal / plain stores while copy_nt is not fixed; a candidate
+    counts its best round), the 36th decides — on every
     rank alike — and later calls run the choice; every result bit-exact
     against the oracle on dataset R (the fold order is the same whatever
     the scheme), in place too, and a nonblocking allreduce of the same size
@@ -419,7 +487,8 @@ def case_autotune(comm, rank, n, salt, big):
     count = big + 11
     comm.set_param("autotune", 1)
     try:
-        for i in range(21):
+        ncalls = 36
+        for i in range(ncalls + 3):
             if i == 3:  # a nonblocking call in the middle of the tuning
                 xs = [inputs(F, count, r, salt + 50) for r in range(n)]
                 exp, _ = orc.allreduce([x.copy() for x in xs], count, SUM.index, F.code)
@@ -435,18 +504,23 @@ def case_autotune(comm, rank, n, salt, big):
             if not ok:
                 return False, f"call {i}: {msg}"
             state = comm.get_param("autotune_state")
-            if state != (1 if i < 17 else 2):
+            if state != (1 if i < ncalls - 1 else 2):
                 return False, f"call {i}: autotune_state {state}"
-        choice = (comm.get_param("autotune_algorithm"), comm.get_param("autotune_blocks"))
-        times = [comm.get_param(f"autotune_us{k}") for k in range(9)]
+        choice = (comm.get_param("autotune_algorithm"), comm.get_param("autotune_blocks"),
+                  comm.get_param("autotune_copy_nt"))
+        nc = comm.get_param("autotune_ncand")
+        if nc != 18:
+            return False, f"{nc} candidates with copy_nt not fixed"
+        times = [comm.get_param(f"autotune_us{k}") for k in range(nc)]
         # decided: a nonblocking and a persistent allreduce of this size take
         # the fastest push-type candidate (no handle swap) with its grid
-        algs = [comm.get_param(f"autotune_alg{k}") for k in range(9)]
-        grids = [comm.get_param(f"autotune_grid{k}") for k in range(9)]
-        push = [k for k in range(9) if algs[k] in (2, 3)]
+        algs = [comm.get_param(f"autotune_alg{k}") for k in range(nc)]
+        grids = [comm.get_param(f"autotune_grid{k}") for k in range(nc)]
+        nts = [comm.get_param(f"autotune_nt{k}") for k in range(nc)]
+        push = [k for k in range(nc) if algs[k] in (2, 3)]
         # (times are whole microseconds: a tie may hide a sub-microsecond order)
         fastest = min(times[k] for k in push)
-        wanted = {(algs[k], grids[k]) for k in push if times[k] == fastest}
+        wanted = {(algs[k], grids[k], nts[k]) for k in push if times[k] == fastest}
         xs = [inputs(F, count, r, salt + 60) for r in range(n)]
         exp, _ = orc.allreduce([x.copy() for x in xs], count, SUM.index, F.code)
         sb = to_dev(xs[rank])
@@ -454,7 +528,8 @@ def case_autotune(comm, rank, n, salt, big):
         req = comm.iallreduce(sb, ob, count, F, SUM)
         req.wait()
         req.free()
-        took_nb = (comm.get_param("nb_tuned_algorithm"), comm.get_param("nb_tuned_blocks"))
+        took_nb = (comm.get_param("nb_tuned_algorithm"), comm.get_param("nb_tuned_blocks"),
+                   comm.get_param("nb_tuned_copy_nt"))
         if not np.array_equal(ob.cpu().numpy().view(np.uint32), exp[rank].view(np.uint32)):
             return False, f"iallreduce after the tuning ({took_nb}) differs"
         ob.zero_()
@@ -463,7 +538,8 @@ def case_autotune(comm, rank, n, salt, big):
             plan.start()
             plan.wait()
         plan.free()
-        took_plan = (comm.get_param("nb_tuned_algorithm"), comm.get_param("nb_tuned_blocks"))
+        took_plan = (comm.get_param("nb_tuned_algorithm"), comm.get_param("nb_tuned_blocks"),
+                     comm.get_param("nb_tuned_copy_nt"))
         if not np.array_equal(ob.cpu().numpy().view(np.uint32), exp[rank].view(np.uint32)):
             return False, f"persistent allreduce after the tuning ({took_plan}) differs"
         if took_nb not in wanted or took_plan != took_nb:
@@ -728,8 +804,8 @@ def case_copy_nt(comm, rank, n, salt, big):
     byte-exact allgather and bcast."""
     F, SUM = mop.MPI_FLOAT, mop.MPI_SUM
     msgs = []
-    saved = comm.get_param("copy_nt")
-    comm.set_param("copy_nt", 1 - saved)  # the non-default store kind (the default runs everywhere else)
+    saved = comm.get_param("copy_nt") if comm.get_param("copy_nt_fixed") else -1
+    comm.set_param("copy_nt", 1 - comm.get_param("copy_nt"))  # the kind the other cases do not run
     try:
         for i, inplace in enumerate((False, True)):
             ok, msg = case_allreduce(comm, rank, n, F, SUM, big + 13, salt + i, inplace=inplace)
@@ -1164,6 +1240,7 @@ def main():
             ("nonblocking_rsb_ag_bcast", lambda: case_nonblocking_mix(comm, rank, n, 150, big)),
             ("nonblocking_reduce_scan_rs", lambda: case_nb_reduce_scan_rs(comm, rank, n, 180, big)),
             ("persistent_rsb_allgather_bcast", lambda: case_persistent_rsb_ag_bcast(comm, rank, n, 190, big)),
+            ("persistent_reduce_scan_rs", lambda: case_persistent_reduce_scan_rs(comm, rank, n, 200, big)),
             ("nonblocking_rsb_ag_bcast_shadow",
              shadowed_nb(lambda: case_nonblocking_mix(comm, rank, n, 160, big))),
         ]

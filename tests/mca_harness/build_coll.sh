@@ -9,6 +9,6 @@ OUT=${1:-$H/coll_harness}
 gcc -std=gnu11 -O1 -DHARNESS_COLL -Wall -Wextra -Wno-unused-parameter -Wno-missing-field-initializers \
     -I"$H/coll_include" -I"$H/include" -I"$R/include" -I"$R/ompi_amd/mca/coll/rocm" \
     -I/opt/rocm/include \
-    "$R/ompi_amd/mca/coll/rocm/coll_rocm_module.c" "$H/coll_harness.c" "$H/dev_helpers.c" "$H/progress_stub.c" \
+    "$R/ompi_amd/mca/coll/rocm/coll_rocm_module.c" "$H/coll_harness.c" "$H/coll_saved.c" "$H/dev_helpers.c" "$H/progress_stub.c" \
     -L"$R/ompi_amd" -lompi_amd -L"$R/oracle" -loracle -L/opt/rocm/lib -lamdhip64 \
-    -Wl,-rpath,"$R/ompi_amd" -Wl,-rpath,"$R/oracle" -Wl,-rpath,/opt/rocm/lib -o "$OUT"
+    -Wl,-rpath,"$R/ompi_amd" -Wl,-rpath,"$R/oracle" -Wl,-rpath,/opt/rocm/lib -lrt -o "$OUT"

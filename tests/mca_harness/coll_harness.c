@@ -31,6 +31,7 @@
 #include "opal/runtime/opal_progress.h"
 #include "../../oracle/oracle.h"
 #include "coll_rocm.h"
+#include "coll_saved.h"
 #include "ompi_amd.h"
 
 extern mca_coll_rocm_component_t mca_coll_rocm_component;
@@ -61,112 +62,7 @@ int ompi_op_ddt_map[64];
     } while (0)
 
 static int g_rank, g_size;
-static int tuned_calls;
-static int t_sdev = -1, t_rdev = -1; /* residency of the last saved allreduce's buffers */
 struct ompi_datatype_t harness_mpi_byte = {ORC_T_BYTE, 1, 1, 1};
-
-/* ---- the previously selected functions ("tuned"): count and succeed ---- */
-/* allreduce also records where its buffers live and, into a host rbuf,
- * writes a marker the caller can look for after a staged copy back */
-static int t_allreduce(const void *s, void *r, int c, struct ompi_datatype_t *d,
-                       struct ompi_op_t *o, struct ompi_communicator_t *cm,
-                       mca_coll_base_module_t *m)
-{
-    tuned_calls++;
-    t_sdev = MPI_IN_PLACE == s ? -1 : ompi_amd_is_device_pointer(s);
-    t_rdev = ompi_amd_is_device_pointer(r);
-    if (!t_rdev && c > 0) ((float *) r)[0] = 42.f;
-    return OMPI_SUCCESS;
-}
-static int t_reduce(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
-                    int root, struct ompi_communicator_t *cm, mca_coll_base_module_t *m)
-{ tuned_calls++; return OMPI_SUCCESS; }
-static int t_rs(const void *s, void *r, const int *c, struct ompi_datatype_t *d,
-                struct ompi_op_t *o, struct ompi_communicator_t *cm, mca_coll_base_module_t *m)
-{ tuned_calls++; return OMPI_SUCCESS; }
-static int t_rsb(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
-                 struct ompi_communicator_t *cm, mca_coll_base_module_t *m)
-{ tuned_calls++; return OMPI_SUCCESS; }
-static int t_scan(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
-                  struct ompi_communicator_t *cm, mca_coll_base_module_t *m)
-{ tuned_calls++; return OMPI_SUCCESS; }
-static int t_allgather(const void *s, int sc, struct ompi_datatype_t *sd, void *r, int rc,
-                       struct ompi_datatype_t *rd, struct ompi_communicator_t *cm,
-                       mca_coll_base_module_t *m) { tuned_calls++; return OMPI_SUCCESS; }
-static int t_bcast(void *b, int c, struct ompi_datatype_t *d, int root,
-                   struct ompi_communicator_t *cm, mca_coll_base_module_t *m)
-{ tuned_calls++; return OMPI_SUCCESS; }
-
-static ompi_request_t t_request;
-static int t_ar_init(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
-                     struct ompi_communicator_t *cm, struct ompi_info_t *info,
-                     ompi_request_t **req, mca_coll_base_module_t *m)
-{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
-
-static int t_iallreduce(const void *s, void *r, int c, struct ompi_datatype_t *d,
-                        struct ompi_op_t *o, struct ompi_communicator_t *cm, ompi_request_t **req,
-                        mca_coll_base_module_t *m)
-{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
-
-static int t_iallgather(const void *s, int sc, struct ompi_datatype_t *sd, void *r, int rc,
-                        struct ompi_datatype_t *rd, struct ompi_communicator_t *cm,
-                        ompi_request_t **req, mca_coll_base_module_t *m)
-{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
-static int t_ibcast(void *b, int c, struct ompi_datatype_t *d, int root,
-                    struct ompi_communicator_t *cm, ompi_request_t **req, mca_coll_base_module_t *m)
-{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
-static int t_irsb(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
-                  struct ompi_communicator_t *cm, ompi_request_t **req, mca_coll_base_module_t *m)
-{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
-
-static int t_ireduce(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
-                     int root, struct ompi_communicator_t *cm, ompi_request_t **req,
-                     mca_coll_base_module_t *m)
-{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
-static int t_iscan(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
-                   struct ompi_communicator_t *cm, ompi_request_t **req, mca_coll_base_module_t *m)
-{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
-static int t_irs(const void *s, void *r, const int *c, struct ompi_datatype_t *d, struct ompi_op_t *o,
-                 struct ompi_communicator_t *cm, ompi_request_t **req, mca_coll_base_module_t *m)
-{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
-static int t_rsb_init(const void *s, void *r, int c, struct ompi_datatype_t *d, struct ompi_op_t *o,
-                      struct ompi_communicator_t *cm, struct ompi_info_t *info, ompi_request_t **req,
-                      mca_coll_base_module_t *m)
-{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
-static int t_ag_init(const void *s, int sc, struct ompi_datatype_t *sd, void *r, int rc,
-                     struct ompi_datatype_t *rd, struct ompi_communicator_t *cm,
-                     struct ompi_info_t *info, ompi_request_t **req, mca_coll_base_module_t *m)
-{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
-static int t_bc_init(void *b, int c, struct ompi_datatype_t *d, int root, struct ompi_communicator_t *cm,
-                     struct ompi_info_t *info, ompi_request_t **req, mca_coll_base_module_t *m)
-{ tuned_calls++; *req = &t_request; return OMPI_SUCCESS; }
-
-static void fill_tuned(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *tm)
-{
-    memset(t, 0, sizeof(*t));
-#define SET(fn, f) do { t->coll_##fn = f; t->coll_##fn##_module = tm; OBJ_RETAIN(tm); } while (0)
-    SET(allreduce, t_allreduce);
-    SET(reduce, t_reduce);
-    SET(reduce_scatter, t_rs);
-    SET(reduce_scatter_block, t_rsb);
-    SET(scan, t_scan);
-    SET(exscan, t_scan);
-    SET(allgather, t_allgather);
-    SET(bcast, t_bcast);
-    SET(iallreduce, t_iallreduce);
-    SET(allreduce_init, t_ar_init);
-    SET(iallgather, t_iallgather);
-    SET(ibcast, t_ibcast);
-    SET(ireduce_scatter_block, t_irsb);
-    SET(ireduce, t_ireduce);
-    SET(iscan, t_iscan);
-    SET(iexscan, t_iscan);
-    SET(ireduce_scatter, t_irs);
-    SET(reduce_scatter_block_init, t_rsb_init);
-    SET(allgather_init, t_ag_init);
-    SET(bcast_init, t_bc_init);
-#undef SET
-}
 
 /* coll_base_comm_select.c:210-232: install what the module provides */
 static void install(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *m)
@@ -179,6 +75,7 @@ static void install(mca_coll_base_comm_coll_t *t, mca_coll_base_module_t *m)
     INST(iallgather) INST(ibcast) INST(ireduce_scatter_block)
     INST(ireduce) INST(iscan) INST(iexscan) INST(ireduce_scatter)
     INST(reduce_scatter_block_init) INST(allgather_init) INST(bcast_init)
+    INST(reduce_init) INST(reduce_scatter_init) INST(scan_init) INST(exscan_init)
 #undef INST
 }
 
@@ -204,6 +101,10 @@ static void release_table(mca_coll_base_comm_coll_t *t)
     OBJ_RELEASE(t->coll_reduce_scatter_block_init_module);
     OBJ_RELEASE(t->coll_allgather_init_module);
     OBJ_RELEASE(t->coll_bcast_init_module);
+    OBJ_RELEASE(t->coll_reduce_init_module);
+    OBJ_RELEASE(t->coll_reduce_scatter_init_module);
+    OBJ_RELEASE(t->coll_scan_init_module);
+    OBJ_RELEASE(t->coll_exscan_init_module);
 }
 
 /* deterministic per-rank floats in [-1, 1): fp sums depend on order */
@@ -247,6 +148,235 @@ static void expect_dev(const void *d, const void *exp, size_t bytes, const char 
     free(got);
 }
 
+/* ---- section 6: one collective on the saved path, checked exactly ---- */
+enum { C_ALLREDUCE, C_REDUCE, C_SCAN, C_EXSCAN, C_RSB, C_RS, C_ALLGATHER, C_BCAST };
+enum { F_BLOCKING, F_NONBLOCKING, F_PERSISTENT };
+static mca_coll_base_comm_coll_t *g_table;
+static ompi_communicator_t *g_comm;
+
+/* packed element bytes of rank r's input */
+static void gen_packed(const ompi_datatype_t *d, size_t count, int r, int salt, char *out)
+{
+    float *f = malloc(count * sizeof(float) + 4);
+    gen(f, count, r, salt);
+    memset(out, 0, count * d->size);
+    for (size_t i = 0; i < count; ++i) {
+        if (HARNESS_T_LONG_DOUBLE == d->id) ((long double *) out)[i] = (long double) f[i] / 3.0L;
+        else if (ORC_T_BYTE == d->id) out[i] = (char) (f[i] * 127.f);
+        else ((float *) out)[i] = f[i];
+    }
+    free(f);
+}
+
+/* typed layout of packed elements: gaps (vector type) hold 0x5A */
+static size_t span_of(const ompi_datatype_t *d, size_t count)
+{
+    return count == 0 ? 0 : (d->contiguous ? count * d->size : (2 * count - 1) * d->size);
+}
+
+static void to_typed(const ompi_datatype_t *d, const char *packed, size_t first, size_t count,
+                     char *typed)
+{
+    const size_t st = d->contiguous ? d->size : 2 * d->size;
+    for (size_t i = 0; i < count; ++i) memcpy(typed + (first + i) * st, packed + i * d->size, d->size);
+}
+
+/* a buffer this rank passes: device memory unless it is the host rank */
+static void *place(const char *typed, size_t bytes, int on_host)
+{
+    void *p;
+    if (on_host) {
+        p = malloc(bytes + 1);
+        memcpy(p, typed, bytes);
+        return p;
+    }
+    return dev_of(typed, bytes + 1);
+}
+
+static void unplace(void *p, int on_host)
+{
+    if (on_host) free(p);
+    else harness_dev_free(p);
+}
+
+static void fetch(void *got, const void *p, size_t bytes, int on_host)
+{
+    if (on_host) memcpy(got, p, bytes);
+    else CHECK(harness_dev_copy_back(got, p, bytes) == 0, "copy back");
+}
+
+static void refill(void *p, const char *typed, size_t bytes, int on_host)
+{
+    if (on_host) memcpy(p, typed, bytes);
+    else CHECK(harness_dev_copy_in(p, typed, bytes) == 0, "copy in");
+}
+
+/* host_rank: -1 every rank on device memory, -2 every rank on host memory,
+ * r >= 0 rank r on host memory and the others on device memory */
+static void saved_case(const char *what, int coll, int form, ompi_datatype_t *d, ompi_op_t *op,
+                       size_t count, int inplace, int salt, int host_rank)
+{
+    static const char *cname[] = {"allreduce", "reduce", "scan", "exscan", "rsb", "rs",
+                                  "allgather", "bcast"};
+    static const char *fname[] = {"blocking", "nonblocking", "persistent"};
+    mca_coll_base_comm_coll_t *t = g_table;
+    const int n = g_size, me = g_rank, root = 1 % n;
+    const int on_host = host_rank == -2 || host_rank == me;
+    const int opc = NULL != op ? op->o_f_to_c_index : 0;
+    const size_t es = d->size;
+    int rcounts[OMPI_AMD_MAX_RANKS];
+    size_t nin = count, nout = count, at_out = 0, rtotal = 0;
+    char **x = malloc(sizeof(char *) * (size_t) n), *exp, *sbuf_t = NULL, *rbuf_t, *got;
+    void *sb = NULL, *rb = NULL;
+    ompi_request_t *rq = NULL;
+    const int calls0 = tuned_calls;
+    int rounds = F_PERSISTENT == form ? 2 : 1, rc = OMPI_SUCCESS;
+    size_t rspan, sspan;
+
+    for (int r = 0; r < n; ++r) {
+        rcounts[r] = (int) count + 3 * r - (r == 1 ? (int) count + 3 : 0);
+        rtotal += (size_t) rcounts[r];
+    }
+    if (C_RSB == coll) nin = count * (size_t) n;
+    if (C_RS == coll) { nin = rtotal; nout = (size_t) rcounts[me]; }
+    if (C_ALLGATHER == coll) { nout = count * (size_t) n; at_out = count * (size_t) me; }
+    /* the receive buffer: in place it carries the input too */
+    if (inplace && (C_RSB == coll || C_RS == coll)) nout = nin;
+    for (int r = 0; r < n; ++r) x[r] = malloc(nin * es + 16);
+    exp = malloc(nout * es + 16);
+    sspan = span_of(d, nin);
+    rspan = span_of(d, nout);
+    sbuf_t = malloc(sspan + 16);
+    rbuf_t = malloc(rspan + 16);
+    got = malloc(rspan + 16);
+    for (int round = 0; round < rounds; ++round) {
+        const int rs = salt * 10 + round;
+        int is_out = 1;
+        for (int r = 0; r < n; ++r) gen_packed(d, nin, r, rs, x[r]);
+        /* the expected bytes of this rank's receive buffer, typed */
+        memset(rbuf_t, 0x5A, rspan + 16);
+        memset(sbuf_t, 0x5A, sspan + 16);
+        to_typed(d, x[me], 0, nin, sbuf_t);
+        switch (coll) {
+        case C_ALLREDUCE: case C_SCAN: case C_EXSCAN:
+            harness_expect_reduction(C_ALLREDUCE == coll ? HARNESS_ALLREDUCE
+                                     : C_SCAN == coll ? HARNESS_SCAN : HARNESS_EXSCAN,
+                                     opc, d, (const char *const *) x, n, me, count, exp);
+            is_out = !(C_EXSCAN == coll && 0 == me);
+            break;
+        case C_REDUCE:
+            harness_expect_reduction(HARNESS_ALLREDUCE, opc, d, (const char *const *) x, n, me,
+                                     count, exp);
+            is_out = me == root;
+            break;
+        case C_RSB: case C_RS: {
+            int eq[OMPI_AMD_MAX_RANKS];
+            for (int r = 0; r < n; ++r) eq[r] = C_RSB == coll ? (int) count : rcounts[r];
+            harness_expect_rs(opc, d, (const char *const *) x, n, me, eq, exp);
+            break;
+        }
+        case C_ALLGATHER:
+            for (int r = 0; r < n; ++r) memcpy(exp + (size_t) r * count * es, x[r], count * es);
+            break;
+        case C_BCAST:
+            memcpy(exp, x[root], count * es);
+            break;
+        }
+        if (round == 0) {  /* buffers: the receive side starts as 0x5A, or the input in place */
+            char *init = malloc(rspan + 16);
+            memset(init, 0x5A, rspan + 16);
+            if (inplace && C_ALLGATHER == coll) to_typed(d, x[me], at_out, count, init);
+            else if (inplace || C_BCAST == coll) to_typed(d, x[me], 0, C_BCAST == coll ? count : nin, init);
+            if (C_BCAST == coll && me != root) memset(init, 0x5A, rspan + 16);
+            rb = place(init, rspan, on_host);
+            if (!inplace && C_BCAST != coll) sb = place(sbuf_t, sspan, on_host);
+            free(init);
+        } else {
+            char *init = malloc(rspan + 16);
+            memset(init, 0x5A, rspan + 16);
+            if (inplace && C_ALLGATHER == coll) to_typed(d, x[me], at_out, count, init);
+            else if (inplace || (C_BCAST == coll && me == root))
+                to_typed(d, x[me], 0, C_BCAST == coll ? count : nin, init);
+            refill(rb, init, rspan, on_host);
+            if (sb) refill(sb, sbuf_t, sspan, on_host);
+            free(init);
+        }
+        if (round == 0 || F_PERSISTENT != form) {
+            const void *s = inplace ? MPI_IN_PLACE : sb;
+            ompi_request_t **rp = &rq;
+            switch (form * 8 + coll) {
+#define B(c) (F_BLOCKING * 8 + (c))
+#define NB(c) (F_NONBLOCKING * 8 + (c))
+#define P(c) (F_PERSISTENT * 8 + (c))
+            case B(C_ALLREDUCE): rc = t->coll_allreduce(s, rb, (int) count, d, op, g_comm, t->coll_allreduce_module); break;
+            case B(C_REDUCE): rc = t->coll_reduce(inplace && me == root ? MPI_IN_PLACE : (inplace ? rb : sb), me == root ? rb : NULL, (int) count, d, op, root, g_comm, t->coll_reduce_module); break;
+            case B(C_SCAN): rc = t->coll_scan(s, rb, (int) count, d, op, g_comm, t->coll_scan_module); break;
+            case B(C_EXSCAN): rc = t->coll_exscan(s, rb, (int) count, d, op, g_comm, t->coll_exscan_module); break;
+            case B(C_RSB): rc = t->coll_reduce_scatter_block(s, rb, (int) count, d, op, g_comm, t->coll_reduce_scatter_block_module); break;
+            case B(C_RS): rc = t->coll_reduce_scatter(s, rb, rcounts, d, op, g_comm, t->coll_reduce_scatter_module); break;
+            case B(C_ALLGATHER): rc = t->coll_allgather(s, (int) count, d, rb, (int) count, d, g_comm, t->coll_allgather_module); break;
+            case B(C_BCAST): rc = t->coll_bcast(rb, (int) count, d, root, g_comm, t->coll_bcast_module); break;
+            case NB(C_ALLREDUCE): rc = t->coll_iallreduce(s, rb, (int) count, d, op, g_comm, rp, t->coll_iallreduce_module); break;
+            case NB(C_REDUCE): rc = t->coll_ireduce(inplace && me == root ? MPI_IN_PLACE : (inplace ? rb : sb), me == root ? rb : NULL, (int) count, d, op, root, g_comm, rp, t->coll_ireduce_module); break;
+            case NB(C_SCAN): rc = t->coll_iscan(s, rb, (int) count, d, op, g_comm, rp, t->coll_iscan_module); break;
+            case NB(C_EXSCAN): rc = t->coll_iexscan(s, rb, (int) count, d, op, g_comm, rp, t->coll_iexscan_module); break;
+            case NB(C_RSB): rc = t->coll_ireduce_scatter_block(s, rb, (int) count, d, op, g_comm, rp, t->coll_ireduce_scatter_block_module); break;
+            case NB(C_RS): rc = t->coll_ireduce_scatter(s, rb, rcounts, d, op, g_comm, rp, t->coll_ireduce_scatter_module); break;
+            case NB(C_ALLGATHER): rc = t->coll_iallgather(s, (int) count, d, rb, (int) count, d, g_comm, rp, t->coll_iallgather_module); break;
+            case NB(C_BCAST): rc = t->coll_ibcast(rb, (int) count, d, root, g_comm, rp, t->coll_ibcast_module); break;
+            case P(C_ALLREDUCE): rc = t->coll_allreduce_init(s, rb, (int) count, d, op, g_comm, NULL, rp, t->coll_allreduce_init_module); break;
+            case P(C_REDUCE): rc = t->coll_reduce_init(inplace && me == root ? MPI_IN_PLACE : (inplace ? rb : sb), me == root ? rb : NULL, (int) count, d, op, root, g_comm, NULL, rp, t->coll_reduce_init_module); break;
+            case P(C_SCAN): rc = t->coll_scan_init(s, rb, (int) count, d, op, g_comm, NULL, rp, t->coll_scan_init_module); break;
+            case P(C_EXSCAN): rc = t->coll_exscan_init(s, rb, (int) count, d, op, g_comm, NULL, rp, t->coll_exscan_init_module); break;
+            case P(C_RSB): rc = t->coll_reduce_scatter_block_init(s, rb, (int) count, d, op, g_comm, NULL, rp, t->coll_reduce_scatter_block_init_module); break;
+            case P(C_RS): rc = t->coll_reduce_scatter_init(s, rb, rcounts, d, op, g_comm, NULL, rp, t->coll_reduce_scatter_init_module); break;
+            case P(C_ALLGATHER): rc = t->coll_allgather_init(s, (int) count, d, rb, (int) count, d, g_comm, NULL, rp, t->coll_allgather_init_module); break;
+            case P(C_BCAST): rc = t->coll_bcast_init(rb, (int) count, d, root, g_comm, NULL, rp, t->coll_bcast_init_module); break;
+#undef B
+#undef NB
+#undef P
+            }
+            CHECK(OMPI_SUCCESS == rc, "%s %s %s: rc %d", what, cname[coll], fname[form], rc);
+            CHECK(tuned_calls == calls0 + 1, "%s %s %s: the saved function was not called (%d)",
+                  what, cname[coll], fname[form], tuned_calls - calls0);
+        }
+        if (F_PERSISTENT == form) CHECK(rq->req_start(1, &rq) == OMPI_SUCCESS, "start");
+        if (F_BLOCKING != form) {
+            harness_wait(rq);
+            CHECK(rq->req_status.MPI_ERROR == OMPI_SUCCESS, "%s %s %s: status %d", what,
+                  cname[coll], fname[form], rq->req_status.MPI_ERROR);
+        }
+        /* compare the receive buffer: results where they belong, every
+         * other byte as it was */
+        if (C_REDUCE == coll && me != root && !inplace) is_out = 0;
+        fetch(got, rb, rspan, on_host);
+        if (is_out) {
+            if (C_RS == coll || C_RSB == coll) {
+                const size_t mine = C_RS == coll ? (size_t) rcounts[me] : count;
+                to_typed(d, exp, 0, mine, rbuf_t);
+                if (inplace) {  /* past the result: the input as it was */
+                    const size_t st = d->contiguous ? es : 2 * es;
+                    for (size_t i = mine; i < nin; ++i) memcpy(rbuf_t + i * st, x[me] + i * es, es);
+                }
+            } else {
+                to_typed(d, exp, 0, nout, rbuf_t);
+            }
+            CHECK(memcmp(got, rbuf_t, rspan) == 0, "%s %s %s round %d (n %d, count %zu): result differs",
+                  what, cname[coll], fname[form], round, n, count);
+        }
+        if (F_NONBLOCKING == form) CHECK(rq->req_free(&rq) == OMPI_SUCCESS, "free");
+    }
+    if (F_PERSISTENT == form) CHECK(rq->req_free(&rq) == OMPI_SUCCESS, "persistent free");
+    if (sb) unplace(sb, on_host);
+    unplace(rb, on_host);
+    for (int r = 0; r < n; ++r) free(x[r]);
+    free(x);
+    free(exp);
+    free(sbuf_t);
+    free(rbuf_t);
+    free(got);
+}
+
 int main(int argc, char **argv)
 {
     const int use_gpu = getenv("HARNESS_GPU") && atoi(getenv("HARNESS_GPU"));
@@ -266,7 +396,8 @@ int main(int argc, char **argv)
     for (i = 0; i < 64; ++i) ompi_op_ddt_map[i] = i;
 
     tm = OBJ_NEW(mca_coll_base_module_t);
-    fill_tuned(&table, tm);
+    harness_saved_init(argv[1], g_rank, g_size);
+    harness_fill_tuned(&table, tm);
     comm = (ompi_communicator_t){g_rank, g_size, 3, 0, &local, &table};
 
     /* selection (coll_base_comm_select.c): init_query, comm_query */
@@ -280,7 +411,8 @@ int main(int argc, char **argv)
               m->coll_iallgather && m->coll_ibcast && m->coll_ireduce_scatter_block &&
               m->coll_ireduce && m->coll_iscan && m->coll_iexscan && m->coll_ireduce_scatter &&
               m->coll_reduce_scatter_block_init && m->coll_allgather_init && m->coll_bcast_init &&
-              m->coll_module_enable,
+              m->coll_reduce_init && m->coll_reduce_scatter_init && m->coll_scan_init &&
+              m->coll_exscan_init && m->coll_module_enable,
           "module function table");
     {
         ompi_communicator_t c1 = comm, ci = comm, cr = comm;
@@ -299,14 +431,17 @@ int main(int argc, char **argv)
         OBJ_RELEASE(m);
         release_table(&table);
         OBJ_RELEASE(tm);
+        harness_saved_fini();
         printf("ok\n");
         return 0;
     }
 
     CHECK(m->coll_module_enable(m, &comm) == OMPI_SUCCESS, "enable");
-    CHECK(tm->super.obj_reference_count == 1 + 20 + 20, "enable retains the saved modules (%d)",
+    CHECK(tm->super.obj_reference_count == 1 + 24 + 24, "enable retains the saved modules (%d)",
           tm->super.obj_reference_count);
     install(&table, m);
+    g_table = &table;
+    g_comm = &comm;
     /* sections 1-8: the per-call residency vote (never locks) */
     mca_coll_rocm_component.residency_lock = 0;
 
@@ -469,63 +604,72 @@ int main(int argc, char **argv)
         free(mine);
         free(all);
     }
-    /* 6. delegation: host buffers, mixed residency, non-intrinsic op */
+    /* 6. the saved functions on device buffers: whatever keeps a call off
+     * the device path — a user op, a derived datatype, a type without a
+     * device kernel (long double), a vector past max_device_mib, a peer
+     * with host buffers — the saved (host) function must get host copies
+     * of this rank's device operands and its results must come back into
+     * them, in blocking, nonblocking and persistent form (the stand-ins fail
+     * the run on any device pointer and compute the result on the host) */
     {
-        const size_t n = 4096;
-        float *h = calloc(n, sizeof(float)), *h2 = calloc(n, sizeof(float));
-        void *d = dev_of(h, n * 4), *d2 = dev_of(h2, n * 4);
-        tuned_calls = 0;
-        CHECK(table.coll_allreduce(h, h2, (int) n, &dfloat, &sum, &comm,
-                                   table.coll_allreduce_module) == OMPI_SUCCESS, "host");
-        CHECK(tuned_calls == 1, "host buffers must go to the saved allreduce");
-        CHECK(table.coll_allreduce(g_rank == 0 ? (void *) h : d, g_rank == 0 ? (void *) h2 : d2,
-                                   (int) n, &dfloat, &sum, &comm,
-                                   table.coll_allreduce_module) == OMPI_SUCCESS, "mixed");
-        CHECK(tuned_calls == 2, "mixed residency must fall back on every rank");
-        CHECK(table.coll_allreduce(d, d2, (int) n, &dfloat, &user, &comm,
-                                   table.coll_allreduce_module) == OMPI_SUCCESS, "user op");
-        CHECK(tuned_calls == 3, "non-intrinsic op must fall back");
-        CHECK(table.coll_scan(h, h2, (int) n, &dfloat, &sum, &comm, table.coll_scan_module) ==
-                  OMPI_SUCCESS && tuned_calls == 4, "host scan falls back");
-        CHECK(table.coll_reduce(h, g_rank == 0 ? h2 : NULL, (int) n, &dfloat, &sum, 0, &comm,
-                                table.coll_reduce_module) == OMPI_SUCCESS && tuned_calls == 5,
-              "host reduce falls back");
-        /* past coll_rocm_max_device_mib (here lowered to 1 MiB): device
-         * buffers of every size-capped slot go to the saved functions on
-         * every rank alike (count, datatype and root agree) */
+        ompi_datatype_t vfloat = {ORC_T_FLOAT, 4, 0, 0}; /* vector: 4 data + 4 gap bytes */
+        ompi_datatype_t ldbl = {HARNESS_T_LONG_DOUBLE, 16, 1, 1};
+        const int live0 = harness_saved_live;
+        static const int reductions[6] = {C_ALLREDUCE, C_REDUCE, C_SCAN, C_EXSCAN, C_RSB, C_RS};
+        /* (a) user op: every reduction, every form, in place where MPI has it */
+        for (int f = 0; f < 3; ++f)
+            for (int k = 0; k < 6; ++k) {
+                saved_case("user op", reductions[k], f, &dfloat, &user, 1500 + 7 * k, 0, 200 + k, -1);
+                if (reductions[k] != C_EXSCAN)
+                    saved_case("user op in place", reductions[k], f, &dfloat, &user, 999, 1, 210 + k, -1);
+            }
+        /* (b) vector datatype: reductions with an intrinsic op, and the
+         * data movers (device path packs only when locked to DEVICE) */
+        for (int f = 0; f < 3; ++f) {
+            saved_case("vector", C_ALLREDUCE, f, &vfloat, &sum, 2001, 0, 220, -1);
+            saved_case("vector in place", C_ALLREDUCE, f, &vfloat, &sum, 2001, 1, 221, -1);
+            saved_case("vector", C_REDUCE, f, &vfloat, &sum, 777, 0, 222, -1);
+            saved_case("vector", C_RS, f, &vfloat, &sum, 300, 0, 223, -1);
+            saved_case("vector", C_ALLGATHER, f, &vfloat, NULL, 333, 0, 224, -1);
+            saved_case("vector in place", C_ALLGATHER, f, &vfloat, NULL, 333, 1, 225, -1);
+            saved_case("vector", C_BCAST, f, &vfloat, NULL, 1234, 0, 226, -1);
+        }
+        /* (c) long double (op/base only) */
+        for (int f = 0; f < 3; ++f) {
+            saved_case("long double", C_ALLREDUCE, f, &ldbl, &sum, 1001, 0, 230, -1);
+            saved_case("long double", C_REDUCE, f, &ldbl, &sum, 1001, 1, 231, -1);
+            saved_case("long double", C_SCAN, f, &ldbl, &sum, 500, 0, 232, -1);
+            saved_case("long double", C_RSB, f, &ldbl, &sum, 250, 0, 233, -1);
+        }
+        /* (d) past coll_rocm_max_device_mib (lowered to 1 MiB): every rank
+         * decides alike (count, datatype and root agree) */
         {
             const int saved_mib = mca_coll_rocm_component.max_device_mib;
             const size_t big = (1u << 20) + 64;
-            void *b1 = NULL, *b2 = NULL;
-            ompi_request_t *rq = NULL;
-            unsigned char *zero = calloc(big * (size_t) g_size, 1);
-            b1 = dev_of(zero, big);
-            b2 = dev_of(zero, big * (size_t) g_size);
-            free(zero);
             mca_coll_rocm_component.max_device_mib = 1;
-            tuned_calls = 0;
-            CHECK(table.coll_allreduce(b1, b2, (int) (big / 4), &dfloat, &sum, &comm,
-                                       table.coll_allreduce_module) == OMPI_SUCCESS &&
-                      tuned_calls == 1, "allreduce past the cap");
-            CHECK(table.coll_bcast(b1, (int) big, &dbyte, 0, &comm, table.coll_bcast_module) ==
-                      OMPI_SUCCESS && tuned_calls == 2, "bcast past the cap");
-            CHECK(table.coll_allgather(b1, (int) big, &dbyte, b2, (int) big, &dbyte, &comm,
-                                       table.coll_allgather_module) == OMPI_SUCCESS &&
-                      tuned_calls == 3, "allgather past the cap");
-            CHECK(table.coll_ibcast(b1, (int) big, &dbyte, 0, &comm, &rq,
-                                    table.coll_ibcast_module) == OMPI_SUCCESS &&
-                      tuned_calls == 4 && rq == &t_request, "ibcast past the cap");
-            CHECK(table.coll_iallgather(b1, (int) big, &dbyte, b2, (int) big, &dbyte, &comm, &rq,
-                                        table.coll_iallgather_module) == OMPI_SUCCESS &&
-                      tuned_calls == 5 && rq == &t_request, "iallgather past the cap");
+            for (int f = 0; f < 3; ++f) {
+                saved_case("past the cap", C_ALLREDUCE, f, &dfloat, &sum, big / 4, 0, 240, -1);
+                saved_case("past the cap", C_BCAST, f, &dbyte, NULL, big, 0, 241, -1);
+                saved_case("past the cap", C_ALLGATHER, f, &dbyte, NULL, big, 0, 242, -1);
+                saved_case("past the cap", C_RSB, f, &dfloat, &sum, big / 4 / (size_t) g_size + 1, 0,
+                           243, -1);
+            }
             mca_coll_rocm_component.max_device_mib = saved_mib;
-            harness_dev_free(b1);
-            harness_dev_free(b2);
         }
-        harness_dev_free(d);
-        harness_dev_free(d2);
-        free(h);
-        free(h2);
+        /* (e) mixed residency: rank 0's buffers are host memory, the vote
+         * sends every rank to the saved functions, the others stage */
+        for (int f = 0; f < 3; ++f) {
+            saved_case("mixed residency", C_ALLREDUCE, f, &dfloat, &sum, 4096, 0, 250, 0);
+            saved_case("mixed residency", C_SCAN, f, &dfloat, &sum, 4096, 0, 251, 0);
+            saved_case("mixed residency", C_BCAST, f, &dbyte, NULL, 5000, 0, 252, 0);
+            saved_case("mixed residency in place", C_ALLGATHER, f, &dbyte, NULL, 700, 1, 253, 0);
+        }
+        /* (f) host buffers on every rank: the saved functions as they are */
+        for (int f = 0; f < 3; ++f) {
+            saved_case("host", C_ALLREDUCE, f, &dfloat, &sum, 4096, 0, 260, -2);
+            saved_case("host", C_REDUCE, f, &dfloat, &sum, 4096, 0, 261, -2);
+        }
+        CHECK(harness_saved_live == live0, "stand-in requests leaked (%d)", harness_saved_live - live0);
     }
     /* 7. persistent allreduce (MPI_Allreduce_init): init once, then three
      * start / wait rounds with fresh inputs (the plan reads the buffers'
@@ -576,8 +720,9 @@ int main(int argc, char **argv)
             tuned_calls = 0;
             CHECK(table.coll_allreduce_init(h, h2, 16, &dfloat, &sum, &comm, NULL, &req,
                                             table.coll_allreduce_init_module) == OMPI_SUCCESS &&
-                      tuned_calls == 1 && req == &t_request,
+                      tuned_calls == 1 && harness_is_saved_request(req),
                   "host allreduce_init falls back");
+            CHECK(req->req_free(&req) == OMPI_SUCCESS, "free");
         }
     }
     /* 8. nonblocking allreduce (MPI_Iallreduce): staged and zero-copy sizes
@@ -623,8 +768,10 @@ int main(int argc, char **argv)
             ompi_request_t *hr = NULL;
             CHECK(table.coll_iallreduce(h, h2, 16, &dfloat, &sum, &comm, &hr,
                                         table.coll_iallreduce_module) == OMPI_SUCCESS &&
-                      tuned_calls == 1 && hr == &t_request,
+                      tuned_calls == 1 && harness_is_saved_request(hr),
                   "host iallreduce falls back");
+            harness_wait(hr);
+            CHECK(hr->req_free(&hr) == OMPI_SUCCESS, "free");
         }
     }
     /* 10. MPI_Ireduce_scatter_block / MPI_Iallgather / MPI_Ibcast on device
@@ -705,8 +852,10 @@ int main(int argc, char **argv)
             unsigned char h[64] = {0};
             ompi_request_t *hr = NULL;
             CHECK(table.coll_ibcast(h, 64, &dbyte, 0, &comm, &hr, table.coll_ibcast_module) ==
-                      OMPI_SUCCESS && tuned_calls == 1 && hr == &t_request,
+                      OMPI_SUCCESS && tuned_calls == 1 && harness_is_saved_request(hr),
                   "host ibcast falls back");
+            harness_wait(hr);
+            CHECK(hr->req_free(&hr) == OMPI_SUCCESS, "free");
         }
     }
     /* 11. MPI_Ireduce / MPI_Iscan / MPI_Iexscan / MPI_Ireduce_scatter and the
@@ -859,9 +1008,14 @@ int main(int argc, char **argv)
             float h[16] = {0}, h2[16] = {0};
             ompi_request_t *hr = NULL;
             CHECK(table.coll_iscan(h, h2, 16, &dfloat, &sum, &comm, &hr, table.coll_iscan_module) ==
-                      OMPI_SUCCESS && tuned_calls == 1 && hr == &t_request, "host iscan falls back");
+                      OMPI_SUCCESS && tuned_calls == 1 && harness_is_saved_request(hr),
+                  "host iscan falls back");
+            harness_wait(hr);
+            CHECK(hr->req_free(&hr) == OMPI_SUCCESS, "free");
             CHECK(table.coll_bcast_init(h, 16, &dbyte, 0, &comm, NULL, &hr, table.coll_bcast_init_module) ==
-                      OMPI_SUCCESS && tuned_calls == 2 && hr == &t_request, "host bcast_init falls back");
+                      OMPI_SUCCESS && tuned_calls == 2 && harness_is_saved_request(hr),
+                  "host bcast_init falls back");
+            CHECK(hr->req_free(&hr) == OMPI_SUCCESS, "free");
         }
     }
     /* 9. residency policy: unanimous votes lock the module, a locked call
@@ -904,15 +1058,23 @@ int main(int argc, char **argv)
         CHECK(b1 == b0 && tuned_calls == 4 && t_sdev == 0 && t_rdev == 0,
               "locked host call: %lld bootstrap calls", (long long) (b1 - b0));
         /* (c) rank 0 brings device buffers: it stages them to the host, the
-         * saved function sees host memory on every rank, and the marker it
-         * wrote comes back into rank 0's device rbuf */
+         * saved function sees host memory on every rank, and its result
+         * comes back into rank 0's device rbuf */
         CHECK(table.coll_allreduce(g_rank == 0 ? d : (void *) h, g_rank == 0 ? d2 : (void *) h2,
                                    (int) n, &dfloat, &sum, &comm,
                                    table.coll_allreduce_module) == OMPI_SUCCESS, "staged to host");
         CHECK(tuned_calls == 5 && t_sdev == 0 && t_rdev == 0, "saved function got host buffers");
-        if (g_rank == 0) {
-            CHECK(harness_dev_copy_back(got, d2, 4) == 0 && got[0] == 42.f,
-                  "staged rbuf copied back (%g)", (double) got[0]);
+        {
+            float *want = malloc(n * 4);
+            harness_expect_reduction(HARNESS_ALLREDUCE, ORC_OP_SUM, &dfloat, (const char *const *) xs,
+                                     g_size, g_rank, n, (char *) want);
+            if (g_rank == 0) {
+                CHECK(harness_dev_copy_back(got, d2, n * 4) == 0 && memcmp(got, want, n * 4) == 0,
+                      "staged rbuf copied back");
+            } else {
+                CHECK(memcmp(h2, want, n * 4) == 0, "host result beside a staging rank");
+            }
+            free(want);
         }
         /* (d) the 4th locked call is a recheck vote: rank 0 staged, so AUTO */
         BOOT(b0);
@@ -1077,6 +1239,7 @@ int main(int argc, char **argv)
     CHECK(tm->super.obj_reference_count == 1, "saved modules released (%d)",
           tm->super.obj_reference_count);
     OBJ_RELEASE(tm);
+    harness_saved_fini();
     printf("ok gpu\n");
     return 0;
 }

@@ -1,6 +1,6 @@
 /* TEST HARNESS ONLY: the coll framework types the glue uses, with the
  * reference's function signatures (ompi/mca/coll/coll.h:141-143, 200-250,
- * 261-274, 293-300, 311-326, 339-343, 349-352, 371-374, 397-400, 471-603). */
+ * 261-274, 293-300, 311-326, 339-343, 349-352, 371-374, 381-400, 471-603). */
 #ifndef HARNESS_COLL_H
 #define HARNESS_COLL_H
 #include <stdbool.h>
@@ -78,6 +78,21 @@ typedef int (*mca_coll_base_module_bcast_init_fn_t)(void *, int, struct ompi_dat
 typedef int (*mca_coll_base_module_reduce_scatter_block_init_fn_t)(
     const void *, void *, int, struct ompi_datatype_t *, struct ompi_op_t *,
     struct ompi_communicator_t *, struct ompi_info_t *, ompi_request_t **, HMOD);
+typedef int (*mca_coll_base_module_exscan_init_fn_t)(const void *, void *, int,
+                                                     struct ompi_datatype_t *, struct ompi_op_t *,
+                                                     struct ompi_communicator_t *,
+                                                     struct ompi_info_t *, ompi_request_t **, HMOD);
+typedef int (*mca_coll_base_module_reduce_init_fn_t)(const void *, void *, int,
+                                                     struct ompi_datatype_t *, struct ompi_op_t *, int,
+                                                     struct ompi_communicator_t *,
+                                                     struct ompi_info_t *, ompi_request_t **, HMOD);
+typedef int (*mca_coll_base_module_reduce_scatter_init_fn_t)(
+    const void *, void *, const int *, struct ompi_datatype_t *, struct ompi_op_t *,
+    struct ompi_communicator_t *, struct ompi_info_t *, ompi_request_t **, HMOD);
+typedef int (*mca_coll_base_module_scan_init_fn_t)(const void *, void *, int,
+                                                   struct ompi_datatype_t *, struct ompi_op_t *,
+                                                   struct ompi_communicator_t *,
+                                                   struct ompi_info_t *, ompi_request_t **, HMOD);
 typedef int (*mca_coll_base_module_enable_1_1_0_fn_t)(HMOD, struct ompi_communicator_t *);
 #undef HMOD
 typedef struct mca_coll_base_module_2_3_0_t {
@@ -103,6 +118,10 @@ typedef struct mca_coll_base_module_2_3_0_t {
     mca_coll_base_module_allreduce_init_fn_t coll_allreduce_init;
     mca_coll_base_module_bcast_init_fn_t coll_bcast_init;
     mca_coll_base_module_reduce_scatter_block_init_fn_t coll_reduce_scatter_block_init;
+    mca_coll_base_module_exscan_init_fn_t coll_exscan_init;
+    mca_coll_base_module_reduce_init_fn_t coll_reduce_init;
+    mca_coll_base_module_reduce_scatter_init_fn_t coll_reduce_scatter_init;
+    mca_coll_base_module_scan_init_fn_t coll_scan_init;
     void *base_data;
 } mca_coll_base_module_2_3_0_t;
 typedef mca_coll_base_module_2_3_0_t mca_coll_base_module_t;
@@ -124,6 +143,7 @@ typedef struct mca_coll_base_comm_coll_t {
     HFN(scan) HFN(iallgather) HFN(iallreduce) HFN(ibcast) HFN(ireduce_scatter_block)
     HFN(iexscan) HFN(ireduce) HFN(ireduce_scatter) HFN(iscan)
     HFN(allgather_init) HFN(allreduce_init) HFN(bcast_init) HFN(reduce_scatter_block_init)
+    HFN(exscan_init) HFN(reduce_init) HFN(reduce_scatter_init) HFN(scan_init)
 } mca_coll_base_comm_coll_t;
 #undef HFN
 #define MCA_COLL_BASE_VERSION_2_0_0 OMPI_MCA_BASE_VERSION_2_1_0("coll", 2, 0, 0)

@@ -58,6 +58,11 @@ static inline int ompi_request_complete(ompi_request_t *request, bool with_signa
     request->req_complete = REQUEST_COMPLETED;
     return 0;
 }
+/* request.h:381-384 */
+static inline int ompi_request_free(ompi_request_t **request)
+{
+    return (*request)->req_free(request);
+}
 extern ompi_request_t harness_request_null;
 #define MPI_REQUEST_NULL (&harness_request_null)
 #endif
