@@ -402,9 +402,13 @@ struct ompi_amd_comm {
     size_t bcast_split_bytes = 4u << 20;  // from this size on (0: never)
     int64_t exports_new = 0, imports_new = 0;  // runtime export / open calls made (cache misses)
     int recycled_exports = 0;             // exports refused: recycled handle bytes (shadowed)
+    int unsafe_exports = 0;               // application buffers of no IPC-safe size (shadowed)
     // streams this communicator launched work on: the current one, plus an
     // event recorded on each earlier one when the calls moved away from it
     // (quiesce() waits for exactly that work, not for the whole device)
+    // (stream_mu: quiesce() also runs on other threads, from the IPC
+    // registry's retirement of a mapping this communicator holds)
+    std::mutex stream_mu;
     bool has_stream = false;
     hipStream_t cur_stream = nullptr;
     std::vector<hipEvent_t> stream_evs;
@@ -662,6 +666,26 @@ static int export_alloc(void *base, size_t size, unsigned long long id, hipIpcMe
     return recycled ? 1 : 0;
 }
 
+// IPC-safe allocation sizes on ROCm 7.2 (tools/ipc_replay_probe.py,
+// profiles/r04_ipc_replay*.jsonl, N = 4 / 8 processes on one MI355X):
+//  - below 2 MiB hipMalloc sub-allocates from a shared chunk, and the import
+//    of such a buffer is refused ("invalid device pointer", the runtime
+//    printing "IPC Attach: Invalid IPC handle! <id> and 0") every time once
+//    another exported buffer of the chunk was freed, and 1-2 times in 400
+//    opens even when none was; an exactly 2 MiB one 1-2 times in 500;
+//  - an allocation whose size is not a multiple of 2 MiB, freed and its
+//    address reused by the next one, gets that one's import refused 2-5 times
+//    in 500 (the registry's retire-then-open order);
+//  - multiples of 2 MiB from 4 MiB up: no refusal in any order (thousands of
+//    opens).
+// Every library allocation peers map is sized accordingly (alloc_exportable),
+// and an application buffer that is not (user_ipc) goes through a shadow.
+constexpr size_t kIpcGrain = 2u << 20, kIpcMinBytes = 4u << 20;
+static size_t ipc_size_for(size_t bytes) {
+    return std::max(kIpcMinBytes, (bytes + kIpcGrain - 1) / kIpcGrain * kIpcGrain);
+}
+static bool ipc_safe_size(size_t size) { return size >= kIpcMinBytes && size % kIpcGrain == 0; }
+
 static unsigned long long buffer_id(const void *p) {
     unsigned long long id = 0;
     if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)p) != hipSuccess) {
@@ -712,6 +736,13 @@ static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d, bool *ip
         if (ipc_failed) *ipc_failed = true;
         record_msg("allocation %p + %zu exceeds the %zu-byte IPC mapping limit", base, size,
                    kMaxIpcBytes);
+        return OMPI_AMD_ERR_HIP;
+    }
+    if (ipc_failed && !ipc_safe_size(size)) {  // a caller with a shadow: use it
+        *ipc_failed = true;
+        ++c->unsafe_exports;
+        record_msg("allocation %p + %zu is not an IPC-safe size (a multiple of 2 MiB from 4 MiB)",
+                   base, size);
         return OMPI_AMD_ERR_HIP;
     }
     hipIpcMemHandle_t h;
@@ -777,7 +808,7 @@ static int drop_retired(ompi_amd_comm_t *c) {
                        it->peer, (unsigned long long)it->id);
             return OMPI_AMD_ERR_BAD_PARAM;
         }
-        ipc_unmap(it->ref);
+        ipc_unmap(it->ref, c);
         it = c->imports.erase(it);
     }
     return OMPI_AMD_SUCCESS;
@@ -811,7 +842,7 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
             if (jt->pins == 0 && (it == c->imports.end() || jt->last_use < it->last_use)) it = jt;
         if (it != c->imports.end()) {
             TRY(quiesce(c));  // an earlier call's kernel may still read it
-            ipc_unmap(it->ref);
+            ipc_unmap(it->ref, c);
             c->imports.erase(it);
         }
     }
@@ -819,7 +850,7 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
     void *base = nullptr;
     {
         host_step st("ipc_map", (size_t)d.size);
-        TRY(ipc_map(alloc_of(d), &ref, &base));
+        TRY(ipc_map(alloc_of(d), c, &ref, &base));
     }
     ++c->imports_new;
     if (pin) ipc_pin(ref, 1);
@@ -902,6 +933,7 @@ static int import_all(ompi_amd_comm_t *c, const call_blob *all, const void *sbuf
 // Work this communicator put on a stream: note the stream; when the calls
 // move to another stream, an event marks the end of the old one's work.
 static void note_stream(ompi_amd_comm_t *c, hipStream_t s) {
+    std::lock_guard<std::mutex> g(c->stream_mu);
     if (c->has_stream && c->cur_stream == s) return;
     if (c->has_stream) {
         hipEvent_t e = nullptr;
@@ -931,17 +963,24 @@ static int quiesce_user(void *c) { return quiesce(static_cast<ompi_amd_comm_t *>
 
 static int quiesce(ompi_amd_comm_t *c) {
     host_step st("quiesce");
-    for (hipEvent_t e : c->stream_evs) {
+    std::vector<hipEvent_t> evs;
+    hipStream_t cur = nullptr;
+    bool has = false;
+    {  // the marks are this call's from here on (note_stream may add new ones)
+        std::lock_guard<std::mutex> g(c->stream_mu);
+        evs.swap(c->stream_evs);
+        cur = c->cur_stream;
+        has = c->has_stream;
+    }
+    int rc = OMPI_AMD_SUCCESS;
+    for (hipEvent_t e : evs) {
         const hipError_t r = hipEventSynchronize(e);
         hip_ignore(hipEventDestroy(e));
-        if (r != hipSuccess) {
-            c->stream_evs.clear();
-            return record_hip(r, "hipEventSynchronize (communicator streams)");
-        }
+        if (r != hipSuccess && rc == OMPI_AMD_SUCCESS)
+            rc = record_hip(r, "hipEventSynchronize (communicator streams)");
     }
-    c->stream_evs.clear();
-    if (c->has_stream)
-        TRY(record_hip(hipStreamSynchronize(c->cur_stream), "hipStreamSynchronize (communicator stream)"));
+    TRY(rc);
+    if (has) TRY(record_hip(hipStreamSynchronize(cur), "hipStreamSynchronize (communicator stream)"));
     return OMPI_AMD_SUCCESS;
 }
 
@@ -958,18 +997,17 @@ static int quiesce(ompi_amd_comm_t *c) {
 // uncached: fine-grained memory (flag pages) instead of ordinary device memory.
 static hipError_t alloc_exportable(size_t bytes, char **out, hipIpcMemHandle_t *h,
                                    bool uncached = false) {
-    // The handle names (pid, address, size): a same-size allocation at a
-    // freed allocation's address gets its handle again.  A process-wide
-    // serial pads every request by a different number of 4 KiB pages, so
-    // library allocations (shadows, landing, control pages) rarely repeat
-    // an earlier (address, size) pair; a repeat that still happens is kept
-    // alive and the next attempt takes the next pad.
-    static std::atomic<unsigned> serial{0};
+    // Sized as ipc_safe_size() demands (a multiple of 2 MiB, at least 4 MiB:
+    // smaller or odd-sized allocations are the ones ROCm 7.2 refuses to
+    // import).  The handle names (pid, address, size): a
+    // same-size allocation at a freed allocation's address gets its handle
+    // again; such a repeat is kept alive while the next attempt allocates
+    // elsewhere.
     std::vector<void *> failed;
     hipError_t e = hipErrorInvalidValue;
     for (int attempt = 0; attempt < 8; ++attempt) {
         void *p = nullptr;
-        const size_t sz = bytes + (size_t)(serial++ % 512u) * 4096u;
+        const size_t sz = ipc_size_for(bytes);
         {
             host_step st("hipMalloc", sz);
             e = uncached ? hipExtMallocWithFlags(&p, sz, hipDeviceMallocUncached) : hipMalloc(&p, sz);
@@ -1034,7 +1072,7 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
         c->peer_land.p[p] = nullptr;
     }
     auto close_old = [&] {
-        for (int p = 0; p < kMaxRanks; ++p) ipc_unmap(old_land[p]);
+        for (int p = 0; p < kMaxRanks; ++p) ipc_unmap(old_land[p], c);
     };
     struct land_blob { buf_desc d; uint64_t token; int ok; };
     land_blob mine{}, all[kMaxRanks];
@@ -1087,7 +1125,7 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
             break;
         }
         void *m = nullptr;
-        if (ipc_map(alloc_of(all[p].d), &c->land_ref[p], &m) != OMPI_AMD_SUCCESS) {
+        if (ipc_map(alloc_of(all[p].d), c, &c->land_ref[p], &m) != OMPI_AMD_SUCCESS) {
             status = 1;
             break;
         }
@@ -1142,7 +1180,7 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     }
     (void)c->boot.barrier();  // nobody reads the new buffers any more
     for (int p = 0; p < kMaxRanks; ++p) {
-        ipc_unmap(c->land_ref[p]);
+        ipc_unmap(c->land_ref[p], c);
         c->land_ref[p] = nullptr;
     }
     if (fresh) hip_ignore(hipFree(fresh));
@@ -2311,8 +2349,8 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
             continue;
         }
         void *f = nullptr, *s = nullptr;
-        rc = ipc_map(alloc_of(all[p].flags), &c->opened[p][0], &f);
-        if (rc == OMPI_AMD_SUCCESS) rc = ipc_map(alloc_of(all[p].scratch), &c->opened[p][1], &s);
+        rc = ipc_map(alloc_of(all[p].flags), c, &c->opened[p][0], &f);
+        if (rc == OMPI_AMD_SUCCESS) rc = ipc_map(alloc_of(all[p].scratch), c, &c->opened[p][1], &s);
         if (rc != OMPI_AMD_SUCCESS) break;
         c->peer_flags.p[p] = (uint64_t *)f;
         c->peer_scratch.p[p] = (const char *)s;
@@ -2334,12 +2372,12 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     (void)quiesce(c);
     (void)c->boot.barrier();  // nobody still reads our memory
     ipc_remove_user(c);
-    for (auto &x : c->imports) ipc_unmap(x.ref);  // the process's mapping stays while others hold it
+    for (auto &x : c->imports) ipc_unmap(x.ref, c);  // the process's mapping stays while others hold it
     c->imports.clear();
     if (c->osc_release) c->osc_release(c->osc_state, 0);  // its peer mappings
     for (int p = 0; p < kMaxRanks; ++p) {
-        for (int k = 0; k < 2; ++k) ipc_unmap(c->opened[p][k]);
-        ipc_unmap(c->land_ref[p]);
+        for (int k = 0; k < 2; ++k) ipc_unmap(c->opened[p][k], c);
+        ipc_unmap(c->land_ref[p], c);
         c->land_ref[p] = nullptr;
     }
     (void)c->boot.barrier();
@@ -2519,6 +2557,7 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "land_blocking")) *v = c->land_blocking;
     else if (!strcmp(key, "copy_nt")) *v = c->copy_nt;
     else if (!strcmp(key, "copy_nt_fixed")) *v = c->copy_nt_fixed;
+    else if (!strcmp(key, "unsafe_exports")) *v = c->unsafe_exports;
     else if (!strncmp(key, "autotune_", 9) && c->tune_last_key >= 0 &&
              c->tune.count(c->tune_last_key) && c->tune.at(c->tune_last_key).done) {
         // the last decided bucket: its choice and every candidate's worst rank

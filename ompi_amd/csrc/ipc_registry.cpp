@@ -4,10 +4,12 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <utility>
 #include <vector>
 
 #include "runtime.h"
@@ -21,13 +23,24 @@ struct ipc_ref {
     int refs = 0;
     int pins = 0;
     bool retired = false;  // closed: the exporter freed the allocation
+    std::vector<std::pair<void *, int>> holders;  // (owner, references)
 };
 
 namespace {
 
+// g_mu guards the tables below; it is never held across a runtime call that
+// can block (an open, a close, a quiesce): those run with it released, and
+// an allocation being opened sits in g_opening so that a second thread
+// asking for it waits for the first open instead of opening it twice.
 std::mutex g_mu;
-std::vector<ipc_ref *> g_live;  // open mappings
-struct user { void *owner; int (*quiesce)(void *); };
+std::condition_variable g_cv;
+std::vector<ipc_ref *> g_live;     // open mappings
+std::vector<ipc_alloc> g_opening;  // opens in progress (g_mu released)
+struct user {
+    void *owner;
+    int (*quiesce)(void *);
+    int busy;  // quiesces of it in progress: ipc_remove_user waits for them
+};
 std::vector<user> g_users;
 ipc_stats g_st{};
 
@@ -40,6 +53,12 @@ bool same_alloc(const ipc_alloc &x, const ipc_alloc &y) {
            same_handle(x.h, y.h);
 }
 
+// the exporter's allocations x and y cannot both be alive
+bool collide(const ipc_alloc &x, const ipc_alloc &y) {
+    return x.pid == y.pid && ((x.base < y.base + y.size && y.base < x.base + x.size) ||
+                              same_handle(x.h, y.h));
+}
+
 bool trace() {
     static const bool on = [] {
         const char *v = getenv("OMPI_AMD_IPC_TRACE");
@@ -48,96 +67,136 @@ bool trace() {
     return on;
 }
 
+void hold(ipc_ref *r, void *owner) {
+    ++r->refs;
+    ++g_st.refs;
+    for (auto &h : r->holders)
+        if (h.first == owner) {
+            ++h.second;
+            return;
+        }
+    r->holders.push_back({owner, 1});
+}
+
+// (g_mu released) the runtime close; the stats under the lock
 void close_mapping(ipc_ref *r) {
     const hipError_t e = hipIpcCloseMemHandle(r->base);
     hip_ignore(e);
-    ++g_st.closes;
-    --g_st.live;
     if (trace())
         fprintf(stderr, "[ipc pid %d] close pid %llu id %llu %p+%llu -> %p%s\n", (int)getpid(),
                 (unsigned long long)r->a.pid, (unsigned long long)r->a.id,
                 (void *)(uintptr_t)r->a.base, (unsigned long long)r->a.size, r->base,
                 r->retired ? " (retired)" : "");
+    std::lock_guard<std::mutex> g(g_mu);
+    ++g_st.closes;
+    --g_st.live;
+}
+
+void done_opening(const ipc_alloc &a) {
+    for (auto it = g_opening.begin(); it != g_opening.end(); ++it)
+        if (same_alloc(*it, a)) {
+            g_opening.erase(it);
+            break;
+        }
+    g_cv.notify_all();
 }
 
 }  // namespace
 
-int ipc_map(const ipc_alloc &a, ipc_ref **ref, void **base) {
+int ipc_map(const ipc_alloc &a, void *owner, ipc_ref **ref, void **base) {
     *ref = nullptr;
     *base = nullptr;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return record_hip(hipErrorInvalidDevice, "hipGetDevice (ipc_map)");
-    std::lock_guard<std::mutex> g(g_mu);
-    for (ipc_ref *r : g_live)
-        if (r->device == dev && same_alloc(r->a, a)) {
-            ++r->refs;
-            ++g_st.refs;
-            ++g_st.shared;
-            *ref = r;
-            *base = r->base;
-            return OMPI_AMD_SUCCESS;
-        }
-    // The exporter's live allocations never overlap and never share handle
-    // bytes: a mapping that does either belongs to an allocation it freed.
-    // It must be closed BEFORE the new handle is opened (the runtime would
-    // answer the open with it).  A pinned one is a program error.
     std::vector<ipc_ref *> stale;
-    for (ipc_ref *r : g_live) {
-        if (r->device != dev || r->a.pid != a.pid) continue;
-        const bool overlap = r->a.base < a.base + a.size && a.base < r->a.base + r->a.size;
-        if (overlap || same_handle(r->a.h, a.h)) stale.push_back(r);
-    }
-    for (ipc_ref *r : stale)
-        if (r->pins > 0) {
-            record_msg("process %llu freed a device buffer (id %llu, %p + %llu) that a persistent "
-                       "operation of this process still maps", (unsigned long long)a.pid,
-                       (unsigned long long)r->a.id, (void *)(uintptr_t)r->a.base,
-                       (unsigned long long)r->a.size);
-            return OMPI_AMD_ERR_BAD_PARAM;
+    std::vector<user> quiet;  // the stale mappings' holders, quiesced before the close
+    {
+        std::unique_lock<std::mutex> g(g_mu);
+        for (;;) {
+            for (ipc_ref *r : g_live)
+                if (r->device == dev && same_alloc(r->a, a)) {
+                    hold(r, owner);
+                    ++g_st.shared;
+                    *ref = r;
+                    *base = r->base;
+                    return OMPI_AMD_SUCCESS;
+                }
+            // another thread opens this allocation or one it collides with:
+            // wait for that open to finish, then look again
+            bool busy = false;
+            for (const ipc_alloc &o : g_opening) busy = busy || collide(o, a);
+            if (!busy) break;
+            g_cv.wait(g);
         }
-    if (!stale.empty()) {
-        // earlier work of any user may still read through these mappings
-        for (const user &u : g_users) {
-            const int rc = u.quiesce(u.owner);
-            if (rc != OMPI_AMD_SUCCESS) return rc;
-        }
-        for (ipc_ref *r : stale) {
+        // The exporter's live allocations never overlap and never share
+        // handle bytes: a mapping that does either belongs to an allocation
+        // it freed.  It must be closed BEFORE the new handle is opened (the
+        // runtime would answer the open with it).  A pinned one is a program
+        // error.
+        for (ipc_ref *r : g_live)
+            if (r->device == dev && collide(r->a, a)) stale.push_back(r);
+        for (ipc_ref *r : stale)
+            if (r->pins > 0) {
+                record_msg("process %llu freed a device buffer (id %llu, %p + %llu) that a persistent "
+                           "operation of this process still maps", (unsigned long long)a.pid,
+                           (unsigned long long)r->a.id, (void *)(uintptr_t)r->a.base,
+                           (unsigned long long)r->a.size);
+                return OMPI_AMD_ERR_BAD_PARAM;
+            }
+        for (ipc_ref *r : stale) {  // nobody shares it from now on
             r->retired = true;
-            close_mapping(r);
+            ++r->refs;  // this retirement's own, until the close below
             ++g_st.retired;
             g_live.erase(std::find(g_live.begin(), g_live.end(), r));
-            if (r->refs == 0) delete r;  // else freed by its last holder's ipc_unmap
+            for (auto &h : r->holders)
+                for (auto &u : g_users)
+                    if (u.owner == h.first &&
+                        std::none_of(quiet.begin(), quiet.end(),
+                                     [&](const user &q) { return q.owner == u.owner; })) {
+                        ++u.busy;
+                        quiet.push_back(u);
+                    }
         }
+        g_opening.push_back(a);
     }
+    // Only the holders of the stale mappings can have device work reading
+    // through them: each drains its own streams (not every communicator's —
+    // one with a deferred call waiting for a peer must not be waited for
+    // here, and the exporter's free already implies the holders' reads of
+    // the freed buffer completed: every collective ends with a barrier).
+    int rc = OMPI_AMD_SUCCESS;
+    for (const user &u : quiet) {
+        const int q = u.quiesce(u.owner);
+        if (rc == OMPI_AMD_SUCCESS) rc = q;
+    }
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        for (const user &q : quiet)
+            for (auto &u : g_users)
+                if (u.owner == q.owner) --u.busy;
+        g_cv.notify_all();
+    }
+    for (ipc_ref *r : stale) {
+        close_mapping(r);
+        std::lock_guard<std::mutex> g(g_mu);
+        if (--r->refs == 0) delete r;  // else freed by its last holder's ipc_unmap
+    }
+    if (rc != OMPI_AMD_SUCCESS) {
+        std::lock_guard<std::mutex> g(g_mu);
+        done_opening(a);
+        return rc;
+    }
+    // One open: the exportable allocations are sized so that the runtime
+    // answers (tools/ipc_replay_probe.py): a refusal is an
+    // error, reported with the buffer, never retried.
     void *m = nullptr;
+    const hipError_t e = hipIpcOpenMemHandle(&m, a.h, hipIpcMemLazyEnablePeerAccess);
+    std::lock_guard<std::mutex> g(g_mu);
     ++g_st.opens;
-    hipError_t e = hipIpcOpenMemHandle(&m, a.h, hipIpcMemLazyEnablePeerAccess);
-    // ROCm 7.2 intermittently refuses the open of a live peer allocation
-    // ("invalid device pointer"; in dmabuf mode the exporter answers the
-    // import through a socket-serving thread it starts at its first export).
-    // Four synthetic storms on one box — 2,240-3,360 opens each: all ranks
-    // opening one exporter at once, exporters busy in device copies and
-    // syncs, exporters freeing before importers close — saw no refusal
-    // (profiles/r03_ipc_storm_probe.jsonl), while the library's suites see
-    // about one per two full runs at N = 4 / 8.  A refusal is tried again
-    // after a short wait, at most three times, counted (ipc_refusals) and
-    // reported on stderr: a transient answer must not fail a collective,
-    // and a persistent one still does after ~30 ms.
-    for (int attempt = 1; e != hipSuccess && attempt <= 3; ++attempt) {
-        (void)hipGetLastError();
-        ++g_st.refusals;
-        fprintf(stderr,
-                "ompi_amd[pid %d]: hipIpcOpenMemHandle refused process %llu buffer id %llu "
-                "(%p + %llu): %s; trying again (%d of 3)\n",
-                (int)getpid(), (unsigned long long)a.pid, (unsigned long long)a.id,
-                (void *)(uintptr_t)a.base, (unsigned long long)a.size, hipGetErrorString(e),
-                attempt);
-        usleep(2000u << attempt);  // 4, 8, 16 ms
-        ++g_st.opens;
-        e = hipIpcOpenMemHandle(&m, a.h, hipIpcMemLazyEnablePeerAccess);
-    }
+    done_opening(a);
     if (e != hipSuccess) {
         (void)hipGetLastError();
+        ++g_st.refusals;
         record_msg("hipIpcOpenMemHandle: %s (process %llu buffer id %llu at %p + %llu)",
                    hipGetErrorString(e), (unsigned long long)a.pid, (unsigned long long)a.id,
                    (void *)(uintptr_t)a.base, (unsigned long long)a.size);
@@ -175,10 +234,9 @@ int ipc_map(const ipc_alloc &a, ipc_ref **ref, void **base) {
     r->a = a;
     r->device = dev;
     r->base = m;
-    r->refs = 1;
+    hold(r, owner);
     g_live.push_back(r);
     ++g_st.live;
-    ++g_st.refs;
     if (trace())
         fprintf(stderr, "[ipc pid %d] open pid %llu id %llu %p+%llu -> %p\n", (int)getpid(),
                 (unsigned long long)a.pid, (unsigned long long)a.id, (void *)(uintptr_t)a.base,
@@ -188,16 +246,29 @@ int ipc_map(const ipc_alloc &a, ipc_ref **ref, void **base) {
     return OMPI_AMD_SUCCESS;
 }
 
-void ipc_unmap(ipc_ref *r) {
+void ipc_unmap(ipc_ref *r, void *owner) {
     if (!r) return;
-    std::lock_guard<std::mutex> g(g_mu);
-    --g_st.refs;
-    if (--r->refs > 0) return;
-    if (!r->retired) {
-        close_mapping(r);
+    bool close = false;
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        --g_st.refs;
+        for (auto it = r->holders.begin(); it != r->holders.end(); ++it)
+            if (it->first == owner) {
+                if (--it->second == 0) r->holders.erase(it);
+                break;
+            }
+        if (--r->refs > 0) return;
+        if (r->retired) {  // already closed by the open that retired it
+            delete r;
+            return;
+        }
         g_live.erase(std::find(g_live.begin(), g_live.end(), r));
+        close = true;
     }
-    delete r;
+    if (close) {
+        close_mapping(r);
+        delete r;
+    }
 }
 
 void ipc_pin(ipc_ref *r, int delta) {
@@ -215,11 +286,17 @@ void *ipc_ref_base(const ipc_ref *r) { return r ? r->base : nullptr; }
 
 void ipc_add_user(void *owner, int (*quiesce)(void *)) {
     std::lock_guard<std::mutex> g(g_mu);
-    g_users.push_back({owner, quiesce});
+    g_users.push_back({owner, quiesce, 0});
 }
 
 void ipc_remove_user(void *owner) {
-    std::lock_guard<std::mutex> g(g_mu);
+    std::unique_lock<std::mutex> g(g_mu);
+    // another thread's open may be draining this user's streams right now
+    g_cv.wait(g, [&] {
+        for (const user &u : g_users)
+            if (u.owner == owner && u.busy > 0) return false;
+        return true;
+    });
     g_users.erase(std::remove_if(g_users.begin(), g_users.end(),
                                  [&](const user &u) { return u.owner == owner; }),
                   g_users.end());

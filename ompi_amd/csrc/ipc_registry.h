@@ -34,11 +34,14 @@ struct ipc_alloc {
 struct ipc_ref;  // one registry entry (opaque)
 
 // Map a peer allocation, or share the mapping the process already holds of
-// it: one more reference.  *base = the mapping of the allocation's first byte.
-int ipc_map(const ipc_alloc &a, ipc_ref **ref, void **base);
-// Drop one reference; the last one closes the mapping (the caller has made
-// sure none of its own device work still reads or writes through it).
-void ipc_unmap(ipc_ref *ref);
+// it: one more reference, held by `owner` (a registered user, see below).
+// *base = the mapping of the allocation's first byte.  Mappings the new
+// allocation collides with are retired first: only their holders are
+// quiesced, and no lock is held across the quiesce, the close or the open.
+int ipc_map(const ipc_alloc &a, void *owner, ipc_ref **ref, void **base);
+// Drop one of owner's references; the last one closes the mapping (the
+// caller has made sure none of its own device work still uses it).
+void ipc_unmap(ipc_ref *ref, void *owner);
 // A persistent operation holds the mapping (MPI_Allreduce_init, a window):
 // an exporter that frees the allocation meanwhile is a program error that
 // the next open of its newer allocation reports instead of unmapping.
@@ -48,13 +51,15 @@ bool ipc_retired(const ipc_ref *ref);
 void *ipc_ref_base(const ipc_ref *ref);
 
 // Users of mappings (communicators) register a function that waits for all
-// of their device work; retiring a mapping runs every one of them first.
+// of their device work; retiring a mapping runs it for each user holding a
+// reference to the mapping.  The function may run on another thread than
+// the user's own (it must be safe against the user's concurrent calls).
 void ipc_add_user(void *owner, int (*quiesce)(void *owner));
 void ipc_remove_user(void *owner);
 
 struct ipc_stats {
     int64_t opens;        // hipIpcOpenMemHandle calls made
-    int64_t refusals;     // opens the runtime refused and that were tried again
+    int64_t refusals;     // opens the runtime refused (each one failed its call)
     int64_t closes;       // hipIpcCloseMemHandle calls made
     int64_t shared;       // ipc_map answered from a mapping the process held
     int64_t retired;      // mappings retired because the exporter freed the allocation

@@ -600,6 +600,7 @@ struct ctl_chunk {
 struct ctl_arena {
     std::vector<ctl_chunk> chunks;
     std::vector<char> used;  // per slot
+    void *owner = nullptr;   // the communicator holding the chunks' mappings
 };
 
 static void ctl_arena_release(void *state, int phase) {
@@ -608,7 +609,7 @@ static void ctl_arena_release(void *state, int phase) {
     if (phase == 0) {  // nobody reads our pages any more: drop the peers' mappings
         for (auto &ch : a->chunks)
             for (auto &r : ch.ref) {
-                ipc_unmap(r);
+                ipc_unmap(r, a->owner);
                 r = nullptr;
             }
         return;
@@ -627,6 +628,7 @@ static int ctl_take(ompi_amd_comm_t *c, int rc_in, int *slot) {
     if (!a) {
         a = new (std::nothrow) ctl_arena;
         if (!a) return OMPI_AMD_ERR_BAD_PARAM;  // every rank: the same allocation failure
+        a->owner = c;
         comm_set_osc_state(c, a, ctl_arena_release);
     }
     for (size_t k = 0; k < a->used.size(); ++k)
@@ -661,7 +663,7 @@ static int ctl_take(ompi_amd_comm_t *c, int rc_in, int *slot) {
         } else {  // one attempt (a refused open is an error)
             void *m = nullptr;
             const ipc_desc &d = all[p].d;
-            rc = ipc_map(ipc_alloc{d.h, d.pid, d.id, d.base, d.size}, &ch.ref[p], &m);
+            rc = ipc_map(ipc_alloc{d.h, d.pid, d.id, d.base, d.size}, c, &ch.ref[p], &m);
             ch.peer[p] = reinterpret_cast<uint32_t *>(static_cast<char *>(m) + d.off);
         }
     }
@@ -670,7 +672,7 @@ static int ctl_take(ompi_amd_comm_t *c, int rc_in, int *slot) {
     if (rc == OMPI_AMD_SUCCESS && (grc != OMPI_AMD_SUCCESS || !all_ok))
         rc = grc != OMPI_AMD_SUCCESS ? grc : OMPI_AMD_ERR_BOOTSTRAP;
     if (rc != OMPI_AMD_SUCCESS) {
-        for (auto &r : ch.ref) ipc_unmap(r);
+        for (auto &r : ch.ref) ipc_unmap(r, c);
         (void)comm_allgather(c, nullptr, nullptr, 0);  // every mapping closed before the free
         if (ch.mine) hip_ignore(hipFree(ch.mine));
         return rc;

@@ -513,9 +513,9 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     const bool host = bytes && !is_device(buf);
     const bool eager = bytes <= kEager && mode != OMPI_AMD_SEND_SYNCHRONOUS;  // Ssend: rendezvous
     std::unique_lock<std::recursive_mutex> alloc_guard(p->mu);
-    if (rc == OMPI_AMD_SUCCESS && eager && !p->eager) {
-        rc = record_hip(hipMalloc((void **)&p->eager, (size_t)p->size * kSlots * kEager),
-                        "hipMalloc (p2p eager area)");
+    if (rc == OMPI_AMD_SUCCESS && eager && !p->eager) {  // peers read its cells: exportable
+        ipc_desc d{};
+        rc = comm_alloc_exportable((size_t)p->size * kSlots * kEager, false, (void **)&p->eager, &d);
         if (rc != OMPI_AMD_SUCCESS) p->eager = nullptr;
     }
     alloc_guard.unlock();
