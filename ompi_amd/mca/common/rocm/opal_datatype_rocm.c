@@ -315,15 +315,35 @@ int32_t opal_rocm_unpack(opal_convertor_t *convertor, struct iovec *iov, uint32_
     return advance(convertor, iov, out_size, max_data, 1);
 }
 
+#if !OPAL_CUDA_SUPPORT
+/* A ROCm-only build has no cbmemcpy hook (opal_convertor.h:120-123): the
+ * reference's host walker would memcpy the device buffer with the CPU.  A
+ * device buffer whose datatype has no device program (more than
+ * FLAT_MAX_ELEMS flattened elements, a leaf that is not predefined) gets
+ * this fAdvance instead: the conversion fails with -1 (the contract's error
+ * return) and nothing is read or written. */
+int32_t opal_rocm_refuse(opal_convertor_t *convertor, struct iovec *iov, uint32_t *out_size,
+                         size_t *max_data)
+{
+    (void) convertor;
+    (void) iov;
+    *out_size = 0;
+    *max_data = 0;
+    return -1;
+}
+#endif
+
 /* The first byte the conversion touches is device memory (the reference's
  * mca_cuda_convertor_init asks the same of pUserBuf, opal_datatype_cuda.c:
  * 44-60; the true lower bound keeps a type with a negative lb inside the
  * allocation). */
+#if !OPAL_CUDA_SUPPORT
 static int device_buffer(const opal_convertor_t *c)
 {
     if (NULL == c->pBaseBuf || NULL == c->pDesc) return 0;
     return ompi_amd_is_device_pointer(c->pBaseBuf + c->pDesc->true_lb);
 }
+#endif
 
 int opal_rocm_convertor_select(opal_convertor_t *convertor)
 {
@@ -337,6 +357,10 @@ int opal_rocm_convertor_select(opal_convertor_t *convertor)
 #else
     /* a ROCm-only build: this seam asks the runtime itself */
     if (!device_buffer(convertor)) return 0;
+    if (!program_of(convertor->pDesc, 1)) {  /* never the CPU on device memory */
+        convertor->fAdvance = opal_rocm_refuse;
+        return 1;
+    }
 #endif
     if (!program_of(convertor->pDesc, 1)) return 0;
     convertor->fAdvance = (f & CONVERTOR_SEND) ? opal_rocm_pack : opal_rocm_unpack;
@@ -345,6 +369,9 @@ int opal_rocm_convertor_select(opal_convertor_t *convertor)
 
 int opal_rocm_convertor_owns(const opal_convertor_t *convertor)
 {
+#if !OPAL_CUDA_SUPPORT
+    if (convertor->fAdvance == opal_rocm_refuse) return 1;
+#endif
     return convertor->fAdvance == opal_rocm_pack || convertor->fAdvance == opal_rocm_unpack;
 }
 

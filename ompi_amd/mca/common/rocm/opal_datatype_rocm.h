@@ -37,9 +37,11 @@ int mca_common_rocm_fill_table(opal_common_cuda_function_table_t *ftable);
 
 /* After prepare_for_send / _recv chose fAdvance: offload it when the
  * convertor is a device conversion the library can run.  Returns 1 when
- * fAdvance now points at opal_rocm_pack / opal_rocm_unpack, 0 when the
- * reference's choice stays (host buffer, NO_OP contiguous fast path, a
- * description too irregular to flatten).  Device residency: CONVERTOR_CUDA
+ * fAdvance now points at opal_rocm_pack / opal_rocm_unpack (or, ROCm-only
+ * build, opal_rocm_refuse for a device description too irregular to
+ * flatten), 0 when the reference's choice stays (host buffer, NO_OP
+ * contiguous fast path; a CUDA-support build's irregular description, whose
+ * host walker copies through cbmemcpy).  Device residency: CONVERTOR_CUDA
  * in an OPAL_CUDA_SUPPORT build; otherwise this seam's own pointer query
  * (so a ROCm-only build, where nothing sets CONVERTOR_CUDA, offloads too). */
 int opal_rocm_convertor_select(opal_convertor_t *convertor);
@@ -60,6 +62,13 @@ int32_t opal_rocm_pack(opal_convertor_t *convertor, struct iovec *iov, uint32_t 
                        size_t *max_data);
 int32_t opal_rocm_unpack(opal_convertor_t *convertor, struct iovec *iov, uint32_t *out_size,
                          size_t *max_data);
+#if !OPAL_CUDA_SUPPORT
+/* A ROCm-only build's fAdvance for a device buffer whose description has no
+ * device program (select returns 1 with it): returns -1 and touches
+ * nothing, since that build has no cbmemcpy for the host walker to use. */
+int32_t opal_rocm_refuse(opal_convertor_t *convertor, struct iovec *iov, uint32_t *out_size,
+                         size_t *max_data);
+#endif
 
 /* Device programs cached per datatype description (tests / finalize). */
 int opal_rocm_program_cache_size(void);

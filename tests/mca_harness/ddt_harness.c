@@ -577,6 +577,67 @@ int main(void)
             return 1;
         }
     }
+    {   /* a description the device program cannot hold (6000 flattened
+         * runs > FLAT_MAX_ELEMS) on device memory: a CUDA-support build keeps
+         * the reference's walker (its cbmemcpy copies device runs); a
+         * ROCm-only build must fail the conversion without the CPU touching
+         * the device buffer */
+        opal_datatype_t dt;
+        dt_elem_desc_t desc[4];
+        opal_convertor_t c;
+        void *dbuf = NULL;
+        char *zero = calloc(3000 * 64, 1), host[256];
+        struct iovec iov = {host, sizeof(host)};
+        uint32_t n = 1;
+        size_t max = sizeof(host);
+        memset(&dt, 0, sizeof(dt));
+        memset(desc, 0, sizeof(desc));
+        desc[0].loop.common.type = OPAL_DATATYPE_LOOP;
+        desc[0].loop.items = 3;
+        desc[0].loop.loops = 3000;
+        desc[0].loop.extent = 64;
+        for (int k = 0; k < 2; ++k) {
+            desc[1 + k].elem.common.type = OPAL_DATATYPE_FLOAT8;
+            desc[1 + k].elem.common.flags = OPAL_DATATYPE_FLAG_DATA;
+            desc[1 + k].elem.count = 1;
+            desc[1 + k].elem.blocklen = 1;
+            desc[1 + k].elem.extent = 8;
+            desc[1 + k].elem.disp = k ? 24 : 0;
+        }
+        desc[3].end_loop.common.type = OPAL_DATATYPE_END_LOOP;
+        desc[3].end_loop.items = 3;
+        desc[3].end_loop.size = 16;
+        dt.size = 3000 * 16;
+        dt.ub = 3000 * 64;
+        dt.true_ub = 2999 * 64 + 32;
+        dt.opt_desc.desc = desc;
+        dt.opt_desc.used = 4;
+        dt.desc = dt.opt_desc;
+        if (harness_dev_alloc_copy(&dbuf, zero, 3000 * 64) != 0) {
+            printf("FAIL: device alloc\n");
+            return 1;
+        }
+        memset(host, 0x5A, sizeof(host));
+        opal_convertor_prepare_for_send(&c, &dt, 1, dbuf);
+#if OPAL_CUDA_SUPPORT
+        (void) iov;
+        (void) n;
+        (void) max;
+        if (opal_rocm_convertor_owns(&c)) {
+            printf("FAIL: an unflattenable description was offloaded\n");
+            return 1;
+        }
+#else
+        if (c.fAdvance != opal_rocm_refuse || opal_convertor_pack(&c, &iov, &n, &max) != -1 ||
+            max != 0 || (unsigned char) host[0] != 0x5A) {
+            printf("FAIL: an unflattenable device description was not refused\n");
+            return 1;
+        }
+#endif
+        printf("ok unflattenable device description (OPAL_CUDA_SUPPORT %d)\n", OPAL_CUDA_SUPPORT);
+        harness_dev_free(dbuf);
+        free(zero);
+    }
     int fails = 0, types = 0;
     spec_t s;
     int r;

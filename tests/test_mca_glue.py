@@ -275,6 +275,10 @@ def test_convertor_seam_fadvance(ddt_harness, golden):
                        input=_ddt_specs(golden) + _ooo_specs(golden),
                        env={**os.environ, "HARNESS_GPU": "1"})
     assert r.returncode == 0 and "all" in r.stdout, (r.stdout[-3000:], r.stderr[-2000:])
+    # a device description past the program's element limit: kept on the
+    # reference's walker (CUDA build: cbmemcpy) or refused (ROCm-only build),
+    # never walked by the CPU over device memory
+    assert "ok unflattenable device description" in r.stdout, r.stdout[-3000:]
     for t in ("unpack_ooo_test1", "unpack_ooo_test2", "unpack_ooo_test3", "unpack_ooo_test4",
               "position_long_double_int", "position_noncontig_vector_int"):
         assert f"ok {t}" in r.stdout, r.stdout[-3000:]
