@@ -75,6 +75,9 @@ const char *ompi_amd_last_error(void);
  * mca_common_cuda_is_gpu_buffer (opal/mca/common/cuda/common_cuda.c:
  * 1739-1792) used by the convertor and the handlers to pick the path. */
 int ompi_amd_is_device_pointer(const void *ptr);
+/* The same answer, and for device memory the allocation holding ptr
+ * (hipMemGetAddressRange): 1 device (*base, *size set), 0 host, <0 error. */
+int ompi_amd_pointer_range(const void *ptr, void **base, size_t *size);
 
 /* The HIP side of the convertor's GPU function table
  * (opal_common_cuda_function_table_t, opal/datatype/opal_datatype_cuda.h:
@@ -92,6 +95,21 @@ int ompi_amd_stream_synchronize(void *stream);
  * residency staging): hipMalloc / hipFree.  bytes == 0 gives NULL. */
 int ompi_amd_device_alloc(void **ptr, size_t bytes);
 int ompi_amd_device_free(void *ptr);
+/* Page-locked host memory (hipHostMalloc / hipHostFree) for staging
+ * windows the device reads and writes directly (the convertor seam's
+ * host-fragment windows).  bytes == 0 gives NULL. */
+int ompi_amd_host_alloc(void **ptr, size_t bytes);
+int ompi_amd_host_free(void *ptr);
+/* Completion markers on a stream — the counterparts of common/cuda's
+ * record / progress of its dtoh / htod events (common_cuda.c:1008-1320)
+ * for a convertor run asynchronously.  ompi_amd_event_record creates the
+ * event at *event the first time (NULL: create) and records it on
+ * `stream` (NULL: the calling thread's); ompi_amd_event_query returns 1
+ * once the work before it finished, 0 while pending, <0 on error. */
+int ompi_amd_event_record(void **event, void *stream);
+int ompi_amd_event_query(void *event);
+int ompi_amd_event_synchronize(void *event);
+int ompi_amd_event_destroy(void *event);
 
 /* ================================================================== */
 /* 1. MPI_Op kernels — replaces op/base's handler loops                */

@@ -113,10 +113,17 @@ PROTOTYPES = [
      [_C.c_void_p, _C.c_size_t, _C.c_void_p, _C.c_size_t, _C.c_void_p, _C.POINTER(_C.c_uint32),
       _C.POINTER(_C.c_size_t), _C.c_void_p]),
     ("ompi_amd_is_device_pointer", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_pointer_range", _C.c_int, [_C.c_void_p, _C.POINTER(_C.c_void_p), _C.POINTER(_C.c_size_t)]),
     ("ompi_amd_memcpy_async", _C.c_int, [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p]),
     ("ompi_amd_memcpy", _C.c_int, [_C.c_void_p, _C.c_void_p, _C.c_size_t]),
     ("ompi_amd_memmove", _C.c_int, [_C.c_void_p, _C.c_void_p, _C.c_size_t]),
     ("ompi_amd_device_alloc", _C.c_int, [_C.POINTER(_C.c_void_p), _C.c_size_t]),
+    ("ompi_amd_host_alloc", _C.c_int, [_C.POINTER(_C.c_void_p), _C.c_size_t]),
+    ("ompi_amd_host_free", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_event_record", _C.c_int, [_C.POINTER(_C.c_void_p), _C.c_void_p]),
+    ("ompi_amd_event_query", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_event_synchronize", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_event_destroy", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_device_free", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_stream_synchronize", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_comm_create", _C.c_int,

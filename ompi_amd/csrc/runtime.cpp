@@ -97,6 +97,19 @@ int ompi_amd_is_device_pointer(const void *ptr) {
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
+int ompi_amd_pointer_range(const void *ptr, void **base, size_t *size) {
+    if (!base || !size) return OMPI_AMD_ERR_BAD_PARAM;
+    *base = nullptr;
+    *size = 0;
+    if (!ompi_amd_is_device_pointer(ptr)) return 0;
+    if (hipMemGetAddressRange((hipDeviceptr_t *)base, size, (hipDeviceptr_t)ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        *base = const_cast<void *>(ptr);  // device, range unknown: this byte only
+        *size = 1;
+    }
+    return 1;
+}
+
 }  // extern "C"
 
 namespace ompi_amd {
@@ -170,6 +183,50 @@ int ompi_amd_device_alloc(void **ptr, size_t bytes) {
 int ompi_amd_device_free(void *ptr) {
     if (!ptr) return OMPI_AMD_SUCCESS;
     return record_hip(hipFree(ptr), "hipFree");
+}
+
+int ompi_amd_host_alloc(void **ptr, size_t bytes) {
+    if (!ptr) return OMPI_AMD_ERR_BAD_PARAM;
+    *ptr = nullptr;
+    if (bytes == 0) return OMPI_AMD_SUCCESS;
+    return record_hip(hipHostMalloc(ptr, bytes, hipHostMallocDefault), "hipHostMalloc");
+}
+
+int ompi_amd_host_free(void *ptr) {
+    if (!ptr) return OMPI_AMD_SUCCESS;
+    return record_hip(hipHostFree(ptr), "hipHostFree");
+}
+
+int ompi_amd_event_record(void **event, void *stream) {
+    if (!event) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!*event) {
+        hipEvent_t e = nullptr;
+        const int rc = record_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+        if (rc != OMPI_AMD_SUCCESS) return rc;
+        *event = e;
+    }
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : thread_stream();
+    return record_hip(hipEventRecord(static_cast<hipEvent_t>(*event), s), "hipEventRecord");
+}
+
+int ompi_amd_event_query(void *event) {
+    if (!event) return OMPI_AMD_ERR_BAD_PARAM;
+    const hipError_t e = hipEventQuery(static_cast<hipEvent_t>(event));
+    if (e == hipErrorNotReady) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return e == hipSuccess ? 1 : record_hip(e, "hipEventQuery");
+}
+
+int ompi_amd_event_synchronize(void *event) {
+    if (!event) return OMPI_AMD_ERR_BAD_PARAM;
+    return record_hip(hipEventSynchronize(static_cast<hipEvent_t>(event)), "hipEventSynchronize");
+}
+
+int ompi_amd_event_destroy(void *event) {
+    if (!event) return OMPI_AMD_SUCCESS;
+    return record_hip(hipEventDestroy(static_cast<hipEvent_t>(event)), "hipEventDestroy");
 }
 
 }  // extern "C"

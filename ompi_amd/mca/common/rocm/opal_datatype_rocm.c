@@ -280,6 +280,219 @@ void opal_rocm_program_cache_clear(void)
     pthread_mutex_unlock(&g_lock);
 }
 
+/* ------------------------------------------------ per-convertor state */
+
+/* What a conversion carries between fAdvance calls (opal_convertor_t has no
+ * field for it): kept beside the convertor, keyed by its address, reset at
+ * every prepare (select) and released when the conversion completes.
+ *
+ *  - deferred device fragments (a caller that asked for it with
+ *    opal_rocm_set_copy_function_async): fAdvance records the iovecs and
+ *    returns; the next flush (opal_rocm_record_event, a synchronous call,
+ *    a set_position) launches one kernel over all of them.  One fAdvance
+ *    per 64 KiB fragment then costs a few host instructions, and a train
+ *    of fragments one launch (the reference pays a cuMemcpy per run per
+ *    fragment, opal_datatype_cuda.c:121-145).
+ *  - host fragments (btl/sm's shared-memory fragments, MPI_Pack into host
+ *    memory): the device never touches a host iovec — that memory is not
+ *    mapped for it.  A send packs a window of up to WIN_BYTES of the stream
+ *    ahead with one launch, copies it to page-locked memory once, and
+ *    serves that fragment and the following ones from there with memcpy; a
+ *    receive gathers host fragments in page-locked memory and unpacks a
+ *    window at a time (at the latest when the stream completes). */
+#define WIN_BYTES ((size_t) 16 << 20)
+
+typedef struct {
+    const opal_convertor_t *conv;
+    void *stream;   /* async stream (ROCm-only build: the convertor has no field) */
+    int defer;      /* device fragments are recorded, launched at the next flush */
+    struct iovec *dq;
+    uint32_t ndq, capdq;
+    size_t dq_pos, dq_end;  /* stream range of the recorded fragments */
+    char *win_dev, *win_host;
+    size_t win_pos, win_end;  /* stream range held in win_host */
+    uintptr_t dev_lo, dev_hi; /* the device allocation the last fragment was in */
+} conv_state;
+
+static conv_state **g_states;
+static int g_nstates, g_capstates;
+static pthread_mutex_t g_state_lock = PTHREAD_MUTEX_INITIALIZER;
+/* released windows, reused (page-locked allocations are slow to make) */
+#define WIN_POOL 4
+static char *g_pool_dev[WIN_POOL], *g_pool_host[WIN_POOL];
+static int g_npool;
+
+/* the last state this thread used, valid while no state was dropped since
+ * (g_epoch): the per-fragment lookup without the lock */
+static unsigned long g_epoch;
+static __thread conv_state *tl_state;
+static __thread unsigned long tl_epoch;
+
+static conv_state *state_of(const opal_convertor_t *c, int create)
+{
+    conv_state *st = NULL;
+    if (tl_state && tl_state->conv == c && tl_epoch == __atomic_load_n(&g_epoch, __ATOMIC_ACQUIRE))
+        return tl_state;
+    pthread_mutex_lock(&g_state_lock);
+    for (int i = 0; i < g_nstates; ++i)
+        if (g_states[i]->conv == c) {
+            st = g_states[i];
+            break;
+        }
+    if (!st && create) {
+        if (g_nstates == g_capstates) {
+            const int cap = g_capstates ? 2 * g_capstates : 16;
+            conv_state **n = realloc(g_states, (size_t) cap * sizeof(*n));
+            if (n) {
+                g_states = n;
+                g_capstates = cap;
+            }
+        }
+        if (g_nstates < g_capstates && (st = calloc(1, sizeof(*st)))) {
+            st->conv = c;
+            g_states[g_nstates++] = st;
+        }
+    }
+    if (st) {
+        tl_state = st;
+        tl_epoch = __atomic_load_n(&g_epoch, __ATOMIC_ACQUIRE);
+    }
+    pthread_mutex_unlock(&g_state_lock);
+    return st;
+}
+
+static void state_drop(const opal_convertor_t *c)
+{
+    conv_state *st = NULL;
+    pthread_mutex_lock(&g_state_lock);
+    for (int i = 0; i < g_nstates; ++i)
+        if (g_states[i]->conv == c) {
+            st = g_states[i];
+            g_states[i] = g_states[--g_nstates];
+            __atomic_add_fetch(&g_epoch, 1, __ATOMIC_RELEASE);  /* every thread's cache */
+            break;
+        }
+    if (st && st->win_dev) {
+        if (g_npool < WIN_POOL) {
+            g_pool_dev[g_npool] = st->win_dev;
+            g_pool_host[g_npool++] = st->win_host;
+            st->win_dev = st->win_host = NULL;
+        }
+    }
+    pthread_mutex_unlock(&g_state_lock);
+    if (!st) return;
+    (void) ompi_amd_device_free(st->win_dev);
+    (void) ompi_amd_host_free(st->win_host);
+    free(st->dq);
+    free(st);
+}
+
+static int state_window(conv_state *st)
+{
+    if (st->win_dev) return 0;
+    pthread_mutex_lock(&g_state_lock);
+    if (g_npool > 0) {
+        st->win_dev = g_pool_dev[--g_npool];
+        st->win_host = g_pool_host[g_npool];
+    }
+    pthread_mutex_unlock(&g_state_lock);
+    if (st->win_dev) return 0;
+    if (0 != ompi_amd_device_alloc((void **) &st->win_dev, WIN_BYTES) ||
+        0 != ompi_amd_host_alloc((void **) &st->win_host, WIN_BYTES)) {
+        (void) ompi_amd_device_free(st->win_dev);
+        st->win_dev = NULL;
+        return -1;
+    }
+    return 0;
+}
+
+static void *stream_of(const opal_convertor_t *c, const conv_state *st)
+{
+    return NULL != st && NULL != st->stream ? st->stream : conv_stream(c);
+}
+
+/* launch the recorded device fragments (one kernel over all of them) */
+static int flush_dq(opal_convertor_t *c, conv_state *st, ompi_amd_ddt_t *prog, int unpack)
+{
+    if (!st || 0 == st->ndq) return 0;
+    uint32_t n = st->ndq;
+    size_t moved = 0;
+    const int rc = unpack
+        ? ompi_amd_ddt_unpack_iov(prog, c->count, c->pBaseBuf, st->dq_pos,
+                                  (ompi_amd_iovec_t *) st->dq, &n, &moved, stream_of(c, st))
+        : ompi_amd_ddt_pack_iov(prog, c->count, c->pBaseBuf, st->dq_pos,
+                                (ompi_amd_iovec_t *) st->dq, &n, &moved, stream_of(c, st));
+    st->ndq = 0;
+    return rc < 0 || moved != st->dq_end - st->dq_pos ? -1 : 0;
+}
+
+/* a receive's gathered host window onto the device, unpacked (and waited
+ * for: the window is refilled only after the device read it) */
+static int flush_win(opal_convertor_t *c, conv_state *st, ompi_amd_ddt_t *prog)
+{
+    if (!st || st->win_end == st->win_pos) return 0;
+    const size_t n = st->win_end - st->win_pos;
+    void *s = stream_of(c, st);
+    struct iovec v = {st->win_dev, n};
+    uint32_t one = 1;
+    size_t moved = 0;
+    int rc = ompi_amd_memcpy_async(st->win_dev, st->win_host, n, s);
+    if (0 == rc)
+        rc = ompi_amd_ddt_unpack_iov(prog, c->count, c->pBaseBuf, st->win_pos,
+                                     (ompi_amd_iovec_t *) &v, &one, &moved, s) < 0 ? -1 : 0;
+    if (0 == rc) rc = ompi_amd_stream_synchronize(s);
+    st->win_pos = st->win_end;
+    return 0 == rc && moved == n ? 0 : -1;
+}
+
+/* a send's window [pos, pos + n) packed on the device and copied to host */
+static int fill_win(opal_convertor_t *c, conv_state *st, ompi_amd_ddt_t *prog, size_t pos, size_t n)
+{
+    void *s = stream_of(c, st);
+    struct iovec v = {st->win_dev, n};
+    uint32_t one = 1;
+    size_t moved = 0;
+    if (ompi_amd_ddt_pack_iov(prog, c->count, c->pBaseBuf, pos, (ompi_amd_iovec_t *) &v, &one,
+                              &moved, s) < 0 || moved != n ||
+        0 != ompi_amd_memcpy_async(st->win_host, st->win_dev, n, s) ||
+        0 != ompi_amd_stream_synchronize(s)) {
+        st->win_pos = st->win_end = 0;
+        return -1;
+    }
+    st->win_pos = pos;
+    st->win_end = pos + n;
+    return 0;
+}
+
+/* a fragment in device memory?  The allocation of the previous one is
+ * remembered, so a train of fragments in one buffer asks the runtime once */
+static int on_device(conv_state *st, const void *p)
+{
+    void *b = NULL;
+    size_t n = 0;
+    if ((uintptr_t) p >= st->dev_lo && (uintptr_t) p < st->dev_hi) return 1;
+    if (1 != ompi_amd_pointer_range(p, &b, &n)) return 0;
+    st->dev_lo = (uintptr_t) b;
+    st->dev_hi = (uintptr_t) b + n;
+    return 1;
+}
+
+static int record_dq(conv_state *st, void *base, size_t len, size_t pos)
+{
+    if (st->ndq == st->capdq) {
+        const uint32_t cap = st->capdq ? 2 * st->capdq : 64;
+        struct iovec *n = realloc(st->dq, (size_t) cap * sizeof(*n));
+        if (!n) return -1;
+        st->dq = n;
+        st->capdq = cap;
+    }
+    if (0 == st->ndq) st->dq_pos = pos;
+    st->dq[st->ndq].iov_base = base;
+    st->dq[st->ndq++].iov_len = len;
+    st->dq_end = pos + len;
+    return 0;
+}
+
 /* ------------------------------------------------------ advance step */
 
 static int32_t advance(opal_convertor_t *conv, struct iovec *iov, uint32_t *out_size,
@@ -287,20 +500,108 @@ static int32_t advance(opal_convertor_t *conv, struct iovec *iov, uint32_t *out_
 {
     ompi_amd_ddt_t *prog = program_of(conv->pDesc, 0);
     if (!prog) return -1;
-    const int rc = unpack
-        ? ompi_amd_ddt_unpack_iov(prog, conv->count, conv->pBaseBuf, conv->bConverted,
-                                  (ompi_amd_iovec_t *)iov, out_size, max_data, conv_stream(conv))
-        : ompi_amd_ddt_pack_iov(prog, conv->count, conv->pBaseBuf, conv->bConverted,
-                                (ompi_amd_iovec_t *)iov, out_size, max_data, conv_stream(conv));
-    if (rc < 0) return -1;
-    /* synchronous unless the PML runs the convertor asynchronously and
-     * waits on its stream itself (CONVERTOR_CUDA_ASYNC, set only by a CUDA
-     * build's opal_cuda_set_copy_function_async) */
-    if (!(conv->flags & CONVERTOR_CUDA_ASYNC) && ompi_amd_stream_synchronize(conv_stream(conv)) != 0)
+    const size_t total = ompi_amd_ddt_size(prog) * conv->count;
+    size_t pos = conv->bConverted;
+    uint32_t used = 0;
+    conv_state *st = state_of(conv, 1);
+    if (!st) return -1;
+    const int defer = st->defer;
+    int direct = 0;  /* device fragments of this call not recorded: launched now */
+    *max_data = 0;
+    for (uint32_t i = 0; i < *out_size && pos < total; ++i) {
+        const size_t take = iov[i].iov_len < total - pos ? iov[i].iov_len : total - pos;
+        iov[i].iov_len = take;
+        used = i + 1;
+        if (0 == take) continue;
+        if (NULL == iov[i].iov_base) return -1;
+        if (on_device(st, iov[i].iov_base)) {
+            if (st->ndq && st->dq_end != pos && 0 != flush_dq(conv, st, prog, unpack)) return -1;
+            if (0 != record_dq(st, iov[i].iov_base, take, pos)) return -1;
+            direct = !defer;
+        } else {  /* a host fragment: through the page-locked window */
+            if (0 != state_window(st)) return -1;
+            for (size_t done = 0; done < take;) {
+                const size_t at = pos + done;
+                if (!unpack) {
+                    if (at < st->win_pos || at >= st->win_end) {
+                        const size_t n = total - at < WIN_BYTES ? total - at : WIN_BYTES;
+                        if (0 != fill_win(conv, st, prog, at, n)) return -1;
+                    }
+                    size_t m = st->win_end - at;
+                    if (m > take - done) m = take - done;
+                    memcpy((char *) iov[i].iov_base + done, st->win_host + (at - st->win_pos), m);
+                    done += m;
+                } else {
+                    if (st->win_end != at || st->win_end - st->win_pos == WIN_BYTES) {
+                        if (0 != flush_win(conv, st, prog)) return -1;
+                        st->win_pos = st->win_end = at;
+                    }
+                    size_t m = WIN_BYTES - (st->win_end - st->win_pos);
+                    if (m > take - done) m = take - done;
+                    memcpy(st->win_host + (st->win_end - st->win_pos), (char *) iov[i].iov_base + done, m);
+                    st->win_end += m;
+                    done += m;
+                }
+            }
+        }
+        pos += take;
+    }
+    if (pos < total) used = *out_size;
+    *out_size = used;
+    *max_data = pos - conv->bConverted;
+    conv->bConverted = pos;
+    const int complete = pos == total;
+    if ((direct || (complete && !defer)) && 0 != flush_dq(conv, st, prog, unpack)) return -1;
+    if (unpack && complete && 0 != flush_win(conv, st, prog)) return -1;
+    /* a launch of this call: synchronous unless the caller runs the
+     * convertor asynchronously and waits on its stream itself
+     * (CONVERTOR_CUDA_ASYNC: opal_cuda_set_copy_function_async in a CUDA
+     * build, opal_rocm_set_copy_function_async here) */
+    if (direct && !(conv->flags & CONVERTOR_CUDA_ASYNC) &&
+        0 != ompi_amd_stream_synchronize(stream_of(conv, st)))
         return -1;
-    conv->bConverted += *max_data;
-    if (rc == 1) conv->flags |= CONVERTOR_COMPLETED;
-    return rc;
+    if (complete) {
+        conv->flags |= CONVERTOR_COMPLETED;
+        if (!defer) state_drop(conv);
+    }
+    return complete ? 1 : 0;
+}
+
+int opal_rocm_set_copy_function_async(opal_convertor_t *convertor, void *stream)
+{
+    conv_state *st = state_of(convertor, 1);
+    if (!st) return -1;
+    convertor->flags |= CONVERTOR_CUDA_ASYNC;
+#if OPAL_CUDA_SUPPORT
+    convertor->stream = stream;
+#endif
+    st->stream = stream;
+    st->defer = 1;
+    return 0;
+}
+
+int opal_rocm_convertor_flush(opal_convertor_t *convertor)
+{
+    conv_state *st = state_of(convertor, 0);
+    ompi_amd_ddt_t *prog;
+    if (!st) return 0;
+    if (!(prog = program_of(convertor->pDesc, 0))) return -1;
+    const int unpack = !(convertor->flags & CONVERTOR_SEND);
+    if (0 != flush_dq(convertor, st, prog, unpack)) return -1;
+    if (unpack && 0 != flush_win(convertor, st, prog)) return -1;
+    return 0;
+}
+
+int opal_rocm_record_event(opal_convertor_t *convertor, void **event)
+{
+    conv_state *st = state_of(convertor, 0);
+    if (0 != opal_rocm_convertor_flush(convertor)) return -1;
+    return 0 == ompi_amd_event_record(event, stream_of(convertor, st)) ? 0 : -1;
+}
+
+void opal_rocm_convertor_release(opal_convertor_t *convertor)
+{
+    state_drop(convertor);
 }
 
 int32_t opal_rocm_pack(opal_convertor_t *convertor, struct iovec *iov, uint32_t *out_size,
@@ -348,6 +649,7 @@ static int device_buffer(const opal_convertor_t *c)
 int opal_rocm_convertor_select(opal_convertor_t *convertor)
 {
     const uint32_t f = convertor->flags;
+    if (g_nstates) state_drop(convertor);  /* a new conversion at this address */
     if ((f & (CONVERTOR_NO_OP | CONVERTOR_COMPLETED | CONVERTOR_SKIP_CUDA_INIT)) ||
         !(f & CONVERTOR_HOMOGENEOUS) || (f & CONVERTOR_WITH_CHECKSUM))
         return 0;
@@ -420,6 +722,8 @@ int32_t opal_rocm_set_position(opal_convertor_t *convertor, size_t *position)
 {
     const opal_datatype_t *dt = convertor->pDesc;
     size_t pos = *position;
+    /* recorded fragments and a gathered window belong to the old position */
+    if (0 != opal_rocm_convertor_flush(convertor)) return -1;
     if ((convertor->flags & CONVERTOR_SEND) && !(dt->flags & OPAL_DATATYPE_FLAG_CONTIGUOUS) &&
         dt->size > 0) {
         const size_t inst = pos / dt->size;

@@ -56,8 +56,13 @@ int opal_rocm_convertor_owns(const opal_convertor_t *convertor);
 int32_t opal_rocm_set_position(opal_convertor_t *convertor, size_t *position);
 
 /* convertor_advance_fct_t implementations: iov[0 .. *out_size) filled
- * (pack) or drained (unpack) from bConverted on in one kernel launch;
- * returns 1 complete, 0 more data pending, -1 error. */
+ * (pack) or drained (unpack) from bConverted on — device fragments in one
+ * kernel launch (or recorded, after opal_rocm_set_copy_function_async),
+ * host fragments through page-locked windows of up to 16 MiB of the stream
+ * (a send packs a window ahead and serves the next fragments from it; a
+ * receive gathers fragments and unpacks a window at a time, the last one
+ * before the call that completes the stream returns); returns 1 complete,
+ * 0 more data pending, -1 error. */
 int32_t opal_rocm_pack(opal_convertor_t *convertor, struct iovec *iov, uint32_t *out_size,
                        size_t *max_data);
 int32_t opal_rocm_unpack(opal_convertor_t *convertor, struct iovec *iov, uint32_t *out_size,
@@ -69,6 +74,27 @@ int32_t opal_rocm_unpack(opal_convertor_t *convertor, struct iovec *iov, uint32_
 int32_t opal_rocm_refuse(opal_convertor_t *convertor, struct iovec *iov, uint32_t *out_size,
                          size_t *max_data);
 #endif
+
+/* Asynchronous conversion (the ROCm counterpart of
+ * opal_cuda_set_copy_function_async, opal_datatype_cuda.c:216-219, which
+ * ob1 calls at pml_ob1_recvfrag.c:598 / pml_ob1_recvreq.c:868): sets
+ * CONVERTOR_CUDA_ASYNC and the stream, and from now on fAdvance records
+ * device fragments instead of launching them — the caller must flush
+ * (opal_rocm_record_event, the counterpart of common_cuda's
+ * mca_common_cuda_record_dtoh_event / _htod_event) before it reads a packed
+ * fragment or reuses a received one.  Host fragments stay synchronous.
+ * Valid until the convertor is prepared again. */
+int opal_rocm_set_copy_function_async(opal_convertor_t *convertor, void *stream);
+/* Launch what the convertor recorded (device fragments; a receive's
+ * gathered host window, waited for).  0 or -1. */
+int opal_rocm_convertor_flush(opal_convertor_t *convertor);
+/* Flush, then mark the point on the convertor's stream: *event (NULL:
+ * created) completes once every fragment converted so far is in place
+ * (ompi_amd_event_query / _synchronize / _destroy).  0 or -1. */
+int opal_rocm_record_event(opal_convertor_t *convertor, void **event);
+/* Forget the convertor's state (its windows return to a pool); prepare
+ * does it by itself — for a convertor destroyed before it completed. */
+void opal_rocm_convertor_release(opal_convertor_t *convertor);
 
 /* Device programs cached per datatype description (tests / finalize). */
 int opal_rocm_program_cache_size(void);

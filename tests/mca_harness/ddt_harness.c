@@ -353,6 +353,47 @@ static int test_type(const spec_t *s)
                        s->chunks[ci], niov, why, bad);
                 ++fails;
             }
+            /* host fragments (btl/sm's shared-memory fragments): the
+             * page-locked windows, never a kernel on host memory */
+            memset(got, 0, total);
+            opal_convertor_prepare_for_send(&c, &dt, s->count, dtyped);
+            if (drive(&c, got, total, s->chunks[ci], niov, 0, why, sizeof(why)) || memcmp(got, exp, total)) {
+                printf("FAIL %s pack into host fragments, chunk %zu x%u: %s\n", s->name, s->chunks[ci],
+                       niov, why);
+                ++fails;
+            }
+            harness_dev_copy_in(dtyped2, bg, tbytes);
+            opal_convertor_prepare_for_recv(&c, &dt, s->count, dtyped2);
+            if (drive(&c, exp, total, s->chunks[ci], niov, 1, why, sizeof(why)) ||
+                harness_dev_copy_back(tgot, dtyped2, tbytes) || memcmp(tgot, texp, tbytes)) {
+                printf("FAIL %s unpack from host fragments, chunk %zu x%u: %s\n", s->name,
+                       s->chunks[ci], niov, why);
+                ++fails;
+            }
+            /* asynchronous conversion: device fragments recorded, one launch
+             * at the event (opal_rocm_set_copy_function_async / _record_event) */
+            for (int dir = 0; dir < 2; ++dir) {
+                void *ev = NULL;
+                harness_dev_copy_in(dtyped2, bg, tbytes);
+                harness_dev_copy_in(dpack, bg, total);
+                if (dir == 0) opal_convertor_prepare_for_send(&c, &dt, s->count, dtyped);
+                else opal_convertor_prepare_for_recv(&c, &dt, s->count, dtyped2);
+                if (opal_rocm_set_copy_function_async(&c, NULL) != 0 ||
+                    drive(&c, dir == 0 ? dpack : dexp, total, s->chunks[ci], niov, dir, why, sizeof(why)) ||
+                    opal_rocm_record_event(&c, &ev) != 0 || ompi_amd_event_synchronize(ev) != 0) {
+                    printf("FAIL %s deferred %s chunk %zu x%u: %s\n", s->name, dir ? "unpack" : "pack",
+                           s->chunks[ci], niov, why);
+                    ++fails;
+                } else if (dir == 0 ? (harness_dev_copy_back(got, dpack, total) || memcmp(got, exp, total))
+                                    : (harness_dev_copy_back(tgot, dtyped2, tbytes) ||
+                                       memcmp(tgot, texp, tbytes))) {
+                    printf("FAIL %s deferred %s chunk %zu x%u: bytes differ\n", s->name,
+                           dir ? "unpack" : "pack", s->chunks[ci], niov);
+                    ++fails;
+                }
+                ompi_amd_event_destroy(ev);
+                opal_rocm_convertor_release(&c);
+            }
         }
     }
     harness_dev_free(dtyped);
@@ -526,6 +567,109 @@ static int test_position(const spec_t *s)
     return fails;
 }
 
+/* HARNESS_BENCH=1: the per-fragment cost of the seam measured from C, the
+ * way a PML drives it — 64 KiB fragments (ob1's default max send size)
+ * over a 256 MiB packed stream of MPI_Type_vector(blocklen 8 doubles,
+ * stride 16): one fAdvance per fragment, synchronous (device fragments),
+ * deferred (opal_rocm_set_copy_function_async + one record_event), and host
+ * fragments (pageable memory, btl/sm-style); against one fAdvance over the
+ * whole fragment train (iov_batch).  One JSON line per (mode, direction). */
+#include <time.h>
+static double now_s(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double) t.tv_sec + 1e-9 * (double) t.tv_nsec;
+}
+
+static int bench(void)
+{
+    const size_t frag = 64 << 10, total = (size_t) 256 << 20, nfrag = total / frag;
+    const size_t nblk = total / 64, tbytes = nblk * 128;
+    dt_elem_desc_t desc[2];
+    opal_datatype_t dt;
+    memset(desc, 0, sizeof(desc));
+    desc[0].elem.common.type = OPAL_DATATYPE_FLOAT8;
+    desc[0].elem.common.flags = OPAL_DATATYPE_FLAG_DATA;
+    desc[0].elem.count = (uint32_t) nblk;
+    desc[0].elem.blocklen = 8;
+    desc[0].elem.extent = 128;
+    desc[1].end_loop.common.type = OPAL_DATATYPE_END_LOOP;
+    desc[1].end_loop.items = 1;
+    desc[1].end_loop.size = total;
+    memset(&dt, 0, sizeof(dt));
+    dt.size = total;
+    dt.ub = dt.true_ub = (ptrdiff_t) tbytes;
+    dt.opt_desc.used = dt.opt_desc.length = 2;
+    dt.opt_desc.desc = desc;
+    void *dtyped = NULL, *dpack = NULL;
+    char *zero = calloc(tbytes, 1), *hpack = malloc(total);
+    struct iovec *all = malloc(nfrag * sizeof(*all));
+    if (harness_dev_alloc_copy(&dtyped, zero, tbytes) || harness_dev_alloc_copy(&dpack, zero, total)) {
+        printf("FAIL bench alloc\n");
+        return 1;
+    }
+    memset(hpack, 1, total);
+    const char *modes[] = {"per_fragment_sync", "per_fragment_deferred", "host_fragments", "iov_batch"};
+    for (int m = 0; m < 4; ++m)
+        for (int dir = 0; dir < 2; ++dir) {
+            double best = 1e30;
+            for (int rep = 0; rep < 3; ++rep) {
+                opal_convertor_t c;
+                char *base = m == 2 ? hpack : (char *) dpack;
+                void *ev = NULL;
+                if (dir == 0) opal_convertor_prepare_for_send(&c, &dt, 1, dtyped);
+                else opal_convertor_prepare_for_recv(&c, &dt, 1, dtyped);
+                if (m == 1) opal_rocm_set_copy_function_async(&c, NULL);
+                ompi_amd_stream_synchronize(NULL);
+                const double t0 = now_s();
+                if (m == 3) {
+                    for (size_t k = 0; k < nfrag; ++k) {
+                        all[k].iov_base = base + k * frag;
+                        all[k].iov_len = frag;
+                    }
+                    uint32_t n = (uint32_t) nfrag;
+                    size_t max = total;
+                    if ((dir ? opal_convertor_unpack(&c, all, &n, &max) : opal_convertor_pack(&c, all, &n, &max)) != 1)
+                        printf("FAIL bench iov_batch\n");
+                } else {
+                    for (size_t k = 0; k < nfrag; ++k) {
+                        struct iovec v = {base + k * frag, frag};
+                        uint32_t n = 1;
+                        size_t max = frag;
+                        if ((dir ? opal_convertor_unpack(&c, &v, &n, &max) : opal_convertor_pack(&c, &v, &n, &max)) < 0) {
+                            printf("FAIL bench fragment %zu\n", k);
+                            break;
+                        }
+                    }
+                    if (m == 1) {
+                        opal_rocm_record_event(&c, &ev);
+                        ompi_amd_event_synchronize(ev);
+                        ompi_amd_event_destroy(ev);
+                    }
+                }
+                ompi_amd_stream_synchronize(NULL);
+                const double t = now_s() - t0;
+                if (t < best) best = t;
+                opal_rocm_convertor_release(&c);
+            }
+            /* algorithmic bytes: the packed stream read / written once and
+             * its typed span (2x, blocks 64 of every 128 B) the other way */
+            printf("{\"bench\": \"ddt_fragments\", \"mode\": \"%s\", \"dir\": \"%s\", "
+                   "\"fragments\": %zu, \"fragment_bytes\": %zu, \"seconds\": %.6f, "
+                   "\"us_per_fragment\": %.3f, \"packed_GBps\": %.1f, \"algorithmic_GBps\": %.1f, "
+                   "\"cuda_support_build\": %d}\n",
+                   modes[m], dir ? "unpack" : "pack", nfrag, frag, best, 1e6 * best / (double) nfrag,
+                   (double) total / best / 1e9, 2.0 * (double) total / best / 1e9, OPAL_CUDA_SUPPORT);
+        }
+    harness_dev_free(dtyped);
+    harness_dev_free(dpack);
+    free(zero);
+    free(hpack);
+    free(all);
+    return 0;
+}
+
 int main(void)
 {
     static const struct { int type; size_t size; } sizes[] = {
@@ -564,6 +708,7 @@ int main(void)
         return 1;
     }
 #endif
+    if (getenv("HARNESS_BENCH") && atoi(getenv("HARNESS_BENCH"))) return bench();
     {   /* a host buffer is never offloaded (either build) */
         static char host_buf[64];
         opal_datatype_t dt;
