@@ -567,6 +567,41 @@ static int32_t advance(opal_convertor_t *conv, struct iovec *iov, uint32_t *out_
     return complete ? 1 : 0;
 }
 
+/* A whole typed buffer to / from a packed device buffer in one launch
+ * (pml/rocm's non-contiguous device messages) */
+static int whole(const opal_datatype_t *dt, size_t count, void *typed, void *packed, void *stream,
+                 int unpack)
+{
+    ompi_amd_ddt_t *prog;
+    if (0 == count || 0 == dt->size) return 0;
+    if (!ompi_amd_is_device_pointer((const char *) typed + dt->true_lb) ||
+        !ompi_amd_is_device_pointer(packed) || !(prog = program_of(dt, 1)))
+        return 1;
+    size_t done = 0;
+    const int rc = unpack
+        ? ompi_amd_ddt_unpack(prog, count, packed, typed, 0, dt->size * count, &done, stream)
+        : ompi_amd_ddt_pack(prog, count, typed, packed, 0, dt->size * count, &done, stream);
+    if (rc < 0 || done != dt->size * count || 0 != ompi_amd_stream_synchronize(stream)) return -1;
+    return 0;
+}
+
+int opal_rocm_device_program(const opal_datatype_t *dt)
+{
+    return NULL != program_of(dt, 1);
+}
+
+int opal_rocm_pack_device(const opal_datatype_t *dt, size_t count, const void *src, void *packed,
+                          void *stream)
+{
+    return whole(dt, count, (void *) src, packed, stream, 0);
+}
+
+int opal_rocm_unpack_device(const opal_datatype_t *dt, size_t count, const void *packed, void *dst,
+                            void *stream)
+{
+    return whole(dt, count, dst, (void *) packed, stream, 1);
+}
+
 int opal_rocm_set_copy_function_async(opal_convertor_t *convertor, void *stream)
 {
     conv_state *st = state_of(convertor, 1);

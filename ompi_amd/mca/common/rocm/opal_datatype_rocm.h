@@ -96,6 +96,18 @@ int opal_rocm_record_event(opal_convertor_t *convertor, void **event);
  * does it by itself — for a convertor destroyed before it completed. */
 void opal_rocm_convertor_release(opal_convertor_t *convertor);
 
+/* count elements of dt at src (device memory) packed into the device
+ * buffer `packed` (dt->size * count bytes), or unpacked from it into dst:
+ * one kernel launch, complete on return.  0 done, 1 not offloadable (host
+ * memory, or no device program: the caller keeps its host path), -1 error.
+ * pml/rocm's non-contiguous device messages (no host round trip). */
+int opal_rocm_pack_device(const opal_datatype_t *dt, size_t count, const void *src, void *packed,
+                          void *stream);
+/* 1 when dt has a device program (the two calls above can take it) */
+int opal_rocm_device_program(const opal_datatype_t *dt);
+int opal_rocm_unpack_device(const opal_datatype_t *dt, size_t count, const void *packed, void *dst,
+                            void *stream);
+
 /* Device programs cached per datatype description (tests / finalize). */
 int opal_rocm_program_cache_size(void);
 void opal_rocm_program_cache_clear(void);

@@ -208,16 +208,90 @@ static size_t type_bytes(struct ompi_datatype_t *dtype, size_t count)
     return size * count;
 }
 
+/* common/rocm (opal_datatype_rocm.h): a device typed buffer packed into /
+ * unpacked from a packed device buffer by one kernel; 1 when the datatype
+ * has no device program.  An ompi_datatype_t begins with its
+ * opal_datatype_t (ompi/datatype/ompi_datatype.h:70-71). */
+struct opal_datatype_t;
+int opal_rocm_pack_device(const struct opal_datatype_t *dt, size_t count, const void *src,
+                          void *packed, void *stream);
+int opal_rocm_unpack_device(const struct opal_datatype_t *dt, size_t count, const void *packed,
+                            void *dst, void *stream);
+int opal_rocm_device_program(const struct opal_datatype_t *dt);
+#define OPAL_DT(d) ((const struct opal_datatype_t *) (d))
+
+/* Device packing buffers, reused (a hipMalloc per message would cost more
+ * than the pack): the smallest free one that fits, else a new one; at most
+ * DEV_POOL kept. */
+#define DEV_POOL 8
+static struct { void *p; size_t cap; } dev_pool[DEV_POOL];
+static int dev_pool_n;
+static opal_mutex_t dev_pool_lock = OPAL_MUTEX_STATIC_INIT;
+
+static void *dev_stage_take(size_t bytes)
+{
+    void *p = NULL;
+    int best = -1;
+    OPAL_THREAD_LOCK(&dev_pool_lock);
+    for (int i = 0; i < dev_pool_n; ++i)
+        if (dev_pool[i].cap >= bytes && (best < 0 || dev_pool[i].cap < dev_pool[best].cap)) best = i;
+    if (best >= 0) {
+        p = dev_pool[best].p;
+        dev_pool[best] = dev_pool[--dev_pool_n];
+    }
+    OPAL_THREAD_UNLOCK(&dev_pool_lock);
+    if (NULL == p && OMPI_AMD_SUCCESS != ompi_amd_device_alloc(&p, bytes)) p = NULL;
+    return p;
+}
+
+/* back to the pool; `bytes` (what the request needed) is a lower bound of
+ * the buffer's capacity */
+static void dev_stage_put(void *p, size_t bytes)
+{
+    if (NULL == p) return;
+    OPAL_THREAD_LOCK(&dev_pool_lock);
+    if (dev_pool_n < DEV_POOL) {
+        dev_pool[dev_pool_n].p = p;
+        dev_pool[dev_pool_n++].cap = bytes;
+        p = NULL;
+    }
+    OPAL_THREAD_UNLOCK(&dev_pool_lock);
+    (void) ompi_amd_device_free(p);
+}
+
+static void stage_free(mca_pml_rocm_request_t *r)
+{
+    if (r->stage_dev) dev_stage_put(r->stage, r->bytes);
+    else free(r->stage);
+    r->stage = NULL;
+    r->stage_dev = 0;
+}
+
 /* what the library gets for the user's buffer: the buffer itself when its
  * layout is contiguous (host or device: the library stages host memory in
- * its own pooled device buffers), else a host buffer with the packed bytes
- * (packed here for a send) */
+ * its own pooled device buffers); a device buffer of a non-contiguous type
+ * is packed on the device into a pooled device buffer (one kernel: no host
+ * round trip — the reference packs device data through the convertor in
+ * the send path, pml_ob1_cuda.c:56-101); a host one is packed on the host */
 static int stage_for(mca_pml_rocm_request_t *r, int fill)
 {
     r->bytes = type_bytes(r->dtype, r->count);
     r->stage = NULL;
+    r->stage_dev = 0;
     if (0 == r->bytes || ompi_datatype_is_contiguous_memory_layout(r->dtype, (int) r->count))
         return OMPI_SUCCESS;
+    if (ompi_amd_is_device_pointer(r->buf) && opal_rocm_device_program(OPAL_DT(r->dtype))) {
+        void *d = dev_stage_take(r->bytes);
+        const int rc = NULL == d ? 1 : fill ? opal_rocm_pack_device(OPAL_DT(r->dtype), r->count,
+                                                                   r->buf, d, NULL) : 0;
+        if (0 == rc) {
+            r->stage = d;
+            r->stage_dev = 1;
+            return OMPI_SUCCESS;
+        }
+        dev_stage_put(d, r->bytes);
+        if (rc < 0) return OMPI_ERROR;
+    }
     r->stage = malloc(r->bytes);
     if (NULL == r->stage) return OMPI_ERR_OUT_OF_RESOURCE;
     if (fill && MPI_SUCCESS != ompi_datatype_sndrcv(r->buf, (int) r->count, r->dtype, r->stage,
@@ -236,6 +310,11 @@ static int unstage_recv(mca_pml_rocm_request_t *r, size_t got)
     size_t size = 0;
     if (NULL == r->stage || 0 == got) return OMPI_SUCCESS;
     (void) ompi_datatype_type_size(r->dtype, &size);
+    if (r->stage_dev)
+        return 0 == opal_rocm_unpack_device(OPAL_DT(r->dtype), size ? got / size : 0, r->stage,
+                                            r->buf, NULL)
+                   ? OMPI_SUCCESS
+                   : OMPI_ERROR;
     return MPI_SUCCESS == ompi_datatype_sndrcv(r->stage, (int) got, MPI_BYTE, r->buf,
                                                (int) (size ? got / size : 0), r->dtype)
                ? OMPI_SUCCESS
@@ -293,8 +372,7 @@ static int finish(mca_pml_rocm_request_t *r, int rc, const ompi_amd_status_t *s)
     else r->super.req_status.MPI_ERROR = err;
     (void) ompi_amd_p2p_free(r->lib);
     r->lib = NULL;
-    free(r->stage);
-    r->stage = NULL;
+    stage_free(r);
     return err;
 }
 
@@ -381,8 +459,7 @@ static int post(mca_pml_rocm_request_t *r)
                             MPI_ANY_TAG == r->tag ? OMPI_AMD_ANY_TAG : r->tag, NULL, &r->lib);
     }
     if (OMPI_AMD_SUCCESS != rc) {
-        free(r->stage);
-        r->stage = NULL;
+        stage_free(r);
         return rocm_err(rc);
     }
     r->super.req_complete = REQUEST_PENDING;
@@ -559,7 +636,7 @@ static int rocm_send(const void *buf, size_t count, struct ompi_datatype_t *dtyp
         rc = rocm_err(wait_lib(lib, &s));
         (void) ompi_amd_p2p_free(lib);
     }
-    free(r.stage);
+    stage_free(&r);
     return rc;
 }
 
@@ -586,7 +663,7 @@ static int rocm_recv(void *buf, size_t count, struct ompi_datatype_t *dtype, int
         (void) ompi_amd_p2p_free(lib);
     }
     if (OMPI_SUCCESS == rc) rc = unstage_recv(&r, s.bytes);
-    free(r.stage);
+    stage_free(&r);
     fill_status(status, &s, rc);
     return rc;
 }

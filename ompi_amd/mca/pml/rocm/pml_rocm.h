@@ -67,9 +67,12 @@ typedef struct mca_pml_rocm_request_t {
     struct ompi_datatype_t *dtype;
     int peer, tag, mode;
     struct ompi_communicator_t *comm;
-    /* host packing of a non-contiguous datatype (NULL: the user buffer
-     * itself goes to the library, host or device) */
+    /* packing of a non-contiguous datatype (NULL: the user buffer itself
+     * goes to the library, host or device): a device buffer from the
+     * component's pool, packed / unpacked by one kernel (stage_dev), or
+     * host memory packed on the host */
     void *stage;
+    int stage_dev;
     size_t bytes;
     struct mca_pml_rocm_request_t *next_active;
 } mca_pml_rocm_request_t;

@@ -50,4 +50,33 @@ int32_t ompi_datatype_sndrcv(const void *sbuf, int32_t scount, const ompi_dataty
     }
     return 0;
 }
+
+/* common/rocm's whole-buffer device pack / unpack (opal_datatype_rocm.c)
+ * over the stand-in types, for the pml harness: one 2-D device copy (a
+ * stand-in type is `size` data bytes every `size` or 2 * `size` bytes);
+ * harness_device_packs counts the calls so a test can see the path taken.
+ * The real implementation is exercised by the ddt harness. */
+int harness_device_packs;
+struct opal_datatype_t;
+int opal_rocm_device_program(const struct opal_datatype_t *dt) { return dt != NULL; }
+static int whole2d(const ompi_datatype_t *d, size_t count, void *typed, void *packed, int unpack)
+{
+    const size_t pitch = d->contiguous ? d->size : 2 * d->size;
+    hipError_t e;
+    if (count == 0) return 0;
+    ++harness_device_packs;
+    e = unpack ? hipMemcpy2D(typed, pitch, packed, d->size, d->size, count, hipMemcpyDeviceToDevice)
+               : hipMemcpy2D(packed, d->size, typed, pitch, d->size, count, hipMemcpyDeviceToDevice);
+    return e == hipSuccess ? 0 : -1;
+}
+int opal_rocm_pack_device(const struct opal_datatype_t *dt, size_t count, const void *src,
+                          void *packed, void *stream)
+{
+    return whole2d((const ompi_datatype_t *) dt, count, (void *) src, packed, 0);
+}
+int opal_rocm_unpack_device(const struct opal_datatype_t *dt, size_t count, const void *packed,
+                            void *dst, void *stream)
+{
+    return whole2d((const ompi_datatype_t *) dt, count, dst, (void *) packed, 1);
+}
 #endif

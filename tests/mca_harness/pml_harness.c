@@ -245,6 +245,40 @@ int main(int argc, char **argv)
         free(h);
         free(t);
     }
+    /* 3b. non-contiguous device buffers on both sides: packed and unpacked
+     * on the device (common/rocm), no host copy of the payload; the
+     * receive buffer's gaps survive */
+    {
+        extern int harness_device_packs;
+        const size_t n = 70001;
+        int *h = malloc(n * 8), *t = malloc(n * 8);
+        void *ds, *dr;
+        ompi_request_t *rs = NULL, *rr = NULL;
+        const int packs0 = harness_device_packs;
+        for (size_t i = 0; i < n; ++i) {
+            h[2 * i] = g_rank * 104729 + (int) i;
+            h[2 * i + 1] = -7;
+        }
+        for (size_t i = 0; i < 2 * n; ++i) t[i] = -1;
+        CHECK(harness_dev_alloc_copy(&ds, h, n * 8) == 0 && harness_dev_alloc_copy(&dr, t, n * 8) == 0,
+              "device gap buffers");
+        CHECK(mca_pml.pml_irecv(dr, n, &gap4, left, 10, &comm, &rr) == OMPI_SUCCESS, "irecv device gap type");
+        CHECK(mca_pml.pml_isend(ds, n, &gap4, right, 10, MCA_PML_BASE_SEND_STANDARD, &comm, &rs) ==
+                  OMPI_SUCCESS, "isend device gap type");
+        wait_req(rr);
+        wait_req(rs);
+        CHECK(harness_dev_copy_back(t, dr, n * 8) == 0, "copy back");
+        for (size_t i = 0; i < n; ++i) {
+            CHECK(t[2 * i] == left * 104729 + (int) i, "device packed element %zu", i);
+            CHECK(t[2 * i + 1] == -1, "device gap %zu overwritten", i);
+        }
+        CHECK(harness_device_packs - packs0 == 2, "device pack + unpack (%d)", harness_device_packs - packs0);
+        CHECK(rr->req_free(&rr) == OMPI_SUCCESS && rs->req_free(&rs) == OMPI_SUCCESS, "free");
+        harness_dev_free(ds);
+        harness_dev_free(dr);
+        free(h);
+        free(t);
+    }
     SECTION(4);
     /* 4. iprobe / probe, then the receive */
     {
