@@ -323,6 +323,49 @@ static int unstage_recv(mca_pml_rocm_request_t *r, size_t got)
 
 static void *lib_buf(mca_pml_rocm_request_t *r) { return NULL != r->stage ? r->stage : r->buf; }
 
+/* ------------------------------------------- the saved PML, device buffers */
+
+/* The saved PML (ob1) moves host memory only.  What pml/rocm leaves to it —
+ * system tags: the collectives' own messages (coll/base algorithms, libnbc
+ * schedules, every collective coll/rocm does not offload) — can still name
+ * device buffers; such a message runs on a host copy of its typed span: a
+ * send copies the span out before the saved PML sees it, a receive gets a
+ * host span (pre-filled, so the type's gaps keep their bytes) and copies it
+ * back when it completes — coll/cuda's staging (coll_cuda_allreduce.c:
+ * 42-72) per message; the reference's ob1 moves device memory itself
+ * (pml_ob1_cuda.c:56-101). */
+static int on_device(const void *buf, size_t count, struct ompi_datatype_t *dtype)
+{
+    ptrdiff_t tlb = 0, text = 0;
+    if (0 == count || NULL == buf) return 0;
+    (void) ompi_datatype_get_true_extent(dtype, &tlb, &text);
+    return ompi_amd_is_device_pointer((const char *) buf + tlb);
+}
+
+/* r->hspan: the host copy of r->buf's typed span (filled from the device) */
+static int host_span(mca_pml_rocm_request_t *r)
+{
+    ptrdiff_t lb, ext, tlb, text;
+    (void) ompi_datatype_get_extent(r->dtype, &lb, &ext);
+    (void) ompi_datatype_get_true_extent(r->dtype, &tlb, &text);
+    r->hbytes = (r->count - 1) * (size_t) ext + (size_t) text;
+    r->hgap = tlb;
+    if (NULL == r->hspan && NULL == (r->hspan = malloc(r->hbytes ? r->hbytes : 1)))
+        return OMPI_ERR_OUT_OF_RESOURCE;
+    return OMPI_AMD_SUCCESS == ompi_amd_memcpy(r->hspan, (char *) r->buf + tlb, r->hbytes) ? OMPI_SUCCESS
+                                                                                       : OMPI_ERROR;
+}
+
+static void *host_base(const mca_pml_rocm_request_t *r) { return r->hspan - r->hgap; }
+
+/* a received host span back into the device buffer */
+static int host_span_back(const mca_pml_rocm_request_t *r)
+{
+    return OMPI_AMD_SUCCESS == ompi_amd_memcpy((char *) r->buf + r->hgap, r->hspan, r->hbytes)
+               ? OMPI_SUCCESS
+               : OMPI_ERROR;
+}
+
 /* Wait for a library request without a time limit, driving opal_progress
  * (other PML traffic, e.g. the system-tag messages of a collective the peer
  * is inside, must keep moving: ob1's blocking calls do the same). */
@@ -376,6 +419,25 @@ static int finish(mca_pml_rocm_request_t *r, int rc, const ompi_amd_status_t *s)
     return err;
 }
 
+/* the saved PML completed a request of a device buffer: its status, the
+ * received span back to the device; a persistent one keeps both for the
+ * next start */
+static void finish_inner(mca_pml_rocm_request_t *r)
+{
+    int err = r->inner->req_status.MPI_ERROR;
+    if (OMPI_SUCCESS == err && !r->is_send) err = host_span_back(r);
+    r->super.req_status = r->inner->req_status;
+    r->super.req_status.MPI_ERROR = err;
+    if (r->super.req_persistent) {
+        r->inner->req_state = OMPI_REQUEST_INACTIVE;
+    } else {
+        (void) ompi_request_free(&r->inner);
+        r->inner = NULL;
+        free(r->hspan);
+        r->hspan = NULL;
+    }
+}
+
 static int rocm_progress(void)
 {
     mca_pml_rocm_request_t **pp, *done = NULL;
@@ -387,6 +449,17 @@ static int rocm_progress(void)
         mca_pml_rocm_request_t *r = *pp;
         ompi_amd_status_t s = {0, 0, 0, 0};
         int fin = 0;
+        if (NULL != r->inner) {  /* a device buffer on the saved PML */
+            if (REQUEST_COMPLETE(r->inner)) {
+                finish_inner(r);
+                *pp = r->next_active;
+                r->next_active = done;
+                done = r;
+            } else {
+                pp = &r->next_active;
+            }
+            continue;
+        }
         const int rc = ompi_amd_p2p_test(r->lib, &fin, &s);
         if (OMPI_AMD_SUCCESS != rc || fin) {
             (void) finish(r, rc, &s);
@@ -479,6 +552,16 @@ static int rocm_start_req(size_t count, ompi_request_t **requests)
         if (NULL == r) continue;
         if (OMPI_REQUEST_ACTIVE == r->super.req_state && !REQUEST_COMPLETE(&r->super))
             return OMPI_ERR_REQUEST;
+        if (NULL != r->inner) {  /* the saved PML's request on the host span */
+            rc = host_span(r);  /* this start's payload / the receive's gap bytes */
+            if (OMPI_SUCCESS == rc) rc = r->inner->req_start(1, &r->inner);
+            if (OMPI_SUCCESS != rc) return rc;
+            r->super.req_complete = REQUEST_PENDING;
+            r->super.req_state = OMPI_REQUEST_ACTIVE;
+            r->super.req_status.MPI_ERROR = OMPI_SUCCESS;
+            link_active(r);
+            continue;
+        }
         rc = post(r);
         if (OMPI_SUCCESS != rc) return rc;
     }
@@ -497,6 +580,13 @@ static int rocm_free_req(ompi_request_t **rptr)
         ompi_amd_status_t s = {0, 0, 0, 0};
         rc = finish(r, wait_lib(r->lib, &s), &s);
     }
+    if (NULL != r->inner) {  /* the host span must outlive the saved PML's transfer */
+        while (OMPI_REQUEST_ACTIVE == r->inner->req_state && !REQUEST_COMPLETE(r->inner)) opal_progress();
+        (void) ompi_request_free(&r->inner);
+        r->inner = NULL;
+    }
+    free(r->hspan);
+    r->hspan = NULL;
     OMPI_REQUEST_FINI(&r->super);
     OBJ_RELEASE(r);
     *rptr = MPI_REQUEST_NULL;
@@ -512,6 +602,8 @@ static void rocm_request_construct(mca_pml_rocm_request_t *r)
     r->super.req_cancel = NULL;
     r->lib = NULL;
     r->stage = NULL;
+    r->inner = NULL;
+    r->hspan = NULL;
     r->next_active = NULL;
 }
 
@@ -536,6 +628,46 @@ static mca_pml_rocm_request_t *new_req(int is_send, void *buf, size_t count,
     return r;
 }
 
+/* A device-buffer operation on the saved PML through the host span: an
+ * active request of ours around the saved PML's (nonblocking), or a
+ * persistent one whose starts refill the span and start it. */
+static int saved_device_op(int is_send, void *buf, size_t count, struct ompi_datatype_t *dtype,
+                           int peer, int tag, int mode, struct ompi_communicator_t *comm,
+                           bool persistent, struct ompi_request_t **request)
+{
+    mca_pml_rocm_request_t *r = new_req(is_send, buf, count, dtype, peer, tag, mode, comm, persistent);
+    int rc;
+    if (NULL == r) return OMPI_ERR_OUT_OF_RESOURCE;
+    rc = host_span(r);
+    if (OMPI_SUCCESS == rc) {
+        void *h = host_base(r);
+        if (is_send)
+            rc = persistent ? mca_pml_rocm_host.pml_isend_init(h, count, dtype, peer, tag,
+                                                              (mca_pml_base_send_mode_t) mode, comm,
+                                                              &r->inner)
+                            : mca_pml_rocm_host.pml_isend(h, count, dtype, peer, tag,
+                                                         (mca_pml_base_send_mode_t) mode, comm, &r->inner);
+        else
+            rc = persistent ? mca_pml_rocm_host.pml_irecv_init(h, count, dtype, peer, tag, comm, &r->inner)
+                            : mca_pml_rocm_host.pml_irecv(h, count, dtype, peer, tag, comm, &r->inner);
+    }
+    if (OMPI_SUCCESS != rc) {  /* the saved PML refused: nothing of it to free */
+        r->inner = NULL;
+        free(r->hspan);
+        r->hspan = NULL;
+        OBJ_RELEASE(r);
+        return rc;
+    }
+    if (!persistent) {
+        r->super.req_complete = REQUEST_PENDING;
+        r->super.req_state = OMPI_REQUEST_ACTIVE;
+        r->super.req_status.MPI_ERROR = OMPI_SUCCESS;
+        link_active(r);
+    }
+    *request = &r->super;
+    return OMPI_SUCCESS;
+}
+
 /* ------------------------------------------------------------- pml entry points */
 
 static int rocm_isend(const void *buf, size_t count, struct ompi_datatype_t *dtype, int dst, int tag,
@@ -544,8 +676,12 @@ static int rocm_isend(const void *buf, size_t count, struct ompi_datatype_t *dty
 {
     mca_pml_rocm_request_t *r;
     int rc;
-    if (NULL == takes_buf(comm, tag, dst, buf, count))
+    if (NULL == takes_buf(comm, tag, dst, buf, count)) {
+        if (on_device(buf, count, dtype))
+            return saved_device_op(1, (void *) buf, count, dtype, dst, tag, (int) mode, comm, false,
+                                   request);
         return mca_pml_rocm_host.pml_isend(buf, count, dtype, dst, tag, mode, comm, request);
+    }
     r = new_req(1, (void *) buf, count, dtype, dst, tag, (int) mode, comm, false);
     if (NULL == r) return OMPI_ERR_OUT_OF_RESOURCE;
     rc = post(r);
@@ -562,8 +698,11 @@ static int rocm_irecv(void *buf, size_t count, struct ompi_datatype_t *dtype, in
 {
     mca_pml_rocm_request_t *r;
     int rc;
-    if (NULL == takes_buf(comm, tag, src, buf, count))
+    if (NULL == takes_buf(comm, tag, src, buf, count)) {
+        if (on_device(buf, count, dtype))
+            return saved_device_op(0, buf, count, dtype, src, tag, 0, comm, false, request);
         return mca_pml_rocm_host.pml_irecv(buf, count, dtype, src, tag, comm, request);
+    }
     r = new_req(0, buf, count, dtype, src, tag, 0, comm, false);
     if (NULL == r) return OMPI_ERR_OUT_OF_RESOURCE;
     rc = post(r);
@@ -580,8 +719,12 @@ static int rocm_isend_init(const void *buf, size_t count, struct ompi_datatype_t
                            struct ompi_request_t **request)
 {
     mca_pml_rocm_request_t *r;
-    if (NULL == takes_buf(comm, tag, dst, buf, count))
+    if (NULL == takes_buf(comm, tag, dst, buf, count)) {
+        if (on_device(buf, count, dtype))
+            return saved_device_op(1, (void *) buf, count, dtype, dst, tag, (int) mode, comm, true,
+                                   request);
         return mca_pml_rocm_host.pml_isend_init(buf, count, dtype, dst, tag, mode, comm, request);
+    }
     r = new_req(1, (void *) buf, count, dtype, dst, tag, (int) mode, comm, true);
     if (NULL == r) return OMPI_ERR_OUT_OF_RESOURCE;
     *request = &r->super;
@@ -592,8 +735,11 @@ static int rocm_irecv_init(void *buf, size_t count, struct ompi_datatype_t *dtyp
                            struct ompi_communicator_t *comm, struct ompi_request_t **request)
 {
     mca_pml_rocm_request_t *r;
-    if (NULL == takes_buf(comm, tag, src, buf, count))
+    if (NULL == takes_buf(comm, tag, src, buf, count)) {
+        if (on_device(buf, count, dtype))
+            return saved_device_op(0, buf, count, dtype, src, tag, 0, comm, true, request);
         return mca_pml_rocm_host.pml_irecv_init(buf, count, dtype, src, tag, comm, request);
+    }
     r = new_req(0, buf, count, dtype, src, tag, 0, comm, true);
     if (NULL == r) return OMPI_ERR_OUT_OF_RESOURCE;
     *request = &r->super;
@@ -624,6 +770,17 @@ static int rocm_send(const void *buf, size_t count, struct ompi_datatype_t *dtyp
     ompi_amd_p2p_request_t *lib = NULL;
     ompi_amd_status_t s = {0, 0, 0, 0};
     int rc;
+    if (NULL == dev && on_device(buf, count, dtype)) {  /* the saved PML on a host copy */
+        memset(&r, 0, sizeof(r));
+        r.buf = (void *) buf;
+        r.count = count;
+        r.dtype = dtype;
+        rc = host_span(&r);
+        if (OMPI_SUCCESS == rc)
+            rc = mca_pml_rocm_host.pml_send(host_base(&r), count, dtype, dst, tag, mode, comm);
+        free(r.hspan);
+        return rc;
+    }
     if (NULL == dev) return mca_pml_rocm_host.pml_send(buf, count, dtype, dst, tag, mode, comm);
     memset(&r, 0, sizeof(r));
     r.buf = (void *) buf;
@@ -648,6 +805,18 @@ static int rocm_recv(void *buf, size_t count, struct ompi_datatype_t *dtype, int
     ompi_amd_comm_t *dev = takes_buf(comm, tag, src, buf, count);
     ompi_amd_p2p_request_t *lib = NULL;
     int rc;
+    if (NULL == dev && on_device(buf, count, dtype)) {  /* the saved PML on a host copy */
+        memset(&r, 0, sizeof(r));
+        r.buf = buf;
+        r.count = count;
+        r.dtype = dtype;
+        rc = host_span(&r);
+        if (OMPI_SUCCESS == rc)
+            rc = mca_pml_rocm_host.pml_recv(host_base(&r), count, dtype, src, tag, comm, status);
+        if (OMPI_SUCCESS == rc) rc = host_span_back(&r);
+        free(r.hspan);
+        return rc;
+    }
     if (NULL == dev) return mca_pml_rocm_host.pml_recv(buf, count, dtype, src, tag, comm, status);
     memset(&r, 0, sizeof(r));
     r.buf = buf;

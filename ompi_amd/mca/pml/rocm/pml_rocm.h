@@ -74,6 +74,12 @@ typedef struct mca_pml_rocm_request_t {
     void *stage;
     int stage_dev;
     size_t bytes;
+    /* a device buffer on the saved PML: its request, and the host copy of
+     * the buffer's typed span it runs on (hspan - hgap = the typed base) */
+    ompi_request_t *inner;
+    char *hspan;
+    ptrdiff_t hgap;
+    size_t hbytes;
     struct mca_pml_rocm_request_t *next_active;
 } mca_pml_rocm_request_t;
 

@@ -9,6 +9,6 @@ OUT=${1:-$H/pml_harness}
 gcc -std=gnu11 -O1 -Wall -Wextra -Wno-unused-parameter -Wno-missing-field-initializers -DHARNESS_COLL \
     -I"$H/pml_include" -I"$H/coll_include" -I"$H/include" -I"$R/include" -I"$R/ompi_amd/mca/pml/rocm" \
     -I/opt/rocm/include \
-    "$R/ompi_amd/mca/pml/rocm/pml_rocm.c" "$H/pml_harness.c" "$H/dev_helpers.c" "$H/progress_stub.c" \
+    "$R/ompi_amd/mca/pml/rocm/pml_rocm.c" "$H/pml_harness.c" "$H/pml_saved.c" "$H/dev_helpers.c" "$H/progress_stub.c" \
     -L"$R/ompi_amd" -lompi_amd -L/opt/rocm/lib -lamdhip64 \
-    -Wl,-rpath,"$R/ompi_amd" -Wl,-rpath,/opt/rocm/lib -o "$OUT"
+    -Wl,-rpath,"$R/ompi_amd" -Wl,-rpath,/opt/rocm/lib -lrt -o "$OUT"

@@ -35,6 +35,7 @@
 #include "ompi/runtime/ompi_rte.h"
 #include "opal/runtime/opal_progress.h"
 #include "pml_rocm.h"
+#include "pml_saved.h"
 #include "ompi_amd.h"
 
 extern int harness_dev_alloc_copy(void **d, const void *h, size_t bytes);
@@ -64,24 +65,51 @@ static int ob1_calls;
 static ompi_request_t ob1_req;
 static int o_add_comm(struct ompi_communicator_t *c) { return OMPI_SUCCESS; }
 static int o_del_comm(struct ompi_communicator_t *c) { return OMPI_SUCCESS; }
+/* tags at or below HARNESS_SYS_TAG: a real host transport (pml_saved.c) */
+#define REAL(tag) ((tag) <= HARNESS_SYS_TAG)
 static int o_isend(const void *b, size_t n, struct ompi_datatype_t *d, int dst, int tag,
                    mca_pml_base_send_mode_t m, struct ompi_communicator_t *c, ompi_request_t **r)
-{ ob1_calls++; *r = &ob1_req; return OMPI_SUCCESS; }
+{
+    ob1_calls++;
+    *r = REAL(tag) ? harness_pml_saved_request(1, (void *) b, n, d, dst, tag, 0) : &ob1_req;
+    return OMPI_SUCCESS;
+}
 static int o_send(const void *b, size_t n, struct ompi_datatype_t *d, int dst, int tag,
                   mca_pml_base_send_mode_t m, struct ompi_communicator_t *c)
-{ ob1_calls++; return OMPI_SUCCESS; }
+{
+    ob1_calls++;
+    if (REAL(tag)) harness_pml_saved_send(b, n, d, dst, tag);
+    return OMPI_SUCCESS;
+}
 static int o_irecv(void *b, size_t n, struct ompi_datatype_t *d, int src, int tag,
                    struct ompi_communicator_t *c, ompi_request_t **r)
-{ ob1_calls++; *r = &ob1_req; return OMPI_SUCCESS; }
+{
+    ob1_calls++;
+    *r = REAL(tag) ? harness_pml_saved_request(0, b, n, d, src, tag, 0) : &ob1_req;
+    return OMPI_SUCCESS;
+}
 static int o_recv(void *b, size_t n, struct ompi_datatype_t *d, int src, int tag,
                   struct ompi_communicator_t *c, ompi_status_public_t *s)
-{ ob1_calls++; return OMPI_SUCCESS; }
+{
+    ob1_calls++;
+    if (REAL(tag))
+        while (!harness_pml_saved_try_recv(b, n, d, src, tag, s)) opal_progress();
+    return OMPI_SUCCESS;
+}
 static int o_isend_init(const void *b, size_t n, struct ompi_datatype_t *d, int dst, int tag,
                         mca_pml_base_send_mode_t m, struct ompi_communicator_t *c, ompi_request_t **r)
-{ ob1_calls++; *r = &ob1_req; return OMPI_SUCCESS; }
+{
+    ob1_calls++;
+    *r = REAL(tag) ? harness_pml_saved_request(1, (void *) b, n, d, dst, tag, 1) : &ob1_req;
+    return OMPI_SUCCESS;
+}
 static int o_irecv_init(void *b, size_t n, struct ompi_datatype_t *d, int src, int tag,
                         struct ompi_communicator_t *c, ompi_request_t **r)
-{ ob1_calls++; *r = &ob1_req; return OMPI_SUCCESS; }
+{
+    ob1_calls++;
+    *r = REAL(tag) ? harness_pml_saved_request(0, b, n, d, src, tag, 1) : &ob1_req;
+    return OMPI_SUCCESS;
+}
 static int o_start(size_t n, ompi_request_t **r) { ob1_calls++; return OMPI_SUCCESS; }
 static int o_iprobe(int s, int t, struct ompi_communicator_t *c, int *m, ompi_status_public_t *st)
 { ob1_calls++; *m = 0; return OMPI_SUCCESS; }
@@ -114,6 +142,7 @@ int main(int argc, char **argv)
     g_size = atoi(argv[3]);
     harness_proc_name.jobid = (unsigned) strtoul(argv[1], NULL, 16);
     comm = (ompi_communicator_t){g_rank, g_size, 5, 0, &local, NULL};
+    harness_pml_saved_init(argv[1], g_rank, g_size);
 
     /* the base selected "ob1" */
     memset(&ob1, 0, sizeof(ob1));
@@ -154,6 +183,7 @@ int main(int argc, char **argv)
         CHECK(mca_pml.pml_iprobe(MPI_ANY_SOURCE, MPI_ANY_TAG, &comm, &m, NULL) == OMPI_SUCCESS &&
                   ob1_calls == 2, "iprobe reaches ob1");
         CHECK(mca_pml.pml_del_comm(&comm) == OMPI_SUCCESS, "del_comm");
+        harness_pml_saved_fini();
         printf("ok\n");
         return 0;
     }
@@ -483,7 +513,83 @@ int main(int argc, char **argv)
         }
         mca_pml_rocm_component.host_path = 0;
     }
+    SECTION(11);
+    /* 11. system-tag traffic on device buffers (the collectives' own
+     * messages: coll/base, libnbc): it stays on ob1, which moves host
+     * memory only, through host copies of the typed spans — the transport
+     * behind ob1 fails the run on any device pointer.  Nonblocking,
+     * blocking, persistent (two starts), a gapped type whose receive gaps
+     * must survive. */
+    {
+        const size_t n = 20000;
+        const int tag = HARNESS_SYS_TAG - 5;
+        int *h = malloc(n * 8), *t = malloc(n * 8);
+        void *ds, *dr;
+        ompi_request_t *rs = NULL, *rr = NULL;
+        const int msgs0 = harness_saved_pml_msgs;
+        for (int form = 0; form < 3; ++form) {
+            for (int gap = 0; gap < 2; ++gap) {
+                ompi_datatype_t *d = gap ? &gap4 : &dint;
+                const int starts = form == 2 ? 2 : 1;
+                for (size_t i = 0; i < 2 * n; ++i) h[i] = (int) (g_rank * 7001 + i * 3 + form * 11 + gap);
+                for (size_t i = 0; i < 2 * n; ++i) t[i] = -1;
+                CHECK(harness_dev_alloc_copy(&ds, h, n * 8) == 0 && harness_dev_alloc_copy(&dr, t, n * 8) == 0,
+                      "device buffers");
+                if (form == 2) {
+                    CHECK(mca_pml.pml_irecv_init(dr, n, d, left, tag, &comm, &rr) == OMPI_SUCCESS &&
+                              mca_pml.pml_isend_init(ds, n, d, right, tag, MCA_PML_BASE_SEND_STANDARD, &comm,
+                                                     &rs) == OMPI_SUCCESS,
+                          "persistent system-tag requests");
+                }
+                for (int st = 0; st < starts; ++st) {
+                    if (st > 0) {  /* fresh data for the second start */
+                        for (size_t i = 0; i < 2 * n; ++i) h[i] += 1000;
+                        CHECK(harness_dev_copy_in(ds, h, n * 8) == 0, "refill");
+                    }
+                    if (form == 0) {
+                        CHECK(mca_pml.pml_irecv(dr, n, d, left, tag, &comm, &rr) == OMPI_SUCCESS &&
+                                  mca_pml.pml_isend(ds, n, d, right, tag, MCA_PML_BASE_SEND_STANDARD, &comm,
+                                                    &rs) == OMPI_SUCCESS,
+                              "nonblocking system-tag calls");
+                    } else if (form == 2) {
+                        CHECK(mca_pml.pml_start(1, &rr) == OMPI_SUCCESS &&
+                                  mca_pml.pml_start(1, &rs) == OMPI_SUCCESS, "starts");
+                    }
+                    if (form == 1) {
+                        CHECK(mca_pml.pml_send(ds, n, d, right, tag, MCA_PML_BASE_SEND_STANDARD, &comm) ==
+                                  OMPI_SUCCESS, "blocking system-tag send");
+                        CHECK(mca_pml.pml_recv(dr, n, d, left, tag, &comm, NULL) == OMPI_SUCCESS,
+                              "blocking system-tag recv");
+                    } else {
+                        wait_req(rr);
+                        wait_req(rs);
+                        CHECK(rr->req_status.MPI_ERROR == OMPI_SUCCESS && rr->req_status._ucount == n * 4,
+                              "system-tag receive status");
+                    }
+                    CHECK(harness_dev_copy_back(t, dr, n * 8) == 0, "copy back");
+                    for (size_t i = 0; i < n; ++i) {
+                        const size_t at = gap ? 2 * i : i;
+                        const int want = (int) (left * 7001 + at * 3 + form * 11 + gap) + 1000 * st;
+                        CHECK(t[at] == want, "form %d gap %d start %d element %zu: %d, want %d", form, gap, st,
+                              i, t[at], want);
+                        if (gap) CHECK(t[2 * i + 1] == -1, "gap %zu overwritten", i);
+                    }
+                }
+                if (form != 1) {
+                    CHECK(rr->req_free(&rr) == OMPI_SUCCESS && rs->req_free(&rs) == OMPI_SUCCESS, "free");
+                }
+                harness_dev_free(ds);
+                harness_dev_free(dr);
+            }
+        }
+        /* 2 messages per call pair, 4 one-start forms + 2 two-start ones */
+        CHECK(harness_saved_pml_msgs - msgs0 == 2 * (2 + 2 + 4), "system-tag messages moved by the host "
+              "transport: %d", harness_saved_pml_msgs - msgs0);
+        free(h);
+        free(t);
+    }
     CHECK(mca_pml.pml_del_comm(&comm) == OMPI_SUCCESS && mca_pml_rocm_comm_of(&comm) == NULL, "del_comm");
+    harness_pml_saved_fini();
     printf("ok gpu\n");
     return 0;
 }
