@@ -157,7 +157,7 @@ def bench_allreduce(args, metric: str, link_gbs: float):
         comm.set_param("autotune", 1)
         _progress(rank, "autotune: one call per candidate")
         calls = 0
-        while calls < 48:  # 18 candidates (9 with copy_nt fixed) x 2 rounds decide at the 36th
+        while calls < 96:  # 36 candidates (18 with copy_nt fixed) x 2 rounds decide at the 72nd
             ours()
             torch.cuda.synchronize()
             calls += 1
@@ -213,7 +213,10 @@ def bench_allreduce(args, metric: str, link_gbs: float):
     # push-land (3): the fold stores its result into every peer's landing
     # buffer (part out), the second phase is a local copy; with user_ipc it
     # is the push scheme
-    fold_bytes = {0: part, 1: 2 * part, 2: part if user else 0.0, 3: part}[alg]
+    # the pipelined schemes (4-6) time one launch per call as "fold": both
+    # transfer phases' bytes arrive during it (scatter or pull, then gather)
+    fold_bytes = {0: part, 1: 2 * part, 2: part if user else 0.0, 3: part,
+                  4: 2 * part, 5: 2 * part, 6: 2 * part}[alg]
     xgmi = {"fold": fold_bytes,
             "gather": part if alg in (0, 2) and not (alg == 2 and user) else 0.0,
             "scatter": part if alg in (2, 3) else 0.0}
@@ -326,6 +329,8 @@ def _schemes(comm, dist, torch, mop, n, rank, shared, tdev, ours, default):
     for ipc in ("staged", "user"):
         comm.set_param("user_ipc", 1 if ipc == "user" else 0)
         for a, name in ALGORITHMS:
+            if ipc == "user" and a in PIPE_ALGS:
+                continue  # with user_ipc they run the phased push / pull
             comm.set_param("algorithm", a)
             comm.set_param("blocks", default["blocks"])
             _progress(rank, f"extras: scheme {name}/{ipc}: exactness check")
@@ -372,7 +377,9 @@ def cpu_baseline_ring(world: int, nbytes: int, factor: float, seconds: float = 1
                       f"busBW = S/t x {factor:.3f}"}
 
 
-ALGORITHMS = ((0, "pull"), (1, "pull_push"), (2, "push"), (3, "push_land"))
+ALGORITHMS = ((0, "pull"), (1, "pull_push"), (2, "push"), (3, "push_land"), (4, "push_pipe"),
+              (5, "land_pipe"), (6, "pull_pipe"))
+PIPE_ALGS = (4, 5, 6)  # one pipelined launch per call (staged only; user_ipc runs them phased)
 BLOCKS = (256, 512, 1024, 2048)  # grid cap of the transfer kernels
 
 

@@ -203,6 +203,15 @@ static red_launch_fn red_fn(int op, int type) {
     default: return nullptr;
     }
 }
+static pipe_launch_fn pipe_fn(int op, int type) {
+    if (type < 0 || type >= OMPI_AMD_TYPE_COUNT) return nullptr;
+    switch (op) {
+#define CASE(k) case k: return pipe_row_##k()[type];
+        OMPI_AMD_COLL_OPS(CASE)
+#undef CASE
+    default: return nullptr;
+    }
+}
 static fused_launch_fn fused_fn(int op, int type) {
     if (type < 0 || type >= OMPI_AMD_TYPE_COUNT) return nullptr;
     switch (op) {
@@ -363,17 +372,20 @@ struct ompi_amd_request {
 // The store kind of the copy and fold kernels (non-temporal or plain) is a
 // third dimension unless param copy_nt fixed it: remote xGMI stores may
 // prefer either, and one GPU cannot tell — 18 candidates
-// then, 9 with it fixed.
-constexpr int kTuneGrid = 9, kTuneCands = 2 * kTuneGrid, kTuneRounds = 2,
+// then, 18 with it fixed.  Schemes: push-gather, push-land, staged pull and
+// their pipelined launches (round 4: phases overlapped by per-slice flags).
+constexpr int kTuneGrid = 18, kTuneCands = 2 * kTuneGrid, kTuneRounds = 2,
               kTuneCalls = kTuneCands * kTuneRounds;
 struct tune_cand {
     int algorithm, blocks, nt;  // nt: 1 non-temporal stores, 0 plain
 };
 static const tune_cand kTune[kTuneCands] = {
     {2, 1024, 1}, {2, 512, 1}, {2, 256, 1}, {3, 1024, 1}, {3, 512, 1}, {3, 256, 1},
-    {0, 1024, 1}, {0, 512, 1}, {0, 256, 1},
+    {0, 1024, 1}, {0, 512, 1}, {0, 256, 1}, {4, 1024, 1}, {4, 512, 1}, {4, 256, 1},
+    {5, 1024, 1}, {5, 512, 1}, {5, 256, 1}, {6, 1024, 1}, {6, 512, 1}, {6, 256, 1},
     {2, 1024, 0}, {2, 512, 0}, {2, 256, 0}, {3, 1024, 0}, {3, 512, 0}, {3, 256, 0},
-    {0, 1024, 0}, {0, 512, 0}, {0, 256, 0}};
+    {0, 1024, 0}, {0, 512, 0}, {0, 256, 0}, {4, 1024, 0}, {4, 512, 0}, {4, 256, 0},
+    {5, 1024, 0}, {5, 512, 0}, {5, 256, 0}, {6, 1024, 0}, {6, 512, 0}, {6, 256, 0}};
 struct tune_bucket {
     int ncand = kTuneCands;  // candidates tried: kTuneGrid when copy_nt is fixed
     int next = 0;            // calls made so far; call k runs candidate k % ncand
@@ -449,6 +461,11 @@ struct ompi_amd_comm {
     int zero_copy = 1;
     int64_t timeout_ms = 30000;
     int max_blocks = 1024;
+    // pipelined schemes: elements of a slice ~ pipe_slice bytes (param
+    // "pipe_slice"); pipe_seq numbers the pipelined calls (flag values)
+    int64_t pipe_slice = 16 << 10;
+    uint64_t pipe_seq = 0;
+    int colocated = 1;  // most ranks of this communicator on one GPU (pipe_args.colocated)
     int algorithm = 2;                    // push: push-gather in the staged mode (no staging copy)
     // param "autotune" (0 here; coll/rocm turns it on): large blocking
     // allreduces pick their scheme and grid by measurement (tune_bucket)
@@ -535,14 +552,24 @@ struct ompi_amd_plan {
 
 namespace ompi_amd {
 
-enum { ALG_PULL = 0, ALG_PULL_PUSH = 1, ALG_PUSH = 2, ALG_PUSH_LAND = 3, ALG_COUNT = 4 };
+enum {
+    ALG_PULL = 0, ALG_PULL_PUSH = 1, ALG_PUSH = 2, ALG_PUSH_LAND = 3,
+    // the staged schemes' phases in one pipelined launch (pipe_allreduce_kernel)
+    ALG_PUSH_PIPE = 4, ALG_LAND_PIPE = 5, ALG_PULL_PIPE = 6,
+    ALG_COUNT = 7
+};
 // push-land is the staged push whose second phase also stores (the owners
 // push their results into every rank's landing buffer) instead of loading;
 // with user_ipc it is the push scheme (results stored into the rbufs)
-static inline bool is_push(int alg) { return alg == ALG_PUSH || alg == ALG_PUSH_LAND; }
+static inline bool is_push(int alg) {
+    return alg == ALG_PUSH || alg == ALG_PUSH_LAND || alg == ALG_PUSH_PIPE || alg == ALG_LAND_PIPE;
+}
+static inline bool is_land(int alg) { return alg == ALG_PUSH_LAND || alg == ALG_LAND_PIPE; }
+static inline bool is_pipe(int alg) { return alg >= ALG_PUSH_PIPE; }
 
 struct ipc_blob {
     buf_desc flags, scratch;
+    int pci[3];  // the rank's GPU (domain, bus, device): ranks sharing one GPU
 };
 
 
@@ -1800,13 +1827,138 @@ static int allreduce_push(ompi_amd_comm_t *c, const void *src, const ptr_set &rp
     return launch_barrier(c, s);
 }
 
+// ---- pipelined staged schemes (pipe_allreduce_kernel): one launch whose
+// per-slice flags replace the barriers between send, fold and gather, then
+// the trailing barrier every landing / shadow call ends with.  The phases'
+// buffers: dst_c[b] where my block b goes (null: my own block), src_f[r]
+// rank r's share of my block, dst_f the fold's results, src_g[b] where
+// block b's result is gathered from.  Element e sits at ptr + e * ext.
+static int launch_pipe(ompi_amd_comm_t *c, int op, int type, const void *src, void *rbuf,
+                       int64_t count, const fold_plan &fp, const ptr_set &dst_c,
+                       const ptr_set &src_f, const ptr_set &dst_f, int ndst,
+                       const ptr_set &src_g, hipStream_t s) {
+    pipe_launch_fn f = pipe_fn(op, type);
+    if (!f) return OMPI_AMD_ERR_UNSUPPORTED;
+    note_stream(c, s);
+    const int n = c->size;
+    const int64_t ext = (int64_t)ompi_amd_type_extent(type);
+    pipe_args a{};
+    a.src = (const char *)src;
+    a.rbuf = (char *)rbuf;
+    a.dst_c = dst_c;
+    a.src_f = src_f;
+    a.dst_f = dst_f;
+    a.ndst = ndst;
+    a.src_g = src_g;
+    a.flags = c->flags + kPipeFlagOff / sizeof(uint64_t);
+    for (int p = 0; p < n; ++p) a.peer_flags.p[p] = c->peer_flags.p[p] + kPipeFlagOff / sizeof(uint64_t);
+    a.rank = c->rank;
+    a.n = n;
+    a.mine = (c->rank + 1) % n;
+    a.order = fp.order;
+    a.first = fp.order == ORDER_RING ? a.mine : fp.first;
+    a.fold_flags = fp.flags;
+    a.nt = c->copy_nt ? 1 : 0;
+    a.colocated = c->colocated;
+    blockcount(count, n, &a.split, &a.early, &a.late);
+    // slices: whole 16-B vectors of ~pipe_slice bytes; every workgroup gets
+    // at least one (small blocks: smaller slices, then fewer workgroups)
+    const int64_t E = std::max<int64_t>(1, 16 / ext);
+    const int64_t groups_max = std::max(1, std::min(c->max_blocks, kPipeMaxGroups));
+    int64_t per = std::max<int64_t>(E, (c->pipe_slice / ext) / E * E);
+    if ((a.early + per - 1) / per < groups_max)
+        per = std::max<int64_t>(E, ((a.early + groups_max - 1) / groups_max + E - 1) / E * E);
+    a.per = per;
+    a.nslices = std::max<int64_t>(1, (a.early + per - 1) / per);
+    const int64_t groups = std::min(groups_max, a.nslices);
+    a.seq = (++c->pipe_seq) << 20;
+    a.timeout_ticks = (uint64_t)c->timeout_ms * 100000ull;  // s_memrealtime: 100 MHz
+    a.err = c->err_dev;
+    a.abort_word = c->flags + kAbortWord;
+    return record_hip(f((unsigned)groups, a, s), "pipelined allreduce launch");
+}
+
+// Whether the pipelined kernel runs this call: one job per block
+// (Rabenseifner's pieces carry per-piece owners) and at most 8 ranks (one
+// node's GPUs; the kernel is built for 8 sources): else the phased schemes.
+static bool pipe_fits(const ompi_amd_comm_t *c, const fold_plan &fp) {
+    return fp.order != ORDER_RABEN && c->size <= 8;
+}
+
+// Push-gather / push-land pipelined: C stores my block b into slot [me] of
+// its owner's landing buffer, F folds my block from my input and my landing
+// slots into rbuf and the result slot [n] (push-land: into slot [n + mine]
+// of every peer's landing buffer instead), G gathers the other blocks from
+// the owners' result slots (push-land: from my own result slots).
+static int allreduce_push_pipe(ompi_amd_comm_t *c, const void *src, void *rbuf, int64_t count,
+                               int op, int type, const fold_plan &fp, hipStream_t s, bool land) {
+    const int n = c->size, mine = (c->rank + 1) % n;
+    const int64_t ext = (int64_t)ompi_amd_type_extent(type);
+    int64_t split, early, late;
+    blockcount(count, n, &split, &early, &late);
+    const size_t slot = push_slot(count, n, type);
+    ptr_set dst_c{}, src_f{}, dst_f{}, src_g{};
+    for (int b = 0; b < n; ++b) {
+        if (b == mine) continue;
+        const int owner = (b + n - 1) % n;
+        const int64_t off = block_off(b, split, early, late) * ext;
+        dst_c.p[b] = c->peer_land.p[owner] + (size_t)c->rank * slot + (off & 15) - off;
+        src_g.p[b] = land ? c->land + (size_t)(n + b) * slot + (off & 15) - off
+                          : c->peer_land.p[owner] + (size_t)n * slot + (off & 15) - off;
+    }
+    const int64_t offm = block_off(mine, split, early, late) * ext;
+    for (int r = 0; r < n; ++r)
+        src_f.p[r] = r == c->rank ? (const char *)src : c->land + (size_t)r * slot + (offm & 15) - offm;
+    dst_f.p[0] = (const char *)rbuf;
+    int ndst = 2;
+    if (land) {
+        for (int k = 1; k < n; ++k) {
+            const int q = (c->rank + k) % n;
+            dst_f.p[k] = c->peer_land.p[q] + (size_t)(n + mine) * slot + (offm & 15) - offm;
+        }
+        ndst = n;
+    } else {
+        dst_f.p[1] = c->land + (size_t)n * slot + (offm & 15) - offm;
+    }
+    // the previous landing call's trailing barrier ended every reader of
+    // these slots: no leading barrier
+    TRY(timed_phase(c, 0, s, [&] {
+        return launch_pipe(c, op, type, src, rbuf, count, fp, dst_c, src_f, dst_f, ndst, src_g, s);
+    }));
+    return launch_barrier(c, s);
+}
+
+// Staged pull pipelined: C copies my blocks other than my own into my
+// shadow `sh` (peers' shadows in sp after the swap), F folds my block from
+// my input and the peers' shadows into rbuf and my shadow, G gathers the
+// other blocks from their owners' shadows.  The staging copy of slice k
+// runs while slices < k are folded and gathered.
+static int allreduce_pull_pipe(ompi_amd_comm_t *c, const ptr_set &sp, char *sh, const void *src,
+                               void *rbuf, int64_t count, int op, int type, const fold_plan &fp,
+                               hipStream_t s) {
+    const int n = c->size, mine = (c->rank + 1) % n;
+    ptr_set dst_c{}, src_f{}, dst_f{}, src_g{};
+    for (int b = 0; b < n; ++b) {
+        if (b == mine) continue;
+        dst_c.p[b] = sh;
+        src_g.p[b] = sp.p[(b + n - 1) % n];
+    }
+    for (int r = 0; r < n; ++r) src_f.p[r] = r == c->rank ? (const char *)src : sp.p[r];
+    dst_f.p[0] = (const char *)rbuf;
+    dst_f.p[1] = sh;
+    TRY(timed_phase(c, 0, s, [&] {
+        return launch_pipe(c, op, type, src, rbuf, count, fp, dst_c, src_f, dst_f, 2, src_g, s);
+    }));
+    return launch_barrier(c, s);
+}
+
 // Landing bytes of the staged push schemes: push-gather needs n input slots
 // and its result slot [n]; push-land n input slots and n result slots (one
 // per block).  Push-land falls back to push-gather when its 2n slots would
 // pass the IPC size limit (every rank computes the same for the same count).
 static size_t staged_push_landing(int n, int algorithm, int64_t count, int type, bool *land) {
     const size_t slot = push_slot(count, n, type);
-    const bool l = algorithm == ALG_PUSH_LAND && slot * (size_t)(2 * n) <= kMaxIpcBytes;
+    const bool l = is_land(algorithm) && slot * (size_t)(2 * n) <= kMaxIpcBytes;
     if (land) *land = l;
     return slot * (size_t)(l ? 2 * n : n + 1);
 }
@@ -1839,6 +1991,8 @@ static int allreduce_push_gather(ompi_amd_comm_t *c, const void *src, void *rbuf
     const size_t slot = push_slot(count, n, type);
     bool land = false;
     TRY(ensure_landing(c, staged_push_landing(n, algorithm, count, type, &land)));
+    if (is_pipe(algorithm) && pipe_fits(c, fp))
+        return allreduce_push_pipe(c, src, rbuf, count, op, type, fp, s, land);
     cp_jobs cj{};
     for (int b = 0; b < n; ++b) {
         if (b == mine) continue;
@@ -2236,13 +2390,18 @@ static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size
     ptr_set sp{}, rp{};
     if (!c->pre && pp.push_gather)
         return allreduce_push_gather(c, src, rbuf, (int64_t)count, op, type, fp, s, pp.algorithm);
-    if (!c->pre && pp.algorithm == ALG_PULL && !c->user_ipc && !c->force_shadow) {
+    if (!c->pre && (pp.algorithm == ALG_PULL || pp.algorithm == ALG_PULL_PIPE) && !c->user_ipc &&
+        !c->force_shadow) {
         // staged pull: the input into this rank's shadow (rbuf's phase mod
         // 256, so results and shadows line up for 16-B vectors), swap
         // shadows, fold / gather through them
         char *base = nullptr;
         TRY(shadow_reserve(c, bytes + 256, &base));
         char *sh = base + ((uintptr_t)rbuf & 255);
+        if (pp.algorithm == ALG_PULL_PIPE && pipe_fits(c, fp)) {  // the copy runs inside the pipeline
+            TRY(exchange_bufs(c, sh, nullptr, &sp, &rp));
+            return allreduce_pull_pipe(c, sp, sh, src, rbuf, (int64_t)count, op, type, fp, s);
+        }
         cp_jobs cj{};
         cj.n = 1;
         cj.j[0] = {(const char *)src, sh, (int64_t)bytes};
@@ -2317,8 +2476,10 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
     // device resources: fine-grained flags, scratch, pinned error word
     c->scratch_bytes = std::max<size_t>(c->small_bytes, 4 << 20);  // per half
     ipc_blob mine{}, all[kMaxRanks];
-    hipError_t e = alloc_exportable(kFlagPageBytes, (char **)&c->flags, &mine.flags.h, true);
-    if (e == hipSuccess) e = hipMemsetAsync(c->flags, 0, kFlagPageBytes, nullptr);
+    // the flag page, then the pipelined schemes' rows (kPipeFlagOff)
+    const size_t flag_bytes = kPipeFlagOff + kPipeFlagBytes;
+    hipError_t e = alloc_exportable(flag_bytes, (char **)&c->flags, &mine.flags.h, true);
+    if (e == hipSuccess) e = hipMemsetAsync(c->flags, 0, flag_bytes, nullptr);
     if (e == hipSuccess) e = alloc_exportable(2 * c->scratch_bytes, &c->scratch, &mine.scratch.h);
     if (e == hipSuccess) e = hipHostMalloc((void **)&c->err_host, 64, hipHostMallocMapped);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&c->err_dev, c->err_host, 0);
@@ -2337,11 +2498,23 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
     }
     describe_alloc(c->flags, &mine.flags);
     describe_alloc(c->scratch, &mine.scratch);
+    if (hipDeviceGetAttribute(&mine.pci[0], hipDeviceAttributePciDomainID, device) != hipSuccess ||
+        hipDeviceGetAttribute(&mine.pci[1], hipDeviceAttributePciBusId, device) != hipSuccess ||
+        hipDeviceGetAttribute(&mine.pci[2], hipDeviceAttributePciDeviceId, device) != hipSuccess) {
+        (void)hipGetLastError();
+        mine.pci[0] = mine.pci[1] = mine.pci[2] = -1;  // unknown: counted as shared
+    }
     *c->err_host = 0;
     ipc_add_user(c, quiesce_user);
     if (rank == 0) rc = p2p_create(c, name, rank, size, 0, &c->p2p);
     if (rc == OMPI_AMD_SUCCESS) rc = c->boot.allgather(&mine, all, sizeof(ipc_blob));
     if (rc == OMPI_AMD_SUCCESS && rank != 0) rc = p2p_create(c, name, rank, size, 1, &c->p2p);
+    for (int p = 0; rc == OMPI_AMD_SUCCESS && p < size; ++p) {
+        int same = 0;
+        for (int q = 0; q < size; ++q)
+            same += (all[q].pci[0] < 0 || memcmp(all[q].pci, all[p].pci, sizeof(all[p].pci)) == 0) ? 1 : 0;
+        c->colocated = std::max(c->colocated, same);
+    }
     for (int p = 0; rc == OMPI_AMD_SUCCESS && p < size; ++p) {
         if (p == rank) {
             c->peer_flags.p[p] = c->flags;
@@ -2517,6 +2690,9 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
         if (v < 0 || v >= ALG_COUNT) return OMPI_AMD_ERR_BAD_PARAM;
         c->algorithm = (int)v;
         c->autotune = 0;  // an explicit scheme is not second-guessed
+    } else if (!strcmp(key, "pipe_slice")) {
+        if (v < 16 || v > (64 << 20)) return OMPI_AMD_ERR_BAD_PARAM;
+        c->pipe_slice = v;
     } else if (!strcmp(key, "force_shadow")) {
         c->force_shadow = v ? 1 : 0;
     } else if (!strcmp(key, "user_ipc")) {
@@ -2543,6 +2719,9 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     if (!c || !key || !v) return OMPI_AMD_ERR_BAD_PARAM;
     if (!strcmp(key, "small_bytes")) *v = (int64_t)c->small_bytes;
     else if (!strcmp(key, "zero_copy")) *v = c->zero_copy;
+    else if (!strcmp(key, "pipe_slice")) *v = c->pipe_slice;
+    else if (!strcmp(key, "pipe_calls")) *v = (int64_t)c->pipe_seq;
+    else if (!strcmp(key, "colocated")) *v = c->colocated;
     else if (!strcmp(key, "timeout_ms")) *v = (int64_t)c->timeout_ms;
     else if (!strcmp(key, "profile")) *v = c->profile;
     else if (!strcmp(key, "blocks")) *v = c->max_blocks;

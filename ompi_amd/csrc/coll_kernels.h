@@ -432,10 +432,235 @@ __global__ __launch_bounds__(kXferThreads) void fused_allreduce_kernel(fused_arg
     }
 }
 
+// ---------------------------------------------------------------- pipelined large allreduce
+// The two-shot schemes' three phases — send (C: my input's blocks to where
+// their owners fold them), fold (F: the owner folds its block and stores the
+// result where the others gather it), gather (G: the other blocks into my
+// rbuf) — in ONE launch with per-slice flags instead of a device barrier
+// between phases.  Every block is cut into slices; workgroup w owns slices
+// w, w + G, w + 2G, ... of every block, and at its iteration p it runs C of
+// its slice p, F of slice p - 1 and G of slice p - 2, then drains its
+// stores, releases once, and tells every peer "C(p) and F(p - 1) done" on
+// its own flag row.  Before iteration p it waits only for the SAME
+// workgroup of every peer to have finished iteration p - 1 (its C(p - 1)
+// feeds my F(p - 1), its F(p - 2) my G(p - 2)): no grid-wide sync, and
+// copy, fold and gather traffic of different slices is in flight together
+// (the staging copy of pull, the scatter of push, overlap the transfers
+// instead of preceding them behind a barrier).  Which buffers the phases
+// touch is the host's choice (coll_ipc.hip: staged pull, push-gather,
+// push-land).  Element e of the vector sits at p + e * sizeof(T) for every
+// pointer below (the host biases landing-slot pointers by their block's
+// offset).  Flag rows live kPipeFlagOff bytes into each rank's flag
+// allocation: [phase C / F][workgroup][peer] of uint64 counters,
+// (seq << 20) + (iterations done), seq the same on every rank per call.
+constexpr int kPipeMaxGroups = 1024;
+constexpr size_t kPipeFlagOff = 64 << 10;
+constexpr size_t kPipeFlagBytes = 2 * (size_t)kPipeMaxGroups * kMaxRanks * sizeof(uint64_t);
+
+struct pipe_args {
+    const char *src;
+    ptr_set dst_c;  // per block: where C sends it (null: not sent — my own block)
+    ptr_set src_f;  // per rank: the fold's sources (virtual order from `first`)
+    ptr_set dst_f;  // the fold's destinations [0, ndst)
+    ptr_set src_g;  // per block: where G gathers it from (null: not gathered)
+    char *rbuf;
+    uint64_t *flags;      // my pipe rows
+    flag_set peer_flags;  // every peer's pipe rows as mapped here
+    int rank, n, mine, ndst, order, first, fold_flags, nt;
+    int colocated;  // most ranks of this communicator sharing one GPU (co-residency cap)
+    int64_t split, early, late;  // ring blocks (blockcount)
+    int64_t per, nslices;        // elements per slice (a multiple of 16 B), slices per block
+    uint64_t seq, timeout_ticks;
+    int *err;
+    uint64_t *abort_word;
+};
+
+__device__ __forceinline__ size_t pipe_row(int phase, int w, int r) {
+    return ((size_t)phase * kPipeMaxGroups + (size_t)w) * kMaxRanks + (size_t)r;
+}
+
+// Bytes [lo, hi) from s to d by one workgroup: 16-B vectors, 4 in flight
+// per lane, when s and d share their phase mod 16; else bytewise.
+__device__ __forceinline__ void pipe_copy(const char *s, char *d, int64_t lo, int64_t hi, bool nt) {
+    const int t = threadIdx.x;
+    if (hi <= lo) return;
+    int64_t head = hi - lo, nv = 0;
+    if ((((uintptr_t)(s + lo) ^ (uintptr_t)(d + lo)) & 15) == 0) {
+        head = min(hi - lo, (int64_t)((16 - ((uintptr_t)(s + lo) & 15)) & 15));
+        nv = (hi - lo - head) / 16;
+    }
+    const u32x4 *sv = reinterpret_cast<const u32x4 *>(s + lo + head);
+    u32x4 *dv = reinterpret_cast<u32x4 *>(d + lo + head);
+    constexpr int S = kXferThreads;
+    int64_t i = t;
+    for (; i + 3 * S < nv; i += 4 * S) {
+        const u32x4 a = __builtin_nontemporal_load(sv + i);
+        const u32x4 b = __builtin_nontemporal_load(sv + i + S);
+        const u32x4 c = __builtin_nontemporal_load(sv + i + 2 * S);
+        const u32x4 e = __builtin_nontemporal_load(sv + i + 3 * S);
+        if (nt) {
+            __builtin_nontemporal_store(a, dv + i);
+            __builtin_nontemporal_store(b, dv + i + S);
+            __builtin_nontemporal_store(c, dv + i + 2 * S);
+            __builtin_nontemporal_store(e, dv + i + 3 * S);
+        } else {
+            dv[i] = a;
+            dv[i + S] = b;
+            dv[i + 2 * S] = c;
+            dv[i + 3 * S] = e;
+        }
+    }
+    for (; i < nv; i += S) {
+        if (nt) __builtin_nontemporal_store(__builtin_nontemporal_load(sv + i), dv + i);
+        else dv[i] = __builtin_nontemporal_load(sv + i);
+    }
+    const int64_t tail0 = lo + head + nv * 16;
+    const int64_t nrest = head + (hi - tail0);
+    for (int64_t k = t; k < nrest; k += S) {
+        const int64_t b = k < head ? lo + k : tail0 + (k - head);
+        d[b] = s[b];
+    }
+}
+
+// Elements [lo, hi) of the fold by one workgroup (reduce_kernel's body).
+template <typename T, int OP, int NM>
+__device__ __forceinline__ void pipe_fold(const pipe_args &a, int64_t lo, int64_t hi) {
+    constexpr int E = 16 / sizeof(T);
+    const int t = threadIdx.x;
+    if (hi <= lo) return;
+    // vector body where every source and destination is 16-B aligned
+    const uintptr_t ph = (uintptr_t)(a.dst_f.p[0] + lo * (int64_t)sizeof(T)) & 15;
+    bool same = true;
+#pragma unroll
+    for (int j = 0; j < NM; ++j)
+        if (j < a.n) same = same && (((uintptr_t)(a.src_f.p[j] + lo * (int64_t)sizeof(T)) & 15) == ph);
+#pragma unroll
+    for (int k = 1; k < NM; ++k)
+        if (k < a.ndst) same = same && (((uintptr_t)(a.dst_f.p[k] + lo * (int64_t)sizeof(T)) & 15) == ph);
+    const int64_t lead = (int64_t)((16 - ph) & 15);
+    int64_t head = hi - lo, nv = 0;
+    if (same && lead % (int64_t)sizeof(T) == 0) {
+        head = min(hi - lo, lead / (int64_t)sizeof(T));
+        nv = (hi - lo - head) / E;
+    }
+    const int64_t v0 = lo + head;
+    for (int64_t i = t; i < nv; i += kXferThreads) {
+        vec16<T> v[NM];
+#pragma unroll
+        for (int j = 0; j < NM; ++j) {
+            if (j < a.n) {
+                const int r = (a.first + j) % a.n;
+                const u32x4 *p = reinterpret_cast<const u32x4 *>(reinterpret_cast<const T *>(a.src_f.p[r]) + v0);
+                v[j].v = __builtin_nontemporal_load(p + i);
+            }
+        }
+        vec16<T> out;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            T s[NM];
+#pragma unroll
+            for (int j = 0; j < NM; ++j) s[j] = v[j].e[e];
+            out.e[e] = fold<T, OP, NM>(s, a.n, a.order, a.fold_flags);
+        }
+#pragma unroll
+        for (int k = 0; k < NM; ++k) {
+            if (k < a.ndst) {
+                u32x4 *q = reinterpret_cast<u32x4 *>(reinterpret_cast<T *>(const_cast<char *>(a.dst_f.p[k])) + v0) + i;
+                if (a.nt) __builtin_nontemporal_store(out.v, q);
+                else *q = out.v;
+            }
+        }
+    }
+    const int64_t tail0 = v0 + nv * E;
+    const int64_t nrest = head + (hi - tail0);
+    for (int64_t k = t; k < nrest; k += kXferThreads) {
+        const int64_t e = k < head ? lo + k : tail0 + (k - head);
+        T s[NM];
+        gather_scalar<T, NM>(s, a.src_f, a.n, a.first, e);
+        const T r = fold<T, OP, NM>(s, a.n, a.order, a.fold_flags);
+#pragma unroll
+        for (int d = 0; d < NM; ++d)
+            if (d < a.ndst) store_elem<T>(reinterpret_cast<T *>(const_cast<char *>(a.dst_f.p[d])) + e, r);
+    }
+}
+
+template <typename T, int OP, int NM>
+__global__ __launch_bounds__(kXferThreads) void pipe_allreduce_kernel(pipe_args a) {
+    const int t = threadIdx.x, w = blockIdx.x, G = gridDim.x;
+    const int64_t P = (a.nslices - w + G - 1) / G;  // my slices (the host sizes G <= nslices)
+    constexpr int64_t ext = sizeof(T);
+    __shared__ int gave_up;
+    if (t == 0) gave_up = 0;
+    __syncthreads();
+    for (int64_t p = 0; p < P + 2; ++p) {
+        const bool doC = p < P, doF = p >= 1 && p <= P, doG = p >= 2;
+        if (p >= 1) {
+            if (t < a.n && t != a.rank) {
+                bool ok = true;
+                if (doF)  // peer t's C(p - 1): its share of my block's slice p - 1
+                    ok = wait_epoch(a.flags + pipe_row(0, w, t), a.seq + (uint64_t)p, a.err,
+                                    a.timeout_ticks, a.abort_word);
+                if (ok && doG)  // peer t's F(p - 2): its block's slice p - 2 folded
+                    ok = wait_epoch(a.flags + pipe_row(1, w, t), a.seq + (uint64_t)(p - 1), a.err,
+                                    a.timeout_ticks, a.abort_word);
+                if (!ok) gave_up = 1;
+            }
+            __syncthreads();
+            if (gave_up) return;  // a peer never arrived: its memory is not ours to read
+            acquire_once();
+        }
+        if (doC) {
+            const int64_t s = w + p * G;
+#pragma unroll
+            for (int b = 0; b < NM; ++b) {
+                if (b >= a.n || !a.dst_c.p[b]) continue;
+                const int64_t off = b < a.split ? b * a.early : b * a.late + a.split;
+                const int64_t cnt = b < a.split ? a.early : a.late;
+                const int64_t lo = off + min(cnt, s * a.per), hi = off + min(cnt, (s + 1) * a.per);
+                pipe_copy(a.src, const_cast<char *>(a.dst_c.p[b]), lo * ext, hi * ext, a.nt);
+            }
+        }
+        if (doF) {
+            const int64_t s = w + (p - 1) * G;
+            const int b = a.mine;
+            const int64_t off = b < a.split ? b * a.early : b * a.late + a.split;
+            const int64_t cnt = b < a.split ? a.early : a.late;
+            pipe_fold<T, OP, NM>(a, off + min(cnt, s * a.per), off + min(cnt, (s + 1) * a.per));
+        }
+        if (doG) {
+            const int64_t s = w + (p - 2) * G;
+#pragma unroll
+            for (int b = 0; b < NM; ++b) {
+                if (b >= a.n || !a.src_g.p[b]) continue;
+                const int64_t off = b < a.split ? b * a.early : b * a.late + a.split;
+                const int64_t cnt = b < a.split ? a.early : a.late;
+                const int64_t lo = off + min(cnt, s * a.per), hi = off + min(cnt, (s + 1) * a.per);
+                pipe_copy(a.src_g.p[b], a.rbuf, lo * ext, hi * ext, a.nt);
+            }
+        }
+        if (doC || doF) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (t == 0) sys_release();
+            __syncthreads();
+            if (t < a.n && t != a.rank) {
+                if (doC)
+                    __hip_atomic_store(a.peer_flags.p[t] + pipe_row(0, w, a.rank), a.seq + (uint64_t)(p + 1),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (doF)
+                    __hip_atomic_store(a.peer_flags.p[t] + pipe_row(1, w, a.rank), a.seq + (uint64_t)p,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
+    xfer_epilogue();
+}
+
 // ---------------------------------------------------------------- launch rows
 using red_launch_fn = hipError_t (*)(dim3, const ptr_set &, const ptr_set &, int, int, int, int,
                                      const red_jobs &, hipStream_t);
 using fused_launch_fn = hipError_t (*)(dim3, const fused_args &, hipStream_t);
+using pipe_launch_fn = hipError_t (*)(unsigned, const pipe_args &, hipStream_t);
 
 // Row `op` of the launch tables: OMPI_AMD_TYPE_COUNT entries, NULL where
 // op/base has no handler (slot_supported).  Defined by coll_kern.hip built
@@ -443,7 +668,8 @@ using fused_launch_fn = hipError_t (*)(dim3, const fused_args &, hipStream_t);
 #define OMPI_AMD_COLL_OPS(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
 #define OMPI_AMD_COLL_ROW_DECL(k)          \
     const red_launch_fn *red_row_##k();    \
-    const fused_launch_fn *fused_row_##k();
+    const fused_launch_fn *fused_row_##k(); \
+    const pipe_launch_fn *pipe_row_##k();
 OMPI_AMD_COLL_OPS(OMPI_AMD_COLL_ROW_DECL)
 #undef OMPI_AMD_COLL_ROW_DECL
 

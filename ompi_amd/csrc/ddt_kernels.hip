@@ -294,6 +294,7 @@ struct ddt_period {
     int64_t nper;       // periods per tile
     int64_t map_bytes;  // LDS bytes holding the map (0: identity)
     const uint16_t *map;  // psize entries: typed offset - lowest, per packed byte
+    int64_t touch;      // unpack: bytes between reads of the typed span before the stores (0: none)
 };
 
 // Stage 16-B vectors [0, nv) of src into LDS (lane t: t, t + 256, ...),
@@ -424,7 +425,6 @@ __device__ __forceinline__ void unpack_tiles(const ddt_period &P, const char *co
                                              int64_t start, int64_t j0, int64_t j1, int64_t tile0,
                                              int64_t tstep, const uint16_t *map, char *data) {
     using T = typename granule<G>::t;
-    typedef unsigned int v4 __attribute__((ext_vector_type(4)));
     const int t = threadIdx.x;
     constexpr int64_t step = (int64_t)G * kDdtThreads;  // packed bytes per lane pass
     const int64_t st_j = step / P.psize, st_q = step % P.psize;
@@ -443,8 +443,21 @@ __device__ __forceinline__ void unpack_tiles(const ddt_period &P, const char *co
         __syncthreads();
         const char *src = data + ((uintptr_t)c0 - A0);
         char *t0 = typed + P.base + jt * P.pext;
+        unsigned seen = 0;
+        if (P.touch) {  // one read per touch bytes of the typed span (clamped to it)
+            const int64_t tspan = (nj - 1) * P.pext + P.span;
+            const int64_t lead = (int64_t)((uintptr_t)t0 & (uintptr_t)(P.touch - 1));
+            for (int64_t k = t; k * P.touch < tspan + lead; k += kDdtThreads) {
+                int64_t o = k * P.touch - lead;
+                o = o < 0 ? 0 : (o > tspan - 1 ? tspan - 1 : o);
+                seen |= *reinterpret_cast<const unsigned char *>(t0 + o);
+            }
+        }
         int64_t r = (int64_t)t * G;
-        if (r >= len) continue;
+        if (r >= len) {
+            asm volatile("" ::"v"(seen));
+            continue;
+        }
         int64_t j = r / P.psize, q = r - j * P.psize;
         constexpr int U = 4;  // granules per lane per pass: U independent stores in flight
         for (; r < len; r += U * step) {
@@ -464,6 +477,7 @@ __device__ __forceinline__ void unpack_tiles(const ddt_period &P, const char *co
             for (int u = 0; u < U; ++u)
                 if (r + u * step < len) *reinterpret_cast<T *>(t0 + off[u]) = v[u];
         }
+        asm volatile("" ::"v"(seen));
     }
 }
 
@@ -674,6 +688,17 @@ static int64_t tile_data_bytes() {
     return v;
 }
 
+// Unpack: read the typed span once (one byte per OMPI_AMD_DDT_UNPACK_TOUCH
+// bytes, a power of two) before the masked stores of a tile.
+static int64_t unpack_touch() {
+    static const int64_t v = [] {
+        const char *e = getenv("OMPI_AMD_DDT_UNPACK_TOUCH");
+        const int64_t x = e ? atoll(e) : 0;
+        return (x >= 4 && x <= 4096 && (x & (x - 1)) == 0) ? x : (int64_t)0;
+    }();
+    return v;
+}
+
 static bool tile_off() {
     static const bool v = getenv("OMPI_AMD_DDT_TILE") && atoi(getenv("OMPI_AMD_DDT_TILE")) == 0;
     return v;
@@ -709,6 +734,7 @@ static bool tile_period(const ompi_amd_ddt_t *ddt, size_t count, int G, bool unp
     }
     if (P.pext < 0 || P.psize % G != 0) return false;
     if (unpack && P.psize > P.pext) return false;  // the tile's packed bytes must fit its LDS
+    P.touch = unpack ? unpack_touch() : 0;
     P.nper = std::max<int64_t>(1, (tile_data_bytes() - P.span) / std::max<int64_t>(P.pext, 1) + 1);
     *lds = (size_t)P.map_bytes + (size_t)(((P.nper - 1) * P.pext + P.span + 15) & ~(int64_t)15) + 32;
     *out = P;

@@ -471,23 +471,67 @@ def case_zero_counts(comm, rank, n, salt):
     return case_allreduce(comm, rank, n, F, SUM, 4099, salt)
 
 
+def case_pipe(comm, rank, n, salt, big):
+    """The pipelined schemes (param "algorithm" 4 push-gather, 5 push-land,
+    6 staged pull: send, fold and gather of one call in one launch with
+    per-slice flags, pipe_allreduce_kernel): bit-exact against the oracle on
+    dataset R at the default slice and at 256-B slices (many passes per
+    workgroup), ragged counts, in place, fp64 and MAXLOC, and on buffers 4 B
+    off 16-B alignment (the kernel's scalar paths); every call must have run
+    the pipelined launch (param pipe_calls)."""
+    F, D, DI = mop.MPI_FLOAT, mop.MPI_DOUBLE, mop.MPI_DOUBLE_INT
+    SUM = mop.MPI_SUM
+    try:
+        for a in (4, 5, 6):
+            comm.set_param("algorithm", a)
+            for sl in (16 << 10, 256):
+                comm.set_param("pipe_slice", sl)
+                runs = [(F, SUM, big + 5, False), (F, SUM, big, True), (D, SUM, big // 2 + 3, False),
+                        (DI, mop.MPI_MAXLOC, 262147, False)]
+                for k, (dt, op, count, inplace) in enumerate(runs):
+                    c0 = comm.get_param("pipe_calls")
+                    ok, msg = case_allreduce(comm, rank, n, dt, op, count, salt + 10 * a + k,
+                                             inplace=inplace)
+                    if not ok:
+                        return False, f"alg {a} slice {sl} {dt.name} {op.name} {count}: {msg}"
+                    if n <= 8 and comm.get_param("pipe_calls") != c0 + 1:
+                        return False, f"alg {a} slice {sl}: the call did not run pipelined"
+            # misaligned: the send buffer 4 B past, the receive buffer 8 B past
+            # a 16-B boundary (each rank alike)
+            count = big + 3
+            xs = [inputs(F, count, r, salt + 77) for r in range(n)]
+            exp, _ = orc.allreduce([x.copy() for x in xs], count, SUM.index, F.code)
+            raw = np.ascontiguousarray(xs[rank]).view(np.uint8)
+            sb = torch.zeros(raw.nbytes + 16, dtype=torch.uint8, device="cuda")
+            sb[4:4 + raw.nbytes].copy_(torch.from_numpy(raw.copy()))
+            ob = torch.zeros(raw.nbytes + 16, dtype=torch.uint8, device="cuda")
+            comm.allreduce(sb[4:], ob[8:], count, F, SUM, blocking=True)
+            got = ob[8:8 + raw.nbytes].cpu().numpy().view(np.float32)
+            if not np.array_equal(got.view(np.uint32), exp[rank].view(np.uint32)):
+                return False, f"alg {a} misaligned: {mismatch(got, exp[rank])}"
+        return True, f"{comm.get_param('pipe_calls')} pipelined calls, colocated {comm.get_param('colocated')}"
+    finally:
+        comm.set_param("pipe_slice", 16 << 10)
+        comm.set_param("algorithm", DEFAULT_ALG[0])
+
+
 def case_autotune(comm, rank, n, salt, big):
-    """param "autotune" (coll/rocm's default): the first 36 large blocking
-    allreduces of a size bucket run the 18 candidates twice each
-    (push-gather, push-land and staged pull x 1024 / 512 / 256 blocks x
-    non-temporal / plain stores while copy_nt is not fixed; a candidate
-    counts its best round), the 36th decides — on every
+    """param "autotune" (coll/rocm's default): the first 72 large blocking
+    allreduces of a size bucket run the 36 candidates twice each
+    (push-gather, push-land, staged pull and their pipelined launches x
+    1024 / 512 / 256 blocks x non-temporal / plain stores while copy_nt is
+    not fixed; a candidate counts its best round), the 72nd decides — on every
     rank alike — and later calls run the choice; every result bit-exact
     against the oracle on dataset R (the fold order is the same whatever
     the scheme), in place too, and a nonblocking allreduce of the same size
     posted meanwhile keeps the default scheme; once decided, a nonblocking
     and a persistent allreduce of that size take the fastest candidate that
-    swaps no handles (push-gather / push-land) with its grid."""
+    swaps no handles (push-gather / push-land, pipelined or not) with its grid."""
     F, SUM = mop.MPI_FLOAT, mop.MPI_SUM
     count = big + 11
     comm.set_param("autotune", 1)
     try:
-        ncalls = 36
+        ncalls = 72
         for i in range(ncalls + 3):
             if i == 3:  # a nonblocking call in the middle of the tuning
                 xs = [inputs(F, count, r, salt + 50) for r in range(n)]
@@ -509,7 +553,7 @@ def case_autotune(comm, rank, n, salt, big):
         choice = (comm.get_param("autotune_algorithm"), comm.get_param("autotune_blocks"),
                   comm.get_param("autotune_copy_nt"))
         nc = comm.get_param("autotune_ncand")
-        if nc != 18:
+        if nc != 36:
             return False, f"{nc} candidates with copy_nt not fixed"
         times = [comm.get_param(f"autotune_us{k}") for k in range(nc)]
         # decided: a nonblocking and a persistent allreduce of this size take
@@ -517,7 +561,7 @@ def case_autotune(comm, rank, n, salt, big):
         algs = [comm.get_param(f"autotune_alg{k}") for k in range(nc)]
         grids = [comm.get_param(f"autotune_grid{k}") for k in range(nc)]
         nts = [comm.get_param(f"autotune_nt{k}") for k in range(nc)]
-        push = [k for k in range(nc) if algs[k] in (2, 3)]
+        push = [k for k in range(nc) if algs[k] in (2, 3, 4, 5)]
         # (times are whole microseconds: a tie may hide a sub-microsecond order)
         fastest = min(times[k] for k in push)
         wanted = {(algs[k], grids[k], nts[k]) for k in push if times[k] == fastest}
@@ -1151,6 +1195,7 @@ def main():
     cases += [
         ("zero_counts_every_entry_point", lambda: case_zero_counts(comm, rank, n, 96)),
         ("autotune_large_allreduce", lambda: case_autotune(comm, rank, n, 97, big)),
+        ("pipelined_schemes", lambda: case_pipe(comm, rank, n, 120, big)),
         ("iallreduce_mixed", lambda: case_iallreduce(comm, rank, n, 90)),
         ("iallreduce_many_outstanding", lambda: case_iallreduce_many(comm, rank, n, 94)),
         ("persistent_small", lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, 3001, 80)),
@@ -1165,7 +1210,7 @@ def main():
     ]
     # zero-copy allreduce under the two push schemes (param "algorithm")
     # the schemes other than the library default (which every unscoped case runs)
-    for alg in [a for a in (0, 1, 2, 3) if a != DEFAULT_ALG[0]]:
+    for alg in [a for a in (0, 1, 2, 3, 4, 5, 6) if a != DEFAULT_ALG[0]]:
         def with_alg(fn, a=alg):
             def run():
                 comm.set_param("algorithm", a)
@@ -1201,7 +1246,7 @@ def main():
     if os.environ.get("COLL_HEADLINE"):  # full-size headline only (tests/test_coll_gpu.py)
         hc = int(os.environ["COLL_HEADLINE"])
         cases = [(f"headline_alg{a}", lambda a=a: case_headline(comm, rank, n, hc, 95 + a, a))
-                 for a in (0, 1, 2, 3)]
+                 for a in (0, 1, 2, 3, 4, 5, 6)]
     def shadowed_nb(fn):  # the export fallback for the nonblocking forms
         def run():
             comm.set_param("force_shadow", 1)

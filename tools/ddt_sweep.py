@@ -69,9 +69,13 @@ def bench_type(name, dt, count, chunks, top_iters=20):
 
 def main():
     top = int(os.environ.get("SWEEP_TOP", 1 << 30))
+    only = os.environ.get("SWEEP_TYPES")  # comma-separated type names (default: all)
+    want = (lambda n: True) if not only else (lambda n: n in only.split(","))
     d = dd.predefined("MPI_DOUBLE")
     sizes = [4096, 1 << 20, 64 << 20, 256 << 20, top]
     for bl in (1, 2, 8, 64):
+        if not want(f"vector_bl{bl}"):
+            continue
         for packed in sizes:
             count = packed // (8 * bl)
             dt = dd.type_vector(count, bl, 2 * bl, d)
@@ -82,11 +86,13 @@ def main():
     lens = [13, 13, 13, 13, 13, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1]
     disps = [286, 308, 330, 352, 374, 396, 419, 442, 465, 488, 511, 534, 557, 580, 603, 626, 649, 672]
     blacs = dd.type_indexed(lens, disps, i32)
-    for packed in (1 << 20, 64 << 20, 256 << 20):
-        bench_type("blacs_indexed", blacs, packed // blacs.size, [packed, 65536])
+    big = [int(x) for x in os.environ.get("SWEEP_SIZES", "1048576,67108864,268435456").split(",")]
+    chunks = lambda p: [p] if os.environ.get("SWEEP_WHOLE") == "1" else [p, 65536]
+    for packed in big if want("blacs_indexed") else ():
+        bench_type("blacs_indexed", blacs, packed // blacs.size, chunks(packed))
     st = dd.type_struct([1, 1], [0, 8], [i32, d])
-    for packed in (1 << 20, 64 << 20, 256 << 20):
-        bench_type("struct_int_double", st, packed // st.size, [packed, 65536])
+    for packed in big if want("struct_int_double") else ():
+        bench_type("struct_int_double", st, packed // st.size, chunks(packed))
 
 
 if __name__ == "__main__":

@@ -154,6 +154,49 @@ __global__ __launch_bounds__(256) void k_pstore(const unsigned char *src, unsign
 template <typename L>
 static double time_ms(L &&launch, int reps);
 
+// blacs-indexed unpack stores without the kernel around them (mode 3):
+// store op k of period j writes sz[k] bytes from packed offset po[k] of the
+// period to typed offset to[k] (a 1548-B period holding 624 B in 18 runs).
+// G4: one op per 4-B granule; WIDE: each run cut into naturally aligned 16 /
+// 8 / 4-B stores.  NT: non-temporal stores.  TOUCH: every lane first reads
+// one byte per 64 B of its period's typed span (brings the lines in before
+// the masked stores).
+struct bop { unsigned short to, po; unsigned char sz; };
+template <bool NT>
+__global__ __launch_bounds__(256) void k_blacs(const unsigned char *src, unsigned char *dst,
+                                               const bop *ops, int nops, size_t nper, int touch) {
+    const size_t j0 = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t total = nper * (size_t)nops;
+    unsigned seen = 0;
+    if (touch) {
+        const size_t per = (size_t)blockIdx.x * 256 / nops;  // first period of this workgroup
+        const size_t last = min(nper, ((size_t)blockIdx.x + 1) * 256 / nops + 1);
+        for (size_t o = per * 1548 + threadIdx.x * 64; o < last * 1548; o += 256 * 64) seen |= dst[o];
+    }
+    if (j0 < total) {
+        const size_t j = j0 / nops;
+        const bop op = ops[j0 - j * nops];
+        const unsigned char *s = src + j * 624 + op.po;
+        unsigned char *d = dst + j * 1548 + op.to;
+        if (op.sz == 16) {
+            typedef unsigned u32x4_ __attribute__((ext_vector_type(4)));
+            u32x4_ v;
+            v.x = *(const unsigned *)s; v.y = *(const unsigned *)(s + 4);
+            v.z = *(const unsigned *)(s + 8); v.w = *(const unsigned *)(s + 12);
+            if (NT) __builtin_nontemporal_store(v, (u32x4_ *)d); else *(u32x4_ *)d = v;
+        } else if (op.sz == 8) {
+            typedef unsigned u32x2_ __attribute__((ext_vector_type(2)));
+            u32x2_ v;
+            v.x = *(const unsigned *)s; v.y = *(const unsigned *)(s + 4);
+            if (NT) __builtin_nontemporal_store(v, (u32x2_ *)d); else *(u32x2_ *)d = v;
+        } else {
+            const unsigned v = *(const unsigned *)s;
+            if (NT) __builtin_nontemporal_store(v, (unsigned *)d); else *(unsigned *)d = v;
+        }
+    }
+    asm volatile("" ::"v"(seen));
+}
+
 template <int W, int P, bool STRUCT>
 static void run_pstore(void *src, void *dst, size_t dst_bytes, const char *name, int reps) {
     const size_t nelem = dst_bytes / P;
@@ -264,6 +307,59 @@ int main(int argc, char **argv) {
         run_pstore<12, 16, true>(B.a, B.c, bytes, "pstore_struct", reps);
         run_pstore<4, 8, false>(B.a, B.c, bytes, "pstore", reps);
         run_pstore<4, 4, false>(B.a, B.c, bytes / 2, "pstore_full", reps);
+        return 0;
+    }
+    if (argc > 2 && atoi(argv[2]) == 3) {  // blacs-indexed unpack store patterns
+        const int lens[18] = {13, 13, 13, 13, 13, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1};
+        const int disps[18] = {286, 308, 330, 352, 374, 396, 419, 442, 465, 488, 511, 534, 557, 580, 603, 626, 649, 672};
+        for (int wide = 0; wide < 2; ++wide) {
+            std::vector<bop> ops;
+            int po = 0;
+            for (int r = 0; r < 18; ++r) {
+                int to = (disps[r] - 286) * 4, left = lens[r] * 4;
+                while (left > 0) {
+                    int sz = 4;
+                    if (wide) {
+                        // widest natural alignment of the typed address (the
+                        // typed base of every period is 1548 * j: 4-B aligned
+                        // only; the probe's buffer is 16-B aligned, j even
+                        // periods keep the alignment of period 0)
+                        if (left >= 16 && to % 16 == 0) sz = 16;
+                        else if (left >= 8 && to % 8 == 0) sz = 8;
+                    }
+                    ops.push_back(bop{(unsigned short)to, (unsigned short)po, (unsigned char)sz});
+                    to += sz; po += sz; left -= sz;
+                }
+            }
+            bop *dops = nullptr;
+            CK(hipMalloc(&dops, ops.size() * sizeof(bop)));
+            CK(hipMemcpy(dops, ops.data(), ops.size() * sizeof(bop), hipMemcpyHostToDevice));
+            // periods spaced 1548 B would break 8/16-B alignment on odd
+            // periods: space them 1552 B? no — keep MPI's layout and use the
+            // 4-B ops on every period for wide = 0; wide = 1 is a bound only
+            // (run on periods of 1552 B, 16-B aligned)
+            const size_t pext = wide ? 1552 : 1548;
+            const size_t nper = (bytes - 4096) / pext;
+            const int nops = (int)ops.size();
+            const unsigned grid = (unsigned)((nper * nops + 255) / 256);
+            for (int nt = 0; nt < 2; ++nt)
+                for (int touch = 0; touch < 2; ++touch) {
+                    const double ms = time_ms([&] {
+                        if (nt) hipLaunchKernelGGL((k_blacs<true>), dim3(grid), dim3(256), 0, 0,
+                                                   (const unsigned char *)B.a, (unsigned char *)B.c, dops, nops, nper, touch);
+                        else hipLaunchKernelGGL((k_blacs<false>), dim3(grid), dim3(256), 0, 0,
+                                                (const unsigned char *)B.a, (unsigned char *)B.c, dops, nops, nper, touch);
+                    }, reps);
+                    const double payload = (double)nper * 624;
+                    const double gbs = 2.0 * payload / (ms * 1e-3) / 1e9;
+                    printf("{\"variant\": \"blacs_%s%s%s\", \"ops_per_period\": %d, \"period_bytes\": %zu, "
+                           "\"payload_bytes\": %.0f, \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f}\n",
+                           wide ? "wide" : "g4", nt ? "_nt" : "", touch ? "_touch" : "", nops, pext, payload,
+                           ms, gbs, gbs / 8000.0);
+                    fflush(stdout);
+                }
+            CK(hipFree(dops));
+        }
         return 0;
     }
     if (argc > 2 && atoi(argv[2]) == 1) {  // cache-policy sweep only
