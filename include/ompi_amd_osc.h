@@ -41,6 +41,7 @@
 #include <stdint.h>
 
 #include "ompi_amd_coll.h"
+#include "ompi_amd_ddt.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -89,6 +90,21 @@ int ompi_amd_accumulate(ompi_amd_win_t *win, const void *origin, size_t count, i
 /* result = target, then target = op(target, origin), as one step. */
 int ompi_amd_get_accumulate(ompi_amd_win_t *win, const void *origin, void *result, size_t count,
                             int type, int target, size_t disp, int op, void *stream);
+/* MPI_Accumulate / MPI_Get_accumulate with derived datatypes
+ * (osc_sm_comm.c:301, 350 -> ompi_osc_base_sndrcv_op,
+ * osc_base_obj_convert.c:160-245): the origin's ocount x odt elements, as a
+ * packed stream of `type` elements, are combined in order into the element
+ * slots of tcount x tdt at the target (get_accumulate: the old elements are
+ * returned into rcount x rdt at result first).  odt / rdt / tdt NULL: `type`
+ * contiguous.  The three type signatures must hold the same number of
+ * `type` elements; pair types (MAXLOC / MINLOC operands) only contiguous. */
+int ompi_amd_accumulate_ddt(ompi_amd_win_t *win, const void *origin, size_t ocount,
+                            const ompi_amd_ddt_t *odt, int target, size_t disp, size_t tcount,
+                            const ompi_amd_ddt_t *tdt, int type, int op, void *stream);
+int ompi_amd_get_accumulate_ddt(ompi_amd_win_t *win, const void *origin, size_t ocount,
+                                const ompi_amd_ddt_t *odt, void *result, size_t rcount,
+                                const ompi_amd_ddt_t *rdt, int target, size_t disp, size_t tcount,
+                                const ompi_amd_ddt_t *tdt, int type, int op, void *stream);
 /* get_accumulate of one element. */
 int ompi_amd_fetch_and_op(ompi_amd_win_t *win, const void *origin, void *result, int type,
                           int target, size_t disp, int op, void *stream);
@@ -141,6 +157,16 @@ int ompi_amd_raccumulate(ompi_amd_win_t *win, const void *origin, size_t count, 
 int ompi_amd_rget_accumulate(ompi_amd_win_t *win, const void *origin, void *result, size_t count,
                              int type, int target, size_t disp, int op, void *stream,
                              ompi_amd_rma_request_t **request);
+/* request-based forms of the derived-datatype calls above */
+int ompi_amd_raccumulate_ddt(ompi_amd_win_t *win, const void *origin, size_t ocount,
+                             const ompi_amd_ddt_t *odt, int target, size_t disp, size_t tcount,
+                             const ompi_amd_ddt_t *tdt, int type, int op, void *stream,
+                             ompi_amd_rma_request_t **req);
+int ompi_amd_rget_accumulate_ddt(ompi_amd_win_t *win, const void *origin, size_t ocount,
+                                 const ompi_amd_ddt_t *odt, void *result, size_t rcount,
+                                 const ompi_amd_ddt_t *rdt, int target, size_t disp,
+                                 size_t tcount, const ompi_amd_ddt_t *tdt, int type, int op,
+                                 void *stream, ompi_amd_rma_request_t **req);
 int ompi_amd_rma_test(ompi_amd_rma_request_t *request, int *done);
 int ompi_amd_rma_wait(ompi_amd_rma_request_t *request);
 int ompi_amd_rma_free(ompi_amd_rma_request_t *request);

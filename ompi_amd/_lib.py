@@ -255,6 +255,19 @@ PROTOTYPES = [
     ("ompi_amd_get_accumulate", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_size_t,
       _C.c_int, _C.c_void_p]),
+    ("ompi_amd_accumulate_ddt", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p, _C.c_int, _C.c_size_t, _C.c_size_t,
+      _C.c_void_p, _C.c_int, _C.c_int, _C.c_void_p]),
+    ("ompi_amd_get_accumulate_ddt", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p,
+      _C.c_int, _C.c_size_t, _C.c_size_t, _C.c_void_p, _C.c_int, _C.c_int, _C.c_void_p]),
+    ("ompi_amd_raccumulate_ddt", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p, _C.c_int, _C.c_size_t, _C.c_size_t,
+      _C.c_void_p, _C.c_int, _C.c_int, _C.c_void_p, _C.c_void_p]),
+    ("ompi_amd_rget_accumulate_ddt", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p,
+      _C.c_int, _C.c_size_t, _C.c_size_t, _C.c_void_p, _C.c_int, _C.c_int, _C.c_void_p,
+      _C.c_void_p]),
     ("ompi_amd_fetch_and_op", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_int, _C.c_int, _C.c_size_t, _C.c_int,
       _C.c_void_p]),

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -24,17 +25,10 @@
 #include <vector>
 
 #include "../../include/ompi_amd_ddt.h"
+#include "ddt_device.h"
 #include "runtime.h"
 
 namespace ompi_amd {
-
-// Division by a launch-invariant 32-bit divisor d as multiply-high + shifts
-// (Granlund-Montgomery round-up method): q = (t + ((n - t) >> s1)) >> s2,
-// t = umulhi(n, m); d = 1 gives m = 0, s1 = s2 = 0.  Exact for every
-// 32-bit n.  Replaces two v_div-style ~40-instruction sequences per granule.
-struct fastdiv {
-    uint32_t m, s1, s2;
-};
 
 static fastdiv make_fdiv(uint32_t d) {
     if (d <= 1) return {0u, 0u, 0u};
@@ -42,69 +36,6 @@ static fastdiv make_fdiv(uint32_t d) {
     while ((1ull << l) < d) ++l;  // ceil(log2 d)
     const uint64_t m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
     return {(uint32_t)m, 1u, l - 1};
-}
-
-__device__ __forceinline__ uint32_t fdiv_q(uint32_t n, const fastdiv &f) {
-    const uint32_t t = __umulhi(n, f.m);
-    return (t + ((n - t) >> f.s1)) >> f.s2;
-}
-
-struct ddt_elem {
-    int64_t count;   // repetitions
-    int64_t blen;    // bytes per repetition
-    int64_t stride;  // bytes between repetitions
-    int64_t disp;    // byte displacement of the first repetition
-    int64_t prefix;  // packed bytes of the type before this element
-    fastdiv bdiv[5];    // blen / G for G = 1, 2, 4, 8, 16 (when it fits 32 bits)
-    uint32_t pad;
-};
-
-constexpr int kDdtThreads = 256;
-constexpr int kDdtUnroll = 8;
-constexpr int kDdtLdsElems = 256;
-
-struct ddt_desc {
-    const ddt_elem *elems;  // device copy
-    int nelem;
-    int64_t size;    // packed bytes per datatype element
-    int64_t extent;
-    fastdiv sdiv;       // size / G of this launch (fast path only)
-};
-
-// Largest i with elems[i].prefix <= q.
-__device__ __forceinline__ int find_elem(const ddt_elem *e, int n, int64_t q) {
-    if (n <= 8) {
-        int i = 0;
-        for (int j = 1; j < n; ++j)
-            if (e[j].prefix <= q) i = j;
-        return i;
-    }
-    int lo = 0, hi = n - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (e[mid].prefix <= q) lo = mid; else hi = mid - 1;
-    }
-    return lo;
-}
-
-template <int G> struct granule;
-template <> struct granule<1> { using t = uint8_t; };
-template <> struct granule<2> { using t = uint16_t; };
-template <> struct granule<4> { using t = uint32_t; };
-template <> struct granule<8> { using t = uint64_t; };
-template <> struct granule<16> { typedef unsigned int t __attribute__((ext_vector_type(4))); };
-
-// Typed-layout byte address of packed stream position p.
-template <typename I>
-__device__ __forceinline__ int64_t typed_offset(const ddt_elem *e, int n, I size, int64_t extent,
-                                                I p) {
-    const I el = p / size;
-    const I q = p - el * size;
-    const int i = find_elem(e, n, (int64_t)q);
-    const I r = q - (I)e[i].prefix;
-    const I k = r / (I)e[i].blen;
-    const I w = r - k * (I)e[i].blen;
-    return (int64_t)el * extent + e[i].disp + (int64_t)k * e[i].stride + (int64_t)w;
 }
 
 // Fast path: all quantities in G-granule units fit 32 bits.
@@ -294,7 +225,7 @@ struct ddt_period {
     int64_t nper;       // periods per tile
     int64_t map_bytes;  // LDS bytes holding the map (0: identity)
     const uint16_t *map;  // psize entries: typed offset - lowest, per packed byte
-    int64_t touch;      // unpack: bytes between reads of the typed span before the stores (0: none)
+    int64_t nt;         // unpack: typed-side stores non-temporal
 };
 
 // Stage 16-B vectors [0, nv) of src into LDS (lane t: t, t + 256, ...),
@@ -443,21 +374,8 @@ __device__ __forceinline__ void unpack_tiles(const ddt_period &P, const char *co
         __syncthreads();
         const char *src = data + ((uintptr_t)c0 - A0);
         char *t0 = typed + P.base + jt * P.pext;
-        unsigned seen = 0;
-        if (P.touch) {  // one read per touch bytes of the typed span (clamped to it)
-            const int64_t tspan = (nj - 1) * P.pext + P.span;
-            const int64_t lead = (int64_t)((uintptr_t)t0 & (uintptr_t)(P.touch - 1));
-            for (int64_t k = t; k * P.touch < tspan + lead; k += kDdtThreads) {
-                int64_t o = k * P.touch - lead;
-                o = o < 0 ? 0 : (o > tspan - 1 ? tspan - 1 : o);
-                seen |= *reinterpret_cast<const unsigned char *>(t0 + o);
-            }
-        }
         int64_t r = (int64_t)t * G;
-        if (r >= len) {
-            asm volatile("" ::"v"(seen));
-            continue;
-        }
+        if (r >= len) continue;
         int64_t j = r / P.psize, q = r - j * P.psize;
         constexpr int U = 4;  // granules per lane per pass: U independent stores in flight
         for (; r < len; r += U * step) {
@@ -473,11 +391,16 @@ __device__ __forceinline__ void unpack_tiles(const ddt_period &P, const char *co
 #pragma unroll
             for (int u = 0; u < U; ++u)
                 if (r + u * step < len) v[u] = *reinterpret_cast<const T *>(src + r + u * step);
+            if (P.nt) {
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (r + u * step < len) *reinterpret_cast<T *>(t0 + off[u]) = v[u];
+                for (int u = 0; u < U; ++u)
+                    if (r + u * step < len) __builtin_nontemporal_store(v[u], reinterpret_cast<T *>(t0 + off[u]));
+            } else {
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (r + u * step < len) *reinterpret_cast<T *>(t0 + off[u]) = v[u];
+            }
         }
-        asm volatile("" ::"v"(seen));
     }
 }
 
@@ -688,15 +611,18 @@ static int64_t tile_data_bytes() {
     return v;
 }
 
-// Unpack: read the typed span once (one byte per OMPI_AMD_DDT_UNPACK_TOUCH
-// bytes, a power of two) before the masked stores of a tile.
-static int64_t unpack_touch() {
-    static const int64_t v = [] {
-        const char *e = getenv("OMPI_AMD_DDT_UNPACK_TOUCH");
-        const int64_t x = e ? atoll(e) : 0;
-        return (x >= 4 && x <= 4096 && (x & (x - 1)) == 0) ? x : (int64_t)0;
+// Unpack: the typed-side stores of a layout whose runs are all shorter than
+// 64 B (every store a partial 64-B segment) go non-temporal.  256 MiB
+// packed, one convertor call (profiles/r04_unpack_nt_ab.jsonl): blacs
+// indexed 1.36 -> 1.63 TB/s, struct{int,double} 2.62 -> 3.72, vector bl2
+// (16-B runs) 1.94 -> 3.07; with 64-B runs (bl8) they cost 8 % (5.1 -> 4.7),
+// so longer runs keep plain stores.  OMPI_AMD_DDT_UNPACK_NT=0 / 1 forces.
+static bool unpack_nt(int64_t max_run) {
+    static const int v = [] {
+        const char *e = getenv("OMPI_AMD_DDT_UNPACK_NT");
+        return e ? atoi(e) : -1;
     }();
-    return v;
+    return v >= 0 ? v != 0 : max_run < 64;
 }
 
 static bool tile_off() {
@@ -734,7 +660,7 @@ static bool tile_period(const ompi_amd_ddt_t *ddt, size_t count, int G, bool unp
     }
     if (P.pext < 0 || P.psize % G != 0) return false;
     if (unpack && P.psize > P.pext) return false;  // the tile's packed bytes must fit its LDS
-    P.touch = unpack ? unpack_touch() : 0;
+    P.nt = unpack && unpack_nt(ident ? P.psize : ddt->max_blen) ? 1 : 0;
     P.nper = std::max<int64_t>(1, (tile_data_bytes() - P.span) / std::max<int64_t>(P.pext, 1) + 1);
     *lds = (size_t)P.map_bytes + (size_t)(((P.nper - 1) * P.pext + P.span + 15) & ~(int64_t)15) + 32;
     *out = P;
@@ -990,6 +916,23 @@ static int ddt_iov(const ompi_amd_ddt_t *ddt, size_t count, void *typed, size_t 
 }  // namespace ompi_amd
 
 using namespace ompi_amd;
+
+namespace ompi_amd {
+bool ddt_view_of(const ompi_amd_ddt_t *ddt, ddt_view *out) {
+    if (!ddt || !ddt->dev || ddt->host.empty() || !out) return false;
+    out->d = ddt_desc{ddt->dev, (int)ddt->host.size(), ddt->size, ddt->extent, {0u, 0u, 0u}};
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    for (const auto &e : ddt->host) {
+        const int64_t last = (e.count - 1) * e.stride;  // stride may be negative
+        lo = std::min(lo, e.disp + std::min<int64_t>(0, last));
+        hi = std::max(hi, e.disp + std::max<int64_t>(0, last) + e.blen);
+    }
+    out->lo = lo;
+    out->hi = hi;
+    out->gran = ddt->gran;
+    return true;
+}
+}  // namespace ompi_amd
 
 extern "C" {
 

@@ -39,6 +39,7 @@
 
 #include "../../include/ompi_amd_osc.h"
 #include "comm_internal.h"
+#include "ddt_device.h"
 #include "ipc_registry.h"
 #include "op_device.h"
 #include "runtime.h"
@@ -393,6 +394,88 @@ make_acc_table(std::integer_sequence<int, O...>) {
     return {{make_acc_row<O>(std::make_integer_sequence<int, OMPI_AMD_TYPE_COUNT>{})...}};
 }
 static const auto g_acc = make_acc_table(std::make_integer_sequence<int, OMPI_AMD_OP_COUNT>{});
+
+// ---- derived datatypes at the target (ompi_osc_base_sndrcv_op,
+// osc_base_obj_convert.c:160-245): the origin's packed stream of primitive
+// elements is combined in order into the primitive slots the target
+// datatype describes.  Element k of the stream sits at
+// typed_offset(k * sizeof(T)) of the target; one lane per element, the
+// datatype program in LDS (ddt_kernel's position -> address mapping).
+// old (get_accumulate; else null): the target's elements before the update,
+// packed.  OP 0: replace (REPLACE), -1: none (NO_OP: fetch only).
+template <typename T, int OP>
+__global__ __launch_bounds__(kOscThreads) void ddt_acc_kernel(ddt_desc d, char *typed, const T *in,
+                                                              T *old, int64_t n,
+                                                              const uint32_t *gate) {
+    if (!gate_open(gate)) return;
+    __shared__ ddt_elem lds[kDdtLdsElems];
+    const ddt_elem *el = d.elems;
+    if (d.nelem <= kDdtLdsElems) {
+        for (int i = threadIdx.x; i < d.nelem; i += kOscThreads) lds[i] = d.elems[i];
+        el = lds;
+    }
+    if (threadIdx.x == 0) osc_acquire();
+    __syncthreads();
+    const int64_t gs = (int64_t)gridDim.x * kOscThreads;
+    for (int64_t k = (int64_t)blockIdx.x * kOscThreads + threadIdx.x; k < n; k += gs) {
+        const int64_t off = typed_offset<uint64_t>(el, d.nelem, (uint64_t)d.size, d.extent,
+                                                   (uint64_t)k * sizeof(T));
+        T *t = reinterpret_cast<T *>(typed + off);
+        const T v = *t;
+        if (old) old[k] = v;
+        if constexpr (OP == 0) {
+            *t = in[k];
+        } else if constexpr (OP > 0) {
+            store_elem(t, opfn<OP, false>::f(v, in[k]));
+        }
+    }
+    osc_epilogue();
+}
+
+using ddt_acc_fn = hipError_t (*)(dim3, const ddt_desc &, char *, const void *, void *, int64_t,
+                                  const uint32_t *, hipStream_t);
+
+template <typename T, int OP>
+static hipError_t ddt_acc_launch(dim3 grid, const ddt_desc &d, char *typed, const void *in,
+                                 void *old, int64_t n, const uint32_t *gate, hipStream_t s) {
+    hipLaunchKernelGGL((ddt_acc_kernel<T, OP>), grid, dim3(kOscThreads), 0, s, d, typed,
+                       static_cast<const T *>(in), static_cast<T *>(old), n, gate);
+    return hipGetLastError();
+}
+template <int OP, int TYPE>
+static constexpr ddt_acc_fn ddt_acc_slot() {
+    if constexpr (slot_supported(OP, TYPE) && !is_pair_type(TYPE))
+        return &ddt_acc_launch<typename type_of<TYPE>::type, OP>;
+    else
+        return nullptr;
+}
+template <int OP, int... T>
+static constexpr std::array<ddt_acc_fn, OMPI_AMD_TYPE_COUNT> make_ddt_acc_row(
+    std::integer_sequence<int, T...>) {
+    return {{ddt_acc_slot<OP, T>()...}};
+}
+template <int... O>
+static constexpr std::array<std::array<ddt_acc_fn, OMPI_AMD_TYPE_COUNT>, OMPI_AMD_OP_COUNT>
+make_ddt_acc_table(std::integer_sequence<int, O...>) {
+    return {{make_ddt_acc_row<O>(std::make_integer_sequence<int, OMPI_AMD_TYPE_COUNT>{})...}};
+}
+static const auto g_ddt_acc = make_ddt_acc_table(std::make_integer_sequence<int, OMPI_AMD_OP_COUNT>{});
+
+// replace / fetch-only by element size (any non-pair type of that size)
+template <int SZ> struct sized;
+template <> struct sized<1> { using t = uint8_t; };
+template <> struct sized<2> { using t = uint16_t; };
+template <> struct sized<4> { using t = uint32_t; };
+template <> struct sized<8> { using t = uint64_t; };
+template <> struct sized<16> { typedef unsigned int t __attribute__((ext_vector_type(4))); };
+static ddt_acc_fn ddt_rw_fn(size_t size, bool replace) {
+    switch (size) {
+#define RW(SZ) case SZ: return replace ? &ddt_acc_launch<sized<SZ>::t, 0> : &ddt_acc_launch<sized<SZ>::t, -1>;
+        RW(1) RW(2) RW(4) RW(8) RW(16)
+#undef RW
+    default: return nullptr;
+    }
+}
 
 struct win_blob {
     ipc_desc base;
@@ -948,6 +1031,121 @@ int ompi_amd_get_accumulate(ompi_amd_win_t *w, const void *origin, void *result,
     return rma_op(w, origin, result, count, type, target, disp, op, stream);
 }
 
+// Derived datatypes on any side (osc_sm_comm.c:135, 191, 301, 350 ->
+// ompi_osc_base_sndrcv_op): a non-contiguous origin is packed on the
+// device first (local, before the lock); under the target's accumulate
+// lock one gated kernel walks the target datatype's element slots, fetching
+// the old elements packed (get_accumulate) and combining the packed origin
+// into them; a non-contiguous result is unpacked from the fetched stream
+// afterwards (local).  Null odt / rdt / tdt: `type` contiguous.  The packed
+// scratch is stream-ordered (hipMallocAsync / hipFreeAsync on the call's
+// stream).
+static int acc_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount, const ompi_amd_ddt_t *odt,
+                   void *result, size_t rcount, const ompi_amd_ddt_t *rdt, int target, size_t disp,
+                   size_t tcount, const ompi_amd_ddt_t *tdt, int type, int op, void *stream) {
+    if (!w || type < 0 || type >= OMPI_AMD_TYPE_COUNT || ompi_amd_type_extent(type) == 0)
+        return OMPI_AMD_ERR_BAD_PARAM;
+    const size_t ext = ompi_amd_type_extent(type);
+    const bool fetch = result != nullptr;
+    const size_t tbytes = (tdt ? ompi_amd_ddt_size(tdt) : ext) * tcount;
+    if (tbytes == 0) return OMPI_AMD_SUCCESS;
+    if ((odt || rdt || tdt) && is_pair_type(type)) {
+        record_msg("osc accumulate: derived datatypes of pair type %d are not provided", type);
+        return OMPI_AMD_ERR_UNSUPPORTED;
+    }
+    if (tbytes % ext != 0 ||
+        (op != OMPI_AMD_OP_NO_OP && (odt ? ompi_amd_ddt_size(odt) : ext) * ocount != tbytes) ||
+        (fetch && (rdt ? ompi_amd_ddt_size(rdt) : ext) * rcount != tbytes) ||
+        (op != OMPI_AMD_OP_NO_OP && !origin)) {
+        record_msg("osc accumulate: origin / result / target type signatures differ");
+        return OMPI_AMD_ERR_BAD_PARAM;
+    }
+    const int64_t n = (int64_t)(tbytes / ext);
+    if (!tdt && !odt && !rdt) return rma_op(w, origin, result, (size_t)n, type, target, disp, op, stream);
+    ddt_acc_fn f = nullptr;
+    if (op == OMPI_AMD_OP_REPLACE || op == OMPI_AMD_OP_NO_OP) f = ddt_rw_fn(ext, op == OMPI_AMD_OP_REPLACE);
+    else if (op > 0 && op < OMPI_AMD_OP_COUNT) f = g_ddt_acc[op][type];
+    if (!f || (op != OMPI_AMD_OP_REPLACE && op != OMPI_AMD_OP_NO_OP && !g_acc[op][type])) {
+        record_msg("osc accumulate: op %d on type %d is not provided", op, type);
+        return OMPI_AMD_ERR_UNSUPPORTED;
+    }
+    // the target's typed span, inside its window
+    ddt_view tv{};
+    if (tdt && !ddt_view_of(tdt, &tv)) return OMPI_AMD_ERR_BAD_PARAM;
+    if (target < 0 || target >= w->size) return OMPI_AMD_ERR_BAD_PARAM;
+    const int64_t base = (int64_t)disp * (int64_t)w->peer_disp[target];
+    const int64_t last = (int64_t)(tcount - 1) * (tdt ? tv.d.extent : (int64_t)ext);
+    const int64_t lo = base + (tdt ? tv.lo + std::min<int64_t>(0, last) : 0);
+    const int64_t hi = base + (tdt ? tv.hi + std::max<int64_t>(0, last) : (int64_t)tbytes);
+    if (lo < 0 || hi > (int64_t)w->peer_bytes[target] || !w->peer_base[target]) {
+        record_msg("osc: target %d typed range [%lld, %lld) outside its %llu-byte window", target,
+                   (long long)lo, (long long)hi, (unsigned long long)w->peer_bytes[target]);
+        return OMPI_AMD_ERR_BAD_PARAM;
+    }
+    char *t = w->peer_base[target] + base;
+    hipStream_t s = win_stream(w, stream);
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    // origin stream, packed (local; before the lock)
+    const void *in = origin;
+    void *po = nullptr, *pr = nullptr;
+    int rc = OMPI_AMD_SUCCESS;
+    if (odt && op != OMPI_AMD_OP_NO_OP) {
+        rc = record_hip(hipMallocAsync(&po, tbytes, s), "hipMallocAsync (osc origin pack)");
+        size_t done = 0;
+        if (rc == OMPI_AMD_SUCCESS) rc = ompi_amd_ddt_pack(odt, ocount, origin, po, 0, tbytes, &done, s);
+        if (rc == OMPI_AMD_SUCCESS && done != tbytes) rc = OMPI_AMD_ERR_BAD_PARAM;
+        in = po;
+    }
+    void *old = result;
+    if (rc == OMPI_AMD_SUCCESS && fetch && rdt) {
+        rc = record_hip(hipMallocAsync(&pr, tbytes, s), "hipMallocAsync (osc result stream)");
+        old = pr;
+    }
+    if (rc == OMPI_AMD_SUCCESS) rc = launch_lock(w, target, 0, s);
+    if (rc == OMPI_AMD_SUCCESS) {
+        const uint32_t *gate = taken_word(w, target, true);
+        if (tdt) {
+            const int64_t blocks = std::max<int64_t>(
+                1, std::min<int64_t>((n + kOscThreads - 1) / kOscThreads, osc_grid_cap()));
+            rc = record_hip(f(dim3((unsigned)blocks), tv.d, t, in, old, n, gate, s),
+                            "osc derived accumulate launch");
+        } else {  // contiguous target: the plain kernels on the packed streams
+            if (fetch) rc = xfer_copy(t, old, tbytes, s, gate);
+            if (rc == OMPI_AMD_SUCCESS) {
+                if (op == OMPI_AMD_OP_REPLACE) rc = xfer_copy(in, t, tbytes, s, gate);
+                else if (op != OMPI_AMD_OP_NO_OP) rc = launch_acc(w, op, type, in, t, (size_t)n, gate, s);
+            }
+        }
+        const int urc = launch_lock(w, target, 1, s);  // always release
+        if (rc == OMPI_AMD_SUCCESS) rc = urc;
+    }
+    if (rc == OMPI_AMD_SUCCESS && pr) {  // the fetched stream into the result layout (local)
+        size_t done = 0;
+        rc = ompi_amd_ddt_unpack(rdt, rcount, pr, result, 0, tbytes, &done, s);
+        if (rc == OMPI_AMD_SUCCESS && done != tbytes) rc = OMPI_AMD_ERR_BAD_PARAM;
+    }
+    if (po) hip_ignore(hipFreeAsync(po, s));
+    if (pr) hip_ignore(hipFreeAsync(pr, s));
+    return rc;
+}
+
+int ompi_amd_accumulate_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount,
+                            const ompi_amd_ddt_t *odt, int target, size_t disp, size_t tcount,
+                            const ompi_amd_ddt_t *tdt, int type, int op, void *stream) {
+    if (op == OMPI_AMD_OP_NO_OP) return OMPI_AMD_ERR_BAD_PARAM;  // MPI_Accumulate forbids it
+    return acc_ddt(w, origin, ocount, odt, nullptr, 0, nullptr, target, disp, tcount, tdt, type, op,
+                   stream);
+}
+
+int ompi_amd_get_accumulate_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount,
+                                const ompi_amd_ddt_t *odt, void *result, size_t rcount,
+                                const ompi_amd_ddt_t *rdt, int target, size_t disp, size_t tcount,
+                                const ompi_amd_ddt_t *tdt, int type, int op, void *stream) {
+    if (!result && tcount) return OMPI_AMD_ERR_BAD_PARAM;
+    return acc_ddt(w, origin, ocount, odt, result, rcount, rdt, target, disp, tcount, tdt, type, op,
+                   stream);
+}
+
 int ompi_amd_fetch_and_op(ompi_amd_win_t *w, const void *origin, void *result, int type,
                           int target, size_t disp, int op, void *stream) {
     return ompi_amd_get_accumulate(w, origin, result, 1, type, target, disp, op, stream);
@@ -1239,6 +1437,28 @@ int ompi_amd_rget_accumulate(ompi_amd_win_t *w, const void *origin, void *result
     return rma_request(w, stream,
                        ompi_amd_get_accumulate(w, origin, result, count, type, target, disp, op,
                                                stream), req);
+}
+
+int ompi_amd_raccumulate_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount,
+                             const ompi_amd_ddt_t *odt, int target, size_t disp, size_t tcount,
+                             const ompi_amd_ddt_t *tdt, int type, int op, void *stream,
+                             ompi_amd_rma_request_t **req) {
+    if (!req) return OMPI_AMD_ERR_BAD_PARAM;
+    return rma_request(w, stream,
+                       ompi_amd_accumulate_ddt(w, origin, ocount, odt, target, disp, tcount, tdt,
+                                               type, op, stream), req);
+}
+
+int ompi_amd_rget_accumulate_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount,
+                                 const ompi_amd_ddt_t *odt, void *result, size_t rcount,
+                                 const ompi_amd_ddt_t *rdt, int target, size_t disp,
+                                 size_t tcount, const ompi_amd_ddt_t *tdt, int type, int op,
+                                 void *stream, ompi_amd_rma_request_t **req) {
+    if (!req) return OMPI_AMD_ERR_BAD_PARAM;
+    return rma_request(w, stream,
+                       ompi_amd_get_accumulate_ddt(w, origin, ocount, odt, result, rcount, rdt,
+                                                   target, disp, tcount, tdt, type, op, stream),
+                       req);
 }
 
 int ompi_amd_rma_test(ompi_amd_rma_request_t *r, int *done) {

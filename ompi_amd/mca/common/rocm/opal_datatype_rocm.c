@@ -590,6 +590,11 @@ int opal_rocm_device_program(const opal_datatype_t *dt)
     return NULL != program_of(dt, 1);
 }
 
+const ompi_amd_ddt_t *opal_rocm_device_ddt(const opal_datatype_t *dt)
+{
+    return program_of(dt, 1);
+}
+
 int opal_rocm_pack_device(const opal_datatype_t *dt, size_t count, const void *src, void *packed,
                           void *stream)
 {

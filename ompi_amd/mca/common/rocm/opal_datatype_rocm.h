@@ -27,6 +27,7 @@
 #include <sys/uio.h>
 
 #include "opal/datatype/opal_convertor.h"
+#include "ompi_amd_ddt.h"
 #if OPAL_CUDA_SUPPORT
 #include "opal/datatype/opal_datatype_cuda.h"
 
@@ -105,6 +106,9 @@ int opal_rocm_pack_device(const opal_datatype_t *dt, size_t count, const void *s
                           void *stream);
 /* 1 when dt has a device program (the two calls above can take it) */
 int opal_rocm_device_program(const opal_datatype_t *dt);
+/* dt's device program itself (NULL: none) — osc/rocm's derived-datatype
+ * accumulates (ompi_amd_accumulate_ddt) */
+const ompi_amd_ddt_t *opal_rocm_device_ddt(const opal_datatype_t *dt);
 int opal_rocm_unpack_device(const opal_datatype_t *dt, size_t count, const void *packed, void *dst,
                             void *stream);
 

@@ -168,15 +168,62 @@ static int acc_ok(struct ompi_datatype_t *odt, int ocount, struct ompi_datatype_
     return ompi_amd_op_supported(op->o_f_to_c_index, t) == 1;
 }
 
+/* Derived datatypes (osc_sm_comm.c:301, 350 -> ompi_osc_base_sndrcv_op):
+ * every side built from one predefined type op/base provides the op on
+ * (REPLACE / NO_OP on any); each side either that type contiguous (program
+ * NULL, count in elements) or a datatype with a device program
+ * (common/rocm's cache of the convertor's programs). */
+struct opal_datatype_t;
+const ompi_amd_ddt_t *opal_rocm_device_ddt(const struct opal_datatype_t *dt);
+
+typedef struct {
+    int type;                    /* op/base type code of the primitive */
+    const ompi_amd_ddt_t *prog;  /* NULL: `type` contiguous */
+    size_t count;
+} ddt_side;
+
+static int ddt_side_of(struct ompi_datatype_t *dt, int count, int prim_id, ddt_side *out)
+{
+    struct ompi_datatype_t *p = ompi_datatype_get_single_predefined_type_from_args(dt);
+    if (NULL == p || (prim_id >= 0 && p->id != prim_id) || type_code(p) < 0) return 0;
+    out->type = type_code(p);
+    if (ompi_datatype_is_predefined(dt) && ompi_datatype_is_contiguous_memory_layout(dt, count)) {
+        out->prog = NULL;
+        out->count = (size_t) count;
+        return 1;
+    }
+    /* an ompi_datatype_t begins with its opal_datatype_t (ompi_datatype.h:70-71) */
+    out->prog = opal_rocm_device_ddt((const struct opal_datatype_t *) dt);
+    out->count = (size_t) count;
+    return NULL != out->prog;
+}
+
+static int acc_ddt_ok(struct ompi_datatype_t *odt, int ocount, struct ompi_datatype_t *tdt,
+                      int tcount, struct ompi_op_t *op, ddt_side *o, ddt_side *t)
+{
+    const int idx = op->o_f_to_c_index;
+    if (!ompi_op_is_intrinsic(op) || !ddt_side_of(tdt, tcount, -1, t)) return 0;
+    struct ompi_datatype_t *prim = ompi_datatype_get_single_predefined_type_from_args(tdt);
+    if (OMPI_AMD_OP_NO_OP != idx && !ddt_side_of(odt, ocount, prim->id, o)) return 0;
+    if (OMPI_AMD_OP_REPLACE == idx || OMPI_AMD_OP_NO_OP == idx) return 1;
+    return ompi_amd_op_supported(idx, t->type) == 1;
+}
+
 static int rocm_accumulate(const void *origin, int ocount, struct ompi_datatype_t *odt,
                            int target, ptrdiff_t disp, int tcount, struct ompi_datatype_t *tdt,
                            struct ompi_op_t *op, struct ompi_win_t *win)
 {
+    ddt_side o, t;
     if (0 == ocount) return OMPI_SUCCESS;
-    if (!acc_ok(odt, ocount, tdt, tcount, op) || disp < 0) return OMPI_ERR_NOT_SUPPORTED;
-    return to_ompi_err(ompi_amd_accumulate(mod(win)->dev_win, origin, (size_t) ocount,
-                                           type_code(tdt), target, (size_t) disp,
-                                           op->o_f_to_c_index, NULL));
+    if (disp < 0) return OMPI_ERR_NOT_SUPPORTED;
+    if (acc_ok(odt, ocount, tdt, tcount, op))
+        return to_ompi_err(ompi_amd_accumulate(mod(win)->dev_win, origin, (size_t) ocount,
+                                               type_code(tdt), target, (size_t) disp,
+                                               op->o_f_to_c_index, NULL));
+    if (!acc_ddt_ok(odt, ocount, tdt, tcount, op, &o, &t)) return OMPI_ERR_NOT_SUPPORTED;
+    return to_ompi_err(ompi_amd_accumulate_ddt(mod(win)->dev_win, origin, o.count, o.prog, target,
+                                               (size_t) disp, t.count, t.prog, t.type,
+                                               op->o_f_to_c_index, NULL));
 }
 
 static int rocm_get_accumulate(const void *origin, int ocount, struct ompi_datatype_t *odt,
@@ -185,13 +232,22 @@ static int rocm_get_accumulate(const void *origin, int ocount, struct ompi_datat
                                struct ompi_op_t *op, struct ompi_win_t *win)
 {
     const int no_op = ompi_op_is_intrinsic(op) && OMPI_AMD_OP_NO_OP == op->o_f_to_c_index;
+    ddt_side o = {0, NULL, 0}, t, r;
     if (0 == tcount) return OMPI_SUCCESS;
-    if (rdt->id != tdt->id || rcount != tcount || disp < 0 ||
-        !acc_ok(no_op ? tdt : odt, no_op ? tcount : ocount, tdt, tcount, op))
+    if (disp < 0) return OMPI_ERR_NOT_SUPPORTED;
+    if (rdt->id == tdt->id && rcount == tcount &&
+        acc_ok(no_op ? tdt : odt, no_op ? tcount : ocount, tdt, tcount, op))
+        return to_ompi_err(ompi_amd_get_accumulate(mod(win)->dev_win, no_op ? NULL : origin,
+                                                   result, (size_t) tcount, type_code(tdt),
+                                                   target, (size_t) disp, op->o_f_to_c_index,
+                                                   NULL));
+    if (!acc_ddt_ok(odt, ocount, tdt, tcount, op, &o, &t) ||
+        !ddt_side_of(rdt, rcount, ompi_datatype_get_single_predefined_type_from_args(tdt)->id, &r))
         return OMPI_ERR_NOT_SUPPORTED;
-    return to_ompi_err(ompi_amd_get_accumulate(mod(win)->dev_win, no_op ? NULL : origin, result,
-                                               (size_t) tcount, type_code(tdt), target,
-                                               (size_t) disp, op->o_f_to_c_index, NULL));
+    return to_ompi_err(ompi_amd_get_accumulate_ddt(mod(win)->dev_win, no_op ? NULL : origin,
+                                                   o.count, o.prog, result, r.count, r.prog,
+                                                   target, (size_t) disp, t.count, t.prog, t.type,
+                                                   op->o_f_to_c_index, NULL));
 }
 
 static int rocm_fetch_and_op(const void *origin, void *result, struct ompi_datatype_t *dt,
@@ -456,11 +512,17 @@ static int rocm_raccumulate(const void *origin, int ocount, struct ompi_datatype
                             struct ompi_op_t *op, struct ompi_win_t *win, ompi_request_t **request)
 {
     ompi_amd_rma_request_t *rma = NULL;
-    if (0 != ocount && (!acc_ok(odt, ocount, tdt, tcount, op) || disp < 0))
-        return OMPI_ERR_NOT_SUPPORTED;
-    return rma_wrap(ompi_amd_raccumulate(mod(win)->dev_win, origin, (size_t) ocount,
-                                         0 != ocount ? type_code(tdt) : 0, target, (size_t) disp,
-                                         op->o_f_to_c_index, NULL, &rma), &rma, win, request);
+    ddt_side o, t;
+    if (0 != ocount && disp < 0) return OMPI_ERR_NOT_SUPPORTED;
+    if (0 == ocount || acc_ok(odt, ocount, tdt, tcount, op))
+        return rma_wrap(ompi_amd_raccumulate(mod(win)->dev_win, origin, (size_t) ocount,
+                                             0 != ocount ? type_code(tdt) : 0, target,
+                                             (size_t) disp, op->o_f_to_c_index, NULL, &rma),
+                        &rma, win, request);
+    if (!acc_ddt_ok(odt, ocount, tdt, tcount, op, &o, &t)) return OMPI_ERR_NOT_SUPPORTED;
+    return rma_wrap(ompi_amd_raccumulate_ddt(mod(win)->dev_win, origin, o.count, o.prog, target,
+                                             (size_t) disp, t.count, t.prog, t.type,
+                                             op->o_f_to_c_index, NULL, &rma), &rma, win, request);
 }
 
 static int rocm_rget_accumulate(const void *origin, int ocount, struct ompi_datatype_t *odt,
@@ -471,13 +533,22 @@ static int rocm_rget_accumulate(const void *origin, int ocount, struct ompi_data
 {
     ompi_amd_rma_request_t *rma = NULL;
     const int no_op = ompi_op_is_intrinsic(op) && OMPI_AMD_OP_NO_OP == op->o_f_to_c_index;
-    if (0 != tcount && (rdt->id != tdt->id || rcount != tcount || disp < 0 ||
-                        !acc_ok(no_op ? tdt : odt, no_op ? tcount : ocount, tdt, tcount, op)))
+    ddt_side o = {0, NULL, 0}, t, r;
+    if (0 != tcount && disp < 0) return OMPI_ERR_NOT_SUPPORTED;
+    if (0 == tcount || (rdt->id == tdt->id && rcount == tcount &&
+                        acc_ok(no_op ? tdt : odt, no_op ? tcount : ocount, tdt, tcount, op)))
+        return rma_wrap(ompi_amd_rget_accumulate(mod(win)->dev_win, no_op ? NULL : origin, result,
+                                                 (size_t) tcount, 0 != tcount ? type_code(tdt) : 0,
+                                                 target, (size_t) disp, op->o_f_to_c_index, NULL,
+                                                 &rma), &rma, win, request);
+    if (!acc_ddt_ok(odt, ocount, tdt, tcount, op, &o, &t) ||
+        !ddt_side_of(rdt, rcount, ompi_datatype_get_single_predefined_type_from_args(tdt)->id, &r))
         return OMPI_ERR_NOT_SUPPORTED;
-    return rma_wrap(ompi_amd_rget_accumulate(mod(win)->dev_win, no_op ? NULL : origin, result,
-                                             (size_t) tcount, 0 != tcount ? type_code(tdt) : 0,
-                                             target, (size_t) disp, op->o_f_to_c_index, NULL,
-                                             &rma), &rma, win, request);
+    return rma_wrap(ompi_amd_rget_accumulate_ddt(mod(win)->dev_win, no_op ? NULL : origin,
+                                                 o.count, o.prog, result, r.count, r.prog, target,
+                                                 (size_t) disp, t.count, t.prog, t.type,
+                                                 op->o_f_to_c_index, NULL, &rma),
+                    &rma, win, request);
 }
 
 /* MPI_Win_shared_query (osc_sm_component.c:455-485): baseptr points to a

@@ -195,6 +195,29 @@ class Window:
                                                      _stream(stream)),
                    f"get_accumulate({op.name}, {datatype.name})")
 
+    @staticmethod
+    def _ddt(dt):
+        return None if dt is None else dt.commit()._handle
+
+    def accumulate_ddt(self, origin, ocount: int, odt, target: int, disp: int, tcount: int, tdt,
+                       prim: Datatype, op: Op, stream=None) -> None:
+        """MPI_Accumulate with derived datatypes (ompi_osc_base_sndrcv_op):
+        odt / tdt are ompi_amd.datatype.Datatype (None: `prim` contiguous)
+        built from the predefined `prim`."""
+        _lib.check(self._lib.ompi_amd_accumulate_ddt(self._h, _ptr(origin), ocount, self._ddt(odt),
+                                                     target, disp, tcount, self._ddt(tdt), prim.code,
+                                                     op.index, _stream(stream)),
+                   f"accumulate_ddt({op.name}, {prim.name})")
+
+    def get_accumulate_ddt(self, origin, ocount: int, odt, result, rcount: int, rdt, target: int,
+                           disp: int, tcount: int, tdt, prim: Datatype, op: Op,
+                           stream=None) -> None:
+        optr = _ptr(origin) if origin is not None else None
+        _lib.check(self._lib.ompi_amd_get_accumulate_ddt(
+            self._h, optr, ocount, self._ddt(odt), _ptr(result), rcount, self._ddt(rdt), target,
+            disp, tcount, self._ddt(tdt), prim.code, op.index, _stream(stream)),
+            f"get_accumulate_ddt({op.name}, {prim.name})")
+
     def fetch_and_op(self, origin, result, datatype: Datatype, target: int, disp: int, op: Op,
                      stream=None) -> None:
         optr = _ptr(origin) if origin is not None else None

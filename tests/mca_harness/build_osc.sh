@@ -6,7 +6,7 @@ set -e
 H=$(cd "$(dirname "$0")" && pwd)
 R=$(cd "$H/../.." && pwd)
 OUT=${1:-$H/osc_harness}
-gcc -std=gnu11 -O1 -Wall -Wextra -Wno-unused-parameter -Wno-missing-field-initializers \
+gcc -std=gnu11 -O1 -DHARNESS_OSC -Wall -Wextra -Wno-unused-parameter -Wno-missing-field-initializers \
     -I"$H/osc_include" -I"$H/coll_include" -I"$H/include" -I"$R/include" \
     -I"$R/ompi_amd/mca/osc/rocm" -I/opt/rocm/include \
     "$R/ompi_amd/mca/osc/rocm/osc_rocm_component.c" "$H/osc_harness.c" "$H/dev_helpers.c" "$H/progress_stub.c" \

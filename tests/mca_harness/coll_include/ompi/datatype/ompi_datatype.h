@@ -36,6 +36,9 @@ static inline int ompi_datatype_get_true_extent(const ompi_datatype_t *d, ptrdif
     *ext = (ptrdiff_t) d->size;
     return 0;
 }
+/* ompi/datatype/ompi_datatype.h (ompi_datatype_args.c:825; harness:
+ * dev_helpers.c, HARNESS_OSC) */
+ompi_datatype_t *ompi_datatype_get_single_predefined_type_from_args(ompi_datatype_t *type);
 /* ompi/datatype/ompi_datatype.h:303-304 (harness: dev_helpers.c, any
  * residency) */
 int32_t ompi_datatype_sndrcv(const void *sbuf, int32_t scount, const ompi_datatype_t *sdtype,

@@ -80,3 +80,41 @@ int opal_rocm_unpack_device(const struct opal_datatype_t *dt, size_t count, cons
     return whole2d((const ompi_datatype_t *) dt, count, dst, (void *) packed, 1);
 }
 #endif
+
+#ifdef HARNESS_OSC
+#include "ompi/datatype/ompi_datatype.h"
+#include "ompi_amd_ddt.h"
+/* ompi_datatype_args.c:825-865 over the stand-in types: a predefined type
+ * is its own primitive; a gapped stand-in (contiguous == 0: `size` data
+ * bytes every 2 * `size`) is built from the predefined type of its id */
+ompi_datatype_t *ompi_datatype_get_single_predefined_type_from_args(ompi_datatype_t *type)
+{
+    static ompi_datatype_t prim[64];
+    if (type->predefined) return type;
+    if (type->id < 0 || type->id >= 64) return (ompi_datatype_t *) 0;
+    prim[type->id] = (ompi_datatype_t){type->id, type->size, 1, 1};
+    return &prim[type->id];
+}
+
+/* common/rocm's device program of a datatype (opal_datatype_rocm.c) for the
+ * stand-in types: one run of `size` bytes, extent 2 * `size` (gapped) */
+struct opal_datatype_t;
+int harness_device_ddts;
+const ompi_amd_ddt_t *opal_rocm_device_ddt(const struct opal_datatype_t *dt)
+{
+    static struct { const void *dt; ompi_amd_ddt_t *prog; } cache[16];
+    static int n;
+    const ompi_datatype_t *d = (const ompi_datatype_t *) dt;
+    for (int i = 0; i < n; ++i)
+        if (cache[i].dt == dt) return cache[i].prog;
+    ompi_amd_ddt_elem_t e = {1, (int64_t) d->size, (int64_t) d->size, 0};
+    ompi_amd_ddt_t *prog = 0;
+    if (n == 16 || ompi_amd_ddt_create_elems(&e, 1, (int64_t) (d->contiguous ? d->size : 2 * d->size),
+                                             &prog) != 0)
+        return 0;
+    ++harness_device_ddts;
+    cache[n].dt = dt;
+    cache[n++].prog = prog;
+    return prog;
+}
+#endif

@@ -153,6 +153,59 @@ int main(int argc, char **argv)
     orc_op_2buff(ORC_OP_SUM, ORC_T_FLOAT, org_rank, init_nxt, n);
     CHECK(0 == memcmp(got, init_nxt, n * 4), "get of the next window");
 
+    /* derived datatypes (osc_sm_comm.c:301, 350 -> ompi_osc_base_sndrcv_op):
+     * a gapped stand-in float type (4 data bytes every 8) at the target and
+     * result; expected values from op/base slot by slot in type-map order */
+    {
+        ompi_datatype_t dgap = {ORC_T_FLOAT, 4, 0, 0};
+        ompi_op_t max = {OMPI_OP_FLAGS_INTRINSIC, ORC_OP_MAX};
+        const size_t k = 4001;
+        float *slots = malloc(k * 4), *oprv = malloc(n * 4), *mine = malloc(n * 4);
+        float *nxtw = malloc(n * 4), *fetched = malloc(2 * k * 4), *pattern = malloc(2 * k * 4);
+        size_t j;
+        extern int harness_device_ddts;
+        fill_exact(oprv, n, prv, 2);
+        memcpy(mine, init, n * 4);  /* my window now: init + prv's origin */
+        orc_op_2buff(ORC_OP_SUM, ORC_T_FLOAT, oprv, mine, n);
+        memcpy(nxtw, init_nxt, n * 4);  /* the next window now */
+        CHECK(m->osc_accumulate(dorg, (int) k, &dfloat, nxt, 0, (int) k, &dgap, &max, &win) ==
+                  OMPI_SUCCESS, "derived-target accumulate");
+        CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence derived 1");
+        for (j = 0; j < k; ++j) slots[j] = mine[2 * j];
+        orc_op_2buff(ORC_OP_MAX, ORC_T_FLOAT, oprv, slots, k);
+        for (j = 0; j < k; ++j) mine[2 * j] = slots[j];
+        for (j = 0; j < k; ++j) slots[j] = nxtw[2 * j];
+        orc_op_2buff(ORC_OP_MAX, ORC_T_FLOAT, org, slots, k);
+        for (j = 0; j < k; ++j) nxtw[2 * j] = slots[j];
+        CHECK(harness_dev_copy_back(got, dbase, n * 4) == 0, "copy back derived 1");
+        CHECK(0 == memcmp(got, mine, n * 4), "derived MAX accumulated into every other float");
+        /* get_accumulate SUM: the old slots into a gapped result */
+        fill_exact(pattern, 2 * k, g_rank, 77);
+        CHECK(harness_dev_copy_in(dgot, pattern, 2 * k * 4) == 0, "result pattern");
+        CHECK(m->osc_get_accumulate(dorg, (int) k, &dfloat, dgot, (int) k, &dgap, nxt, 0, (int) k,
+                                    &dgap, &sum, &win) == OMPI_SUCCESS, "derived get_accumulate");
+        CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence derived 2");
+        CHECK(harness_dev_copy_back(fetched, dgot, 2 * k * 4) == 0, "copy back fetched");
+        for (j = 0; j < k; ++j) {
+            CHECK(0 == memcmp(&fetched[2 * j], &nxtw[2 * j], 4), "fetched slot %zu", j);
+            CHECK(0 == memcmp(&fetched[2 * j + 1], &pattern[2 * j + 1], 4), "result gap %zu", j);
+        }
+        for (j = 0; j < k; ++j) slots[j] = mine[2 * j];
+        orc_op_2buff(ORC_OP_SUM, ORC_T_FLOAT, oprv, slots, k);
+        for (j = 0; j < k; ++j) mine[2 * j] = slots[j];
+        CHECK(harness_dev_copy_back(got, dbase, n * 4) == 0, "copy back derived 2");
+        CHECK(0 == memcmp(got, mine, n * 4), "derived get_accumulate summed");
+        CHECK(harness_device_ddts > 0, "the device programs were used");
+        CHECK(m->osc_accumulate(dorg, 3, &dfloat, nxt, 0, 3, &dgap, &user, &win) ==
+                  OMPI_ERR_NOT_SUPPORTED, "user op on a derived type refused");
+        /* the window as the next sections expect it: init + prv's origin */
+        memcpy(mine, init, n * 4);
+        orc_op_2buff(ORC_OP_SUM, ORC_T_FLOAT, oprv, mine, n);
+        CHECK(harness_dev_copy_in(dbase, mine, n * 4) == 0, "restore window");
+        CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence derived 3");
+        free(slots), free(oprv), free(mine), free(nxtw), free(fetched), free(pattern);
+    }
+
     /* passive target: each rank puts its rank id at displacement `rank` of
      * rank 0's window under an exclusive lock */
     {

@@ -410,6 +410,121 @@ def case_get_accumulate(comm, rank, n, salt, count=50001):
         win.free()
 
 
+def _slots(dt, count, elem):
+    """Byte offsets of the `elem`-byte primitive slots of count x dt, in
+    type-map order (what ompi_osc_base_sndrcv_op walks)."""
+    offs = []
+    for i in range(count):
+        for d, bl in dt.runs:
+            offs.extend(i * dt.extent + d + b for b in range(0, bl, elem))
+    return np.array(offs, dtype=np.int64)
+
+
+def case_acc_ddt(comm, rank, n, salt):
+    """MPI_Accumulate / MPI_Get_accumulate with derived datatypes
+    (osc_sm_comm.c:301, 350 -> ompi_osc_base_sndrcv_op): each rank updates
+    the next rank's window through a target datatype (vector, blacs-style
+    indexed), from a contiguous or a strided origin, with SUM, MAX (specials),
+    REPLACE, and get_accumulate into a strided result; expected values from
+    the oracle's op/base restatement applied slot by slot in type-map order
+    (bit-exact), gaps of the window untouched."""
+    from ompi_amd import datatype as dd
+    F, D = mop.MPI_FLOAT, mop.MPI_DOUBLE
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    f32, f64 = dd.predefined("MPI_FLOAT"), dd.predefined("MPI_DOUBLE")
+    lens = [13, 13, 13, 13, 13, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1]
+    disps = [286, 308, 330, 352, 374, 396, 419, 442, 465, 488, 511, 534, 557, 580, 603, 626, 649, 672]
+    runs = [
+        # (name, prim, target type, tcount, origin type or None, op, kind)
+        ("vector_sum", F, dd.type_vector(997, 3, 7, f32), 3, None, mop.MPI_SUM, "R"),
+        ("indexed_max", F, dd.type_indexed(lens, disps, f32), 40, dd.type_vector(40 * 156, 1, 2, f32),
+         mop.MPI_MAX, "S"),
+        ("vector_replace", D, dd.type_vector(501, 2, 5, f64), 2, dd.type_vector(1002, 2, 3, f64),
+         mop.MPI_REPLACE, "R"),
+        ("contig_target_min", D, None, 4001, dd.type_vector(4001, 1, 3, f64), mop.MPI_MIN, "S"),
+    ]
+    disp_unit, disp = 4, 6  # the target region starts 24 B into the window
+    for k, (name, prim, tdt, tcount, odt, op, kind) in enumerate(runs):
+        el = prim.extent
+        m = (tdt.size * tcount if tdt else el * tcount) // el  # primitive elements
+        span = ((tcount - 1) * tdt.extent + tdt.true_span) if tdt else m * el
+        wbytes = disp * disp_unit + span + 64
+        init = [np.frombuffer(payload(r, salt + k, wbytes), np.uint8).copy() for r in range(n)]
+        for r in range(n):  # real values in the window (gaps keep their payload bytes)
+            vals = fp_inputs(prim, wbytes // el, r, salt + 10 + k, kind)
+            init[r][:(wbytes // el) * el] = vals.view(np.uint8)
+        org_packed = [fp_inputs(prim, m, r, salt + 20 + k, kind) for r in range(n)]
+        if odt is None:
+            org_buf = [p_.view(np.uint8) for p_ in org_packed]
+            ocount = m
+        else:  # the packed values at the origin type's slots, junk between
+            ocount = 1
+            assert odt.size == m * el
+            oslots = _slots(odt, 1, el)
+            org_buf = []
+            for r in range(n):
+                b = np.frombuffer(payload(r, salt + 30 + k, int(oslots.max()) + el), np.uint8).copy()
+                for j, o in enumerate(oslots):
+                    b[o:o + el] = org_packed[r][j:j + 1].view(np.uint8)
+                org_buf.append(b)
+        base = dev(init[rank])
+        win = osc.Window.create(comm, base, wbytes, disp_unit=disp_unit)
+        try:
+            o = dev(org_buf[rank])
+            win.fence(stream=STREAM)
+            win.accumulate_ddt(o, ocount, odt, nxt, disp, tcount, tdt, prim, op, stream=STREAM)
+            win.fence(stream=STREAM, blocking=True)
+            exp = init[rank].copy()
+            tslots = disp * disp_unit + (_slots(tdt, tcount, el) if tdt else np.arange(m) * el)
+            cur = np.concatenate([exp[t:t + el] for t in tslots]).view(prim.np_dtype).copy()
+            if op is mop.MPI_REPLACE:
+                cur = org_packed[prv].copy()
+            else:
+                orc.op_2buff(op.index, prim.code, org_packed[prv].copy(), cur, m)
+            cb = cur.view(np.uint8)
+            for j, t in enumerate(tslots):
+                exp[t:t + el] = cb[j * el:(j + 1) * el]
+            ok, msg = eq(host(base), exp, f"{name}: window")
+            if not ok:
+                return ok, msg
+        finally:
+            win.free()
+        comm_barrier()
+    # get_accumulate: the old target slots into a strided result, then SUM
+    tdt, tcount, prim = dd.type_vector(333, 2, 5, f32), 4, F
+    rdt = dd.type_vector(333 * 2 * 4, 1, 2, f32)
+    el, m = 4, 333 * 2 * 4
+    span = (tcount - 1) * tdt.extent + tdt.true_span
+    wbytes = span + 64
+    init = [fp_inputs(prim, wbytes // 4, r, salt + 50, "E").view(np.uint8).copy() for r in range(n)]
+    org = [fp_inputs(prim, m, r, salt + 51, "E") for r in range(n)]
+    base = dev(init[rank])
+    win = osc.Window.create(comm, base, wbytes, disp_unit=1)
+    try:
+        o = dev(org[rank])
+        res = zeros(2 * m * 4)
+        win.fence(stream=STREAM)
+        win.get_accumulate_ddt(o, m, None, res, 1, rdt, nxt, 0, tcount, tdt, prim, mop.MPI_SUM,
+                               stream=STREAM)
+        win.fence(stream=STREAM, blocking=True)
+        tslots = _slots(tdt, tcount, 4)
+        old = np.concatenate([init[nxt][t:t + 4] for t in tslots]).view(np.float32)
+        got = host(res).view(np.float32)
+        ok, msg = eq(got[0::2], old, "get_accumulate: fetched into the strided result")
+        if not ok:
+            return ok, msg
+        ok, msg = eq(got[1::2], np.zeros(m, np.float32), "get_accumulate: result gaps untouched")
+        if not ok:
+            return ok, msg
+        exp = init[rank].copy()
+        mine_old = np.concatenate([exp[t:t + 4] for t in tslots]).view(np.float32) + org[prv]
+        for j, t in enumerate(tslots):
+            exp[t:t + 4] = mine_old[j:j + 1].view(np.uint8)
+        return eq(host(base), exp, "get_accumulate: window")
+    finally:
+        win.free()
+
+
 def case_fetch_and_op_counter(comm, rank, n, k=25):
     """Shared counter on rank 0: k fetch_and_op(+1) per rank; the fetched
     values over all ranks are exactly 0 .. n*k-1 (each increment atomic)."""
@@ -785,6 +900,7 @@ def main():
         ("osc_acc_concurrent_maxloc",
          lambda: case_acc_concurrent(comm, rank, n, DI, mop.MPI_MAXLOC, 30001, 91)),
         ("osc_get_accumulate", lambda: case_get_accumulate(comm, rank, n, 92)),
+        ("osc_accumulate_derived_datatypes", lambda: case_acc_ddt(comm, rank, n, 150)),
         ("osc_fetch_and_op_counter", lambda: case_fetch_and_op_counter(comm, rank, n)),
         ("osc_compare_and_swap", lambda: case_cas(comm, rank, n)),
         ("osc_passive_exclusive_rmw", lambda: case_passive_exclusive(comm, rank, n)),
