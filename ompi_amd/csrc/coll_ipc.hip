@@ -461,9 +461,12 @@ struct ompi_amd_comm {
     int zero_copy = 1;
     int64_t timeout_ms = 30000;
     int max_blocks = 1024;
-    // pipelined schemes: elements of a slice ~ pipe_slice bytes (param
-    // "pipe_slice"); pipe_seq numbers the pipelined calls (flag values)
-    int64_t pipe_slice = 16 << 10;
+    // pipelined schemes: every workgroup of the grid runs pipe_passes
+    // slices of each block (param "pipe_passes"), none under pipe_slice
+    // bytes (param "pipe_slice"; smaller messages use fewer workgroups);
+    // pipe_seq numbers the pipelined calls (flag values)
+    int64_t pipe_slice = 64 << 10;
+    int pipe_passes = 1;
     uint64_t pipe_seq = 0;
     int colocated = 1;  // most ranks of this communicator on one GPU (pipe_args.colocated)
     int algorithm = 2;                    // push: push-gather in the staged mode (no staging copy)
@@ -1861,13 +1864,17 @@ static int launch_pipe(ompi_amd_comm_t *c, int op, int type, const void *src, vo
     a.nt = c->copy_nt ? 1 : 0;
     a.colocated = c->colocated;
     blockcount(count, n, &a.split, &a.early, &a.late);
-    // slices: whole 16-B vectors of ~pipe_slice bytes; every workgroup gets
-    // at least one (small blocks: smaller slices, then fewer workgroups)
+    // slices: whole 16-B vectors, pipe_passes per workgroup of the grid,
+    // none under pipe_slice bytes.  Each pass costs the workgroup one
+    // system-scope release and acquire (L2 write-back / invalidate): on one
+    // shared GPU, 16 KiB slices (32 passes) ran 2.7x the phased scheme,
+    // >= 1 MiB slices (one pass) 0.89x it for the staged pull at N = 2,
+    // 256 MiB (profiles/r04_pipe_slices_n2.jsonl)
     const int64_t E = std::max<int64_t>(1, 16 / ext);
     const int64_t groups_max = std::max(1, std::min(c->max_blocks, kPipeMaxGroups));
-    int64_t per = std::max<int64_t>(E, (c->pipe_slice / ext) / E * E);
-    if ((a.early + per - 1) / per < groups_max)
-        per = std::max<int64_t>(E, ((a.early + groups_max - 1) / groups_max + E - 1) / E * E);
+    const int64_t want = groups_max * std::max(1, c->pipe_passes);
+    int64_t per = ((a.early + want - 1) / want + E - 1) / E * E;
+    per = std::max<int64_t>(per, std::max<int64_t>(E, (c->pipe_slice / ext + E - 1) / E * E));
     a.per = per;
     a.nslices = std::max<int64_t>(1, (a.early + per - 1) / per);
     const int64_t groups = std::min(groups_max, a.nslices);
@@ -2693,6 +2700,9 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
     } else if (!strcmp(key, "pipe_slice")) {
         if (v < 16 || v > (64 << 20)) return OMPI_AMD_ERR_BAD_PARAM;
         c->pipe_slice = v;
+    } else if (!strcmp(key, "pipe_passes")) {
+        if (v < 1 || v > 4096) return OMPI_AMD_ERR_BAD_PARAM;
+        c->pipe_passes = (int)v;
     } else if (!strcmp(key, "force_shadow")) {
         c->force_shadow = v ? 1 : 0;
     } else if (!strcmp(key, "user_ipc")) {
@@ -2720,6 +2730,7 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     if (!strcmp(key, "small_bytes")) *v = (int64_t)c->small_bytes;
     else if (!strcmp(key, "zero_copy")) *v = c->zero_copy;
     else if (!strcmp(key, "pipe_slice")) *v = c->pipe_slice;
+    else if (!strcmp(key, "pipe_passes")) *v = c->pipe_passes;
     else if (!strcmp(key, "pipe_calls")) *v = (int64_t)c->pipe_seq;
     else if (!strcmp(key, "colocated")) *v = c->colocated;
     else if (!strcmp(key, "timeout_ms")) *v = (int64_t)c->timeout_ms;

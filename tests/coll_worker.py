@@ -475,8 +475,8 @@ def case_pipe(comm, rank, n, salt, big):
     """The pipelined schemes (param "algorithm" 4 push-gather, 5 push-land,
     6 staged pull: send, fold and gather of one call in one launch with
     per-slice flags, pipe_allreduce_kernel): bit-exact against the oracle on
-    dataset R at the default slice and at 256-B slices (many passes per
-    workgroup), ragged counts, in place, fp64 and MAXLOC, and on buffers 4 B
+    dataset R at the default (one pass per workgroup) and at 8 passes of
+    slices down to 256 B, ragged counts, in place, fp64 and MAXLOC, and on buffers 4 B
     off 16-B alignment (the kernel's scalar paths); every call must have run
     the pipelined launch (param pipe_calls)."""
     F, D, DI = mop.MPI_FLOAT, mop.MPI_DOUBLE, mop.MPI_DOUBLE_INT
@@ -484,8 +484,9 @@ def case_pipe(comm, rank, n, salt, big):
     try:
         for a in (4, 5, 6):
             comm.set_param("algorithm", a)
-            for sl in (16 << 10, 256):
+            for sl, passes in ((64 << 10, 1), (256, 8)):
                 comm.set_param("pipe_slice", sl)
+                comm.set_param("pipe_passes", passes)
                 runs = [(F, SUM, big + 5, False), (F, SUM, big, True), (D, SUM, big // 2 + 3, False),
                         (DI, mop.MPI_MAXLOC, 262147, False)]
                 for k, (dt, op, count, inplace) in enumerate(runs):
@@ -511,7 +512,8 @@ def case_pipe(comm, rank, n, salt, big):
                 return False, f"alg {a} misaligned: {mismatch(got, exp[rank])}"
         return True, f"{comm.get_param('pipe_calls')} pipelined calls, colocated {comm.get_param('colocated')}"
     finally:
-        comm.set_param("pipe_slice", 16 << 10)
+        comm.set_param("pipe_slice", 64 << 10)
+        comm.set_param("pipe_passes", 1)
         comm.set_param("algorithm", DEFAULT_ALG[0])
 
 
