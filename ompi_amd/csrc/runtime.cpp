@@ -117,21 +117,37 @@ namespace ompi_amd {
 // The op handlers classify every operand on every call (ompi_op_reduce has
 // no residency hint).  A pure-host reduction (op/avx or op/base underneath)
 // should not pay a runtime pointer query per operand per call: each thread
-// remembers the last 8 host regions it classified, at 2 MiB granularity.
-// Device allocations live in the GPU's own virtual-address aperture, never
-// in a range that was host memory, so a granule once seen as host stays
-// host; device pointers are always queried (the device path's cost is the
-// kernel anyway).
+// remembers the last 8 host regions it classified, at 2 MiB granularity —
+// only memory the runtime does not know at all (unregistered pageable:
+// hipPointerGetAttributes fails), never pinned, registered or managed
+// memory — and each remembered region is queried again after 1024 hits.
+// Limitation: if such a region is unmapped and its addresses
+// reused by an allocation the runtime does know (hipMallocManaged,
+// hipHostRegister, an imported allocation), up to 1024 further calls of
+// that thread may still classify it as host and take the host path; device
+// pointers proper (the GPU's own aperture) are always queried.
 int device_pointer_cached(const void *p) {
     static thread_local uintptr_t host_gran[8];  // granule + 1 (0 = empty)
+    static thread_local unsigned hits[8];
     static thread_local unsigned next;
     if (!p) return 0;
     const uintptr_t g = ((uintptr_t)p >> 21) + 1;
-    for (uintptr_t h : host_gran)
-        if (h == g) return 0;
-    const int d = ompi_amd_is_device_pointer(p);
-    if (!d) host_gran[next++ & 7] = g;
-    return d;
+    for (int i = 0; i < 8; ++i)
+        if (host_gran[i] == g) {
+            if (++hits[i] < 1024) return 0;
+            host_gran[i] = 0;  // stale for too long: ask the runtime again
+            break;
+        }
+    hipPointerAttribute_t attr;
+    memset(&attr, 0, sizeof(attr));
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {  // unregistered host memory
+        (void)hipGetLastError();
+        const unsigned k = next++ & 7;
+        host_gran[k] = g;
+        hits[k] = 0;
+        return 0;
+    }
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
 }  // namespace ompi_amd

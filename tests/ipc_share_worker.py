@@ -12,7 +12,10 @@ IPC registry (ompi_amd/csrc/ipc_registry.h) must hand both the same mapping
   3. a new window on A over X, then B is destroyed: the window's put / get
      stay byte-exact;
   4. a peer's freed + reallocated buffer mapped again: the registry retires
-     the stale mapping once (ipc_retired) and the result is exact.
+     the stale mapping once (ipc_retired) and the result is exact;
+  5. A's nonblocking allreduce launched on rank 0 only, while B's blocking
+     allreduce retires stale mappings there: B completes at once (only the
+     stale mappings' holders are quiesced) and both results are exact.
 
 Prints one JSON line per step; exits 0 only if all passed.
 """
@@ -136,6 +139,42 @@ def main():
         retired = B.get_param("ipc_retired") - retired0
         report("realloc_retires_once", ok and ok2, "; ".join(m for m in (msg, msg2) if m),
                ipc_retired=retired)
+        # 5. a deferred call of A launched on rank 0 but not yet on its peers
+        # while B's blocking call on rank 0 retires a stale mapping (ADVICE
+        # r3): the registry quiesces only the stale mapping's holders (B), so
+        # rank 0 does not wait for A's kernels — which wait on device for
+        # peers that sit in B's host rendezvous until rank 0 arrives
+        import time
+        A.set_param("user_ipc", 1)
+        A.set_param("algorithm", 0)
+        zs_h = [data(r, count, 14) for r in range(n)]
+        zexp, _ = orc.allreduce([z.copy() for z in zs_h], count, SUM.index, F.code)
+        zs = torch.from_numpy(zs_h[rank]).cuda()
+        zo = torch.zeros(count, device="cuda")
+        torch.cuda.synchronize()
+        del X
+        torch.cuda.empty_cache()
+        X = torch.zeros(count + 64, device="cuda")  # peers' B mappings of the old X go stale
+        torch.cuda.synchronize()
+        retired0 = B.get_param("ipc_retired")
+        dist.barrier()
+        if rank != 0:
+            req = A.iallreduce(zs, zo, count, F, SUM)   # posted, not launched here yet
+        dist.barrier()
+        if rank == 0:
+            req = A.iallreduce(zs, zo, count, F, SUM)   # every peer posted: launched on rank 0
+        t0 = time.time()
+        ok, msg = allreduce_check(X, 13)
+        dt = time.time() - t0
+        req.wait()
+        req.free()
+        torch.cuda.synchronize()
+        zgot = zo.cpu().numpy()
+        okz = np.array_equal(zgot.view(np.uint32), zexp[rank].view(np.uint32))
+        report("deferred_on_A_while_B_retires", ok and okz and dt < 10.0,
+               "; ".join(m for m in (msg, "" if okz else "A's iallreduce differs",
+                                     "" if dt < 10.0 else f"B's call took {dt:.1f} s") if m),
+               b_call_s=round(dt, 3), ipc_retired=B.get_param("ipc_retired") - retired0)
     except Exception as e:  # noqa: BLE001
         report("exception", False, f"{type(e).__name__}: {e}")
     torch.cuda.synchronize()
