@@ -423,6 +423,10 @@ struct ompi_amd_comm {
     std::mutex stream_mu;
     bool has_stream = false;
     hipStream_t cur_stream = nullptr;
+    // another communicator launched on cur_stream after this one's last
+    // launch there: stream_evs holds the mark of this one's end on it, and
+    // quiesce() must not synchronise the stream (note_stream)
+    bool cur_closed = false;
     std::vector<hipEvent_t> stream_evs;
     char *shadow = nullptr;               // export fallback of blocking calls (shadow_set)
     size_t shadow_bytes = 0;
@@ -962,9 +966,54 @@ static int import_all(ompi_amd_comm_t *c, const call_blob *all, const void *sbuf
 
 // Work this communicator put on a stream: note the stream; when the calls
 // move to another stream, an event marks the end of the old one's work.
+// The communicator that launched last on each stream (process-wide): when
+// another one launches there, an event marks where the first one's work on
+// that stream ends, so that quiescing it (the IPC registry retiring a
+// mapping it holds) waits for its own kernels only — not for a later
+// communicator's, which may be waiting on device for peers that are
+// themselves waiting for this rank (a deferred call of A
+// launched here, B retiring a mapping on the same stream).
+static std::mutex g_stream_owner_mu;
+static std::vector<std::pair<hipStream_t, ompi_amd_comm_t *>> g_stream_owner;
+
+static void mark_end(ompi_amd_comm_t *o, hipStream_t s) {
+    std::lock_guard<std::mutex> g(o->stream_mu);
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) {
+        if (hipEventRecord(e, s) == hipSuccess) o->stream_evs.push_back(e);
+        else hip_ignore(hipEventDestroy(e));
+    }
+    (void)hipGetLastError();
+    if (o->has_stream && o->cur_stream == s) o->cur_closed = true;
+}
+
+static void forget_streams(ompi_amd_comm_t *c) {
+    std::lock_guard<std::mutex> g(g_stream_owner_mu);
+    g_stream_owner.erase(std::remove_if(g_stream_owner.begin(), g_stream_owner.end(),
+                                        [&](const std::pair<hipStream_t, ompi_amd_comm_t *> &p) {
+                                            return p.second == c;
+                                        }),
+                         g_stream_owner.end());
+}
+
 static void note_stream(ompi_amd_comm_t *c, hipStream_t s) {
+    {
+        std::lock_guard<std::mutex> g(g_stream_owner_mu);
+        bool found = false;
+        for (auto &p : g_stream_owner)
+            if (p.first == s) {
+                if (p.second != c) mark_end(p.second, s);
+                p.second = c;
+                found = true;
+                break;
+            }
+        if (!found) g_stream_owner.emplace_back(s, c);
+    }
     std::lock_guard<std::mutex> g(c->stream_mu);
-    if (c->has_stream && c->cur_stream == s) return;
+    if (c->has_stream && c->cur_stream == s) {
+        c->cur_closed = false;
+        return;
+    }
     if (c->has_stream) {
         hipEvent_t e = nullptr;
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) {
@@ -984,6 +1033,7 @@ static void note_stream(ompi_amd_comm_t *c, hipStream_t s) {
     }
     c->cur_stream = s;
     c->has_stream = true;
+    c->cur_closed = false;
 }
 
 // Wait until every kernel this communicator launched has finished (its
@@ -1000,7 +1050,7 @@ static int quiesce(ompi_amd_comm_t *c) {
         std::lock_guard<std::mutex> g(c->stream_mu);
         evs.swap(c->stream_evs);
         cur = c->cur_stream;
-        has = c->has_stream;
+        has = c->has_stream && !c->cur_closed;  // closed: a mark in evs bounds it
     }
     int rc = OMPI_AMD_SUCCESS;
     for (hipEvent_t e : evs) {
@@ -2580,6 +2630,7 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
             if (e) hip_ignore(hipEventDestroy(e));
     if (c->p2p) p2p_destroy(c->p2p);
     c->boot.detach();
+    forget_streams(c);
     delete c;
     return OMPI_AMD_SUCCESS;
 }

@@ -226,7 +226,6 @@ struct ddt_period {
     int64_t map_bytes;  // LDS bytes holding the map (0: identity)
     const uint16_t *map;  // psize entries: typed offset - lowest, per packed byte
     int64_t nt;         // unpack: typed-side stores non-temporal
-    int64_t chunk;      // unpack launch: tiles per workgroup, contiguous (0: strided by the grid)
 };
 
 // Stage 16-B vectors [0, nv) of src into LDS (lane t: t, t + 256, ...),
@@ -355,13 +354,12 @@ __global__ __launch_bounds__(kDdtThreads) void ddt_pack_tile_kernel(ddt_period P
 template <int G, bool IDENT>
 __device__ __forceinline__ void unpack_tiles(const ddt_period &P, const char *contig, char *typed,
                                              int64_t start, int64_t j0, int64_t j1, int64_t tile0,
-                                             int64_t tstep, const uint16_t *map, char *data,
-                                             int64_t tlimit = INT64_MAX) {
+                                             int64_t tstep, const uint16_t *map, char *data) {
     using T = typename granule<G>::t;
     const int t = threadIdx.x;
     constexpr int64_t step = (int64_t)G * kDdtThreads;  // packed bytes per lane pass
     const int64_t st_j = step / P.psize, st_q = step % P.psize;
-    for (int64_t tile = tile0; tile < tlimit; tile += tstep) {
+    for (int64_t tile = tile0;; tile += tstep) {
         const int64_t jt = j0 + tile * P.nper;
         if (jt >= j1) break;
         const int64_t nj = min(P.nper, j1 - jt);
@@ -413,12 +411,8 @@ __global__ __launch_bounds__(kDdtThreads) void ddt_unpack_tile_kernel(ddt_period
                                                                      int64_t j0, int64_t j1) {
     extern __shared__ __attribute__((aligned(16))) char lds[];
     const uint16_t *map = stage_map<IDENT>(P, lds);
-    if (P.chunk > 0)  // a contiguous run of tiles per workgroup
-        unpack_tiles<G, IDENT>(P, contig, typed, start, j0, j1, (int64_t)blockIdx.x * P.chunk, 1,
-                               map, lds + P.map_bytes, (int64_t)(blockIdx.x + 1) * P.chunk);
-    else
-        unpack_tiles<G, IDENT>(P, contig, typed, start, j0, j1, blockIdx.x, gridDim.x, map,
-                               lds + P.map_bytes);
+    unpack_tiles<G, IDENT>(P, contig, typed, start, j0, j1, blockIdx.x, gridDim.x, map,
+                           lds + P.map_bytes);
 }
 
 // One launch over a whole iovec array (the convertor's fAdvance with
@@ -680,10 +674,11 @@ static bool tile_period(const ompi_amd_ddt_t *ddt, size_t count, int G, bool unp
     P.nt = unpack && unpack_nt(ident ? P.psize : ddt->max_blen) ? 1 : 0;
     const int64_t tb = unpack ? unpack_tile_bytes() : tile_data_bytes();
     P.nper = std::max<int64_t>(1, (tb - P.span) / std::max<int64_t>(P.pext, 1) + 1);
-    // LDS: the map, then the tile's staged bytes (unpack: only the packed
-    // bytes of its periods; pack: their typed span), + 32 for the 16-B phase
-    const int64_t staged = unpack ? P.nper * P.psize : (P.nper - 1) * P.pext + P.span;
-    *lds = (size_t)P.map_bytes + (size_t)((staged + 15) & ~(int64_t)15) + 32;
+    // LDS: the map, then the tile's typed span (the unpack stages only the
+    // packed bytes of its periods, but sizing its LDS to those — more
+    // workgroups per CU — measured slower: vector bl64 5.4 -> 4.9 TB/s,
+    // profiles/r04_unpack_tile_sweep.jsonl), + 32 for the 16-B phase
+    *lds = (size_t)P.map_bytes + (size_t)(((P.nper - 1) * P.pext + P.span + 15) & ~(int64_t)15) + 32;
     *out = P;
     *ident_out = ident;
     return true;
@@ -702,11 +697,6 @@ static bool tile_run(const ompi_amd_ddt_t *ddt, size_t count, int G, char *typed
     if (j1 <= j0) return false;
     const int64_t tiles = (j1 - j0 + P.nper - 1) / P.nper;
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(tiles, 2048));
-    static const int order = [] {
-        const char *e = getenv("OMPI_AMD_DDT_TILE_ORDER");
-        return e ? atoi(e) : 0;
-    }();
-    if (UNPACK && order == 1) P.chunk = (tiles + grid - 1) / grid;
     hipError_t e = hipSuccess;
 #define TILE(GG)                                                                               \
     case GG:                                                                                   \

@@ -4,6 +4,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -80,13 +81,15 @@ void hold(ipc_ref *r, void *owner) {
 
 // (g_mu released) the runtime close; the stats under the lock
 void close_mapping(ipc_ref *r) {
+    const auto t0 = std::chrono::steady_clock::now();
     const hipError_t e = hipIpcCloseMemHandle(r->base);
     hip_ignore(e);
     if (trace())
-        fprintf(stderr, "[ipc pid %d] close pid %llu id %llu %p+%llu -> %p%s\n", (int)getpid(),
+        fprintf(stderr, "[ipc pid %d] close pid %llu id %llu %p+%llu -> %p%s (%.3f ms)\n", (int)getpid(),
                 (unsigned long long)r->a.pid, (unsigned long long)r->a.id,
                 (void *)(uintptr_t)r->a.base, (unsigned long long)r->a.size, r->base,
-                r->retired ? " (retired)" : "");
+                r->retired ? " (retired)" : "",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     std::lock_guard<std::mutex> g(g_mu);
     ++g_st.closes;
     --g_st.live;
@@ -190,7 +193,10 @@ int ipc_map(const ipc_alloc &a, void *owner, ipc_ref **ref, void **base) {
     // answers (tools/ipc_replay_probe.py): a refusal is an
     // error, reported with the buffer, never retried.
     void *m = nullptr;
+    const auto t_open = std::chrono::steady_clock::now();
     const hipError_t e = hipIpcOpenMemHandle(&m, a.h, hipIpcMemLazyEnablePeerAccess);
+    const double open_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_open).count();
     std::lock_guard<std::mutex> g(g_mu);
     ++g_st.opens;
     done_opening(a);
@@ -238,9 +244,9 @@ int ipc_map(const ipc_alloc &a, void *owner, ipc_ref **ref, void **base) {
     g_live.push_back(r);
     ++g_st.live;
     if (trace())
-        fprintf(stderr, "[ipc pid %d] open pid %llu id %llu %p+%llu -> %p\n", (int)getpid(),
+        fprintf(stderr, "[ipc pid %d] open pid %llu id %llu %p+%llu -> %p (%.3f ms)\n", (int)getpid(),
                 (unsigned long long)a.pid, (unsigned long long)a.id, (void *)(uintptr_t)a.base,
-                (unsigned long long)a.size, m);
+                (unsigned long long)a.size, m, open_ms);
     *ref = r;
     *base = m;
     return OMPI_AMD_SUCCESS;

@@ -63,12 +63,13 @@ def main():
         ok_all &= bool(ok)
         print(json.dumps({"rank": rank, "case": step, "ok": bool(ok), "msg": msg, **kw}), flush=True)
 
-    def allreduce_check(X, salt):
+    def allreduce_check(X, salt, stream=None):
         xs = [data(r, count, salt) for r in range(n)]
         exp, _ = orc.allreduce([x.copy() for x in xs], count, SUM.index, F.code)
         X[:count].copy_(torch.from_numpy(xs[rank]))
         y = torch.zeros(count, device="cuda")
-        B.allreduce(X, y, count, F, SUM, blocking=True)
+        torch.cuda.synchronize()
+        B.allreduce(X, y, count, F, SUM, stream=stream, blocking=True)
         got = y.cpu().numpy()
         ok = np.array_equal(got.view(np.uint32), exp[rank].view(np.uint32))
         return ok, "" if ok else f"{int((got != exp[rank]).sum())} of {count} differ"
@@ -164,7 +165,10 @@ def main():
         if rank == 0:
             req = A.iallreduce(zs, zo, count, F, SUM)   # every peer posted: launched on rank 0
         t0 = time.time()
-        ok, msg = allreduce_check(X, 13)
+        # B on a stream of its own: device work of communicators sharing
+        # one stream is serialised by the stream itself (A's launched call
+        # would hold B's kernels back whatever the registry does)
+        ok, msg = allreduce_check(X, 13, stream=torch.cuda.Stream())
         dt = time.time() - t0
         req.wait()
         req.free()
