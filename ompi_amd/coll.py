@@ -115,6 +115,12 @@ class Communicator:
             _lib.check(self._lib.ompi_amd_comm_destroy(self._h), "comm_destroy")
             self._h = None
 
+    def sync(self, stream=None) -> None:
+        """ompi_amd_comm_sync: this communicator's calls on `stream` done
+        (what coll/rocm's blocking collectives wait with); while it waits,
+        the other communicators' ready nonblocking calls are launched."""
+        _lib.check(self._lib.ompi_amd_comm_sync(self._h, _stream(stream)), "comm_sync")
+
     def _finish(self, rc: int, what: str, blocking: bool, stream) -> None:
         _lib.check(rc, what)
         if blocking:

@@ -125,6 +125,9 @@ void ShmBoot::detach() {
     unlinked_ = true;
 }
 
+static void (*g_idle)() = nullptr;
+void set_boot_idle_hook(void (*fn)()) { g_idle = fn; }
+
 int ShmBoot::post(const void *mine, size_t len, uint64_t *ticket) {
     if (!map_ || len > kBlob) return OMPI_AMD_ERR_BAD_PARAM;
     const uint64_t s = seq_ + 1;
@@ -141,6 +144,7 @@ int ShmBoot::post(const void *mine, size_t len, uint64_t *ticket) {
                                    (unsigned long long)(s - kRing));
                         return OMPI_AMD_ERR_TIMEOUT;
                     }
+                    if (g_idle) g_idle();
                     sched_yield();
                 }
             }
@@ -169,6 +173,7 @@ int ShmBoot::test(uint64_t ticket, void *all, size_t len, bool block, bool *read
                                (unsigned long long)ticket);
                     return OMPI_AMD_ERR_TIMEOUT;
                 }
+                if (g_idle) g_idle();
                 sched_yield();
             }
         }

@@ -19,6 +19,10 @@
 
 namespace ompi_amd {
 
+// Called while a rendezvous waits for a peer (coll_ipc.hip: launches other
+// communicators' ready nonblocking calls, MPI's progress rule).
+void set_boot_idle_hook(void (*fn)());
+
 class ShmBoot {
   public:
     static constexpr size_t kBlob = 2048;

@@ -421,6 +421,10 @@ struct ompi_amd_comm {
     // (stream_mu: quiesce() also runs on other threads, from the IPC
     // registry's retirement of a mapping this communicator holds)
     std::mutex stream_mu;
+    // api_mu: held by every entry point for its whole call (recursive: entry
+    // points call each other); progress_others() takes it with try_lock
+    std::recursive_mutex api_mu;
+    std::atomic<int> npending{0};  // deferred calls not yet launched (pending.size())
     bool has_stream = false;
     hipStream_t cur_stream = nullptr;
     // another communicator launched on cur_stream after this one's last
@@ -2331,7 +2335,87 @@ static int agree_root0_inplace(ompi_amd_comm_t *c, path_params *pp, bool inplace
 // has posted its handle-swap half; block = wait for them (the blocking entry
 // points do, so their device work follows the deferred calls' on every rank).
 // max_launch: stop after launching that many deferred calls (-1: no limit).
-static int progress(ompi_amd_comm_t *c, bool block, int max_launch = -1) {
+static int progress(ompi_amd_comm_t *c, bool block, int max_launch = -1);
+
+// ---- progress across communicators (MPI's progress rule for nonblocking
+// collectives).  A nonblocking call of communicator A launched on this rank
+// waits on device for its peers; a peer may be blocked in a call of
+// communicator B that only completes once this rank gets through B — and
+// this rank may itself be held in B by the runtime (hipIpcCloseMemHandle
+// of a retired mapping waits for every kernel of the device, A's spinning
+// one included: measured 20 s, the device timeout, tests/ipc_share_worker.py
+// step 5).  So every blocking wait of the library (host rendezvous, stream
+// and event waits) launches the other communicators' ready deferred calls
+// while it waits, as opal_progress drives libnbc's schedules.
+static std::mutex g_comms_mu;
+static std::vector<ompi_amd_comm_t *> g_comms;
+static thread_local std::vector<const ompi_amd_comm_t *> tl_held;  // entry points this thread is in
+static thread_local bool tl_in_progress = false;
+
+struct api_guard {
+    ompi_amd_comm_t *c;
+    explicit api_guard(ompi_amd_comm_t *cc) : c(cc) {
+        if (!c) return;
+        c->api_mu.lock();
+        tl_held.push_back(c);
+    }
+    ~api_guard() {
+        if (!c) return;
+        tl_held.pop_back();
+        c->api_mu.unlock();
+    }
+    api_guard(const api_guard &) = delete;
+    api_guard &operator=(const api_guard &) = delete;
+};
+
+// Launch what is ready among the other communicators' deferred calls (never
+// blocks on a peer; skips a communicator another thread is in, and the ones
+// this thread is in).
+static void progress_others() {
+    if (tl_in_progress) return;
+    std::unique_lock<std::mutex> g(g_comms_mu, std::try_to_lock);
+    if (!g.owns_lock()) return;
+    tl_in_progress = true;
+    for (ompi_amd_comm_t *o : g_comms) {
+        if (o->npending.load() == 0 ||
+            std::find(tl_held.begin(), tl_held.end(), o) != tl_held.end() || !o->api_mu.try_lock())
+            continue;
+        tl_held.push_back(o);
+        if (set_dev(o) == OMPI_AMD_SUCCESS) (void)progress(o, false);
+        tl_held.pop_back();
+        o->api_mu.unlock();
+    }
+    tl_in_progress = false;
+    if (!tl_held.empty()) (void)set_dev(const_cast<ompi_amd_comm_t *>(tl_held.back()));
+}
+
+// bootstrap.cpp's idle hook (its rendezvous spin loops)
+static void boot_idle() { progress_others(); }
+static const bool g_boot_idle_set = [] {
+    set_boot_idle_hook(boot_idle);
+    return true;
+}();
+
+// hipStreamSynchronize / hipEventSynchronize with progress_others() while
+// waiting
+static hipError_t wait_stream(hipStream_t s) {
+    for (unsigned spins = 0;; ++spins) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e != hipErrorNotReady) return e;
+        progress_others();
+        if (spins > 64) usleep(20);
+    }
+}
+static hipError_t wait_event(hipEvent_t ev) {
+    for (unsigned spins = 0;; ++spins) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) return e;
+        progress_others();
+        if (spins > 64) usleep(20);
+    }
+}
+
+static int progress(ompi_amd_comm_t *c, bool block, int max_launch) {
     while (!c->pending.empty() && max_launch-- != 0) {
         pending_op o = c->pending.front();
         call_blob all[kMaxRanks];
@@ -2342,6 +2426,7 @@ static int progress(ompi_amd_comm_t *c, bool block, int max_launch = -1) {
             if (rc == OMPI_AMD_SUCCESS && !ready) return OMPI_AMD_SUCCESS;
         }
         c->pending.pop_front();
+        c->npending.fetch_sub(1);
         if (rc == OMPI_AMD_SUCCESS) {
             c->pre = o.ticket ? all : nullptr;
             rc = shadow_in(c, o.sh, o.stream);
@@ -2591,12 +2676,21 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
         return rc;
     }
     if (rank == 0 && c->p2p) p2p_unlink(c->p2p);  // every rank has it mapped
+    {
+        std::lock_guard<std::mutex> g(g_comms_mu);
+        g_comms.push_back(c);
+    }
     *out = c;
     return OMPI_AMD_SUCCESS;
 }
 
 int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     if (!c) return OMPI_AMD_SUCCESS;
+    {  // no progress_others() reaches it from here on
+        std::lock_guard<std::mutex> g(g_comms_mu);
+        g_comms.erase(std::remove(g_comms.begin(), g_comms.end(), c), g_comms.end());
+    }
+    { std::lock_guard<std::recursive_mutex> w(c->api_mu); }  // (and none is still in it)
     hip_ignore(hipSetDevice(c->device));
     (void)drain(c);  // deferred nonblocking calls every peer will also launch
     (void)quiesce(c);
@@ -2659,6 +2753,7 @@ int ompi_amd_coll_reduce_order(int size, size_t msg_bytes, size_t count, int roo
 }
 
 int ompi_amd_comm_phase_ms(ompi_amd_comm_t *c, int phase, double *total_ms, int *calls) {
+    api_guard api_(c);
     if (!c || phase < 0 || phase > 2 || !total_ms || !calls) return OMPI_AMD_ERR_BAD_PARAM;
     double tot = 0.0;
     int n = 0;
@@ -2679,6 +2774,7 @@ int ompi_amd_comm_phase_ms(ompi_amd_comm_t *c, int phase, double *total_ms, int 
 }
 
 int ompi_amd_comm_agree(ompi_amd_comm_t *c, int local_ok, int *all_ok) {
+    api_guard api_(c);
     if (!c || !all_ok) return OMPI_AMD_ERR_BAD_PARAM;
     int mine = local_ok ? 1 : 0, all[kMaxRanks];
     TRY(drain(c));
@@ -2690,6 +2786,7 @@ int ompi_amd_comm_agree(ompi_amd_comm_t *c, int local_ok, int *all_ok) {
 }
 
 int ompi_amd_comm_vote(ompi_amd_comm_t *c, int local_yes, int *n_yes) {
+    api_guard api_(c);
     if (!c || !n_yes) return OMPI_AMD_ERR_BAD_PARAM;
     int mine = local_yes ? 1 : 0, all[kMaxRanks];
     TRY(drain(c));
@@ -2701,10 +2798,11 @@ int ompi_amd_comm_vote(ompi_amd_comm_t *c, int local_yes, int *n_yes) {
 }
 
 int ompi_amd_comm_sync(ompi_amd_comm_t *c, void *stream) {
+    api_guard api_(c);
     if (!c) return OMPI_AMD_ERR_BAD_PARAM;
     TRY(set_dev(c));
     TRY(drain(c));
-    TRY(record_hip(hipStreamSynchronize(as_stream(stream)), "hipStreamSynchronize"));
+    TRY(record_hip(wait_stream(as_stream(stream)), "hipStreamSynchronize"));
     return check_sticky(c);
 }
 
@@ -2716,6 +2814,7 @@ int ompi_amd_comm_error(const ompi_amd_comm_t *c) {
 }
 
 int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
+    api_guard api_(c);
     if (!c || !key) return OMPI_AMD_ERR_BAD_PARAM;
     if (!strcmp(key, "small_bytes")) {
         if (v < 0) return OMPI_AMD_ERR_BAD_PARAM;
@@ -2860,6 +2959,7 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
 
 int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                        int op, void *stream) {
+    api_guard api_(c);
     if (!c || !rbuf) return OMPI_AMD_ERR_BAD_PARAM;
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
     TRY(check_sticky(c));
@@ -2936,6 +3036,7 @@ int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
 
 int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                         int op, void *stream, ompi_amd_request_t **out) {
+    api_guard api_(c);
     if (!c || !rbuf || !out) return OMPI_AMD_ERR_BAD_PARAM;
     *out = nullptr;
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
@@ -3018,6 +3119,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
         }
     }
     c->pending.push_back(o);
+    c->npending.fetch_add(1);
     *out = req;
     return progress(c, false);
 }
@@ -3070,6 +3172,7 @@ static int nb_post(ompi_amd_comm_t *c, pending_op &o, const void **exp, size_t b
         return rc;
     }
     c->pending.push_back(o);
+    c->npending.fetch_add(1);
     *out = req;
     return progress(c, false);
 }
@@ -3096,6 +3199,7 @@ static int nb_grow_landing(ompi_amd_comm_t *c, size_t need, ompi_amd_request *re
 
 int ompi_amd_ireduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t rcount,
                                    int type, int op, void *stream, ompi_amd_request_t **out) {
+    api_guard api_(c);
     if (!c || !rbuf || !out) return OMPI_AMD_ERR_BAD_PARAM;
     *out = nullptr;
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
@@ -3131,6 +3235,7 @@ int ompi_amd_ireduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *r
 
 int ompi_amd_iallgather(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t bytes,
                         void *stream, ompi_amd_request_t **out) {
+    api_guard api_(c);
     if (!c || !rbuf || !out) return OMPI_AMD_ERR_BAD_PARAM;
     *out = nullptr;
     ompi_amd_request *req = nullptr;
@@ -3154,6 +3259,7 @@ int ompi_amd_iallgather(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
 
 int ompi_amd_ibcast(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, void *stream,
                     ompi_amd_request_t **out) {
+    api_guard api_(c);
     if (!c || !buf || !out || root < 0 || root >= c->size) return OMPI_AMD_ERR_BAD_PARAM;
     *out = nullptr;
     ompi_amd_request *req = nullptr;
@@ -3200,6 +3306,7 @@ static int nb_landing(ompi_amd_comm_t *c, size_t need, ompi_amd_request *req) {
 
 int ompi_amd_ireduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                      int op, int root, void *stream, ompi_amd_request_t **out) {
+    api_guard api_(c);
     if (!c || !out || root < 0 || root >= c->size || (c->rank == root && !rbuf))
         return OMPI_AMD_ERR_BAD_PARAM;
     *out = nullptr;
@@ -3230,6 +3337,7 @@ int ompi_amd_ireduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t co
         return rc;
     }
     c->pending.push_back(o);
+    c->npending.fetch_add(1);
     *out = req;
     return progress(c, false);
 }
@@ -3252,17 +3360,20 @@ static int iscan_common(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
 
 int ompi_amd_iscan(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                    int op, void *stream, ompi_amd_request_t **out) {
+    api_guard api_(c);
     return iscan_common(c, sbuf, rbuf, count, type, op, stream, false, out);
 }
 
 int ompi_amd_iexscan(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                      int op, void *stream, ompi_amd_request_t **out) {
+    api_guard api_(c);
     return iscan_common(c, sbuf, rbuf, count, type, op, stream, true, out);
 }
 
 int ompi_amd_ireduce_scatter(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
                              const size_t *rcounts, int type, int op, void *stream,
                              ompi_amd_request_t **out) {
+    api_guard api_(c);
     if (!c || !rbuf || !rcounts || !out) return OMPI_AMD_ERR_BAD_PARAM;
     *out = nullptr;
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
@@ -3286,6 +3397,7 @@ int ompi_amd_ireduce_scatter(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
 
 int ompi_amd_reduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                     int op, int root, void *stream) {
+    api_guard api_(c);
     if (!c || root < 0 || root >= c->size || (c->rank == root && !rbuf))
         return OMPI_AMD_ERR_BAD_PARAM;
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
@@ -3397,6 +3509,7 @@ static int reduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
 
 int ompi_amd_reduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
                                   size_t rcount, int type, int op, void *stream) {
+    api_guard api_(c);
     if (!c || !rbuf) return OMPI_AMD_ERR_BAD_PARAM;
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
     TRY(check_sticky(c));
@@ -3445,6 +3558,7 @@ static red_order tuned_reduce_scatter_order(int n, size_t total_bytes, int block
 
 int ompi_amd_reduce_scatter(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
                             const size_t *rcounts, int type, int op, void *stream) {
+    api_guard api_(c);
     if (!c || !rbuf || !rcounts) return OMPI_AMD_ERR_BAD_PARAM;
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
     TRY(check_sticky(c));
@@ -3478,18 +3592,21 @@ static int rs_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, const size_
 
 int ompi_amd_scan(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                   int op, void *stream) {
+    api_guard api_(c);
     if (c) TRY(drain(c));
     return scan_common(c, sbuf, rbuf, count, type, op, stream, false);
 }
 
 int ompi_amd_exscan(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                     int op, void *stream) {
+    api_guard api_(c);
     if (c) TRY(drain(c));
     return scan_common(c, sbuf, rbuf, count, type, op, stream, true);
 }
 
 int ompi_amd_allgather(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t bytes,
                        void *stream) {
+    api_guard api_(c);
     if (!c || !rbuf) return OMPI_AMD_ERR_BAD_PARAM;
     TRY(check_sticky(c));
     TRY(drain(c));
@@ -3533,6 +3650,7 @@ static int allgather_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size
 }
 
 int ompi_amd_bcast(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, void *stream) {
+    api_guard api_(c);
     if (!c || !buf || root < 0 || root >= c->size) return OMPI_AMD_ERR_BAD_PARAM;
     TRY(check_sticky(c));
     TRY(drain(c));
@@ -3772,6 +3890,7 @@ static int bcast_land(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, hip
 
 int ompi_amd_allreduce_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count,
                             int type, int op, ompi_amd_plan_t **out) {
+    api_guard api_(c);
     if (!c || !rbuf || !out) return OMPI_AMD_ERR_BAD_PARAM;
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
     TRY(check_sticky(c));
@@ -3913,6 +4032,7 @@ static int plan_nb_new(ompi_amd_comm_t *c, int nb_kind, const void *src, void *r
 
 int ompi_amd_reduce_scatter_block_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
                                        size_t rcount, int type, int op, ompi_amd_plan_t **out) {
+    api_guard api_(c);
     if (!c || !rbuf || !out) return OMPI_AMD_ERR_BAD_PARAM;
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
     return plan_nb_new(c, PEND_RSB, sbuf, rbuf, rcount, type, op, 0, 0, out);
@@ -3920,18 +4040,21 @@ int ompi_amd_reduce_scatter_block_init(ompi_amd_comm_t *c, const void *sbuf, voi
 
 int ompi_amd_allgather_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t bytes,
                             ompi_amd_plan_t **out) {
+    api_guard api_(c);
     if (!c || !rbuf || !out) return OMPI_AMD_ERR_BAD_PARAM;
     return plan_nb_new(c, PEND_ALLGATHER, sbuf, rbuf, 0, 0, 0, 0, bytes, out);
 }
 
 int ompi_amd_bcast_init(ompi_amd_comm_t *c, void *buf, size_t bytes, int root,
                         ompi_amd_plan_t **out) {
+    api_guard api_(c);
     if (!c || !buf || !out || root < 0 || root >= c->size) return OMPI_AMD_ERR_BAD_PARAM;
     return plan_nb_new(c, PEND_BCAST, buf, buf, 0, 0, 0, root, bytes, out);
 }
 
 int ompi_amd_reduce_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                          int op, int root, ompi_amd_plan_t **out) {
+    api_guard api_(c);
     if (!c || !out || root < 0 || root >= c->size || (c->rank == root && !rbuf))
         return OMPI_AMD_ERR_BAD_PARAM;
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
@@ -3940,6 +4063,7 @@ int ompi_amd_reduce_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_
 
 int ompi_amd_reduce_scatter_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
                                  const size_t *rcounts, int type, int op, ompi_amd_plan_t **out) {
+    api_guard api_(c);
     if (!c || !rbuf || !rcounts || !out) return OMPI_AMD_ERR_BAD_PARAM;
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
     TRY(plan_nb_new(c, PEND_RS, sbuf, rbuf, 0, type, op, 0, 0, out));
@@ -3958,15 +4082,18 @@ static int scan_init_common(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, si
 
 int ompi_amd_scan_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type, int op,
                        ompi_amd_plan_t **out) {
+    api_guard api_(c);
     return scan_init_common(c, sbuf, rbuf, count, type, op, false, out);
 }
 
 int ompi_amd_exscan_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                          int op, ompi_amd_plan_t **out) {
+    api_guard api_(c);
     return scan_init_common(c, sbuf, rbuf, count, type, op, true, out);
 }
 
 int ompi_amd_plan_start(ompi_amd_plan_t *pl, void *stream) {
+    api_guard api_(pl ? pl->c : nullptr);
     if (!pl || !pl->c) return OMPI_AMD_ERR_BAD_PARAM;
     if (pl->kind == 4) {  // posts a nonblocking call: never waits for a peer
         TRY(plan_nb_post(pl, stream));
@@ -3982,6 +4109,7 @@ int ompi_amd_plan_start(ompi_amd_plan_t *pl, void *stream) {
 }
 
 int ompi_amd_plan_test(ompi_amd_plan_t *pl, int *done) {
+    api_guard api_(pl ? pl->c : nullptr);
     if (!pl || !done) return OMPI_AMD_ERR_BAD_PARAM;
     *done = 1;
     if (!pl->started) return OMPI_AMD_SUCCESS;
@@ -4000,6 +4128,7 @@ int ompi_amd_plan_test(ompi_amd_plan_t *pl, int *done) {
 }
 
 int ompi_amd_plan_wait(ompi_amd_plan_t *pl) {
+    api_guard api_(pl ? pl->c : nullptr);
     if (!pl) return OMPI_AMD_ERR_BAD_PARAM;
     if (!pl->started) return OMPI_AMD_SUCCESS;
     if (pl->kind == 4) return pl->req ? ompi_amd_request_wait(pl->req) : OMPI_AMD_SUCCESS;
@@ -4007,11 +4136,12 @@ int ompi_amd_plan_wait(ompi_amd_plan_t *pl) {
         TRY(record_hip(hipEventRecord(pl->done, pl->stream), "plan completion event"));
         pl->recorded = true;
     }
-    TRY(record_hip(hipEventSynchronize(pl->done), "plan wait"));
+    TRY(record_hip(wait_event(pl->done), "plan wait"));
     return check_sticky(pl->c);
 }
 
 int ompi_amd_plan_free(ompi_amd_plan_t *pl) {
+    api_guard api_(pl ? pl->c : nullptr);
     if (!pl) return OMPI_AMD_SUCCESS;
     if (pl->kind == 4) {
         const int rc = pl->req ? ompi_amd_request_free(pl->req) : OMPI_AMD_SUCCESS;
@@ -4033,6 +4163,7 @@ int ompi_amd_plan_free(ompi_amd_plan_t *pl) {
 }
 
 int ompi_amd_request_test(ompi_amd_request_t *r, int *done) {
+    api_guard api_(r ? r->c : nullptr);
     if (!r || !done) return OMPI_AMD_ERR_BAD_PARAM;
     *done = 0;
     if (!r->launched) {
@@ -4053,6 +4184,7 @@ int ompi_amd_request_test(ompi_amd_request_t *r, int *done) {
 }
 
 int ompi_amd_request_wait(ompi_amd_request_t *r) {
+    api_guard api_(r ? r->c : nullptr);
     if (!r) return OMPI_AMD_ERR_BAD_PARAM;
     if (!r->launched) {
         TRY(set_dev(r->c));
@@ -4063,11 +4195,12 @@ int ompi_amd_request_wait(ompi_amd_request_t *r) {
         TRY(record_hip(hipEventRecord(r->ev, r->stream), "request event"));
         r->recorded = true;
     }
-    TRY(record_hip(hipEventSynchronize(r->ev), "request wait"));
+    TRY(record_hip(wait_event(r->ev), "request wait"));
     return check_sticky(r->c);
 }
 
 int ompi_amd_request_free(ompi_amd_request_t *r) {
+    api_guard api_(r ? r->c : nullptr);
     if (!r) return OMPI_AMD_SUCCESS;
     // the peers launch it whatever this rank does: launch and finish it too
     const int rc = ompi_amd_request_wait(r);

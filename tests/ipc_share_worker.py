@@ -63,13 +63,12 @@ def main():
         ok_all &= bool(ok)
         print(json.dumps({"rank": rank, "case": step, "ok": bool(ok), "msg": msg, **kw}), flush=True)
 
-    def allreduce_check(X, salt, stream=None):
+    def allreduce_check(X, salt):
         xs = [data(r, count, salt) for r in range(n)]
         exp, _ = orc.allreduce([x.copy() for x in xs], count, SUM.index, F.code)
         X[:count].copy_(torch.from_numpy(xs[rank]))
         y = torch.zeros(count, device="cuda")
-        torch.cuda.synchronize()
-        B.allreduce(X, y, count, F, SUM, stream=stream, blocking=True)
+        B.allreduce(X, y, count, F, SUM, blocking=True)
         got = y.cpu().numpy()
         ok = np.array_equal(got.view(np.uint32), exp[rank].view(np.uint32))
         return ok, "" if ok else f"{int((got != exp[rank]).sum())} of {count} differ"
@@ -142,22 +141,52 @@ def main():
                ipc_retired=retired)
         # 5. a deferred call of A launched on rank 0 but not yet on its peers
         # while B's blocking call on rank 0 retires a stale mapping (ADVICE
-        # r3): the registry quiesces only the stale mapping's holders (B), so
-        # rank 0 does not wait for A's kernels — which wait on device for
-        # peers that sit in B's host rendezvous until rank 0 arrives
+        # r3): the registry quiesces only the stale mapping's holders (B),
+        # and only up to B's own last kernels on each stream; the runtime's
+        # close of the retired mapping still waits for every kernel of the
+        # device (A's, spinning on its peers), so the peers' waits in B must
+        # launch A meanwhile (progress_others, MPI's progress rule).  B's send
+        # buffer is a raw hipMalloc freed and allocated again (same size:
+        # normally the same address), so the peers' mappings of it go stale.
+        import ctypes
         import time
+        # the HIP runtime this process already runs (torch's): dlopen of
+        # its exact path returns that handle, not a second runtime
+        with open("/proc/self/maps") as f_:
+            hip_path = next(ln.split()[-1] for ln in f_ if "libamdhip64.so" in ln)
+        hip = ctypes.CDLL(hip_path)
+        nbytes = 22 << 20  # a whole number of 2 MiB pages (exportable as is)
+
+        def raw(vals):
+            p_ = ctypes.c_void_p()
+            assert hip.hipMalloc(ctypes.byref(p_), ctypes.c_size_t(nbytes)) == 0
+            h = np.zeros(nbytes // 4, np.float32)
+            h[:count] = vals
+            assert hip.hipMemcpy(p_, h.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(nbytes), 1) == 0
+            return p_
+
         A.set_param("user_ipc", 1)
         A.set_param("algorithm", 0)
+        y = torch.zeros(count, device="cuda")
+        xs = [data(r, count, 15) for r in range(n)]
+        p1 = raw(xs[rank])
+        torch.cuda.synchronize()
+        B.allreduce(p1.value, y, count, F, SUM, blocking=True)  # peers map p1
+        torch.cuda.synchronize()
+        dist.barrier()
+        assert hip.hipFree(p1) == 0
+        xs = [data(r, count, 13) for r in range(n)]
+        xexp, _ = orc.allreduce([x.copy() for x in xs], count, SUM.index, F.code)
+        p2 = raw(xs[rank])
         zs_h = [data(r, count, 14) for r in range(n)]
         zexp, _ = orc.allreduce([z.copy() for z in zs_h], count, SUM.index, F.code)
         zs = torch.from_numpy(zs_h[rank]).cuda()
         zo = torch.zeros(count, device="cuda")
-        torch.cuda.synchronize()
-        del X
-        torch.cuda.empty_cache()
-        X = torch.zeros(count + 64, device="cuda")  # peers' B mappings of the old X go stale
-        torch.cuda.synchronize()
+        sB = torch.cuda.Stream()
+        torch.cuda.synchronize()  # nothing of A is on the device yet
         retired0 = B.get_param("ipc_retired")
+        reused = [None] * n
+        dist.all_gather_object(reused, p2.value == p1.value)
         dist.barrier()
         if rank != 0:
             req = A.iallreduce(zs, zo, count, F, SUM)   # posted, not launched here yet
@@ -165,20 +194,30 @@ def main():
         if rank == 0:
             req = A.iallreduce(zs, zo, count, F, SUM)   # every peer posted: launched on rank 0
         t0 = time.time()
-        # B on a stream of its own: device work of communicators sharing
-        # one stream is serialised by the stream itself (A's launched call
-        # would hold B's kernels back whatever the registry does)
-        ok, msg = allreduce_check(X, 13, stream=torch.cuda.Stream())
+        # B on a stream of its own, and no device-wide synchronisation until
+        # A completes: device work of communicators sharing one stream is
+        # serialised by the stream itself (A's launched call would hold B's
+        # kernels back whatever the registry does)
+        # (waits as coll/rocm's blocking call does: ompi_amd_comm_sync, which
+        # launches A's deferred call on a rank whose peers already posted it)
+        B.allreduce(p2.value, y, count, F, SUM, stream=sB)
+        B.sync(sB)
         dt = time.time() - t0
         req.wait()
         req.free()
         torch.cuda.synchronize()
-        zgot = zo.cpu().numpy()
-        okz = np.array_equal(zgot.view(np.uint32), zexp[rank].view(np.uint32))
-        report("deferred_on_A_while_B_retires", ok and okz and dt < 10.0,
-               "; ".join(m for m in (msg, "" if okz else "A's iallreduce differs",
-                                     "" if dt < 10.0 else f"B's call took {dt:.1f} s") if m),
-               b_call_s=round(dt, 3), ipc_retired=B.get_param("ipc_retired") - retired0)
+        ok = np.array_equal(y.cpu().numpy().view(np.uint32), xexp[rank].view(np.uint32))
+        okz = np.array_equal(zo.cpu().numpy().view(np.uint32), zexp[rank].view(np.uint32))
+        retired = B.get_param("ipc_retired") - retired0
+        # a peer's reallocation at the same address must have been retired here
+        need = any(reused[q] for q in range(n) if q != rank)
+        report("deferred_on_A_while_B_retires", ok and okz and dt < 10.0 and (retired > 0 or not need),
+               "; ".join(m for m in ("" if ok else "B's allreduce differs",
+                                     "" if okz else "A's iallreduce differs",
+                                     "" if dt < 10.0 else f"B's call took {dt:.1f} s",
+                                     "" if retired > 0 or not need else "no stale mapping retired") if m),
+               b_call_s=round(dt, 3), ipc_retired=retired, peers_reused_address=need)
+        assert hip.hipFree(p2) == 0
     except Exception as e:  # noqa: BLE001
         report("exception", False, f"{type(e).__name__}: {e}")
     torch.cuda.synchronize()
