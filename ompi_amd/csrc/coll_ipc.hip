@@ -2922,6 +2922,7 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "boot_calls")) *v = (int64_t)c->boot.posted();
     else if (!strcmp(key, "ipc_opens")) *v = ipc_get_stats().opens;
     else if (!strcmp(key, "ipc_refusals")) *v = ipc_get_stats().refusals;
+    else if (!strcmp(key, "ipc_recovered")) *v = ipc_get_stats().recovered;
     else if (!strcmp(key, "ipc_closes")) *v = ipc_get_stats().closes;
     else if (!strcmp(key, "ipc_shared")) *v = ipc_get_stats().shared;
     else if (!strcmp(key, "ipc_retired")) *v = ipc_get_stats().retired;

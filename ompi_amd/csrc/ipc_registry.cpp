@@ -194,11 +194,26 @@ int ipc_map(const ipc_alloc &a, void *owner, ipc_ref **ref, void **base) {
     // error, reported with the buffer, never retried.
     void *m = nullptr;
     const auto t_open = std::chrono::steady_clock::now();
-    const hipError_t e = hipIpcOpenMemHandle(&m, a.h, hipIpcMemLazyEnablePeerAccess);
+    hipError_t e = hipIpcOpenMemHandle(&m, a.h, hipIpcMemLazyEnablePeerAccess);
+    // Residual: a range the exporter freed and allocated
+    // again — the mapping of the old allocation retired and closed just
+    // above — is, about once in several hundred such re-imports at N = 8,
+    // refused with "invalid device pointer" although its size is IPC-safe;
+    // the same open 4 ms later succeeds (the replay probe's recycle_gap
+    // order: 0 refusals).  Only that case is tried again, once, and counted.
+    bool again = false;
+    if (e != hipSuccess && !stale.empty()) {
+        (void)hipGetLastError();
+        usleep(4000);
+        m = nullptr;
+        e = hipIpcOpenMemHandle(&m, a.h, hipIpcMemLazyEnablePeerAccess);
+        again = true;
+    }
     const double open_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_open).count();
     std::lock_guard<std::mutex> g(g_mu);
-    ++g_st.opens;
+    g_st.opens += again ? 2 : 1;
+    if (again && e == hipSuccess) ++g_st.recovered;
     done_opening(a);
     if (e != hipSuccess) {
         (void)hipGetLastError();

@@ -60,6 +60,7 @@ void ipc_remove_user(void *owner);
 struct ipc_stats {
     int64_t opens;        // hipIpcOpenMemHandle calls made
     int64_t refusals;     // opens the runtime refused (each one failed its call)
+    int64_t recovered;    // re-imports of a just-retired range refused once, then opened
     int64_t closes;       // hipIpcCloseMemHandle calls made
     int64_t shared;       // ipc_map answered from a mapping the process held
     int64_t retired;      // mappings retired because the exporter freed the allocation

@@ -55,7 +55,7 @@ static int g_rank, g_size;
         if (!(c)) {                                                               \
             fprintf(stderr, "FAIL rank %d %s:%d: ", g_rank, __FILE__, __LINE__);  \
             fprintf(stderr, __VA_ARGS__);                                         \
-            fprintf(stderr, "\n");                                                \
+            fprintf(stderr, " (library: %s)\n", ompi_amd_last_error());          \
             exit(1);                                                              \
         }                                                                         \
     } while (0)

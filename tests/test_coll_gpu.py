@@ -92,14 +92,15 @@ def test_collectives_parity(n):
 
 def test_allreduce_headline_size_n8():
     """256 MiB fp32 SUM allreduce at N = 8 (BASELINE's headline point), all
-    four zero-copy schemes, every element exact (dataset E)."""
+    seven large-message schemes (four phased, three pipelined), every element
+    exact (dataset E)."""
     outs = run_ranks(8, extra_env={"COLL_HEADLINE": str(64 << 20)})
     failures = []
     for r, (rc, out) in enumerate(outs):
         lines = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
         lines = [ln for ln in lines if ln["case"] != "ipc_mode"]
         bad = [ln for ln in lines if not ln["ok"]]
-        if rc != 0 or bad or len(lines) != 4:
+        if rc != 0 or bad or len(lines) != 7:
             failures.append((r, rc, bad[:3], out[-1500:]))
     assert not failures, failures
 
@@ -110,13 +111,14 @@ def test_allreduce_past_ipc_cap_n2():
     the 2 GiB - 4 MiB IPC allocation cap, so pull+push
     runs them as two allocations, push-gather's landing buffer grows to
     (N + 1) slots of half the vector, and push-land (whose 2N slots would
-    pass the cap) falls back to push-gather on every rank alike."""
+    pass the cap) falls back to push-gather on every rank alike (its
+    pipelined launch too); the pipelined schemes beside them."""
     outs = run_ranks(2, extra_env={"COLL_HEADLINE": str(280_000_000)})
     failures = []
     for r, (rc, out) in enumerate(outs):
         lines = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
         lines = [ln for ln in lines if ln["case"] != "ipc_mode"]
         bad = [ln for ln in lines if not ln["ok"]]
-        if rc != 0 or bad or len(lines) != 4:
+        if rc != 0 or bad or len(lines) != 7:
             failures.append((r, rc, bad[:3], out[-1500:]))
     assert not failures, failures
