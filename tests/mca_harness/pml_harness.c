@@ -24,6 +24,7 @@
  * usage: pml_harness <segment-name-hex> <rank> <size>; prints "ok" / "ok gpu".
  */
 #include <stdio.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -65,8 +66,11 @@ static int ob1_calls;
 static ompi_request_t ob1_req;
 static int o_add_comm(struct ompi_communicator_t *c) { return OMPI_SUCCESS; }
 static int o_del_comm(struct ompi_communicator_t *c) { return OMPI_SUCCESS; }
-/* tags at or below HARNESS_SYS_TAG: a real host transport (pml_saved.c) */
-#define REAL(tag) ((tag) <= HARNESS_SYS_TAG)
+/* tags at or below HARNESS_SYS_TAG: a real host transport (pml_saved.c);
+ * HARNESS_PML_BENCH=1: every tag (the host_path A/B: ob1's place taken by
+ * a one-copy-in, one-copy-out shared-memory transport, as btl/sm) */
+static int g_ob1_all;
+#define REAL(tag) ((tag) <= HARNESS_SYS_TAG || g_ob1_all)
 static int o_isend(const void *b, size_t n, struct ompi_datatype_t *d, int dst, int tag,
                    mca_pml_base_send_mode_t m, struct ompi_communicator_t *c, ompi_request_t **r)
 {
@@ -189,6 +193,51 @@ int main(int argc, char **argv)
     }
     CHECK(mca_pml_rocm_comm_of(&comm) != NULL, "library communicator created");
     const int right = (g_rank + 1) % g_size, left = (g_rank + g_size - 1) % g_size;
+
+    if (getenv("HARNESS_PML_BENCH") && atoi(getenv("HARNESS_PML_BENCH")) && g_size == 2) {
+        /* host-buffer ping-pong through pml/rocm with
+         * pml_rocm_host_path = 0 (the library's staged path) and 1 (the
+         * saved PML, here the shared-memory transport above) */
+        const size_t sizes[6] = {8, 1024, 16384, 65536, 131072, 262144};
+        g_ob1_all = 1;
+        for (int hp = 0; hp < 2; ++hp) {
+            mca_pml_rocm_component.host_path = hp;
+            for (int k = 0; k < 6; ++k) {
+                const size_t n = sizes[k];
+                const int iters = n <= 16384 ? 500 : 100;
+                unsigned char *b = malloc(n);
+                memset(b, g_rank, n);
+                for (int it = -10; it < iters; ++it) {  /* 10 warm-up round trips */
+                    static struct timespec t0;
+                    if (it == 0) clock_gettime(CLOCK_MONOTONIC, &t0);
+                    if (g_rank == 0) {
+                        CHECK(mca_pml.pml_send(b, n, &dbyte, 1, 90, MCA_PML_BASE_SEND_STANDARD, &comm) ==
+                                  OMPI_SUCCESS, "bench send");
+                        CHECK(mca_pml.pml_recv(b, n, &dbyte, 1, 90, &comm, NULL) == OMPI_SUCCESS, "bench recv");
+                    } else {
+                        CHECK(mca_pml.pml_recv(b, n, &dbyte, 0, 90, &comm, NULL) == OMPI_SUCCESS, "bench recv");
+                        CHECK(mca_pml.pml_send(b, n, &dbyte, 0, 90, MCA_PML_BASE_SEND_STANDARD, &comm) ==
+                                  OMPI_SUCCESS, "bench send");
+                    }
+                    if (it == iters - 1 && g_rank == 0) {
+                        struct timespec t1;
+                        clock_gettime(CLOCK_MONOTONIC, &t1);
+                        const double us = ((t1.tv_sec - t0.tv_sec) * 1e9 + (t1.tv_nsec - t0.tv_nsec)) /
+                                          1e3 / iters / 2;  /* one way */
+                        printf("{\"host_path\": %d, \"bytes\": %zu, \"one_way_us\": %.2f, \"GBps\": %.3f, "
+                               "\"iters\": %d, \"path\": \"%s\"}\n", hp, n, us, n / us / 1e3, iters,
+                               hp ? "saved PML (shm one-copy transport, ob1 + btl/sm stand-in)"
+                                  : "library (pinned stage + device IPC)");
+                        fflush(stdout);
+                    }
+                }
+                free(b);
+            }
+        }
+        CHECK(mca_pml.pml_del_comm(&comm) == OMPI_SUCCESS, "del_comm");
+        harness_pml_saved_fini();
+        return 0;
+    }
 
     SECTION(1);
     /* 1. ring isend / irecv on device buffers */

@@ -84,8 +84,10 @@ void harness_pml_saved_send(const void *buf, size_t count, const ompi_datatype_t
     if (bytes > SLOT_BYTES) die("message larger than a mailbox slot");
     while (p->posted - __atomic_load_n(&p->taken, __ATOMIC_ACQUIRE) >= SLOTS) sched_yield();
     struct slot *s = &p->s[p->posted % SLOTS];
-    for (size_t i = 0; i < count; ++i)
-        memcpy(s->data + i * d->size, (const char *) buf + i * stride_of(d), d->size);
+    if (d->contiguous) memcpy(s->data, buf, bytes);
+    else
+        for (size_t i = 0; i < count; ++i)
+            memcpy(s->data + i * d->size, (const char *) buf + i * stride_of(d), d->size);
     s->tag = tag;
     s->bytes = bytes;
     __atomic_store_n(&s->full, 1, __ATOMIC_RELEASE);
@@ -104,8 +106,10 @@ int harness_pml_saved_try_recv(void *buf, size_t count, const ompi_datatype_t *d
     if (!__atomic_load_n(&s->full, __ATOMIC_ACQUIRE)) return 0;
     if (s->tag != tag) die("message order: another tag at the head of the mailbox");
     if (s->bytes > count * d->size) die("truncation");
-    for (size_t i = 0; i < s->bytes / d->size; ++i)
-        memcpy((char *) buf + i * stride_of(d), s->data + i * d->size, d->size);
+    if (d->contiguous) memcpy(buf, s->data, s->bytes);
+    else
+        for (size_t i = 0; i < s->bytes / d->size; ++i)
+            memcpy((char *) buf + i * stride_of(d), s->data + i * d->size, d->size);
     if (st) {
         st->MPI_SOURCE = src;
         st->MPI_TAG = tag;
