@@ -40,10 +40,17 @@
 //            MPI_Ssend still completes at the receiver's FIN.  Past the
 //            pool's cap (param p2p_stage_mib), or with p2p_user_ipc = 1, the
 //            receiver maps the send buffer itself (rendezvous, as before).
-//   host     host send buffers always go through a stage (eager cell or
-//            pool: the copy kernel cannot read pageable memory); a receive
-//            into host memory lands in a device receive stage first and is
-//            copied out before it completes.
+//   host     a host send buffer of at most kInline bytes travels inside
+//            its mailbox slot, one of at most kHostMax bytes through the
+//            sender's host stage (a ring of kHostStage bytes per rank in
+//            the same shared segment) — ob1 / btl/sm's path for host memory:
+//            one copy in, one copy out (or one host-to-device copy into a
+//            device receive buffer), no device work on the sender (round 4,
+//            profiles/r04_pml_host_path_ab*.jsonl); larger host send buffers,
+//            or a full ring, go through a device stage (eager cell or pool:
+//            the copy kernel cannot read pageable memory); a staged message
+//            received into host memory lands in a device receive stage first
+//            and is copied out before it completes.
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
@@ -70,6 +77,9 @@ namespace ompi_amd {
 
 constexpr int kSlots = 64;
 constexpr size_t kEager = 4096;
+constexpr size_t kInline = 1024;  // host payload carried in the slot itself
+constexpr size_t kHostStage = 8u << 20;  // per rank, in the mailbox segment (touched pages only)
+constexpr size_t kHostMax = 2u << 20;    // largest message through it
 
 enum : uint32_t { S_FREE = 0, S_POSTED = 1, S_MATCHED = 2, S_DONE = 3 };
 
@@ -80,6 +90,8 @@ struct alignas(64) msg_slot {
     uint64_t bytes;
     uint64_t raw;  // the send buffer's address (messages to self)
     ipc_desc d;    // the send buffer for peers
+    uint32_t inl;  // 1: payload in `inline_data`; 2: in the sender's host stage at offset `raw`
+    char inline_data[kInline];
 };
 
 struct alignas(64) pair_q {
@@ -118,6 +130,17 @@ struct p2p_state {
     std::deque<ompi_amd_p2p_request *> recvs;  // posted receives not matched yet
     std::recursive_mutex mu;
     char *eager = nullptr;  // [size][kSlots] cells of kEager bytes, allocated at first use
+    // this rank's host stage ring (bytes [htail, hhead) in flight, monotonic
+    // counters) and the messages holding it, oldest first
+    uint64_t hhead = 0, htail = 0;
+    struct hchunk { int dst; uint64_t seq, end; };
+    std::deque<hchunk> hflight;
+    int64_t host_stage_sends = 0;
+    bool host_stage_touched = false;
+    char *host_stage(int r) {
+        return reinterpret_cast<char *>(q) + sizeof(pair_q) * (size_t)size * (size_t)size +
+               (size_t)r * kHostStage;
+    }
 
     pair_q &pair(int src, int dst) { return q[(size_t)src * (size_t)size + (size_t)dst]; }
 };
@@ -184,6 +207,7 @@ int p2p_get_param(p2p_state *p, const char *key, int64_t *v) {
     else if (!strcmp(key, "p2p_direct_sends")) *v = p->direct_sends;
     else if (!strcmp(key, "p2p_host_sends")) *v = p->host_sends;
     else if (!strcmp(key, "p2p_host_recvs")) *v = p->host_recvs;
+    else if (!strcmp(key, "p2p_host_stage_sends")) *v = p->host_stage_sends;
     else return OMPI_AMD_ERR_UNSUPPORTED;
     return OMPI_AMD_SUCCESS;
 }
@@ -199,7 +223,7 @@ int p2p_create(ompi_amd_comm_t *c, const char *name, int rank, int size, int pha
     snprintf(p->name, sizeof(p->name), "/ompi_amd_%s.p2p", name);
     for (char *ch = p->name + 1; *ch; ++ch)
         if (*ch == '/') *ch = '_';
-    p->bytes = sizeof(pair_q) * (size_t)size * (size_t)size;
+    p->bytes = sizeof(pair_q) * (size_t)size * (size_t)size + kHostStage * (size_t)size;
     int fd = -1;
     if (phase == 0) {  // rank 0, before the communicator's first rendezvous
         shm_unlink(p->name);
@@ -280,6 +304,31 @@ static void reclaim(p2p_state *p) {
             ++it;
         }
     }
+}
+
+// Host-stage chunks whose message the receiver finished (oldest first: the
+// ring frees in order).  Under p->mu.
+static void reclaim_host(p2p_state *p) {
+    while (!p->hflight.empty()) {
+        const auto &h = p->hflight.front();
+        msg_slot &m = p->pair(p->rank, h.dst).slot[h.seq % kSlots];
+        if (m.seq == h.seq && m.state.load(std::memory_order_acquire) != S_DONE) break;
+        p->htail = h.end;
+        p->hflight.pop_front();
+    }
+}
+
+// A contiguous chunk of `bytes` of this rank's host stage (offset in *off),
+// or false when the ring has no room now.  Under p->mu.
+static bool take_host(p2p_state *p, size_t bytes, uint64_t *off, uint64_t *end) {
+    reclaim_host(p);
+    uint64_t at = p->hhead;
+    const uint64_t pos = at % kHostStage;
+    if (pos + bytes > kHostStage) at += kHostStage - pos;  // no wrap inside a chunk
+    if (at + bytes - p->htail > kHostStage) return false;
+    *off = at % kHostStage;
+    *end = at + bytes;
+    return true;
 }
 
 // The smallest free stage of `pool` that holds `bytes`, or a new one
@@ -364,8 +413,22 @@ static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s
     }
     r->st.error = r->rc;
     if (n == 0) return;
-    const char *src = nullptr;
     int rc = OMPI_AMD_SUCCESS;
+    if (m->inl) {  // a host send out of the slot or the sender's host stage (host: done now)
+        const char *from = m->inl == 1 ? m->inline_data : p->host_stage(s) + m->raw;
+        if (r->host_dst) {
+            memcpy(r->host_dst, from, n);
+            return;
+        }
+        rc = record_hip(hipMemcpyAsync(r->buf, from, n, hipMemcpyHostToDevice, r->stream),
+                        "hipMemcpyAsync (p2p host-stage receive)");
+        if (rc == OMPI_AMD_SUCCESS && !r->ev)
+            rc = record_hip(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming), "hipEventCreate (p2p)");
+        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipEventRecord(r->ev, r->stream), "hipEventRecord (p2p)");
+        if (rc != OMPI_AMD_SUCCESS) r->rc = r->st.error = rc;
+        return;
+    }
+    const char *src = nullptr;
     if (s == p->rank) {
         src = reinterpret_cast<const char *>(m->raw);
     } else {
@@ -512,8 +575,10 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     const hipStream_t s = as_stream(stream);
     const bool host = bytes && !is_device(buf);
     const bool eager = bytes <= kEager && mode != OMPI_AMD_SEND_SYNCHRONOUS;  // Ssend: rendezvous
+    const bool inl = host && eager && bytes <= kInline;  // no device work at all
+    const bool hostable = host && !inl && mode != OMPI_AMD_SEND_SYNCHRONOUS && bytes <= kHostMax;
     std::unique_lock<std::recursive_mutex> alloc_guard(p->mu);
-    if (rc == OMPI_AMD_SUCCESS && eager && !p->eager) {  // peers read its cells: exportable
+    if (rc == OMPI_AMD_SUCCESS && eager && !inl && !p->eager) {  // peers read its cells: exportable
         ipc_desc d{};
         rc = comm_alloc_exportable((size_t)p->size * kSlots * kEager, false, (void **)&p->eager, &d);
         if (rc != OMPI_AMD_SUCCESS) p->eager = nullptr;
@@ -559,7 +624,20 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
         return crc == OMPI_AMD_SUCCESS ? record_hip(hipStreamSynchronize(s), "hipStreamSynchronize (stage)")
                                        : crc;
     };
-    if (eager && bytes) {  // stage into this slot's cell; the send completes now
+    uint64_t hoff = 0, hend = 0;
+    const bool hstaged = hostable && take_host(p, bytes, &hoff, &hend);
+    if (inl) {  // into the slot itself; the send completes now
+        memcpy(m.inline_data, buf, bytes);
+    } else if (hstaged) {  // into this rank's host stage; the send completes now
+        if (!p->host_stage_touched) {  // fault the ring's pages in once, not per message
+            memset(p->host_stage(p->rank), 0, kHostStage);
+            p->host_stage_touched = true;
+        }
+        memcpy(p->host_stage(p->rank) + hoff, buf, bytes);
+        p->hflight.push_back({dst, seq, hend});
+        p->hhead = hend;
+        ++p->host_stage_sends;
+    } else if (eager && bytes) {  // stage into this slot's cell; the send completes now
         char *cell = p->eager + ((size_t)dst * kSlots + seq % kSlots) * kEager;
         rc = copy_in(cell);
         src = cell;
@@ -598,7 +676,7 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
         }
     }
     if (host) ++p->host_sends;
-    if (rc == OMPI_AMD_SUCCESS && bytes && dst != p->rank && !staged) {
+    if (rc == OMPI_AMD_SUCCESS && bytes && dst != p->rank && !staged && !inl && !hstaged) {
         rc = comm_export(c, src, &d);
         if (!eager) ++p->direct_sends;
     }
@@ -609,13 +687,14 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     m.tag = tag;
     m.seq = seq;
     m.bytes = bytes;
-    m.raw = reinterpret_cast<uint64_t>(src);
+    m.raw = hstaged ? hoff : reinterpret_cast<uint64_t>(src);
     m.d = d;
+    m.inl = inl ? 1u : hstaged ? 2u : 0u;
     m.state.store(S_POSTED, std::memory_order_release);
     q.posted.store(seq + 1, std::memory_order_release);
     r->seq = seq;
     // the user's buffer is free again once staged (Ssend: at the FIN)
-    r->done = eager || (staged && mode != OMPI_AMD_SEND_SYNCHRONOUS);
+    r->done = eager || hstaged || (staged && mode != OMPI_AMD_SEND_SYNCHRONOUS);
     *out = r;
     return OMPI_AMD_SUCCESS;
 }
