@@ -52,6 +52,7 @@
 // system-scope release (buffer_wbl2 sc0 sc1).
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -2397,22 +2398,47 @@ static const bool g_boot_idle_set = [] {
 }();
 
 // hipStreamSynchronize / hipEventSynchronize with progress_others() while
-// waiting
-static hipError_t wait_stream(hipStream_t s) {
+// waiting.  The first 2 ms poll with the core yielded between queries: a
+// small collective completes in a few µs, and any sleep costs at least the
+// kernel's timer slack (50 µs by default; usleep(20) measured 77 µs per
+// wait, tools/nb_latency_probe.py).  Longer waits sleep 50 µs per poll.
+template <class Q>
+static hipError_t poll_wait(Q query) {
+    const auto t0 = std::chrono::steady_clock::now();
     for (unsigned spins = 0;; ++spins) {
-        const hipError_t e = hipStreamQuery(s);
+        const hipError_t e = query();
         if (e != hipErrorNotReady) return e;
         progress_others();
-        if (spins > 64) usleep(20);
+        if (spins < 256) continue;
+        if (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(2))
+            sched_yield();
+        else
+            usleep(50);
     }
 }
-static hipError_t wait_event(hipEvent_t ev) {
-    for (unsigned spins = 0;; ++spins) {
-        const hipError_t e = hipEventQuery(ev);
-        if (e != hipErrorNotReady) return e;
-        progress_others();
-        if (spins > 64) usleep(20);
+// A stream is polled through an event recorded on it: hipEventQuery
+// answers in ~13.5 µs launch-to-observed against ~20 µs for hipStreamQuery
+// (tools/sync_latency_probe.hip; hipStreamSynchronize 12 µs, but it cannot
+// run other communicators' progress while it blocks).
+static hipError_t wait_stream(hipStream_t s) {
+    static thread_local hipEvent_t evs[64] = {};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess || dev < 0 || dev >= 64) return poll_wait([s] { return hipStreamQuery(s); });
+    if (!evs[dev]) {
+        e = hipEventCreateWithFlags(&evs[dev], hipEventDisableTiming);
+        if (e != hipSuccess) {
+            evs[dev] = nullptr;
+            return e;
+        }
     }
+    hipEvent_t ev = evs[dev];
+    e = hipEventRecord(ev, s);
+    if (e != hipSuccess) return e;
+    return poll_wait([ev] { return hipEventQuery(ev); });
+}
+static hipError_t wait_event(hipEvent_t ev) {
+    return poll_wait([ev] { return hipEventQuery(ev); });
 }
 
 static int progress(ompi_amd_comm_t *c, bool block, int max_launch) {

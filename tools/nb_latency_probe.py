@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Small-call latency breakdown, N ranks sharing one GPU: blocking allreduce
 vs MPI_Iallreduce (post, wait, free timed separately) vs a persistent start,
-and device / host sendrecv at small sizes.  One JSON line per point from
+and device-buffer sendrecv at small sizes.  One JSON line per point from
 rank 0 (max over ranks of the per-call mean).
 
 usage: python tools/nb_latency_probe.py N [sizes_bytes,...]
@@ -74,7 +74,7 @@ def worker():
         row["exact"] = bool(torch.all(y == float(n)).item())
         # device sendrecv ring
         src, dst = (rank + 1) % n, (rank - 1) % n
-        for kind in ("device", "host"):
+        for kind in ("device",):  # host buffers: tools/pml_host_path_ab.sh
             dev = "cuda" if kind == "device" else "cpu"
             a = torch.full((count,), float(rank), device=dev)
             b = torch.empty_like(a)
