@@ -21,6 +21,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "mpi.h"
 #include "ompi/communicator/communicator.h"
@@ -377,6 +378,104 @@ static void saved_case(const char *what, int coll, int form, ompi_datatype_t *d,
     free(got);
 }
 
+/* HARNESS_COLL_BENCH=1 (GPU): MPI_Allreduce, MPI_Iallreduce + wait and
+ * MPI_Allreduce_init start + wait, fp32 SUM on device buffers, called
+ * through the installed table the way the MPI layer calls coll/rocm (the
+ * osu_allreduce shape): mean per call over K calls after W warm-up calls
+ * (enough to finish the autotune), each timed region opened by an 8-B
+ * allreduce; one JSON line per size from rank 0.  Every input is 1.0, so
+ * every result is exactly the rank count. */
+static double now_us(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double) ts.tv_sec * 1e6 + (double) ts.tv_nsec * 1e-3;
+}
+
+static int bench(mca_coll_base_comm_coll_t *t, ompi_communicator_t *comm, ompi_datatype_t *f,
+                 ompi_op_t *sum)
+{
+    static const size_t sizes[] = {8, 64, 1024, 16384, 65536, 262144, 1 << 20, 4 << 20,
+                                   16 << 20, 64 << 20, 256 << 20};
+    float one = 1.f, sync_h[2] = {1.f, 1.f};
+    void *sync_d = dev_of(sync_h, sizeof(sync_h)), *sync_r = dev_of(sync_h, sizeof(sync_h));
+    for (size_t z = 0; z < sizeof(sizes) / sizeof(sizes[0]); ++z) {
+        const size_t bytes = sizes[z], n = bytes / 4;
+        const int k = bytes <= (1 << 20) ? 200 : bytes <= (16 << 20) ? 40 : 10;
+        const int w = 80;  /* the autotune decides at call 72 */
+        float *h = malloc(bytes), *exp = malloc(bytes);
+        double us[3];
+        void *ds, *dr;
+        ompi_request_t *req = NULL;
+        for (size_t i = 0; i < n; ++i) { h[i] = one; exp[i] = (float) g_size; }
+        ds = dev_of(h, bytes);
+        dr = dev_of(h, bytes);
+#define SYNC() CHECK(t->coll_allreduce(sync_d, sync_r, 2, f, sum, comm, t->coll_allreduce_module) == \
+                     OMPI_SUCCESS, "sync allreduce")
+#define AR() CHECK(t->coll_allreduce(ds, dr, (int) n, f, sum, comm, t->coll_allreduce_module) == \
+                   OMPI_SUCCESS, "allreduce")
+        for (int i = 0; i < w; ++i) AR();
+        SYNC();
+        {
+            const double t0 = now_us();
+            for (int i = 0; i < k; ++i) AR();
+            us[0] = (now_us() - t0) / k;
+        }
+        expect_dev(dr, exp, bytes, "bench allreduce");
+        for (int i = 0; i < 5; ++i) {
+            CHECK(t->coll_iallreduce(ds, dr, (int) n, f, sum, comm, &req, t->coll_iallreduce_module) ==
+                      OMPI_SUCCESS, "iallreduce");
+            harness_wait(req);
+            CHECK(req->req_free(&req) == OMPI_SUCCESS, "free");
+        }
+        SYNC();
+        {
+            const double t0 = now_us();
+            for (int i = 0; i < k; ++i) {
+                CHECK(t->coll_iallreduce(ds, dr, (int) n, f, sum, comm, &req,
+                                         t->coll_iallreduce_module) == OMPI_SUCCESS, "iallreduce");
+                harness_wait(req);
+                CHECK(req->req_free(&req) == OMPI_SUCCESS, "free");
+            }
+            us[1] = (now_us() - t0) / k;
+        }
+        expect_dev(dr, exp, bytes, "bench iallreduce");
+        CHECK(t->coll_allreduce_init(ds, dr, (int) n, f, sum, comm, NULL, &req,
+                                     t->coll_allreduce_init_module) == OMPI_SUCCESS, "allreduce_init");
+        for (int i = 0; i < 5; ++i) {
+            CHECK(req->req_start(1, &req) == OMPI_SUCCESS, "start");
+            harness_wait(req);
+        }
+        SYNC();
+        {
+            const double t0 = now_us();
+            for (int i = 0; i < k; ++i) {
+                CHECK(req->req_start(1, &req) == OMPI_SUCCESS, "start");
+                harness_wait(req);
+            }
+            us[2] = (now_us() - t0) / k;
+        }
+        CHECK(req->req_free(&req) == OMPI_SUCCESS, "persistent free");
+        expect_dev(dr, exp, bytes, "bench persistent allreduce");
+#undef AR
+#undef SYNC
+        if (g_rank == 0)
+            printf("{\"ranks\": %d, \"bytes\": %zu, \"calls\": %d, \"allreduce_us\": %.2f, "
+                   "\"iallreduce_wait_us\": %.2f, \"persistent_start_wait_us\": %.2f, "
+                   "\"busbw_GBps\": %.3f, \"exact\": true}\n",
+                   g_size, bytes, k, us[0], us[1], us[2],
+                   (double) bytes / (us[0] * 1e3) * 2.0 * (g_size - 1) / g_size);
+        fflush(stdout);
+        harness_dev_free(ds);
+        harness_dev_free(dr);
+        free(h);
+        free(exp);
+    }
+    harness_dev_free(sync_d);
+    harness_dev_free(sync_r);
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
     const int use_gpu = getenv("HARNESS_GPU") && atoi(getenv("HARNESS_GPU"));
@@ -442,6 +541,16 @@ int main(int argc, char **argv)
     install(&table, m);
     g_table = &table;
     g_comm = &comm;
+    /* the bench runs with the component's defaults (residency locks after
+     * coll_rocm_residency_lock unanimous votes, as in an application) */
+    if (getenv("HARNESS_COLL_BENCH") && atoi(getenv("HARNESS_COLL_BENCH"))) {
+        bench(&table, &comm, &dfloat, &sum);
+        release_table(&table);
+        OBJ_RELEASE(m);
+        OBJ_RELEASE(tm);
+        harness_saved_fini();
+        return 0;
+    }
     /* sections 1-8: the per-call residency vote (never locks) */
     mca_coll_rocm_component.residency_lock = 0;
 
