@@ -73,6 +73,7 @@
 #include "../../include/ompi_amd_coll.h"
 #include "bootstrap.h"
 #include "comm_internal.h"
+#include "host_mark.h"
 #include "coll_kernels.h"
 #include "ipc_registry.h"
 #include "op_device.h"
@@ -346,8 +347,6 @@ enum { PEND_ALLREDUCE = 0, PEND_RSB = 1, PEND_ALLGATHER = 2, PEND_BCAST = 3, PEN
 using namespace ompi_amd;
 
 // A nonblocking collective's completion (MPI_Request of MPI_Iallreduce).
-static void mark_word_put(uint64_t *w);
-
 struct ompi_amd_request {
     ~ompi_amd_request() { mark_word_put(mark); }  // freed after its wait: the mark has landed
     ompi_amd_comm_t *c = nullptr;
@@ -2405,123 +2404,14 @@ static const bool g_boot_idle_set = [] {
     return true;
 }();
 
-// ---- host-observed completion marks.  A one-wave kernel enqueued after a
-// call's work stores a sequence number into a word of pinned, coherent host
-// memory with a system-scope release; the host spins on that word.  Launch
-// to observed completion of a tiny kernel: 6.3 µs this way, 11.8 µs
-// polling hipEventQuery, 11.2 µs in hipStreamSynchronize (stream order puts
-// the mark after every earlier kernel of the stream: the same point an event
-// recorded there marks; tools/sync_latency_probe.hip).  The event recorded
-// beside it stays the backstop: errors, and a mark that never arrives.
-__global__ void host_mark_kernel(uint64_t *word, uint64_t v) {
-    if (threadIdx.x == 0) __hip_atomic_store(word, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-static std::mutex g_mark_mu;
-static std::vector<uint64_t *> g_mark_free;  // words of pinned pages (never returned)
-static std::atomic<uint64_t> g_mark_seq{0};  // monotonic: a reused word only grows
-
-static uint64_t *mark_word_get() {
-    static const bool on = [] {  // OMPI_AMD_HOST_MARKS=0: events only (A/B)
-        const char *e = getenv("OMPI_AMD_HOST_MARKS");
-        return !(e && atoi(e) == 0);
-    }();
-    if (!on) return nullptr;
-    std::lock_guard<std::mutex> g(g_mark_mu);
-    if (g_mark_free.empty()) {
-        void *pg = nullptr;
-        if (hipHostMalloc(&pg, 4096, hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess) {
-            (void)hipGetLastError();
-            return nullptr;
-        }
-        auto *w = static_cast<uint64_t *>(pg);
-        for (int k = 0; k < 4096 / 64; ++k) {  // one word per 64-B line
-            w[k * 8] = 0;
-            g_mark_free.push_back(w + k * 8);
-        }
-    }
-    uint64_t *w = g_mark_free.back();
-    g_mark_free.pop_back();
-    return w;
-}
-
-static void mark_word_put(uint64_t *w) {
-    if (!w) return;  // (a freed request / plan: its wait is over, its mark landed or failed)
-    std::lock_guard<std::mutex> g(g_mark_mu);
-    g_mark_free.push_back(w);
-}
-
-// enqueue the mark on `s`; the value to wait for, 0 if none was launched
-static uint64_t mark_launch(uint64_t *w, hipStream_t s) {
-    if (!w) return 0;
-    const uint64_t v = g_mark_seq.fetch_add(1) + 1;
-    hipLaunchKernelGGL(host_mark_kernel, dim3(1), dim3(64), 0, s, w, v);
-    if (hipGetLastError() != hipSuccess) return 0;
-    return v;
-}
-
-static bool mark_seen(const uint64_t *w, uint64_t v) {
-    return w && v && __atomic_load_n(w, __ATOMIC_ACQUIRE) >= v;
-}
-
-// hipStreamSynchronize / hipEventSynchronize with progress_others() while
-// waiting.  The first 2 ms poll with the core yielded between queries: a
-// small collective completes in a few µs, and any sleep costs at least the
-// kernel's timer slack (50 µs by default; usleep(20) measured 77 µs per
-// wait, tools/nb_latency_probe.py).  Longer waits sleep 50 µs per poll.
-template <class Q>
-static hipError_t poll_wait(Q query) {
-    const auto t0 = std::chrono::steady_clock::now();
-    for (unsigned spins = 0;; ++spins) {
-        const hipError_t e = query(spins);
-        if (e != hipErrorNotReady) return e;
-        progress_others();
-        if (spins < 256) continue;
-        if (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(2))
-            sched_yield();
-        else
-            usleep(50);
-    }
-}
-// A stream is waited for through a mark enqueued on it (this thread's word;
-// hipStreamQuery every 64 polls reports errors and an idle stream), or,
-// without one, an event recorded on it: hipEventQuery answers in ~12 µs
-// launch-to-observed against ~18-20 µs for hipStreamQuery.
-static hipError_t wait_stream(hipStream_t s) {
-    static thread_local uint64_t *word = mark_word_get();
-    const uint64_t v = mark_launch(word, s);
-    if (v)
-        return poll_wait([s, v](unsigned spins) {
-            if (mark_seen(word, v)) return hipSuccess;
-            return spins % 64 == 63 ? hipStreamQuery(s) : hipErrorNotReady;
-        });
-    static thread_local hipEvent_t evs[64] = {};
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess || dev < 0 || dev >= 64)
-        return poll_wait([s](unsigned) { return hipStreamQuery(s); });
-    if (!evs[dev]) {
-        e = hipEventCreateWithFlags(&evs[dev], hipEventDisableTiming);
-        if (e != hipSuccess) {
-            evs[dev] = nullptr;
-            return e;
-        }
-    }
-    hipEvent_t ev = evs[dev];
-    e = hipEventRecord(ev, s);
-    if (e != hipSuccess) return e;
-    return poll_wait([ev](unsigned) { return hipEventQuery(ev); });
-}
+// The library's waits (host_mark.h) run the other communicators' ready
+// deferred calls between polls.
+static hipError_t wait_stream(hipStream_t s) { return mark_stream_wait(s, progress_others); }
 static hipError_t wait_event(hipEvent_t ev) {
-    return poll_wait([ev](unsigned) { return hipEventQuery(ev); });
+    return mark_event_wait(ev, nullptr, 0, progress_others);
 }
-// an event and the mark enqueued right after it: whichever shows first
 static hipError_t wait_marked(hipEvent_t ev, const uint64_t *w, uint64_t v) {
-    if (!v) return wait_event(ev);
-    return poll_wait([ev, w, v](unsigned spins) {
-        if (mark_seen(w, v)) return hipSuccess;
-        return spins % 64 == 63 ? hipEventQuery(ev) : hipErrorNotReady;
-    });
+    return mark_event_wait(ev, w, v, progress_others);
 }
 
 static int progress(ompi_amd_comm_t *c, bool block, int max_launch) {

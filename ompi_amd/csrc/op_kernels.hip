@@ -17,6 +17,7 @@
 #include <array>
 #include <utility>
 
+#include "host_mark.h"
 #include "op_device.h"
 #include "runtime.h"
 
@@ -311,7 +312,7 @@ static int reduce_mixed(int op, int type, bool three, const void *in1, const voi
     if (rc == OMPI_AMD_SUCCESS && dout != out)
         rc = record_hip(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, s),
                         "op handler: result to host");
-    if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipStreamSynchronize(s), "op sync");
+    if (rc == OMPI_AMD_SUCCESS) rc = record_hip(mark_stream_wait(s, no_idle), "op sync");
     return rc;
 }
 
@@ -330,7 +331,7 @@ static void handler2(const void *in, void *inout, int *count, ompi_datatype_t **
     int rc;
     if (kind == 1) {
         rc = op_launch(OP, TYPE, false, inout, in, inout, (size_t)*count, s);
-        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipStreamSynchronize(s), "op sync");
+        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(mark_stream_wait(s, no_idle), "op sync");
     } else {
         rc = reduce_mixed(OP, TYPE, false, in, nullptr, inout, (size_t)*count, s);
     }
@@ -352,7 +353,7 @@ static void handler3(const void *in1, const void *in2, void *out, int *count,
     int rc;
     if (kind == 1) {
         rc = op_launch(OP, TYPE, true, in1, in2, out, (size_t)*count, s);
-        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipStreamSynchronize(s), "op sync");
+        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(mark_stream_wait(s, no_idle), "op sync");
     } else {
         rc = reduce_mixed(OP, TYPE, true, in1, in2, out, (size_t)*count, s);
     }

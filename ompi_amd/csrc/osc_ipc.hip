@@ -37,6 +37,7 @@
 #include <utility>
 #include <vector>
 
+#include "host_mark.h"
 #include "../../include/ompi_amd_osc.h"
 #include "comm_internal.h"
 #include "ddt_device.h"
@@ -994,7 +995,7 @@ int ompi_amd_win_unlock_all(ompi_amd_win_t *w, void *stream) {
 int ompi_amd_win_flush(ompi_amd_win_t *w, int target, void *stream) {
     if (!w) return OMPI_AMD_ERR_BAD_PARAM;
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
-    OSC_TRY(record_hip(hipStreamSynchronize(win_stream(w, stream)), "hipStreamSynchronize (flush)"));
+    OSC_TRY(record_hip(mark_stream_wait(win_stream(w, stream), no_idle), "hipStreamSynchronize (flush)"));
     return comm_sticky(w->c);
 }
 

@@ -69,6 +69,7 @@
 #include <new>
 #include <vector>
 
+#include "host_mark.h"
 #include "../../include/ompi_amd_p2p.h"
 #include "comm_internal.h"
 #include "runtime.h"
@@ -517,9 +518,25 @@ static int wait_one(ompi_amd_p2p_request *r) {
         if (done) return rc;
         if (++spins > 64) sched_yield();
         if (over(r->p, t0)) {
-            record_msg("p2p %s timed out after %.1f s (peer %d, tag %d)",
-                       r->is_send ? "send" : "receive", limit_s(r->p),
-                       r->is_send ? r->peer : r->src, r->is_send ? -1 : r->tag);
+            // what the request was waiting for, for the report
+            p2p_state *p = r->p;
+            std::lock_guard<std::recursive_mutex> g(p->mu);
+            const int peer = r->is_send ? r->peer : r->src;
+            unsigned long long posted = 0, scan = 0;
+            int st = -1;
+            if (peer >= 0 && peer < p->size) {
+                const pair_q &q = r->is_send ? p->pair(p->rank, peer) : p->pair(peer, p->rank);
+                posted = (unsigned long long)q.posted.load(std::memory_order_acquire);
+                scan = r->is_send ? 0 : (unsigned long long)p->scan_from[(size_t)peer];
+                if (r->is_send) st = (int)q.slot[r->seq % kSlots].state.load(std::memory_order_acquire);
+            }
+            const int ev = r->ev ? (int)hipEventQuery(r->ev) : -1;
+            (void)hipGetLastError();
+            record_msg("p2p %s timed out after %.1f s (peer %d, tag %d; matched %d, copy event %d, "
+                       "posted %llu, scanned from %llu, slot state %d, seq %llu)",
+                       r->is_send ? "send" : "receive", limit_s(r->p), peer,
+                       r->is_send ? -1 : r->tag, r->matched ? 1 : 0, ev, posted, scan, st,
+                       (unsigned long long)r->seq);
             return OMPI_AMD_ERR_TIMEOUT;
         }
     }
@@ -587,7 +604,7 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     // the buffer is read from now on (by a staging copy or the receiver):
     // its producers must be done
     if (rc == OMPI_AMD_SUCCESS && !host)
-        rc = record_hip(hipStreamSynchronize(s), "hipStreamSynchronize (send)");
+        rc = record_hip(hipStreamSynchronize(s), "hipStreamSynchronize (send)");  // usually idle
     if (rc != OMPI_AMD_SUCCESS) return rc;
     auto *r = new (std::nothrow) ompi_amd_p2p_request;
     if (!r) return OMPI_AMD_ERR_BAD_PARAM;
@@ -621,7 +638,7 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
         const int crc = host ? record_hip(hipMemcpyAsync(to, buf, bytes, hipMemcpyHostToDevice, s),
                                           "hipMemcpyAsync (p2p send stage)")
                              : xfer_copy(buf, to, bytes, s);
-        return crc == OMPI_AMD_SUCCESS ? record_hip(hipStreamSynchronize(s), "hipStreamSynchronize (stage)")
+        return crc == OMPI_AMD_SUCCESS ? record_hip(mark_stream_wait(s, no_idle), "hipStreamSynchronize (stage)")
                                        : crc;
     };
     uint64_t hoff = 0, hend = 0;

@@ -1,4 +1,5 @@
 // Host runtime helpers: error capture, per-thread streams, pointer queries.
+#include "host_mark.h"
 #include "runtime.h"
 
 #include <cstdarg>
@@ -163,7 +164,7 @@ int ompi_amd_memcpy_async(void *dst, const void *src, size_t bytes, void *stream
 
 int ompi_amd_stream_synchronize(void *stream) {
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : thread_stream();
-    return record_hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+    return record_hip(mark_stream_wait(s, no_idle), "hipStreamSynchronize");
 }
 
 int ompi_amd_memcpy(void *dst, const void *src, size_t bytes) {
@@ -171,7 +172,7 @@ int ompi_amd_memcpy(void *dst, const void *src, size_t bytes) {
     if (!dst || !src) return OMPI_AMD_ERR_BAD_PARAM;
     hipStream_t s = thread_stream();
     int rc = record_hip(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s), "hipMemcpyAsync");
-    if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipStreamSynchronize(s), "hipStreamSynchronize");
+    if (rc == OMPI_AMD_SUCCESS) rc = record_hip(mark_stream_wait(s, no_idle), "hipStreamSynchronize");
     return rc;
 }
 

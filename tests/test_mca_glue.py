@@ -76,11 +76,16 @@ def _run_coll_harness(exe, n, gpu, timeout):
     return outs
 
 
+def _assert_all(results, expect):
+    """Every rank printed `expect` and exited 0; a failure shows every rank's
+    stderr tail (a hang on one rank is usually explained by another)."""
+    assert all(rc == 0 and out == expect for rc, out, _ in results), results
+
+
 def test_coll_component_selection(coll_harness):
     """comm_query accepts node-local intra-communicators of 2..16 ranks;
     init_query refuses without a device (coll_base_comm_select.c protocol)."""
-    for rc, out, err in _run_coll_harness(coll_harness, 2, False, 60):
-        assert rc == 0 and out == "ok", (rc, out, err)
+    _assert_all(_run_coll_harness(coll_harness, 2, False, 60), "ok")
 
 
 @pytest.mark.gpu
@@ -90,8 +95,7 @@ def test_coll_component_device_path(coll_harness, n):
     through the communicator's table runs on device buffers and matches the
     oracle bit for bit; host / mixed / user-op calls go to the saved
     functions on every rank; release destroys the device communicator."""
-    for rc, out, err in _run_coll_harness(coll_harness, n, True, 150):
-        assert rc == 0 and out == "ok gpu", (rc, out, err)
+    _assert_all(_run_coll_harness(coll_harness, n, True, 150), "ok gpu")
 
 
 # ---- pml/rocm (ompi_amd/mca/pml/rocm) through tests/mca_harness/pml_harness.c ----
@@ -111,8 +115,7 @@ def test_pml_component_interposition(pml_harness):
     installs itself in mca_pml (pml_v_component.c:123-160's pattern); with
     no device no communicator gets library state and every call reaches
     the saved PML."""
-    for rc, out, err in _run_coll_harness(pml_harness, 2, False, 60):
-        assert rc == 0 and out == "ok", (rc, out, err)
+    _assert_all(_run_coll_harness(pml_harness, 2, False, 60), "ok")
 
 
 @pytest.mark.gpu
@@ -124,8 +127,7 @@ def test_pml_component_device_path(pml_harness, n):
     persistent requests started three times with fresh data, truncation;
     system tags, PROC_NULL and matched probes of system tags reach the saved
     PML; add_comm / del_comm create and destroy the library communicator."""
-    for rc, out, err in _run_coll_harness(pml_harness, n, True, 150):
-        assert rc == 0 and out == "ok gpu", (rc, out, err)
+    _assert_all(_run_coll_harness(pml_harness, n, True, 150), "ok gpu")
 
 
 # ---- osc/rocm (ompi_amd/mca/osc/rocm) through tests/mca_harness/osc_harness.c ----
@@ -146,8 +148,7 @@ def test_osc_component_selection(osc_harness):
     """osc_init refuses without a device; osc_query refuses host memory,
     allocate without the device info key, inter-communicators, remote peers
     and dynamic windows (ompi_osc_base_select protocol)."""
-    for rc, out, err in _run_coll_harness(osc_harness, 1, False, 60):
-        assert rc == 0 and out == "ok", (rc, out, err)
+    _assert_all(_run_coll_harness(osc_harness, 1, False, 60), "ok")
 
 
 @pytest.mark.gpu
@@ -157,8 +158,7 @@ def test_osc_component_device_path(osc_harness, n):
     component: fence epochs with accumulate (bit-exact vs op/base) and get,
     an exclusive-lock put epoch, a fetch_and_op counter, refusal of user ops,
     mismatched datatypes and PSCW, free."""
-    for rc, out, err in _run_coll_harness(osc_harness, n, True, 150):
-        assert rc == 0 and out == "ok gpu", (rc, out, err)
+    _assert_all(_run_coll_harness(osc_harness, n, True, 150), "ok gpu")
 
 
 # ---- the convertor seam (ompi_amd/mca/common/rocm) through tests/mca_harness/ddt_harness.c ----
