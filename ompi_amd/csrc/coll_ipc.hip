@@ -521,6 +521,7 @@ struct ompi_amd_comm {
     // per-phase kernel timing (param "profile"): event pairs per call
     int profile = 0;
     std::vector<hipEvent_t> ev_free;
+    std::vector<hipEvent_t> req_ev_free;  // nonblocking requests' completion events, reused
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_phase[3];  // fold, gather, scatter
     // nonblocking calls not launched yet, and the swapped blobs of the one
     // being launched (exchange_bufs takes them instead of a rendezvous)
@@ -2414,6 +2415,20 @@ static hipError_t wait_marked(hipEvent_t ev, const uint64_t *w, uint64_t v) {
     return mark_event_wait(ev, w, v, progress_others);
 }
 
+// a nonblocking request's completion event: from the communicator's pool
+// (hipEventCreate on every MPI_I* call costs more than the call's launch)
+static hipError_t req_event_get(ompi_amd_comm_t *c, hipEvent_t *ev) {
+    if (!c->req_ev_free.empty()) {
+        *ev = c->req_ev_free.back();
+        c->req_ev_free.pop_back();
+        return hipSuccess;
+    }
+    return hipEventCreateWithFlags(ev, hipEventDisableTiming);
+}
+static void req_event_put(ompi_amd_comm_t *c, hipEvent_t ev) {
+    if (ev) c->req_ev_free.push_back(ev);
+}
+
 static int progress(ompi_amd_comm_t *c, bool block, int max_launch) {
     while (!c->pending.empty() && max_launch-- != 0) {
         pending_op o = c->pending.front();
@@ -2718,6 +2733,7 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
             hip_ignore(hipEventDestroy(pr.second));
         }
     for (auto e : c->ev_free) hip_ignore(hipEventDestroy(e));
+    for (auto e : c->req_ev_free) hip_ignore(hipEventDestroy(e));
     for (auto &kv : c->tune)
         for (auto e : kv.second.ev)
             if (e) hip_ignore(hipEventDestroy(e));
@@ -3046,7 +3062,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
     if (!req) return OMPI_AMD_ERR_BAD_PARAM;
     req->c = c;
     req->mark = mark_word_get();
-    int rc = record_hip(hipEventCreateWithFlags(&req->ev, hipEventDisableTiming), "request event");
+    int rc = record_hip(req_event_get(c, &req->ev), "request event");
     if (rc != OMPI_AMD_SUCCESS) {
         delete req;
         return rc;
@@ -3058,7 +3074,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
         rc = drain(c);
         if (rc == OMPI_AMD_SUCCESS) rc = agree_root0_inplace(c, &pp, inplace);
         if (rc != OMPI_AMD_SUCCESS) {
-            hip_ignore(hipEventDestroy(req->ev));
+            req_event_put(req->c, req->ev);
             delete req;
             return rc;
         }
@@ -3072,7 +3088,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
             rc = drain(c);
             if (rc == OMPI_AMD_SUCCESS) rc = ensure_landing(c, need);
             if (rc != OMPI_AMD_SUCCESS) {
-                hip_ignore(hipEventDestroy(req->ev));
+                req_event_put(req->c, req->ev);
                 delete req;
                 return rc;
             }
@@ -3112,7 +3128,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
         if (rc == OMPI_AMD_SUCCESS) rc = export_buf(c, o.rbuf, &mine.r);
         if (rc == OMPI_AMD_SUCCESS) rc = c->boot.post(&mine, sizeof(mine), &o.ticket);
         if (rc != OMPI_AMD_SUCCESS) {
-            hip_ignore(hipEventDestroy(req->ev));
+            req_event_put(req->c, req->ev);
             arena_free(c, req->shadow);
             arena_free(c, req->shadow2);
             delete req;
@@ -3139,7 +3155,7 @@ static int nb_begin(ompi_amd_comm_t *c, ompi_amd_request **out) {
     if (!req) return OMPI_AMD_ERR_BAD_PARAM;
     req->c = c;
     req->mark = mark_word_get();
-    const int rc = record_hip(hipEventCreateWithFlags(&req->ev, hipEventDisableTiming), "request event");
+    const int rc = record_hip(req_event_get(c, &req->ev), "request event");
     if (rc != OMPI_AMD_SUCCESS) {
         delete req;
         return rc;
@@ -3167,7 +3183,7 @@ static int nb_post(ompi_amd_comm_t *c, pending_op &o, const void **exp, size_t b
         if (rc == OMPI_AMD_SUCCESS) rc = c->boot.post(&mine, sizeof(mine), &o.ticket);
     }
     if (rc != OMPI_AMD_SUCCESS) {
-        hip_ignore(hipEventDestroy(req->ev));
+        req_event_put(req->c, req->ev);
         arena_free(c, req->shadow);
         arena_free(c, req->shadow2);
         delete req;
@@ -3193,7 +3209,7 @@ static int nb_grow_landing(ompi_amd_comm_t *c, size_t need, ompi_amd_request *re
         if (rc == OMPI_AMD_SUCCESS) rc = ensure_landing(c, need);
     }
     if (rc != OMPI_AMD_SUCCESS) {
-        hip_ignore(hipEventDestroy(req->ev));
+        req_event_put(req->c, req->ev);
         delete req;
     }
     return rc;
@@ -3223,7 +3239,7 @@ int ompi_amd_ireduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *r
             if (rc == OMPI_AMD_SUCCESS) rc = ensure_landing(c, slot * (size_t)(c->size + 1));
         }
         if (rc != OMPI_AMD_SUCCESS) {
-            hip_ignore(hipEventDestroy(req->ev));
+            req_event_put(req->c, req->ev);
             delete req;
             return rc;
         }
@@ -3300,7 +3316,7 @@ static int nb_landing(ompi_amd_comm_t *c, size_t need, ompi_amd_request *req) {
         if (rc == OMPI_AMD_SUCCESS) rc = ensure_landing(c, need);
     }
     if (rc != OMPI_AMD_SUCCESS) {
-        hip_ignore(hipEventDestroy(req->ev));
+        req_event_put(req->c, req->ev);
         delete req;
     }
     return rc;
@@ -3334,7 +3350,7 @@ int ompi_amd_ireduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t co
     mine.flags = (c->rank == root && in_place(sbuf, rbuf)) ? 1 : 0;
     if (rc == OMPI_AMD_SUCCESS) rc = c->boot.post(&mine, sizeof(mine), &o.ticket);
     if (rc != OMPI_AMD_SUCCESS) {
-        hip_ignore(hipEventDestroy(req->ev));
+        req_event_put(req->c, req->ev);
         delete req;
         return rc;
     }
@@ -4216,7 +4232,7 @@ int ompi_amd_request_free(ompi_amd_request_t *r) {
     if (!r) return OMPI_AMD_SUCCESS;
     // the peers launch it whatever this rank does: launch and finish it too
     const int rc = ompi_amd_request_wait(r);
-    if (r->ev) hip_ignore(hipEventDestroy(r->ev));
+    req_event_put(r->c, r->ev);  // its wait is over
     // the call's trailing barrier has passed: no peer reads the shadow any more
     arena_free(r->c, r->shadow);
     arena_free(r->c, r->shadow2);

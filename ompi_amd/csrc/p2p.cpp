@@ -137,6 +137,7 @@ struct p2p_state {
     struct hchunk { int dst; uint64_t seq, end; };
     std::deque<hchunk> hflight;
     int64_t host_stage_sends = 0;
+    std::vector<hipEvent_t> ev_free;  // receive copies' events, reused
     bool host_stage_touched = false;
     char *host_stage(int r) {
         return reinterpret_cast<char *>(q) + sizeof(pair_q) * (size_t)size * (size_t)size +
@@ -164,6 +165,8 @@ struct ompi_amd_p2p_request {
     int src = OMPI_AMD_ANY_SOURCE, tag = OMPI_AMD_ANY_TAG;
     hipStream_t stream = nullptr;
     hipEvent_t ev = nullptr;
+    uint64_t *mark = nullptr;  // host-observed completion of the copy (host_mark.h), with `ev`
+    uint64_t mark_seq = 0;
     bool matched = false;
     msg_slot *slot = nullptr;  // matched message
     void *pinned = nullptr;    // sender mapping held during the copy
@@ -265,6 +268,7 @@ void p2p_destroy(p2p_state *p) {
     if (!p) return;
     if (p->q) munmap(p->q, p->bytes);
     if (p->eager) hip_ignore(hipFree(p->eager));
+    for (hipEvent_t e : p->ev_free) hip_ignore(hipEventDestroy(e));
     // the communicator's final rendezvous has passed: no peer reads a stage
     for (auto &f : p->staged) hip_ignore(hipFree(f.st.buf));
     for (auto &st : p->send_free) hip_ignore(hipFree(st.buf));
@@ -397,6 +401,26 @@ static msg_slot *find(p2p_state *p, int src, int tag, int *from_rank) {
     return nullptr;
 }
 
+// The copy's completion on r->stream: an event (from the state's pool) and
+// a host mark right after it.
+static int record_copy(p2p_state *p, ompi_amd_p2p_request *r) {
+    int rc = OMPI_AMD_SUCCESS;
+    if (!r->ev) {
+        if (!p->ev_free.empty()) {
+            r->ev = p->ev_free.back();
+            p->ev_free.pop_back();
+        } else {
+            rc = record_hip(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming), "hipEventCreate (p2p)");
+        }
+    }
+    if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipEventRecord(r->ev, r->stream), "hipEventRecord (p2p)");
+    if (rc == OMPI_AMD_SUCCESS) {
+        if (!r->mark) r->mark = mark_word_get();
+        r->mark_seq = mark_launch(r->mark, r->stream);
+    }
+    return rc;
+}
+
 // Claim `m` for receive `r` and launch its copy.
 static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s) {
     m->state.store(S_MATCHED, std::memory_order_release);
@@ -423,9 +447,7 @@ static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s
         }
         rc = record_hip(hipMemcpyAsync(r->buf, from, n, hipMemcpyHostToDevice, r->stream),
                         "hipMemcpyAsync (p2p host-stage receive)");
-        if (rc == OMPI_AMD_SUCCESS && !r->ev)
-            rc = record_hip(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming), "hipEventCreate (p2p)");
-        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipEventRecord(r->ev, r->stream), "hipEventRecord (p2p)");
+        if (rc == OMPI_AMD_SUCCESS) rc = record_copy(p, r);
         if (rc != OMPI_AMD_SUCCESS) r->rc = r->st.error = rc;
         return;
     }
@@ -448,11 +470,7 @@ static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s
     if (rc == OMPI_AMD_SUCCESS && r->host_dst)
         rc = record_hip(hipMemcpyAsync(r->host_dst, dst, n, hipMemcpyDeviceToHost, r->stream),
                         "hipMemcpyAsync (p2p receive to host)");
-    if (rc == OMPI_AMD_SUCCESS) {
-        if (!r->ev) rc = record_hip(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming),
-                                    "hipEventCreate (p2p)");
-        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipEventRecord(r->ev, r->stream), "hipEventRecord (p2p)");
-    }
+    if (rc == OMPI_AMD_SUCCESS) rc = record_copy(p, r);
     if (rc != OMPI_AMD_SUCCESS) r->rc = r->st.error = rc;
 }
 
@@ -486,7 +504,7 @@ static int test_one(ompi_amd_p2p_request *r, bool *done) {
         if (m.seq != r->seq || m.state.load(std::memory_order_acquire) == S_DONE) r->done = true;
     } else if (r->matched) {
         bool copied = true;
-        if (r->ev) {
+        if (r->ev && !mark_seen(r->mark, r->mark_seq)) {
             const hipError_t e = hipEventQuery(r->ev);
             if (e == hipErrorNotReady) {
                 copied = false;
@@ -766,7 +784,11 @@ int ompi_amd_p2p_free(ompi_amd_p2p_request_t *r) {
         if (!r->done) cancel_recv(r);
     }
     if (!r->done) return rc;  // a matched copy or a send the mailbox still references: keep it
-    if (r->ev) hip_ignore(hipEventDestroy(r->ev));
+    if (r->ev) {  // done: its copy is over
+        std::lock_guard<std::recursive_mutex> g(r->p->mu);
+        r->p->ev_free.push_back(r->ev);
+    }
+    mark_word_put(r->mark);
     delete r;
     return rc;
 }
