@@ -79,7 +79,9 @@ def _run_coll_harness(exe, n, gpu, timeout):
 def _assert_all(results, expect):
     """Every rank printed `expect` and exited 0; a failure shows every rank's
     stderr tail (a hang on one rank is usually explained by another)."""
-    assert all(rc == 0 and out == expect for rc, out, _ in results), results
+    if not all(rc == 0 and out == expect for rc, out, _ in results):
+        raise AssertionError("\n".join(f"--- rank {r}: rc {rc}, stdout {out!r}\n{err}"
+                                        for r, (rc, out, err) in enumerate(results)))
 
 
 def test_coll_component_selection(coll_harness):
