@@ -13,6 +13,7 @@ arriving at this GPU during the launch over its event-timed duration.
 from __future__ import annotations
 
 import os
+import sys
 import time
 
 
@@ -111,6 +112,13 @@ def bench_allreduce(args, metric: str, link_gbs: float):
     # one-GPU box); RCCL refuses two ranks per GPU, so gloo carries the
     # timing barrier and the comparator is skipped.
     shared = os.environ.get("OMPI_AMD_BENCH_SHARE_GPU") == "1"
+    nlocal = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    if not shared and torch.cuda.device_count() < nlocal:
+        # fewer GPUs than local ranks: a labelled rehearsal rather than a
+        # crash in set_device (the line carries "shared_gpu_rehearsal": true)
+        print(f"[bench] {torch.cuda.device_count()} GPU(s) for {nlocal} local ranks: "
+              "every rank on cuda:0 (shared-GPU rehearsal)", file=sys.stderr, flush=True)
+        shared = True
     if shared:
         local = 0
     torch.cuda.set_device(local)
