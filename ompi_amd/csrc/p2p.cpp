@@ -137,6 +137,7 @@ struct p2p_state {
     std::deque<hchunk> hflight;
     int64_t host_stage_sends = 0;
     int64_t export_refusals = 0;  // sends staged because the runtime refused the export
+    int refuse_exports = 0;       // test hook (param p2p_refuse_exports)
     std::vector<hipEvent_t> ev_free;  // receive copies' events, reused
     bool host_stage_touched = false;
     char *host_stage(int r) {
@@ -192,6 +193,8 @@ int p2p_set_param(p2p_state *p, const char *key, int64_t v) {
     } else if (!strcmp(key, "p2p_stage_mib")) {
         if (v < 0) return OMPI_AMD_ERR_BAD_PARAM;
         p->stage_cap = (size_t)v << 20;
+    } else if (!strcmp(key, "p2p_refuse_exports")) {  // test hook: act as if the runtime refused
+        p->refuse_exports = v ? 1 : 0;
     } else {
         return OMPI_AMD_ERR_UNSUPPORTED;  // not a p2p key
     }
@@ -718,7 +721,8 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     }
     if (host) ++p->host_sends;
     if (rc == OMPI_AMD_SUCCESS && bytes && dst != p->rank && !staged && !inl && !hstaged) {
-        rc = comm_export(c, src, &d);
+        rc = p->refuse_exports && !eager ? record_hip(hipErrorInvalidValue, "hipIpcGetMemHandle (refusal forced)")
+                                         : comm_export(c, src, &d);
         if (rc != OMPI_AMD_SUCCESS && !eager && !host) {
             // ROCm 7.2 now and then refuses hipIpcGetMemHandle ("invalid
             // argument") for a fresh application allocation of an IPC-safe

@@ -87,6 +87,25 @@ def case_ring(comm, rank, n, nbytes, salt, soff=0, roff=0):
     return ok, msg
 
 
+def case_export_refused(comm, rank, n, salt, nbytes=(8 << 20) + 12):
+    """p2p_user_ipc = 1 with the export of the send buffer refused (the test
+    hook acts as the runtime's intermittent hipIpcGetMemHandle refusal): the
+    message goes through a library stage, byte-exact, counted in
+    p2p_export_refusals and p2p_staged_sends."""
+    comm.set_param("p2p_user_ipc", 1)
+    comm.set_param("p2p_refuse_exports", 1)
+    try:
+        r0, s0 = comm.get_param("p2p_export_refusals"), comm.get_param("p2p_staged_sends")
+        ok, msg = case_ring(comm, rank, n, nbytes, salt, soff=4, roff=8)
+        r1, s1 = comm.get_param("p2p_export_refusals"), comm.get_param("p2p_staged_sends")
+    finally:
+        comm.set_param("p2p_refuse_exports", 0)
+        comm.set_param("p2p_user_ipc", 0)
+    if ok and (r1 - r0 != 1 or s1 - s0 != 1):
+        return False, f"refusals {r1 - r0}, staged sends {s1 - s0} (want 1, 1)"
+    return ok, msg
+
+
 def case_tags_out_of_order(comm, rank, n, salt):
     """Three sends with tags 5, 6, 7; receives posted as 7, 5, 6."""
     nxt, prv = (rank + 1) % n, (rank - 1) % n
@@ -868,6 +887,7 @@ def main():
         ("p2p_ring_4099B_misaligned", lambda: case_ring(comm, rank, n, 4099, 3, soff=3, roff=5)),
         ("p2p_ring_64MiB", lambda: case_ring(comm, rank, n, 64 << 20, 4)),
         ("p2p_ring_16MiB_plus_odd", lambda: case_ring(comm, rank, n, (16 << 20) + 13, 5, 16, 16)),
+        ("p2p_export_refused_staged", lambda: case_export_refused(comm, rank, n, 6)),
         ("p2p_tags_out_of_order", lambda: case_tags_out_of_order(comm, rank, n, 6)),
         ("p2p_same_tag_order", lambda: case_same_tag_order(comm, rank, n, 20)),
         ("p2p_any_source_any_tag", lambda: case_any_source(comm, rank, n, 70)),

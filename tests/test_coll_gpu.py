@@ -122,3 +122,22 @@ def test_allreduce_past_ipc_cap_n2():
         if rc != 0 or bad or len(lines) != 7:
             failures.append((r, rc, bad[:3], out[-1500:]))
     assert not failures, failures
+
+
+def test_waits_without_host_marks_n3():
+    """The library's waits with host-observed completion marks off
+    (OMPI_AMD_HOST_MARKS=0: blocking syncs, request and plan waits on events
+    only): nonblocking and persistent allreduces, the
+    pipelined nonblocking case and the nonblocking rsb / allgather / bcast
+    stay exact against the oracle."""
+    cases = ("iallreduce_mixed,iallreduce_many_outstanding,persistent_small,persistent_big,"
+             "pipelined_nonblocking,nonblocking_rsb_ag_bcast,ar_sum_f32_big")
+    outs = run_ranks(3, extra_env={"OMPI_AMD_HOST_MARKS": "0", "COLL_CASES": cases}, tag="nomarks_n")
+    failures = []
+    for r, (rc, out) in enumerate(outs):
+        lines = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+        lines = [ln for ln in lines if ln["case"] != "ipc_mode"]
+        bad = [ln for ln in lines if not ln["ok"]]
+        if rc != 0 or bad or len(lines) != 7:
+            failures.append((r, rc, bad[:3], [ln["case"] for ln in lines], out[-1500:]))
+    assert not failures, failures
