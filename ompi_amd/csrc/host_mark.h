@@ -1,7 +1,7 @@
 // Host-observed completion marks and the library's host-side waits.
 //
 // A one-wave kernel enqueued after a call's work stores a sequence number
-// into a word of pinned, coherent host memory with a system-scope release;
+// into a word of pinned, coherent host memory (system scope, written through);
 // the host spins on that word.  Launch to observed completion of a tiny
 // kernel on MI355X: 6.3 µs this way, 11.8 µs polling hipEventQuery, 11.2 µs
 // inside hipStreamSynchronize, 17.6 µs polling hipStreamQuery

@@ -9,8 +9,13 @@
 
 namespace ompi_amd {
 
+// A relaxed system-scope store (written through to host memory): the
+// earlier kernels of the stream completed, with their own end-of-dispatch
+// release, before this one started, so no fence is needed here — a release
+// fence at system scope writes back the L2 first (3.2 µs average kernel
+// time with it, profiles/r04_seam_kernel_stats_release.csv).
 __global__ void host_mark_kernel(uint64_t *word, uint64_t v) {
-    if (threadIdx.x == 0) __hip_atomic_store(word, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) __hip_atomic_store(word, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 static std::mutex g_mark_mu;
