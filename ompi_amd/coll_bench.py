@@ -684,7 +684,9 @@ def single_gpu_rows(mib: int = 256):
     GPU and every kernel is HBM-bound exactly like the op kernel.  Event-
     timed on a dedicated stream; algorithmic HBM bytes per call: accumulate
     3 x S (read target, read origin, write target), get_accumulate 5 x S
-    (+ fetch copy), put and the p2p receive copy 2 x S."""
+    (+ fetch copy), put and the p2p receive copy 2 x S, the derived-target
+    accumulate 1.5 x S (S/2 packed origin bytes into every other double:
+    origin read, target slots read and written)."""
     import torch
 
     from . import coll, osc, pml
@@ -710,6 +712,8 @@ def single_gpu_rows(mib: int = 256):
         b.synchronize()
         return a.elapsed_time(b) / iters / 1e3
 
+    from . import datatype as ddt
+    tvec = ddt.type_vector(S // 16, 1, 2, ddt.predefined("MPI_DOUBLE")).commit()
     rows = {}
     try:
         for name, fn, factor in (
@@ -718,6 +722,11 @@ def single_gpu_rows(mib: int = 256):
             ("get_accumulate_sum_f32", lambda: win.get_accumulate(x, r, S // 4, mop.MPI_FLOAT, 0,
                                                                   0, mop.MPI_SUM, stream=s), 5),
             ("put", lambda: win.put(x, 0, 0, S, stream=s), 2),
+            # derived target (MPI_Type_vector of single doubles at stride 2,
+            # spanning the window): the origin's S/2 packed bytes folded into
+            # every other double — read origin, read + write target slots
+            ("accumulate_ddt_vector_bl1_f64", lambda: win.accumulate_ddt(
+                x, S // 16, None, 0, 0, 1, tvec, mop.MPI_DOUBLE, mop.MPI_SUM, stream=s), 1.5),
             ("sendrecv_self", lambda: pml.sendrecv(comm, x, 0, 1, r, 0, 1, stream=s), 2),
         ):
             t = timed(fn)

@@ -82,11 +82,35 @@ __device__ __forceinline__ int64_t typed_offset(const ddt_elem *e, int n, I size
     return (int64_t)el * extent + e[i].disp + (int64_t)k * e[i].stride + (int64_t)w;
 }
 
+inline fastdiv make_fdiv(uint32_t d) {  // host side
+    if (d <= 1) return {0u, 0u, 0u};
+    uint32_t l = 0;
+    while ((1ull << l) < d) ++l;  // ceil(log2 d)
+    const uint64_t m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+    return {(uint32_t)m, 1u, l - 1};
+}
+
+// Fast path: all quantities in G-granule units fit 32 bits.
+template <int G>
+__device__ __forceinline__ int64_t typed_offset_fast(const ddt_elem *e, int n, uint32_t size_g,
+                                                     const fastdiv &sdiv, int64_t extent,
+                                                     uint32_t pg) {
+    constexpr int LG = G == 16 ? 4 : G == 8 ? 3 : G == 4 ? 2 : G == 2 ? 1 : 0;
+    const uint32_t el = fdiv_q(pg, sdiv);
+    const uint32_t q = pg - el * size_g;
+    const int i = find_elem(e, n, (int64_t)q << LG);
+    const uint32_t r = q - (uint32_t)(e[i].prefix >> LG);
+    const uint32_t k = fdiv_q(r, e[i].bdiv[LG]);
+    const uint32_t w = r - k * (uint32_t)(e[i].blen >> LG);
+    return (int64_t)el * extent + e[i].disp + (int64_t)k * e[i].stride + ((int64_t)w << LG);
+}
+
 // A program as other translation units see it (ddt_view_of).
 struct ddt_view {
     ddt_desc d;
     int64_t lo, hi;  // lowest / one past the highest typed byte of one instance
     int gran;        // power of two dividing every run, displacement and stride
+    int64_t max_blen;  // longest run
 };
 // false: not a valid program
 bool ddt_view_of(const ompi_amd_ddt_t *ddt, ddt_view *out);

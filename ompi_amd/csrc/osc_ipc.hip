@@ -404,7 +404,24 @@ static const auto g_acc = make_acc_table(std::make_integer_sequence<int, OMPI_AM
 // datatype program in LDS (ddt_kernel's position -> address mapping).
 // old (get_accumulate; else null): the target's elements before the update,
 // packed.  OP 0: replace (REPLACE), -1: none (NO_OP: fetch only).
-template <typename T, int OP>
+// Target position k (in elements of T) -> typed byte offset.  FAST: every
+// quantity in element units fits 32 bits and each run length has its
+// multiply-high divisor (ddt_device.h), instead of two 64-bit divisions
+// per element.
+template <typename T, bool FAST>
+__device__ __forceinline__ int64_t acc_offset(const ddt_desc &d, const ddt_elem *el, int64_t k) {
+    if constexpr (FAST)
+        return typed_offset_fast<(int)sizeof(T)>(el, d.nelem, (uint32_t)(d.size / (int64_t)sizeof(T)),
+                                                 d.sdiv, d.extent, (uint32_t)k);
+    else
+        return typed_offset<uint64_t>(el, d.nelem, (uint64_t)d.size, d.extent, (uint64_t)k * sizeof(T));
+}
+
+// Derived-target accumulate: element k of the packed origin stream `in`
+// combines into the k-th primitive slot of the target datatype.  Four
+// elements per lane per pass, their loads issued before any store.
+constexpr int kAccUnroll = 4;
+template <typename T, int OP, bool FAST>
 __global__ __launch_bounds__(kOscThreads) void ddt_acc_kernel(ddt_desc d, char *typed, const T *in,
                                                               T *old, int64_t n,
                                                               const uint32_t *gate) {
@@ -417,30 +434,48 @@ __global__ __launch_bounds__(kOscThreads) void ddt_acc_kernel(ddt_desc d, char *
     }
     if (threadIdx.x == 0) osc_acquire();
     __syncthreads();
-    const int64_t gs = (int64_t)gridDim.x * kOscThreads;
-    for (int64_t k = (int64_t)blockIdx.x * kOscThreads + threadIdx.x; k < n; k += gs) {
-        const int64_t off = typed_offset<uint64_t>(el, d.nelem, (uint64_t)d.size, d.extent,
-                                                   (uint64_t)k * sizeof(T));
-        T *t = reinterpret_cast<T *>(typed + off);
-        const T v = *t;
-        if (old) old[k] = v;
-        if constexpr (OP == 0) {
-            *t = in[k];
-        } else if constexpr (OP > 0) {
-            store_elem(t, opfn<OP, false>::f(v, in[k]));
+    const int64_t chunk = (int64_t)kOscThreads * kAccUnroll;
+    const int64_t gs = (int64_t)gridDim.x * chunk;
+    for (int64_t b = (int64_t)blockIdx.x * chunk + threadIdx.x; b < n; b += gs) {
+        T *t[kAccUnroll];
+        T v[kAccUnroll], x[kAccUnroll];
+#pragma unroll
+        for (int u = 0; u < kAccUnroll; ++u) {
+            const int64_t k = b + (int64_t)u * kOscThreads;
+            t[u] = nullptr;
+            if (k < n) {
+                t[u] = reinterpret_cast<T *>(typed + acc_offset<T, FAST>(d, el, k));
+                v[u] = *t[u];
+                if constexpr (OP >= 0) x[u] = in[k];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kAccUnroll; ++u) {
+            const int64_t k = b + (int64_t)u * kOscThreads;
+            if (!t[u]) continue;
+            if (old) old[k] = v[u];
+            if constexpr (OP == 0) {
+                *t[u] = x[u];
+            } else if constexpr (OP > 0) {
+                store_elem(t[u], opfn<OP, false>::f(v[u], x[u]));
+            }
         }
     }
     osc_epilogue();
 }
 
 using ddt_acc_fn = hipError_t (*)(dim3, const ddt_desc &, char *, const void *, void *, int64_t,
-                                  const uint32_t *, hipStream_t);
+                                  const uint32_t *, bool, hipStream_t);
 
 template <typename T, int OP>
 static hipError_t ddt_acc_launch(dim3 grid, const ddt_desc &d, char *typed, const void *in,
-                                 void *old, int64_t n, const uint32_t *gate, hipStream_t s) {
-    hipLaunchKernelGGL((ddt_acc_kernel<T, OP>), grid, dim3(kOscThreads), 0, s, d, typed,
-                       static_cast<const T *>(in), static_cast<T *>(old), n, gate);
+                                 void *old, int64_t n, const uint32_t *gate, bool fast, hipStream_t s) {
+    if (fast)  // d.sdiv holds size / sizeof(T)
+        hipLaunchKernelGGL((ddt_acc_kernel<T, OP, true>), grid, dim3(kOscThreads), 0, s, d, typed,
+                           static_cast<const T *>(in), static_cast<T *>(old), n, gate);
+    else
+        hipLaunchKernelGGL((ddt_acc_kernel<T, OP, false>), grid, dim3(kOscThreads), 0, s, d, typed,
+                           static_cast<const T *>(in), static_cast<T *>(old), n, gate);
     return hipGetLastError();
 }
 template <int OP, int TYPE>
@@ -1107,8 +1142,18 @@ static int acc_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount, const o
         const uint32_t *gate = taken_word(w, target, true);
         if (tdt) {
             const int64_t blocks = std::max<int64_t>(
-                1, std::min<int64_t>((n + kOscThreads - 1) / kOscThreads, osc_grid_cap()));
-            rc = record_hip(f(dim3((unsigned)blocks), tv.d, t, in, old, n, gate, s),
+                1, std::min<int64_t>((n + kOscThreads * kAccUnroll - 1) / (kOscThreads * kAccUnroll),
+                                     osc_grid_cap()));
+            // element-unit arithmetic in 32 bits when everything fits and every
+            // run, displacement and stride is a multiple of the element
+            ddt_desc dd = tv.d;
+            const int64_t e = (int64_t)ext;
+            static const bool fast_on = !(getenv("OMPI_AMD_OSC_DDT_FAST") &&
+                                          atoi(getenv("OMPI_AMD_OSC_DDT_FAST")) == 0);
+            const bool fast = fast_on && (e == 1 || e == 2 || e == 4 || e == 8 || e == 16) && tv.gran % e == 0 &&
+                              n < (1ll << 32) && dd.size / e < (1ll << 32) && tv.max_blen / e < (1ll << 32);
+            if (fast) dd.sdiv = make_fdiv((uint32_t)(dd.size / e));
+            rc = record_hip(f(dim3((unsigned)blocks), dd, t, in, old, n, gate, fast, s),
                             "osc derived accumulate launch");
         } else {  // contiguous target: the plain kernels on the packed streams
             if (fetch) rc = xfer_copy(t, old, tbytes, s, gate);

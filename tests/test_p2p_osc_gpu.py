@@ -27,3 +27,15 @@ def test_p2p_osc_parity(n):
             if bad:  # every failing rank's first message, short (the rank that failed first shows)
                 first.append(f"rank {r}: {bad[0]['case']}: {bad[0]['msg'][:300]}")
     assert not failures, ("\n".join(first), failures)
+
+
+def test_osc_derived_accumulate_generic_offsets_n3():
+    """The derived-datatype accumulates with the 64-bit typed-offset path
+    (OMPI_AMD_OSC_DDT_FAST=0; the default takes 32-bit multiply-high
+    divisors whenever the element counts fit): same oracle check."""
+    outs = run_ranks(3, timeout=300, worker=WORKER, tag="p2p_osc_slowddt_n",
+                     extra_env={"OMPI_AMD_OSC_DDT_FAST": "0",
+                                "P2P_OSC_ONLY": "osc_accumulate_derived_datatypes"})
+    for r, (rc, out) in enumerate(outs):
+        lines = [json.loads(ln) for ln in out.splitlines() if ln.startswith("{")]
+        assert rc == 0 and len(lines) == 1 and lines[0]["ok"], (r, rc, out[-2000:])
