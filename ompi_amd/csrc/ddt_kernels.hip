@@ -603,14 +603,19 @@ static bool unpack_nt(int64_t max_run) {
 }
 
 // Unpack: typed bytes one tile spans (its LDS holds only the packed bytes
-// of those periods); OMPI_AMD_DDT_UNPACK_TILE_BYTES, default the pack's.
-static int64_t unpack_tile_bytes() {
+// of those periods); OMPI_AMD_DDT_UNPACK_TILE_BYTES, default the pack's —
+// halved for periods of many runs (>= 8 elements): 256 MiB blacs-indexed
+// unpack (13 runs of 4-52 B) 1.62 -> 1.97 TB/s at 8 KiB, while
+// struct{int,double} (2 runs) and vector layouts (1 run) are faster at
+// 16 KiB (profiles/r04_unpack_tile_sweep.jsonl, r04_blacs_sweep_nt.jsonl).
+static int64_t unpack_tile_bytes(size_t runs) {
     static const int64_t v = [] {
         const char *e = getenv("OMPI_AMD_DDT_UNPACK_TILE_BYTES");
         const int64_t x = e ? atoll(e) : 0;
-        return (x >= 1024 && x <= (1 << 20)) ? x : tile_data_bytes();
+        return (x >= 1024 && x <= (1 << 20)) ? x : 0;
     }();
-    return v;
+    if (v) return v;
+    return runs >= 8 ? std::max<int64_t>(4096, tile_data_bytes() / 2) : tile_data_bytes();
 }
 
 static bool tile_off() {
@@ -649,7 +654,7 @@ static bool tile_period(const ompi_amd_ddt_t *ddt, size_t count, int G, bool unp
     if (P.pext < 0 || P.psize % G != 0) return false;
     if (unpack && P.psize > P.pext) return false;  // the tile's packed bytes must fit its LDS
     P.nt = unpack && unpack_nt(ident ? P.psize : ddt->max_blen) ? 1 : 0;
-    const int64_t tb = unpack ? unpack_tile_bytes() : tile_data_bytes();
+    const int64_t tb = unpack ? unpack_tile_bytes(ident ? 1 : ddt->host.size()) : tile_data_bytes();
     P.nper = std::max<int64_t>(1, (tb - P.span) / std::max<int64_t>(P.pext, 1) + 1);
     // LDS: the map, then the tile's typed span (the unpack stages only the
     // packed bytes of its periods, but sizing its LDS to those — more
