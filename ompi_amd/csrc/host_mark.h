@@ -65,8 +65,14 @@ hipError_t mark_stream_wait(hipStream_t s, I idle) {
             idle);
     static thread_local hipEvent_t evs[64] = {};
     int dev = 0;
+    hipDevice_t sdev = -1;
     hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess || dev < 0 || dev >= 64)
+    if (e == hipSuccess && hipStreamGetDevice(s, &sdev) != hipSuccess) {
+        (void)hipGetLastError();
+        sdev = -1;
+    }
+    // an event of this device records only into this device's streams
+    if (e != hipSuccess || dev < 0 || dev >= 64 || sdev != dev)
         return poll_wait([s](unsigned) { return hipStreamQuery(s); }, idle);
     if (!evs[dev]) {
         e = hipEventCreateWithFlags(&evs[dev], hipEventDisableTiming);
