@@ -197,6 +197,14 @@ def main():
         res = bench_op(args)
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline_op(args.cpu_seconds)
+            try:  # BASELINE configs[0]: the host-only allreduce row (never breaks the line)
+                from ompi_amd import coll_bench
+                row = coll_bench.cpu_baseline_ring(8, 64 << 20, 2.0 * 7 / 8, warmup=5, iters=20)
+                row["config"] = ("BASELINE configs[0]: MPI_Allreduce MPI_SUM MPI_FLOAT 64 MiB, 8 host "
+                                 "processes, coll/tuned ring_segmented (1 MiB segments) + op/base")
+                res["cpu_allreduce_configs0"] = row
+            except Exception as e:  # noqa: BLE001
+                res["cpu_allreduce_configs0_error"] = f"{type(e).__name__}: {e}"
         if not args.no_extras:
             try:  # SURVEY §8f rows 1 / 4 on one GPU; never breaks the headline
                 from ompi_amd import coll_bench

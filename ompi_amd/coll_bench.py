@@ -239,6 +239,15 @@ def bench_allreduce(args, metric: str, link_gbs: float):
     dom = max(xg, key=lambda k: xg[k]["kernel_ms"]) if xg else None
     red_gbs = xg[dom]["gbs"] if dom else None
     roof = (world - 1) * link_gbs
+    # the kernel behind each phase timer: the pipelined schemes (4-6) run
+    # one pipe_allreduce_kernel per call, timed as "fold"
+    kernel = ({"fold": "pipe_allreduce_kernel<float,SUM>"} if alg in PIPE_ALGS and not user else
+              {"fold": "reduce_kernel<float,SUM,8>", "gather": "copy_kernel",
+               "scatter": "copy_kernel"}).get(dom)
+    # HBM + fabric bytes per launch of that phase's kernel from the committed
+    # PMC passes (profiles/pmc.json, tools/profile_allreduce_pmc.sh): L2-to-
+    # fabric requests of the launching GPU, local and peer memory alike
+    traffic = _phase_traffic(world, alg, user, dom)
     res = {
         "metric": metric,
         "value": round(busbw, 2),
@@ -255,21 +264,23 @@ def bench_allreduce(args, metric: str, link_gbs: float):
         "config": {"workload": "MPI_Allreduce fp32 SUM 256 MiB per rank, xGMI IPC ring-order "
                                "fused reduce (BASELINE configs[3] headline point)",
                    "count": n, "bytes": S, "op": "MPI_SUM", "datatype": "MPI_FLOAT",
-                   "parallelism": f"{world} ranks, 1 GPU each", "busbw_factor": factor,
+                   "parallelism": (f"{world} ranks sharing cuda:0" if shared
+                                   else f"{world} ranks, 1 GPU each"), "busbw_factor": factor,
                    "algorithm": best_name, "algorithm_is_library_default": True,
                    "library_default_scheme": default_name, "autotune": autotune,
                    "bit_exact_dataset_E": default_exact,
                    "ipc_mode_legacy": comm.get_param("ipc_mode_legacy"),
                    "schemes": {}},
+        # in the shared-GPU rehearsal no byte crosses xGMI (every "peer" is
+        # this GPU's HBM): a fraction of R(N) would be meaningless, so none
         "roofline": {"bound": "xgmi", "achieved": red_gbs,
                      "peak": roof, "unit": "GB/s",
-                     "frac": round(red_gbs / roof, 4) if red_gbs else None,
-                     "traffic": None,
-                     "kernel": {"fold": "reduce_kernel<float,SUM>", "gather": "copy_kernel",
-                                "scatter": "copy_kernel"}.get(dom),
+                     "frac": round(red_gbs / roof, 4) if red_gbs and not shared else None,
+                     "traffic": traffic,
+                     "kernel": kernel,
                      "phase": dom, "kernel_ms": xg[dom]["kernel_ms"] if dom else None,
                      "phases": ph,
-                     "busbw_frac_of_R": round(busbw / roof, 4)},
+                     "busbw_frac_of_R": None if shared else round(busbw / roof, 4)},
         "rccl_comparator": ({"busbw": round(busbw_rccl, 2), "unit": "GB/s",
                              "ms_per_step": round(t_rccl * 1e3 / args.steps, 4)}
                             if t_rccl else None),
@@ -322,6 +333,28 @@ def bench_allreduce(args, metric: str, link_gbs: float):
     return res if rank == 0 else None
 
 
+def _phase_traffic(world: int, alg: int, user: bool, phase):
+    """Bytes per launch of `phase`'s kernel under scheme `alg` at `world`
+    ranks from profiles/pmc.json (FETCH_SIZE x 2 + WRITE_SIZE, separate
+    rocprofv3 --pmc passes of tools/allreduce_pmc_probe.py: the ranks share
+    one MI355X there, so peer accesses are counted as the same L2-to-fabric
+    requests a dedicated GPU sends over xGMI), or None when no pass exists
+    for this (N, scheme, phase)."""
+    import json as _json
+
+    if phase is None or user:
+        return None
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    try:
+        with open(os.path.join(root, "profiles", "pmc.json")) as f:
+            entry = _json.load(f).get(f"allreduce_256MiB_n{world}_{dict(ALGORITHMS)[alg]}")
+    except (OSError, ValueError):
+        return None
+    if not entry or phase not in entry.get("phases", {}):
+        return None
+    return entry["phases"][phase]["traffic"]
+
+
 def _schemes(comm, dist, torch, mop, n, rank, shared, tdev, ours, default):
     """Every data-movement scheme x transfer grid, measured after the
     headline (config.schemes only; the headline is the library default).
@@ -357,12 +390,15 @@ def _schemes(comm, dist, torch, mop, n, rank, shared, tdev, ours, default):
     return schemes
 
 
-def cpu_baseline_ring(world: int, nbytes: int, factor: float, seconds: float = 10.0) -> dict:
+def cpu_baseline_ring(world: int, nbytes: int, factor: float, seconds: float = 10.0,
+                      warmup: int = 2, iters: int | None = None) -> dict:
     """The reference's CPU path for this metric, restated: coll/tuned's
     ring_segmented allreduce (coll_base_allreduce.c:618-856) with op/base's
     loop as the reduction, `world` host processes over POSIX shared memory
-    (tools/cpu_ring_baseline.c, linked against the oracle), on the same
-    message size.  A bounded sample of about `seconds` of ring time."""
+    (tools/cpu_ring_baseline.c, linked against the oracle; bit-exact with the
+    oracle's ring_segmented on dataset R, tests/test_coll_cpu.py), on the
+    same message size.  A bounded sample of about `seconds` of ring time,
+    or exactly `iters` timed iterations after `warmup`."""
     import json as _json
     import subprocess
 
@@ -371,9 +407,10 @@ def cpu_baseline_ring(world: int, nbytes: int, factor: float, seconds: float = 1
     if not os.path.exists(exe):
         subprocess.run(["make", "-C", os.path.join(root, "tools"), "cpu_ring_baseline"],
                        check=True, capture_output=True)
-    est = nbytes / 1.5e9  # seconds per iteration at the ~1.7 GB/s algbw seen in round 1
-    iters = max(5, min(200, int(seconds / max(est, 1e-6))))
-    out = subprocess.run([exe, str(world), str(nbytes), "2", str(iters)], check=True,
+    if iters is None:
+        est = nbytes / 1.5e9  # seconds per iteration at the ~1.7 GB/s algbw seen in round 1
+        iters = max(5, min(200, int(seconds / max(est, 1e-6))))
+    out = subprocess.run([exe, str(world), str(nbytes), str(warmup), str(iters)], check=True,
                          capture_output=True, text=True, timeout=600)
     line = _json.loads(out.stdout.strip().splitlines()[-1])
     import bench as _bench  # host_cpu(): nproc and CPU model beside the cores used
@@ -381,7 +418,8 @@ def cpu_baseline_ring(world: int, nbytes: int, factor: float, seconds: float = 1
             **_bench.host_cpu(),
             "sample": f"ring_segmented restatement (tools/cpu_ring_baseline.c, oracle op/base "
                       f"loop), {world} processes x 1 core over POSIX shm, {nbytes} B per rank, "
-                      f"{iters} timed iterations (median {line['median_s']:.4f} s); value is "
+                      f"{iters} timed iterations after {warmup} warm-ups (median "
+                      f"{line['median_s']:.4f} s, algbw {line['algbw_GBps']} GB/s); value is "
                       f"busBW = S/t x {factor:.3f}"}
 
 

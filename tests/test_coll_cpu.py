@@ -110,3 +110,34 @@ def test_block_partition_matches_oracle():
                 tot += cnt
             assert tot == count
             assert sorted(coll.block_owner(n, b) for b in range(n)) == list(range(n))
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_cpu_ring_baseline_matches_oracle(tmp_path, n):
+    """The N-process CPU baseline (tools/cpu_ring_baseline.c, the bench's
+    `cpu_baseline` for the allreduce and for BASELINE configs[0]) computes
+    exactly what the oracle's ring_segmented does: dataset R (U(-1,1), where
+    summation orders round differently) at several phases and ragged
+    blocks, every rank, every element bit-exact."""
+    from oracle import oracle as orc
+    exe = os.path.join(ROOT, "tools", "cpu_ring_baseline")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "tools"), "cpu_ring_baseline"], check=True,
+                       capture_output=True)
+    seg = (1 << 20) // 4
+    count = 3 * n * seg + 1001  # three phases plus a ragged tail
+    xs = [np.random.default_rng(20261015 + r).uniform(-1, 1, count).astype(np.float32) for r in range(n)]
+    for r, x in enumerate(xs):
+        x.tofile(tmp_path / f"in.{r}")
+    subprocess.run([exe, str(n), str(count * 4), "0", "1", str(tmp_path / "in"), str(tmp_path / "out")],
+                   check=True, capture_output=True, timeout=300)
+    exp, alg = orc.allreduce_forced(xs, count, 3, 15, orc.ALG_RING_SEGMENTED, segsize=1 << 20)
+    assert alg == orc.ALG_RING_SEGMENTED
+    differs = False
+    for r in range(n):
+        got = np.fromfile(tmp_path / f"out.{r}", dtype=np.float32)
+        assert np.array_equal(got.view(np.uint32), exp[r].view(np.uint32)), r
+        # the data really distinguishes orders (N > 2: a left-to-right sum
+        # rounds differently somewhere)
+        differs = differs or not np.array_equal(got, sum(xs[1:], xs[0].copy()))
+    assert differs or n == 2

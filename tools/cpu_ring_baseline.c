@@ -12,8 +12,12 @@
  * straight out of the mailbox — one copy per byte, the cost of btl/sm's
  * single-copy path.
  *
- * usage: cpu_ring_baseline <nranks> <bytes> <warmup> <iters>
- * prints one JSON line (rank 0): median seconds, GB/s, busBW.
+ * usage: cpu_ring_baseline <nranks> <bytes> <warmup> <iters> [<in> <out>]
+ * prints one JSON line (rank 0): median seconds, GB/s, busBW.  With <in> and
+ * <out>, rank r reads its input from the raw float32 file <in>.<r> instead of
+ * generating dataset E and writes its result to <out>.<r>: the CPU test
+ * (tests/test_coll_cpu.py) feeds dataset R this way and compares every
+ * element bit-exactly with the oracle's ring_segmented.
  */
 #define _GNU_SOURCE
 #include <sched.h>
@@ -29,13 +33,12 @@
 
 #include "../oracle/oracle.h"
 
-#define SLOT (1u << 20)
+#define SEGSIZE (1u << 20) /* coll_tuned_allreduce_algorithm_segmentsize */
 
 typedef struct {
     _Atomic uint64_t full[2];   /* sequence number of the message in slot */
     _Atomic uint64_t freed[2];  /* sequence number the receiver released */
     char pad[32];
-    char data[2][SLOT];
 } mailbox_t;
 
 typedef struct {
@@ -45,8 +48,15 @@ typedef struct {
 } ctl_t;
 
 static mailbox_t *boxes;
+static char *slots;     /* [N][2][slot_bytes]: mailbox r's two message slots */
+static size_t slot_bytes;
 static ctl_t *ctl;
 static int N;
+
+static char *slot_data(int box, int slot)
+{
+    return slots + ((size_t) box * 2 + (size_t) slot) * slot_bytes;
+}
 
 static double now(void)
 {
@@ -77,7 +87,7 @@ static void send_to(int dst, const void *buf, size_t bytes)
     /* wait until the receiver released the message two sends ago */
     while (s > 2 && atomic_load_explicit(&b->freed[slot], memory_order_acquire) < s - 2)
         sched_yield();
-    memcpy(b->data[slot], buf, bytes);
+    memcpy(slot_data(dst, slot), buf, bytes);
     atomic_store_explicit(&b->full[slot], s, memory_order_release);
 }
 
@@ -87,7 +97,7 @@ static const void *recv_wait(int me)
     uint64_t s = ++recv_seq;
     int slot = (int) (s & 1);
     while (atomic_load_explicit(&b->full[slot], memory_order_acquire) < s) sched_yield();
-    return b->data[slot];
+    return slot_data(me, slot);
 }
 
 static void recv_done(int me)
@@ -103,18 +113,36 @@ static void blockcount(size_t count, size_t n, size_t *split, size_t *early, siz
     if (*split) *early += 1;
 }
 
-/* ring_segmented, float SUM: the reference's phase / block / segment plan */
-static void allreduce(int r, const float *sbuf, float *rbuf, size_t count)
+/* The phase count of ring_segmented (coll_base_allreduce.c:661-665); below
+   N segments the reference runs the plain ring (:655-659), i.e. one phase. */
+static size_t phases(size_t count)
 {
-    const size_t seg = SLOT / sizeof(float);
-    size_t split, early, late, nph, ph;
-    int k;
-    memcpy(rbuf, sbuf, count * sizeof(float));
-    nph = count / ((size_t) N * seg);
+    const size_t seg = SEGSIZE / sizeof(float);
+    size_t nph = count / ((size_t) N * seg);
     if ((count % ((size_t) N * seg) >= (size_t) N) &&
         (count % ((size_t) N * seg) > ((size_t) N * seg) / 2))
         nph++;
-    if (nph == 0) nph = 1;
+    return nph ? nph : 1;
+}
+
+/* The largest message: a phase segment of an early block (the reference's
+   max_segcount, :674-678), which exceeds the segment size by up to half of
+   it; the allgather's fragments are at most one segment. */
+static size_t max_message(size_t count)
+{
+    size_t split, early, late, sp, e, l;
+    blockcount(count, (size_t) N, &split, &early, &late);
+    blockcount(early, phases(count), &sp, &e, &l);
+    return (e > SEGSIZE / sizeof(float) ? e : SEGSIZE / sizeof(float)) * sizeof(float);
+}
+
+/* ring_segmented, float SUM: the reference's phase / block / segment plan */
+static void allreduce(int r, const float *sbuf, float *rbuf, size_t count)
+{
+    const size_t seg = SEGSIZE / sizeof(float);
+    size_t split, early, late, nph = phases(count), ph;
+    int k;
+    memcpy(rbuf, sbuf, count * sizeof(float));
     blockcount(count, (size_t) N, &split, &early, &late);
     for (ph = 0; ph < nph; ph++) {
 #define RANGE(b, off, cnt)                                                        \
@@ -182,9 +210,14 @@ int main(int argc, char **argv)
     size_t bytes, count;
     int warm, iters, r;
     double *times;
-    if (argc < 5) {
-        fprintf(stderr, "usage: %s nranks bytes warmup iters\n", argv[0]);
+    const char *in_prefix = NULL, *out_prefix = NULL;
+    if (argc != 5 && argc != 7) {
+        fprintf(stderr, "usage: %s nranks bytes warmup iters [in-prefix out-prefix]\n", argv[0]);
         return 2;
+    }
+    if (argc == 7) {
+        in_prefix = argv[5];
+        out_prefix = argv[6];
     }
     N = atoi(argv[1]);
     bytes = strtoull(argv[2], NULL, 10);
@@ -193,6 +226,13 @@ int main(int argc, char **argv)
     count = bytes / sizeof(float);
     boxes = mmap(NULL, sizeof(mailbox_t) * (size_t) N, PROT_READ | PROT_WRITE,
                  MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+    slot_bytes = (max_message(count) + 63) & ~(size_t) 63;
+    slots = mmap(NULL, slot_bytes * 2 * (size_t) N, PROT_READ | PROT_WRITE,
+                 MAP_SHARED | MAP_ANONYMOUS, -1, 0);
+    if (boxes == MAP_FAILED || slots == MAP_FAILED) {
+        perror("mmap");
+        return 1;
+    }
     ctl = mmap(NULL, sizeof(ctl_t), PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
     times = mmap(NULL, sizeof(double) * (size_t) iters * (size_t) N, PROT_READ | PROT_WRITE,
                  MAP_SHARED | MAP_ANONYMOUS, -1, 0);
@@ -207,8 +247,20 @@ int main(int argc, char **argv)
             CPU_ZERO(&set);
             CPU_SET(r % (int) sysconf(_SC_NPROCESSORS_ONLN), &set);
             sched_setaffinity(0, sizeof(set), &set);  /* --bind-to core */
-            for (i = 0; i < count; i++)               /* dataset E: k * 2^-8 */
-                s[i] = (float) ((int) ((i * 2654435761u + (unsigned) r * 97u) % 2049u) - 1024) / 256.0f;
+            if (in_prefix) {  /* the caller's input (dataset R in the CPU test) */
+                char path[4096];
+                FILE *f;
+                snprintf(path, sizeof(path), "%s.%d", in_prefix, r);
+                f = fopen(path, "rb");
+                if (!f || fread(s, 1, bytes, f) != bytes) {
+                    fprintf(stderr, "rank %d: cannot read %s\n", r, path);
+                    _exit(1);
+                }
+                fclose(f);
+            } else {
+                for (i = 0; i < count; i++)  /* dataset E: k * 2^-8 */
+                    s[i] = (float) ((int) ((i * 2654435761u + (unsigned) r * 97u) % 2049u) - 1024) / 256.0f;
+            }
             for (it = 0; it < warm + iters; it++) {
                 double t0;
                 barrier();
@@ -216,6 +268,18 @@ int main(int argc, char **argv)
                 allreduce(r, s, o, count);
                 barrier();
                 if (it >= warm) times[(size_t) (it - warm) * N + r] = now() - t0;
+            }
+            if (out_prefix) {  /* the result, for the caller's comparison */
+                char path[4096];
+                FILE *f;
+                snprintf(path, sizeof(path), "%s.%d", out_prefix, r);
+                f = fopen(path, "wb");
+                if (!f || fwrite(o, 1, bytes, f) != bytes) {
+                    fprintf(stderr, "rank %d: cannot write %s\n", r, path);
+                    _exit(1);
+                }
+                fclose(f);
+                _exit(0);
             }
             /* dataset E sums exactly in any order: check every element */
             for (i = 0; i < count; i++) {
