@@ -118,6 +118,15 @@ int ompi_amd_comm_agree(ompi_amd_comm_t *comm, int local_ok, int *all_ok);
  * "boot_calls". */
 int ompi_amd_comm_vote(ompi_amd_comm_t *comm, int local_yes, int *n_yes);
 
+/* This rank cannot take part in a collective its peers will run on the
+ * device (e.g. staging its operands failed after the path was agreed):
+ * make `rc` (an OMPI_AMD_ERR_* code) this communicator's sticky error and
+ * raise every peer's abort word, so the peers' barrier waits give up within
+ * about 1 ms and their calls fail with OMPI_AMD_ERR_TIMEOUT instead of
+ * waiting out timeout_ms.  The communicator is unusable afterwards (MPI:
+ * an error in a collective leaves it undefined). */
+int ompi_amd_comm_abort(ompi_amd_comm_t *comm, int rc);
+
 /* Wait for `stream` (NULL = per-thread) and report a sticky device error:
  * the blocking completion the MPI entry points need. */
 int ompi_amd_comm_sync(ompi_amd_comm_t *comm, void *stream);

@@ -105,6 +105,19 @@ int ompi_amd_get_accumulate_ddt(ompi_amd_win_t *win, const void *origin, size_t 
                                 const ompi_amd_ddt_t *odt, void *result, size_t rcount,
                                 const ompi_amd_ddt_t *rdt, int target, size_t disp, size_t tcount,
                                 const ompi_amd_ddt_t *tdt, int type, int op, void *stream);
+/* MPI_Put / MPI_Get with derived datatypes (osc_sm_comm.c:24-100,
+ * 209-270: ompi_datatype_sndrcv of any datatype pair): the origin's ocount x
+ * odt bytes, in type-map order, into (put) or out of (get) the tcount x tdt
+ * layout at the target; only the target type's bytes are written, its gaps
+ * keep theirs.  odt / tdt NULL: `ocount` / `tcount` contiguous bytes.  Both
+ * sides must move the same number of bytes.  No accumulate lock (put and
+ * get are not atomic); inside a passive epoch the epoch's lock gates it. */
+int ompi_amd_put_ddt(ompi_amd_win_t *win, const void *origin, size_t ocount,
+                     const ompi_amd_ddt_t *odt, int target, size_t disp, size_t tcount,
+                     const ompi_amd_ddt_t *tdt, void *stream);
+int ompi_amd_get_ddt(ompi_amd_win_t *win, void *origin, size_t ocount, const ompi_amd_ddt_t *odt,
+                     int target, size_t disp, size_t tcount, const ompi_amd_ddt_t *tdt,
+                     void *stream);
 /* get_accumulate of one element. */
 int ompi_amd_fetch_and_op(ompi_amd_win_t *win, const void *origin, void *result, int type,
                           int target, size_t disp, int op, void *stream);
@@ -158,6 +171,12 @@ int ompi_amd_rget_accumulate(ompi_amd_win_t *win, const void *origin, void *resu
                              int type, int target, size_t disp, int op, void *stream,
                              ompi_amd_rma_request_t **request);
 /* request-based forms of the derived-datatype calls above */
+int ompi_amd_rput_ddt(ompi_amd_win_t *win, const void *origin, size_t ocount,
+                      const ompi_amd_ddt_t *odt, int target, size_t disp, size_t tcount,
+                      const ompi_amd_ddt_t *tdt, void *stream, ompi_amd_rma_request_t **req);
+int ompi_amd_rget_ddt(ompi_amd_win_t *win, void *origin, size_t ocount, const ompi_amd_ddt_t *odt,
+                      int target, size_t disp, size_t tcount, const ompi_amd_ddt_t *tdt, void *stream,
+                      ompi_amd_rma_request_t **req);
 int ompi_amd_raccumulate_ddt(ompi_amd_win_t *win, const void *origin, size_t ocount,
                              const ompi_amd_ddt_t *odt, int target, size_t disp, size_t tcount,
                              const ompi_amd_ddt_t *tdt, int type, int op, void *stream,

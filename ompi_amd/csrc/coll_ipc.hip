@@ -420,6 +420,7 @@ struct ompi_amd_comm {
     int64_t exports_new = 0, imports_new = 0;  // runtime export / open calls made (cache misses)
     int recycled_exports = 0;             // exports refused: recycled handle bytes (shadowed)
     int unsafe_exports = 0;               // application buffers of no IPC-safe size (shadowed)
+    int aged_exports = 0;                 // application buffers older than an IPC close (shadowed)
     // streams this communicator launched work on: the current one, plus an
     // event recorded on each earlier one when the calls moved away from it
     // (quiesce() waits for exactly that work, not for the whole device)
@@ -713,6 +714,22 @@ static int export_alloc(void *base, size_t size, unsigned long long id, hipIpcMe
     return recycled ? 1 : 0;
 }
 
+// Whether this process exported (base, size, id) before: its handle was
+// made before any later close, so it stays valid (ipc_close_watermark).
+static bool export_known(void *base, size_t size, unsigned long long id) {
+    std::lock_guard<std::mutex> g(g_exp_mu);
+    for (const auto &r : g_exp)
+        if (r.base == base && r.size == size && r.id == id) return true;
+    return false;
+}
+
+// An allocation this process may not export any more: it predates a close
+// of one of its IPC mappings (ROCm 7.2 then refuses its export, for good,
+// 10-30 % of the time — ipc_registry.h) and was not exported before.
+static bool export_aged(void *base, size_t size, unsigned long long id) {
+    return id < ipc_close_watermark() && !export_known(base, size, id);
+}
+
 // IPC-safe allocation sizes on ROCm 7.2 (tools/ipc_replay_probe.py,
 // profiles/r04_ipc_replay*.jsonl, N = 4 / 8 processes on one MI355X):
 //  - below 2 MiB hipMalloc sub-allocates from a shared chunk, and the import
@@ -790,6 +807,16 @@ static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d, bool *ip
         ++c->unsafe_exports;
         record_msg("allocation %p + %zu is not an IPC-safe size (a multiple of 2 MiB from 4 MiB)",
                    base, size);
+        return OMPI_AMD_ERR_HIP;
+    }
+    // A caller with a shadow never offers an allocation a close spoiled
+    // (ipc_registry.h).  One without (a window over the caller's memory)
+    // tries: most such exports work, and a refusal fails every rank alike.
+    if (ipc_failed && export_aged(base, size, id)) {
+        *ipc_failed = true;
+        ++c->aged_exports;
+        record_msg("allocation %p + %zu (id %llu) predates an IPC close of this process: not exported "
+                   "(DESIGN.md §4.6)", base, size, id);
         return OMPI_AMD_ERR_HIP;
     }
     hipIpcMemHandle_t h;
@@ -2812,6 +2839,14 @@ int ompi_amd_comm_vote(ompi_amd_comm_t *c, int local_yes, int *n_yes) {
     return OMPI_AMD_SUCCESS;
 }
 
+int ompi_amd_comm_abort(ompi_amd_comm_t *c, int rc) {
+    api_guard api_(c);
+    if (!c || rc >= 0) return OMPI_AMD_ERR_BAD_PARAM;
+    TRY(set_dev(c));
+    abort_peers(c, rc);
+    return OMPI_AMD_SUCCESS;
+}
+
 int ompi_amd_comm_sync(ompi_amd_comm_t *c, void *stream) {
     api_guard api_(c);
     if (!c) return OMPI_AMD_ERR_BAD_PARAM;
@@ -2913,6 +2948,7 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "copy_nt")) *v = c->copy_nt;
     else if (!strcmp(key, "copy_nt_fixed")) *v = c->copy_nt_fixed;
     else if (!strcmp(key, "unsafe_exports")) *v = c->unsafe_exports;
+    else if (!strcmp(key, "aged_exports")) *v = c->aged_exports;
     else if (!strncmp(key, "autotune_", 9) && c->tune_last_key >= 0 &&
              c->tune.count(c->tune_last_key) && c->tune.at(c->tune_last_key).done) {
         // the last decided bucket: its choice and every candidate's worst rank
@@ -2937,7 +2973,7 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "boot_calls")) *v = (int64_t)c->boot.posted();
     else if (!strcmp(key, "ipc_opens")) *v = ipc_get_stats().opens;
     else if (!strcmp(key, "ipc_refusals")) *v = ipc_get_stats().refusals;
-    else if (!strcmp(key, "ipc_recovered")) *v = ipc_get_stats().recovered;
+    else if (!strcmp(key, "ipc_close_watermark")) *v = (int64_t)ipc_close_watermark();
     else if (!strcmp(key, "ipc_closes")) *v = ipc_get_stats().closes;
     else if (!strcmp(key, "ipc_shared")) *v = ipc_get_stats().shared;
     else if (!strcmp(key, "ipc_retired")) *v = ipc_get_stats().retired;
@@ -4292,6 +4328,16 @@ int comm_export(ompi_amd_comm_t *c, const void *ptr, ipc_desc *d) {
     const int rc = export_buf(c, ptr, &b);
     memcpy(d, &b, sizeof(b));
     return rc;
+}
+
+bool comm_ipc_safe(const void *ptr) {
+    void *base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange((hipDeviceptr_t *)&base, &size, (hipDeviceptr_t)ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return ipc_safe_size(size) && size <= kMaxIpcBytes && !export_aged(base, size, buffer_id(ptr));
 }
 
 int comm_import(ompi_amd_comm_t *c, int peer, const ipc_desc &d, const char **out, bool pin,

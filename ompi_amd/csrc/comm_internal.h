@@ -47,6 +47,12 @@ int comm_arena_alloc(ompi_amd_comm_t *c, size_t bytes, void **out);
 void comm_arena_free(ompi_amd_comm_t *c, void *p);
 // Export a device buffer (cached per allocation).
 int comm_export(ompi_amd_comm_t *c, const void *ptr, ipc_desc *d);
+// Whether peers can map ptr's allocation as it is: an IPC-safe size (a
+// multiple of 2 MiB from 4 MiB) within the mapping limit,
+// and not spoiled by a later IPC close of this process unless exported
+// before it (ipc_close_watermark).  A caller with a library stage sends
+// other allocations through it.
+bool comm_ipc_safe(const void *ptr);
 // Map a peer's exported buffer (cached, LRU).  pin: held until comm_unpin.
 int comm_import(ompi_amd_comm_t *c, int peer, const ipc_desc &d, const char **out, bool pin,
                 void **base);

@@ -53,15 +53,8 @@ __device__ __forceinline__ void move_byte(const ddt_elem *el, const ddt_desc &d,
 // UNPACK = false: contig[p - start] = typed[p];  true: typed[p] = contig[p - start].
 // I = uint32_t: fast-division path (stream position / G < 2^32).
 template <int G, bool UNPACK, typename I>
-__global__ __launch_bounds__(kDdtThreads) void ddt_kernel(ddt_desc d, const char *src, char *dst,
-                                                          ddt_window w) {
-    __shared__ ddt_elem lds[kDdtLdsElems];
-    const ddt_elem *el = d.elems;
-    if (d.nelem <= kDdtLdsElems) {
-        for (int i = threadIdx.x; i < d.nelem; i += kDdtThreads) lds[i] = d.elems[i];
-        __syncthreads();
-        el = lds;
-    }
+__device__ __forceinline__ void ddt_body(const ddt_desc &d, const ddt_elem *el, int nelem, const char *src,
+                                         char *dst, const ddt_window &w) {
     using T = typename granule<G>::t;
     constexpr int U = kDdtUnroll;
     const int64_t stride = (int64_t)gridDim.x * kDdtThreads;
@@ -77,10 +70,10 @@ __global__ __launch_bounds__(kDdtThreads) void ddt_kernel(ddt_desc d, const char
             const int64_t p = w.body0 + j * G;
             if (j < w.ngran) {
                 if constexpr (sizeof(I) == 4)
-                    toff[u] = typed_offset_fast<G>(el, d.nelem, (uint32_t)(d.size / G), d.sdiv,
+                    toff[u] = typed_offset_fast<G>(el, nelem, (uint32_t)(d.size / G), d.sdiv,
                                                    d.extent, (uint32_t)(p / G));
                 else
-                    toff[u] = typed_offset<I>(el, d.nelem, (I)d.size, d.extent, (I)p);
+                    toff[u] = typed_offset<I>(el, nelem, (I)d.size, d.extent, (I)p);
             }
         }
 #pragma unroll
@@ -104,8 +97,30 @@ __global__ __launch_bounds__(kDdtThreads) void ddt_kernel(ddt_desc d, const char
     if (blockIdx.x == gridDim.x - 1) {
         for (int64_t k = threadIdx.x; k < w.head + w.tail; k += kDdtThreads) {
             const int64_t p = k < w.head ? w.start + k : w.tail0 + (k - w.head);
-            move_byte<UNPACK>(el, d, src, dst, p, w.start);
+            const int64_t t = typed_offset<uint64_t>(el, nelem, (uint64_t)d.size, d.extent, (uint64_t)p);
+            if (!UNPACK) dst[p - w.start] = src[t];
+            else dst[t] = src[p - w.start];
         }
+    }
+}
+
+// The element table's address space is known at every read (a table that
+// may live in LDS or global memory makes every read a flat load — five per
+// granule — as osc_ipc.hip's ddt_acc_kernel measured): one element in
+// registers (nelem a constant 1), up to kDdtLdsElems in LDS, else global.
+template <int G, bool UNPACK, typename I>
+__global__ __launch_bounds__(kDdtThreads) void ddt_kernel(ddt_desc d, const char *src, char *dst,
+                                                          ddt_window w) {
+    __shared__ ddt_elem lds[kDdtLdsElems];
+    if (d.nelem == 1) {
+        const ddt_elem e0 = d.elems[0];
+        ddt_body<G, UNPACK, I>(d, &e0, 1, src, dst, w);
+    } else if (d.nelem <= kDdtLdsElems) {
+        for (int i = threadIdx.x; i < d.nelem; i += kDdtThreads) lds[i] = d.elems[i];
+        __syncthreads();
+        ddt_body<G, UNPACK, I>(d, lds, d.nelem, src, dst, w);
+    } else {
+        ddt_body<G, UNPACK, I>(d, d.elems, d.nelem, src, dst, w);
     }
 }
 
@@ -401,16 +416,8 @@ __global__ __launch_bounds__(kDdtThreads) void ddt_unpack_tile_kernel(ddt_period
 // fragment train costs one launch instead of one per fragment.
 
 template <int G, bool UNPACK>
-__global__ __launch_bounds__(kDdtThreads) void ddt_iov_kernel(ddt_desc d, char *typed,
-                                                              const iov_job *jobs) {
-    __shared__ ddt_elem lds[kDdtLdsElems];
-    const ddt_elem *el = d.elems;
-    if (d.nelem <= kDdtLdsElems) {
-        for (int i = threadIdx.x; i < d.nelem; i += kDdtThreads) lds[i] = d.elems[i];
-        __syncthreads();
-        el = lds;
-    }
-    const iov_job jb = jobs[blockIdx.y];
+__device__ __forceinline__ void ddt_iov_body(const ddt_desc &d, const ddt_elem *el, int nelem, char *typed,
+                                             const iov_job &jb) {
     const int64_t start = jb.start, end = jb.start + jb.len;
     const int64_t body0 = min(end, (start + G - 1) / G * G);
     const int64_t body1 = max(body0, end / G * G);
@@ -426,7 +433,7 @@ __global__ __launch_bounds__(kDdtThreads) void ddt_iov_kernel(ddt_desc d, char *
         for (int u = 0; u < U; ++u) {
             const int64_t j = j0 + u * stride;
             if (j < ngran)
-                toff[u] = typed_offset<uint64_t>(el, d.nelem, (uint64_t)d.size, d.extent,
+                toff[u] = typed_offset<uint64_t>(el, nelem, (uint64_t)d.size, d.extent,
                                                  (uint64_t)(body0 + j * G));
         }
 #pragma unroll
@@ -449,11 +456,29 @@ __global__ __launch_bounds__(kDdtThreads) void ddt_iov_kernel(ddt_desc d, char *
         const int64_t head = body0 - start, tail = end - body1;
         for (int64_t k = threadIdx.x; k < head + tail; k += kDdtThreads) {
             const int64_t p = k < head ? start + k : body1 + (k - head);
-            const int64_t t = typed_offset<uint64_t>(el, d.nelem, (uint64_t)d.size, d.extent,
+            const int64_t t = typed_offset<uint64_t>(el, nelem, (uint64_t)d.size, d.extent,
                                                      (uint64_t)p);
             if (UNPACK) typed[t] = c[p];
             else c[p] = typed[t];
         }
+    }
+}
+
+// element table in registers / LDS / global memory, as ddt_kernel
+template <int G, bool UNPACK>
+__global__ __launch_bounds__(kDdtThreads) void ddt_iov_kernel(ddt_desc d, char *typed,
+                                                              const iov_job *jobs) {
+    __shared__ ddt_elem lds[kDdtLdsElems];
+    const iov_job jb = jobs[blockIdx.y];
+    if (d.nelem == 1) {
+        const ddt_elem e0 = d.elems[0];
+        ddt_iov_body<G, UNPACK>(d, &e0, 1, typed, jb);
+    } else if (d.nelem <= kDdtLdsElems) {
+        for (int i = threadIdx.x; i < d.nelem; i += kDdtThreads) lds[i] = d.elems[i];
+        __syncthreads();
+        ddt_iov_body<G, UNPACK>(d, lds, d.nelem, typed, jb);
+    } else {
+        ddt_iov_body<G, UNPACK>(d, d.elems, d.nelem, typed, jb);
     }
 }
 

@@ -52,10 +52,18 @@ hipError_t poll_wait(Q query, I idle) {
 // Everything enqueued on `s` so far is done: through this thread's mark
 // word (hipStreamQuery every 64 polls reports errors and an idle stream),
 // or, without marks, an event recorded on `s`.
+//
+// host_reads: the caller reads host memory the GPU wrote on `s` (a
+// device-to-host copy) once this returns.  A mark then proves nothing: the
+// copy's kernel may have ended with an agent-scope release (the runtime
+// relaxes it when a kernel follows on the stream), leaving host lines in
+// some XCD's L2 — and a fence inside the one-wave mark kernel writes back
+// only its own XCD's L2.  Such waits use the event, whose completion the
+// runtime makes host-visible.
 template <class I>
-hipError_t mark_stream_wait(hipStream_t s, I idle) {
+hipError_t mark_stream_wait(hipStream_t s, I idle, bool host_reads = false) {
     static thread_local uint64_t *word = mark_word_get();
-    const uint64_t v = mark_launch(word, s);
+    const uint64_t v = host_reads ? 0 : mark_launch(word, s);
     if (v)
         return poll_wait(
             [s, v](unsigned spins) {

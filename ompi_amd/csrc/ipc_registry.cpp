@@ -4,6 +4,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -44,6 +45,27 @@ struct user {
 };
 std::vector<user> g_users;
 ipc_stats g_st{};
+std::atomic<uint64_t> g_close_mark{0};  // ipc_close_watermark()
+
+// After a close: the buffer id of a fresh allocation — every allocation
+// with a lower id existed at the close (ipc_registry.h).
+void note_close() {
+    void *p = nullptr;
+    if (hipMalloc(&p, 4096) != hipSuccess) {
+        (void)hipGetLastError();
+        g_close_mark.store(UINT64_MAX);  // no id to compare with: spoil everything older
+        return;
+    }
+    unsigned long long id = 0;
+    if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)p) != hipSuccess) {
+        (void)hipGetLastError();
+        id = UINT64_MAX;
+    }
+    hip_ignore(hipFree(p));
+    uint64_t cur = g_close_mark.load();
+    while (cur < id && !g_close_mark.compare_exchange_weak(cur, id)) {
+    }
+}
 
 bool same_handle(const hipIpcMemHandle_t &x, const hipIpcMemHandle_t &y) {
     return memcmp(&x, &y, sizeof(x)) == 0;
@@ -84,6 +106,7 @@ void close_mapping(ipc_ref *r) {
     const auto t0 = std::chrono::steady_clock::now();
     const hipError_t e = hipIpcCloseMemHandle(r->base);
     hip_ignore(e);
+    note_close();
     if (trace())
         fprintf(stderr, "[ipc pid %d] close pid %llu id %llu %p+%llu -> %p%s (%.3f ms)\n", (int)getpid(),
                 (unsigned long long)r->a.pid, (unsigned long long)r->a.id,
@@ -189,31 +212,17 @@ int ipc_map(const ipc_alloc &a, void *owner, ipc_ref **ref, void **base) {
         done_opening(a);
         return rc;
     }
-    // One open: the exportable allocations are sized so that the runtime
-    // answers (tools/ipc_replay_probe.py): a refusal is an
-    // error, reported with the buffer, never retried.
+    // One open, never retried: the exportable allocations are sized so that
+    // the runtime answers, and no exporter hands out an
+    // allocation a close of its own spoiled (ipc_close_watermark) — a
+    // refusal is an error, reported with the buffer.
     void *m = nullptr;
     const auto t_open = std::chrono::steady_clock::now();
-    hipError_t e = hipIpcOpenMemHandle(&m, a.h, hipIpcMemLazyEnablePeerAccess);
-    // Residual: a range the exporter freed and allocated
-    // again — the mapping of the old allocation retired and closed just
-    // above — is, about once in several hundred such re-imports at N = 8,
-    // refused with "invalid device pointer" although its size is IPC-safe;
-    // the same open 4 ms later succeeds (the replay probe's recycle_gap
-    // order: 0 refusals).  Only that case is tried again, once, and counted.
-    bool again = false;
-    if (e != hipSuccess && !stale.empty()) {
-        (void)hipGetLastError();
-        usleep(4000);
-        m = nullptr;
-        e = hipIpcOpenMemHandle(&m, a.h, hipIpcMemLazyEnablePeerAccess);
-        again = true;
-    }
+    const hipError_t e = hipIpcOpenMemHandle(&m, a.h, hipIpcMemLazyEnablePeerAccess);
     const double open_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_open).count();
     std::lock_guard<std::mutex> g(g_mu);
-    g_st.opens += again ? 2 : 1;
-    if (again && e == hipSuccess) ++g_st.recovered;
+    ++g_st.opens;
     done_opening(a);
     if (e != hipSuccess) {
         (void)hipGetLastError();
@@ -242,6 +251,7 @@ int ipc_map(const ipc_alloc &a, void *owner, ipc_ref **ref, void **base) {
         const uint64_t up = (a.size + (2u << 20) - 1) & ~(uint64_t)((2u << 20) - 1);
         if (mb != m || ms < a.size || ms > up) {
             hip_ignore(hipIpcCloseMemHandle(m));
+            note_close();
             ++g_st.closes;
             record_msg("hipIpcOpenMemHandle for process %llu buffer id %llu (%llu bytes) returned "
                        "a mapping of %zu bytes at %p", (unsigned long long)a.pid,
@@ -322,6 +332,8 @@ void ipc_remove_user(void *owner) {
                                  [&](const user &u) { return u.owner == owner; }),
                   g_users.end());
 }
+
+uint64_t ipc_close_watermark() { return g_close_mark.load(); }
 
 ipc_stats ipc_get_stats() {
     std::lock_guard<std::mutex> g(g_mu);

@@ -57,10 +57,21 @@ void *ipc_ref_base(const ipc_ref *ref);
 void ipc_add_user(void *owner, int (*quiesce)(void *owner));
 void ipc_remove_user(void *owner);
 
+// Closing an IPC mapping spoils the exportability of device allocations
+// this process already has: ROCm 7.2's hipIpcGetMemHandle then refuses
+// ("invalid argument"), for good, 10-30 % of the allocations that existed
+// at the close, and none made after it (tools/ipc_p2p_replay.py,
+// profiles/r05_ipc_p2p_replay*.jsonl: the round-4 refused exports).  Every
+// close here records the buffer id of an allocation made right after it
+// (HIP_POINTER_ATTRIBUTE_BUFFER_ID grows with every allocation): an
+// allocation with a lower id predates a close and is not exported unless it
+// was exported before (its handle stays valid); callers send it through a
+// library stage or shadow instead.
+uint64_t ipc_close_watermark();
+
 struct ipc_stats {
     int64_t opens;        // hipIpcOpenMemHandle calls made
     int64_t refusals;     // opens the runtime refused (each one failed its call)
-    int64_t recovered;    // re-imports of a just-retired range refused once, then opened
     int64_t closes;       // hipIpcCloseMemHandle calls made
     int64_t shared;       // ipc_map answered from a mapping the process held
     int64_t retired;      // mappings retired because the exporter freed the allocation

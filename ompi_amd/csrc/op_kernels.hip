@@ -312,7 +312,8 @@ static int reduce_mixed(int op, int type, bool three, const void *in1, const voi
     if (rc == OMPI_AMD_SUCCESS && dout != out)
         rc = record_hip(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, s),
                         "op handler: result to host");
-    if (rc == OMPI_AMD_SUCCESS) rc = record_hip(mark_stream_wait(s, no_idle), "op sync");
+    // the caller reads a host `out` at once: the event wait (host_mark.h)
+    if (rc == OMPI_AMD_SUCCESS) rc = record_hip(mark_stream_wait(s, no_idle, dout != out), "op sync");
     return rc;
 }
 

@@ -409,12 +409,13 @@ static const auto g_acc = make_acc_table(std::make_integer_sequence<int, OMPI_AM
 // multiply-high divisor (ddt_device.h), instead of two 64-bit divisions
 // per element.
 template <typename T, bool FAST>
-__device__ __forceinline__ int64_t acc_offset(const ddt_desc &d, const ddt_elem *el, int64_t k) {
+__device__ __forceinline__ int64_t acc_offset(const ddt_desc &d, const ddt_elem *el, int nelem,
+                                              int64_t k) {
     if constexpr (FAST)
-        return typed_offset_fast<(int)sizeof(T)>(el, d.nelem, (uint32_t)(d.size / (int64_t)sizeof(T)),
+        return typed_offset_fast<(int)sizeof(T)>(el, nelem, (uint32_t)(d.size / (int64_t)sizeof(T)),
                                                  d.sdiv, d.extent, (uint32_t)k);
     else
-        return typed_offset<uint64_t>(el, d.nelem, (uint64_t)d.size, d.extent, (uint64_t)k * sizeof(T));
+        return typed_offset<uint64_t>(el, nelem, (uint64_t)d.size, d.extent, (uint64_t)k * sizeof(T));
 }
 
 // Derived-target accumulate: element k of the packed origin stream `in`
@@ -422,18 +423,8 @@ __device__ __forceinline__ int64_t acc_offset(const ddt_desc &d, const ddt_elem 
 // elements per lane per pass, their loads issued before any store.
 constexpr int kAccUnroll = 4;
 template <typename T, int OP, bool FAST>
-__global__ __launch_bounds__(kOscThreads) void ddt_acc_kernel(ddt_desc d, char *typed, const T *in,
-                                                              T *old, int64_t n,
-                                                              const uint32_t *gate) {
-    if (!gate_open(gate)) return;
-    __shared__ ddt_elem lds[kDdtLdsElems];
-    const ddt_elem *el = d.elems;
-    if (d.nelem <= kDdtLdsElems) {
-        for (int i = threadIdx.x; i < d.nelem; i += kOscThreads) lds[i] = d.elems[i];
-        el = lds;
-    }
-    if (threadIdx.x == 0) osc_acquire();
-    __syncthreads();
+__device__ __forceinline__ void ddt_acc_body(const ddt_desc &d, const ddt_elem *el, int nelem, char *typed,
+                                             const T *in, T *old, int64_t n) {
     const int64_t chunk = (int64_t)kOscThreads * kAccUnroll;
     const int64_t gs = (int64_t)gridDim.x * chunk;
     for (int64_t b = (int64_t)blockIdx.x * chunk + threadIdx.x; b < n; b += gs) {
@@ -444,7 +435,7 @@ __global__ __launch_bounds__(kOscThreads) void ddt_acc_kernel(ddt_desc d, char *
             const int64_t k = b + (int64_t)u * kOscThreads;
             t[u] = nullptr;
             if (k < n) {
-                t[u] = reinterpret_cast<T *>(typed + acc_offset<T, FAST>(d, el, k));
+                t[u] = reinterpret_cast<T *>(typed + acc_offset<T, FAST>(d, el, nelem, k));
                 v[u] = *t[u];
                 if constexpr (OP >= 0) x[u] = in[k];
             }
@@ -460,6 +451,33 @@ __global__ __launch_bounds__(kOscThreads) void ddt_acc_kernel(ddt_desc d, char *
                 store_elem(t[u], opfn<OP, false>::f(v[u], x[u]));
             }
         }
+    }
+}
+
+// The element table's address space must be known where the loop reads it
+// (else every read is a flat load, five per element: 1.70 TB/s on the
+// bench's vector target, against 2.73 TB/s for the same loop reading LDS,
+// tools/ddt_acc_probe.hip): a single-element type (every vector) keeps its
+// element in registers (a constant nelem of 1 lets the compiler scalarise
+// it), up to kDdtLdsElems stage in LDS, longer tables stay in global memory.
+template <typename T, int OP, bool FAST>
+__global__ __launch_bounds__(kOscThreads) void ddt_acc_kernel(ddt_desc d, char *typed, const T *in,
+                                                              T *old, int64_t n,
+                                                              const uint32_t *gate) {
+    if (!gate_open(gate)) return;
+    __shared__ ddt_elem lds[kDdtLdsElems];
+    if (threadIdx.x == 0) osc_acquire();
+    if (d.nelem == 1) {
+        const ddt_elem e0 = d.elems[0];
+        __syncthreads();
+        ddt_acc_body<T, OP, FAST>(d, &e0, 1, typed, in, old, n);
+    } else if (d.nelem <= kDdtLdsElems) {
+        for (int i = threadIdx.x; i < d.nelem; i += kOscThreads) lds[i] = d.elems[i];
+        __syncthreads();
+        ddt_acc_body<T, OP, FAST>(d, lds, d.nelem, typed, in, old, n);
+    } else {
+        __syncthreads();
+        ddt_acc_body<T, OP, FAST>(d, d.elems, d.nelem, typed, in, old, n);
     }
     osc_epilogue();
 }
@@ -1175,6 +1193,100 @@ static int acc_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount, const o
     return rc;
 }
 
+// MPI_Put / MPI_Get with derived datatypes (osc_sm_comm.c:24-100, 209-270:
+// ompi_datatype_sndrcv of any origin / target pair).  The origin side is a
+// packed byte stream on this GPU (a non-contiguous origin is packed before
+// a put, and unpacked from it after a get, by the convertor's kernels); the
+// target side moves in one launch of ddt_acc_kernel over G-byte granules (G
+// the widest power of two dividing every run, displacement, stride and
+// extent of the target type and both addresses): REPLACE stores granule k
+// of the stream into the k-th granule slot of the target type, NO_OP loads
+// it out — the derived accumulate's element walk with no element type, its
+// per-workgroup system-scope acquire / release and the epoch gate, and no
+// accumulate lock (put and get are not atomic, osc/sm takes none either).
+// A side's program NULL: `count` contiguous bytes.
+static int rma_ddt(ompi_amd_win_t *w, void *origin, size_t ocount, const ompi_amd_ddt_t *odt,
+                   int target, size_t disp, size_t tcount, const ompi_amd_ddt_t *tdt, bool put,
+                   void *stream) {
+    if (!w) return OMPI_AMD_ERR_BAD_PARAM;
+    const size_t obytes = odt ? ompi_amd_ddt_size(odt) * ocount : ocount;
+    const size_t tbytes = tdt ? ompi_amd_ddt_size(tdt) * tcount : tcount;
+    if (obytes != tbytes) {
+        record_msg("osc %s: origin (%zu bytes) and target (%zu bytes) type signatures differ",
+                   put ? "put" : "get", obytes, tbytes);
+        return OMPI_AMD_ERR_BAD_PARAM;
+    }
+    if (tbytes == 0) return OMPI_AMD_SUCCESS;
+    if (!origin) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!odt && !tdt)
+        return put ? ompi_amd_put(w, origin, tbytes, target, disp, stream)
+                   : ompi_amd_get(w, origin, tbytes, target, disp, stream);
+    ddt_view tv{};
+    if (tdt && !ddt_view_of(tdt, &tv)) return OMPI_AMD_ERR_BAD_PARAM;
+    if (target < 0 || target >= w->size) return OMPI_AMD_ERR_BAD_PARAM;
+    const int64_t base = (int64_t)disp * (int64_t)w->peer_disp[target];
+    const int64_t last = tdt ? (int64_t)(tcount - 1) * tv.d.extent : 0;
+    const int64_t lo = base + (tdt ? tv.lo + std::min<int64_t>(0, last) : 0);
+    const int64_t hi = base + (tdt ? tv.hi + std::max<int64_t>(0, last) : (int64_t)tbytes);
+    if (lo < 0 || hi > (int64_t)w->peer_bytes[target] || !w->peer_base[target]) {
+        record_msg("osc: target %d typed range [%lld, %lld) outside its %llu-byte window", target,
+                   (long long)lo, (long long)hi, (unsigned long long)w->peer_bytes[target]);
+        return OMPI_AMD_ERR_BAD_PARAM;
+    }
+    char *t = w->peer_base[target] + base;
+    hipStream_t s = win_stream(w, stream);
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    const uint32_t *gate = epoch_gate(w, target);
+    int rc = OMPI_AMD_SUCCESS;
+    char *packed = static_cast<char *>(origin);
+    void *tmp = nullptr;
+    if (odt) {  // the origin's packed stream, local
+        rc = record_hip(hipMallocAsync(&tmp, tbytes, s), "hipMallocAsync (osc origin stream)");
+        packed = static_cast<char *>(tmp);
+        if (rc == OMPI_AMD_SUCCESS && put) {
+            size_t done = 0;
+            rc = ompi_amd_ddt_pack(odt, ocount, origin, tmp, 0, tbytes, &done, s);
+            if (rc == OMPI_AMD_SUCCESS && done != tbytes) rc = OMPI_AMD_ERR_BAD_PARAM;
+        }
+    }
+    if (rc == OMPI_AMD_SUCCESS && !tdt) {  // contiguous target: one copy
+        rc = put ? xfer_copy(packed, t, tbytes, s, gate) : xfer_copy(t, packed, tbytes, s, gate);
+    } else if (rc == OMPI_AMD_SUCCESS) {
+        int64_t g = tv.gran;
+        while (g > 1 && (((uintptr_t)t | (uintptr_t)packed) & (uintptr_t)(g - 1))) g >>= 1;
+        g = std::min<int64_t>(g, 16);
+        const ddt_acc_fn f = ddt_rw_fn((size_t)g, put);
+        const int64_t n = (int64_t)tbytes / g;
+        const int64_t blocks = std::max<int64_t>(
+            1, std::min<int64_t>((n + kOscThreads * kAccUnroll - 1) / (kOscThreads * kAccUnroll),
+                                 osc_grid_cap()));
+        ddt_desc dd = tv.d;
+        const bool fast = tv.gran % g == 0 && n < (1ll << 32) && dd.size / g < (1ll << 32) &&
+                          tv.max_blen / g < (1ll << 32);
+        if (fast) dd.sdiv = make_fdiv((uint32_t)(dd.size / g));
+        rc = record_hip(f(dim3((unsigned)blocks), dd, t, put ? packed : nullptr, put ? nullptr : packed, n,
+                          gate, fast, s),
+                        put ? "osc derived put launch" : "osc derived get launch");
+    }
+    if (rc == OMPI_AMD_SUCCESS && odt && !put) {  // the fetched stream into the origin's layout
+        size_t done = 0;
+        rc = ompi_amd_ddt_unpack(odt, ocount, tmp, origin, 0, tbytes, &done, s);
+        if (rc == OMPI_AMD_SUCCESS && done != tbytes) rc = OMPI_AMD_ERR_BAD_PARAM;
+    }
+    if (tmp) hip_ignore(hipFreeAsync(tmp, s));
+    return rc;
+}
+
+int ompi_amd_put_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount, const ompi_amd_ddt_t *odt,
+                     int target, size_t disp, size_t tcount, const ompi_amd_ddt_t *tdt, void *stream) {
+    return rma_ddt(w, const_cast<void *>(origin), ocount, odt, target, disp, tcount, tdt, true, stream);
+}
+
+int ompi_amd_get_ddt(ompi_amd_win_t *w, void *origin, size_t ocount, const ompi_amd_ddt_t *odt,
+                     int target, size_t disp, size_t tcount, const ompi_amd_ddt_t *tdt, void *stream) {
+    return rma_ddt(w, origin, ocount, odt, target, disp, tcount, tdt, false, stream);
+}
+
 int ompi_amd_accumulate_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount,
                             const ompi_amd_ddt_t *odt, int target, size_t disp, size_t tcount,
                             const ompi_amd_ddt_t *tdt, int type, int op, void *stream) {
@@ -1483,6 +1595,22 @@ int ompi_amd_rget_accumulate(ompi_amd_win_t *w, const void *origin, void *result
     return rma_request(w, stream,
                        ompi_amd_get_accumulate(w, origin, result, count, type, target, disp, op,
                                                stream), req);
+}
+
+int ompi_amd_rput_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount,
+                      const ompi_amd_ddt_t *odt, int target, size_t disp, size_t tcount,
+                      const ompi_amd_ddt_t *tdt, void *stream, ompi_amd_rma_request_t **req) {
+    if (!req) return OMPI_AMD_ERR_BAD_PARAM;
+    return rma_request(w, stream, ompi_amd_put_ddt(w, origin, ocount, odt, target, disp, tcount, tdt, stream),
+                       req);
+}
+
+int ompi_amd_rget_ddt(ompi_amd_win_t *w, void *origin, size_t ocount, const ompi_amd_ddt_t *odt,
+                      int target, size_t disp, size_t tcount, const ompi_amd_ddt_t *tdt, void *stream,
+                      ompi_amd_rma_request_t **req) {
+    if (!req) return OMPI_AMD_ERR_BAD_PARAM;
+    return rma_request(w, stream, ompi_amd_get_ddt(w, origin, ocount, odt, target, disp, tcount, tdt, stream),
+                       req);
 }
 
 int ompi_amd_raccumulate_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount,

@@ -42,8 +42,11 @@
 //            receiver maps the send buffer itself (rendezvous, as before).
 //   host     a host send buffer of at most kInline bytes travels inside
 //            its mailbox slot, one of at most kHostMax bytes through the
-//            sender's host stage (a ring of kHostStage bytes per rank in
-//            the same shared segment) — ob1 / btl/sm's path for host memory:
+//            sender's host stage (a ring of kHostStage bytes per rank: its
+//            own shared segment, created and reserved with posix_fallocate at
+//            the rank's first such send, mapped by a receiver at the first
+//            message through it; a reservation /dev/shm cannot hold turns the
+//            ring off for that rank) — ob1 / btl/sm's path for host memory:
 //            one copy in, one copy out (or one host-to-device copy into a
 //            device receive buffer), no device work on the sender (round 4,
 //            profiles/r04_pml_host_path_ab*.jsonl); larger host send buffers,
@@ -78,7 +81,7 @@ namespace ompi_amd {
 constexpr int kSlots = 64;
 constexpr size_t kEager = 4096;
 constexpr size_t kInline = 1024;  // host payload carried in the slot itself
-constexpr size_t kHostStage = 8u << 20;  // per rank, in the mailbox segment (touched pages only)
+constexpr size_t kHostStage = 8u << 20;  // per rank, its own segment (created at first use)
 constexpr size_t kHostMax = 2u << 20;    // largest message through it
 
 enum : uint32_t { S_FREE = 0, S_POSTED = 1, S_MATCHED = 2, S_DONE = 3 };
@@ -136,13 +139,49 @@ struct p2p_state {
     struct hchunk { int dst; uint64_t seq, end; };
     std::deque<hchunk> hflight;
     int64_t host_stage_sends = 0;
-    int64_t export_refusals = 0;  // sends staged because the runtime refused the export
-    int refuse_exports = 0;       // test hook (param p2p_refuse_exports)
+    int64_t unsafe_sends = 0;  // user_ipc sends staged: no IPC-safe size, or older than an IPC close
+    int age_all = 0;           // test hook (param p2p_age_all): treat every buffer as older
     std::vector<hipEvent_t> ev_free;  // receive copies' events, reused
-    bool host_stage_touched = false;
+    // host stage rings: [rank] this process's mapping (nullptr: not yet);
+    // this rank's own is created at its first host-staged send
+    std::vector<char *> hring;
+    bool hring_off = false;  // this rank's could not be reserved: device stages instead
+    void ring_name(int r, char *out, size_t n) const { snprintf(out, n, "%s.h%d", name, r); }
+    // rank r's ring, mapped on first use (r's sender created it before it
+    // posted the message that names it); nullptr when it cannot be mapped
     char *host_stage(int r) {
-        return reinterpret_cast<char *>(q) + sizeof(pair_q) * (size_t)size * (size_t)size +
-               (size_t)r * kHostStage;
+        if (hring[(size_t)r]) return hring[(size_t)r];
+        char nm[300];
+        ring_name(r, nm, sizeof(nm));
+        const int fd = shm_open(nm, O_RDWR, 0600);
+        if (fd < 0) return nullptr;
+        void *m = mmap(nullptr, kHostStage, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        close(fd);
+        if (m == MAP_FAILED) return nullptr;
+        return hring[(size_t)r] = static_cast<char *>(m);
+    }
+    // this rank's ring, created and reserved (posix_fallocate: the pages
+    // exist, so no later store can SIGBUS on a full /dev/shm); false when
+    // /dev/shm cannot hold it — the ring stays off and device stages carry
+    // host messages instead
+    bool own_ring() {
+        if (hring[(size_t)rank]) return true;
+        if (hring_off) return false;
+        char nm[300];
+        ring_name(rank, nm, sizeof(nm));
+        shm_unlink(nm);
+        const int fd = shm_open(nm, O_CREAT | O_EXCL | O_RDWR, 0600);
+        bool ok = fd >= 0 && ftruncate(fd, (off_t)kHostStage) == 0 &&
+                  posix_fallocate(fd, 0, (off_t)kHostStage) == 0;
+        void *m = ok ? mmap(nullptr, kHostStage, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0) : MAP_FAILED;
+        if (fd >= 0) close(fd);
+        if (m == MAP_FAILED) {
+            if (fd >= 0) shm_unlink(nm);
+            hring_off = true;
+            return false;
+        }
+        hring[(size_t)rank] = static_cast<char *>(m);
+        return true;
     }
 
     pair_q &pair(int src, int dst) { return q[(size_t)src * (size_t)size + (size_t)dst]; }
@@ -193,8 +232,8 @@ int p2p_set_param(p2p_state *p, const char *key, int64_t v) {
     } else if (!strcmp(key, "p2p_stage_mib")) {
         if (v < 0) return OMPI_AMD_ERR_BAD_PARAM;
         p->stage_cap = (size_t)v << 20;
-    } else if (!strcmp(key, "p2p_refuse_exports")) {  // test hook: act as if the runtime refused
-        p->refuse_exports = v ? 1 : 0;
+    } else if (!strcmp(key, "p2p_age_all")) {  // test hook: as if every buffer predated an IPC close
+        p->age_all = v ? 1 : 0;
     } else {
         return OMPI_AMD_ERR_UNSUPPORTED;  // not a p2p key
     }
@@ -213,7 +252,7 @@ int p2p_get_param(p2p_state *p, const char *key, int64_t *v) {
     else if (!strcmp(key, "p2p_host_sends")) *v = p->host_sends;
     else if (!strcmp(key, "p2p_host_recvs")) *v = p->host_recvs;
     else if (!strcmp(key, "p2p_host_stage_sends")) *v = p->host_stage_sends;
-    else if (!strcmp(key, "p2p_export_refusals")) *v = p->export_refusals;
+    else if (!strcmp(key, "p2p_unsafe_sends")) *v = p->unsafe_sends;
     else return OMPI_AMD_ERR_UNSUPPORTED;
     return OMPI_AMD_SUCCESS;
 }
@@ -229,7 +268,8 @@ int p2p_create(ompi_amd_comm_t *c, const char *name, int rank, int size, int pha
     snprintf(p->name, sizeof(p->name), "/ompi_amd_%s.p2p", name);
     for (char *ch = p->name + 1; *ch; ++ch)
         if (*ch == '/') *ch = '_';
-    p->bytes = sizeof(pair_q) * (size_t)size * (size_t)size + kHostStage * (size_t)size;
+    p->bytes = sizeof(pair_q) * (size_t)size * (size_t)size;
+    p->hring.assign((size_t)size, nullptr);
     int fd = -1;
     if (phase == 0) {  // rank 0, before the communicator's first rendezvous
         shm_unlink(p->name);
@@ -269,6 +309,13 @@ void p2p_unlink(p2p_state *p) {
 void p2p_destroy(p2p_state *p) {
     if (!p) return;
     if (p->q) munmap(p->q, p->bytes);
+    for (char *h : p->hring)
+        if (h) munmap(h, kHostStage);
+    if (p->hring[(size_t)p->rank]) {  // every peer's receive from it completed (final rendezvous)
+        char nm[300];
+        p->ring_name(p->rank, nm, sizeof(nm));
+        shm_unlink(nm);
+    }
     if (p->eager) hip_ignore(hipFree(p->eager));
     for (hipEvent_t e : p->ev_free) hip_ignore(hipEventDestroy(e));
     // the communicator's final rendezvous has passed: no peer reads a stage
@@ -328,6 +375,7 @@ static void reclaim_host(p2p_state *p) {
 // A contiguous chunk of `bytes` of this rank's host stage (offset in *off),
 // or false when the ring has no room now.  Under p->mu.
 static bool take_host(p2p_state *p, size_t bytes, uint64_t *off, uint64_t *end) {
+    if (!p->own_ring()) return false;
     reclaim_host(p);
     uint64_t at = p->hhead;
     const uint64_t pos = at % kHostStage;
@@ -440,7 +488,13 @@ static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s
     if (n == 0) return;
     int rc = OMPI_AMD_SUCCESS;
     if (m->inl) {  // a host send out of the slot or the sender's host stage (host: done now)
-        const char *from = m->inl == 1 ? m->inline_data : p->host_stage(s) + m->raw;
+        const char *ring = m->inl == 2 ? p->host_stage(s) : nullptr;
+        if (m->inl == 2 && !ring) {
+            r->rc = r->st.error = OMPI_AMD_ERR_BOOTSTRAP;
+            record_msg("p2p: cannot map rank %d's host stage", s);
+            return;
+        }
+        const char *from = m->inl == 1 ? m->inline_data : ring + m->raw;
         if (r->host_dst) {
             memcpy(r->host_dst, from, n);
             return;
@@ -619,11 +673,15 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
         if (rc != OMPI_AMD_SUCCESS) p->eager = nullptr;
     }
     alloc_guard.unlock();
-    // the buffer is read from now on (by a staging copy or the receiver):
-    // its producers must be done
-    if (rc == OMPI_AMD_SUCCESS && !host)
-        rc = record_hip(hipStreamSynchronize(s), "hipStreamSynchronize (send)");  // usually idle
     if (rc != OMPI_AMD_SUCCESS) return rc;
+    // A copy into an eager cell or a stage runs on `s`, after the buffer's
+    // producers in stream order; only a message the receiver reads from the
+    // buffer itself (direct, or to self) needs them done first — a host wait
+    // the eager and staged paths no longer pay (one hipStreamSynchronize of
+    // the two per small device message).
+    auto producers_done = [&]() -> int {
+        return host ? OMPI_AMD_SUCCESS : record_hip(hipStreamSynchronize(s), "hipStreamSynchronize (send)");
+    };
     auto *r = new (std::nothrow) ompi_amd_p2p_request;
     if (!r) return OMPI_AMD_ERR_BAD_PARAM;
     r->p = p;
@@ -660,7 +718,7 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
                                        : crc;
     };
     // The message into a library stage (peers read library memory).  must: a
-    // host buffer, or a device buffer the runtime refused to export — wait
+    // host buffer, or a device buffer peers cannot map reliably — wait
     // for a stage, past the cap once if nothing is in flight; otherwise one
     // try, and without a stage the message goes from the buffer itself.
     auto stage_send = [&](bool must) -> int {
@@ -684,7 +742,7 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
             }
             if (!got)
                 return record_hip(hipErrorOutOfMemory,
-                                  host ? "p2p send stage (host buffer)" : "p2p send stage (export refused)");
+                                  host ? "p2p send stage (host buffer)" : "p2p send stage (device buffer)");
         }
         if (!got) return OMPI_AMD_SUCCESS;
         const int crc = copy_in(st.buf);
@@ -704,10 +762,6 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     if (inl) {  // into the slot itself; the send completes now
         memcpy(m.inline_data, buf, bytes);
     } else if (hstaged) {  // into this rank's host stage; the send completes now
-        if (!p->host_stage_touched) {  // fault the ring's pages in once, not per message
-            memset(p->host_stage(p->rank), 0, kHostStage);
-            p->host_stage_touched = true;
-        }
         memcpy(p->host_stage(p->rank) + hoff, buf, bytes);
         p->hflight.push_back({dst, seq, hend});
         p->hhead = hend;
@@ -718,20 +772,25 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
         src = cell;
     } else if (bytes && (host || (dst != p->rank && !p->user_ipc))) {
         rc = stage_send(host);
+    } else if (bytes && dst != p->rank && (p->age_all || !comm_ipc_safe(src))) {
+        // p2p_user_ipc: an allocation peers could not map reliably — not an
+        // IPC-safe size, or older than an IPC close of this process, which
+        // ROCm 7.2 may refuse to export — goes through a
+        // stage, as the collectives send such a buffer through a shadow
+        ++p->unsafe_sends;
+        rc = stage_send(true);
     }
     if (host) ++p->host_sends;
     if (rc == OMPI_AMD_SUCCESS && bytes && dst != p->rank && !staged && !inl && !hstaged) {
-        rc = p->refuse_exports && !eager ? record_hip(hipErrorInvalidValue, "hipIpcGetMemHandle (refusal forced)")
-                                         : comm_export(c, src, &d);
-        if (rc != OMPI_AMD_SUCCESS && !eager && !host) {
-            // ROCm 7.2 now and then refuses hipIpcGetMemHandle ("invalid
-            // argument") for a fresh application allocation of an IPC-safe
-            // size (8 MiB, pml harness section 9 with p2p_user_ipc = 1, once
-            // in ~40 runs): the message goes through a library stage instead
-            ++p->export_refusals;
-            rc = stage_send(true);
-        }
+        // library memory (eager cells, stages: exported at allocation) or an
+        // application buffer comm_ipc_safe() accepted: the runtime answers
+        // (DESIGN.md §4.6); a refusal is an error
+        if (!eager) rc = producers_done();  // the receiver reads the buffer itself
+        if (rc == OMPI_AMD_SUCCESS) rc = comm_export(c, src, &d);
         if (!eager && !staged) ++p->direct_sends;
+    } else if (rc == OMPI_AMD_SUCCESS && bytes && dst == p->rank && !staged && !inl && !hstaged &&
+               !eager) {
+        rc = producers_done();  // a receive of this process copies from the buffer
     }
     if (rc != OMPI_AMD_SUCCESS) {
         delete r;

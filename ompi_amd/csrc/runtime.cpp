@@ -162,9 +162,12 @@ int ompi_amd_memcpy_async(void *dst, const void *src, size_t bytes, void *stream
     return record_hip(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s), "hipMemcpyAsync");
 }
 
+// The convertor's synchronous fAdvance waits here, and a send window's
+// bytes are read from pinned host memory right after (fill_win): a host
+// read, so the event wait (host_mark.h).
 int ompi_amd_stream_synchronize(void *stream) {
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : thread_stream();
-    return record_hip(mark_stream_wait(s, no_idle), "hipStreamSynchronize");
+    return record_hip(mark_stream_wait(s, no_idle, true), "hipStreamSynchronize");
 }
 
 int ompi_amd_memcpy(void *dst, const void *src, size_t bytes) {
@@ -172,7 +175,9 @@ int ompi_amd_memcpy(void *dst, const void *src, size_t bytes) {
     if (!dst || !src) return OMPI_AMD_ERR_BAD_PARAM;
     hipStream_t s = thread_stream();
     int rc = record_hip(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s), "hipMemcpyAsync");
-    if (rc == OMPI_AMD_SUCCESS) rc = record_hip(mark_stream_wait(s, no_idle), "hipStreamSynchronize");
+    if (rc == OMPI_AMD_SUCCESS)  // the host may read dst now: the event wait
+        rc = record_hip(mark_stream_wait(s, no_idle, !ompi_amd_is_device_pointer(dst)),
+                        "hipStreamSynchronize");
     return rc;
 }
 

@@ -50,6 +50,7 @@ typedef struct mca_coll_rocm_module_t {
     int since_check, mismatched; /* locked: calls since the last recheck, own stagings */
     void *dstage[2], *hstage[2]; /* grow-only staging per operand slot */
     size_t dstage_bytes[2], hstage_bytes[2];
+    int fail_stage;              /* test hook: the next staging allocation fails */
 } mca_coll_rocm_module_t;
 
 enum { ROCM_RES_AUTO = 0, ROCM_RES_DEVICE = 1, ROCM_RES_HOST = 2 };

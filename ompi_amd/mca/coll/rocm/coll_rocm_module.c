@@ -464,6 +464,10 @@ static char *stage_buf(void *ctx, int slot, int on_dev, size_t bytes)
     mca_coll_rocm_module_t *m = (mca_coll_rocm_module_t *) ctx;
     void **p = on_dev ? &m->dstage[slot] : &m->hstage[slot];
     size_t *have = on_dev ? &m->dstage_bytes[slot] : &m->hstage_bytes[slot];
+    if (m->fail_stage) {  /* test hook (coll harness): as if the allocation failed */
+        m->fail_stage = 0;
+        return NULL;
+    }
     if (bytes > *have) {
         const size_t want = bytes > 2 * *have ? bytes : 2 * *have;
         if (on_dev) {
@@ -578,6 +582,20 @@ static int rocm_unstage(mca_coll_rocm_module_t *m, const rocm_operand_t *o, int 
  * to host memory first and its outputs back after, as coll/cuda does for
  * every call it wraps (coll_cuda_allreduce.c:42-72).  Host operands go as
  * they are. */
+/* A staging failure after the device path was agreed (locked DEVICE: no
+ * message at all) would leave the peers in the collective's first barrier
+ * until timeout_ms: this rank raises the communicator's abort word instead,
+ * so every rank's call fails within about 1 ms.  (On the saved host path
+ * the peers are inside coll/tuned's messages, as with any rank that fails
+ * a host collective: MPI_ERRORS_ARE_FATAL ends the job.) */
+static int rocm_staging_failed(mca_coll_rocm_module_t *m, int path, int rc)
+{
+    if (OMPI_SUCCESS != rc && ROCM_DEVICE == path)
+        (void) ompi_amd_comm_abort(m->dev_comm, OMPI_ERR_OUT_OF_RESOURCE == rc ? OMPI_AMD_ERR_HIP
+                                                                               : OMPI_AMD_ERR_BAD_PARAM);
+    return rc;
+}
+
 static int rocm_begin(mca_coll_rocm_module_t *m, int uniform_ok, int local_dev,
                       rocm_operand_t *o, int n, int *path)
 {
@@ -587,7 +605,7 @@ static int rocm_begin(mca_coll_rocm_module_t *m, int uniform_ok, int local_dev,
         o[i].how = 0;
         o[i].hbuf = NULL;
     }
-    return rocm_stage(m, o, n, ROCM_DEVICE == *path);
+    return rocm_staging_failed(m, *path, rocm_stage(m, o, n, ROCM_DEVICE == *path));
 }
 
 static int rocm_dev_finish(mca_coll_rocm_module_t *m, const rocm_operand_t *o, int n, int rc)
@@ -1044,11 +1062,11 @@ static int rocm_nb_begin(mca_coll_rocm_module_t *m, int uniform_ok, int local_ok
         return OMPI_SUCCESS;  /* the saved function takes host operands as they are */
     }
     st = calloc(1, sizeof(*st));
-    if (NULL == st) return OMPI_ERR_OUT_OF_RESOURCE;
+    if (NULL == st) return rocm_staging_failed(m, *path, OMPI_ERR_OUT_OF_RESOURCE);
     rc = rocm_stage_with(nb_buf, st, o, n, ROCM_DEVICE == *path);
     if (OMPI_SUCCESS != rc) {
         nb_stage_free(st);
-        return rc;
+        return rocm_staging_failed(m, *path, rc);
     }
     memcpy(st->o, o, (size_t) n * sizeof(*o));
     st->n = n;

@@ -11,9 +11,10 @@
  * Request-based RMA completes its request from the opal_progress callback
  * once the call's kernels have run.  MPI_Win_allocate_shared windows keep
  * every rank's segment in one device allocation that all ranks map
- * (MPI_Win_shared_query hands out the addresses).  Predefined datatypes with equal origin and
- * target signatures; everything else returns OMPI_ERR_NOT_SUPPORTED, as
- * osc/sm rejects what it cannot do.  Blocking MPI semantics come from the
+ * (MPI_Win_shared_query hands out the addresses).  Put and get take any
+ * datatype pair the convertor has device programs for; accumulates any
+ * pair built from one predefined type; everything else returns
+ * OMPI_ERR_NOT_SUPPORTED.  Blocking MPI semantics come from the
  * stream synchronisation in fence / unlock / flush (ompi_amd_comm_sync,
  * which also turns a peer that never released a lock into
  * OMPI_ERR_TIMEOUT).
@@ -138,22 +139,55 @@ static int complete(ompi_osc_rocm_module_t *m, int rc)
 
 /* ------------------------------------------------------------ communication */
 
+/* One side of MPI_Put / MPI_Get with any datatype (osc_sm_comm.c:24-100,
+ * 209-270 move it with ompi_datatype_sndrcv): a contiguous predefined type
+ * as bytes (program NULL), any other datatype through the device program
+ * common/rocm's cache built for the convertor. */
+struct opal_datatype_t;
+const ompi_amd_ddt_t *opal_rocm_device_ddt(const struct opal_datatype_t *dt);
+
+static int rma_side(struct ompi_datatype_t *dt, int count, const ompi_amd_ddt_t **prog, size_t *n)
+{
+    const size_t bytes = span(dt, count);
+    if (0 != bytes) {
+        *prog = NULL;
+        *n = bytes;
+        return 1;
+    }
+    /* an ompi_datatype_t begins with its opal_datatype_t (ompi_datatype.h:70-71) */
+    *prog = opal_rocm_device_ddt((const struct opal_datatype_t *) dt);
+    *n = (size_t) count;
+    return NULL != *prog;
+}
+
 static int rocm_put(const void *origin, int ocount, struct ompi_datatype_t *odt, int target,
                     ptrdiff_t disp, int tcount, struct ompi_datatype_t *tdt, struct ompi_win_t *win)
 {
+    const ompi_amd_ddt_t *op = NULL, *tp = NULL;
+    size_t on = 0, tn = 0;
     const size_t bytes = span(odt, ocount);
     if (0 == ocount) return OMPI_SUCCESS;
-    if (0 == bytes || bytes != span(tdt, tcount) || disp < 0) return OMPI_ERR_NOT_SUPPORTED;
-    return to_ompi_err(ompi_amd_put(mod(win)->dev_win, origin, bytes, target, (size_t) disp, NULL));
+    if (disp < 0) return OMPI_ERR_NOT_SUPPORTED;
+    if (0 != bytes && bytes == span(tdt, tcount))
+        return to_ompi_err(ompi_amd_put(mod(win)->dev_win, origin, bytes, target, (size_t) disp, NULL));
+    if (!rma_side(odt, ocount, &op, &on) || !rma_side(tdt, tcount, &tp, &tn)) return OMPI_ERR_NOT_SUPPORTED;
+    return to_ompi_err(ompi_amd_put_ddt(mod(win)->dev_win, origin, on, op, target, (size_t) disp, tn, tp,
+                                        NULL));
 }
 
 static int rocm_get(void *origin, int ocount, struct ompi_datatype_t *odt, int target,
                     ptrdiff_t disp, int tcount, struct ompi_datatype_t *tdt, struct ompi_win_t *win)
 {
+    const ompi_amd_ddt_t *op = NULL, *tp = NULL;
+    size_t on = 0, tn = 0;
     const size_t bytes = span(odt, ocount);
     if (0 == ocount) return OMPI_SUCCESS;
-    if (0 == bytes || bytes != span(tdt, tcount) || disp < 0) return OMPI_ERR_NOT_SUPPORTED;
-    return to_ompi_err(ompi_amd_get(mod(win)->dev_win, origin, bytes, target, (size_t) disp, NULL));
+    if (disp < 0) return OMPI_ERR_NOT_SUPPORTED;
+    if (0 != bytes && bytes == span(tdt, tcount))
+        return to_ompi_err(ompi_amd_get(mod(win)->dev_win, origin, bytes, target, (size_t) disp, NULL));
+    if (!rma_side(odt, ocount, &op, &on) || !rma_side(tdt, tcount, &tp, &tn)) return OMPI_ERR_NOT_SUPPORTED;
+    return to_ompi_err(ompi_amd_get_ddt(mod(win)->dev_win, origin, on, op, target, (size_t) disp, tn, tp,
+                                        NULL));
 }
 
 /* same predefined type on both sides, same count (osc_sm_comm.c:289-303 reduces
@@ -173,9 +207,6 @@ static int acc_ok(struct ompi_datatype_t *odt, int ocount, struct ompi_datatype_
  * (REPLACE / NO_OP on any); each side either that type contiguous (program
  * NULL, count in elements) or a datatype with a device program
  * (common/rocm's cache of the convertor's programs). */
-struct opal_datatype_t;
-const ompi_amd_ddt_t *opal_rocm_device_ddt(const struct opal_datatype_t *dt);
-
 typedef struct {
     int type;                    /* op/base type code of the primitive */
     const ompi_amd_ddt_t *prog;  /* NULL: `type` contiguous */
@@ -488,11 +519,16 @@ static int rocm_rput(const void *origin, int ocount, struct ompi_datatype_t *odt
                      struct ompi_win_t *win, ompi_request_t **request)
 {
     ompi_amd_rma_request_t *rma = NULL;
+    const ompi_amd_ddt_t *op = NULL, *tp = NULL;
+    size_t on = 0, tn = 0;
     const size_t bytes = span(odt, ocount);
-    if (0 != ocount && (0 == bytes || bytes != span(tdt, tcount) || disp < 0))
-        return OMPI_ERR_NOT_SUPPORTED;
-    return rma_wrap(ompi_amd_rput(mod(win)->dev_win, origin, bytes, target, (size_t) disp, NULL,
-                                  &rma), &rma, win, request);
+    if (disp < 0) return OMPI_ERR_NOT_SUPPORTED;
+    if (0 == ocount || (0 != bytes && bytes == span(tdt, tcount)))
+        return rma_wrap(ompi_amd_rput(mod(win)->dev_win, origin, 0 == ocount ? 0 : bytes, target,
+                                      (size_t) disp, NULL, &rma), &rma, win, request);
+    if (!rma_side(odt, ocount, &op, &on) || !rma_side(tdt, tcount, &tp, &tn)) return OMPI_ERR_NOT_SUPPORTED;
+    return rma_wrap(ompi_amd_rput_ddt(mod(win)->dev_win, origin, on, op, target, (size_t) disp, tn, tp,
+                                      NULL, &rma), &rma, win, request);
 }
 
 static int rocm_rget(void *origin, int ocount, struct ompi_datatype_t *odt, int target,
@@ -500,11 +536,16 @@ static int rocm_rget(void *origin, int ocount, struct ompi_datatype_t *odt, int 
                      struct ompi_win_t *win, ompi_request_t **request)
 {
     ompi_amd_rma_request_t *rma = NULL;
+    const ompi_amd_ddt_t *op = NULL, *tp = NULL;
+    size_t on = 0, tn = 0;
     const size_t bytes = span(odt, ocount);
-    if (0 != ocount && (0 == bytes || bytes != span(tdt, tcount) || disp < 0))
-        return OMPI_ERR_NOT_SUPPORTED;
-    return rma_wrap(ompi_amd_rget(mod(win)->dev_win, origin, bytes, target, (size_t) disp, NULL,
-                                  &rma), &rma, win, request);
+    if (disp < 0) return OMPI_ERR_NOT_SUPPORTED;
+    if (0 == ocount || (0 != bytes && bytes == span(tdt, tcount)))
+        return rma_wrap(ompi_amd_rget(mod(win)->dev_win, origin, 0 == ocount ? 0 : bytes, target,
+                                      (size_t) disp, NULL, &rma), &rma, win, request);
+    if (!rma_side(odt, ocount, &op, &on) || !rma_side(tdt, tcount, &tp, &tn)) return OMPI_ERR_NOT_SUPPORTED;
+    return rma_wrap(ompi_amd_rget_ddt(mod(win)->dev_win, origin, on, op, target, (size_t) disp, tn, tp,
+                                      NULL, &rma), &rma, win, request);
 }
 
 static int rocm_raccumulate(const void *origin, int ocount, struct ompi_datatype_t *odt,
@@ -601,23 +642,51 @@ static const ompi_osc_base_module_t rocm_module_template = {
 
 /* ------------------------------------------------------------ selection */
 
+/* A window whose ranks disagree about device memory (see rocm_query),
+ * refused by the rocm_select that follows the query on this thread. */
+static _Thread_local struct ompi_win_t *mixed_win;
+
+/* The osc framework selects per rank (ompi_osc_base_select,
+ * osc_base_init.c:33-80: the highest-priority query wins, locally), but
+ * whether a window is a device window may differ between ranks: MPI lets
+ * MPI_Win_create bases live in device memory on some ranks and host memory
+ * on others, and the info key of the allocating flavors is per rank too.
+ * Every rank of the communicator runs this query at the same point of its
+ * collective ompi_osc_base_select, so the decision is agreed here, over the
+ * communicator's own allreduce (as osc/rdma agrees on its setup,
+ * osc_rdma_component.c:533): no rank holds device memory -> -1 on every
+ * rank (the host components take the window alike); device memory only ->
+ * this component everywhere; both -> this component everywhere, and
+ * rocm_select refuses the window on every rank with the same error (peers
+ * cannot map a host base; no component serves the mix). */
 static int rocm_query(struct ompi_win_t *win, void **base, size_t size, int disp_unit,
                       struct ompi_communicator_t *comm, struct opal_info_t *info, int flavor)
 {
     bool dev = false;
-    int flag = 0;
+    int flag = 0, v[2] = {0, 0};  /* some rank has device memory / host memory */
     if (ompi_amd_device_count() <= 0 || OMPI_COMM_IS_INTER(comm) ||
         ompi_group_have_remote_peers(comm->c_local_group) ||
         ompi_comm_size(comm) > OMPI_AMD_MAX_RANKS)
         return -1;
-    if (MPI_WIN_FLAVOR_CREATE == flavor)
-        return (0 == size || 1 == ompi_amd_is_device_pointer(*base)) ? mca_osc_rocm_component.priority
-                                                                      : -1;
-    if (MPI_WIN_FLAVOR_ALLOCATE == flavor || MPI_WIN_FLAVOR_SHARED == flavor) {
+    if (MPI_WIN_FLAVOR_CREATE == flavor) {
+        if (0 != size) {
+            dev = 1 == ompi_amd_is_device_pointer(*base);
+            v[0] = dev;
+            v[1] = !dev;
+        }
+    } else if (MPI_WIN_FLAVOR_ALLOCATE == flavor || MPI_WIN_FLAVOR_SHARED == flavor) {
         (void) opal_info_get_bool(info, "ompi_amd_device", &dev, &flag);
-        return (flag && dev) ? mca_osc_rocm_component.priority : -1;
+        v[0] = flag && dev;
+        v[1] = !v[0];
+    } else {
+        return -1;  /* dynamic windows stay with osc/rdma */
     }
-    return -1;  /* dynamic windows stay with osc/rdma */
+    if (OMPI_SUCCESS != comm->c_coll->coll_allreduce(MPI_IN_PLACE, v, 2, MPI_INT, MPI_MAX, comm,
+                                                     comm->c_coll->coll_allreduce_module))
+        return -1;
+    if (!v[0]) return -1;
+    mixed_win = v[1] ? win : NULL;
+    return mca_osc_rocm_component.priority;
 }
 
 static int rocm_select(struct ompi_win_t *win, void **base, size_t size, int disp_unit,
@@ -626,7 +695,12 @@ static int rocm_select(struct ompi_win_t *win, void **base, size_t size, int dis
 {
     char name[128];
     int rc, all_ok = 0, local_ok;
-    ompi_osc_rocm_module_t *m = calloc(1, sizeof(*m));
+    ompi_osc_rocm_module_t *m;
+    if (mixed_win == win) {  /* agreed in rocm_query: every rank refuses alike */
+        mixed_win = NULL;
+        return OMPI_ERR_NOT_SUPPORTED;
+    }
+    m = calloc(1, sizeof(*m));
     if (NULL == m) return OMPI_ERR_NOT_AVAILABLE;
     m->super = rocm_module_template;
     m->comm = comm;
@@ -641,7 +715,8 @@ static int rocm_select(struct ompi_win_t *win, void **base, size_t size, int dis
         return to_ompi_err(rc);
     }
     (void) ompi_amd_comm_set_param(m->dev_comm, "timeout_ms", mca_osc_rocm_component.timeout_ms);
-    /* residency may differ between ranks (query is local): decide together */
+    /* agreed in rocm_query already; the library confirms it on its own
+     * rendezvous (a failure here fails every rank alike) */
     local_ok = MPI_WIN_FLAVOR_CREATE != flavor || 0 == size ||
                1 == ompi_amd_is_device_pointer(*base);
     rc = ompi_amd_comm_agree(m->dev_comm, local_ok, &all_ok);

@@ -342,7 +342,18 @@ static int on_device(const void *buf, size_t count, struct ompi_datatype_t *dtyp
     return ompi_amd_is_device_pointer((const char *) buf + tlb);
 }
 
-/* r->hspan: the host copy of r->buf's typed span (filled from the device) */
+/* A received span goes back to the device whole (pre-filled, so the type's
+ * gaps carry the device's own bytes) only for a non-contiguous type the
+ * convertor has no device program for; every other receive writes back
+ * exactly the bytes the message delivered (host_span_back). */
+static int recv_whole_span(const mca_pml_rocm_request_t *r)
+{
+    return !ompi_datatype_is_contiguous_memory_layout(r->dtype, (int) r->count) &&
+           !opal_rocm_device_program(OPAL_DT(r->dtype));
+}
+
+/* r->hspan: host memory for r->buf's typed span; a send's is filled from
+ * the device (the payload), a receive's only when it goes back whole */
 static int host_span(mca_pml_rocm_request_t *r)
 {
     ptrdiff_t lb, ext, tlb, text;
@@ -352,18 +363,57 @@ static int host_span(mca_pml_rocm_request_t *r)
     r->hgap = tlb;
     if (NULL == r->hspan && NULL == (r->hspan = malloc(r->hbytes ? r->hbytes : 1)))
         return OMPI_ERR_OUT_OF_RESOURCE;
+    if (!r->is_send && !recv_whole_span(r)) return OMPI_SUCCESS;
     return OMPI_AMD_SUCCESS == ompi_amd_memcpy(r->hspan, (char *) r->buf + tlb, r->hbytes) ? OMPI_SUCCESS
                                                                                        : OMPI_ERROR;
 }
 
 static void *host_base(const mca_pml_rocm_request_t *r) { return r->hspan - r->hgap; }
 
-/* a received host span back into the device buffer */
-static int host_span_back(const mca_pml_rocm_request_t *r)
+/* A received host span back into the device buffer: the `got` bytes the
+ * message delivered and nothing else, as ob1 writes exactly the typed bytes
+ * through the convertor.  Several receives can be in flight into one device
+ * buffer with interleaved typed spans (coll/base's linear gather into a
+ * resized column type, an alltoall of vectors): copying a whole span back
+ * would overwrite the other receives' elements with this one's stale
+ * gaps.  Contiguous layout: the received prefix.  Otherwise the received
+ * elements are packed on the host, copied into a pooled device stage and
+ * scattered by the type's device program (one kernel, typed bytes only). */
+static int host_span_back(const mca_pml_rocm_request_t *r, size_t got)
 {
-    return OMPI_AMD_SUCCESS == ompi_amd_memcpy((char *) r->buf + r->hgap, r->hspan, r->hbytes)
-               ? OMPI_SUCCESS
-               : OMPI_ERROR;
+    size_t size = 0, elems, bytes;
+    char *packed;
+    void *d;
+    int rc;
+    if (0 == got || 0 == r->count) return OMPI_SUCCESS;
+    if (ompi_datatype_is_contiguous_memory_layout(r->dtype, (int) r->count)) {
+        bytes = got < r->hbytes ? got : r->hbytes;
+        return OMPI_AMD_SUCCESS == ompi_amd_memcpy((char *) r->buf + r->hgap, r->hspan, bytes)
+                   ? OMPI_SUCCESS
+                   : OMPI_ERROR;
+    }
+    if (recv_whole_span(r))
+        return OMPI_AMD_SUCCESS == ompi_amd_memcpy((char *) r->buf + r->hgap, r->hspan, r->hbytes)
+                   ? OMPI_SUCCESS
+                   : OMPI_ERROR;
+    (void) ompi_datatype_type_size(r->dtype, &size);
+    elems = size ? got / size : 0;
+    if (elems > r->count) elems = r->count;
+    bytes = elems * size;
+    if (0 == bytes) return OMPI_SUCCESS;
+    if (NULL == (packed = malloc(bytes))) return OMPI_ERR_OUT_OF_RESOURCE;
+    rc = MPI_SUCCESS == ompi_datatype_sndrcv(host_base(r), (int) elems, r->dtype, packed, (int) bytes,
+                                             MPI_BYTE)
+             ? OMPI_SUCCESS
+             : OMPI_ERROR;
+    d = OMPI_SUCCESS == rc ? dev_stage_take(bytes) : NULL;
+    if (OMPI_SUCCESS == rc && NULL == d) rc = OMPI_ERR_OUT_OF_RESOURCE;
+    if (OMPI_SUCCESS == rc && OMPI_AMD_SUCCESS != ompi_amd_memcpy(d, packed, bytes)) rc = OMPI_ERROR;
+    if (OMPI_SUCCESS == rc && 0 != opal_rocm_unpack_device(OPAL_DT(r->dtype), elems, d, r->buf, NULL))
+        rc = OMPI_ERROR;
+    dev_stage_put(d, bytes);
+    free(packed);
+    return rc;
 }
 
 /* Wait for a library request without a time limit, driving opal_progress
@@ -425,7 +475,7 @@ static int finish(mca_pml_rocm_request_t *r, int rc, const ompi_amd_status_t *s)
 static void finish_inner(mca_pml_rocm_request_t *r)
 {
     int err = r->inner->req_status.MPI_ERROR;
-    if (OMPI_SUCCESS == err && !r->is_send) err = host_span_back(r);
+    if (OMPI_SUCCESS == err && !r->is_send) err = host_span_back(r, r->inner->req_status._ucount);
     r->super.req_status = r->inner->req_status;
     r->super.req_status.MPI_ERROR = err;
     if (r->super.req_persistent) {
@@ -553,7 +603,7 @@ static int rocm_start_req(size_t count, ompi_request_t **requests)
         if (OMPI_REQUEST_ACTIVE == r->super.req_state && !REQUEST_COMPLETE(&r->super))
             return OMPI_ERR_REQUEST;
         if (NULL != r->inner) {  /* the saved PML's request on the host span */
-            rc = host_span(r);  /* this start's payload / the receive's gap bytes */
+            rc = host_span(r);  /* this start's payload (a receive: its gap bytes, if whole) */
             if (OMPI_SUCCESS == rc) rc = r->inner->req_start(1, &r->inner);
             if (OMPI_SUCCESS != rc) return rc;
             r->super.req_complete = REQUEST_PENDING;
@@ -772,6 +822,7 @@ static int rocm_send(const void *buf, size_t count, struct ompi_datatype_t *dtyp
     int rc;
     if (NULL == dev && on_device(buf, count, dtype)) {  /* the saved PML on a host copy */
         memset(&r, 0, sizeof(r));
+        r.is_send = 1;
         r.buf = (void *) buf;
         r.count = count;
         r.dtype = dtype;
@@ -810,10 +861,11 @@ static int rocm_recv(void *buf, size_t count, struct ompi_datatype_t *dtype, int
         r.buf = buf;
         r.count = count;
         r.dtype = dtype;
+        ompi_status_public_t own, *st = NULL != status ? status : &own;  /* MPI_STATUS_IGNORE */
         rc = host_span(&r);
         if (OMPI_SUCCESS == rc)
-            rc = mca_pml_rocm_host.pml_recv(host_base(&r), count, dtype, src, tag, comm, status);
-        if (OMPI_SUCCESS == rc) rc = host_span_back(&r);
+            rc = mca_pml_rocm_host.pml_recv(host_base(&r), count, dtype, src, tag, comm, st);
+        if (OMPI_SUCCESS == rc) rc = host_span_back(&r, st->_ucount);
         free(r.hspan);
         return rc;
     }

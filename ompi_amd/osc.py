@@ -199,6 +199,20 @@ class Window:
     def _ddt(dt):
         return None if dt is None else dt.commit()._handle
 
+    def put_ddt(self, origin, ocount: int, odt, target: int, disp: int, tcount: int, tdt,
+                stream=None) -> None:
+        """MPI_Put with derived datatypes (osc_sm_comm.c:24-100): odt / tdt
+        are ompi_amd.datatype.Datatype, None meaning `ocount` / `tcount`
+        contiguous bytes."""
+        _lib.check(self._lib.ompi_amd_put_ddt(self._h, _ptr(origin), ocount, self._ddt(odt), target, disp,
+                                              tcount, self._ddt(tdt), _stream(stream)), "put_ddt")
+
+    def get_ddt(self, origin, ocount: int, odt, target: int, disp: int, tcount: int, tdt,
+                stream=None) -> None:
+        """MPI_Get with derived datatypes (osc_sm_comm.c:209-270)."""
+        _lib.check(self._lib.ompi_amd_get_ddt(self._h, _ptr(origin), ocount, self._ddt(odt), target, disp,
+                                              tcount, self._ddt(tdt), _stream(stream)), "get_ddt")
+
     def accumulate_ddt(self, origin, ocount: int, odt, target: int, disp: int, tcount: int, tdt,
                        prim: Datatype, op: Op, stream=None) -> None:
         """MPI_Accumulate with derived datatypes (ompi_osc_base_sndrcv_op):
@@ -242,6 +256,16 @@ class Window:
         n = origin.numel() * origin.element_size() if nbytes is None else nbytes
         return self._req(self._lib.ompi_amd_rput, "rput", _ptr(origin), n, target, disp,
                          _stream(stream))
+
+    def rput_ddt(self, origin, ocount: int, odt, target: int, disp: int, tcount: int, tdt,
+                 stream=None) -> RmaRequest:
+        return self._req(self._lib.ompi_amd_rput_ddt, "rput_ddt", _ptr(origin), ocount, self._ddt(odt),
+                         target, disp, tcount, self._ddt(tdt), _stream(stream))
+
+    def rget_ddt(self, origin, ocount: int, odt, target: int, disp: int, tcount: int, tdt,
+                 stream=None) -> RmaRequest:
+        return self._req(self._lib.ompi_amd_rget_ddt, "rget_ddt", _ptr(origin), ocount, self._ddt(odt),
+                         target, disp, tcount, self._ddt(tdt), _stream(stream))
 
     def rget(self, origin, target: int, disp: int, nbytes: int | None = None,
              stream=None) -> RmaRequest:

@@ -1376,7 +1376,7 @@ def main():
                          "state": {k: comm.get_param(k) for k in (
                              "epoch", "shadowed", "recycled_exports", "exports_new", "imports_new",
                              "imports", "landing_bytes", "boot_calls", "memcpy_token_mismatch",
-                             "ipc_opens", "ipc_closes", "ipc_shared", "ipc_retired", "ipc_live", "ipc_recovered",
+                             "ipc_opens", "ipc_closes", "ipc_shared", "ipc_retired", "ipc_live", "ipc_close_watermark",
                              "ipc_refusals")}})
         ok_all &= bool(ok)
     # zero-copy disabled: everything staged through the scratch

@@ -1331,6 +1331,27 @@ int main(int argc, char **argv)
             }
             CHECK(rq->req_free(&rq) == OMPI_SUCCESS && tuned_calls == 0, "persistent free");
         }
+        /* (j) a staging failure on rank 0 under the DEVICE lock (VERDICT r4
+         * item 7): its MPI_Allreduce returns the error, and every peer's
+         * call fails within 1 s through the abort word instead of waiting
+         * out the barrier timeout.  The communicator is unusable afterwards:
+         * the section's last call. */
+        {
+            struct timespec t0, t1;
+            double secs;
+            int rc;
+            CHECK(rm->mode == ROCM_RES_DEVICE, "still locked to DEVICE (mode %d)", rm->mode);
+            rm->fail_stage = 0 == g_rank;
+            clock_gettime(CLOCK_MONOTONIC, &t0);
+            rc = table.coll_allreduce(0 == g_rank ? (void *) h : d, 0 == g_rank ? (void *) h2 : d2,
+                                      (int) n, &dfloat, &sum, &comm, table.coll_allreduce_module);
+            clock_gettime(CLOCK_MONOTONIC, &t1);
+            secs = (double) (t1.tv_sec - t0.tv_sec) + 1e-9 * (double) (t1.tv_nsec - t0.tv_nsec);
+            CHECK(OMPI_SUCCESS != rc, "the call with rank 0's staging failure succeeded");
+            CHECK(secs < 1.0, "failed after %.3f s (the peers waited for the barrier timeout)", secs);
+            fprintf(stderr, "rank %d: staging failure on rank 0 -> rc %d after %.1f ms\n", g_rank, rc,
+                    secs * 1e3);
+        }
 #undef BOOT
         harness_dev_free(d);
         harness_dev_free(d2);

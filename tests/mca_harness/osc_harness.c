@@ -10,6 +10,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "mpi.h"
 #include "ompi/communicator/communicator.h"
@@ -24,6 +25,7 @@
 #include "../../oracle/oracle.h"
 #include "osc_rocm.h"
 #include "ompi_amd.h"
+#include "coll_saved.h"
 
 extern int harness_dev_alloc_copy(void **d, const void *h, size_t bytes);
 extern int harness_dev_copy_in(void *d, const void *h, size_t bytes);
@@ -32,6 +34,9 @@ extern int harness_dev_free(void *d);
 
 harness_proc_name_t harness_proc_name = {4242, 0};
 int ompi_op_ddt_map[64];
+OBJ_CLASS_INSTANCE(mca_coll_base_module_t, opal_object_t, NULL, NULL);
+ompi_datatype_t harness_mpi_int = {ORC_T_INT32, 4, 1, 1};
+ompi_op_t harness_mpi_max = {OMPI_OP_FLAGS_INTRINSIC, ORC_OP_MAX};
 
 #define CHECK(c, ...)                                                   \
     do {                                                                \
@@ -64,6 +69,8 @@ int main(int argc, char **argv)
     ompi_op_t sum = {OMPI_OP_FLAGS_INTRINSIC, ORC_OP_SUM}, user = {0, ORC_OP_SUM};
     opal_info_t dev_info = {"ompi_amd_device", "true", NULL};
     ompi_osc_base_component_t *c = &mca_osc_rocm_component.super;
+    mca_coll_base_comm_coll_t table;
+    mca_coll_base_module_t *tm;
     int i;
 
     if (argc < 4) return 2;
@@ -72,7 +79,11 @@ int main(int argc, char **argv)
     g_size = atoi(argv[3]);
     for (i = 0; i < 64; ++i) ompi_op_ddt_map[i] = i;
     local.grp_proc_count = g_size;
-    comm = (ompi_communicator_t){g_rank, g_size, 5, 0, &local, NULL};
+    /* the communicator's collectives (the query's agreement): host stand-ins */
+    tm = OBJ_NEW(mca_coll_base_module_t);
+    harness_saved_init(argv[1], g_rank, g_size);
+    harness_fill_tuned(&table, tm);
+    comm = (ompi_communicator_t){g_rank, g_size, 5, 0, &local, &table};
     if (c->osc_version.mca_register_component_params)
         c->osc_version.mca_register_component_params();
 
@@ -99,6 +110,7 @@ int main(int argc, char **argv)
               "shared without the device info key");
     }
     if (!use_gpu) {
+        harness_saved_fini();
         printf("ok\n");
         return 0;
     }
@@ -116,6 +128,46 @@ int main(int argc, char **argv)
     CHECK(harness_dev_alloc_copy(&dbase, init, n * 4) == 0, "device window");
     CHECK(harness_dev_alloc_copy(&dorg, org, n * 4) == 0, "device origin");
     CHECK(harness_dev_alloc_copy(&dgot, init, n * 4) == 0, "device result");
+
+    /* residency differs between ranks: the framework
+     * selects per rank, so the query agrees over the communicator.  Host
+     * memory everywhere: no rank takes osc/rocm.  Rank 0 on host memory,
+     * the others on device memory: every rank takes osc/rocm and every
+     * rank's select refuses the window with the same error at once (no
+     * rank waits for a peer).  Rank 0 with an empty window on a host
+     * pointer: a device window. */
+    {
+        ompi_win_t mw = {0};
+        float hostbuf[64];
+        void *hb = hostbuf, *mb = 0 == g_rank ? (void *) hostbuf : dbase;
+        struct timespec t0, t1;
+        double secs;
+        int rc;
+        CHECK(c->osc_query(&mw, &hb, sizeof(hostbuf), 4, &comm, NULL, MPI_WIN_FLAVOR_CREATE) < 0,
+              "host windows on every rank stay with the host components");
+        prio = c->osc_query(&mw, &mb, 64 * 4, 4, &comm, NULL, MPI_WIN_FLAVOR_CREATE);
+        CHECK(prio == 101, "mixed residency: every rank takes osc/rocm (%d)", prio);
+        clock_gettime(CLOCK_MONOTONIC, &t0);
+        rc = c->osc_select(&mw, &mb, 64 * 4, 4, &comm, NULL, MPI_WIN_FLAVOR_CREATE, &model);
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        secs = (double) (t1.tv_sec - t0.tv_sec) + 1e-9 * (double) (t1.tv_nsec - t0.tv_nsec);
+        CHECK(rc == OMPI_ERR_NOT_SUPPORTED && NULL == mw.w_osc_module,
+              "mixed residency refused alike (rc %d)", rc);
+        CHECK(secs < 1.0, "mixed residency refused in %.3f s", secs);
+        /* an empty host-pointer window beside device windows is a device window */
+        mb = 0 == g_rank ? (void *) hostbuf : dbase;
+        CHECK(c->osc_query(&mw, &mb, 0 == g_rank ? 0 : 64 * 4, 4, &comm, NULL, MPI_WIN_FLAVOR_CREATE) == 101,
+              "empty window on a host pointer");
+        CHECK(c->osc_select(&mw, &mb, 0 == g_rank ? 0 : 64 * 4, 4, &comm, NULL, MPI_WIN_FLAVOR_CREATE,
+                            &model) == OMPI_SUCCESS && mw.w_osc_module, "select with an empty rank");
+        CHECK(((ompi_osc_base_module_t *) mw.w_osc_module)->osc_free(&mw) == OMPI_SUCCESS, "free");
+        /* the allocating flavor's info key on some ranks only: refused alike */
+        CHECK(c->osc_query(&mw, &hb, 64, 8, &comm, 0 == g_rank ? NULL : &dev_info,
+                           MPI_WIN_FLAVOR_ALLOCATE) == 101, "info key on some ranks");
+        CHECK(c->osc_select(&mw, &hb, 64, 8, &comm, 0 == g_rank ? NULL : &dev_info,
+                            MPI_WIN_FLAVOR_ALLOCATE, &model) == OMPI_ERR_NOT_SUPPORTED,
+              "allocate with the info key on some ranks refused alike");
+    }
 
     prio = c->osc_query(&win, &dbase, n * 4, 4, &comm, NULL, MPI_WIN_FLAVOR_CREATE);
     CHECK(prio == 101, "query on device memory: %d", prio);
@@ -203,6 +255,36 @@ int main(int argc, char **argv)
         orc_op_2buff(ORC_OP_SUM, ORC_T_FLOAT, oprv, mine, n);
         CHECK(harness_dev_copy_in(dbase, mine, n * 4) == 0, "restore window");
         CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence derived 3");
+        /* derived put / get (osc_sm_comm.c:24-100, 209-270): my origin's
+         * first k floats into every other float of the next window (its
+         * gaps untouched), then those slots of the next window back into
+         * a gapped origin layout whose gaps survive */
+        {
+            const size_t kk = 3001;
+            float *expw = malloc(n * 4), *pat = malloc(2 * kk * 4), *back = malloc(2 * kk * 4);
+            const int ddts0 = harness_device_ddts;
+            CHECK(m->osc_put(dorg, (int) kk, &dfloat, nxt, 0, (int) kk, &dgap, &win) == OMPI_SUCCESS,
+                  "derived-target put");
+            CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence derived put");
+            memcpy(expw, mine, n * 4);
+            for (j = 0; j < kk; ++j) expw[2 * j] = oprv[j];
+            CHECK(harness_dev_copy_back(got, dbase, n * 4) == 0, "copy back derived put");
+            CHECK(0 == memcmp(got, expw, n * 4), "derived put: every other float, gaps untouched");
+            fill_exact(pat, 2 * kk, g_rank, 78);
+            CHECK(harness_dev_copy_in(dgot, pat, 2 * kk * 4) == 0, "get pattern");
+            CHECK(m->osc_get(dgot, (int) kk, &dgap, nxt, 0, (int) kk, &dgap, &win) == OMPI_SUCCESS,
+                  "derived get into a gapped origin");
+            CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence derived get");
+            CHECK(harness_dev_copy_back(back, dgot, 2 * kk * 4) == 0, "copy back derived get");
+            for (j = 0; j < kk; ++j) {
+                CHECK(0 == memcmp(&back[2 * j], &org[j], 4), "derived get slot %zu", j);
+                CHECK(0 == memcmp(&back[2 * j + 1], &pat[2 * j + 1], 4), "derived get gap %zu", j);
+            }
+            CHECK(harness_device_ddts >= ddts0, "device programs");
+            CHECK(harness_dev_copy_in(dbase, mine, n * 4) == 0, "restore window after put");
+            CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence derived 4");
+            free(expw), free(pat), free(back);
+        }
         free(slots), free(oprv), free(mine), free(nxtw), free(fetched), free(pattern);
     }
 
@@ -387,6 +469,7 @@ int main(int argc, char **argv)
     harness_dev_free(dbase);
     harness_dev_free(dorg);
     harness_dev_free(dgot);
+    harness_saved_fini();
     printf("ok gpu\n");
     return 0;
 }

@@ -15,4 +15,12 @@
 #define MPI_PROC_NULL (-2)
 #define MPI_ERR_WIN 53
 #define MPI_ERR_RMA_ATTACH 69
+/* the predefined handles the glue's agreement uses (ompi/include/mpi.h.in:
+ * OMPI_PREDEFINED_GLOBAL): harness objects, defined by osc_harness.c */
+struct ompi_datatype_t;
+struct ompi_op_t;
+extern struct ompi_datatype_t harness_mpi_int;
+extern struct ompi_op_t harness_mpi_max;
+#define MPI_INT (&harness_mpi_int)
+#define MPI_MAX (&harness_mpi_max)
 #endif

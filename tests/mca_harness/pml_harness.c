@@ -481,11 +481,12 @@ int main(int argc, char **argv)
         ompi_amd_comm_t *dev = mca_pml_rocm_comm_of(&comm);
         const size_t n = 8u << 20;
         unsigned char *h = malloc(n), *got = malloc(n);
-        int64_t staged0 = 0, staged1 = 0, refused0 = 0, refused1 = 0;
+        int64_t staged0 = 0, staged1 = 0, aged0 = 0, aged1 = 0, direct0 = 0, direct1 = 0;
         for (int mode = 0; mode < 2; ++mode) {
             CHECK(ompi_amd_comm_set_param(dev, "p2p_user_ipc", mode) == OMPI_AMD_SUCCESS, "p2p_user_ipc");
             (void) ompi_amd_comm_get_param(dev, "p2p_staged_sends", &staged0);
-            (void) ompi_amd_comm_get_param(dev, "p2p_export_refusals", &refused0);
+            (void) ompi_amd_comm_get_param(dev, "p2p_unsafe_sends", &aged0);
+            (void) ompi_amd_comm_get_param(dev, "p2p_direct_sends", &direct0);
             for (int it = 0; it < 3; ++it) {
                 void *ds, *dr;
                 ompi_status_public_t st;
@@ -509,15 +510,21 @@ int main(int argc, char **argv)
                 harness_dev_free(dr);
             }
             (void) ompi_amd_comm_get_param(dev, "p2p_staged_sends", &staged1);
-            (void) ompi_amd_comm_get_param(dev, "p2p_export_refusals", &refused1);
-            /* mode 1: every send from the buffer itself, except one the
-             * runtime refused to export (it goes through a stage instead) */
-            CHECK(mode == 0 ? staged1 - staged0 == 3 : staged1 - staged0 == refused1 - refused0,
-                  "mode %d: %lld staged sends, %lld refused exports", mode,
-                  (long long) (staged1 - staged0), (long long) (refused1 - refused0));
-            if (refused1 > refused0)
-                fprintf(stderr, "rank %d: %lld export(s) refused by the runtime, staged\n", g_rank,
-                        (long long) (refused1 - refused0));
+            (void) ompi_amd_comm_get_param(dev, "p2p_unsafe_sends", &aged1);
+            (void) ompi_amd_comm_get_param(dev, "p2p_direct_sends", &direct1);
+            /* mode 0: every send staged.  mode 1: from the buffer itself,
+             * except a buffer allocated before this rank closed an IPC
+             * mapping (its receive retired the peer's freed buffer): ROCm
+             * 7.2 may refuse to export that one, so it is
+             * staged without being offered — no runtime refusal reaches the
+             * send (the round-4 intermittent failure of this section) */
+            CHECK(mode == 0 ? staged1 - staged0 == 3
+                            : staged1 - staged0 == aged1 - aged0 && (staged1 - staged0) + (direct1 - direct0) == 3,
+                  "mode %d: %lld staged sends, %lld aged, %lld direct", mode, (long long) (staged1 - staged0),
+                  (long long) (aged1 - aged0), (long long) (direct1 - direct0));
+            if (mode == 1)
+                fprintf(stderr, "rank %d: user_ipc sends: %lld direct, %lld staged (older than an IPC close)\n",
+                        g_rank, (long long) (direct1 - direct0), (long long) (aged1 - aged0));
         }
         (void) ompi_amd_comm_set_param(dev, "p2p_user_ipc", 0);
         free(h);
@@ -642,6 +649,45 @@ int main(int argc, char **argv)
         /* 2 messages per call pair, 4 one-start forms + 2 two-start ones */
         CHECK(harness_saved_pml_msgs - msgs0 == 2 * (2 + 2 + 4), "system-tag messages moved by the host "
               "transport: %d", harness_saved_pml_msgs - msgs0);
+        free(h);
+        free(t);
+    }
+    SECTION(12);
+    /* 12. two system-tag receives in flight into ONE device buffer whose
+     * typed spans interleave (the gapped type at offsets 0 and 4: each
+     * one's elements sit in the other's gaps, as a linear gather into a
+     * resized column type lays them out).  Each receive must write back
+     * only the bytes it received: a whole-span copy of the second to
+     * complete would put its stale pre-fill over the first one's data
+     * (ADVICE r4, high). */
+    {
+        const size_t n = 12345;
+        const int tag = HARNESS_SYS_TAG - 21;  /* tag and tag + 1: no other section uses them */
+        int *h = malloc(n * 8), *t = malloc(n * 8);
+        void *ds, *dr;
+        ompi_request_t *ra = NULL, *rb = NULL;
+        for (size_t i = 0; i < 2 * n; ++i) h[i] = (int) (g_rank * 9001 + i * 5 + 3);
+        for (size_t i = 0; i < 2 * n; ++i) t[i] = -7;
+        CHECK(harness_dev_alloc_copy(&ds, h, n * 8) == 0 && harness_dev_alloc_copy(&dr, t, n * 8) == 0,
+              "device buffers");
+        CHECK(mca_pml.pml_irecv(dr, n, &gap4, left, tag, &comm, &ra) == OMPI_SUCCESS &&
+                  mca_pml.pml_irecv((char *) dr + 4, n, &gap4, left, tag + 1, &comm, &rb) == OMPI_SUCCESS,
+              "two interleaved receives");
+        /* the even elements of ds into the first, the odd ones into the second */
+        CHECK(mca_pml.pml_send(ds, n, &gap4, right, tag, MCA_PML_BASE_SEND_STANDARD, &comm) == OMPI_SUCCESS &&
+                  mca_pml.pml_send((char *) ds + 4, n, &gap4, right, tag + 1, MCA_PML_BASE_SEND_STANDARD,
+                                   &comm) == OMPI_SUCCESS,
+              "two sends");
+        wait_req(ra);
+        wait_req(rb);
+        CHECK(ra->req_status.MPI_ERROR == OMPI_SUCCESS && rb->req_status.MPI_ERROR == OMPI_SUCCESS,
+              "interleaved receive status");
+        CHECK(harness_dev_copy_back(t, dr, n * 8) == 0, "copy back");
+        for (size_t i = 0; i < 2 * n; ++i)
+            CHECK(t[i] == (int) (left * 9001 + i * 5 + 3), "interleaved receives, int %zu: %d", i, t[i]);
+        CHECK(ra->req_free(&ra) == OMPI_SUCCESS && rb->req_free(&rb) == OMPI_SUCCESS, "free");
+        harness_dev_free(ds);
+        harness_dev_free(dr);
         free(h);
         free(t);
     }

@@ -104,7 +104,11 @@ int harness_pml_saved_try_recv(void *buf, size_t count, const ompi_datatype_t *d
     if (__atomic_load_n(&p->posted, __ATOMIC_ACQUIRE) == p->taken) return 0;
     struct slot *s = &p->s[p->taken % SLOTS];
     if (!__atomic_load_n(&s->full, __ATOMIC_ACQUIRE)) return 0;
-    if (s->tag != tag) die("message order: another tag at the head of the mailbox");
+    if (s->tag != tag) {
+        fprintf(stderr, "saved PML stand-in: receive (src %d, tag %d) found tag %d at the head\n", src, tag,
+                s->tag);
+        die("message order: another tag at the head of the mailbox");
+    }
     if (s->bytes > count * d->size) die("truncation");
     if (d->contiguous) memcpy(buf, s->data, s->bytes);
     else
@@ -161,8 +165,12 @@ static void s_launch(sreq *q)
         return;
     }
     q->super.req_complete = REQUEST_PENDING;
-    q->next = g_pending;
-    g_pending = q;
+    q->next = NULL;  /* posting order: receives match in the order they were posted (MPI) */
+    {
+        sreq **pp = &g_pending;
+        while (*pp) pp = &(*pp)->next;
+        *pp = q;
+    }
     (void) opal_progress_register(s_progress);
 }
 

@@ -87,22 +87,24 @@ def case_ring(comm, rank, n, nbytes, salt, soff=0, roff=0):
     return ok, msg
 
 
-def case_export_refused(comm, rank, n, salt, nbytes=(8 << 20) + 12):
-    """p2p_user_ipc = 1 with the export of the send buffer refused (the test
-    hook acts as the runtime's intermittent hipIpcGetMemHandle refusal): the
+def case_aged_buffer_staged(comm, rank, n, salt, nbytes=(8 << 20) + 12):
+    """p2p_user_ipc = 1 with the send buffer older than an IPC close of this
+    process (the test hook p2p_age_all makes every buffer so; pml harness
+    section 9 makes it happen for real): ROCm 7.2 may refuse to export such
+    an allocation, so it is never offered for export — the
     message goes through a library stage, byte-exact, counted in
-    p2p_export_refusals and p2p_staged_sends."""
+    p2p_unsafe_sends and p2p_staged_sends."""
     comm.set_param("p2p_user_ipc", 1)
-    comm.set_param("p2p_refuse_exports", 1)
+    comm.set_param("p2p_age_all", 1)
     try:
-        r0, s0 = comm.get_param("p2p_export_refusals"), comm.get_param("p2p_staged_sends")
+        u0, s0 = comm.get_param("p2p_unsafe_sends"), comm.get_param("p2p_staged_sends")
         ok, msg = case_ring(comm, rank, n, nbytes, salt, soff=4, roff=8)
-        r1, s1 = comm.get_param("p2p_export_refusals"), comm.get_param("p2p_staged_sends")
+        u1, s1 = comm.get_param("p2p_unsafe_sends"), comm.get_param("p2p_staged_sends")
     finally:
-        comm.set_param("p2p_refuse_exports", 0)
+        comm.set_param("p2p_age_all", 0)
         comm.set_param("p2p_user_ipc", 0)
-    if ok and (r1 - r0 != 1 or s1 - s0 != 1):
-        return False, f"refusals {r1 - r0}, staged sends {s1 - s0} (want 1, 1)"
+    if ok and (u1 - u0 != 1 or s1 - s0 != 1):
+        return False, f"aged sends {u1 - u0}, staged sends {s1 - s0} (want 1, 1)"
     return ok, msg
 
 
@@ -544,6 +546,104 @@ def case_acc_ddt(comm, rank, n, salt):
         win.free()
 
 
+def case_put_get_ddt(comm, rank, n, salt):
+    """MPI_Put / MPI_Get with derived datatypes (osc_sm_comm.c:24-100,
+    209-270: ompi_datatype_sndrcv of any origin / target pair): each rank
+    puts into the next rank's window through a target datatype (vector of
+    single doubles, blacs-style indexed floats, struct {int, double} with its
+    4-byte hole), from a contiguous or a strided origin, then gets it back
+    into a gapped origin layout; request-based rput / rget under lock_all.
+    Expected bytes: the origin's bytes in type-map order at the target type's
+    byte slots; every other byte of the window and of the origin buffer
+    untouched (byte-exact)."""
+    from ompi_amd import datatype as dd
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    f32, f64, i32 = dd.predefined("MPI_FLOAT"), dd.predefined("MPI_DOUBLE"), dd.predefined("MPI_INT32_T")
+    lens = [13, 13, 13, 13, 13, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1]
+    disps = [286, 308, 330, 352, 374, 396, 419, 442, 465, 488, 511, 534, 557, 580, 603, 626, 649, 672]
+    pair = dd.type_struct([1, 1], [0, 8], [i32, f64])
+    runs = [
+        # (name, target type, tcount, origin type or None (contiguous bytes), request-based)
+        ("vector_bl1_f64", dd.type_vector(20011, 1, 2, f64), 3, None, False),
+        ("blacs_indexed_f32", dd.type_indexed(lens, disps, f32), 37, dd.type_vector(37 * 156, 1, 3, f32), False),
+        ("struct_int_double", pair, 50003, dd.type_vector(50003, 1, 2, pair), False),
+        ("vector_bl3_f32_requests", dd.type_vector(4099, 3, 7, f32), 5, None, True),
+    ]
+    disp_unit, disp = 8, 3  # the target region starts 24 B into the window
+    for k, (name, tdt, tcount, odt, req) in enumerate(runs):
+        tbytes = tdt.size * tcount
+        span = (tcount - 1) * tdt.extent + tdt.true_span
+        wbytes = disp * disp_unit + span + 64
+        init = [np.frombuffer(payload(r, salt + k, wbytes), np.uint8).copy() for r in range(n)]
+        data = [np.frombuffer(payload(r, salt + 10 + k, tbytes), np.uint8).copy() for r in range(n)]
+        tslots = disp * disp_unit + _slots(tdt, tcount, 1)
+        if odt is None:
+            ocount, oslots, obytes = tbytes, np.arange(tbytes), tbytes
+        else:
+            ocount = 1
+            assert odt.size == tbytes
+            oslots = _slots(odt, 1, 1)
+            obytes = int(oslots.max()) + 1
+        org = []
+        for r in range(n):  # the data at the origin type's byte slots, junk between
+            b = np.frombuffer(payload(r, salt + 20 + k, obytes), np.uint8).copy()
+            b[oslots] = data[r]
+            org.append(b)
+        base = dev(init[rank])
+        win = osc.Window.create(comm, base, wbytes, disp_unit=disp_unit)
+        try:
+            o = dev(org[rank])
+            if req:
+                win.lock_all(stream=STREAM)
+                r1 = win.rput_ddt(o, ocount, odt, nxt, disp, tcount, tdt, stream=STREAM)
+                r1.wait()
+                r1.free()
+                win.unlock_all(stream=STREAM)
+                comm_barrier()
+            else:
+                win.fence(stream=STREAM)
+                win.put_ddt(o, ocount, odt, nxt, disp, tcount, tdt, stream=STREAM)
+                win.fence(stream=STREAM, blocking=True)
+            exp = init[rank].copy()
+            exp[tslots] = data[prv]
+            ok, msg = eq(host(base), exp, f"{name}: put into the window")
+            if not ok:
+                return ok, msg
+            # get it back from the next rank (which now holds my data) into a
+            # fresh origin layout whose gaps must survive
+            junk = np.frombuffer(payload(rank, salt + 40 + k, obytes), np.uint8).copy()
+            back = dev(junk)
+            if req:
+                win.lock_all(stream=STREAM)
+                r2 = win.rget_ddt(back, ocount, odt, nxt, disp, tcount, tdt, stream=STREAM)
+                r2.wait()
+                r2.free()
+                win.unlock_all(stream=STREAM)
+            else:
+                win.get_ddt(back, ocount, odt, nxt, disp, tcount, tdt, stream=STREAM)
+                win.fence(stream=STREAM, blocking=True)
+            expo = junk.copy()
+            expo[oslots] = data[rank]
+            ok, msg = eq(host(back), expo, f"{name}: get into the origin layout")
+            if not ok:
+                return ok, msg
+        finally:
+            win.free()
+        comm_barrier()
+    # mismatched signatures are refused
+    win = osc.Window.allocate(comm, 4096, disp_unit=1)
+    try:
+        src = dev(payload(rank, salt, 64))
+        try:
+            win.put_ddt(src, 64, None, nxt, 0, 7, dd.type_vector(4, 2, 3, f32), stream=STREAM)
+            return False, "a put with unequal origin / target byte counts was accepted"
+        except _lib.OmpiAmdError:
+            pass
+    finally:
+        win.free()
+    return True, ""
+
+
 def case_fetch_and_op_counter(comm, rank, n, k=25):
     """Shared counter on rank 0: k fetch_and_op(+1) per rank; the fetched
     values over all ranks are exactly 0 .. n*k-1 (each increment atomic)."""
@@ -887,7 +987,7 @@ def main():
         ("p2p_ring_4099B_misaligned", lambda: case_ring(comm, rank, n, 4099, 3, soff=3, roff=5)),
         ("p2p_ring_64MiB", lambda: case_ring(comm, rank, n, 64 << 20, 4)),
         ("p2p_ring_16MiB_plus_odd", lambda: case_ring(comm, rank, n, (16 << 20) + 13, 5, 16, 16)),
-        ("p2p_export_refused_staged", lambda: case_export_refused(comm, rank, n, 6)),
+        ("p2p_aged_buffer_staged", lambda: case_aged_buffer_staged(comm, rank, n, 6)),
         ("p2p_tags_out_of_order", lambda: case_tags_out_of_order(comm, rank, n, 6)),
         ("p2p_same_tag_order", lambda: case_same_tag_order(comm, rank, n, 20)),
         ("p2p_any_source_any_tag", lambda: case_any_source(comm, rank, n, 70)),
@@ -921,6 +1021,7 @@ def main():
          lambda: case_acc_concurrent(comm, rank, n, DI, mop.MPI_MAXLOC, 30001, 91)),
         ("osc_get_accumulate", lambda: case_get_accumulate(comm, rank, n, 92)),
         ("osc_accumulate_derived_datatypes", lambda: case_acc_ddt(comm, rank, n, 150)),
+        ("osc_put_get_derived_datatypes", lambda: case_put_get_ddt(comm, rank, n, 160)),
         ("osc_fetch_and_op_counter", lambda: case_fetch_and_op_counter(comm, rank, n)),
         ("osc_compare_and_swap", lambda: case_cas(comm, rank, n)),
         ("osc_passive_exclusive_rmw", lambda: case_passive_exclusive(comm, rank, n)),

@@ -19,9 +19,16 @@ from ompi_amd import op as mop  # noqa: E402
 
 S = int(os.environ.get("ACC_MIB", "256")) << 20
 iters = int(os.environ.get("ACC_ITERS", "10"))
+# ACC_WIN=allocate (the bench row: MPI_Win_allocate, the shadow arena) or
+# create (MPI_Win_create over a torch allocation)
+how = os.environ.get("ACC_WIN", "allocate")
 s = torch.cuda.Stream()
 comm = coll.Communicator(f"ddtacc_{os.getpid()}", 0, 1, torch.cuda.current_device())
-win = osc.Window.allocate(comm, S, disp_unit=4)
+if how == "create":
+    wmem = torch.zeros(S // 4, device="cuda")
+    win = osc.Window.create(comm, wmem, S, disp_unit=4)
+else:
+    win = osc.Window.allocate(comm, S, disp_unit=4)
 x = torch.ones(S // 4, device="cuda")
 tvec = ddt.type_vector(S // 16, 1, 2, ddt.predefined("MPI_DOUBLE")).commit()
 torch.cuda.synchronize()
@@ -42,7 +49,7 @@ try:
     b.record(s)
     b.synchronize()
     t = a.elapsed_time(b) / iters / 1e3
-    print(json.dumps({"row": "accumulate_ddt_vector_bl1_f64", "bytes": S, "ms": round(t * 1e3, 4),
+    print(json.dumps({"row": "accumulate_ddt_vector_bl1_f64", "window": how, "bytes": S, "ms": round(t * 1e3, 4),
                       "algorithmic_bytes": int(1.5 * S), "hbm_gbs": round(1.5 * S / t / 1e9, 1),
                       "frac_of_8TBs": round(1.5 * S / t / 8e12, 4)}), flush=True)
 finally:
