@@ -118,6 +118,14 @@ int ompi_amd_comm_agree(ompi_amd_comm_t *comm, int local_ok, int *all_ok);
  * "boot_calls". */
 int ompi_amd_comm_vote(ompi_amd_comm_t *comm, int local_yes, int *n_yes);
 
+/* MPI_Allreduce's blocking form: ompi_amd_allreduce on the per-thread
+ * stream, then the wait ompi_amd_comm_sync would do.  A fused small
+ * allreduce (<= fused_bytes) stores its own host-observed completion from
+ * its last workgroup, so the wait needs no mark kernel behind it (coll/rocm's
+ * blocking allreduce; OMPI_AMD_FUSED_MARK=0 turns the embedded mark off). */
+int ompi_amd_allreduce_wait(ompi_amd_comm_t *comm, const void *sbuf, void *rbuf, size_t count,
+                            int type, int op);
+
 /* This rank cannot take part in a collective its peers will run on the
  * device (e.g. staging its operands failed after the path was agreed):
  * make `rc` (an OMPI_AMD_ERR_* code) this communicator's sticky error and

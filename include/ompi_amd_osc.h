@@ -79,6 +79,19 @@ int ompi_amd_win_unlock_all(ompi_amd_win_t *win, void *stream);
 /* MPI_Win_flush: the calls enqueued so far on `stream` are complete at the
  * target when the host returns (synchronises the stream). */
 int ompi_amd_win_flush(ompi_amd_win_t *win, int target, void *stream);
+/* MPI_Win_sync (osc.h osc_sync): the window's public and private copies
+ * merged (separate model, below); nothing to do otherwise. */
+int ompi_amd_win_sync(ompi_amd_win_t *win, void *stream);
+/* The window's memory model (MPI_WIN_MODEL): UNIFIED, or SEPARATE when some
+ * rank's MPI_Win_create memory cannot be mapped by its peers as it is (not
+ * an IPC-safe size, or older than an IPC close of that process): that rank's
+ * RMA target is a public copy in library memory, merged with the caller's
+ * memory (the private copy) at every fence, post / wait, lock / unlock of
+ * its own window and MPI_Win_sync; every rank of the window then reports
+ * SEPARATE and takes part in the fence's merge step. */
+#define OMPI_AMD_WIN_UNIFIED 0
+#define OMPI_AMD_WIN_SEPARATE 1
+int ompi_amd_win_model(const ompi_amd_win_t *win);
 
 int ompi_amd_put(ompi_amd_win_t *win, const void *origin, size_t bytes, int target, size_t disp,
                  void *stream);

@@ -18,10 +18,14 @@
  * are matched in the order they were sent, receives in the order they were
  * posted, MPI_ANY_SOURCE / MPI_ANY_TAG as wildcards.
  *
- * Completion semantics.  A send synchronises `stream` first (its data must
- * be final).  Messages of at most 4 KiB (btl/smcuda's eager limit) are
- * copied into the sender's device eager area and the send completes at
- * once (ob1's eager protocol).  Larger ones are copied into a library-owned
+ * Completion semantics.  A send's data is read in `stream` order (after
+ * the work already queued on it).  Messages of at most 4 KiB (btl/smcuda's
+ * eager limit) are copied into the sender's device eager area (ob1's eager
+ * protocol): from a device buffer by a kernel on `stream` that publishes
+ * the cell itself — the message is posted at once, the receiver's copy
+ * waits for the cell on the device, and the send completes when that
+ * kernel has run; from a host buffer before the call returns.  Larger ones
+ * (after a synchronisation of `stream`) are copied into a library-owned
  * send stage (a pool of exported device buffers that live as long as the
  * communicator) and the send completes once staged — the receiver pulls
  * from the stage, so no peer ever maps an application buffer; MPI_Ssend

@@ -137,6 +137,8 @@ PROTOTYPES = [
     ("ompi_amd_comm_agree", _C.c_int, [_C.c_void_p, _C.c_int, _C.POINTER(_C.c_int)]),
     ("ompi_amd_comm_vote", _C.c_int, [_C.c_void_p, _C.c_int, _C.POINTER(_C.c_int)]),
     ("ompi_amd_comm_abort", _C.c_int, [_C.c_void_p, _C.c_int]),
+    ("ompi_amd_allreduce_wait", _C.c_int, [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t,
+                                           _C.c_int, _C.c_int]),
     ("ompi_amd_comm_sync", _C.c_int, [_C.c_void_p, _C.c_void_p]),
     ("ompi_amd_comm_phase_ms", _C.c_int,
      [_C.c_void_p, _C.c_int, _C.POINTER(_C.c_double), _C.POINTER(_C.c_int)]),
@@ -256,6 +258,8 @@ PROTOTYPES = [
     ("ompi_amd_get_accumulate", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_size_t,
       _C.c_int, _C.c_void_p]),
+    ("ompi_amd_win_sync", _C.c_int, [_C.c_void_p, _C.c_void_p]),
+    ("ompi_amd_win_model", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_put_ddt", _C.c_int, [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p, _C.c_int,
                                     _C.c_size_t, _C.c_size_t, _C.c_void_p, _C.c_void_p]),
     ("ompi_amd_get_ddt", _C.c_int, [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p, _C.c_int,

@@ -140,6 +140,14 @@ class Communicator:
                                           op.index, _stream(stream))
         self._finish(rc, f"allreduce({op.name},{datatype.name})", blocking, stream)
 
+    def allreduce_wait(self, sbuf, rbuf, count: int, datatype: Datatype, op: Op) -> None:
+        """MPI_Allreduce's blocking form on the per-thread stream
+        (ompi_amd_allreduce_wait: a fused small call stores its own
+        completion mark)."""
+        _lib.check(self._lib.ompi_amd_allreduce_wait(self._h, _ptr(sbuf), _ptr(rbuf), count,
+                                                     datatype.code, op.index),
+                   f"allreduce_wait({op.name},{datatype.name})")
+
     def iallreduce(self, sbuf, rbuf, count: int, datatype: Datatype, op: Op,
                    stream=None) -> "Request":
         """MPI_Iallreduce: returns without waiting for any peer."""

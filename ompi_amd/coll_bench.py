@@ -277,6 +277,14 @@ def bench_allreduce(args, metric: str, link_gbs: float):
                      "peak": roof, "unit": "GB/s",
                      "frac": round(red_gbs / roof, 4) if red_gbs and not shared else None,
                      "traffic": traffic,
+                     # why None: every MI355X pass so far shared one GPU
+                     # between the ranks, where the device-wide TCC counters
+                     # of a rank-0 dispatch also count the peers' concurrent
+                     # kernels (they meet at device barriers), so no per-
+                     # launch figure of one rank exists to commit
+                     "traffic_source": ("profiles/pmc.json" if traffic is not None else
+                                        "none: no dedicated-GPU PMC pass (shared-GPU counters "
+                                        "mix the ranks' concurrent kernels)"),
                      "kernel": kernel,
                      "phase": dom, "kernel_ms": xg[dom]["kernel_ms"] if dom else None,
                      "phases": ph,

@@ -419,6 +419,8 @@ struct ompi_amd_comm {
     size_t bcast_split_bytes = 4u << 20;  // from this size on (0: never)
     int64_t exports_new = 0, imports_new = 0;  // runtime export / open calls made (cache misses)
     int recycled_exports = 0;             // exports refused: recycled handle bytes (shadowed)
+    int64_t reused_exports = 0;           // not exported: an address exported before under another id (shadowed)
+    int reuse_shadow = 1;                 // param "reuse_shadow": 0 exports such allocations (registry tests)
     int unsafe_exports = 0;               // application buffers of no IPC-safe size (shadowed)
     int aged_exports = 0;                 // application buffers older than an IPC close (shadowed)
     // streams this communicator launched work on: the current one, plus an
@@ -458,6 +460,8 @@ struct ompi_amd_comm {
     size_t arena_bytes = 0;
     int shadowed = 0;                     // zero-copy calls that needed it
     int force_shadow = 0;                 // param "force_shadow": take the fallback always (tests)
+    int win_shadow = 0;                   // param "osc_win_shadow": 1 = every MPI_Win_create shadowed (tests)
+    int64_t shadow_windows = 0;           // MPI_Win_create windows in the separate model (osc_ipc.hip)
     // param "user_ipc" (env OMPI_AMD_USER_IPC): export the caller's buffers
     // to peers (zero-copy).  Off by default: every zero-copy-size call stages
     // through the shadow arena (exported once, never freed), because on ROCm
@@ -469,6 +473,12 @@ struct ompi_amd_comm {
     int *err_host = nullptr, *err_dev = nullptr;
     uint64_t *dbg_host = nullptr, *dbg_dev = nullptr;  // OMPI_AMD_DEBUG_PROGRESS=1 (barrier_kernel)
     uint64_t epoch = 0;
+    // ompi_amd_allreduce_wait: the fused launch stores its own host mark
+    // (fused_mark: this communicator's pinned word; want_mark set for the
+    // duration of that call; mark_embedded the value it stores, 0 none)
+    uint64_t *fused_mark = nullptr;
+    bool want_mark = false;
+    uint64_t mark_embedded = 0;
     // params
     size_t small_bytes = 1 << 20;
     size_t fused_bytes = 64 << 10;
@@ -723,6 +733,24 @@ static bool export_known(void *base, size_t size, unsigned long long id) {
     return false;
 }
 
+// An allocation at an address this process exported before under another
+// buffer id (the earlier allocation freed, the address handed out again):
+// a peer that mapped the earlier one retires that mapping and opens this
+// one's handle right after the close, and ROCm 7.2 refused such an open
+// ("invalid device pointer") about once in several hundred re-imports of a
+// 20 MiB torch segment (round 4's N = 8 user_ipc_free_realloc, round 5's
+// ipc-share realloc step) — no replay order reproduces it on demand, so the
+// sequence is avoided instead: such an allocation is never exported where
+// the caller has somewhere else to put the bytes (shadow, stage, public
+// window copy).  Library allocations never reuse an exported address
+// (alloc_exportable keeps a repeated one alive).
+static bool export_reused(void *base, unsigned long long id) {
+    std::lock_guard<std::mutex> g(g_exp_mu);
+    for (const auto &r : g_exp)
+        if (r.base == base && r.id != id) return true;
+    return false;
+}
+
 // An allocation this process may not export any more: it predates a close
 // of one of its IPC mappings (ROCm 7.2 then refuses its export, for good,
 // 10-30 % of the time — ipc_registry.h) and was not exported before.
@@ -812,6 +840,13 @@ static int export_buf(ompi_amd_comm_t *c, const void *ptr, buf_desc *d, bool *ip
     // A caller with a shadow never offers an allocation a close spoiled
     // (ipc_registry.h).  One without (a window over the caller's memory)
     // tries: most such exports work, and a refusal fails every rank alike.
+    if (ipc_failed && c->reuse_shadow && export_reused(base, id)) {
+        *ipc_failed = true;
+        ++c->reused_exports;
+        record_msg("allocation %p + %zu (id %llu) reuses an address this process exported before: not "
+                   "exported (DESIGN.md §4.6)", base, size, id);
+        return OMPI_AMD_ERR_HIP;
+    }
     if (ipc_failed && export_aged(base, size, id)) {
         *ipc_failed = true;
         ++c->aged_exports;
@@ -1759,7 +1794,14 @@ static int allreduce_fused(ompi_amd_comm_t *c, const void *src, void *rbuf, int6
     const int64_t cols = std::max<int64_t>(
         1, std::min<int64_t>((most + 4 * kXferThreads - 1) / (4 * kXferThreads),
                              kFusedMaxGroups / rows));
-    return record_hip(f(dim3((unsigned)cols, (unsigned)rows), a, s), "fused allreduce launch");
+    if (c->want_mark && c->fused_mark) {  // the blocking entry's completion, by the kernel itself
+        a.done = reinterpret_cast<uint32_t *>(c->flags) + kFusedDoneWord;
+        a.mark = c->fused_mark;
+        a.mark_v = mark_reserve();
+    }
+    TRY(record_hip(f(dim3((unsigned)cols, (unsigned)rows), a, s), "fused allreduce launch"));
+    if (a.mark) c->mark_embedded = a.mark_v;
+    return OMPI_AMD_SUCCESS;
 }
 
 // ---- medium allreduce, staged two-shot: my input -> my scratch, barrier,
@@ -2688,6 +2730,7 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
         mine.pci[0] = mine.pci[1] = mine.pci[2] = -1;  // unknown: counted as shared
     }
     *c->err_host = 0;
+    c->fused_mark = mark_word_get();  // nullptr with marks off: ompi_amd_allreduce_wait syncs instead
     ipc_add_user(c, quiesce_user);
     if (rank == 0) rc = p2p_create(c, name, rank, size, 0, &c->p2p);
     if (rc == OMPI_AMD_SUCCESS) rc = c->boot.allgather(&mine, all, sizeof(ipc_blob));
@@ -2759,6 +2802,7 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
             hip_ignore(hipEventDestroy(pr.first));
             hip_ignore(hipEventDestroy(pr.second));
         }
+    mark_word_put(c->fused_mark);  // its last wait is over (destroy drained the streams)
     for (auto e : c->ev_free) hip_ignore(hipEventDestroy(e));
     for (auto e : c->req_ev_free) hip_ignore(hipEventDestroy(e));
     for (auto &kv : c->tune)
@@ -2839,6 +2883,24 @@ int ompi_amd_comm_vote(ompi_amd_comm_t *c, int local_yes, int *n_yes) {
     return OMPI_AMD_SUCCESS;
 }
 
+int ompi_amd_allreduce_wait(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
+                            int op) {
+    if (!c) return OMPI_AMD_ERR_BAD_PARAM;
+    static const bool on = !(getenv("OMPI_AMD_FUSED_MARK") && atoi(getenv("OMPI_AMD_FUSED_MARK")) == 0);
+    c->want_mark = on;
+    c->mark_embedded = 0;
+    const int rc = ompi_amd_allreduce(c, sbuf, rbuf, count, type, op, nullptr);
+    c->want_mark = false;
+    const uint64_t v = c->mark_embedded;
+    c->mark_embedded = 0;
+    if (rc != OMPI_AMD_SUCCESS || !v) return rc != OMPI_AMD_SUCCESS ? rc : ompi_amd_comm_sync(c, nullptr);
+    // the fused kernel was the call's last launch on the per-thread stream,
+    // and it stores the mark itself: no mark kernel behind it
+    api_guard api_(c);
+    TRY(record_hip(mark_value_wait(thread_stream(), c->fused_mark, v, progress_others), "allreduce wait"));
+    return check_sticky(c);
+}
+
 int ompi_amd_comm_abort(ompi_amd_comm_t *c, int rc) {
     api_guard api_(c);
     if (!c || rc >= 0) return OMPI_AMD_ERR_BAD_PARAM;
@@ -2905,6 +2967,10 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
         c->pipe_passes = (int)v;
     } else if (!strcmp(key, "force_shadow")) {
         c->force_shadow = v ? 1 : 0;
+    } else if (!strcmp(key, "reuse_shadow")) {
+        c->reuse_shadow = v ? 1 : 0;
+    } else if (!strcmp(key, "osc_win_shadow")) {
+        c->win_shadow = v ? 1 : 0;
     } else if (!strcmp(key, "user_ipc")) {
         c->user_ipc = v ? 1 : 0;
         c->autotune = 0;
@@ -2996,6 +3062,10 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "recycled_exports")) *v = c->recycled_exports;
     else if (!strcmp(key, "imports_new")) *v = c->imports_new;
     else if (!strcmp(key, "force_shadow")) *v = c->force_shadow;
+    else if (!strcmp(key, "osc_win_shadow")) *v = c->win_shadow;
+    else if (!strcmp(key, "reuse_shadow")) *v = c->reuse_shadow;
+    else if (!strcmp(key, "reused_exports")) *v = c->reused_exports;
+    else if (!strcmp(key, "osc_shadow_windows")) *v = c->shadow_windows;
     else if (!strcmp(key, "user_ipc")) *v = c->user_ipc;
     else if (!strcmp(key, "imports")) *v = (int64_t)c->imports.size();
     else if (!strncmp(key, "p2p_", 4) && p2p_get_param(c->p2p, key, v) == OMPI_AMD_SUCCESS) return OMPI_AMD_SUCCESS;
@@ -4337,7 +4407,17 @@ bool comm_ipc_safe(const void *ptr) {
         (void)hipGetLastError();
         return false;
     }
-    return ipc_safe_size(size) && size <= kMaxIpcBytes && !export_aged(base, size, buffer_id(ptr));
+    const unsigned long long id = buffer_id(ptr);
+    return ipc_safe_size(size) && size <= kMaxIpcBytes && !export_aged(base, size, id) &&
+           !export_reused(base, id);
+}
+
+bool comm_win_needs_shadow(ompi_amd_comm_t *c, const void *base) {
+    if (c->win_shadow || !comm_ipc_safe(base)) {
+        ++c->shadow_windows;
+        return true;
+    }
+    return false;
 }
 
 int comm_import(ompi_amd_comm_t *c, int peer, const ipc_desc &d, const char **out, bool pin,

@@ -387,7 +387,16 @@ struct fused_args {
     int64_t count, split, early, late;
     uint64_t epoch, timeout_ticks;
     int *err;
+    // ompi_amd_allreduce_wait: the last workgroup to finish stores mark_v
+    // into the pinned host word `mark` (done: a zeroed counter in my flag
+    // page) — the host's wait needs no mark kernel after this one
+    uint32_t *done;
+    uint64_t *mark;
+    uint64_t mark_v;
 };
+
+// flag-page word (uint32 index) of the fused kernel's finished-workgroup counter
+constexpr int kFusedDoneWord = 8192 / (int)sizeof(uint32_t);
 
 template <typename T, int OP>
 __global__ __launch_bounds__(kXferThreads) void fused_allreduce_kernel(fused_args a) {
@@ -429,6 +438,18 @@ __global__ __launch_bounds__(kXferThreads) void fused_allreduce_kernel(fused_arg
         T v[kMaxRanks];
         gather_scalar<T>(v, a.peers, a.n, first, e);
         store_elem<T>(dst + e, fold<T, OP>(v, a.n, a.order, 0));
+    }
+    if (a.mark) {  // the host-observed completion, by the last workgroup
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // my results, device-wide
+            const uint32_t total = gridDim.x * gridDim.y;
+            if (__hip_atomic_fetch_add(a.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
+                __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(a.mark, a.mark_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
     }
 }
 

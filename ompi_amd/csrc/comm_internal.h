@@ -53,6 +53,9 @@ int comm_export(ompi_amd_comm_t *c, const void *ptr, ipc_desc *d);
 // before it (ipc_close_watermark).  A caller with a library stage sends
 // other allocations through it.
 bool comm_ipc_safe(const void *ptr);
+// MPI_Win_create over base: run it through a public copy (separate model)?
+// Not IPC-safe (above), or param osc_win_shadow; counted (osc_shadow_windows).
+bool comm_win_needs_shadow(ompi_amd_comm_t *c, const void *base);
 // Map a peer's exported buffer (cached, LRU).  pin: held until comm_unpin.
 int comm_import(ompi_amd_comm_t *c, int peer, const ipc_desc &d, const char **out, bool pin,
                 void **base);
@@ -69,6 +72,13 @@ int comm_copy(ompi_amd_comm_t *c, const void *src, void *dst, size_t bytes, hipS
 // osc_ipc.hip: the byte copy of put / get and the p2p receive (persistent
 // grid, one acquire per workgroup; src or dst may be peer memory).
 // gate: a CTL_TAKEN_* word that must read 1 for the copy to run (NULL: none).
+// p2p eager cells (osc_ipc.hip, one workgroup, bytes <= 4 KiB): eager_put
+// copies src into the cell, then stores v into *flag (system scope, after a
+// release); eager_get waits (bounded by ticks of s_memrealtime: err set,
+// nothing copied) until *flag == v, then copies the cell out.
+int eager_put(const void *src, char *cell, size_t bytes, uint64_t *flag, uint64_t v, hipStream_t s);
+int eager_get(const char *cell, void *dst, size_t bytes, const uint64_t *flag, uint64_t v, int *err,
+              uint64_t ticks, hipStream_t s);
 int xfer_copy(const void *src, void *dst, size_t bytes, hipStream_t s,
               const uint32_t *gate = nullptr);
 // Point-to-point mailboxes of the communicator (created with it).

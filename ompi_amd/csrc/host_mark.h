@@ -24,6 +24,9 @@ uint64_t *mark_word_get();      // nullptr when marks are off or pinned memory i
 void mark_word_put(uint64_t *w);
 // enqueue the mark on `s`: the value to wait for, 0 if none was launched
 uint64_t mark_launch(uint64_t *w, hipStream_t s);
+// the next mark value, for a kernel that stores its own mark (the fused
+// small allreduce's last workgroup, ompi_amd_allreduce_wait)
+uint64_t mark_reserve();
 
 inline bool mark_seen(const uint64_t *w, uint64_t v) {
     return w && v && __atomic_load_n(w, __ATOMIC_ACQUIRE) >= v;
@@ -93,6 +96,19 @@ hipError_t mark_stream_wait(hipStream_t s, I idle, bool host_reads = false) {
     e = hipEventRecord(ev, s);
     if (e != hipSuccess) return e;
     return poll_wait([ev](unsigned) { return hipEventQuery(ev); }, idle);
+}
+
+// A mark some kernel already on `s` stores itself: its value, or the
+// stream's own completion (hipStreamQuery every 64 polls: errors, and a
+// kernel that gave up before its mark).
+template <class I>
+hipError_t mark_value_wait(hipStream_t s, const uint64_t *w, uint64_t v, I idle) {
+    return poll_wait(
+        [s, w, v](unsigned spins) {
+            if (mark_seen(w, v)) return hipSuccess;
+            return spins % 64 == 63 ? hipStreamQuery(s) : hipErrorNotReady;
+        },
+        idle);
 }
 
 // An event and the mark (value v in w) enqueued right after it: whichever

@@ -55,9 +55,11 @@ void mark_word_put(uint64_t *w) {
     g_mark_free.push_back(w);
 }
 
+uint64_t mark_reserve() { return g_mark_seq.fetch_add(1) + 1; }
+
 uint64_t mark_launch(uint64_t *w, hipStream_t s) {
     if (!w) return 0;
-    const uint64_t v = g_mark_seq.fetch_add(1) + 1;
+    const uint64_t v = mark_reserve();
     hipLaunchKernelGGL(host_mark_kernel, dim3(1), dim3(64), 0, s, w, v);
     if (hipGetLastError() != hipSuccess) return 0;
     return v;

@@ -38,6 +38,7 @@ std::mutex g_mu;
 std::condition_variable g_cv;
 std::vector<ipc_ref *> g_live;     // open mappings
 std::vector<ipc_alloc> g_opening;  // opens in progress (g_mu released)
+std::vector<ipc_alloc> g_closing;  // retired mappings not closed yet (g_mu released)
 struct user {
     void *owner;
     int (*quiesce)(void *);
@@ -149,8 +150,11 @@ int ipc_map(const ipc_alloc &a, void *owner, ipc_ref **ref, void **base) {
                 }
             // another thread opens this allocation or one it collides with:
             // wait for that open to finish, then look again
+            // (or a retired mapping it collides with is still being closed:
+            // the runtime would answer the open with that mapping)
             bool busy = false;
             for (const ipc_alloc &o : g_opening) busy = busy || collide(o, a);
+            for (const ipc_alloc &o : g_closing) busy = busy || collide(o, a);
             if (!busy) break;
             g_cv.wait(g);
         }
@@ -171,6 +175,7 @@ int ipc_map(const ipc_alloc &a, void *owner, ipc_ref **ref, void **base) {
             }
         for (ipc_ref *r : stale) {  // nobody shares it from now on
             r->retired = true;
+            g_closing.push_back(r->a);
             ++r->refs;  // this retirement's own, until the close below
             ++g_st.retired;
             g_live.erase(std::find(g_live.begin(), g_live.end(), r));
@@ -205,6 +210,12 @@ int ipc_map(const ipc_alloc &a, void *owner, ipc_ref **ref, void **base) {
     for (ipc_ref *r : stale) {
         close_mapping(r);
         std::lock_guard<std::mutex> g(g_mu);
+        for (auto it = g_closing.begin(); it != g_closing.end(); ++it)
+            if (same_alloc(*it, r->a)) {
+                g_closing.erase(it);
+                break;
+            }
+        g_cv.notify_all();
         if (--r->refs == 0) delete r;  // else freed by its last holder's ipc_unmap
     }
     if (rc != OMPI_AMD_SUCCESS) {

@@ -535,7 +535,8 @@ struct win_blob {
     ipc_desc base;
     uint64_t bytes;
     int64_t disp_unit;
-    int64_t failed;  // this rank could not set up its side
+    int64_t failed;    // this rank could not set up its side
+    int64_t shadowed;  // this rank's window runs through a public copy (separate model)
 };
 
 }  // namespace ompi_amd
@@ -578,6 +579,18 @@ struct ompi_amd_win {
     void *shared_pin = nullptr;   // others: the pinned import of rank 0's allocation
     bool shared_owner = false;    // rank 0: frees shared_seg (arena or hipFree)
     bool shared_arena = false;
+    // MPI_Win_create over memory peers cannot map reliably (no IPC-safe
+    // size, or older than an IPC close of this process):
+    // the window runs in MPI's separate memory model — peers' RMA reaches a
+    // public copy in the exported arena (shadow), the owner's own loads and
+    // stores the private copy (base), and every synchronisation merges them
+    // against the state of the last one (snap).  separate: some rank of the
+    // window has a shadow (every rank then takes part in the fence's merge
+    // step and reports MPI_WIN_SEPARATE).
+    char *shadow = nullptr;
+    char *snap = nullptr;
+    bool owns_shadow = false;  // past the arena's limit: hipFree'd, not returned to the arena
+    bool separate = false;
 };
 
 namespace ompi_amd {
@@ -650,6 +663,72 @@ int xfer_copy(const void *src, void *dst, size_t bytes, hipStream_t s, const uin
                        dim3(kXferThreads), 0, s, static_cast<const char *>(src),
                        static_cast<char *>(dst), (int64_t)bytes, gate);
     return record_hip(hipGetLastError(), "xfer copy launch");
+}
+
+// p2p eager cells (p2p.cpp).  One workgroup: at most 4 KiB, 16-B granules
+// when both sides are 16-B aligned, else bytes.
+__device__ __forceinline__ void eager_bytes(const char *src, char *dst, int64_t bytes) {
+    if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+        const int64_t nv = bytes / 16;
+        for (int64_t i = threadIdx.x; i < nv; i += blockDim.x)
+            reinterpret_cast<u32x4 *>(dst)[i] = reinterpret_cast<const u32x4 *>(src)[i];
+        for (int64_t i = nv * 16 + threadIdx.x; i < bytes; i += blockDim.x) dst[i] = src[i];
+    } else {
+        for (int64_t i = threadIdx.x; i < bytes; i += blockDim.x) dst[i] = src[i];
+    }
+}
+
+// The sender's copy into its cell, then the cell's flag = v (system scope,
+// after a release): the message is posted before this kernel runs, and the
+// receiver's copy waits for the flag on the device instead of the sender
+// waiting for this kernel on the host.
+__global__ __launch_bounds__(256) void eager_put_kernel(const char *src, char *cell, int64_t bytes,
+                                                        uint64_t *flag, uint64_t v) {
+    eager_bytes(src, cell, bytes);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        osc_release();
+        __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// The receiver's copy out of the sender's cell once its flag is v (bounded:
+// past `ticks` the communicator's sticky error, nothing copied).
+__global__ __launch_bounds__(256) void eager_get_kernel(const char *cell, char *dst, int64_t bytes,
+                                                        const uint64_t *flag, uint64_t v, int *err,
+                                                        uint64_t ticks) {
+    __shared__ int ok;
+    if (threadIdx.x == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        ok = 1;
+        while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != v) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+                __hip_atomic_store(err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                ok = 0;
+                break;
+            }
+        }
+        osc_acquire();
+    }
+    __syncthreads();
+    if (!ok) return;
+    eager_bytes(cell, dst, bytes);
+    osc_epilogue();
+}
+
+int eager_put(const void *src, char *cell, size_t bytes, uint64_t *flag, uint64_t v, hipStream_t s) {
+    hipLaunchKernelGGL(eager_put_kernel, dim3(1), dim3(256), 0, s, static_cast<const char *>(src), cell,
+                       (int64_t)bytes, flag, v);
+    return record_hip(hipGetLastError(), "p2p eager copy launch");
+}
+
+int eager_get(const char *cell, void *dst, size_t bytes, const uint64_t *flag, uint64_t v, int *err,
+              uint64_t ticks, hipStream_t s) {
+    hipLaunchKernelGGL(eager_get_kernel, dim3(1), dim3(256), 0, s, cell, static_cast<char *>(dst),
+                       (int64_t)bytes, flag, v, err, ticks);
+    return record_hip(hipGetLastError(), "p2p eager receive launch");
 }
 
 static int launch_acc(ompi_amd_win_t *w, int op, int type, const void *origin, void *target,
@@ -837,10 +916,75 @@ static int ctl_give(ompi_amd_comm_t *c, int slot) {
     return rc;
 }
 
+// Three-way merge of a separate-model window (ompi_amd_win.shadow): byte b
+// changed in the private copy since the last merge (p != s) -> the public
+// copy takes it; else changed in the public copy (q != s) -> the private
+// copy takes it; the snapshot becomes the merged value.  MPI forbids a
+// local store and an RMA update of one location in the same epoch, so no
+// byte changes on both sides.  Only changed bytes are stored into the two
+// copies: an RMA of a passive epoch may still be updating other bytes of
+// the public copy during MPI_Win_sync, and a stale rewrite would undo it.
+// Words whose bytes all agree (the common case) cost three loads and no
+// store.  HBM-bound: 3 x bytes read per merge, plus the changed words.
+__global__ __launch_bounds__(kOscThreads) void win_merge_kernel(char *priv, char *pub, char *snap,
+                                                                int64_t bytes) {
+    if (threadIdx.x == 0) osc_acquire();  // the peers' released RMA into pub
+    __syncthreads();
+    const int64_t words = bytes / 4;
+    const int64_t gs = (int64_t)gridDim.x * blockDim.x;
+    uint32_t *p = reinterpret_cast<uint32_t *>(priv), *q = reinterpret_cast<uint32_t *>(pub),
+             *sn = reinterpret_cast<uint32_t *>(snap);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words + (bytes % 4); i += gs) {
+        if (i < words) {
+            const uint32_t pv = p[i], qv = q[i], sv = sn[i];
+            if (pv == sv && qv == sv) continue;
+            uint32_t mv = 0;
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t sh = 8u * (uint32_t)k;
+                const uint8_t pb = (uint8_t)(pv >> sh), qb = (uint8_t)(qv >> sh), sb = (uint8_t)(sv >> sh);
+                const uint8_t mb = pb != sb ? pb : qb;
+                mv |= (uint32_t)mb << sh;
+                if (pb != sb) reinterpret_cast<uint8_t *>(q + i)[k] = pb;
+                else if (qb != sb) reinterpret_cast<uint8_t *>(p + i)[k] = qb;
+            }
+            sn[i] = mv;
+        } else {  // the last bytes past the whole words
+            const int64_t b = words * 4 + (i - words);
+            const char pb = priv[b], qb = pub[b], sb = snap[b];
+            if (pb != sb) pub[b] = pb;
+            else if (qb != sb) priv[b] = qb;
+            snap[b] = pb != sb ? pb : qb;
+        }
+    }
+    osc_epilogue();  // the public copy's new bytes, to the peers
+}
+
+static void win_release_shadow(ompi_amd_win_t *w) {
+    if (w->snap) hip_ignore(hipFree(w->snap));
+    if (w->shadow) {
+        if (w->owns_shadow) hip_ignore(hipFree(w->shadow));
+        else comm_arena_free(w->c, w->shadow);
+    }
+    w->snap = w->shadow = nullptr;
+}
+
+// this rank's copies merged (a no-op for a window without a shadow here)
+static int win_merge(ompi_amd_win_t *w, hipStream_t s) {
+    if (!w->shadow || !w->bytes) return OMPI_AMD_SUCCESS;
+    const int64_t units = (int64_t)(w->bytes / 4) + (int64_t)(w->bytes % 4);
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((units + kOscThreads - 1) / kOscThreads,
+                                                                  osc_grid_cap()));
+    hipLaunchKernelGGL(win_merge_kernel, dim3((unsigned)blocks), dim3(kOscThreads), 0, s, w->base, w->shadow,
+                       w->snap, (int64_t)w->bytes);
+    return record_hip(hipGetLastError(), "osc window merge launch");
+}
+
 // shared: every rank's base as this process maps it (MPI_Win_allocate_shared),
 // so nothing is exported or imported for the bases.
+// user: the caller's memory (MPI_Win_create), shadowed when peers cannot
+// map it reliably.
 static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit, bool owns,
-                     ompi_amd_win_t **out, char *const *shared = nullptr) {
+                     ompi_amd_win_t **out, char *const *shared = nullptr, bool user = false) {
     auto *w = new (std::nothrow) ompi_amd_win;
     if (!w) return OMPI_AMD_ERR_BAD_PARAM;
     w->c = c;
@@ -855,7 +999,28 @@ static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit
     win_blob mine{}, all[kOscMaxRanks];
     mine.bytes = bytes;
     mine.disp_unit = disp_unit;
-    if (rc == OMPI_AMD_SUCCESS && bytes && !shared) rc = comm_export(c, base, &mine.base);
+    // the caller's memory (MPI_Win_create) that peers could not map
+    // reliably: a public copy in the exported arena, the separate model
+    if (rc == OMPI_AMD_SUCCESS && bytes && user && comm_win_needs_shadow(c, base)) {
+        void *pub = nullptr;
+        rc = comm_arena_alloc(c, bytes, &pub);
+        if (rc == OMPI_AMD_ERR_UNSUPPORTED) {  // past the arena's limit: an allocation of its own
+            ipc_desc d;
+            rc = comm_alloc_exportable(bytes, false, &pub, &d);
+            w->owns_shadow = rc == OMPI_AMD_SUCCESS;
+        }
+        if (rc == OMPI_AMD_SUCCESS) {
+            w->shadow = static_cast<char *>(pub);
+            rc = record_hip(hipMalloc((void **)&w->snap, bytes), "hipMalloc (window snapshot)");
+        }
+        if (rc == OMPI_AMD_SUCCESS)
+            rc = record_hip(hipMemcpy(w->shadow, base, bytes, hipMemcpyDeviceToDevice), "window public copy");
+        if (rc == OMPI_AMD_SUCCESS)
+            rc = record_hip(hipMemcpy(w->snap, base, bytes, hipMemcpyDeviceToDevice), "window snapshot");
+        mine.shadowed = 1;
+    }
+    if (rc == OMPI_AMD_SUCCESS && bytes && !shared)
+        rc = comm_export(c, w->shadow ? w->shadow : static_cast<char *>(base), &mine.base);
     // every rank takes part in the rendezvous, whatever failed locally
     mine.failed = rc == OMPI_AMD_SUCCESS ? 0 : 1;
     const int arc = comm_allgather(c, &mine, all, sizeof(win_blob));
@@ -868,8 +1033,9 @@ static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit
         }
         w->peer_bytes[p] = all[p].bytes;
         w->peer_disp[p] = all[p].disp_unit;
+        w->separate = w->separate || all[p].shadowed != 0;
         if (p == w->rank) {
-            w->peer_base[p] = w->base;
+            w->peer_base[p] = w->shadow ? w->shadow : w->base;  // RMA reaches the public copy
             w->peer_ctl[p] = w->ctl;
             continue;
         }
@@ -891,6 +1057,7 @@ static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit
         for (int p = 0; p < w->size; ++p)
             if (w->pinned[p]) comm_unpin(c, w->pinned[p]);
         (void)ctl_give(c, w->ctl_slot);  // nobody used it: every rank failed here together
+        win_release_shadow(w);
         delete w;
         return rc;
     }
@@ -911,7 +1078,7 @@ int ompi_amd_win_create(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_u
     }
     int rc = record_hip(hipSetDevice(comm_device(c)), "hipSetDevice");
     if (rc != OMPI_AMD_SUCCESS) return rc;
-    return win_setup(c, bytes ? base : nullptr, bytes, disp_unit, false, out);
+    return win_setup(c, bytes ? base : nullptr, bytes, disp_unit, false, out, nullptr, true);
 }
 
 int ompi_amd_win_allocate(ompi_amd_comm_t *c, size_t bytes, int disp_unit, void **base,
@@ -987,6 +1154,7 @@ int ompi_amd_win_free(ompi_amd_win_t *w) {
     if (w->query) hip_ignore(hipStreamDestroy(w->query));
     if (w->owns_base && w->base) hip_ignore(hipFree(w->base));
     if (w->arena_base && w->base) comm_arena_free(c, w->base);  // nobody maps it per window
+    win_release_shadow(w);  // no peer maps the public copy any more
     if (rc == OMPI_AMD_SUCCESS) rc = comm_sticky(c);
     delete w;
     return rc;
@@ -995,7 +1163,24 @@ int ompi_amd_win_free(ompi_amd_win_t *w) {
 int ompi_amd_win_fence(ompi_amd_win_t *w, int assert_, void *stream) {
     if (!w) return OMPI_AMD_ERR_BAD_PARAM;
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
-    return comm_barrier(w->c, win_stream(w, stream));
+    const hipStream_t s = win_stream(w, stream);
+    OSC_TRY(comm_barrier(w->c, s));
+    if (!w->separate) return OMPI_AMD_SUCCESS;
+    // separate model: every epoch's RMA into the public copies is done;
+    // merge them with the private copies, and let no peer start the next
+    // epoch before every rank merged (a second device barrier)
+    OSC_TRY(win_merge(w, s));
+    return comm_barrier(w->c, s);
+}
+
+int ompi_amd_win_sync(ompi_amd_win_t *w, void *stream) {
+    if (!w) return OMPI_AMD_ERR_BAD_PARAM;
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    return win_merge(w, win_stream(w, stream));
+}
+
+int ompi_amd_win_model(const ompi_amd_win_t *w) {
+    return !w ? OMPI_AMD_ERR_BAD_PARAM : w->separate ? OMPI_AMD_WIN_SEPARATE : OMPI_AMD_WIN_UNIFIED;
 }
 
 int ompi_amd_win_lock(ompi_amd_win_t *w, int lock_type, int target, int assert_, void *stream) {
@@ -1007,13 +1192,15 @@ int ompi_amd_win_lock(ompi_amd_win_t *w, int lock_type, int target, int assert_,
         return OMPI_AMD_ERR_BAD_PARAM;  // MPI_ERR_RMA_SYNC (osc_sm_passive_target.c:122-124)
     }
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    const bool excl = lock_type == OMPI_AMD_LOCK_EXCLUSIVE;
     if (assert_ & OMPI_AMD_MODE_NOCHECK) {
         w->held[target] = HELD_NOCHECK;
-        return OMPI_AMD_SUCCESS;
+    } else {
+        OSC_TRY(launch_lock(w, target, excl ? 2 : 4, win_stream(w, stream)));
+        w->held[target] = excl ? HELD_EXCLUSIVE : HELD_SHARED;
     }
-    const bool excl = lock_type == OMPI_AMD_LOCK_EXCLUSIVE;
-    OSC_TRY(launch_lock(w, target, excl ? 2 : 4, win_stream(w, stream)));
-    w->held[target] = excl ? HELD_EXCLUSIVE : HELD_SHARED;
+    // separate model: a lock of one's own window synchronises its copies
+    if (target == w->rank) OSC_TRY(win_merge(w, win_stream(w, stream)));
     return OMPI_AMD_SUCCESS;
 }
 
@@ -1025,7 +1212,8 @@ int ompi_amd_win_unlock(ompi_amd_win_t *w, int target, void *stream) {
         return OMPI_AMD_ERR_BAD_PARAM;
     }
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
-    int rc = OMPI_AMD_SUCCESS;
+    int rc = target == w->rank ? win_merge(w, win_stream(w, stream)) : OMPI_AMD_SUCCESS;
+    if (rc != OMPI_AMD_SUCCESS) return rc;
     if (h == HELD_EXCLUSIVE) rc = launch_lock(w, target, 3, win_stream(w, stream));
     else if (h == HELD_SHARED) rc = launch_lock(w, target, 5, win_stream(w, stream));
     w->held[target] = HELD_NONE;
@@ -1465,6 +1653,7 @@ int ompi_amd_win_post(ompi_amd_win_t *w, const int *ranks, int n, int assert_, v
     // MPI_MODE_NOCHECK: the origins start without waiting for this post
     // (osc_sm_active_target.c:239); the window is still released
     if (assert_ & OMPI_AMD_MODE_NOCHECK) g.n = 0;
+    OSC_TRY(win_merge(w, win_stream(w, stream)));  // separate model: the exposed copy up to date
     OSC_TRY(pscw_launch(w, 0, g, win_stream(w, stream)));
     w->posted = true;
     w->complete_want += (uint32_t)n;  // every origin of the group completes once
@@ -1517,6 +1706,7 @@ int ompi_amd_win_wait(ompi_amd_win_t *w, void *stream) {
     g.want[0] = w->complete_want;
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
     OSC_TRY(pscw_launch(w, 3, g, win_stream(w, stream)));
+    OSC_TRY(win_merge(w, win_stream(w, stream)));  // separate model: the origins' RMA, private too
     w->posted = false;
     return OMPI_AMD_SUCCESS;
 }
@@ -1544,6 +1734,7 @@ int ompi_amd_win_test(ompi_amd_win_t *w, int *flag) {
         pscw_group g{};
         g.want[0] = w->complete_want;
         OSC_TRY(pscw_launch(w, 3, g, win_stream(w, nullptr)));
+        OSC_TRY(win_merge(w, win_stream(w, nullptr)));
         *flag = 1;
         w->posted = false;
     }

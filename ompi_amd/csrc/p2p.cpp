@@ -25,11 +25,17 @@
 //            completed; the send completes when it sees DONE.
 //   eager    messages of at most kEager bytes (btl/smcuda's 4 KiB eager
 //            limit, btl_smcuda_component.c:197) are first copied into the
-//            sender's device eager area (one kEager cell per ring slot, the
-//            area exported once) and the send completes at once, as ob1's
-//            eager protocol does: MPI_Send of a small message never waits
-//            for the receiver.  The cell is reused only after the slot is
-//            DONE.
+//            sender's device eager area (one cell per ring slot, the area
+//            exported once), as ob1's eager protocol does: MPI_Send of a
+//            small message never waits for the receiver.  From a device
+//            buffer the copy kernel itself publishes the cell (a flag word
+//            after the data = sequence + 1) and the message is posted as
+//            soon as the kernel is launched: the receiver's copy kernel waits
+//            for the flag on the device, so the sender's copy and the
+//            receiver's match and launch overlap instead of the sender
+//            synchronising its stream first; the send
+//            completes when its copy kernel has run.  The cell is reused
+//            only after the slot is DONE.
 //   staged   larger messages are copied into a library-owned send stage
 //            (a pool of exported device buffers, never freed while the
 //            communicator lives) and the receiver pulls from there, so no
@@ -80,6 +86,7 @@ namespace ompi_amd {
 
 constexpr int kSlots = 64;
 constexpr size_t kEager = 4096;
+constexpr size_t kCell = kEager + 64;  // the data, then the cell's flag word (its own line)
 constexpr size_t kInline = 1024;  // host payload carried in the slot itself
 constexpr size_t kHostStage = 8u << 20;  // per rank, its own segment (created at first use)
 constexpr size_t kHostMax = 2u << 20;    // largest message through it
@@ -93,7 +100,8 @@ struct alignas(64) msg_slot {
     uint64_t bytes;
     uint64_t raw;  // the send buffer's address (messages to self)
     ipc_desc d;    // the send buffer for peers
-    uint32_t inl;  // 1: payload in `inline_data`; 2: in the sender's host stage at offset `raw`
+    uint32_t inl;  // 1: payload in `inline_data`; 2: in the sender's host stage at offset `raw`;
+                   // 3: in an eager cell whose flag (cell + kEager) becomes seq + 1
     char inline_data[kInline];
 };
 
@@ -132,7 +140,7 @@ struct p2p_state {
     std::vector<uint64_t> scan_from;  // per source: first sequence possibly still POSTED
     std::deque<ompi_amd_p2p_request *> recvs;  // posted receives not matched yet
     std::recursive_mutex mu;
-    char *eager = nullptr;  // [size][kSlots] cells of kEager bytes, allocated at first use
+    char *eager = nullptr;  // [size][kSlots] cells of kCell bytes (zeroed), allocated at first use
     // this rank's host stage ring (bytes [htail, hhead) in flight, monotonic
     // counters) and the messages holding it, oldest first
     uint64_t hhead = 0, htail = 0;
@@ -487,7 +495,7 @@ static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s
     r->st.error = r->rc;
     if (n == 0) return;
     int rc = OMPI_AMD_SUCCESS;
-    if (m->inl) {  // a host send out of the slot or the sender's host stage (host: done now)
+    if (m->inl == 1 || m->inl == 2) {  // a host send out of the slot or the sender's host stage (host: done now)
         const char *ring = m->inl == 2 ? p->host_stage(s) : nullptr;
         if (m->inl == 2 && !ring) {
             r->rc = r->st.error = OMPI_AMD_ERR_BOOTSTRAP;
@@ -520,7 +528,16 @@ static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s
             rc = record_hip(hipErrorOutOfMemory, "p2p receive stage");
         }
     }
-    if (rc == OMPI_AMD_SUCCESS) rc = xfer_copy(src, dst, n, r->stream);
+    if (rc == OMPI_AMD_SUCCESS) {
+        if (m->inl == 3) {  // an eager cell: the copy waits for the sender's kernel to publish it
+            const int64_t ms = comm_timeout_ms(p->c);
+            const uint64_t ticks = ms > 0 ? (uint64_t)ms * 100000ull : (1ull << 62);  // 100 MHz
+            rc = eager_get(src, dst, n, reinterpret_cast<const uint64_t *>(src + kEager), m->seq + 1,
+                           comm_err_dev(p->c), ticks, r->stream);
+        } else {
+            rc = xfer_copy(src, dst, n, r->stream);
+        }
+    }
     if (rc == OMPI_AMD_SUCCESS && r->host_dst)
         rc = record_hip(hipMemcpyAsync(r->host_dst, dst, n, hipMemcpyDeviceToHost, r->stream),
                         "hipMemcpyAsync (p2p receive to host)");
@@ -553,7 +570,13 @@ static int test_one(ompi_amd_p2p_request *r, bool *done) {
         return r->rc;
     }
     *done = false;
-    if (r->is_send) {
+    if (r->is_send && r->ev) {  // a device eager send: complete once its copy into the cell ran
+        const hipError_t e = hipEventQuery(r->ev);
+        if (e != hipErrorNotReady) {
+            if (e != hipSuccess) r->rc = record_hip(e, "p2p eager copy");
+            r->done = true;
+        }
+    } else if (r->is_send) {
         msg_slot &m = p->pair(p->rank, r->peer).slot[r->seq % kSlots];
         if (m.seq != r->seq || m.state.load(std::memory_order_acquire) == S_DONE) r->done = true;
     } else if (r->matched) {
@@ -572,6 +595,12 @@ static int test_one(ompi_amd_p2p_request *r, bool *done) {
             if (r->has_rstage) {
                 p->recv_free.push_back(r->rstage);
                 r->has_rstage = false;
+            }
+            // an eager receive whose wait for the sender's flag timed out
+            // copied nothing: the communicator's error says so
+            if (r->slot->inl == 3 && r->rc == OMPI_AMD_SUCCESS) {
+                const int se = comm_sticky(p->c);
+                if (se != OMPI_AMD_SUCCESS) r->rc = r->st.error = se;
             }
             r->slot->state.store(S_DONE, std::memory_order_release);  // the FIN
             r->done = true;
@@ -669,7 +698,13 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     std::unique_lock<std::recursive_mutex> alloc_guard(p->mu);
     if (rc == OMPI_AMD_SUCCESS && eager && !inl && !p->eager) {  // peers read its cells: exportable
         ipc_desc d{};
-        rc = comm_alloc_exportable((size_t)p->size * kSlots * kEager, false, (void **)&p->eager, &d);
+        const size_t area = (size_t)p->size * kSlots * kCell;
+        rc = comm_alloc_exportable(area, false, (void **)&p->eager, &d);
+        if (rc == OMPI_AMD_SUCCESS) {  // every flag 0: no sequence + 1 yet
+            rc = record_hip(hipMemset(p->eager, 0, area), "hipMemset (p2p eager area)");
+            if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipDeviceSynchronize(), "hipDeviceSynchronize (eager area)");
+            if (rc != OMPI_AMD_SUCCESS) hip_ignore(hipFree(p->eager));
+        }
         if (rc != OMPI_AMD_SUCCESS) p->eager = nullptr;
     }
     alloc_guard.unlock();
@@ -759,6 +794,7 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     };
     uint64_t hoff = 0, hend = 0;
     const bool hstaged = hostable && take_host(p, bytes, &hoff, &hend);
+    bool flagged = false;  // a device eager send: the copy kernel publishes the cell
     if (inl) {  // into the slot itself; the send completes now
         memcpy(m.inline_data, buf, bytes);
     } else if (hstaged) {  // into this rank's host stage; the send completes now
@@ -766,9 +802,16 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
         p->hflight.push_back({dst, seq, hend});
         p->hhead = hend;
         ++p->host_stage_sends;
-    } else if (eager && bytes) {  // stage into this slot's cell; the send completes now
-        char *cell = p->eager + ((size_t)dst * kSlots + seq % kSlots) * kEager;
-        rc = copy_in(cell);
+    } else if (eager && bytes) {  // stage into this slot's cell
+        char *cell = p->eager + ((size_t)dst * kSlots + seq % kSlots) * kCell;
+        if (host) {  // a host buffer past the host ring: copied in now
+            rc = copy_in(cell);
+        } else {  // posted at once; the receiver's copy waits for the flag
+            rc = eager_put(buf, cell, bytes, reinterpret_cast<uint64_t *>(cell + kEager), seq + 1, s);
+            r->stream = s;
+            if (rc == OMPI_AMD_SUCCESS) rc = record_copy(p, r);
+            flagged = true;
+        }
         src = cell;
     } else if (bytes && (host || (dst != p->rank && !p->user_ipc))) {
         rc = stage_send(host);
@@ -793,6 +836,7 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
         rc = producers_done();  // a receive of this process copies from the buffer
     }
     if (rc != OMPI_AMD_SUCCESS) {
+        if (r->ev) p->ev_free.push_back(r->ev);
         delete r;
         return rc;
     }
@@ -801,12 +845,13 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     m.bytes = bytes;
     m.raw = hstaged ? hoff : reinterpret_cast<uint64_t>(src);
     m.d = d;
-    m.inl = inl ? 1u : hstaged ? 2u : 0u;
+    m.inl = inl ? 1u : hstaged ? 2u : flagged ? 3u : 0u;
     m.state.store(S_POSTED, std::memory_order_release);
     q.posted.store(seq + 1, std::memory_order_release);
     r->seq = seq;
     // the user's buffer is free again once staged (Ssend: at the FIN)
-    r->done = eager || hstaged || (staged && mode != OMPI_AMD_SEND_SYNCHRONOUS);
+    // (a device eager send: once its copy kernel ran, test_one)
+    r->done = (eager && !flagged) || hstaged || (staged && mode != OMPI_AMD_SEND_SYNCHRONOUS);
     *out = r;
     return OMPI_AMD_SUCCESS;
 }

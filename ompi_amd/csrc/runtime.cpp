@@ -2,6 +2,10 @@
 #include "host_mark.h"
 #include "runtime.h"
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -46,6 +50,26 @@ __attribute__((constructor)) static void ipc_mode_default() {
 }
 
 int ipc_mode_env_at_load() { return g_ipc_env_at_load; }
+
+// OMPI_AMD_BACKTRACE=1 (diagnostics): a host SIGSEGV / SIGBUS prints the
+// raw call stack (library offsets, for addr2line on the same .so) to stderr
+// before the default action.
+static void crash_trace(int sig) {
+    void *pc[64];
+    const int n = backtrace(pc, 64);
+    static const char head[] = "[ompi_amd] fatal signal, call stack:\n";
+    (void)!write(2, head, sizeof(head) - 1);
+    backtrace_symbols_fd(pc, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+
+__attribute__((constructor)) static void crash_trace_init() {
+    const char *v = getenv("OMPI_AMD_BACKTRACE");
+    if (!v || atoi(v) == 0) return;
+    signal(SIGSEGV, crash_trace);
+    signal(SIGBUS, crash_trace);
+}
 
 const char *ipc_mode_env_now() {
     const char *v = getenv("HSA_ENABLE_IPC_MODE_LEGACY");

@@ -653,9 +653,11 @@ int mca_coll_rocm_allreduce(const void *sbuf, void *rbuf, int count,
                                       m->c_coll.coll_allreduce_module);
         return rocm_unstage(m, o, 2, rc);
     }
-    rc = ompi_amd_allreduce(m->dev_comm, inplace ? o[1].use : o[0].use, o[1].use, (size_t) count,
-                            type_code(dtype), op->o_f_to_c_index, NULL);
-    return rocm_dev_finish(m, o, 2, rc);
+    /* the call and its wait in one: a fused small allreduce stores its own
+     * completion mark, so the wait launches nothing behind it */
+    rc = ompi_amd_allreduce_wait(m->dev_comm, inplace ? o[1].use : o[0].use, o[1].use, (size_t) count,
+                                 type_code(dtype), op->o_f_to_c_index);
+    return rocm_unstage(m, o, 2, to_ompi_err(rc));
 }
 
 /* MPI_Reduce: rbuf is significant at the root only (MPI-3.1 §5.9.1), so

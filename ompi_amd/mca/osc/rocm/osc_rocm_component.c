@@ -336,7 +336,13 @@ static int rocm_flush(int target, struct ompi_win_t *win)
 
 static int rocm_flush_all(struct ompi_win_t *win) { return rocm_flush(0, win); }
 
-static int rocm_sync(struct ompi_win_t *win) { return complete(mod(win), OMPI_AMD_SUCCESS); }
+/* MPI_Win_sync: the window's copies merged when it runs in the separate
+ * model (ompi_amd_win_model), else only the caller's work completed */
+static int rocm_sync(struct ompi_win_t *win)
+{
+    ompi_osc_rocm_module_t *m = mod(win);
+    return complete(m, ompi_amd_win_sync(m->dev_win, NULL));
+}
 
 static int rocm_free(struct ompi_win_t *win)
 {
@@ -740,6 +746,9 @@ static int rocm_select(struct ompi_win_t *win, void **base, size_t size, int dis
         return to_ompi_err(rc);
     }
     win->w_osc_module = &m->super;
-    *model = MPI_WIN_UNIFIED;
+    /* MPI_WIN_SEPARATE when some rank's MPI_Win_create memory is reached
+     * through a public copy (include/ompi_amd_osc.h); every rank agrees */
+    *model = OMPI_AMD_WIN_SEPARATE == ompi_amd_win_model(m->dev_win) ? MPI_WIN_SEPARATE
+                                                                      : MPI_WIN_UNIFIED;
     return OMPI_SUCCESS;
 }

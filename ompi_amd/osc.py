@@ -34,6 +34,8 @@ from .op import Datatype, Op
 LOCK_EXCLUSIVE = 1   # MPI_LOCK_EXCLUSIVE (mpi.h.in:548)
 LOCK_SHARED = 2      # MPI_LOCK_SHARED (mpi.h.in:549)
 MODE_NOCHECK = 1     # MPI_MODE_NOCHECK (mpi.h.in:542)
+WIN_UNIFIED = 0      # MPI_WIN_UNIFIED (mpi.h.in:556)
+WIN_SEPARATE = 1     # MPI_WIN_SEPARATE (mpi.h.in:557)
 
 
 class RmaRequest:
@@ -140,6 +142,19 @@ class Window:
     def unlock_all(self, stream=None, blocking: bool = True) -> None:
         self._done(self._lib.ompi_amd_win_unlock_all(self._h, _stream(stream)), "win_unlock_all",
                    blocking, stream)
+
+    @property
+    def model(self) -> int:
+        """MPI_WIN_MODEL: WIN_SEPARATE when some rank's MPI_Win_create
+        memory is reached through a public copy (include/ompi_amd_osc.h)."""
+        m = self._lib.ompi_amd_win_model(self._h)
+        if m < 0:
+            _lib.check(m, "win_model")
+        return m
+
+    def sync(self, stream=None) -> None:
+        """MPI_Win_sync: the public and private copies merged."""
+        _lib.check(self._lib.ompi_amd_win_sync(self._h, _stream(stream)), "win_sync")
 
     def flush(self, target: int, stream=None) -> None:
         _lib.check(self._lib.ompi_amd_win_flush(self._h, target, _stream(stream)), "win_flush")

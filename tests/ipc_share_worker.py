@@ -11,11 +11,15 @@ IPC registry (ompi_amd/csrc/ipc_registry.h) must hand both the same mapping
      its references must not unmap B's);
   3. a new window on A over X, then B is destroyed: the window's put / get
      stay byte-exact;
-  4. a peer's freed + reallocated buffer mapped again: the registry retires
-     the stale mapping once (ipc_retired) and the result is exact;
+  4. a freed + reallocated buffer at the address it had: the exporter does
+     not export it again (reused_exports; ROCm 7.2 may refuse the peers'
+     re-import right after they retire the old mapping) and
+     the call runs through the shadow, exact;
   5. A's nonblocking allreduce launched on rank 0 only, while B's blocking
-     allreduce retires stale mappings there: B completes at once (only the
-     stale mappings' holders are quiesced) and both results are exact.
+     allreduce retires stale mappings there (B exports reused addresses:
+     param reuse_shadow = 0, to drive the registry's retire path): B
+     completes at once (only the stale mappings' holders are quiesced) and
+     both results are exact.
 
 Prints one JSON line per step; exits 0 only if all passed.
 """
@@ -131,14 +135,20 @@ def main():
         win.free()
         torch.cuda.synchronize()
         retired0 = B.get_param("ipc_retired")
+        reused0 = B.get_param("reused_exports")
+        old_ptr = X.data_ptr()
         del X
         torch.cuda.empty_cache()
         dist.barrier()
         X = torch.zeros(count + 64, device="cuda")
+        same = X.data_ptr() == old_ptr
         ok2, msg2 = allreduce_check(X, 12)
         retired = B.get_param("ipc_retired") - retired0
-        report("realloc_retires_once", ok and ok2, "; ".join(m for m in (msg, msg2) if m),
-               ipc_retired=retired)
+        reused = B.get_param("reused_exports") - reused0
+        report("realloc_same_address_shadowed", ok and ok2 and (reused >= 1 or not same),
+               "; ".join(m for m in (msg, msg2, "" if reused >= 1 or not same else
+                                     "a reused address was exported again") if m),
+               same_address=same, reused_exports=reused, ipc_retired=retired)
         # 5. a deferred call of A launched on rank 0 but not yet on its peers
         # while B's blocking call on rank 0 retires a stale mapping (ADVICE
         # r3): the registry quiesces only the stale mapping's holders (B),
@@ -167,6 +177,7 @@ def main():
 
         A.set_param("user_ipc", 1)
         A.set_param("algorithm", 0)
+        B.set_param("reuse_shadow", 0)
         y = torch.zeros(count, device="cuda")
         xs = [data(r, count, 15) for r in range(n)]
         p1 = raw(xs[rank])

@@ -12,6 +12,7 @@
 #define MPI_WIN_FLAVOR_DYNAMIC 3
 #define MPI_WIN_FLAVOR_SHARED 4
 #define MPI_WIN_UNIFIED 0
+#define MPI_WIN_SEPARATE 1
 #define MPI_PROC_NULL (-2)
 #define MPI_ERR_WIN 53
 #define MPI_ERR_RMA_ATTACH 69

@@ -139,16 +139,28 @@ typedef struct sreq {
 
 static sreq *g_pending;
 
+/* Receives match in posting order per source: once one pending receive of
+ * a source finds nothing, the later ones of that source wait too (the
+ * message at the head may be the earlier receive's, still being posted) —
+ * so a head whose tag differs from the first pending receive's is an order
+ * error. */
 static int s_progress(void)
 {
     int n = 0;
+    unsigned long long blocked = 0;  /* sources (< 64) with an unmatched earlier receive */
     for (sreq **pp = &g_pending; *pp;) {
         sreq *q = *pp;
+        const unsigned long long bit = 1ull << (q->peer & 63);
+        if (blocked & bit) {
+            pp = &q->next;
+            continue;
+        }
         if (harness_pml_saved_try_recv(q->buf, q->count, q->d, q->peer, q->tag, &q->super.req_status)) {
             *pp = q->next;
             ompi_request_complete(&q->super, true);
             ++n;
         } else {
+            blocked |= bit;
             pp = &q->next;
         }
     }

@@ -600,6 +600,7 @@ def case_put_get_ddt(comm, rank, n, salt):
                 r1.free()
                 win.unlock_all(stream=STREAM)
                 comm_barrier()
+                win.sync(stream=STREAM)  # MPI_Win_sync: the separate model's private copy
             else:
                 win.fence(stream=STREAM)
                 win.put_ddt(o, ocount, odt, nxt, disp, tcount, tdt, stream=STREAM)
@@ -642,6 +643,79 @@ def case_put_get_ddt(comm, rank, n, salt):
     finally:
         win.free()
     return True, ""
+
+
+def case_separate_window(comm, rank, n, salt, nbytes=100003, force=False):
+    """MPI_Win_create over memory peers cannot map reliably (a torch tensor
+    of a small-pool 2 MiB segment: not an IPC-safe size) runs
+    in the separate model (include/ompi_amd_osc.h): MPI_WIN_MODEL is
+    SEPARATE on every rank; a fence brings the peers' puts into the caller's
+    memory and the caller's own stores to the peers; passive-target puts
+    reach it at MPI_Win_sync and at a lock of its own window.  force: the
+    osc_win_shadow hook on a 64 MiB + 12 B tensor (IPC-safe segment)."""
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    if force:
+        comm.set_param("osc_win_shadow", 1)
+    w0 = comm.get_param("osc_shadow_windows")
+    try:
+        base = dev(payload(rank, salt, nbytes))
+        win = osc.Window.create(comm, base, nbytes)
+    finally:
+        if force:
+            comm.set_param("osc_win_shadow", 0)
+    try:
+        if win.model != osc.WIN_SEPARATE or comm.get_param("osc_shadow_windows") != w0 + 1:
+            return False, f"model {win.model}, shadow windows {comm.get_param('osc_shadow_windows') - w0}"
+        half = nbytes // 2
+        # 1. fence epoch: put into the next rank's first half
+        src = dev(payload(rank, salt + 1, half))
+        win.fence(stream=STREAM)
+        win.put(src, nxt, 0, half, stream=STREAM)
+        win.fence(stream=STREAM, blocking=True)
+        exp = payload(rank, salt, nbytes).copy()
+        exp[:half] = payload(prv, salt + 1, half)
+        ok, msg = eq(host(base), exp, "fence: peer's put in the private copy")
+        if not ok:
+            return ok, msg
+        # 2. my own stores between fences reach the peers' gets
+        mine = payload(rank, salt + 2, nbytes - half)
+        with torch.cuda.stream(STREAM):
+            base[half:].copy_(torch.from_numpy(mine.copy()).to("cuda", non_blocking=False))
+        STREAM.synchronize()
+        win.fence(stream=STREAM)
+        back = zeros(nbytes - half)
+        win.get(back, prv, half, stream=STREAM)
+        win.fence(stream=STREAM, blocking=True)
+        ok, msg = eq(host(back), payload(prv, salt + 2, nbytes - half), "fence: peer's local stores in the public copy")
+        if not ok:
+            return ok, msg
+        # 3. passive target: a put under lock_all, seen after MPI_Win_sync
+        tail = dev(payload(rank, salt + 3, 4099))
+        win.lock_all(stream=STREAM)
+        win.put(tail, nxt, 7, 4099, stream=STREAM)
+        win.unlock_all(stream=STREAM, blocking=True)
+        comm_barrier()
+        win.sync(stream=STREAM)
+        exp[half:] = payload(rank, salt + 2, nbytes - half)
+        exp[7:7 + 4099] = payload(prv, salt + 3, 4099)
+        ok, msg = eq(host(base), exp, "win_sync: passive put in the private copy")
+        if not ok:
+            return ok, msg
+        comm_barrier()
+        # 4. a lock of my own window synchronises too
+        tail2 = dev(payload(rank, salt + 4, 999))
+        win.lock(nxt, osc.LOCK_EXCLUSIVE, stream=STREAM)
+        win.put(tail2, nxt, nbytes - 999, 999, stream=STREAM)
+        win.unlock(nxt, stream=STREAM, blocking=True)
+        comm_barrier()
+        win.lock(rank, osc.LOCK_SHARED, stream=STREAM)
+        win.unlock(rank, stream=STREAM, blocking=True)
+        exp[nbytes - 999:] = payload(prv, salt + 4, 999)
+        ok, msg = eq(host(base), exp, "lock of the own window: passive put in the private copy")
+        comm_barrier()
+        return ok, msg
+    finally:
+        win.free()
 
 
 def case_fetch_and_op_counter(comm, rank, n, k=25):
@@ -874,6 +948,7 @@ def case_request_rma(comm, rank, n, salt, count=65537):
             r.free()
         win.unlock_all(stream=STREAM)
         comm_barrier()
+        win.sync(stream=STREAM)  # MPI_Win_sync: the separate model's private copy
         mine = host(base).view(np.float32)
         ok, msg = eq(mine[:count], src[prv], "rput")
         if not ok:
@@ -1022,6 +1097,9 @@ def main():
         ("osc_get_accumulate", lambda: case_get_accumulate(comm, rank, n, 92)),
         ("osc_accumulate_derived_datatypes", lambda: case_acc_ddt(comm, rank, n, 150)),
         ("osc_put_get_derived_datatypes", lambda: case_put_get_ddt(comm, rank, n, 160)),
+        ("osc_separate_model_small_tensor", lambda: case_separate_window(comm, rank, n, 170)),
+        ("osc_separate_model_forced_64MiB",
+         lambda: case_separate_window(comm, rank, n, 171, nbytes=(64 << 20) + 12, force=True)),
         ("osc_fetch_and_op_counter", lambda: case_fetch_and_op_counter(comm, rank, n)),
         ("osc_compare_and_swap", lambda: case_cas(comm, rank, n)),
         ("osc_passive_exclusive_rmw", lambda: case_passive_exclusive(comm, rank, n)),

@@ -39,13 +39,14 @@ __device__ __forceinline__ void release_sys() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// round 5: the library keeps a single-element type's element in registers
+// (osc_ipc.hip ddt_acc_kernel); this loop does the same
 template <int THREADS, int UNROLL>
 __global__ __launch_bounds__(THREADS) void k_acc(ddt_desc d, char *typed, const double *in, int64_t n) {
-    __shared__ ddt_elem lds[kDdtLdsElems];
-    for (int i = threadIdx.x; i < d.nelem; i += THREADS) lds[i] = d.elems[i];
     if (threadIdx.x == 0) acquire_sys();
+    const ddt_elem e0 = d.elems[0];
     __syncthreads();
-    const ddt_elem *el = lds;
+    const ddt_elem *el = &e0;
     const int64_t chunk = (int64_t)THREADS * UNROLL;
     const int64_t gs = (int64_t)gridDim.x * chunk;
     for (int64_t b = (int64_t)blockIdx.x * chunk + threadIdx.x; b < n; b += gs) {
@@ -57,7 +58,7 @@ __global__ __launch_bounds__(THREADS) void k_acc(ddt_desc d, char *typed, const 
             t[u] = nullptr;
             if (k < n) {
                 t[u] = reinterpret_cast<double *>(
-                    typed + typed_offset_fast<8>(el, d.nelem, (uint32_t)(d.size / 8), d.sdiv, d.extent,
+                    typed + typed_offset_fast<8>(el, 1, (uint32_t)(d.size / 8), d.sdiv, d.extent,
                                                  (uint32_t)k));
                 v[u] = *t[u];
                 x[u] = in[k];
