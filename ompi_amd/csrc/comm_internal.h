@@ -75,10 +75,13 @@ int comm_copy(ompi_amd_comm_t *c, const void *src, void *dst, size_t bytes, hipS
 // p2p eager cells (osc_ipc.hip, one workgroup, bytes <= 4 KiB): eager_put
 // copies src into the cell, then stores v into *flag (system scope, after a
 // release); eager_get waits (bounded by ticks of s_memrealtime: err set,
-// nothing copied) until *flag == v, then copies the cell out.
-int eager_put(const void *src, char *cell, size_t bytes, uint64_t *flag, uint64_t v, hipStream_t s);
+// nothing copied) until *flag == v, then copies the cell out.  Both store
+// mark_v into the pinned host word *mark (when not null) as their last
+// action, so the host sees completion without an event (host_mark.h).
+int eager_put(const void *src, char *cell, size_t bytes, uint64_t *flag, uint64_t v, uint64_t *mark,
+              uint64_t mark_v, hipStream_t s);
 int eager_get(const char *cell, void *dst, size_t bytes, const uint64_t *flag, uint64_t v, int *err,
-              uint64_t ticks, hipStream_t s);
+              uint64_t ticks, uint64_t *mark, uint64_t mark_v, hipStream_t s);
 int xfer_copy(const void *src, void *dst, size_t bytes, hipStream_t s,
               const uint32_t *gate = nullptr);
 // Point-to-point mailboxes of the communicator (created with it).

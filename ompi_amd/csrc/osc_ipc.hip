@@ -683,13 +683,15 @@ __device__ __forceinline__ void eager_bytes(const char *src, char *dst, int64_t 
 // receiver's copy waits for the flag on the device instead of the sender
 // waiting for this kernel on the host.
 __global__ __launch_bounds__(256) void eager_put_kernel(const char *src, char *cell, int64_t bytes,
-                                                        uint64_t *flag, uint64_t v) {
+                                                        uint64_t *flag, uint64_t v, uint64_t *mark,
+                                                        uint64_t mark_v) {
     eager_bytes(src, cell, bytes);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         osc_release();
         __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (mark) __hip_atomic_store(mark, mark_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -697,7 +699,7 @@ __global__ __launch_bounds__(256) void eager_put_kernel(const char *src, char *c
 // past `ticks` the communicator's sticky error, nothing copied).
 __global__ __launch_bounds__(256) void eager_get_kernel(const char *cell, char *dst, int64_t bytes,
                                                         const uint64_t *flag, uint64_t v, int *err,
-                                                        uint64_t ticks) {
+                                                        uint64_t ticks, uint64_t *mark, uint64_t mark_v) {
     __shared__ int ok;
     if (threadIdx.x == 0) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -713,21 +715,24 @@ __global__ __launch_bounds__(256) void eager_get_kernel(const char *cell, char *
         osc_acquire();
     }
     __syncthreads();
-    if (!ok) return;
-    eager_bytes(cell, dst, bytes);
+    if (ok) eager_bytes(cell, dst, bytes);
     osc_epilogue();
+    // the host's completion word (also after a timeout: the host then reads
+    // the communicator's sticky error)
+    if (threadIdx.x == 0 && mark) __hip_atomic_store(mark, mark_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-int eager_put(const void *src, char *cell, size_t bytes, uint64_t *flag, uint64_t v, hipStream_t s) {
+int eager_put(const void *src, char *cell, size_t bytes, uint64_t *flag, uint64_t v, uint64_t *mark,
+              uint64_t mark_v, hipStream_t s) {
     hipLaunchKernelGGL(eager_put_kernel, dim3(1), dim3(256), 0, s, static_cast<const char *>(src), cell,
-                       (int64_t)bytes, flag, v);
+                       (int64_t)bytes, flag, v, mark, mark_v);
     return record_hip(hipGetLastError(), "p2p eager copy launch");
 }
 
 int eager_get(const char *cell, void *dst, size_t bytes, const uint64_t *flag, uint64_t v, int *err,
-              uint64_t ticks, hipStream_t s) {
+              uint64_t ticks, uint64_t *mark, uint64_t mark_v, hipStream_t s) {
     hipLaunchKernelGGL(eager_get_kernel, dim3(1), dim3(256), 0, s, cell, static_cast<char *>(dst),
-                       (int64_t)bytes, flag, v, err, ticks);
+                       (int64_t)bytes, flag, v, err, ticks, mark, mark_v);
     return record_hip(hipGetLastError(), "p2p eager receive launch");
 }
 

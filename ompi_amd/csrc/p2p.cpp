@@ -80,6 +80,7 @@
 
 #include "../../include/ompi_amd_p2p.h"
 #include "comm_internal.h"
+#include "host_mark.h"
 #include "runtime.h"
 
 namespace ompi_amd {
@@ -213,6 +214,10 @@ struct ompi_amd_p2p_request {
     int src = OMPI_AMD_ANY_SOURCE, tag = OMPI_AMD_ANY_TAG;
     hipStream_t stream = nullptr;
     hipEvent_t ev = nullptr;
+    // an eager copy kernel's completion word (pinned host memory, host_mark.h):
+    // done once *mark >= mark_v; no event is recorded then
+    uint64_t *mark = nullptr;
+    uint64_t mark_v = 0;
     bool matched = false;
     msg_slot *slot = nullptr;  // matched message
     void *pinned = nullptr;    // sender mapping held during the copy
@@ -477,6 +482,16 @@ static int record_copy(p2p_state *p, ompi_amd_p2p_request *r) {
     return rc;
 }
 
+// A completion word for an eager copy kernel of `r` (none: the event).
+static void take_mark(ompi_amd_p2p_request *r) {
+    r->mark = mark_word_get();
+    r->mark_v = r->mark ? mark_reserve() : 0;
+}
+
+static bool mark_landed(const ompi_amd_p2p_request *r) {
+    return __atomic_load_n(r->mark, __ATOMIC_ACQUIRE) >= r->mark_v;
+}
+
 // Claim `m` for receive `r` and launch its copy.
 static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s) {
     m->state.store(S_MATCHED, std::memory_order_release);
@@ -532,8 +547,9 @@ static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s
         if (m->inl == 3) {  // an eager cell: the copy waits for the sender's kernel to publish it
             const int64_t ms = comm_timeout_ms(p->c);
             const uint64_t ticks = ms > 0 ? (uint64_t)ms * 100000ull : (1ull << 62);  // 100 MHz
+            if (!r->host_dst) take_mark(r);  // a host receive's copy out still needs the event
             rc = eager_get(src, dst, n, reinterpret_cast<const uint64_t *>(src + kEager), m->seq + 1,
-                           comm_err_dev(p->c), ticks, r->stream);
+                           comm_err_dev(p->c), ticks, r->mark, r->mark_v, r->stream);
         } else {
             rc = xfer_copy(src, dst, n, r->stream);
         }
@@ -541,7 +557,7 @@ static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s
     if (rc == OMPI_AMD_SUCCESS && r->host_dst)
         rc = record_hip(hipMemcpyAsync(r->host_dst, dst, n, hipMemcpyDeviceToHost, r->stream),
                         "hipMemcpyAsync (p2p receive to host)");
-    if (rc == OMPI_AMD_SUCCESS) rc = record_copy(p, r);
+    if (rc == OMPI_AMD_SUCCESS && !r->mark) rc = record_copy(p, r);
     if (rc != OMPI_AMD_SUCCESS) r->rc = r->st.error = rc;
 }
 
@@ -570,7 +586,9 @@ static int test_one(ompi_amd_p2p_request *r, bool *done) {
         return r->rc;
     }
     *done = false;
-    if (r->is_send && r->ev) {  // a device eager send: complete once its copy into the cell ran
+    if (r->is_send && r->mark) {  // a device eager send: complete once its copy into the cell ran
+        r->done = mark_landed(r);
+    } else if (r->is_send && r->ev) {
         const hipError_t e = hipEventQuery(r->ev);
         if (e != hipErrorNotReady) {
             if (e != hipSuccess) r->rc = record_hip(e, "p2p eager copy");
@@ -581,7 +599,9 @@ static int test_one(ompi_amd_p2p_request *r, bool *done) {
         if (m.seq != r->seq || m.state.load(std::memory_order_acquire) == S_DONE) r->done = true;
     } else if (r->matched) {
         bool copied = true;
-        if (r->ev) {
+        if (r->mark) {
+            copied = mark_landed(r);
+        } else if (r->ev) {
             const hipError_t e = hipEventQuery(r->ev);
             if (e == hipErrorNotReady) {
                 copied = false;
@@ -807,9 +827,11 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
         if (host) {  // a host buffer past the host ring: copied in now
             rc = copy_in(cell);
         } else {  // posted at once; the receiver's copy waits for the flag
-            rc = eager_put(buf, cell, bytes, reinterpret_cast<uint64_t *>(cell + kEager), seq + 1, s);
             r->stream = s;
-            if (rc == OMPI_AMD_SUCCESS) rc = record_copy(p, r);
+            take_mark(r);
+            rc = eager_put(buf, cell, bytes, reinterpret_cast<uint64_t *>(cell + kEager), seq + 1, r->mark,
+                           r->mark_v, s);
+            if (rc == OMPI_AMD_SUCCESS && !r->mark) rc = record_copy(p, r);
             flagged = true;
         }
         src = cell;
@@ -837,6 +859,7 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     }
     if (rc != OMPI_AMD_SUCCESS) {
         if (r->ev) p->ev_free.push_back(r->ev);
+        mark_word_put(r->mark);  // its kernel never launched (or failed to)
         delete r;
         return rc;
     }
@@ -910,6 +933,7 @@ int ompi_amd_p2p_free(ompi_amd_p2p_request_t *r) {
         std::lock_guard<std::recursive_mutex> g(r->p->mu);
         r->p->ev_free.push_back(r->ev);
     }
+    mark_word_put(r->mark);  // done: its mark landed
     delete r;
     return rc;
 }
