@@ -69,9 +69,6 @@ int comm_sticky(ompi_amd_comm_t *c);
 // Byte copy kernel (16-/4-/1-byte granules by the common phase of src and
 // dst; src or dst may be peer memory), system-scope acquire/release.
 int comm_copy(ompi_amd_comm_t *c, const void *src, void *dst, size_t bytes, hipStream_t s);
-// osc_ipc.hip: the byte copy of put / get and the p2p receive (persistent
-// grid, one acquire per workgroup; src or dst may be peer memory).
-// gate: a CTL_TAKEN_* word that must read 1 for the copy to run (NULL: none).
 // p2p eager cells (osc_ipc.hip, one workgroup, bytes <= 4 KiB): eager_put
 // copies src into the cell, then stores v into *flag (system scope, after a
 // release); eager_get waits (bounded by ticks of s_memrealtime: err set,
@@ -82,8 +79,29 @@ int eager_put(const void *src, char *cell, size_t bytes, uint64_t *flag, uint64_
               uint64_t mark_v, hipStream_t s);
 int eager_get(const char *cell, void *dst, size_t bytes, const uint64_t *flag, uint64_t v, int *err,
               uint64_t ticks, uint64_t *mark, uint64_t mark_v, hipStream_t s);
+// osc_ipc.hip: the byte copy of put / get and the p2p receive (persistent
+// grid, one acquire per workgroup; src or dst may be peer memory).
+// gate: a CTL_TAKEN_* word that must read 1 for the copy to run (NULL: none).
 int xfer_copy(const void *src, void *dst, size_t bytes, hipStream_t s,
               const uint32_t *gate = nullptr);
+// The same copy with device-side signalling (p2p staged messages): every
+// workgroup first waits until *wait == wait_v (bounded by ticks: *err set,
+// nothing copied; wait NULL: no wait); after the last workgroup finished
+// (counter *done, zero at rest, reset by that workgroup) *flag = flag_v
+// (system scope, after a release) and the pinned host word *mark = mark_v,
+// each when not NULL.
+struct xfer_sig {
+    const uint64_t *wait = nullptr;
+    uint64_t wait_v = 0;
+    int *err = nullptr;
+    uint64_t ticks = 0;
+    uint64_t *flag = nullptr;
+    uint64_t flag_v = 0;
+    uint64_t *mark = nullptr;
+    uint64_t mark_v = 0;
+    uint32_t *done = nullptr;
+};
+int xfer_copy_sig(const void *src, void *dst, size_t bytes, hipStream_t s, const xfer_sig &sig);
 // Point-to-point mailboxes of the communicator (created with it).
 p2p_state *comm_p2p(ompi_amd_comm_t *c);
 // The one-sided part's per-communicator state (NULL until it sets one).

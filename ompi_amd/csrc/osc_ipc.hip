@@ -303,11 +303,7 @@ __global__ __launch_bounds__(kOscThreads) void acc_kernel(const T *__restrict__ 
 // else 4-B or 1-B granules; one acquire per workgroup, persistent grid (as
 // acc_kernel).
 template <int THREADS, int UNROLL>
-__global__ __launch_bounds__(THREADS) void xfer_kernel(const char *src, char *dst, int64_t bytes,
-                                                       const uint32_t *gate) {
-    if (!gate_open(gate)) return;
-    if (threadIdx.x == 0) osc_acquire();
-    __syncthreads();
+__device__ __forceinline__ void xfer_body(const char *src, char *dst, int64_t bytes) {
     const uintptr_t phase = (uintptr_t)src ^ (uintptr_t)dst;
     const int g = (phase & 15) == 0 ? 16 : ((phase & 3) == 0 ? 4 : 1);
     int64_t head = (int64_t)((g - ((uintptr_t)src & (uintptr_t)(g - 1))) & (uintptr_t)(g - 1));
@@ -346,7 +342,53 @@ __global__ __launch_bounds__(THREADS) void xfer_kernel(const char *src, char *ds
         const int64_t i = k < head ? k : tail0 + (k - head);
         dst[i] = src[i];
     }
+}
+
+template <int THREADS, int UNROLL>
+__global__ __launch_bounds__(THREADS) void xfer_kernel(const char *src, char *dst, int64_t bytes,
+                                                       const uint32_t *gate) {
+    if (!gate_open(gate)) return;
+    if (threadIdx.x == 0) osc_acquire();
+    __syncthreads();
+    xfer_body<THREADS, UNROLL>(src, dst, bytes);
     osc_epilogue();
+}
+
+// xfer_kernel with the signalling of comm_internal.h's xfer_sig.
+template <int THREADS, int UNROLL>
+__global__ __launch_bounds__(THREADS) void xfer_sig_kernel(const char *src, char *dst, int64_t bytes,
+                                                           xfer_sig sg) {
+    __shared__ int ok;
+    if (threadIdx.x == 0) {
+        ok = 1;
+        if (sg.wait) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(sg.wait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != sg.wait_v) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > sg.ticks) {
+                    __hip_atomic_store(sg.err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                    ok = 0;
+                    break;
+                }
+            }
+        }
+        osc_acquire();
+    }
+    __syncthreads();
+    if (ok) xfer_body<THREADS, UNROLL>(src, dst, bytes);
+    osc_epilogue();  // this workgroup's stores released at system scope
+    if (threadIdx.x != 0 || (!sg.flag && !sg.mark)) return;
+    if (gridDim.x > 1) {
+        // the last workgroup to finish signals (its acquire-release RMW
+        // orders every other workgroup's released stores before the flag)
+        const uint32_t prev = __hip_atomic_fetch_add(sg.done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (prev != gridDim.x - 1) return;
+        __hip_atomic_store(sg.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        osc_release();
+    }
+    if (sg.flag) __hip_atomic_store(sg.flag, sg.flag_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (sg.mark) __hip_atomic_store(sg.mark, sg.mark_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Compare-and-swap of one element of `size` data bytes (osc_sm_comm.c:386-396).
@@ -734,6 +776,21 @@ int eager_get(const char *cell, void *dst, size_t bytes, const uint64_t *flag, u
     hipLaunchKernelGGL(eager_get_kernel, dim3(1), dim3(256), 0, s, cell, static_cast<char *>(dst),
                        (int64_t)bytes, flag, v, err, ticks, mark, mark_v);
     return record_hip(hipGetLastError(), "p2p eager receive launch");
+}
+
+int xfer_copy_sig(const void *src, void *dst, size_t bytes, hipStream_t s, const xfer_sig &sig) {
+    const int64_t units = (int64_t)(bytes / 16) + 1;
+    const int64_t per = (int64_t)kXferThreads * kXferUnroll;
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((units + per - 1) / per,
+                                                                  osc_grid_cap()));
+    if (blocks > 1 && (sig.flag || sig.mark) && !sig.done) {
+        record_msg("xfer_copy_sig: a multi-workgroup copy that signals needs a counter");
+        return OMPI_AMD_ERR_BAD_PARAM;
+    }
+    hipLaunchKernelGGL((xfer_sig_kernel<kXferThreads, kXferUnroll>), dim3((unsigned)blocks),
+                       dim3(kXferThreads), 0, s, static_cast<const char *>(src), static_cast<char *>(dst),
+                       (int64_t)bytes, sig);
+    return record_hip(hipGetLastError(), "signalled copy launch");
 }
 
 static int launch_acc(ompi_amd_win_t *w, int op, int type, const void *origin, void *target,

@@ -41,8 +41,12 @@
 //            communicator lives) and the receiver pulls from there, so no
 //            peer ever maps an application buffer — the (process, address)
 //            identity of an IPC handle cannot go stale under the
-//            application's frees.  A standard send
-//            completes once staged (ob1 may buffer a standard send too);
+//            application's frees.  From a device buffer
+//            the stage copy signals like an eager cell (its last workgroup
+//            sets the slot's cell flag), the message is posted at launch and
+//            the receiver's copy waits for the flag on the device; a
+//            standard send completes once staged (ob1 may buffer a standard
+//            send too);
 //            MPI_Ssend still completes at the receiver's FIN.  Past the
 //            pool's cap (param p2p_stage_mib), or with p2p_user_ipc = 1, the
 //            receiver maps the send buffer itself (rendezvous, as before).
@@ -102,7 +106,9 @@ struct alignas(64) msg_slot {
     uint64_t raw;  // the send buffer's address (messages to self)
     ipc_desc d;    // the send buffer for peers
     uint32_t inl;  // 1: payload in `inline_data`; 2: in the sender's host stage at offset `raw`;
-                   // 3: in an eager cell whose flag (cell + kEager) becomes seq + 1
+                   // 3: in an eager cell whose flag (cell + kEager) becomes seq + 1;
+                   // 4: in a send stage (d) whose copy kernel sets the slot's cell flag (fd)
+    ipc_desc fd;   // inl 4: the sender's eager cell of this slot (its flag word)
     char inline_data[kInline];
 };
 
@@ -141,7 +147,13 @@ struct p2p_state {
     std::vector<uint64_t> scan_from;  // per source: first sequence possibly still POSTED
     std::deque<ompi_amd_p2p_request *> recvs;  // posted receives not matched yet
     std::recursive_mutex mu;
-    char *eager = nullptr;  // [size][kSlots] cells of kCell bytes (zeroed), allocated at first use
+    // [size][kSlots] cells of kCell bytes, then [size][kSlots] 64-B lines of
+    // receive copy counters (zeroed), allocated at first use
+    char *eager = nullptr;
+    uint32_t *recv_done(int src, uint64_t seq) {
+        return reinterpret_cast<uint32_t *>(eager + (size_t)size * kSlots * kCell +
+                                            ((size_t)src * kSlots + seq % kSlots) * 64);
+    }
     // this rank's host stage ring (bytes [htail, hhead) in flight, monotonic
     // counters) and the messages holding it, oldest first
     uint64_t hhead = 0, htail = 0;
@@ -221,6 +233,7 @@ struct ompi_amd_p2p_request {
     bool matched = false;
     msg_slot *slot = nullptr;  // matched message
     void *pinned = nullptr;    // sender mapping held during the copy
+    void *pinned2 = nullptr;   // inl 4: the sender's eager area (the stage's flag)
     ompi_amd_status_t st{};
     void *host_dst = nullptr;  // a host receive buffer: the copy lands in `rstage` first
     stage rstage{};
@@ -428,6 +441,22 @@ static bool take_stage(p2p_state *p, std::vector<stage> &pool, size_t bytes, boo
 
 static bool is_device(const void *ptr) { return ompi_amd_is_device_pointer(ptr) != 0; }
 
+// The eager area (exportable: peers read its cells and flags), allocated
+// zeroed at the first device send or signalled receive.  Under p->mu.
+static int eager_area(p2p_state *p) {
+    if (p->eager) return OMPI_AMD_SUCCESS;
+    ipc_desc d{};
+    const size_t area = (size_t)p->size * kSlots * (kCell + 64);
+    int rc = comm_alloc_exportable(area, false, (void **)&p->eager, &d);
+    if (rc == OMPI_AMD_SUCCESS) {  // every flag 0 (no sequence + 1 yet), every counter 0
+        rc = record_hip(hipMemset(p->eager, 0, area), "hipMemset (p2p eager area)");
+        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipDeviceSynchronize(), "hipDeviceSynchronize (eager area)");
+        if (rc != OMPI_AMD_SUCCESS) hip_ignore(hipFree(p->eager));
+    }
+    if (rc != OMPI_AMD_SUCCESS) p->eager = nullptr;
+    return rc;
+}
+
 static bool tag_ok(int want, int have) { return want == OMPI_AMD_ANY_TAG || want == have; }
 
 // The earliest POSTED message from `s` a receive with `tag` matches.
@@ -550,6 +579,23 @@ static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s
             if (!r->host_dst) take_mark(r);  // a host receive's copy out still needs the event
             rc = eager_get(src, dst, n, reinterpret_cast<const uint64_t *>(src + kEager), m->seq + 1,
                            comm_err_dev(p->c), ticks, r->mark, r->mark_v, r->stream);
+        } else if (m->inl == 4) {  // a signalled stage: the copy waits for the sender's flag
+            const char *fc = nullptr;
+            rc = comm_import(p->c, s, m->fd, &fc, true, &r->pinned2);
+            if (rc == OMPI_AMD_SUCCESS) rc = eager_area(p);  // this rank's copy counters
+            if (rc == OMPI_AMD_SUCCESS) {
+                const int64_t ms = comm_timeout_ms(p->c);
+                xfer_sig sg;
+                sg.wait = reinterpret_cast<const uint64_t *>(fc + kEager);
+                sg.wait_v = m->seq + 1;
+                sg.err = comm_err_dev(p->c);
+                sg.ticks = ms > 0 ? (uint64_t)ms * 100000ull : (1ull << 62);
+                if (!r->host_dst) take_mark(r);
+                sg.mark = r->mark;
+                sg.mark_v = r->mark_v;
+                sg.done = p->recv_done(s, m->seq);
+                rc = xfer_copy_sig(src, dst, n, r->stream, sg);
+            }
         } else {
             rc = xfer_copy(src, dst, n, r->stream);
         }
@@ -611,14 +657,15 @@ static int test_one(ompi_amd_p2p_request *r, bool *done) {
         }
         if (copied) {
             if (r->pinned) comm_unpin(p->c, r->pinned);
-            r->pinned = nullptr;
+            if (r->pinned2) comm_unpin(p->c, r->pinned2);
+            r->pinned = r->pinned2 = nullptr;
             if (r->has_rstage) {
                 p->recv_free.push_back(r->rstage);
                 r->has_rstage = false;
             }
             // an eager receive whose wait for the sender's flag timed out
             // copied nothing: the communicator's error says so
-            if (r->slot->inl == 3 && r->rc == OMPI_AMD_SUCCESS) {
+            if ((r->slot->inl == 3 || r->slot->inl == 4) && r->rc == OMPI_AMD_SUCCESS) {
                 const int se = comm_sticky(p->c);
                 if (se != OMPI_AMD_SUCCESS) r->rc = r->st.error = se;
             }
@@ -716,17 +763,7 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     const bool inl = host && eager && bytes <= kInline;  // no device work at all
     const bool hostable = host && !inl && mode != OMPI_AMD_SEND_SYNCHRONOUS && bytes <= kHostMax;
     std::unique_lock<std::recursive_mutex> alloc_guard(p->mu);
-    if (rc == OMPI_AMD_SUCCESS && eager && !inl && !p->eager) {  // peers read its cells: exportable
-        ipc_desc d{};
-        const size_t area = (size_t)p->size * kSlots * kCell;
-        rc = comm_alloc_exportable(area, false, (void **)&p->eager, &d);
-        if (rc == OMPI_AMD_SUCCESS) {  // every flag 0: no sequence + 1 yet
-            rc = record_hip(hipMemset(p->eager, 0, area), "hipMemset (p2p eager area)");
-            if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipDeviceSynchronize(), "hipDeviceSynchronize (eager area)");
-            if (rc != OMPI_AMD_SUCCESS) hip_ignore(hipFree(p->eager));
-        }
-        if (rc != OMPI_AMD_SUCCESS) p->eager = nullptr;
-    }
+    if (rc == OMPI_AMD_SUCCESS && !inl) rc = eager_area(p);  // peers read its cells and flags
     alloc_guard.unlock();
     if (rc != OMPI_AMD_SUCCESS) return rc;
     // A copy into an eager cell or a stage runs on `s`, after the buffer's
@@ -763,8 +800,8 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     }
     reclaim(p);
     const void *src = buf;
-    ipc_desc d{};
-    bool staged = false;
+    ipc_desc d{}, fd{};
+    bool staged = false, sflagged = false;
     auto copy_in = [&](char *to) {
         const int crc = host ? record_hip(hipMemcpyAsync(to, buf, bytes, hipMemcpyHostToDevice, s),
                                           "hipMemcpyAsync (p2p send stage)")
@@ -800,7 +837,26 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
                                   host ? "p2p send stage (host buffer)" : "p2p send stage (device buffer)");
         }
         if (!got) return OMPI_AMD_SUCCESS;
-        const int crc = copy_in(st.buf);
+        int crc;
+        if (!host && mode != OMPI_AMD_SEND_SYNCHRONOUS) {
+            // posted at once: the stage copy sets this slot's cell flag when
+            // its last workgroup is done, and the receiver's copy waits for it
+            char *cell = p->eager + ((size_t)dst * kSlots + seq % kSlots) * kCell;
+            xfer_sig sg;
+            sg.flag = reinterpret_cast<uint64_t *>(cell + kEager);
+            sg.flag_v = seq + 1;
+            sg.done = reinterpret_cast<uint32_t *>(cell + kEager + 8);
+            r->stream = s;
+            take_mark(r);
+            sg.mark = r->mark;
+            sg.mark_v = r->mark_v;
+            crc = xfer_copy_sig(buf, st.buf, bytes, s, sg);
+            if (crc == OMPI_AMD_SUCCESS && !r->mark) crc = record_copy(p, r);
+            if (crc == OMPI_AMD_SUCCESS) crc = comm_export(c, cell, &fd);
+            sflagged = true;
+        } else {
+            crc = copy_in(st.buf);
+        }
         if (crc != OMPI_AMD_SUCCESS) {
             p->send_free.push_back(st);
             return crc;
@@ -868,13 +924,14 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     m.bytes = bytes;
     m.raw = hstaged ? hoff : reinterpret_cast<uint64_t>(src);
     m.d = d;
-    m.inl = inl ? 1u : hstaged ? 2u : flagged ? 3u : 0u;
+    m.fd = fd;
+    m.inl = inl ? 1u : hstaged ? 2u : flagged ? 3u : sflagged ? 4u : 0u;
     m.state.store(S_POSTED, std::memory_order_release);
     q.posted.store(seq + 1, std::memory_order_release);
     r->seq = seq;
     // the user's buffer is free again once staged (Ssend: at the FIN)
     // (a device eager send: once its copy kernel ran, test_one)
-    r->done = (eager && !flagged) || hstaged || (staged && mode != OMPI_AMD_SEND_SYNCHRONOUS);
+    r->done = (eager && !flagged) || hstaged || (staged && !sflagged && mode != OMPI_AMD_SEND_SYNCHRONOUS);
     *out = r;
     return OMPI_AMD_SUCCESS;
 }
