@@ -479,6 +479,13 @@ struct ompi_amd_comm {
     uint64_t *fused_mark = nullptr;
     bool want_mark = false;
     uint64_t mark_embedded = 0;
+    // the word and completion-counter slot the next fused launch signals
+    // (want_mark): fused_mark and slot 0 for the blocking call, a plan's own
+    // word and slot for a persistent start (plan_enqueue)
+    uint64_t *mark_word = nullptr;
+    int mark_slot = 0;
+    std::vector<int> done_free;  // counter slots of freed plans
+    int done_next = 1;           // slot 0: the blocking call
     // params
     size_t small_bytes = 1 << 20;
     size_t fused_bytes = 64 << 10;
@@ -568,6 +575,12 @@ struct ompi_amd_plan {
     bool started = false, recorded = false;
     uint64_t *mark = nullptr;  // host-observed completion word, with `done`
     uint64_t mark_seq = 0;
+    // a small-path start whose fused kernel stores `mark` itself: the value
+    // (0: none — the event and a mark kernel at the first test / wait), the
+    // plan's completion-counter slot in the flag page, backstop poll count
+    uint64_t embedded = 0;
+    int done_slot = -1;
+    unsigned polls = 0;
     ~ompi_amd_plan() { mark_word_put(mark); }
     shadow_set sh;  // export fallback (src / rbuf above are then the shadows)
     // kind 4: a persistent reduce_scatter_block / allgather / bcast — every
@@ -1794,9 +1807,9 @@ static int allreduce_fused(ompi_amd_comm_t *c, const void *src, void *rbuf, int6
     const int64_t cols = std::max<int64_t>(
         1, std::min<int64_t>((most + 4 * kXferThreads - 1) / (4 * kXferThreads),
                              kFusedMaxGroups / rows));
-    if (c->want_mark && c->fused_mark) {  // the blocking entry's completion, by the kernel itself
-        a.done = reinterpret_cast<uint32_t *>(c->flags) + kFusedDoneWord;
-        a.mark = c->fused_mark;
+    if (c->want_mark && c->mark_word) {  // the call's completion, by the kernel itself
+        a.done = reinterpret_cast<uint32_t *>(c->flags) + kFusedDoneWord + kFusedDoneStride * c->mark_slot;
+        a.mark = c->mark_word;
         a.mark_v = mark_reserve();
     }
     TRY(record_hip(f(dim3((unsigned)cols, (unsigned)rows), a, s), "fused allreduce launch"));
@@ -2883,11 +2896,17 @@ int ompi_amd_comm_vote(ompi_amd_comm_t *c, int local_yes, int *n_yes) {
     return OMPI_AMD_SUCCESS;
 }
 
+static bool fused_mark_on() {
+    static const bool on = !(getenv("OMPI_AMD_FUSED_MARK") && atoi(getenv("OMPI_AMD_FUSED_MARK")) == 0);
+    return on;
+}
+
 int ompi_amd_allreduce_wait(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                             int op) {
     if (!c) return OMPI_AMD_ERR_BAD_PARAM;
-    static const bool on = !(getenv("OMPI_AMD_FUSED_MARK") && atoi(getenv("OMPI_AMD_FUSED_MARK")) == 0);
-    c->want_mark = on;
+    c->want_mark = fused_mark_on();
+    c->mark_word = c->fused_mark;
+    c->mark_slot = 0;
     c->mark_embedded = 0;
     const int rc = ompi_amd_allreduce(c, sbuf, rbuf, count, type, op, nullptr);
     c->want_mark = false;
@@ -4083,8 +4102,26 @@ static int plan_enqueue(ompi_amd_plan_t *pl, void *stream) {
     if (pl->kind == 0) {  // the small paths: a plain call with the parameters of the init
         TRY(check_sticky(c));
         TRY(drain(c));
-        return allreduce_impl(c, pl->src == pl->rbuf ? (const void *)1 : pl->src, pl->rbuf,
-                              (size_t)pl->count, pl->type, pl->op, as_stream(stream), pl->pp);
+        // a fused launch stores the plan's mark itself (its own counter slot:
+        // plans of one communicator may be in flight together)
+        if (pl->done_slot < 0 && pl->mark && fused_mark_on()) {
+            if (!c->done_free.empty()) {
+                pl->done_slot = c->done_free.back();
+                c->done_free.pop_back();
+            } else if (c->done_next < kFusedDoneSlots) {
+                pl->done_slot = c->done_next++;
+            }
+        }
+        c->want_mark = pl->done_slot >= 0;
+        c->mark_word = pl->mark;
+        c->mark_slot = std::max(pl->done_slot, 0);
+        c->mark_embedded = 0;
+        const int rc = allreduce_impl(c, pl->src == pl->rbuf ? (const void *)1 : pl->src, pl->rbuf,
+                                      (size_t)pl->count, pl->type, pl->op, as_stream(stream), pl->pp);
+        c->want_mark = false;
+        pl->embedded = c->mark_embedded;
+        c->mark_embedded = 0;
+        return rc;
     }
     TRY(check_sticky(c));
     TRY(set_dev(c));
@@ -4226,6 +4263,8 @@ int ompi_amd_plan_start(ompi_amd_plan_t *pl, void *stream) {
         return OMPI_AMD_SUCCESS;
     }
     TRY(drain(pl->c));  // device order: deferred nonblocking calls first
+    pl->embedded = 0;
+    pl->polls = 0;
     TRY(plan_enqueue(pl, stream));
     pl->started = true;
     pl->recorded = false;
@@ -4239,6 +4278,16 @@ int ompi_amd_plan_test(ompi_amd_plan_t *pl, int *done) {
     *done = 1;
     if (!pl->started) return OMPI_AMD_SUCCESS;
     if (pl->kind == 4) return pl->req ? ompi_amd_request_test(pl->req, done) : OMPI_AMD_SUCCESS;
+    if (pl->embedded) {  // the fused kernel's own mark; the stream backs it up now and then
+        if (mark_seen(pl->mark, pl->embedded)) return check_sticky(pl->c);
+        if (++pl->polls % 64 == 0) {
+            const hipError_t e = hipStreamQuery(pl->stream);
+            if (e == hipSuccess) return check_sticky(pl->c);
+            if (e != hipErrorNotReady) return record_hip(e, "plan test");
+        }
+        *done = 0;
+        return OMPI_AMD_SUCCESS;
+    }
     if (!pl->recorded) {
         TRY(record_hip(hipEventRecord(pl->done, pl->stream), "plan completion event"));
         pl->mark_seq = mark_launch(pl->mark, pl->stream);
@@ -4259,6 +4308,10 @@ int ompi_amd_plan_wait(ompi_amd_plan_t *pl) {
     if (!pl) return OMPI_AMD_ERR_BAD_PARAM;
     if (!pl->started) return OMPI_AMD_SUCCESS;
     if (pl->kind == 4) return pl->req ? ompi_amd_request_wait(pl->req) : OMPI_AMD_SUCCESS;
+    if (pl->embedded) {
+        TRY(record_hip(mark_value_wait(pl->stream, pl->mark, pl->embedded, progress_others), "plan wait"));
+        return check_sticky(pl->c);
+    }
     if (!pl->recorded) {
         TRY(record_hip(hipEventRecord(pl->done, pl->stream), "plan completion event"));
         pl->mark_seq = mark_launch(pl->mark, pl->stream);
@@ -4286,6 +4339,10 @@ int ompi_amd_plan_free(ompi_amd_plan_t *pl) {
         arena_free(pl->c, pl->sh.mem2);
     }
     if (pl->done) hip_ignore(hipEventDestroy(pl->done));
+    if (pl->c && pl->done_slot >= 0) {  // its last start was waited for (MPI_Request_free of a started plan: above)
+        if (pl->started && pl->embedded) (void)ompi_amd_plan_wait(pl);
+        pl->c->done_free.push_back(pl->done_slot);
+    }
     delete pl;
     return OMPI_AMD_SUCCESS;
 }

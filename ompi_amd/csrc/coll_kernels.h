@@ -397,6 +397,11 @@ struct fused_args {
 
 // flag-page word (uint32 index) of the fused kernel's finished-workgroup counter
 constexpr int kFusedDoneWord = 8192 / (int)sizeof(uint32_t);
+// completion counters of fused launches that store their own mark: slot k
+// at word kFusedDoneWord + kFusedDoneStride * k (own 64-B line), slot 0 the
+// blocking call's, the others persistent plans' (up to kPipeFlagOff)
+constexpr int kFusedDoneStride = 64 / (int)sizeof(uint32_t);
+constexpr int kFusedDoneSlots = (64 << 10) / 64 - 8192 / 64;
 
 template <typename T, int OP>
 __global__ __launch_bounds__(kXferThreads) void fused_allreduce_kernel(fused_args a) {

@@ -230,6 +230,7 @@ struct ompi_amd_p2p_request {
     // done once *mark >= mark_v; no event is recorded then
     uint64_t *mark = nullptr;
     uint64_t mark_v = 0;
+    unsigned polls = 0;
     bool matched = false;
     msg_slot *slot = nullptr;  // matched message
     void *pinned = nullptr;    // sender mapping held during the copy
@@ -517,8 +518,19 @@ static void take_mark(ompi_amd_p2p_request *r) {
     r->mark_v = r->mark ? mark_reserve() : 0;
 }
 
-static bool mark_landed(const ompi_amd_p2p_request *r) {
-    return __atomic_load_n(r->mark, __ATOMIC_ACQUIRE) >= r->mark_v;
+// Whether r's copy kernel stored its mark.  Every 64th unanswered poll the
+// stream backs it up: idle with no mark means the kernel never ran (its
+// launch failed after all): the request ends with an error instead of
+// waiting for ever (the PML glue's waits have no time limit).
+static bool mark_landed(ompi_amd_p2p_request *r) {
+    if (__atomic_load_n(r->mark, __ATOMIC_ACQUIRE) >= r->mark_v) return true;
+    if (++r->polls % 64 != 0) return false;
+    const hipError_t e = hipStreamQuery(r->stream);
+    if (e == hipErrorNotReady) return false;
+    if (__atomic_load_n(r->mark, __ATOMIC_ACQUIRE) >= r->mark_v) return true;
+    r->rc = r->st.error = e != hipSuccess ? record_hip(e, "p2p copy")
+                                          : (record_msg("p2p copy kernel ended without its mark"), OMPI_AMD_ERR_HIP);
+    return true;
 }
 
 // Claim `m` for receive `r` and launch its copy.
