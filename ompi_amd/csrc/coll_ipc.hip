@@ -359,6 +359,11 @@ struct ompi_amd_request {
     int rc = OMPI_AMD_SUCCESS;
     char *shadow = nullptr;  // export-fallback memory of the call, freed with the request
     char *shadow2 = nullptr; //   and its separate result region, if any
+    // a small allreduce launched on the fused kernel that stores `mark`
+    // itself: the value (0: none), its completion-counter slot, polls
+    uint64_t embedded = 0;
+    int done_slot = -1;
+    unsigned polls = 0;
 };
 
 // ------------------------------------------------------------------ comm
@@ -2426,6 +2431,30 @@ static int agree_root0_inplace(ompi_amd_comm_t *c, path_params *pp, bool inplace
 // has posted its handle-swap half; block = wait for them (the blocking entry
 // points do, so their device work follows the deferred calls' on every rank).
 // max_launch: stop after launching that many deferred calls (-1: no limit).
+// Whether fused small allreduces store their own completion marks (env
+// OMPI_AMD_FUSED_MARK=0: a mark kernel behind them instead, for A/B runs).
+static bool fused_mark_on() {
+    static const bool on = !(getenv("OMPI_AMD_FUSED_MARK") && atoi(getenv("OMPI_AMD_FUSED_MARK")) == 0);
+    return on;
+}
+
+// A completion-counter slot of the flag page for a fused launch that
+// signals its own mark (kFusedDoneSlots; slot 0 is the blocking call's);
+// -1 when all are taken (the call then waits through a mark kernel).
+static int done_slot_take(ompi_amd_comm_t *c) {
+    if (!fused_mark_on()) return -1;
+    if (!c->done_free.empty()) {
+        const int k = c->done_free.back();
+        c->done_free.pop_back();
+        return k;
+    }
+    return c->done_next < kFusedDoneSlots ? c->done_next++ : -1;
+}
+
+static void done_slot_give(ompi_amd_comm_t *c, int k) {
+    if (k > 0) c->done_free.push_back(k);
+}
+
 static int progress(ompi_amd_comm_t *c, bool block, int max_launch = -1);
 
 // ---- progress across communicators (MPI's progress rule for nonblocking
@@ -2559,8 +2588,20 @@ static int progress(ompi_amd_comm_t *c, bool block, int max_launch) {
                     c->force_shadow = fs;
                     break;
                 }
-                default:
+                default: {
+                    // a fused launch stores the request's mark itself
+                    const int slot = o.req->mark ? done_slot_take(c) : -1;
+                    c->want_mark = slot >= 0;
+                    c->mark_word = o.req->mark;
+                    c->mark_slot = std::max(slot, 0);
+                    c->mark_embedded = 0;
                     rc = allreduce_impl(c, o.sbuf, o.rbuf, o.count, o.type, o.op, o.stream, o.pp);
+                    c->want_mark = false;
+                    o.req->embedded = c->mark_embedded;
+                    c->mark_embedded = 0;
+                    if (o.req->embedded) o.req->done_slot = slot;
+                    else done_slot_give(c, slot);  // not a fused launch: unused
+                }
                 }
             }
             if (rc == OMPI_AMD_SUCCESS) rc = shadow_out(c, o.sh, o.stream);
@@ -2894,11 +2935,6 @@ int ompi_amd_comm_vote(ompi_amd_comm_t *c, int local_yes, int *n_yes) {
     for (int p = 0; p < c->size; ++p) k += all[p];
     *n_yes = k;
     return OMPI_AMD_SUCCESS;
-}
-
-static bool fused_mark_on() {
-    static const bool on = !(getenv("OMPI_AMD_FUSED_MARK") && atoi(getenv("OMPI_AMD_FUSED_MARK")) == 0);
-    return on;
 }
 
 int ompi_amd_allreduce_wait(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
@@ -4104,14 +4140,7 @@ static int plan_enqueue(ompi_amd_plan_t *pl, void *stream) {
         TRY(drain(c));
         // a fused launch stores the plan's mark itself (its own counter slot:
         // plans of one communicator may be in flight together)
-        if (pl->done_slot < 0 && pl->mark && fused_mark_on()) {
-            if (!c->done_free.empty()) {
-                pl->done_slot = c->done_free.back();
-                c->done_free.pop_back();
-            } else if (c->done_next < kFusedDoneSlots) {
-                pl->done_slot = c->done_next++;
-            }
-        }
+        if (pl->done_slot < 0 && pl->mark) pl->done_slot = done_slot_take(c);
         c->want_mark = pl->done_slot >= 0;
         c->mark_word = pl->mark;
         c->mark_slot = std::max(pl->done_slot, 0);
@@ -4341,7 +4370,7 @@ int ompi_amd_plan_free(ompi_amd_plan_t *pl) {
     if (pl->done) hip_ignore(hipEventDestroy(pl->done));
     if (pl->c && pl->done_slot >= 0) {  // its last start was waited for (MPI_Request_free of a started plan: above)
         if (pl->started && pl->embedded) (void)ompi_amd_plan_wait(pl);
-        pl->c->done_free.push_back(pl->done_slot);
+        done_slot_give(pl->c, pl->done_slot);
     }
     delete pl;
     return OMPI_AMD_SUCCESS;
@@ -4357,6 +4386,21 @@ int ompi_amd_request_test(ompi_amd_request_t *r, int *done) {
         if (!r->launched) return OMPI_AMD_SUCCESS;
     }
     if (r->rc != OMPI_AMD_SUCCESS) return r->rc;
+    if (r->embedded) {  // the fused kernel's own mark; the stream backs it up now and then
+        if (mark_seen(r->mark, r->embedded)) {
+            *done = 1;
+            return check_sticky(r->c);
+        }
+        if (++r->polls % 64 == 0) {
+            const hipError_t e = hipStreamQuery(r->stream);
+            if (e != hipSuccess && e != hipErrorNotReady) return record_hip(e, "request test");
+            if (e == hipSuccess) {
+                *done = 1;
+                return check_sticky(r->c);
+            }
+        }
+        return OMPI_AMD_SUCCESS;
+    }
     if (!r->recorded) {
         TRY(record_hip(hipEventRecord(r->ev, r->stream), "request event"));
         r->mark_seq = mark_launch(r->mark, r->stream);
@@ -4381,6 +4425,10 @@ int ompi_amd_request_wait(ompi_amd_request_t *r) {
         TRY(progress(r->c, true));
     }
     if (r->rc != OMPI_AMD_SUCCESS) return r->rc;
+    if (r->embedded) {
+        TRY(record_hip(mark_value_wait(r->stream, r->mark, r->embedded, progress_others), "request wait"));
+        return check_sticky(r->c);
+    }
     if (!r->recorded) {
         TRY(record_hip(hipEventRecord(r->ev, r->stream), "request event"));
         r->mark_seq = mark_launch(r->mark, r->stream);
@@ -4396,6 +4444,7 @@ int ompi_amd_request_free(ompi_amd_request_t *r) {
     // the peers launch it whatever this rank does: launch and finish it too
     const int rc = ompi_amd_request_wait(r);
     req_event_put(r->c, r->ev);  // its wait is over
+    done_slot_give(r->c, r->done_slot);  // its kernel finished (the wait above)
     // the call's trailing barrier has passed: no peer reads the shadow any more
     arena_free(r->c, r->shadow);
     arena_free(r->c, r->shadow2);
