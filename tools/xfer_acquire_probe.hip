@@ -1,0 +1,88 @@
+// Local device-to-device copy (osc_ipc.hip xfer_kernel's body: 16-B
+// granules, 4 per lane in flight, non-temporal) over 256 MiB, by the
+// workgroup-entry fence it pays and the grid: system-scope acquire (shipped),
+// agent-scope acquire, none; persistent 256 workgroups vs one chunk each.
+// Output: one JSON line per variant; GB/s = 2 x bytes / time.
+// Build: hipcc --offload-arch=gfx950 -O3 -o xfer_acquire_probe xfer_acquire_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                         \
+    do {                                                                              \
+        hipError_t e_ = (x);                                                          \
+        if (e_ != hipSuccess) {                                                       \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                                  \
+        }                                                                             \
+    } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int FENCE, int REL>  // FENCE: 0 none, 1 agent acquire, 2 system acquire; REL: per-WG system release
+__global__ __launch_bounds__(256) void k_copy(const u32x4 *src, u32x4 *dst, long n) {
+    if (FENCE && threadIdx.x == 0) {
+        if (FENCE == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    }
+    __syncthreads();
+    const long chunk = 256L * 4;
+    for (long base = (long)blockIdx.x * chunk + threadIdx.x; base < n; base += (long)gridDim.x * chunk) {
+        u32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const long i = base + (long)u * 256;
+            if (i < n) v[u] = __builtin_nontemporal_load(src + i);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const long i = base + (long)u * 256;
+            if (i < n) __builtin_nontemporal_store(v[u], dst + i);
+        }
+    }
+    if (!REL) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
+template <int FENCE, int REL>
+static void run(const char *name, const u32x4 *s, u32x4 *d, long n, int grid) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((k_copy<FENCE, REL>), dim3(grid), dim3(256), 0, 0, s, d, n);
+    CK(hipDeviceSynchronize());
+    const int iters = 20;
+    CK(hipEventRecord(a));
+    for (int i = 0; i < iters; ++i) hipLaunchKernelGGL((k_copy<FENCE, REL>), dim3(grid), dim3(256), 0, 0, s, d, n);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    ms /= iters;
+    const double gbs = 2.0 * (double)n * 16 / (ms * 1e-3) / 1e9;
+    printf("{\"fence\": \"%s\", \"release\": %d, \"grid\": %d, \"ms\": %.4f, \"gbs\": %.1f, \"frac_of_8TBs\": %.4f}\n", name, REL, grid,
+           ms, gbs, gbs / 8000.0);
+    fflush(stdout);
+}
+
+int main() {
+    const long bytes = 256L << 20, n = bytes / 16;
+    u32x4 *s = nullptr, *d = nullptr;
+    CK(hipMalloc(&s, bytes));
+    CK(hipMalloc(&d, bytes));
+    CK(hipMemset(s, 1, bytes));
+    CK(hipMemset(d, 0, bytes));
+    const int full = (int)((n + 1023) / 1024);
+    for (int grid : {256, 512, 1024, 2048, 4096, full}) {
+        run<2, 1>("system", s, d, n, grid);
+        run<2, 0>("system", s, d, n, grid);
+        run<0, 0>("none", s, d, n, grid);
+    }
+    return 0;
+}
