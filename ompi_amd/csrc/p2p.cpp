@@ -150,6 +150,12 @@ struct p2p_state {
     // [size][kSlots] cells of kCell bytes, then [size][kSlots] 64-B lines of
     // receive copy counters (zeroed), allocated at first use
     char *eager = nullptr;
+    ipc_desc eager_d{};  // its export (made at allocation): a cell's is this one at the cell's offset
+    ipc_desc cell_desc(const char *cell) const {
+        ipc_desc d = eager_d;
+        d.off += (uint64_t)(cell - eager);
+        return d;
+    }
     uint32_t *recv_done(int src, uint64_t seq) {
         return reinterpret_cast<uint32_t *>(eager + (size_t)size * kSlots * kCell +
                                             ((size_t)src * kSlots + seq % kSlots) * 64);
@@ -446,12 +452,18 @@ static bool is_device(const void *ptr) { return ompi_amd_is_device_pointer(ptr) 
 // zeroed at the first device send or signalled receive.  Under p->mu.
 static int eager_area(p2p_state *p) {
     if (p->eager) return OMPI_AMD_SUCCESS;
-    ipc_desc d{};
     const size_t area = (size_t)p->size * kSlots * (kCell + 64);
-    int rc = comm_alloc_exportable(area, false, (void **)&p->eager, &d);
+    int rc = comm_alloc_exportable(area, false, (void **)&p->eager, &p->eager_d);
     if (rc == OMPI_AMD_SUCCESS) {  // every flag 0 (no sequence + 1 yet), every counter 0
-        rc = record_hip(hipMemset(p->eager, 0, area), "hipMemset (p2p eager area)");
-        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipDeviceSynchronize(), "hipDeviceSynchronize (eager area)");
+        // on a stream of its own that waits for nothing else: this can run
+        // inside a receive's progress while this process's earlier copy
+        // kernels still wait for peers (a device-wide or null-stream
+        // synchronisation here could wait on them, and they on this rank)
+        hipStream_t z = nullptr;
+        rc = record_hip(hipStreamCreateWithFlags(&z, hipStreamNonBlocking), "hipStreamCreate (eager area)");
+        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipMemsetAsync(p->eager, 0, area, z), "hipMemset (p2p eager area)");
+        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipStreamSynchronize(z), "hipStreamSynchronize (eager area)");
+        if (z) hip_ignore(hipStreamDestroy(z));
         if (rc != OMPI_AMD_SUCCESS) hip_ignore(hipFree(p->eager));
     }
     if (rc != OMPI_AMD_SUCCESS) p->eager = nullptr;
@@ -864,7 +876,7 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
             sg.mark_v = r->mark_v;
             crc = xfer_copy_sig(buf, st.buf, bytes, s, sg);
             if (crc == OMPI_AMD_SUCCESS && !r->mark) crc = record_copy(p, r);
-            if (crc == OMPI_AMD_SUCCESS) crc = comm_export(c, cell, &fd);
+            fd = p->cell_desc(cell);
             sflagged = true;
         } else {
             crc = copy_in(st.buf);
@@ -919,7 +931,9 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
         // application buffer comm_ipc_safe() accepted: the runtime answers
         // (DESIGN.md §4.6); a refusal is an error
         if (!eager) rc = producers_done();  // the receiver reads the buffer itself
-        if (rc == OMPI_AMD_SUCCESS) rc = comm_export(c, src, &d);
+        if (rc == OMPI_AMD_SUCCESS)
+            rc = eager ? (d = p->cell_desc(static_cast<const char *>(src)), OMPI_AMD_SUCCESS)
+                       : comm_export(c, src, &d);
         if (!eager && !staged) ++p->direct_sends;
     } else if (rc == OMPI_AMD_SUCCESS && bytes && dst == p->rank && !staged && !inl && !hstaged &&
                !eager) {
