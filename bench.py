@@ -211,6 +211,11 @@ def main():
                 res["next_rows_n1"] = coll_bench.single_gpu_rows()
             except Exception as e:  # noqa: BLE001
                 res["next_rows_n1_error"] = f"{type(e).__name__}: {e}"
+            try:  # BASELINE configs[1] / [2] at their top sizes; never breaks the headline
+                from ompi_amd import coll_bench
+                res["config_rows_n1"] = coll_bench.config_rows()
+            except Exception as e:  # noqa: BLE001
+                res["config_rows_n1_error"] = f"{type(e).__name__}: {e}"
     print(json.dumps(res), flush=True)
 
 

@@ -783,3 +783,91 @@ def single_gpu_rows(mib: int = 256):
         win.free()
         comm.free()
     return rows
+
+
+def config_rows():
+    """BASELINE configs[1] and configs[2] beside the N = 1 headline (bench.py
+    extras; the full sweeps are tools/op_sweep.py and tools/ddt_sweep.py).
+    Op: 3-buffer SUM / MAX / BAND over int32 / fp32 / fp64 at 64 MiB and
+    1 GiB per buffer, MAXLOC DOUBLE_INT at 1 GiB; algorithmic bytes 3 x n x
+    extent.  Convertor: one pack and one unpack call over 256 MiB packed for
+    vector bl 1 / 2 / 8 / 64 doubles (stride 2 x bl), blacs-style indexed
+    and struct {int, double}; algorithmic bytes 2 x packed.  Event-timed on
+    a dedicated stream, median of three batches."""
+    import statistics
+
+    import torch
+
+    from . import datatype as dd
+    from . import op as mop
+
+    s = torch.cuda.Stream()
+
+    def timed(fn, iters):
+        for _ in range(2):
+            fn()
+        s.synchronize()
+        vals = []
+        for _ in range(3):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(s)
+            for _ in range(iters):
+                fn()
+            b.record(s)
+            b.synchronize()
+            vals.append(a.elapsed_time(b) / iters)
+        return statistics.median(vals)
+
+    top = 1 << 30
+    a = torch.empty(top, dtype=torch.uint8, device="cuda").random_()
+    bb = torch.empty(top, dtype=torch.uint8, device="cuda").random_()
+    o = torch.empty(top, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    op_rows = []
+    cases = [(mop.MPI_SUM, mop.MPI_INT32_T), (mop.MPI_SUM, mop.MPI_FLOAT), (mop.MPI_SUM, mop.MPI_DOUBLE),
+             (mop.MPI_MAX, mop.MPI_INT32_T), (mop.MPI_MAX, mop.MPI_FLOAT), (mop.MPI_MAX, mop.MPI_DOUBLE),
+             (mop.MPI_BAND, mop.MPI_INT32_T), (mop.MPI_MAXLOC, mop.MPI_DOUBLE_INT)]
+    for op, dt in cases:
+        for nbytes in ((top,) if op is mop.MPI_MAXLOC else (64 << 20, top)):
+            n = nbytes // dt.extent
+            ms = timed(lambda: mop.reduce_local_3buff_async(a, bb, o, n, dt, op, stream=s),
+                       10 if nbytes == top else 40)
+            gbs = 3 * n * dt.extent / (ms * 1e-3) / 1e9
+            op_rows.append({"op": op.name, "type": dt.name, "bytes": nbytes, "ms": round(ms, 4),
+                            "hbm_gbs": round(gbs, 1), "frac_of_8TBs": round(gbs / 8000.0, 4)})
+    del a, bb, o
+    torch.cuda.empty_cache()
+
+    S = 256 << 20
+    d = dd.predefined("MPI_DOUBLE")
+    i32 = dd.predefined("MPI_INT")
+    lens = [13, 13, 13, 13, 13, 13, 12, 11, 10, 9, 8, 7, 6, 5, 4, 3, 2, 1]
+    disps = [286, 308, 330, 352, 374, 396, 419, 442, 465, 488, 511, 534, 557, 580, 603, 626, 649, 672]
+    types = [(f"vector_bl{bl}", dd.type_vector(S // (8 * bl), bl, 2 * bl, d), 1) for bl in (1, 2, 8, 64)]
+    blacs = dd.type_indexed(lens, disps, i32)
+    types.append(("blacs_indexed", blacs, S // blacs.size))
+    st = dd.type_struct([1, 1], [0, 8], [i32, d])
+    types.append(("struct_int_double", st, S // st.size))
+    ddt_rows = []
+    packed = torch.empty(S, dtype=torch.uint8, device="cuda")
+    for name, dt, count in types:
+        total = dt.size * count
+        typed = torch.empty((count - 1) * dt.extent + dt.true_span, dtype=torch.uint8,
+                            device="cuda").random_()
+        torch.cuda.synchronize()
+        for kind in ("pack", "unpack"):
+            def one():
+                cv = dd.Convertor()
+                if kind == "pack":
+                    cv.prepare_for_send(dt, count, typed, stream=s)
+                    cv.pack(packed.data_ptr(), total)
+                else:
+                    cv.prepare_for_recv(dt, count, typed, stream=s)
+                    cv.unpack(packed.data_ptr(), total)
+            ms = timed(one, 5)
+            gbs = 2 * total / (ms * 1e-3) / 1e9
+            ddt_rows.append({"type": name, "kind": kind, "packed_bytes": total, "ms": round(ms, 4),
+                             "hbm_gbs": round(gbs, 1), "frac_of_8TBs": round(gbs / 8000.0, 4)})
+        del typed
+        dt.free()
+    return {"configs1_op_3buff": op_rows, "configs2_convertor_256MiB": ddt_rows}
