@@ -146,6 +146,10 @@ struct p2p_state {
     bool unlinked = false;
     std::vector<uint64_t> scan_from;  // per source: first sequence possibly still POSTED
     std::deque<ompi_amd_p2p_request *> recvs;  // posted receives not matched yet
+    // matched receives whose copy may still run: progress completes them
+    // (FIN to the sender) whatever call drives it, so a rank blocked in a
+    // send on a full ring still frees its peers' slots (MPI progress)
+    std::vector<ompi_amd_p2p_request *> matched;
     std::recursive_mutex mu;
     // [size][kSlots] cells of kCell bytes, then [size][kSlots] 64-B lines of
     // receive copy counters (zeroed), allocated at first use
@@ -473,9 +477,17 @@ static int eager_area(p2p_state *p) {
 static bool tag_ok(int want, int have) { return want == OMPI_AMD_ANY_TAG || want == have; }
 
 // The earliest POSTED message from `s` a receive with `tag` matches.
-static msg_slot *find_from(p2p_state *p, int s, int tag) {
+// snap: the published counts one matching pass works with (loaded at the
+// pass's first look at each source, ~0 = not yet): senders publish
+// concurrently, and a message published while the pass is between two
+// receives must not go to the later one when the earlier one also matches
+// it (MPI's posting order; found by the ring-wrap test at N = 8).  NULL:
+// the count as it is now (a probe).
+constexpr uint64_t kNoSnap = ~0ull;
+static msg_slot *find_from(p2p_state *p, int s, int tag, uint64_t *snap) {
     pair_q &q = p->pair(s, p->rank);
-    const uint64_t posted = q.posted.load(std::memory_order_acquire);
+    if (snap && snap[s] == kNoSnap) snap[s] = q.posted.load(std::memory_order_acquire);
+    const uint64_t posted = snap ? snap[s] : q.posted.load(std::memory_order_acquire);
     uint64_t &from = p->scan_from[(size_t)s];
     // skip the prefix that is no longer POSTED (matched or recycled)
     while (from < posted) {
@@ -491,14 +503,14 @@ static msg_slot *find_from(p2p_state *p, int s, int tag) {
     return nullptr;
 }
 
-static msg_slot *find(p2p_state *p, int src, int tag, int *from_rank) {
+static msg_slot *find(p2p_state *p, int src, int tag, int *from_rank, uint64_t *snap = nullptr) {
     if (src != OMPI_AMD_ANY_SOURCE) {
         *from_rank = src;
-        return find_from(p, src, tag);
+        return find_from(p, src, tag, snap);
     }
     for (int k = 0; k < p->size; ++k) {
         const int s = (p->rank + k) % p->size;  // self first, then rank+1, ...
-        if (msg_slot *m = find_from(p, s, tag)) {
+        if (msg_slot *m = find_from(p, s, tag, snap)) {
             *from_rank = s;
             return m;
         }
@@ -545,8 +557,21 @@ static bool mark_landed(ompi_amd_p2p_request *r) {
     return true;
 }
 
+// OMPI_AMD_P2P_TRACE=1 (diagnostics): one stderr line per post, match and FIN.
+static bool p2p_trace() {
+    static const bool on = [] {
+        const char *v = getenv("OMPI_AMD_P2P_TRACE");
+        return v && atoi(v) != 0;
+    }();
+    return on;
+}
+
 // Claim `m` for receive `r` and launch its copy.
 static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s) {
+    if (p2p_trace())
+        fprintf(stderr, "[p2p %d] match req %p cap %zu <- src %d seq %llu tag %d bytes %llu inl %u state %u\n",
+                p->rank, (void *)r, r->cap, s, (unsigned long long)m->seq, m->tag, (unsigned long long)m->bytes,
+                m->inl, m->state.load());
     m->state.store(S_MATCHED, std::memory_order_release);
     r->matched = true;
     r->slot = m;
@@ -557,8 +582,8 @@ static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s
     if (n > r->cap) {  // MPI_ERR_TRUNCATE: copy what fits (ob1 does the same)
         n = r->cap;
         r->rc = OMPI_AMD_ERR_TRUNCATE;
-        record_msg("p2p receive truncated: message %llu bytes, buffer %zu",
-                   (unsigned long long)m->bytes, r->cap);
+        record_msg("p2p receive truncated: message %llu bytes, buffer %zu (source %d, tag %d, seq %llu)",
+                   (unsigned long long)m->bytes, r->cap, s, m->tag, (unsigned long long)m->seq);
     }
     r->st.error = r->rc;
     if (n == 0) return;
@@ -632,17 +657,65 @@ static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s
 }
 
 // Match posted receives against published messages, in posting order.
+// A matched receive whose copy finished: release what it held, check the
+// communicator's error (an eager wait that timed out copied nothing), FIN.
+// false while the copy still runs.  Under p->mu.
+static bool finish_recv(p2p_state *p, ompi_amd_p2p_request *r) {
+    bool copied = true;
+    if (r->mark) {
+        copied = mark_landed(r);
+    } else if (r->ev) {
+        const hipError_t e = hipEventQuery(r->ev);
+        if (e == hipErrorNotReady) {
+            copied = false;
+        } else if (e != hipSuccess) {
+            r->rc = r->st.error = record_hip(e, "p2p copy");
+        }
+    }
+    if (!copied) return false;
+    if (r->pinned) comm_unpin(p->c, r->pinned);
+    if (r->pinned2) comm_unpin(p->c, r->pinned2);
+    r->pinned = r->pinned2 = nullptr;
+    if (r->has_rstage) {
+        p->recv_free.push_back(r->rstage);
+        r->has_rstage = false;
+    }
+    if ((r->slot->inl == 3 || r->slot->inl == 4) && r->rc == OMPI_AMD_SUCCESS) {
+        const int se = comm_sticky(p->c);
+        if (se != OMPI_AMD_SUCCESS) r->rc = r->st.error = se;
+    }
+    if (p2p_trace())
+        fprintf(stderr, "[p2p %d] FIN req %p seq %llu state %u\n", p->rank, (void *)r,
+                (unsigned long long)r->slot->seq, r->slot->state.load());
+    r->slot->state.store(S_DONE, std::memory_order_release);  // the FIN
+    r->done = true;
+    return true;
+}
+
+// Match posted receives against published messages, in posting order, and
+// complete matched receives whose copies are over.  Under p->mu.
 static void progress(p2p_state *p) {
+    uint64_t snap[OMPI_AMD_MAX_RANKS];
+    for (int k = 0; k < p->size; ++k) snap[k] = kNoSnap;
     for (auto it = p->recvs.begin(); it != p->recvs.end();) {
         ompi_amd_p2p_request *r = *it;
         int s = -1;
-        msg_slot *m = find(p, r->src, r->tag, &s);
+        msg_slot *m = find(p, r->src, r->tag, &s, snap);
         if (!m) {
             ++it;
             continue;
         }
         start_recv(p, r, m, s);
+        p->matched.push_back(r);
         it = p->recvs.erase(it);
+    }
+    for (size_t i = 0; i < p->matched.size();) {
+        if (finish_recv(p, p->matched[i])) {
+            p->matched[i] = p->matched.back();
+            p->matched.pop_back();
+        } else {
+            ++i;
+        }
     }
 }
 
@@ -667,36 +740,8 @@ static int test_one(ompi_amd_p2p_request *r, bool *done) {
     } else if (r->is_send) {
         msg_slot &m = p->pair(p->rank, r->peer).slot[r->seq % kSlots];
         if (m.seq != r->seq || m.state.load(std::memory_order_acquire) == S_DONE) r->done = true;
-    } else if (r->matched) {
-        bool copied = true;
-        if (r->mark) {
-            copied = mark_landed(r);
-        } else if (r->ev) {
-            const hipError_t e = hipEventQuery(r->ev);
-            if (e == hipErrorNotReady) {
-                copied = false;
-            } else if (e != hipSuccess) {
-                r->rc = r->st.error = record_hip(e, "p2p copy");
-            }
-        }
-        if (copied) {
-            if (r->pinned) comm_unpin(p->c, r->pinned);
-            if (r->pinned2) comm_unpin(p->c, r->pinned2);
-            r->pinned = r->pinned2 = nullptr;
-            if (r->has_rstage) {
-                p->recv_free.push_back(r->rstage);
-                r->has_rstage = false;
-            }
-            // an eager receive whose wait for the sender's flag timed out
-            // copied nothing: the communicator's error says so
-            if ((r->slot->inl == 3 || r->slot->inl == 4) && r->rc == OMPI_AMD_SUCCESS) {
-                const int se = comm_sticky(p->c);
-                if (se != OMPI_AMD_SUCCESS) r->rc = r->st.error = se;
-            }
-            r->slot->state.store(S_DONE, std::memory_order_release);  // the FIN
-            r->done = true;
-        }
     }
+    // a matched receive completes in progress() above (finish_recv)
     *done = r->done;
     return r->done ? r->rc : OMPI_AMD_SUCCESS;
 }
@@ -952,6 +997,9 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     m.d = d;
     m.fd = fd;
     m.inl = inl ? 1u : hstaged ? 2u : flagged ? 3u : sflagged ? 4u : 0u;
+    if (p2p_trace())
+        fprintf(stderr, "[p2p %d] post -> dst %d seq %llu tag %d bytes %zu inl %u\n", p->rank, dst,
+                (unsigned long long)seq, tag, bytes, m.inl);
     m.state.store(S_POSTED, std::memory_order_release);
     q.posted.store(seq + 1, std::memory_order_release);
     r->seq = seq;
@@ -980,6 +1028,8 @@ int ompi_amd_irecv(ompi_amd_comm_t *c, void *buf, size_t bytes, int src, int tag
     r->cap = bytes;
     r->src = src;
     r->tag = tag;
+    if (p2p_trace())
+        fprintf(stderr, "[p2p %d] irecv req %p cap %zu src %d tag %d\n", p->rank, (void *)r, bytes, src, tag);
     r->stream = as_stream(stream);
     std::lock_guard<std::recursive_mutex> g(p->mu);
     p->recvs.push_back(r);

@@ -151,6 +151,48 @@ def case_same_tag_order(comm, rank, n, salt, k=40):
     return not fails, "; ".join(fails[:3])
 
 
+def case_ring_wraps(comm, rank, n, salt, k=150):
+    """k isends to the next rank before any receive is posted, alternating
+    eager (<= 4 KiB) and staged sizes from device buffers: the 64-slot
+    ring wraps twice, so eager cells, their flag words (seq + 1) and the
+    staged copies' completion counters are reused while earlier messages'
+    copy kernels may still run (a sender waits for its slot's FIN).  The
+    receives come in sending order; every byte checked."""
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    sizes = [3001 if i % 2 == 0 else 96 * 1024 + 7 * i for i in range(k)]
+    sends = [dev(payload(rank, salt + i, b)) for i, b in enumerate(sizes)]
+    reqs = []
+    fails = []
+    got = 0
+    rbufs = [zeros(b) for b in sizes]
+    rreqs = []
+    for i in range(k):
+        reqs.append(pml.isend(comm, sends[i], nxt, 11, stream=STREAM))
+        # keep receives ~48 behind: the 65th unmatched send would wait for a slot
+        if i >= 48:
+            rreqs.append(pml.irecv(comm, rbufs[got], prv, 11, stream=STREAM))
+            got += 1
+    while got < k:
+        rreqs.append(pml.irecv(comm, rbufs[got], prv, 11, stream=STREAM))
+        got += 1
+    for i, rq in enumerate(rreqs):
+        try:
+            st = rq.wait()
+        except _lib.OmpiAmdError as e:
+            return False, f"receive {i} of {k} ({sizes[i]} B): {e}"
+        if st.bytes != sizes[i]:
+            fails.append(f"msg {i}: {st.bytes} bytes")
+            continue
+        ok, msg = eq(host(rbufs[i]), payload(prv, salt + i, sizes[i]), f"msg {i}")
+        if not ok:
+            fails.append(msg)
+        rq.free()
+    for rq in reqs:
+        rq.wait()
+        rq.free()
+    return not fails, "; ".join(fails[:3])
+
+
 def case_recv_timeout_cancel(comm, rank, n, salt):
     """A receive that times out is withdrawn: the message sent
     after the timeout is not copied into the abandoned buffer, and the next
@@ -1065,6 +1107,7 @@ def main():
         ("p2p_aged_buffer_staged", lambda: case_aged_buffer_staged(comm, rank, n, 6)),
         ("p2p_tags_out_of_order", lambda: case_tags_out_of_order(comm, rank, n, 6)),
         ("p2p_same_tag_order", lambda: case_same_tag_order(comm, rank, n, 20)),
+        ("p2p_ring_wraps_eager_and_staged", lambda: case_ring_wraps(comm, rank, n, 400)),
         ("p2p_any_source_any_tag", lambda: case_any_source(comm, rank, n, 70)),
         ("p2p_probe_truncate", lambda: case_probe_truncate(comm, rank, n, 71)),
         ("p2p_self", lambda: case_self(comm, rank, n, 72)),
