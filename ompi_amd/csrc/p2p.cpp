@@ -127,6 +127,7 @@ struct stage {
     char *buf = nullptr;
     size_t cap = 0;
     ipc_desc d{};
+    bool arena = false;  // a range of the communicator's exported arena (freed with it)
 };
 
 struct p2p_state {
@@ -356,8 +357,11 @@ void p2p_destroy(p2p_state *p) {
     if (p->eager) hip_ignore(hipFree(p->eager));
     for (hipEvent_t e : p->ev_free) hip_ignore(hipEventDestroy(e));
     // the communicator's final rendezvous has passed: no peer reads a stage
-    for (auto &f : p->staged) hip_ignore(hipFree(f.st.buf));
-    for (auto &st : p->send_free) hip_ignore(hipFree(st.buf));
+    // (arena stages went with the communicator's arena)
+    for (auto &f : p->staged)
+        if (!f.st.arena) hip_ignore(hipFree(f.st.buf));
+    for (auto &st : p->send_free)
+        if (!st.arena) hip_ignore(hipFree(st.buf));
     for (auto &st : p->recv_free) hip_ignore(hipFree(st.buf));
     if (p->rank == 0) p2p_unlink(p);
     delete p;
@@ -440,7 +444,18 @@ static bool take_stage(p2p_state *p, std::vector<stage> &pool, size_t bytes, boo
     stage st;
     st.cap = cls;
     if (exported) {
-        if (comm_alloc_exportable(cls, false, (void **)&st.buf, &st.d) != OMPI_AMD_SUCCESS) return false;
+        // from the communicator's exported arena: its chunks grow
+        // geometrically and each is exported once, so a receiver maps a
+        // handful of chunks instead of one allocation (of at least the 4 MiB
+        // IPC minimum) per stage; past the arena's limit, one of its own
+        void *m = nullptr;
+        if (comm_arena_alloc(p->c, cls, &m) == OMPI_AMD_SUCCESS && comm_export(p->c, m, &st.d) == OMPI_AMD_SUCCESS) {
+            st.buf = static_cast<char *>(m);
+            st.arena = true;
+        } else {
+            if (m) comm_arena_free(p->c, m);
+            if (comm_alloc_exportable(cls, false, (void **)&st.buf, &st.d) != OMPI_AMD_SUCCESS) return false;
+        }
         p->stage_bytes += cls;
     } else if (hipMalloc((void **)&st.buf, cls) != hipSuccess) {
         (void)hipGetLastError();

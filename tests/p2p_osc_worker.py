@@ -243,6 +243,41 @@ def case_any_source(comm, rank, n, salt):
     return seen == set(range(1, n)), f"sources {sorted(seen)}"
 
 
+def case_fan_in_any_source(comm, rank, n, salt, k=40):
+    """Every rank but 0 isends k messages to rank 0 (eager and staged sizes
+    alternating, tags cycling 0..2); rank 0 posts all (n-1)*k receives as
+    ANY_SOURCE / ANY_TAG at once, while the senders publish: every message
+    arrives exactly once, intact, and per source in sending order
+    (MPI's non-overtaking rule across wildcard receives)."""
+    size_of = lambda i: 1000 + i if i % 2 == 0 else 70000 + i
+    if rank != 0:
+        sends = [dev(payload(rank, salt + i, size_of(i))) for i in range(k)]
+        reqs = [pml.isend(comm, sends[i], 0, i % 3, stream=STREAM) for i in range(k)]
+        for rq in reqs:
+            rq.wait()
+            rq.free()
+        return True, ""
+    total = (n - 1) * k
+    bufs = [zeros(80000) for _ in range(total)]
+    rreqs = [pml.irecv(comm, bufs[j], pml.ANY_SOURCE, pml.ANY_TAG, stream=STREAM) for j in range(total)]
+    last = {}
+    seen = set()
+    for j, rq in enumerate(rreqs):
+        st = rq.wait()
+        i = st.bytes - 1000 if st.bytes < 70000 else st.bytes - 70000
+        if not 0 <= i < k or size_of(i) != st.bytes or st.tag != i % 3 or (st.source, i) in seen:
+            return False, f"receive {j}: status {st}"
+        if last.get(st.source, -1) >= i:
+            return False, f"receive {j}: message {i} of rank {st.source} after message {last[st.source]}"
+        last[st.source] = i
+        seen.add((st.source, i))
+        ok, msg = eq(host(bufs[j])[:st.bytes], payload(st.source, salt + i, st.bytes), f"{st.source}:{i}")
+        if not ok:
+            return ok, msg
+        rq.free()
+    return len(seen) == total, f"{len(seen)} of {total} messages"
+
+
 def case_probe_truncate(comm, rank, n, salt):
     """probe reports the size; a short receive raises MPI_ERR_TRUNCATE with
     the prefix delivered; traffic continues afterwards."""
@@ -1109,6 +1144,7 @@ def main():
         ("p2p_same_tag_order", lambda: case_same_tag_order(comm, rank, n, 20)),
         ("p2p_ring_wraps_eager_and_staged", lambda: case_ring_wraps(comm, rank, n, 400)),
         ("p2p_any_source_any_tag", lambda: case_any_source(comm, rank, n, 70)),
+        ("p2p_fan_in_any_source_order", lambda: case_fan_in_any_source(comm, rank, n, 500)),
         ("p2p_probe_truncate", lambda: case_probe_truncate(comm, rank, n, 71)),
         ("p2p_self", lambda: case_self(comm, rank, n, 72)),
         ("p2p_recv_timeout_cancel", lambda: case_recv_timeout_cancel(comm, rank, n, 75)),
