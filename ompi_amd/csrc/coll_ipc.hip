@@ -1108,10 +1108,22 @@ static void note_stream(ompi_amd_comm_t *c, hipStream_t s) {
         return;
     }
     if (c->has_stream) {
+        // the communicator's calls run one after the other on the device
+        // whatever streams they were issued on (MPI orders a communicator's
+        // collectives; the staged calls' scratch halves, the barrier rows and
+        // the landing buffers are reused call after call on that premise):
+        // the new stream waits for the last one's work so far
+        // (hipStreamLegacy, the C ABI's spelling of the legacy null
+        // stream, as the null handle: hipStreamWaitEvent does not take it)
+        auto plain = [](hipStream_t x) { return x == hipStreamLegacy ? nullptr : x; };
         hipEvent_t e = nullptr;
         if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) {
-            if (hipEventRecord(e, c->cur_stream) == hipSuccess) c->stream_evs.push_back(e);
-            else hip_ignore(hipEventDestroy(e));
+            if (hipEventRecord(e, plain(c->cur_stream)) == hipSuccess) {
+                hip_ignore(hipStreamWaitEvent(plain(s), e, 0));
+                c->stream_evs.push_back(e);
+            } else {
+                hip_ignore(hipEventDestroy(e));
+            }
         }
         // forget marks that have fired
         for (auto it = c->stream_evs.begin(); c->stream_evs.size() > 8 && it != c->stream_evs.end();) {

@@ -28,8 +28,13 @@ const char *ipc_mode_env_now();
 // The stream handlers of this thread run on (ompi_amd_set_thread_stream).
 hipStream_t thread_stream();
 // `void *` stream argument of the C ABI -> hipStream_t (NULL = per-thread).
+// The C ABI's stream argument: NULL = this thread's per-thread stream;
+// hipStreamLegacy (1) = the legacy null stream, passed on as the null handle
+// (hipStreamWaitEvent does not accept the special handle; this library is
+// built with the legacy default stream, so both name the same stream).
 inline hipStream_t as_stream(void *s) {
-    return s ? static_cast<hipStream_t>(s) : hipStreamPerThread;
+    if (!s) return hipStreamPerThread;
+    return static_cast<hipStream_t>(s) == hipStreamLegacy ? nullptr : static_cast<hipStream_t>(s);
 }
 
 int op_set_max_blocks(int64_t v);

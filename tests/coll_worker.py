@@ -787,6 +787,74 @@ def case_iallreduce_many(comm, rank, n, salt, calls=12):
     return not msgs, "; ".join(msgs)
 
 
+def case_small_marks_two_streams(comm, rank, n, salt, rounds=6):
+    """Small allreduces whose fused kernels store their own completion marks
+    (blocking, nonblocking and persistent: one flag-page counter slot per
+    call in flight): per round, eight MPI_Iallreduce calls
+    alternating between two streams, two persistent plans started on
+    either stream, and a blocking call, all outstanding together; waited
+    in reverse order (requests by test polling for half of them); every
+    result bit-exact against the oracle, and the plans' counter slots
+    reused round after round."""
+    F, I32 = mop.MPI_FLOAT, mop.MPI_INT32_T
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    sizes = [1, 7, 1000, 4099, 16384, 3, 65537 // 4, 2]
+    pa_x = [inputs(F, 777, r, salt + 100) for r in range(n)]
+    pb_x = [inputs(I32, 5000, r, salt + 101) for r in range(n)]
+    pa_s, pb_s = to_dev(pa_x[rank]), to_dev(pb_x[rank])
+    pa_o, pb_o = torch.zeros_like(pa_s), torch.zeros_like(pb_s)
+    pa_exp, _ = orc.allreduce([x.copy() for x in pa_x], 777, mop.MPI_SUM.index, F.code)
+    pb_exp, _ = orc.allreduce([x.copy() for x in pb_x], 5000, mop.MPI_MAX.index, I32.code)
+    pa = comm.allreduce_init(pa_s, pa_o, 777, F, mop.MPI_SUM)
+    pb = comm.allreduce_init(pb_s, pb_o, 5000, I32, mop.MPI_MAX)
+    msgs = []
+    try:
+        for rd in range(rounds):
+            prepared = []
+            for i, cnt in enumerate(sizes):
+                xs = [inputs(F, cnt, r, salt + 10 * rd + i) for r in range(n)]
+                exp, _ = orc.allreduce([x.copy() for x in xs], cnt, mop.MPI_SUM.index, F.code)
+                x = to_dev(xs[rank])
+                prepared.append((cnt, x, torch.zeros_like(x), exp[rank]))
+            bx = [inputs(F, 33, r, salt + 10 * rd + 9) for r in range(n)]
+            bexp, _ = orc.allreduce([x.copy() for x in bx], 33, mop.MPI_SUM.index, F.code)
+            b_s = to_dev(bx[rank])
+            b_o = torch.zeros_like(b_s)
+            torch.cuda.synchronize()
+            reqs = [comm.iallreduce(x, o, cnt, F, mop.MPI_SUM, stream=(s1 if i % 2 == 0 else s2))
+                    for i, (cnt, x, o, _) in enumerate(prepared)]
+            pa.start(stream=s1 if rd % 2 == 0 else s2)
+            pb.start(stream=s2 if rd % 2 == 0 else s1)
+            comm.allreduce(b_s, b_o, 33, F, mop.MPI_SUM, blocking=True)
+            pb.wait()
+            pa.wait()
+            for i in reversed(range(len(reqs))):
+                if i % 2:
+                    while not reqs[i].test():
+                        pass
+                else:
+                    reqs[i].wait()
+            torch.cuda.synchronize()
+            for r in reqs:
+                r.free()
+            for i, (cnt, x, o, exp) in enumerate(prepared):
+                ok, msg = checked(o.cpu().numpy()[:cnt * 4].view(np.float32), exp)
+                if not ok:
+                    msgs.append(f"round {rd} call {i}: {msg}")
+            for what, got, exp in (("blocking", b_o.cpu().numpy()[:33 * 4].view(np.float32), bexp[rank]),
+                                   ("plan SUM", pa_o.cpu().numpy()[:777 * 4].view(np.float32), pa_exp[rank]),
+                                   ("plan MAX", pb_o.cpu().numpy()[:5000 * 4].view(np.int32), pb_exp[rank])):
+                ok, msg = checked(got, exp)
+                if not ok:
+                    msgs.append(f"round {rd} {what}: {msg}")
+            if msgs:
+                break
+    finally:
+        pa.free()
+        pb.free()
+    return not msgs, "; ".join(msgs[:3])
+
+
 def headline_input(rank: int, count: int, salt: int) -> np.ndarray:
     """Dataset E at full size without materialising every rank's vector:
     x_r[i] = (((i * 2654435761 + r * 40503 + salt) mod 2049) - 1024) * 2^-8,
@@ -1227,6 +1295,7 @@ def main():
         ("pipelined_schemes", lambda: case_pipe(comm, rank, n, 120, big)),
         ("iallreduce_mixed", lambda: case_iallreduce(comm, rank, n, 90)),
         ("iallreduce_many_outstanding", lambda: case_iallreduce_many(comm, rank, n, 94)),
+        ("small_marks_two_streams", lambda: case_small_marks_two_streams(comm, rank, n, 700)),
         ("persistent_small", lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, 3001, 80)),
         ("persistent_mid_inplace",
          lambda: case_persistent(comm, rank, n, D, mop.MPI_SUM, 70001, 81, inplace=True)),
