@@ -855,6 +855,106 @@ def case_small_marks_two_streams(comm, rank, n, salt, rounds=6):
     return not msgs, "; ".join(msgs[:3])
 
 
+def case_random_sequence(comm, rank, n, salt, calls=48):
+    """A seeded random sequence (the same on every rank) of blocking-form
+    collectives enqueued without any wait between them — allreduce, reduce
+    (random root, sometimes in place), scan, exscan, reduce_scatter_block,
+    reduce_scatter (uneven counts), allgather, bcast (random root) — plus
+    MPI_Iallreduce requests waited only at the end; sizes from one element
+    to past the zero-copy threshold, fp32 SUM / int32 MAX / fp64 SUM.  Every
+    call's per-call resources (scratch halves, landing slots, barrier rows,
+    shadows) are reused by the next ones while earlier calls may still run;
+    every result is checked against the oracle after one synchronisation."""
+    F, D, I32 = mop.MPI_FLOAT, mop.MPI_DOUBLE, mop.MPI_INT32_T
+    rng = np.random.default_rng(4242 + salt)
+    kinds = ["allreduce", "iallreduce", "reduce", "scan", "exscan", "rsb", "rs", "allgather", "bcast"]
+    sizes = [1, 7, 2500, 70001, 300007, (1 << 20) // 4 + 3]
+    types = [(F, mop.MPI_SUM), (I32, mop.MPI_MAX), (D, mop.MPI_SUM)]
+    checks, reqs, keep = [], [], []
+    for c in range(calls):
+        kind = kinds[rng.integers(len(kinds))]
+        cnt = int(sizes[rng.integers(len(sizes))])
+        dt, op = types[rng.integers(len(types))]
+        root = int(rng.integers(n))
+        inplace = bool(rng.integers(2))
+        sl = salt + 100 * c
+        if kind in ("allreduce", "iallreduce"):
+            xs = [inputs(dt, cnt, r, sl) for r in range(n)]
+            exp, _ = orc.allreduce([x.copy() for x in xs], cnt, op.index, dt.code)
+            x = to_dev(xs[rank])
+            o = torch.zeros_like(x)
+            if kind == "allreduce":
+                comm.allreduce(x, o, cnt, dt, op)
+            else:
+                reqs.append(comm.iallreduce(x, o, cnt, dt, op))
+            checks.append((c, kind, o, cnt, dt, exp[rank]))
+            keep.append(x)
+        elif kind == "reduce":
+            xs = [inputs(dt, cnt, r, sl) for r in range(n)]
+            exp, _ = orc.reduce([x.copy() for x in xs], cnt, op.index, dt.code, root, inplace)
+            x = to_dev(xs[rank])
+            if rank == root:
+                o = x if inplace else torch.zeros_like(x)
+                comm.reduce(coll.IN_PLACE if inplace else x, o, cnt, dt, op, root)
+                checks.append((c, kind, o, cnt, dt, exp))
+            else:
+                comm.reduce(x, None, cnt, dt, op, root)
+            keep.append(x)
+        elif kind in ("scan", "exscan"):
+            xs = [inputs(dt, cnt, r, sl) for r in range(n)]
+            exp = orc.scan([x.copy() for x in xs], cnt, op.index, dt.code, kind == "exscan")
+            x = to_dev(xs[rank])
+            o = torch.zeros_like(x)
+            (comm.exscan if kind == "exscan" else comm.scan)(x, o, cnt, dt, op)
+            if not (kind == "exscan" and rank == 0):
+                checks.append((c, kind, o, cnt, dt, exp[rank]))
+            keep.append(x)
+        elif kind == "rsb":
+            rc = max(1, cnt // n)
+            xs = [inputs(dt, rc * n, r, sl) for r in range(n)]
+            exp = orc.reduce_scatter_block([x.copy() for x in xs], rc, op.index, dt.code)
+            x = to_dev(xs[rank])
+            o = torch.zeros(rc * dt.extent, dtype=torch.uint8, device="cuda")
+            comm.reduce_scatter_block(x, o, rc, dt, op)
+            checks.append((c, kind, o, rc, dt, exp[rank]))
+            keep.append(x)
+        elif kind == "rs":
+            rcounts = [max(0, cnt // n + (r * 7 % 5) - 2) for r in range(n)]
+            xs = [inputs(dt, sum(rcounts), r, sl) for r in range(n)]
+            exp, _ = orc.reduce_scatter([x.copy() for x in xs], rcounts, op.index, dt.code)
+            x = to_dev(xs[rank], extra=16)
+            o = torch.zeros((rcounts[rank] + 1) * dt.extent, dtype=torch.uint8, device="cuda")
+            comm.reduce_scatter(x, o, rcounts, dt, op)
+            checks.append((c, kind, o, rcounts[rank], dt, exp[rank]))
+            keep.append(x)
+        elif kind == "allgather":
+            nb = cnt * 4
+            xs = [inputs(F, cnt, r, sl) for r in range(n)]
+            x = to_dev(xs[rank])
+            o = torch.zeros(nb * n, dtype=torch.uint8, device="cuda")
+            comm.allgather(x, o, nb)
+            checks.append((c, kind, o, cnt * n, F, np.concatenate(xs)))
+            keep.append(x)
+        else:  # bcast
+            nb = cnt * 4
+            xs = inputs(F, cnt, root, sl)
+            b = to_dev(xs) if rank == root else torch.zeros(nb, dtype=torch.uint8, device="cuda")
+            comm.bcast(b, nb, root)
+            checks.append((c, kind, b, cnt, F, xs))
+    for r_ in reqs:
+        r_.wait()
+    torch.cuda.synchronize()
+    for r_ in reqs:
+        r_.free()
+    msgs = []
+    for c, kind, o, cnt, dt, exp in checks:
+        got = o.cpu().numpy()[:cnt * dt.extent].view(dt.np_dtype)
+        ok, msg = checked(got, np.asarray(exp).view(dt.np_dtype))
+        if not ok:
+            msgs.append(f"call {c} {kind} ({cnt} x {dt.name}): {msg}")
+    return not msgs, "; ".join(msgs[:3])
+
+
 def headline_input(rank: int, count: int, salt: int) -> np.ndarray:
     """Dataset E at full size without materialising every rank's vector:
     x_r[i] = (((i * 2654435761 + r * 40503 + salt) mod 2049) - 1024) * 2^-8,
@@ -1296,6 +1396,8 @@ def main():
         ("iallreduce_mixed", lambda: case_iallreduce(comm, rank, n, 90)),
         ("iallreduce_many_outstanding", lambda: case_iallreduce_many(comm, rank, n, 94)),
         ("small_marks_two_streams", lambda: case_small_marks_two_streams(comm, rank, n, 700)),
+        ("random_sequence", lambda: case_random_sequence(comm, rank, n, 800)),
+        ("random_sequence_user_ipc", user_ipc(lambda: case_random_sequence(comm, rank, n, 900))),
         ("persistent_small", lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, 3001, 80)),
         ("persistent_mid_inplace",
          lambda: case_persistent(comm, rank, n, D, mop.MPI_SUM, 70001, 81, inplace=True)),

@@ -851,6 +851,52 @@ def case_cas(comm, rank, n):
         win.free()
 
 
+def case_passive_acc_all_to_all(comm, rank, n, salt, count=20011, rounds=6):
+    """Passive target under contention: every round, every rank opens
+    lock_all and accumulates (SUM, exact data) its origin into the SAME
+    region of EVERY rank's window, flushes, closes; a second region takes a
+    put from the next rank under an exclusive lock of that target.  Every
+    target's accumulate lock serialises the n concurrent updates; after the
+    last round each window holds init + rounds x sum of the origins
+    (bit-exact: exact data) and the last put, checked after MPI_Win_sync."""
+    F = mop.MPI_FLOAT
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    init = fp_inputs(F, count, 99, salt, "E")
+    org = [fp_inputs(F, count, r, salt + 1, "E") for r in range(n)]
+    base = dev(np.concatenate([init, np.zeros(count, np.float32)]))
+    win = osc.Window.create(comm, base, base.numel(), disp_unit=4)
+    try:
+        o = dev(org[rank])
+        comm_barrier()
+        for rd in range(rounds):
+            win.lock_all(stream=STREAM)
+            for t in range(n):
+                win.accumulate(o, count, F, (rank + t) % n, 0, mop.MPI_SUM, stream=STREAM)
+            for t in range(n):
+                win.flush(t, stream=STREAM)
+            win.unlock_all(stream=STREAM)
+            mark = dev(np.full(count, rd * 1000 + rank, np.float32))
+            win.lock(nxt, osc.LOCK_EXCLUSIVE, stream=STREAM)
+            win.put(mark, nxt, count, count * 4, stream=STREAM)
+            win.unlock(nxt, stream=STREAM, blocking=True)
+        comm_barrier()
+        win.sync(stream=STREAM)
+        got = host(base).view(np.float32)
+        exp = init.copy()
+        total = np.zeros(count, np.float32)
+        for r in range(n):
+            orc.op_2buff(mop.MPI_SUM.index, F.code, org[r].copy(), total, count)
+        for _ in range(rounds):
+            orc.op_2buff(mop.MPI_SUM.index, F.code, total.copy(), exp, count)
+        ok, msg = eq(got[:count], exp, "accumulated region")
+        if not ok:
+            # exact data: any order gives the same bits; a difference is a lost or doubled update
+            return ok, msg
+        return eq(got[count:], np.full(count, (rounds - 1) * 1000 + prv, np.float32), "last put")
+    finally:
+        win.free()
+
+
 def case_passive_exclusive(comm, rank, n, k=10):
     """Read-modify-write of a counter under MPI_Win_lock(EXCLUSIVE): get,
     +1 on the device, put, unlock — k times per rank; final = n*k."""
@@ -1182,6 +1228,7 @@ def main():
         ("osc_fetch_and_op_counter", lambda: case_fetch_and_op_counter(comm, rank, n)),
         ("osc_compare_and_swap", lambda: case_cas(comm, rank, n)),
         ("osc_passive_exclusive_rmw", lambda: case_passive_exclusive(comm, rank, n)),
+        ("osc_passive_acc_all_to_all", lambda: case_passive_acc_all_to_all(comm, rank, n, 180)),
         ("osc_lock_all_get", lambda: case_lock_all(comm, rank, n, 93)),
         ("osc_pscw_ring", lambda: case_pscw_ring(comm, rank, n, 94)),
         ("osc_pscw_ring_test", lambda: case_pscw_ring(comm, rank, n, 95, epochs=2, use_test=True)),
