@@ -135,9 +135,82 @@ struct ddt_walk {
     int64_t size_g;                            // count * bg
 };
 
+struct ddt_step {
+    int64_t el, k, w;  // a constant advance of the walk, split like a position
+};
+__device__ __forceinline__ ddt_step walk_split(const ddt_walk &v, int64_t D) {
+    const int64_t q = D % v.size_g;
+    return {D / v.size_g, q / v.bg, q % v.bg};
+}
+__device__ __forceinline__ void walk_adv(const ddt_walk &v, int64_t &el, int64_t &k, int64_t &w,
+                                         const ddt_step &d) {
+    w += d.w;
+    k += d.k;
+    if (w >= v.bg) { w -= v.bg; ++k; }
+    if (k >= v.count) { k -= v.count; ++el; }
+    el += d.el;
+}
+
+// 16-B granules: chunked persistent shape (the xfer kernels'): workgroup b
+// moves chunks b, b + grid, ... of 256 x kVecChunkU packed granules, lane t
+// granules t, t + 256, ... of each, non-temporal on both sides.  The walk
+// advances by two constants (+256 granules inside a chunk, to the next chunk
+// after its last).  256 MiB packed, vector of 64-double runs at stride 128
+// (tools/ddt_vec_probe.hip, profiles/r05_ddt_vec_probe.jsonl): 0.640 of
+// 8 TB/s in the one-pass shape below, 0.764 chunked at 512 workgroups (a
+// contiguous copy in the same shape: 0.769).
+constexpr int kVecChunkU = 4;
+constexpr int kVecChunkGrid = 512;
+
+template <bool UNPACK>
+__device__ __forceinline__ void ddt_vec16_body(const ddt_walk &v, const char *src, char *dst,
+                                               const ddt_window &w) {
+    using T = typename granule<16>::t;
+    constexpr int U = kVecChunkU;
+    constexpr int64_t C = (int64_t)kDdtThreads * U;
+    int64_t j = (int64_t)blockIdx.x * C + threadIdx.x;
+    if (j >= w.ngran) return;
+    const ddt_step d1 = walk_split(v, kDdtThreads);
+    const ddt_step d2 = walk_split(v, (int64_t)gridDim.x * C - (int64_t)(U - 1) * kDdtThreads);
+    const int64_t pg0 = w.body0 / 16 + j;
+    int64_t el = pg0 / v.size_g;
+    const int64_t q = pg0 - el * v.size_g;
+    int64_t k = q / v.bg;
+    int64_t ww = q - k * v.bg;
+    for (; j < w.ngran; j += (int64_t)gridDim.x * C) {
+        int64_t toff[U];
+        T val[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            toff[u] = el * v.extent + v.disp + k * v.stride + ww * 16;
+            if (u + 1 < U) walk_adv(v, el, k, ww, d1);
+        }
+        walk_adv(v, el, k, ww, d2);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t jj = j + (int64_t)u * kDdtThreads;
+            const int64_t c = w.body0 + jj * 16 - w.start;
+            if (jj < w.ngran)
+                val[u] = __builtin_nontemporal_load(
+                    reinterpret_cast<const T *>(UNPACK ? src + c : src + toff[u]));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t jj = j + (int64_t)u * kDdtThreads;
+            const int64_t c = w.body0 + jj * 16 - w.start;
+            if (jj < w.ngran)
+                __builtin_nontemporal_store(val[u], reinterpret_cast<T *>(UNPACK ? dst + toff[u] : dst + c));
+        }
+    }
+}
+
 template <int G, bool UNPACK>
 __global__ __launch_bounds__(kDdtThreads) void ddt_vec_kernel(ddt_walk v, const char *src,
                                                               char *dst, ddt_window w) {
+    if constexpr (G == 16) {
+        ddt_vec16_body<UNPACK>(v, src, dst, w);
+        return;
+    }
     using T = typename granule<G>::t;
     constexpr int U = kDdtUnroll;
     const int64_t S = (int64_t)gridDim.x * kDdtThreads;  // granules per step
@@ -560,6 +633,9 @@ static hipError_t launch_vec(int G, const ddt_walk &v, const ddt_desc &d, const 
     if (w.ngran > 0) {
         int64_t blocks = (w.ngran + kDdtThreads * kDdtUnroll - 1) / (kDdtThreads * kDdtUnroll);
         blocks = std::max<int64_t>(1, std::min<int64_t>(blocks, 1 << 20));
+        if (G == 16)  // chunked persistent grid (ddt_vec16_body)
+            blocks = std::max<int64_t>(1, std::min<int64_t>(
+                kVecChunkGrid, (w.ngran + kDdtThreads * kVecChunkU - 1) / (kDdtThreads * kVecChunkU)));
         const dim3 grid((unsigned)blocks), block(kDdtThreads);
         switch (G) {
         case 16: hipLaunchKernelGGL((ddt_vec_kernel<16, UNPACK>), grid, block, 0, s, v, src, dst, w); break;

@@ -48,7 +48,7 @@ def bench_type(name, dt, count, chunks, top_iters=20):
                 pos += n
 
         for kind in ("pack", "unpack"):
-            iters = max(2, min(top_iters, (1 << 28) // max(total, 1)))
+            iters = max(10, min(top_iters, (1 << 28) // max(total, 1)))
             run(kind)
             torch.cuda.synchronize()
             vals = []
