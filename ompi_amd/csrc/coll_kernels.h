@@ -53,7 +53,12 @@ struct red_jobs { red_job j[2 * kMaxRanks]; int n; };
 struct cp_job { const char *src; char *dst; int64_t bytes; };
 struct cp_jobs { cp_job j[kMaxRanks]; int n; };
 
-__device__ __forceinline__ void sys_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
+// the acquiring lane waits for its invalidate before the barrier that
+// lets the other waves load (Guideline 16: the fence itself does not wait)
+__device__ __forceinline__ void sys_acquire() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 __device__ __forceinline__ void sys_release() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

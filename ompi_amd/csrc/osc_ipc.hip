@@ -74,7 +74,13 @@ struct peer_ctl_set {
     uint32_t *p[OMPI_AMD_MAX_RANKS];
 };
 
-__device__ __forceinline__ void osc_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, ""); }
+// The acquiring lane waits for its invalidate before the workgroup barrier
+// that usually follows: the other waves' loads must not pass it (the
+// fence's own lowering does not wait; cdna_hip_programming.md Guideline 16).
+__device__ __forceinline__ void osc_acquire() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
 __device__ __forceinline__ void osc_release() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -117,6 +123,26 @@ __device__ __forceinline__ bool gate_open(const uint32_t *gate) {
     return open != 0;
 }
 
+// The target's accumulate lock (opal_atomic_lock, osc_sm_comm.c:296-305):
+// spin on a compare-and-swap 0 -> 1 of its CTL_ACC word, bounded (sticky
+// timeout); false at once when the communicator already failed.
+__device__ __forceinline__ bool acc_lock_take(uint32_t *ctl, int *err, uint64_t ticks) {
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return false;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        uint32_t expect = 0;
+        if (__hip_atomic_compare_exchange_strong(ctl + CTL_ACC, &expect, 1u, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
+            return true;
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+            __hip_atomic_store(err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            return false;
+        }
+    }
+}
+
 // kind: 0 accumulate lock, 1 accumulate unlock, 2 start_exclusive,
 // 3 end_exclusive, 4 start_shared, 5 end_shared (osc_sm_passive_target.c:57-110)
 // taken: this rank's CTL_TAKEN_* word for the target (its own control page).
@@ -134,27 +160,10 @@ __global__ __launch_bounds__(64) void lock_kernel(uint32_t *ctl, int kind, int *
     // would otherwise free another rank's lock)
     if ((kind == 1 || kind == 3 || kind == 5) && ld_sys(taken) != 1u) return;
     switch (kind) {
-    case 0: {  // opal_atomic_lock: spin on a compare-and-swap 0 -> 1
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        uint32_t got = 0;
-        for (;;) {
-            uint32_t expect = 0;
-            if (__hip_atomic_compare_exchange_strong(ctl + CTL_ACC, &expect, 1u, __ATOMIC_RELAXED,
-                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
-                got = 1;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
-                __hip_atomic_store(err, (int)OMPI_AMD_ERR_TIMEOUT, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-                break;
-            }
-        }
-        st_sys(taken, got);
+    case 0:  // opal_atomic_lock
+        st_sys(taken, acc_lock_take(ctl, err, ticks) ? 1u : 0u);
         osc_acquire();
         break;
-    }
     case 1:
         osc_release();
         __hip_atomic_store(ctl + CTL_ACC, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -392,12 +401,14 @@ __global__ __launch_bounds__(THREADS) void xfer_sig_kernel(const char *src, char
 }
 
 // Compare-and-swap of one element of `size` data bytes (osc_sm_comm.c:386-396).
+// Under the target's accumulate lock, taken and released in this one launch
+// (as rma_small_kernel).
 __global__ __launch_bounds__(64) void cas_kernel(const unsigned char *origin,
                                                  const unsigned char *compare,
                                                  unsigned char *result, unsigned char *target,
-                                                 int size, const uint32_t *gate) {
+                                                 int size, uint32_t *ctl, int *err, uint64_t ticks) {
     if (threadIdx.x != 0) return;
-    if (ld_sys(const_cast<uint32_t *>(gate)) != 1u) return;
+    if (!acc_lock_take(ctl, err, ticks)) return;
     osc_acquire();
     unsigned char old[16];
     bool same = true;
@@ -409,6 +420,7 @@ __global__ __launch_bounds__(64) void cas_kernel(const unsigned char *origin,
     if (same)
         for (int b = 0; b < size; ++b) target[b] = origin[b];
     osc_release();
+    __hip_atomic_store(ctl + CTL_ACC, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 using acc_launch_fn = hipError_t (*)(dim3, const void *, void *, int64_t, int, const uint32_t *,
@@ -437,6 +449,87 @@ make_acc_table(std::integer_sequence<int, O...>) {
     return {{make_acc_row<O>(std::make_integer_sequence<int, OMPI_AMD_TYPE_COUNT>{})...}};
 }
 static const auto g_acc = make_acc_table(std::make_integer_sequence<int, OMPI_AMD_OP_COUNT>{});
+
+// Small accumulate-lock operations in ONE single-workgroup launch: take the
+// target's accumulate lock, fetch the old elements (get_accumulate /
+// fetch_and_op), combine or replace, release, unlock — osc_sm_comm.c's
+// opal_atomic_lock / copy + ompi_op_reduce / opal_atomic_unlock sequence
+// (:296-305, :340-356, :424-438) with the lock held inside one kernel
+// instead of across three or four launches (lock, fetch copy, op, unlock).
+// MODE: 0 replace, 1 combine with OP, 2 fetch only (NO_OP).  T: the
+// element type (MODE 1) or the widest granule both pointers and the byte
+// count allow (MODE 0 / 2: bytes move unchanged).
+enum { RMA_REPLACE = 0, RMA_COMBINE = 1, RMA_FETCH = 2 };
+constexpr size_t kRmaSmallBytes = 16 << 10;
+
+template <typename T, int OP, int MODE>
+__global__ __launch_bounds__(kOscThreads) void rma_small_kernel(const T *origin, T *result, T *target,
+                                                                int64_t n, uint32_t *ctl, int *err,
+                                                                uint64_t ticks) {
+    __shared__ int ok;
+    if (threadIdx.x == 0) {
+        ok = acc_lock_take(ctl, err, ticks) ? 1 : 0;
+        if (ok) osc_acquire();
+    }
+    __syncthreads();
+    if (!ok) return;
+    for (int64_t i = threadIdx.x; i < n; i += kOscThreads) {
+        const T old = target[i];
+        if (result) result[i] = old;
+        if constexpr (MODE == RMA_REPLACE) {
+            target[i] = origin[i];
+        } else if constexpr (MODE == RMA_COMBINE) {
+            store_elem(target + i, opfn<OP, false>::f(old, origin[i]));
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        osc_release();
+        __hip_atomic_store(ctl + CTL_ACC, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+using rma_small_fn = hipError_t (*)(const void *, void *, void *, int64_t, uint32_t *, int *, uint64_t,
+                                    hipStream_t);
+
+template <typename T, int OP, int MODE>
+static hipError_t rma_small_launch(const void *o, void *r, void *t, int64_t n, uint32_t *ctl, int *err,
+                                   uint64_t ticks, hipStream_t s) {
+    hipLaunchKernelGGL((rma_small_kernel<T, OP, MODE>), dim3(1), dim3(kOscThreads), 0, s,
+                       static_cast<const T *>(o), static_cast<T *>(r), static_cast<T *>(t), n, ctl, err,
+                       ticks);
+    return hipGetLastError();
+}
+template <int OP, int TYPE>
+static constexpr rma_small_fn rma_small_slot() {
+    if constexpr (slot_supported(OP, TYPE))
+        return &rma_small_launch<typename type_of<TYPE>::type, OP, RMA_COMBINE>;
+    else
+        return nullptr;
+}
+template <int OP, int... T>
+static constexpr std::array<rma_small_fn, OMPI_AMD_TYPE_COUNT> make_small_row(std::integer_sequence<int, T...>) {
+    return {{rma_small_slot<OP, T>()...}};
+}
+template <int... O>
+static constexpr std::array<std::array<rma_small_fn, OMPI_AMD_TYPE_COUNT>, OMPI_AMD_OP_COUNT>
+make_small_table(std::integer_sequence<int, O...>) {
+    return {{make_small_row<O>(std::make_integer_sequence<int, OMPI_AMD_TYPE_COUNT>{})...}};
+}
+static const auto g_rma_small = make_small_table(std::make_integer_sequence<int, OMPI_AMD_OP_COUNT>{});
+
+// replace / fetch-only by granule (16, 8, 4, 2, 1 bytes)
+template <int MODE>
+static rma_small_fn rma_small_bytes_fn(int g) {
+    switch (g) {
+    case 16: return &rma_small_launch<u32x4, 0, MODE>;
+    case 8: return &rma_small_launch<uint64_t, 0, MODE>;
+    case 4: return &rma_small_launch<uint32_t, 0, MODE>;
+    case 2: return &rma_small_launch<uint16_t, 0, MODE>;
+    default: return &rma_small_launch<uint8_t, 0, MODE>;
+    }
+}
 
 // ---- derived datatypes at the target (ompi_osc_base_sndrcv_op,
 // osc_base_obj_convert.c:160-245): the origin's packed stream of primitive
@@ -826,6 +919,16 @@ static hipStream_t win_stream(ompi_amd_win_t *w, void *stream) {
     return s;
 }
 
+// rma_op's single-launch form (rma_small_kernel) up to this many bytes;
+// OMPI_AMD_OSC_SMALL_BYTES overrides, 0 turns it off.
+static size_t rma_small_bytes() {
+    static const size_t v = [] {
+        const char *e = getenv("OMPI_AMD_OSC_SMALL_BYTES");
+        return e ? (size_t)atoll(e) : (size_t)kRmaSmallBytes;
+    }();
+    return v;
+}
+
 // accumulate / get_accumulate / fetch_and_op under the accumulate lock
 // (osc_sm_comm.c:296-305, :340-356, :424-438).
 static int rma_op(ompi_amd_win_t *w, const void *origin, void *result, size_t count, int type,
@@ -844,6 +947,22 @@ static int rma_op(ompi_amd_win_t *w, const void *origin, void *result, size_t co
     OSC_TRY(target_ptr(w, target, disp, bytes, &t));
     hipStream_t s = win_stream(w, stream);
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    if (bytes <= rma_small_bytes()) {  // lock, fetch, combine, unlock: one launch
+        rma_small_fn f = nullptr;
+        int64_t n = (int64_t)count;
+        if (op == OMPI_AMD_OP_REPLACE || op == OMPI_AMD_OP_NO_OP) {
+            const uintptr_t a = (uintptr_t)origin | (uintptr_t)result | (uintptr_t)t | (uintptr_t)bytes;
+            int g = 16;
+            while (g > 1 && (a & (uintptr_t)(g - 1))) g >>= 1;
+            f = op == OMPI_AMD_OP_REPLACE ? rma_small_bytes_fn<RMA_REPLACE>(g) : rma_small_bytes_fn<RMA_FETCH>(g);
+            n = (int64_t)(bytes / (size_t)g);
+        } else {
+            f = g_rma_small[op][type];
+        }
+        if (f)
+            return record_hip(f(origin, result, t, n, w->peer_ctl[target], comm_err_dev(w->c), ticks_of(w), s),
+                              "osc small accumulate launch");
+    }
     OSC_TRY(launch_lock(w, target, 0, s));
     const uint32_t *gate = taken_word(w, target, true);
     int rc = OMPI_AMD_SUCCESS;
@@ -1570,15 +1689,12 @@ int ompi_amd_compare_and_swap(ompi_amd_win_t *w, const void *origin, const void 
     OSC_TRY(target_ptr(w, target, disp, size, &t));
     hipStream_t s = win_stream(w, stream);
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
-    OSC_TRY(launch_lock(w, target, 0, s));
     hipLaunchKernelGGL(cas_kernel, dim3(1), dim3(64), 0, s,
                        static_cast<const unsigned char *>(origin),
                        static_cast<const unsigned char *>(compare),
                        static_cast<unsigned char *>(result), reinterpret_cast<unsigned char *>(t),
-                       (int)size, (const uint32_t *)taken_word(w, target, true));
-    const int rc = record_hip(hipGetLastError(), "osc compare_and_swap launch");
-    const int urc = launch_lock(w, target, 1, s);
-    return rc != OMPI_AMD_SUCCESS ? rc : urc;
+                       (int)size, w->peer_ctl[target], comm_err_dev(w->c), ticks_of(w));
+    return record_hip(hipGetLastError(), "osc compare_and_swap launch");
 }
 
 // ---- shared windows (osc_sm_component.c:244-360, 455-485) ----

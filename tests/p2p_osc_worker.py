@@ -851,10 +851,13 @@ def case_cas(comm, rank, n):
         win.free()
 
 
-def case_passive_acc_all_to_all(comm, rank, n, salt, count=20011, rounds=6):
+def case_passive_acc_all_to_all(comm, rank, n, salt, count=20011, rounds=6, small=1001):
     """Passive target under contention: every round, every rank opens
     lock_all and accumulates (SUM, exact data) its origin into the SAME
-    region of EVERY rank's window, flushes, closes; a second region takes a
+    region of EVERY rank's window — the whole region (kernels behind a lock
+    kernel) and its first `small` elements (the single-launch form that
+    takes the lock inside its kernel), so both forms contend for each
+    target's accumulate lock — flushes, closes; a second region takes a
     put from the next rank under an exclusive lock of that target.  Every
     target's accumulate lock serialises the n concurrent updates; after the
     last round each window holds init + rounds x sum of the origins
@@ -872,6 +875,7 @@ def case_passive_acc_all_to_all(comm, rank, n, salt, count=20011, rounds=6):
             win.lock_all(stream=STREAM)
             for t in range(n):
                 win.accumulate(o, count, F, (rank + t) % n, 0, mop.MPI_SUM, stream=STREAM)
+                win.accumulate(o, small, F, (rank + t) % n, 0, mop.MPI_SUM, stream=STREAM)
             for t in range(n):
                 win.flush(t, stream=STREAM)
             win.unlock_all(stream=STREAM)
@@ -888,6 +892,9 @@ def case_passive_acc_all_to_all(comm, rank, n, salt, count=20011, rounds=6):
             orc.op_2buff(mop.MPI_SUM.index, F.code, org[r].copy(), total, count)
         for _ in range(rounds):
             orc.op_2buff(mop.MPI_SUM.index, F.code, total.copy(), exp, count)
+            head = exp[:small].copy()
+            orc.op_2buff(mop.MPI_SUM.index, F.code, total[:small].copy(), head, small)
+            exp[:small] = head
         ok, msg = eq(got[:count], exp, "accumulated region")
         if not ok:
             # exact data: any order gives the same bits; a difference is a lost or doubled update
