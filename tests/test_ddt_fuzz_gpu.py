@@ -12,45 +12,12 @@ the same bytes (gap bytes untouched)."""
 import numpy as np
 import pytest
 
+from ddt_random import rand_type, span_of
 from ompi_amd import datatype as dd
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
-BASES = ["MPI_CHAR", "MPI_SHORT", "MPI_INT", "MPI_DOUBLE", "MPI_DOUBLE"]
-
-
-def rand_type(rng, depth):
-    if depth == 0 or rng.random() < 0.2:
-        return dd.predefined(BASES[rng.integers(len(BASES))])
-    old = rand_type(rng, depth - 1)
-    k = int(rng.integers(4))
-    if k == 0:
-        return dd.type_contiguous(int(rng.integers(1, 6)), old)
-    if k == 1:
-        bl = int(rng.integers(1, 9))
-        stride = bl + int(rng.choice([0, 1, 3, bl, 40]))
-        return dd.type_vector(int(rng.integers(1, 60)), bl, stride, old)
-    if k == 2:
-        nb = int(rng.integers(1, 9))
-        bls, disps, pos = [], [], int(rng.integers(0, 5))
-        for _ in range(nb):
-            b = int(rng.integers(0, 7))
-            bls.append(b)
-            disps.append(pos)
-            pos += b + int(rng.integers(0, 7))
-        return dd.type_indexed(bls, disps, old)
-    m = int(rng.integers(2, 4))
-    types = [old] + [rand_type(rng, depth - 1) for _ in range(m - 1)]
-    bls, disps, pos = [], [], int(rng.integers(0, 9))
-    for t in types:
-        b = int(rng.integers(1, 4))
-        bls.append(b)
-        disps.append(pos)
-        # past the member's last byte (typemaps must not overlap: an
-        # overlapping receive type is erroneous, its unpack order-dependent)
-        pos += (b - 1) * t.extent + max(t.true_span, t.ub) + int(rng.integers(0, 13))
-    return dd.type_struct(bls, disps, types)
 
 
 def make_case(seed):
@@ -65,10 +32,6 @@ def make_case(seed):
     count = max(1, target // dt.size)
     count = min(count, max(1, (48 << 20) // max(dt.extent, 1)))
     return rng, dt, count
-
-
-def span_of(dt, count):
-    return (count - 1) * dt.extent + dt.true_span
 
 
 def dev_rand(n, seed):
