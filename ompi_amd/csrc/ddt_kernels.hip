@@ -155,12 +155,13 @@ __device__ __forceinline__ void walk_adv(const ddt_walk &v, int64_t &el, int64_t
 // moves chunks b, b + grid, ... of 256 x kVecChunkU packed granules, lane t
 // granules t, t + 256, ... of each, non-temporal on both sides.  The walk
 // advances by two constants (+256 granules inside a chunk, to the next chunk
-// after its last).  256 MiB packed, vector of 64-double runs at stride 128
-// (tools/ddt_vec_probe.hip, profiles/r05_ddt_vec_probe.jsonl): 0.640 of
-// 8 TB/s in the one-pass shape below, 0.764 chunked at 512 workgroups (a
-// contiguous copy in the same shape: 0.769).
+// after its last).  Vector of 64-double runs at stride 128
+// (tools/ddt_vec_probe.hip, profiles/r05_ddt_vec_probe*.jsonl), one-pass
+// shape below -> chunked at 2048 workgroups: 0.640 -> 0.758 of 8 TB/s at
+// 256 MiB packed, 0.619 -> 0.721 at 1 GiB (out of the Infinity Cache);
+// 2-KiB runs 0.623 -> 0.694 at 1 GiB (512 workgroups: 0.609).
 constexpr int kVecChunkU = 4;
-constexpr int kVecChunkGrid = 512;
+constexpr int kVecChunkGrid = 2048;
 
 template <bool UNPACK>
 __device__ __forceinline__ void ddt_vec16_body(const ddt_walk &v, const char *src, char *dst,

@@ -229,11 +229,13 @@ static void check(const char *name, const char *typed_h, const char *out_d, long
     free(h);
 }
 
-int main() {
-    const long packed = 256L << 20;
+int main(int argc, char **argv) {
+    // argv[1]: packed MiB (default 256; 1024 keeps the buffers out of the
+    // 256 MB Infinity Cache)
+    const long packed = (argc > 1 ? atol(argv[1]) : 256L) << 20;
     CK(hipEventCreate(&ea));
     CK(hipEventCreate(&eb));
-    for (int bl : {2, 8, 64, 256}) {  // doubles per run: 256 B, 512 B (the bench's bl64), 2 KiB
+    for (int bl : {64, 256}) {  // doubles per run: 512 B (the bench row), 2 KiB
         const long blen = bl * 8L, stride = 2 * blen, runs = packed / blen, span = runs * stride;
         char *typed = nullptr, *out = nullptr;
         CK(hipMalloc(&typed, span));
