@@ -51,6 +51,60 @@ __global__ __launch_bounds__(256) void k_copy(const u32x4 *src, u32x4 *dst, long
     }
 }
 
+// The shipped shape with THREADS x UNROLL per workgroup (system acquire at
+// entry, system release per workgroup at exit).
+template <int THREADS, int UNROLL>
+__global__ __launch_bounds__(THREADS) void k_copy_shape(const u32x4 *src, u32x4 *dst, long n) {
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    const long chunk = (long)THREADS * UNROLL;
+    for (long base = (long)blockIdx.x * chunk + threadIdx.x; base < n; base += (long)gridDim.x * chunk) {
+        u32x4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const long i = base + (long)u * THREADS;
+            if (i < n) v[u] = __builtin_nontemporal_load(src + i);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const long i = base + (long)u * THREADS;
+            if (i < n) __builtin_nontemporal_store(v[u], dst + i);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
+template <int THREADS, int UNROLL>
+static void run_shape(const u32x4 *s, u32x4 *d, long n, int grid) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i)
+        hipLaunchKernelGGL((k_copy_shape<THREADS, UNROLL>), dim3(grid), dim3(THREADS), 0, 0, s, d, n);
+    CK(hipDeviceSynchronize());
+    const int iters = 20;
+    CK(hipEventRecord(a));
+    for (int i = 0; i < iters; ++i)
+        hipLaunchKernelGGL((k_copy_shape<THREADS, UNROLL>), dim3(grid), dim3(THREADS), 0, 0, s, d, n);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    ms /= iters;
+    const double gbs = 2.0 * (double)n * 16 / (ms * 1e-3) / 1e9;
+    printf("{\"shape\": \"%dx%d\", \"grid\": %d, \"ms\": %.4f, \"gbs\": %.1f, \"frac_of_8TBs\": %.4f}\n",
+           THREADS, UNROLL, grid, ms, gbs, gbs / 8000.0);
+    fflush(stdout);
+}
+
 // The same body with its stores through a buffer descriptor carrying cache
 // policy bits AUX (gfx950 CPol: sc0 = 1, nt = 2, sc1 = 16): write-through
 // stores (sc1) leave no dirty lines for the per-workgroup system-scope
@@ -191,6 +245,18 @@ int main(int argc, char **argv) {
         CK(hipExtMallocWithFlags((void **)&d, bytes, hipDeviceMallocFinegrained));
         CK(hipMemset(d, 0, bytes));
         printf("{\"destination\": \"fine-grained\"}\n");
+    }
+    if (argc > 1 && !strcmp(argv[1], "shape")) {  // bytes in flight per workgroup, fences in
+        for (int grid : {256, 512}) {
+            run_shape<256, 4>(s, d, n, grid);
+            run_shape<256, 8>(s, d, n, grid);
+            run_shape<256, 16>(s, d, n, grid);
+            run_shape<512, 4>(s, d, n, grid);
+            run_shape<512, 8>(s, d, n, grid);
+            run_shape<1024, 4>(s, d, n, grid);
+            run_shape<1024, 8>(s, d, n, grid);
+        }
+        return 0;
     }
     if (argc > 1 && !strcmp(argv[1], "wt")) {  // store cache policy under the shipped release
         for (int grid : {256, 512, 1024}) {
