@@ -193,6 +193,69 @@ def case_ring_wraps(comm, rank, n, salt, k=150):
     return not fails, "; ".join(fails[:3])
 
 
+def case_random_channels(comm, rank, n, salt, per_rank=36):
+    """A seeded random message plan shared by every rank: per_rank x n
+    messages between random (source, destination) pairs, self included, on
+    three tags, sizes from 0 B to 2 MiB across the eager, staged and direct
+    paths, standard or synchronous mode.  Each rank posts its sends and its
+    receives (buffers sometimes larger than the message) in a random
+    interleaving of its own that keeps plan order on every (source, tag)
+    channel, then waits for its receives in a random order and for its
+    sends.  MPI's non-overtaking rule fixes which message each receive gets:
+    the i-th receive of a channel gets the channel's i-th send; every byte
+    and every status checked."""
+    rng = np.random.default_rng(SEED + salt)
+    sizes = [0, 1, 17, 4096, 4097, 65536 + 13, 300001, (2 << 20) + 5]
+    plan = []
+    for k in range(per_rank * n):
+        plan.append((int(rng.integers(n)), int(rng.integers(n)), 31 + int(rng.integers(3)),
+                     int(rng.choice(sizes)), int(rng.integers(4)) == 0))
+    mine_s = [(k, m) for k, m in enumerate(plan) if m[0] == rank]
+    mine_r = [(k, m) for k, m in enumerate(plan) if m[1] == rank]
+    local = np.random.default_rng(SEED + salt + 1000 + rank)
+    order = ["s"] * len(mine_s) + ["r"] * len(mine_r)
+    local.shuffle(order)
+    sreqs, rreqs, keep = [], [], []
+    si = ri = 0
+    for kind in order:
+        if kind == "s":
+            k, (src, dst, tag, nb, sync) = mine_s[si]
+            si += 1
+            buf = dev(payload(rank, salt + k, nb)) if nb else zeros(16)
+            keep.append(buf)
+            mode = pml.SEND_SYNCHRONOUS if sync else pml.SEND_STANDARD
+            sreqs.append(pml.isend(comm, buf, dst, tag, nbytes=nb, mode=mode, stream=STREAM))
+        else:
+            k, (src, dst, tag, nb, _) = mine_r[ri]
+            ri += 1
+            extra = int(local.choice([0, 0, 16, 4096]))
+            buf = zeros(nb + extra + 1)
+            rreqs.append((k, src, tag, nb, buf, pml.irecv(comm, buf, src, tag, nbytes=nb + extra,
+                                                          stream=STREAM)))
+    fails = []
+    for i in local.permutation(len(rreqs)):
+        k, src, tag, nb, buf, rq = rreqs[i]
+        try:
+            st = rq.wait()
+        except _lib.OmpiAmdError as e:
+            return False, f"receive of message {k} ({nb} B from {src}, tag {tag}): {e}"
+        if st.bytes != nb or st.source != src or st.tag != tag:
+            fails.append(f"message {k}: status ({st.source}, {st.tag}, {st.bytes} B), "
+                         f"expected ({src}, {tag}, {nb} B)")
+        else:
+            got = host(buf)
+            ok, msg = eq(got[:nb], payload(src, salt + k, nb), f"message {k} ({nb} B from {src})")
+            if ok and got[nb] != 0:
+                ok, msg = False, f"message {k}: byte past the message written"
+            if not ok:
+                fails.append(msg)
+        rq.free()
+    for rq in sreqs:
+        rq.wait()
+        rq.free()
+    return not fails, "; ".join(fails[:3])
+
+
 def case_recv_timeout_cancel(comm, rank, n, salt):
     """A receive that times out is withdrawn: the message sent
     after the timeout is not copied into the abandoned buffer, and the next
@@ -1198,6 +1261,8 @@ def main():
         ("p2p_ring_wraps_eager_and_staged", lambda: case_ring_wraps(comm, rank, n, 400)),
         ("p2p_any_source_any_tag", lambda: case_any_source(comm, rank, n, 70)),
         ("p2p_fan_in_any_source_order", lambda: case_fan_in_any_source(comm, rank, n, 500)),
+        ("p2p_random_channels", lambda: case_random_channels(comm, rank, n, 600)),
+        ("p2p_random_channels_b", lambda: case_random_channels(comm, rank, n, 601)),
         ("p2p_probe_truncate", lambda: case_probe_truncate(comm, rank, n, 71)),
         ("p2p_self", lambda: case_self(comm, rank, n, 72)),
         ("p2p_recv_timeout_cancel", lambda: case_recv_timeout_cancel(comm, rank, n, 75)),
