@@ -193,7 +193,7 @@ def case_ring_wraps(comm, rank, n, salt, k=150):
     return not fails, "; ".join(fails[:3])
 
 
-def case_random_channels(comm, rank, n, salt, per_rank=36):
+def case_random_channels(comm, rank, n, salt, per_rank=36, wild=0.0):
     """A seeded random message plan shared by every rank: per_rank x n
     messages between random (source, destination) pairs, self included, on
     three tags, sizes from 0 B to 2 MiB across the eager, staged and direct
@@ -203,13 +203,23 @@ def case_random_channels(comm, rank, n, salt, per_rank=36):
     channel, then waits for its receives in a random order and for its
     sends.  MPI's non-overtaking rule fixes which message each receive gets:
     the i-th receive of a channel gets the channel's i-th send; every byte
-    and every status checked."""
+    and every status checked.  wild > 0: that share of the messages travel
+    on tag 40 and are received with MPI_ANY_SOURCE (buffers of the largest
+    size); non-overtaking then fixes only the order per source, so the j-th
+    wildcard receive that a source's message matched (in posting order)
+    must hold that source's j-th tag-40 message to this rank."""
     rng = np.random.default_rng(SEED + salt)
     sizes = [0, 1, 17, 4096, 4097, 65536 + 13, 300001, (2 << 20) + 5]
     plan = []
     for k in range(per_rank * n):
-        plan.append((int(rng.integers(n)), int(rng.integers(n)), 31 + int(rng.integers(3)),
-                     int(rng.choice(sizes)), int(rng.integers(4)) == 0))
+        src, dst = int(rng.integers(n)), int(rng.integers(n))
+        tag = 40 if rng.random() < wild else 31 + int(rng.integers(3))
+        plan.append((src, dst, tag, int(rng.choice(sizes)), int(rng.integers(4)) == 0))
+    wild_from = {}  # source -> [(k, bytes)] of its tag-40 messages to this rank, in plan order
+    for k, (src, dst, tag, nb, _) in enumerate(plan):
+        if dst == rank and tag == 40:
+            wild_from.setdefault(src, []).append((k, nb))
+    wild_seen = {}
     mine_s = [(k, m) for k, m in enumerate(plan) if m[0] == rank]
     mine_r = [(k, m) for k, m in enumerate(plan) if m[1] == rank]
     local = np.random.default_rng(SEED + salt + 1000 + rank)
@@ -229,16 +239,30 @@ def case_random_channels(comm, rank, n, salt, per_rank=36):
             k, (src, dst, tag, nb, _) = mine_r[ri]
             ri += 1
             extra = int(local.choice([0, 0, 16, 4096]))
+            if tag == 40:  # any source: room for the largest message
+                nb, src, k = max(sizes), pml.ANY_SOURCE, -1
             buf = zeros(nb + extra + 1)
             rreqs.append((k, src, tag, nb, buf, pml.irecv(comm, buf, src, tag, nbytes=nb + extra,
                                                           stream=STREAM)))
     fails = []
+    waited = {}
     for i in local.permutation(len(rreqs)):
         k, src, tag, nb, buf, rq = rreqs[i]
         try:
-            st = rq.wait()
+            waited[i] = rq.wait()
         except _lib.OmpiAmdError as e:
             return False, f"receive of message {k} ({nb} B from {src}, tag {tag}): {e}"
+    for i, (k, src, tag, nb, buf, rq) in enumerate(rreqs):  # posting order
+        st = waited[i]
+        if tag == 40:  # the j-th match from st.source is that source's j-th message
+            j = wild_seen.get(st.source, 0)
+            wild_seen[st.source] = j + 1
+            if st.tag != 40 or j >= len(wild_from.get(st.source, [])):
+                fails.append(f"wildcard receive {i}: unexpected ({st.source}, {st.tag})")
+                rq.free()
+                continue
+            k, nb = wild_from[st.source][j]
+            src = st.source
         if st.bytes != nb or st.source != src or st.tag != tag:
             fails.append(f"message {k}: status ({st.source}, {st.tag}, {st.bytes} B), "
                          f"expected ({src}, {tag}, {nb} B)")
@@ -1263,6 +1287,7 @@ def main():
         ("p2p_fan_in_any_source_order", lambda: case_fan_in_any_source(comm, rank, n, 500)),
         ("p2p_random_channels", lambda: case_random_channels(comm, rank, n, 600)),
         ("p2p_random_channels_b", lambda: case_random_channels(comm, rank, n, 601)),
+        ("p2p_random_channels_any_source", lambda: case_random_channels(comm, rank, n, 602, wild=0.3)),
         ("p2p_probe_truncate", lambda: case_probe_truncate(comm, rank, n, 71)),
         ("p2p_self", lambda: case_self(comm, rank, n, 72)),
         ("p2p_recv_timeout_cancel", lambda: case_recv_timeout_cancel(comm, rank, n, 75)),
