@@ -1074,6 +1074,114 @@ def case_pscw_ring(comm, rank, n, salt, nbytes=200003, epochs=3, use_test=False)
         win.free()
 
 
+def case_osc_random_epochs(comm, rank, n, salt, epochs=10):
+    """A seeded random sequence of access epochs of every kind (fence, a
+    lock_all passive epoch closed by unlock_all and a barrier, a PSCW ring
+    epoch, an exclusive lock of one target), each with a random set of
+    operations per origin — puts into the slots of each target's put area
+    this origin owns (slot s belongs to origin s mod N: no two origins write
+    one slot in an epoch), gets of owned slots it does not put to in the
+    same epoch (their value is the one from before the epoch), accumulates
+    (SUM, exact small integers) anywhere in the accumulate area, sizes from
+    one element to 64 Ki — replayed on a CPU model of every window.  Gets
+    checked when their epoch closes; every window checked at the end."""
+    F = mop.MPI_FLOAT
+    slot, nslots = 1024, 8 * n  # floats per put slot; slots per window
+    put_n, acc_n = slot * nslots, 1 << 17
+    W = put_n + acc_n
+    rng = np.random.default_rng(SEED + salt)  # the plan: the same on every rank
+    model = [np.zeros(W, np.float32) for _ in range(n)]
+    base = zeros(W * 4)
+    win = osc.Window.create(comm, base, W * 4, disp_unit=4)
+    fails = []
+    try:
+        comm_barrier()
+        for e in range(epochs):
+            kind = ["fence", "lock_all", "pscw", "lock_one"][int(rng.integers(4))]
+            excl = int(rng.integers(n))  # lock_one: every origin's target
+            ops = []  # (origin, what, target, disp, count, data seed)
+            for o in range(n):
+                targets = ([(o + 1) % n] if kind == "pscw" else [excl] if kind == "lock_one"
+                           else list(range(n)))
+                owned = [sl for sl in range(nslots) if sl % n == o]
+                for _ in range(int(rng.integers(1, 5))):
+                    t = targets[int(rng.integers(len(targets)))]
+                    what = ["put", "get", "acc", "acc"][int(rng.integers(4))]
+                    if what == "acc":
+                        cnt = int(rng.choice([1, 7, 1000, 65536]))
+                        ops.append((o, "acc", t, put_n + int(rng.integers(acc_n - cnt + 1)), cnt,
+                                    int(rng.integers(1 << 30))))
+                    else:
+                        sl = owned[int(rng.integers(len(owned)))]
+                        cnt = int(rng.integers(1, slot + 1))
+                        ops.append((o, what, t, sl * slot, cnt, int(rng.integers(1 << 30))))
+            # two puts, or a get and a put, of one (origin, target, slot) in
+            # one epoch would conflict (unordered): keep the first put, drop the get
+            puts, kept = set(), []
+            for op in ops:
+                key = (op[0], op[2], op[3] // slot)
+                if op[1] == "put":
+                    if key in puts:
+                        continue
+                    puts.add(key)
+                kept.append(op)
+            ops = [op for op in kept if not (op[1] == "get" and (op[0], op[2], op[3] // slot) in puts)]
+            before = [m.copy() for m in model]
+            mine, keep = [], []
+            if kind == "fence":
+                win.fence(stream=STREAM)
+            elif kind == "lock_all":
+                win.lock_all(stream=STREAM)
+            elif kind == "pscw":
+                win.post([(rank - 1) % n], stream=STREAM)
+                win.start([(rank + 1) % n], stream=STREAM)
+            else:
+                win.lock(excl, osc.LOCK_EXCLUSIVE, stream=STREAM)
+            for o, what, t, d, cnt, sd in ops:
+                vals = np.random.default_rng(sd).integers(-64, 65, cnt).astype(np.float32)
+                if what == "put":
+                    model[t][d:d + cnt] = vals
+                elif what == "acc":
+                    model[t][d:d + cnt] += vals
+                if o != rank:
+                    continue
+                if what == "get":
+                    buf = zeros(cnt * 4)
+                    win.get(buf, t, d, cnt * 4, stream=STREAM)
+                    mine.append((buf, before[t][d:d + cnt].copy(), f"epoch {e} ({kind}) get from {t}@{d}"))
+                else:
+                    src = dev(vals)
+                    keep.append(src)
+                    if what == "put":
+                        win.put(src, t, d, cnt * 4, stream=STREAM)
+                    else:
+                        win.accumulate(src, cnt, F, t, d, mop.MPI_SUM, stream=STREAM)
+            if kind == "fence":
+                win.fence(stream=STREAM, blocking=True)
+            elif kind == "lock_all":
+                win.unlock_all(stream=STREAM)
+                comm_barrier()
+            elif kind == "pscw":
+                win.complete(stream=STREAM)
+                win.wait(stream=STREAM, blocking=True)
+                comm_barrier()  # every origin's epoch closed before the next one starts
+            else:
+                win.unlock(excl, stream=STREAM)
+                comm_barrier()
+            for buf, exp, what in mine:
+                ok, msg = eq(host(buf).view(np.float32), exp, what)
+                if not ok:
+                    fails.append(msg)
+        win.fence(stream=STREAM, blocking=True)
+        comm_barrier()
+        ok, msg = eq(host(base).view(np.float32), model[rank], f"window of rank {rank}")
+        if not ok:
+            fails.append(msg)
+    finally:
+        win.free()
+    return not fails, "; ".join(fails[:3])
+
+
 def case_pscw_all_to_one(comm, rank, n, salt, count=100003):
     """Rank 0 posts to every other rank; each origin accumulates (SUM, exact
     data) into its own slice of rank 0's window, then rank 0 waits: every
@@ -1331,6 +1439,8 @@ def main():
         ("osc_pscw_ring_test", lambda: case_pscw_ring(comm, rank, n, 95, epochs=2, use_test=True)),
         ("osc_pscw_all_to_one_acc", lambda: case_pscw_all_to_one(comm, rank, n, 96)),
         ("osc_pscw_errors", lambda: case_pscw_errors(comm, rank, n)),
+        ("osc_random_epochs", lambda: case_osc_random_epochs(comm, rank, n, 700)),
+        ("osc_random_epochs_b", lambda: case_osc_random_epochs(comm, rank, n, 701, epochs=16)),
         ("osc_request_rma", lambda: case_request_rma(comm, rank, n, 97)),
         ("osc_shared_window", lambda: case_shared_window(comm, rank, n, 98)),
         ("osc_shared_window_noncontig", lambda: case_shared_window(comm, rank, n, 99, noncontig=True)),
