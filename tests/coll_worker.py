@@ -787,6 +787,79 @@ def case_iallreduce_many(comm, rank, n, salt, calls=12):
     return not msgs, "; ".join(msgs)
 
 
+def case_cross_comm_order(comm, rank, n, salt, stream_per_comm=False):
+    """Two communicators over the same ranks, nonblocking allreduces posted
+    in OPPOSITE orders on even and odd ranks (MPI orders collectives per
+    communicator only: rank 0 posts A then B while rank 1 posts B then A,
+    then every rank waits for both) — at the fused, staged and large sizes,
+    on one stream per rank (what coll/rocm's per-thread stream gives) or one
+    per communicator; then persistent plans (made in one order) started in
+    opposite orders.  A library that launched each call's kernels in post
+    order on the shared stream would deadlock here (A's kernel behind B's on
+    one rank, B's behind A's on the other)."""
+    F = mop.MPI_FLOAT
+    comm2 = coll.Communicator.from_torch_distributed(device=comm.device)
+    comm2.set_param("timeout_ms", 20000)
+    s1 = torch.cuda.Stream()
+    s2 = torch.cuda.Stream() if stream_per_comm else s1
+    msgs = []
+    try:
+        for count in (7, 70001, (3 << 20) + 5):
+            xs1 = [inputs(F, count, r, salt) for r in range(n)]
+            xs2 = [inputs(F, count, r, salt + 1) for r in range(n)]
+            e1, _ = orc.allreduce([x.copy() for x in xs1], count, mop.MPI_SUM.index, F.code)
+            e2, _ = orc.allreduce([x.copy() for x in xs2], count, mop.MPI_SUM.index, F.code)
+            x1, x2 = to_dev(xs1[rank]), to_dev(xs2[rank])
+            o1, o2 = torch.zeros_like(x1), torch.zeros_like(x2)
+            torch.cuda.synchronize()
+            if rank % 2 == 0:
+                r1 = comm.iallreduce(x1, o1, count, F, mop.MPI_SUM, stream=s1)
+                r2 = comm2.iallreduce(x2, o2, count, F, mop.MPI_SUM, stream=s2)
+            else:
+                r2 = comm2.iallreduce(x2, o2, count, F, mop.MPI_SUM, stream=s2)
+                r1 = comm.iallreduce(x1, o1, count, F, mop.MPI_SUM, stream=s1)
+            for r_ in ((r1, r2) if rank % 2 == 0 else (r2, r1)):
+                r_.wait()
+            torch.cuda.synchronize()
+            r1.free()
+            r2.free()
+            for o, e, what in ((o1, e1, "A"), (o2, e2, "B")):
+                ok, msg = checked(o.cpu().numpy()[:count * 4].view(np.float32), e[rank])
+                if not ok:
+                    msgs.append(f"{count} floats on {what}: {msg}")
+            if comm.error() or comm2.error():
+                msgs.append(f"{count} floats: device error {comm.error()} / {comm2.error()}")
+                break
+            # persistent: plans made in the same order everywhere (their init
+            # is collective), started in opposite orders, three times
+            p1 = comm.allreduce_init(x1, o1, count, F, mop.MPI_SUM)
+            p2 = comm2.allreduce_init(x2, o2, count, F, mop.MPI_SUM)
+            try:
+                for _ in range(3):
+                    if rank % 2 == 0:
+                        p1.start(stream=s1)
+                        p2.start(stream=s2)
+                    else:
+                        p2.start(stream=s2)
+                        p1.start(stream=s1)
+                    p1.wait()
+                    p2.wait()
+                torch.cuda.synchronize()
+            finally:
+                p1.free()
+                p2.free()
+            for o, e, what in ((o1, e1, "A (persistent)"), (o2, e2, "B (persistent)")):
+                ok, msg = checked(o.cpu().numpy()[:count * 4].view(np.float32), e[rank])
+                if not ok:
+                    msgs.append(f"{count} floats on {what}: {msg}")
+            if comm.error() or comm2.error():
+                msgs.append(f"{count} floats (persistent): device error {comm.error()} / {comm2.error()}")
+                break
+    finally:
+        comm2.free()
+    return not msgs, "; ".join(msgs[:3])
+
+
 def case_small_marks_two_streams(comm, rank, n, salt, rounds=6):
     """Small allreduces whose fused kernels store their own completion marks
     (blocking, nonblocking and persistent: one flag-page counter slot per
@@ -1527,6 +1600,12 @@ def main():
                 comm, rank, n, D, mop.MPI_SUM, big // 2, 112, inplace=True), 2))),
         ]
     only = os.environ.get("COLL_CASES")
+    if only and "cross_comm" in only:
+        # opt-in: the known limitation of DESIGN.md §8 item 8 (device-side
+        # waits across communicators posted in opposite orders time out)
+        cases += [("cross_comm_order_one_stream", lambda: case_cross_comm_order(comm, rank, n, 190)),
+                  ("cross_comm_order_two_streams",
+                   lambda: case_cross_comm_order(comm, rank, n, 191, True))]
     # COLL_FROM / COLL_UNTIL: a contiguous slice of the list (history-dependent failures)
     first, last = os.environ.get("COLL_FROM"), os.environ.get("COLL_UNTIL")
     if first or last:
