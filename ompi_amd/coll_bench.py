@@ -732,7 +732,9 @@ def single_gpu_rows(mib: int = 256):
     3 x S (read target, read origin, write target), get_accumulate 5 x S
     (+ fetch copy), put and the p2p receive copy 2 x S, the derived-target
     accumulate 1.5 x S (S/2 packed origin bytes into every other double:
-    origin read, target slots read and written)."""
+    origin read, target slots read and written).  Plus two latency rows in
+    microseconds (host clock): fetch_and_op and an 8-byte accumulate, each
+    followed by MPI_Win_flush, under lock_all."""
     import torch
 
     from . import coll, osc, pml
@@ -779,6 +781,29 @@ def single_gpu_rows(mib: int = 256):
             gbs = factor * S / t / 1e9
             rows[name] = {"bytes": S, "ms": round(t * 1e3, 4), "hbm_gbs": round(gbs, 1),
                           "frac_of_8TBs": round(gbs / 8000.0, 4)}
+        # small one-sided latency under lock_all (host clock, each call
+        # completed by MPI_Win_flush): the single-launch accumulate-lock path
+        import time as _time
+        one = torch.ones(1, dtype=torch.int64, device="cuda")
+        res1 = torch.empty(1, dtype=torch.int64, device="cuda")
+        win.lock_all(stream=s)
+        try:
+            for name, fn in (
+                ("fetch_and_op_i64_flush_us",
+                 lambda: win.fetch_and_op(one, res1, mop.MPI_INT64_T, 0, 0, mop.MPI_SUM, stream=s)),
+                ("accumulate_8B_f32_flush_us",
+                 lambda: win.accumulate(x, 2, mop.MPI_FLOAT, 0, 64, mop.MPI_SUM, stream=s)),
+            ):
+                for _ in range(5):
+                    fn()
+                    win.flush(0, stream=s)
+                t0 = _time.perf_counter()
+                for _ in range(50):
+                    fn()
+                    win.flush(0, stream=s)
+                rows[name] = round((_time.perf_counter() - t0) / 50 * 1e6, 2)
+        finally:
+            win.unlock_all(stream=s)
     finally:
         win.free()
         comm.free()
