@@ -1601,7 +1601,7 @@ def main():
         ]
     only = os.environ.get("COLL_CASES")
     if only and "cross_comm" in only:
-        # opt-in: the known limitation of DESIGN.md §8 item 8 (device-side
+        # opt-in: the known limitation of DESIGN.md §8 item 9 (device-side
         # waits across communicators posted in opposite orders time out)
         cases += [("cross_comm_order_one_stream", lambda: case_cross_comm_order(comm, rank, n, 190)),
                   ("cross_comm_order_two_streams",
