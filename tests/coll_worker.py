@@ -928,6 +928,11 @@ def case_small_marks_two_streams(comm, rank, n, salt, rounds=6):
     return not msgs, "; ".join(msgs[:3])
 
 
+# STRESS_SEED (env): shifts the seeds of the randomized cases (more plans
+# than the committed ones, same checks)
+STRESS_SEED = int(os.environ.get("STRESS_SEED", "0"))
+
+
 def case_random_sequence(comm, rank, n, salt, calls=48):
     """A seeded random sequence (the same on every rank) of blocking-form
     collectives enqueued without any wait between them — allreduce, reduce
@@ -1469,8 +1474,8 @@ def main():
         ("iallreduce_mixed", lambda: case_iallreduce(comm, rank, n, 90)),
         ("iallreduce_many_outstanding", lambda: case_iallreduce_many(comm, rank, n, 94)),
         ("small_marks_two_streams", lambda: case_small_marks_two_streams(comm, rank, n, 700)),
-        ("random_sequence", lambda: case_random_sequence(comm, rank, n, 800)),
-        ("random_sequence_user_ipc", user_ipc(lambda: case_random_sequence(comm, rank, n, 900))),
+        ("random_sequence", lambda: case_random_sequence(comm, rank, n, 800 + STRESS_SEED)),
+        ("random_sequence_user_ipc", user_ipc(lambda: case_random_sequence(comm, rank, n, 900 + STRESS_SEED))),
         ("persistent_small", lambda: case_persistent(comm, rank, n, F, mop.MPI_SUM, 3001, 80)),
         ("persistent_mid_inplace",
          lambda: case_persistent(comm, rank, n, D, mop.MPI_SUM, 70001, 81, inplace=True)),

@@ -193,6 +193,11 @@ def case_ring_wraps(comm, rank, n, salt, k=150):
     return not fails, "; ".join(fails[:3])
 
 
+# STRESS_SEED (env): shifts the seeds of the randomized cases (more plans
+# than the committed ones, same checks)
+STRESS_SEED = int(os.environ.get("STRESS_SEED", "0"))
+
+
 def case_random_channels(comm, rank, n, salt, per_rank=36, wild=0.0):
     """A seeded random message plan shared by every rank: per_rank x n
     messages between random (source, destination) pairs, self included, on
@@ -1393,9 +1398,9 @@ def main():
         ("p2p_ring_wraps_eager_and_staged", lambda: case_ring_wraps(comm, rank, n, 400)),
         ("p2p_any_source_any_tag", lambda: case_any_source(comm, rank, n, 70)),
         ("p2p_fan_in_any_source_order", lambda: case_fan_in_any_source(comm, rank, n, 500)),
-        ("p2p_random_channels", lambda: case_random_channels(comm, rank, n, 600)),
-        ("p2p_random_channels_b", lambda: case_random_channels(comm, rank, n, 601)),
-        ("p2p_random_channels_any_source", lambda: case_random_channels(comm, rank, n, 602, wild=0.3)),
+        ("p2p_random_channels", lambda: case_random_channels(comm, rank, n, 600 + STRESS_SEED)),
+        ("p2p_random_channels_b", lambda: case_random_channels(comm, rank, n, 601 + STRESS_SEED)),
+        ("p2p_random_channels_any_source", lambda: case_random_channels(comm, rank, n, 602 + STRESS_SEED, wild=0.3)),
         ("p2p_probe_truncate", lambda: case_probe_truncate(comm, rank, n, 71)),
         ("p2p_self", lambda: case_self(comm, rank, n, 72)),
         ("p2p_recv_timeout_cancel", lambda: case_recv_timeout_cancel(comm, rank, n, 75)),
@@ -1439,8 +1444,8 @@ def main():
         ("osc_pscw_ring_test", lambda: case_pscw_ring(comm, rank, n, 95, epochs=2, use_test=True)),
         ("osc_pscw_all_to_one_acc", lambda: case_pscw_all_to_one(comm, rank, n, 96)),
         ("osc_pscw_errors", lambda: case_pscw_errors(comm, rank, n)),
-        ("osc_random_epochs", lambda: case_osc_random_epochs(comm, rank, n, 700)),
-        ("osc_random_epochs_b", lambda: case_osc_random_epochs(comm, rank, n, 701, epochs=16)),
+        ("osc_random_epochs", lambda: case_osc_random_epochs(comm, rank, n, 700 + STRESS_SEED)),
+        ("osc_random_epochs_b", lambda: case_osc_random_epochs(comm, rank, n, 701 + STRESS_SEED, epochs=16)),
         ("osc_request_rma", lambda: case_request_rma(comm, rank, n, 97)),
         ("osc_shared_window", lambda: case_shared_window(comm, rank, n, 98)),
         ("osc_shared_window_noncontig", lambda: case_shared_window(comm, rank, n, 99, noncontig=True)),
