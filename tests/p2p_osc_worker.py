@@ -1174,12 +1174,15 @@ def case_osc_random_epochs(comm, rank, n, salt, epochs=10):
                 win.unlock(excl, stream=STREAM)
                 comm_barrier()
             for buf, exp, what in mine:
-                ok, msg = eq(host(buf).view(np.float32), exp, what)
+                ok, msg = eq(host(buf).view(np.float32), exp, f"{what} (model {win.model})")
                 if not ok:
                     fails.append(msg)
         win.fence(stream=STREAM, blocking=True)
         comm_barrier()
-        ok, msg = eq(host(base).view(np.float32), model[rank], f"window of rank {rank}")
+        win.sync(stream=STREAM)  # MPI_Win_sync: the private copy of a separate-model window
+        STREAM.synchronize()
+        ok, msg = eq(host(base).view(np.float32), model[rank],
+                     f"window of rank {rank} (model {win.model})")
         if not ok:
             fails.append(msg)
     finally:
