@@ -1079,7 +1079,7 @@ def case_pscw_ring(comm, rank, n, salt, nbytes=200003, epochs=3, use_test=False)
         win.free()
 
 
-def case_osc_random_epochs(comm, rank, n, salt, epochs=10):
+def case_osc_random_epochs(comm, rank, n, salt, epochs=10, separate=False):
     """A seeded random sequence of access epochs of every kind (fence, a
     lock_all passive epoch closed by unlock_all and a barrier, a PSCW ring
     epoch, an exclusive lock of one target), each with a random set of
@@ -1097,8 +1097,16 @@ def case_osc_random_epochs(comm, rank, n, salt, epochs=10):
     rng = np.random.default_rng(SEED + salt)  # the plan: the same on every rank
     model = [np.zeros(W, np.float32) for _ in range(n)]
     base = zeros(W * 4)
-    win = osc.Window.create(comm, base, W * 4, disp_unit=4)
+    if separate:  # every window through a public copy (the separate model)
+        comm.set_param("osc_win_shadow", 1)
+    try:
+        win = osc.Window.create(comm, base, W * 4, disp_unit=4)
+    finally:
+        if separate:
+            comm.set_param("osc_win_shadow", 0)
     fails = []
+    if separate and win.model != osc.WIN_SEPARATE:
+        fails.append(f"model {win.model}, want WIN_SEPARATE")
     try:
         comm_barrier()
         for e in range(epochs):
@@ -1449,6 +1457,8 @@ def main():
         ("osc_pscw_errors", lambda: case_pscw_errors(comm, rank, n)),
         ("osc_random_epochs", lambda: case_osc_random_epochs(comm, rank, n, 700 + STRESS_SEED)),
         ("osc_random_epochs_b", lambda: case_osc_random_epochs(comm, rank, n, 701 + STRESS_SEED, epochs=16)),
+        ("osc_random_epochs_separate", lambda: case_osc_random_epochs(comm, rank, n, 702 + STRESS_SEED,
+                                                                      separate=True)),
         ("osc_request_rma", lambda: case_request_rma(comm, rank, n, 97)),
         ("osc_shared_window", lambda: case_shared_window(comm, rank, n, 98)),
         ("osc_shared_window_noncontig", lambda: case_shared_window(comm, rank, n, 99, noncontig=True)),
