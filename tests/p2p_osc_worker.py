@@ -1097,6 +1097,7 @@ def case_osc_random_epochs(comm, rank, n, salt, epochs=10, separate=False):
     rng = np.random.default_rng(SEED + salt)  # the plan: the same on every rank
     model = [np.zeros(W, np.float32) for _ in range(n)]
     base = zeros(W * 4)
+    w0 = comm.get_param("osc_shadow_windows")
     if separate:  # every window through a public copy (the separate model)
         comm.set_param("osc_win_shadow", 1)
     try:
@@ -1104,6 +1105,7 @@ def case_osc_random_epochs(comm, rank, n, salt, epochs=10, separate=False):
     finally:
         if separate:
             comm.set_param("osc_win_shadow", 0)
+    shadowed = comm.get_param("osc_shadow_windows") - w0  # this rank's window through a public copy
     fails = []
     if separate and win.model != osc.WIN_SEPARATE:
         fails.append(f"model {win.model}, want WIN_SEPARATE")
@@ -1190,7 +1192,7 @@ def case_osc_random_epochs(comm, rank, n, salt, epochs=10, separate=False):
         win.sync(stream=STREAM)  # MPI_Win_sync: the private copy of a separate-model window
         STREAM.synchronize()
         ok, msg = eq(host(base).view(np.float32), model[rank],
-                     f"window of rank {rank} (model {win.model})")
+                     f"window of rank {rank} (model {win.model}, shadowed here {shadowed})")
         if not ok:
             fails.append(msg)
     finally:
