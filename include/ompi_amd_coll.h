@@ -159,6 +159,14 @@ int ompi_amd_coll_owner(int size, int block);
  * tree, rooted at *first.  Host-only. */
 int ompi_amd_coll_reduce_order(int size, size_t msg_bytes, size_t count, int root,
                                int root_inplace, int *order, int *first);
+/* The same under coll_tuned_use_dynamic_rules with coll_tuned_reduce_algorithm
+ * = forced (coll_tuned_reduce_decision.c:146-179): 1 basic_linear, 3 pipeline,
+ * 4 binary, 5 binomial (0: the fixed decision above).  The others (2 chain
+ * with fan-out, 6 in-order binary, 7 Rabenseifner) return
+ * OMPI_AMD_ERR_UNSUPPORTED: the device path does not run them and coll/rocm
+ * leaves those reductions to coll/tuned.  Host-only. */
+int ompi_amd_coll_reduce_order_forced(int size, size_t msg_bytes, size_t count, int root,
+                                      int root_inplace, int forced, int *order, int *first);
 
 /* MPI_IN_PLACE is spelled sbuf == rbuf or sbuf == (void *)1.
  * Stream-ordered: results are valid when `stream` reaches this point; the

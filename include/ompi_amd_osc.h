@@ -92,6 +92,13 @@ int ompi_amd_win_sync(ompi_amd_win_t *win, void *stream);
 #define OMPI_AMD_WIN_UNIFIED 0
 #define OMPI_AMD_WIN_SEPARATE 1
 int ompi_amd_win_model(const ompi_amd_win_t *win);
+/* Diagnostics (no MPI counterpart): this rank's private copy (the window
+ * memory), its public copy and the last merge's snapshot; *pub and *snap
+ * are NULL where the window is unified on this rank. */
+int ompi_amd_win_copies(const ompi_amd_win_t *win, void **priv, void **pub, void **snap);
+/* Diagnostics: rank `peer`'s window memory as this process reaches it (the
+ * address RMA toward `peer` targets: its public copy, mapped). */
+int ompi_amd_win_peer_base(const ompi_amd_win_t *win, int peer, void **base);
 
 int ompi_amd_put(ompi_amd_win_t *win, const void *origin, size_t bytes, int target, size_t disp,
                  void *stream);

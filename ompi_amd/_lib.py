@@ -148,6 +148,9 @@ PROTOTYPES = [
     ("ompi_amd_coll_reduce_order", _C.c_int,
      [_C.c_int, _C.c_size_t, _C.c_size_t, _C.c_int, _C.c_int, _C.POINTER(_C.c_int),
       _C.POINTER(_C.c_int)]),
+    ("ompi_amd_coll_reduce_order_forced", _C.c_int,
+     [_C.c_int, _C.c_size_t, _C.c_size_t, _C.c_int, _C.c_int, _C.c_int, _C.POINTER(_C.c_int),
+      _C.POINTER(_C.c_int)]),
     ("ompi_amd_allreduce", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_int, _C.c_int, _C.c_void_p]),
     ("ompi_amd_allreduce_init", _C.c_int,
@@ -260,6 +263,9 @@ PROTOTYPES = [
       _C.c_int, _C.c_void_p]),
     ("ompi_amd_win_sync", _C.c_int, [_C.c_void_p, _C.c_void_p]),
     ("ompi_amd_win_model", _C.c_int, [_C.c_void_p]),
+    ("ompi_amd_win_peer_base", _C.c_int, [_C.c_void_p, _C.c_int, _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_win_copies", _C.c_int, [_C.c_void_p, _C.POINTER(_C.c_void_p), _C.POINTER(_C.c_void_p),
+                                       _C.POINTER(_C.c_void_p)]),
     ("ompi_amd_put_ddt", _C.c_int, [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p, _C.c_int,
                                     _C.c_size_t, _C.c_size_t, _C.c_void_p, _C.c_void_p]),
     ("ompi_amd_get_ddt", _C.c_int, [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p, _C.c_int,

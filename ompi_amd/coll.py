@@ -383,13 +383,16 @@ ORDER_NAMES = {0: "ring", 1: "recursive_doubling", 2: "chain", 3: "binomial", 4:
 
 
 def reduce_order(nranks: int, msg_bytes: int, count: int, root: int,
-                 root_inplace: bool = False) -> tuple[str, int]:
+                 root_inplace: bool = False, forced: int = 0) -> tuple[str, int]:
     """(operand order, virtual-rank-0) the library folds a reduce / rsb in:
-    coll/tuned's fixed reduce decision (coll_tuned_decision_fixed.c:354-428)."""
+    coll/tuned's fixed reduce decision (coll_tuned_decision_fixed.c:354-428),
+    or its forced algorithm `forced` (coll_tuned_reduce_decision.c:146-179;
+    OmpiAmdError ERR_UNSUPPORTED for the ones the device path leaves to tuned)."""
     o, f = ctypes.c_int(), ctypes.c_int()
-    _lib.check(_lib.load().ompi_amd_coll_reduce_order(nranks, msg_bytes, count, root,
-                                                      1 if root_inplace else 0, ctypes.byref(o),
-                                                      ctypes.byref(f)), "coll_reduce_order")
+    _lib.check(_lib.load().ompi_amd_coll_reduce_order_forced(nranks, msg_bytes, count, root,
+                                                             1 if root_inplace else 0, forced,
+                                                             ctypes.byref(o), ctypes.byref(f)),
+               "coll_reduce_order")
     return ORDER_NAMES[o.value], f.value
 
 

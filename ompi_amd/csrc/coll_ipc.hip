@@ -249,7 +249,33 @@ static int64_t block_cnt(int64_t b, int64_t split, int64_t early, int64_t late) 
 // The operand order of coll/tuned's reduce for a commutative op
 // (coll_tuned_decision_fixed.c:354-428; msg = type size * count).
 struct red_order { int order, first, flags; };
-static red_order tuned_reduce_order(int n, size_t msg, size_t count, int root, bool root_inplace) {
+// forced: coll_tuned_reduce_algorithm under coll_tuned_use_dynamic_rules
+// (coll_tuned_reduce_decision.c:146-179) — 1 basic_linear, 3 pipeline,
+// 4 binary, 5 binomial; segmentation does not change an element's operand
+// order (coll_base_reduce.c:62-260 folds each segment child by child), so
+// the segment size is irrelevant here.  0 (and every value the library does
+// not implement, which set_param refuses): the fixed decision.
+// coll/tuned's forced-algorithm numbers the device path implements
+// (coll_tuned_reduce_decision.c:35-44, coll_tuned_reduce_scatter_decision.c:
+// 36-42, coll_tuned_reduce_scatter_block_decision.c:34-40).
+enum { TUNED_RED_LINEAR = 1, TUNED_RED_PIPELINE = 3, TUNED_RED_BINARY = 4, TUNED_RED_BINOMIAL = 5 };
+enum { TUNED_RS_NONOVERLAPPING = 1, TUNED_RS_HALVING = 2, TUNED_RS_RING = 3 };
+enum { TUNED_RSB_BASIC_LINEAR = 1 };
+static bool tuned_red_alg_ok(int64_t v) {
+    return v == 0 || v == TUNED_RED_LINEAR || v == TUNED_RED_PIPELINE || v == TUNED_RED_BINARY ||
+           v == TUNED_RED_BINOMIAL;
+}
+
+static red_order tuned_reduce_order(int n, size_t msg, size_t count, int root, bool root_inplace,
+                                    int forced = 0) {
+    const int flr = root_inplace ? FOLD_ROOT_INPLACE : 0;
+    switch (forced) {
+    case TUNED_RED_LINEAR: return {ORDER_CHAIN, 0, 0};
+    case TUNED_RED_PIPELINE: return {ORDER_CHAIN, root, flr};
+    case TUNED_RED_BINARY: return {ORDER_BINARY, root, flr};
+    case TUNED_RED_BINOMIAL: return {ORDER_BINOMIAL, root, flr};
+    default: break;
+    }
     const double a1 = 0.6016 / 1024.0, b1 = 1.3496;
     const double a2 = 0.0410 / 1024.0, b2 = 9.7128;
     const double a3 = 0.0422 / 1024.0, b3 = 1.1614;
@@ -300,6 +326,7 @@ struct path_params {
     int push_gather;    // push / push-land scheme, staged (user_ipc 0): no handle swap at all
     int blocks = 0;     // transfer grid of a deferred call (nb_tuned); 0: the communicator's
     int copy_nt = -1;   // store kind of the copy / fold kernels (autotune); -1: the communicator's
+    int red_alg = 0;    // coll_tuned_reduce_algorithm forced (nonoverlapping's reduce), 0: fixed
 };
 
 // Export fallback.  hipIpcGetMemHandle sometimes refuses a live device
@@ -440,6 +467,10 @@ struct ompi_amd_comm {
     std::atomic<int> npending{0};  // deferred calls not yet launched (pending.size())
     bool has_stream = false;
     hipStream_t cur_stream = nullptr;
+    // param own_stream (coll/rocm sets it): every call runs on `own`, a
+    // stream on a hardware queue of its own (comm_stream)
+    int own_stream = 0;
+    hipStream_t own = nullptr;
     // another communicator launched on cur_stream after this one's last
     // launch there: stream_evs holds the mark of this one's end on it, and
     // quiesce() must not synchronise the stream (note_stream)
@@ -466,6 +497,7 @@ struct ompi_amd_comm {
     int shadowed = 0;                     // zero-copy calls that needed it
     int force_shadow = 0;                 // param "force_shadow": take the fallback always (tests)
     int win_shadow = 0;                   // param "osc_win_shadow": 1 = every MPI_Win_create shadowed (tests)
+    int win_separate = 1;                 // param "osc_win_separate": 0 = refuse a window that needs a public copy
     int64_t shadow_windows = 0;           // MPI_Win_create windows in the separate model (osc_ipc.hip)
     // param "user_ipc" (env OMPI_AMD_USER_IPC): export the caller's buffers
     // to peers (zero-copy).  Off by default: every zero-copy-size call stages
@@ -526,6 +558,9 @@ struct ompi_amd_comm {
     int copy_nt = 1;
     int copy_nt_fixed = 0;
     int tuned_alg = 0;                    // coll_tuned_allreduce_algorithm (forced), 0 = fixed
+    int tuned_red_alg = 0;                // coll_tuned_reduce_algorithm (forced, TUNED_RED_*)
+    int tuned_rs_alg = 0;                 // coll_tuned_reduce_scatter_algorithm (TUNED_RS_*)
+    int tuned_rsb_alg = 0;                // coll_tuned_reduce_scatter_block_algorithm (TUNED_RSB_*)
     // this communicator's references to peer mappings (the mappings
     // themselves are process-wide: ipc_registry.h), least recently used
     // evicted past 256
@@ -1712,7 +1747,8 @@ static int pof2_floor(int n) {
     return a;
 }
 
-static fold_plan allreduce_fold(int n, int tuned_alg, size_t count, int type, bool root0_inplace) {
+static fold_plan allreduce_fold(int n, int tuned_alg, size_t count, int type, bool root0_inplace,
+                                int red_alg = 0) {
     const size_t msg = type_size(type) * count;
     const fold_plan tree{ORDER_TREE, 0, 0}, ring{ORDER_RING, 0, 0};
     // basic_linear: basic linear reduce to 0 (acc = x[n-1]; acc = f(acc, x[i]),
@@ -1721,7 +1757,7 @@ static fold_plan allreduce_fold(int n, int tuned_alg, size_t count, int type, bo
     switch (tuned_alg) {
     case TUNED_AR_BASIC_LINEAR: return linear;
     case TUNED_AR_NONOVERLAPPING: {  // tuned reduce to 0 + bcast (:54-86)
-        const red_order ro = tuned_reduce_order(n, msg, count, 0, root0_inplace);
+        const red_order ro = tuned_reduce_order(n, msg, count, 0, root0_inplace, red_alg);
         return {ro.order, ro.first, ro.flags};
     }
     case TUNED_AR_RECURSIVE_DOUBLING: return tree;
@@ -2313,6 +2349,41 @@ static int reduce_my_block(ompi_amd_comm_t *c, const void *src, void *rbuf, size
 
 // scan (exclusive = false) / exscan: rank r folds ranks 0..r (0..r-1) in
 // the linear scan's order, which is the ring fold at first = 0.
+// The stream a call of c runs on.  By default the caller's (stream-ordered
+// after its producers).  With param own_stream — coll/rocm sets it: MPI
+// callers hand over buffers that are ready at the call — every call of the
+// communicator runs on one stream of its own, created with a CU mask of
+// every CU so that HIP gives it a hardware queue of its own instead of one
+// of the GPU_MAX_HW_QUEUES it shares among a process's streams.  A device
+// wait of one communicator (a barrier spinning on its peers) then never sits
+// in front of another communicator's kernels in one in-order queue: MPI lets
+// ranks issue different communicators' collectives — and point-to-point
+// traffic — in different orders (two nonblocking collectives posted in
+// opposite orders), and with one queue per process that was a
+// cycle of waits across ranks.  No event joins the caller's stream: the
+// buffers are ready when the call is made.
+static hipStream_t comm_stream(ompi_amd_comm_t *c, void *stream) {
+    if (!c || !c->own_stream) return as_stream(stream);
+    if (!c->own) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess ||
+            cus <= 0)
+            cus = 256;
+        std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xffffffffu);
+        if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+        if (hipExtStreamCreateWithCUMask(&c->own, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+            (void)hipGetLastError();
+            c->own = nullptr;
+            if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+                (void)hipGetLastError();
+                c->own = nullptr;
+                return as_stream(stream);
+            }
+        }
+    }
+    return c->own;
+}
+
 static int scan_common(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                        int op, void *stream, bool exclusive) {
     if (!c || !rbuf) return OMPI_AMD_ERR_BAD_PARAM;
@@ -2320,7 +2391,7 @@ static int scan_common(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
     TRY(check_sticky(c));
     if (count == 0) return OMPI_AMD_SUCCESS;
     TRY(set_dev(c));
-    hipStream_t s = as_stream(stream);
+    hipStream_t s = comm_stream(c, stream);
     const size_t bytes = count * ompi_amd_type_extent(type);
     const bool inplace = in_place(sbuf, rbuf);
     const void *src = inplace ? rbuf : sbuf;
@@ -2352,8 +2423,10 @@ static int scan_common(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
 }  // namespace ompi_amd
 
 static path_params params_of(const ompi_amd_comm_t *c) {
-    return {c->small_bytes, c->fused_bytes, c->zero_copy, c->algorithm, c->tuned_alg, 0,
-            is_push(c->algorithm) && !c->user_ipc && !c->force_shadow ? 1 : 0, 0};
+    path_params pp{c->small_bytes, c->fused_bytes, c->zero_copy, c->algorithm, c->tuned_alg, 0,
+                   is_push(c->algorithm) && !c->user_ipc && !c->force_shadow ? 1 : 0, 0};
+    pp.red_alg = c->tuned_red_alg;
+    return pp;
 }
 
 // Whether an allreduce of `count` elements takes a zero-copy path (and so
@@ -2364,7 +2437,7 @@ static bool allreduce_swaps(const ompi_amd_comm_t *c, const path_params &pp, siz
     const int n = c->size;
     if (n == 1 || count == 0) return false;
     const size_t bytes = count * ompi_amd_type_extent(type);
-    const fold_plan fp = allreduce_fold(n, pp.tuned_alg, count, type, pp.root0_inplace != 0);
+    const fold_plan fp = allreduce_fold(n, pp.tuned_alg, count, type, pp.root0_inplace != 0, pp.red_alg);
     const bool tree = fp.order == ORDER_TREE;
     if ((tree || fp.order == ORDER_RING) && bytes <= pp.fused_bytes && bytes <= c->scratch_bytes)
         return false;
@@ -2531,6 +2604,7 @@ static const bool g_boot_idle_set = [] {
 // The library's waits (host_mark.h) run the other communicators' ready
 // deferred calls between polls.
 static hipError_t wait_stream(hipStream_t s) { return mark_stream_wait(s, progress_others); }
+
 static hipError_t wait_event(hipEvent_t ev) {
     return mark_event_wait(ev, nullptr, 0, progress_others);
 }
@@ -2661,7 +2735,7 @@ static int allreduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size
         return record_hip(hipMemcpyAsync(rbuf, src, bytes, hipMemcpyDeviceToDevice, s), "copy");
     }
     // the operand order coll/tuned would use (fixed decision or forced)
-    const fold_plan fp = allreduce_fold(n, pp.tuned_alg, count, type, pp.root0_inplace != 0);
+    const fold_plan fp = allreduce_fold(n, pp.tuned_alg, count, type, pp.root0_inplace != 0, pp.red_alg);
     const bool tree = fp.order == ORDER_TREE;
     if ((tree || fp.order == ORDER_RING) && bytes <= pp.fused_bytes && bytes <= c->scratch_bytes)
         return allreduce_fused(c, src, rbuf, (int64_t)count, op, type, tree, s);
@@ -2752,9 +2826,15 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
     if (const char *t = getenv("OMPI_AMD_COLL_TIMEOUT_MS")) c->timeout_ms = atoll(t);
     // coll/tuned's own forcing variables (coll_tuned_allreduce_decision.c:
     // 37-101): honoured when dynamic rules are on, as tuned does
+    // (the environment form, for callers outside Open MPI; coll/rocm reads
+    // them through the MCA variable system and sets them per communicator)
     if (const char *d = getenv("OMPI_MCA_coll_tuned_use_dynamic_rules")) {
         const char *a = getenv("OMPI_MCA_coll_tuned_allreduce_algorithm");
         if (atoi(d) && a && atoi(a) >= 0 && atoi(a) < TUNED_AR_COUNT) c->tuned_alg = atoi(a);
+        const char *r = getenv("OMPI_MCA_coll_tuned_reduce_algorithm");
+        if (atoi(d) && r && tuned_red_alg_ok(atoi(r))) c->tuned_red_alg = atoi(r);
+        const char *rs = getenv("OMPI_MCA_coll_tuned_reduce_scatter_algorithm");
+        if (atoi(d) && rs && atoi(rs) >= 0 && atoi(rs) <= TUNED_RS_RING) c->tuned_rs_alg = atoi(rs);
     }
     if (const char *u = getenv("OMPI_AMD_USER_IPC")) c->user_ipc = atoi(u) ? 1 : 0;
     if (const char *a = getenv("OMPI_AMD_COLL_ALGORITHM")) {
@@ -2877,6 +2957,7 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     if (c->p2p) p2p_destroy(c->p2p);
     c->boot.detach();
     forget_streams(c);
+    if (c->own) hip_ignore(hipStreamDestroy(c->own));  // drained above
     delete c;
     return OMPI_AMD_SUCCESS;
 }
@@ -2893,6 +2974,16 @@ int ompi_amd_coll_block(size_t count, int size, int block, size_t *off, size_t *
 int ompi_amd_coll_owner(int size, int block) {
     if (size < 1 || block < 0 || block >= size) return -1;
     return (block + size - 1) % size;
+}
+
+int ompi_amd_coll_reduce_order_forced(int size, size_t msg_bytes, size_t count, int root,
+                                      int root_inplace, int forced, int *order, int *first) {
+    if (size < 1 || root < 0 || root >= size || !order || !first) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!tuned_red_alg_ok(forced)) return OMPI_AMD_ERR_UNSUPPORTED;
+    const red_order ro = tuned_reduce_order(size, msg_bytes, count, root, root_inplace != 0, forced);
+    *order = ro.order;
+    *first = ro.first;
+    return OMPI_AMD_SUCCESS;
 }
 
 int ompi_amd_coll_reduce_order(int size, size_t msg_bytes, size_t count, int root,
@@ -2964,7 +3055,7 @@ int ompi_amd_allreduce_wait(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, si
     // the fused kernel was the call's last launch on the per-thread stream,
     // and it stores the mark itself: no mark kernel behind it
     api_guard api_(c);
-    TRY(record_hip(mark_value_wait(thread_stream(), c->fused_mark, v, progress_others), "allreduce wait"));
+    TRY(record_hip(mark_value_wait(comm_stream(c, nullptr), c->fused_mark, v, progress_others), "allreduce wait"));
     return check_sticky(c);
 }
 
@@ -2981,7 +3072,7 @@ int ompi_amd_comm_sync(ompi_amd_comm_t *c, void *stream) {
     if (!c) return OMPI_AMD_ERR_BAD_PARAM;
     TRY(set_dev(c));
     TRY(drain(c));
-    TRY(record_hip(wait_stream(as_stream(stream)), "hipStreamSynchronize"));
+    TRY(record_hip(wait_stream(comm_stream(c, stream)), "hipStreamSynchronize"));
     return check_sticky(c);
 }
 
@@ -3038,12 +3129,25 @@ int ompi_amd_comm_set_param(ompi_amd_comm_t *c, const char *key, int64_t v) {
         c->reuse_shadow = v ? 1 : 0;
     } else if (!strcmp(key, "osc_win_shadow")) {
         c->win_shadow = v ? 1 : 0;
+    } else if (!strcmp(key, "osc_win_separate")) {
+        c->win_separate = v ? 1 : 0;
     } else if (!strcmp(key, "user_ipc")) {
         c->user_ipc = v ? 1 : 0;
         c->autotune = 0;
     } else if (!strcmp(key, "tuned_allreduce_algorithm")) {
         if (v < 0 || v >= TUNED_AR_COUNT) return OMPI_AMD_ERR_BAD_PARAM;
         c->tuned_alg = (int)v;
+    } else if (!strcmp(key, "own_stream")) {
+        c->own_stream = v ? 1 : 0;
+    } else if (!strcmp(key, "tuned_reduce_algorithm")) {
+        if (!tuned_red_alg_ok(v)) return OMPI_AMD_ERR_UNSUPPORTED;  // the caller keeps tuned's path
+        c->tuned_red_alg = (int)v;
+    } else if (!strcmp(key, "tuned_reduce_scatter_algorithm")) {
+        if (v < 0 || v > TUNED_RS_RING) return OMPI_AMD_ERR_UNSUPPORTED;
+        c->tuned_rs_alg = (int)v;
+    } else if (!strcmp(key, "tuned_reduce_scatter_block_algorithm")) {
+        if (v < 0 || v > TUNED_RSB_BASIC_LINEAR) return OMPI_AMD_ERR_UNSUPPORTED;
+        c->tuned_rsb_alg = (int)v;
     } else if (!strncmp(key, "p2p_", 4) && p2p_set_param(c->p2p, key, v) != OMPI_AMD_ERR_UNSUPPORTED) {
         return p2p_set_param(c->p2p, key, v);
     } else {
@@ -3102,6 +3206,10 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
         else return OMPI_AMD_ERR_BAD_PARAM;
     }
     else if (!strcmp(key, "tuned_allreduce_algorithm")) *v = c->tuned_alg;
+    else if (!strcmp(key, "tuned_reduce_algorithm")) *v = c->tuned_red_alg;
+    else if (!strcmp(key, "own_stream")) *v = c->own_stream;
+    else if (!strcmp(key, "tuned_reduce_scatter_algorithm")) *v = c->tuned_rs_alg;
+    else if (!strcmp(key, "tuned_reduce_scatter_block_algorithm")) *v = c->tuned_rsb_alg;
     else if (!strcmp(key, "landing_bytes")) *v = (int64_t)c->land_bytes;
     else if (!strcmp(key, "boot_calls")) *v = (int64_t)c->boot.posted();
     else if (!strcmp(key, "ipc_opens")) *v = ipc_get_stats().opens;
@@ -3130,6 +3238,7 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "imports_new")) *v = c->imports_new;
     else if (!strcmp(key, "force_shadow")) *v = c->force_shadow;
     else if (!strcmp(key, "osc_win_shadow")) *v = c->win_shadow;
+    else if (!strcmp(key, "osc_win_separate")) *v = c->win_separate;
     else if (!strcmp(key, "reuse_shadow")) *v = c->reuse_shadow;
     else if (!strcmp(key, "reused_exports")) *v = c->reused_exports;
     else if (!strcmp(key, "osc_shadow_windows")) *v = c->shadow_windows;
@@ -3155,7 +3264,7 @@ int ompi_amd_allreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
     TRY(drain(c));
     path_params pp = params_of(c);
     TRY(agree_root0_inplace(c, &pp, in_place(sbuf, rbuf)));
-    const hipStream_t s = as_stream(stream);
+    const hipStream_t s = comm_stream(c, stream);
     tune_bucket *tb = nullptr;
     int cand = -1;
     const int save_alg = c->algorithm, save_blocks = c->max_blocks;
@@ -3252,7 +3361,20 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
             return rc;
         }
     }
-    pending_op o{0, inplace ? rbuf : sbuf, rbuf, count, type, op, as_stream(stream), pp, req};
+    if (c->own_stream && allreduce_push_gathers(c, pp, count, type) &&
+        staged_push_landing(c->size, pp.algorithm, (int64_t)count, type, nullptr) > c->land_bytes) {
+        // growing the landing buffer is a blocking host rendezvous of this
+        // communicator; MPI lets ranks post different communicators'
+        // nonblocking calls in different orders, and two such growths
+        // posted in opposite orders wait for each other.  The staged pull
+        // instead: its handle swap is split (post now, launch from progress)
+        // and it needs no landing buffer.  Every rank decides alike (the
+        // landing size is the same everywhere).
+        pp.algorithm = ALG_PULL;
+        pp.push_gather = 0;
+        pp.blocks = 0;
+    }
+    pending_op o{0, inplace ? rbuf : sbuf, rbuf, count, type, op, comm_stream(c, stream), pp, req};
     if (allreduce_push_gathers(c, pp, count, type)) {
         // no swap: only the landing buffer must be big enough before the
         // launch (growing is collective and blocking: every rank here alike)
@@ -3398,7 +3520,7 @@ int ompi_amd_ireduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *r
     TRY(nb_begin(c, &req));
     const bool inplace = in_place(sbuf, rbuf);
     const size_t total = rcount * (size_t)c->size * ompi_amd_type_extent(type);
-    pending_op o{0, inplace ? rbuf : sbuf, rbuf, rcount, type, op, as_stream(stream), params_of(c), req};
+    pending_op o{0, inplace ? rbuf : sbuf, rbuf, rcount, type, op, comm_stream(c, stream), params_of(c), req};
     o.kind = PEND_RSB;
     const bool swap = nb_swaps(c, total);
     if (swap && !c->user_ipc && !c->force_shadow) {
@@ -3433,7 +3555,7 @@ int ompi_amd_iallgather(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
     TRY(nb_begin(c, &req));
     char *my_slot = (char *)rbuf + (size_t)c->rank * bytes;
     const bool inplace = sbuf == (const void *)1 || sbuf == (const void *)my_slot;
-    pending_op o{0, inplace ? (const void *)my_slot : sbuf, rbuf, bytes, 0, 0, as_stream(stream),
+    pending_op o{0, inplace ? (const void *)my_slot : sbuf, rbuf, bytes, 0, 0, comm_stream(c, stream),
                  params_of(c), req};
     o.kind = PEND_ALLGATHER;
     // in place: keep the (void *)1 spelling unless peers read a shadow
@@ -3455,7 +3577,7 @@ int ompi_amd_ibcast(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, void 
     *out = nullptr;
     ompi_amd_request *req = nullptr;
     TRY(nb_begin(c, &req));
-    pending_op o{0, buf, buf, bytes, 0, 0, as_stream(stream), params_of(c), req};
+    pending_op o{0, buf, buf, bytes, 0, 0, comm_stream(c, stream), params_of(c), req};
     o.kind = PEND_BCAST;
     o.root = root;
     if (nb_swaps(c, bytes)) {
@@ -3506,7 +3628,7 @@ int ompi_amd_ireduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t co
     TRY(nb_begin(c, &req));
     const int n = c->size;
     const size_t bytes = count * ompi_amd_type_extent(type);
-    pending_op o{0, sbuf, rbuf, count, type, op, as_stream(stream), params_of(c), req};
+    pending_op o{0, sbuf, rbuf, count, type, op, comm_stream(c, stream), params_of(c), req};
     o.kind = PEND_REDUCE;
     o.root = root;
     if (n > 1 && count > 0 && bytes > c->small_bytes && c->zero_copy) {
@@ -3541,7 +3663,7 @@ static int iscan_common(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
     ompi_amd_request *req = nullptr;
     TRY(nb_begin(c, &req));
     const size_t bytes = count * ompi_amd_type_extent(type);
-    pending_op o{0, sbuf, rbuf, count, type, op, as_stream(stream), params_of(c), req};
+    pending_op o{0, sbuf, rbuf, count, type, op, comm_stream(c, stream), params_of(c), req};
     o.kind = PEND_SCAN;
     o.exclusive = exclusive;
     if (c->size > 1 && count > 0 && bytes > c->small_bytes && c->zero_copy)
@@ -3571,7 +3693,7 @@ int ompi_amd_ireduce_scatter(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
     ompi_amd_request *req = nullptr;
     TRY(nb_begin(c, &req));
     const size_t ext = ompi_amd_type_extent(type);
-    pending_op o{0, sbuf, rbuf, 0, type, op, as_stream(stream), params_of(c), req};
+    pending_op o{0, sbuf, rbuf, 0, type, op, comm_stream(c, stream), params_of(c), req};
     o.kind = PEND_RS;
     o.rcounts.assign(rcounts, rcounts + c->size);
     size_t total = 0, maxc = 0;
@@ -3601,7 +3723,7 @@ int ompi_amd_reduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t cou
     int flag = root_inplace ? 1 : 0, flags_all[kMaxRanks];
     if (c->size > 1) TRY(c->boot.allgather(&flag, flags_all, sizeof(int)));
     return reduce_impl(c, sbuf, rbuf, count, type, op, root, c->size > 1 ? flags_all[root] != 0 : root_inplace,
-                       as_stream(stream));
+                       comm_stream(c, stream));
 }
 
 // root_inplace_all: whether the root passed MPI_IN_PLACE (known to every rank)
@@ -3618,7 +3740,8 @@ static int reduce_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
         if (root_inplace) return OMPI_AMD_SUCCESS;
         return record_hip(hipMemcpyAsync(rbuf, src, bytes, hipMemcpyDeviceToDevice, s), "copy");
     }
-    const red_order ro = tuned_reduce_order(n, type_size(type) * count, count, root, root_inplace_all);
+    const red_order ro = tuned_reduce_order(n, type_size(type) * count, count, root, root_inplace_all,
+                                            c->tuned_red_alg);
     red_jobs jobs;
     if (bytes <= c->small_bytes || !c->zero_copy) {
         // staged: everyone stages, the root folds everything
@@ -3706,7 +3829,7 @@ int ompi_amd_reduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *rb
     TRY(check_sticky(c));
     TRY(drain(c));
     const bool inplace = in_place(sbuf, rbuf);
-    return rsb_impl(c, inplace ? rbuf : sbuf, rbuf, rcount, type, op, inplace, as_stream(stream));
+    return rsb_impl(c, inplace ? rbuf : sbuf, rbuf, rcount, type, op, inplace, comm_stream(c, stream));
 }
 
 // src: the input (rbuf itself in place, n * rcount elements)
@@ -3724,7 +3847,7 @@ static int rsb_impl(ompi_amd_comm_t *c, const void *src, void *rbuf, size_t rcou
     // basic_linear rsb = tuned reduce of the whole vector to rank 0 (never
     // in place at that level) + scatter: my block folds in that order
     const size_t tcount = rcount * (size_t)n;
-    const red_order ro = tuned_reduce_order(n, type_size(type) * tcount, tcount, 0, false);
+    const red_order ro = tuned_reduce_order(n, type_size(type) * tcount, tcount, 0, false, c->tuned_red_alg);
     return reduce_my_block(c, src, rbuf, total, (int64_t)(rcount * (size_t)c->rank),
                            (int64_t)rcount, (int64_t)rcount, op, type, ro, inplace, s);
 }
@@ -3732,11 +3855,18 @@ static int rsb_impl(ompi_amd_comm_t *c, const void *src, void *rbuf, size_t rcou
 // coll/tuned's reduce_scatter decision (coll_tuned_decision_fixed.c:
 // 466-512, commutative): recursive halving for small totals or
 // power-of-two sizes up to 256 KiB, else the ring.
-static red_order tuned_reduce_scatter_order(int n, size_t total_bytes, int block) {
+// forced (coll_tuned_reduce_scatter_algorithm, :135-145): 2 recursive
+// halving, 3 ring; 1 non-overlapping is a tuned reduce of the whole vector
+// to rank 0 + scatterv (coll_base_reduce_scatter.c:42-92), rank 0 in place
+// exactly when every rank is; rs_impl builds that one.
+static red_order tuned_reduce_scatter_order(int n, size_t total_bytes, int block, int forced = 0) {
     int pow2 = 1;
     while (pow2 < n) pow2 <<= 1;
-    if (total_bytes <= 12 * 1024 || (total_bytes <= 256 * 1024 && pow2 == n) ||
-        (double)n >= 0.0012 * (double)total_bytes + 8.0) {
+    const bool halving = forced == TUNED_RS_HALVING ||
+        (forced != TUNED_RS_RING &&
+         (total_bytes <= 12 * 1024 || (total_bytes <= 256 * 1024 && pow2 == n) ||
+          (double)n >= 0.0012 * (double)total_bytes + 8.0));
+    if (halving) {
         int adj = 1;
         while (adj * 2 <= n) adj *= 2;
         const int remain = n - adj;
@@ -3754,7 +3884,7 @@ int ompi_amd_reduce_scatter(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
     if (!ompi_amd_op_supported(op, type)) return OMPI_AMD_ERR_UNSUPPORTED;
     TRY(check_sticky(c));
     TRY(drain(c));
-    return rs_impl(c, sbuf, rbuf, rcounts, type, op, as_stream(stream));
+    return rs_impl(c, sbuf, rbuf, rcounts, type, op, comm_stream(c, stream));
 }
 
 static int rs_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, const size_t *rcounts,
@@ -3776,7 +3906,9 @@ static int rs_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, const size_
         return record_hip(hipMemcpyAsync(rbuf, src, rcounts[0] * ext, hipMemcpyDeviceToDevice, s),
                           "copy");
     }
-    const red_order ro = tuned_reduce_scatter_order(n, total * type_size(type), c->rank);
+    const red_order ro = c->tuned_rs_alg == TUNED_RS_NONOVERLAPPING
+                             ? tuned_reduce_order(n, type_size(type) * total, total, 0, inplace, c->tuned_red_alg)
+                             : tuned_reduce_scatter_order(n, total * type_size(type), c->rank, c->tuned_rs_alg);
     return reduce_my_block(c, src, rbuf, total * ext, (int64_t)off, (int64_t)rcounts[c->rank],
                            (int64_t)maxc, op, type, ro, inplace, s, rcounts);
 }
@@ -3802,8 +3934,8 @@ int ompi_amd_allgather(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t 
     TRY(check_sticky(c));
     TRY(drain(c));
     if (c->land_blocking && ag_landing_need(c, bytes))  // grown here: collective, every rank alike
-        return allgather_land(c, sbuf, rbuf, bytes, as_stream(stream));
-    return allgather_impl(c, sbuf, rbuf, bytes, as_stream(stream));
+        return allgather_land(c, sbuf, rbuf, bytes, comm_stream(c, stream));
+    return allgather_impl(c, sbuf, rbuf, bytes, comm_stream(c, stream));
 }
 
 static int allgather_impl(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t bytes,
@@ -3846,8 +3978,8 @@ int ompi_amd_bcast(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, void *
     TRY(check_sticky(c));
     TRY(drain(c));
     if (c->land_blocking && bcast_landing_need(c, bytes))
-        return bcast_land(c, buf, bytes, root, as_stream(stream));
-    return bcast_impl(c, buf, buf, bytes, root, as_stream(stream));
+        return bcast_land(c, buf, bytes, root, comm_stream(c, stream));
+    return bcast_impl(c, buf, buf, bytes, root, comm_stream(c, stream));
 }
 
 // root_src: what the root's peers read (buf, or a deferred call's shadow)
@@ -4113,7 +4245,7 @@ int ompi_amd_allreduce_init(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, si
     const bool small = n == 1 || count == 0 || !allreduce_swaps(c, pl->pp, count, type) || push_gather;
     if (rc == OMPI_AMD_SUCCESS && push_gather)
         rc = ensure_landing(c, staged_push_landing(n, pl->pp.algorithm, (int64_t)count, type, nullptr));
-    pl->fp = allreduce_fold(n, pl->pp.tuned_alg, count, type, pl->pp.root0_inplace != 0);
+    pl->fp = allreduce_fold(n, pl->pp.tuned_alg, count, type, pl->pp.root0_inplace != 0, pl->pp.red_alg);
     if (!small) {
         pl->kind = is_push(c->algorithm) ? 3 : c->algorithm == ALG_PULL_PUSH ? 2 : 1;
         if (pl->kind == 3) rc = ensure_landing(c, push_slot(pl->count, n, type) * (size_t)n);
@@ -4158,7 +4290,7 @@ static int plan_enqueue(ompi_amd_plan_t *pl, void *stream) {
         c->mark_slot = std::max(pl->done_slot, 0);
         c->mark_embedded = 0;
         const int rc = allreduce_impl(c, pl->src == pl->rbuf ? (const void *)1 : pl->src, pl->rbuf,
-                                      (size_t)pl->count, pl->type, pl->op, as_stream(stream), pl->pp);
+                                      (size_t)pl->count, pl->type, pl->op, comm_stream(c, stream), pl->pp);
         c->want_mark = false;
         pl->embedded = c->mark_embedded;
         c->mark_embedded = 0;
@@ -4166,7 +4298,7 @@ static int plan_enqueue(ompi_amd_plan_t *pl, void *stream) {
     }
     TRY(check_sticky(c));
     TRY(set_dev(c));
-    hipStream_t s = as_stream(stream);
+    hipStream_t s = comm_stream(c, stream);
     TRY(shadow_in(c, pl->sh, s));
     int rc;
     if (pl->kind == 3) {
@@ -4309,7 +4441,7 @@ int ompi_amd_plan_start(ompi_amd_plan_t *pl, void *stream) {
     TRY(plan_enqueue(pl, stream));
     pl->started = true;
     pl->recorded = false;
-    pl->stream = as_stream(stream);
+    pl->stream = comm_stream(pl->c, stream);
     return OMPI_AMD_SUCCESS;
 }
 
@@ -4530,6 +4662,8 @@ bool comm_ipc_safe(const void *ptr) {
            !export_reused(base, id);
 }
 
+bool comm_win_separate_ok(ompi_amd_comm_t *c) { return c->win_separate != 0 || c->win_shadow != 0; }
+
 bool comm_win_needs_shadow(ompi_amd_comm_t *c, const void *base) {
     if (c->win_shadow || !comm_ipc_safe(base)) {
         ++c->shadow_windows;
@@ -4555,6 +4689,8 @@ int comm_barrier(ompi_amd_comm_t *c, hipStream_t s) {
 }
 
 int comm_sticky(ompi_amd_comm_t *c) { return check_sticky(c); }
+
+hipStream_t comm_call_stream(ompi_amd_comm_t *c, void *stream) { return comm_stream(c, stream); }
 
 int comm_copy(ompi_amd_comm_t *c, const void *src, void *dst, size_t bytes, hipStream_t s) {
     cp_jobs jobs{};

@@ -55,6 +55,10 @@ int comm_export(ompi_amd_comm_t *c, const void *ptr, ipc_desc *d);
 bool comm_ipc_safe(const void *ptr);
 // MPI_Win_create over base: run it through a public copy (separate model)?
 // Not IPC-safe (above), or param osc_win_shadow; counted (osc_shadow_windows).
+// Whether a window may run in the separate model (param osc_win_separate;
+// osc/rocm's osc_rocm_separate_model): otherwise a window that needs a
+// public copy fails on every rank.
+bool comm_win_separate_ok(ompi_amd_comm_t *c);
 bool comm_win_needs_shadow(ompi_amd_comm_t *c, const void *base);
 // Map a peer's exported buffer (cached, LRU).  pin: held until comm_unpin.
 int comm_import(ompi_amd_comm_t *c, int peer, const ipc_desc &d, const char **out, bool pin,
@@ -64,6 +68,9 @@ void comm_unpin(ompi_amd_comm_t *c, void *base);
 int comm_drain(ompi_amd_comm_t *c);
 // Device barrier over every rank of c on stream s (stream-ordered epoch).
 int comm_barrier(ompi_amd_comm_t *c, hipStream_t s);
+// The stream a call of c runs on: the caller's, or the communicator's own
+// (param own_stream; coll_ipc.hip comm_stream).
+hipStream_t comm_call_stream(ompi_amd_comm_t *c, void *stream);
 // The sticky device error word (a barrier or lock that timed out).
 int comm_sticky(ompi_amd_comm_t *c);
 // Byte copy kernel (16-/4-/1-byte granules by the common phase of src and

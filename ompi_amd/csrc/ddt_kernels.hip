@@ -1114,6 +1114,10 @@ int ompi_amd_ddt_create_elems(const ompi_amd_ddt_elem_t *elems, int nelems, int6
             err = hipMemcpy(d->dmap, imap.data(), imap.size() * sizeof(uint16_t),
                             hipMemcpyHostToDevice);
     }
+    // a copy from pageable memory may return before the bytes reach the
+    // device, and the kernels that read the program run on
+    // other (non-blocking) streams: wait for the null stream's copies here
+    if (err == hipSuccess) err = hipStreamSynchronize(nullptr);
     if (err != hipSuccess) {
         int rc = record_hip(err, "ddt descriptor upload");
         if (d->dev) hip_ignore(hipFree(d->dev));

@@ -47,10 +47,35 @@ struct user {
 std::vector<user> g_users;
 ipc_stats g_st{};
 std::atomic<uint64_t> g_close_mark{0};  // ipc_close_watermark()
+std::atomic<bool> g_close_pending{false};
+std::mutex g_probe_mu;
+std::vector<void *> g_probes;  // watermark probes, freed in batches
 
-// After a close: the buffer id of a fresh allocation — every allocation
-// with a lower id existed at the close (ipc_registry.h).
+// A close happened: the watermark moves at the next ipc_close_watermark().
+// Nothing here touches the device — closes run inside point-to-point
+// progress and LRU evictions, where a device-wide synchronisation (hipFree)
+// could wait on this process's kernels that wait on peers.
+void resolve_close_mark();
 void note_close() {
+    g_close_pending.store(true, std::memory_order_release);
+    // OMPI_AMD_EAGER_CLOSE_MARK=1 (diagnostics): the round-5
+    // behaviour — the probe allocation made and freed at the close itself
+    static const bool eager = [] {
+        const char *e = getenv("OMPI_AMD_EAGER_CLOSE_MARK");
+        return e && atoi(e) != 0;
+    }();
+    if (eager) resolve_close_mark();
+}
+
+// The buffer id of a fresh allocation, taken after the closes noted so far:
+// every allocation with a lower id existed at those closes (ipc_registry.h).
+// Taking it later than the close only counts more allocations as older —
+// more conservative, never less.  Runs on the host paths that ask before an
+// export (comm_ipc_safe and the exporters), not inside progress; the probes
+// are freed 256 at a time.
+void resolve_close_mark() {
+    if (!g_close_pending.exchange(false, std::memory_order_acq_rel)) return;
+    std::lock_guard<std::mutex> g(g_probe_mu);
     void *p = nullptr;
     if (hipMalloc(&p, 4096) != hipSuccess) {
         (void)hipGetLastError();
@@ -62,7 +87,15 @@ void note_close() {
         (void)hipGetLastError();
         id = UINT64_MAX;
     }
-    hip_ignore(hipFree(p));
+    g_probes.push_back(p);
+    static const bool eager = [] {
+        const char *e = getenv("OMPI_AMD_EAGER_CLOSE_MARK");
+        return e && atoi(e) != 0;
+    }();
+    if (eager || g_probes.size() >= 256) {
+        for (void *q : g_probes) hip_ignore(hipFree(q));
+        g_probes.clear();
+    }
     uint64_t cur = g_close_mark.load();
     while (cur < id && !g_close_mark.compare_exchange_weak(cur, id)) {
     }
@@ -344,7 +377,10 @@ void ipc_remove_user(void *owner) {
                   g_users.end());
 }
 
-uint64_t ipc_close_watermark() { return g_close_mark.load(); }
+uint64_t ipc_close_watermark() {
+    resolve_close_mark();
+    return g_close_mark.load();
+}
 
 ipc_stats ipc_get_stats() {
     std::lock_guard<std::mutex> g(g_mu);

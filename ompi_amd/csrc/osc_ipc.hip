@@ -914,7 +914,7 @@ static int launch_acc(ompi_amd_win_t *w, int op, int type, const void *origin, v
 // The stream of a window call, remembered so that win_free waits for this
 // window's work only (not for every stream of the device).
 static hipStream_t win_stream(ompi_amd_win_t *w, void *stream) {
-    const hipStream_t s = as_stream(stream);
+    const hipStream_t s = comm_call_stream(w->c, stream);
     if (std::find(w->streams.begin(), w->streams.end(), s) == w->streams.end()) w->streams.push_back(s);
     return s;
 }
@@ -1182,7 +1182,13 @@ static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit
     mine.disp_unit = disp_unit;
     // the caller's memory (MPI_Win_create) that peers could not map
     // reliably: a public copy in the exported arena, the separate model
-    if (rc == OMPI_AMD_SUCCESS && bytes && user && comm_win_needs_shadow(c, base)) {
+    const bool need_copy = rc == OMPI_AMD_SUCCESS && bytes && user && comm_win_needs_shadow(c, base);
+    if (need_copy && !comm_win_separate_ok(c)) {
+        record_msg("osc window: memory peers cannot map as it is (not an IPC-safe size, or older than "
+                   "an IPC close of this process) and the separate model is off (osc_win_separate 0)");
+        rc = OMPI_AMD_ERR_UNSUPPORTED;  // joins the rendezvous: every rank fails alike
+    }
+    if (rc == OMPI_AMD_SUCCESS && need_copy) {
         void *pub = nullptr;
         rc = comm_arena_alloc(c, bytes, &pub);
         if (rc == OMPI_AMD_ERR_UNSUPPORTED) {  // past the arena's limit: an allocation of its own
@@ -1194,10 +1200,26 @@ static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit
             w->shadow = static_cast<char *>(pub);
             rc = record_hip(hipMalloc((void **)&w->snap, bytes), "hipMalloc (window snapshot)");
         }
-        if (rc == OMPI_AMD_SUCCESS)
-            rc = record_hip(hipMemcpy(w->shadow, base, bytes, hipMemcpyDeviceToDevice), "window public copy");
-        if (rc == OMPI_AMD_SUCCESS)
-            rc = record_hip(hipMemcpy(w->snap, base, bytes, hipMemcpyDeviceToDevice), "window snapshot");
+        // both copies complete before this rank joins the rendezvous below:
+        // peers may put into the public copy as soon as the window exists.
+        // (hipMemcpy device-to-device returns before the copy is done; that
+        // was the round-5 "one-sided mismatch after point-to-point traffic":
+        // an epoch-0 put landed in the public copy and the still-running
+        // initial copy overwrote it — DESIGN.md §4.9.)  A stream of its own,
+        // non-blocking: the legacy stream would also wait for this process's
+        // blocking streams, whose kernels may be waiting for these peers.
+        if (rc == OMPI_AMD_SUCCESS) {
+            hipStream_t z = nullptr;
+            rc = record_hip(hipStreamCreateWithFlags(&z, hipStreamNonBlocking), "window copy stream");
+            if (rc == OMPI_AMD_SUCCESS)
+                rc = record_hip(hipMemcpyAsync(w->shadow, base, bytes, hipMemcpyDeviceToDevice, z),
+                                "window public copy");
+            if (rc == OMPI_AMD_SUCCESS)
+                rc = record_hip(hipMemcpyAsync(w->snap, base, bytes, hipMemcpyDeviceToDevice, z),
+                                "window snapshot");
+            if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipStreamSynchronize(z), "window copies");
+            if (z) hip_ignore(hipStreamDestroy(z));
+        }
         mine.shadowed = 1;
     }
     if (rc == OMPI_AMD_SUCCESS && bytes && !shared)
@@ -1362,6 +1384,20 @@ int ompi_amd_win_sync(ompi_amd_win_t *w, void *stream) {
 
 int ompi_amd_win_model(const ompi_amd_win_t *w) {
     return !w ? OMPI_AMD_ERR_BAD_PARAM : w->separate ? OMPI_AMD_WIN_SEPARATE : OMPI_AMD_WIN_UNIFIED;
+}
+
+int ompi_amd_win_copies(const ompi_amd_win_t *w, void **priv, void **pub, void **snap) {
+    if (!w || !priv || !pub || !snap) return OMPI_AMD_ERR_BAD_PARAM;
+    *priv = w->base;
+    *pub = w->shadow;
+    *snap = w->snap;
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_win_peer_base(const ompi_amd_win_t *w, int peer, void **base) {
+    if (!w || !base || peer < 0 || peer >= w->size) return OMPI_AMD_ERR_BAD_PARAM;
+    *base = w->peer_base[peer];
+    return OMPI_AMD_SUCCESS;
 }
 
 int ompi_amd_win_lock(ompi_amd_win_t *w, int lock_type, int target, int assert_, void *stream) {

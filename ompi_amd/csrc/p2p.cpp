@@ -841,7 +841,7 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     if (mode < OMPI_AMD_SEND_SYNCHRONOUS || mode > OMPI_AMD_SEND_STANDARD)
         return OMPI_AMD_ERR_BAD_PARAM;
     int rc = record_hip(hipSetDevice(comm_device(c)), "hipSetDevice");
-    const hipStream_t s = as_stream(stream);
+    const hipStream_t s = comm_call_stream(c, stream);
     const bool host = bytes && !is_device(buf);
     const bool eager = bytes <= kEager && mode != OMPI_AMD_SEND_SYNCHRONOUS;  // Ssend: rendezvous
     const bool inl = host && eager && bytes <= kInline;  // no device work at all
@@ -897,9 +897,20 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     // host buffer, or a device buffer peers cannot map reliably — wait
     // for a stage, past the cap once if nothing is in flight; otherwise one
     // try, and without a stage the message goes from the buffer itself.
-    auto stage_send = [&](bool must) -> int {
+    auto stage_send = [&](bool must, bool must_if_unsafe = false) -> int {
         stage st;
         bool got = take_stage(p, p->send_free, bytes, true, &st);
+        if (!got && !must && must_if_unsafe && (p->age_all || !comm_ipc_safe(src))) {
+            // no stage free and the buffer cannot go out by itself: a stage
+            // past the cap rather than a wait (an MPI_Isend must return
+            // whether or not the receiver has posted yet)
+            ++p->unsafe_sends;
+            const size_t cap = p->stage_cap;
+            p->stage_cap = p->stage_bytes + stage_class(bytes);
+            got = take_stage(p, p->send_free, bytes, true, &st);
+            p->stage_cap = cap;
+            if (!got) return record_hip(hipErrorOutOfMemory, "p2p send stage (device buffer past the cap)");
+        }
         if (!got && must) {
             const double t1 = now_s();
             while (!got) {
@@ -976,7 +987,9 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
         }
         src = cell;
     } else if (bytes && (host || (dst != p->rank && !p->user_ipc))) {
-        rc = stage_send(host);
+        // one try at a stage; a device buffer that cannot go out by itself
+        // (not IPC-safe, or older than an IPC close) waits for one instead
+        rc = stage_send(host, !host);
     } else if (bytes && dst != p->rank && (p->age_all || !comm_ipc_safe(src))) {
         // p2p_user_ipc: an allocation peers could not map reliably — not an
         // IPC-safe size, or older than an IPC close of this process, which
@@ -1045,7 +1058,7 @@ int ompi_amd_irecv(ompi_amd_comm_t *c, void *buf, size_t bytes, int src, int tag
     r->tag = tag;
     if (p2p_trace())
         fprintf(stderr, "[p2p %d] irecv req %p cap %zu src %d tag %d\n", p->rank, (void *)r, bytes, src, tag);
-    r->stream = as_stream(stream);
+    r->stream = comm_call_stream(c, stream);
     std::lock_guard<std::recursive_mutex> g(p->mu);
     p->recvs.push_back(r);
     progress(p);

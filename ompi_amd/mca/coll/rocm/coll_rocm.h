@@ -51,7 +51,13 @@ typedef struct mca_coll_rocm_module_t {
     void *dstage[2], *hstage[2]; /* grow-only staging per operand slot */
     size_t dstage_bytes[2], hstage_bytes[2];
     int fail_stage;              /* test hook: the next staging allocation fails */
+    /* coll/tuned's forcing state read at enable (rocm_tuned_config): the
+     * blocking reductions whose tuned algorithm the device path does not
+     * run (ROCM_TUNED_* bits) stay with the saved functions */
+    int tuned_decline;
 } mca_coll_rocm_module_t;
+
+enum { ROCM_TUNED_ALLREDUCE = 1, ROCM_TUNED_REDUCE = 2, ROCM_TUNED_RS = 4, ROCM_TUNED_RSB = 8 };
 
 enum { ROCM_RES_AUTO = 0, ROCM_RES_DEVICE = 1, ROCM_RES_HOST = 2 };
 
@@ -72,6 +78,7 @@ typedef struct mca_coll_rocm_component_t {
     int residency_lock;  /* coll_rocm_residency_lock: unanimous votes before locking (0 never) */
     int residency_recheck; /* coll_rocm_residency_recheck: locked calls per recheck vote (0 never) */
     int max_device_mib;  /* coll_rocm_max_device_mib: larger calls go to the saved functions */
+    int own_stream;      /* coll_rocm_own_stream: each communicator's calls on a hardware queue of its own */
 } mca_coll_rocm_component_t;
 
 OMPI_MODULE_DECLSPEC extern mca_coll_rocm_component_t mca_coll_rocm_component;

@@ -77,6 +77,7 @@ mca_coll_rocm_component_t mca_coll_rocm_component = {
     .residency_lock = 8,
     .residency_recheck = 256,
     .max_device_mib = 1024,
+    .own_stream = 1,
 };
 
 static int rocm_register(void)
@@ -164,7 +165,82 @@ static int rocm_register(void)
                                            MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_coll_rocm_component.max_device_mib);
+    (void) mca_base_component_var_register(c, "own_stream",
+                                           "1: each communicator's collectives run on a stream with a "
+                                           "hardware queue of its own (MPI lets ranks order different "
+                                           "communicators' calls differently; device waits of one "
+                                           "must not queue in front of another's)",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_coll_rocm_component.own_stream);
     return OMPI_SUCCESS;
+}
+
+/* ------------------------------------------------------------- coll/tuned */
+
+/* An int (or bool) variable of coll/tuned through the MCA variable system —
+ * whatever set it: the environment, an mca-params.conf file, the command
+ * line or MPI_T — or dflt when tuned is not built or the variable is not
+ * registered. */
+static int tuned_var_int(const char *name, int dflt, int is_bool)
+{
+    const int idx = mca_base_var_find("ompi", "coll", "tuned", name);
+    const void *v = NULL;
+    if (idx < 0 || OPAL_SUCCESS != mca_base_var_get_value(idx, &v, NULL, NULL) || NULL == v) return dflt;
+    return is_bool ? (int) *(const bool *) v : *(const int *) v;
+}
+
+static int tuned_var_set_string(const char *name)
+{
+    const int idx = mca_base_var_find("ompi", "coll", "tuned", name);
+    const void *v = NULL;
+    if (idx < 0 || OPAL_SUCCESS != mca_base_var_get_value(idx, &v, NULL, NULL) || NULL == v) return 0;
+    const char *str = *(char *const *) v;
+    return NULL != str && '\0' != str[0];
+}
+
+/*
+ * coll/tuned's own forcing, as its module reads it at communicator creation
+ * (coll_tuned_module.c:211-231, coll_tuned_component.c:170-192): only with
+ * coll_tuned_use_dynamic_rules, a forced algorithm per collective
+ * (coll_tuned_<coll>_algorithm) and a rules file
+ * (coll_tuned_dynamic_rules_filename, read per communicator and message size
+ * by coll_tuned_dynamic_file.c:57).  The device path must fold in the order
+ * coll/tuned would, so each forced algorithm it implements goes to the
+ * library; a blocking reduction whose tuned algorithm it does not implement
+ * — or any of them under a rules file, whose per-size choices the library
+ * does not replay — is declined here and runs in the saved function (on host
+ * copies of device operands, as every declined call does).  Nonblocking and
+ * persistent reductions are libnbc's in the reference, which these variables
+ * do not steer.
+ */
+static void rocm_tuned_config(mca_coll_rocm_module_t *m)
+{
+    const int dyn = tuned_var_int("use_dynamic_rules", 0, 1);
+    int ar = 0, red = 0, rs = 0, rsb = 0, red_ok;
+    m->tuned_decline = 0;
+    if (dyn && tuned_var_set_string("dynamic_rules_filename"))
+        m->tuned_decline = ROCM_TUNED_ALLREDUCE | ROCM_TUNED_REDUCE | ROCM_TUNED_RS | ROCM_TUNED_RSB;
+    if (dyn) {  /* without dynamic rules tuned ignores its forcing variables */
+        ar = tuned_var_int("allreduce_algorithm", 0, 0);
+        red = tuned_var_int("reduce_algorithm", 0, 0);
+        rs = tuned_var_int("reduce_scatter_algorithm", 0, 0);
+        rsb = tuned_var_int("reduce_scatter_block_algorithm", 0, 0);
+    }
+    red_ok = OMPI_AMD_SUCCESS == ompi_amd_comm_set_param(m->dev_comm, "tuned_reduce_algorithm", red);
+    if (!red_ok) m->tuned_decline |= ROCM_TUNED_REDUCE;
+    /* allreduce 2 (nonoverlapping) reduces through coll/tuned's reduce */
+    if (OMPI_AMD_SUCCESS != ompi_amd_comm_set_param(m->dev_comm, "tuned_allreduce_algorithm", ar) ||
+        (2 == ar && !red_ok))
+        m->tuned_decline |= ROCM_TUNED_ALLREDUCE;
+    /* reduce_scatter 1 (non-overlapping) reduces through it too */
+    if (OMPI_AMD_SUCCESS != ompi_amd_comm_set_param(m->dev_comm, "tuned_reduce_scatter_algorithm", rs) ||
+        (1 == rs && !red_ok))
+        m->tuned_decline |= ROCM_TUNED_RS;
+    /* reduce_scatter_block: basic_linear (the fixed choice, 1) reduces through it */
+    if (OMPI_AMD_SUCCESS != ompi_amd_comm_set_param(m->dev_comm, "tuned_reduce_scatter_block_algorithm",
+                                                    rsb) || !red_ok)
+        m->tuned_decline |= ROCM_TUNED_RSB;
 }
 
 /* ------------------------------------------------------------- module */
@@ -177,6 +253,7 @@ static void rocm_module_construct(mca_coll_rocm_module_t *m)
     m->forced = 0;
     m->streak_dev = m->streak_host = 0;
     m->since_check = m->mismatched = 0;
+    m->tuned_decline = 0;
     for (int k = 0; k < 2; ++k) {
         m->dstage[k] = m->hstage[k] = NULL;
         m->dstage_bytes[k] = m->hstage_bytes[k] = 0;
@@ -323,6 +400,8 @@ int mca_coll_rocm_module_enable(mca_coll_base_module_t *module, struct ompi_comm
     (void) ompi_amd_comm_set_param(m->dev_comm, "user_ipc", mca_coll_rocm_component.user_ipc);
     (void) ompi_amd_comm_set_param(m->dev_comm, "land_blocking", mca_coll_rocm_component.land_blocking);
     (void) ompi_amd_comm_set_param(m->dev_comm, "copy_nt", mca_coll_rocm_component.copy_nt);
+    (void) ompi_amd_comm_set_param(m->dev_comm, "own_stream", mca_coll_rocm_component.own_stream);
+    rocm_tuned_config(m);
     /* last: setting the scheme turns autotuning off */
     (void) ompi_amd_comm_set_param(m->dev_comm, "autotune", mca_coll_rocm_component.autotune);
     if (ROCM_RES_DEVICE == mca_coll_rocm_component.residency ||
@@ -646,7 +725,8 @@ int mca_coll_rocm_allreduce(const void *sbuf, void *rbuf, int count,
     rocm_operand_t o[2] = {{(void *) sbuf, (size_t) count, dtype, 1, 0},
                            {rbuf, (size_t) count, dtype, inplace, 1}};
     int path, rc;
-    rc = rocm_begin(m, reduction_ok_n(dtype, op, (size_t) count), dev(sbuf) && dev(rbuf), o, 2, &path);
+    rc = rocm_begin(m, reduction_ok_n(dtype, op, (size_t) count) && !(m->tuned_decline & ROCM_TUNED_ALLREDUCE),
+                    dev(sbuf) && dev(rbuf), o, 2, &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
         rc = m->c_coll.coll_allreduce(o[0].use, o[1].use, count, dtype, op, comm,
@@ -671,7 +751,7 @@ int mca_coll_rocm_reduce(const void *sbuf, void *rbuf, int count, struct ompi_da
     rocm_operand_t o[2] = {{(void *) sbuf, (size_t) count, dtype, 1, 0},
                            {is_root ? rbuf : NULL, (size_t) count, dtype, MPI_IN_PLACE == sbuf, 1}};
     int path, rc;
-    rc = rocm_begin(m, reduction_ok_n(dtype, op, (size_t) count),
+    rc = rocm_begin(m, reduction_ok_n(dtype, op, (size_t) count) && !(m->tuned_decline & ROCM_TUNED_REDUCE),
                     is_root ? dev(rbuf) && dev(sbuf) : ompi_amd_is_device_pointer(sbuf), o, 2, &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
@@ -734,7 +814,8 @@ int mca_coll_rocm_reduce_scatter(const void *sbuf, void *rbuf, const int *rcount
         rocm_operand_t o[2] = {{(void *) sbuf, total, dtype, 1, 0},
                                {rbuf, inplace ? total : (size_t) rcounts[ompi_comm_rank(comm)],
                                 dtype, inplace, 1}};
-        rc = rocm_begin(m, reduction_ok_n(dtype, op, total), dev(sbuf) && dev(rbuf), o, 2, &path);
+        rc = rocm_begin(m, reduction_ok_n(dtype, op, total) && !(m->tuned_decline & ROCM_TUNED_RS),
+                        dev(sbuf) && dev(rbuf), o, 2, &path);
         if (OMPI_SUCCESS != rc) return rc;
         if (ROCM_DEVICE != path) {
             rc = m->c_coll.coll_reduce_scatter(o[0].use, o[1].use, rcounts, dtype, op, comm,
@@ -759,7 +840,8 @@ int mca_coll_rocm_reduce_scatter_block(const void *sbuf, void *rbuf, int rcount,
     rocm_operand_t o[2] = {{(void *) sbuf, all, dtype, 1, 0},
                            {rbuf, inplace ? all : (size_t) rcount, dtype, inplace, 1}};
     int path, rc;
-    rc = rocm_begin(m, reduction_ok_n(dtype, op, all), dev(sbuf) && dev(rbuf), o, 2, &path);
+    rc = rocm_begin(m, reduction_ok_n(dtype, op, all) && !(m->tuned_decline & ROCM_TUNED_RSB),
+                    dev(sbuf) && dev(rbuf), o, 2, &path);
     if (OMPI_SUCCESS != rc) return rc;
     if (ROCM_DEVICE != path) {
         rc = m->c_coll.coll_reduce_scatter_block(o[0].use, o[1].use, rcount, dtype, op, comm,

@@ -43,6 +43,9 @@ typedef struct ompi_osc_rocm_component_t {
     ompi_osc_base_component_t super;
     int priority;    /* osc_rocm_priority */
     int timeout_ms;  /* osc_rocm_timeout_ms */
+    int separate_model; /* osc_rocm_separate_model: MPI_Win_create memory peers cannot map gets a
+                         * public copy (MPI_WIN_SEPARATE); 0 refuses such a window on every rank */
+    int own_stream;     /* osc_rocm_own_stream: a window's epochs on a hardware queue of their own */
     unsigned windows;  /* windows created so far (names the device communicator) */
 } ompi_osc_rocm_component_t;
 

@@ -69,6 +69,8 @@ ompi_osc_rocm_component_t mca_osc_rocm_component = {
     },
     .priority = 101,
     .timeout_ms = 30000,
+    .separate_model = 1,
+    .own_stream = 1,
     .windows = 0,
 };
 
@@ -84,6 +86,23 @@ static int rocm_register(void)
                                            MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_9,
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_osc_rocm_component.timeout_ms);
+    (void) mca_base_component_var_register(c, "separate_model",
+                                           "1: an MPI_Win_create window over memory its peers cannot "
+                                           "map as it is (not an IPC-safe size, or allocated before an "
+                                           "IPC close of the process) runs in MPI's separate memory "
+                                           "model through a public copy (MPI_WIN_MODEL then reports "
+                                           "MPI_WIN_SEPARATE); 0: such a window fails on every rank",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_9,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_osc_rocm_component.separate_model);
+    (void) mca_base_component_var_register(c, "own_stream",
+                                           "1: a window's epochs and RMA run on a stream with a "
+                                           "hardware queue of its own (a lock or PSCW wait on the "
+                                           "device never queues in front of other communicators' "
+                                           "kernels)",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_9,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_osc_rocm_component.own_stream);
     return OMPI_SUCCESS;
 }
 
@@ -670,6 +689,9 @@ static int rocm_query(struct ompi_win_t *win, void **base, size_t size, int disp
 {
     bool dev = false;
     int flag = 0, v[2] = {0, 0};  /* some rank has device memory / host memory */
+    /* a refusal is for the select that follows this query: a query whose
+     * select never ran (another component won) leaves nothing behind */
+    mixed_win = NULL;
     if (ompi_amd_device_count() <= 0 || OMPI_COMM_IS_INTER(comm) ||
         ompi_group_have_remote_peers(comm->c_local_group) ||
         ompi_comm_size(comm) > OMPI_AMD_MAX_RANKS)
@@ -721,6 +743,8 @@ static int rocm_select(struct ompi_win_t *win, void **base, size_t size, int dis
         return to_ompi_err(rc);
     }
     (void) ompi_amd_comm_set_param(m->dev_comm, "timeout_ms", mca_osc_rocm_component.timeout_ms);
+    (void) ompi_amd_comm_set_param(m->dev_comm, "osc_win_separate", mca_osc_rocm_component.separate_model);
+    (void) ompi_amd_comm_set_param(m->dev_comm, "own_stream", mca_osc_rocm_component.own_stream);
     /* agreed in rocm_query already; the library confirms it on its own
      * rendezvous (a failure here fails every rank alike) */
     local_ok = MPI_WIN_FLAVOR_CREATE != flavor || 0 == size ||

@@ -52,6 +52,7 @@ mca_pml_rocm_component_t mca_pml_rocm_component = {
     },
     .enable = 1,
     .timeout_ms = 0,
+    .own_stream = 1,
     .host_path = 0,
 };
 
@@ -67,6 +68,14 @@ static int rocm_register(void)
                                            MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
                                            MCA_BASE_VAR_SCOPE_READONLY,
                                            &mca_pml_rocm_component.enable);
+    (void) mca_base_component_var_register(c, "own_stream",
+                                           "1: a communicator's device transfers run on a stream with "
+                                           "a hardware queue of its own (a receive's copy waiting on "
+                                           "the device for its sender never queues in front of "
+                                           "another communicator's kernels)",
+                                           MCA_BASE_VAR_TYPE_INT, NULL, 0, 0, OPAL_INFO_LVL_6,
+                                           MCA_BASE_VAR_SCOPE_READONLY,
+                                           &mca_pml_rocm_component.own_stream);
     (void) mca_base_component_var_register(c, "timeout_ms",
                                            "Host wait limit of a library transfer (0: none, MPI "
                                            "semantics)",
@@ -135,6 +144,7 @@ static int rocm_add_comm(struct ompi_communicator_t *comm)
     }
     /* host waits follow MPI: no limit unless the parameter sets one */
     (void) ompi_amd_comm_set_param(dev, "p2p_timeout_ms", mca_pml_rocm_component.timeout_ms);
+    (void) ompi_amd_comm_set_param(dev, "own_stream", mca_pml_rocm_component.own_stream);
     e = (struct rocm_comm *) calloc(1, sizeof(*e));
     if (NULL == e) {
         (void) ompi_amd_comm_destroy(dev);

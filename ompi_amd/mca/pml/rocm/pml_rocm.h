@@ -45,6 +45,7 @@ typedef struct mca_pml_rocm_component_t {
     mca_pml_base_component_2_0_0_t super;
     int enable;          /* pml_rocm_enable (1): interpose at close */
     int timeout_ms;      /* pml_rocm_timeout_ms: host wait limit (0, the default: none) */
+    int own_stream;      /* pml_rocm_own_stream: a communicator's transfers on a hardware queue of their own */
     int host_path;       /* pml_rocm_host_path: 1 = host buffers to the saved PML */
 } mca_pml_rocm_component_t;
 

@@ -152,6 +152,20 @@ class Window:
             _lib.check(m, "win_model")
         return m
 
+    def copies(self):
+        """Diagnostics: (private, public, snapshot) device addresses of this
+        rank's copies; public and snapshot are 0 where the window is unified."""
+        p, q, s = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        _lib.check(self._lib.ompi_amd_win_copies(self._h, ctypes.byref(p), ctypes.byref(q),
+                                                 ctypes.byref(s)), "win_copies")
+        return p.value or 0, q.value or 0, s.value or 0
+
+    def peer_base(self, peer: int) -> int:
+        """Diagnostics: the address RMA toward `peer` targets in this process."""
+        b = ctypes.c_void_p()
+        _lib.check(self._lib.ompi_amd_win_peer_base(self._h, peer, ctypes.byref(b)), "win_peer_base")
+        return b.value or 0
+
     def sync(self, stream=None) -> None:
         """MPI_Win_sync: the public and private copies merged."""
         _lib.check(self._lib.ompi_amd_win_sync(self._h, _stream(stream)), "win_sync")

@@ -368,6 +368,17 @@ int orc_allreduce(int algorithm, int n, const void *const *sb, void *const *rb,
 int orc_allreduce_forced(int algorithm, int n, const void *const *sb, void *const *rb,
                          size_t count, int op, int type, size_t segsize, int root0_inplace)
 {
+    return orc_allreduce_forced_red(algorithm, n, sb, rb, count, op, type, segsize, root0_inplace,
+                                    ORC_RED_TUNED);
+}
+
+/* red_alg: the algorithm of coll/tuned's reduce that nonoverlapping calls
+ * through comm->c_coll->coll_reduce (its own forced reduce algorithm when
+ * dynamic rules are on; ORC_RED_TUNED = the fixed decision). */
+int orc_allreduce_forced_red(int algorithm, int n, const void *const *sb, void *const *rb,
+                             size_t count, int op, int type, size_t segsize, int root0_inplace,
+                             int red_alg)
+{
     const size_t ext = orc_type_extent(type);
     if (n < 1 || ext == 0 || !orc_op_defined(op, type)) return -1;
     if (count == 0) return algorithm;
@@ -394,7 +405,7 @@ int orc_allreduce_forced(int algorithm, int n, const void *const *sb, void *cons
     case ORC_AR_BASIC_LINEAR:
         return ar_reduce_bcast(n, sb, rb, count, op, type, ORC_RED_LINEAR, 0, ORC_AR_BASIC_LINEAR);
     case ORC_AR_NONOVERLAPPING:
-        return ar_reduce_bcast(n, sb, rb, count, op, type, ORC_RED_TUNED, root0_inplace,
+        return ar_reduce_bcast(n, sb, rb, count, op, type, red_alg, root0_inplace,
                                ORC_AR_NONOVERLAPPING);
     case ORC_AR_RECURSIVE_DOUBLING: return ar_recursive_doubling(n, sb, rb, count, op, type);
     case ORC_AR_RING: return ar_ring(n, sb, rb, count, op, type);

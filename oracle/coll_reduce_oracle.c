@@ -198,8 +198,26 @@ int orc_reduce(int algorithm, int n, const void *const *sb, void *rbuf_root, siz
     return algorithm;
 }
 
-/* rsb basic_linear: tuned reduce of n*rcount elements to rank 0 (never in
- * place at the reduce level: sbuf = rbuf is passed as sbuf), then scatter. */
+/* rsb basic_linear (coll_base_reduce_scatter_block.c:54-111): a reduce of
+ * n*rcount elements to rank 0 through comm->c_coll->coll_reduce — coll/tuned's,
+ * so its forced algorithm (red_alg, ORC_RED_*; 0 = the fixed decision) when
+ * dynamic rules are on — never in place at the reduce level (sbuf = rbuf is
+ * passed as sbuf), then scatter. */
+int orc_reduce_scatter_block_alg(int n, const void *const *sb, void *const *rb,
+                                 size_t rcount, int op, int type, int red_alg)
+{
+    const size_t ext = orc_type_extent(type), total = rcount * (size_t)n;
+    char *acc;
+    int r, alg;
+    if (ext == 0 || !orc_op_defined(op, type)) return -1;
+    acc = malloc(total * ext + 1);
+    alg = orc_reduce(red_alg, n, sb, acc, total, op, type, 0, 0);
+    if (alg < 0) { free(acc); return alg; }
+    for (r = 0; r < n; r++) memcpy(rb[r], acc + (size_t)r * rcount * ext, rcount * ext);
+    free(acc);
+    return alg;
+}
+
 int orc_reduce_scatter_block(int n, const void *const *sb, void *const *rb,
                              size_t rcount, int op, int type)
 {
@@ -372,6 +390,32 @@ static void rs_ring(int n, const void *const *sb, void *const *rb, const size_t 
     }
     for (r = 0; r < n; r++) { free(acc[r]); free(msg[r]); free(nmsg[r]); }
     free(acc); free(msg); free(nmsg); free(disps);
+}
+
+/* reduce_scatter non-overlapping (coll_base_reduce_scatter.c:42-92): a
+ * reduce of the whole vector to rank 0 through comm->c_coll->coll_reduce
+ * (coll/tuned's: red_alg as above), rank 0 in place when it passed
+ * MPI_IN_PLACE (:62-68), then scatterv of the blocks. */
+int orc_reduce_scatter_nonoverlapping(int n, const void *const *sb, void *const *rb,
+                                      const size_t *rcounts, int op, int type, int red_alg,
+                                      int inplace)
+{
+    const size_t ext = orc_type_extent(type);
+    size_t total = 0, off = 0;
+    char *acc;
+    int r, alg;
+    if (n < 1 || ext == 0 || !orc_op_defined(op, type)) return -1;
+    for (r = 0; r < n; r++) total += rcounts[r];
+    if (total == 0) return 0;
+    acc = malloc(total * ext + 1);
+    alg = orc_reduce(red_alg, n, sb, acc, total, op, type, 0, inplace);
+    if (alg < 0) { free(acc); return alg; }
+    for (r = 0; r < n; r++) {
+        memcpy(rb[r], acc + off * ext, rcounts[r] * ext);
+        off += rcounts[r];
+    }
+    free(acc);
+    return alg;
 }
 
 int orc_reduce_scatter(int algorithm, int n, const void *const *sb, void *const *rb,

@@ -89,6 +89,9 @@ int orc_allreduce(int algorithm, int nranks, const void *const *sbufs,
 int orc_allreduce_forced(int algorithm, int nranks, const void *const *sbufs,
                          void *const *rbufs, size_t count, int op, int type,
                          size_t segsize, int root0_inplace);
+int orc_allreduce_forced_red(int algorithm, int nranks, const void *const *sbufs,
+                             void *const *rbufs, size_t count, int op, int type, size_t segsize,
+                             int root0_inplace, int red_alg);
 
 /* Block partition COLL_BASE_COMPUTE_BLOCKCOUNT (coll_base_functions.h:425-431) */
 void orc_blockcount(size_t count, int nblocks, size_t *split,
@@ -118,6 +121,11 @@ int orc_reduce_scatter_block(int nranks, const void *const *sbufs,
 /* reduce_scatter with per-rank counts (coll_tuned_decision_fixed.c:466-512,
  * coll_base_reduce_scatter.c:132-623).  rbufs[r] receives rcounts[r]
  * elements.  Returns the algorithm run. */
+int orc_reduce_scatter_block_alg(int nranks, const void *const *sbufs, void *const *rbufs,
+                                 size_t rcount, int op, int type, int red_alg);
+int orc_reduce_scatter_nonoverlapping(int nranks, const void *const *sbufs, void *const *rbufs,
+                                      const size_t *rcounts, int op, int type, int red_alg,
+                                      int inplace);
 enum { ORC_RS_TUNED = 0, ORC_RS_HALVING = 1, ORC_RS_RING = 2 };
 int orc_reduce_scatter_decision(int nranks, size_t total_bytes);
 int orc_reduce_scatter(int algorithm, int nranks, const void *const *sbufs,

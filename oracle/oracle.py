@@ -50,6 +50,12 @@ def lib():
                                            c.c_size_t, c.c_int]
         L.orc_reduce_scatter_block.argtypes = [c.c_int, c.POINTER(c.c_void_p),
                                                c.POINTER(c.c_void_p), c.c_size_t, c.c_int, c.c_int]
+        L.orc_reduce_scatter_block_alg.argtypes = [c.c_int, c.POINTER(c.c_void_p),
+                                                   c.POINTER(c.c_void_p), c.c_size_t, c.c_int,
+                                                   c.c_int, c.c_int]
+        L.orc_reduce_scatter_nonoverlapping.argtypes = [c.c_int, c.POINTER(c.c_void_p),
+                                                        c.POINTER(c.c_void_p), c.POINTER(c.c_size_t),
+                                                        c.c_int, c.c_int, c.c_int, c.c_int]
         L.orc_reduce_decision.argtypes = [c.c_int, c.c_size_t, c.c_size_t]
         L.orc_reduce.argtypes = [c.c_int, c.c_int, c.POINTER(c.c_void_p), c.c_void_p,
                                  c.c_size_t, c.c_int, c.c_int, c.c_int, c.c_int]
@@ -125,13 +131,15 @@ def allreduce_forced(sbufs: list[np.ndarray], count: int, op: int, type_code: in
 
 
 def reduce_scatter_block(sbufs: list[np.ndarray], rcount: int, op: int,
-                         type_code: int) -> list[np.ndarray]:
+                         type_code: int, red_alg: int = 0) -> list[np.ndarray]:
+    """basic_linear rsb; red_alg: coll/tuned's forced reduce algorithm
+    (RED_*, 0 = its fixed decision) for the reduce it calls."""
     n = len(sbufs)
     ext = lib().orc_type_extent(type_code)
     rbufs = [np.zeros(rcount * ext, dtype=np.uint8) for _ in range(n)]
     sp = (ctypes.c_void_p * n)(*[_p(s) for s in sbufs])
     rp = (ctypes.c_void_p * n)(*[_p(r) for r in rbufs])
-    if lib().orc_reduce_scatter_block(n, sp, rp, rcount, op, type_code) < 0:
+    if lib().orc_reduce_scatter_block_alg(n, sp, rp, rcount, op, type_code, red_alg) < 0:
         raise ValueError("oracle rsb failed")
     return rbufs
 
@@ -157,6 +165,7 @@ def reduce(sbufs: list[np.ndarray], count: int, op: int, type_code: int, root: i
 
 
 RS_TUNED, RS_HALVING, RS_RING = 0, 1, 2
+RS_NONOVERLAPPING = 3  # reduce to rank 0 (coll/tuned's, red_alg) + scatterv
 
 
 def reduce_scatter_decision(n: int, total_bytes: int) -> int:
@@ -164,7 +173,8 @@ def reduce_scatter_decision(n: int, total_bytes: int) -> int:
 
 
 def reduce_scatter(sbufs: list[np.ndarray], rcounts: list[int], op: int, type_code: int,
-                   algorithm: int = RS_TUNED) -> tuple[list[np.ndarray], int]:
+                   algorithm: int = RS_TUNED, red_alg: int = 0,
+                   inplace: bool = False) -> tuple[list[np.ndarray], int]:
     """coll/tuned reduce_scatter: (per-rank results, algorithm run)."""
     n = len(sbufs)
     rbufs = [np.zeros(max(1, rc), dtype=sbufs[0].dtype)[:rc] for rc in rcounts]
@@ -173,7 +183,12 @@ def reduce_scatter(sbufs: list[np.ndarray], rcounts: list[int], op: int, type_co
     sp = (ctypes.c_void_p * n)(*[_p(s) for s in sbufs])
     rp = (ctypes.c_void_p * n)(*[_p(r) for r in rbufs])
     rc = (ctypes.c_size_t * n)(*rcounts)
-    alg = lib().orc_reduce_scatter(algorithm, n, sp, rp, rc, op, type_code)
+    if algorithm == RS_NONOVERLAPPING:
+        alg = lib().orc_reduce_scatter_nonoverlapping(n, sp, rp, rc, op, type_code, red_alg,
+                                                      1 if inplace else 0)
+        alg = RS_NONOVERLAPPING if alg >= 0 else alg
+    else:
+        alg = lib().orc_reduce_scatter(algorithm, n, sp, rp, rc, op, type_code)
     if alg < 0:
         raise ValueError(f"oracle reduce_scatter failed ({alg})")
     return [r[:c] for r, c in zip(rbufs, rcounts)], alg

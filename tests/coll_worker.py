@@ -787,7 +787,7 @@ def case_iallreduce_many(comm, rank, n, salt, calls=12):
     return not msgs, "; ".join(msgs)
 
 
-def case_cross_comm_order(comm, rank, n, salt, stream_per_comm=False):
+def case_cross_comm_order(comm, rank, n, salt, stream_per_comm=False, own=False):
     """Two communicators over the same ranks, nonblocking allreduces posted
     in OPPOSITE orders on even and odd ranks (MPI orders collectives per
     communicator only: rank 0 posts A then B while rank 1 posts B then A,
@@ -800,6 +800,9 @@ def case_cross_comm_order(comm, rank, n, salt, stream_per_comm=False):
     F = mop.MPI_FLOAT
     comm2 = coll.Communicator.from_torch_distributed(device=comm.device)
     comm2.set_param("timeout_ms", 20000)
+    if own:  # what coll/rocm sets (coll_rocm_own_stream): each communicator on a queue of its own
+        comm.set_param("own_stream", 1)
+        comm2.set_param("own_stream", 1)
     s1 = torch.cuda.Stream()
     s2 = torch.cuda.Stream() if stream_per_comm else s1
     msgs = []
@@ -857,6 +860,8 @@ def case_cross_comm_order(comm, rank, n, salt, stream_per_comm=False):
                 break
     finally:
         comm2.free()
+        if own:
+            comm.set_param("own_stream", 0)
     return not msgs, "; ".join(msgs[:3])
 
 
@@ -1605,6 +1610,9 @@ def main():
                 comm, rank, n, D, mop.MPI_SUM, big // 2, 112, inplace=True), 2))),
         ]
     only = os.environ.get("COLL_CASES")
+    # the MPI path (coll/rocm's own_stream): opposite-order nonblocking and
+    # persistent calls on two communicators complete
+    cases += [("cross_comm_order_own_stream", lambda: case_cross_comm_order(comm, rank, n, 192, own=True))]
     if only and "cross_comm" in only:
         # opt-in: the known limitation of DESIGN.md §8 item 9 (device-side
         # waits across communicators posted in opposite orders time out)

@@ -476,6 +476,134 @@ static int bench(mca_coll_base_comm_coll_t *t, ompi_communicator_t *comm, ompi_d
     return 0;
 }
 
+/* ---- section T: coll/tuned's forcing variables (HARNESS_TUNED=1) ----
+ * Run with some of OMPI_MCA_coll_tuned_{use_dynamic_rules, allreduce_algorithm,
+ * reduce_algorithm, reduce_scatter_algorithm, reduce_scatter_block_algorithm,
+ * dynamic_rules_filename} in the environment (the harness's MCA variable
+ * stand-in reads them as the MCA system would).  Each blocking reduction
+ * either runs on the device in exactly the order coll/tuned would run with
+ * those settings (the oracle's forced algorithms, fp SUM, bit-exact), or —
+ * where the glue does not implement that order — reaches the saved function
+ * (tuned_calls) and returns what it computed. */
+static int env_int(const char *n)
+{
+    const char *v = getenv(n);
+    return v ? atoi(v) : 0;
+}
+
+static void tuned_section(mca_coll_base_comm_coll_t *t, ompi_communicator_t *comm, ompi_datatype_t *df,
+                          ompi_op_t *sum)
+{
+    const int dyn = env_int("OMPI_MCA_coll_tuned_use_dynamic_rules");
+    const char *file = getenv("OMPI_MCA_coll_tuned_dynamic_rules_filename");
+    const int rules = dyn && file && file[0];
+    const int ar = dyn ? env_int("OMPI_MCA_coll_tuned_allreduce_algorithm") : 0;
+    const int red = dyn ? env_int("OMPI_MCA_coll_tuned_reduce_algorithm") : 0;
+    const int rs = dyn ? env_int("OMPI_MCA_coll_tuned_reduce_scatter_algorithm") : 0;
+    const int rsb = dyn ? env_int("OMPI_MCA_coll_tuned_reduce_scatter_block_algorithm") : 0;
+    const int red_ok = red == 0 || red == 1 || red == 3 || red == 4 || red == 5;
+    const int dev_red = !rules && red_ok;
+    const int dev_ar = !rules && ar >= 0 && ar <= 6 && !(ar == 2 && !red_ok);
+    const int dev_rs = !rules && rs >= 0 && rs <= 3 && !(rs == 1 && !red_ok);
+    const int dev_rsb = !rules && (rsb == 0 || rsb == 1) && red_ok;
+    const size_t sizes[2] = {3000, 400003};  /* staged and zero-copy */
+    const int root = g_size - 1;
+    for (int k = 0; k < 2; ++k) {
+        const size_t n = sizes[k];
+        float **xs = all_inputs(n, 90 + k);
+        float **rb = malloc(sizeof(float *) * (size_t) g_size);
+        float *exp = calloc(n, sizeof(float));
+        void *ds = dev_of(xs[g_rank], n * 4), *dr = dev_of(exp, n * 4);
+        int calls;
+        for (int r = 0; r < g_size; ++r) rb[r] = calloc(n, sizeof(float));
+        /* allreduce */
+        if (dev_ar) {
+            CHECK(orc_allreduce_forced_red(ar, g_size, (const void *const *) xs, (void *const *) rb, n,
+                                           ORC_OP_SUM, ORC_T_FLOAT, 0, 0, red) >= 0, "oracle allreduce");
+            memcpy(exp, rb[g_rank], n * 4);
+        } else {
+            harness_expect_reduction(HARNESS_ALLREDUCE, ORC_OP_SUM, df, (const char *const *) xs, g_size,
+                                     g_rank, n, (char *) exp);
+        }
+        calls = tuned_calls;
+        CHECK(t->coll_allreduce(ds, dr, (int) n, df, sum, comm, t->coll_allreduce_module) == OMPI_SUCCESS,
+              "forced allreduce");
+        CHECK((tuned_calls - calls) == !dev_ar, "allreduce %d: saved calls %d, want %d", ar,
+              tuned_calls - calls, !dev_ar);
+        expect_dev(dr, exp, n * 4, dev_ar ? "forced allreduce" : "declined allreduce");
+        /* reduce to the last rank */
+        if (dev_red) {
+            CHECK(orc_reduce(red, g_size, (const void *const *) xs, exp, n, ORC_OP_SUM, ORC_T_FLOAT, root,
+                             0) >= 0, "oracle reduce");
+        } else {
+            harness_expect_reduction(HARNESS_ALLREDUCE, ORC_OP_SUM, df, (const char *const *) xs, g_size,
+                                     g_rank, n, (char *) exp);
+        }
+        calls = tuned_calls;
+        CHECK(t->coll_reduce(ds, g_rank == root ? dr : NULL, (int) n, df, sum, root, comm,
+                             t->coll_reduce_module) == OMPI_SUCCESS, "forced reduce");
+        CHECK((tuned_calls - calls) == !dev_red, "reduce %d: saved calls %d", red, tuned_calls - calls);
+        if (g_rank == root) expect_dev(dr, exp, n * 4, dev_red ? "forced reduce" : "declined reduce");
+        /* reduce_scatter_block: n / size elements each */
+        {
+            const size_t rc = n / (size_t) g_size;
+            if (dev_rsb) {
+                CHECK(orc_reduce_scatter_block_alg(g_size, (const void *const *) xs, (void *const *) rb, rc,
+                                                   ORC_OP_SUM, ORC_T_FLOAT, red) >= 0, "oracle rsb");
+                memcpy(exp, rb[g_rank], rc * 4);
+            } else {
+                float *all = calloc(n, sizeof(float));
+                harness_expect_reduction(HARNESS_ALLREDUCE, ORC_OP_SUM, df, (const char *const *) xs,
+                                         g_size, g_rank, rc * (size_t) g_size, (char *) all);
+                memcpy(exp, all + rc * (size_t) g_rank, rc * 4);
+                free(all);
+            }
+            calls = tuned_calls;
+            CHECK(t->coll_reduce_scatter_block(ds, dr, (int) rc, df, sum, comm,
+                                               t->coll_reduce_scatter_block_module) == OMPI_SUCCESS,
+                  "forced rsb");
+            CHECK((tuned_calls - calls) == !dev_rsb, "rsb %d/%d: saved calls %d", rsb, red, tuned_calls - calls);
+            expect_dev(dr, exp, rc * 4, dev_rsb ? "forced rsb" : "declined rsb");
+        }
+        /* reduce_scatter, uneven blocks */
+        {
+            int rcounts[OMPI_AMD_MAX_RANKS];
+            size_t rcz[OMPI_AMD_MAX_RANKS], tot = 0;
+            for (int r = 0; r < g_size; ++r) {
+                rcounts[r] = (int) (n / (size_t) g_size) - 3 * r;
+                rcz[r] = (size_t) rcounts[r];
+                tot += rcz[r];
+            }
+            if (dev_rs) {
+                if (rs == 1) {
+                    CHECK(orc_reduce_scatter_nonoverlapping(g_size, (const void *const *) xs, (void *const *) rb,
+                                                            rcz, ORC_OP_SUM, ORC_T_FLOAT, red, 0) >= 0,
+                          "oracle rs nonoverlapping");
+                } else {
+                    CHECK(orc_reduce_scatter(rs == 2 ? ORC_RS_HALVING : rs == 3 ? ORC_RS_RING : ORC_RS_TUNED,
+                                             g_size, (const void *const *) xs, (void *const *) rb, rcz,
+                                             ORC_OP_SUM, ORC_T_FLOAT) >= 0, "oracle rs");
+                }
+                memcpy(exp, rb[g_rank], rcz[g_rank] * 4);
+            } else {
+                harness_expect_rs(ORC_OP_SUM, df, (const char *const *) xs, g_size, g_rank, rcounts, (char *) exp);
+            }
+            (void) tot;
+            calls = tuned_calls;
+            CHECK(t->coll_reduce_scatter(ds, dr, rcounts, df, sum, comm, t->coll_reduce_scatter_module) ==
+                      OMPI_SUCCESS, "forced reduce_scatter");
+            CHECK((tuned_calls - calls) == !dev_rs, "rs %d/%d: saved calls %d", rs, red, tuned_calls - calls);
+            expect_dev(dr, exp, rcz[g_rank] * 4, dev_rs ? "forced reduce_scatter" : "declined reduce_scatter");
+        }
+        harness_dev_free(ds);
+        harness_dev_free(dr);
+        for (int r = 0; r < g_size; ++r) free(rb[r]);
+        free(rb);
+        free(exp);
+        free_inputs(xs);
+    }
+}
+
 int main(int argc, char **argv)
 {
     const int use_gpu = getenv("HARNESS_GPU") && atoi(getenv("HARNESS_GPU"));
@@ -553,6 +681,15 @@ int main(int argc, char **argv)
     }
     /* sections 1-8: the per-call residency vote (never locks) */
     mca_coll_rocm_component.residency_lock = 0;
+    if (getenv("HARNESS_TUNED") && atoi(getenv("HARNESS_TUNED"))) {
+        tuned_section(&table, &comm, &dfloat, &sum);
+        release_table(&table);
+        OBJ_RELEASE(m);
+        OBJ_RELEASE(tm);
+        harness_saved_fini();
+        printf("ok gpu tuned\n");
+        return 0;
+    }
 
     /* 1. allreduce: staged (1000) and zero-copy (300001) sizes */
     {

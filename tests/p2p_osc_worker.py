@@ -108,6 +108,42 @@ def case_aged_buffer_staged(comm, rank, n, salt, nbytes=(8 << 20) + 12):
     return ok, msg
 
 
+def case_stage_cap_aged(comm, rank, n, salt, nbytes=(4 << 20) + 8, k=8):
+    """Staged sends (p2p_user_ipc = 0) with the send-stage pool at its cap
+    (p2p_stage_mib 8, k outstanding sends of 4 MiB + 8 each way) and every
+    buffer older than an IPC close (test hook p2p_age_all): a send that finds
+    no free stage must not go out from the buffer itself (it may not be
+    exportable) nor wait for the receiver — it takes a stage past the cap;
+    every message byte-exact, p2p_unsafe_sends counts the ones past the cap.
+    (the fallback to exporting the user buffer.)"""
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    cap0 = comm.get_param("p2p_stage_mib")
+    comm.set_param("p2p_stage_mib", 8)
+    comm.set_param("p2p_age_all", 1)
+    try:
+        u0, d0 = comm.get_param("p2p_unsafe_sends"), comm.get_param("p2p_direct_sends")
+        srcs = [dev(payload(rank, salt + j, nbytes)) for j in range(k)]
+        sreqs = [pml.isend(comm, srcs[j], nxt, 40 + j, stream=STREAM) for j in range(k)]
+        rbufs = [zeros(nbytes) for _ in range(k)]
+        rreqs = [pml.irecv(comm, rbufs[j], prv, 40 + j, stream=STREAM) for j in range(k)]
+        for j in range(k):
+            rreqs[j].wait()
+            ok, msg = eq(host(rbufs[j]), payload(prv, salt + j, nbytes), f"message {j}")
+            if not ok:
+                return ok, msg
+            rreqs[j].free()
+        for rq in sreqs:
+            rq.wait()
+            rq.free()
+        u1, d1 = comm.get_param("p2p_unsafe_sends"), comm.get_param("p2p_direct_sends")
+    finally:
+        comm.set_param("p2p_age_all", 0)
+        comm.set_param("p2p_stage_mib", cap0)
+    if d1 != d0 or u1 - u0 < 1:
+        return False, f"direct sends {d1 - d0} (want 0), past-the-cap sends {u1 - u0} (want >= 1)"
+    return True, ""
+
+
 def case_tags_out_of_order(comm, rank, n, salt):
     """Three sends with tags 5, 6, 7; receives posted as 7, 5, 6."""
     nxt, prv = (rank + 1) % n, (rank - 1) % n
@@ -1107,10 +1143,80 @@ def case_osc_random_epochs(comm, rank, n, salt, epochs=10, separate=False):
             comm.set_param("osc_win_shadow", 0)
     shadowed = comm.get_param("osc_shadow_windows") - w0  # this rank's window through a public copy
     fails = []
+    diag = os.environ.get("OSC_DIAG") == "1"  # every copy checked at every epoch close
+    diag_end = os.environ.get("OSC_DIAG") == "2"  # the copies checked once, at the end (no extra syncs)
+    mine_ops = []  # (epoch, kind, origin, what, disp, count) aimed at this rank
+    all_ops = []   # (epoch, kind, origin, what, target, disp, count, seed): the whole plan so far
+
+    def raw(addr):
+        out = np.empty(W * 4, np.uint8)
+        _lib.check(_lib.load().ompi_amd_memcpy(out.ctypes.data, addr, W * 4), "memcpy")
+        return out
+
+    def check_copies(e, kind):
+        STREAM.synchronize()
+        torch.cuda.synchronize()
+        priv, pub, snap = win.copies()
+        want = model[rank].view(np.uint8)
+        got = {"priv": raw(priv)}
+        if pub:
+            got["pub"], got["snap"] = raw(pub), raw(snap)
+        notes = []
+        if pub and not np.array_equal(got["pub"], want):
+            bad = np.flatnonzero(got["pub"] != want)
+            notes.append(f"public != model: {bad.size} bytes from {bad[0]}")
+        if pub and not np.array_equal(got["priv"], got["snap"]):
+            bad = np.flatnonzero(got["priv"] != got["snap"])
+            notes.append(f"private != snapshot: {bad.size} bytes from {bad[0]}")
+        if not pub and not np.array_equal(got["priv"], want):
+            bad = np.flatnonzero(got["priv"] != want)
+            notes.append(f"unified window != model: {bad.size} bytes from {bad[0]}")
+        if notes:
+            first = int(bad[0]) // 4
+            near = [op for op in mine_ops if op[4] <= first < op[4] + op[5]]
+            src = got["pub"] if pub else got["priv"]
+            gv = float(src.view(np.float32)[first])
+            mv = float(model[rank][first])
+            # which planned operation (any target) puts gv at this offset?
+            cands = []
+            for (ee, kk, oo, ww, tt, dd, cc, sd) in all_ops:
+                if ww == "put" and dd <= first < dd + cc:
+                    v = np.random.default_rng(sd).integers(-64, 65, cc).astype(np.float32)[first - dd]
+                    if float(v) == gv:
+                        cands.append((ee, kk, oo, tt, dd, cc))
+            notes.append(f"at float {first}: public {gv} model {mv}; puts of that value there: {cands[:6]}")
+            line = (f"DIAG rank {rank} epoch {e} ({kind}, shadowed {shadowed}): " + "; ".join(notes) +
+                    f"; ops on float {first}: {near[-6:]}")
+            print(line, file=sys.stderr, flush=True)
+            fails.append(line)
+            return False
+        return True
     if separate and win.model != osc.WIN_SEPARATE:
         fails.append(f"model {win.model}, want WIN_SEPARATE")
     try:
         comm_barrier()
+        if diag:  # a failed check is recorded; every rank goes on (the epochs are collective)
+            check_copies(-1, "create")
+            # every rank's mapping of every peer's window reaches that peer's
+            # RMA target: each rank stamps its own (public) copy, peers read
+            lib = _lib.load()
+            priv, pub, snap = win.copies()
+            mine = pub or priv
+            stamp = np.full(64, rank + 1, np.uint8)
+            _lib.check(lib.ompi_amd_memcpy(mine, stamp.ctypes.data, 64), "stamp")
+            torch.cuda.synchronize()
+            comm_barrier()
+            for p in range(n):
+                got = np.zeros(64, np.uint8)
+                _lib.check(lib.ompi_amd_memcpy(got.ctypes.data, win.peer_base(p), 64), "read stamp")
+                if not np.all(got == p + 1):
+                    line = f"DIAG rank {rank}: mapping of rank {p}'s window holds stamp {got[:4].tolist()}"
+                    print(line, file=sys.stderr, flush=True)
+                    fails.append(line)
+            comm_barrier()
+            _lib.check(lib.ompi_amd_memcpy(mine, np.zeros(64, np.uint8).ctypes.data, 64), "unstamp")
+            torch.cuda.synchronize()
+            comm_barrier()
         for e in range(epochs):
             kind = ["fence", "lock_all", "pscw", "lock_one"][int(rng.integers(4))]
             excl = int(rng.integers(n))  # lock_one: every origin's target
@@ -1154,6 +1260,9 @@ def case_osc_random_epochs(comm, rank, n, salt, epochs=10, separate=False):
                 win.lock(excl, osc.LOCK_EXCLUSIVE, stream=STREAM)
             for o, what, t, d, cnt, sd in ops:
                 vals = np.random.default_rng(sd).integers(-64, 65, cnt).astype(np.float32)
+                if t == rank and what != "get":
+                    mine_ops.append((e, kind, o, what, d, cnt))
+                all_ops.append((e, kind, o, what, t, d, cnt, sd))
                 if what == "put":
                     model[t][d:d + cnt] = vals
                 elif what == "acc":
@@ -1187,6 +1296,10 @@ def case_osc_random_epochs(comm, rank, n, salt, epochs=10, separate=False):
                 ok, msg = eq(host(buf).view(np.float32), exp, f"{what} (model {win.model})")
                 if not ok:
                     fails.append(msg)
+            if diag:  # every rank's check between two barriers: passive epochs start at once
+                comm_barrier()
+                check_copies(e, kind)
+                comm_barrier()
         win.fence(stream=STREAM, blocking=True)
         comm_barrier()
         win.sync(stream=STREAM)  # MPI_Win_sync: the private copy of a separate-model window
@@ -1195,9 +1308,62 @@ def case_osc_random_epochs(comm, rank, n, salt, epochs=10, separate=False):
                      f"window of rank {rank} (model {win.model}, shadowed here {shadowed})")
         if not ok:
             fails.append(msg)
+        if diag_end and not ok:
+            torch.cuda.synchronize()
+            priv, pub, snap = win.copies()
+            cp = {"priv": raw(priv)}
+            if pub:
+                cp["pub"], cp["snap"] = raw(pub), raw(snap)
+            want = model[rank].view(np.uint8)
+            parts = []
+            for k, v in cp.items():
+                badk = np.flatnonzero(v != want)
+                parts.append(f"{k}: {badk.size} bad" + (f" from {badk[0]}" if badk.size else ""))
+            bad = np.flatnonzero(cp["priv"] != want)
+            fl = sorted(set((bad // 4).tolist()))
+            first = fl[0]
+            runs, st = [], fl[0]
+            for a, b in zip(fl, fl[1:] + [None]):
+                if b != a + 1:
+                    runs.append((st, a))
+                    st = b
+            gotv = cp["priv"].view(np.float32)
+            near = [op for op in mine_ops if any(op[4] <= r0 < op[4] + op[5] or r0 <= op[4] <= r1
+                                                 for r0, r1 in runs[:4])]
+            line = (f"DIAG2 rank {rank}: " + "; ".join(parts) + f"; bad float runs {runs[:6]}; "
+                    f"priv {gotv[first]} model {model[rank][first]}; ops there {near[:8]}")
+            print(line, file=sys.stderr, flush=True)
+            fails.append(line)
     finally:
         win.free()
     return not fails, "; ".join(fails[:3])
+
+
+def case_separate_refused(comm, rank, n):
+    """osc_win_separate 0 (osc/rocm's osc_rocm_separate_model 0): an
+    MPI_Win_create window over memory peers cannot map as it is (a small
+    tensor: not an IPC-safe size) fails on every rank with
+    OMPI_AMD_ERR_UNSUPPORTED instead of running through a public copy; a
+    window over an exportable allocation still works (unified)."""
+    comm.set_param("osc_win_separate", 0)
+    try:
+        small = zeros(4096 + 12)
+        try:
+            w = osc.Window.create(comm, small, small.numel(), disp_unit=1)
+            w.free()
+            return False, "a window needing a public copy was created with the separate model off"
+        except _lib.OmpiAmdError as e:
+            if e.code != _lib.ERR_UNSUPPORTED:
+                return False, f"refusal code {e.code}"
+        w = osc.Window.allocate(comm, 4096, disp_unit=1)
+        try:
+            if w.model != osc.WIN_UNIFIED:
+                return False, f"allocated window model {w.model}"
+        finally:
+            w.free()
+        return True, ""
+    finally:
+        comm.set_param("osc_win_separate", 1)
 
 
 def case_pscw_all_to_one(comm, rank, n, salt, count=100003):
@@ -1406,6 +1572,7 @@ def main():
         ("p2p_ring_64MiB", lambda: case_ring(comm, rank, n, 64 << 20, 4)),
         ("p2p_ring_16MiB_plus_odd", lambda: case_ring(comm, rank, n, (16 << 20) + 13, 5, 16, 16)),
         ("p2p_aged_buffer_staged", lambda: case_aged_buffer_staged(comm, rank, n, 6)),
+        ("p2p_stage_cap_aged", lambda: case_stage_cap_aged(comm, rank, n, 8)),
         ("p2p_tags_out_of_order", lambda: case_tags_out_of_order(comm, rank, n, 6)),
         ("p2p_same_tag_order", lambda: case_same_tag_order(comm, rank, n, 20)),
         ("p2p_ring_wraps_eager_and_staged", lambda: case_ring_wraps(comm, rank, n, 400)),
@@ -1414,6 +1581,12 @@ def main():
         ("p2p_random_channels", lambda: case_random_channels(comm, rank, n, 600 + STRESS_SEED)),
         ("p2p_random_channels_b", lambda: case_random_channels(comm, rank, n, 601 + STRESS_SEED)),
         ("p2p_random_channels_any_source", lambda: case_random_channels(comm, rank, n, 602 + STRESS_SEED, wild=0.3)),
+        # right after the random point-to-point traffic (which ages the
+        # allocator's blocks, so MPI_Win_create windows get public copies):
+        # the plans that lost epoch-0 puts in round 5 (the window's initial
+        # copies completing after peers' first RMA)
+        ("osc_random_epochs_after_p2p_s3000", lambda: case_osc_random_epochs(comm, rank, n, 3700 + STRESS_SEED)),
+        ("osc_random_epochs_after_p2p_s5000", lambda: case_osc_random_epochs(comm, rank, n, 5700 + STRESS_SEED)),
         ("p2p_probe_truncate", lambda: case_probe_truncate(comm, rank, n, 71)),
         ("p2p_self", lambda: case_self(comm, rank, n, 72)),
         ("p2p_recv_timeout_cancel", lambda: case_recv_timeout_cancel(comm, rank, n, 75)),
@@ -1446,6 +1619,7 @@ def main():
         ("osc_accumulate_derived_datatypes", lambda: case_acc_ddt(comm, rank, n, 150)),
         ("osc_put_get_derived_datatypes", lambda: case_put_get_ddt(comm, rank, n, 160)),
         ("osc_separate_model_small_tensor", lambda: case_separate_window(comm, rank, n, 170)),
+        ("osc_separate_model_refused", lambda: case_separate_refused(comm, rank, n)),
         ("osc_separate_model_forced_64MiB",
          lambda: case_separate_window(comm, rank, n, 171, nbytes=(64 << 20) + 12, force=True)),
         ("osc_fetch_and_op_counter", lambda: case_fetch_and_op_counter(comm, rank, n)),
@@ -1457,7 +1631,8 @@ def main():
         ("osc_pscw_ring_test", lambda: case_pscw_ring(comm, rank, n, 95, epochs=2, use_test=True)),
         ("osc_pscw_all_to_one_acc", lambda: case_pscw_all_to_one(comm, rank, n, 96)),
         ("osc_pscw_errors", lambda: case_pscw_errors(comm, rank, n)),
-        ("osc_random_epochs", lambda: case_osc_random_epochs(comm, rank, n, 700 + STRESS_SEED)),
+        ("osc_random_epochs", lambda: case_osc_random_epochs(comm, rank, n, 700 + STRESS_SEED,
+                                                             separate=os.environ.get("OSC_FORCE_SHADOW") == "1")),
         ("osc_random_epochs_b", lambda: case_osc_random_epochs(comm, rank, n, 701 + STRESS_SEED, epochs=16)),
         ("osc_random_epochs_separate", lambda: case_osc_random_epochs(comm, rank, n, 702 + STRESS_SEED,
                                                                       separate=True)),
@@ -1466,6 +1641,10 @@ def main():
         ("osc_shared_window_noncontig", lambda: case_shared_window(comm, rank, n, 99, noncontig=True)),
     ]
     only = os.environ.get("P2P_OSC_ONLY")
+    pick = os.environ.get("P2P_OSC_CASES")  # exact names, comma-separated, run in list order
+    if pick:
+        byname = dict(cases)
+        cases = [(nm, byname[nm]) for nm in pick.split(",")]
     all_ok = True
     for name, fn in cases:
         if only and only not in name:

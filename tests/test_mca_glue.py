@@ -49,12 +49,13 @@ def coll_harness(tmp_path_factory):
     return out
 
 
-def _run_coll_harness(exe, n, gpu, timeout):
+def _run_coll_harness(exe, n, gpu, timeout, extra_env=None):
     import secrets
     name = secrets.token_hex(3)
     # the HSA IPC mode is inherited (the library's load-time default when
     # unset), as an mpirun job gets it: INTEGRATION.md §6
-    env = {**os.environ, "HARNESS_GPU": "1" if gpu else "0", "OMPI_AMD_COLL_TIMEOUT_MS": "20000"}
+    env = {**os.environ, "HARNESS_GPU": "1" if gpu else "0", "OMPI_AMD_COLL_TIMEOUT_MS": "20000",
+           **(extra_env or {})}
     procs = [subprocess.Popen([exe, name, str(r), str(n)], stdout=subprocess.PIPE,
                               stderr=subprocess.PIPE, text=True, env=env) for r in range(n)]
     outs, deadline = [], time.time() + timeout
@@ -98,6 +99,41 @@ def test_coll_component_device_path(coll_harness, n):
     oracle bit for bit; host / mixed / user-op calls go to the saved
     functions on every rank; release destroys the device communicator."""
     _assert_all(_run_coll_harness(coll_harness, n, True, 150), "ok gpu")
+
+
+_T = "OMPI_MCA_coll_tuned_"
+TUNED_SETTINGS = {
+    # every forced order the device path runs: binary reduce, nonoverlapping
+    # allreduce and reduce_scatter through it, basic_linear rsb through it
+    "binary_reduce": {_T + "use_dynamic_rules": "1", _T + "reduce_algorithm": "4",
+                      _T + "allreduce_algorithm": "2", _T + "reduce_scatter_algorithm": "1"},
+    "binomial_raben_halving": {_T + "use_dynamic_rules": "1", _T + "reduce_algorithm": "5",
+                               _T + "allreduce_algorithm": "6", _T + "reduce_scatter_algorithm": "2",
+                               _T + "reduce_scatter_block_algorithm": "1"},
+    # in-order binary reduce and recursive-halving rsb are not run on the
+    # device: reduce, rsb and the nonoverlapping allreduce go to coll/tuned
+    "declined_orders": {_T + "use_dynamic_rules": "1", _T + "reduce_algorithm": "6",
+                        _T + "allreduce_algorithm": "2", _T + "reduce_scatter_algorithm": "3",
+                        _T + "reduce_scatter_block_algorithm": "3"},
+    # a rules file: every blocking reduction goes to coll/tuned
+    "rules_file": {_T + "use_dynamic_rules": "1", _T + "dynamic_rules_filename": "/tmp/rules.conf",
+                   _T + "allreduce_algorithm": "3"},
+    # forcing without dynamic rules is ignored by tuned, and so here
+    "not_dynamic": {_T + "use_dynamic_rules": "0", _T + "reduce_algorithm": "6",
+                    _T + "reduce_scatter_block_algorithm": "3"},
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("setting", sorted(TUNED_SETTINGS))
+def test_coll_component_tuned_forcing(coll_harness, n, setting):
+    """coll/tuned's forcing variables, read through the MCA variable system
+    (VERDICT r5 item 3): blocking allreduce / reduce / reduce_scatter_block /
+    reduce_scatter either fold on the device in the order coll/tuned would
+    run (oracle, fp SUM, bit-exact) or go to the saved function."""
+    env = {**TUNED_SETTINGS[setting], "HARNESS_TUNED": "1"}
+    _assert_all(_run_coll_harness(coll_harness, n, True, 150, env), "ok gpu tuned")
 
 
 # ---- pml/rocm (ompi_amd/mca/pml/rocm) through tests/mca_harness/pml_harness.c ----

@@ -327,3 +327,56 @@ def test_forced_nonoverlapping_is_tuned_reduce_then_bcast(orc, n, inplace):
     red, _ = orc.reduce([x.copy() for x in xs], count, SUM, F32, 0, inplace)
     for r in range(n):
         assert np.array_equal(res[r].view(np.uint32), red.view(np.uint32))
+
+
+def test_library_forced_reduce_orders(orc):
+    """coll_tuned_reduce_algorithm forced (dynamic rules on): the library's
+    order for 1 / 3 / 4 / 5 is the one the oracle runs for that algorithm
+    whatever the fixed decision would say; 2 / 6 / 7 are refused (coll/rocm
+    then leaves the reduction to coll/tuned)."""
+    from ompi_amd import _lib, coll
+    names = {1: "chain", 3: "chain", 4: "binary", 5: "binomial"}
+    for n in (2, 3, 4, 8, 9):
+        for msg in (4, 511, 4096, 1 << 20):
+            count = max(1, msg // 4)
+            for forced, name in names.items():
+                for root in (0, n - 1):
+                    got, first = coll.reduce_order(n, count * 4, count, root, forced=forced)
+                    assert got == name, (n, msg, forced)
+                    assert first == (0 if forced == 1 else root)
+            for forced in (2, 6, 7):
+                with pytest.raises(_lib.OmpiAmdError) as e:
+                    coll.reduce_order(n, count * 4, count, 0, forced=forced)
+                assert e.value.code == _lib.ERR_UNSUPPORTED
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+def test_oracle_forced_rsb_and_rs_nonoverlapping(orc, n):
+    """rsb basic_linear and reduce_scatter non-overlapping call coll/tuned's
+    reduce to rank 0 (coll_base_reduce_scatter_block.c:95-97,
+    coll_base_reduce_scatter.c:42-92), so a forced reduce algorithm changes
+    their fp order: the oracle's forms equal its reduce with that algorithm,
+    cut into the blocks."""
+    rcount = 300
+    xs = _inputs(n, n * rcount, 77 + n, False)
+    for alg in (0, 1, 3, 4, 5):
+        full, _ = orc.reduce(xs, n * rcount, SUM, F32, 0, False, algorithm=alg)
+        rb = orc.reduce_scatter_block([x.copy() for x in xs], rcount, SUM, F32, red_alg=alg)
+        for r in range(n):
+            assert _bits_equal(rb[r].view(np.float32), full[r * rcount:(r + 1) * rcount]), (alg, r)
+        rcounts = [rcount + (r % 3) - 1 for r in range(n)]
+        tot = sum(rcounts)
+        ys = [x[:tot].copy() for x in xs]
+        for inplace in (False, True):
+            full2, _ = orc.reduce(ys, tot, SUM, F32, 0, inplace, algorithm=alg)
+            got, ran = orc.reduce_scatter(ys, rcounts, SUM, F32, algorithm=orc.RS_NONOVERLAPPING,
+                                          red_alg=alg, inplace=inplace)
+            assert ran == orc.RS_NONOVERLAPPING
+            off = 0
+            for r in range(n):
+                assert _bits_equal(got[r], full2[off:off + rcounts[r]]), (alg, inplace, r)
+                off += rcounts[r]
+    # the forced orders really differ from the fixed one on these inputs
+    a = orc.reduce_scatter_block([x.copy() for x in xs], rcount, SUM, F32, red_alg=1)
+    b = orc.reduce_scatter_block([x.copy() for x in xs], rcount, SUM, F32, red_alg=5)
+    assert n == 2 or any(not _bits_equal(a[r].view(np.float32), b[r].view(np.float32)) for r in range(n))
