@@ -663,6 +663,8 @@ int main(int argc, char **argv)
         return 0;
     }
 
+    if (getenv("HARNESS_OWN_STREAM"))  /* the component parameter, as the MCA system would set it */
+        mca_coll_rocm_component.own_stream = atoi(getenv("HARNESS_OWN_STREAM"));
     CHECK(m->coll_module_enable(m, &comm) == OMPI_SUCCESS, "enable");
     CHECK(tm->super.obj_reference_count == 1 + 24 + 24, "enable retains the saved modules (%d)",
           tm->super.obj_reference_count);
