@@ -61,6 +61,19 @@ int ompi_amd_win_create(ompi_amd_comm_t *comm, void *base, size_t bytes, int dis
 /* MPI_Win_allocate: the window's memory is allocated here (zeroed). */
 int ompi_amd_win_allocate(ompi_amd_comm_t *comm, size_t bytes, int disp_unit, void **base,
                           ompi_amd_win_t **win);
+/* MPI_Win_create_dynamic (collective; osc/rdma's flavor, osc_rdma_dynamic.c):
+ * a window with no memory; displacements are the target's absolute
+ * addresses (disp_unit 1) inside regions the target attached.
+ * MPI_Win_attach (local): device memory peers can map as it is (an
+ * IPC-safe allocation no IPC close of this process predates) — host memory
+ * returns OMPI_AMD_ERR_NOT_DEVICE, other device memory
+ * OMPI_AMD_ERR_UNSUPPORTED (MPI_ERR_RMA_ATTACH), at most 64 regions per
+ * rank, none overlapping.  MPI_Win_detach (local): base as attached.  An
+ * origin finds the target's region at each access; accessing memory the
+ * target has not attached is OMPI_AMD_ERR_BAD_PARAM (MPI_ERR_RMA_RANGE). */
+int ompi_amd_win_create_dynamic(ompi_amd_comm_t *comm, ompi_amd_win_t **win);
+int ompi_amd_win_attach(ompi_amd_win_t *win, void *base, size_t size);
+int ompi_amd_win_detach(ompi_amd_win_t *win, const void *base);
 /* MPI_Win_free (collective; waits for every rank's outstanding work). */
 int ompi_amd_win_free(ompi_amd_win_t *win);
 /* MPI_Win_fence: a device barrier on `stream` over the window's ranks.

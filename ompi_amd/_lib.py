@@ -264,6 +264,9 @@ PROTOTYPES = [
     ("ompi_amd_win_sync", _C.c_int, [_C.c_void_p, _C.c_void_p]),
     ("ompi_amd_win_model", _C.c_int, [_C.c_void_p]),
     ("ompi_amd_win_peer_base", _C.c_int, [_C.c_void_p, _C.c_int, _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_win_create_dynamic", _C.c_int, [_C.c_void_p, _C.POINTER(_C.c_void_p)]),
+    ("ompi_amd_win_attach", _C.c_int, [_C.c_void_p, _C.c_void_p, _C.c_size_t]),
+    ("ompi_amd_win_detach", _C.c_int, [_C.c_void_p, _C.c_void_p]),
     ("ompi_amd_win_copies", _C.c_int, [_C.c_void_p, _C.POINTER(_C.c_void_p), _C.POINTER(_C.c_void_p),
                                        _C.POINTER(_C.c_void_p)]),
     ("ompi_amd_put_ddt", _C.c_int, [_C.c_void_p, _C.c_void_p, _C.c_size_t, _C.c_void_p, _C.c_int,

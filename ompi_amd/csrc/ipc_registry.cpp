@@ -47,34 +47,17 @@ struct user {
 std::vector<user> g_users;
 ipc_stats g_st{};
 std::atomic<uint64_t> g_close_mark{0};  // ipc_close_watermark()
-std::atomic<bool> g_close_pending{false};
 std::mutex g_probe_mu;
-std::vector<void *> g_probes;  // watermark probes, freed in batches
+std::vector<void *> g_probes;  // watermark probes, freed in batches (not here)
 
-// A close happened: the watermark moves at the next ipc_close_watermark().
-// Nothing here touches the device — closes run inside point-to-point
-// progress and LRU evictions, where a device-wide synchronisation (hipFree)
-// could wait on this process's kernels that wait on peers.
-void resolve_close_mark();
+// After a close: the buffer id of a fresh allocation — every allocation
+// with a lower id existed at the close (ipc_registry.h).  The probe is
+// allocated now (an allocation made later must not count as older) but not
+// freed here: closes run inside point-to-point progress and LRU evictions,
+// and hipFree synchronises the whole device, which could wait on this
+// process's kernels that wait on peers.  ipc_close_watermark(),
+// called on host paths before an export, frees the probes 256 at a time.
 void note_close() {
-    g_close_pending.store(true, std::memory_order_release);
-    // OMPI_AMD_EAGER_CLOSE_MARK=1 (diagnostics): the round-5
-    // behaviour — the probe allocation made and freed at the close itself
-    static const bool eager = [] {
-        const char *e = getenv("OMPI_AMD_EAGER_CLOSE_MARK");
-        return e && atoi(e) != 0;
-    }();
-    if (eager) resolve_close_mark();
-}
-
-// The buffer id of a fresh allocation, taken after the closes noted so far:
-// every allocation with a lower id existed at those closes (ipc_registry.h).
-// Taking it later than the close only counts more allocations as older —
-// more conservative, never less.  Runs on the host paths that ask before an
-// export (comm_ipc_safe and the exporters), not inside progress; the probes
-// are freed 256 at a time.
-void resolve_close_mark() {
-    if (!g_close_pending.exchange(false, std::memory_order_acq_rel)) return;
     std::lock_guard<std::mutex> g(g_probe_mu);
     void *p = nullptr;
     if (hipMalloc(&p, 4096) != hipSuccess) {
@@ -88,17 +71,16 @@ void resolve_close_mark() {
         id = UINT64_MAX;
     }
     g_probes.push_back(p);
-    static const bool eager = [] {
-        const char *e = getenv("OMPI_AMD_EAGER_CLOSE_MARK");
-        return e && atoi(e) != 0;
-    }();
-    if (eager || g_probes.size() >= 256) {
-        for (void *q : g_probes) hip_ignore(hipFree(q));
-        g_probes.clear();
-    }
     uint64_t cur = g_close_mark.load();
     while (cur < id && !g_close_mark.compare_exchange_weak(cur, id)) {
     }
+}
+
+void free_probes() {
+    std::lock_guard<std::mutex> g(g_probe_mu);
+    if (g_probes.size() < 256) return;
+    for (void *q : g_probes) hip_ignore(hipFree(q));
+    g_probes.clear();
 }
 
 bool same_handle(const hipIpcMemHandle_t &x, const hipIpcMemHandle_t &y) {
@@ -378,7 +360,7 @@ void ipc_remove_user(void *owner) {
 }
 
 uint64_t ipc_close_watermark() {
-    resolve_close_mark();
+    free_probes();
     return g_close_mark.load();
 }
 

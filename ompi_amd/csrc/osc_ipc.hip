@@ -29,8 +29,14 @@
 // stores before the next holder's loads.
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <array>
+#include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -620,6 +626,108 @@ __global__ __launch_bounds__(kOscThreads) void ddt_acc_kernel(ddt_desc d, char *
 using ddt_acc_fn = hipError_t (*)(dim3, const ddt_desc &, char *, const void *, void *, int64_t,
                                   const uint32_t *, bool, hipStream_t);
 
+// ---- derived datatypes of pair type (MAXLOC / MINLOC operands) ----
+// ompi_osc_base_sndrcv_op (osc_base_obj_convert.c:73-245) converts the
+// origin into the target's primitive slots element by element; a pair's
+// packed element is its members back to back (DOUBLE_INT: 8 + 4 = 12 bytes)
+// while its memory element carries the struct's padding (16 bytes, the
+// int at offset 8; SHORT_INT: the int at offset 4 after 2 bytes of gap).
+// One lane per pair: each member is located on its own — through the
+// target program (the member's packed position -> typed offset, so a
+// program whose runs split a pair still maps each member), or at
+// k * extent + its struct offset for a contiguous side — loaded bytewise
+// (a packed double need not be 8-byte aligned), combined with op/base's
+// LOC rule (f(target, origin), the 2-buffer form), and only the members'
+// bytes are stored: a pair's gap bytes in the window stay as they were.
+// OP 0 replace, -1 fetch only.
+struct pair_side {
+    char *p;        // the stream or buffer
+    int64_t stride; // bytes per pair: the packed size, or the extent
+    int32_t koff;   // byte offset of the index member within one pair
+};
+
+template <typename S>
+__device__ __forceinline__ void pair_ld(const char *a, const char *b, S *x) {
+    __builtin_memcpy(&x->v, a, sizeof(x->v));
+    __builtin_memcpy(&x->k, b, sizeof(x->k));
+}
+
+template <typename S, int OP>
+__global__ __launch_bounds__(kOscThreads) void ddt_pair_kernel(ddt_desc d, char *typed, pair_side in,
+                                                               pair_side old, int64_t n,
+                                                               const uint32_t *gate) {
+    if (!gate_open(gate)) return;
+    if (threadIdx.x == 0) osc_acquire();
+    __syncthreads();
+    constexpr int64_t P = (int64_t)(sizeof(S::v) + sizeof(S::k));  // packed pair
+    const int64_t gs = (int64_t)gridDim.x * kOscThreads;
+    for (int64_t k = (int64_t)blockIdx.x * kOscThreads + threadIdx.x; k < n; k += gs) {
+        char *tv, *tk;
+        if (d.nelem > 0) {
+            tv = typed + typed_offset<uint64_t>(d.elems, d.nelem, (uint64_t)d.size, d.extent, (uint64_t)(k * P));
+            tk = typed + typed_offset<uint64_t>(d.elems, d.nelem, (uint64_t)d.size, d.extent,
+                                                (uint64_t)(k * P + (int64_t)sizeof(S::v)));
+        } else {  // contiguous target: memory pairs
+            tv = typed + k * (int64_t)sizeof(S);
+            tk = tv + offsetof(S, k);
+        }
+        S x;
+        pair_ld(tv, tk, &x);
+        if (old.p) {
+            char *o = old.p + k * old.stride;
+            __builtin_memcpy(o, &x.v, sizeof(x.v));
+            __builtin_memcpy(o + old.koff, &x.k, sizeof(x.k));
+        }
+        if constexpr (OP >= 0) {
+            const char *ip = in.p + k * in.stride;
+            S y;
+            pair_ld(ip, ip + in.koff, &y);
+            S r = y;
+            if constexpr (OP > 0) r = opfn<OP, false>::f(x, y);
+            __builtin_memcpy(tv, &r.v, sizeof(r.v));
+            __builtin_memcpy(tk, &r.k, sizeof(r.k));
+        }
+    }
+    osc_epilogue();
+}
+
+using pair_fn = void (*)(dim3, const ddt_desc &, char *, pair_side, pair_side, int64_t, const uint32_t *,
+                         hipStream_t);
+template <typename S, int OP>
+static void pair_launch(dim3 grid, const ddt_desc &d, char *typed, pair_side in, pair_side old, int64_t n,
+                        const uint32_t *gate, hipStream_t s) {
+    hipLaunchKernelGGL((ddt_pair_kernel<S, OP>), grid, dim3(kOscThreads), 0, s, d, typed, in, old, n, gate);
+}
+template <typename S>
+static pair_fn pair_fn_of(int op) {
+    switch (op) {
+    case OMPI_AMD_OP_MAXLOC: return &pair_launch<S, OMPI_AMD_OP_MAXLOC>;
+    case OMPI_AMD_OP_MINLOC: return &pair_launch<S, OMPI_AMD_OP_MINLOC>;
+    case OMPI_AMD_OP_REPLACE: return &pair_launch<S, 0>;
+    case OMPI_AMD_OP_NO_OP: return &pair_launch<S, -1>;
+    default: return nullptr;
+    }
+}
+// (fn, packed pair size, struct size, index member offset) of a pair type
+static bool pair_info(int type, int op, pair_fn *f, int64_t *packed, int64_t *ext, int32_t *koff) {
+    switch (type) {
+#define PAIR(T, S)                                                     \
+    case T:                                                            \
+        *f = pair_fn_of<S>(op);                                        \
+        *packed = (int64_t)(sizeof(S::v) + sizeof(S::k));              \
+        *ext = (int64_t)sizeof(S);                                     \
+        *koff = (int32_t)offsetof(S, k);                               \
+        return *f != nullptr;
+        PAIR(OMPI_AMD_TYPE_FLOAT_INT, float_int_t)
+        PAIR(OMPI_AMD_TYPE_DOUBLE_INT, double_int_t)
+        PAIR(OMPI_AMD_TYPE_LONG_INT, long_int_t)
+        PAIR(OMPI_AMD_TYPE_2INT, two_int_t)
+        PAIR(OMPI_AMD_TYPE_SHORT_INT, short_int_t)
+#undef PAIR
+    default: return false;
+    }
+}
+
 template <typename T, int OP>
 static hipError_t ddt_acc_launch(dim3 grid, const ddt_desc &d, char *typed, const void *in,
                                  void *old, int64_t n, const uint32_t *gate, bool fast, hipStream_t s) {
@@ -726,11 +834,87 @@ struct ompi_amd_win {
     char *snap = nullptr;
     bool owns_shadow = false;  // past the arena's limit: hipFree'd, not returned to the arena
     bool separate = false;
+    // MPI_Win_create_dynamic: every rank's attached regions in a host
+    // shared-memory table (one slot per rank, a sequence lock each), and
+    // this process's mappings of peers' regions (pinned until win_free)
+    bool dynamic = false;
+    struct dyn_table *dyn = nullptr;
+    size_t dyn_bytes = 0;
+    struct dyn_map {
+        int target;
+        uint64_t base, size, id, abase;
+        const char *p;
+        void *pin;
+    };
+    std::vector<dyn_map> dyn_maps;
+};
+
+#define OSC_TRY(x)                               \
+    do {                                         \
+        int rc_ = (x);                           \
+        if (rc_ != OMPI_AMD_SUCCESS) return rc_; \
+    } while (0)
+
+// ---- dynamic windows (MPI_Win_create_dynamic / _attach / _detach;
+// osc/rdma's region table, osc_rdma_dynamic.c:162-300, in host shared
+// memory here: every attach is local, and an origin finds the target's
+// region — its absolute address is the displacement — when it accesses it)
+constexpr int kDynRegions = 64;
+struct dyn_region {
+    uint64_t base, size;
+    ompi_amd::ipc_desc d;  // the attached device memory, exported at attach
+};
+struct dyn_table {
+    std::atomic<uint64_t> version;  // odd while the owner edits its regions
+    uint32_t n, pad;
+    dyn_region r[kDynRegions];
 };
 
 namespace ompi_amd {
 
 enum { HELD_NONE = 0, HELD_EXCLUSIVE = 1, HELD_SHARED = 2, HELD_NOCHECK = 3 };
+
+// A consistent copy of rank t's region table (the owner's sequence lock).
+static int dyn_read(ompi_amd_win_t *w, int t, dyn_table *out) {
+    const dyn_table &src = w->dyn[t];
+    for (int spin = 0; spin < (1 << 20); ++spin) {
+        const uint64_t v1 = src.version.load(std::memory_order_acquire);
+        if (v1 & 1) continue;
+        out->n = std::min<uint32_t>(src.n, kDynRegions);
+        memcpy(out->r, src.r, sizeof(dyn_region) * out->n);
+        std::atomic_thread_fence(std::memory_order_acquire);
+        if (src.version.load(std::memory_order_relaxed) == v1) return OMPI_AMD_SUCCESS;
+    }
+    record_msg("osc: rank %d's dynamic region table stayed busy", t);
+    return OMPI_AMD_ERR_TIMEOUT;
+}
+
+static int dyn_resolve(ompi_amd_win_t *w, int target, int64_t lo, int64_t hi, char **out) {
+    static thread_local dyn_table tab;
+    OSC_TRY(dyn_read(w, target, &tab));
+    for (uint32_t i = 0; i < tab.n; ++i) {
+        const dyn_region &r = tab.r[i];
+        if ((uint64_t)lo < r.base || (uint64_t)hi > r.base + r.size) continue;
+        if (target == w->rank) {  // own memory: the address itself
+            *out = reinterpret_cast<char *>((uintptr_t)lo);
+            return OMPI_AMD_SUCCESS;
+        }
+        for (const auto &m : w->dyn_maps)
+            if (m.target == target && m.base == r.base && m.size == r.size && m.id == r.d.id &&
+                m.abase == r.d.base) {
+                *out = const_cast<char *>(m.p) + (lo - (int64_t)r.base);
+                return OMPI_AMD_SUCCESS;
+            }
+        ompi_amd_win::dyn_map m{target, r.base, r.size, r.d.id, r.d.base, nullptr, nullptr};
+        OSC_TRY(comm_import(w->c, target, r.d, &m.p, true, &m.pin));
+        w->dyn_maps.push_back(m);
+        *out = const_cast<char *>(m.p) + (lo - (int64_t)r.base);
+        return OMPI_AMD_SUCCESS;
+    }
+    record_msg("osc: [0x%llx, 0x%llx) is not inside a region rank %d attached to the dynamic window",
+               (unsigned long long)lo, (unsigned long long)hi, target);
+    return OMPI_AMD_ERR_BAD_PARAM;
+}
 
 static uint64_t ticks_of(ompi_amd_win_t *w) {
     return (uint64_t)comm_timeout_ms(w->c) * 100000ull;  // s_memrealtime: 100 MHz
@@ -756,17 +940,44 @@ static const uint32_t *epoch_gate(ompi_amd_win_t *w, int target) {
     return (h == HELD_EXCLUSIVE || h == HELD_SHARED) ? taken_word(w, target, false) : nullptr;
 }
 
+static int dyn_resolve(ompi_amd_win_t *w, int target, int64_t lo, int64_t hi, char **out);
+
+// The address, in this process, of byte `base` of target's window, after
+// checking that [base + lo, base + hi) lies inside it: inside the window's
+// bytes, or — a dynamic window (MPI_Win_create_dynamic), whose
+// displacements are the target's absolute addresses — inside one region the
+// target attached.
+static int target_span(ompi_amd_win_t *w, int target, int64_t base, int64_t lo, int64_t hi, char **out) {
+    if (target < 0 || target >= w->size) return OMPI_AMD_ERR_BAD_PARAM;
+    if (w->dynamic) {
+        char *p = nullptr;
+        OSC_TRY(dyn_resolve(w, target, base + lo, base + hi, &p));
+        *out = p - lo;
+        return OMPI_AMD_SUCCESS;
+    }
+    if (base + lo < 0 || base + hi > (int64_t)w->peer_bytes[target] || !w->peer_base[target]) {
+        record_msg("osc: target %d range [%lld, %lld) outside its %llu-byte window", target,
+                   (long long)(base + lo), (long long)(base + hi), (unsigned long long)w->peer_bytes[target]);
+        return OMPI_AMD_ERR_BAD_PARAM;
+    }
+    *out = w->peer_base[target] + base;
+    return OMPI_AMD_SUCCESS;
+}
+
 // Target address of (target, disp) with room for `bytes`.
 static int target_ptr(ompi_amd_win_t *w, int target, size_t disp, size_t bytes, char **out) {
     if (target < 0 || target >= w->size) return OMPI_AMD_ERR_BAD_PARAM;
-    const uint64_t off = (uint64_t)disp * (uint64_t)w->peer_disp[target];
-    if (off > w->peer_bytes[target] || bytes > w->peer_bytes[target] - off) {
-        record_msg("osc: target %d range [%llu, +%zu) outside its %llu-byte window", target,
-                   (unsigned long long)off, bytes, (unsigned long long)w->peer_bytes[target]);
-        return OMPI_AMD_ERR_BAD_PARAM;
+    const int64_t off = (int64_t)((uint64_t)disp * (uint64_t)w->peer_disp[target]);
+    if (bytes == 0) {  // an empty access (at the window's end, or anywhere in a dynamic window)
+        if (w->dynamic) {
+            *out = nullptr;
+            return OMPI_AMD_SUCCESS;
+        }
+        if (off < 0 || (uint64_t)off > w->peer_bytes[target]) return OMPI_AMD_ERR_BAD_PARAM;
+        *out = w->peer_base[target] ? w->peer_base[target] + off : nullptr;
+        return OMPI_AMD_SUCCESS;
     }
-    *out = w->peer_base[target] ? w->peer_base[target] + off : nullptr;
-    return OMPI_AMD_SUCCESS;
+    return target_span(w, target, off, 0, (int64_t)bytes, out);
 }
 
 
@@ -905,11 +1116,6 @@ static int launch_acc(ompi_amd_win_t *w, int op, int type, const void *origin, v
                       "osc accumulate launch");
 }
 
-#define OSC_TRY(x)                               \
-    do {                                         \
-        int rc_ = (x);                           \
-        if (rc_ != OMPI_AMD_SUCCESS) return rc_; \
-    } while (0)
 
 // The stream of a window call, remembered so that win_free waits for this
 // window's work only (not for every stream of the device).
@@ -1165,7 +1371,8 @@ static int win_merge(ompi_amd_win_t *w, hipStream_t s) {
 // user: the caller's memory (MPI_Win_create), shadowed when peers cannot
 // map it reliably.
 static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit, bool owns,
-                     ompi_amd_win_t **out, char *const *shared = nullptr, bool user = false) {
+                     ompi_amd_win_t **out, char *const *shared = nullptr, bool user = false,
+                     bool failed_here = false) {
     auto *w = new (std::nothrow) ompi_amd_win;
     if (!w) return OMPI_AMD_ERR_BAD_PARAM;
     w->c = c;
@@ -1175,6 +1382,7 @@ static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit
     w->bytes = bytes;
     w->owns_base = owns;
     int rc = comm_drain(c);  // collective order: deferred nonblocking calls first
+    if (failed_here && rc == OMPI_AMD_SUCCESS) rc = OMPI_AMD_ERR_BOOTSTRAP;  // still joins the rendezvous
     rc = ctl_take(c, rc, &w->ctl_slot);
     if (rc == OMPI_AMD_SUCCESS) w->ctl = ctl_page(c, w->ctl_slot, w->rank);
     win_blob mine{}, all[kOscMaxRanks];
@@ -1332,6 +1540,121 @@ int ompi_amd_win_allocate(ompi_amd_comm_t *c, size_t bytes, int disp_unit, void 
     return OMPI_AMD_SUCCESS;
 }
 
+int ompi_amd_win_create_dynamic(ompi_amd_comm_t *c, ompi_amd_win_t **out) {
+    if (!c || !out) return OMPI_AMD_ERR_BAD_PARAM;
+    int rc = record_hip(hipSetDevice(comm_device(c)), "hipSetDevice");
+    // the region tables: one POSIX shared-memory segment, rank 0 creates it
+    // and names it in a rendezvous, the others map it, rank 0 unlinks it
+    const int me = comm_rank(c), n = comm_size(c);
+    const size_t bytes = sizeof(dyn_table) * (size_t)n;
+    struct name_blob {
+        char name[64];
+        int64_t failed;
+    } mine{}, all[kOscMaxRanks];
+    static std::atomic<unsigned> serial{0};
+    dyn_table *map = nullptr;
+    if (me == 0 && rc == OMPI_AMD_SUCCESS) {
+        snprintf(mine.name, sizeof(mine.name), "/ompi_amd_dyn_%d_%u", (int)getpid(), serial++);
+        const int fd = shm_open(mine.name, O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd < 0 || ftruncate(fd, (off_t)bytes) != 0) rc = OMPI_AMD_ERR_BOOTSTRAP;
+        if (rc == OMPI_AMD_SUCCESS) {
+            void *m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            map = m == MAP_FAILED ? nullptr : static_cast<dyn_table *>(m);
+            if (!map) rc = OMPI_AMD_ERR_BOOTSTRAP;
+        }
+        if (fd >= 0) close(fd);
+        if (rc != OMPI_AMD_SUCCESS) record_msg("osc dynamic window: cannot create %s", mine.name);
+    }
+    mine.failed = rc == OMPI_AMD_SUCCESS ? 0 : 1;
+    const int arc = comm_allgather(c, &mine, all, sizeof(name_blob));
+    if (rc == OMPI_AMD_SUCCESS) rc = arc;
+    if (rc == OMPI_AMD_SUCCESS && all[0].failed) rc = OMPI_AMD_ERR_BOOTSTRAP;
+    if (rc == OMPI_AMD_SUCCESS && me != 0) {
+        const int fd = shm_open(all[0].name, O_RDWR, 0600);
+        if (fd >= 0) {
+            void *m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            map = m == MAP_FAILED ? nullptr : static_cast<dyn_table *>(m);
+            close(fd);
+        }
+        if (!map) {
+            record_msg("osc dynamic window: cannot map %s", all[0].name);
+            rc = OMPI_AMD_ERR_BOOTSTRAP;
+        }
+    }
+    ompi_amd_win_t *w = nullptr;
+    // the window proper (control pages, no memory); its rendezvous also
+    // tells rank 0 that every rank has mapped the tables
+    const int src = win_setup(c, nullptr, 0, 1, false, &w, nullptr, false, rc != OMPI_AMD_SUCCESS);
+    if (me == 0 && mine.name[0]) shm_unlink(mine.name);
+    if (rc == OMPI_AMD_SUCCESS) rc = src;
+    if (rc != OMPI_AMD_SUCCESS) {
+        if (map) munmap(map, bytes);
+        if (w) (void)ompi_amd_win_free(w);
+        return rc;
+    }
+    w->dynamic = true;
+    w->dyn = map;
+    w->dyn_bytes = bytes;
+    for (int p = 0; p < n; ++p) w->peer_disp[p] = 1;  // displacements are addresses
+    *out = w;
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_win_attach(ompi_amd_win_t *w, void *base, size_t size) {
+    if (!w || (size && !base)) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!w->dynamic) return OMPI_AMD_ERR_UNSUPPORTED;  // another flavor (MPI_ERR_RMA_ATTACH)
+    if (size == 0) return OMPI_AMD_SUCCESS;
+    if (!ompi_amd_is_device_pointer(base)) {  // osc/rdma's host path cannot reach device peers
+        record_msg("osc dynamic window: attached memory is not device memory");
+        return OMPI_AMD_ERR_NOT_DEVICE;
+    }
+    // peers map it as it is: it must be exportable (an IPC-safe allocation
+    // that predates no IPC close of this process); a dynamic
+    // window has no public copy to fall back on
+    if (!comm_ipc_safe(base)) {
+        record_msg("osc dynamic window: memory at %p cannot be exported reliably (not an IPC-safe size, "
+                   "or older than an IPC close of this process)", base);
+        return OMPI_AMD_ERR_UNSUPPORTED;
+    }
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    dyn_region r{};
+    r.base = (uint64_t)(uintptr_t)base;
+    r.size = size;
+    OSC_TRY(comm_export(w->c, base, &r.d));
+    dyn_table &t = w->dyn[w->rank];
+    if (t.n >= (uint32_t)kDynRegions) {
+        record_msg("osc dynamic window: more than %d attached regions", kDynRegions);
+        return OMPI_AMD_ERR_UNSUPPORTED;  // osc/rdma's limit is a parameter too
+    }
+    for (uint32_t i = 0; i < t.n; ++i)
+        if (r.base < t.r[i].base + t.r[i].size && t.r[i].base < r.base + r.size) {
+            record_msg("osc dynamic window: region overlaps an attached one");
+            return OMPI_AMD_ERR_BAD_PARAM;
+        }
+    t.version.fetch_add(1, std::memory_order_acq_rel);
+    t.r[t.n] = r;
+    std::atomic_thread_fence(std::memory_order_release);
+    t.n = t.n + 1;
+    t.version.fetch_add(1, std::memory_order_release);
+    return OMPI_AMD_SUCCESS;
+}
+
+int ompi_amd_win_detach(ompi_amd_win_t *w, const void *base) {
+    if (!w) return OMPI_AMD_ERR_BAD_PARAM;
+    if (!w->dynamic) return OMPI_AMD_ERR_UNSUPPORTED;  // another flavor (MPI_ERR_RMA_ATTACH)
+    dyn_table &t = w->dyn[w->rank];
+    for (uint32_t i = 0; i < t.n; ++i)
+        if (t.r[i].base == (uint64_t)(uintptr_t)base) {
+            t.version.fetch_add(1, std::memory_order_acq_rel);
+            for (uint32_t j = i + 1; j < t.n; ++j) t.r[j - 1] = t.r[j];
+            t.n = t.n - 1;
+            t.version.fetch_add(1, std::memory_order_release);
+            return OMPI_AMD_SUCCESS;
+        }
+    record_msg("osc dynamic window: no region attached at %p", base);
+    return OMPI_AMD_ERR_BAD_PARAM;  // MPI_ERR_RMA_RANGE at the MPI level
+}
+
 int ompi_amd_win_free(ompi_amd_win_t *w) {
     if (!w) return OMPI_AMD_SUCCESS;
     ompi_amd_comm_t *c = w->c;
@@ -1345,6 +1668,11 @@ int ompi_amd_win_free(ompi_amd_win_t *w) {
     if (rc == OMPI_AMD_SUCCESS) rc = brc;
     for (int p = 0; p < w->size; ++p)
         if (w->pinned[p]) comm_unpin(c, w->pinned[p]);
+    for (auto &m : w->dyn_maps)
+        if (m.pin) comm_unpin(c, m.pin);
+    w->dyn_maps.clear();
+    if (w->dyn) munmap(w->dyn, w->dyn_bytes);
+    w->dyn = nullptr;
     const int crc = ctl_give(c, w->ctl_slot);  // the peers' last kernels on it are done
     if (rc == OMPI_AMD_SUCCESS) rc = crc;
     if (w->shared_pin) comm_unpin(c, w->shared_pin);
@@ -1499,6 +1827,82 @@ int ompi_amd_get_accumulate(ompi_amd_win_t *w, const void *origin, void *result,
 // afterwards (local).  Null odt / rdt / tdt: `type` contiguous.  The packed
 // scratch is stream-ordered (hipMallocAsync / hipFreeAsync on the call's
 // stream).
+// acc_ddt for MAXLOC / MINLOC operand types (ddt_pair_kernel above): every
+// side's signature counts packed pairs; a contiguous side (NULL program)
+// holds `count` memory pairs (extent apart), a derived one the packed
+// stream its program describes (the origin packed, the result unpacked, by
+// the convertor's kernels, as for the other types).
+static int acc_ddt_pair(ompi_amd_win_t *w, const void *origin, size_t ocount, const ompi_amd_ddt_t *odt,
+                        void *result, size_t rcount, const ompi_amd_ddt_t *rdt, int target, size_t disp,
+                        size_t tcount, const ompi_amd_ddt_t *tdt, int type, int op, void *stream) {
+    pair_fn f = nullptr;
+    int64_t P = 0, E = 0;
+    int32_t koff = 0;
+    if (!pair_info(type, op, &f, &P, &E, &koff)) {
+        record_msg("osc accumulate: op %d on pair type %d is not provided", op, type);
+        return OMPI_AMD_ERR_UNSUPPORTED;
+    }
+    const bool fetch = result != nullptr;
+    const size_t tsig = tdt ? ompi_amd_ddt_size(tdt) * tcount : (size_t)P * tcount;
+    if (tsig == 0) return OMPI_AMD_SUCCESS;
+    if (tsig % (size_t)P != 0 ||
+        (op != OMPI_AMD_OP_NO_OP && (odt ? ompi_amd_ddt_size(odt) * ocount : (size_t)P * ocount) != tsig) ||
+        (fetch && (rdt ? ompi_amd_ddt_size(rdt) * rcount : (size_t)P * rcount) != tsig) ||
+        (op != OMPI_AMD_OP_NO_OP && !origin)) {
+        record_msg("osc accumulate: origin / result / target type signatures differ (pair type %d)", type);
+        return OMPI_AMD_ERR_BAD_PARAM;
+    }
+    const int64_t n = (int64_t)(tsig / (size_t)P);
+    ddt_view tv{};
+    if (tdt && !ddt_view_of(tdt, &tv)) return OMPI_AMD_ERR_BAD_PARAM;
+    if (target < 0 || target >= w->size) return OMPI_AMD_ERR_BAD_PARAM;
+    const int64_t base = (int64_t)disp * (int64_t)w->peer_disp[target];
+    const int64_t last = (int64_t)(tcount - 1) * (tdt ? tv.d.extent : E);
+    const int64_t lo = base + (tdt ? tv.lo + std::min<int64_t>(0, last) : 0);
+    const int64_t hi = base + (tdt ? tv.hi + std::max<int64_t>(0, last) : n * E);
+    char *t = nullptr;
+    OSC_TRY(target_span(w, target, base, lo - base, hi - base, &t));
+    hipStream_t s = win_stream(w, stream);
+    OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
+    const int32_t pk = (int32_t)(P - (int64_t)sizeof(int));  // packed: the index right after the value
+    pair_side in{const_cast<char *>(static_cast<const char *>(origin)), E, koff};
+    pair_side old{static_cast<char *>(result), E, koff};
+    void *po = nullptr, *pr = nullptr;
+    int rc = OMPI_AMD_SUCCESS;
+    if (odt && op != OMPI_AMD_OP_NO_OP) {  // the origin's packed pairs (local; before the lock)
+        rc = record_hip(hipMallocAsync(&po, tsig, s), "hipMallocAsync (osc origin pack)");
+        size_t done = 0;
+        if (rc == OMPI_AMD_SUCCESS) rc = ompi_amd_ddt_pack(odt, ocount, origin, po, 0, tsig, &done, s);
+        if (rc == OMPI_AMD_SUCCESS && done != tsig) rc = OMPI_AMD_ERR_BAD_PARAM;
+        in = pair_side{static_cast<char *>(po), P, pk};
+    }
+    if (op == OMPI_AMD_OP_NO_OP) in.p = nullptr;
+    if (rc == OMPI_AMD_SUCCESS && fetch && rdt) {
+        rc = record_hip(hipMallocAsync(&pr, tsig, s), "hipMallocAsync (osc result stream)");
+        old = pair_side{static_cast<char *>(pr), P, pk};
+    }
+    if (rc == OMPI_AMD_SUCCESS) rc = launch_lock(w, target, 0, s);
+    if (rc == OMPI_AMD_SUCCESS) {
+        const uint32_t *gate = taken_word(w, target, true);
+        ddt_desc dd{};
+        if (tdt) dd = tv.d;  // else nelem 0: a contiguous target
+        const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n + kOscThreads - 1) / kOscThreads,
+                                                                      osc_grid_cap()));
+        f(dim3((unsigned)blocks), dd, t, in, old, n, gate, s);
+        rc = record_hip(hipGetLastError(), "osc pair accumulate launch");
+        const int urc = launch_lock(w, target, 1, s);  // always release
+        if (rc == OMPI_AMD_SUCCESS) rc = urc;
+    }
+    if (rc == OMPI_AMD_SUCCESS && pr) {  // the fetched pairs into the result layout (local)
+        size_t done = 0;
+        rc = ompi_amd_ddt_unpack(rdt, rcount, pr, result, 0, tsig, &done, s);
+        if (rc == OMPI_AMD_SUCCESS && done != tsig) rc = OMPI_AMD_ERR_BAD_PARAM;
+    }
+    if (po) hip_ignore(hipFreeAsync(po, s));
+    if (pr) hip_ignore(hipFreeAsync(pr, s));
+    return rc;
+}
+
 static int acc_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount, const ompi_amd_ddt_t *odt,
                    void *result, size_t rcount, const ompi_amd_ddt_t *rdt, int target, size_t disp,
                    size_t tcount, const ompi_amd_ddt_t *tdt, int type, int op, void *stream) {
@@ -1506,12 +1910,11 @@ static int acc_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount, const o
         return OMPI_AMD_ERR_BAD_PARAM;
     const size_t ext = ompi_amd_type_extent(type);
     const bool fetch = result != nullptr;
+    if ((odt || rdt || tdt) && is_pair_type(type))
+        return acc_ddt_pair(w, origin, ocount, odt, result, rcount, rdt, target, disp, tcount, tdt, type, op,
+                            stream);
     const size_t tbytes = (tdt ? ompi_amd_ddt_size(tdt) : ext) * tcount;
     if (tbytes == 0) return OMPI_AMD_SUCCESS;
-    if ((odt || rdt || tdt) && is_pair_type(type)) {
-        record_msg("osc accumulate: derived datatypes of pair type %d are not provided", type);
-        return OMPI_AMD_ERR_UNSUPPORTED;
-    }
     if (tbytes % ext != 0 ||
         (op != OMPI_AMD_OP_NO_OP && (odt ? ompi_amd_ddt_size(odt) : ext) * ocount != tbytes) ||
         (fetch && (rdt ? ompi_amd_ddt_size(rdt) : ext) * rcount != tbytes) ||
@@ -1536,12 +1939,8 @@ static int acc_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount, const o
     const int64_t last = (int64_t)(tcount - 1) * (tdt ? tv.d.extent : (int64_t)ext);
     const int64_t lo = base + (tdt ? tv.lo + std::min<int64_t>(0, last) : 0);
     const int64_t hi = base + (tdt ? tv.hi + std::max<int64_t>(0, last) : (int64_t)tbytes);
-    if (lo < 0 || hi > (int64_t)w->peer_bytes[target] || !w->peer_base[target]) {
-        record_msg("osc: target %d typed range [%lld, %lld) outside its %llu-byte window", target,
-                   (long long)lo, (long long)hi, (unsigned long long)w->peer_bytes[target]);
-        return OMPI_AMD_ERR_BAD_PARAM;
-    }
-    char *t = w->peer_base[target] + base;
+    char *t = nullptr;
+    OSC_TRY(target_span(w, target, base, lo - base, hi - base, &t));
     hipStream_t s = win_stream(w, stream);
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
     // origin stream, packed (local; before the lock)
@@ -1633,12 +2032,8 @@ static int rma_ddt(ompi_amd_win_t *w, void *origin, size_t ocount, const ompi_am
     const int64_t last = tdt ? (int64_t)(tcount - 1) * tv.d.extent : 0;
     const int64_t lo = base + (tdt ? tv.lo + std::min<int64_t>(0, last) : 0);
     const int64_t hi = base + (tdt ? tv.hi + std::max<int64_t>(0, last) : (int64_t)tbytes);
-    if (lo < 0 || hi > (int64_t)w->peer_bytes[target] || !w->peer_base[target]) {
-        record_msg("osc: target %d typed range [%lld, %lld) outside its %llu-byte window", target,
-                   (long long)lo, (long long)hi, (unsigned long long)w->peer_bytes[target]);
-        return OMPI_AMD_ERR_BAD_PARAM;
-    }
-    char *t = w->peer_base[target] + base;
+    char *t = nullptr;
+    OSC_TRY(target_span(w, target, base, lo - base, hi - base, &t));
     hipStream_t s = win_stream(w, stream);
     OSC_TRY(record_hip(hipSetDevice(comm_device(w->c)), "hipSetDevice"));
     const uint32_t *gate = epoch_gate(w, target);

@@ -627,11 +627,23 @@ static int rocm_shared_query(struct ompi_win_t *win, int rank, size_t *size, int
     return OMPI_AMD_ERR_UNSUPPORTED == rc ? MPI_ERR_WIN : to_ompi_err(rc);
 }
 
-/* MPI_Win_attach / MPI_Win_detach: this component makes no dynamic windows
- * (rocm_query leaves that flavor to osc/rdma), so as osc/sm for its own
- * flavors (osc_sm_component.c:488-511) */
-static int rocm_attach(struct ompi_win_t *w, void *b, size_t s) { return MPI_ERR_RMA_ATTACH; }
-static int rocm_detach(struct ompi_win_t *w, const void *b) { return MPI_ERR_RMA_ATTACH; }
+/* MPI_Win_attach / MPI_Win_detach (osc_rdma_dynamic.c:162-300 for the
+ * host flavor): device memory peers can map into a dynamic window made with
+ * the ompi_amd_device info key.  Host memory, device memory peers cannot
+ * map as it is, or a window of another flavor (as osc/sm,
+ * osc_sm_component.c:488-511): MPI_ERR_RMA_ATTACH; detaching what was not
+ * attached: MPI_ERR_RMA_RANGE. */
+static int rocm_attach(struct ompi_win_t *w, void *b, size_t s)
+{
+    const int rc = ompi_amd_win_attach(mod(w)->dev_win, b, s);
+    return OMPI_AMD_SUCCESS == rc ? OMPI_SUCCESS : MPI_ERR_RMA_ATTACH;
+}
+static int rocm_detach(struct ompi_win_t *w, const void *b)
+{
+    const int rc = ompi_amd_win_detach(mod(w)->dev_win, b);
+    return OMPI_AMD_SUCCESS == rc ? OMPI_SUCCESS
+         : OMPI_AMD_ERR_UNSUPPORTED == rc ? MPI_ERR_RMA_ATTACH : MPI_ERR_RMA_RANGE;
+}
 
 static const ompi_osc_base_module_t rocm_module_template = {
     .osc_win_shared_query = rocm_shared_query,
@@ -702,12 +714,17 @@ static int rocm_query(struct ompi_win_t *win, void **base, size_t size, int disp
             v[0] = dev;
             v[1] = !dev;
         }
-    } else if (MPI_WIN_FLAVOR_ALLOCATE == flavor || MPI_WIN_FLAVOR_SHARED == flavor) {
+    } else if (MPI_WIN_FLAVOR_ALLOCATE == flavor || MPI_WIN_FLAVOR_SHARED == flavor ||
+               MPI_WIN_FLAVOR_DYNAMIC == flavor) {
+        /* a dynamic window holds device memory only when the application
+         * says so at creation (what it attaches comes later): with the info
+         * key this component takes it and refuses host attaches; without
+         * it osc/rdma keeps dynamic windows, for host memory */
         (void) opal_info_get_bool(info, "ompi_amd_device", &dev, &flag);
         v[0] = flag && dev;
         v[1] = !v[0];
     } else {
-        return -1;  /* dynamic windows stay with osc/rdma */
+        return -1;
     }
     if (OMPI_SUCCESS != comm->c_coll->coll_allreduce(MPI_IN_PLACE, v, 2, MPI_INT, MPI_MAX, comm,
                                                      comm->c_coll->coll_allreduce_module))
@@ -751,7 +768,9 @@ static int rocm_select(struct ompi_win_t *win, void **base, size_t size, int dis
                1 == ompi_amd_is_device_pointer(*base);
     rc = ompi_amd_comm_agree(m->dev_comm, local_ok, &all_ok);
     if (OMPI_AMD_SUCCESS == rc && !all_ok) rc = OMPI_AMD_ERR_UNSUPPORTED;
-    if (OMPI_AMD_SUCCESS == rc && MPI_WIN_FLAVOR_SHARED == flavor) {
+    if (OMPI_AMD_SUCCESS == rc && MPI_WIN_FLAVOR_DYNAMIC == flavor) {
+        rc = ompi_amd_win_create_dynamic(m->dev_comm, &m->dev_win);
+    } else if (OMPI_AMD_SUCCESS == rc && MPI_WIN_FLAVOR_SHARED == flavor) {
         /* one allocation, segments back to back unless alloc_shared_noncontig
          * (osc_sm_component.c:259-268) */
         bool noncontig = false;

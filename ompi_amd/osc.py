@@ -104,6 +104,28 @@ class Window:
                                                           ctypes.byref(h)), "win_allocate_shared")
         return cls(comm, h, b.value or 0, nbytes)
 
+    @classmethod
+    def create_dynamic(cls, comm: Communicator) -> "Window":
+        """MPI_Win_create_dynamic (collective): no memory until attach();
+        displacements are the target's absolute addresses."""
+        h = ctypes.c_void_p()
+        _lib.check(comm._lib.ompi_amd_win_create_dynamic(comm._h, ctypes.byref(h)),
+                   "win_create_dynamic")
+        return cls(comm, h, 0, 0)
+
+    def attach(self, base, nbytes: int | None = None) -> int:
+        """MPI_Win_attach (local) of device memory; returns its address (the
+        displacement peers use, after the application shares it)."""
+        if nbytes is None:
+            nbytes = base.numel() * base.element_size()
+        ptr = _ptr(base)
+        _lib.check(self._lib.ompi_amd_win_attach(self._h, ptr, nbytes), "win_attach")
+        return ptr
+
+    def detach(self, base) -> None:
+        """MPI_Win_detach (local)."""
+        _lib.check(self._lib.ompi_amd_win_detach(self._h, _ptr(base)), "win_detach")
+
     def shared_query(self, rank: int):
         """MPI_Win_shared_query: (size, disp_unit, address in this process)
         of `rank`'s segment; rank < 0 (MPI_PROC_NULL) = the first nonzero one."""

@@ -104,8 +104,8 @@ int main(int argc, char **argv)
         CHECK(c->osc_query(&w, &hb, 0, 4, &ci, &dev_info, MPI_WIN_FLAVOR_ALLOCATE) < 0, "inter");
         CHECK(c->osc_query(&w, &hb, 0, 4, &cr, &dev_info, MPI_WIN_FLAVOR_ALLOCATE) < 0,
               "remote peers");
-        CHECK(c->osc_query(&w, &hb, 0, 4, &comm, &dev_info, MPI_WIN_FLAVOR_DYNAMIC) < 0,
-              "dynamic windows");
+        CHECK(c->osc_query(&w, &hb, 0, 4, &comm, NULL, MPI_WIN_FLAVOR_DYNAMIC) < 0,
+              "dynamic windows without the device info key (osc/rdma keeps them)");
         CHECK(c->osc_query(&w, &hb, 0, 4, &comm, NULL, MPI_WIN_FLAVOR_SHARED) < 0,
               "shared without the device info key");
     }
@@ -450,6 +450,51 @@ int main(int argc, char **argv)
         CHECK(sm->osc_free(&swin) == OMPI_SUCCESS, "free shared");
         free(buf);
         free(ref);
+    }
+
+    /* MPI_Win_create_dynamic with the device info key:
+     * a 4 MiB device region attached on every rank, its address shared,
+     * MPI_Put of 1000 floats into the next rank's region at an absolute
+     * displacement under fences, bit-exact; host memory refused at attach
+     * (MPI_ERR_RMA_ATTACH), a second detach refused (MPI_ERR_RMA_RANGE) */
+    {
+        ompi_win_t dw = {0};
+        void *nb = NULL, *reg = NULL, *zero = calloc(1, 4 << 20), *hostbuf = calloc(1, 4096);
+        int addr[4 * OMPI_AMD_MAX_RANKS] = {0};
+        const size_t k = 1000;
+        CHECK(c->osc_query(&dw, &nb, 0, 1, &comm, &dev_info, MPI_WIN_FLAVOR_DYNAMIC) == 101,
+              "query dynamic with the device info key");
+        CHECK(c->osc_select(&dw, &nb, 0, 1, &comm, &dev_info, MPI_WIN_FLAVOR_DYNAMIC, &model) ==
+                  OMPI_SUCCESS && dw.w_osc_module, "select dynamic");
+        ompi_osc_base_module_t *dm = dw.w_osc_module;
+        CHECK(harness_dev_alloc_copy(&reg, zero, 4 << 20) == 0, "dynamic region");
+        CHECK(dm->osc_win_attach(&dw, reg, 4 << 20) == OMPI_SUCCESS, "attach a device region");
+        CHECK(dm->osc_win_attach(&dw, hostbuf, 4096) == MPI_ERR_RMA_ATTACH, "host attach refused");
+        for (int q = 0; q < 4; ++q)  /* the address in 16-bit pieces: MAX over ints gathers them */
+            addr[4 * g_rank + q] = (int) (((uint64_t) (uintptr_t) reg >> (16 * q)) & 0xffff);
+        CHECK(comm.c_coll->coll_allreduce(MPI_IN_PLACE, addr, 4 * g_size, &harness_mpi_int, &harness_mpi_max,
+                                          &comm, comm.c_coll->coll_allreduce_module) == OMPI_SUCCESS,
+              "address exchange");
+        uint64_t an = 0;
+        for (int q = 0; q < 4; ++q) an |= (uint64_t) (unsigned) addr[4 * nxt + q] << (16 * q);
+        CHECK(dm->osc_fence(0, &dw) == OMPI_SUCCESS, "dynamic fence 1");
+        CHECK(dm->osc_put(dorg, (int) k, &dfloat, nxt, (ptrdiff_t) (an + 256), (int) k, &dfloat, &dw) ==
+                  OMPI_SUCCESS, "dynamic put");
+        CHECK(dm->osc_fence(0, &dw) == OMPI_SUCCESS, "dynamic fence 2");
+        {
+            float *gotd = malloc(k * 4), *want = malloc(n * 4);
+            fill_exact(want, n, prv, 2);  /* the previous rank's origin */
+            CHECK(harness_dev_copy_back(gotd, (char *) reg + 256, k * 4) == 0, "dynamic copy back");
+            CHECK(0 == memcmp(gotd, want, k * 4), "dynamic put landed in the attached region");
+            free(gotd);
+            free(want);
+        }
+        CHECK(dm->osc_win_detach(&dw, reg) == OMPI_SUCCESS, "detach");
+        CHECK(dm->osc_win_detach(&dw, reg) == MPI_ERR_RMA_RANGE, "second detach refused");
+        CHECK(dm->osc_free(&dw) == OMPI_SUCCESS, "free dynamic");
+        harness_dev_free(reg);
+        free(zero);
+        free(hostbuf);
     }
 
     /* MPI_Win_allocate: a shared counter, fetch_and_op from every rank */

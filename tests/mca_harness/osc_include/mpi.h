@@ -15,6 +15,7 @@
 #define MPI_WIN_SEPARATE 1
 #define MPI_PROC_NULL (-2)
 #define MPI_ERR_WIN 53
+#define MPI_ERR_RMA_RANGE 68
 #define MPI_ERR_RMA_ATTACH 69
 /* the predefined handles the glue's agreement uses (ompi/include/mpi.h.in:
  * OMPI_PREDEFINED_GLOBAL): harness objects, defined by osc_harness.c */

@@ -8,6 +8,7 @@ buffers.  Expected results come from the deterministic per-rank inputs and,
 for accumulates, from the CPU oracle's op/base restatement applied in the
 target's order.  One JSON line per case; exit 0 only if all passed.
 """
+import ctypes
 import json
 import os
 import sys
@@ -644,6 +645,143 @@ def _slots(dt, count, elem):
         for d, bl in dt.runs:
             offs.extend(i * dt.extent + d + b for b in range(0, bl, elem))
     return np.array(offs, dtype=np.int64)
+
+
+def _pairs(prim, m, r, salt, seed_junk):
+    """m memory pairs of `prim` (DOUBLE_INT 16 B, SHORT_INT 8 B): small
+    integer values (ties exercise the lowest-index rule), random indices,
+    junk in the padding."""
+    g = np.random.default_rng(SEED + 131 * salt + r)
+    mem = np.frombuffer(payload(r, seed_junk, m * prim.extent), np.uint8).copy().reshape(m, prim.extent)
+    v = g.integers(-8, 9, m)
+    k = g.integers(0, 1 << 20, m).astype(np.int32)
+    if prim is mop.MPI_DOUBLE_INT:
+        mem[:, 0:8] = v.astype(np.float64).view(np.uint8).reshape(m, 8)
+        mem[:, 8:12] = k.view(np.uint8).reshape(m, 4)
+    else:  # SHORT_INT: short at 0, int at 4 (bytes 2-3 padding)
+        mem[:, 0:2] = v.astype(np.int16).view(np.uint8).reshape(m, 2)
+        mem[:, 4:8] = k.view(np.uint8).reshape(m, 4)
+    return mem
+
+
+def _member_bytes(prim):
+    """Byte ranges of a pair's members (what MPI owns; the rest is padding)."""
+    return [(0, 8), (8, 12)] if prim is mop.MPI_DOUBLE_INT else [(0, 2), (4, 8)]
+
+
+def case_acc_ddt_pair(comm, rank, n, salt):
+    """MPI_Accumulate / MPI_Get_accumulate of pair types (MAXLOC / MINLOC
+    operands) with derived datatypes (ompi_osc_base_sndrcv_op,
+    osc_base_obj_convert.c:73-245): a vector of MPI_DOUBLE_INT at the
+    target from a contiguous or a strided origin (12-byte packed pairs into
+    16-byte slots), REPLACE, a contiguous MPI_SHORT_INT target (int at
+    offset 4) from a strided origin, and get_accumulate into a strided
+    result; expected from the oracle's op/base LOC rule pair by pair in
+    type-map order, bit-exact, every padding and gap byte of the window (and
+    of the result) untouched."""
+    from ompi_amd import datatype as dd
+    DI, SI = mop.MPI_DOUBLE_INT, mop.MPI_SHORT_INT
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    di = dd.from_runs("double_int", [(0, 12)], 16)
+    si = dd.from_runs("short_int", [(0, 2), (4, 4)], 8)
+    runs = [
+        # (name, prim, target type, tcount, origin type or None, op)
+        ("double_int_vector_maxloc", DI, dd.type_vector(300, 1, 2, di), 2, None, mop.MPI_MAXLOC),
+        ("double_int_vector_minloc_strided_origin", DI, dd.type_vector(150, 2, 3, di), 2,
+         dd.type_vector(600, 1, 3, di), mop.MPI_MINLOC),
+        ("double_int_vector_replace", DI, dd.type_vector(200, 1, 3, di), 1, dd.type_vector(200, 1, 2, di),
+         mop.MPI_REPLACE),
+        ("short_int_contig_target_minloc", SI, None, 500, dd.type_vector(500, 1, 2, si), mop.MPI_MINLOC),
+    ]
+    disp_unit, disp = 8, 3
+    for k, (name, prim, tdt, tcount, odt, op) in enumerate(runs):
+        E, mem_b = prim.extent, _member_bytes(prim)
+        m = (tdt.size // prim.size) * tcount if tdt else tcount  # pairs
+        span = ((tcount - 1) * tdt.extent + tdt.true_span) if tdt else m * E
+        wbytes = disp * disp_unit + span + 64
+        init = [np.frombuffer(payload(r, salt + k, wbytes), np.uint8).copy() for r in range(n)]
+        tslots = disp * disp_unit + (np.array([i * tdt.extent + d for i in range(tcount) for d, _ in tdt.runs
+                                               if d % E == 0], np.int64) if tdt else np.arange(m) * E)
+        assert len(tslots) == m
+        for r in range(n):  # real pairs in the window's target slots (gaps keep payload bytes)
+            pr = _pairs(prim, m, r, salt + 10 + k, salt + 11 + k)
+            for j, t in enumerate(tslots):
+                init[r][t:t + E] = pr[j]
+        org_mem = [_pairs(prim, m, r, salt + 20 + k, salt + 21 + k) for r in range(n)]
+        if odt is None:
+            org_buf, ocount = [om.reshape(-1) for om in org_mem], m
+        else:  # the pairs at the origin type's slots, junk between
+            ocount = 1
+            oslots = np.array([d for d, _ in odt.runs if d % E == 0], np.int64)
+            assert len(oslots) == m
+            org_buf = []
+            for r in range(n):
+                b = np.frombuffer(payload(r, salt + 30 + k, int(oslots.max()) + E), np.uint8).copy()
+                for j, o in enumerate(oslots):
+                    b[o:o + E] = org_mem[r][j]
+                org_buf.append(b)
+        base = dev(init[rank])
+        win = osc.Window.create(comm, base, wbytes, disp_unit=disp_unit)
+        try:
+            o = dev(org_buf[rank])
+            win.fence(stream=STREAM)
+            win.accumulate_ddt(o, ocount, odt, nxt, disp, tcount, tdt, prim, op, stream=STREAM)
+            win.fence(stream=STREAM, blocking=True)
+            exp = init[rank].copy()
+            cur = np.stack([exp[t:t + E] for t in tslots]).copy()
+            if op is mop.MPI_REPLACE:
+                new = org_mem[prv].copy()
+            else:
+                new = cur.copy()
+                orc.op_2buff(op.index, prim.code, org_mem[prv].reshape(-1).copy(), new.reshape(-1), m)
+            for j, t in enumerate(tslots):
+                for a, b in mem_b:  # only the members; the padding keeps the window's bytes
+                    exp[t + a:t + b] = new[j, a:b]
+            ok, msg = eq(host(base), exp, f"{name}: window")
+            if not ok:
+                return ok, msg
+        finally:
+            win.free()
+        comm_barrier()
+    # get_accumulate MAXLOC: the old target pairs into a strided result
+    prim, E = DI, 16
+    tdt, tcount = dd.type_vector(120, 1, 2, di), 3
+    rdt = dd.type_vector(360, 1, 2, di)
+    m = 360
+    span = (tcount - 1) * tdt.extent + tdt.true_span
+    wbytes = span + 64
+    tslots = np.array([i * tdt.extent + d for i in range(tcount) for d, _ in tdt.runs], np.int64)
+    init = [np.frombuffer(payload(r, salt + 50, wbytes), np.uint8).copy() for r in range(n)]
+    for r in range(n):
+        pr = _pairs(prim, m, r, salt + 51, salt + 52)
+        for j, t in enumerate(tslots):
+            init[r][t:t + E] = pr[j]
+    org = [_pairs(prim, m, r, salt + 53, salt + 54) for r in range(n)]
+    base = dev(init[rank])
+    win = osc.Window.create(comm, base, wbytes, disp_unit=1)
+    try:
+        o = dev(org[rank].reshape(-1))
+        res = zeros(2 * m * E)
+        win.fence(stream=STREAM)
+        win.get_accumulate_ddt(o, m, None, res, 1, rdt, nxt, 0, tcount, tdt, prim, mop.MPI_MAXLOC,
+                               stream=STREAM)
+        win.fence(stream=STREAM, blocking=True)
+        got = host(res).reshape(2 * m, E)
+        old = np.stack([init[nxt][t:t + E] for t in tslots])
+        exp = np.zeros((2 * m, E), np.uint8)
+        exp[0::2, 0:12] = old[:, 0:12]  # the fetched members; padding and odd slots stay zero
+        ok, msg = eq(got, exp, "get_accumulate MAXLOC: fetched into the strided result")
+        if not ok:
+            return ok, msg
+        cur = np.stack([init[rank][t:t + E] for t in tslots]).copy()
+        new = cur.copy()
+        orc.op_2buff(mop.MPI_MAXLOC.index, prim.code, org[prv].reshape(-1).copy(), new.reshape(-1), m)
+        expw = init[rank].copy()
+        for j, t in enumerate(tslots):
+            expw[t:t + 12] = new[j, 0:12]
+        return eq(host(base), expw, "get_accumulate MAXLOC: window")
+    finally:
+        win.free()
 
 
 def case_acc_ddt(comm, rank, n, salt):
@@ -1366,6 +1504,120 @@ def case_separate_refused(comm, rank, n):
         comm.set_param("osc_win_separate", 1)
 
 
+def case_dynamic_window(comm, rank, n, salt):
+    """MPI_Win_create_dynamic / MPI_Win_attach / MPI_Win_detach over device
+    memory (osc/rdma's flavor, osc_rdma_dynamic.c:162-300): each rank
+    attaches a 4 MiB hipMalloc region and shares its address; puts,
+    accumulates (SUM fp32) and gets at absolute addresses under fence and
+    lock_all epochs reach exactly the attached regions; a second region
+    attached later is found; host memory and memory peers cannot map (a small
+    tensor) are refused at attach; an access outside every attached region
+    and one into a detached region are refused at the call."""
+    lib = _lib.load()
+    F = mop.MPI_FLOAT
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    R = 4 << 20
+    regions, failures = [], []
+
+    def region(seed):
+        for _ in range(3):  # a fresh address (never exported before) is exportable
+            p = ctypes.c_void_p()
+            _lib.check(lib.ompi_amd_device_alloc(ctypes.byref(p), R), "device_alloc")
+            regions.append(p.value)
+            init = payload(rank, seed, R)
+            _lib.check(lib.ompi_amd_memcpy(p.value, init.ctypes.data, R), "fill")
+            try:
+                win.attach(p.value, R)
+                return p.value, init
+            except _lib.OmpiAmdError as e:
+                if e.code != _lib.ERR_UNSUPPORTED:
+                    raise
+        raise RuntimeError("no exportable 4 MiB region in three tries")
+
+    def raw(addr, nb):
+        out = np.empty(nb, np.uint8)
+        _lib.check(lib.ompi_amd_memcpy(out.ctypes.data, addr, nb), "read")
+        return out
+
+    win = osc.Window.create_dynamic(comm)
+    try:
+        a, init = region(salt)
+        addrs = [None] * n
+        dist.all_gather_object(addrs, a)  # the application shares the address (MPI_Get_address + a send)
+        inits = [payload(r, salt, R) for r in range(n)]
+        pb, acc_n, gb = 65536 + 13, 100001, 4096
+        src = dev(payload(rank, salt + 1, pb))
+        accv = fp_inputs(F, acc_n, rank, salt + 2, "E")
+        acc = dev(accv)
+        got = zeros(gb)
+        comm_barrier()
+        win.fence(stream=STREAM)
+        win.put(src, nxt, addrs[nxt] + 1000, pb, stream=STREAM)
+        win.accumulate(acc, acc_n, F, nxt, addrs[nxt] + (2 << 20), mop.MPI_SUM, stream=STREAM)
+        win.get(got, nxt, addrs[nxt] + (3 << 20), gb, stream=STREAM)
+        win.fence(stream=STREAM, blocking=True)
+        comm_barrier()
+        exp = init.copy()
+        exp[1000:1000 + pb] = payload(prv, salt + 1, pb)
+        cur = exp[2 << 20:(2 << 20) + acc_n * 4].view(np.float32).copy()
+        orc.op_2buff(mop.MPI_SUM.index, F.code, fp_inputs(F, acc_n, prv, salt + 2, "E").copy(), cur, acc_n)
+        exp[2 << 20:(2 << 20) + acc_n * 4] = cur.view(np.uint8)
+        ok, msg = eq(raw(a, R), exp, "fence epoch: attached region")
+        if not ok:
+            failures.append(msg)
+        ok, msg = eq(host(got), inits[nxt][3 << 20:(3 << 20) + gb], "fence epoch: get")
+        if not ok:
+            failures.append(msg)
+        # a second region, attached later, under lock_all
+        b, init_b = region(salt + 5)
+        addrs_b = [None] * n
+        dist.all_gather_object(addrs_b, b)
+        src2 = dev(payload(rank, salt + 6, 12345))
+        comm_barrier()
+        win.lock_all(stream=STREAM)
+        win.put(src2, nxt, addrs_b[nxt] + 777, 12345, stream=STREAM)
+        win.unlock_all(stream=STREAM)
+        comm_barrier()
+        exp_b = init_b.copy()
+        exp_b[777:777 + 12345] = payload(prv, salt + 6, 12345)
+        ok, msg = eq(raw(b, R), exp_b, "lock_all epoch: second region")
+        if not ok:
+            failures.append(msg)
+        # refusals at attach and at the access
+        hostbuf = np.zeros(1 << 22, np.uint8)
+        small = zeros(4096 + 12)
+        for what, fn, code in (
+                ("attach of host memory", lambda: win.attach(hostbuf.ctypes.data, hostbuf.nbytes),
+                 _lib.ERR_NOT_DEVICE),
+                ("attach of memory peers cannot map", lambda: win.attach(small), _lib.ERR_UNSUPPORTED),
+                ("put outside every attached region",
+                 lambda: win.put(src2, nxt, addrs[nxt] + R + 64, 256, stream=STREAM), _lib.ERR_BAD_PARAM),
+                ("put across a region's end",
+                 lambda: win.put(src2, nxt, addrs[nxt] + R - 100, 256, stream=STREAM), _lib.ERR_BAD_PARAM)):
+            try:
+                fn()
+                failures.append(what + " accepted")
+            except _lib.OmpiAmdError as e:
+                if e.code != code:
+                    failures.append(f"{what}: code {e.code}, want {code}")
+        win.detach(b)
+        comm_barrier()  # every rank detached its second region
+        try:
+            win.put(src2, nxt, addrs_b[nxt] + 777, 64, stream=STREAM)
+            failures.append("put into a detached region accepted")
+        except _lib.OmpiAmdError as e:
+            if e.code != _lib.ERR_BAD_PARAM:
+                failures.append(f"put into a detached region: code {e.code}")
+        win.detach(a)
+        STREAM.synchronize()
+    finally:
+        comm_barrier()
+        win.free()
+        for p_ in regions:
+            lib.ompi_amd_device_free(p_)
+    return not failures, "; ".join(failures[:3])
+
+
 def case_pscw_all_to_one(comm, rank, n, salt, count=100003):
     """Rank 0 posts to every other rank; each origin accumulates (SUM, exact
     data) into its own slice of rank 0's window, then rank 0 waits: every
@@ -1618,6 +1870,7 @@ def main():
         ("osc_get_accumulate", lambda: case_get_accumulate(comm, rank, n, 92)),
         ("osc_accumulate_derived_datatypes", lambda: case_acc_ddt(comm, rank, n, 150)),
         ("osc_put_get_derived_datatypes", lambda: case_put_get_ddt(comm, rank, n, 160)),
+        ("osc_accumulate_derived_pair_types", lambda: case_acc_ddt_pair(comm, rank, n, 165)),
         ("osc_separate_model_small_tensor", lambda: case_separate_window(comm, rank, n, 170)),
         ("osc_separate_model_refused", lambda: case_separate_refused(comm, rank, n)),
         ("osc_separate_model_forced_64MiB",
@@ -1637,6 +1890,7 @@ def main():
         ("osc_random_epochs_separate", lambda: case_osc_random_epochs(comm, rank, n, 702 + STRESS_SEED,
                                                                       separate=True)),
         ("osc_request_rma", lambda: case_request_rma(comm, rank, n, 97)),
+        ("osc_dynamic_window", lambda: case_dynamic_window(comm, rank, n, 99)),
         ("osc_shared_window", lambda: case_shared_window(comm, rank, n, 98)),
         ("osc_shared_window_noncontig", lambda: case_shared_window(comm, rank, n, 99, noncontig=True)),
     ]
