@@ -4,15 +4,19 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
+/* A copy from pageable memory may return before the bytes reach the
+ * device (the DMA from the staging buffer still runs): wait for it, so a
+ * peer's RMA that follows the next rendezvous cannot be overwritten. */
+int harness_dev_copy_in(void *d, const void *h, size_t bytes)
+{
+    if (hipMemcpy(d, h, bytes, hipMemcpyHostToDevice) != hipSuccess) return -1;
+    return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+}
+
 int harness_dev_alloc_copy(void **d, const void *h, size_t bytes)
 {
     if (hipMalloc(d, bytes) != hipSuccess) return -1;
-    return hipMemcpy(*d, h, bytes, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
-}
-
-int harness_dev_copy_in(void *d, const void *h, size_t bytes)
-{
-    return hipMemcpy(d, h, bytes, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+    return harness_dev_copy_in(*d, h, bytes);
 }
 
 int harness_dev_copy_back(void *h, const void *d, size_t bytes)

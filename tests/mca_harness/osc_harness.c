@@ -477,6 +477,7 @@ int main(int argc, char **argv)
               "address exchange");
         uint64_t an = 0;
         for (int q = 0; q < 4; ++q) an |= (uint64_t) (unsigned) addr[4 * nxt + q] << (16 * q);
+        CHECK(harness_dev_copy_in(dorg, org, k * 4) == 0, "origin");  /* earlier sections reused it */
         CHECK(dm->osc_fence(0, &dw) == OMPI_SUCCESS, "dynamic fence 1");
         CHECK(dm->osc_put(dorg, (int) k, &dfloat, nxt, (ptrdiff_t) (an + 256), (int) k, &dfloat, &dw) ==
                   OMPI_SUCCESS, "dynamic put");
@@ -485,7 +486,9 @@ int main(int argc, char **argv)
             float *gotd = malloc(k * 4), *want = malloc(n * 4);
             fill_exact(want, n, prv, 2);  /* the previous rank's origin */
             CHECK(harness_dev_copy_back(gotd, (char *) reg + 256, k * 4) == 0, "dynamic copy back");
-            CHECK(0 == memcmp(gotd, want, k * 4), "dynamic put landed in the attached region");
+            CHECK(0 == memcmp(gotd, want, k * 4),
+                  "dynamic put landed in the attached region (got %g %g, want %g %g; region %p, next's %llx)",
+                  gotd[0], gotd[1], want[0], want[1], reg, (unsigned long long) an);
             free(gotd);
             free(want);
         }
