@@ -89,7 +89,9 @@ int ompi_amd_comm_size(const ompi_amd_comm_t *comm);
  *                   for tests */
 int ompi_amd_comm_set_param(ompi_amd_comm_t *comm, const char *key, int64_t value);
 /* Read a parameter above, or a state counter: "landing_bytes" (current
- * landing-buffer capacity), "imports" (this communicator's references to
+ * landing-buffer capacity), "landing_deferred_growths" (growths nonblocking
+ * calls queued and progress completed), "landing_retired" (buffers those
+ * growths replaced, freed at the next blocking growth or destroy), "imports" (this communicator's references to
  * peer mappings), "shadowed" (zero-copy calls that ran through the export
  * fallback), and the process-wide IPC registry's counters (mappings are
  * shared by every communicator, window and message of the process and

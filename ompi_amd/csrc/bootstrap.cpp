@@ -158,6 +158,15 @@ int ShmBoot::post(const void *mine, size_t len, uint64_t *ticket) {
     return OMPI_AMD_SUCCESS;
 }
 
+bool ShmBoot::can_post() const {
+    if (!map_) return false;
+    const uint64_t s = seq_ + 1;
+    if (s <= kRing) return true;
+    for (int r = 0; r < size_; ++r)
+        if (slot(r)->done.load(std::memory_order_acquire) < s - kRing) return false;
+    return true;
+}
+
 int ShmBoot::test(uint64_t ticket, void *all, size_t len, bool block, bool *ready) {
     *ready = false;
     if (!map_ || len > kBlob || ticket != done_ + 1 || ticket > seq_) return OMPI_AMD_ERR_BAD_PARAM;

@@ -11,7 +11,8 @@
 // its ticket without waiting; test() completes tickets in order once every
 // rank has posted.  Up to kRing - 1 tickets may be outstanding (a post
 // waits only for ring slots every rank has consumed) — the nonblocking
-// collectives post at call time and complete from progress.
+// collectives post at call time (or, while the ring is full, from progress:
+// can_post) and complete from progress.
 #pragma once
 
 #include <cstddef>
@@ -45,6 +46,8 @@ class ShmBoot {
     // block = true it waits (bounded by the attach timeout).
     int post(const void *mine, size_t len, uint64_t *ticket);
     int test(uint64_t ticket, void *all, size_t len, bool block, bool *ready);
+    // post() would not wait: the ring slot it overwrites was read by every rank
+    bool can_post() const;
     uint64_t posted() const { return seq_; }
     uint64_t consumed() const { return done_; }
 

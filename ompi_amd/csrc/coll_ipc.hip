@@ -304,6 +304,13 @@ struct call_blob {
     buf_desc s, r;
     uint64_t flags;  // per-call rank flags (bit 0: MPI_IN_PLACE)
 };
+// a landing-buffer growth's contribution: the new buffer, the token stamped
+// into its last bytes, whether this rank's allocation / export worked
+struct land_blob {
+    buf_desc d;
+    uint64_t token;
+    int ok;
+};
 
 // The parameters a path decision reads, captured when a nonblocking call is
 // posted so that its deferred launch takes the path every rank agreed on.
@@ -364,10 +371,23 @@ struct pending_op {
     bool exclusive = false;        // scan: exscan
     bool land = false;             // allgather / bcast through the landing buffers (no swap)
     std::vector<size_t> rcounts;   // reduce_scatter
+    // the ticket's blob while the rendezvous ring is full (nb_ticket): it is
+    // posted from progress, in queue order, once every rank read the slot
+    bool unposted = false;
+    size_t blob_len = 0;
+    union {
+        call_blob call;
+        land_blob land;
+    } blob{};
+    // PEND_GROW: this rank's new landing buffer (allocated and stamped at
+    // post time), its size and token
+    char *grow = nullptr;
+    size_t grow_bytes = 0;
+    uint64_t grow_token = 0;
 };
 
 enum { PEND_ALLREDUCE = 0, PEND_RSB = 1, PEND_ALLGATHER = 2, PEND_BCAST = 3, PEND_REDUCE = 4,
-       PEND_SCAN = 5, PEND_RS = 6 };
+       PEND_SCAN = 5, PEND_RS = 6, PEND_GROW = 7 };
 
 }  // namespace ompi_amd
 
@@ -445,6 +465,19 @@ struct ompi_amd_comm {
     size_t land_bytes = 0;                //   allreduce, large scan/exscan)
     ptr_set peer_land{};
     ipc_ref *land_ref[kMaxRanks] = {};   // peers' landing buffers (IPC registry references)
+    // Deferred growth (nonblocking calls, PEND_GROW): land_planned is the
+    // size once every queued growth has launched — what a post compares
+    // against; the buffers a growth replaced stay alive (and mapped) until
+    // the next point where every rank's earlier kernels are known done
+    // (a blocking growth, destroy): land_retired / land_ref_retired.
+    size_t land_planned = 0;
+    std::vector<char *> land_retired;
+    std::vector<ipc_ref *> land_ref_retired;
+    bool land_failed = false;             // a deferred growth failed: nothing after it launches
+    int unposted = 0;                     // pending ops whose ticket waits for a ring slot
+    hipStream_t side = nullptr;           // growth token stamps / checks (non-blocking stream)
+    uint64_t *peek_host = nullptr;        //   and where the check's kernel loads land
+    int64_t deferred_growths = 0;         // landing growths taken from progress (counter)
     std::vector<uint64_t> land_tokens;    // every rank's token of every landing growth (diagnostics)
     int memcpy_token_mismatch = 0;        // landing tokens right by kernel load, wrong by hipMemcpy
     int bcast_split = 0;                  // bcasts that ran as scatter + allgather
@@ -1271,11 +1304,47 @@ static uint64_t landing_token(int rank) {
 // its buffer is read back through every new mapping, as an assertion: a
 // mismatch fails the growth on every rank with the peer and both tokens
 // named (no retry).
+constexpr size_t kLandTag = 64;  // a landing buffer's last kLandTag bytes hold its token
+
+// the allocation a growth from `cur` usable bytes to `need` makes (32 MiB
+// steps, at least doubling); every rank computes it alike
+static size_t landing_want(size_t cur, size_t need) {
+    constexpr size_t kStep = 32u << 20;
+    return std::max((need + kLandTag + kStep - 1) / kStep * kStep,
+                    cur ? std::min(2 * (cur + kLandTag), kMaxIpcBytes) : 0);
+}
+
+// Buffers deferred growths replaced: called where every rank's earlier
+// kernels of this communicator are done (after a quiesce + barrier).
+static void free_retired_landing(ompi_amd_comm_t *c) {
+    for (ipc_ref *r : c->land_ref_retired) ipc_unmap(r, c);
+    c->land_ref_retired.clear();
+    for (char *p : c->land_retired) hip_ignore(hipFree(p));  // peers' mappings keep it alive
+    c->land_retired.clear();
+}
+
+// a new landing buffer's descriptor (its handle is already in d->h)
+static void land_desc(char *fresh, size_t want, buf_desc *d) {
+    d->id = buffer_id(fresh);
+    d->base = (uint64_t)(uintptr_t)fresh;
+    d->size = want;
+    d->pid = (uint64_t)getpid();
+    d->valid = 1;
+    // the registry keys on the allocation's real range (alloc_exportable pads it)
+    void *ab = nullptr;
+    size_t as = 0;
+    if (hipMemGetAddressRange((hipDeviceptr_t *)&ab, &as, (hipDeviceptr_t)fresh) == hipSuccess) {
+        d->base = (uint64_t)(uintptr_t)ab;
+        d->size = as;
+    } else {
+        (void)hipGetLastError();
+    }
+}
+
 static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     if (need <= c->land_bytes) return OMPI_AMD_SUCCESS;
-    constexpr size_t kStep = 32u << 20, kTag = 64;  // the last kTag bytes hold the token
-    const size_t want = std::max((need + kTag + kStep - 1) / kStep * kStep,
-                                 c->land_bytes ? std::min(2 * (c->land_bytes + kTag), kMaxIpcBytes) : 0);
+    constexpr size_t kTag = kLandTag;
+    const size_t want = landing_want(c->land_bytes, need);
     if (want > kMaxIpcBytes) {  // every rank decides alike (same need)
         record_msg("landing buffer of %zu bytes exceeds the %zu-byte IPC mapping limit", want,
                    kMaxIpcBytes);
@@ -1283,6 +1352,7 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     }
     TRY(quiesce(c));
     TRY(c->boot.barrier());  // every rank's earlier kernels are done
+    free_retired_landing(c);
     // the old mappings stay open until the new ones are (so the new ones
     // get fresh addresses in this process), then close
     ipc_ref *old_land[kMaxRanks];
@@ -1294,29 +1364,12 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     auto close_old = [&] {
         for (int p = 0; p < kMaxRanks; ++p) ipc_unmap(old_land[p], c);
     };
-    struct land_blob { buf_desc d; uint64_t token; int ok; };
     land_blob mine{}, all[kMaxRanks];
     char *fresh = nullptr;
     hipError_t e = alloc_exportable(want, &fresh, &mine.d.h);
     mine.token = landing_token(c->rank);
-    if (e == hipSuccess) {
-        mine.d.id = buffer_id(fresh);
-        mine.d.base = (uint64_t)(uintptr_t)fresh;
-        mine.d.size = want;
-        mine.d.pid = (uint64_t)getpid();
-        mine.d.valid = 1;
-        // the registry keys on the allocation's real range (alloc_exportable pads it)
-        void *ab = nullptr;
-        size_t as = 0;
-        if (hipMemGetAddressRange((hipDeviceptr_t *)&ab, &as, (hipDeviceptr_t)fresh) == hipSuccess) {
-            mine.d.base = (uint64_t)(uintptr_t)ab;
-            mine.d.size = as;
-        } else {
-            (void)hipGetLastError();
-        }
-    } else {
-        record_hip(e, "landing buffer: hipMalloc / hipIpcGetMemHandle");
-    }
+    if (e == hipSuccess) land_desc(fresh, want, &mine.d);
+    else record_hip(e, "landing buffer: hipMalloc / hipIpcGetMemHandle");
     // hipMemcpy from pageable memory may return once the bytes are staged,
     // before they reach the device: a peer reading through its mapping right
     // after the rendezvous below would see whatever the memory held before
@@ -1330,7 +1383,7 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     int rc = c->boot.allgather(&mine, all, sizeof(mine));  // also: nobody uses the old one now
     if (c->land) hip_ignore(hipFree(c->land));  // peers' mappings keep it alive until they close them
     c->land = nullptr;
-    c->land_bytes = 0;
+    c->land_bytes = c->land_planned = 0;
     if (rc != OMPI_AMD_SUCCESS) {
         close_old();
         if (fresh) hip_ignore(hipFree(fresh));
@@ -1395,7 +1448,7 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
         c->land = fresh;
         for (int p = 0; p < c->size; ++p)
             c->peer_land.p[p] = p == c->rank ? c->land : (const char *)ipc_ref_base(c->land_ref[p]);
-        c->land_bytes = want - kTag;
+        c->land_bytes = c->land_planned = want - kTag;
         return OMPI_AMD_SUCCESS;
     }
     (void)c->boot.barrier();  // nobody reads the new buffers any more
@@ -1408,6 +1461,163 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
         record_msg("landing buffer growth failed on another rank (%s)",
                    worst == 2 ? "stale IPC mapping" : "HIP error");
     return rc != OMPI_AMD_SUCCESS ? rc : OMPI_AMD_ERR_HIP;
+}
+
+// ---- deferred landing growth (nonblocking calls) ----
+// A nonblocking call that needs a bigger landing buffer cannot grow it at
+// post time: ensure_landing is a rendezvous of the communicator, and MPI
+// lets ranks post different communicators' calls in different orders — two
+// growths posted in opposite orders wait for each other.
+// So the post does only local work: it allocates and stamps this rank's new
+// buffer, posts the descriptor as a ticket and queues a PEND_GROW ahead of
+// the call.  Progress, once the growth is at the queue front and every
+// rank's descriptor is in, maps the peers' new buffers, checks their tokens
+// and switches the communicator over.  Every rank switches at the same queue
+// position, so a call launched before the switch uses the old buffers on
+// every rank; those stay allocated and mapped until the next point where
+// every rank's earlier kernels are known done (free_retired_landing).
+// Nothing here waits for device work of any communicator: the stamp and the
+// check run on a non-blocking stream of their own.
+
+// Post a deferred call's ticket now — or, while the rendezvous ring is full
+// (or earlier tickets still wait), keep the blob for progress to post in
+// queue order: a full ring would otherwise hold the post until peers launch
+// older calls, and they may be held in another communicator's call.
+static int nb_ticket(ompi_amd_comm_t *c, pending_op &o, const void *blob, size_t len) {
+    memcpy(&o.blob, blob, len);
+    o.blob_len = len;
+    if (c->unposted == 0 && c->boot.can_post()) return c->boot.post(blob, len, &o.ticket);
+    o.unposted = true;
+    ++c->unposted;
+    return OMPI_AMD_SUCCESS;
+}
+
+// Post the queued tickets that fit the ring, in queue order; block_front:
+// the queue's front one is posted even if that waits for a ring slot.
+static int post_queued(ompi_amd_comm_t *c, bool block_front) {
+    for (auto &p : c->pending) {
+        if (c->unposted == 0) break;
+        if (!p.unposted) continue;
+        if (!(block_front && &p == &c->pending.front()) && !c->boot.can_post()) break;
+        TRY(c->boot.post(&p.blob, p.blob_len, &p.ticket));
+        p.unposted = false;
+        --c->unposted;
+    }
+    return OMPI_AMD_SUCCESS;
+}
+
+static hipError_t side_stream(ompi_amd_comm_t *c) {
+    if (c->side) return hipSuccess;
+    return hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
+}
+
+// Queue a growth to `need` usable bytes unless the queued ones reach it.
+// Every rank decides alike: the same calls are posted on every rank.
+static int nb_grow(ompi_amd_comm_t *c, size_t need) {
+    if (need <= c->land_planned) return OMPI_AMD_SUCCESS;
+    const size_t want = landing_want(c->land_planned, need);
+    if (want > kMaxIpcBytes) {
+        record_msg("landing buffer of %zu bytes exceeds the %zu-byte IPC mapping limit", want,
+                   kMaxIpcBytes);
+        return OMPI_AMD_ERR_UNSUPPORTED;
+    }
+    land_blob mine{};
+    char *fresh = nullptr;
+    hipError_t e = alloc_exportable(want, &fresh, &mine.d.h);
+    mine.token = landing_token(c->rank);
+    if (e == hipSuccess) land_desc(fresh, want, &mine.d);
+    else record_hip(e, "landing buffer (deferred growth): hipMalloc / hipIpcGetMemHandle");
+    // the stamp has reached the device before the descriptor is published
+    if (e == hipSuccess) e = side_stream(c);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(fresh + want - kLandTag, &mine.token, sizeof(mine.token),
+                           hipMemcpyHostToDevice, c->side);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->side);
+    if (e != hipSuccess && mine.d.valid) record_hip(e, "landing token write");
+    mine.ok = e == hipSuccess;  // a failure is posted too: every rank fails the growth alike
+    pending_op g{};
+    g.kind = PEND_GROW;
+    g.grow = fresh;
+    g.grow_bytes = want;
+    g.grow_token = mine.token;
+    const int rc = nb_ticket(c, g, &mine, sizeof(mine));
+    if (rc != OMPI_AMD_SUCCESS) {
+        if (fresh) hip_ignore(hipFree(fresh));
+        return rc;
+    }
+    c->pending.push_back(g);
+    c->npending.fetch_add(1);
+    c->land_planned = want - kLandTag;
+    return OMPI_AMD_SUCCESS;
+}
+
+// A queued growth at the front of the queue with every rank's descriptor
+// (`all`): map, check the tokens by kernel loads through the new mappings,
+// switch.  On failure nothing after it launches (land_failed): those calls
+// were sized for the new buffers.
+static int grow_launch(ompi_amd_comm_t *c, const pending_op &g, const land_blob *all) {
+    const size_t want = g.grow_bytes;
+    ipc_ref *refs[kMaxRanks] = {};
+    void *maps[kMaxRanks] = {};
+    int status = all[c->rank].ok ? 0 : 1;  // 0 ok, 1 HIP failure somewhere, 2 token mismatch
+    for (int p = 0; p < c->size && status == 0; ++p) {
+        if (p == c->rank) continue;
+        if (!all[p].ok) {
+            record_msg("landing buffer: rank %d failed to allocate or export its buffer", p);
+            status = 1;
+        } else if (ipc_map(alloc_of(all[p].d), c, &refs[p], &maps[p]) != OMPI_AMD_SUCCESS) {
+            status = 1;
+        }
+    }
+    hipError_t e = hipSuccess;
+    if (status == 0 && !c->peek_host) {
+        e = hipHostMalloc((void **)&c->peek_host, kMaxRanks * sizeof(uint64_t), hipHostMallocMapped);
+        if (e != hipSuccess) c->peek_host = nullptr;
+    }
+    uint64_t *peek_dev = nullptr;
+    if (status == 0 && e == hipSuccess) e = hipHostGetDevicePointer((void **)&peek_dev, c->peek_host, 0);
+    if (status == 0 && e == hipSuccess) e = side_stream(c);
+    for (int p = 0; status == 0 && e == hipSuccess && p < c->size; ++p) {
+        if (p == c->rank) continue;
+        c->peek_host[p] = 0;
+        hipLaunchKernelGGL(peek_kernel, dim3(1), dim3(1), 0, c->side,
+                           (const uint64_t *)((char *)maps[p] + want - kLandTag), peek_dev + p);
+        e = hipGetLastError();
+    }
+    if (status == 0 && e == hipSuccess) e = hipStreamSynchronize(c->side);
+    if (status == 0 && e != hipSuccess) {
+        record_hip(e, "landing token check (deferred growth)");
+        status = 1;
+    }
+    for (int p = 0; status == 0 && p < c->size; ++p) {
+        if (p == c->rank) continue;
+        const uint64_t seen = __atomic_load_n(&c->peek_host[p], __ATOMIC_ACQUIRE);
+        if (seen != all[p].token) {
+            record_msg("landing buffer of rank %d (id %llu): the IPC mapping %p shows token "
+                       "%016llx, expected %016llx (deferred growth)", p,
+                       (unsigned long long)all[p].d.id, maps[p], (unsigned long long)seen,
+                       (unsigned long long)all[p].token);
+            status = 2;
+        }
+    }
+    for (int q = 0; q < c->size; ++q) c->land_tokens.push_back(all[q].token);
+    if (status != 0) {
+        for (int p = 0; p < kMaxRanks; ++p) ipc_unmap(refs[p], c);
+        if (g.grow) c->land_retired.push_back(g.grow);  // peers may have mapped it
+        c->land_failed = true;
+        return OMPI_AMD_ERR_HIP;
+    }
+    if (c->land) c->land_retired.push_back(c->land);
+    for (int p = 0; p < kMaxRanks; ++p) {
+        if (c->land_ref[p]) c->land_ref_retired.push_back(c->land_ref[p]);
+        c->land_ref[p] = refs[p];
+    }
+    c->land = g.grow;
+    for (int p = 0; p < c->size; ++p)
+        c->peer_land.p[p] = p == c->rank ? c->land : (const char *)ipc_ref_base(c->land_ref[p]);
+    c->land_bytes = want - kLandTag;
+    ++c->deferred_growths;
+    return OMPI_AMD_SUCCESS;
 }
 
 static int launch_barrier(ompi_amd_comm_t *c, hipStream_t s) {
@@ -2628,6 +2838,40 @@ static void req_event_put(ompi_amd_comm_t *c, hipEvent_t ev) {
 
 static int progress(ompi_amd_comm_t *c, bool block, int max_launch) {
     while (!c->pending.empty() && max_launch-- != 0) {
+        if (c->unposted) {  // tickets the full ring held back (nb_ticket)
+            TRY(post_queued(c, block && c->pending.front().unposted));
+            if (c->pending.front().unposted) return OMPI_AMD_SUCCESS;
+        }
+        if (c->land_failed) {
+            // a deferred growth failed (every peer was told: abort_peers):
+            // the calls behind it were sized for the buffers it would have
+            // made, so they complete with the error, unlaunched
+            pending_op o = c->pending.front();
+            c->pending.pop_front();
+            c->npending.fetch_sub(1);
+            if (o.grow) c->land_retired.push_back(o.grow);
+            if (o.req) {
+                o.req->rc = OMPI_AMD_ERR_HIP;
+                o.req->launched = true;
+            }
+            continue;
+        }
+        if (c->pending.front().kind == PEND_GROW) {
+            const pending_op g = c->pending.front();
+            land_blob lall[kMaxRanks];
+            bool ready = false;
+            int rc = c->boot.test(g.ticket, lall, sizeof(land_blob), block, &ready);
+            if (rc == OMPI_AMD_SUCCESS && !ready) return OMPI_AMD_SUCCESS;
+            c->pending.pop_front();
+            c->npending.fetch_sub(1);
+            if (rc == OMPI_AMD_SUCCESS) rc = grow_launch(c, g, lall);
+            else c->land_failed = true;
+            if (rc != OMPI_AMD_SUCCESS) {
+                abort_peers(c, rc);
+                return rc;
+            }
+            continue;
+        }
         pending_op o = c->pending.front();
         call_blob all[kMaxRanks];
         int rc = OMPI_AMD_SUCCESS;
@@ -2704,6 +2948,16 @@ static int progress(ompi_amd_comm_t *c, bool block, int max_launch) {
         }
     }
     return OMPI_AMD_SUCCESS;
+}
+
+// After a nonblocking post: launch what is ready, here and on the other
+// communicators (any call into the library progresses them all, as
+// opal_progress does: a peer's kernels of another communicator may be
+// waiting for this rank's launch of them).
+static int post_progress(ompi_amd_comm_t *c) {
+    const int rc = progress(c, false);
+    progress_others();
+    return rc;
 }
 
 static int drain(ompi_amd_comm_t *c) {
@@ -2923,6 +3177,8 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     { std::lock_guard<std::recursive_mutex> w(c->api_mu); }  // (and none is still in it)
     hip_ignore(hipSetDevice(c->device));
     (void)drain(c);  // deferred nonblocking calls every peer will also launch
+    for (auto &o : c->pending)  // left by a failed drain: queued growths' buffers
+        if (o.grow) c->land_retired.push_back(o.grow);
     (void)quiesce(c);
     (void)c->boot.barrier();  // nobody still reads our memory
     ipc_remove_user(c);
@@ -2934,11 +3190,16 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
         ipc_unmap(c->land_ref[p], c);
         c->land_ref[p] = nullptr;
     }
+    for (ipc_ref *r : c->land_ref_retired) ipc_unmap(r, c);
+    c->land_ref_retired.clear();
     (void)c->boot.barrier();
     if (c->osc_release) c->osc_release(c->osc_state, 1);  // its own memory
     if (c->flags) hip_ignore(hipFree(c->flags));
     if (c->scratch) hip_ignore(hipFree(c->scratch));
     if (c->land) hip_ignore(hipFree(c->land));
+    for (char *q : c->land_retired) hip_ignore(hipFree(q));
+    c->land_retired.clear();
+    if (c->peek_host) hip_ignore(hipHostFree(c->peek_host));
     for (auto &ch : c->arena) hip_ignore(hipFree(ch.base));  // shadows included
     c->arena.clear();
     if (c->err_host) hip_ignore(hipHostFree(c->err_host));
@@ -2958,6 +3219,7 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     c->boot.detach();
     forget_streams(c);
     if (c->own) hip_ignore(hipStreamDestroy(c->own));  // drained above
+    if (c->side) hip_ignore(hipStreamDestroy(c->side));
     delete c;
     return OMPI_AMD_SUCCESS;
 }
@@ -3211,6 +3473,8 @@ int ompi_amd_comm_get_param(const ompi_amd_comm_t *c, const char *key, int64_t *
     else if (!strcmp(key, "tuned_reduce_scatter_algorithm")) *v = c->tuned_rs_alg;
     else if (!strcmp(key, "tuned_reduce_scatter_block_algorithm")) *v = c->tuned_rsb_alg;
     else if (!strcmp(key, "landing_bytes")) *v = (int64_t)c->land_bytes;
+    else if (!strcmp(key, "landing_deferred_growths")) *v = c->deferred_growths;
+    else if (!strcmp(key, "landing_retired")) *v = (int64_t)c->land_retired.size();
     else if (!strcmp(key, "boot_calls")) *v = (int64_t)c->boot.posted();
     else if (!strcmp(key, "ipc_opens")) *v = ipc_get_stats().opens;
     else if (!strcmp(key, "ipc_refusals")) *v = ipc_get_stats().refusals;
@@ -3361,50 +3625,21 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
             return rc;
         }
     }
-    if (c->own_stream && allreduce_push_gathers(c, pp, count, type) &&
-        staged_push_landing(c->size, pp.algorithm, (int64_t)count, type, nullptr) > c->land_bytes) {
-        // growing the landing buffer is a blocking host rendezvous of this
-        // communicator; MPI lets ranks post different communicators'
-        // nonblocking calls in different orders, and two such growths
-        // posted in opposite orders wait for each other.  The staged pull
-        // instead: its handle swap is split (post now, launch from progress)
-        // and it needs no landing buffer.  Every rank decides alike (the
-        // landing size is the same everywhere).
-        pp.algorithm = ALG_PULL;
-        pp.push_gather = 0;
-        pp.blocks = 0;
-    }
     pending_op o{0, inplace ? rbuf : sbuf, rbuf, count, type, op, comm_stream(c, stream), pp, req};
     if (allreduce_push_gathers(c, pp, count, type)) {
-        // no swap: only the landing buffer must be big enough before the
-        // launch (growing is collective and blocking: every rank here alike)
-        const size_t need = staged_push_landing(c->size, pp.algorithm, (int64_t)count, type, nullptr);
-        if (need > c->land_bytes) {
-            rc = drain(c);
-            if (rc == OMPI_AMD_SUCCESS) rc = ensure_landing(c, need);
-            if (rc != OMPI_AMD_SUCCESS) {
-                req_event_put(req->c, req->ev);
-                delete req;
-                return rc;
-            }
+        // no swap: only the landing buffer must be big enough at the launch
+        // (a growth queued ahead of this call: nb_grow)
+        rc = nb_grow(c, staged_push_landing(c->size, pp.algorithm, (int64_t)count, type, nullptr));
+        if (rc != OMPI_AMD_SUCCESS) {
+            req_event_put(req->c, req->ev);
+            delete req;
+            return rc;
         }
     } else if (allreduce_swaps(c, pp, count, type)) {
         // post this rank's half of the handle swap now; the launch waits for
         // the peers' halves (progress / the next collective call)
         const bool push = is_push(pp.algorithm);
-        if (push) {
-            const size_t need = push_slot((int64_t)count, c->size, type) * (size_t)c->size;
-            if (need > c->land_bytes) {  // collective growth: every rank decides alike
-                rc = drain(c);
-                if (rc == OMPI_AMD_SUCCESS) rc = ensure_landing(c, need);
-            }
-        }
-        // this rank's own posted-but-unlaunched tickets occupy ring slots a
-        // new post would overwrite (ShmBoot::kRing): launch the oldest
-        // deferred calls first (blocking on their peers' posts, which those
-        // peers make before this one)
-        while (rc == OMPI_AMD_SUCCESS && c->boot.posted() - c->boot.consumed() >= ShmBoot::kRing - 1)
-            rc = progress(c, true, 1);
+        if (push) rc = nb_grow(c, push_slot((int64_t)count, c->size, type) * (size_t)c->size);
         // export fallback with memory of its own (several calls may be
         // outstanding): the posted descriptors are the shadows'
         const size_t bytes = count * ompi_amd_type_extent(type);
@@ -3421,7 +3656,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
         call_blob mine{};
         if (rc == OMPI_AMD_SUCCESS && !push) rc = export_buf(c, o.sbuf, &mine.s);
         if (rc == OMPI_AMD_SUCCESS) rc = export_buf(c, o.rbuf, &mine.r);
-        if (rc == OMPI_AMD_SUCCESS) rc = c->boot.post(&mine, sizeof(mine), &o.ticket);
+        if (rc == OMPI_AMD_SUCCESS) rc = nb_ticket(c, o, &mine, sizeof(mine));
         if (rc != OMPI_AMD_SUCCESS) {
             req_event_put(req->c, req->ev);
             arena_free(c, req->shadow);
@@ -3433,7 +3668,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
     c->pending.push_back(o);
     c->npending.fetch_add(1);
     *out = req;
-    return progress(c, false);
+    return post_progress(c);
 }
 
 // ---- nonblocking reduce_scatter_block / allgather / bcast ----
@@ -3464,8 +3699,6 @@ static int nb_post(ompi_amd_comm_t *c, pending_op &o, const void **exp, size_t b
     int rc = OMPI_AMD_SUCCESS;
     ompi_amd_request *req = o.req;
     if (exp) {
-        while (rc == OMPI_AMD_SUCCESS && c->boot.posted() - c->boot.consumed() >= ShmBoot::kRing - 1)
-            rc = progress(c, true, 1);
         void *none = nullptr;
         const int saved = c->force_shadow;
         if (force) c->force_shadow = 1;
@@ -3475,7 +3708,7 @@ static int nb_post(ompi_amd_comm_t *c, pending_op &o, const void **exp, size_t b
         req->shadow2 = o.sh.mem2;
         call_blob mine{};
         if (rc == OMPI_AMD_SUCCESS) rc = export_buf(c, *exp, &mine.s);
-        if (rc == OMPI_AMD_SUCCESS) rc = c->boot.post(&mine, sizeof(mine), &o.ticket);
+        if (rc == OMPI_AMD_SUCCESS) rc = nb_ticket(c, o, &mine, sizeof(mine));
     }
     if (rc != OMPI_AMD_SUCCESS) {
         req_event_put(req->c, req->ev);
@@ -3487,7 +3720,7 @@ static int nb_post(ompi_amd_comm_t *c, pending_op &o, const void **exp, size_t b
     c->pending.push_back(o);
     c->npending.fetch_add(1);
     *out = req;
-    return progress(c, false);
+    return post_progress(c);
 }
 
 static bool nb_swaps(const ompi_amd_comm_t *c, size_t bytes) {
@@ -3498,11 +3731,7 @@ static bool nb_swaps(const ompi_amd_comm_t *c, size_t bytes) {
 // and blocking: every rank posts the same call alike); on failure the
 // request is released.
 static int nb_grow_landing(ompi_amd_comm_t *c, size_t need, ompi_amd_request *req) {
-    int rc = OMPI_AMD_SUCCESS;
-    if (need > c->land_bytes) {
-        rc = drain(c);
-        if (rc == OMPI_AMD_SUCCESS) rc = ensure_landing(c, need);
-    }
+    const int rc = nb_grow(c, need);
     if (rc != OMPI_AMD_SUCCESS) {
         req_event_put(req->c, req->ev);
         delete req;
@@ -3528,16 +3757,7 @@ int ompi_amd_ireduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *r
         // launch; only the landing buffer must be big enough beforehand
         // (its growth is collective: every rank posts this call alike)
         const size_t slot = (rcount * ompi_amd_type_extent(type) + 16 + 255) & ~(size_t)255;
-        int rc = OMPI_AMD_SUCCESS;
-        if (slot * (size_t)(c->size + 1) > c->land_bytes) {
-            rc = drain(c);
-            if (rc == OMPI_AMD_SUCCESS) rc = ensure_landing(c, slot * (size_t)(c->size + 1));
-        }
-        if (rc != OMPI_AMD_SUCCESS) {
-            req_event_put(req->c, req->ev);
-            delete req;
-            return rc;
-        }
+        TRY(nb_grow_landing(c, slot * (size_t)(c->size + 1), req));
         o.inplace = inplace;
         return nb_post(c, o, nullptr, 0, false, out);
     }
@@ -3604,18 +3824,6 @@ int ompi_amd_ibcast(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, void 
 // ireduce posts one ticket carrying the root's MPI_IN_PLACE flag (it
 // changes the root's first combine, coll_base_reduce.c:170-171), so no
 // rank waits for a peer at post time.
-static int nb_landing(ompi_amd_comm_t *c, size_t need, ompi_amd_request *req) {
-    int rc = OMPI_AMD_SUCCESS;
-    if (need > c->land_bytes) {
-        rc = drain(c);
-        if (rc == OMPI_AMD_SUCCESS) rc = ensure_landing(c, need);
-    }
-    if (rc != OMPI_AMD_SUCCESS) {
-        req_event_put(req->c, req->ev);
-        delete req;
-    }
-    return rc;
-}
 
 int ompi_amd_ireduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
                      int op, int root, void *stream, ompi_amd_request_t **out) {
@@ -3635,15 +3843,12 @@ int ompi_amd_ireduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t co
         int64_t split, early, late;
         blockcount((int64_t)count, n, &split, &early, &late);
         const size_t slot = ((size_t)early * ompi_amd_type_extent(type) + 16 + 255) & ~(size_t)255;
-        TRY(nb_landing(c, slot * (size_t)n + ((bytes + 255) & ~(size_t)255), req));
+        TRY(nb_grow_landing(c, slot * (size_t)n + ((bytes + 255) & ~(size_t)255), req));
     }
     if (n == 1 || count == 0) return nb_post(c, o, nullptr, 0, false, out);
-    int rc = OMPI_AMD_SUCCESS;
-    while (rc == OMPI_AMD_SUCCESS && c->boot.posted() - c->boot.consumed() >= ShmBoot::kRing - 1)
-        rc = progress(c, true, 1);
     call_blob mine{};
     mine.flags = (c->rank == root && in_place(sbuf, rbuf)) ? 1 : 0;
-    if (rc == OMPI_AMD_SUCCESS) rc = c->boot.post(&mine, sizeof(mine), &o.ticket);
+    const int rc = nb_ticket(c, o, &mine, sizeof(mine));
     if (rc != OMPI_AMD_SUCCESS) {
         req_event_put(req->c, req->ev);
         delete req;
@@ -3652,7 +3857,7 @@ int ompi_amd_ireduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t co
     c->pending.push_back(o);
     c->npending.fetch_add(1);
     *out = req;
-    return progress(c, false);
+    return post_progress(c);
 }
 
 static int iscan_common(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t count, int type,
@@ -3667,7 +3872,7 @@ static int iscan_common(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
     o.kind = PEND_SCAN;
     o.exclusive = exclusive;
     if (c->size > 1 && count > 0 && bytes > c->small_bytes && c->zero_copy)
-        TRY(nb_landing(c, bytes + 256, req));
+        TRY(nb_grow_landing(c, bytes + 256, req));
     return nb_post(c, o, nullptr, 0, false, out);
 }
 
@@ -3703,7 +3908,7 @@ int ompi_amd_ireduce_scatter(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
     }
     if (c->size > 1 && total * ext > c->small_bytes && c->zero_copy) {  // reduce_my_block's staged push
         const size_t slot = (maxc * ext + 16 + 255) & ~(size_t)255;
-        TRY(nb_landing(c, slot * (size_t)(c->size + 1), req));
+        TRY(nb_grow_landing(c, slot * (size_t)(c->size + 1), req));
     }
     return nb_post(c, o, nullptr, 0, false, out);
 }

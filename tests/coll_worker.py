@@ -7,6 +7,7 @@ and checks the result against the CPU oracle, which each rank evaluates for
 all ranks from the deterministic per-rank inputs.  Prints one JSON line per
 case and exits 0 only if all passed.
 """
+import functools
 import json
 import os
 import sys
@@ -865,6 +866,191 @@ def case_cross_comm_order(comm, rank, n, salt, stream_per_comm=False, own=False)
     return not msgs, "; ".join(msgs[:3])
 
 
+def case_cross_comm_grow(comm, rank, n, salt, nring=12):
+    """Two fresh communicators (coll/rocm's own_stream), even ranks posting
+    A's calls before B's and odd ranks B's before A's, then waiting in the
+    opposite order: (1) nonblocking calls whose landing buffer must grow —
+    ireduce_scatter_block, iscan, ireduce, iallgather, ibcast past the
+    staged size — each growth queued at post and completed from progress
+    (a growth at post time is a rendezvous, and two posted
+    in opposite orders wait for each other); (2) `nring` ireduces per
+    communicator, more tickets than the rendezvous ring holds (a full ring
+    queues the rest for progress instead of waiting at the post)."""
+    F, I32 = mop.MPI_FLOAT, mop.MPI_INT32_T
+    SUM, MAX = mop.MPI_SUM, mop.MPI_MAX
+    comms = []
+    for _ in range(2):
+        cc = coll.Communicator.from_torch_distributed(device=comm.device)
+        cc.set_param("timeout_ms", 20000)
+        cc.set_param("own_stream", 1)
+        comms.append(cc)
+    msgs = []
+
+    def prep(ci, kind, count, dt, op, root, sl):
+        # inputs, expected results and buffers made before anything is
+        # posted: the posts then follow each other at once (a rank busy on
+        # the host between posts leaves a peer's launched kernels waiting)
+        cc = comms[ci]
+        xs = [inputs(dt, count * (n if kind == "rsb" else 1), r, sl) for r in range(n)]
+        s = to_dev(xs[rank])
+        what = f"comm {ci} {kind} {count} {dt.name}"
+        if kind == "rsb":
+            exp = orc.reduce_scatter_block([x.copy() for x in xs], count, op.index, dt.code)
+            o = torch.zeros(count * dt.extent, dtype=torch.uint8, device="cuda")
+            return (lambda: cc.ireduce_scatter_block(s, o, count, dt, op)), o, exp[rank].view(xs[0].dtype), s, what
+        if kind == "scan":
+            exp = orc.scan([x.copy() for x in xs], count, op.index, dt.code, False)
+            o = torch.zeros_like(s)
+            return (lambda: cc.iscan(s, o, count, dt, op)), o, exp[rank], s, what
+        if kind == "red":
+            exp, _ = orc.reduce([x.copy() for x in xs], count, op.index, dt.code, root, False)
+            o = torch.zeros_like(s) if rank == root else None
+            return (lambda: cc.ireduce(s, o, count, dt, op, root)), o, (exp if rank == root else None), s, what
+        if kind == "ag":
+            o = torch.zeros(n * count * dt.extent, dtype=torch.uint8, device="cuda")
+            return (lambda: cc.iallgather(s, o, count * dt.extent)), o, np.concatenate(xs), s, what
+        o = s if rank == root else torch.zeros_like(s)
+        return (lambda: cc.ibcast(o, count * dt.extent, root)), o, xs[root], s, what
+
+    def post(prepared):
+        torch.cuda.synchronize()  # MPI semantics: the buffers are ready at the call
+        return [(go(), o, want, s_, what) for go, o, want, s_, what in prepared]
+
+    def finish(posted, tag):
+        for p in reversed(posted):
+            p[0].wait()
+        torch.cuda.synchronize()
+        for r_, o, want, _, what in posted:
+            r_.free()
+            if want is None:
+                continue
+            got = o.cpu().numpy().view(np.uint8)[:want.nbytes].view(want.dtype)
+            ok, msg = checked(got, want)
+            if not ok:
+                msgs.append(f"{tag} {what}: {msg}")
+
+    try:
+        plan = [("rsb", 300001, F, SUM, 0), ("scan", 400001, I32, MAX, 0),
+                ("red", 700001, F, SUM, n - 1), ("ag", 500001, I32, MAX, 0),
+                ("bc", 900001, F, SUM, n // 2)]
+        order = [(ci, j) for ci in ((0, 1) if rank % 2 == 0 else (1, 0)) for j in range(len(plan))]
+        posted = post([prep(ci, *plan[j], salt + 10 * ci + j) for ci, j in order])
+        finish(posted, "growth")
+        grows = [cc.get_param("landing_deferred_growths") for cc in comms]
+        if n > 1 and min(grows) < 1:
+            msgs.append(f"no deferred landing growth taken: {grows}")
+        order = [(ci, j) for ci in ((0, 1) if rank % 2 == 0 else (1, 0)) for j in range(nring)]
+        posted = post([prep(ci, "red", 777 + j, F, SUM, j % n, salt + 100 + 10 * ci + j)
+                       for ci, j in order])
+        finish(posted, "ring")
+        for cc in comms:
+            if cc.error():
+                msgs.append(f"device error {cc.error()}")
+    finally:
+        for cc in comms:
+            cc.free()
+    return not msgs, "; ".join(msgs[:3])
+
+
+def case_cross_comm_random(comm, rank, n, salt, ncomm=3, per_comm=6):
+    """Randomized MPI-path ordering (coll/rocm's own_stream): three
+    communicators over the same ranks, each with a sequence of nonblocking
+    collectives drawn from one seed (the same on every rank: MPI orders a
+    communicator's collectives) — iallreduce (up to past the zero-copy
+    threshold), ireduce_scatter_block, iallgather, ibcast, ireduce, iscan
+    below it — and every rank interleaving the three sequences in its OWN
+    random order (legal: MPI orders nothing across communicators), then
+    waiting for the requests in its own random order. Every result checked
+    against the oracle; a device wait of one communicator queued in front
+    of another's kernels would time out here."""
+    F, I32 = mop.MPI_FLOAT, mop.MPI_INT32_T
+    SUM, MAX = mop.MPI_SUM, mop.MPI_MAX
+    plan_rng = np.random.default_rng(SEED + salt)
+    comms = []
+    for _ in range(ncomm):
+        cc = coll.Communicator.from_torch_distributed(device=comm.device)
+        cc.set_param("timeout_ms", 20000)
+        cc.set_param("own_stream", 1)
+        comms.append(cc)
+    seqs = []
+    for ci in range(ncomm):
+        seq = []
+        for j in range(per_comm):
+            kind = ["ar", "ar", "rsb", "ag", "bc", "red", "scan"][int(plan_rng.integers(7))]
+            count = int(plan_rng.choice([1, 777, 20000, 200001, 700001 if kind == "ar" else 60001]))
+            dt, op = (F, SUM) if plan_rng.integers(2) else (I32, MAX)
+            root = int(plan_rng.integers(n))
+            seq.append((kind, count, dt, op, root, salt + 10 * ci + j))
+        seqs.append(seq)
+    mine = np.random.default_rng(SEED + salt + 1000 * (rank + 1))
+    order = [ci for ci in range(ncomm) for _ in range(per_comm)]
+    mine.shuffle(order)  # this rank's interleaving of the communicators' sequences
+    nxt = [0] * ncomm
+    prepared, posted, msgs = [], [], []
+    try:
+        # inputs, expected results and buffers first: the posts then follow
+        # each other at once (a rank busy on the host between posts leaves a
+        # peer's launched kernels waiting for it, up to the device timeout)
+        for ci in order:
+            kind, count, dt, op, root, sl = seqs[ci][nxt[ci]]
+            nxt[ci] += 1
+            cc = comms[ci]
+            xs = [inputs(dt, count * (n if kind == "rsb" else 1), r, sl) for r in range(n)]
+            s = to_dev(xs[rank])
+            if kind == "ar":
+                exp, _ = orc.allreduce([x.copy() for x in xs], count, op.index, dt.code)
+                o = torch.zeros_like(s)
+                go = functools.partial(cc.iallreduce, s, o, count, dt, op)
+                want = exp[rank]
+            elif kind == "rsb":
+                exp = orc.reduce_scatter_block([x.copy() for x in xs], count, op.index, dt.code)
+                o = torch.zeros(count * dt.extent, dtype=torch.uint8, device="cuda")
+                go = functools.partial(cc.ireduce_scatter_block, s, o, count, dt, op)
+                want = exp[rank].view(xs[0].dtype)
+            elif kind == "ag":
+                o = torch.zeros(n * count * dt.extent, dtype=torch.uint8, device="cuda")
+                go = functools.partial(cc.iallgather, s, o, count * dt.extent)
+                want = np.concatenate(xs)
+            elif kind == "bc":
+                o = s if rank == root else torch.zeros_like(s)
+                go = functools.partial(cc.ibcast, o, count * dt.extent, root)
+                want = xs[root]
+            elif kind == "red":
+                exp, _ = orc.reduce([x.copy() for x in xs], count, op.index, dt.code, root, False)
+                o = torch.zeros_like(s) if rank == root else None
+                go = functools.partial(cc.ireduce, s, o, count, dt, op, root)
+                want = exp if rank == root else None
+            else:
+                exp = orc.scan([x.copy() for x in xs], count, op.index, dt.code, False)
+                o = torch.zeros_like(s)
+                go = functools.partial(cc.iscan, s, o, count, dt, op)
+                want = exp[rank]
+            prepared.append((go, o, want, s, f"comm {ci} {kind} {count} {dt.name}"))
+        torch.cuda.synchronize()  # MPI semantics: the buffers are ready at the call
+        for go, o, want, s, what in prepared:
+            posted.append((go(), o, want, what))
+        wait_order = list(range(len(posted)))
+        mine.shuffle(wait_order)
+        for i in wait_order:
+            posted[i][0].wait()
+        torch.cuda.synchronize()
+        for r_, o, want, what in posted:
+            r_.free()
+            if want is None:
+                continue
+            got = o.cpu().numpy().view(np.uint8)[:want.nbytes].view(want.dtype)
+            ok, msg = checked(got, want)
+            if not ok:
+                msgs.append(f"{what}: {msg}")
+        for cc in comms:
+            if cc.error():
+                msgs.append(f"device error {cc.error()}")
+    finally:
+        for cc in comms:
+            cc.free()
+    return not msgs, "; ".join(msgs[:3])
+
+
 def case_small_marks_two_streams(comm, rank, n, salt, rounds=6):
     """Small allreduces whose fused kernels store their own completion marks
     (blocking, nonblocking and persistent: one flag-page counter slot per
@@ -1613,7 +1799,10 @@ def main():
     # the MPI path (coll/rocm's own_stream): opposite-order nonblocking and
     # persistent calls on two communicators complete
     if not os.environ.get("COLL_HEADLINE"):
-        cases += [("cross_comm_order_own_stream", lambda: case_cross_comm_order(comm, rank, n, 192, own=True))]
+        cases += [("cross_comm_order_own_stream", lambda: case_cross_comm_order(comm, rank, n, 192, own=True)),
+                  ("cross_comm_grow_own_stream", lambda: case_cross_comm_grow(comm, rank, n, 195)),
+                  ("cross_comm_random_own_stream", lambda: case_cross_comm_random(comm, rank, n, 193)),
+                  ("cross_comm_random_own_stream_b", lambda: case_cross_comm_random(comm, rank, n, 194))]
     if only and "cross_comm" in only:
         # opt-in: the known limitation of DESIGN.md §8 item 9 (device-side
         # waits across communicators posted in opposite orders time out)

@@ -280,6 +280,20 @@ int main(int argc, char **argv)
                   "derived get into a gapped origin");
             CHECK(m->osc_fence(0, &win) == OMPI_SUCCESS, "fence derived get");
             CHECK(harness_dev_copy_back(back, dgot, 2 * kk * 4) == 0, "copy back derived get");
+            {  /* which slots, and what they hold (pattern: never written; origin: the put) */
+                size_t bad = 0, first = kk, last = 0, as_pat = 0;
+                for (j = 0; j < kk; ++j)
+                    if (0 != memcmp(&back[2 * j], &org[j], 4)) {
+                        ++bad;
+                        if (first == kk) first = j;
+                        last = j;
+                        as_pat += 0 == memcmp(&back[2 * j], &pat[2 * j], 4);
+                    }
+                if (bad)
+                    fprintf(stderr, "rank %d: derived get: %zu of %zu slots wrong [%zu, %zu], %zu still "
+                            "the pattern; slot %zu holds %g, expected %g\n", g_rank, bad, kk, first,
+                            last, as_pat, first, back[2 * first], org[first]);
+            }
             for (j = 0; j < kk; ++j) {
                 CHECK(0 == memcmp(&back[2 * j], &org[j], 4), "derived get slot %zu", j);
                 CHECK(0 == memcmp(&back[2 * j + 1], &pat[2 * j + 1], 4), "derived get gap %zu", j);
