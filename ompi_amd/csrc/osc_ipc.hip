@@ -847,6 +847,12 @@ struct ompi_amd_win {
         void *pin;
     };
     std::vector<dyn_map> dyn_maps;
+    // packed-stream scratch of the derived-datatype calls (osc_scratch)
+    char *scr[2] = {};
+    size_t scr_cap[2] = {};
+    std::vector<char *> scr_old;  // buffers a growth replaced (kernels may still read them)
+    hipEvent_t scr_ev = nullptr;  // after the last call's use, on scr_last
+    hipStream_t scr_last = nullptr;
 };
 
 #define OSC_TRY(x)                               \
@@ -854,6 +860,44 @@ struct ompi_amd_win {
         int rc_ = (x);                           \
         if (rc_ != OMPI_AMD_SUCCESS) return rc_; \
     } while (0)
+
+// Scratch of a derived-datatype call (the origin's packed stream, the
+// fetched result stream): two regions kept for the window's life and grown
+// geometrically, ordered between calls by stream order — a call on another
+// stream than the previous user's first waits for that use (an event).
+// Not the stream-ordered pool (hipMallocAsync / hipFreeAsync): with it, a
+// derived get at N = 3 on one GPU intermittently unpacked zeros for part of
+// the fetched stream (1 of 12 repeats, 4 of 12 with a one-workgroup fetch);
+// with this scratch 0 of 48 (tools/osc_flake_probe.sh).
+static int osc_scratch(ompi_amd_win_t *w, hipStream_t s, int slot, size_t bytes, void **out) {
+    *out = nullptr;
+    if (w->scr_last && w->scr_last != s && w->scr_ev)
+        OSC_TRY(record_hip(hipStreamWaitEvent(s, w->scr_ev, 0), "hipStreamWaitEvent (osc scratch)"));
+    w->scr_last = nullptr;  // until osc_scratch_done records this call's use
+    if (bytes > w->scr_cap[slot]) {
+        const size_t want = std::max(bytes, 2 * w->scr_cap[slot]);
+        char *p = nullptr;
+        OSC_TRY(record_hip(hipMalloc(&p, want), "hipMalloc (osc scratch)"));
+        if (w->scr[slot]) w->scr_old.push_back(w->scr[slot]);
+        w->scr[slot] = p;
+        w->scr_cap[slot] = want;
+    }
+    *out = w->scr[slot];
+    return OMPI_AMD_SUCCESS;
+}
+
+static void osc_scratch_done(ompi_amd_win_t *w, hipStream_t s) {
+    if (!w->scr_ev && hipEventCreateWithFlags(&w->scr_ev, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        w->scr_ev = nullptr;
+    }
+    if (w->scr_ev && hipEventRecord(w->scr_ev, s) == hipSuccess) {
+        w->scr_last = s;
+    } else {
+        (void)hipGetLastError();
+        hip_ignore(hipStreamSynchronize(s));  // no event: the next user must not overtake this one
+    }
+}
 
 // ---- dynamic windows (MPI_Win_create_dynamic / _attach / _detach;
 // osc/rdma's region table, osc_rdma_dynamic.c:162-300, in host shared
@@ -1686,6 +1730,9 @@ int ompi_amd_win_free(ompi_amd_win_t *w) {
     if (w->owns_base && w->base) hip_ignore(hipFree(w->base));
     if (w->arena_base && w->base) comm_arena_free(c, w->base);  // nobody maps it per window
     win_release_shadow(w);  // no peer maps the public copy any more
+    for (char *q : w->scr) if (q) hip_ignore(hipFree(q));  // the streams were synchronised above
+    for (char *q : w->scr_old) hip_ignore(hipFree(q));
+    if (w->scr_ev) hip_ignore(hipEventDestroy(w->scr_ev));
     if (rc == OMPI_AMD_SUCCESS) rc = comm_sticky(c);
     delete w;
     return rc;
@@ -1825,8 +1872,7 @@ int ompi_amd_get_accumulate(ompi_amd_win_t *w, const void *origin, void *result,
 // the old elements packed (get_accumulate) and combining the packed origin
 // into them; a non-contiguous result is unpacked from the fetched stream
 // afterwards (local).  Null odt / rdt / tdt: `type` contiguous.  The packed
-// scratch is stream-ordered (hipMallocAsync / hipFreeAsync on the call's
-// stream).
+// streams live in the window's scratch (osc_scratch).
 // acc_ddt for MAXLOC / MINLOC operand types (ddt_pair_kernel above): every
 // side's signature counts packed pairs; a contiguous side (NULL program)
 // holds `count` memory pairs (extent apart), a derived one the packed
@@ -1870,7 +1916,7 @@ static int acc_ddt_pair(ompi_amd_win_t *w, const void *origin, size_t ocount, co
     void *po = nullptr, *pr = nullptr;
     int rc = OMPI_AMD_SUCCESS;
     if (odt && op != OMPI_AMD_OP_NO_OP) {  // the origin's packed pairs (local; before the lock)
-        rc = record_hip(hipMallocAsync(&po, tsig, s), "hipMallocAsync (osc origin pack)");
+        rc = osc_scratch(w, s, 0, tsig, &po);
         size_t done = 0;
         if (rc == OMPI_AMD_SUCCESS) rc = ompi_amd_ddt_pack(odt, ocount, origin, po, 0, tsig, &done, s);
         if (rc == OMPI_AMD_SUCCESS && done != tsig) rc = OMPI_AMD_ERR_BAD_PARAM;
@@ -1878,7 +1924,7 @@ static int acc_ddt_pair(ompi_amd_win_t *w, const void *origin, size_t ocount, co
     }
     if (op == OMPI_AMD_OP_NO_OP) in.p = nullptr;
     if (rc == OMPI_AMD_SUCCESS && fetch && rdt) {
-        rc = record_hip(hipMallocAsync(&pr, tsig, s), "hipMallocAsync (osc result stream)");
+        rc = osc_scratch(w, s, 1, tsig, &pr);
         old = pair_side{static_cast<char *>(pr), P, pk};
     }
     if (rc == OMPI_AMD_SUCCESS) rc = launch_lock(w, target, 0, s);
@@ -1898,8 +1944,7 @@ static int acc_ddt_pair(ompi_amd_win_t *w, const void *origin, size_t ocount, co
         rc = ompi_amd_ddt_unpack(rdt, rcount, pr, result, 0, tsig, &done, s);
         if (rc == OMPI_AMD_SUCCESS && done != tsig) rc = OMPI_AMD_ERR_BAD_PARAM;
     }
-    if (po) hip_ignore(hipFreeAsync(po, s));
-    if (pr) hip_ignore(hipFreeAsync(pr, s));
+    if (po || pr) osc_scratch_done(w, s);
     return rc;
 }
 
@@ -1948,7 +1993,7 @@ static int acc_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount, const o
     void *po = nullptr, *pr = nullptr;
     int rc = OMPI_AMD_SUCCESS;
     if (odt && op != OMPI_AMD_OP_NO_OP) {
-        rc = record_hip(hipMallocAsync(&po, tbytes, s), "hipMallocAsync (osc origin pack)");
+        rc = osc_scratch(w, s, 0, tbytes, &po);
         size_t done = 0;
         if (rc == OMPI_AMD_SUCCESS) rc = ompi_amd_ddt_pack(odt, ocount, origin, po, 0, tbytes, &done, s);
         if (rc == OMPI_AMD_SUCCESS && done != tbytes) rc = OMPI_AMD_ERR_BAD_PARAM;
@@ -1956,7 +2001,7 @@ static int acc_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount, const o
     }
     void *old = result;
     if (rc == OMPI_AMD_SUCCESS && fetch && rdt) {
-        rc = record_hip(hipMallocAsync(&pr, tbytes, s), "hipMallocAsync (osc result stream)");
+        rc = osc_scratch(w, s, 1, tbytes, &pr);
         old = pr;
     }
     if (rc == OMPI_AMD_SUCCESS) rc = launch_lock(w, target, 0, s);
@@ -1992,8 +2037,7 @@ static int acc_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount, const o
         rc = ompi_amd_ddt_unpack(rdt, rcount, pr, result, 0, tbytes, &done, s);
         if (rc == OMPI_AMD_SUCCESS && done != tbytes) rc = OMPI_AMD_ERR_BAD_PARAM;
     }
-    if (po) hip_ignore(hipFreeAsync(po, s));
-    if (pr) hip_ignore(hipFreeAsync(pr, s));
+    if (po || pr) osc_scratch_done(w, s);
     return rc;
 }
 
@@ -2041,7 +2085,7 @@ static int rma_ddt(ompi_amd_win_t *w, void *origin, size_t ocount, const ompi_am
     char *packed = static_cast<char *>(origin);
     void *tmp = nullptr;
     if (odt) {  // the origin's packed stream, local
-        rc = record_hip(hipMallocAsync(&tmp, tbytes, s), "hipMallocAsync (osc origin stream)");
+        rc = osc_scratch(w, s, 0, tbytes, &tmp);
         packed = static_cast<char *>(tmp);
         if (rc == OMPI_AMD_SUCCESS && put) {
             size_t done = 0;
@@ -2073,7 +2117,7 @@ static int rma_ddt(ompi_amd_win_t *w, void *origin, size_t ocount, const ompi_am
         rc = ompi_amd_ddt_unpack(odt, ocount, tmp, origin, 0, tbytes, &done, s);
         if (rc == OMPI_AMD_SUCCESS && done != tbytes) rc = OMPI_AMD_ERR_BAD_PARAM;
     }
-    if (tmp) hip_ignore(hipFreeAsync(tmp, s));
+    if (tmp) osc_scratch_done(w, s);
     return rc;
 }
 

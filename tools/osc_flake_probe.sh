@@ -2,9 +2,9 @@
 # settings; one line per config: passes / failures and the first mismatch.
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/oscflake
-for cfg in "BASE=1" "OMPI_AMD_DDT_TILE=0" "OMPI_AMD_OSC_MAX_BLOCKS=1"; do
+for cfg in ${CFGS:-BASE=1 OMPI_AMD_DDT_TILE=0 OMPI_AMD_OSC_MAX_BLOCKS=1}; do
   ok=0; bad=0; first=""
-  for i in $(seq 1 12); do
+  for i in $(seq 1 ${REPS:-12}); do
     env $cfg timeout -k 10 120 python -u -m pytest -x -q --timeout 100 --timeout-method thread -m gpu \
       tests/test_mca_glue.py -k "osc_component_device_path and 3" > gpurun_out/oscflake/run.log 2>&1
     rc=$?
