@@ -9,6 +9,7 @@ for accumulates, from the CPU oracle's op/base restatement applied in the
 target's order.  One JSON line per case; exit 0 only if all passed.
 """
 import ctypes
+import functools
 import json
 import os
 import sys
@@ -540,6 +541,103 @@ def case_put_get(comm, rank, n, nbytes, salt):
         return eq(host(back), payload(rank, salt, nbytes), "get")
     finally:
         win.free()
+
+
+def case_cross_layer(comm, rank, n, salt, k=4):
+    """MPI's progress rule across layers and communicators, on the MPI path
+    (coll/rocm, pml/rocm and osc/rocm each give a communicator a queue of its
+    own: param own_stream): every rank interleaves, in its OWN random order,
+    nonblocking collectives on communicator A (in A's order on every rank) (iallreduce at the fused,
+    staged and zero-copy sizes, ireduce_scatter_block, iallgather) and a ring
+    of isends / irecvs on communicator B (eager and rendezvous sizes, one tag
+    each); then, with all of that outstanding, a fence epoch of puts on a
+    window of communicator C (blocking, every rank alike); then waits for
+    the requests in its own random order. Every result is checked."""
+    F = mop.MPI_FLOAT
+    nxt, prv = (rank + 1) % n, (rank - 1) % n
+    comms = []
+    for _ in range(3):
+        cc = coll.Communicator.from_torch_distributed(device=comm.device)
+        cc.set_param("timeout_ms", 20000)
+        cc.set_param("own_stream", 1)
+        comms.append(cc)
+    ca, cb, cw = comms
+    mine = np.random.default_rng(SEED + salt + 1000 * (rank + 1))
+    win = None
+    try:
+        posts = []  # (go, check)
+        for i, (kind, count) in enumerate([("ar", 7), ("ar", 70001), ("ar", (1 << 20) + 3),
+                                           ("rsb", 50001), ("ag", 40001)]):
+            xs = [np.random.default_rng(SEED + salt + 31 * i + r).standard_normal(
+                count * (n if kind == "rsb" else 1)).astype(np.float32) for r in range(n)]
+            s = dev(xs[rank])
+            if kind == "ar":
+                exp = orc.allreduce([x.copy() for x in xs], count, mop.MPI_SUM.index, F.code)[0][rank]
+                o = zeros(count * 4)
+                go = functools.partial(ca.iallreduce, s, o, count, F, mop.MPI_SUM)
+            elif kind == "rsb":
+                exp = orc.reduce_scatter_block([x.copy() for x in xs], count, mop.MPI_SUM.index,
+                                               F.code)[rank].view(np.float32)
+                o = zeros(count * 4)
+                go = functools.partial(ca.ireduce_scatter_block, s, o, count, F, mop.MPI_SUM)
+            else:
+                exp = np.concatenate(xs)
+                o = zeros(n * count * 4)
+                go = functools.partial(ca.iallgather, s, o, count * 4)
+            posts.append((go, (o, exp, f"A {kind} {count}"), s))
+        for j in range(k):
+            nb = (17, 4099, (1 << 20) + 5, (8 << 20) + 1)[j % 4]
+            s = dev(payload(rank, salt + 50 + j, nb))
+            r = zeros(nb)
+            posts.append((functools.partial(pml.isend, cb, s, nxt, 900 + j, nb, stream=STREAM), None, s))
+            posts.append((functools.partial(pml.irecv, cb, r, prv, 900 + j, nb, stream=STREAM),
+                          (r, payload(prv, salt + 50 + j, nb), f"B recv {nb}"), r))
+        wbytes = (3 << 20) + 44
+        wbase = zeros(wbytes)
+        win = osc.Window.create(cw, wbase, wbytes)
+        wsrc = dev(payload(rank, salt + 90, wbytes - 40))
+        torch.cuda.synchronize()
+        # this rank's own interleaving of A's calls (in A's order: MPI orders
+        # a communicator's collectives) with B's isends / irecvs (any order:
+        # they match by tag)
+        acalls, bcalls = posts[:5], posts[5:]
+        mine.shuffle(bcalls)
+        lanes = ["A"] * len(acalls) + ["B"] * len(bcalls)
+        mine.shuffle(lanes)
+        ai, bi = iter(acalls), iter(bcalls)
+        posts = [next(ai) if ln == "A" else next(bi) for ln in lanes]
+        reqs = [(go(), chk) for go, chk, _ in posts]
+        win.fence(stream=STREAM)
+        win.put(wsrc, nxt, 40, wbytes - 40, stream=STREAM)
+        win.fence(stream=STREAM, blocking=True)
+        order = list(range(len(reqs)))
+        mine.shuffle(order)
+        for i in order:
+            reqs[i][0].wait()
+        torch.cuda.synchronize()
+        msgs = []
+        for req, chk in reqs:
+            req.free()
+            if chk is None:
+                continue
+            buf, exp, what = chk
+            ok, msg = eq(host(buf)[:exp.nbytes], exp, what)
+            if not ok:
+                msgs.append(msg)
+        want = np.zeros(wbytes, np.uint8)
+        want[40:] = payload(prv, salt + 90, wbytes - 40)
+        ok, msg = eq(host(wbase), want, "C put")
+        if not ok:
+            msgs.append(msg)
+        for cc in comms:
+            if cc.error():
+                msgs.append(f"device error {cc.error()}")
+        return not msgs, "; ".join(msgs[:3])
+    finally:
+        if win is not None:
+            win.free()
+        for cc in comms:
+            cc.free()
 
 
 def case_acc_disjoint(comm, rank, n, dt, op, count, salt, kind="R"):
@@ -1893,6 +1991,7 @@ def main():
         ("osc_dynamic_window", lambda: case_dynamic_window(comm, rank, n, 99)),
         ("osc_shared_window", lambda: case_shared_window(comm, rank, n, 98)),
         ("osc_shared_window_noncontig", lambda: case_shared_window(comm, rank, n, 99, noncontig=True)),
+        ("cross_layer_progress", lambda: case_cross_layer(comm, rank, n, 2100 + STRESS_SEED)),
     ]
     only = os.environ.get("P2P_OSC_ONLY")
     pick = os.environ.get("P2P_OSC_CASES")  # exact names, comma-separated, run in list order
