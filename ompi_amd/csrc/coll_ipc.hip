@@ -65,6 +65,7 @@
 #include <cstring>
 #include <deque>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <utility>
@@ -467,16 +468,14 @@ struct ompi_amd_comm {
     ipc_ref *land_ref[kMaxRanks] = {};   // peers' landing buffers (IPC registry references)
     // Deferred growth (nonblocking calls, PEND_GROW): land_planned is the
     // size once every queued growth has launched — what a post compares
-    // against; the buffers a growth replaced stay alive (and mapped) until
-    // the next point where every rank's earlier kernels are known done
-    // (a blocking growth, destroy): land_retired / land_ref_retired.
+    // against.  The buffers any growth replaced stay allocated (and mapped)
+    // until destroy: land_retired / land_ref_retired (hipFree and IPC
+    // closes may wait for every kernel of the device).
     size_t land_planned = 0;
     std::vector<char *> land_retired;
     std::vector<ipc_ref *> land_ref_retired;
     bool land_failed = false;             // a deferred growth failed: nothing after it launches
     int unposted = 0;                     // pending ops whose ticket waits for a ring slot
-    hipStream_t side = nullptr;           // growth token stamps / checks (non-blocking stream)
-    uint64_t *peek_host = nullptr;        //   and where the check's kernel loads land
     int64_t deferred_growths = 0;         // landing growths taken from progress (counter)
     std::vector<uint64_t> land_tokens;    // every rank's token of every landing growth (diagnostics)
     int memcpy_token_mismatch = 0;        // landing tokens right by kernel load, wrong by hipMemcpy
@@ -722,7 +721,7 @@ static std::vector<export_rec> g_exp;
 
 // 0: *h exported (fresh if *fresh), 1: recycled handle bytes, <0: the
 // runtime refused (*e).
-static int quiesce(ompi_amd_comm_t *c);
+static int quiesce(ompi_amd_comm_t *c, const char *why = "quiesce");
 
 // OMPI_AMD_IPC_TRACE=1: one stderr line per new export and per new import
 // (handle words 0-15), for diagnosing mapping mix-ups after the fact.
@@ -1036,7 +1035,7 @@ static int import_buf(ompi_amd_comm_t *c, int peer, const buf_desc &d, const cha
         for (auto jt = c->imports.begin(); jt != c->imports.end(); ++jt)
             if (jt->pins == 0 && (it == c->imports.end() || jt->last_use < it->last_use)) it = jt;
         if (it != c->imports.end()) {
-            TRY(quiesce(c));  // an earlier call's kernel may still read it
+            TRY(quiesce(c, "quiesce (import eviction)"));  // an earlier call's kernel may still read it
             ipc_unmap(it->ref, c);
             c->imports.erase(it);
         }
@@ -1212,10 +1211,18 @@ static void note_stream(ompi_amd_comm_t *c, hipStream_t s) {
 // Wait until every kernel this communicator launched has finished (its
 // streams only: an application's unrelated work on the device is not
 // waited for, unlike hipDeviceSynchronize).
-static int quiesce_user(void *c) { return quiesce(static_cast<ompi_amd_comm_t *>(c)); }
+}  // namespace ompi_amd
+// (defined below, outside the namespace, beside progress_others)
+static hipError_t wait_stream(hipStream_t s);
+static hipError_t wait_event(hipEvent_t ev);
+namespace ompi_amd {
 
-static int quiesce(ompi_amd_comm_t *c) {
-    host_step st("quiesce");
+static int quiesce_user(void *c) {
+    return quiesce(static_cast<ompi_amd_comm_t *>(c), "quiesce (holder of a stale IPC mapping)");
+}
+
+static int quiesce(ompi_amd_comm_t *c, const char *why) {
+    host_step st(why);
     std::vector<hipEvent_t> evs;
     hipStream_t cur = nullptr;
     bool has = false;
@@ -1225,15 +1232,18 @@ static int quiesce(ompi_amd_comm_t *c) {
         cur = c->cur_stream;
         has = c->has_stream && !c->cur_closed;  // closed: a mark in evs bounds it
     }
+    // the waits launch other communicators' ready deferred calls meanwhile
+    // (progress_others): this communicator's kernels may be waiting for a
+    // peer that waits for this rank's launch of another communicator's call
     int rc = OMPI_AMD_SUCCESS;
     for (hipEvent_t e : evs) {
-        const hipError_t r = hipEventSynchronize(e);
+        const hipError_t r = ::wait_event(e);
         hip_ignore(hipEventDestroy(e));
         if (r != hipSuccess && rc == OMPI_AMD_SUCCESS)
             rc = record_hip(r, "hipEventSynchronize (communicator streams)");
     }
     TRY(rc);
-    if (has) TRY(record_hip(hipStreamSynchronize(cur), "hipStreamSynchronize (communicator stream)"));
+    if (has) TRY(record_hip(::wait_stream(cur), "hipStreamSynchronize (communicator stream)"));
     return OMPI_AMD_SUCCESS;
 }
 
@@ -1248,19 +1258,89 @@ static int quiesce(ompi_amd_comm_t *c) {
 // (export_alloc): a colliding one is kept alive while the next is made,
 // so that the runtime cannot hand out the same handle again.
 // uncached: fine-grained memory (flag pages) instead of ordinary device memory.
+// Library allocations peers map (flag pages, staging scratch, landing
+// buffers, shadow arena chunks, osc control pages and public copies) are
+// recycled, not freed: release_exportable keeps them for the next request
+// of the same size and kind, which gets the same address, buffer id and
+// handle, so a peer still mapping it shares that mapping.  A hipFree — and
+// the IPC close a peer must make before it opens a new allocation at a
+// freed address — waits for every kernel of the device, and with other
+// communicators' kernels waiting on peers that wait for this rank, that
+// stalled a nonblocking post until the device timeout.
+// Past kRecycleCap bytes kept, a release frees.
+struct recycled_block {
+    char *p;
+    size_t size;
+    bool uncached;
+    int device;
+};
+static std::mutex g_recycle_mu;
+static std::vector<recycled_block> g_recycle_free;
+static std::map<char *, recycled_block> g_recycle_used;
+static size_t g_recycle_free_bytes = 0;
+constexpr size_t kRecycleCap = 16ull << 30;
+
+static void release_exportable(void *ptr) {
+    if (!ptr) return;
+    char *p = static_cast<char *>(ptr);
+    {
+        std::lock_guard<std::mutex> g(g_recycle_mu);
+        auto it = g_recycle_used.find(p);
+        if (it != g_recycle_used.end()) {
+            const recycled_block b = it->second;
+            g_recycle_used.erase(it);
+            if (g_recycle_free_bytes + b.size <= kRecycleCap) {
+                g_recycle_free.push_back(b);
+                g_recycle_free_bytes += b.size;
+                return;
+            }
+        }
+    }
+    hip_ignore(hipFree(p));
+}
+
 static hipError_t alloc_exportable(size_t bytes, char **out, hipIpcMemHandle_t *h,
                                    bool uncached = false) {
     // Sized as ipc_safe_size() demands (a multiple of 2 MiB, at least 4 MiB:
     // smaller or odd-sized allocations are the ones ROCm 7.2 refuses to
     // import).  The handle names (pid, address, size): a
     // same-size allocation at a freed allocation's address gets its handle
-    // again; such a repeat is kept alive while the next attempt allocates
-    // elsewhere.
+    // again; such a repeat is kept alive (for good: freeing it would wait for
+    // the device, see above) while the next attempt allocates elsewhere.
+    static std::vector<void *> g_quarantine;  // under g_recycle_mu
+    const size_t want_sz = ipc_size_for(bytes);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) (void)hipGetLastError();
+    {
+        std::lock_guard<std::mutex> g(g_recycle_mu);
+        for (auto it = g_recycle_free.begin(); it != g_recycle_free.end(); ++it)
+            if (it->size == want_sz && it->uncached == uncached && it->device == dev) {
+                const recycled_block b = *it;
+                g_recycle_free.erase(it);
+                g_recycle_free_bytes -= b.size;
+                g_recycle_used[b.p] = b;
+                *out = b.p;
+                void *base = nullptr;
+                size_t range = 0;
+                if (hipMemGetAddressRange((hipDeviceptr_t *)&base, &range, (hipDeviceptr_t)b.p) != hipSuccess) {
+                    (void)hipGetLastError();
+                    base = b.p;
+                    range = b.size;
+                }
+                bool fresh = false;
+                hipError_t e = hipSuccess;
+                // exported before: the recorded handle comes back
+                if (export_alloc(base, range, buffer_id(b.p), h, &e, &fresh) == 0) return hipSuccess;
+                g_recycle_used.erase(b.p);  // not expected: fall through to a new allocation
+                g_quarantine.push_back(b.p);
+                break;
+            }
+    }
     std::vector<void *> failed;
     hipError_t e = hipErrorInvalidValue;
     for (int attempt = 0; attempt < 8; ++attempt) {
         void *p = nullptr;
-        const size_t sz = ipc_size_for(bytes);
+        const size_t sz = want_sz;
         {
             host_step st("hipMalloc", sz);
             e = uncached ? hipExtMallocWithFlags(&p, sz, hipDeviceMallocUncached) : hipMalloc(&p, sz);
@@ -1277,13 +1357,18 @@ static hipError_t alloc_exportable(size_t bytes, char **out, hipIpcMemHandle_t *
         const int rc = export_alloc(base, range, buffer_id(p), h, &e, &fresh);
         if (rc == 0) {
             *out = (char *)p;
+            std::lock_guard<std::mutex> g(g_recycle_mu);
+            g_recycle_used[(char *)p] = recycled_block{(char *)p, sz, uncached, dev};
             break;
         }
         if (rc == 1) e = hipErrorInvalidValue;  // recycled handle bytes
         (void)hipGetLastError();
         failed.push_back(p);  // keep it alive so the next try gets another range and handle
     }
-    for (void *p : failed) hip_ignore(hipFree(p));
+    if (!failed.empty()) {
+        std::lock_guard<std::mutex> g(g_recycle_mu);
+        g_quarantine.insert(g_quarantine.end(), failed.begin(), failed.end());
+    }
     return e;
 }
 
@@ -1314,15 +1399,6 @@ static size_t landing_want(size_t cur, size_t need) {
                     cur ? std::min(2 * (cur + kLandTag), kMaxIpcBytes) : 0);
 }
 
-// Buffers deferred growths replaced: called where every rank's earlier
-// kernels of this communicator are done (after a quiesce + barrier).
-static void free_retired_landing(ompi_amd_comm_t *c) {
-    for (ipc_ref *r : c->land_ref_retired) ipc_unmap(r, c);
-    c->land_ref_retired.clear();
-    for (char *p : c->land_retired) hip_ignore(hipFree(p));  // peers' mappings keep it alive
-    c->land_retired.clear();
-}
-
 // a new landing buffer's descriptor (its handle is already in d->h)
 static void land_desc(char *fresh, size_t want, buf_desc *d) {
     d->id = buffer_id(fresh);
@@ -1350,9 +1426,11 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
                    kMaxIpcBytes);
         return OMPI_AMD_ERR_UNSUPPORTED;
     }
-    TRY(quiesce(c));
+    if (host_trace())
+        fprintf(stderr, "[trace pid %d] blocking landing growth: need %zu, have %zu, planned %zu, %zu queued\n",
+                (int)getpid(), need, c->land_bytes, c->land_planned, c->pending.size());
+    TRY(quiesce(c, "quiesce (landing growth)"));
     TRY(c->boot.barrier());  // every rank's earlier kernels are done
-    free_retired_landing(c);
     // the old mappings stay open until the new ones are (so the new ones
     // get fresh addresses in this process), then close
     ipc_ref *old_land[kMaxRanks];
@@ -1361,8 +1439,12 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
         c->land_ref[p] = nullptr;
         c->peer_land.p[p] = nullptr;
     }
+    // the old mappings are kept with the communicator (their buffers stay
+    // allocated until destroy: see below), not closed here — a close may
+    // wait for every kernel of the device
     auto close_old = [&] {
-        for (int p = 0; p < kMaxRanks; ++p) ipc_unmap(old_land[p], c);
+        for (int p = 0; p < kMaxRanks; ++p)
+            if (old_land[p]) c->land_ref_retired.push_back(old_land[p]);
     };
     land_blob mine{}, all[kMaxRanks];
     char *fresh = nullptr;
@@ -1381,12 +1463,14 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     if (e != hipSuccess && mine.d.valid) record_hip(e, "landing token write");
     mine.ok = e == hipSuccess;
     int rc = c->boot.allgather(&mine, all, sizeof(mine));  // also: nobody uses the old one now
-    if (c->land) hip_ignore(hipFree(c->land));  // peers' mappings keep it alive until they close them
+    // freed with the communicator, not here: hipFree waits for every kernel
+    // of the device, other communicators' spinning ones included
+    if (c->land) c->land_retired.push_back(c->land);
     c->land = nullptr;
     c->land_bytes = c->land_planned = 0;
     if (rc != OMPI_AMD_SUCCESS) {
         close_old();
-        if (fresh) hip_ignore(hipFree(fresh));
+        release_exportable(fresh);
         return rc;
     }
     int status = mine.ok ? 0 : 1;  // 0 ok, 1 local HIP failure, 2 token mismatch
@@ -1456,7 +1540,7 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
         ipc_unmap(c->land_ref[p], c);
         c->land_ref[p] = nullptr;
     }
-    if (fresh) hip_ignore(hipFree(fresh));
+    release_exportable(fresh);
     if (rc == OMPI_AMD_SUCCESS && status == 0)
         record_msg("landing buffer growth failed on another rank (%s)",
                    worst == 2 ? "stale IPC mapping" : "HIP error");
@@ -1468,16 +1552,20 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
 // post time: ensure_landing is a rendezvous of the communicator, and MPI
 // lets ranks post different communicators' calls in different orders — two
 // growths posted in opposite orders wait for each other.
-// So the post does only local work: it allocates and stamps this rank's new
-// buffer, posts the descriptor as a ticket and queues a PEND_GROW ahead of
-// the call.  Progress, once the growth is at the queue front and every
-// rank's descriptor is in, maps the peers' new buffers, checks their tokens
-// and switches the communicator over.  Every rank switches at the same queue
-// position, so a call launched before the switch uses the old buffers on
-// every rank; those stay allocated and mapped until the next point where
-// every rank's earlier kernels are known done (free_retired_landing).
-// Nothing here waits for device work of any communicator: the stamp and the
-// check run on a non-blocking stream of their own.
+// So the post does only local work: it allocates this rank's new buffer,
+// posts the descriptor and token as a ticket and queues a PEND_GROW ahead
+// of the call.  Progress, once the growth is at the queue front and every
+// rank's descriptor is in, maps the peers' new buffers and switches the
+// communicator over.  No token check: the blocking growth's stamp and
+// read-back need a stream of their own or a host wait on the device (a
+// stream created for them cost a hardware queue); the
+// registry's retirement of colliding mappings is what keeps a new mapping
+// on the new allocation.
+// Every rank switches at the same queue position, so a call launched
+// before the switch uses the old buffers on every rank; those stay
+// allocated and mapped until the communicator is destroyed (as a blocking
+// growth keeps the buffers it replaces: hipFree and IPC closes may wait for
+// every kernel of the device).  Nothing here waits for device work.
 
 // Post a deferred call's ticket now — or, while the rendezvous ring is full
 // (or earlier tickets still wait), keep the blob for progress to post in
@@ -1506,14 +1594,13 @@ static int post_queued(ompi_amd_comm_t *c, bool block_front) {
     return OMPI_AMD_SUCCESS;
 }
 
-static hipError_t side_stream(ompi_amd_comm_t *c) {
-    if (c->side) return hipSuccess;
-    return hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
-}
-
-// Queue a growth to `need` usable bytes unless the queued ones reach it.
-// Every rank decides alike: the same calls are posted on every rank.
-static int nb_grow(ompi_amd_comm_t *c, size_t need) {
+// Queue a growth to `need` usable bytes unless the queued ones reach it,
+// ahead of a call on stream `s`.
+// Every rank decides alike: the same calls are posted on every rank.  Only
+// local work here — no stream is touched (a stream created for it alone
+// costs a hardware queue: on a shared GPU that took 8-B sendrecvs from 31
+// to 96 µs at 2 ranks, tools/p2p_osc_rows.py ROWS_PRE=iar_big).
+static int nb_grow(ompi_amd_comm_t *c, size_t need, hipStream_t s) {
     if (need <= c->land_planned) return OMPI_AMD_SUCCESS;
     const size_t want = landing_want(c->land_planned, need);
     if (want > kMaxIpcBytes) {
@@ -1523,26 +1610,20 @@ static int nb_grow(ompi_amd_comm_t *c, size_t need) {
     }
     land_blob mine{};
     char *fresh = nullptr;
-    hipError_t e = alloc_exportable(want, &fresh, &mine.d.h);
+    const hipError_t e = alloc_exportable(want, &fresh, &mine.d.h);
     mine.token = landing_token(c->rank);
     if (e == hipSuccess) land_desc(fresh, want, &mine.d);
     else record_hip(e, "landing buffer (deferred growth): hipMalloc / hipIpcGetMemHandle");
-    // the stamp has reached the device before the descriptor is published
-    if (e == hipSuccess) e = side_stream(c);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(fresh + want - kLandTag, &mine.token, sizeof(mine.token),
-                           hipMemcpyHostToDevice, c->side);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->side);
-    if (e != hipSuccess && mine.d.valid) record_hip(e, "landing token write");
     mine.ok = e == hipSuccess;  // a failure is posted too: every rank fails the growth alike
     pending_op g{};
     g.kind = PEND_GROW;
+    g.stream = s;
     g.grow = fresh;
     g.grow_bytes = want;
     g.grow_token = mine.token;
     const int rc = nb_ticket(c, g, &mine, sizeof(mine));
     if (rc != OMPI_AMD_SUCCESS) {
-        if (fresh) hip_ignore(hipFree(fresh));
+        release_exportable(fresh);
         return rc;
     }
     c->pending.push_back(g);
@@ -1552,14 +1633,13 @@ static int nb_grow(ompi_amd_comm_t *c, size_t need) {
 }
 
 // A queued growth at the front of the queue with every rank's descriptor
-// (`all`): map, check the tokens by kernel loads through the new mappings,
-// switch.  On failure nothing after it launches (land_failed): those calls
-// were sized for the new buffers.
+// (`all`): map the peers' new buffers and switch.  On failure nothing after
+// it launches (land_failed): those calls were sized for the new buffers.
 static int grow_launch(ompi_amd_comm_t *c, const pending_op &g, const land_blob *all) {
     const size_t want = g.grow_bytes;
     ipc_ref *refs[kMaxRanks] = {};
     void *maps[kMaxRanks] = {};
-    int status = all[c->rank].ok ? 0 : 1;  // 0 ok, 1 HIP failure somewhere, 2 token mismatch
+    int status = all[c->rank].ok ? 0 : 1;
     for (int p = 0; p < c->size && status == 0; ++p) {
         if (p == c->rank) continue;
         if (!all[p].ok) {
@@ -1567,37 +1647,6 @@ static int grow_launch(ompi_amd_comm_t *c, const pending_op &g, const land_blob 
             status = 1;
         } else if (ipc_map(alloc_of(all[p].d), c, &refs[p], &maps[p]) != OMPI_AMD_SUCCESS) {
             status = 1;
-        }
-    }
-    hipError_t e = hipSuccess;
-    if (status == 0 && !c->peek_host) {
-        e = hipHostMalloc((void **)&c->peek_host, kMaxRanks * sizeof(uint64_t), hipHostMallocMapped);
-        if (e != hipSuccess) c->peek_host = nullptr;
-    }
-    uint64_t *peek_dev = nullptr;
-    if (status == 0 && e == hipSuccess) e = hipHostGetDevicePointer((void **)&peek_dev, c->peek_host, 0);
-    if (status == 0 && e == hipSuccess) e = side_stream(c);
-    for (int p = 0; status == 0 && e == hipSuccess && p < c->size; ++p) {
-        if (p == c->rank) continue;
-        c->peek_host[p] = 0;
-        hipLaunchKernelGGL(peek_kernel, dim3(1), dim3(1), 0, c->side,
-                           (const uint64_t *)((char *)maps[p] + want - kLandTag), peek_dev + p);
-        e = hipGetLastError();
-    }
-    if (status == 0 && e == hipSuccess) e = hipStreamSynchronize(c->side);
-    if (status == 0 && e != hipSuccess) {
-        record_hip(e, "landing token check (deferred growth)");
-        status = 1;
-    }
-    for (int p = 0; status == 0 && p < c->size; ++p) {
-        if (p == c->rank) continue;
-        const uint64_t seen = __atomic_load_n(&c->peek_host[p], __ATOMIC_ACQUIRE);
-        if (seen != all[p].token) {
-            record_msg("landing buffer of rank %d (id %llu): the IPC mapping %p shows token "
-                       "%016llx, expected %016llx (deferred growth)", p,
-                       (unsigned long long)all[p].d.id, maps[p], (unsigned long long)seen,
-                       (unsigned long long)all[p].token);
-            status = 2;
         }
     }
     for (int q = 0; q < c->size; ++q) c->land_tokens.push_back(all[q].token);
@@ -1729,7 +1778,7 @@ static int shadow_reserve(ompi_amd_comm_t *c, size_t need, char **out, int k = 0
     }
     // the old shadow's last readers are the peers of an earlier call, done
     // once this rank's stream passed that call's trailing barrier
-    TRY(quiesce(c));
+    TRY(quiesce(c, "quiesce (shadow growth)"));
     arena_free(c, sh);
     const size_t want = std::max(need, std::min(2 * bytes, kMaxIpcBytes));
     sh = nullptr;
@@ -2839,6 +2888,7 @@ static void req_event_put(ompi_amd_comm_t *c, hipEvent_t ev) {
 static int progress(ompi_amd_comm_t *c, bool block, int max_launch) {
     while (!c->pending.empty() && max_launch-- != 0) {
         if (c->unposted) {  // tickets the full ring held back (nb_ticket)
+            std::unique_ptr<host_step> st(block ? new host_step("post queued tickets (blocking)") : nullptr);
             TRY(post_queued(c, block && c->pending.front().unposted));
             if (c->pending.front().unposted) return OMPI_AMD_SUCCESS;
         }
@@ -2877,6 +2927,7 @@ static int progress(ompi_amd_comm_t *c, bool block, int max_launch) {
         int rc = OMPI_AMD_SUCCESS;
         if (o.ticket) {
             bool ready = false;
+            std::unique_ptr<host_step> st(block ? new host_step("ticket test (blocking)", o.ticket) : nullptr);
             rc = c->boot.test(o.ticket, all, sizeof(call_blob), block, &ready);
             if (rc == OMPI_AMD_SUCCESS && !ready) return OMPI_AMD_SUCCESS;
         }
@@ -3179,7 +3230,7 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     (void)drain(c);  // deferred nonblocking calls every peer will also launch
     for (auto &o : c->pending)  // left by a failed drain: queued growths' buffers
         if (o.grow) c->land_retired.push_back(o.grow);
-    (void)quiesce(c);
+    (void)quiesce(c, "quiesce (destroy)");
     (void)c->boot.barrier();  // nobody still reads our memory
     ipc_remove_user(c);
     for (auto &x : c->imports) ipc_unmap(x.ref, c);  // the process's mapping stays while others hold it
@@ -3194,13 +3245,13 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     c->land_ref_retired.clear();
     (void)c->boot.barrier();
     if (c->osc_release) c->osc_release(c->osc_state, 1);  // its own memory
-    if (c->flags) hip_ignore(hipFree(c->flags));
-    if (c->scratch) hip_ignore(hipFree(c->scratch));
-    if (c->land) hip_ignore(hipFree(c->land));
-    for (char *q : c->land_retired) hip_ignore(hipFree(q));
+    // recycled for later communicators, not freed (release_exportable)
+    release_exportable(c->flags);
+    release_exportable(c->scratch);
+    release_exportable(c->land);
+    for (char *q : c->land_retired) release_exportable(q);
     c->land_retired.clear();
-    if (c->peek_host) hip_ignore(hipHostFree(c->peek_host));
-    for (auto &ch : c->arena) hip_ignore(hipFree(ch.base));  // shadows included
+    for (auto &ch : c->arena) release_exportable(ch.base);  // shadows included
     c->arena.clear();
     if (c->err_host) hip_ignore(hipHostFree(c->err_host));
     if (c->dbg_host) hip_ignore(hipHostFree(c->dbg_host));
@@ -3219,7 +3270,6 @@ int ompi_amd_comm_destroy(ompi_amd_comm_t *c) {
     c->boot.detach();
     forget_streams(c);
     if (c->own) hip_ignore(hipStreamDestroy(c->own));  // drained above
-    if (c->side) hip_ignore(hipStreamDestroy(c->side));
     delete c;
     return OMPI_AMD_SUCCESS;
 }
@@ -3629,7 +3679,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
     if (allreduce_push_gathers(c, pp, count, type)) {
         // no swap: only the landing buffer must be big enough at the launch
         // (a growth queued ahead of this call: nb_grow)
-        rc = nb_grow(c, staged_push_landing(c->size, pp.algorithm, (int64_t)count, type, nullptr));
+        rc = nb_grow(c, staged_push_landing(c->size, pp.algorithm, (int64_t)count, type, nullptr), o.stream);
         if (rc != OMPI_AMD_SUCCESS) {
             req_event_put(req->c, req->ev);
             delete req;
@@ -3639,7 +3689,7 @@ int ompi_amd_iallreduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
         // post this rank's half of the handle swap now; the launch waits for
         // the peers' halves (progress / the next collective call)
         const bool push = is_push(pp.algorithm);
-        if (push) rc = nb_grow(c, push_slot((int64_t)count, c->size, type) * (size_t)c->size);
+        if (push) rc = nb_grow(c, push_slot((int64_t)count, c->size, type) * (size_t)c->size, o.stream);
         // export fallback with memory of its own (several calls may be
         // outstanding): the posted descriptors are the shadows'
         const size_t bytes = count * ompi_amd_type_extent(type);
@@ -3730,8 +3780,8 @@ static bool nb_swaps(const ompi_amd_comm_t *c, size_t bytes) {
 // A deferred call's landing buffer grown at post time (growth is collective
 // and blocking: every rank posts the same call alike); on failure the
 // request is released.
-static int nb_grow_landing(ompi_amd_comm_t *c, size_t need, ompi_amd_request *req) {
-    const int rc = nb_grow(c, need);
+static int nb_grow_landing(ompi_amd_comm_t *c, size_t need, ompi_amd_request *req, hipStream_t s) {
+    const int rc = nb_grow(c, need, s);
     if (rc != OMPI_AMD_SUCCESS) {
         req_event_put(req->c, req->ev);
         delete req;
@@ -3757,7 +3807,7 @@ int ompi_amd_ireduce_scatter_block(ompi_amd_comm_t *c, const void *sbuf, void *r
         // launch; only the landing buffer must be big enough beforehand
         // (its growth is collective: every rank posts this call alike)
         const size_t slot = (rcount * ompi_amd_type_extent(type) + 16 + 255) & ~(size_t)255;
-        TRY(nb_grow_landing(c, slot * (size_t)(c->size + 1), req));
+        TRY(nb_grow_landing(c, slot * (size_t)(c->size + 1), req, o.stream));
         o.inplace = inplace;
         return nb_post(c, o, nullptr, 0, false, out);
     }
@@ -3782,7 +3832,7 @@ int ompi_amd_iallgather(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
     if (inplace) o.sbuf = (const void *)1;
     if (!nb_swaps(c, bytes)) return nb_post(c, o, nullptr, 0, false, out);
     if (const size_t need = ag_landing_need(c, bytes)) {
-        TRY(nb_grow_landing(c, need, req));
+        TRY(nb_grow_landing(c, need, req, o.stream));
         o.land = true;  // stores into the peers' landing buffers: nothing to post
         return nb_post(c, o, nullptr, 0, false, out);
     }
@@ -3802,7 +3852,7 @@ int ompi_amd_ibcast(ompi_amd_comm_t *c, void *buf, size_t bytes, int root, void 
     o.root = root;
     if (nb_swaps(c, bytes)) {
         if (const size_t need = bcast_landing_need(c, bytes)) {
-            TRY(nb_grow_landing(c, need, req));
+            TRY(nb_grow_landing(c, need, req, o.stream));
             o.land = true;  // stores into the peers' landing buffers: nothing to post
             return nb_post(c, o, nullptr, 0, false, out);
         }
@@ -3843,7 +3893,7 @@ int ompi_amd_ireduce(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t co
         int64_t split, early, late;
         blockcount((int64_t)count, n, &split, &early, &late);
         const size_t slot = ((size_t)early * ompi_amd_type_extent(type) + 16 + 255) & ~(size_t)255;
-        TRY(nb_grow_landing(c, slot * (size_t)n + ((bytes + 255) & ~(size_t)255), req));
+        TRY(nb_grow_landing(c, slot * (size_t)n + ((bytes + 255) & ~(size_t)255), req, o.stream));
     }
     if (n == 1 || count == 0) return nb_post(c, o, nullptr, 0, false, out);
     call_blob mine{};
@@ -3872,7 +3922,7 @@ static int iscan_common(ompi_amd_comm_t *c, const void *sbuf, void *rbuf, size_t
     o.kind = PEND_SCAN;
     o.exclusive = exclusive;
     if (c->size > 1 && count > 0 && bytes > c->small_bytes && c->zero_copy)
-        TRY(nb_grow_landing(c, bytes + 256, req));
+        TRY(nb_grow_landing(c, bytes + 256, req, o.stream));
     return nb_post(c, o, nullptr, 0, false, out);
 }
 
@@ -3908,7 +3958,7 @@ int ompi_amd_ireduce_scatter(ompi_amd_comm_t *c, const void *sbuf, void *rbuf,
     }
     if (c->size > 1 && total * ext > c->small_bytes && c->zero_copy) {  // reduce_my_block's staged push
         const size_t slot = (maxc * ext + 16 + 255) & ~(size_t)255;
-        TRY(nb_grow_landing(c, slot * (size_t)(c->size + 1), req));
+        TRY(nb_grow_landing(c, slot * (size_t)(c->size + 1), req, o.stream));
     }
     return nb_post(c, o, nullptr, 0, false, out);
 }
@@ -4825,6 +4875,8 @@ void comm_set_osc_state(ompi_amd_comm_t *c, void *state, void (*release)(void *,
 int comm_allgather(ompi_amd_comm_t *c, const void *mine, void *all, size_t len) {
     return c->boot.allgather(mine, all, len);
 }
+
+void comm_release_exportable(void *p) { release_exportable(p); }
 
 int comm_alloc_exportable(size_t bytes, bool uncached, void **out, ipc_desc *d) {
     memset(d, 0, sizeof(*d));

@@ -39,6 +39,9 @@ int comm_allgather(ompi_amd_comm_t *c, const void *mine, void *all, size_t len);
 // A fresh device allocation whose IPC handle no earlier allocation of this
 // process had (uncached: fine-grained), described in *d.
 int comm_alloc_exportable(size_t bytes, bool uncached, void **out, ipc_desc *d);
+// Give back memory from comm_alloc_exportable (kept for a later request of
+// the same size instead of freed; anything else is freed).
+void comm_release_exportable(void *p);
 // Device memory from the communicator's exported arena (the shadow arena:
 // chunks exported once, mapped by each peer once, freed at comm_destroy),
 // so a peer maps nothing new per buffer.  comm_arena_free: once no peer

@@ -118,7 +118,23 @@ void hold(ipc_ref *r, void *owner) {
 }
 
 // (g_mu released) the runtime close; the stats under the lock
+// OMPI_AMD_TRACE=1: the runtime's IPC opens and closes with their duration
+// (a close may wait for every kernel of the device)
+struct reg_step {
+    const char *what;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    explicit reg_step(const char *w) : what(w) {}
+    ~reg_step() {
+        static const bool on = getenv("OMPI_AMD_TRACE") && *getenv("OMPI_AMD_TRACE") == '1';
+        if (!on) return;
+        const double ms =
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        fprintf(stderr, "[trace pid %d] %s done %.3f ms\n", (int)getpid(), what, ms);
+    }
+};
+
 void close_mapping(ipc_ref *r) {
+    reg_step st("hipIpcCloseMemHandle");
     const auto t0 = std::chrono::steady_clock::now();
     const hipError_t e = hipIpcCloseMemHandle(r->base);
     hip_ignore(e);
@@ -244,7 +260,11 @@ int ipc_map(const ipc_alloc &a, void *owner, ipc_ref **ref, void **base) {
     // refusal is an error, reported with the buffer.
     void *m = nullptr;
     const auto t_open = std::chrono::steady_clock::now();
-    const hipError_t e = hipIpcOpenMemHandle(&m, a.h, hipIpcMemLazyEnablePeerAccess);
+    hipError_t e;
+    {
+        reg_step st("hipIpcOpenMemHandle");
+        e = hipIpcOpenMemHandle(&m, a.h, hipIpcMemLazyEnablePeerAccess);
+    }
     const double open_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_open).count();
     std::lock_guard<std::mutex> g(g_mu);

@@ -1262,7 +1262,7 @@ static void ctl_arena_release(void *state, int phase) {
         return;
     }
     for (auto &ch : a->chunks)  // every peer dropped its mappings of ours
-        if (ch.mine) hip_ignore(hipFree(ch.mine));
+        if (ch.mine) comm_release_exportable(ch.mine);
     delete a;
 }
 
@@ -1321,7 +1321,7 @@ static int ctl_take(ompi_amd_comm_t *c, int rc_in, int *slot) {
     if (rc != OMPI_AMD_SUCCESS) {
         for (auto &r : ch.ref) ipc_unmap(r, c);
         (void)comm_allgather(c, nullptr, nullptr, 0);  // every mapping closed before the free
-        if (ch.mine) hip_ignore(hipFree(ch.mine));
+        if (ch.mine) comm_release_exportable(ch.mine);
         return rc;
     }
     *slot = (int)a->used.size();
@@ -1393,7 +1393,7 @@ __global__ __launch_bounds__(kOscThreads) void win_merge_kernel(char *priv, char
 static void win_release_shadow(ompi_amd_win_t *w) {
     if (w->snap) hip_ignore(hipFree(w->snap));
     if (w->shadow) {
-        if (w->owns_shadow) hip_ignore(hipFree(w->shadow));
+        if (w->owns_shadow) comm_release_exportable(w->shadow);
         else comm_arena_free(w->c, w->shadow);
     }
     w->snap = w->shadow = nullptr;
@@ -1563,7 +1563,7 @@ int ompi_amd_win_allocate(ompi_amd_comm_t *c, size_t bytes, int disp_unit, void 
     auto release = [&] {
         if (!m) return;
         if (arena) comm_arena_free(c, m);
-        else hip_ignore(hipFree(m));
+        else comm_release_exportable(m);
     };
     // a local failure still joins the rendezvous (as a zero-byte window) so
     // that no peer waits; the collective result reports it
@@ -1724,10 +1724,10 @@ int ompi_amd_win_free(ompi_amd_win_t *w) {
     if (rc == OMPI_AMD_SUCCESS) rc = brc2;
     if (w->shared_owner && w->shared_seg) {
         if (w->shared_arena) comm_arena_free(c, w->shared_seg);
-        else hip_ignore(hipFree(w->shared_seg));
+        else comm_release_exportable(w->shared_seg);
     }
     if (w->query) hip_ignore(hipStreamDestroy(w->query));
-    if (w->owns_base && w->base) hip_ignore(hipFree(w->base));
+    if (w->owns_base && w->base) comm_release_exportable(w->base);
     if (w->arena_base && w->base) comm_arena_free(c, w->base);  // nobody maps it per window
     win_release_shadow(w);  // no peer maps the public copy any more
     for (char *q : w->scr) if (q) hip_ignore(hipFree(q));  // the streams were synchronised above
@@ -2224,7 +2224,7 @@ int ompi_amd_win_allocate_shared(ompi_amd_comm_t *c, size_t bytes, int disp_unit
     auto release_owner = [&] {
         if (me != 0 || !m) return;
         if (arena) comm_arena_free(c, m);
-        else hip_ignore(hipFree(m));
+        else comm_release_exportable(m);
     };
     int all_ok = 0;
     const int grc = ompi_amd_comm_agree(c, rc == OMPI_AMD_SUCCESS, &all_ok);

@@ -16,10 +16,19 @@ namespace ompi_amd {
 static thread_local char tls_err[512] = "";
 static thread_local hipStream_t tls_stream = nullptr;
 
+// OMPI_AMD_TRACE=1: every recorded error also goes to stderr when it is
+// recorded (a rank that fails inside progress names its cause even if the
+// call that reports it never comes)
+static bool trace_errors() {
+    static const bool on = getenv("OMPI_AMD_TRACE") && *getenv("OMPI_AMD_TRACE") == '1';
+    return on;
+}
+
 int record_hip(hipError_t e, const char *what) {
     if (e == hipSuccess) return OMPI_AMD_SUCCESS;
     (void)hipGetLastError();  // reported through the status: not left for the application's checks
     snprintf(tls_err, sizeof(tls_err), "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+    if (trace_errors()) fprintf(stderr, "[trace pid %d] error: %s\n", (int)getpid(), tls_err);
     return OMPI_AMD_ERR_HIP;
 }
 
@@ -28,6 +37,7 @@ void record_msg(const char *fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(tls_err, sizeof(tls_err), fmt, ap);
     va_end(ap);
+    if (trace_errors()) fprintf(stderr, "[trace pid %d] error: %s\n", (int)getpid(), tls_err);
 }
 
 hipStream_t thread_stream() { return tls_stream ? tls_stream : hipStreamPerThread; }

@@ -11,6 +11,7 @@ import functools
 import json
 import os
 import sys
+import time
 import traceback
 
 import numpy as np
@@ -946,6 +947,10 @@ def case_cross_comm_grow(comm, rank, n, salt, nring=12):
         for cc in comms:
             if cc.error():
                 msgs.append(f"device error {cc.error()}")
+    except Exception:  # reported now: the frees below may wait for peers
+        traceback.print_exc()
+        sys.stderr.flush()
+        raise
     finally:
         for cc in comms:
             cc.free()
@@ -1027,12 +1032,20 @@ def case_cross_comm_random(comm, rank, n, salt, ncomm=3, per_comm=6):
                 want = exp[rank]
             prepared.append((go, o, want, s, f"comm {ci} {kind} {count} {dt.name}"))
         torch.cuda.synchronize()  # MPI semantics: the buffers are ready at the call
+        timing = os.environ.get("CROSS_TIMING") == "1"
         for go, o, want, s, what in prepared:
+            t0 = time.perf_counter()
             posted.append((go(), o, want, what))
+            if timing:
+                print(f"[post] {what} {1e3 * (time.perf_counter() - t0):.2f} ms", file=sys.stderr, flush=True)
         wait_order = list(range(len(posted)))
         mine.shuffle(wait_order)
         for i in wait_order:
+            t0 = time.perf_counter()
             posted[i][0].wait()
+            if timing:
+                print(f"[wait] {posted[i][3]} {1e3 * (time.perf_counter() - t0):.2f} ms", file=sys.stderr,
+                      flush=True)
         torch.cuda.synchronize()
         for r_, o, want, what in posted:
             r_.free()
@@ -1045,6 +1058,10 @@ def case_cross_comm_random(comm, rank, n, salt, ncomm=3, per_comm=6):
         for cc in comms:
             if cc.error():
                 msgs.append(f"device error {cc.error()}")
+    except Exception:  # reported now: the frees below may wait for peers
+        traceback.print_exc()
+        sys.stderr.flush()
+        raise
     finally:
         for cc in comms:
             cc.free()

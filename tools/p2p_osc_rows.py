@@ -29,7 +29,25 @@ def rank_main():
     comm = coll.Communicator.from_torch_distributed(device=dev)
     if os.environ.get("ROWS_OWN_STREAM") == "1":
         comm.set_param("own_stream", 1)
+    pre = os.environ.get("ROWS_PRE", "")
+    if pre:
+        # a collective first, as the bench's allreduce legs run before these
+        # rows: iar_big / ar_big a (non)blocking allreduce past the zero-copy
+        # size (a landing growth: queued at post / at the call), iar_small a
+        # staged one (no growth)
+        x = torch.ones((16 << 20) if pre.endswith("big") else 1024, device="cuda")
+        y = torch.empty_like(x)
+        torch.cuda.synchronize()
+        for kind in pre.split("+")[0].split(","):  # e.g. ar,iar_big: a blocking call, then a nonblocking one
+            if kind.startswith("iar"):
+                comm.iallreduce(x, y, x.numel(), mop.MPI_FLOAT, mop.MPI_SUM).wait()
+            else:
+                comm.allreduce(x, y, x.numel(), mop.MPI_FLOAT, mop.MPI_SUM)
+        torch.cuda.synchronize()
     res = coll_bench._p2p_osc_rows(comm, dist, torch, mop, n, rank, "cpu")
+    res["pre"] = pre
+    res["deferred_growths"] = comm.get_param("landing_deferred_growths")
+    res["landing_bytes"] = comm.get_param("landing_bytes")
     if rank == 0:
         print(json.dumps({"ranks": n, "gpus": ngpu, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default"),
                           "own_stream": os.environ.get("ROWS_OWN_STREAM", "0"), **res}), flush=True)
