@@ -41,6 +41,18 @@ def rank_main():
         for kind in pre.split("+")[0].split(","):  # e.g. ar,iar_big: a blocking call, then a nonblocking one
             if kind.startswith("iar"):
                 comm.iallreduce(x, y, x.numel(), mop.MPI_FLOAT, mop.MPI_SUM).wait()
+            elif kind.startswith("pers"):  # a persistent plan: init, two starts, free
+                pl = comm.allreduce_init(x, y, x.numel(), mop.MPI_FLOAT, mop.MPI_SUM)
+                for _ in range(2):
+                    pl.start()
+                    pl.wait()
+                pl.free()
+            elif kind.startswith("scan"):
+                comm.scan(x, y, x.numel(), mop.MPI_FLOAT, mop.MPI_SUM)
+            elif kind.startswith("auto"):  # autotuned blocking calls (the bench's rows run with it on)
+                comm.set_param("autotune", 1)
+                for _ in range(40):
+                    comm.allreduce(x, y, x.numel(), mop.MPI_FLOAT, mop.MPI_SUM)
             else:
                 comm.allreduce(x, y, x.numel(), mop.MPI_FLOAT, mop.MPI_SUM)
         torch.cuda.synchronize()
