@@ -92,8 +92,11 @@ int eager_get(const char *cell, void *dst, size_t bytes, const uint64_t *flag, u
 // osc_ipc.hip: the byte copy of put / get and the p2p receive (persistent
 // grid, one acquire per workgroup; src or dst may be peer memory).
 // gate: a CTL_TAKEN_* word that must read 1 for the copy to run (NULL: none).
+// remote_dst: dst is memory of another GPU (a per-workgroup system-scope
+// release ends the copy); false: this GPU's memory (the kernel boundary's
+// release covers it).
 int xfer_copy(const void *src, void *dst, size_t bytes, hipStream_t s,
-              const uint32_t *gate = nullptr);
+              const uint32_t *gate = nullptr, bool remote_dst = true);
 // The same copy with device-side signalling (p2p staged messages): every
 // workgroup first waits until *wait == wait_v (bounded by ticks: *err set,
 // nothing copied; wait NULL: no wait); after the last workgroup finished

@@ -661,7 +661,7 @@ static void start_recv(p2p_state *p, ompi_amd_p2p_request *r, msg_slot *m, int s
                 rc = xfer_copy_sig(src, dst, n, r->stream, sg);
             }
         } else {
-            rc = xfer_copy(src, dst, n, r->stream);
+            rc = xfer_copy(src, dst, n, r->stream, nullptr, false);  // dst: this GPU's memory
         }
     }
     if (rc == OMPI_AMD_SUCCESS && r->host_dst)
@@ -889,7 +889,7 @@ int ompi_amd_isend(ompi_amd_comm_t *c, const void *buf, size_t bytes, int dst, i
     auto copy_in = [&](char *to) {
         const int crc = host ? record_hip(hipMemcpyAsync(to, buf, bytes, hipMemcpyHostToDevice, s),
                                           "hipMemcpyAsync (p2p send stage)")
-                             : xfer_copy(buf, to, bytes, s);
+                             : xfer_copy(buf, to, bytes, s, nullptr, false);  // a stage of this GPU
         return crc == OMPI_AMD_SUCCESS ? record_hip(hipStreamSynchronize(s), "hipStreamSynchronize (stage)")
                                        : crc;
     };
