@@ -886,10 +886,11 @@ static int osc_scratch(ompi_amd_win_t *w, hipStream_t s, int slot, size_t bytes,
     w->scr_last = nullptr;  // until osc_scratch_done records this call's use
     if (bytes > w->scr_cap[slot]) {
         const size_t want = std::max(bytes, 2 * w->scr_cap[slot]);
-        char *p = nullptr;
-        OSC_TRY(record_hip(hipMalloc(&p, want), "hipMalloc (osc scratch)"));
+        void *p = nullptr;
+        ipc_desc d;  // recycled memory (comm_release_exportable), not exported
+        OSC_TRY(comm_alloc_exportable(want, false, &p, &d));
         if (w->scr[slot]) w->scr_old.push_back(w->scr[slot]);
-        w->scr[slot] = p;
+        w->scr[slot] = static_cast<char *>(p);
         w->scr_cap[slot] = want;
     }
     *out = w->scr[slot];
@@ -1413,7 +1414,7 @@ __global__ __launch_bounds__(kOscThreads) void win_merge_kernel(char *priv, char
 }
 
 static void win_release_shadow(ompi_amd_win_t *w) {
-    if (w->snap) hip_ignore(hipFree(w->snap));
+    if (w->snap) comm_release_exportable(w->snap);
     if (w->shadow) {
         if (w->owns_shadow) comm_release_exportable(w->shadow);
         else comm_arena_free(w->c, w->shadow);
@@ -1485,7 +1486,10 @@ static int win_setup(ompi_amd_comm_t *c, void *base, size_t bytes, int disp_unit
         }
         if (rc == OMPI_AMD_SUCCESS) {
             w->shadow = static_cast<char *>(pub);
-            rc = record_hip(hipMalloc((void **)&w->snap, bytes), "hipMalloc (window snapshot)");
+            ipc_desc sd;  // recycled memory (comm_release_exportable), not exported
+            void *snap = nullptr;
+            rc = comm_alloc_exportable(bytes, false, &snap, &sd);
+            w->snap = static_cast<char *>(snap);
         }
         // both copies complete before this rank joins the rendezvous below:
         // peers may put into the public copy as soon as the window exists.
@@ -1766,8 +1770,8 @@ int ompi_amd_win_free(ompi_amd_win_t *w) {
     if (w->owns_base && w->base) comm_release_exportable(w->base);
     if (w->arena_base && w->base) comm_arena_free(c, w->base);  // nobody maps it per window
     win_release_shadow(w);  // no peer maps the public copy any more
-    for (char *q : w->scr) if (q) hip_ignore(hipFree(q));  // the streams were synchronised above
-    for (char *q : w->scr_old) hip_ignore(hipFree(q));
+    for (char *q : w->scr) if (q) comm_release_exportable(q);  // the streams were synchronised above
+    for (char *q : w->scr_old) comm_release_exportable(q);
     if (w->scr_ev) hip_ignore(hipEventDestroy(w->scr_ev));
     if (rc == OMPI_AMD_SUCCESS) rc = comm_sticky(c);
     delete w;

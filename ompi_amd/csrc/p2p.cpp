@@ -354,15 +354,15 @@ void p2p_destroy(p2p_state *p) {
         p->ring_name(p->rank, nm, sizeof(nm));
         shm_unlink(nm);
     }
-    if (p->eager) hip_ignore(hipFree(p->eager));
+    if (p->eager) comm_release_exportable(p->eager);  // recycled: a hipFree waits for the device
     for (hipEvent_t e : p->ev_free) hip_ignore(hipEventDestroy(e));
     // the communicator's final rendezvous has passed: no peer reads a stage
     // (arena stages went with the communicator's arena)
     for (auto &f : p->staged)
-        if (!f.st.arena) hip_ignore(hipFree(f.st.buf));
+        if (!f.st.arena) comm_release_exportable(f.st.buf);
     for (auto &st : p->send_free)
-        if (!st.arena) hip_ignore(hipFree(st.buf));
-    for (auto &st : p->recv_free) hip_ignore(hipFree(st.buf));
+        if (!st.arena) comm_release_exportable(st.buf);
+    for (auto &st : p->recv_free) comm_release_exportable(st.buf);
     if (p->rank == 0) p2p_unlink(p);
     delete p;
 }
