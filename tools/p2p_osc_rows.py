@@ -60,6 +60,8 @@ def rank_main():
     res["pre"] = pre
     res["deferred_growths"] = comm.get_param("landing_deferred_growths")
     res["landing_bytes"] = comm.get_param("landing_bytes")
+    res["ipc_live"] = comm.get_param("ipc_live")
+    res["landing_retired"] = comm.get_param("landing_retired")
     if rank == 0:
         print(json.dumps({"ranks": n, "gpus": ngpu, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default"),
                           "own_stream": os.environ.get("ROWS_OWN_STREAM", "0"), **res}), flush=True)
