@@ -139,6 +139,31 @@ __global__ void peek_kernel(const uint64_t *src, uint64_t *dst) {
     *dst = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// A deferred landing growth's token stamp and check (grow_launch), on the
+// stream of the call it was queued for: land_stamp_kernel stores this
+// rank's token into the last bytes of its new buffer, a device barrier of
+// the communicator follows (every rank's stamp is out before any check),
+// then land_check_kernel reads every peer's token through this process's
+// new mapping of that peer's buffer.  A mapping that shows another token —
+// it reaches another allocation — raises the communicator's error word and
+// the peers' abort word.  No host wait and no stream of its own.
+struct tok_set { uint64_t t[kMaxRanks]; };
+struct tok_ptrs { const uint64_t *p[kMaxRanks]; };
+__global__ void land_stamp_kernel(uint64_t *mine, uint64_t token) {
+    __hip_atomic_store(mine, token, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    sys_release();
+}
+__global__ __launch_bounds__(64) void land_check_kernel(tok_ptrs peers, tok_set expect, int rank, int size,
+                                                        int *err, uint64_t *abort_word) {
+    const int t = threadIdx.x;
+    sys_acquire();
+    if (t >= size || t == rank) return;
+    if (__hip_atomic_load(peers.p[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != expect.t[t]) {
+        __hip_atomic_store(err, (int)OMPI_AMD_ERR_HIP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(abort_word, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // NT: non-temporal stores (streaming cache policy) — param "copy_nt" (which
 // also sets the fold kernels' FOLD_NT_STORE), an A/B the 8-GPU bench
 // measures for the remote stores of the scatter and push phases
@@ -1555,12 +1580,10 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
 // So the post does only local work: it allocates this rank's new buffer,
 // posts the descriptor and token as a ticket and queues a PEND_GROW ahead
 // of the call.  Progress, once the growth is at the queue front and every
-// rank's descriptor is in, maps the peers' new buffers and switches the
-// communicator over.  No token check: the blocking growth's stamp and
-// read-back need a stream of their own or a host wait on the device (a
-// stream created for them cost a hardware queue); the
-// registry's retirement of colliding mappings is what keeps a new mapping
-// on the new allocation.
+// rank's descriptor is in, maps the peers' new buffers, queues the token
+// stamp and check on the call's stream (device work only: a host-side
+// check would need a stream of its own, and one more stream cost a
+// hardware queue) and switches the communicator over.
 // Every rank switches at the same queue position, so a call launched
 // before the switch uses the old buffers on every rank; those stay
 // allocated and mapped until the communicator is destroyed (as a blocking
@@ -1633,8 +1656,11 @@ static int nb_grow(ompi_amd_comm_t *c, size_t need, hipStream_t s) {
 }
 
 // A queued growth at the front of the queue with every rank's descriptor
-// (`all`): map the peers' new buffers and switch.  On failure nothing after
-// it launches (land_failed): those calls were sized for the new buffers.
+// (`all`): map the peers' new buffers, queue the token stamp / barrier /
+// check on the growth's stream, switch.  On failure nothing after it
+// launches (land_failed): those calls were sized for the new buffers.
+static int launch_barrier(ompi_amd_comm_t *c, hipStream_t s);
+
 static int grow_launch(ompi_amd_comm_t *c, const pending_op &g, const land_blob *all) {
     const size_t want = g.grow_bytes;
     ipc_ref *refs[kMaxRanks] = {};
@@ -1648,6 +1674,25 @@ static int grow_launch(ompi_amd_comm_t *c, const pending_op &g, const land_blob 
         } else if (ipc_map(alloc_of(all[p].d), c, &refs[p], &maps[p]) != OMPI_AMD_SUCCESS) {
             status = 1;
         }
+    }
+    if (status == 0) {
+        tok_ptrs peers{};
+        tok_set expect{};
+        for (int p = 0; p < c->size; ++p) {
+            expect.t[p] = all[p].token;
+            if (p != c->rank) peers.p[p] = (const uint64_t *)((char *)maps[p] + want - kLandTag);
+        }
+        note_stream(c, g.stream);
+        hipLaunchKernelGGL(land_stamp_kernel, dim3(1), dim3(1), 0, g.stream,
+                           (uint64_t *)(g.grow + want - kLandTag), g.grow_token);
+        int rc = record_hip(hipGetLastError(), "landing stamp launch (deferred growth)");
+        if (rc == OMPI_AMD_SUCCESS) rc = launch_barrier(c, g.stream);
+        if (rc == OMPI_AMD_SUCCESS) {
+            hipLaunchKernelGGL(land_check_kernel, dim3(1), dim3(64), 0, g.stream, peers, expect, c->rank,
+                               c->size, c->err_dev, c->flags + kAbortWord);
+            rc = record_hip(hipGetLastError(), "landing check launch (deferred growth)");
+        }
+        if (rc != OMPI_AMD_SUCCESS) status = 1;
     }
     for (int q = 0; q < c->size; ++q) c->land_tokens.push_back(all[q].token);
     if (status != 0) {
