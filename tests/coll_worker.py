@@ -1818,8 +1818,9 @@ def main():
     if not os.environ.get("COLL_HEADLINE"):
         cases += [("cross_comm_order_own_stream", lambda: case_cross_comm_order(comm, rank, n, 192, own=True)),
                   ("cross_comm_grow_own_stream", lambda: case_cross_comm_grow(comm, rank, n, 195)),
-                  ("cross_comm_random_own_stream", lambda: case_cross_comm_random(comm, rank, n, 193)),
-                  ("cross_comm_random_own_stream_b", lambda: case_cross_comm_random(comm, rank, n, 194))]
+                  ("cross_comm_random_own_stream", lambda: case_cross_comm_random(comm, rank, n, 193 + STRESS_SEED)),
+                  ("cross_comm_random_own_stream_b",
+                   lambda: case_cross_comm_random(comm, rank, n, 194 + STRESS_SEED))]
     if only and "cross_comm" in only:
         # opt-in: the known limitation of DESIGN.md §8 item 9 (device-side
         # waits across communicators posted in opposite orders time out)
