@@ -405,8 +405,8 @@ struct pending_op {
         call_blob call;
         land_blob land;
     } blob{};
-    // PEND_GROW: this rank's new landing buffer (allocated and stamped at
-    // post time), its size and token
+    // PEND_GROW: this rank's new landing buffer (allocated at post time,
+    // stamped on the device at launch), its size and token
     char *grow = nullptr;
     size_t grow_bytes = 0;
     uint64_t grow_token = 0;
