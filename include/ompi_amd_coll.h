@@ -90,8 +90,8 @@ int ompi_amd_comm_size(const ompi_amd_comm_t *comm);
 int ompi_amd_comm_set_param(ompi_amd_comm_t *comm, const char *key, int64_t value);
 /* Read a parameter above, or a state counter: "landing_bytes" (current
  * landing-buffer capacity), "landing_deferred_growths" (growths nonblocking
- * calls queued and progress completed), "landing_retired" (buffers those
- * growths replaced, freed at the next blocking growth or destroy), "imports" (this communicator's references to
+ * calls queued and progress completed), "landing_retired" (landing buffers
+ * any growth replaced, kept until the communicator is destroyed), "imports" (this communicator's references to
  * peer mappings), "shadowed" (zero-copy calls that ran through the export
  * fallback), and the process-wide IPC registry's counters (mappings are
  * shared by every communicator, window and message of the process and
