@@ -1241,6 +1241,7 @@ static void note_stream(ompi_amd_comm_t *c, hipStream_t s) {
 static hipError_t wait_stream(hipStream_t s);
 static hipError_t wait_event(hipEvent_t ev);
 namespace ompi_amd {
+static hipStream_t comm_stream(ompi_amd_comm_t *c, void *stream);  // below
 
 static int quiesce_user(void *c) {
     return quiesce(static_cast<ompi_amd_comm_t *>(c), "quiesce (holder of a stale IPC mapping)");
@@ -1481,10 +1482,15 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     // before they reach the device: a peer reading through its mapping right
     // after the rendezvous below would see whatever the memory held before
     // (round 2 saw exactly that as a "token mismatch").  Wait for the copy.
+    // The communicator's own stream (drained above), not the null stream:
+    // a null-stream operation also waits for every blocking stream of the
+    // process — other communicators' queues on the MPI path, whose kernels
+    // may be waiting on peers.
+    const hipStream_t ls = comm_stream(c, nullptr);
     if (e == hipSuccess)
         e = hipMemcpyAsync(fresh + want - kTag, &mine.token, sizeof(mine.token),
-                           hipMemcpyHostToDevice, nullptr);
-    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+                           hipMemcpyHostToDevice, ls);
+    if (e == hipSuccess) e = ::wait_stream(ls);
     if (e != hipSuccess && mine.d.valid) record_hip(e, "landing token write");
     mine.ok = e == hipSuccess;
     int rc = c->boot.allgather(&mine, all, sizeof(mine));  // also: nobody uses the old one now
@@ -1516,13 +1522,14 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
         // collectives' kernels see) into this communicator's own scratch,
         // and by hipMemcpy from the mapping, to tell the two apart
         uint64_t seen = 0, seen_memcpy = 0;
-        hipLaunchKernelGGL(peek_kernel, dim3(1), dim3(1), 0, nullptr,
+        hipLaunchKernelGGL(peek_kernel, dim3(1), dim3(1), 0, ls,
                            (const uint64_t *)((char *)m + want - kTag), (uint64_t *)c->scratch);
         e = hipGetLastError();
-        if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
-        if (e == hipSuccess) e = hipMemcpy(&seen, c->scratch, sizeof(seen), hipMemcpyDeviceToHost);
         if (e == hipSuccess)
-            e = hipMemcpy(&seen_memcpy, (char *)m + want - kTag, sizeof(seen), hipMemcpyDeviceToHost);
+            e = hipMemcpyAsync(&seen, c->scratch, sizeof(seen), hipMemcpyDeviceToHost, ls);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(&seen_memcpy, (char *)m + want - kTag, sizeof(seen), hipMemcpyDeviceToHost, ls);
+        if (e == hipSuccess) e = ::wait_stream(ls);
         if (e == hipSuccess && seen == all[p].token && seen_memcpy != seen) {
             ++c->memcpy_token_mismatch;  // the kernel sees the right buffer; hipMemcpy does not
             record_msg("landing buffer of rank %d: kernel load sees the token, hipMemcpy through "
