@@ -3207,7 +3207,11 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
     // the flag page, then the pipelined schemes' rows (kPipeFlagOff)
     const size_t flag_bytes = kPipeFlagOff + kPipeFlagBytes;
     hipError_t e = alloc_exportable(flag_bytes, (char **)&c->flags, &mine.flags.h, true);
-    if (e == hipSuccess) e = hipMemsetAsync(c->flags, 0, flag_bytes, nullptr);
+    // on the per-thread stream, not the null stream: a null-stream operation
+    // also waits for every blocking stream of the process (other
+    // communicators' queues on the MPI path, whose kernels may be waiting on
+    // peers that are in this creation)
+    if (e == hipSuccess) e = hipMemsetAsync(c->flags, 0, flag_bytes, hipStreamPerThread);
     if (e == hipSuccess) e = alloc_exportable(2 * c->scratch_bytes, &c->scratch, &mine.scratch.h);
     if (e == hipSuccess) e = hipHostMalloc((void **)&c->err_host, 64, hipHostMallocMapped);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&c->err_dev, c->err_host, 0);
@@ -3218,7 +3222,7 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
             e = hipHostGetDevicePointer((void **)&c->dbg_dev, c->dbg_host, 0);
         }
     }
-    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);  // the flag page is zero
+    if (e == hipSuccess) e = hipStreamSynchronize(hipStreamPerThread);  // the flag page is zero
     if (e != hipSuccess) {
         rc = record_hip(e, "comm device resources");
         ompi_amd_comm_destroy(c);
