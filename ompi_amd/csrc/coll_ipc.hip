@@ -1241,7 +1241,6 @@ static void note_stream(ompi_amd_comm_t *c, hipStream_t s) {
 static hipError_t wait_stream(hipStream_t s);
 static hipError_t wait_event(hipEvent_t ev);
 namespace ompi_amd {
-static hipStream_t comm_stream(ompi_amd_comm_t *c, void *stream);  // below
 
 static int quiesce_user(void *c) {
     return quiesce(static_cast<ompi_amd_comm_t *>(c), "quiesce (holder of a stale IPC mapping)");
@@ -1482,11 +1481,19 @@ static int ensure_landing(ompi_amd_comm_t *c, size_t need) {
     // before they reach the device: a peer reading through its mapping right
     // after the rendezvous below would see whatever the memory held before
     // (round 2 saw exactly that as a "token mismatch").  Wait for the copy.
-    // The communicator's own stream (drained above), not the null stream:
-    // a null-stream operation also waits for every blocking stream of the
-    // process — other communicators' queues on the MPI path, whose kernels
-    // may be waiting on peers.
-    const hipStream_t ls = comm_stream(c, nullptr);
+    // A stream the communicator already ran on (drained above): its own
+    // queue on the MPI path, else the stream of its last call (the null
+    // stream before any).  Not the null stream by choice — a null-stream
+    // operation also waits for every blocking stream of the process, other
+    // communicators' queues on the MPI path, whose kernels may be waiting on
+    // peers — and not a stream this process has not used yet: a first use
+    // gives the process one more hardware queue, which on a shared GPU cost
+    // the MPI path 4x in latency.
+    hipStream_t ls = nullptr;
+    {
+        std::lock_guard<std::mutex> g(c->stream_mu);
+        ls = c->own ? c->own : (c->has_stream ? c->cur_stream : nullptr);
+    }
     if (e == hipSuccess)
         e = hipMemcpyAsync(fresh + want - kTag, &mine.token, sizeof(mine.token),
                            hipMemcpyHostToDevice, ls);
@@ -3207,11 +3214,7 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
     // the flag page, then the pipelined schemes' rows (kPipeFlagOff)
     const size_t flag_bytes = kPipeFlagOff + kPipeFlagBytes;
     hipError_t e = alloc_exportable(flag_bytes, (char **)&c->flags, &mine.flags.h, true);
-    // on the per-thread stream, not the null stream: a null-stream operation
-    // also waits for every blocking stream of the process (other
-    // communicators' queues on the MPI path, whose kernels may be waiting on
-    // peers that are in this creation)
-    if (e == hipSuccess) e = hipMemsetAsync(c->flags, 0, flag_bytes, hipStreamPerThread);
+    if (e == hipSuccess) e = hipMemsetAsync(c->flags, 0, flag_bytes, nullptr);
     if (e == hipSuccess) e = alloc_exportable(2 * c->scratch_bytes, &c->scratch, &mine.scratch.h);
     if (e == hipSuccess) e = hipHostMalloc((void **)&c->err_host, 64, hipHostMallocMapped);
     if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&c->err_dev, c->err_host, 0);
@@ -3222,7 +3225,7 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
             e = hipHostGetDevicePointer((void **)&c->dbg_dev, c->dbg_host, 0);
         }
     }
-    if (e == hipSuccess) e = hipStreamSynchronize(hipStreamPerThread);  // the flag page is zero
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);  // the flag page is zero
     if (e != hipSuccess) {
         rc = record_hip(e, "comm device resources");
         ompi_amd_comm_destroy(c);

@@ -1107,21 +1107,17 @@ int ompi_amd_ddt_create_elems(const ompi_amd_ddt_elem_t *elems, int nelems, int6
     }
     const size_t nb = d->host.size() * sizeof(ddt_elem);
     hipError_t err = hipMalloc(&d->dev, nb);
-    // the per-thread stream, not the null stream (which also waits for every
-    // blocking stream of the process: other communicators' queues on the
-    // MPI path, whose kernels may be waiting on peers)
-    const hipStream_t up = hipStreamPerThread;
-    if (err == hipSuccess) err = hipMemcpyAsync(d->dev, d->host.data(), nb, hipMemcpyHostToDevice, up);
+    if (err == hipSuccess) err = hipMemcpy(d->dev, d->host.data(), nb, hipMemcpyHostToDevice);
     if (err == hipSuccess && d->inst_tile) {
         err = hipMalloc(&d->dmap, imap.size() * sizeof(uint16_t));
         if (err == hipSuccess)
-            err = hipMemcpyAsync(d->dmap, imap.data(), imap.size() * sizeof(uint16_t),
-                                 hipMemcpyHostToDevice, up);
+            err = hipMemcpy(d->dmap, imap.data(), imap.size() * sizeof(uint16_t),
+                            hipMemcpyHostToDevice);
     }
     // a copy from pageable memory may return before the bytes reach the
     // device, and the kernels that read the program run on
-    // other streams: wait for the copies here
-    if (err == hipSuccess) err = hipStreamSynchronize(up);
+    // other (non-blocking) streams: wait for the null stream's copies here
+    if (err == hipSuccess) err = hipStreamSynchronize(nullptr);
     if (err != hipSuccess) {
         int rc = record_hip(err, "ddt descriptor upload");
         if (d->dev) hip_ignore(hipFree(d->dev));

@@ -1317,9 +1317,9 @@ static int ctl_take(ompi_amd_comm_t *c, int rc_in, int *slot) {
     if (rc == OMPI_AMD_SUCCESS) {
         rc = comm_alloc_exportable(CTL_BYTES * kCtlPerChunk, true, (void **)&ch.mine, &mine.d);
         if (rc == OMPI_AMD_SUCCESS)
-            rc = record_hip(hipMemsetAsync(ch.mine, 0, CTL_BYTES * kCtlPerChunk, hipStreamPerThread), "osc control arena");
+            rc = record_hip(hipMemset(ch.mine, 0, CTL_BYTES * kCtlPerChunk), "osc control arena");
         if (rc == OMPI_AMD_SUCCESS)
-            rc = record_hip(hipStreamSynchronize(hipStreamPerThread), "osc control arena");
+            rc = record_hip(hipStreamSynchronize(nullptr), "osc control arena");
     }
     mine.failed = rc == OMPI_AMD_SUCCESS ? 0 : 1;
     const int arc = comm_allgather(c, &mine, all, sizeof(chunk_blob));
@@ -1361,15 +1361,11 @@ static uint32_t *ctl_page(ompi_amd_comm_t *c, int slot, int p) {
 }
 
 // after the window's last use everywhere: zero this rank's page, free the slot
-// (memsets here and at window creation run on the per-thread stream, not
-// the null stream, which also waits for every blocking stream of the
-// process: other communicators' queues on the MPI path)
 static int ctl_give(ompi_amd_comm_t *c, int slot) {
     if (slot < 0) return OMPI_AMD_SUCCESS;
     auto *a = static_cast<ctl_arena *>(comm_osc_state(c));
-    int rc = record_hip(hipMemsetAsync(ctl_page(c, slot, comm_rank(c)), 0, CTL_BYTES, hipStreamPerThread),
-                        "osc control page reset");
-    if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipStreamSynchronize(hipStreamPerThread), "osc control page reset");
+    int rc = record_hip(hipMemset(ctl_page(c, slot, comm_rank(c)), 0, CTL_BYTES), "osc control page reset");
+    if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipStreamSynchronize(nullptr), "osc control page reset");
     a->used[(size_t)slot] = 0;
     return rc;
 }
@@ -1600,9 +1596,9 @@ int ompi_amd_win_allocate(ompi_amd_comm_t *c, size_t bytes, int disp_unit, void 
             ipc_desc d;
             rc = comm_alloc_exportable(bytes, false, &m, &d);
         }
-        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipMemsetAsync(m, 0, bytes, hipStreamPerThread), "hipMemset (window)");
+        if (rc == OMPI_AMD_SUCCESS) rc = record_hip(hipMemset(m, 0, bytes), "hipMemset (window)");
         if (rc == OMPI_AMD_SUCCESS)
-            rc = record_hip(hipStreamSynchronize(hipStreamPerThread), "hipStreamSynchronize (window memset)");
+            rc = record_hip(hipStreamSynchronize(nullptr), "hipStreamSynchronize (window memset)");
     }
     auto release = [&] {
         if (!m) return;
@@ -2249,9 +2245,9 @@ int ompi_amd_win_allocate_shared(ompi_amd_comm_t *c, size_t bytes, int disp_unit
         else if (rc == OMPI_AMD_ERR_UNSUPPORTED)
             rc = comm_alloc_exportable(prefix[n] ? prefix[n] : 1, false, (void **)&m, &mine.d);
         if (rc == OMPI_AMD_SUCCESS && prefix[n])
-            rc = record_hip(hipMemsetAsync(m, 0, prefix[n], hipStreamPerThread), "hipMemset (shared window)");
+            rc = record_hip(hipMemset(m, 0, prefix[n]), "hipMemset (shared window)");
         if (rc == OMPI_AMD_SUCCESS)
-            rc = record_hip(hipStreamSynchronize(hipStreamPerThread), "hipStreamSynchronize (shared window)");
+            rc = record_hip(hipStreamSynchronize(nullptr), "hipStreamSynchronize (shared window)");
     }
     mine.failed = rc == OMPI_AMD_SUCCESS ? 0 : 1;
     const int arc = comm_allgather(c, &mine, all, sizeof(seg_blob));
