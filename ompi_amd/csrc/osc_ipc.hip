@@ -261,10 +261,13 @@ constexpr int kOscUnroll = 4;
 // (tools/osc_probe.py; env OMPI_AMD_OSC_MAX_BLOCKS overrides).
 constexpr int kOscMaxBlocks = 256;  // one per CU: 6.26 TB/s vs 3.40 at 2048 (256 MiB fp32 SUM)
 
+// sys: the target is another GPU's memory — every workgroup ends with a
+// system-scope release (as xfer_kernel's SYS); this GPU's memory is covered
+// by the kernel boundary's release.
 template <typename T, int OP>
 __global__ __launch_bounds__(kOscThreads) void acc_kernel(const T *__restrict__ origin, T *target,
                                                           int64_t n, int vec,
-                                                          const uint32_t *gate) {
+                                                          const uint32_t *gate, int sys) {
     if (!gate_open(gate)) return;
     // one system-scope acquire per workgroup (it invalidates this CU's L1
     // and the XCD's L2 for every wave of the CU): lane 0, then the barrier
@@ -310,7 +313,7 @@ __global__ __launch_bounds__(kOscThreads) void acc_kernel(const T *__restrict__ 
         const T r = F::f(target[i], origin[i]);
         store_elem(target + i, r);
     }
-    osc_epilogue();
+    if (sys) osc_epilogue();
 }
 
 // Byte copy for put / get / fetches and the p2p receive: 16-B granules
@@ -437,15 +440,15 @@ __global__ __launch_bounds__(64) void cas_kernel(const unsigned char *origin,
 }
 
 using acc_launch_fn = hipError_t (*)(dim3, const void *, void *, int64_t, int, const uint32_t *,
-                                     hipStream_t);
+                                     int, hipStream_t);
 
 template <int OP, int TYPE>
 static hipError_t acc_launch_slot(dim3 grid, const void *o, void *t, int64_t n, int vec,
-                                  const uint32_t *gate, hipStream_t s) {
+                                  const uint32_t *gate, int sys, hipStream_t s) {
     if constexpr (slot_supported(OP, TYPE)) {
         using T = typename type_of<TYPE>::type;
         hipLaunchKernelGGL((acc_kernel<T, OP>), grid, dim3(kOscThreads), 0, s,
-                           static_cast<const T *>(o), static_cast<T *>(t), n, vec, gate);
+                           static_cast<const T *>(o), static_cast<T *>(t), n, vec, gate, sys);
         return hipGetLastError();
     } else {
         return hipErrorInvalidValue;
@@ -1019,6 +1022,19 @@ static int target_span(ompi_amd_win_t *w, int target, int64_t base, int64_t lo, 
     return OMPI_AMD_SUCCESS;
 }
 
+// Whether p (a mapping of a peer's window, or an origin buffer) is device
+// memory of GPU `dev`; host memory and anything unknown count as not (the
+// conservative copy, with the system-scope release).
+static bool on_this_device(const void *p, int dev) {
+    if (!p) return true;
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice && a.device == dev;
+}
+
 // A copy into target's window needs the system-scope release (another
 // GPU's memory, or a dynamic window's region, not classified).
 static bool remote_dst(const ompi_amd_win_t *w, int target) {
@@ -1165,7 +1181,7 @@ int xfer_copy_sig(const void *src, void *dst, size_t bytes, hipStream_t s, const
 }
 
 static int launch_acc(ompi_amd_win_t *w, int op, int type, const void *origin, void *target,
-                      size_t count, const uint32_t *gate, hipStream_t s) {
+                      size_t count, const uint32_t *gate, hipStream_t s, bool remote) {
     acc_launch_fn f = (op >= 0 && op < OMPI_AMD_OP_COUNT && type >= 0 && type < OMPI_AMD_TYPE_COUNT)
                           ? g_acc[op][type]
                           : nullptr;
@@ -1179,7 +1195,7 @@ static int launch_acc(ompi_amd_win_t *w, int op, int type, const void *origin, v
     const int64_t units = vec ? (int64_t)(count * ext / 16) : (int64_t)count;
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((units + per - 1) / per,
                                                                   osc_grid_cap()));
-    return record_hip(f(dim3((unsigned)blocks), origin, target, (int64_t)count, vec, gate, s),
+    return record_hip(f(dim3((unsigned)blocks), origin, target, (int64_t)count, vec, gate, remote ? 1 : 0, s),
                       "osc accumulate launch");
 }
 
@@ -1239,10 +1255,11 @@ static int rma_op(ompi_amd_win_t *w, const void *origin, void *result, size_t co
     OSC_TRY(launch_lock(w, target, 0, s));
     const uint32_t *gate = taken_word(w, target, true);
     int rc = OMPI_AMD_SUCCESS;
-    if (result) rc = xfer_copy(t, result, bytes, s, gate);
+    const bool remote = remote_dst(w, target);
+    if (result) rc = xfer_copy(t, result, bytes, s, gate, !on_this_device(result, comm_device(w->c)));
     if (rc == OMPI_AMD_SUCCESS) {
-        if (op == OMPI_AMD_OP_REPLACE) rc = xfer_copy(origin, t, bytes, s, gate);
-        else if (op != OMPI_AMD_OP_NO_OP) rc = launch_acc(w, op, type, origin, t, count, gate, s);
+        if (op == OMPI_AMD_OP_REPLACE) rc = xfer_copy(origin, t, bytes, s, gate, remote);
+        else if (op != OMPI_AMD_OP_NO_OP) rc = launch_acc(w, op, type, origin, t, count, gate, s, remote);
     }
     const int urc = launch_lock(w, target, 1, s);  // always release
     return rc != OMPI_AMD_SUCCESS ? rc : urc;
@@ -1433,18 +1450,6 @@ static int win_merge(ompi_amd_win_t *w, hipStream_t s) {
     return record_hip(hipGetLastError(), "osc window merge launch");
 }
 
-// Whether p (a mapping of a peer's window, or an origin buffer) is device
-// memory of GPU `dev`; host memory and anything unknown count as not (the
-// conservative copy, with the system-scope release).
-static bool on_this_device(const void *p, int dev) {
-    if (!p) return true;
-    hipPointerAttribute_t a{};
-    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    return a.type == hipMemoryTypeDevice && a.device == dev;
-}
 
 // shared: every rank's base as this process maps it (MPI_Win_allocate_shared),
 // so nothing is exported or imported for the bases.
@@ -2064,10 +2069,11 @@ static int acc_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount, const o
             rc = record_hip(f(dim3((unsigned)blocks), dd, t, in, old, n, gate, fast, s),
                             "osc derived accumulate launch");
         } else {  // contiguous target: the plain kernels on the packed streams
-            if (fetch) rc = xfer_copy(t, old, tbytes, s, gate);
+            if (fetch) rc = xfer_copy(t, old, tbytes, s, gate, !on_this_device(old, comm_device(w->c)));
             if (rc == OMPI_AMD_SUCCESS) {
-                if (op == OMPI_AMD_OP_REPLACE) rc = xfer_copy(in, t, tbytes, s, gate);
-                else if (op != OMPI_AMD_OP_NO_OP) rc = launch_acc(w, op, type, in, t, (size_t)n, gate, s);
+                if (op == OMPI_AMD_OP_REPLACE) rc = xfer_copy(in, t, tbytes, s, gate, remote_dst(w, target));
+                else if (op != OMPI_AMD_OP_NO_OP)
+                    rc = launch_acc(w, op, type, in, t, (size_t)n, gate, s, remote_dst(w, target));
             }
         }
         const int urc = launch_lock(w, target, 1, s);  // always release
