@@ -3213,19 +3213,23 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
     ipc_blob mine{}, all[kMaxRanks];
     // the flag page, then the pipelined schemes' rows (kPipeFlagOff)
     const size_t flag_bytes = kPipeFlagOff + kPipeFlagBytes;
-    hipError_t e = alloc_exportable(flag_bytes, (char **)&c->flags, &mine.flags.h, true);
-    if (e == hipSuccess) e = hipMemsetAsync(c->flags, 0, flag_bytes, nullptr);
-    if (e == hipSuccess) e = alloc_exportable(2 * c->scratch_bytes, &c->scratch, &mine.scratch.h);
-    if (e == hipSuccess) e = hipHostMalloc((void **)&c->err_host, 64, hipHostMallocMapped);
-    if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&c->err_dev, c->err_host, 0);
-    if (e == hipSuccess && getenv("OMPI_AMD_DEBUG_PROGRESS") && atoi(getenv("OMPI_AMD_DEBUG_PROGRESS"))) {
-        e = hipHostMalloc((void **)&c->dbg_host, (2 + kMaxRanks) * sizeof(uint64_t), hipHostMallocMapped);
-        if (e == hipSuccess) {
-            memset(c->dbg_host, 0, (2 + kMaxRanks) * sizeof(uint64_t));
-            e = hipHostGetDevicePointer((void **)&c->dbg_dev, c->dbg_host, 0);
+    hipError_t e;
+    {
+        host_step st("comm_create device resources", (size_t)rank);
+        e = alloc_exportable(flag_bytes, (char **)&c->flags, &mine.flags.h, true);
+        if (e == hipSuccess) e = hipMemsetAsync(c->flags, 0, flag_bytes, nullptr);
+        if (e == hipSuccess) e = alloc_exportable(2 * c->scratch_bytes, &c->scratch, &mine.scratch.h);
+        if (e == hipSuccess) e = hipHostMalloc((void **)&c->err_host, 64, hipHostMallocMapped);
+        if (e == hipSuccess) e = hipHostGetDevicePointer((void **)&c->err_dev, c->err_host, 0);
+        if (e == hipSuccess && getenv("OMPI_AMD_DEBUG_PROGRESS") && atoi(getenv("OMPI_AMD_DEBUG_PROGRESS"))) {
+            e = hipHostMalloc((void **)&c->dbg_host, (2 + kMaxRanks) * sizeof(uint64_t), hipHostMallocMapped);
+            if (e == hipSuccess) {
+                memset(c->dbg_host, 0, (2 + kMaxRanks) * sizeof(uint64_t));
+                e = hipHostGetDevicePointer((void **)&c->dbg_dev, c->dbg_host, 0);
+            }
         }
+        if (e == hipSuccess) e = hipStreamSynchronize(nullptr);  // the flag page is zero
     }
-    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);  // the flag page is zero
     if (e != hipSuccess) {
         rc = record_hip(e, "comm device resources");
         ompi_amd_comm_destroy(c);
@@ -3258,6 +3262,7 @@ int ompi_amd_comm_create(const char *name, int rank, int size, int device,
             continue;
         }
         void *f = nullptr, *s = nullptr;
+        host_step st("comm_create map peer", (size_t)p);
         rc = ipc_map(alloc_of(all[p].flags), c, &c->opened[p][0], &f);
         if (rc == OMPI_AMD_SUCCESS) rc = ipc_map(alloc_of(all[p].scratch), c, &c->opened[p][1], &s);
         if (rc != OMPI_AMD_SUCCESS) break;

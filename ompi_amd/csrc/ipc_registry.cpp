@@ -123,7 +123,10 @@ void hold(ipc_ref *r, void *owner) {
 struct reg_step {
     const char *what;
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
-    explicit reg_step(const char *w) : what(w) {}
+    explicit reg_step(const char *w) : what(w) {
+        static const bool on = getenv("OMPI_AMD_TRACE") && *getenv("OMPI_AMD_TRACE") == '1';
+        if (on) fprintf(stderr, "[trace pid %d] %s ...\n", (int)getpid(), what);
+    }
     ~reg_step() {
         static const bool on = getenv("OMPI_AMD_TRACE") && *getenv("OMPI_AMD_TRACE") == '1';
         if (!on) return;
