@@ -4,6 +4,7 @@
 
 #include <execinfo.h>
 #include <signal.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <cstdarg>
@@ -74,11 +75,28 @@ static void crash_trace(int sig) {
     raise(sig);
 }
 
+// ... and SIGUSR2 prints the main thread's stack and continues (a hung
+// rank's launcher sends it before the kill: tests/test_coll_gpu.py run_ranks)
+static void stack_dump(int sig) {
+    if (syscall(SYS_gettid) != getpid()) {  // delivered to another thread: pass it on
+        syscall(SYS_tgkill, getpid(), getpid(), sig);
+        return;
+    }
+    void *pc[64];
+    const int n = backtrace(pc, 64);
+    static const char head[] = "[ompi_amd] SIGUSR2 call stack:\n";
+    (void)!write(2, head, sizeof(head) - 1);
+    backtrace_symbols_fd(pc, n, 2);
+}
+
 __attribute__((constructor)) static void crash_trace_init() {
     const char *v = getenv("OMPI_AMD_BACKTRACE");
     if (!v || atoi(v) == 0) return;
+    void *warm[2];
+    (void)backtrace(warm, 2);  // loads the unwinder outside a handler
     signal(SIGSEGV, crash_trace);
     signal(SIGBUS, crash_trace);
+    signal(SIGUSR2, stack_dump);
 }
 
 const char *ipc_mode_env_now() {

@@ -11,6 +11,8 @@ import os
 import socket
 import subprocess
 import sys
+import signal
+import time
 
 import pytest
 
@@ -66,7 +68,12 @@ def run_ranks(n, timeout=600, extra_env=None, worker=WORKER, tag="n"):
                 f.close()
             outs.append((p.returncode, out))
     finally:
-        for p in procs:
+        alive = [p for p in procs if p.poll() is None]
+        if alive and (extra_env or {}).get("OMPI_AMD_BACKTRACE", os.environ.get("OMPI_AMD_BACKTRACE")) == "1":
+            for p in alive:  # the library prints each hung rank's native stack
+                os.kill(p.pid, signal.SIGUSR2)
+            time.sleep(3)
+        for p in alive:
             if p.poll() is None:
                 p.kill()
     return outs
