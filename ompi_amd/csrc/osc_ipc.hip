@@ -614,7 +614,7 @@ __device__ __forceinline__ void ddt_acc_body(const ddt_desc &d, const ddt_elem *
 template <typename T, int OP, bool FAST>
 __global__ __launch_bounds__(kOscThreads) void ddt_acc_kernel(ddt_desc d, char *typed, const T *in,
                                                               T *old, int64_t n,
-                                                              const uint32_t *gate) {
+                                                              const uint32_t *gate, int sys) {
     if (!gate_open(gate)) return;
     __shared__ ddt_elem lds[kDdtLdsElems];
     if (threadIdx.x == 0) osc_acquire();
@@ -630,11 +630,11 @@ __global__ __launch_bounds__(kOscThreads) void ddt_acc_kernel(ddt_desc d, char *
         __syncthreads();
         ddt_acc_body<T, OP, FAST>(d, d.elems, d.nelem, typed, in, old, n);
     }
-    osc_epilogue();
+    if (sys) osc_epilogue();  // sys: the target is another GPU's memory (acc_kernel)
 }
 
 using ddt_acc_fn = hipError_t (*)(dim3, const ddt_desc &, char *, const void *, void *, int64_t,
-                                  const uint32_t *, bool, hipStream_t);
+                                  const uint32_t *, bool, hipStream_t, int);
 
 // ---- derived datatypes of pair type (MAXLOC / MINLOC operands) ----
 // ompi_osc_base_sndrcv_op (osc_base_obj_convert.c:73-245) converts the
@@ -740,13 +740,14 @@ static bool pair_info(int type, int op, pair_fn *f, int64_t *packed, int64_t *ex
 
 template <typename T, int OP>
 static hipError_t ddt_acc_launch(dim3 grid, const ddt_desc &d, char *typed, const void *in,
-                                 void *old, int64_t n, const uint32_t *gate, bool fast, hipStream_t s) {
+                                 void *old, int64_t n, const uint32_t *gate, bool fast, hipStream_t s,
+                                 int sys) {
     if (fast)  // d.sdiv holds size / sizeof(T)
         hipLaunchKernelGGL((ddt_acc_kernel<T, OP, true>), grid, dim3(kOscThreads), 0, s, d, typed,
-                           static_cast<const T *>(in), static_cast<T *>(old), n, gate);
+                           static_cast<const T *>(in), static_cast<T *>(old), n, gate, sys);
     else
         hipLaunchKernelGGL((ddt_acc_kernel<T, OP, false>), grid, dim3(kOscThreads), 0, s, d, typed,
-                           static_cast<const T *>(in), static_cast<T *>(old), n, gate);
+                           static_cast<const T *>(in), static_cast<T *>(old), n, gate, sys);
     return hipGetLastError();
 }
 template <int OP, int TYPE>
@@ -2066,7 +2067,8 @@ static int acc_ddt(ompi_amd_win_t *w, const void *origin, size_t ocount, const o
             const bool fast = fast_on && (e == 1 || e == 2 || e == 4 || e == 8 || e == 16) && tv.gran % e == 0 &&
                               n < (1ll << 32) && dd.size / e < (1ll << 32) && tv.max_blen / e < (1ll << 32);
             if (fast) dd.sdiv = make_fdiv((uint32_t)(dd.size / e));
-            rc = record_hip(f(dim3((unsigned)blocks), dd, t, in, old, n, gate, fast, s),
+            rc = record_hip(f(dim3((unsigned)blocks), dd, t, in, old, n, gate, fast, s,
+                              remote_dst(w, target) ? 1 : 0),
                             "osc derived accumulate launch");
         } else {  // contiguous target: the plain kernels on the packed streams
             if (fetch) rc = xfer_copy(t, old, tbytes, s, gate, !on_this_device(old, comm_device(w->c)));
@@ -2157,7 +2159,8 @@ static int rma_ddt(ompi_amd_win_t *w, void *origin, size_t ocount, const ompi_am
                           tv.max_blen / g < (1ll << 32);
         if (fast) dd.sdiv = make_fdiv((uint32_t)(dd.size / g));
         rc = record_hip(f(dim3((unsigned)blocks), dd, t, put ? packed : nullptr, put ? nullptr : packed, n,
-                          gate, fast, s),
+                          gate, fast, s,
+                          (put ? remote_dst(w, target) : !on_this_device(packed, comm_device(w->c))) ? 1 : 0),
                         put ? "osc derived put launch" : "osc derived get launch");
     }
     if (rc == OMPI_AMD_SUCCESS && odt && !put) {  // the fetched stream into the origin's layout
