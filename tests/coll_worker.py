@@ -12,6 +12,7 @@ import json
 import os
 import sys
 import time
+import signal
 import traceback
 
 import numpy as np
@@ -1527,6 +1528,8 @@ def report(rank, n, obj):
 def main():
     rank, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     import faulthandler
+    # a hung rank's Python stack, on the launcher's SIGUSR1 (test_coll_gpu.run_ranks)
+    faulthandler.register(signal.SIGUSR1, all_threads=True)
     # a rank stuck for a minute prints every thread's stack (then again each
     # minute): a hang names the call it sits in
     faulthandler.dump_traceback_later(60, repeat=True, file=sys.stderr)

@@ -8,11 +8,13 @@ buffers.  Expected results come from the deterministic per-rank inputs and,
 for accumulates, from the CPU oracle's op/base restatement applied in the
 target's order.  One JSON line per case; exit 0 only if all passed.
 """
+import faulthandler
 import ctypes
 import functools
 import json
 import os
 import sys
+import signal
 import traceback
 
 import numpy as np
@@ -1905,6 +1907,11 @@ def comm_barrier():
 
 
 def main():
+    # a hung rank's Python stack, on the launcher's SIGUSR1 (test_coll_gpu.run_ranks)
+    faulthandler.register(signal.SIGUSR1, all_threads=True)
+    # a rank stuck for a minute prints every thread's stack (then again each
+    # minute), as coll_worker.py does
+    faulthandler.dump_traceback_later(60, repeat=True, file=sys.stderr)
     global STREAM
     rank, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     device = int(os.environ.get("OMPI_AMD_DEVICE", "0"))

@@ -70,7 +70,10 @@ def run_ranks(n, timeout=600, extra_env=None, worker=WORKER, tag="n"):
     finally:
         alive = [p for p in procs if p.poll() is None]
         if alive and (extra_env or {}).get("OMPI_AMD_BACKTRACE", os.environ.get("OMPI_AMD_BACKTRACE")) == "1":
-            for p in alive:  # the library prints each hung rank's native stack
+            for p in alive:  # each hung rank prints its Python stack, then its native one
+                os.kill(p.pid, signal.SIGUSR1)
+            time.sleep(2)
+            for p in alive:
                 os.kill(p.pid, signal.SIGUSR2)
             time.sleep(3)
         for p in alive:
