@@ -15,6 +15,7 @@ import json
 import os
 import sys
 import signal
+import time
 import traceback
 
 import numpy as np
@@ -1912,6 +1913,14 @@ def main():
     # a rank stuck for a minute prints every thread's stack (then again each
     # minute), as coll_worker.py does
     faulthandler.dump_traceback_later(60, repeat=True, file=sys.stderr)
+    if os.environ.get("OMPI_AMD_BACKTRACE") == "1":  # ... and its native stack
+        import threading
+
+        def native_dumps():
+            while True:
+                time.sleep(60)
+                os.kill(os.getpid(), signal.SIGUSR2)
+        threading.Thread(target=native_dumps, daemon=True).start()
     global STREAM
     rank, n = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     device = int(os.environ.get("OMPI_AMD_DEVICE", "0"))
